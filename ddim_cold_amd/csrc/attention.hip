@@ -1,0 +1,410 @@
+// Fused multi-head self-attention for gfx950 (ViT.py:105-117 semantics:
+// softmax(Q K^T * hd^-0.5) -> Dropout -> @V), forward + backward, any N, hd in {32, 64}.
+//
+// Forward (flash-style, online softmax, never materialises N x N):
+//   workgroup = 4 waves = 64 query rows of one (b, h); each wave owns 16 queries.
+//   K/V tiles of 64 keys staged in LDS with a 32-B row pad (conflict-free for
+//   ds_read_b128 row reads AND ds_read_b64_tr_b16 transposed reads).
+//   Scores are computed SWAPPED, S^T = K Q^T, so each lane holds 16 keys of ONE
+//   query: the row max / row sum need only 2 cross-lane shuffles, and the
+//   probability tile P^T is already the B operand of O^T += V^T P^T
+//   (bf16-packed registers, no LDS round trip).  V^T fragments come from the V
+//   tile through the hardware transposing LDS read.  Dropout on P uses the
+//   counter hash (regenerated in backward).  Saves LSE per query.
+//
+// Backward (no atomics, deterministic, recompute P from LSE):
+//   kernel 1 (per 64-query block): delta = rowsum(dO*O) (stored), dQ.
+//       S^T = K Q^T, dP^T = V dO^T, dS^T = P^T (M*dP^T - delta), dQ^T += K^T dS^T.
+//   kernel 2 (per 64-key block, each wave 16 keys held as register fragments):
+//       S = Q K^T, dP = dO V^T, dV^T += dO^T (P*M), dK^T += Q^T dS.
+//   dQ/dK/dV are written token-major into dqkv [B*N, 3D] (the layout of the
+//   qkv Linear's output columns) so the qkv dgrad/wgrad GEMMs consume it directly.
+#include "common.h"
+#include "kernels.h"
+
+namespace dc {
+
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+template <int HD>
+struct AC {
+  static constexpr int S = 2 * HD + 32;   // LDS row stride in bytes
+  static constexpr int TILE = 64 * S;     // one 64-row tile
+  static constexpr int KS = HD / 32;      // MFMA k-steps over hd
+  static constexpr int DT = HD / 16;      // 16-row tiles over hd
+  static constexpr int CPR = HD / 8;      // 16-B chunks per row
+};
+
+// stage rows r0..r0+63 of a [N][HD] bf16 matrix into a padded LDS image
+template <int HD>
+__device__ __forceinline__ void stage64(char* lds, const bf16* __restrict__ base, int r0, int N) {
+  for (int c = threadIdx.x; c < 64 * AC<HD>::CPR; c += 256) {
+    const int r = c / AC<HD>::CPR, cc = c % AC<HD>::CPR;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (r0 + r < N) v = *reinterpret_cast<const u32x4*>(base + (size_t)(r0 + r) * HD + cc * 8);
+    *reinterpret_cast<u32x4*>(lds + r * AC<HD>::S + cc * 16) = v;
+  }
+}
+
+// standard-order fragment (row r, k-step s) from a padded row image
+template <int HD>
+__device__ __forceinline__ bf16x8 frag_row(const char* lds, int r, int s, int g) {
+  return *reinterpret_cast<const bf16x8*>(lds + r * AC<HD>::S + (32 * s + 8 * g) * 2);
+}
+
+// standard-order fragment straight from global memory (row < N else zero)
+template <int HD>
+__device__ __forceinline__ bf16x8 frag_glb(const bf16* __restrict__ base, int row, int N, int s, int g) {
+  if (row < N) return *reinterpret_cast<const bf16x8*>(base + (size_t)row * HD + 32 * s + 8 * g);
+  bf16x8 z;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z[j] = f2bf(0.f);
+  return z;
+}
+
+__device__ __forceinline__ bf16x8 pack8(const f32x4& a, const f32x4& b) {
+  bf16x8 v;
+  v[0] = f2bf(a[0]); v[1] = f2bf(a[1]); v[2] = f2bf(a[2]); v[3] = f2bf(a[3]);
+  v[4] = f2bf(b[0]); v[5] = f2bf(b[1]); v[6] = f2bf(b[2]); v[7] = f2bf(b[3]);
+  return v;
+}
+
+// ============================================================================ forward
+template <int HD>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                       float* __restrict__ lse, int B, int H, int N, float scale,
+                                                       const int64_t* __restrict__ rng, int site, uint32_t thr,
+                                                       float dsc) {
+  using C = AC<HD>;
+  __shared__ __attribute__((aligned(16))) char lds[2 * C::TILE];
+  char* Kl = lds;
+  char* Vl = lds + C::TILE;
+  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const size_t mat = (size_t)N * HD;
+  const bf16* qb = qkv + (size_t)bh * mat;
+  const bf16* kb = qkv + ((size_t)B * H + bh) * mat;
+  const bf16* vb = qkv + ((size_t)2 * B * H + bh) * mat;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
+  const int q = blockIdx.x * 64 + wave * 16 + li;  // this lane's query (column of S^T)
+  const float sl2 = scale * LOG2E;
+  const uint32_t salt = thr ? site_salt(rng, site) : 0u;
+
+  bf16x8 qf[C::KS];
+#pragma unroll
+  for (int s = 0; s < C::KS; ++s) qf[s] = frag_glb<HD>(qb, q, N, s, g);
+
+  f32x4 o[C::DT];
+#pragma unroll
+  for (int d = 0; d < C::DT; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+
+  for (int kv0 = 0; kv0 < N; kv0 += 64) {
+    __syncthreads();
+    stage64<HD>(Kl, kb, kv0, N);
+    stage64<HD>(Vl, vb, kv0, N);
+    __syncthreads();
+    f32x4 st[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) st[t] = mfma16(frag_row<HD>(Kl, 16 * t + li, s, g), qf[s], st[t]);
+    }
+    float mt = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kv0 + 16 * t + 4 * g + r;
+        const float v = key < N ? st[t][r] * sl2 : -INFINITY;
+        st[t][r] = v;
+        mt = fmaxf(mt, v);
+      }
+    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float m_new = fmaxf(m_run, mt);
+    const float alpha = exp2f(m_run - m_new);
+    float ls = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float pv = exp2f(st[t][r] - m_new);
+        ls += pv;
+        if (thr) {
+          const int key = kv0 + 16 * t + 4 * g + r;
+          const uint32_t idx = (uint32_t)(((size_t)bh * N + q) * N + key);
+          pv = dropout_keep(salt, idx, thr) ? pv * dsc : 0.f;
+        }
+        st[t][r] = pv;
+      }
+    ls += __shfl_xor(ls, 16, 64);
+    ls += __shfl_xor(ls, 32, 64);
+    l_run = l_run * alpha + ls;
+    m_run = m_new;
+#pragma unroll
+    for (int d = 0; d < C::DT; ++d) o[d] *= alpha;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 pb = pack8(st[2 * s2], st[2 * s2 + 1]);
+#pragma unroll
+      for (int d = 0; d < C::DT; ++d) o[d] = mfma16(frag_t<C::S>(Vl, 16 * d, s2, lane), pb, o[d]);
+    }
+  }
+  if (q < N) {
+    const float inv = 1.f / l_run;
+    const int D = H * HD;
+    bf16* orow = out + ((size_t)b * N + q) * D + h * HD;
+#pragma unroll
+    for (int d = 0; d < C::DT; ++d) {
+      bf16x4 v;
+      v[0] = f2bf(o[d][0] * inv); v[1] = f2bf(o[d][1] * inv);
+      v[2] = f2bf(o[d][2] * inv); v[3] = f2bf(o[d][3] * inv);
+      *reinterpret_cast<bf16x4*>(orow + 16 * d + 4 * g) = v;
+    }
+    if (g == 0) lse[(size_t)bh * N + q] = (m_run + log2f(l_run)) * LN2;
+  }
+}
+
+// ============================================================================ backward: dQ (+delta)
+template <int HD>
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ qkv,
+                                                          const bf16* __restrict__ out, const float* __restrict__ lse,
+                                                          float* __restrict__ delta, bf16* __restrict__ dqkv, int B,
+                                                          int H, int N, float scale, const int64_t* __restrict__ rng,
+                                                          int site, uint32_t thr, float dsc) {
+  using C = AC<HD>;
+  __shared__ __attribute__((aligned(16))) char lds[2 * C::TILE];
+  char* Kl = lds;
+  char* Vl = lds + C::TILE;
+  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const int D = H * HD;
+  const size_t mat = (size_t)N * HD;
+  const bf16* qb = qkv + (size_t)bh * mat;
+  const bf16* kb = qkv + ((size_t)B * H + bh) * mat;
+  const bf16* vb = qkv + ((size_t)2 * B * H + bh) * mat;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
+  const int q = blockIdx.x * 64 + wave * 16 + li;
+  const bool qv = q < N;
+  const float sl2 = scale * LOG2E;
+  const uint32_t salt = thr ? site_salt(rng, site) : 0u;
+
+  // dO and O rows of this lane's query are token-major [B, N, D] with head offset h*HD
+  const bf16* dorow = dout + ((size_t)b * N + (qv ? q : 0)) * D + h * HD;
+  const bf16* orow = out + ((size_t)b * N + (qv ? q : 0)) * D + h * HD;
+  bf16x8 qf[C::KS], df[C::KS];
+  float dl = 0.f;
+#pragma unroll
+  for (int s = 0; s < C::KS; ++s) {
+    qf[s] = frag_glb<HD>(qb, q, N, s, g);
+    bf16x8 dv, ov;
+    if (qv) {
+      dv = *reinterpret_cast<const bf16x8*>(dorow + 32 * s + 8 * g);
+      ov = *reinterpret_cast<const bf16x8*>(orow + 32 * s + 8 * g);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { dv[j] = f2bf(0.f); ov[j] = f2bf(0.f); }
+    }
+    df[s] = dv;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dl += bf2f(dv[j]) * bf2f(ov[j]);
+  }
+  dl += __shfl_xor(dl, 16, 64);
+  dl += __shfl_xor(dl, 32, 64);
+  if (qv && g == 0) delta[(size_t)bh * N + q] = dl;
+  const float lse2 = qv ? lse[(size_t)bh * N + q] * LOG2E : INFINITY;
+
+  f32x4 dq[C::DT];
+#pragma unroll
+  for (int d = 0; d < C::DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int kv0 = 0; kv0 < N; kv0 += 64) {
+    __syncthreads();
+    stage64<HD>(Kl, kb, kv0, N);
+    stage64<HD>(Vl, vb, kv0, N);
+    __syncthreads();
+    f32x4 ds[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) {
+        st = mfma16(frag_row<HD>(Kl, 16 * t + li, s, g), qf[s], st);
+        dp = mfma16(frag_row<HD>(Vl, 16 * t + li, s, g), df[s], dp);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kv0 + 16 * t + 4 * g + r;
+        const float pr = key < N ? exp2f(st[r] * sl2 - lse2) : 0.f;
+        float dpv = dp[r];
+        if (thr) {
+          const uint32_t idx = (uint32_t)(((size_t)bh * N + q) * N + key);
+          dpv = dropout_keep(salt, idx, thr) ? dpv * dsc : 0.f;
+        }
+        ds[t][r] = pr * (dpv - dl);
+      }
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 sb = pack8(ds[2 * s2], ds[2 * s2 + 1]);
+#pragma unroll
+      for (int d = 0; d < C::DT; ++d) dq[d] = mfma16(frag_t<C::S>(Kl, 16 * d, s2, lane), sb, dq[d]);
+    }
+  }
+  if (qv) {
+    bf16* row = dqkv + ((size_t)b * N + q) * (3 * D) + h * HD;
+#pragma unroll
+    for (int d = 0; d < C::DT; ++d) {
+      bf16x4 v;
+      v[0] = f2bf(dq[d][0] * scale); v[1] = f2bf(dq[d][1] * scale);
+      v[2] = f2bf(dq[d][2] * scale); v[3] = f2bf(dq[d][3] * scale);
+      *reinterpret_cast<bf16x4*>(row + 16 * d + 4 * g) = v;
+    }
+  }
+}
+
+// ============================================================================ backward: dK, dV
+template <int HD>
+__global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restrict__ dout,
+                                                           const bf16* __restrict__ qkv,
+                                                           const float* __restrict__ lse,
+                                                           const float* __restrict__ delta,
+                                                           bf16* __restrict__ dqkv, int B, int H, int N, float scale,
+                                                           const int64_t* __restrict__ rng, int site, uint32_t thr,
+                                                           float dsc) {
+  using C = AC<HD>;
+  __shared__ __attribute__((aligned(16))) char lds[2 * C::TILE];
+  __shared__ float s_lse[64], s_del[64];
+  char* Ql = lds;
+  char* Dl = lds + C::TILE;
+  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const int D = H * HD;
+  const size_t mat = (size_t)N * HD;
+  const bf16* qb = qkv + (size_t)bh * mat;
+  const bf16* kb = qkv + ((size_t)B * H + bh) * mat;
+  const bf16* vb = qkv + ((size_t)2 * B * H + bh) * mat;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
+  const int key = blockIdx.x * 64 + wave * 16 + li;  // this lane's key (column of S)
+  const float sl2 = scale * LOG2E;
+  const uint32_t salt = thr ? site_salt(rng, site) : 0u;
+
+  bf16x8 kf[C::KS], vf[C::KS];
+#pragma unroll
+  for (int s = 0; s < C::KS; ++s) {
+    kf[s] = frag_glb<HD>(kb, key, N, s, g);
+    vf[s] = frag_glb<HD>(vb, key, N, s, g);
+  }
+  f32x4 dk[C::DT], dv[C::DT];
+#pragma unroll
+  for (int d = 0; d < C::DT; ++d) {
+    dk[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dv[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  for (int q0 = 0; q0 < N; q0 += 64) {
+    __syncthreads();
+    stage64<HD>(Ql, qb, q0, N);
+    // dO rows (token-major, head slice) into the padded image
+    for (int c = threadIdx.x; c < 64 * C::CPR; c += 256) {
+      const int r = c / C::CPR, cc = c % C::CPR;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (q0 + r < N) v = *reinterpret_cast<const u32x4*>(dout + ((size_t)b * N + q0 + r) * D + h * HD + cc * 8);
+      *reinterpret_cast<u32x4*>(Dl + r * C::S + cc * 16) = v;
+    }
+    if (threadIdx.x < 64) {
+      const int qq = q0 + threadIdx.x;
+      s_lse[threadIdx.x] = qq < N ? lse[(size_t)bh * N + qq] * LOG2E : INFINITY;
+      s_del[threadIdx.x] = qq < N ? delta[(size_t)bh * N + qq] : 0.f;
+    }
+    __syncthreads();
+    f32x4 pm[4], ds[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) {
+        st = mfma16(frag_row<HD>(Ql, 16 * t + li, s, g), kf[s], st);
+        dp = mfma16(frag_row<HD>(Dl, 16 * t + li, s, g), vf[s], dp);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qr = 16 * t + 4 * g + r;
+        const int qq = q0 + qr;
+        const float pr = exp2f(st[r] * sl2 - s_lse[qr]);
+        float pd = pr, dpv = dp[r];
+        if (thr) {
+          const uint32_t idx = (uint32_t)(((size_t)bh * N + qq) * N + key);
+          const bool kp = dropout_keep(salt, idx, thr);
+          pd = kp ? pr * dsc : 0.f;
+          dpv = kp ? dpv * dsc : 0.f;
+        }
+        pm[t][r] = pd;
+        ds[t][r] = pr * (dpv - s_del[qr]);
+      }
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 pb = pack8(pm[2 * s2], pm[2 * s2 + 1]);
+      const bf16x8 sb = pack8(ds[2 * s2], ds[2 * s2 + 1]);
+#pragma unroll
+      for (int d = 0; d < C::DT; ++d) {
+        dv[d] = mfma16(frag_t<C::S>(Dl, 16 * d, s2, lane), pb, dv[d]);
+        dk[d] = mfma16(frag_t<C::S>(Ql, 16 * d, s2, lane), sb, dk[d]);
+      }
+    }
+  }
+  if (key < N) {
+    bf16* row = dqkv + ((size_t)b * N + key) * (3 * D) + h * HD;
+#pragma unroll
+    for (int d = 0; d < C::DT; ++d) {
+      bf16x4 kv, vv;
+      kv[0] = f2bf(dk[d][0] * scale); kv[1] = f2bf(dk[d][1] * scale);
+      kv[2] = f2bf(dk[d][2] * scale); kv[3] = f2bf(dk[d][3] * scale);
+      vv[0] = f2bf(dv[d][0]); vv[1] = f2bf(dv[d][1]);
+      vv[2] = f2bf(dv[d][2]); vv[3] = f2bf(dv[d][3]);
+      *reinterpret_cast<bf16x4*>(row + D + 16 * d + 4 * g) = kv;
+      *reinterpret_cast<bf16x4*>(row + 2 * D + 16 * d + 4 * g) = vv;
+    }
+  }
+}
+
+}  // namespace dc
+
+using namespace dc;
+
+void attn_fwd_launch(const void* qkv, void* o, float* lse, int B, int H, int N, int hd, float scale,
+                     const int64_t* rng, int site, double p, hipStream_t stream) {
+  const dim3 grid((N + 63) / 64, B * H);
+  const uint32_t thr = drop_threshold_host(p);
+  const float dsc = p > 0 ? 1.f / (1.f - (float)p) : 1.f;
+  const bf16* q = reinterpret_cast<const bf16*>(qkv);
+  bf16* out = reinterpret_cast<bf16*>(o);
+  if (hd == 32)
+    hipLaunchKernelGGL(attn_fwd_kernel<32>, grid, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc);
+  else if (hd == 64)
+    hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc);
+  else
+    throw std::runtime_error("attention: head dim must be 32 or 64");
+}
+
+void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const float* lse, void* dqkv,
+                        float* delta, int B, int H, int N, int hd, float scale, const int64_t* rng, int site,
+                        double p, hipStream_t stream) {
+  const dim3 grid((N + 63) / 64, B * H);
+  const uint32_t thr = drop_threshold_host(p);
+  const float dsc = p > 0 ? 1.f / (1.f - (float)p) : 1.f;
+  const bf16* d = reinterpret_cast<const bf16*>(dout);
+  const bf16* q = reinterpret_cast<const bf16*>(qkv);
+  const bf16* oo = reinterpret_cast<const bf16*>(o);
+  bf16* dq = reinterpret_cast<bf16*>(dqkv);
+  if (hd == 32) {
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<32>, grid, dim3(256), 0, stream, d, q, oo, lse, delta, dq, B, H, N, scale, rng, site, thr, dsc);
+    hipLaunchKernelGGL(attn_bwd_dkv_kernel<32>, grid, dim3(256), 0, stream, d, q, lse, delta, dq, B, H, N, scale, rng, site, thr, dsc);
+  } else if (hd == 64) {
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<64>, grid, dim3(256), 0, stream, d, q, oo, lse, delta, dq, B, H, N, scale, rng, site, thr, dsc);
+    hipLaunchKernelGGL(attn_bwd_dkv_kernel<64>, grid, dim3(256), 0, stream, d, q, lse, delta, dq, B, H, N, scale, rng, site, thr, dsc);
+  } else {
+    throw std::runtime_error("attention: head dim must be 32 or 64");
+  }
+}

@@ -1,0 +1,486 @@
+// TORCH_LIBRARY registrations for the ddim_cold_amd HIP kernels.
+//
+// Every op validates shapes / dtypes / contiguity / device on the host before
+// launching (a mis-shaped launch of a hand-written kernel can fault the GPU),
+// allocates its outputs through the PyTorch caching allocator (graph-capture
+// safe) and launches on the current HIP stream.  Op contracts are documented
+// (and implemented in plain PyTorch) in ddim_cold_amd/ops/reference.py.
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/core/DeviceGuard.h>
+
+#include "kernels.h"
+
+using at::Tensor;
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
+#define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
+#define CHECK_DT(x, dt) TORCH_CHECK((x).scalar_type() == (dt), #x " must be " #dt ", got ", (x).scalar_type())
+#define CHECK_IN(x, dt) \
+  CHECK_CUDA(x);        \
+  CHECK_CONTIG(x);      \
+  CHECK_DT(x, dt)
+
+constexpr auto F32 = at::kFloat;
+constexpr auto BF16 = at::kBFloat16;
+constexpr auto I64 = at::kLong;
+
+void check_rng(const Tensor& rng) {
+  CHECK_IN(rng, I64);
+  TORCH_CHECK(rng.numel() >= 2, "rng must hold {seed, step}");
+}
+
+void check_linear(const Tensor& a, const Tensor& w, int64_t K) {
+  TORCH_CHECK(a.dim() == 2 && w.dim() == 2, "linear operands must be 2-D");
+  TORCH_CHECK(a.size(1) == K && w.size(1) == K, "linear K mismatch");
+  TORCH_CHECK(K % 8 == 0, "K must be a multiple of 8 (16-B vector loads)");
+}
+
+GemmArgs nt_args(const Tensor& a, const Tensor& w) {
+  GemmArgs g;
+  g.A = a.data_ptr();
+  g.B = w.data_ptr();
+  g.M = (int)a.size(0);
+  g.N = (int)w.size(0);
+  g.K = (int)a.size(1);
+  g.lda = g.K;
+  g.ldb = g.K;
+  return g;
+}
+
+std::tuple<Tensor, Tensor> patch_embed_fwd(Tensor img, Tensor t, Tensor w_pe, Tensor b_pe, Tensor cls, Tensor pos,
+                                           Tensor temb, Tensor rng, int64_t site, double p, int64_t patch) {
+  CHECK_IN(img, F32); CHECK_IN(t, I64); CHECK_IN(w_pe, BF16); CHECK_IN(b_pe, F32);
+  CHECK_IN(cls, F32); CHECK_IN(pos, F32); CHECK_IN(temb, F32); check_rng(rng);
+  const c10::DeviceGuard guard(img.device());
+  TORCH_CHECK(img.dim() == 4, "img must be [B,C,H,W]");
+  const int B = img.size(0), C = img.size(1), H = img.size(2), W = img.size(3), P = patch;
+  TORCH_CHECK(H % P == 0 && W % P == 0, "image size must be divisible by patch");
+  const int D = w_pe.size(0), F = C * P * P;
+  TORCH_CHECK(w_pe.numel() == (int64_t)D * F, "patch-embed weight shape mismatch");
+  TORCH_CHECK(F % 8 == 0, "C*p*p must be a multiple of 8");
+  const int NP = (H / P) * (W / P), N = NP + 1;
+  TORCH_CHECK(pos.numel() == (int64_t)N * D && cls.numel() == D && b_pe.numel() == D, "embedding shapes");
+  TORCH_CHECK(temb.dim() == 2 && temb.size(1) == D, "time embedding shape");
+  TORCH_CHECK(t.numel() == B, "t must be [B]");
+  auto x = at::empty({B, N, D}, img.options());
+  auto patches = at::empty({(int64_t)B * NP, F}, img.options().dtype(BF16));
+  patchify_cls_launch(img.data_ptr<float>(), t.data_ptr<int64_t>(), cls.data_ptr<float>(), pos.data_ptr<float>(),
+                      temb.data_ptr<float>(), patches.data_ptr(), x.data_ptr<float>(), B, C, H, W, P, D,
+                      rng.data_ptr<int64_t>(), site, p, cur_stream());
+  GemmArgs g;
+  g.A = patches.data_ptr();
+  g.B = w_pe.data_ptr();
+  g.M = B * NP; g.N = D; g.K = F; g.lda = F; g.ldb = F;
+  g.C = x.data_ptr(); g.ldc = D;
+  g.bias = b_pe.data_ptr<float>();
+  g.rng = rng.data_ptr<int64_t>(); g.site_drop = site; g.p_drop = p;
+  g.tokens = NP; g.batch = B;
+  g.pos = pos.data_ptr<float>(); g.temb = temb.data_ptr<float>(); g.tsteps = t.data_ptr<int64_t>(); g.emb_dim = D;
+  gemm_nt(g, EPI_EMBED, cur_stream());
+  return {x, patches};
+}
+
+std::tuple<Tensor, Tensor, Tensor> layernorm_fwd(Tensor x, Tensor gamma, Tensor beta, double eps) {
+  CHECK_IN(x, F32); CHECK_IN(gamma, F32); CHECK_IN(beta, F32);
+  const c10::DeviceGuard guard(x.device());
+  const int D = x.size(-1);
+  const int M = x.numel() / D;
+  TORCH_CHECK(gamma.numel() == D && beta.numel() == D, "layernorm affine shape");
+  auto y = at::empty(x.sizes(), x.options().dtype(BF16));
+  auto mean = at::empty({M}, x.options());
+  auto rstd = at::empty({M}, x.options());
+  layernorm_fwd_launch(x.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(), y.data_ptr(),
+                       mean.data_ptr<float>(), rstd.data_ptr<float>(), M, D, (float)eps, cur_stream());
+  return {y, mean, rstd};
+}
+
+Tensor qkv_fwd(Tensor a, Tensor w, Tensor b, int64_t B, int64_t N, int64_t H) {
+  CHECK_IN(a, BF16); CHECK_IN(w, BF16); CHECK_IN(b, F32);
+  const c10::DeviceGuard guard(a.device());
+  const int D = a.size(1);
+  check_linear(a, w, D);
+  TORCH_CHECK(w.size(0) == 3 * D && b.numel() == 3 * D && a.size(0) == B * N && D % H == 0, "qkv shapes");
+  auto out = at::empty({3, B, H, N, D / H}, a.options());
+  GemmArgs g = nt_args(a, w);
+  g.C = out.data_ptr(); g.ldc = 3 * D; g.bias = b.data_ptr<float>();
+  g.tokens = N; g.batch = B; g.heads = H; g.hd = D / H;
+  gemm_nt(g, EPI_QKV, cur_stream());
+  return out;
+}
+
+std::tuple<Tensor, Tensor> attn_fwd(Tensor qkv, double scale, Tensor rng, int64_t site, double p) {
+  CHECK_IN(qkv, BF16); check_rng(rng);
+  const c10::DeviceGuard guard(qkv.device());
+  TORCH_CHECK(qkv.dim() == 5 && qkv.size(0) == 3, "qkv must be [3,B,H,N,hd]");
+  const int B = qkv.size(1), H = qkv.size(2), N = qkv.size(3), hd = qkv.size(4);
+  TORCH_CHECK(hd == 32 || hd == 64, "head dim must be 32 or 64");
+  auto o = at::empty({B, N, H * hd}, qkv.options());
+  auto lse = at::empty({B, H, N}, qkv.options().dtype(F32));
+  attn_fwd_launch(qkv.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), B, H, N, hd, (float)scale,
+                  rng.data_ptr<int64_t>(), site, p, cur_stream());
+  return {o, lse};
+}
+
+Tensor linear_residual_fwd(Tensor a, Tensor w, Tensor b, Tensor x, int64_t N, Tensor rng, int64_t site_drop,
+                           double p_drop, int64_t site_dp, double p_dp) {
+  CHECK_IN(a, BF16); CHECK_IN(w, BF16); CHECK_IN(b, F32); CHECK_IN(x, F32); check_rng(rng);
+  const c10::DeviceGuard guard(a.device());
+  const int K = a.size(-1);
+  auto a2 = a.view({-1, K});
+  check_linear(a2, w, K);
+  const int M = a2.size(0), Dout = w.size(0);
+  TORCH_CHECK(x.numel() == (int64_t)M * Dout && b.numel() == Dout && M % N == 0, "residual shapes");
+  auto out = at::empty(x.sizes(), x.options());
+  GemmArgs g = nt_args(a2, w);
+  g.C = out.data_ptr(); g.ldc = Dout; g.bias = b.data_ptr<float>(); g.res = x.data_ptr<float>();
+  g.rng = rng.data_ptr<int64_t>(); g.site_drop = site_drop; g.p_drop = p_drop; g.site_dp = site_dp; g.p_dp = p_dp;
+  g.tokens = N;
+  gemm_nt(g, EPI_RESID, cur_stream());
+  return out;
+}
+
+std::tuple<Tensor, Tensor> linear_gelu_fwd(Tensor a, Tensor w, Tensor b, Tensor rng, int64_t site, double p) {
+  CHECK_IN(a, BF16); CHECK_IN(w, BF16); CHECK_IN(b, F32); check_rng(rng);
+  const c10::DeviceGuard guard(a.device());
+  const int K = a.size(-1);
+  auto a2 = a.view({-1, K});
+  check_linear(a2, w, K);
+  const int M = a2.size(0), Hm = w.size(0);
+  TORCH_CHECK(b.numel() == Hm, "bias shape");
+  auto u = at::empty({M, Hm}, a.options());
+  auto h = at::empty({M, Hm}, a.options());
+  GemmArgs g = nt_args(a2, w);
+  g.C = u.data_ptr(); g.ldc = Hm; g.C2 = h.data_ptr(); g.bias = b.data_ptr<float>();
+  g.rng = rng.data_ptr<int64_t>(); g.site_drop = site; g.p_drop = p;
+  gemm_nt(g, EPI_GELU, cur_stream());
+  return {u, h};
+}
+
+Tensor head_fwd(Tensor a, Tensor w, Tensor b, int64_t B, int64_t C, int64_t H, int64_t W, int64_t patch) {
+  CHECK_IN(a, BF16); CHECK_IN(w, BF16); CHECK_IN(b, F32);
+  const c10::DeviceGuard guard(a.device());
+  const int K = a.size(-1);
+  auto a2 = a.view({-1, K});
+  check_linear(a2, w, K);
+  const int N = (H / patch) * (W / patch) + 1;
+  TORCH_CHECK(a2.size(0) == B * N && w.size(0) == C * patch * patch && b.numel() == w.size(0), "head shapes");
+  auto img = at::empty({B, C, H, W}, a.options().dtype(F32));
+  GemmArgs g = nt_args(a2, w);
+  g.C = img.data_ptr(); g.bias = b.data_ptr<float>();
+  g.tokens = N; g.batch = B; g.chans = C; g.img_h = H; g.img_w = W; g.patch = patch;
+  gemm_nt(g, EPI_HEAD, cur_stream());
+  return img;
+}
+
+std::tuple<Tensor, Tensor> smooth_l1_fwd_bwd(Tensor pred, Tensor target, int64_t N, int64_t patch, double beta) {
+  CHECK_IN(pred, F32); CHECK_IN(target, F32);
+  const c10::DeviceGuard guard(pred.device());
+  TORCH_CHECK(pred.sizes() == target.sizes() && pred.dim() == 4, "pred/target shape");
+  const int B = pred.size(0), C = pred.size(1), H = pred.size(2), W = pred.size(3);
+  TORCH_CHECK(N == (H / patch) * (W / patch) + 1, "token count");
+  auto loss = at::zeros({1}, pred.options());
+  auto dtok = at::empty({(int64_t)B * N, C * patch * patch}, pred.options().dtype(BF16));
+  smooth_l1_launch(pred.data_ptr<float>(), target.data_ptr<float>(), loss.data_ptr<float>(), dtok.data_ptr(), B, C,
+                   H, W, patch, (float)beta, cur_stream());
+  return {loss, dtok};
+}
+
+Tensor img_to_tokgrad(Tensor dimg, int64_t N, int64_t patch) {
+  CHECK_IN(dimg, F32);
+  const c10::DeviceGuard guard(dimg.device());
+  const int B = dimg.size(0), C = dimg.size(1), H = dimg.size(2), W = dimg.size(3);
+  TORCH_CHECK(N == (H / patch) * (W / patch) + 1, "token count");
+  auto dtok = at::empty({(int64_t)B * N, C * patch * patch}, dimg.options().dtype(BF16));
+  img_to_tokgrad_launch(dimg.data_ptr<float>(), dtok.data_ptr(), B, C, H, W, patch, cur_stream());
+  return dtok;
+}
+
+Tensor linear_dgrad(Tensor dy, Tensor w, bool out_fp32) {
+  CHECK_IN(dy, BF16); CHECK_IN(w, BF16);
+  const c10::DeviceGuard guard(dy.device());
+  TORCH_CHECK(dy.dim() == 2 && w.dim() == 2 && dy.size(1) == w.size(0), "dgrad shapes");
+  const int M = dy.size(0), Nout = w.size(0), K = w.size(1);
+  TORCH_CHECK(Nout % 8 == 0 && K % 8 == 0, "dgrad dims must be multiples of 8");
+  auto dx = at::empty({M, K}, dy.options().dtype(out_fp32 ? F32 : BF16));
+  GemmArgs g;
+  g.A = dy.data_ptr(); g.B = w.data_ptr();
+  g.M = M; g.N = K; g.K = Nout; g.lda = Nout; g.ldb = K;
+  g.C = dx.data_ptr(); g.ldc = K;
+  gemm_dgrad(g, out_fp32 ? EPI_F32 : EPI_BF16, cur_stream());
+  return dx;
+}
+
+Tensor linear_dgrad_gelu(Tensor dy, Tensor w, Tensor u, Tensor rng, int64_t site, double p) {
+  CHECK_IN(dy, BF16); CHECK_IN(w, BF16); CHECK_IN(u, BF16); check_rng(rng);
+  const c10::DeviceGuard guard(dy.device());
+  TORCH_CHECK(dy.dim() == 2 && w.dim() == 2 && dy.size(1) == w.size(0), "dgrad shapes");
+  const int M = dy.size(0), Nout = w.size(0), K = w.size(1);
+  TORCH_CHECK(u.numel() == (int64_t)M * K, "u shape");
+  TORCH_CHECK(Nout % 8 == 0 && K % 8 == 0, "dgrad dims must be multiples of 8");
+  auto du = at::empty({M, K}, dy.options());
+  GemmArgs g;
+  g.A = dy.data_ptr(); g.B = w.data_ptr();
+  g.M = M; g.N = K; g.K = Nout; g.lda = Nout; g.ldb = K;
+  g.C = du.data_ptr(); g.ldc = K; g.aux = u.data_ptr();
+  g.rng = rng.data_ptr<int64_t>(); g.site_drop = site; g.p_drop = p;
+  gemm_dgrad(g, EPI_DGELU, cur_stream());
+  return du;
+}
+
+void linear_wgrad(Tensor dy, Tensor x, Tensor dw, c10::optional<Tensor> db) {
+  CHECK_IN(dy, BF16); CHECK_IN(x, BF16); CHECK_IN(dw, F32);
+  const c10::DeviceGuard guard(dy.device());
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0), "wgrad shapes");
+  const int M = dy.size(0), Nout = dy.size(1), K = x.size(1);
+  TORCH_CHECK(dw.numel() == (int64_t)Nout * K, "dw shape");
+  TORCH_CHECK(Nout % 8 == 0 && K % 8 == 0, "wgrad dims must be multiples of 8");
+  float* dbp = nullptr;
+  if (db.has_value() && db->defined()) {
+    CHECK_IN((*db), F32);
+    TORCH_CHECK(db->numel() == Nout, "db shape");
+    dbp = db->data_ptr<float>();
+  }
+  GemmArgs g;
+  g.A = dy.data_ptr(); g.B = x.data_ptr();
+  g.M = Nout; g.N = K; g.K = M; g.lda = Nout; g.ldb = K;
+  g.C = dw.data_ptr(); g.ldc = K; g.bias = dbp;
+  // split the token reduction so the grid fills the chip (fp32 atomics combine slices)
+  const int tiles = ((Nout + 63) / 64) * ((K + 63) / 64);
+  const int kt = (M + 63) / 64;
+  int splits = (512 + tiles - 1) / tiles;
+  if (splits > kt) splits = kt;
+  if (splits < 1) splits = 1;
+  gemm_wgrad(g, splits, cur_stream());
+}
+
+std::tuple<Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma,
+                                         c10::optional<Tensor> g_res, Tensor dgamma, Tensor dbeta, int64_t N,
+                                         Tensor rng, int64_t site_drop, double p_drop, int64_t site_dp, double p_dp,
+                                         bool emit_gy) {
+  CHECK_IN(dy, F32); CHECK_IN(x, F32); CHECK_IN(mean, F32); CHECK_IN(rstd, F32); CHECK_IN(gamma, F32);
+  CHECK_IN(dgamma, F32); CHECK_IN(dbeta, F32); check_rng(rng);
+  const c10::DeviceGuard guard(x.device());
+  const int D = x.size(-1), M = x.numel() / D;
+  TORCH_CHECK(dy.numel() == x.numel() && mean.numel() == M && rstd.numel() == M && gamma.numel() == D &&
+                  dgamma.numel() == D && dbeta.numel() == D && M % N == 0,
+              "layernorm_bwd shapes");
+  const float* gr = nullptr;
+  if (g_res.has_value() && g_res->defined()) {
+    CHECK_IN((*g_res), F32);
+    TORCH_CHECK(g_res->numel() == x.numel(), "g_res shape");
+    gr = g_res->data_ptr<float>();
+  }
+  auto g_out = at::empty(x.sizes(), x.options());
+  Tensor gy = emit_gy ? at::empty({M, D}, x.options().dtype(BF16)) : at::empty({0}, x.options().dtype(BF16));
+  layernorm_bwd_launch(dy.data_ptr<float>(), x.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                       gamma.data_ptr<float>(), gr, g_out.data_ptr<float>(), emit_gy ? gy.data_ptr() : nullptr,
+                       dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), M, D, N, rng.data_ptr<int64_t>(),
+                       site_drop, p_drop, site_dp, p_dp, cur_stream());
+  return {g_out, gy};
+}
+
+Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, double scale, Tensor rng, int64_t site, double p) {
+  CHECK_IN(dout, BF16); CHECK_IN(qkv, BF16); CHECK_IN(o, BF16); CHECK_IN(lse, F32); check_rng(rng);
+  const c10::DeviceGuard guard(qkv.device());
+  TORCH_CHECK(qkv.dim() == 5 && qkv.size(0) == 3, "qkv must be [3,B,H,N,hd]");
+  const int B = qkv.size(1), H = qkv.size(2), N = qkv.size(3), hd = qkv.size(4);
+  TORCH_CHECK(hd == 32 || hd == 64, "head dim must be 32 or 64");
+  TORCH_CHECK(dout.numel() == (int64_t)B * N * H * hd && o.numel() == dout.numel() &&
+                  lse.numel() == (int64_t)B * H * N,
+              "attn_bwd shapes");
+  auto dqkv = at::empty({(int64_t)B * N, 3 * H * hd}, qkv.options());
+  auto delta = at::empty({(int64_t)B * H * N}, lse.options());
+  attn_bwd_launch(dout.data_ptr(), qkv.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), dqkv.data_ptr(),
+                  delta.data_ptr<float>(), B, H, N, hd, (float)scale, rng.data_ptr<int64_t>(), site, p,
+                  cur_stream());
+  return dqkv;
+}
+
+Tensor embed_bwd(Tensor g, Tensor t, Tensor rng, int64_t site, double p, Tensor dcls, Tensor dpos, Tensor dtemb) {
+  CHECK_IN(g, F32); CHECK_IN(t, I64); check_rng(rng); CHECK_IN(dcls, F32); CHECK_IN(dpos, F32); CHECK_IN(dtemb, F32);
+  const c10::DeviceGuard guard(g.device());
+  TORCH_CHECK(g.dim() == 3, "g must be [B,N,D]");
+  const int B = g.size(0), N = g.size(1), D = g.size(2);
+  TORCH_CHECK(t.numel() == B && dcls.numel() == D && dpos.numel() == (int64_t)N * D && dtemb.size(-1) == D,
+              "embed_bwd shapes");
+  auto gpatch = at::empty({(int64_t)B * (N - 1), D}, g.options().dtype(BF16));
+  embed_bwd_launch(g.data_ptr<float>(), t.data_ptr<int64_t>(), dcls.data_ptr<float>(), dpos.data_ptr<float>(),
+                   dtemb.data_ptr<float>(), gpatch.data_ptr(), B, N, D, rng.data_ptr<int64_t>(), site, p,
+                   cur_stream());
+  return gpatch;
+}
+
+void sqnorm(Tensor g, Tensor out, double scale) {
+  CHECK_IN(g, F32); CHECK_IN(out, F32);
+  const c10::DeviceGuard guard(g.device());
+  sqnorm_launch(g.data_ptr<float>(), g.numel(), out.data_ptr<float>(), (float)scale, cur_stream());
+}
+
+void adamw_step(Tensor p, Tensor g, Tensor m, Tensor v, c10::optional<Tensor> pbf, Tensor sq, Tensor step,
+                Tensor hyper, double grad_scale) {
+  CHECK_IN(p, F32); CHECK_IN(g, F32); CHECK_IN(m, F32); CHECK_IN(v, F32); CHECK_IN(sq, F32); CHECK_IN(step, I64);
+  CHECK_IN(hyper, F32);
+  const c10::DeviceGuard guard(p.device());
+  const int64_t n = p.numel();
+  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n && hyper.numel() >= 8 && step.numel() >= 2,
+              "adamw shapes");
+  void* pb = nullptr;
+  if (pbf.has_value() && pbf->defined()) {
+    CHECK_IN((*pbf), BF16);
+    TORCH_CHECK(pbf->numel() == n, "bf16 shadow size");
+    pb = pbf->data_ptr();
+  }
+  adamw_launch(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), pb, n,
+               sq.data_ptr<float>(), step.data_ptr<int64_t>(), hyper.data_ptr<float>(), (float)grad_scale,
+               cur_stream());
+}
+
+void advance_counters(Tensor step, Tensor rng, c10::optional<Tensor> sq) {
+  CHECK_IN(step, I64); check_rng(rng);
+  const c10::DeviceGuard guard(step.device());
+  const float* s = nullptr;
+  if (sq.has_value() && sq->defined()) {
+    CHECK_IN((*sq), F32);
+    s = sq->data_ptr<float>();
+  }
+  advance_counters_launch(step.data_ptr<int64_t>(), rng.data_ptr<int64_t>(), s, cur_stream());
+}
+
+std::tuple<Tensor, Tensor> ddim_step(Tensor x_t, Tensor x0_raw, Tensor coef) {
+  CHECK_IN(x_t, F32); CHECK_IN(x0_raw, F32); CHECK_IN(coef, F32);
+  const c10::DeviceGuard guard(x_t.device());
+  TORCH_CHECK(x_t.numel() == x0_raw.numel() && coef.numel() >= 4, "ddim_step shapes");
+  auto xn = at::empty_like(x_t);
+  auto x0 = at::empty_like(x_t);
+  ddim_step_launch(x_t.data_ptr<float>(), x0_raw.data_ptr<float>(), xn.data_ptr<float>(), x0.data_ptr<float>(),
+                   coef.data_ptr<float>(), x_t.numel(), cur_stream());
+  return {xn, x0};
+}
+
+void ddim_step_(Tensor x, Tensor x0_raw, Tensor x0_out, Tensor coef) {
+  CHECK_IN(x, F32); CHECK_IN(x0_raw, F32); CHECK_IN(x0_out, F32); CHECK_IN(coef, F32);
+  const c10::DeviceGuard guard(x.device());
+  TORCH_CHECK(x.numel() == x0_raw.numel() && x0_out.numel() == x.numel() && coef.numel() >= 4, "ddim_step_ shapes");
+  ddim_step_launch(x.data_ptr<float>(), x0_raw.data_ptr<float>(), x.data_ptr<float>(), x0_out.data_ptr<float>(),
+                   coef.data_ptr<float>(), x.numel(), cur_stream());
+}
+
+void randn_(Tensor out, Tensor rng, int64_t site) {
+  CHECK_IN(out, F32); check_rng(rng);
+  const c10::DeviceGuard guard(out.device());
+  randn_launch(out.data_ptr<float>(), out.numel(), rng.data_ptr<int64_t>(), site, cur_stream());
+}
+
+Tensor q_sample(Tensor x0, Tensor t, Tensor eps, int64_t total_steps) {
+  CHECK_IN(x0, F32); CHECK_IN(t, I64); CHECK_IN(eps, F32);
+  const c10::DeviceGuard guard(x0.device());
+  TORCH_CHECK(x0.sizes() == eps.sizes() && t.numel() == x0.size(0), "q_sample shapes");
+  auto out = at::empty_like(x0);
+  const int B = x0.size(0);
+  q_sample_launch(x0.data_ptr<float>(), t.data_ptr<int64_t>(), eps.data_ptr<float>(), out.data_ptr<float>(), B,
+                  x0.numel() / B, total_steps, cur_stream());
+  return out;
+}
+
+std::tuple<Tensor, Tensor> pixelate_pair(Tensor img, c10::optional<Tensor> idx, Tensor t, int64_t B) {
+  CHECK_IN(img, F32); CHECK_IN(t, I64);
+  const c10::DeviceGuard guard(img.device());
+  TORCH_CHECK(img.dim() == 4 && t.numel() == B, "pixelate shapes");
+  const int64_t* ip = nullptr;
+  if (idx.has_value() && idx->defined()) {
+    CHECK_IN((*idx), I64);
+    TORCH_CHECK(idx->numel() == B, "idx shape");
+    ip = idx->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(img.size(0) == B, "img batch");
+  }
+  const int C = img.size(1), H = img.size(2), W = img.size(3);
+  auto xt = at::empty({B, C, H, W}, img.options());
+  auto xtm1 = at::empty({B, C, H, W}, img.options());
+  pixelate_pair_launch(img.data_ptr<float>(), ip, t.data_ptr<int64_t>(), xt.data_ptr<float>(), xtm1.data_ptr<float>(),
+                       B, C, H, W, cur_stream());
+  return {xt, xtm1};
+}
+
+void cold_batch(Tensor pool, Tensor rng, int64_t site, Tensor x_t, Tensor x_tm1, Tensor t, Tensor idx_ws,
+                int64_t max_t) {
+  CHECK_IN(pool, F32); check_rng(rng); CHECK_IN(x_t, F32); CHECK_IN(x_tm1, F32); CHECK_IN(t, I64);
+  CHECK_IN(idx_ws, I64);
+  const c10::DeviceGuard guard(pool.device());
+  const int B = x_t.size(0), C = x_t.size(1), H = x_t.size(2), W = x_t.size(3);
+  TORCH_CHECK(pool.dim() == 4 && pool.size(1) == C && pool.size(2) == H && pool.size(3) == W, "pool shape");
+  TORCH_CHECK(x_tm1.sizes() == x_t.sizes() && t.numel() == B && idx_ws.numel() == B, "cold_batch shapes");
+  TORCH_CHECK(max_t >= 1 && (1 << max_t) <= W, "max_t");
+  cold_batch_launch(pool.data_ptr<float>(), pool.size(0), rng.data_ptr<int64_t>(), site, x_t.data_ptr<float>(),
+                    x_tm1.data_ptr<float>(), t.data_ptr<int64_t>(), idx_ws.data_ptr<int64_t>(), B, C, H, W, max_t,
+                    cur_stream());
+}
+
+}  // namespace
+
+TORCH_LIBRARY(ddim_cold, m) {
+  m.def("patch_embed_fwd(Tensor img, Tensor t, Tensor w_pe, Tensor b_pe, Tensor cls, Tensor pos, Tensor temb, "
+        "Tensor rng, int site, float p, int patch) -> (Tensor, Tensor)");
+  m.def("layernorm_fwd(Tensor x, Tensor gamma, Tensor beta, float eps) -> (Tensor, Tensor, Tensor)");
+  m.def("qkv_fwd(Tensor a, Tensor w, Tensor b, int B, int N, int H) -> Tensor");
+  m.def("attn_fwd(Tensor qkv, float scale, Tensor rng, int site, float p) -> (Tensor, Tensor)");
+  m.def("linear_residual_fwd(Tensor a, Tensor w, Tensor b, Tensor x, int N, Tensor rng, int site_drop, "
+        "float p_drop, int site_dp, float p_dp) -> Tensor");
+  m.def("linear_gelu_fwd(Tensor a, Tensor w, Tensor b, Tensor rng, int site, float p) -> (Tensor, Tensor)");
+  m.def("head_fwd(Tensor a, Tensor w, Tensor b, int B, int C, int H, int W, int patch) -> Tensor");
+  m.def("smooth_l1_fwd_bwd(Tensor pred, Tensor target, int N, int patch, float beta) -> (Tensor, Tensor)");
+  m.def("img_to_tokgrad(Tensor dimg, int N, int patch) -> Tensor");
+  m.def("linear_dgrad(Tensor dy, Tensor w, bool out_fp32) -> Tensor");
+  m.def("linear_dgrad_gelu(Tensor dy, Tensor w, Tensor u, Tensor rng, int site, float p) -> Tensor");
+  m.def("linear_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, Tensor(b!)? db) -> ()");
+  m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor? g_res, "
+        "Tensor(a!) dgamma, Tensor(b!) dbeta, int N, Tensor rng, int site_drop, float p_drop, int site_dp, "
+        "float p_dp, bool emit_gy) -> (Tensor, Tensor)");
+  m.def("attn_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, float scale, Tensor rng, int site, float p) -> Tensor");
+  m.def("embed_bwd(Tensor g, Tensor t, Tensor rng, int site, float p, Tensor(a!) dcls, Tensor(b!) dpos, "
+        "Tensor(c!) dtemb) -> Tensor");
+  m.def("sqnorm(Tensor g, Tensor(a!) out, float scale) -> ()");
+  m.def("adamw_step(Tensor(a!) p, Tensor(b!) g, Tensor(c!) m, Tensor(d!) v, Tensor(e!)? pbf, Tensor sq, "
+        "Tensor step, Tensor hyper, float grad_scale) -> ()");
+  m.def("advance_counters(Tensor(a!) step, Tensor(b!) rng, Tensor? sq) -> ()");
+  m.def("ddim_step(Tensor x_t, Tensor x0_raw, Tensor coef) -> (Tensor, Tensor)");
+  m.def("ddim_step_(Tensor(a!) x, Tensor x0_raw, Tensor(b!) x0_out, Tensor coef) -> ()");
+  m.def("randn_(Tensor(a!) out, Tensor rng, int site) -> ()");
+  m.def("q_sample(Tensor x0, Tensor t, Tensor eps, int total_steps) -> Tensor");
+  m.def("pixelate_pair(Tensor img, Tensor? idx, Tensor t, int B) -> (Tensor, Tensor)");
+  m.def("cold_batch(Tensor pool, Tensor rng, int site, Tensor(a!) x_t, Tensor(b!) x_tm1, Tensor(c!) t, "
+        "Tensor(d!) idx_ws, int max_t) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
+  m.impl("patch_embed_fwd", &patch_embed_fwd);
+  m.impl("layernorm_fwd", &layernorm_fwd);
+  m.impl("qkv_fwd", &qkv_fwd);
+  m.impl("attn_fwd", &attn_fwd);
+  m.impl("linear_residual_fwd", &linear_residual_fwd);
+  m.impl("linear_gelu_fwd", &linear_gelu_fwd);
+  m.impl("head_fwd", &head_fwd);
+  m.impl("smooth_l1_fwd_bwd", &smooth_l1_fwd_bwd);
+  m.impl("img_to_tokgrad", &img_to_tokgrad);
+  m.impl("linear_dgrad", &linear_dgrad);
+  m.impl("linear_dgrad_gelu", &linear_dgrad_gelu);
+  m.impl("linear_wgrad", &linear_wgrad);
+  m.impl("layernorm_bwd", &layernorm_bwd);
+  m.impl("attn_bwd", &attn_bwd);
+  m.impl("embed_bwd", &embed_bwd);
+  m.impl("sqnorm", &sqnorm);
+  m.impl("adamw_step", &adamw_step);
+  m.impl("advance_counters", &advance_counters);
+  m.impl("ddim_step", &ddim_step);
+  m.impl("ddim_step_", &ddim_step_);
+  m.impl("randn_", &randn_);
+  m.impl("q_sample", &q_sample);
+  m.impl("pixelate_pair", &pixelate_pair);
+  m.impl("cold_batch", &cold_batch);
+}

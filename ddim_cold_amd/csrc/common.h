@@ -1,0 +1,111 @@
+// Common gfx950 (CDNA4) device helpers for the ddim_cold_amd kernels.
+//
+// * bf16 storage as __bf16, fp32 math/accumulation.
+// * MFMA fragment types for v_mfma_f32_16x16x32_bf16 (wave64: lane l holds
+//   A[row l&15][k 8(l>>4)+j] / B[k][col l&15]; C/D col = l&15,
+//   row = 4(l>>4)+reg).
+// * Counter-based dropout hash — bit-identical to
+//   ddim_cold_amd/ops/reference.py (keep_mask / site_salt).  Masks are never
+//   stored: forward and backward regenerate them from (seed, step, site, idx),
+//   and (seed, step) are read from device memory so graph replays draw fresh
+//   masks every step.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dc {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+#define DC_LDS __attribute__((address_space(3)))
+
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// ds_read_b64_tr_b16: per 16-lane group, lane 4q+p addresses row q cols 4p..4p+3
+// of a 4x16 block; lane i receives column i (4 rows) -> elements 0..3.
+__device__ __forceinline__ bf16x4 lds_read_tr(const bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((DC_LDS bf16x4*)(p));
+}
+
+// MFMA operand fragment from a transposed LDS image [k rows][cols] (row stride
+// STRIDE bytes): operand rows c0..c0+15, permuted k order
+//   element j of lane group g <-> k = 32s + (j<4 ? 4g+j : 16+4g+(j-4)).
+template <int STRIDE>
+__device__ __forceinline__ bf16x8 frag_t(const char* lds, int c0, int s, int lane) {
+  const int i = lane & 15, g = lane >> 4, q = i >> 2, p = i & 3;
+  const int ra = 32 * s + 4 * g + q;
+  const char* pa = lds + ra * STRIDE + (c0 + 4 * p) * 2;
+  const bf16x4 lo = lds_read_tr(reinterpret_cast<const bf16*>(pa));
+  const bf16x4 hi = lds_read_tr(reinterpret_cast<const bf16*>(pa + 16 * STRIDE));
+  bf16x8 v;
+  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  return v;
+}
+
+// ----------------------------------------------------------------------------- RNG
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+// rng = device pointer to int64[2] = {seed, step}
+__device__ __forceinline__ uint32_t site_salt(const int64_t* rng, int site) {
+  const uint64_t seed = (uint64_t)rng[0];
+  const uint64_t step = (uint64_t)rng[1];
+  const uint32_t s_lo = (uint32_t)seed, s_hi = (uint32_t)(seed >> 32);
+  const uint32_t a = mix32((uint32_t)step * 0x9E3779B9u + s_hi);
+  const uint32_t b = mix32(s_lo ^ a);
+  return mix32(b + (uint32_t)site * 0x85EBCA6Bu);
+}
+
+__device__ __forceinline__ bool dropout_keep(uint32_t salt, uint32_t idx, uint32_t thresh) {
+  return mix32((idx * 0x9E3779B1u) ^ salt) >= thresh;
+}
+
+inline uint32_t drop_threshold_host(double p) {
+  double v = p * 4294967296.0 + 0.5;
+  if (v >= 4294967295.0) return 0xFFFFFFFFu;
+  if (v <= 0.0) return 0u;
+  return (uint32_t)v;
+}
+
+// ----------------------------------------------------------------------------- reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ float gelu_f(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = __expf(-0.5f * x * x) * 0.39894228040143268f;
+  return cdf + x * pdf;
+}
+
+inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+}  // namespace dc

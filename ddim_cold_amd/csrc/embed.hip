@@ -1,0 +1,175 @@
+// Patch-embedding front end, embedding backward, and the smooth-L1 loss.
+//
+//  * patchify_cls: NCHW fp32 image -> conv-im2col rows [B*P, C*p*p] bf16 (the A
+//    operand of the patch-embed MFMA GEMM, whose EPI_EMBED epilogue adds
+//    bias + pos_embed + time_embed[t] + dropout and scatters to token rows);
+//    the same launch writes the cls rows  x[b,0,:] = Dropout(cls + pos[0] + temb[t_b]).
+//    (ViT.py:150-155 PatchEmbed, ViT.py:199-206 prepare_tokens)
+//  * embed_bwd: grads of cls/pos/time embeddings + patch-row grad for the conv
+//    weight-gradient GEMM (pos_drop mask regenerated).
+//  * smooth_l1: mean smooth-L1 (multi_gpu_trainer.py:124) fused with its
+//    gradient, written straight into the token layout the head backward GEMMs
+//    read (inverse of the head's unpatchify; cls rows zero).
+#include "common.h"
+#include "kernels.h"
+
+namespace dc {
+
+__global__ __launch_bounds__(256) void patchify_cls_kernel(const float* __restrict__ img, const int64_t* __restrict__ t,
+                                                           const float* __restrict__ cls, const float* __restrict__ pos,
+                                                           const float* __restrict__ temb, bf16* __restrict__ patches,
+                                                           float* __restrict__ x, int B, int C, int H, int W, int P,
+                                                           int D, const int64_t* __restrict__ rng, int site,
+                                                           uint32_t thr, float dsc) {
+  const int Hp = H / P, Wp = W / P, NP = Hp * Wp, F = C * P * P;
+  const size_t n_patch = (size_t)B * NP * F;
+  const size_t n_cls = (size_t)B * D;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < n_patch + n_cls;
+       e += (size_t)gridDim.x * blockDim.x) {
+    if (e < n_patch) {
+      const int k = (int)(e % F);
+      const size_t row = e / F;
+      const int b = (int)(row / NP), pidx = (int)(row % NP);
+      const int hp = pidx / Wp, wp = pidx - hp * Wp;
+      const int c = k / (P * P), ij = k - c * P * P, i = ij / P, j = ij - i * P;
+      patches[e] = f2bf(img[(((size_t)b * C + c) * H + hp * P + i) * W + wp * P + j]);
+    } else {
+      const size_t e2 = e - n_patch;
+      const int b = (int)(e2 / D), d = (int)(e2 % D);
+      float v = cls[d] + pos[d] + temb[(size_t)t[b] * D + d];
+      const size_t idx = (size_t)b * (NP + 1) * D + d;
+      if (thr) v = dropout_keep(site_salt(rng, site), (uint32_t)idx, thr) ? v * dsc : 0.f;
+      x[idx] = v;
+    }
+  }
+}
+
+// part A: (n,d) -> dpos (+dcls) ; part B: (b,d) -> dtemb[t_b] ; part C: patch-row grads (bf16)
+__global__ __launch_bounds__(256) void embed_bwd_kernel(const float* __restrict__ g, const int64_t* __restrict__ t,
+                                                        float* __restrict__ dcls, float* __restrict__ dpos,
+                                                        float* __restrict__ dtemb, bf16* __restrict__ gpatch, int B,
+                                                        int N, int D, const int64_t* __restrict__ rng, int site,
+                                                        uint32_t thr, float dsc, int blocksA, int blocksB) {
+  const uint32_t salt = thr ? site_salt(rng, site) : 0u;
+  auto gm = [&](size_t idx) -> float {
+    const float v = g[idx];
+    if (!thr) return v;
+    return dropout_keep(salt, (uint32_t)idx, thr) ? v * dsc : 0.f;
+  };
+  const int bid = blockIdx.x;
+  if (bid < blocksA) {
+    const int e = bid * 256 + threadIdx.x;
+    if (e >= N * D) return;
+    const int n = e / D, d = e - n * D;
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += gm(((size_t)b * N + n) * D + d);
+    dpos[e] += s;
+    if (n == 0) dcls[d] += s;
+  } else if (bid < blocksA + blocksB) {
+    const int e = (bid - blocksA) * 256 + threadIdx.x;
+    if (e >= B * D) return;
+    const int b = e / D, d = e - b * D;
+    float s = 0.f;
+    for (int n = 0; n < N; ++n) s += gm(((size_t)b * N + n) * D + d);
+    atomicAdd(dtemb + (size_t)t[b] * D + d, s);
+  } else {
+    const size_t total = (size_t)B * (N - 1) * D;
+    for (size_t e = (size_t)(bid - blocksA - blocksB) * 256 + threadIdx.x; e < total;
+         e += (size_t)(gridDim.x - blocksA - blocksB) * 256) {
+      const size_t row = e / D;
+      const int d = (int)(e - row * D);
+      const int b = (int)(row / (N - 1)), i = (int)(row % (N - 1));
+      gpatch[e] = f2bf(gm(((size_t)b * N + 1 + i) * D + d));
+    }
+  }
+}
+
+template <bool LOSS>
+__global__ __launch_bounds__(256) void tokgrad_kernel(const float* __restrict__ pred, const float* __restrict__ target,
+                                                      float* __restrict__ loss, bf16* __restrict__ dtok, int B, int C,
+                                                      int H, int W, int P, float beta, float inv_numel) {
+  __shared__ float red[4];
+  const int Wp = W / P, NP = (H / P) * Wp, N = NP + 1, F = C * P * P;
+  const size_t n_img = (size_t)B * C * H * W;
+  const size_t n_cls = (size_t)B * F;
+  float acc = 0.f;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < n_img + n_cls;
+       e += (size_t)gridDim.x * blockDim.x) {
+    if (e < n_img) {
+      const int xw = (int)(e % W);
+      size_t r = e / W;
+      const int yh = (int)(r % H);
+      r /= H;
+      const int c = (int)(r % C);
+      const int b = (int)(r / C);
+      float gv;
+      if (LOSS) {
+        const float d = pred[e] - target[e];
+        const float ad = fabsf(d);
+        acc += ad < beta ? 0.5f * d * d / beta : ad - 0.5f * beta;
+        gv = fminf(fmaxf(d / beta, -1.f), 1.f) * inv_numel;
+      } else {
+        gv = pred[e];
+      }
+      const int hp = yh / P, a = yh - hp * P, wp = xw / P, bb = xw - wp * P;
+      const int tok = 1 + hp * Wp + wp;
+      const int f = (a * P + bb) * C + c;
+      dtok[((size_t)b * N + tok) * F + f] = f2bf(gv);
+    } else {
+      const size_t e2 = e - n_img;
+      const int b = (int)(e2 / F), f = (int)(e2 % F);
+      dtok[(size_t)b * N * F + f] = f2bf(0.f);
+    }
+  }
+  if (LOSS) {
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(loss, (red[0] + red[1] + red[2] + red[3]) * inv_numel);
+  }
+}
+
+static int grid_for(size_t n) {
+  size_t g = (n + 255) / 256;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace dc
+
+using namespace dc;
+
+void patchify_cls_launch(const float* img, const int64_t* t, const float* cls, const float* pos, const float* temb,
+                         void* patches, float* x, int B, int C, int H, int W, int patch, int D, const int64_t* rng,
+                         int site, double p, hipStream_t stream) {
+  const size_t n = (size_t)B * (H / patch) * (W / patch) * C * patch * patch + (size_t)B * D;
+  const uint32_t thr = drop_threshold_host(p);
+  const float dsc = p > 0 ? 1.f / (1.f - (float)p) : 1.f;
+  hipLaunchKernelGGL(patchify_cls_kernel, dim3(grid_for(n)), dim3(256), 0, stream, img, t, cls, pos, temb,
+                     reinterpret_cast<bf16*>(patches), x, B, C, H, W, patch, D, rng, site, thr, dsc);
+}
+
+void embed_bwd_launch(const float* g, const int64_t* t, float* dcls, float* dpos, float* dtemb, void* gpatch, int B,
+                      int N, int D, const int64_t* rng, int site, double p, hipStream_t stream) {
+  const int blocksA = cdiv(N * D, 256), blocksB = cdiv(B * D, 256);
+  const int blocksC = grid_for((size_t)B * (N - 1) * D);
+  const uint32_t thr = drop_threshold_host(p);
+  const float dsc = p > 0 ? 1.f / (1.f - (float)p) : 1.f;
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3(blocksA + blocksB + blocksC), dim3(256), 0, stream, g, t, dcls, dpos,
+                     dtemb, reinterpret_cast<bf16*>(gpatch), B, N, D, rng, site, thr, dsc, blocksA, blocksB);
+}
+
+void smooth_l1_launch(const float* pred, const float* target, float* loss, void* dtok, int B, int C, int H, int W,
+                      int patch, float beta, hipStream_t stream) {
+  const size_t n_img = (size_t)B * C * H * W;
+  const size_t n = n_img + (size_t)B * C * patch * patch;
+  hipLaunchKernelGGL(tokgrad_kernel<true>, dim3(grid_for(n)), dim3(256), 0, stream, pred, target, loss,
+                     reinterpret_cast<bf16*>(dtok), B, C, H, W, patch, beta, 1.0f / (float)n_img);
+}
+
+void img_to_tokgrad_launch(const float* dimg, void* dtok, int B, int C, int H, int W, int patch, hipStream_t stream) {
+  const size_t n = (size_t)B * C * H * W + (size_t)B * C * patch * patch;
+  hipLaunchKernelGGL(tokgrad_kernel<false>, dim3(grid_for(n)), dim3(256), 0, stream, dimg, nullptr, nullptr,
+                     reinterpret_cast<bf16*>(dtok), B, C, H, W, patch, 1.f, 1.f);
+}

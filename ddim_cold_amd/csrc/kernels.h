@@ -1,0 +1,88 @@
+// Host-side launch API of the ddim_cold_amd HIP kernels (no torch headers here,
+// so the .hip translation units compile fast; bindings.cpp adapts tensors).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdexcept>
+
+enum GemmEpi : int {
+  EPI_BF16 = 0,    // C bf16 = acc (+bias)
+  EPI_F32 = 1,     // C f32 = acc (+bias)
+  EPI_QKV = 2,     // +bias, scatter to head-major [3,B,H,N,hd] bf16
+  EPI_RESID = 3,   // C f32 = res + DropPath(Dropout(acc+bias))
+  EPI_GELU = 4,    // C = u = acc+bias (bf16) ; C2 = h = Dropout(GELU(u)) (bf16)
+  EPI_HEAD = 5,    // +bias, unpatchify token rows into a [B,C,H,W] f32 image
+  EPI_EMBED = 6,   // patch rows -> token rows: +bias +pos +temb[t], Dropout, f32
+  EPI_DGELU = 7,   // C bf16 = Dropout(acc) * GELU'(aux)
+  EPI_ATOMIC = 8,  // C f32 += acc (split-K / gradient accumulate) ; bias -> fused column sum
+};
+
+struct GemmArgs {
+  const void* A = nullptr;
+  const void* B = nullptr;
+  int M = 0, N = 0, K = 0, lda = 0, ldb = 0;
+  void* C = nullptr;
+  int ldc = 0;
+  const float* bias = nullptr;
+  const float* res = nullptr;
+  void* C2 = nullptr;
+  const void* aux = nullptr;
+  const int64_t* rng = nullptr;
+  int site_drop = 0;
+  double p_drop = 0.0;
+  int site_dp = 0;
+  double p_dp = 0.0;
+  int tokens = 1, batch = 1, heads = 1, hd = 1;
+  int chans = 1, img_h = 1, img_w = 1, patch = 1;
+  const float* pos = nullptr;
+  const float* temb = nullptr;
+  const int64_t* tsteps = nullptr;
+  int emb_dim = 0;
+};
+
+void gemm_nt(const GemmArgs& a, int epi, hipStream_t stream);
+void gemm_dgrad(const GemmArgs& a, int epi, hipStream_t stream);
+void gemm_wgrad(const GemmArgs& a, int splits, hipStream_t stream);
+
+// LayerNorm (layernorm.hip)
+void layernorm_fwd_launch(const float* x, const float* gamma, const float* beta, void* y_bf16, float* mean,
+                          float* rstd, int M, int D, float eps, hipStream_t stream);
+void layernorm_bwd_launch(const float* dy, const float* x, const float* mean, const float* rstd,
+                          const float* gamma, const float* g_res, float* g_out, void* gy_bf16, float* dgamma,
+                          float* dbeta, int M, int D, int tokens, const int64_t* rng, int site_drop,
+                          double p_drop, int site_dp, double p_dp, hipStream_t stream);
+
+// Attention (attention.hip)
+void attn_fwd_launch(const void* qkv, void* o, float* lse, int B, int H, int N, int hd, float scale,
+                     const int64_t* rng, int site, double p, hipStream_t stream);
+void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const float* lse, void* dqkv,
+                     float* delta, int B, int H, int N, int hd, float scale, const int64_t* rng, int site,
+                     double p, hipStream_t stream);
+
+// Embedding / head / loss (embed.hip)
+void patchify_cls_launch(const float* img, const int64_t* t, const float* cls, const float* pos,
+                         const float* temb, void* patches, float* x, int B, int C, int H, int W, int patch,
+                         int D, const int64_t* rng, int site, double p, hipStream_t stream);
+void embed_bwd_launch(const float* g, const int64_t* t, float* dcls, float* dpos, float* dtemb, void* gpatch,
+                      int B, int N, int D, const int64_t* rng, int site, double p, hipStream_t stream);
+void smooth_l1_launch(const float* pred, const float* target, float* loss, void* dtok, int B, int C, int H,
+                      int W, int patch, float beta, hipStream_t stream);
+void img_to_tokgrad_launch(const float* dimg, void* dtok, int B, int C, int H, int W, int patch,
+                           hipStream_t stream);
+
+// Optimizer (optim.hip)
+void sqnorm_launch(const float* g, int64_t n, float* out, float scale, hipStream_t stream);
+void adamw_launch(float* p, float* g, float* m, float* v, void* p_bf16, int64_t n, const float* sqnorm,
+                  const int64_t* step, const float* hyper, float grad_scale, hipStream_t stream);
+void advance_counters_launch(int64_t* step, int64_t* rng, const float* sqnorm, hipStream_t stream);
+
+// Diffusion / data (diffusion.hip)
+void ddim_step_launch(const float* x_t, const float* x0_raw, float* x_next, float* x0_out, const float* coef,
+                      int64_t n, hipStream_t stream);
+void pixelate_pair_launch(const float* img, const int64_t* idx, const int64_t* t, float* x_t, float* x_tm1,
+                          int B, int C, int H, int W, hipStream_t stream);
+void randn_launch(float* out, int64_t n, const int64_t* rng, int site, hipStream_t stream);
+void q_sample_launch(const float* x0, const int64_t* t, const float* eps, float* out, int B, int64_t per,
+                     int total_steps, hipStream_t stream);
+void cold_batch_launch(const float* pool, int pool_n, const int64_t* rng, int site, float* x_t, float* x_tm1,
+                       int64_t* t, int64_t* idx_ws, int B, int C, int H, int W, int max_t, hipStream_t stream);

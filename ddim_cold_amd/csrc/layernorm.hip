@@ -1,0 +1,186 @@
+// LayerNorm forward / backward for the ViT residual stream (nn.LayerNorm,
+// eps 1e-5 — ViT.py:124,128,182).  fp32 residual stream in, bf16 normalised
+// activations out (the next GEMM's A operand), fp32 mean/rstd saved.
+//
+// One wave64 per row, the row held in registers (D/128 float2 per lane,
+// 512-B coalesced wave accesses), shuffle reductions only — no LDS in the
+// forward.  The backward additionally fuses:
+//   * the residual-gradient add  g_out = g_res + dLN/dx,
+//   * the *next* residual branch's gradient prep  gy = bf16(g_out * dropout
+//     mask * drop-path scale)  (masks regenerated from the counter hash),
+//   * dgamma/dbeta column partials reduced per workgroup through LDS then one
+//     fp32 atomic per column per workgroup.
+#include "common.h"
+#include "kernels.h"
+
+namespace dc {
+
+template <int VEC>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, bf16* __restrict__ y,
+                                                     float* __restrict__ mean, float* __restrict__ rstd, int M,
+                                                     float eps) {
+  constexpr int D = VEC * 128;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const float2* xr = reinterpret_cast<const float2*>(x + (size_t)row * D);
+  float2 v[VEC];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    v[i] = xr[lane + 64 * i];
+    s += v[i].x + v[i].y;
+  }
+  const float mu = wave_sum(s) * (1.0f / D);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    const float a = v[i].x - mu, b = v[i].y - mu;
+    q += a * a + b * b;
+  }
+  const float rs = rsqrtf(wave_sum(q) * (1.0f / D) + eps);
+  const float2* g2 = reinterpret_cast<const float2*>(gamma);
+  const float2* b2 = reinterpret_cast<const float2*>(beta);
+  bf16x2* yr = reinterpret_cast<bf16x2*>(y + (size_t)row * D);
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    const int c = lane + 64 * i;
+    const float2 gg = g2[c], bb = b2[c];
+    bf16x2 o;
+    o[0] = f2bf((v[i].x - mu) * rs * gg.x + bb.x);
+    o[1] = f2bf((v[i].y - mu) * rs * gg.y + bb.y);
+    yr[c] = o;
+  }
+  if (lane == 0) {
+    mean[row] = mu;
+    rstd[row] = rs;
+  }
+}
+
+template <int VEC>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                                     const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                     const float* __restrict__ gamma, const float* __restrict__ g_res,
+                                                     float* __restrict__ g_out, bf16* __restrict__ gy,
+                                                     float* __restrict__ dgamma, float* __restrict__ dbeta, int M,
+                                                     int tokens, const int64_t* __restrict__ rng, int site_drop,
+                                                     uint32_t thr_drop, float sc_drop, int site_dp, uint32_t thr_dp,
+                                                     float sc_dp) {
+  constexpr int D = VEC * 128;
+  __shared__ float red[4][2 * D];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float2* g2 = reinterpret_cast<const float2*>(gamma);
+  float2 dgam[VEC], dbet[VEC], gm[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    dgam[i] = make_float2(0.f, 0.f);
+    dbet[i] = make_float2(0.f, 0.f);
+    gm[i] = g2[lane + 64 * i];
+  }
+  uint32_t salt_drop = 0, salt_dp = 0;
+  if (gy) {
+    if (thr_drop) salt_drop = site_salt(rng, site_drop);
+    if (thr_dp) salt_dp = site_salt(rng, site_dp);
+  }
+  for (int row = blockIdx.x * 4 + wave; row < M; row += gridDim.x * 4) {
+    const float2* xr = reinterpret_cast<const float2*>(x + (size_t)row * D);
+    const float2* dr = reinterpret_cast<const float2*>(dy + (size_t)row * D);
+    const float mu = mean[row], rs = rstd[row];
+    float2 xh[VEC], dxh[VEC];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      const int c = lane + 64 * i;
+      const float2 xv = xr[c], dv = dr[c];
+      xh[i] = make_float2((xv.x - mu) * rs, (xv.y - mu) * rs);
+      dgam[i].x += dv.x * xh[i].x;
+      dgam[i].y += dv.y * xh[i].y;
+      dbet[i].x += dv.x;
+      dbet[i].y += dv.y;
+      dxh[i] = make_float2(dv.x * gm[i].x, dv.y * gm[i].y);
+      s1 += dxh[i].x + dxh[i].y;
+      s2 += dxh[i].x * xh[i].x + dxh[i].y * xh[i].y;
+    }
+    const float c1 = wave_sum(s1) * (1.0f / D);
+    const float c2 = wave_sum(s2) * (1.0f / D);
+    float dpsc = 1.f;
+    if (gy && thr_dp) dpsc = dropout_keep(salt_dp, (uint32_t)(row / tokens), thr_dp) ? sc_dp : 0.f;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      const int c = lane + 64 * i;
+      float2 o = make_float2((dxh[i].x - c1 - xh[i].x * c2) * rs, (dxh[i].y - c1 - xh[i].y * c2) * rs);
+      if (g_res) {
+        const float2 r = reinterpret_cast<const float2*>(g_res + (size_t)row * D)[c];
+        o.x += r.x;
+        o.y += r.y;
+      }
+      reinterpret_cast<float2*>(g_out + (size_t)row * D)[c] = o;
+      if (gy) {
+        float a = o.x * dpsc, b = o.y * dpsc;
+        if (thr_drop) {
+          const uint32_t idx = (uint32_t)((size_t)row * D + 2 * c);
+          a = dropout_keep(salt_drop, idx, thr_drop) ? a * sc_drop : 0.f;
+          b = dropout_keep(salt_drop, idx + 1, thr_drop) ? b * sc_drop : 0.f;
+        }
+        bf16x2 h;
+        h[0] = f2bf(a);
+        h[1] = f2bf(b);
+        reinterpret_cast<bf16x2*>(gy + (size_t)row * D)[c] = h;
+      }
+    }
+  }
+  // column partials: waves -> LDS -> one atomic per column per workgroup
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    const int c = 2 * (lane + 64 * i);
+    red[wave][c] = dgam[i].x;
+    red[wave][c + 1] = dgam[i].y;
+    red[wave][D + c] = dbet[i].x;
+    red[wave][D + c + 1] = dbet[i].y;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * D; c += 256) {
+    const float s = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+    if (c < D) atomicAdd(dgamma + c, s);
+    else atomicAdd(dbeta + (c - D), s);
+  }
+}
+
+}  // namespace dc
+
+using namespace dc;
+
+#define LN_DISPATCH(D, ...)                                                   \
+  switch ((D) / 128) {                                                        \
+    case 1: { constexpr int VEC = 1; __VA_ARGS__; } break;                    \
+    case 2: { constexpr int VEC = 2; __VA_ARGS__; } break;                    \
+    case 3: { constexpr int VEC = 3; __VA_ARGS__; } break;                    \
+    case 4: { constexpr int VEC = 4; __VA_ARGS__; } break;                    \
+    case 6: { constexpr int VEC = 6; __VA_ARGS__; } break;                    \
+    case 8: { constexpr int VEC = 8; __VA_ARGS__; } break;                    \
+    default: throw std::runtime_error("layernorm: D must be 128*{1,2,3,4,6,8}"); \
+  }
+
+void layernorm_fwd_launch(const float* x, const float* gamma, const float* beta, void* y_bf16, float* mean,
+                          float* rstd, int M, int D, float eps, hipStream_t stream) {
+  if (D % 128) throw std::runtime_error("layernorm: D % 128 != 0");
+  const int grid = (M + 3) / 4;
+  LN_DISPATCH(D, hipLaunchKernelGGL(ln_fwd_kernel<VEC>, dim3(grid), dim3(256), 0, stream, x, gamma, beta,
+                                    reinterpret_cast<bf16*>(y_bf16), mean, rstd, M, eps));
+}
+
+void layernorm_bwd_launch(const float* dy, const float* x, const float* mean, const float* rstd,
+                          const float* gamma, const float* g_res, float* g_out, void* gy_bf16, float* dgamma,
+                          float* dbeta, int M, int D, int tokens, const int64_t* rng, int site_drop,
+                          double p_drop, int site_dp, double p_dp, hipStream_t stream) {
+  if (D % 128) throw std::runtime_error("layernorm: D % 128 != 0");
+  int grid = (M + 15) / 16;  // ~4 rows per wave
+  if (grid < 1) grid = 1;
+  const uint32_t td = drop_threshold_host(p_drop), tp = drop_threshold_host(p_dp);
+  const float sd = p_drop > 0 ? 1.f / (1.f - (float)p_drop) : 1.f;
+  const float sp = p_dp > 0 ? 1.f / (1.f - (float)p_dp) : 1.f;
+  LN_DISPATCH(D, hipLaunchKernelGGL(ln_bwd_kernel<VEC>, dim3(grid), dim3(256), 0, stream, dy, x, mean, rstd,
+                                    gamma, g_res, g_out, reinterpret_cast<bf16*>(gy_bf16), dgamma, dbeta, M,
+                                    tokens, rng, site_drop, td, sd, site_dp, tp, sp));
+}

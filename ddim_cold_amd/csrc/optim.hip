@@ -1,0 +1,101 @@
+// Fused optimizer for the flat parameter arena (multi_gpu_trainer.py:89-134:
+// AdamW(wd=0.05) + clip_grad_norm_(1.0) + CosineAnnealingLR stepped per
+// iteration + zero_grad), graph-capturable: every scalar that changes per step
+// (Adam step, scheduler step, RNG step) lives in device memory.
+//
+//   sqnorm  : sum((g*scale)^2) over the whole grad arena -> one fp32 (atomics per block)
+//   adamw   : clip coef from the norm, cosine LR from the device step, bias
+//             corrections, decoupled weight decay, moment updates, fp32 master
+//             update, bf16 shadow-weight refresh (what the GEMMs read), and the
+//             grad zeroing — one pass over the arena.  A non-finite norm skips
+//             the update (GradScaler semantics, multi_gpu_trainer.py:131).
+//   advance : bump {adam step (unless skipped), scheduler step} and the RNG step.
+#include "common.h"
+#include "kernels.h"
+
+namespace dc {
+
+__global__ __launch_bounds__(256) void sqnorm_kernel(const float* __restrict__ g, int64_t n, float* out, float scale) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  const int64_t n4 = n / 4;
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 v = g4[i];
+    acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    acc += g[i] * g[i];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, (red[0] + red[1] + red[2] + red[3]) * scale * scale);
+}
+
+// hyper = {base_lr, beta1, beta2, eps, weight_decay, max_norm, T_max, eta_min}
+// step  = {adam_step, sched_step}
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
+                                                    float* __restrict__ v, bf16* __restrict__ pb, int64_t n,
+                                                    const float* __restrict__ sqnorm, const int64_t* __restrict__ step,
+                                                    const float* __restrict__ hyper, float grad_scale) {
+  const float sq = *sqnorm;
+  const bool skip = !isfinite(sq);
+  const float base_lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
+  const float max_norm = hyper[5], tmax = hyper[6], eta_min = hyper[7];
+  float coef = grad_scale;
+  if (max_norm > 0.f) coef *= fminf(1.f, max_norm / (sqrtf(sq) + 1e-6f));
+  const double t = (double)(step[0] + 1);
+  const float bc1 = (float)(1.0 - pow((double)b1, t));
+  const float bc2 = (float)(1.0 - pow((double)b2, t));
+  float lr = base_lr;
+  if (tmax > 0.f) lr = eta_min + (base_lr - eta_min) * 0.5f * (1.f + cosf(3.14159265358979f * (float)step[1] / tmax));
+  const float step_size = lr / bc1;
+  const float inv_sbc2 = 1.f / sqrtf(bc2);
+  const float decay = 1.f - lr * wd;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float gi = g[i] * coef;
+    g[i] = 0.f;
+    if (skip) continue;
+    float pi = p[i] * decay;
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    pi -= step_size * mi / (sqrtf(vi) * inv_sbc2 + eps);
+    m[i] = mi;
+    v[i] = vi;
+    p[i] = pi;
+    if (pb) pb[i] = f2bf(pi);
+  }
+}
+
+__global__ void advance_kernel(int64_t* step, int64_t* rng, const float* sqnorm) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    if (sqnorm == nullptr || isfinite(*sqnorm)) step[0] += 1;
+    step[1] += 1;
+    rng[1] += 1;
+  }
+}
+
+}  // namespace dc
+
+using namespace dc;
+
+static int opt_grid(int64_t n) {
+  int64_t g = (n + 255) / 256;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+void sqnorm_launch(const float* g, int64_t n, float* out, float scale, hipStream_t stream) {
+  hipLaunchKernelGGL(sqnorm_kernel, dim3(opt_grid(n / 4 + 1)), dim3(256), 0, stream, g, n, out, scale);
+}
+
+void adamw_launch(float* p, float* g, float* m, float* v, void* p_bf16, int64_t n, const float* sqnorm,
+                  const int64_t* step, const float* hyper, float grad_scale, hipStream_t stream) {
+  hipLaunchKernelGGL(adamw_kernel, dim3(opt_grid(n)), dim3(256), 0, stream, p, g, m, v,
+                     reinterpret_cast<bf16*>(p_bf16), n, sqnorm, step, hyper, grad_scale);
+}
+
+void advance_counters_launch(int64_t* step, int64_t* rng, const float* sqnorm, hipStream_t stream) {
+  hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(64), 0, stream, step, rng, sqnorm);
+}

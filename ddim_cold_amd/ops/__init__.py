@@ -1,0 +1,236 @@
+"""Fused-op layer: one Python entry point per HIP kernel op.
+
+GPU tensors go to ``torch.ops.ddim_cold.<op>`` (hand-written gfx950 kernels in
+``csrc/``); CPU tensors go to the bit-compatible PyTorch reference in
+:mod:`.reference`.  On a GPU the native path is mandatory (see
+:mod:`._ext`): a missing extension raises instead of silently running eager
+PyTorch.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _ext
+from . import reference as ref
+from ._ext import force_reference
+
+__all__ = [
+    "native_available", "patch_embed_fwd", "layernorm_fwd", "qkv_fwd", "attn_fwd",
+    "linear_residual_fwd", "linear_gelu_fwd", "head_fwd", "smooth_l1_fwd_bwd", "img_to_tokgrad",
+    "linear_dgrad", "linear_dgrad_gelu", "linear_wgrad", "layernorm_bwd", "attn_bwd", "embed_bwd",
+    "sqnorm", "adamw_step", "advance_counters", "ddim_step", "ddim_step_", "randn_", "q_sample",
+    "pixelate_pair", "cold_batch",
+]
+
+
+def native_available() -> bool:
+    return _ext.available()
+
+
+def _hip(t: torch.Tensor) -> bool:
+    return _ext.require_for(t)
+
+
+def _ops():
+    return torch.ops.ddim_cold
+
+
+# ----------------------------------------------------------------------------- forward
+def patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site: int, p: float, patch: int):
+    if _hip(img):
+        return _ops().patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site, float(p), patch)
+    return ref.patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site, p, patch)
+
+
+def layernorm_fwd(x, gamma, beta, eps: float = 1e-5):
+    if _hip(x):
+        return _ops().layernorm_fwd(x, gamma, beta, float(eps))
+    return ref.layernorm_fwd(x, gamma, beta, eps)
+
+
+def qkv_fwd(a, w, b, B: int, N: int, H: int):
+    if _hip(a):
+        return _ops().qkv_fwd(a, w, b, B, N, H)
+    return ref.qkv_fwd(a, w, b, B, N, H)
+
+
+def attn_fwd(qkv, scale: float, rng, site: int, p: float):
+    if _hip(qkv):
+        return _ops().attn_fwd(qkv, float(scale), rng, site, float(p))
+    return ref.attn_fwd(qkv, scale, rng, site, p)
+
+
+def linear_residual_fwd(a, w, b, x, N: int, rng, site_drop: int, p_drop: float, site_dp: int, p_dp: float):
+    if _hip(a):
+        return _ops().linear_residual_fwd(a, w, b, x, N, rng, site_drop, float(p_drop), site_dp, float(p_dp))
+    return ref.linear_residual_fwd(a, w, b, x, N, rng, site_drop, p_drop, site_dp, p_dp)
+
+
+def linear_gelu_fwd(a, w, b, rng, site: int, p: float):
+    if _hip(a):
+        return _ops().linear_gelu_fwd(a, w, b, rng, site, float(p))
+    return ref.linear_gelu_fwd(a, w, b, rng, site, p)
+
+
+def head_fwd(a, w, b, B: int, C: int, H: int, W: int, patch: int):
+    if _hip(a):
+        return _ops().head_fwd(a, w, b, B, C, H, W, patch)
+    return ref.head_fwd(a, w, b, B, C, H, W, patch)
+
+
+def smooth_l1_fwd_bwd(pred, target, N: int, patch: int, beta: float = 1.0):
+    if _hip(pred):
+        return _ops().smooth_l1_fwd_bwd(pred, target, N, patch, float(beta))
+    return ref.smooth_l1_fwd_bwd(pred, target, N, patch, beta)
+
+
+def img_to_tokgrad(dimg, N: int, patch: int):
+    if _hip(dimg):
+        return _ops().img_to_tokgrad(dimg.contiguous(), N, patch)
+    return ref.img_to_tokgrad(dimg, N, patch)
+
+
+# ----------------------------------------------------------------------------- backward
+def linear_dgrad(dy, w, out_fp32: bool):
+    if _hip(dy):
+        return _ops().linear_dgrad(dy, w, bool(out_fp32))
+    return ref.linear_dgrad(dy, w, out_fp32)
+
+
+def linear_dgrad_gelu(dy, w, u, rng, site: int, p: float):
+    if _hip(dy):
+        return _ops().linear_dgrad_gelu(dy, w, u, rng, site, float(p))
+    return ref.linear_dgrad_gelu(dy, w, u, rng, site, p)
+
+
+def linear_wgrad(dy, x, dw, db: Optional[torch.Tensor]):
+    if _hip(dy):
+        return _ops().linear_wgrad(dy, x, dw, db)
+    return ref.linear_wgrad(dy, x, dw, db)
+
+
+def layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dgamma, dbeta, N: int, rng, site_drop: int, p_drop: float,
+                  site_dp: int, p_dp: float, emit_gy: bool):
+    if _hip(x):
+        g_out, gy = _ops().layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dgamma, dbeta, N, rng, site_drop,
+                                         float(p_drop), site_dp, float(p_dp), bool(emit_gy))
+        return g_out, (gy if emit_gy else None)
+    return ref.layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dgamma, dbeta, N, rng, site_drop, p_drop,
+                             site_dp, p_dp, emit_gy)
+
+
+def attn_bwd(do, qkv, o, lse, scale: float, rng, site: int, p: float):
+    if _hip(qkv):
+        return _ops().attn_bwd(do, qkv, o, lse, float(scale), rng, site, float(p))
+    return ref.attn_bwd(do, qkv, o, lse, scale, rng, site, p)
+
+
+def embed_bwd(g, t, rng, site: int, p: float, dcls, dpos, dtemb):
+    if _hip(g):
+        return _ops().embed_bwd(g, t, rng, site, float(p), dcls, dpos, dtemb)
+    return ref.embed_bwd(g, t, rng, site, p, dcls, dpos, dtemb)
+
+
+# ----------------------------------------------------------------------------- optimizer
+def sqnorm(g, out, scale: float = 1.0):
+    if _hip(g):
+        return _ops().sqnorm(g, out, float(scale))
+    out.add_((g.float() * scale).pow(2).sum().reshape(out.shape))
+
+
+def adamw_step(p, g, m, v, pbf, sq, step, hyper, grad_scale: float = 1.0):
+    """Fused AdamW over a flat arena (see csrc/optim.hip for the exact math)."""
+    if _hip(p):
+        return _ops().adamw_step(p, g, m, v, pbf, sq, step, hyper, float(grad_scale))
+    import math
+    sqv = float(sq.reshape(-1)[0])
+    base_lr, b1, b2, eps, wd, max_norm, tmax, eta_min = (float(x) for x in hyper.tolist()[:8])
+    coef = grad_scale
+    if max_norm > 0:
+        coef *= min(1.0, max_norm / (math.sqrt(sqv) + 1e-6)) if math.isfinite(sqv) else 1.0
+    gi = g * coef
+    g.zero_()
+    if not math.isfinite(sqv):
+        return
+    t = int(step[0]) + 1
+    bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
+    lr = base_lr
+    if tmax > 0:
+        lr = eta_min + (base_lr - eta_min) * 0.5 * (1 + math.cos(math.pi * int(step[1]) / tmax))
+    p.mul_(1 - lr * wd)
+    m.mul_(b1).add_(gi, alpha=1 - b1)
+    v.mul_(b2).addcmul_(gi, gi, value=1 - b2)
+    p.addcdiv_(m, v.sqrt() / math.sqrt(bc2) + eps, value=-lr / bc1)
+    if pbf is not None:
+        pbf.copy_(p.to(torch.bfloat16))
+
+
+def advance_counters(step, rng, sq=None):
+    if _hip(step):
+        return _ops().advance_counters(step, rng, sq)
+    import math
+    if sq is None or math.isfinite(float(sq.reshape(-1)[0])):
+        step[0] += 1
+    step[1] += 1
+    rng[1] += 1
+
+
+# ----------------------------------------------------------------------------- diffusion / data
+def ddim_step(x_t, x0_raw, coef):
+    if _hip(x_t):
+        return _ops().ddim_step(x_t, x0_raw, coef)
+    return ref.ddim_step(x_t, x0_raw, [float(c) for c in coef.tolist()[:4]])
+
+
+def ddim_step_(x, x0_raw, x0_out, coef):
+    if _hip(x):
+        return _ops().ddim_step_(x, x0_raw, x0_out, coef)
+    xn, x0 = ref.ddim_step(x, x0_raw, [float(c) for c in coef.tolist()[:4]])
+    x.copy_(xn)
+    x0_out.copy_(x0)
+
+
+def randn_(out, rng, site: int):
+    if _hip(out):
+        return _ops().randn_(out, rng, site)
+    salt = ref.site_salt(rng, site)
+    n = out.numel()
+    pairs = (n + 1) // 2
+    i = torch.arange(pairs, dtype=torch.int64)
+    ha = ref.mix32(ref._mul32((2 * i) & ref.MASK32, ref.GOLDEN) ^ salt)
+    hb = ref.mix32(ref._mul32((2 * i + 1) & ref.MASK32, ref.GOLDEN) ^ salt)
+    a = ((ha >> 8).double() + 0.5) / 16777216.0
+    b = ((hb >> 8).double() + 0.5) / 16777216.0
+    r = torch.sqrt(-2.0 * torch.log(a))
+    z = torch.stack((r * torch.cos(2 * torch.pi * b), r * torch.sin(2 * torch.pi * b)), dim=1).reshape(-1)[:n]
+    out.copy_(z.float().view(out.shape))
+
+
+def q_sample(x0, t, eps, total_steps: int):
+    if _hip(x0):
+        return _ops().q_sample(x0, t, eps, total_steps)
+    return ref.q_sample(x0, t, eps, total_steps)
+
+
+def pixelate_pair(img, idx, t, B: int):
+    if _hip(img):
+        return _ops().pixelate_pair(img, idx, t, B)
+    src = img if idx is None else img[idx]
+    xt = torch.stack([ref.pixelate(src[i:i + 1], 2 ** int(t[i]))[0] for i in range(B)])
+    xtm1 = torch.stack([ref.pixelate(src[i:i + 1], 2 ** (int(t[i]) - 1))[0] for i in range(B)])
+    return xt, xtm1
+
+
+def cold_batch(pool, rng, site: int, x_t, x_tm1, t, idx_ws, max_t: int):
+    if _hip(pool):
+        return _ops().cold_batch(pool, rng, site, x_t, x_tm1, t, idx_ws, max_t)
+    salt = ref.site_salt(rng, site)
+    B = x_t.shape[0]
+    b = torch.arange(B, dtype=torch.int64)
+    idx_ws.copy_(ref.mix32(ref._mul32((2 * b) & ref.MASK32, ref.GOLDEN) ^ salt) % pool.shape[0])
+    t.copy_(1 + ref.mix32(ref._mul32((2 * b + 1) & ref.MASK32, ref.GOLDEN) ^ salt) % max_t)
+    a, c = pixelate_pair(pool, idx_ws, t, B)
+    x_t.copy_(a)
+    x_tm1.copy_(c)

@@ -1,0 +1,348 @@
+"""TrainEngine — the MI355X training step runtime.
+
+One training step of the reference (multi_gpu_trainer.py:115-134:
+autocast forward, smooth-L1, backward with DDP all-reduce, unscale, clip 1.0,
+AdamW step, cosine LR step, zero_grad) re-designed for a latency-bound
+7 M-parameter model on MI355X:
+
+* **Flat arenas.**  All parameters live in one fp32 arena (``nn.Parameter.data``
+  are views), gradients in a second (``param.grad`` are views), Adam moments
+  in two more, plus a bf16 shadow of the parameters that the MFMA GEMMs read.
+  Every param offset is 256-B aligned.  All-reduce buckets are contiguous arena
+  ranges: no pack/unpack kernels.
+* **Fused optimizer.**  3 launches per step (global grad-norm, AdamW + clip +
+  cosine LR + bf16 shadow refresh + grad zeroing, counter bump); the LR /
+  Adam step / RNG step live in device memory so the step is graph-replayable.
+* **Side-stream weight gradients.**  wgrad GEMMs (nothing on the critical
+  path depends on them) run on a second HIP stream, overlapping the
+  dgrad/attention chain of the backward.
+* **Segmented hipGraph capture + bucketed RCCL all-reduce.**  The step is
+  captured as ``n_buckets + 1`` graphs split at transformer-block boundaries
+  of the backward.  Between segment replays the host enqueues the finished
+  bucket's ``all_reduce`` (RCCL over xGMI via ``torch.distributed`` 'nccl') on
+  a communication stream, so bucket k's reduction overlaps the backward of
+  the remaining blocks; the optimizer segment waits on the comm stream.  With
+  one GPU the whole step is a single graph.  Buckets default to ~2 blocks
+  (~7 MB fp32 for ViT-tiny): few enough collectives for the per-call latency
+  of 7-link point-to-point xGMI rings, large enough to overlap.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Callable, Dict, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+from ..models.program import ModelTensors, ViTProgram, collect, is_matrix_param
+
+ALIGN = 64  # elements (256 B fp32)
+
+
+@dataclass
+class EngineConfig:
+    lr: float = 3.125e-4
+    weight_decay: float = 0.05
+    betas: Tuple[float, float] = (0.9, 0.999)
+    eps: float = 1e-8
+    max_grad_norm: float = 1.0
+    t_max: int = 0            # cosine annealing period in optimizer steps (0: constant LR)
+    eta_min: float = 0.0
+    use_graph: bool = True
+    graph_warmup: int = 3     # eager steps before capture
+    bucket_blocks: int = 2    # transformer blocks per all-reduce bucket
+    wgrad_stream: bool = True
+    seed: int = 42
+    loss_beta: float = 1.0
+    ema_decay: float = 0.99
+    ema_init: float = 5.0     # multi_gpu_trainer.py:52 (loss_rec = 5.0)
+
+
+def _align(n: int) -> int:
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+class TrainEngine:
+    def __init__(self, model, cfg: EngineConfig = EngineConfig(), device=None, process_group=None):
+        self.cfg = cfg
+        self.model = model
+        self.device = torch.device(device) if device is not None else next(model.parameters()).device
+        model.to(self.device)
+        self.prog = ViTProgram.from_model(model)
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
+        self.rank = dist.get_rank(process_group) if self.world > 1 else 0
+        self.is_cuda = self.device.type == "cuda"
+        self._build_arenas()
+        dev = self.device
+        self.rng = torch.tensor([cfg.seed, 0], dtype=torch.int64, device=dev)
+        self.step_ctr = torch.zeros(2, dtype=torch.int64, device=dev)  # {adam step, scheduler step}
+        b1, b2 = cfg.betas
+        self.hyper = torch.tensor([cfg.lr, b1, b2, cfg.eps, cfg.weight_decay, cfg.max_grad_norm,
+                                   float(cfg.t_max), cfg.eta_min], dtype=torch.float32, device=dev)
+        self.sqnorm = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.loss_last = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.loss_ema = torch.full((1,), cfg.ema_init, dtype=torch.float32, device=dev)
+        self.side = torch.cuda.Stream(device=dev) if (self.is_cuda and cfg.wgrad_stream) else None
+        self.comm = torch.cuda.Stream(device=dev) if (self.is_cuda and self.world > 1) else None
+        self._graphs: Optional[List[torch.cuda.CUDAGraph]] = None
+        self._eager_steps = 0
+        self.batch_fn: Optional[Callable] = None
+        self._static = None
+        self.steps_done = 0
+        if self.world > 1:
+            dist.broadcast(self.flat_p, src=0, group=self.pg)
+            self._refresh_shadow()
+        model._engine = self
+
+    # ------------------------------------------------------------------ arenas
+    def _build_arenas(self):
+        named = list(self.model.named_parameters())
+        self.names = [n for n, _ in named]
+        self.offsets: Dict[str, Tuple[int, int]] = {}
+        off = 0
+        for n, p in named:
+            self.offsets[n] = (off, p.numel())
+            off += _align(p.numel())
+        self.numel = off
+        dev = self.device
+        self.flat_p = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.flat_g = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.flat_m = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.flat_v = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.flat_pb = torch.zeros(off, dtype=torch.bfloat16, device=dev)
+        views_p, views_g = {}, {}
+        for n, p in named:
+            o, k = self.offsets[n]
+            vp = self.flat_p[o:o + k].view_as(p)
+            vp.copy_(p.data)
+            p.data = vp
+            vg = self.flat_g[o:o + k].view_as(p)
+            p.grad = vg
+            views_g[n] = vg
+        self._refresh_shadow()
+        for n, p in named:
+            o, k = self.offsets[n]
+            views_p[n] = self.flat_pb[o:o + k].view(p.shape) if is_matrix_param(n) else p.data
+        c = self.prog.cfg
+        self.param_tensors: ModelTensors = collect(views_p, c.depth, c.dim)
+        self.grad_tensors: ModelTensors = collect(views_g, c.depth, c.dim)
+        if not c.learn_temb:
+            self.grad_tensors.temb = None
+        # all-reduce buckets: contiguous arena ranges, boundaries after block groups (backward order)
+        L = c.depth
+        starts = [self.offsets[f"blocks.{i}.norm1.weight"][0] for i in range(L)]
+        bb = max(1, self.cfg.bucket_blocks)
+        self.bucket_after: Dict[int, int] = {}
+        bounds = []
+        end = self.numel
+        j = 0
+        for i in range(L - 1, -1, -1):
+            if (L - 1 - i) % bb == bb - 1 and i > 0:
+                bounds.append((starts[i], end))
+                self.bucket_after[i] = j
+                end = starts[i]
+                j += 1
+        bounds.append((0, end))
+        self.bucket_after[-1] = j
+        self.buckets = bounds
+
+    def _refresh_shadow(self):
+        self.flat_pb.copy_(self.flat_p.to(torch.bfloat16))
+
+    # ------------------------------------------------------------------ step program
+    def set_batch_fn(self, fn: Callable):
+        """``fn() -> (x_t, target, t)`` device tensors; called inside the captured region."""
+        self.batch_fn = fn
+        self._graphs = None
+
+    def _wgrad(self, dy, x, dw, db):
+        if self.side is None:
+            ops.linear_wgrad(dy, x, dw, db)
+            return
+        cur = torch.cuda.current_stream(self.device)
+        self.side.wait_stream(cur)
+        with torch.cuda.stream(self.side):
+            ops.linear_wgrad(dy, x, dw, db)
+
+    def _join_side(self):
+        if self.side is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.side)
+
+    def _step_iter(self):
+        c = self.prog.cfg
+        img, tgt, t = self.batch_fn()
+        out, S = self.prog.forward(self.param_tensors, img, t, self.rng, True)
+        loss, dtok = ops.smooth_l1_fwd_bwd(out, tgt, c.tokens, c.patch, self.cfg.loss_beta)
+        self.loss_last.copy_(loss)
+        self.loss_ema.mul_(self.cfg.ema_decay).add_(loss, alpha=1.0 - self.cfg.ema_decay)
+        del out
+        for i in self.prog.backward_iter(self.param_tensors, self.grad_tensors, S, dtok, self.rng, True,
+                                         wgrad=self._wgrad):
+            if i in self.bucket_after:
+                self._join_side()
+                yield ("bucket", self.bucket_after[i])
+        S = None
+        self.prog._keep = None
+        # optimizer: grads are SUM-reduced over ranks -> average via grad_scale
+        gs = 1.0 / self.world
+        self.sqnorm.zero_()
+        ops.sqnorm(self.flat_g, self.sqnorm, gs)
+        ops.adamw_step(self.flat_p, self.flat_g, self.flat_m, self.flat_v, self.flat_pb, self.sqnorm,
+                       self.step_ctr, self.hyper, gs)
+        ops.advance_counters(self.step_ctr, self.rng, self.sqnorm)
+        yield ("done", -1)
+
+    def _allreduce(self, k: int):
+        if self.world <= 1:
+            return
+        a, b = self.buckets[k]
+        view = self.flat_g[a:b]
+        if self.comm is not None:
+            self.comm.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.comm):
+                dist.all_reduce(view, group=self.pg)
+        else:
+            dist.all_reduce(view, group=self.pg)
+
+    def _join_comm(self):
+        if self.comm is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.comm)
+
+    def _run_eager(self):
+        gen = self._step_iter()
+        for kind, k in gen:
+            if kind == "bucket":
+                self._allreduce(k)
+                if k == len(self.buckets) - 1:
+                    self._join_comm()
+
+    def _capture(self):
+        pool = torch.cuda.graph_pool_handle()
+        graphs = []
+        gen = self._step_iter()
+        nseg = len(self.buckets) + 1 if self.world > 1 else 1
+        if nseg == 1:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                for _ in gen:
+                    pass
+            graphs.append(g)
+        else:
+            for _ in range(nseg):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    next(gen)
+                graphs.append(g)
+        self._graphs = graphs
+
+    def _replay(self):
+        gs = self._graphs
+        if len(gs) == 1:
+            gs[0].replay()
+            return
+        nb = len(self.buckets)
+        for k in range(nb):
+            gs[k].replay()
+            self._allreduce(k)
+        self._join_comm()
+        gs[nb].replay()
+
+    def train_step(self):
+        """Run one optimizer step on the batch produced by ``batch_fn``.
+
+        Returns the device loss tensor (no host sync)."""
+        if self.batch_fn is None:
+            raise RuntimeError("set_batch_fn() or use step(x, target, t)")
+        use_graph = self.cfg.use_graph and self.is_cuda
+        if use_graph and self._graphs is None and self._eager_steps >= self.cfg.graph_warmup:
+            self._capture()
+        if use_graph and self._graphs is not None:
+            self._replay()
+        else:
+            self._run_eager()
+            self._eager_steps += 1
+        self.steps_done += 1
+        return self.loss_last
+
+    def step(self, x_t: torch.Tensor, target: torch.Tensor, t: torch.Tensor):
+        """Convenience: copy an externally produced batch into static buffers and step."""
+        if self._static is None or self._static[0].shape != x_t.shape:
+            self._static = (torch.empty_like(x_t, device=self.device), torch.empty_like(target, device=self.device),
+                            torch.empty(t.shape, dtype=torch.int64, device=self.device))
+            st = self._static
+            self.set_batch_fn(lambda: st)
+        sx, sy, st_ = self._static
+        sx.copy_(x_t, non_blocking=True)
+        sy.copy_(target, non_blocking=True)
+        st_.copy_(t, non_blocking=True)
+        return self.train_step()
+
+    # ------------------------------------------------------------------ state
+    def current_lr(self) -> float:
+        step = int(self.step_ctr[1].item())
+        c = self.cfg
+        if c.t_max <= 0:
+            return c.lr
+        return c.eta_min + (c.lr - c.eta_min) * 0.5 * (1 + math.cos(math.pi * step / c.t_max))
+
+    def _param_list(self):
+        return [p for _, p in self.model.named_parameters()]
+
+    def optimizer_state_dict(self) -> dict:
+        """torch.optim.AdamW-format state dict (interchangeable with the reference's lastepoch.pkl)."""
+        params = self._param_list()
+        opt = torch.optim.AdamW(params, lr=self.current_lr(), betas=self.cfg.betas, eps=self.cfg.eps,
+                                weight_decay=self.cfg.weight_decay)
+        adam_step = float(self.step_ctr[0].item())
+        if adam_step > 0:
+            for n, p in zip(self.names, params):
+                o, k = self.offsets[n]
+                opt.state[p] = {"step": torch.tensor(adam_step),
+                                "exp_avg": self.flat_m[o:o + k].view_as(p).clone(),
+                                "exp_avg_sq": self.flat_v[o:o + k].view_as(p).clone()}
+        sd = opt.state_dict()
+        sd["param_groups"][0]["initial_lr"] = self.cfg.lr
+        return sd
+
+    def load_optimizer_state_dict(self, sd: dict):
+        st = sd.get("state", {})
+        params = self._param_list()
+        step = 0
+        for i, (n, p) in enumerate(zip(self.names, params)):
+            s = st.get(i)
+            if s is None:
+                continue
+            o, k = self.offsets[n]
+            self.flat_m[o:o + k].copy_(s["exp_avg"].reshape(-1).to(self.device))
+            self.flat_v[o:o + k].copy_(s["exp_avg_sq"].reshape(-1).to(self.device))
+            step = int(float(s["step"]))
+        self.step_ctr[0] = step
+
+    def scheduler_state_dict(self) -> dict:
+        """torch CosineAnnealingLR-format state dict."""
+        params = self._param_list()
+        opt = torch.optim.AdamW(params, lr=self.cfg.lr)
+        sch = torch.optim.lr_scheduler.CosineAnnealingLR(opt, max(self.cfg.t_max, 1), self.cfg.eta_min)
+        sd = sch.state_dict()
+        last = int(self.step_ctr[1].item())
+        sd["last_epoch"] = last
+        sd["_step_count"] = last + 1
+        sd["_last_lr"] = [self.current_lr()]
+        return sd
+
+    def load_scheduler_state_dict(self, sd: dict):
+        self.step_ctr[1] = int(sd.get("last_epoch", 0))
+
+    def sync_params_from_model(self):
+        """Call after loading weights into ``model`` (its params are arena views)."""
+        self._refresh_shadow()
+
+    def detach(self):
+        """Release the model from the engine (params stay on the device, as plain tensors)."""
+        for n, p in self.model.named_parameters():
+            p.data = p.data.clone()
+            p.grad = None
+        self.model._engine = None

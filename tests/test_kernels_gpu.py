@@ -1,0 +1,330 @@
+"""Numerics of every hand-written HIP kernel vs the plain-PyTorch fp32 reference.
+
+Each test runs the op through ``torch.ops.ddim_cold`` (gfx950 kernel) and through
+:mod:`ddim_cold_amd.ops.reference` on the same GPU inputs (the reference is
+ordinary PyTorch fp32 math with the same bf16 rounding points and the same
+counter-hash dropout masks), then compares.
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from ddim_cold_amd import ops
+from ddim_cold_amd.ops import reference as ref
+
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True)
+def _native():
+    from ddim_cold_amd.ops import _ext
+    _ext.load(raise_on_error=True)
+    torch.manual_seed(0)
+
+
+def rng(seed=1234, step=5):
+    return torch.tensor([seed, step], dtype=torch.int64, device=DEV)
+
+
+def close(a, b, atol, rtol=0.0, name=""):
+    a, b = a.float(), b.float()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol).sum().item()
+    assert bad == 0, f"{name}: {bad} mismatches, max err {err.max().item():.3e}"
+
+
+def bf(*shape, scale=1.0):
+    return (torch.randn(*shape, device=DEV) * scale).to(torch.bfloat16)
+
+
+# ------------------------------------------------------------------ LayerNorm
+@pytest.mark.parametrize("M,D", [(2080, 384), (8224, 256), (37, 128), (100, 768)])
+def test_layernorm_fwd(M, D):
+    x = torch.randn(M, D, device=DEV) * 3 + 1
+    g = torch.randn(D, device=DEV)
+    b = torch.randn(D, device=DEV)
+    y, mu, rs = ops.layernorm_fwd(x, g, b, 1e-5)
+    yr, mur, rsr = ref.layernorm_fwd(x, g, b, 1e-5)
+    close(mu, mur, 1e-5, 1e-5, "mean")
+    close(rs, rsr, 1e-5, 1e-4, "rstd")
+    close(y, yr, 2e-2, 1e-2, "y")
+
+
+@pytest.mark.parametrize("emit,p", [(True, 0.1), (False, 0.0), (True, 0.0)])
+def test_layernorm_bwd(emit, p):
+    M, D, N = 2080, 384, 65
+    x = torch.randn(M, D, device=DEV)
+    g = torch.randn(D, device=DEV)
+    b = torch.randn(D, device=DEV)
+    _, mu, rs = ref.layernorm_fwd(x, g, b)
+    dy = torch.randn(M, D, device=DEV)
+    gres = torch.randn(M, D, device=DEV)
+    dg1, db1 = torch.zeros(D, device=DEV), torch.zeros(D, device=DEV)
+    dg2, db2 = torch.zeros(D, device=DEV), torch.zeros(D, device=DEV)
+    r = rng()
+    go, gy = ops.layernorm_bwd(dy, x, mu, rs, g, gres, dg1, db1, N, r, 7, p, 8, 0.2 if p else 0.0, emit)
+    gor, gyr = ref.layernorm_bwd(dy, x, mu, rs, g, gres, dg2, db2, N, r, 7, p, 8, 0.2 if p else 0.0, emit)
+    close(go, gor, 1e-4, 1e-4, "g_out")
+    close(dg1, dg2, 1e-2, 1e-4, "dgamma")
+    close(db1, db2, 1e-2, 1e-4, "dbeta")
+    if emit:
+        close(gy, gyr, 1e-2, 1e-2, "gy")
+    else:
+        assert gy is None
+
+
+# ------------------------------------------------------------------ GEMMs
+@pytest.mark.parametrize("B,N,H,D", [(32, 65, 12, 384), (4, 257, 4, 256), (3, 17, 2, 64 * 2)])
+def test_qkv_fwd(B, N, H, D):
+    a = bf(B * N, D)
+    w = bf(3 * D, D, scale=0.05)
+    b = torch.randn(3 * D, device=DEV)
+    out = ops.qkv_fwd(a, w, b, B, N, H)
+    outr = ref.qkv_fwd(a, w, b, B, N, H)
+    assert out.shape == (3, B, H, N, D // H)
+    close(out, outr, 2e-2, 1e-2, "qkv")
+
+
+@pytest.mark.parametrize("M,K,Nout,pd,pdp", [(2080, 384, 384, 0.1, 0.1), (2080, 384, 384, 0.0, 0.0),
+                                              (8224, 256, 256, 0.1, 0.0), (100, 48, 40, 0.0, 0.3)])
+def test_linear_residual(M, K, Nout, pd, pdp):
+    N = 65 if M % 65 == 0 else (257 if M % 257 == 0 else M // 4 if M % 4 == 0 else M)
+    a = bf(M, K)
+    w = bf(Nout, K, scale=0.05)
+    b = torch.randn(Nout, device=DEV)
+    x = torch.randn(M, Nout, device=DEV)
+    r = rng()
+    y = ops.linear_residual_fwd(a, w, b, x, N, r, 3, pd, 4, pdp)
+    yr = ref.linear_residual_fwd(a, w, b, x, N, r, 3, pd, 4, pdp)
+    close(y, yr, 1e-3, 1e-4, "resid")
+
+
+def test_gemm_asymmetric_identity():
+    """A = I with an asymmetric B catches a transposed C write (guide §3)."""
+    K = 64
+    a = torch.eye(K, device=DEV).to(torch.bfloat16)
+    w = (torch.arange(K * K, device=DEV).float().view(K, K) % 97 / 97.0).to(torch.bfloat16)
+    x = torch.zeros(K, K, device=DEV)
+    y = ops.linear_residual_fwd(a, w, torch.zeros(K, device=DEV), x, K, rng(), 0, 0.0, 0, 0.0)
+    close(y, w.float().t(), 1e-6, 0, "identity")
+
+
+def test_linear_gelu():
+    M, K, Hm = 2080, 384, 384
+    a, w, b = bf(M, K), bf(Hm, K, scale=0.05), torch.randn(Hm, device=DEV)
+    r = rng()
+    u, h = ops.linear_gelu_fwd(a, w, b, r, 9, 0.1)
+    ur, hr = ref.linear_gelu_fwd(a, w, b, r, 9, 0.1)
+    close(u, ur, 2e-2, 1e-2, "u")
+    close(h, hr, 2e-2, 1e-2, "h")
+
+
+@pytest.mark.parametrize("B,C,H,W,p,D", [(4, 3, 64, 64, 8, 384), (2, 3, 64, 64, 4, 256), (2, 3, 200, 200, 8, 384)])
+def test_head_fwd(B, C, H, W, p, D):
+    N = (H // p) * (W // p) + 1
+    a = bf(B * N, D)
+    w = bf(C * p * p, D, scale=0.05)
+    b = torch.randn(C * p * p, device=DEV)
+    img = ops.head_fwd(a, w, b, B, C, H, W, p)
+    imgr = ref.head_fwd(a, w, b, B, C, H, W, p)
+    close(img, imgr, 1e-3, 1e-3, "head")
+
+
+@pytest.mark.parametrize("B,C,H,W,p,D,pd", [(4, 3, 64, 64, 8, 384, 0.1), (2, 3, 64, 64, 4, 256, 0.0)])
+def test_patch_embed(B, C, H, W, p, D, pd):
+    N = (H // p) * (W // p) + 1
+    img = torch.randn(B, C, H, W, device=DEV)
+    t = torch.randint(0, 2000, (B,), device=DEV)
+    w = bf(D, C * p * p, scale=0.05)
+    b, cls, pos = torch.randn(D, device=DEV), torch.randn(D, device=DEV), torch.randn(N, D, device=DEV)
+    temb = torch.randn(2000, D, device=DEV)
+    r = rng()
+    x, pt = ops.patch_embed_fwd(img, t, w, b, cls, pos, temb, r, 1, pd, p)
+    xr, ptr = ref.patch_embed_fwd(img, t, w, b, cls, pos, temb, r, 1, pd, p)
+    close(pt, ptr, 0, 0, "patches")
+    close(x, xr, 1e-3, 1e-3, "tokens")
+
+
+@pytest.mark.parametrize("M,Nout,K", [(2080, 384, 384), (2080, 1152, 384), (2080, 192, 384), (8224, 256, 256),
+                                      (100, 48, 40)])
+def test_dgrad(M, Nout, K):
+    dy = bf(M, Nout)
+    w = bf(Nout, K, scale=0.05)
+    for fp32 in (True, False):
+        dx = ops.linear_dgrad(dy, w, fp32)
+        dxr = ref.linear_dgrad(dy, w, fp32)
+        close(dx, dxr, 2e-2 if not fp32 else 1e-3, 1e-2, f"dgrad fp32={fp32}")
+
+
+def test_dgrad_gelu():
+    M, N, K = 2080, 384, 384
+    dy, w, u = bf(M, N), bf(N, K, scale=0.05), bf(M, K)
+    r = rng()
+    du = ops.linear_dgrad_gelu(dy, w, u, r, 11, 0.1)
+    dur = ref.linear_dgrad_gelu(dy, w, u, r, 11, 0.1)
+    close(du, dur, 2e-2, 1e-2, "dgelu")
+
+
+@pytest.mark.parametrize("M,Nout,K", [(2080, 384, 384), (2080, 1152, 384), (2080, 192, 384), (8224, 256, 256),
+                                      (2048, 384, 192), (100, 48, 40)])
+def test_wgrad(M, Nout, K):
+    dy, x = bf(M, Nout), bf(M, K)
+    dw0 = torch.randn(Nout, K, device=DEV)
+    db0 = torch.randn(Nout, device=DEV)
+    dw1, db1 = dw0.clone(), db0.clone()
+    ops.linear_wgrad(dy, x, dw1, db1)
+    dw2, db2 = dw0.clone(), db0.clone()
+    ref.linear_wgrad(dy, x, dw2, db2)
+    close(dw1, dw2, 2e-2, 1e-4, "dw")
+    close(db1, db2, 2e-2, 1e-4, "db")
+
+
+# ------------------------------------------------------------------ attention
+@pytest.mark.parametrize("B,H,N,hd,p", [(4, 12, 65, 32, 0.0), (4, 12, 65, 32, 0.1), (2, 4, 257, 64, 0.1),
+                                        (1, 2, 17, 32, 0.0), (1, 6, 626, 64, 0.0), (2, 3, 130, 64, 0.2)])
+def test_attention_fwd_bwd(B, H, N, hd, p):
+    qkv = bf(3, B, H, N, hd)
+    r = rng()
+    scale = hd ** -0.5
+    o, lse = ops.attn_fwd(qkv, scale, r, 5, p)
+    or_, lser = ref.attn_fwd(qkv, scale, r, 5, p)
+    close(lse, lser, 1e-3, 1e-4, "lse")
+    close(o, or_, 2e-2, 2e-2, "o")
+    do = bf(B, N, H * hd)
+    dq = ops.attn_bwd(do, qkv, o, lse, scale, r, 5, p)
+    dqr = ref.attn_bwd(do, qkv, o, lse, scale, r, 5, p)
+    assert dq.shape == (B * N, 3 * H * hd)
+    close(dq, dqr, 3e-2, 3e-2, "dqkv")
+
+
+def test_attention_spike_rescale():
+    """Force a running-max jump at the second KV tile (online-softmax rescale branch)."""
+    B, H, N, hd = 1, 1, 130, 32
+    qkv = bf(3, B, H, N, hd, scale=0.5)
+    qkv[1, 0, 0, 100] = 8.0   # one key far to the right with a large dot product
+    qkv[0, 0, 0, :] = 8.0
+    r = rng()
+    o, lse = ops.attn_fwd(qkv, hd ** -0.5, r, 5, 0.0)
+    or_, lser = ref.attn_fwd(qkv, hd ** -0.5, r, 5, 0.0)
+    close(lse, lser, 1e-3, 1e-4, "lse")
+    close(o, or_, 2e-2, 2e-2, "o")
+
+
+# ------------------------------------------------------------------ embedding / loss
+def test_embed_bwd():
+    B, N, D = 32, 65, 384
+    g = torch.randn(B, N, D, device=DEV)
+    t = torch.tensor([3, 3, 7] + list(range(100, 129)), device=DEV)
+    r = rng()
+    outs = []
+    for fn in (ops.embed_bwd, ref.embed_bwd):
+        dcls, dpos, dtemb = torch.zeros(D, device=DEV), torch.zeros(N, D, device=DEV), torch.zeros(2000, D, device=DEV)
+        gp = fn(g, t, r, 1, 0.1, dcls, dpos, dtemb)
+        outs.append((gp, dcls, dpos, dtemb))
+    for a, b, n in zip(outs[0], outs[1], ["gpatch", "dcls", "dpos", "dtemb"]):
+        close(a, b, 2e-2 if n == "gpatch" else 1e-3, 1e-3, n)
+
+
+@pytest.mark.parametrize("p", [8, 4])
+def test_smooth_l1(p):
+    B, C, H, W = 8, 3, 64, 64
+    N = (H // p) * (W // p) + 1
+    pred = torch.randn(B, C, H, W, device=DEV) * 1.5
+    tgt = torch.randn(B, C, H, W, device=DEV)
+    loss, dt = ops.smooth_l1_fwd_bwd(pred, tgt, N, p, 1.0)
+    lr_, dtr = ref.smooth_l1_fwd_bwd(pred, tgt, N, p, 1.0)
+    torch.testing.assert_close(loss, lr_, rtol=1e-4, atol=1e-6)
+    ref_loss = torch.nn.functional.smooth_l1_loss(pred, tgt)
+    torch.testing.assert_close(loss[0], ref_loss, rtol=1e-4, atol=1e-6)
+    close(dt, dtr, 1e-9, 1e-2, "dtok")
+    dimg = torch.randn(B, C, H, W, device=DEV)
+    close(ops.img_to_tokgrad(dimg, N, p), ref.img_to_tokgrad(dimg, N, p), 0, 1e-2, "tokgrad")
+
+
+# ------------------------------------------------------------------ optimizer
+def test_fused_adamw_matches_torch():
+    torch.manual_seed(1)
+    n = 100_003
+    p0 = torch.randn(n, device=DEV)
+    steps = 4
+    # torch reference: AdamW(wd=0.05) + clip 1.0 + cosine LR (per-step)
+    pt = p0.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([pt], lr=3e-3, weight_decay=0.05)
+    sch = torch.optim.lr_scheduler.CosineAnnealingLR(opt, 10, 0.0)
+    # fused
+    p, g, m, v = p0.clone(), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    pb = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    sq = torch.zeros(1, device=DEV)
+    step = torch.zeros(2, dtype=torch.int64, device=DEV)
+    r = rng()
+    hyper = torch.tensor([3e-3, 0.9, 0.999, 1e-8, 0.05, 1.0, 10.0, 0.0], device=DEV)
+    for s in range(steps):
+        grad = torch.randn(n, device=DEV) * (0.001 if s % 2 else 0.1)
+        pt.grad = grad.clone()
+        torch.nn.utils.clip_grad_norm_([pt], 1.0)
+        opt.step()
+        sch.step()
+        g.copy_(grad)
+        sq.zero_()
+        ops.sqnorm(g, sq, 1.0)
+        ops.adamw_step(p, g, m, v, pb, sq, step, hyper, 1.0)
+        ops.advance_counters(step, r, sq)
+    torch.testing.assert_close(p, pt.detach(), rtol=1e-5, atol=1e-6)
+    assert torch.all(g == 0)
+    close(pb, p, 1e-2, 1e-2, "bf16 shadow")
+    assert step.tolist() == [steps, steps]
+
+
+# ------------------------------------------------------------------ diffusion / data
+def test_ddim_step():
+    x = torch.randn(64, 3, 64, 64, device=DEV)
+    x0 = torch.randn_like(x) * 2
+    c = ref.ddim_coeffs(2000, 1999, 20)
+    coef = torch.tensor(c, device=DEV)
+    xn, x0c = ops.ddim_step(x, x0, coef)
+    xr, x0r = ref.ddim_step(x, x0, c)
+    close(xn, xr, 1e-4, 1e-5, "x_next")
+    close(x0c, x0r, 0, 0, "x0")
+
+
+def test_randn_stats():
+    out = torch.empty(1_000_001, device=DEV)
+    ops.randn_(out, rng(), 3)
+    assert abs(out.mean().item()) < 5e-3
+    assert abs(out.std().item() - 1) < 5e-3
+    out2 = torch.empty(1001, device=DEV)
+    ops.randn_(out2, rng(), 3)
+    cpu = torch.empty(1001)
+    ops.randn_(cpu, rng().cpu(), 3)
+    close(out2.cpu(), cpu, 1e-4, 1e-4, "randn hip vs cpu")
+
+
+@pytest.mark.parametrize("H", [64, 200, 32])
+def test_pixelate_pair(H):
+    B = 6
+    img = torch.randn(B, 3, H, H, device=DEV)
+    t = torch.tensor([1, 2, 3, 4, 5, 6 if H >= 64 else 5], device=DEV)
+    xt, xtm1 = ops.pixelate_pair(img, None, t, B)
+    for i in range(B):
+        close(xt[i:i + 1], ref.pixelate(img[i:i + 1], 2 ** int(t[i])), 0, 0, "x_t")
+        close(xtm1[i:i + 1], ref.pixelate(img[i:i + 1], 2 ** (int(t[i]) - 1)), 0, 0, "x_t-1")
+
+
+def test_cold_batch_and_q_sample():
+    pool = torch.randn(50, 3, 64, 64, device=DEV)
+    B = 32
+    xt, xtm1 = torch.empty(B, 3, 64, 64, device=DEV), torch.empty(B, 3, 64, 64, device=DEV)
+    t, idx = torch.empty(B, dtype=torch.int64, device=DEV), torch.empty(B, dtype=torch.int64, device=DEV)
+    ops.cold_batch(pool, rng(), 2, xt, xtm1, t, idx, 6)
+    assert t.min().item() >= 1 and t.max().item() <= 6
+    a, b = ops.pixelate_pair(pool, idx, t, B)
+    close(xt, a, 0, 0, "cold x_t")
+    close(xtm1, b, 0, 0, "cold x_t-1")
+    x0 = torch.randn(B, 3, 8, 8, device=DEV)
+    eps = torch.randn_like(x0)
+    tt = torch.randint(0, 2000, (B,), device=DEV)
+    close(ops.q_sample(x0, tt, eps, 2000), ref.q_sample(x0, tt, eps, 2000), 1e-5, 1e-5, "q_sample")
