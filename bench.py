@@ -1,0 +1,159 @@
+#!/usr/bin/env python3
+"""Headline benchmark: train img/s (whole node), ViT-tiny 64x64 cold diffusion.
+
+Config = the reference's measured run (20220822.yaml, ViT-tiny
+D=384 depth 7 12 heads p=8, per-GPU batch 32 = batch_size 16 x2 (AMP),
+AdamW wd 0.05 + clip 1.0 + cosine LR, smooth-L1, cold pixelation task), on
+synthetic Oxford-Flowers-shaped images generated on the device and
+random-init weights (no datasets / checkpoints available offline).
+Weak scaling: per-GPU batch fixed at 32, N ranks, data parallel over RCCL.
+
+Timed region: exactly K full optimizer steps (on-device batch draw + forward +
+loss + backward + bucketed all-reduce + clip + AdamW + LR schedule), bracketed
+by barrier + synchronize on both sides; max over ranks.  Also reports (extra
+keys, rank 0, outside the timed region) the DDIM k=20 / N=64 sampler
+throughput of the hipGraph-captured sampling loop.
+
+    python bench.py                       # 1 GPU
+    torchrun --nproc-per-node N bench.py --gpus N --steps K --warmup W
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import torch
+import torch.distributed as dist
+
+BASELINE_IMG_S_PER_GPU = 709.0  # 22.2 steps/s x 32 img (train.log, RTX 3090 fp16 AMP)
+
+
+def _init_single(dev_index=0):
+    """1-rank RCCL process group (exercises the collective/segmented path on one GPU)."""
+    import datetime
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29517")
+    backend = "nccl" if torch.cuda.is_available() else "gloo"
+    kw = {}
+    if backend == "nccl":
+        torch.cuda.set_device(dev_index)
+        kw["device_id"] = torch.device("cuda", dev_index)
+    dist.init_process_group(backend, rank=0, world_size=1, timeout=datetime.timedelta(seconds=300), **kw)
+    return False
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--model", default="vit_tiny")
+    ap.add_argument("--batch", type=int, default=32, help="per-GPU batch (yaml batch_size 16 x2 for AMP)")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--bucket-blocks", type=int, default=2)
+    ap.add_argument("--no-sampler", action="store_true")
+    ap.add_argument("--no-wgrad-stream", action="store_true")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="init the RCCL process group and run segmented graphs + collectives even with 1 rank")
+    ap.add_argument("--sampler-k", type=int, default=20)
+    ap.add_argument("--sampler-n", type=int, default=64)
+    args = ap.parse_args()
+
+    from ddim_cold_amd.parallel.dist import init_distributed, all_reduce_max, barrier, cleanup, env_world
+    world, rank, local = env_world()
+    distributed = init_distributed(world_size=max(world, 2) if args.force_dist and world == 1 else None) \
+        if not (args.force_dist and world == 1) else _init_single(dev_index=local)
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
+    n = world if distributed else 1
+
+    from ddim_cold_amd.models import build_model
+    from ddim_cold_amd.train.engine import EngineConfig, TrainEngine
+    from ddim_cold_amd.data.synthetic import ColdBatcher, synthetic_pool
+
+    torch.manual_seed(1234)
+    model = build_model(args.model).to(dev).train()
+    base_lr = 0.005
+    lr = base_lr * args.batch * n / 512  # multi_gpu_trainer.py:196
+    cfg = EngineConfig(lr=lr, t_max=512 * 100, use_graph=not args.no_graph, bucket_blocks=args.bucket_blocks,
+                       seed=42, force_segments=args.force_dist,
+                       wgrad_stream=not args.no_wgrad_stream)
+    engine = TrainEngine(model, cfg, device=dev)
+    pool = synthetic_pool(1024, tuple(model.img_size), seed=7 + rank, device=dev)
+    engine.set_batch_fn(ColdBatcher(pool, args.batch, engine.rng))
+
+    for _ in range(args.warmup):
+        engine.train_step()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        engine.train_step()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    elapsed = all_reduce_max(elapsed, dev)
+    loss = float(engine.loss_last.item())
+    if not math.isfinite(loss):
+        raise SystemExit(f"non-finite loss {loss}")
+
+    ms = elapsed / args.steps * 1e3
+    value = n * args.batch * args.steps / elapsed
+    extra = {}
+    if rank == 0 and not args.no_sampler and dev.type == "cuda":
+        from ddim_cold_amd.diffusion.samplers import DDIMSampler
+        model.eval()
+        s = DDIMSampler(model, dev, k=args.sampler_k)
+        g = torch.Generator().manual_seed(0)
+        s.sample(args.sampler_n, generator=g)  # capture
+        torch.cuda.synchronize()
+        reps = 5
+        ts = time.perf_counter()
+        for _ in range(reps):
+            s.sample(args.sampler_n, generator=g)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - ts) / reps
+        extra = {"ddim_sampler_img_per_s": round(args.sampler_n / dt, 1),
+                 "ddim_sampler_ms_per_batch": round(dt * 1e3, 3),
+                 "ddim_sampler_config": {"k": args.sampler_k, "N": args.sampler_n, "steps": len(s.ts),
+                                         "graph": True}}
+        model.train()
+    if rank == 0:
+        out = {
+            "metric": "train imgs/sec (whole node) ViT-tiny 64x64",
+            "value": round(value, 1),
+            "unit": "img/s",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / (BASELINE_IMG_S_PER_GPU * n), 3),
+            "dtype": "bf16",
+            "data": "synthetic (on-device Oxford-Flowers-shaped pool, cold pixelation pairs), random-init weights",
+            "config": {"model": f"{args.model} (D=384, depth=7, heads=12, patch=8, 64x64)", "global_batch": args.batch * n,
+                       "per_gpu_batch": args.batch, "seq_len": model.num_tokens, "parallelism": f"dp{n}",
+                       "graph": not args.no_graph, "bucket_blocks": args.bucket_blocks,
+                       "optimizer": "AdamW(wd=0.05)+clip1.0+cosine", "final_loss": round(loss, 5)},
+        }
+        out.update(extra)
+        print(json.dumps(out), flush=True)
+    cleanup()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,88 @@
+"""Synthetic, Oxford-Flowers-shaped image pools generated on the device.
+
+There is no network access for datasets, so benchmarks and smoke tests use a
+deterministic pool of smooth random RGB images in [-1, 1] (low-frequency
+fields: a coarse random grid bilinearly upsampled plus a few radial "petal"
+patterns), resident in HBM.  Training batches are then drawn *on device*
+inside the captured step (pool index + cold timestep t from the counter RNG,
+pixelation of (x_t, x_{t-1}) in one kernel: ``ops.cold_batch``), replacing the
+reference's CPU DataLoader workers (multi_gpu_trainer.py:63-64,
+diffusion_loader.py:84-97).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+
+SITE_DATA = 3
+SITE_NOISE = 4
+
+
+def synthetic_pool(n: int, size=(64, 64), channels: int = 3, seed: int = 0, device="cpu") -> torch.Tensor:
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    H, W = size
+    coarse = torch.rand(n, channels, 6, 6, generator=g) * 2 - 1
+    img = F.interpolate(coarse, size=(H, W), mode="bicubic", align_corners=False)
+    yy, xx = torch.meshgrid(torch.linspace(-1, 1, H), torch.linspace(-1, 1, W), indexing="ij")
+    r = torch.sqrt(xx ** 2 + yy ** 2)
+    th = torch.atan2(yy, xx)
+    petals = torch.randint(3, 9, (n, 1, 1, 1), generator=g).float()
+    phase = torch.rand(n, 1, 1, 1, generator=g) * 2 * math.pi
+    radius = 0.4 + 0.4 * torch.rand(n, 1, 1, 1, generator=g)
+    flower = torch.sigmoid(12 * (radius * (0.6 + 0.4 * torch.cos(petals * th + phase)) - r))
+    color = torch.rand(n, channels, 1, 1, generator=g) * 2 - 1
+    img = 0.5 * img + flower * color
+    return img.clamp(-1, 1).contiguous().to(device)
+
+
+class ColdBatcher:
+    """Device-side cold-diffusion batch source (graph-capturable).
+
+    Each call draws B pool indices and t ~ U{1..max_t} from the engine's RNG
+    state and writes (x_t, x_{t-1}, t) into static buffers.
+    """
+
+    def __init__(self, pool: torch.Tensor, batch: int, rng: torch.Tensor, max_t: int | None = None):
+        self.pool = pool
+        B, (C, H, W) = batch, pool.shape[1:]
+        self.max_t = max_t or int(math.log2(W))
+        dev = pool.device
+        self.x_t = torch.empty(B, C, H, W, device=dev)
+        self.x_tm1 = torch.empty(B, C, H, W, device=dev)
+        self.t = torch.empty(B, dtype=torch.int64, device=dev)
+        self.idx = torch.empty(B, dtype=torch.int64, device=dev)
+        self.rng = rng
+
+    def __call__(self):
+        ops.cold_batch(self.pool, self.rng, SITE_DATA, self.x_t, self.x_tm1, self.t, self.idx, self.max_t)
+        return self.x_t, self.x_tm1, self.t
+
+
+class GaussianBatcher:
+    """Device-side Gaussian DDIM batch source: (q_sample(x0, t, eps), x0, t) with t ~ U{0..T-1}."""
+
+    def __init__(self, pool: torch.Tensor, batch: int, rng: torch.Tensor, total_steps: int = 2000):
+        self.pool = pool
+        B, (C, H, W) = batch, pool.shape[1:]
+        dev = pool.device
+        self.T = total_steps
+        self.x0 = torch.empty(B, C, H, W, device=dev)
+        self.eps = torch.empty(B, C, H, W, device=dev)
+        self.rng = rng
+        self.u = torch.empty(2 * B, device=dev)
+        self.B = B
+
+    def __call__(self):
+        ops.randn_(self.eps, self.rng, SITE_NOISE)
+        ops.randn_(self.u, self.rng, SITE_DATA)
+        # uniform indices / timesteps from the normal draws via the Gaussian CDF
+        u = 0.5 * (1 + torch.erf(self.u / math.sqrt(2)))
+        idx = (u[: self.B] * self.pool.shape[0]).long().clamp_(0, self.pool.shape[0] - 1)
+        t = (u[self.B:] * self.T).long().clamp_(0, self.T - 1)
+        torch.index_select(self.pool, 0, idx, out=self.x0)
+        x_t = ops.q_sample(self.x0, t, self.eps, self.T)
+        return x_t, self.x0, t

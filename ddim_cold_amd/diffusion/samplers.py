@@ -1,0 +1,266 @@
+"""Samplers: DDIM k-step (+ trajectory), cold de-pixelation, draft->drawing img2img.
+
+Reference behaviour: ``ViT.py:220-256`` (DDIM sampler / sequence),
+``ViT_draft2drawing.py:259-309`` (cold sampler / sequence),
+``ViT_draft2drawing.py:378-419`` (img2img).
+
+MI355X design: the reference issues one H2D timestep copy, ~150 forward
+kernels and ~8 elementwise DDIM kernels per step from Python and syncs with a
+D2H copy per recorded step.  Here the *whole* sampling loop is captured once
+as a hipGraph (static noise buffer, device-resident timestep and coefficient
+tables, the fused ``ddim_step_`` kernel doing clamp + eps-hat + update in one
+fp32 pass, trajectory written to a device buffer and copied back once), so a
+replay is a single host call.  Graphs are cached per (N, k) and re-captured
+if the weights they read were reallocated.
+
+Sampling always runs the denoiser in eval mode (no dropout); the reference's
+``ViT.py`` CLI forgot ``model.eval()``.
+"""
+from __future__ import annotations
+
+import math
+import time
+from typing import List, Optional, Sequence
+
+import torch
+
+from .. import ops
+from .schedule import cold_steps, ddim_coefficients, ddim_table, img2img_alpha
+
+
+def _use_fused(model, device) -> bool:
+    from ..models.vit import _fused_allowed
+    probe = torch.empty(0, device=device)
+    return _fused_allowed(probe)
+
+
+class _Denoiser:
+    """x0-prediction f(x, t) in eval mode via the fused program (GPU) or the reference (CPU)."""
+
+    def __init__(self, model, device):
+        self.model = model
+        self.device = torch.device(device)
+        self.fused = _use_fused(model, self.device)
+        if self.fused:
+            from ..models.program import model_tensors
+            self.prog = model.program()
+            self.P = model_tensors(model)
+            self.rng = torch.zeros(2, dtype=torch.int64, device=self.device)
+
+    def key(self):
+        eng = getattr(self.model, "_engine", None)
+        if eng is not None:
+            return ("engine", id(eng))
+        return tuple((p.data_ptr(), p._version) for p in self.model.parameters())
+
+    def __call__(self, x, t):
+        if self.fused:
+            out, _ = self.prog.forward(self.P, x, t, self.rng, False, save=False)
+            return out
+        was = self.model.training
+        self.model.eval()
+        try:
+            return self.model.forward_reference(x, t)
+        finally:
+            self.model.train(was)
+
+
+def _cache(model) -> dict:
+    return model.__dict__.setdefault("_sampler_graphs", {})
+
+
+class _GraphLoop:
+    """Capture ``body()`` (a full sampling loop on static buffers) into one hipGraph."""
+
+    def __init__(self, body, device):
+        self.body = body
+        self.device = device
+        self.graph = None
+
+    def run(self, use_graph: bool):
+        if not use_graph or self.device.type != "cuda":
+            self.body()
+            return
+        if self.graph is None:
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                self.body()  # warm-up (allocator, kernels); also produces this call's result
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.body()
+            self.graph = g
+            return
+        self.graph.replay()
+
+
+class DDIMSampler:
+    def __init__(self, model, device, k: int = 10, use_graph: bool = True):
+        self.model = model
+        self.device = torch.device(device)
+        self.k = k
+        self.T = model.total_steps
+        self.ts, coef = ddim_table(self.T, k, device=self.device)
+        self.coef = coef
+        self.use_graph = use_graph and self.device.type == "cuda"
+        self.H, self.W = model.img_size
+        self.C = model.in_chans
+
+    def _state(self, N: int, record: bool):
+        key = ("ddim", N, self.k, record, str(self.device))
+        den = _Denoiser(self.model, self.device)
+        cache = _cache(self.model)
+        st = cache.get(key)
+        if st is not None and st["key"] == den.key():
+            return st
+        dev = self.device
+        x = torch.zeros(N, self.C, self.H, self.W, device=dev)
+        x0 = torch.zeros_like(x)
+        tt = torch.tensor(self.ts, dtype=torch.int64, device=dev).unsqueeze(1).expand(-1, N).contiguous()
+        traj = torch.zeros(len(self.ts), N, self.C, self.H, self.W, device=dev) if record else None
+        coef = self.coef
+
+        def body():
+            for i in range(len(self.ts)):
+                x0_raw = den(x, tt[i])
+                ops.ddim_step_(x, x0_raw, x0, coef[i])
+                if traj is not None:
+                    traj[i].copy_(x0)
+
+        st = {"key": den.key(), "x": x, "x0": x0, "traj": traj, "loop": _GraphLoop(body, dev)}
+        cache[key] = st
+        return st
+
+    @torch.no_grad()
+    def sample(self, N: int, generator: Optional[torch.Generator] = None, verbose: bool = False,
+               noise: Optional[torch.Tensor] = None) -> torch.Tensor:
+        st = self._state(N, False)
+        t0 = time.time()
+        if noise is None:
+            noise = torch.normal(0.0, 1.0, (N, self.C, self.H, self.W), generator=generator)
+        st["x"].copy_(noise)
+        st["loop"].run(self.use_graph)
+        out = (st["x0"].cpu() + 1) / 2
+        if verbose:
+            print(f"ddim k={self.k} N={N}: {len(self.ts)} steps in {time.time() - t0:.3f}s")
+        return out
+
+    @torch.no_grad()
+    def sequence(self, N: int, generator: Optional[torch.Generator] = None,
+                 noise: Optional[torch.Tensor] = None) -> List[torch.Tensor]:
+        st = self._state(N, True)
+        if noise is None:
+            noise = torch.normal(0.0, 1.0, (N, self.C, self.H, self.W), generator=generator)
+        st["x"].copy_(noise)
+        first = (noise.cpu() + 1) / 2
+        st["loop"].run(self.use_graph)
+        traj = (st["traj"].cpu() + 1) / 2
+        return [first] + [traj[i] for i in range(traj.shape[0])]
+
+
+class ColdSampler:
+    """Cold de-pixelation sampler: start from constant-colour images, x <- clamp(f(x, t)) for t = S..1."""
+
+    def __init__(self, model, device, use_graph: bool = True, steps: Optional[int] = None):
+        self.model = model
+        self.device = torch.device(device)
+        self.steps = steps or cold_steps(model.img_size[1])
+        self.use_graph = use_graph and self.device.type == "cuda"
+        self.H, self.W = model.img_size
+        self.C = model.in_chans
+
+    def _state(self, N: int):
+        key = ("cold", N, self.steps, str(self.device))
+        den = _Denoiser(self.model, self.device)
+        cache = _cache(self.model)
+        st = cache.get(key)
+        if st is not None and st["key"] == den.key():
+            return st
+        dev = self.device
+        x = torch.zeros(N, self.C, self.H, self.W, device=dev)
+        ts = list(range(self.steps, 0, -1))
+        tt = torch.tensor(ts, dtype=torch.int64, device=dev).unsqueeze(1).expand(-1, N).contiguous()
+        traj = torch.zeros(len(ts), N, self.C, self.H, self.W, device=dev)
+
+        def body():
+            for i in range(len(ts)):
+                x0_raw = den(x, tt[i])
+                torch.clamp(x0_raw, -1.0, 1.0, out=x)
+                traj[i].copy_(x)
+
+        st = {"key": den.key(), "x": x, "traj": traj, "loop": _GraphLoop(body, dev)}
+        cache[key] = st
+        return st
+
+    def _init(self, N, generator):
+        c = torch.normal(0.0, 1.0, (N, self.C), generator=generator)
+        return c[:, :, None, None].expand(-1, -1, self.H, self.W).contiguous()
+
+    @torch.no_grad()
+    def sample(self, N: int, generator=None) -> torch.Tensor:
+        st = self._state(N)
+        st["x"].copy_(self._init(N, generator))
+        st["loop"].run(self.use_graph)
+        return (st["x"].cpu() + 1) / 2
+
+    @torch.no_grad()
+    def sequence(self, N: int, generator=None) -> List[torch.Tensor]:
+        st = self._state(N)
+        init = self._init(N, generator)
+        st["x"].copy_(init)
+        st["loop"].run(self.use_graph)
+        traj = (st["traj"].cpu() + 1) / 2
+        return [(init + 1) / 2] + [traj[i] for i in range(traj.shape[0])]
+
+
+@torch.no_grad()
+def img2img(model, draft: torch.Tensor, t_starts: Sequence[int] = tuple(range(1599, 2000, 50)), k: int = 10,
+            device=None, generator: Optional[torch.Generator] = None, use_graph: bool = True) -> torch.Tensor:
+    """Zero-shot draft->drawing (SDEdit-style) for several noise levels at once.
+
+    For each t_start: x = sqrt(1-a) eps + sqrt(a) draft, a = 1 - sqrt(t_start/T)
+    (ViT_draft2drawing.py:395-396, note t_start/T not (t+1)/T), then DDIM with
+    jump k down to the grid's last step; returns the final x0-hat per t_start
+    as CPU images in [0, 1], shape [len(t_starts), C, H, W].
+
+    All t_starts on one k-grid run as ONE batch with per-sample activity masks
+    (the reference loops them one at a time at batch 1).
+    """
+    device = torch.device(device) if device is not None else next(model.parameters()).device
+    T = model.total_steps
+    starts = list(t_starts)
+    B = len(starts)
+    C, H, W = model.in_chans, *model.img_size
+    if draft.dim() == 3:
+        draft = draft.unsqueeze(0)
+    draft = draft.to(device).float()
+    if draft.shape[0] == 1:
+        draft = draft.expand(B, -1, -1, -1)
+    top = max(starts)
+    if any((top - s) % k for s in starts):
+        # different grids: run them one by one
+        return torch.cat([img2img(model, draft[i:i + 1], [s], k, device, generator, use_graph)
+                          for i, s in enumerate(starts)])
+    ts = list(range(top, 0, -k))
+    if ts[-1] + 1 - k < 0:
+        raise ValueError(f"k={k} incompatible with t_start={top}")
+    eps = torch.normal(0.0, 1.0, (B, C, H, W), generator=generator).to(device)
+    alpha = torch.tensor([img2img_alpha(s, T) for s in starts], device=device).view(B, 1, 1, 1)
+    x = (torch.sqrt(1 - alpha) * eps + torch.sqrt(alpha) * draft).contiguous()
+    x0 = torch.zeros_like(x)
+    st = torch.tensor(starts, device=device)
+    tt = torch.tensor(ts, dtype=torch.int64, device=device).unsqueeze(1).expand(-1, B).contiguous()
+    active = torch.stack([(st >= t) for t in ts]).view(len(ts), B, 1, 1, 1)
+    coef = torch.tensor([ddim_coefficients(T, t, k) for t in ts], dtype=torch.float32, device=device)
+    den = _Denoiser(model, device)
+
+    def body():
+        for i in range(len(ts)):
+            x0_raw = den(x, tt[i])
+            xn, x0c = ops.ddim_step(x, x0_raw, coef[i])
+            torch.where(active[i], xn, x, out=x)
+            torch.where(active[i], x0c, x0, out=x0)
+
+    _GraphLoop(body, device).run(use_graph and device.type == "cuda")
+    return (x0.cpu() + 1) / 2

@@ -58,6 +58,7 @@ class EngineConfig:
     loss_beta: float = 1.0
     ema_decay: float = 0.99
     ema_init: float = 5.0     # multi_gpu_trainer.py:52 (loss_rec = 5.0)
+    force_segments: bool = False  # segmented capture + collectives even at world size 1 (testing)
 
 
 def _align(n: int) -> int:
@@ -72,8 +73,10 @@ class TrainEngine:
         model.to(self.device)
         self.prog = ViTProgram.from_model(model)
         self.pg = process_group
-        self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
-        self.rank = dist.get_rank(process_group) if self.world > 1 else 0
+        self.dist_on = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(process_group) if self.dist_on else 1
+        self.rank = dist.get_rank(process_group) if self.dist_on else 0
+        self.segmented = self.world > 1 or cfg.force_segments
         self.is_cuda = self.device.type == "cuda"
         self._build_arenas()
         dev = self.device
@@ -86,7 +89,7 @@ class TrainEngine:
         self.loss_last = torch.zeros(1, dtype=torch.float32, device=dev)
         self.loss_ema = torch.full((1,), cfg.ema_init, dtype=torch.float32, device=dev)
         self.side = torch.cuda.Stream(device=dev) if (self.is_cuda and cfg.wgrad_stream) else None
-        self.comm = torch.cuda.Stream(device=dev) if (self.is_cuda and self.world > 1) else None
+        self.comm = torch.cuda.Stream(device=dev) if (self.is_cuda and self.segmented) else None
         self._graphs: Optional[List[torch.cuda.CUDAGraph]] = None
         self._eager_steps = 0
         self.batch_fn: Optional[Callable] = None
@@ -196,7 +199,7 @@ class TrainEngine:
         yield ("done", -1)
 
     def _allreduce(self, k: int):
-        if self.world <= 1:
+        if not self.dist_on or (self.world <= 1 and not self.cfg.force_segments):
             return
         a, b = self.buckets[k]
         view = self.flat_g[a:b]
@@ -223,7 +226,7 @@ class TrainEngine:
         pool = torch.cuda.graph_pool_handle()
         graphs = []
         gen = self._step_iter()
-        nseg = len(self.buckets) + 1 if self.world > 1 else 1
+        nseg = len(self.buckets) + 1 if self.segmented else 1
         if nseg == 1:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool):
