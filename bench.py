@@ -56,7 +56,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--bucket-blocks", type=int, default=2)
     ap.add_argument("--no-sampler", action="store_true")
-    ap.add_argument("--no-wgrad-stream", action="store_true")
+    ap.add_argument("--wgrad-stream", action="store_true")
     ap.add_argument("--force-dist", action="store_true",
                     help="init the RCCL process group and run segmented graphs + collectives even with 1 rank")
     ap.add_argument("--sampler-k", type=int, default=20)
@@ -84,7 +84,7 @@ def main():
     lr = base_lr * args.batch * n / 512  # multi_gpu_trainer.py:196
     cfg = EngineConfig(lr=lr, t_max=512 * 100, use_graph=not args.no_graph, bucket_blocks=args.bucket_blocks,
                        seed=42, force_segments=args.force_dist,
-                       wgrad_stream=not args.no_wgrad_stream)
+                       wgrad_stream=args.wgrad_stream)
     engine = TrainEngine(model, cfg, device=dev)
     pool = synthetic_pool(1024, tuple(model.img_size), seed=7 + rank, device=dev)
     engine.set_batch_fn(ColdBatcher(pool, args.batch, engine.rng))

@@ -109,6 +109,7 @@ def build(force: bool = False, jobs: int | None = None, resource_usage: bool = F
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-8000:]}")
+        _check_stubs(OUT + ".tmp")
         os.replace(OUT + ".tmp", OUT)
         with open(OUT + ".objs", "w") as fh:
             fh.write("\n".join(os.path.basename(o) for o in objs))
@@ -117,6 +118,15 @@ def build(force: bool = False, jobs: int | None = None, resource_usage: bool = F
     elif verbose:
         print(f"[ddim_cold_amd.build] up to date: {OUT}")
     return OUT
+
+
+def _check_stubs(so):
+    """Fail the build if any kernel launch stub is undefined (a hipcc template-instantiation bug)."""
+    r = subprocess.run(["nm", "-u", so], capture_output=True, text=True)
+    bad = [l.split()[-1] for l in r.stdout.splitlines() if "__device_stub__" in l]
+    if bad:
+        os.remove(so)
+        raise RuntimeError("undefined kernel launch stubs (add explicit instantiations):\n  " + "\n  ".join(bad))
 
 
 def _stale_link(objs):

@@ -11,6 +11,7 @@
 #include <c10/core/DeviceGuard.h>
 
 #include "kernels.h"
+#include <cstdlib>
 
 using at::Tensor;
 
@@ -184,10 +185,11 @@ std::tuple<Tensor, Tensor> smooth_l1_fwd_bwd(Tensor pred, Tensor target, int64_t
   TORCH_CHECK(pred.sizes() == target.sizes() && pred.dim() == 4, "pred/target shape");
   const int B = pred.size(0), C = pred.size(1), H = pred.size(2), W = pred.size(3);
   TORCH_CHECK(N == (H / patch) * (W / patch) + 1, "token count");
-  auto loss = at::zeros({1}, pred.options());
+  auto loss = at::empty({1}, pred.options());
+  auto parts = at::empty({L1_PARTS}, pred.options());
   auto dtok = at::empty({(int64_t)B * N, C * patch * patch}, pred.options().dtype(BF16));
-  smooth_l1_launch(pred.data_ptr<float>(), target.data_ptr<float>(), loss.data_ptr<float>(), dtok.data_ptr(), B, C,
-                   H, W, patch, (float)beta, cur_stream());
+  smooth_l1_launch(pred.data_ptr<float>(), target.data_ptr<float>(), loss.data_ptr<float>(), parts.data_ptr<float>(),
+                   dtok.data_ptr(), B, C, H, W, patch, (float)beta, cur_stream());
   return {loss, dtok};
 }
 
@@ -250,10 +252,17 @@ void linear_wgrad(Tensor dy, Tensor x, Tensor dw, c10::optional<Tensor> db) {
   g.A = dy.data_ptr(); g.B = x.data_ptr();
   g.M = Nout; g.N = K; g.K = M; g.lda = Nout; g.ldb = K;
   g.C = dw.data_ptr(); g.ldc = K; g.bias = dbp;
-  // split the token reduction so the grid fills the chip (fp32 atomics combine slices)
+  // split the token reduction so the grid fills the chip; fp32 atomics combine the
+  // slices, so keep the split count small (atomic bytes = splits x |dW|, chip-wide
+  // atomic rate ~1.3 TB/s)
   const int tiles = ((Nout + 63) / 64) * ((K + 63) / 64);
   const int kt = (M + 63) / 64;
-  int splits = (512 + tiles - 1) / tiles;
+  static const int max_splits = [] {
+    const char* e = getenv("DDIM_COLD_WGRAD_SPLITS");
+    return e ? atoi(e) : 8;
+  }();
+  int splits = (256 + tiles - 1) / tiles;
+  if (splits > max_splits) splits = max_splits;
   if (splits > kt) splits = kt;
   if (splits < 1) splits = 1;
   gemm_wgrad(g, splits, cur_stream());
@@ -262,7 +271,7 @@ void linear_wgrad(Tensor dy, Tensor x, Tensor dw, c10::optional<Tensor> db) {
 std::tuple<Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma,
                                          c10::optional<Tensor> g_res, Tensor dgamma, Tensor dbeta, int64_t N,
                                          Tensor rng, int64_t site_drop, double p_drop, int64_t site_dp, double p_dp,
-                                         bool emit_gy) {
+                                         bool emit_gy, c10::optional<Tensor> ws) {
   CHECK_IN(dy, F32); CHECK_IN(x, F32); CHECK_IN(mean, F32); CHECK_IN(rstd, F32); CHECK_IN(gamma, F32);
   CHECK_IN(dgamma, F32); CHECK_IN(dbeta, F32); check_rng(rng);
   const c10::DeviceGuard guard(x.device());
@@ -276,13 +285,34 @@ std::tuple<Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tenso
     TORCH_CHECK(g_res->numel() == x.numel(), "g_res shape");
     gr = g_res->data_ptr<float>();
   }
+  const int R = ln_replicas();
+  const bool own_ws = !(ws.has_value() && ws->defined());
+  Tensor w = own_ws ? at::zeros({R, 2 * D}, x.options()) : *ws;
+  if (!own_ws) {
+    CHECK_IN(w, F32);
+    TORCH_CHECK(w.numel() == (int64_t)R * 2 * D, "ln ws must hold ln_replicas x 2D floats");
+  }
   auto g_out = at::empty(x.sizes(), x.options());
   Tensor gy = emit_gy ? at::empty({M, D}, x.options().dtype(BF16)) : at::empty({0}, x.options().dtype(BF16));
   layernorm_bwd_launch(dy.data_ptr<float>(), x.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                        gamma.data_ptr<float>(), gr, g_out.data_ptr<float>(), emit_gy ? gy.data_ptr() : nullptr,
-                       dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), M, D, N, rng.data_ptr<int64_t>(),
-                       site_drop, p_drop, site_dp, p_dp, cur_stream());
+                       w.data_ptr<float>(), M, D, N, rng.data_ptr<int64_t>(), site_drop, p_drop, site_dp, p_dp,
+                       cur_stream());
+  if (own_ws) {
+    auto s = w.sum(0);
+    dgamma.add_(s.narrow(0, 0, D));
+    dbeta.add_(s.narrow(0, D, D));
+  }
   return {g_out, gy};
+}
+
+void replica_reduce_(Tensor ws, Tensor dst_ptrs, int64_t C) {
+  CHECK_IN(ws, F32); CHECK_IN(dst_ptrs, I64);
+  const c10::DeviceGuard guard(ws.device());
+  const int G = dst_ptrs.numel();
+  TORCH_CHECK(ws.numel() == (int64_t)G * ln_replicas() * C, "replica ws shape");
+  replica_reduce_launch(ws.data_ptr<float>(), reinterpret_cast<float* const*>(dst_ptrs.data_ptr<int64_t>()), G, C,
+                        cur_stream());
 }
 
 Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, double scale, Tensor rng, int64_t site, double p) {
@@ -318,6 +348,7 @@ Tensor embed_bwd(Tensor g, Tensor t, Tensor rng, int64_t site, double p, Tensor 
 
 void sqnorm(Tensor g, Tensor out, double scale) {
   CHECK_IN(g, F32); CHECK_IN(out, F32);
+  TORCH_CHECK(out.numel() >= SQ_PARTS, "sqnorm: out must hold SQ_PARTS partials");
   const c10::DeviceGuard guard(g.device());
   sqnorm_launch(g.data_ptr<float>(), g.numel(), out.data_ptr<float>(), (float)scale, cur_stream());
 }
@@ -330,6 +361,7 @@ void adamw_step(Tensor p, Tensor g, Tensor m, Tensor v, c10::optional<Tensor> pb
   const int64_t n = p.numel();
   TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n && hyper.numel() >= 8 && step.numel() >= 2,
               "adamw shapes");
+  TORCH_CHECK(sq.numel() >= SQ_PARTS, "adamw: sq must hold SQ_PARTS partials");
   void* pb = nullptr;
   if (pbf.has_value() && pbf->defined()) {
     CHECK_IN((*pbf), BF16);
@@ -347,6 +379,7 @@ void advance_counters(Tensor step, Tensor rng, c10::optional<Tensor> sq) {
   const float* s = nullptr;
   if (sq.has_value() && sq->defined()) {
     CHECK_IN((*sq), F32);
+    TORCH_CHECK(sq->numel() >= SQ_PARTS, "advance: sq must hold SQ_PARTS partials");
     s = sq->data_ptr<float>();
   }
   advance_counters_launch(step.data_ptr<int64_t>(), rng.data_ptr<int64_t>(), s, cur_stream());
@@ -441,7 +474,8 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("linear_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, Tensor(b!)? db) -> ()");
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor? g_res, "
         "Tensor(a!) dgamma, Tensor(b!) dbeta, int N, Tensor rng, int site_drop, float p_drop, int site_dp, "
-        "float p_dp, bool emit_gy) -> (Tensor, Tensor)");
+        "float p_dp, bool emit_gy, Tensor(c!)? ws=None) -> (Tensor, Tensor)");
+  m.def("replica_reduce_(Tensor(a!) ws, Tensor dst_ptrs, int C) -> ()");
   m.def("attn_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, float scale, Tensor rng, int site, float p) -> Tensor");
   m.def("embed_bwd(Tensor g, Tensor t, Tensor rng, int site, float p, Tensor(a!) dcls, Tensor(b!) dpos, "
         "Tensor(c!) dtemb) -> Tensor");
@@ -472,6 +506,7 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("linear_dgrad_gelu", &linear_dgrad_gelu);
   m.impl("linear_wgrad", &linear_wgrad);
   m.impl("layernorm_bwd", &layernorm_bwd);
+  m.impl("replica_reduce_", &replica_reduce_);
   m.impl("attn_bwd", &attn_bwd);
   m.impl("embed_bwd", &embed_bwd);
   m.impl("sqnorm", &sqnorm);

@@ -62,7 +62,15 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const float* __restrict_
     if (e >= N * D) return;
     const int n = e / D, d = e - n * D;
     float s = 0.f;
-    for (int b = 0; b < B; ++b) s += gm(((size_t)b * N + n) * D + d);
+    int b = 0;
+    for (; b + 8 <= B; b += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = g[((size_t)(b + u) * N + n) * D + d];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += thr ? (dropout_keep(salt, (uint32_t)(((size_t)(b + u) * N + n) * D + d), thr) ? v[u] * dsc : 0.f) : v[u];
+    }
+    for (; b < B; ++b) s += gm(((size_t)b * N + n) * D + d);
     dpos[e] += s;
     if (n == 0) dcls[d] += s;
   } else if (bid < blocksA + blocksB) {
@@ -70,8 +78,17 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const float* __restrict_
     if (e >= B * D) return;
     const int b = e / D, d = e - b * D;
     float s = 0.f;
-    for (int n = 0; n < N; ++n) s += gm(((size_t)b * N + n) * D + d);
-    atomicAdd(dtemb + (size_t)t[b] * D + d, s);
+    int n = 0;
+    for (; n + 8 <= N; n += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = g[((size_t)b * N + n + u) * D + d];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += thr ? (dropout_keep(salt, (uint32_t)(((size_t)b * N + n + u) * D + d), thr) ? v[u] * dsc : 0.f) : v[u];
+    }
+    for (; n < N; ++n) s += gm(((size_t)b * N + n) * D + d);
+    const int64_t tb = t[b];
+    atomicAdd(dtemb + (size_t)tb * D + d, s);
   } else {
     const size_t total = (size_t)B * (N - 1) * D;
     for (size_t e = (size_t)(bid - blocksA - blocksB) * 256 + threadIdx.x; e < total;
@@ -86,7 +103,7 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const float* __restrict_
 
 template <bool LOSS>
 __global__ __launch_bounds__(256) void tokgrad_kernel(const float* __restrict__ pred, const float* __restrict__ target,
-                                                      float* __restrict__ loss, bf16* __restrict__ dtok, int B, int C,
+                                                      float* __restrict__ parts, bf16* __restrict__ dtok, int B, int C,
                                                       int H, int W, int P, float beta, float inv_numel) {
   __shared__ float red[4];
   const int Wp = W / P, NP = (H / P) * Wp, N = NP + 1, F = C * P * P;
@@ -125,8 +142,18 @@ __global__ __launch_bounds__(256) void tokgrad_kernel(const float* __restrict__ 
     acc = wave_sum(acc);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
     __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(loss, (red[0] + red[1] + red[2] + red[3]) * inv_numel);
+    if (threadIdx.x == 0) parts[blockIdx.x] = (red[0] + red[1] + red[2] + red[3]) * inv_numel;
   }
+}
+
+__global__ __launch_bounds__(256) void sum_parts_kernel(const float* __restrict__ parts, int n, float* __restrict__ out) {
+  __shared__ float red[4];
+  float v = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) v += parts[i];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = red[0] + red[1] + red[2] + red[3];
 }
 
 static int grid_for(size_t n) {
@@ -160,12 +187,15 @@ void embed_bwd_launch(const float* g, const int64_t* t, float* dcls, float* dpos
                      dtemb, reinterpret_cast<bf16*>(gpatch), B, N, D, rng, site, thr, dsc, blocksA, blocksB);
 }
 
-void smooth_l1_launch(const float* pred, const float* target, float* loss, void* dtok, int B, int C, int H, int W,
-                      int patch, float beta, hipStream_t stream) {
+void smooth_l1_launch(const float* pred, const float* target, float* loss, float* partials, void* dtok, int B,
+                      int C, int H, int W, int patch, float beta, hipStream_t stream) {
   const size_t n_img = (size_t)B * C * H * W;
   const size_t n = n_img + (size_t)B * C * patch * patch;
-  hipLaunchKernelGGL(tokgrad_kernel<true>, dim3(grid_for(n)), dim3(256), 0, stream, pred, target, loss,
+  int grid = grid_for(n);
+  if (grid > L1_PARTS) grid = L1_PARTS;
+  hipLaunchKernelGGL(tokgrad_kernel<true>, dim3(grid), dim3(256), 0, stream, pred, target, partials,
                      reinterpret_cast<bf16*>(dtok), B, C, H, W, patch, beta, 1.0f / (float)n_img);
+  hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(256), 0, stream, partials, grid, loss);
 }
 
 void img_to_tokgrad_launch(const float* dimg, void* dtok, int B, int C, int H, int W, int patch, hipStream_t stream) {

@@ -26,6 +26,7 @@
 // Reference semantics covered: nn.Linear / Conv2d-as-GEMM in ViT.py:79-103,150,183.
 #include "common.h"
 #include "kernels.h"
+#include <cstdlib>
 
 namespace dc {
 
@@ -60,6 +61,14 @@ struct GemmParams {
 };
 
 constexpr int BK = 64;
+
+static bool dma_disabled() {
+  static const bool off = [] {
+    const char* e = getenv("DDIM_COLD_GEMM_NO_DMA");
+    return e && e[0] == '1';
+  }();
+  return off;
+}
 
 __device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
 
@@ -120,19 +129,38 @@ __device__ __forceinline__ bf16x8 frag_k_perm(const char* lds, int r, int s, int
   u32x4 v = {lo[0], lo[1], hi[0], hi[1]};
   return __builtin_bit_cast(bf16x8, v);
 }
+// Epilogue in two phases: (1) every global load the epilogue needs (bias per
+// column, residual / saved pre-activation / pos+time embedding per element) is
+// issued for the whole fragment tile, (2) compute + store.  Interleaving them
+// per element serialises the tile on memory latency (the loads may alias the
+// stores through GemmParams, so the compiler cannot hoist them).
 template <int EPI>
-__device__ __forceinline__ void epilogue(const GemmParams& p, int m, int n, float v, uint32_t salt_drop,
-                                         uint32_t salt_dp) {
+__device__ __forceinline__ bool epi_needs_elem() {
+  return EPI == EPI_RESID || EPI == EPI_DGELU || EPI == EPI_EMBED;
+}
+template <int EPI>
+__device__ __forceinline__ float epi_load_elem(const GemmParams& p, int m, int n) {
+  if (EPI == EPI_RESID) return p.res[(size_t)m * p.N + n];
+  if (EPI == EPI_DGELU) return bf2f(p.aux[(size_t)m * p.N + n]);
+  if (EPI == EPI_EMBED) {
+    const int Pn = p.tokens;
+    const int b = m / Pn, patch = m - b * Pn;
+    return p.pos[(size_t)(patch + 1) * p.emb_dim + n] + p.temb[(size_t)p.tsteps[b] * p.emb_dim + n];
+  }
+  return 0.f;
+}
+
+template <int EPI>
+__device__ __forceinline__ void epilogue(const GemmParams& p, int m, int n, float v, float bias, float pre,
+                                         uint32_t salt_drop, uint32_t salt_dp) {
+  v += bias;
   if (EPI == EPI_BF16) {
-    if (p.bias) v += p.bias[n];
     reinterpret_cast<bf16*>(p.C)[(size_t)m * p.ldc + n] = f2bf(v);
   } else if (EPI == EPI_F32) {
-    if (p.bias) v += p.bias[n];
     reinterpret_cast<float*>(p.C)[(size_t)m * p.ldc + n] = v;
   } else if (EPI == EPI_ATOMIC) {
     atomicAdd(reinterpret_cast<float*>(p.C) + (size_t)m * p.ldc + n, v);
   } else if (EPI == EPI_QKV) {
-    if (p.bias) v += p.bias[n];
     const int D = p.heads * p.hd;
     const int s = n / D, rem = n - s * D;
     const int h = rem / p.hd, d = rem - h * p.hd;
@@ -140,16 +168,14 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int m, int n, floa
     const size_t idx = ((((size_t)s * p.batch + b) * p.heads + h) * p.tokens + tok) * p.hd + d;
     reinterpret_cast<bf16*>(p.C)[idx] = f2bf(v);
   } else if (EPI == EPI_RESID) {
-    if (p.bias) v += p.bias[n];
     const size_t idx = (size_t)m * p.N + n;
     if (p.thr_drop) v = dropout_keep(salt_drop, (uint32_t)idx, p.thr_drop) ? v * p.scale_drop : 0.f;
     if (p.thr_dp) {
       const int b = m / p.tokens;
       v = dropout_keep(salt_dp, (uint32_t)b, p.thr_dp) ? v * p.scale_dp : 0.f;
     }
-    reinterpret_cast<float*>(p.C)[idx] = p.res[idx] + v;
+    reinterpret_cast<float*>(p.C)[idx] = pre + v;
   } else if (EPI == EPI_GELU) {
-    if (p.bias) v += p.bias[n];
     const size_t idx = (size_t)m * p.N + n;
     reinterpret_cast<bf16*>(p.C)[idx] = f2bf(v);
     float h = gelu_f(v);
@@ -158,28 +184,58 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int m, int n, floa
   } else if (EPI == EPI_DGELU) {
     const size_t idx = (size_t)m * p.N + n;
     if (p.thr_drop) v = dropout_keep(salt_drop, (uint32_t)idx, p.thr_drop) ? v * p.scale_drop : 0.f;
-    v *= gelu_grad_f(bf2f(p.aux[idx]));
-    reinterpret_cast<bf16*>(p.C)[idx] = f2bf(v);
+    reinterpret_cast<bf16*>(p.C)[idx] = f2bf(v * gelu_grad_f(pre));
   } else if (EPI == EPI_HEAD) {
     const int b = m / p.tokens, tok = m - b * p.tokens;
     if (tok == 0) return;
-    if (p.bias) v += p.bias[n];
     const int P = p.patch;
     const int Wp = p.img_w / P;
     const int patch = tok - 1, hp = patch / Wp, wp = patch - hp * Wp;
     const int c = n % p.chans, ab = n / p.chans, a = ab / P, bb = ab - a * P;
     reinterpret_cast<float*>(p.C)[(((size_t)b * p.chans + c) * p.img_h + hp * P + a) * p.img_w + wp * P + bb] = v;
   } else if (EPI == EPI_EMBED) {
-    // m = b*P + patch ; token row = b*(P+1) + 1 + patch
-    const int Pn = p.tokens;  // patches per sample
+    const int Pn = p.tokens;
     const int b = m / Pn, patch = m - b * Pn;
-    const int tok = patch + 1;
-    const size_t row = (size_t)b * (Pn + 1) + tok;
-    v += p.bias[n] + p.pos[(size_t)tok * p.emb_dim + n] + p.temb[(size_t)p.tsteps[b] * p.emb_dim + n];
-    const size_t idx = row * p.emb_dim + n;
+    const size_t idx = ((size_t)b * (Pn + 1) + patch + 1) * p.emb_dim + n;
+    v += pre;
     if (p.thr_drop) v = dropout_keep(salt_drop, (uint32_t)idx, p.thr_drop) ? v * p.scale_drop : 0.f;
     reinterpret_cast<float*>(p.C)[idx] = v;
   }
+}
+
+// whole-tile epilogue: acc[FM][FN] fragment tiles at (mb + i*16 + 4g + r, nb + j*16 + li)
+template <int EPI, int FM, int FN>
+__device__ __forceinline__ void run_epilogue(const GemmParams& p, const f32x4 (&acc)[FM][FN], int mb, int nb,
+                                             int g, int li) {
+  float colb[FN];
+  const bool has_bias = (EPI != EPI_ATOMIC) && p.bias != nullptr;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = nb + j * 16 + li;
+    colb[j] = (has_bias && n < p.N) ? p.bias[n] : 0.f;
+  }
+  float pre[FM][FN][4];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = mb + i * 16 + 4 * g + r, n = nb + j * 16 + li;
+        pre[i][j][r] = (epi_needs_elem<EPI>() && m < p.M && n < p.N) ? epi_load_elem<EPI>(p, m, n) : 0.f;
+      }
+  uint32_t salt_drop = 0, salt_dp = 0;
+  if (p.thr_drop) salt_drop = site_salt(p.rng, p.site_drop);
+  if (p.thr_dp) salt_dp = site_salt(p.rng, p.site_dp);
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = mb + i * 16 + 4 * g + r, n = nb + j * 16 + li;
+        if (m < p.M && n < p.N) epilogue<EPI>(p, m, n, acc[i][j][r], colb[j], pre[i][j][r], salt_drop, salt_dp);
+      }
 }
 
 template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EPI>
@@ -218,9 +274,14 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // fused bias-gradient column sum (wgrad with AT: A image is [k][BM])
-  const bool do_db = (EPI == EPI_ATOMIC) && AT && (p.bias != nullptr) && (tn == 0);
-  float db_acc = 0.f;
+  // fused bias-gradient row sums of A (wgrad): one extra MFMA vs an all-ones fragment
+  const bool do_db = (EPI == EPI_ATOMIC) && AT && (p.bias != nullptr) && (tn == 0) && (wn == 0);
+  f32x4 dbacc[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) dbacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = f2bf(1.f);
 
   SA sa;
   SB sb;
@@ -241,13 +302,6 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
     }
     const char* la = smem + cur * STAGE_BYTES;
     const char* lb = la + SA::BYTES;
-    if (AT && do_db && threadIdx.x < BM) {
-      const char* col = la + threadIdx.x * 2;
-      float s = 0.f;
-#pragma unroll 8
-      for (int r = 0; r < BK; ++r) s += bf2f(*reinterpret_cast<const bf16*>(col + r * SA::STRIDE_T));
-      db_acc += s;
-    }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       bf16x8 af[FM], bfr[FN];
@@ -269,6 +323,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+      if (EPI == EPI_ATOMIC && AT && do_db) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) dbacc[i] = mfma16(af[i], ones, dbacc[i]);
+      }
     }
     if (more) {
       sa.store(smem + (cur ^ 1) * STAGE_BYTES);
@@ -278,21 +336,221 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
     cur ^= 1;
   }
 
-  if (do_db && threadIdx.x < BM && m0 + (int)threadIdx.x < p.M) atomicAdd(const_cast<float*>(p.bias) + m0 + threadIdx.x, db_acc);
-
-  uint32_t salt_drop = 0, salt_dp = 0;
-  if (p.thr_drop) salt_drop = site_salt(p.rng, p.site_drop);
-  if (p.thr_dp) salt_dp = site_salt(p.rng, p.site_dp);
+  if (EPI == EPI_ATOMIC && AT && do_db && li == 0) {
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm * TM + i * 16 + 4 * g + r;
-        const int n = n0 + wn * TN + j * 16 + li;
-        if (m < p.M && n < p.N) epilogue<EPI>(p, m, n, acc[i][j][r], salt_drop, salt_dp);
+        if (m < p.M) atomicAdd(const_cast<float*>(p.bias) + m, dbacc[i][r]);
       }
+  }
+
+  run_epilogue<EPI, FM, FN>(p, acc, m0 + wm * TM, n0 + wn * TN, g, li);
+}
+
+
+// ============================================================================ LDS-DMA ring variant
+// Operand tiles go global -> LDS with bounds-checked `buffer_load_dwordx4 ... lds`
+// (no VGPR staging; rows past the end of a tensor read as zero, so ragged M / K
+// tails need no masking), up to S-1 K-tiles in flight behind counted
+// `s_waitcnt vmcnt(N)` and ONE raw s_barrier per K-tile (a __syncthreads would
+// emit vmcnt(0) and drain the ring).  LDS images (128-B rows, 1-KiB DMA pieces
+// = 8 rows each, swizzle applied on the per-lane SOURCE address):
+//   k-contiguous operand  [rows][64 k]  chunk' = chunk ^ ((row>>1)&7)
+//   transposed operand    [64 k][64]    chunk' = chunk ^ (row & 6)   (tr-read conflict-free)
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <int LPT>
+__device__ __forceinline__ void vm_wait_rem(int rem) {
+  switch (rem) {
+    case 0: vm_wait<0>(); break;
+    case 1: vm_wait<LPT>(); break;
+    case 2: vm_wait<2 * LPT>(); break;
+    case 3: vm_wait<3 * LPT>(); break;
+    default: vm_wait<4 * LPT>(); break;
+  }
+}
+__device__ __forceinline__ void raw_barrier() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ bf16x8 frag_t_swz(const char* lds, int c0, int s, int lane) {
+  const int i = lane & 15, g = lane >> 4, q = i >> 2, p = i & 3;
+  const int ra = 32 * s + 4 * g + q;
+  const int chunk = (c0 >> 3) + (p >> 1);
+  const int off = ra * 128 + 16 * (chunk ^ (ra & 6)) + 8 * (p & 1);
+  const bf16x4 lo = lds_read_tr(reinterpret_cast<const bf16*>(lds + off));
+  const bf16x4 hi = lds_read_tr(reinterpret_cast<const bf16*>(lds + off + 16 * 128));
+  bf16x8 v;
+  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  return v;
+}
+
+template <int R, bool T>
+struct DmaOperand {
+  static constexpr int BYTES = R * 128;          // one 64-deep K tile
+  static constexpr int PER_WAVE = BYTES / 4096;  // 1-KiB pieces per wave
+  bf16* base;
+  int nbytes;
+  int voff[PER_WAVE];  // per-lane byte offset of piece j at k-tile 0
+  int kstep;           // byte advance per K tile
+
+  __device__ __forceinline__ void init(const bf16* base, int ld, int rows_total_bytes_rows, int row0, int wave,
+                                       int lane) {
+    // rows_total_bytes_rows: number of rows of the stored matrix (for the OOB range)
+    this->base = const_cast<bf16*>(base);
+    nbytes = rows_total_bytes_rows * ld * 2;
+#pragma unroll
+    for (int j = 0; j < PER_WAVE; ++j) {
+      const int piece = wave * PER_WAVE + j;
+      const int r = piece * 8 + (lane >> 3), pc = lane & 7;
+      if (!T) {
+        const int lc = pc ^ ((r >> 1) & 7);
+        voff[j] = ((row0 + r) * ld + 8 * lc) * 2;
+      } else {
+        const int lc = pc ^ (r & 6);
+        voff[j] = (r * ld + row0 + 8 * lc) * 2;
+      }
+    }
+    kstep = T ? 64 * ld * 2 : 64 * 2;
+  }
+  __device__ __forceinline__ void issue(char* lds_tile, int kt, int wave) const {
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, nbytes, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < PER_WAVE; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsrc, (DC_LDS void*)(lds_tile + (wave * PER_WAVE + j) * 1024), 16, voff[j] + kt * kstep, 0, 0, 0);
+  }
+};
+
+template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EPI, int S>
+__global__ __launch_bounds__(256) void gemm_dma_kernel(GemmParams p) {
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(!AT || BM == 64, "transposed A needs BM == 64");
+  static_assert(!BT || BN == 64, "transposed B needs BN == 64");
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr bool PERM = AT || BT;
+  using OA = DmaOperand<BM, AT>;
+  using OB = DmaOperand<BN, BT>;
+  constexpr int STAGE = OA::BYTES + OB::BYTES;
+  constexpr int LPT = OA::PER_WAVE + OB::PER_WAVE;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tiles_n = (p.N + BN - 1) / BN;
+  const int tiles_m = (p.M + BM - 1) / BM;
+  const int nwg = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, idx = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+  }
+  const int tm = bid / tiles_n, tn = bid - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int total_kt = (p.K + BK - 1) / BK;
+  const int kt0 = blockIdx.z * p.ktiles_per_split;
+  const int nk = min(total_kt, kt0 + p.ktiles_per_split) - kt0;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int g = lane >> 4, li = lane & 15;
+
+  OA oa;
+  OB ob;
+  // stored A: non-T [M][lda] (rows M) ; T [K][lda] (rows K).  Same for B with N.
+  oa.init(p.A, p.lda, AT ? p.K : p.M, m0, wave, lane);
+  ob.init(p.B, p.ldb, BT ? p.K : p.N, n0, wave, lane);
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // fused bias gradient (wgrad): row sums of A via one extra MFMA against an
+  // all-ones fragment per k-step, in the waves of the first column tile only
+  const bool do_db = (EPI == EPI_ATOMIC) && AT && (p.bias != nullptr) && (tn == 0) && (wn == 0);
+  f32x4 dbacc[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) dbacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = f2bf(1.f);
+
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nk) {
+      oa.issue(smem + s * STAGE, kt0 + s, wave);
+      ob.issue(smem + s * STAGE + OA::BYTES, kt0 + s, wave);
+    }
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int rem = min(S - 2, nk - 1 - kt);
+    vm_wait_rem<LPT>(rem);
+    raw_barrier();
+    if (kt + S - 1 < nk) {
+      const int st = (kt + S - 1) % S;
+      oa.issue(smem + st * STAGE, kt0 + kt + S - 1, wave);
+      ob.issue(smem + st * STAGE + OA::BYTES, kt0 + kt + S - 1, wave);
+    }
+    const char* la = smem + (kt % S) * STAGE;
+    const char* lb = la + OA::BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int r = wm * TM + i * 16;
+        if (AT) af[i] = frag_t_swz(la, r, s, lane);
+        else if (PERM) af[i] = frag_k_perm(la, r + li, s, g);
+        else af[i] = frag_k(la, r + li, s, g);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int r = wn * TN + j * 16;
+        if (BT) bfr[j] = frag_t_swz(lb, r, s, lane);
+        else if (PERM) bfr[j] = frag_k_perm(lb, r + li, s, g);
+        else bfr[j] = frag_k(lb, r + li, s, g);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+      if (EPI == EPI_ATOMIC && AT && do_db) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) dbacc[i] = mfma16(af[i], ones, dbacc[i]);
+      }
+    }
+  }
+
+  if (EPI == EPI_ATOMIC && AT && do_db && li == 0) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * TM + i * 16 + 4 * g + r;
+        if (m < p.M) atomicAdd(const_cast<float*>(p.bias) + m, dbacc[i][r]);
+      }
+  }
+
+  run_epilogue<EPI, FM, FN>(p, acc, m0 + wm * TM, n0 + wn * TN, g, li);
+}
+
+template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EPI>
+static void launch_dma(GemmParams p, int splits, hipStream_t stream) {
+  constexpr int S = 4;
+  constexpr int lds = S * (BM * 128 + BN * 128);
+  const int total_kt = (p.K + BK - 1) / BK;
+  p.ktiles_per_split = (total_kt + splits - 1) / splits;
+  splits = (total_kt + p.ktiles_per_split - 1) / p.ktiles_per_split;
+  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, WM, WN, AT, BT, EPI, S>), dim3(tiles, 1, splits), dim3(256), lds,
+                     stream, p);
 }
 
 template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EPI>
@@ -308,13 +566,54 @@ static void launch_cfg(GemmParams p, int splits, hipStream_t stream) {
   hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, AT, BT, EPI>), grid, dim3(256), lds, stream, p);
 }
 
-// tile choice: 64x64 when it yields >= ~1 wave of workgroups per CU, else 32x64
+// (tag dispatch instead of `if constexpr`: hipcc 7.2 silently drops the host
+// stub of a kernel template first referenced inside an if-constexpr branch)
+template <bool AT, bool BT, int EPI>
+struct DmaSmall {
+  static void launch(GemmParams p, int splits, hipStream_t stream, bool big) {
+    if (big) launch_dma<64, 64, 2, 2, AT, BT, EPI>(p, splits, stream);
+    else launch_dma<32, 64, 2, 2, AT, BT, EPI>(p, splits, stream);
+  }
+};
+template <bool BT, int EPI>
+struct DmaSmall<true, BT, EPI> {
+  static void launch(GemmParams p, int splits, hipStream_t stream, bool) {
+    launch_dma<64, 64, 2, 2, true, BT, EPI>(p, splits, stream);
+  }
+};
+
+// tile choice: 64x64 when it yields >= ~1 wave of workgroups per CU, else 32x64.
+// The LDS-DMA ring kernel needs K % 64 == 0 for k-contiguous operands (transposed
+// operands get zero rows past K from the buffer bounds check).
 template <bool AT, bool BT, int EPI>
 static void launch_auto(GemmParams p, int splits, hipStream_t stream) {
   const int tiles64 = ((p.M + 63) / 64) * ((p.N + 63) / 64);
-  if (tiles64 * splits >= 240) launch_cfg<64, 64, 2, 2, AT, BT, EPI>(p, splits, stream);
+  const bool big = tiles64 * splits >= 240 || AT;
+  const bool dma_ok = (AT || BT || p.K % 64 == 0) && (AT || p.K % 64 == 0) && !dma_disabled();
+  if (dma_ok) {
+    DmaSmall<AT, BT, EPI>::launch(p, splits, stream, big);
+    return;
+  }
+  if (big) launch_cfg<64, 64, 2, 2, AT, BT, EPI>(p, splits, stream);
   else launch_cfg<32, 64, 2, 2, AT, BT, EPI>(p, splits, stream);
 }
+
+// Explicit instantiations: hipcc 7.2 intermittently fails to emit host launch
+// stubs for implicitly instantiated kernel templates (undefined
+// __device_stub__ at dlopen); build.py also checks the .so for that.
+#define DC_INST_DMA(BM, AT, BT, EPI) template __global__ void gemm_dma_kernel<BM, 64, 2, 2, AT, BT, EPI, 4>(GemmParams);
+#define DC_INST_DMA2(AT, BT, EPI) DC_INST_DMA(64, AT, BT, EPI) DC_INST_DMA(32, AT, BT, EPI)
+DC_INST_DMA2(false, false, EPI_BF16)
+DC_INST_DMA2(false, false, EPI_F32)
+DC_INST_DMA2(false, false, EPI_QKV)
+DC_INST_DMA2(false, false, EPI_RESID)
+DC_INST_DMA2(false, false, EPI_GELU)
+DC_INST_DMA2(false, false, EPI_HEAD)
+DC_INST_DMA2(false, false, EPI_EMBED)
+DC_INST_DMA2(false, true, EPI_BF16)
+DC_INST_DMA2(false, true, EPI_F32)
+DC_INST_DMA2(false, true, EPI_DGELU)
+DC_INST_DMA(64, true, true, EPI_ATOMIC)
 
 }  // namespace dc
 

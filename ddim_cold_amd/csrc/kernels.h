@@ -47,10 +47,14 @@ void gemm_wgrad(const GemmArgs& a, int splits, hipStream_t stream);
 // LayerNorm (layernorm.hip)
 void layernorm_fwd_launch(const float* x, const float* gamma, const float* beta, void* y_bf16, float* mean,
                           float* rstd, int M, int D, float eps, hipStream_t stream);
+// dgamma||dbeta partials go into ws [ln_replicas()][2D] (must be zero on entry);
+// replica_reduce_launch adds them into the destinations and re-zeroes ws.
 void layernorm_bwd_launch(const float* dy, const float* x, const float* mean, const float* rstd,
-                          const float* gamma, const float* g_res, float* g_out, void* gy_bf16, float* dgamma,
-                          float* dbeta, int M, int D, int tokens, const int64_t* rng, int site_drop,
-                          double p_drop, int site_dp, double p_dp, hipStream_t stream);
+                          const float* gamma, const float* g_res, float* g_out, void* gy_bf16, float* dgb_ws, int M,
+                          int D, int tokens, const int64_t* rng, int site_drop, double p_drop, int site_dp,
+                          double p_dp, hipStream_t stream);
+int ln_replicas();
+void replica_reduce_launch(float* ws, float* const* dsts_dev, int G, int C, hipStream_t stream);
 
 // Attention (attention.hip)
 void attn_fwd_launch(const void* qkv, void* o, float* lse, int B, int H, int N, int hd, float scale,
@@ -65,13 +69,17 @@ void patchify_cls_launch(const float* img, const int64_t* t, const float* cls, c
                          int D, const int64_t* rng, int site, double p, hipStream_t stream);
 void embed_bwd_launch(const float* g, const int64_t* t, float* dcls, float* dpos, float* dtemb, void* gpatch,
                       int B, int N, int D, const int64_t* rng, int site, double p, hipStream_t stream);
-void smooth_l1_launch(const float* pred, const float* target, float* loss, void* dtok, int B, int C, int H,
-                      int W, int patch, float beta, hipStream_t stream);
+void smooth_l1_launch(const float* pred, const float* target, float* loss, float* partials, void* dtok, int B,
+                      int C, int H, int W, int patch, float beta, hipStream_t stream);
+constexpr int L1_PARTS = 512;
 void img_to_tokgrad_launch(const float* dimg, void* dtok, int B, int C, int H, int W, int patch,
                            hipStream_t stream);
 
 // Optimizer (optim.hip)
-void sqnorm_launch(const float* g, int64_t n, float* out, float scale, hipStream_t stream);
+// sqnorm writes SQ_PARTS per-block partial sums of (g*scale)^2 (no atomics);
+// adamw / advance sum the partials themselves.
+constexpr int SQ_PARTS = 1024;
+void sqnorm_launch(const float* g, int64_t n, float* partials, float scale, hipStream_t stream);
 void adamw_launch(float* p, float* g, float* m, float* v, void* p_bf16, int64_t n, const float* sqnorm,
                   const int64_t* step, const float* hyper, float grad_scale, hipStream_t stream);
 void advance_counters_launch(int64_t* step, int64_t* rng, const float* sqnorm, hipStream_t stream);

@@ -15,6 +15,8 @@
 
 namespace dc {
 
+constexpr int LN_REPLICAS = 16;
+
 template <int VEC>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, bf16* __restrict__ y,
@@ -43,10 +45,16 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
   const float2* g2 = reinterpret_cast<const float2*>(gamma);
   const float2* b2 = reinterpret_cast<const float2*>(beta);
   bf16x2* yr = reinterpret_cast<bf16x2*>(y + (size_t)row * D);
+  float2 gv[VEC], bv[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    gv[i] = g2[lane + 64 * i];
+    bv[i] = b2[lane + 64 * i];
+  }
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
     const int c = lane + 64 * i;
-    const float2 gg = g2[c], bb = b2[c];
+    const float2 gg = gv[i], bb = bv[i];
     bf16x2 o;
     o[0] = f2bf((v[i].x - mu) * rs * gg.x + bb.x);
     o[1] = f2bf((v[i].y - mu) * rs * gg.y + bb.y);
@@ -63,7 +71,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const float* __restrict__ gamma, const float* __restrict__ g_res,
                                                      float* __restrict__ g_out, bf16* __restrict__ gy,
-                                                     float* __restrict__ dgamma, float* __restrict__ dbeta, int M,
+                                                     float* __restrict__ dgb_ws, int M,
                                                      int tokens, const int64_t* __restrict__ rng, int site_drop,
                                                      uint32_t thr_drop, float sc_drop, int site_dp, uint32_t thr_dp,
                                                      float sc_dp) {
@@ -83,22 +91,43 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
     if (thr_drop) salt_drop = site_salt(rng, site_drop);
     if (thr_dp) salt_dp = site_salt(rng, site_dp);
   }
-  for (int row = blockIdx.x * 4 + wave; row < M; row += gridDim.x * 4) {
+  // 2 rows per wave, both rows' loads issued before any use (latency-bound op)
+  constexpr int RPW = 2;
+  float2 xv[RPW][VEC], dv[RPW][VEC], rv[RPW][VEC];
+  float muv[RPW], rsv[RPW];
+  int rows[RPW];
+#pragma unroll
+  for (int j = 0; j < RPW; ++j) {
+    rows[j] = (blockIdx.x * 4 + wave) * RPW + j;
+    const int row = rows[j] < M ? rows[j] : M - 1;
     const float2* xr = reinterpret_cast<const float2*>(x + (size_t)row * D);
     const float2* dr = reinterpret_cast<const float2*>(dy + (size_t)row * D);
-    const float mu = mean[row], rs = rstd[row];
+    const float2* gr = reinterpret_cast<const float2*>(g_res + (size_t)row * D);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      xv[j][i] = xr[lane + 64 * i];
+      dv[j][i] = dr[lane + 64 * i];
+      rv[j][i] = g_res ? gr[lane + 64 * i] : make_float2(0.f, 0.f);
+    }
+    muv[j] = mean[row];
+    rsv[j] = rstd[row];
+  }
+#pragma unroll
+  for (int j = 0; j < RPW; ++j) {
+    const int row = rows[j];
+    if (row >= M) continue;
+    const float mu = muv[j], rs = rsv[j];
     float2 xh[VEC], dxh[VEC];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
-      const int c = lane + 64 * i;
-      const float2 xv = xr[c], dv = dr[c];
-      xh[i] = make_float2((xv.x - mu) * rs, (xv.y - mu) * rs);
-      dgam[i].x += dv.x * xh[i].x;
-      dgam[i].y += dv.y * xh[i].y;
-      dbet[i].x += dv.x;
-      dbet[i].y += dv.y;
-      dxh[i] = make_float2(dv.x * gm[i].x, dv.y * gm[i].y);
+      const float2 dvv = dv[j][i];
+      xh[i] = make_float2((xv[j][i].x - mu) * rs, (xv[j][i].y - mu) * rs);
+      dgam[i].x += dvv.x * xh[i].x;
+      dgam[i].y += dvv.y * xh[i].y;
+      dbet[i].x += dvv.x;
+      dbet[i].y += dvv.y;
+      dxh[i] = make_float2(dvv.x * gm[i].x, dvv.y * gm[i].y);
       s1 += dxh[i].x + dxh[i].y;
       s2 += dxh[i].x * xh[i].x + dxh[i].y * xh[i].y;
     }
@@ -109,12 +138,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
       const int c = lane + 64 * i;
-      float2 o = make_float2((dxh[i].x - c1 - xh[i].x * c2) * rs, (dxh[i].y - c1 - xh[i].y * c2) * rs);
-      if (g_res) {
-        const float2 r = reinterpret_cast<const float2*>(g_res + (size_t)row * D)[c];
-        o.x += r.x;
-        o.y += r.y;
-      }
+      float2 o = make_float2((dxh[i].x - c1 - xh[i].x * c2) * rs + rv[j][i].x,
+                             (dxh[i].y - c1 - xh[i].y * c2) * rs + rv[j][i].y);
       reinterpret_cast<float2*>(g_out + (size_t)row * D)[c] = o;
       if (gy) {
         float a = o.x * dpsc, b = o.y * dpsc;
@@ -140,11 +165,32 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
     red[wave][D + c + 1] = dbet[i].y;
   }
   __syncthreads();
+  // dgamma||dbeta replicas: ws[R][2D], workgroup b adds into replica b % R (spreads the
+  // same-address atomic contention of ~M/8 workgroups over R replicas)
+  float* rep = dgb_ws + (size_t)(blockIdx.x % LN_REPLICAS) * 2 * D;
   for (int c = threadIdx.x; c < 2 * D; c += 256) {
     const float s = red[0][c] + red[1][c] + red[2][c] + red[3][c];
-    if (c < D) atomicAdd(dgamma + c, s);
-    else atomicAdd(dbeta + (c - D), s);
+    atomicAdd(rep + c, s);
   }
+}
+
+// dst[g][c] += sum_r ws[g][r][c]; ws zeroed.  One launch finalises many LayerNorms.
+__global__ __launch_bounds__(256) void replica_reduce_kernel(float* __restrict__ ws, float* const* __restrict__ dsts,
+                                                             int C) {
+  const int gi = blockIdx.y;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float* w = ws + (size_t)gi * LN_REPLICAS * C + c;
+  float v[LN_REPLICAS];
+#pragma unroll
+  for (int r = 0; r < LN_REPLICAS; ++r) v[r] = w[(size_t)r * C];
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < LN_REPLICAS; ++r) {
+    s += v[r];
+    w[(size_t)r * C] = 0.f;
+  }
+  dsts[gi][c] += s;
 }
 
 }  // namespace dc
@@ -171,16 +217,21 @@ void layernorm_fwd_launch(const float* x, const float* gamma, const float* beta,
 }
 
 void layernorm_bwd_launch(const float* dy, const float* x, const float* mean, const float* rstd,
-                          const float* gamma, const float* g_res, float* g_out, void* gy_bf16, float* dgamma,
-                          float* dbeta, int M, int D, int tokens, const int64_t* rng, int site_drop,
-                          double p_drop, int site_dp, double p_dp, hipStream_t stream) {
+                          const float* gamma, const float* g_res, float* g_out, void* gy_bf16, float* dgb_ws, int M,
+                          int D, int tokens, const int64_t* rng, int site_drop, double p_drop, int site_dp,
+                          double p_dp, hipStream_t stream) {
   if (D % 128) throw std::runtime_error("layernorm: D % 128 != 0");
-  int grid = (M + 15) / 16;  // ~4 rows per wave
-  if (grid < 1) grid = 1;
+  const int grid = (M + 7) / 8;  // 4 waves x 2 rows
   const uint32_t td = drop_threshold_host(p_drop), tp = drop_threshold_host(p_dp);
   const float sd = p_drop > 0 ? 1.f / (1.f - (float)p_drop) : 1.f;
   const float sp = p_dp > 0 ? 1.f / (1.f - (float)p_dp) : 1.f;
   LN_DISPATCH(D, hipLaunchKernelGGL(ln_bwd_kernel<VEC>, dim3(grid), dim3(256), 0, stream, dy, x, mean, rstd,
-                                    gamma, g_res, g_out, reinterpret_cast<bf16*>(gy_bf16), dgamma, dbeta, M,
+                                    gamma, g_res, g_out, reinterpret_cast<bf16*>(gy_bf16), dgb_ws, M,
                                     tokens, rng, site_drop, td, sd, site_dp, tp, sp));
+}
+
+int ln_replicas() { return LN_REPLICAS; }
+
+void replica_reduce_launch(float* ws, float* const* dsts_dev, int G, int C, hipStream_t stream) {
+  hipLaunchKernelGGL(replica_reduce_kernel, dim3((C + 255) / 256, G), dim3(256), 0, stream, ws, dsts_dev, C);
 }

@@ -3,7 +3,8 @@
 // iteration + zero_grad), graph-capturable: every scalar that changes per step
 // (Adam step, scheduler step, RNG step) lives in device memory.
 //
-//   sqnorm  : sum((g*scale)^2) over the whole grad arena -> one fp32 (atomics per block)
+//   sqnorm  : sum((g*scale)^2) over the grad arena -> SQ_PARTS per-block partials (no
+//             same-address atomics; every consumer block sums the 4 KiB of partials)
 //   adamw   : clip coef from the norm, cosine LR from the device step, bias
 //             corrections, decoupled weight decay, moment updates, fp32 master
 //             update, bf16 shadow-weight refresh (what the GEMMs read), and the
@@ -14,6 +15,19 @@
 #include "kernels.h"
 
 namespace dc {
+
+// sum of SQ_PARTS partials by one workgroup (every adamw block does this redundantly:
+// 4 KiB from L2, no atomics, no extra launch)
+__device__ __forceinline__ float sum_parts(const float* __restrict__ parts) {
+  __shared__ float red[4];
+  float v = 0.f;
+#pragma unroll
+  for (int i = 0; i < SQ_PARTS / 256; ++i) v += parts[threadIdx.x + 256 * i];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
 
 __global__ __launch_bounds__(256) void sqnorm_kernel(const float* __restrict__ g, int64_t n, float* out, float scale) {
   __shared__ float red[4];
@@ -29,7 +43,7 @@ __global__ __launch_bounds__(256) void sqnorm_kernel(const float* __restrict__ g
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(out, (red[0] + red[1] + red[2] + red[3]) * scale * scale);
+  if (threadIdx.x == 0) out[blockIdx.x] = (red[0] + red[1] + red[2] + red[3]) * scale * scale;
 }
 
 // hyper = {base_lr, beta1, beta2, eps, weight_decay, max_norm, T_max, eta_min}
@@ -38,7 +52,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, float
                                                     float* __restrict__ v, bf16* __restrict__ pb, int64_t n,
                                                     const float* __restrict__ sqnorm, const int64_t* __restrict__ step,
                                                     const float* __restrict__ hyper, float grad_scale) {
-  const float sq = *sqnorm;
+  const float sq = sum_parts(sqnorm);
   const bool skip = !isfinite(sq);
   const float base_lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
   const float max_norm = hyper[5], tmax = hyper[6], eta_min = hyper[7];
@@ -67,9 +81,10 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, float
   }
 }
 
-__global__ void advance_kernel(int64_t* step, int64_t* rng, const float* sqnorm) {
+__global__ __launch_bounds__(256) void advance_kernel(int64_t* step, int64_t* rng, const float* sqnorm) {
+  const float sq = sqnorm ? sum_parts(sqnorm) : 0.f;
   if (threadIdx.x == 0 && blockIdx.x == 0) {
-    if (sqnorm == nullptr || isfinite(*sqnorm)) step[0] += 1;
+    if (sqnorm == nullptr || isfinite(sq)) step[0] += 1;
     step[1] += 1;
     rng[1] += 1;
   }
@@ -87,7 +102,7 @@ static int opt_grid(int64_t n) {
 }
 
 void sqnorm_launch(const float* g, int64_t n, float* out, float scale, hipStream_t stream) {
-  hipLaunchKernelGGL(sqnorm_kernel, dim3(opt_grid(n / 4 + 1)), dim3(256), 0, stream, g, n, out, scale);
+  hipLaunchKernelGGL(sqnorm_kernel, dim3(SQ_PARTS), dim3(256), 0, stream, g, n, out, scale);
 }
 
 void adamw_launch(float* p, float* g, float* m, float* v, void* p_bf16, int64_t n, const float* sqnorm,
@@ -97,5 +112,5 @@ void adamw_launch(float* p, float* g, float* m, float* v, void* p_bf16, int64_t 
 }
 
 void advance_counters_launch(int64_t* step, int64_t* rng, const float* sqnorm, hipStream_t stream) {
-  hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(64), 0, stream, step, rng, sqnorm);
+  hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(256), 0, stream, step, rng, sqnorm);
 }

@@ -191,13 +191,19 @@ class ViTProgram:
 
     # ------------------------------------------------------------------ backward
     def backward_iter(self, P: ModelTensors, G: ModelTensors, S: Saved, dtok: torch.Tensor, rng: torch.Tensor,
-                      training: bool = True, wgrad: Callable = immediate_wgrad) -> Iterator[int]:
+                      training: bool = True, wgrad: Callable = immediate_wgrad,
+                      ln_ws: Optional[torch.Tensor] = None) -> Iterator[int]:
         """Hand-written backward; yields the block index after each block's grads
         are issued (L-1 first, then ..., 0) and -1 after the embedding grads.
 
         ``G`` tensors are fp32 accumulators (``+=``).  ``wgrad`` lets the engine
-        route weight-gradient GEMMs to a side stream.
+        route weight-gradient GEMMs to a side stream.  ``ln_ws`` ([2L+1, R, 2D],
+        zero) collects LayerNorm dgamma/dbeta replicas in backward order (final
+        norm, then norm2/norm1 of blocks L-1..0); the caller finalises them
+        with ``ops.replica_reduce_``.
         """
+        def ws(k):
+            return None if ln_ws is None else ln_ws[k]
         c = self.cfg
         N, D = c.tokens, c.dim
         pd = c.drop if training else 0.0
@@ -208,7 +214,7 @@ class ViTProgram:
         wgrad(dtok, S.lf, G.head_w, G.head_b)
         _, _, _, _, sf2, sd2 = block_sites(L - 1)
         g, gy = ops.layernorm_bwd(dlf, S.xL, S.mf, S.rf, P.nw, None, G.nw, G.nb, N, rng, sf2, pd, sd2,
-                                  dpr[L - 1], True)
+                                  dpr[L - 1], True, ws(0))
         keep = []
         for i in range(L - 1, -1, -1):
             x0, l1, m1, r1, qkv, o, lse, x1, l2, m2, r2, u, h = S.blocks[i]
@@ -218,8 +224,9 @@ class ViTProgram:
             du = ops.linear_dgrad_gelu(gy, bp.fc2_w, u, rng, sf1, pd)
             wgrad(du, l2, bg.fc1_w, bg.fc1_b)
             dl2 = ops.linear_dgrad(du, bp.fc1_w, True)
+            k2 = 1 + 2 * (L - 1 - i)
             g1, gy1 = ops.layernorm_bwd(dl2, x1, m2, r2, bp.n2w, g, bg.n2w, bg.n2b, N, rng, sp, pd, sd1, dpr[i],
-                                        True)
+                                        True, ws(k2))
             wgrad(gy1, o, bg.proj_w, bg.proj_b)
             do = ops.linear_dgrad(gy1, bp.proj_w, False)
             dqkv = ops.attn_bwd(do, qkv, o, lse, c.scale, rng, sa, ad)
@@ -228,10 +235,10 @@ class ViTProgram:
             if i > 0:
                 _, _, _, _, psf2, psd2 = block_sites(i - 1)
                 g, gy = ops.layernorm_bwd(dl1, x0, m1, r1, bp.n1w, g1, bg.n1w, bg.n1b, N, rng, psf2, pd, psd2,
-                                          dpr[i - 1], True)
+                                          dpr[i - 1], True, ws(k2 + 1))
             else:
                 g, gy = ops.layernorm_bwd(dl1, x0, m1, r1, bp.n1w, g1, bg.n1w, bg.n1b, N, rng, 0, 0.0, 0, 0.0,
-                                          False)
+                                          False, ws(k2 + 1))
             keep.append((gy1, du, dqkv))
             yield i
         B = S.t.shape[0]

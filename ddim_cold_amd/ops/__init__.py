@@ -111,14 +111,37 @@ def linear_wgrad(dy, x, dw, db: Optional[torch.Tensor]):
     return ref.linear_wgrad(dy, x, dw, db)
 
 
+LN_REPLICAS = 16  # csrc/layernorm.hip LN_REPLICAS
+
+
 def layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dgamma, dbeta, N: int, rng, site_drop: int, p_drop: float,
-                  site_dp: int, p_dp: float, emit_gy: bool):
+                  site_dp: int, p_dp: float, emit_gy: bool, ws: Optional[torch.Tensor] = None):
+    """LayerNorm backward.  With ``ws`` ([LN_REPLICAS, 2D], zero on entry) the
+    dgamma||dbeta partials stay in the replica workspace (finalise later with
+    :func:`replica_reduce_`); otherwise they are added into dgamma / dbeta."""
     if _hip(x):
         g_out, gy = _ops().layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dgamma, dbeta, N, rng, site_drop,
-                                         float(p_drop), site_dp, float(p_dp), bool(emit_gy))
+                                         float(p_drop), site_dp, float(p_dp), bool(emit_gy), ws)
         return g_out, (gy if emit_gy else None)
+    if ws is not None:
+        D = x.shape[-1]
+        dg, db = ws[0, :D], ws[0, D:]
+        return ref.layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dg, db, N, rng, site_drop, p_drop,
+                                 site_dp, p_dp, emit_gy)
     return ref.layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dgamma, dbeta, N, rng, site_drop, p_drop,
                              site_dp, p_dp, emit_gy)
+
+
+def replica_reduce_(ws, dst_ptrs, C: int, dsts=None):
+    """dst[g] += ws[g].sum(0) for G LayerNorm replica workspaces; ws re-zeroed.
+
+    ``dst_ptrs`` is a device int64 tensor of destination addresses (GPU); the
+    CPU path takes the destination tensors in ``dsts`` instead."""
+    if _hip(ws):
+        return _ops().replica_reduce_(ws, dst_ptrs, C)
+    for g, d in enumerate(dsts):
+        d.add_(ws[g].sum(0))
+    ws.zero_()
 
 
 def attn_bwd(do, qkv, o, lse, scale: float, rng, site: int, p: float):
@@ -134,10 +157,15 @@ def embed_bwd(g, t, rng, site: int, p: float, dcls, dpos, dtemb):
 
 
 # ----------------------------------------------------------------------------- optimizer
+SQ_PARTS = 1024  # csrc/kernels.h
+
+
 def sqnorm(g, out, scale: float = 1.0):
+    """Per-block partial sums of (g*scale)^2 into ``out`` (>= SQ_PARTS floats, fully overwritten)."""
     if _hip(g):
         return _ops().sqnorm(g, out, float(scale))
-    out.add_((g.float() * scale).pow(2).sum().reshape(out.shape))
+    out.zero_()
+    out[0] = (g.float() * scale).pow(2).sum()
 
 
 def adamw_step(p, g, m, v, pbf, sq, step, hyper, grad_scale: float = 1.0):
@@ -145,7 +173,7 @@ def adamw_step(p, g, m, v, pbf, sq, step, hyper, grad_scale: float = 1.0):
     if _hip(p):
         return _ops().adamw_step(p, g, m, v, pbf, sq, step, hyper, float(grad_scale))
     import math
-    sqv = float(sq.reshape(-1)[0])
+    sqv = float(sq.sum())
     base_lr, b1, b2, eps, wd, max_norm, tmax, eta_min = (float(x) for x in hyper.tolist()[:8])
     coef = grad_scale
     if max_norm > 0:
@@ -171,7 +199,7 @@ def advance_counters(step, rng, sq=None):
     if _hip(step):
         return _ops().advance_counters(step, rng, sq)
     import math
-    if sq is None or math.isfinite(float(sq.reshape(-1)[0])):
+    if sq is None or math.isfinite(float(sq.sum())):
         step[0] += 1
     step[1] += 1
     rng[1] += 1

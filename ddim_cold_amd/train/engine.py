@@ -53,7 +53,7 @@ class EngineConfig:
     use_graph: bool = True
     graph_warmup: int = 3     # eager steps before capture
     bucket_blocks: int = 2    # transformer blocks per all-reduce bucket
-    wgrad_stream: bool = True
+    wgrad_stream: bool = False  # measured: side-stream wgrad overlap is slower on MI355X (1.79 vs 1.53 ms)
     seed: int = 42
     loss_beta: float = 1.0
     ema_decay: float = 0.99
@@ -85,7 +85,7 @@ class TrainEngine:
         b1, b2 = cfg.betas
         self.hyper = torch.tensor([cfg.lr, b1, b2, cfg.eps, cfg.weight_decay, cfg.max_grad_norm,
                                    float(cfg.t_max), cfg.eta_min], dtype=torch.float32, device=dev)
-        self.sqnorm = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.sqnorm = torch.zeros(ops.SQ_PARTS, dtype=torch.float32, device=dev)  # per-block partials
         self.loss_last = torch.zeros(1, dtype=torch.float32, device=dev)
         self.loss_ema = torch.full((1,), cfg.ema_init, dtype=torch.float32, device=dev)
         self.side = torch.cuda.Stream(device=dev) if (self.is_cuda and cfg.wgrad_stream) else None
@@ -151,6 +151,32 @@ class TrainEngine:
         bounds.append((0, end))
         self.bucket_after[-1] = j
         self.buckets = bounds
+        # LayerNorm dgamma/dbeta replica workspace in backward order: final norm,
+        # then norm2, norm1 of blocks L-1 .. 0; destinations = grad-arena views
+        # (weight and bias of one LayerNorm are adjacent: one [2D] range).
+        D = c.dim
+        order = ["norm"]
+        for i in range(L - 1, -1, -1):
+            order += [f"blocks.{i}.norm2", f"blocks.{i}.norm1"]
+        self.ln_order = order
+        dsts = []
+        for nm in order:
+            ow, _ = self.offsets[nm + ".weight"]
+            ob, _ = self.offsets[nm + ".bias"]
+            assert ob == ow + D, "LayerNorm weight/bias must be adjacent in the arena"
+            dsts.append(self.flat_g[ow:ow + 2 * D])
+        self.ln_dsts = dsts
+        self.ln_ws = torch.zeros(len(order), ops.LN_REPLICAS, 2 * D, dtype=torch.float32, device=dev)
+        self.ln_ptrs = torch.tensor([t.data_ptr() for t in dsts], dtype=torch.int64, device=dev) \
+            if dev.type == "cuda" else None
+        # LN index range finalised at each bucket boundary (backward order)
+        self.ln_done_at = {}
+        done = 1
+        for i in range(L - 1, -1, -1):
+            done += 2
+            if i in self.bucket_after:
+                self.ln_done_at[i] = done
+        self.ln_done_at[-1] = len(order)
 
     def _refresh_shadow(self):
         self.flat_pb.copy_(self.flat_p.to(torch.bfloat16))
@@ -182,16 +208,21 @@ class TrainEngine:
         self.loss_last.copy_(loss)
         self.loss_ema.mul_(self.cfg.ema_decay).add_(loss, alpha=1.0 - self.cfg.ema_decay)
         del out
+        ln_lo = 0
         for i in self.prog.backward_iter(self.param_tensors, self.grad_tensors, S, dtok, self.rng, True,
-                                         wgrad=self._wgrad):
-            if i in self.bucket_after:
+                                         wgrad=self._wgrad, ln_ws=self.ln_ws):
+            if i in self.bucket_after and (self.segmented or i == -1):
+                hi = self.ln_done_at[i]
+                if hi > ln_lo:
+                    ops.replica_reduce_(self.ln_ws[ln_lo:hi], None if self.ln_ptrs is None else self.ln_ptrs[ln_lo:hi],
+                                        2 * c.dim, dsts=self.ln_dsts[ln_lo:hi])
+                    ln_lo = hi
                 self._join_side()
                 yield ("bucket", self.bucket_after[i])
         S = None
         self.prog._keep = None
         # optimizer: grads are SUM-reduced over ranks -> average via grad_scale
         gs = 1.0 / self.world
-        self.sqnorm.zero_()
         ops.sqnorm(self.flat_g, self.sqnorm, gs)
         ops.adamw_step(self.flat_p, self.flat_g, self.flat_m, self.flat_v, self.flat_pb, self.sqnorm,
                        self.step_ctr, self.hyper, gs)

@@ -258,7 +258,7 @@ def test_fused_adamw_matches_torch():
     # fused
     p, g, m, v = p0.clone(), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
     pb = torch.empty(n, device=DEV, dtype=torch.bfloat16)
-    sq = torch.zeros(1, device=DEV)
+    sq = torch.zeros(ops.SQ_PARTS, device=DEV)
     step = torch.zeros(2, dtype=torch.int64, device=DEV)
     r = rng()
     hyper = torch.tensor([3e-3, 0.9, 0.999, 1e-8, 0.05, 1.0, 10.0, 0.0], device=DEV)
@@ -269,7 +269,6 @@ def test_fused_adamw_matches_torch():
         opt.step()
         sch.step()
         g.copy_(grad)
-        sq.zero_()
         ops.sqnorm(g, sq, 1.0)
         ops.adamw_step(p, g, m, v, pb, sq, step, hyper, 1.0)
         ops.advance_counters(step, r, sq)
