@@ -442,7 +442,7 @@ std::tuple<Tensor, Tensor> pixelate_pair(Tensor img, c10::optional<Tensor> idx, 
 }
 
 void cold_batch(Tensor pool, Tensor rng, int64_t site, Tensor x_t, Tensor x_tm1, Tensor t, Tensor idx_ws,
-                int64_t max_t) {
+                int64_t max_t, bool draw_idx) {
   CHECK_IN(pool, F32); check_rng(rng); CHECK_IN(x_t, F32); CHECK_IN(x_tm1, F32); CHECK_IN(t, I64);
   CHECK_IN(idx_ws, I64);
   const c10::DeviceGuard guard(pool.device());
@@ -452,7 +452,7 @@ void cold_batch(Tensor pool, Tensor rng, int64_t site, Tensor x_t, Tensor x_tm1,
   TORCH_CHECK(max_t >= 1 && (1 << max_t) <= W, "max_t");
   cold_batch_launch(pool.data_ptr<float>(), pool.size(0), rng.data_ptr<int64_t>(), site, x_t.data_ptr<float>(),
                     x_tm1.data_ptr<float>(), t.data_ptr<int64_t>(), idx_ws.data_ptr<int64_t>(), B, C, H, W, max_t,
-                    cur_stream());
+                    draw_idx, cur_stream());
 }
 
 }  // namespace
@@ -489,7 +489,7 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("q_sample(Tensor x0, Tensor t, Tensor eps, int total_steps) -> Tensor");
   m.def("pixelate_pair(Tensor img, Tensor? idx, Tensor t, int B) -> (Tensor, Tensor)");
   m.def("cold_batch(Tensor pool, Tensor rng, int site, Tensor(a!) x_t, Tensor(b!) x_tm1, Tensor(c!) t, "
-        "Tensor(d!) idx_ws, int max_t) -> ()");
+        "Tensor(d!) idx_ws, int max_t, bool draw_idx=True) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {

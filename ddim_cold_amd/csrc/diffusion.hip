@@ -90,10 +90,10 @@ __global__ __launch_bounds__(256) void pixelate_pair_kernel(const float* __restr
 }
 
 __global__ void cold_draw_kernel(const int64_t* __restrict__ rng, int site, int pool_n, int max_t, int B,
-                                 int64_t* __restrict__ idx, int64_t* __restrict__ t) {
+                                 int64_t* __restrict__ idx, int64_t* __restrict__ t, int draw_idx) {
   const uint32_t salt = site_salt(rng, site);
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
-    idx[b] = mix32(((uint32_t)(2 * b) * 0x9E3779B1u) ^ salt) % (uint32_t)pool_n;
+    if (draw_idx) idx[b] = mix32(((uint32_t)(2 * b) * 0x9E3779B1u) ^ salt) % (uint32_t)pool_n;
     t[b] = 1 + mix32(((uint32_t)(2 * b + 1) * 0x9E3779B1u) ^ salt) % (uint32_t)max_t;
   }
 }
@@ -131,7 +131,9 @@ void pixelate_pair_launch(const float* img, const int64_t* idx, const int64_t* t
 }
 
 void cold_batch_launch(const float* pool, int pool_n, const int64_t* rng, int site, float* x_t, float* x_tm1,
-                       int64_t* t, int64_t* idx_ws, int B, int C, int H, int W, int max_t, hipStream_t stream) {
-  hipLaunchKernelGGL(cold_draw_kernel, dim3(1), dim3(256), 0, stream, rng, site, pool_n, max_t, B, idx_ws, t);
+                       int64_t* t, int64_t* idx_ws, int B, int C, int H, int W, int max_t, bool draw_idx,
+                       hipStream_t stream) {
+  hipLaunchKernelGGL(cold_draw_kernel, dim3(1), dim3(256), 0, stream, rng, site, pool_n, max_t, B, idx_ws, t,
+                     draw_idx ? 1 : 0);
   pixelate_pair_launch(pool, idx_ws, t, x_t, x_tm1, B, C, H, W, stream);
 }

@@ -134,69 +134,91 @@ __device__ __forceinline__ bf16x8 frag_k_perm(const char* lds, int r, int s, int
 // issued for the whole fragment tile, (2) compute + store.  Interleaving them
 // per element serialises the tile on memory latency (the loads may alias the
 // stores through GemmParams, so the compiler cannot hoist them).
+// The epilogue is "load everything, then compute + store": interleaving per-element
+// loads (bias / residual / saved pre-activation / embeddings, which may alias the
+// stores through GemmParams) with stores serialises the tile on memory latency.
+// Every output index is separable, idx = rowoff(m) + coloff(n), so the integer
+// divisions (token -> sample, column -> head / pixel) are done once per row and
+// once per column of the lane's fragment, not per element.
+struct RowInfo {
+  long long off;  // row part of the destination index (-1: skip row)
+  int b;          // sample index (drop-path) / helper
+};
+
 template <int EPI>
-__device__ __forceinline__ bool epi_needs_elem() {
-  return EPI == EPI_RESID || EPI == EPI_DGELU || EPI == EPI_EMBED;
-}
-template <int EPI>
-__device__ __forceinline__ float epi_load_elem(const GemmParams& p, int m, int n) {
-  if (EPI == EPI_RESID) return p.res[(size_t)m * p.N + n];
-  if (EPI == EPI_DGELU) return bf2f(p.aux[(size_t)m * p.N + n]);
-  if (EPI == EPI_EMBED) {
+__device__ __forceinline__ RowInfo epi_row(const GemmParams& p, int m) {
+  RowInfo ri;
+  ri.b = 0;
+  if (EPI == EPI_QKV) {
+    const int b = m / p.tokens, tok = m - b * p.tokens;
+    ri.off = ((long long)b * p.heads * p.tokens + tok) * p.hd;
+  } else if (EPI == EPI_RESID) {
+    ri.off = (long long)m * p.N;
+    ri.b = m / p.tokens;
+  } else if (EPI == EPI_GELU || EPI == EPI_DGELU) {
+    ri.off = (long long)m * p.N;
+  } else if (EPI == EPI_HEAD) {
+    const int b = m / p.tokens, tok = m - b * p.tokens;
+    if (tok == 0) {
+      ri.off = -1;
+    } else {
+      const int P = p.patch, Wp = p.img_w / P;
+      const int patch = tok - 1, hp = patch / Wp, wp = patch - hp * Wp;
+      ri.off = (long long)b * p.chans * p.img_h * p.img_w + (long long)hp * P * p.img_w + wp * P;
+    }
+  } else if (EPI == EPI_EMBED) {
     const int Pn = p.tokens;
     const int b = m / Pn, patch = m - b * Pn;
-    return p.pos[(size_t)(patch + 1) * p.emb_dim + n] + p.temb[(size_t)p.tsteps[b] * p.emb_dim + n];
+    ri.off = ((long long)b * (Pn + 1) + patch + 1) * p.emb_dim;
+    ri.b = b;
+  } else {
+    ri.off = (long long)m * p.ldc;
   }
-  return 0.f;
+  return ri;
 }
 
 template <int EPI>
-__device__ __forceinline__ void epilogue(const GemmParams& p, int m, int n, float v, float bias, float pre,
-                                         uint32_t salt_drop, uint32_t salt_dp) {
-  v += bias;
-  if (EPI == EPI_BF16) {
-    reinterpret_cast<bf16*>(p.C)[(size_t)m * p.ldc + n] = f2bf(v);
-  } else if (EPI == EPI_F32) {
-    reinterpret_cast<float*>(p.C)[(size_t)m * p.ldc + n] = v;
-  } else if (EPI == EPI_ATOMIC) {
-    atomicAdd(reinterpret_cast<float*>(p.C) + (size_t)m * p.ldc + n, v);
-  } else if (EPI == EPI_QKV) {
+__device__ __forceinline__ long long epi_col(const GemmParams& p, int n) {
+  if (EPI == EPI_QKV) {
     const int D = p.heads * p.hd;
     const int s = n / D, rem = n - s * D;
     const int h = rem / p.hd, d = rem - h * p.hd;
-    const int b = m / p.tokens, tok = m - b * p.tokens;
-    const size_t idx = ((((size_t)s * p.batch + b) * p.heads + h) * p.tokens + tok) * p.hd + d;
+    return (long long)s * p.batch * p.heads * p.tokens * p.hd + (long long)h * p.tokens * p.hd + d;
+  }
+  if (EPI == EPI_HEAD) {
+    const int P = p.patch;
+    const int c = n % p.chans, ab = n / p.chans, a = ab / P, bb = ab - a * P;
+    return (long long)c * p.img_h * p.img_w + (long long)a * p.img_w + bb;
+  }
+  return n;
+}
+
+template <int EPI>
+__device__ __forceinline__ void epilogue(const GemmParams& p, long long idx, int rb, float v, float pre,
+                                         uint32_t salt_drop, uint32_t salt_dp) {
+  if (EPI == EPI_BF16) {
+    reinterpret_cast<bf16*>(p.C)[idx] = f2bf(v);
+  } else if (EPI == EPI_F32) {
+    reinterpret_cast<float*>(p.C)[idx] = v;
+  } else if (EPI == EPI_ATOMIC) {
+    atomicAdd(reinterpret_cast<float*>(p.C) + idx, v);
+  } else if (EPI == EPI_QKV) {
     reinterpret_cast<bf16*>(p.C)[idx] = f2bf(v);
   } else if (EPI == EPI_RESID) {
-    const size_t idx = (size_t)m * p.N + n;
     if (p.thr_drop) v = dropout_keep(salt_drop, (uint32_t)idx, p.thr_drop) ? v * p.scale_drop : 0.f;
-    if (p.thr_dp) {
-      const int b = m / p.tokens;
-      v = dropout_keep(salt_dp, (uint32_t)b, p.thr_dp) ? v * p.scale_dp : 0.f;
-    }
+    if (p.thr_dp) v = dropout_keep(salt_dp, (uint32_t)rb, p.thr_dp) ? v * p.scale_dp : 0.f;
     reinterpret_cast<float*>(p.C)[idx] = pre + v;
   } else if (EPI == EPI_GELU) {
-    const size_t idx = (size_t)m * p.N + n;
     reinterpret_cast<bf16*>(p.C)[idx] = f2bf(v);
     float h = gelu_f(v);
     if (p.thr_drop) h = dropout_keep(salt_drop, (uint32_t)idx, p.thr_drop) ? h * p.scale_drop : 0.f;
     reinterpret_cast<bf16*>(p.C2)[idx] = f2bf(h);
   } else if (EPI == EPI_DGELU) {
-    const size_t idx = (size_t)m * p.N + n;
     if (p.thr_drop) v = dropout_keep(salt_drop, (uint32_t)idx, p.thr_drop) ? v * p.scale_drop : 0.f;
     reinterpret_cast<bf16*>(p.C)[idx] = f2bf(v * gelu_grad_f(pre));
   } else if (EPI == EPI_HEAD) {
-    const int b = m / p.tokens, tok = m - b * p.tokens;
-    if (tok == 0) return;
-    const int P = p.patch;
-    const int Wp = p.img_w / P;
-    const int patch = tok - 1, hp = patch / Wp, wp = patch - hp * Wp;
-    const int c = n % p.chans, ab = n / p.chans, a = ab / P, bb = ab - a * P;
-    reinterpret_cast<float*>(p.C)[(((size_t)b * p.chans + c) * p.img_h + hp * P + a) * p.img_w + wp * P + bb] = v;
+    reinterpret_cast<float*>(p.C)[idx] = v;
   } else if (EPI == EPI_EMBED) {
-    const int Pn = p.tokens;
-    const int b = m / Pn, patch = m - b * Pn;
-    const size_t idx = ((size_t)b * (Pn + 1) + patch + 1) * p.emb_dim + n;
     v += pre;
     if (p.thr_drop) v = dropout_keep(salt_drop, (uint32_t)idx, p.thr_drop) ? v * p.scale_drop : 0.f;
     reinterpret_cast<float*>(p.C)[idx] = v;
@@ -207,13 +229,28 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int m, int n, floa
 template <int EPI, int FM, int FN>
 __device__ __forceinline__ void run_epilogue(const GemmParams& p, const f32x4 (&acc)[FM][FN], int mb, int nb,
                                              int g, int li) {
+  constexpr bool ELEM = EPI == EPI_RESID || EPI == EPI_DGELU || EPI == EPI_EMBED;
+  RowInfo rows[FM][4];
+  long long cols[FN];
+  bool colok[FN];
   float colb[FN];
   const bool has_bias = (EPI != EPI_ATOMIC) && p.bias != nullptr;
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int n = nb + j * 16 + li;
-    colb[j] = (has_bias && n < p.N) ? p.bias[n] : 0.f;
+    colok[j] = n < p.N;
+    cols[j] = epi_col<EPI>(p, n);
+    colb[j] = (has_bias && colok[j]) ? p.bias[n] : 0.f;
   }
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = mb + i * 16 + 4 * g + r;
+      rows[i][r] = epi_row<EPI>(p, m < p.M ? m : p.M - 1);
+      if (m >= p.M) rows[i][r].off = -1;
+    }
+  // phase 1: element loads
   float pre[FM][FN][4];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -221,9 +258,20 @@ __device__ __forceinline__ void run_epilogue(const GemmParams& p, const f32x4 (&
     for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = mb + i * 16 + 4 * g + r, n = nb + j * 16 + li;
-        pre[i][j][r] = (epi_needs_elem<EPI>() && m < p.M && n < p.N) ? epi_load_elem<EPI>(p, m, n) : 0.f;
+        float v = 0.f;
+        if (ELEM && rows[i][r].off >= 0 && colok[j]) {
+          const int n = nb + j * 16 + li;
+          if (EPI == EPI_RESID) v = p.res[rows[i][r].off + n];
+          if (EPI == EPI_DGELU) v = bf2f(p.aux[rows[i][r].off + n]);
+          if (EPI == EPI_EMBED) {
+            const int m = mb + i * 16 + 4 * g + r;
+            const int patch = m - rows[i][r].b * p.tokens;
+            v = p.pos[(size_t)(patch + 1) * p.emb_dim + n] + p.temb[(size_t)p.tsteps[rows[i][r].b] * p.emb_dim + n];
+          }
+        }
+        pre[i][j][r] = v;
       }
+  // phase 2: compute + store
   uint32_t salt_drop = 0, salt_dp = 0;
   if (p.thr_drop) salt_drop = site_salt(p.rng, p.site_drop);
   if (p.thr_dp) salt_dp = site_salt(p.rng, p.site_dp);
@@ -232,10 +280,10 @@ __device__ __forceinline__ void run_epilogue(const GemmParams& p, const f32x4 (&
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = mb + i * 16 + 4 * g + r, n = nb + j * 16 + li;
-        if (m < p.M && n < p.N) epilogue<EPI>(p, m, n, acc[i][j][r], colb[j], pre[i][j][r], salt_drop, salt_dp);
-      }
+      for (int r = 0; r < 4; ++r)
+        if (rows[i][r].off >= 0 && colok[j])
+          epilogue<EPI>(p, rows[i][r].off + cols[j], rows[i][r].b, acc[i][j][r] + colb[j], pre[i][j][r], salt_drop,
+                        salt_dp);
 }
 
 template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EPI>

@@ -93,4 +93,5 @@ void randn_launch(float* out, int64_t n, const int64_t* rng, int site, hipStream
 void q_sample_launch(const float* x0, const int64_t* t, const float* eps, float* out, int B, int64_t per,
                      int total_steps, hipStream_t stream);
 void cold_batch_launch(const float* pool, int pool_n, const int64_t* rng, int site, float* x_t, float* x_tm1,
-                       int64_t* t, int64_t* idx_ws, int B, int C, int H, int W, int max_t, hipStream_t stream);
+                       int64_t* t, int64_t* idx_ws, int B, int C, int H, int W, int max_t, bool draw_idx,
+                       hipStream_t stream);

@@ -42,11 +42,15 @@ def synthetic_pool(n: int, size=(64, 64), channels: int = 3, seed: int = 0, devi
 class ColdBatcher:
     """Device-side cold-diffusion batch source (graph-capturable).
 
-    Each call draws B pool indices and t ~ U{1..max_t} from the engine's RNG
-    state and writes (x_t, x_{t-1}, t) into static buffers.
+    Each call draws t ~ U{1..max_t} (and, unless ``idx`` is given, B pool
+    indices) from the engine's RNG state and writes (x_t, target, t) into static
+    buffers.  target = x_{t-1} (``ColdDownSampleDataset``) or x0 (``target='x0'``,
+    ``ColdDownSampleDataset_au``).  With ``idx`` (a static device int64[B] the host
+    fills each step from a shard table) the batch follows DistributedSampler order.
     """
 
-    def __init__(self, pool: torch.Tensor, batch: int, rng: torch.Tensor, max_t: int | None = None):
+    def __init__(self, pool: torch.Tensor, batch: int, rng: torch.Tensor, max_t: int | None = None,
+                 target: str = "prev", idx: torch.Tensor | None = None):
         self.pool = pool
         B, (C, H, W) = batch, pool.shape[1:]
         self.max_t = max_t or int(math.log2(W))
@@ -54,18 +58,24 @@ class ColdBatcher:
         self.x_t = torch.empty(B, C, H, W, device=dev)
         self.x_tm1 = torch.empty(B, C, H, W, device=dev)
         self.t = torch.empty(B, dtype=torch.int64, device=dev)
-        self.idx = torch.empty(B, dtype=torch.int64, device=dev)
+        self.draw = idx is None
+        self.idx = torch.empty(B, dtype=torch.int64, device=dev) if idx is None else idx
         self.rng = rng
+        self.target = target
 
     def __call__(self):
-        ops.cold_batch(self.pool, self.rng, SITE_DATA, self.x_t, self.x_tm1, self.t, self.idx, self.max_t)
+        ops.cold_batch(self.pool, self.rng, SITE_DATA, self.x_t, self.x_tm1, self.t, self.idx, self.max_t,
+                       self.draw)
+        if self.target == "x0":
+            torch.index_select(self.pool, 0, self.idx, out=self.x_tm1)
         return self.x_t, self.x_tm1, self.t
 
 
 class GaussianBatcher:
-    """Device-side Gaussian DDIM batch source: (q_sample(x0, t, eps), x0, t) with t ~ U{0..T-1}."""
+    """Device-side Gaussian DDIM batch source: (q_sample(x0, t, eps), x0, t), t ~ U{0..T-1}."""
 
-    def __init__(self, pool: torch.Tensor, batch: int, rng: torch.Tensor, total_steps: int = 2000):
+    def __init__(self, pool: torch.Tensor, batch: int, rng: torch.Tensor, total_steps: int = 2000,
+                 idx: torch.Tensor | None = None):
         self.pool = pool
         B, (C, H, W) = batch, pool.shape[1:]
         dev = pool.device
@@ -75,14 +85,30 @@ class GaussianBatcher:
         self.rng = rng
         self.u = torch.empty(2 * B, device=dev)
         self.B = B
+        self.idx = idx
 
     def __call__(self):
         ops.randn_(self.eps, self.rng, SITE_NOISE)
         ops.randn_(self.u, self.rng, SITE_DATA)
         # uniform indices / timesteps from the normal draws via the Gaussian CDF
         u = 0.5 * (1 + torch.erf(self.u / math.sqrt(2)))
-        idx = (u[: self.B] * self.pool.shape[0]).long().clamp_(0, self.pool.shape[0] - 1)
         t = (u[self.B:] * self.T).long().clamp_(0, self.T - 1)
+        if self.idx is None:
+            idx = (u[: self.B] * self.pool.shape[0]).long().clamp_(0, self.pool.shape[0] - 1)
+        else:
+            idx = self.idx
         torch.index_select(self.pool, 0, idx, out=self.x0)
         x_t = ops.q_sample(self.x0, t, self.eps, self.T)
         return x_t, self.x0, t
+
+
+def make_batcher(kind: str, pool: torch.Tensor, batch: int, rng: torch.Tensor, total_steps: int = 2000,
+                 idx: torch.Tensor | None = None):
+    """Batch source for a dataset kind: 'cold' | 'cold_x0' | 'gaussian' (config key ``dataset``)."""
+    if kind == "cold":
+        return ColdBatcher(pool, batch, rng, idx=idx)
+    if kind == "cold_x0":
+        return ColdBatcher(pool, batch, rng, target="x0", idx=idx)
+    if kind == "gaussian":
+        return GaussianBatcher(pool, batch, rng, total_steps, idx=idx)
+    raise ValueError(kind)

@@ -251,13 +251,16 @@ def pixelate_pair(img, idx, t, B: int):
     return xt, xtm1
 
 
-def cold_batch(pool, rng, site: int, x_t, x_tm1, t, idx_ws, max_t: int):
+def cold_batch(pool, rng, site: int, x_t, x_tm1, t, idx_ws, max_t: int, draw_idx: bool = True):
+    """Cold pixelation batch on device: t ~ U{1..max_t} (and pool indices unless
+    ``draw_idx`` is False, in which case ``idx_ws`` holds them), x_t / x_{t-1}."""
     if _hip(pool):
-        return _ops().cold_batch(pool, rng, site, x_t, x_tm1, t, idx_ws, max_t)
+        return _ops().cold_batch(pool, rng, site, x_t, x_tm1, t, idx_ws, max_t, bool(draw_idx))
     salt = ref.site_salt(rng, site)
     B = x_t.shape[0]
     b = torch.arange(B, dtype=torch.int64)
-    idx_ws.copy_(ref.mix32(ref._mul32((2 * b) & ref.MASK32, ref.GOLDEN) ^ salt) % pool.shape[0])
+    if draw_idx:
+        idx_ws.copy_(ref.mix32(ref._mul32((2 * b) & ref.MASK32, ref.GOLDEN) ^ salt) % pool.shape[0])
     t.copy_(1 + ref.mix32(ref._mul32((2 * b + 1) & ref.MASK32, ref.GOLDEN) ^ salt) % max_t)
     a, c = pixelate_pair(pool, idx_ws, t, B)
     x_t.copy_(a)
