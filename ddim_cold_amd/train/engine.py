@@ -105,10 +105,18 @@ class TrainEngine:
         named = list(self.model.named_parameters())
         self.names = [n for n, _ in named]
         self.offsets: Dict[str, Tuple[int, int]] = {}
+        # LayerNorm weight+bias are packed back to back (one [2D] range for the
+        # replica finalize); every other tensor starts 256-B aligned.
+        ln_prefixes = {n[: -len(".weight")] for n, p in named
+                       if n.endswith(".weight") and p.dim() == 1 and (n.startswith("norm") or ".norm" in n)}
         off = 0
         for n, p in named:
+            ln_bias = n.endswith(".bias") and n[: -len(".bias")] in ln_prefixes
+            if not ln_bias:
+                off = _align(off)
             self.offsets[n] = (off, p.numel())
-            off += _align(p.numel())
+            off += p.numel()
+        off = _align(off)
         self.numel = off
         dev = self.device
         self.flat_p = torch.zeros(off, dtype=torch.float32, device=dev)

@@ -1,0 +1,153 @@
+"""TrainEngine semantics on CPU: AdamW/clip/cosine vs torch.optim, optimizer-state formats,
+and data-parallel gradient parity over gloo (world size 2)."""
+import os
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from ddim_cold_amd.models import DiffusionVisionTransformer
+from ddim_cold_amd.models.program import collect, is_matrix_param
+from ddim_cold_amd.ops import reference as ref
+from ddim_cold_amd.parallel.dist import free_port
+from ddim_cold_amd.train.engine import EngineConfig, TrainEngine
+
+CFG = dict(img_size=[16, 16], patch_size=4, embed_dim=32, depth=3, num_heads=2)
+
+
+def _model(drop=True, seed=0):
+    torch.manual_seed(seed)
+    kw = dict(drop_rate=0.1, attn_drop_rate=0.1, drop_path_rate=0.2) if drop else dict(drop_rate=0.0, attn_drop_rate=0.0, drop_path_rate=0.0)
+    return DiffusionVisionTransformer(**CFG, **kw).train()
+
+
+def _batch(B, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(B, 3, 16, 16, generator=g)
+    y = torch.randn(B, 3, 16, 16, generator=g).clamp(-1, 1)
+    t = torch.randint(0, 2000, (B,), generator=g)
+    return x, y, t
+
+
+def _grads(model, x, y, t, rng):
+    """Gradients of one step computed directly with the program (bf16 shadow weights, like the engine)."""
+    from ddim_cold_amd.models.program import ViTProgram
+    prog = ViTProgram.from_model(model)
+    c = prog.cfg
+    views = {n: (p.detach().to(torch.bfloat16) if is_matrix_param(n) else p.detach())
+             for n, p in model.named_parameters()}
+    grads = {n: torch.zeros_like(p) for n, p in model.named_parameters()}
+    P = collect(views, c.depth, c.dim)
+    G = collect(grads, c.depth, c.dim)
+    out, S = prog.forward(P, x, t, rng, True)
+    loss, dtok = ref.smooth_l1_fwd_bwd(out, y, c.tokens, c.patch)
+    prog.backward(P, G, S, dtok, rng, True)
+    return grads, float(loss)
+
+
+def test_engine_matches_torch_adamw_clip_cosine():
+    model = _model()
+    ref_model = _model()
+    cfg = EngineConfig(lr=1e-3, t_max=5, max_grad_norm=0.05, seed=11)
+    eng = TrainEngine(model, cfg, device="cpu")
+    opt = torch.optim.AdamW(ref_model.parameters(), lr=1e-3, betas=cfg.betas, eps=cfg.eps, weight_decay=0.05)
+    sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, 5)
+    names = [n for n, _ in ref_model.named_parameters()]
+    for step in range(3):
+        x, y, t = _batch(4, seed=step)
+        g, loss_val = _grads(ref_model, x, y, t, torch.tensor([11, step]))
+        for n, p in ref_model.named_parameters():
+            p.grad = g[n].clone()
+        torch.nn.utils.clip_grad_norm_(ref_model.parameters(), 0.05)
+        opt.step()
+        sched.step()
+        loss = eng.step(x, y, t)
+        assert float(loss) == pytest.approx(loss_val, rel=1e-6)
+    sd_e, sd_r = model.state_dict(), ref_model.state_dict()
+    for n in names:
+        assert torch.allclose(sd_e[n], sd_r[n], atol=2e-6, rtol=1e-5), n
+    assert eng.current_lr() == pytest.approx(sched.get_last_lr()[0])
+    assert int(eng.step_ctr[0]) == 3 and int(eng.rng[1]) == 3
+    # optimizer / scheduler state dicts load into the torch classes (reference lastepoch.pkl layout)
+    osd = eng.optimizer_state_dict()
+    o2 = torch.optim.AdamW(_model().parameters(), lr=1e-3, weight_decay=0.05)
+    o2.load_state_dict(osd)
+    st_r = opt.state_dict()["state"]
+    for i in range(len(names)):
+        assert torch.allclose(osd["state"][i]["exp_avg"], st_r[i]["exp_avg"], atol=1e-7)
+        assert float(osd["state"][i]["step"]) == 3
+    ssd = eng.scheduler_state_dict()
+    s2 = torch.optim.lr_scheduler.CosineAnnealingLR(o2, 5)
+    s2.load_state_dict(ssd)
+    assert s2.last_epoch == 3
+    # round trip into a fresh engine
+    eng2 = TrainEngine(_model(), cfg, device="cpu")
+    eng2.load_optimizer_state_dict(osd)
+    eng2.load_scheduler_state_dict(ssd)
+    assert torch.equal(eng2.flat_m, eng.flat_m) and torch.equal(eng2.flat_v, eng.flat_v)
+    assert int(eng2.step_ctr[0]) == 3 and int(eng2.step_ctr[1]) == 3
+
+
+def test_engine_params_are_arena_views():
+    model = _model()
+    eng = TrainEngine(model, EngineConfig(), device="cpu")
+    for n, p in model.named_parameters():
+        o, k = eng.offsets[n]
+        assert p.data.data_ptr() == eng.flat_p[o:].data_ptr()
+        assert p.grad.data_ptr() == eng.flat_g[o:].data_ptr()
+        is_ln_bias = n.endswith(".bias") and p.dim() == 1 and "norm" in n
+        assert o % 64 == 0 or (is_ln_bias and o % 4 == 0), n
+    # buckets tile the arena exactly
+    cover = sorted(eng.buckets)
+    assert cover[0][0] == 0 and cover[-1][1] == eng.numel
+    assert all(a[1] == b[0] for a, b in zip(cover, cover[1:]))
+
+
+def test_nonfinite_grad_skips_update():
+    model = _model()
+    eng = TrainEngine(model, EngineConfig(), device="cpu")
+    before = eng.flat_p.clone()
+    x, y, t = _batch(2)
+    x[0, 0, 0, 0] = float("nan")
+    eng.step(x, y, t)
+    assert torch.equal(eng.flat_p, before)
+    assert int(eng.step_ctr[0]) == 0 and int(eng.step_ctr[1]) == 1
+
+
+def _ddp_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        model = _model(drop=False, seed=rank)  # different init per rank: engine must broadcast rank 0's
+        eng = TrainEngine(model, EngineConfig(lr=1e-3, weight_decay=0.0, max_grad_norm=0.0, bucket_blocks=1),
+                          device="cpu")
+        x, y, t = _batch(4, seed=5)
+        b = 4 // world
+        eng.step(x[rank * b:(rank + 1) * b], y[rank * b:(rank + 1) * b], t[rank * b:(rank + 1) * b])
+        m = eng.flat_m.clone()
+        ms = [torch.zeros_like(m) for _ in range(world)]
+        dist.all_gather(ms, m)
+        if rank == 0:
+            torch.save({"m": m, "p": eng.flat_p.clone(), "same": all(torch.equal(ms[0], q) for q in ms)},
+                       out_path)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_data_parallel_gloo_matches_single_process():
+    """Bucketed all-reduce over 2 ranks == one process on the full batch (no dropout)."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "r.pt")
+        mp.start_processes(_ddp_worker, args=(2, free_port(), out), nprocs=2, join=True, start_method="spawn")
+        r = torch.load(out, weights_only=True)
+    assert r["same"]
+    model = _model(drop=False, seed=0)
+    eng = TrainEngine(model, EngineConfig(lr=1e-3, weight_decay=0.0, max_grad_norm=0.0), device="cpu")
+    x, y, t = _batch(4, seed=5)
+    eng.step(x, y, t)
+    m1 = eng.flat_m
+    # exp_avg after one step = (1-b1) * mean-gradient
+    err = (r["m"] - m1).abs().max().item() / m1.abs().max().item()
+    assert err < 1e-4, err

@@ -1,0 +1,124 @@
+"""Experiment layer on CPU: YAML config rules, trainer loop, log format, checkpoints, resume,
+2-rank gloo training, CLI entry points."""
+import dataclasses
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+import yaml
+
+from ddim_cold_amd.config import ExperimentConfig, find_config, load_config
+from ddim_cold_amd.train import checkpoint as ckpt
+from ddim_cold_amd.train.trainer import Paths, launch
+from ddim_cold_amd.utils.logging import parse_log
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_reference_config_rules():
+    cfg = load_config(os.path.join(ROOT, "configs", "20220822.yaml")).validate()
+    assert cfg.per_gpu_batch == 32  # AMP doubles the batch (multi_gpu_trainer.py:187-190)
+    assert cfg.lr == pytest.approx(0.005 * 32 * 1 / 512)
+    cfg8 = dataclasses.replace(cfg, num_gpus=8, AMP=False)
+    assert cfg8.per_gpu_batch == 16 and cfg8.lr == pytest.approx(0.005 * 16 * 8 / 512)
+    assert find_config("20220822").endswith("20220822.yaml")
+
+
+def test_config_errors(tmp_path):
+    p = tmp_path / "bad.yaml"
+    p.write_text("batch_size: 4\nnot_a_key: 1\n")
+    with pytest.raises(ValueError, match="not_a_key"):
+        load_config(str(p))
+    with pytest.raises(ValueError):
+        ExperimentConfig(image_size=[64, 64], patch_size=7, synthetic=True).validate()
+    with pytest.raises(ValueError):
+        ExperimentConfig(dataStorage=["", ""]).validate()
+
+
+def _tiny_cfg(**kw):
+    base = dict(initializing="init.pkl", framework="_tiny", num_gpus=1, batch_size=4, epoch=[0, 2],
+                image_size=[16, 16], patch_size=4, embed_dim=32, depth=2, head=2, synthetic=True,
+                synthetic_size=64, log_every=2, graph=False)
+    base.update(kw)
+    return ExperimentConfig(**base).validate()
+
+
+def test_trainer_log_checkpoints_and_resume(tmp_path):
+    cfg = _tiny_cfg(ckpt_dir=str(tmp_path / "Saved_Models"))
+    paths = Paths.make(cfg, "exp", root=str(tmp_path))
+    res = launch(cfg, "exp", paths, backend="gloo")
+    spe = 64 // 8
+    assert res["steps"] == 2 * spe
+    with open(paths.log) as f:
+        text = f.read()
+    assert text.startswith("Date: ") and f"TrainSet batchs:{spe}" in text and "TestSet batchs:1" in text
+    steps, epochs = parse_log(paths.log)
+    assert [s for s, _, _ in steps] == list(range(2, 2 * spe + 1, 2))
+    assert [e for e, _ in epochs] == [0, 1]
+    assert os.path.isfile(os.path.join(paths.saved_dir, "init.pkl"))
+    last = torch.load(os.path.join(paths.ckpt_dir, "lastepoch.pkl"), weights_only=True)
+    assert {"epoch", "steps", "loss_rec", "metric", "state_dict", "scheduler", "optimizer"} <= set(last)
+    assert last["epoch"] == 1 and last["steps"] == 2 * spe
+    assert all(k.startswith("module.") for k in last["state_dict"])
+    assert last["scheduler"]["last_epoch"] == 2 * spe and last["scheduler"]["T_max"] == 2 * spe
+    best = torch.load(os.path.join(paths.ckpt_dir, "bestloss.pkl"), weights_only=True)
+    assert not any(k.startswith("module.") for k in best)
+    opt = torch.optim.AdamW([torch.nn.Parameter(v.clone()) for v in best.values()])
+    opt.load_state_dict(last["optimizer"])
+
+    # resume: epoch+1, steps continue, optimizer/scheduler restored
+    cfg2 = dataclasses.replace(cfg, resume=os.path.join(paths.ckpt_dir, "lastepoch.pkl"), epoch=[0, 3])
+    res2 = launch(cfg2, "exp", paths, backend="gloo")
+    assert res2["steps"] == 3 * spe
+    assert [e for e, _ in res2["history"]] == [2]
+    with open(paths.log) as f:
+        text = f.read()
+    assert "resuming from epoch        2 of" in text and "recovering best_loss" in text
+    last2 = torch.load(os.path.join(paths.ckpt_dir, "lastepoch.pkl"), weights_only=True)
+    assert float(last2["optimizer"]["state"][0]["step"]) == 3 * spe
+
+
+def test_checkpoint_weights_roundtrip(tmp_path):
+    from ddim_cold_amd.models import DiffusionVisionTransformer
+    m = DiffusionVisionTransformer(img_size=[16, 16], patch_size=4, embed_dim=32, depth=1, num_heads=2)
+    p = str(tmp_path / "w.pkl")
+    ckpt.save_weights(m, p)
+    m2 = DiffusionVisionTransformer(img_size=[16, 16], patch_size=4, embed_dim=32, depth=1, num_heads=2)
+    ckpt.load_weights(m2, p)
+    assert all(torch.equal(a, b) for a, b in zip(m.state_dict().values(), m2.state_dict().values()))
+    # DDP-prefixed dict and lastepoch-style dict both load
+    torch.save({"state_dict": ckpt.add_prefix(m.state_dict()), "epoch": 3}, p)
+    ckpt.load_weights(m2, p)
+
+
+def test_trainer_two_ranks_gloo(tmp_path):
+    cfg = _tiny_cfg(num_gpus=2, epoch=[0, 1], ckpt_dir=str(tmp_path / "Saved_Models"))
+    paths = Paths.make(cfg, "exp2", root=str(tmp_path))
+    res = launch(cfg, "exp2", paths, backend="gloo")
+    assert res["steps"] == 64 // 2 // 8
+    steps, epochs = parse_log(paths.log)
+    assert len(epochs) == 1 and epochs[0][1] > 0
+
+
+def test_cli_entry_points(tmp_path):
+    cfg = dict(initializing="init.pkl", framework="_cli", num_gpus=1, batch_size=4, epoch=[0, 1],
+               image_size=[16, 16], patch_size=4, embed_dim=32, depth=1, head=2, synthetic=True,
+               synthetic_size=32, log_every=100, graph=False, dataStorage=["", ""])
+    p = tmp_path / "cliexp.yaml"
+    p.write_text(yaml.safe_dump(cfg))
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "multi_gpu_trainer.py"), str(p), "--root", str(tmp_path),
+                        "--backend", "gloo"], capture_output=True, text=True, env=env, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-2000:]
+    log = tmp_path / "Saved_Models" / "cliexp_cli" / "train.log"
+    assert log.is_file() and (tmp_path / "Saved_Models" / "cliexp_cli" / "cliexp.yaml").is_file()
+    w = tmp_path / "Saved_Models" / "cliexp_cli" / "lastepoch.pkl"
+    out = tmp_path / "out"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "ViT.py"), "--model", "oxford_flower", "--sample_n", "2",
+                        "--acc_k", "400", "--seq_n", "1", "--seq_k", "500", "--out_dir", str(out)],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert any(f.endswith(".png") for f in os.listdir(out))
+    assert w.is_file()
