@@ -61,6 +61,8 @@ def main():
                     help="init the RCCL process group and run segmented graphs + collectives even with 1 rank")
     ap.add_argument("--sampler-k", type=int, default=20)
     ap.add_argument("--sampler-n", type=int, default=64)
+    ap.add_argument("--no-eager-baseline", action="store_true",
+                    help="skip timing the plain eager PyTorch sampler (BASELINE.md's sampling comparator)")
     args = ap.parse_args()
 
     from ddim_cold_amd.parallel.dist import init_distributed, all_reduce_max, barrier, cleanup, env_world
@@ -130,6 +132,16 @@ def main():
                  "ddim_sampler_ms_per_batch": round(dt * 1e3, 3),
                  "ddim_sampler_config": {"k": args.sampler_k, "N": args.sampler_n, "steps": len(s.ts),
                                          "graph": True}}
+        if not args.no_eager_baseline:
+            # the sampling yardstick is a plain eager PyTorch-ROCm
+            # implementation of the same math on the same GPU (fp32, as the
+            # reference samples; bf16-autocast variant reported too)
+            from ddim_cold_amd.bench.eager_sampler import time_eager_sampler
+            e32 = time_eager_sampler(model, dev, args.sampler_k, args.sampler_n)
+            ebf = time_eager_sampler(model, dev, args.sampler_k, args.sampler_n, autocast_bf16=True)
+            extra["ddim_sampler_eager_torch_fp32_img_per_s"] = round(args.sampler_n / e32, 1)
+            extra["ddim_sampler_eager_torch_bf16_img_per_s"] = round(args.sampler_n / ebf, 1)
+            extra["ddim_sampler_vs_eager_fp32"] = round(e32 / dt, 2)
         model.train()
     if rank == 0:
         out = {

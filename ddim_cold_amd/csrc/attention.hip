@@ -21,6 +21,7 @@
 //   qkv Linear's output columns) so the qkv dgrad/wgrad GEMMs consume it directly.
 #include "common.h"
 #include "kernels.h"
+#include <cstdlib>
 
 namespace dc {
 
@@ -369,6 +370,316 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
   }
 }
 
+// ============================================================================ short sequences (N <= 128)
+// One workgroup per (b, h) holding the WHOLE sequence: NP = 32*ceil(N/32) padded
+// rows, NP/16 waves (one 16-query / 16-key strip each).  For the ViT-tiny shape
+// (N = 65, hd = 32) the flash kernels above pad to 128 queries x 128 keys and
+// launch 2 workgroups per head; here one 6-wave workgroup does exact (not
+// online) softmax over 96 keys and the backward is ONE kernel:
+//   phase A (wave = 16 queries): S^T = K Q^T, dP^T = V dO^T, delta, P and dS
+//            (dropout applied) written to LDS as [q][key] images, dQ^T += K^T dS^T;
+//   phase B (wave = 16 keys):    dV^T += dO^T P, dK^T += Q^T dS, contracting over
+//            all queries through transposing LDS reads of the images.
+// Latency rules: every global load of the kernel (all staged images, O rows,
+// LSE) is issued before the first wait (row addresses clamped, padded rows
+// zeroed by select, no branches), and dropout is a template flag so the
+// softmax / dS loops stay branch-free.  Dropout masks are bit-identical to the
+// flash kernels (same element index).
+template <int HD, int NP>
+struct ShortImg {
+  static constexpr int NT = NP * 4;        // threads of the workgroup
+  static constexpr int CPR = HD / 8;       // 16-B chunks per row
+  static constexpr int PER = NP * CPR / NT;  // chunks per thread (= HD / 32)
+  static constexpr int RS = 2 * HD + 32;   // padded LDS row stride (bytes)
+  u32x4 v[PER];
+  __device__ __forceinline__ void load(const bf16* __restrict__ base, size_t ld, int N) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = threadIdx.x + i * NT;
+      const int r = c / CPR, cc = c - r * CPR;
+      const int rr = r < N ? r : N - 1;
+      const u32x4 x = *reinterpret_cast<const u32x4*>(base + (size_t)rr * ld + cc * 8);
+      const u32x4 z = {0u, 0u, 0u, 0u};
+      v[i] = r < N ? x : z;
+    }
+  }
+  __device__ __forceinline__ void store(char* img) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = threadIdx.x + i * NT;
+      const int r = c / CPR, cc = c - r * CPR;
+      *reinterpret_cast<u32x4*>(img + r * RS + cc * 16) = v[i];
+    }
+  }
+};
+
+__device__ __forceinline__ bf16x4 pack4(const f32x4& a) {
+  bf16x4 v;
+  v[0] = f2bf(a[0]); v[1] = f2bf(a[1]); v[2] = f2bf(a[2]); v[3] = f2bf(a[3]);
+  return v;
+}
+
+template <int HD, int NP, bool DROP>
+__global__ __launch_bounds__(NP * 4) void attn_fwd_short_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                                float* __restrict__ lse, int B, int H, int N,
+                                                                float scale, const int64_t* __restrict__ rng,
+                                                                int site, uint32_t thr, float dsc) {
+  using I = ShortImg<HD, NP>;
+  constexpr int RS = I::RS, KS = HD / 32, DT = HD / 16, KT = NP / 16;
+  __shared__ __attribute__((aligned(16))) char lds[2 * NP * RS];
+  char* Kl = lds;
+  char* Vl = lds + NP * RS;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const size_t mat = (size_t)N * HD;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
+  const int q = wave * 16 + li;
+  I ik, iv;
+  ik.load(qkv + ((size_t)B * H + bh) * mat, HD, N);
+  iv.load(qkv + ((size_t)2 * B * H + bh) * mat, HD, N);
+  bf16x8 qf[KS];
+  {
+    const bf16* qrow = qkv + (size_t)bh * mat + (size_t)(q < N ? q : N - 1) * HD;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qrow + 32 * s + 8 * g);
+  }
+  const uint32_t salt = DROP ? site_salt(rng, site) : 0u;
+  ik.store(Kl);
+  iv.store(Vl);
+  __syncthreads();
+  if (wave * 16 >= N) return;  // no barrier follows
+  const float sl2 = scale * LOG2E;
+  f32x4 st[KT];
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) st[t] = mfma16(frag_row<HD>(Kl, 16 * t + li, s, g), qf[s], st[t]);
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < KT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = (16 * t + 4 * g + r) < N ? st[t][r] * sl2 : -INFINITY;
+      st[t][r] = v;
+      mx = fmaxf(mx, v);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float l = 0.f;
+  const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * N);
+#pragma unroll
+  for (int t = 0; t < KT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float pv = exp2f(st[t][r] - mx);
+      l += pv;
+      if (DROP) pv = dropout_keep(salt, rowidx + (uint32_t)(16 * t + 4 * g + r), thr) ? pv * dsc : 0.f;
+      st[t][r] = pv;
+    }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  f32x4 o[DT];
+#pragma unroll
+  for (int d = 0; d < DT; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s2 = 0; s2 < NP / 32; ++s2) {
+    const bf16x8 pb = pack8(st[2 * s2], st[2 * s2 + 1]);
+#pragma unroll
+    for (int d = 0; d < DT; ++d) o[d] = mfma16(frag_t<RS>(Vl, 16 * d, s2, lane), pb, o[d]);
+  }
+  if (q < N) {
+    const float inv = 1.f / l;
+    bf16* orow = out + ((size_t)b * N + q) * (H * HD) + h * HD;
+#pragma unroll
+    for (int d = 0; d < DT; ++d) *reinterpret_cast<bf16x4*>(orow + 16 * d + 4 * g) = pack4(o[d] * inv);
+    if (g == 0) lse[(size_t)bh * N + q] = (mx + log2f(l)) * LN2;
+  }
+}
+
+template <int HD, int NP, bool DROP>
+__global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __restrict__ dout,
+                                                                const bf16* __restrict__ qkv,
+                                                                const bf16* __restrict__ out,
+                                                                const float* __restrict__ lse,
+                                                                bf16* __restrict__ dqkv, int B, int H, int N,
+                                                                float scale, const int64_t* __restrict__ rng,
+                                                                int site, uint32_t thr, float dsc) {
+  using I = ShortImg<HD, NP>;
+  constexpr int RS = I::RS, PS = 2 * NP + 32, KS = HD / 32, DT = HD / 16, KT = NP / 16;
+  __shared__ __attribute__((aligned(16))) char lds[4 * NP * RS + 2 * NP * PS];
+  char* Ql = lds;
+  char* Kl = Ql + NP * RS;
+  char* Vl = Kl + NP * RS;
+  char* Dl = Vl + NP * RS;
+  char* Pl = Dl + NP * RS;   // [q][key] dropped probabilities
+  char* Sl = Pl + NP * PS;   // [q][key] dS
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int D = H * HD;
+  const size_t mat = (size_t)N * HD;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
+  const int q = wave * 16 + li;
+  const bool qv = q < N;
+  const int qc = qv ? q : N - 1;
+  // ---- every global load up front
+  I iq, ik, iv, id;
+  iq.load(qkv + (size_t)bh * mat, HD, N);
+  ik.load(qkv + ((size_t)B * H + bh) * mat, HD, N);
+  iv.load(qkv + ((size_t)2 * B * H + bh) * mat, HD, N);
+  id.load(dout + (size_t)b * N * D + h * HD, D, N);
+  bf16x8 of[KS];
+  {
+    const bf16* orow = out + ((size_t)b * N + qc) * D + h * HD;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) of[s] = *reinterpret_cast<const bf16x8*>(orow + 32 * s + 8 * g);
+  }
+  const float lse_raw = lse[(size_t)bh * N + qc];
+  const uint32_t salt = DROP ? site_salt(rng, site) : 0u;
+  iq.store(Ql);
+  ik.store(Kl);
+  iv.store(Vl);
+  id.store(Dl);
+  __syncthreads();
+
+  // ---- phase A: this wave's 16 queries against all keys
+  const float lse2 = qv ? lse_raw * LOG2E : INFINITY;
+  const float sl2 = scale * LOG2E;
+  bf16x8 qf[KS], df[KS];
+  float dl = 0.f;  // delta = rowsum(dO * O) of this lane's query
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    qf[s] = frag_row<HD>(Ql, q, s, g);
+    df[s] = frag_row<HD>(Dl, q, s, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dl += bf2f(df[s][j]) * bf2f(of[s][j]);
+  }
+  dl += __shfl_xor(dl, 16, 64);
+  dl += __shfl_xor(dl, 32, 64);
+  const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * N);
+  f32x4 ds[KT];
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      st = mfma16(frag_row<HD>(Kl, 16 * t + li, s, g), qf[s], st);
+      dp = mfma16(frag_row<HD>(Vl, 16 * t + li, s, g), df[s], dp);
+    }
+    f32x4 pm;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int key = 16 * t + 4 * g + r;
+      const float pr = key < N ? exp2f(st[r] * sl2 - lse2) : 0.f;
+      float pd = pr, dpv = dp[r];
+      if (DROP) {
+        const bool kp = dropout_keep(salt, rowidx + (uint32_t)key, thr);
+        pd = kp ? pr * dsc : 0.f;
+        dpv = kp ? dpv * dsc : 0.f;
+      }
+      pm[r] = pd;
+      ds[t][r] = pr * (dpv - dl);
+    }
+    *reinterpret_cast<bf16x4*>(Pl + q * PS + (16 * t + 4 * g) * 2) = pack4(pm);
+    *reinterpret_cast<bf16x4*>(Sl + q * PS + (16 * t + 4 * g) * 2) = pack4(ds[t]);
+  }
+  f32x4 dq[DT];
+#pragma unroll
+  for (int d = 0; d < DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s2 = 0; s2 < NP / 32; ++s2) {
+    const bf16x8 sb = pack8(ds[2 * s2], ds[2 * s2 + 1]);
+#pragma unroll
+    for (int d = 0; d < DT; ++d) dq[d] = mfma16(frag_t<RS>(Kl, 16 * d, s2, lane), sb, dq[d]);
+  }
+  if (qv) {
+    bf16* row = dqkv + ((size_t)b * N + q) * (3 * D) + h * HD;
+#pragma unroll
+    for (int d = 0; d < DT; ++d) *reinterpret_cast<bf16x4*>(row + 16 * d + 4 * g) = pack4(dq[d] * scale);
+  }
+  __syncthreads();
+
+  // ---- phase B: this wave's 16 keys against all queries
+  const int key = wave * 16 + li;
+  f32x4 dk[DT], dv[DT];
+#pragma unroll
+  for (int d = 0; d < DT; ++d) {
+    dk[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dv[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int s = 0; s < NP / 32; ++s) {
+    const bf16x8 pb = frag_t<PS>(Pl, 16 * wave, s, lane);
+    const bf16x8 sb = frag_t<PS>(Sl, 16 * wave, s, lane);
+#pragma unroll
+    for (int d = 0; d < DT; ++d) {
+      dv[d] = mfma16(frag_t<RS>(Dl, 16 * d, s, lane), pb, dv[d]);
+      dk[d] = mfma16(frag_t<RS>(Ql, 16 * d, s, lane), sb, dk[d]);
+    }
+  }
+  if (key < N) {
+    bf16* row = dqkv + ((size_t)b * N + key) * (3 * D) + h * HD;
+#pragma unroll
+    for (int d = 0; d < DT; ++d) {
+      *reinterpret_cast<bf16x4*>(row + D + 16 * d + 4 * g) = pack4(dk[d] * scale);
+      *reinterpret_cast<bf16x4*>(row + 2 * D + 16 * d + 4 * g) = pack4(dv[d]);
+    }
+  }
+}
+
+template <int HD, int NP, bool DROP>
+struct ShortLaunch {
+  static void run(bool bwd, const bf16* d, const bf16* q, const bf16* o, float* lse, const float* lse_in,
+                  bf16* outp, int B, int H, int N, float scale, const int64_t* rng, int site, uint32_t thr,
+                  float dsc, hipStream_t stream) {
+    if (!bwd)
+      hipLaunchKernelGGL((attn_fwd_short_kernel<HD, NP, DROP>), dim3(B * H), dim3(NP * 4), 0, stream, q, outp, lse,
+                         B, H, N, scale, rng, site, thr, dsc);
+    else
+      hipLaunchKernelGGL((attn_bwd_short_kernel<HD, NP, DROP>), dim3(B * H), dim3(NP * 4), 0, stream, d, q, o,
+                         lse_in, outp, B, H, N, scale, rng, site, thr, dsc);
+  }
+};
+
+template <int HD, int NP>
+static void launch_short(bool bwd, const bf16* d, const bf16* q, const bf16* o, float* lse, const float* lse_in,
+                         bf16* outp, int B, int H, int N, float scale, const int64_t* rng, int site, uint32_t thr,
+                         float dsc, hipStream_t stream) {
+  if (thr) ShortLaunch<HD, NP, true>::run(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream);
+  else ShortLaunch<HD, NP, false>::run(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream);
+}
+
+template <int HD>
+static void dispatch_short(bool bwd, const bf16* d, const bf16* q, const bf16* o, float* lse, const float* lse_in,
+                           bf16* outp, int B, int H, int N, float scale, const int64_t* rng, int site, uint32_t thr,
+                           float dsc, hipStream_t stream) {
+  switch ((N + 31) / 32) {
+    case 1: launch_short<HD, 32>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream); break;
+    case 2: launch_short<HD, 64>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream); break;
+    case 3: launch_short<HD, 96>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream); break;
+    default: launch_short<HD, 128>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream); break;
+  }
+}
+
+#define DC_INST_SHORT1(HD, NP, DR)                                                                                 \
+  template __global__ void attn_fwd_short_kernel<HD, NP, DR>(const bf16*, bf16*, float*, int, int, int, float,    \
+                                                             const int64_t*, int, uint32_t, float);               \
+  template __global__ void attn_bwd_short_kernel<HD, NP, DR>(const bf16*, const bf16*, const bf16*, const float*, \
+                                                             bf16*, int, int, int, float, const int64_t*, int,    \
+                                                             uint32_t, float);
+#define DC_INST_SHORT(HD, NP) DC_INST_SHORT1(HD, NP, true) DC_INST_SHORT1(HD, NP, false)
+DC_INST_SHORT(32, 32) DC_INST_SHORT(32, 64) DC_INST_SHORT(32, 96) DC_INST_SHORT(32, 128)
+DC_INST_SHORT(64, 32) DC_INST_SHORT(64, 64) DC_INST_SHORT(64, 96) DC_INST_SHORT(64, 128)
+
+constexpr int SHORT_MAX_N = 128;
+
+static bool short_disabled() {
+  static const bool off = [] {
+    const char* e = getenv("DDIM_COLD_ATTN_NO_SHORT");
+    return e && e[0] == '1';
+  }();
+  return off;
+}
+
 }  // namespace dc
 
 using namespace dc;
@@ -380,6 +691,11 @@ void attn_fwd_launch(const void* qkv, void* o, float* lse, int B, int H, int N, 
   const float dsc = p > 0 ? 1.f / (1.f - (float)p) : 1.f;
   const bf16* q = reinterpret_cast<const bf16*>(qkv);
   bf16* out = reinterpret_cast<bf16*>(o);
+  if (N <= SHORT_MAX_N && !short_disabled() && (hd == 32 || hd == 64)) {
+    if (hd == 32) dispatch_short<32>(false, nullptr, q, nullptr, lse, nullptr, out, B, H, N, scale, rng, site, thr, dsc, stream);
+    else dispatch_short<64>(false, nullptr, q, nullptr, lse, nullptr, out, B, H, N, scale, rng, site, thr, dsc, stream);
+    return;
+  }
   if (hd == 32)
     hipLaunchKernelGGL(attn_fwd_kernel<32>, grid, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc);
   else if (hd == 64)
@@ -398,6 +714,11 @@ void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const flo
   const bf16* q = reinterpret_cast<const bf16*>(qkv);
   const bf16* oo = reinterpret_cast<const bf16*>(o);
   bf16* dq = reinterpret_cast<bf16*>(dqkv);
+  if (N <= SHORT_MAX_N && !short_disabled() && (hd == 32 || hd == 64)) {
+    if (hd == 32) dispatch_short<32>(true, d, q, oo, nullptr, lse, dq, B, H, N, scale, rng, site, thr, dsc, stream);
+    else dispatch_short<64>(true, d, q, oo, nullptr, lse, dq, B, H, N, scale, rng, site, thr, dsc, stream);
+    return;
+  }
   if (hd == 32) {
     hipLaunchKernelGGL(attn_bwd_dq_kernel<32>, grid, dim3(256), 0, stream, d, q, oo, lse, delta, dq, B, H, N, scale, rng, site, thr, dsc);
     hipLaunchKernelGGL(attn_bwd_dkv_kernel<32>, grid, dim3(256), 0, stream, d, q, lse, delta, dq, B, H, N, scale, rng, site, thr, dsc);

@@ -62,6 +62,13 @@ struct GemmParams {
 
 constexpr int BK = 64;
 
+constexpr int WG_MAX = 6;
+struct WgradGroup {
+  GemmParams p[WG_MAX];
+  int tile_start[WG_MAX + 1];
+  int n;
+};
+
 static bool dma_disabled() {
   static const bool off = [] {
     const char* e = getenv("DDIM_COLD_GEMM_NO_DMA");
@@ -202,6 +209,8 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, long long idx, int
     reinterpret_cast<float*>(p.C)[idx] = v;
   } else if (EPI == EPI_ATOMIC) {
     atomicAdd(reinterpret_cast<float*>(p.C) + idx, v);
+  } else if (EPI == EPI_ACC) {
+    reinterpret_cast<float*>(p.C)[idx] = pre + v;  // pre = old C (loaded in phase 1)
   } else if (EPI == EPI_QKV) {
     reinterpret_cast<bf16*>(p.C)[idx] = f2bf(v);
   } else if (EPI == EPI_RESID) {
@@ -229,12 +238,12 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, long long idx, int
 template <int EPI, int FM, int FN>
 __device__ __forceinline__ void run_epilogue(const GemmParams& p, const f32x4 (&acc)[FM][FN], int mb, int nb,
                                              int g, int li) {
-  constexpr bool ELEM = EPI == EPI_RESID || EPI == EPI_DGELU || EPI == EPI_EMBED;
+  constexpr bool ELEM = EPI == EPI_RESID || EPI == EPI_DGELU || EPI == EPI_EMBED || EPI == EPI_ACC;
   RowInfo rows[FM][4];
   long long cols[FN];
   bool colok[FN];
   float colb[FN];
-  const bool has_bias = (EPI != EPI_ATOMIC) && p.bias != nullptr;
+  const bool has_bias = (EPI != EPI_ATOMIC) && (EPI != EPI_ACC) && p.bias != nullptr;
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int n = nb + j * 16 + li;
@@ -262,6 +271,7 @@ __device__ __forceinline__ void run_epilogue(const GemmParams& p, const f32x4 (&
         if (ELEM && rows[i][r].off >= 0 && colok[j]) {
           const int n = nb + j * 16 + li;
           if (EPI == EPI_RESID) v = p.res[rows[i][r].off + n];
+          if (EPI == EPI_ACC) v = reinterpret_cast<const float*>(p.C)[rows[i][r].off + n];
           if (EPI == EPI_DGELU) v = bf2f(p.aux[rows[i][r].off + n]);
           if (EPI == EPI_EMBED) {
             const int m = mb + i * 16 + 4 * g + r;
@@ -477,7 +487,7 @@ struct DmaOperand {
 };
 
 template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EPI, int S>
-__global__ __launch_bounds__(256) void gemm_dma_kernel(GemmParams p) {
+__device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int tn) {
   static_assert(WM * WN == 4, "4 waves");
   static_assert(!AT || BM == 64, "transposed A needs BM == 64");
   static_assert(!BT || BN == 64, "transposed B needs BN == 64");
@@ -490,19 +500,11 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(GemmParams p) {
   constexpr int LPT = OA::PER_WAVE + OB::PER_WAVE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
-  const int tiles_n = (p.N + BN - 1) / BN;
-  const int tiles_m = (p.M + BM - 1) / BM;
-  const int nwg = tiles_m * tiles_n;
-  int bid = blockIdx.x;
-  {
-    const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, idx = bid >> 3;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-  }
-  const int tm = bid / tiles_n, tn = bid - tm * tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int total_kt = (p.K + BK - 1) / BK;
   const int kt0 = blockIdx.z * p.ktiles_per_split;
   const int nk = min(total_kt, kt0 + p.ktiles_per_split) - kt0;
+  if (nk <= 0) return;  // empty split slice (grouped launches); no barrier reached
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -522,7 +524,8 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(GemmParams p) {
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // fused bias gradient (wgrad): row sums of A via one extra MFMA against an
   // all-ones fragment per k-step, in the waves of the first column tile only
-  const bool do_db = (EPI == EPI_ATOMIC) && AT && (p.bias != nullptr) && (tn == 0) && (wn == 0);
+  constexpr bool WG = (EPI == EPI_ATOMIC || EPI == EPI_ACC) && AT;
+  const bool do_db = WG && (p.bias != nullptr) && (tn == 0) && (wn == 0);
   f32x4 dbacc[FM];
 #pragma unroll
   for (int i = 0; i < FM; ++i) dbacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -569,24 +572,70 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(GemmParams p) {
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
-      if (EPI == EPI_ATOMIC && AT && do_db) {
+      if (WG && do_db) {
 #pragma unroll
         for (int i = 0; i < FM; ++i) dbacc[i] = mfma16(af[i], ones, dbacc[i]);
       }
     }
   }
 
-  if (EPI == EPI_ATOMIC && AT && do_db && li == 0) {
+  if (WG && do_db && li == 0) {
+    float* db = const_cast<float*>(p.bias);
+    float old[FM][4];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)  // all loads first (see the epilogue note)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * TM + i * 16 + 4 * g + r;
+        old[i][r] = (EPI == EPI_ACC && m < p.M) ? db[m] : 0.f;
+      }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm * TM + i * 16 + 4 * g + r;
-        if (m < p.M) atomicAdd(const_cast<float*>(p.bias) + m, dbacc[i][r]);
+        if (m < p.M) {
+          if (EPI == EPI_ATOMIC) atomicAdd(db + m, dbacc[i][r]);
+          else db[m] = old[i][r] + dbacc[i][r];
+        }
       }
   }
 
   run_epilogue<EPI, FM, FN>(p, acc, m0 + wm * TM, n0 + wn * TN, g, li);
+}
+
+// bijective XCD-aware remap: consecutive block ids land on different XCDs
+// (round robin); give each XCD a contiguous range of tiles instead
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, idx = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EPI, int S>
+__global__ __launch_bounds__(256) void gemm_dma_kernel(GemmParams p) {
+  const int tiles_n = (p.N + BN - 1) / BN;
+  const int tiles_m = (p.M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tm = bid / tiles_n;
+  gemm_dma_body<BM, BN, WM, WN, AT, BT, EPI, S>(p, tm, bid - tm * tiles_n);
+}
+
+// Grouped weight-gradient GEMM: up to WG_MAX independent dW = dy^T x problems
+// (the four linears of a transformer block, plus the head / patch embedding)
+// in ONE launch.  Tiles of all problems share the grid (XCD-aware), blockIdx.z
+// is the token (K) split of every problem.
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_wgrad_group_kernel(WgradGroup gp) {
+  const int bid = xcd_remap(blockIdx.x, gp.tile_start[gp.n]);
+  int i = 0;
+#pragma unroll
+  for (int j = 1; j < WG_MAX; ++j)
+    if (j < gp.n && bid >= gp.tile_start[j]) i = j;
+  const GemmParams& p = gp.p[i];
+  const int tiles_n = (p.N + 63) / 64;
+  const int local = bid - gp.tile_start[i];
+  const int tm = local / tiles_n;
+  gemm_dma_body<64, 64, 2, 2, true, true, EPI, 4>(p, tm, local - tm * tiles_n);
 }
 
 template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EPI>
@@ -662,6 +711,8 @@ DC_INST_DMA2(false, true, EPI_BF16)
 DC_INST_DMA2(false, true, EPI_F32)
 DC_INST_DMA2(false, true, EPI_DGELU)
 DC_INST_DMA(64, true, true, EPI_ATOMIC)
+template __global__ void gemm_wgrad_group_kernel<EPI_ATOMIC>(WgradGroup);
+template __global__ void gemm_wgrad_group_kernel<EPI_ACC>(WgradGroup);
 
 }  // namespace dc
 
@@ -718,4 +769,24 @@ void gemm_dgrad(const GemmArgs& a, int epi, hipStream_t stream) {
 void gemm_wgrad(const GemmArgs& a, int splits, hipStream_t stream) {
   GemmParams p = base_params(a);
   launch_auto<true, true, EPI_ATOMIC>(p, splits, stream);
+}
+
+void gemm_wgrad_group(const GemmArgs* probs, int n, int splits, hipStream_t stream) {
+  if (n < 1 || n > WG_MAX) throw std::runtime_error("gemm_wgrad_group: 1..6 problems per launch");
+  WgradGroup gp{};
+  gp.n = n;
+  int tiles = 0;
+  for (int i = 0; i < n; ++i) {
+    gp.p[i] = base_params(probs[i]);
+    const int kt = (gp.p[i].K + BK - 1) / BK;
+    gp.p[i].ktiles_per_split = (kt + splits - 1) / splits;
+    gp.tile_start[i] = tiles;
+    tiles += ((gp.p[i].M + 63) / 64) * ((gp.p[i].N + 63) / 64);
+  }
+  for (int i = n; i <= WG_MAX; ++i) gp.tile_start[i] = tiles;
+  constexpr int lds = 4 * (64 * 128 + 64 * 128);
+  if (splits == 1)
+    hipLaunchKernelGGL(gemm_wgrad_group_kernel<EPI_ACC>, dim3(tiles, 1, 1), dim3(256), lds, stream, gp);
+  else
+    hipLaunchKernelGGL(gemm_wgrad_group_kernel<EPI_ATOMIC>, dim3(tiles, 1, splits), dim3(256), lds, stream, gp);
 }

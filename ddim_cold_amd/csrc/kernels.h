@@ -15,6 +15,7 @@ enum GemmEpi : int {
   EPI_EMBED = 6,   // patch rows -> token rows: +bias +pos +temb[t], Dropout, f32
   EPI_DGELU = 7,   // C bf16 = Dropout(acc) * GELU'(aux)
   EPI_ATOMIC = 8,  // C f32 += acc (split-K / gradient accumulate) ; bias -> fused column sum
+  EPI_ACC = 9,     // C f32 += acc, one writer per element (no split) ; bias likewise
 };
 
 struct GemmArgs {
@@ -43,6 +44,9 @@ struct GemmArgs {
 void gemm_nt(const GemmArgs& a, int epi, hipStream_t stream);
 void gemm_dgrad(const GemmArgs& a, int epi, hipStream_t stream);
 void gemm_wgrad(const GemmArgs& a, int splits, hipStream_t stream);
+// grouped dW += dy^T x for n <= 6 problems in one launch; splits == 1 -> plain
+// read-add-write (one writer per element), else fp32 atomics over token slices
+void gemm_wgrad_group(const GemmArgs* probs, int n, int splits, hipStream_t stream);
 
 // LayerNorm (layernorm.hip)
 void layernorm_fwd_launch(const float* x, const float* gamma, const float* beta, void* y_bf16, float* mean,

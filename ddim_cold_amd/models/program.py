@@ -191,19 +191,29 @@ class ViTProgram:
 
     # ------------------------------------------------------------------ backward
     def backward_iter(self, P: ModelTensors, G: ModelTensors, S: Saved, dtok: torch.Tensor, rng: torch.Tensor,
-                      training: bool = True, wgrad: Callable = immediate_wgrad,
+                      training: bool = True, wgrad: Optional[Callable] = None,
                       ln_ws: Optional[torch.Tensor] = None) -> Iterator[int]:
         """Hand-written backward; yields the block index after each block's grads
         are issued (L-1 first, then ..., 0) and -1 after the embedding grads.
 
-        ``G`` tensors are fp32 accumulators (``+=``).  ``wgrad`` lets the engine
-        route weight-gradient GEMMs to a side stream.  ``ln_ws`` ([2L+1, R, 2D],
+        ``G`` tensors are fp32 accumulators (``+=``).  By default the weight
+        gradients of each block (qkv, proj, fc1, fc2; plus the head with the
+        last block) are batched and issued as ONE grouped GEMM launch at the end
+        of the block (``ops.WgradBatch``); a ``wgrad`` callable instead issues
+        each one immediately (e.g. on a side stream).  ``ln_ws`` ([2L+1, R, 2D],
         zero) collects LayerNorm dgamma/dbeta replicas in backward order (final
         norm, then norm2/norm1 of blocks L-1..0); the caller finalises them
         with ``ops.replica_reduce_``.
         """
         def ws(k):
             return None if ln_ws is None else ln_ws[k]
+        batch = None
+        if wgrad is None:
+            batch = wgrad = ops.WgradBatch()
+
+        def flush():
+            if batch is not None:
+                batch.flush()
         c = self.cfg
         N, D = c.tokens, c.dim
         pd = c.drop if training else 0.0
@@ -240,16 +250,18 @@ class ViTProgram:
                 g, gy = ops.layernorm_bwd(dl1, x0, m1, r1, bp.n1w, g1, bg.n1w, bg.n1b, N, rng, 0, 0.0, 0, 0.0,
                                           False, ws(k2 + 1))
             keep.append((gy1, du, dqkv))
+            flush()
             yield i
         B = S.t.shape[0]
         temb_g = G.temb if G.temb is not None else torch.zeros_like(P.temb)
         gpatch = ops.embed_bwd(g.view(B, N, D), S.t, rng, SITE_EMBED, pd, G.cls, G.pos, temb_g)
         wgrad(gpatch, S.patches, G.pe_w, G.pe_b)
+        flush()
         keep.append(gpatch)
         self._keep = keep  # holds side-stream operands alive until the caller joins
         yield -1
 
-    def backward(self, P, G, S, dtok, rng, training=True, wgrad=immediate_wgrad):
+    def backward(self, P, G, S, dtok, rng, training=True, wgrad=None):
         for _ in self.backward_iter(P, G, S, dtok, rng, training, wgrad):
             pass
         self._keep = None

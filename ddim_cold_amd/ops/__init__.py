@@ -111,6 +111,33 @@ def linear_wgrad(dy, x, dw, db: Optional[torch.Tensor]):
     return ref.linear_wgrad(dy, x, dw, db)
 
 
+def linear_wgrad_group(jobs):
+    """``dW_i += dy_i^T x_i`` (and ``db_i += colsum(dy_i)``) for a list of
+    ``(dy, x, dw, db)`` jobs in ONE grouped launch (csrc/gemm.hip
+    ``gemm_wgrad_group_kernel``)."""
+    if not jobs:
+        return
+    if _hip(jobs[0][0]):
+        dys, xs, dws, dbs = (list(z) for z in zip(*jobs))
+        return _ops().linear_wgrad_group(dys, xs, dws, dbs)
+    for dy, x, dw, db in jobs:
+        ref.linear_wgrad(dy, x, dw, db)
+
+
+class WgradBatch:
+    """Collects weight-gradient GEMMs and issues them as one grouped launch on ``flush``."""
+
+    def __init__(self):
+        self.jobs = []
+
+    def __call__(self, dy, x, dw, db):
+        self.jobs.append((dy, x, dw, db))
+
+    def flush(self):
+        jobs, self.jobs = self.jobs, []
+        linear_wgrad_group(jobs)
+
+
 LN_REPLICAS = 16  # csrc/layernorm.hip LN_REPLICAS
 
 

@@ -13,9 +13,11 @@ AdamW step, cosine LR step, zero_grad) re-designed for a latency-bound
 * **Fused optimizer.**  3 launches per step (global grad-norm, AdamW + clip +
   cosine LR + bf16 shadow refresh + grad zeroing, counter bump); the LR /
   Adam step / RNG step live in device memory so the step is graph-replayable.
-* **Side-stream weight gradients.**  wgrad GEMMs (nothing on the critical
-  path depends on them) run on a second HIP stream, overlapping the
-  dgrad/attention chain of the backward.
+* **Grouped weight gradients.**  The four weight-gradient GEMMs of a block
+  (and the head's, with the last block) are one grouped launch at the end of
+  the block's backward (``ops.WgradBatch``): 216 output tiles fill the chip
+  without a token split, so no atomics.  (Issuing them one by one on a side
+  stream, ``wgrad_stream=True``, measured slower.)
 * **Segmented hipGraph capture + bucketed RCCL all-reduce.**  The step is
   captured as ``n_buckets + 1`` graphs split at transformer-block boundaries
   of the backward.  Between segment replays the host enqueues the finished
@@ -196,9 +198,6 @@ class TrainEngine:
         self._graphs = None
 
     def _wgrad(self, dy, x, dw, db):
-        if self.side is None:
-            ops.linear_wgrad(dy, x, dw, db)
-            return
         cur = torch.cuda.current_stream(self.device)
         self.side.wait_stream(cur)
         with torch.cuda.stream(self.side):
@@ -218,7 +217,7 @@ class TrainEngine:
         del out
         ln_lo = 0
         for i in self.prog.backward_iter(self.param_tensors, self.grad_tensors, S, dtok, self.rng, True,
-                                         wgrad=self._wgrad, ln_ws=self.ln_ws):
+                                         wgrad=self._wgrad if self.side is not None else None, ln_ws=self.ln_ws):
             if i in self.bucket_after and (self.segmented or i == -1):
                 hi = self.ln_done_at[i]
                 if hi > ln_lo:

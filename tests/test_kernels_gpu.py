@@ -183,9 +183,35 @@ def test_wgrad(M, Nout, K):
     close(db1, db2, 2e-2, 1e-4, "db")
 
 
+@pytest.mark.parametrize("big", [True, False])
+def test_linear_wgrad_group(big):
+    """Grouped launch == per-problem reference (unsplit read-add-write and split atomic paths)."""
+    M = 2080
+    shapes = [(1152, 384), (384, 384), (384, 384), (384, 384), (192, 384)] if big else [(384, 192), (64, 96)]
+    jobs, refs = [], []
+    for i, (nout, k) in enumerate(shapes):
+        m = M if big or i == 0 else 512
+        dy, x = bf(m, nout), bf(m, k)
+        dw0 = torch.randn(nout, k, device=DEV) * 0.1
+        db0 = torch.randn(nout, device=DEV) if i % 2 == 0 else None
+        dw, db = dw0.clone(), (db0.clone() if db0 is not None else None)
+        jobs.append((dy, x, dw, db))
+        dw2, db2 = dw0.clone(), (db0.clone() if db0 is not None else None)
+        ref.linear_wgrad(dy, x, dw2, db2)
+        refs.append((dw2, db2))
+    ops.linear_wgrad_group(jobs)
+    for (dy, x, dw, db), (dw2, db2) in zip(jobs, refs):
+        close(dw, dw2, 2e-2, 1e-4, "dw")
+        if db is not None:
+            close(db, db2, 2e-2, 1e-4, "db")
+
+
 # ------------------------------------------------------------------ attention
 @pytest.mark.parametrize("B,H,N,hd,p", [(4, 12, 65, 32, 0.0), (4, 12, 65, 32, 0.1), (2, 4, 257, 64, 0.1),
-                                        (1, 2, 17, 32, 0.0), (1, 6, 626, 64, 0.0), (2, 3, 130, 64, 0.2)])
+                                        (1, 2, 17, 32, 0.0), (1, 6, 626, 64, 0.0), (2, 3, 130, 64, 0.2),
+                                        # short-sequence path (N <= 128): every padded size, both head dims
+                                        (2, 3, 100, 64, 0.1), (3, 5, 128, 32, 0.1), (2, 2, 64, 64, 0.0),
+                                        (2, 4, 32, 32, 0.1), (2, 4, 33, 64, 0.0), (8, 4, 97, 32, 0.0)])
 def test_attention_fwd_bwd(B, H, N, hd, p):
     qkv = bf(3, B, H, N, hd)
     r = rng()

@@ -57,6 +57,9 @@ def main():
     res["wgrad 384x384"] = t(lambda: ops.linear_wgrad(a, a, dw, db))
     dw3, db3 = torch.zeros(3 * D, D, device=dev), torch.zeros(3 * D, device=dev)
     res["wgrad 1152x384"] = t(lambda: ops.linear_wgrad(dqkv, a, dw3, db3))
+    h_ = bf(M, D)
+    blk = [(a, h_, dw, db), (a, h_, dw.clone(), db.clone()), (a, h_, dw.clone(), db.clone()), (dqkv, a, dw3, db3)]
+    res["wgrad group (block: 3x384^2 + 1152x384)"] = t(lambda: ops.linear_wgrad_group(blk))
     g, bb = torch.randn(D, device=dev), torch.randn(D, device=dev)
     res["ln fwd"] = t(lambda: ops.layernorm_fwd(x, g, bb))
     _, mu, rs = ops.layernorm_fwd(x, g, bb)
