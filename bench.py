@@ -86,7 +86,8 @@ def main():
     lr = base_lr * args.batch * n / 512  # multi_gpu_trainer.py:196
     cfg = EngineConfig(lr=lr, t_max=512 * 100, use_graph=not args.no_graph, bucket_blocks=args.bucket_blocks,
                        seed=42, force_segments=args.force_dist,
-                       wgrad_stream=args.wgrad_stream)
+                       wgrad_stream=args.wgrad_stream,
+                       temb_rows=int(math.log2(model.img_size[1])) + 1)  # cold t in 1..log2(W)
     engine = TrainEngine(model, cfg, device=dev)
     pool = synthetic_pool(1024, tuple(model.img_size), seed=7 + rank, device=dev)
     engine.set_batch_fn(ColdBatcher(pool, args.batch, engine.rng))

@@ -215,6 +215,43 @@ class ColdSampler:
 
 
 @torch.no_grad()
+def ddim_from_starts(model, x: torch.Tensor, starts: Sequence[int], k: int, device=None,
+                     use_graph: bool = True) -> torch.Tensor:
+    """DDIM (jump ``k``) from per-sample start steps, all samples in ONE batch.
+
+    Sample i joins the shared descending grid at its own ``starts[i]`` (per-sample
+    activity masks); all starts must lie on one k-grid (``(max - s) % k == 0``).
+    Returns the final clamped x0-hat on the device, in [-1, 1].
+    """
+    device = torch.device(device) if device is not None else x.device
+    T = model.total_steps
+    B = x.shape[0]
+    top = max(starts)
+    if any((top - s) % k for s in starts):
+        raise ValueError("all start steps must share one k-grid")
+    ts = list(range(top, 0, -k))
+    if ts[-1] + 1 - k < 0:
+        raise ValueError(f"k={k} incompatible with t_start={top}")
+    x = x.to(device).float().contiguous()
+    x0 = torch.zeros_like(x)
+    st = torch.tensor(list(starts), device=device)
+    tt = torch.tensor(ts, dtype=torch.int64, device=device).unsqueeze(1).expand(-1, B).contiguous()
+    active = torch.stack([(st >= t) for t in ts]).view(len(ts), B, 1, 1, 1)
+    coef = torch.tensor([ddim_coefficients(T, t, k) for t in ts], dtype=torch.float32, device=device)
+    den = _Denoiser(model, device)
+
+    def body():
+        for i in range(len(ts)):
+            x0_raw = den(x, tt[i])
+            xn, x0c = ops.ddim_step(x, x0_raw, coef[i])
+            torch.where(active[i], xn, x, out=x)
+            torch.where(active[i], x0c, x0, out=x0)
+
+    _GraphLoop(body, device).run(use_graph and device.type == "cuda")
+    return x0
+
+
+@torch.no_grad()
 def img2img(model, draft: torch.Tensor, t_starts: Sequence[int] = tuple(range(1599, 2000, 50)), k: int = 10,
             device=None, generator: Optional[torch.Generator] = None, use_graph: bool = True) -> torch.Tensor:
     """Zero-shot draft->drawing (SDEdit-style) for several noise levels at once.
@@ -242,25 +279,8 @@ def img2img(model, draft: torch.Tensor, t_starts: Sequence[int] = tuple(range(15
         # different grids: run them one by one
         return torch.cat([img2img(model, draft[i:i + 1], [s], k, device, generator, use_graph)
                           for i, s in enumerate(starts)])
-    ts = list(range(top, 0, -k))
-    if ts[-1] + 1 - k < 0:
-        raise ValueError(f"k={k} incompatible with t_start={top}")
     eps = torch.normal(0.0, 1.0, (B, C, H, W), generator=generator).to(device)
     alpha = torch.tensor([img2img_alpha(s, T) for s in starts], device=device).view(B, 1, 1, 1)
-    x = (torch.sqrt(1 - alpha) * eps + torch.sqrt(alpha) * draft).contiguous()
-    x0 = torch.zeros_like(x)
-    st = torch.tensor(starts, device=device)
-    tt = torch.tensor(ts, dtype=torch.int64, device=device).unsqueeze(1).expand(-1, B).contiguous()
-    active = torch.stack([(st >= t) for t in ts]).view(len(ts), B, 1, 1, 1)
-    coef = torch.tensor([ddim_coefficients(T, t, k) for t in ts], dtype=torch.float32, device=device)
-    den = _Denoiser(model, device)
-
-    def body():
-        for i in range(len(ts)):
-            x0_raw = den(x, tt[i])
-            xn, x0c = ops.ddim_step(x, x0_raw, coef[i])
-            torch.where(active[i], xn, x, out=x)
-            torch.where(active[i], x0c, x0, out=x0)
-
-    _GraphLoop(body, device).run(use_graph and device.type == "cuda")
+    x = torch.sqrt(1 - alpha) * eps + torch.sqrt(alpha) * draft
+    x0 = ddim_from_starts(model, x, starts, k, device, use_graph)
     return (x0.cpu() + 1) / 2

@@ -61,6 +61,11 @@ class EngineConfig:
     ema_decay: float = 0.99
     ema_init: float = 5.0     # multi_gpu_trainer.py:52 (loss_rec = 5.0)
     force_segments: bool = False  # segmented capture + collectives even at world size 1 (testing)
+    # rows of time_embed that can receive gradient (t < temb_rows for every sample);
+    # the rest are all-zero on every rank and are left out of the all-reduce.
+    # Cold diffusion draws t in 1..log2(W) (7 rows), so for ViT-tiny this drops
+    # 3.1 MB of the 28.7 MB gradient all-reduce.  None: all rows.
+    temb_rows: Optional[int] = None
 
 
 def _align(n: int) -> int:
@@ -161,6 +166,18 @@ class TrainEngine:
         bounds.append((0, end))
         self.bucket_after[-1] = j
         self.buckets = bounds
+        # sub-ranges actually all-reduced per bucket (inactive time_embed rows skipped)
+        self.bucket_ranges = []
+        to, tn = self.offsets["time_embed.weight"]
+        rows = self.cfg.temb_rows
+        skip = None
+        if rows is not None and 0 < rows < self.prog.cfg.total_steps:
+            skip = (to + rows * c.dim, to + tn)
+        for a, b in bounds:
+            if skip is not None and a <= skip[0] and skip[1] <= b:
+                self.bucket_ranges.append([r for r in ((a, skip[0]), (skip[1], b)) if r[1] > r[0]])
+            else:
+                self.bucket_ranges.append([(a, b)])
         # LayerNorm dgamma/dbeta replica workspace in backward order: final norm,
         # then norm2, norm1 of blocks L-1 .. 0; destinations = grad-arena views
         # (weight and bias of one LayerNorm are adjacent: one [2D] range).
@@ -239,14 +256,15 @@ class TrainEngine:
     def _allreduce(self, k: int):
         if not self.dist_on or (self.world <= 1 and not self.cfg.force_segments):
             return
-        a, b = self.buckets[k]
-        view = self.flat_g[a:b]
+        views = [self.flat_g[a:b] for a, b in self.bucket_ranges[k]]
         if self.comm is not None:
             self.comm.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(self.comm):
-                dist.all_reduce(view, group=self.pg)
+                for v in views:
+                    dist.all_reduce(v, group=self.pg)
         else:
-            dist.all_reduce(view, group=self.pg)
+            for v in views:
+                dist.all_reduce(v, group=self.pg)
 
     def _join_comm(self):
         if self.comm is not None:

@@ -143,8 +143,9 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
         printLog("TrainSet batchs:" + str(steps_per_epoch), paths.log)
         printLog("TestSet batchs:" + str(val_batches), paths.log)
 
+    temb_rows = int(math.log2(cfg.image_size[1])) + 1 if cfg.dataset.startswith("cold") else None
     ecfg = EngineConfig(lr=cfg.lr, t_max=steps_per_epoch * cfg.epoch[1], use_graph=cfg.graph,
-                        bucket_blocks=cfg.bucket_blocks, seed=cfg.seed * 1000 + rank)
+                        bucket_blocks=cfg.bucket_blocks, seed=cfg.seed * 1000 + rank, temb_rows=temb_rows)
     engine = TrainEngine(model, ecfg, device=device)
     idx_dev = torch.zeros(B, dtype=torch.int64, device=device)
     engine.set_batch_fn(make_batcher(cfg.dataset, train_pool, B, engine.rng, cfg.total_steps, idx=idx_dev))

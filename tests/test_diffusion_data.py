@@ -198,3 +198,17 @@ def test_img2img_batched_equals_sequential(tiny):
                 x0 = tiny.forward_reference(x, torch.full((1,), t))
                 x, x0c = ref.ddim_step(x, x0, sch.ddim_coefficients(2000, t, 400))
             assert torch.allclose(out[i], ((x0c + 1) / 2)[0], atol=1e-5), s
+
+
+def test_slerp_and_interpolate(tiny):
+    from ddim_cold_amd.diffusion.interpolate import interpolate, slerp
+    a, b = torch.randn(1, 3, 4, 4), torch.randn(1, 3, 4, 4)
+    lam = torch.tensor([0.0, 0.5, 1.0])
+    s = slerp(a, b, lam)
+    assert torch.allclose(s[0], b[0], atol=1e-5) and torch.allclose(s[2], a[0], atol=1e-5)
+    img1, img2 = torch.rand(3, 16, 16) * 2 - 1, torch.rand(3, 16, 16) * 2 - 1
+    out = interpolate(tiny, img1, img2, t_starts=[399, 799], k=400, lambdas=torch.linspace(0, 1, 3), device="cpu",
+                      generator=torch.Generator().manual_seed(0))
+    assert out.shape == (3, 3, 3, 16, 16)
+    assert torch.allclose(out[0, 0], (img1 + 1) / 2) and torch.allclose(out[0, 2], (img2 + 1) / 2)
+    assert out.min() >= 0 and out.max() <= 1

@@ -121,9 +121,11 @@ def _ddp_worker(rank, world, port, out_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         model = _model(drop=False, seed=rank)  # different init per rank: engine must broadcast rank 0's
-        eng = TrainEngine(model, EngineConfig(lr=1e-3, weight_decay=0.0, max_grad_norm=0.0, bucket_blocks=1),
-                          device="cpu")
+        eng = TrainEngine(model, EngineConfig(lr=1e-3, weight_decay=0.0, max_grad_norm=0.0, bucket_blocks=1,
+                                              temb_rows=7), device="cpu")
+        assert len(eng.bucket_ranges[-1]) == 2  # inactive time_embed rows skipped
         x, y, t = _batch(4, seed=5)
+        t = t % 6 + 1  # cold-diffusion timesteps
         b = 4 // world
         eng.step(x[rank * b:(rank + 1) * b], y[rank * b:(rank + 1) * b], t[rank * b:(rank + 1) * b])
         m = eng.flat_m.clone()
@@ -146,7 +148,7 @@ def test_data_parallel_gloo_matches_single_process():
     model = _model(drop=False, seed=0)
     eng = TrainEngine(model, EngineConfig(lr=1e-3, weight_decay=0.0, max_grad_norm=0.0), device="cpu")
     x, y, t = _batch(4, seed=5)
-    eng.step(x, y, t)
+    eng.step(x, y, t % 6 + 1)
     m1 = eng.flat_m
     # exp_avg after one step = (1-b1) * mean-gradient
     err = (r["m"] - m1).abs().max().item() / m1.abs().max().item()
