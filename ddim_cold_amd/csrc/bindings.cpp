@@ -146,6 +146,41 @@ Tensor linear_residual_fwd(Tensor a, Tensor w, Tensor b, Tensor x, int64_t N, Te
   return out;
 }
 
+// x_new = x + DropPath(Dropout(a w^T + b)); (ln, mean, rstd) = LayerNorm(x_new)
+std::tuple<Tensor, Tensor, Tensor, Tensor> linear_residual_ln_fwd(Tensor a, Tensor w, Tensor b, Tensor x,
+                                                                  Tensor gamma, Tensor beta, double eps, int64_t N,
+                                                                  Tensor rng, int64_t site_drop, double p_drop,
+                                                                  int64_t site_dp, double p_dp) {
+  CHECK_IN(a, BF16); CHECK_IN(w, BF16); CHECK_IN(b, F32); CHECK_IN(x, F32); CHECK_IN(gamma, F32);
+  CHECK_IN(beta, F32); check_rng(rng);
+  const c10::DeviceGuard guard(a.device());
+  const int K = a.size(-1);
+  auto a2 = a.view({-1, K});
+  check_linear(a2, w, K);
+  const int M = a2.size(0), D = w.size(0);
+  TORCH_CHECK(x.numel() == (int64_t)M * D && b.numel() == D && gamma.numel() == D && beta.numel() == D &&
+                  M % N == 0, "residual+LN shapes");
+  TORCH_CHECK(gemm_resid_ln_supported(D, K), "residual+LN GEMM: unsupported width D=", D, " / K=", K);
+  auto x_out = at::empty(x.sizes(), x.options());
+  auto ln = at::empty({M, D}, a.options());
+  auto mean = at::empty({M}, x.options());
+  auto rstd = at::empty({M}, x.options());
+  GemmLnArgs g;
+  g.A = a2.data_ptr(); g.W = w.data_ptr(); g.M = M; g.K = K; g.D = D;
+  g.bias = b.data_ptr<float>(); g.res = x.data_ptr<float>(); g.x_out = x_out.data_ptr<float>();
+  g.gamma = gamma.data_ptr<float>(); g.beta = beta.data_ptr<float>(); g.ln_out = ln.data_ptr();
+  g.mean = mean.data_ptr<float>(); g.rstd = rstd.data_ptr<float>(); g.eps = (float)eps;
+  g.tokens = N; g.rng = rng.data_ptr<int64_t>();
+  g.site_drop = site_drop; g.p_drop = p_drop; g.site_dp = site_dp; g.p_dp = p_dp;
+  static const int bm_env = [] {
+    const char* e = getenv("DDIM_COLD_LN_GEMM_BM");
+    return e ? atoi(e) : 0;
+  }();
+  g.bm = bm_env ? bm_env : 32;
+  gemm_resid_ln(g, cur_stream());
+  return {x_out, ln, mean, rstd};
+}
+
 std::tuple<Tensor, Tensor> linear_gelu_fwd(Tensor a, Tensor w, Tensor b, Tensor rng, int64_t site, double p) {
   CHECK_IN(a, BF16); CHECK_IN(w, BF16); CHECK_IN(b, F32); check_rng(rng);
   const c10::DeviceGuard guard(a.device());
@@ -513,6 +548,8 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("linear_residual_fwd(Tensor a, Tensor w, Tensor b, Tensor x, int N, Tensor rng, int site_drop, "
         "float p_drop, int site_dp, float p_dp) -> Tensor");
   m.def("linear_gelu_fwd(Tensor a, Tensor w, Tensor b, Tensor rng, int site, float p) -> (Tensor, Tensor)");
+  m.def("linear_residual_ln_fwd(Tensor a, Tensor w, Tensor b, Tensor x, Tensor gamma, Tensor beta, float eps, "
+        "int N, Tensor rng, int site_drop, float p_drop, int site_dp, float p_dp) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("head_fwd(Tensor a, Tensor w, Tensor b, int B, int C, int H, int W, int patch) -> Tensor");
   m.def("smooth_l1_fwd_bwd(Tensor pred, Tensor target, int N, int patch, float beta) -> (Tensor, Tensor)");
   m.def("img_to_tokgrad(Tensor dimg, int N, int patch) -> Tensor");
@@ -553,6 +590,7 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("linear_dgrad", &linear_dgrad);
   m.impl("linear_dgrad_gelu", &linear_dgrad_gelu);
   m.impl("linear_wgrad", &linear_wgrad);
+  m.impl("linear_residual_ln_fwd", &linear_residual_ln_fwd);
   m.impl("linear_wgrad_group", &linear_wgrad_group);
   m.impl("layernorm_bwd", &layernorm_bwd);
   m.impl("replica_reduce_", &replica_reduce_);

@@ -26,6 +26,7 @@
 // Reference semantics covered: nn.Linear / Conv2d-as-GEMM in ViT.py:79-103,150,183.
 #include "common.h"
 #include "kernels.h"
+#include "gemm_common.h"
 #include <cstdlib>
 
 namespace dc {
@@ -60,7 +61,6 @@ struct GemmParams {
   int ktiles_per_split;
 };
 
-constexpr int BK = 64;
 
 constexpr int WG_MAX = 6;
 struct WgradGroup {
@@ -76,8 +76,6 @@ static bool dma_disabled() {
   }();
   return off;
 }
-
-__device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
 
 template <int R, bool T>
 struct Stage {
@@ -122,20 +120,6 @@ struct Stage {
   }
 };
 
-// fragment of a k-contiguous image, standard k order
-__device__ __forceinline__ bf16x8 frag_k(const char* lds, int r, int s, int g) {
-  const int chunk = 4 * s + g;
-  return *reinterpret_cast<const bf16x8*>(lds + r * 128 + 16 * (chunk ^ swz(r)));
-}
-// fragment of a k-contiguous image, permuted k order
-__device__ __forceinline__ bf16x8 frag_k_perm(const char* lds, int r, int s, int g) {
-  const int ca = 4 * s + (g >> 1), cb = ca + 2;
-  const int sub = 8 * (g & 1);
-  const u32x2 lo = *reinterpret_cast<const u32x2*>(lds + r * 128 + 16 * (ca ^ swz(r)) + sub);
-  const u32x2 hi = *reinterpret_cast<const u32x2*>(lds + r * 128 + 16 * (cb ^ swz(r)) + sub);
-  u32x4 v = {lo[0], lo[1], hi[0], hi[1]};
-  return __builtin_bit_cast(bf16x8, v);
-}
 // Epilogue in two phases: (1) every global load the epilogue needs (bias per
 // column, residual / saved pre-activation / pos+time embedding per element) is
 // issued for the whole fragment tile, (2) compute + store.  Interleaving them
@@ -417,75 +401,6 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
 // = 8 rows each, swizzle applied on the per-lane SOURCE address):
 //   k-contiguous operand  [rows][64 k]  chunk' = chunk ^ ((row>>1)&7)
 //   transposed operand    [64 k][64]    chunk' = chunk ^ (row & 6)   (tr-read conflict-free)
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-template <int LPT>
-__device__ __forceinline__ void vm_wait_rem(int rem) {
-  switch (rem) {
-    case 0: vm_wait<0>(); break;
-    case 1: vm_wait<LPT>(); break;
-    case 2: vm_wait<2 * LPT>(); break;
-    case 3: vm_wait<3 * LPT>(); break;
-    default: vm_wait<4 * LPT>(); break;
-  }
-}
-__device__ __forceinline__ void raw_barrier() {
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-__device__ __forceinline__ bf16x8 frag_t_swz(const char* lds, int c0, int s, int lane) {
-  const int i = lane & 15, g = lane >> 4, q = i >> 2, p = i & 3;
-  const int ra = 32 * s + 4 * g + q;
-  const int chunk = (c0 >> 3) + (p >> 1);
-  const int off = ra * 128 + 16 * (chunk ^ (ra & 6)) + 8 * (p & 1);
-  const bf16x4 lo = lds_read_tr(reinterpret_cast<const bf16*>(lds + off));
-  const bf16x4 hi = lds_read_tr(reinterpret_cast<const bf16*>(lds + off + 16 * 128));
-  bf16x8 v;
-  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
-  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
-  return v;
-}
-
-template <int R, bool T>
-struct DmaOperand {
-  static constexpr int BYTES = R * 128;          // one 64-deep K tile
-  static constexpr int PER_WAVE = BYTES / 4096;  // 1-KiB pieces per wave
-  bf16* base;
-  int nbytes;
-  int voff[PER_WAVE];  // per-lane byte offset of piece j at k-tile 0
-  int kstep;           // byte advance per K tile
-
-  __device__ __forceinline__ void init(const bf16* base, int ld, int rows_total_bytes_rows, int row0, int wave,
-                                       int lane) {
-    // rows_total_bytes_rows: number of rows of the stored matrix (for the OOB range)
-    this->base = const_cast<bf16*>(base);
-    nbytes = rows_total_bytes_rows * ld * 2;
-#pragma unroll
-    for (int j = 0; j < PER_WAVE; ++j) {
-      const int piece = wave * PER_WAVE + j;
-      const int r = piece * 8 + (lane >> 3), pc = lane & 7;
-      if (!T) {
-        const int lc = pc ^ ((r >> 1) & 7);
-        voff[j] = ((row0 + r) * ld + 8 * lc) * 2;
-      } else {
-        const int lc = pc ^ (r & 6);
-        voff[j] = (r * ld + row0 + 8 * lc) * 2;
-      }
-    }
-    kstep = T ? 64 * ld * 2 : 64 * 2;
-  }
-  __device__ __forceinline__ void issue(char* lds_tile, int kt, int wave) const {
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, nbytes, 0x00020000);
-#pragma unroll
-    for (int j = 0; j < PER_WAVE; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rsrc, (DC_LDS void*)(lds_tile + (wave * PER_WAVE + j) * 1024), 16, voff[j] + kt * kstep, 0, 0, 0);
-  }
-};
-
 template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EPI, int S>
 __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int tn) {
   static_assert(WM * WN == 4, "4 waves");
@@ -602,13 +517,6 @@ __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int t
   }
 
   run_epilogue<EPI, FM, FN>(p, acc, m0 + wm * TM, n0 + wn * TN, g, li);
-}
-
-// bijective XCD-aware remap: consecutive block ids land on different XCDs
-// (round robin); give each XCD a contiguous range of tiles instead
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, idx = bid >> 3;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
 template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EPI, int S>

@@ -48,6 +48,31 @@ void gemm_wgrad(const GemmArgs& a, int splits, hipStream_t stream);
 // read-add-write (one writer per element), else fp32 atomics over token slices
 void gemm_wgrad_group(const GemmArgs* probs, int n, int splits, hipStream_t stream);
 
+// Row-panel GEMM + residual + LayerNorm epilogue (gemm_ln.hip)
+struct GemmLnArgs {
+  const void* A = nullptr;      // [M][K] bf16
+  const void* W = nullptr;      // [D][K] bf16
+  int M = 0, K = 0, D = 0;
+  const float* bias = nullptr;  // [D]
+  const float* res = nullptr;   // [M][D] residual stream in
+  float* x_out = nullptr;       // [M][D] residual stream out
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
+  void* ln_out = nullptr;       // [M][D] bf16
+  float* mean = nullptr;
+  float* rstd = nullptr;
+  float eps = 1e-5f;
+  int tokens = 1;
+  const int64_t* rng = nullptr;
+  int site_drop = 0;
+  double p_drop = 0.0;
+  int site_dp = 0;
+  double p_dp = 0.0;
+  int bm = 32;                  // row-panel height (32 or 64)
+};
+bool gemm_resid_ln_supported(int D, int K);
+void gemm_resid_ln(const GemmLnArgs& a, hipStream_t stream);
+
 // LayerNorm (layernorm.hip)
 void layernorm_fwd_launch(const float* x, const float* gamma, const float* beta, void* y_bf16, float* mean,
                           float* rstd, int M, int D, float eps, hipStream_t stream);

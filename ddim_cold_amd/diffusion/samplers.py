@@ -15,10 +15,19 @@ if the weights they read were reallocated.
 
 Sampling always runs the denoiser in eval mode (no dropout); the reference's
 ``ViT.py`` CLI forgot ``model.eval()``.
+
+Concurrent chains (option): the samples of a batch never interact, so the
+batch can be split into ``streams`` chunks whose whole chains run on separate
+HIP streams, forked once at the start of the captured loop and joined once at
+the end.  Measured on MI355X (ViT-tiny, N=64, k=20, graph-captured): 1 chain
+46.9 ms, 2 chains 56.2, 4 chains 76.2 — the graph's parallel branches do not
+overlap, so the default is one chain (``DDIM_COLD_SAMPLER_STREAMS`` overrides).
 """
 from __future__ import annotations
 
+import contextlib
 import math
+import os
 import time
 from typing import List, Optional, Sequence
 
@@ -65,6 +74,38 @@ class _Denoiser:
             self.model.train(was)
 
 
+def default_streams(N: int, device) -> int:
+    env = os.environ.get("DDIM_COLD_SAMPLER_STREAMS")
+    if env:
+        return max(1, int(env))
+    return 1
+
+
+class _Chains:
+    """Split a batch into independent chains, each on its own stream (fork/join around the whole loop)."""
+
+    def __init__(self, N: int, device, streams: int):
+        n = max(1, min(streams, N))
+        bounds = [N * c // n for c in range(n + 1)]
+        self.slices = [slice(bounds[c], bounds[c + 1]) for c in range(n)]
+        cuda = device.type == "cuda" and n > 1
+        self.streams = [torch.cuda.Stream(device=device) for _ in range(n)] if cuda else [None] * n
+        self.device = device
+
+    def run(self, chain):
+        """``chain(sl)`` issues the whole loop for batch slice ``sl``."""
+        main = torch.cuda.current_stream(self.device) if self.streams[0] is not None else None
+        for st in self.streams:
+            if st is not None:
+                st.wait_stream(main)
+        for sl, st in zip(self.slices, self.streams):
+            with (torch.cuda.stream(st) if st is not None else contextlib.nullcontext()):
+                chain(sl)
+        for st in self.streams:
+            if st is not None:
+                main.wait_stream(st)
+
+
 def _cache(model) -> dict:
     return model.__dict__.setdefault("_sampler_graphs", {})
 
@@ -96,7 +137,7 @@ class _GraphLoop:
 
 
 class DDIMSampler:
-    def __init__(self, model, device, k: int = 10, use_graph: bool = True):
+    def __init__(self, model, device, k: int = 10, use_graph: bool = True, streams: Optional[int] = None):
         self.model = model
         self.device = torch.device(device)
         self.k = k
@@ -106,9 +147,11 @@ class DDIMSampler:
         self.use_graph = use_graph and self.device.type == "cuda"
         self.H, self.W = model.img_size
         self.C = model.in_chans
+        self.streams = streams
 
     def _state(self, N: int, record: bool):
-        key = ("ddim", N, self.k, record, str(self.device))
+        nstreams = self.streams or default_streams(N, self.device)
+        key = ("ddim", N, self.k, record, str(self.device), nstreams)
         den = _Denoiser(self.model, self.device)
         cache = _cache(self.model)
         st = cache.get(key)
@@ -120,15 +163,17 @@ class DDIMSampler:
         tt = torch.tensor(self.ts, dtype=torch.int64, device=dev).unsqueeze(1).expand(-1, N).contiguous()
         traj = torch.zeros(len(self.ts), N, self.C, self.H, self.W, device=dev) if record else None
         coef = self.coef
+        chains = _Chains(N, dev, nstreams)
 
-        def body():
+        def chain(sl):
+            xs, x0s = x[sl], x0[sl]
             for i in range(len(self.ts)):
-                x0_raw = den(x, tt[i])
-                ops.ddim_step_(x, x0_raw, x0, coef[i])
+                x0_raw = den(xs, tt[i][sl])
+                ops.ddim_step_(xs, x0_raw, x0s, coef[i])
                 if traj is not None:
-                    traj[i].copy_(x0)
+                    traj[i][sl].copy_(x0s)
 
-        st = {"key": den.key(), "x": x, "x0": x0, "traj": traj, "loop": _GraphLoop(body, dev)}
+        st = {"key": den.key(), "x": x, "x0": x0, "traj": traj, "loop": _GraphLoop(lambda: chains.run(chain), dev)}
         cache[key] = st
         return st
 
@@ -162,8 +207,10 @@ class DDIMSampler:
 class ColdSampler:
     """Cold de-pixelation sampler: start from constant-colour images, x <- clamp(f(x, t)) for t = S..1."""
 
-    def __init__(self, model, device, use_graph: bool = True, steps: Optional[int] = None):
+    def __init__(self, model, device, use_graph: bool = True, steps: Optional[int] = None,
+                 streams: Optional[int] = None):
         self.model = model
+        self.streams = streams
         self.device = torch.device(device)
         self.steps = steps or cold_steps(model.img_size[1])
         self.use_graph = use_graph and self.device.type == "cuda"
@@ -171,7 +218,8 @@ class ColdSampler:
         self.C = model.in_chans
 
     def _state(self, N: int):
-        key = ("cold", N, self.steps, str(self.device))
+        nstreams = self.streams or default_streams(N, self.device)
+        key = ("cold", N, self.steps, str(self.device), nstreams)
         den = _Denoiser(self.model, self.device)
         cache = _cache(self.model)
         st = cache.get(key)
@@ -182,14 +230,16 @@ class ColdSampler:
         ts = list(range(self.steps, 0, -1))
         tt = torch.tensor(ts, dtype=torch.int64, device=dev).unsqueeze(1).expand(-1, N).contiguous()
         traj = torch.zeros(len(ts), N, self.C, self.H, self.W, device=dev)
+        chains = _Chains(N, dev, nstreams)
 
-        def body():
+        def chain(sl):
+            xs = x[sl]
             for i in range(len(ts)):
-                x0_raw = den(x, tt[i])
-                torch.clamp(x0_raw, -1.0, 1.0, out=x)
-                traj[i].copy_(x)
+                x0_raw = den(xs, tt[i][sl])
+                torch.clamp(x0_raw, -1.0, 1.0, out=xs)
+                traj[i][sl].copy_(xs)
 
-        st = {"key": den.key(), "x": x, "traj": traj, "loop": _GraphLoop(body, dev)}
+        st = {"key": den.key(), "x": x, "traj": traj, "loop": _GraphLoop(lambda: chains.run(chain), dev)}
         cache[key] = st
         return st
 
@@ -239,15 +289,17 @@ def ddim_from_starts(model, x: torch.Tensor, starts: Sequence[int], k: int, devi
     active = torch.stack([(st >= t) for t in ts]).view(len(ts), B, 1, 1, 1)
     coef = torch.tensor([ddim_coefficients(T, t, k) for t in ts], dtype=torch.float32, device=device)
     den = _Denoiser(model, device)
+    chains = _Chains(B, device, default_streams(B, device))
 
-    def body():
+    def chain(sl):
+        xs, x0s = x[sl], x0[sl]
         for i in range(len(ts)):
-            x0_raw = den(x, tt[i])
-            xn, x0c = ops.ddim_step(x, x0_raw, coef[i])
-            torch.where(active[i], xn, x, out=x)
-            torch.where(active[i], x0c, x0, out=x0)
+            x0_raw = den(xs, tt[i][sl])
+            xn, x0c = ops.ddim_step(xs, x0_raw, coef[i])
+            torch.where(active[i][sl], xn, xs, out=xs)
+            torch.where(active[i][sl], x0c, x0s, out=x0s)
 
-    _GraphLoop(body, device).run(use_graph and device.type == "cuda")
+    _GraphLoop(lambda: chains.run(chain), device).run(use_graph and device.type == "cuda")
     return x0
 
 

@@ -21,6 +21,7 @@ Reference dropout placement: ``ViT.py:82,101,103,127,137,175``.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Callable, Dict, Iterator, List, Optional
 
@@ -29,6 +30,7 @@ import torch
 from .. import ops
 
 SITE_EMBED = 1
+FUSE_LN = os.environ.get("DDIM_COLD_FUSE_LN", "0") == "1"  # residual GEMM + LayerNorm in one kernel
 
 
 def block_sites(i: int):
@@ -170,20 +172,38 @@ class ViTProgram:
                                          c.patch)
         x = x.view(M, D)
         S = Saved(t=t, patches=patches) if save else None
+        # Each residual GEMM carries the LayerNorm that follows it (proj -> norm2,
+        # fc2 -> next block's norm1 / the final norm): ops.linear_residual_ln_fwd.
+        # Off by default: the row-panel kernel concentrates the epilogue traffic on
+        # M/32 workgroups and measured slower than GEMM + LayerNorm (15.5 vs 9.3 us
+        # at M=2080; profiles/README.md).  DDIM_COLD_FUSE_LN=1 enables it.
+        fuse = FUSE_LN and ops.residual_ln_fusable(D, D) and ops.residual_ln_fusable(D, c.hidden)
+        l1, m1, r1 = ops.layernorm_fwd(x, P.blocks[0].n1w, P.blocks[0].n1b, c.eps)
+        L = len(P.blocks)
         for i, bp in enumerate(P.blocks):
             sa, sp, sd1, sf1, sf2, sd2 = block_sites(i)
             x0 = x
-            l1, m1, r1 = ops.layernorm_fwd(x0, bp.n1w, bp.n1b, c.eps)
             qkv = ops.qkv_fwd(l1, bp.qkv_w, bp.qkv_b, B, N, c.heads)
             o, lse = ops.attn_fwd(qkv, c.scale, rng, sa, ad)
             o = o.view(M, D)
-            x1 = ops.linear_residual_fwd(o, bp.proj_w, bp.proj_b, x0, N, rng, sp, pd, sd1, dpr[i])
-            l2, m2, r2 = ops.layernorm_fwd(x1, bp.n2w, bp.n2b, c.eps)
+            if fuse:
+                x1, l2, m2, r2 = ops.linear_residual_ln_fwd(o, bp.proj_w, bp.proj_b, x0, bp.n2w, bp.n2b, c.eps, N,
+                                                            rng, sp, pd, sd1, dpr[i])
+            else:
+                x1 = ops.linear_residual_fwd(o, bp.proj_w, bp.proj_b, x0, N, rng, sp, pd, sd1, dpr[i])
+                l2, m2, r2 = ops.layernorm_fwd(x1, bp.n2w, bp.n2b, c.eps)
             u, h = ops.linear_gelu_fwd(l2, bp.fc1_w, bp.fc1_b, rng, sf1, pd)
-            x = ops.linear_residual_fwd(h, bp.fc2_w, bp.fc2_b, x1, N, rng, sf2, pd, sd2, dpr[i])
+            nw, nb = (P.blocks[i + 1].n1w, P.blocks[i + 1].n1b) if i + 1 < L else (P.nw, P.nb)
+            if fuse:
+                x, ln_n, m_n, r_n = ops.linear_residual_ln_fwd(h, bp.fc2_w, bp.fc2_b, x1, nw, nb, c.eps, N, rng, sf2,
+                                                               pd, sd2, dpr[i])
+            else:
+                x = ops.linear_residual_fwd(h, bp.fc2_w, bp.fc2_b, x1, N, rng, sf2, pd, sd2, dpr[i])
+                ln_n, m_n, r_n = ops.layernorm_fwd(x, nw, nb, c.eps)
             if save:
                 S.blocks.append((x0, l1, m1, r1, qkv, o, lse, x1, l2, m2, r2, u, h))
-        lf, mf, rf = ops.layernorm_fwd(x, P.nw, P.nb, c.eps)
+            l1, m1, r1 = ln_n, m_n, r_n
+        lf, mf, rf = l1, m1, r1
         out = ops.head_fwd(lf, P.head_w, P.head_b, B, c.chans, c.img_h, c.img_w, c.patch)
         if save:
             S.xL, S.lf, S.mf, S.rf = x, lf, mf, rf

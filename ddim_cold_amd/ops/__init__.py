@@ -68,6 +68,21 @@ def linear_residual_fwd(a, w, b, x, N: int, rng, site_drop: int, p_drop: float, 
     return ref.linear_residual_fwd(a, w, b, x, N, rng, site_drop, p_drop, site_dp, p_dp)
 
 
+def residual_ln_fusable(D: int, K: int) -> bool:
+    """Widths the row-panel GEMM + LayerNorm kernel is instantiated for (csrc/gemm_ln.hip)."""
+    return D in (256, 384, 512) and K % 64 == 0
+
+
+def linear_residual_ln_fwd(a, w, b, x, gamma, beta, eps: float, N: int, rng, site_drop: int, p_drop: float,
+                           site_dp: int, p_dp: float):
+    """(x_new, ln(x_new) bf16, mean, rstd) with x_new = x + DropPath(Dropout(a w^T + b)):
+    the residual GEMM and the following LayerNorm in one launch."""
+    if _hip(a):
+        return _ops().linear_residual_ln_fwd(a, w, b, x, gamma, beta, float(eps), N, rng, site_drop,
+                                             float(p_drop), site_dp, float(p_dp))
+    return ref.linear_residual_ln_fwd(a, w, b, x, gamma, beta, eps, N, rng, site_drop, p_drop, site_dp, p_dp)
+
+
 def linear_gelu_fwd(a, w, b, rng, site: int, p: float):
     if _hip(a):
         return _ops().linear_gelu_fwd(a, w, b, rng, site, float(p))

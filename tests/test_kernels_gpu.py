@@ -183,6 +183,23 @@ def test_wgrad(M, Nout, K):
     close(db1, db2, 2e-2, 1e-4, "db")
 
 
+@pytest.mark.parametrize("M,D,K,N,pd,pdp", [(2080, 384, 384, 65, 0.1, 0.1), (130, 256, 256, 65, 0.0, 0.0),
+                                             (4160, 384, 384, 65, 0.0, 0.0), (100, 512, 128, 50, 0.2, 0.3)])
+def test_linear_residual_ln(M, D, K, N, pd, pdp):
+    """Row-panel GEMM + residual + LayerNorm epilogue == residual GEMM then LayerNorm."""
+    a, w = bf(M, K), bf(D, K, scale=0.05)
+    b = torch.randn(D, device=DEV)
+    x = torch.randn(M, D, device=DEV)
+    g, be = torch.randn(D, device=DEV), torch.randn(D, device=DEV)
+    r = rng()
+    xn, ln, mu, rs = ops.linear_residual_ln_fwd(a, w, b, x, g, be, 1e-5, N, r, 3, pd, 4, pdp)
+    xr, lr, mr, rr = ref.linear_residual_ln_fwd(a, w, b, x, g, be, 1e-5, N, r, 3, pd, 4, pdp)
+    close(xn, xr, 2e-3, 2e-3, "x")
+    close(mu, mr, 1e-3, 1e-3, "mean")
+    close(rs, rr, 1e-3, 1e-3, "rstd")
+    close(ln.float(), lr.float(), 3e-2, 2e-2, "ln")
+
+
 @pytest.mark.parametrize("big", [True, False])
 def test_linear_wgrad_group(big):
     """Grouped launch == per-problem reference (unsplit read-add-write and split atomic paths)."""

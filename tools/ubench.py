@@ -45,6 +45,12 @@ def main():
     res["hipblaslt mm 384x384x2080 (wgrad)"] = t(lambda: torch.matmul(a.t(), a))
     res["resid p=0.1"] = t(lambda: ops.linear_residual_fwd(a, w, b, x, N, r, 3, 0.1, 4, 0.1))
     res["resid p=0"] = t(lambda: ops.linear_residual_fwd(a, w, b, x, N, r, 3, 0.0, 4, 0.0))
+    g0, b0 = torch.randn(D, device=dev), torch.randn(D, device=dev)
+    res["resid+LN fused p=0.1"] = t(lambda: ops.linear_residual_ln_fwd(a, w, b, x, g0, b0, 1e-5, N, r, 3, 0.1, 4, 0.1))
+    a2, x2 = bf(2 * M, D), torch.randn(2 * M, D, device=dev)
+    res["resid+LN fused M=4160 p=0"] = t(lambda: ops.linear_residual_ln_fwd(a2, w, b, x2, g0, b0, 1e-5, N, r, 3, 0., 4, 0.))
+    res["resid M=4160 p=0"] = t(lambda: ops.linear_residual_fwd(a2, w, b, x2, N, r, 3, 0.0, 4, 0.0))
+    res["ln fwd M=4160"] = t(lambda: ops.layernorm_fwd(x2, g0, b0))
     res["qkv"] = t(lambda: ops.qkv_fwd(a, w3, b3, B, N, H))
     res["plain bf16 out 2080x1152 (qkv shape, EPI_BF16 via dgrad-free path)"] = t(lambda: ops.linear_dgrad(a, w3.t().contiguous(), False))
     k0 = torch.zeros(M, 0, device=dev, dtype=torch.bfloat16)
