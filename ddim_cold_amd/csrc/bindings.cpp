@@ -101,6 +101,26 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_fwd(Tensor x, Tensor gamma, Tensor 
   return {y, mean, rstd};
 }
 
+// y = a w^T (+ b): plain nn.Linear, bf16 or fp32 output
+Tensor linear_fwd(Tensor a, Tensor w, c10::optional<Tensor> b, bool out_fp32) {
+  CHECK_IN(a, BF16); CHECK_IN(w, BF16);
+  const c10::DeviceGuard guard(a.device());
+  const int K = a.size(-1);
+  auto a2 = a.view({-1, K});
+  check_linear(a2, w, K);
+  const int M = a2.size(0), Dout = w.size(0);
+  auto out = at::empty({M, Dout}, a.options().dtype(out_fp32 ? at::kFloat : at::kBFloat16));
+  GemmArgs g = nt_args(a2, w);
+  g.C = out.data_ptr(); g.ldc = Dout;
+  if (b.has_value() && b->defined()) {
+    CHECK_IN((*b), F32);
+    TORCH_CHECK(b->numel() == Dout, "bias shape");
+    g.bias = b->data_ptr<float>();
+  }
+  gemm_nt(g, out_fp32 ? EPI_F32 : EPI_BF16, cur_stream());
+  return out;
+}
+
 Tensor qkv_fwd(Tensor a, Tensor w, Tensor b, int64_t B, int64_t N, int64_t H) {
   CHECK_IN(a, BF16); CHECK_IN(w, BF16); CHECK_IN(b, F32);
   const c10::DeviceGuard guard(a.device());
@@ -548,6 +568,7 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("linear_residual_fwd(Tensor a, Tensor w, Tensor b, Tensor x, int N, Tensor rng, int site_drop, "
         "float p_drop, int site_dp, float p_dp) -> Tensor");
   m.def("linear_gelu_fwd(Tensor a, Tensor w, Tensor b, Tensor rng, int site, float p) -> (Tensor, Tensor)");
+  m.def("linear_fwd(Tensor a, Tensor w, Tensor? b, bool out_fp32) -> Tensor");
   m.def("linear_residual_ln_fwd(Tensor a, Tensor w, Tensor b, Tensor x, Tensor gamma, Tensor beta, float eps, "
         "int N, Tensor rng, int site_drop, float p_drop, int site_dp, float p_dp) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("head_fwd(Tensor a, Tensor w, Tensor b, int B, int C, int H, int W, int patch) -> Tensor");
@@ -590,6 +611,7 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("linear_dgrad", &linear_dgrad);
   m.impl("linear_dgrad_gelu", &linear_dgrad_gelu);
   m.impl("linear_wgrad", &linear_wgrad);
+  m.impl("linear_fwd", &linear_fwd);
   m.impl("linear_residual_ln_fwd", &linear_residual_ln_fwd);
   m.impl("linear_wgrad_group", &linear_wgrad_group);
   m.impl("layernorm_bwd", &layernorm_bwd);

@@ -71,6 +71,11 @@ struct WgradGroup {
   int n;
 };
 
+static bool getenv_flag(const char* name) {
+  const char* e = getenv(name);
+  return e && e[0] == '1';
+}
+
 static bool dma_disabled() {
   static const bool off = [] {
     const char* e = getenv("DDIM_COLD_GEMM_NO_DMA");
@@ -323,125 +328,148 @@ __device__ __forceinline__ f32x4 ld4bf(const bf16* p) {
 // Vector epilogue: the MFMA accumulator layout (lane = column, 4 registers =
 // 4 rows) is transposed inside lane quads so each lane owns 4 CONSECUTIVE
 // columns of one row; every load/store of the epilogue is then one 8-/16-byte
-// vector access instead of four 2-/4-byte scalar ones (the scalar form made the
-// epilogue as long as the whole main loop).  Requires N % 4 == 0 and output
-// columns contiguous in groups of 4 (all epilogues except HEAD).
+// vector access instead of four 2-/4-byte scalar ones.  Requires N % 4 == 0 and
+// output columns contiguous in groups of 4 (all epilogues except HEAD).
+//
+// Split in two so the epilogue's global loads (bias, residual, saved
+// pre-activation, embeddings, accumulate target) can be issued BEFORE the main
+// loop (`prefetch`) and land while the MFMAs run: at these sizes a GEMM is a
+// chain of ~3 dependent memory round trips and this removes one of them.
 template <int EPI, int FM, int FN>
-__device__ __forceinline__ void run_epilogue_vec(const GemmParams& p, const f32x4 (&acc_in)[FM][FN], int mb, int nb,
-                                                 int g, int li) {
-  constexpr bool PRE = EPI == EPI_RESID || EPI == EPI_DGELU || EPI == EPI_EMBED || EPI == EPI_ACC;
-  const int x = li & 3, q = li >> 2;
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = quad_transpose(acc_in[i][j], x);
+struct VecEpi {
+  static constexpr bool PRE = EPI == EPI_RESID || EPI == EPI_DGELU || EPI == EPI_EMBED || EPI == EPI_ACC;
   RowInfo rows[FM];
   long long cols[FN];
   bool colok[FN];
   f32x4 colb[FN];
-  const bool has_bias = (EPI != EPI_ATOMIC) && (EPI != EPI_ACC) && p.bias != nullptr;
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int n = nb + j * 16 + 4 * q;
-    colok[j] = n < p.N;
-    cols[j] = epi_col<EPI>(p, n);
-    colb[j] = (has_bias && colok[j]) ? ld4(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    const int m = mb + i * 16 + 4 * g + x;
-    rows[i] = epi_row<EPI>(p, m < p.M ? m : p.M - 1);
-    if (m >= p.M) rows[i].off = -1;
-  }
-  // phase 1: every element load of the epilogue
   f32x4 pre[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
+
+  __device__ __forceinline__ void prefetch(const GemmParams& p, int mb, int nb, int g, int li) {
+    const int x = li & 3, q = li >> 2;
+    const bool has_bias = (EPI != EPI_ATOMIC) && (EPI != EPI_ACC) && p.bias != nullptr;
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (PRE && rows[i].off >= 0 && colok[j]) {
-        const int n = nb + j * 16 + 4 * q;
-        if (EPI == EPI_RESID) v = ld4(p.res + rows[i].off + n);
-        if (EPI == EPI_DGELU) v = ld4bf(p.aux + rows[i].off + n);
-        if (EPI == EPI_ACC) v = ld4(reinterpret_cast<const float*>(p.C) + rows[i].off + n);
-        if (EPI == EPI_EMBED) {
-          const int m = mb + i * 16 + 4 * g + x;
-          const int patch = m - rows[i].b * p.tokens;
-          v = ld4(p.pos + (size_t)(patch + 1) * p.emb_dim + n) +
-              ld4(p.temb + (size_t)p.tsteps[rows[i].b] * p.emb_dim + n);
-        }
-      }
-      pre[i][j] = v;
+      const int n = nb + j * 16 + 4 * q;
+      colok[j] = n < p.N;
+      cols[j] = epi_col<EPI>(p, n);
+      colb[j] = (has_bias && colok[j]) ? ld4(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
-  // phase 2: compute + vector stores
-  uint32_t salt_drop = 0, salt_dp = 0;
-  if (p.thr_drop) salt_drop = site_salt(p.rng, p.site_drop);
-  if (p.thr_dp) salt_dp = site_salt(p.rng, p.site_dp);
 #pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    if (rows[i].off < 0) continue;
-    const bool keep_row = (EPI == EPI_RESID && p.thr_dp) ? dropout_keep(salt_dp, (uint32_t)rows[i].b, p.thr_dp) : true;
+    for (int i = 0; i < FM; ++i) {
+      const int m = mb + i * 16 + 4 * g + x;
+      rows[i] = epi_row<EPI>(p, m < p.M ? m : p.M - 1);
+      if (m >= p.M) rows[i].off = -1;
+    }
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      if (!colok[j]) continue;
-      const long long idx = rows[i].off + cols[j];
-      f32x4 v = acc[i][j] + colb[j];
-      if (EPI == EPI_BF16 || EPI == EPI_QKV) {
-        st4bf(reinterpret_cast<bf16*>(p.C) + idx, v);
-      } else if (EPI == EPI_F32) {
-        st4(reinterpret_cast<float*>(p.C) + idx, v);
-      } else if (EPI == EPI_ATOMIC) {
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) atomicAdd(reinterpret_cast<float*>(p.C) + idx + c, v[c]);
-      } else if (EPI == EPI_ACC) {
-        st4(reinterpret_cast<float*>(p.C) + idx, pre[i][j] + v);
-      } else if (EPI == EPI_RESID) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          float e = v[c];
-          if (p.thr_drop) e = dropout_keep(salt_drop, (uint32_t)(idx + c), p.thr_drop) ? e * p.scale_drop : 0.f;
-          if (p.thr_dp) e = keep_row ? e * p.scale_dp : 0.f;
-          v[c] = pre[i][j][c] + e;
+      for (int j = 0; j < FN; ++j) {
+        f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (PRE && rows[i].off >= 0 && colok[j]) {
+          const int n = nb + j * 16 + 4 * q;
+          if (EPI == EPI_RESID) v = ld4(p.res + rows[i].off + n);
+          if (EPI == EPI_DGELU) v = ld4bf(p.aux + rows[i].off + n);
+          if (EPI == EPI_ACC) v = ld4(reinterpret_cast<const float*>(p.C) + rows[i].off + n);
+          if (EPI == EPI_EMBED) {
+            const int m = mb + i * 16 + 4 * g + x;
+            const int patch = m - rows[i].b * p.tokens;
+            v = ld4(p.pos + (size_t)(patch + 1) * p.emb_dim + n) +
+                ld4(p.temb + (size_t)p.tsteps[rows[i].b] * p.emb_dim + n);
+          }
         }
-        st4(reinterpret_cast<float*>(p.C) + idx, v);
-      } else if (EPI == EPI_GELU) {
-        st4bf(reinterpret_cast<bf16*>(p.C) + idx, v);
-        f32x4 h;
+        pre[i][j] = v;
+      }
+  }
+
+  __device__ __forceinline__ void finish(const GemmParams& p, const f32x4 (&acc_in)[FM][FN], int li) {
+    const int x = li & 3;
+    f32x4 acc[FM][FN];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          float e = gelu_f(v[c]);
-          if (p.thr_drop) e = dropout_keep(salt_drop, (uint32_t)(idx + c), p.thr_drop) ? e * p.scale_drop : 0.f;
-          h[c] = e;
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = quad_transpose(acc_in[i][j], x);
+    uint32_t salt_drop = 0, salt_dp = 0;
+    if (p.thr_drop) salt_drop = site_salt(p.rng, p.site_drop);
+    if (p.thr_dp) salt_dp = site_salt(p.rng, p.site_dp);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      if (rows[i].off < 0) continue;
+      const bool keep_row =
+          (EPI == EPI_RESID && p.thr_dp) ? dropout_keep(salt_dp, (uint32_t)rows[i].b, p.thr_dp) : true;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        if (!colok[j]) continue;
+        const long long idx = rows[i].off + cols[j];
+        f32x4 v = acc[i][j] + colb[j];
+        if (EPI == EPI_BF16 || EPI == EPI_QKV) {
+          st4bf(reinterpret_cast<bf16*>(p.C) + idx, v);
+        } else if (EPI == EPI_F32) {
+          st4(reinterpret_cast<float*>(p.C) + idx, v);
+        } else if (EPI == EPI_ATOMIC) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) atomicAdd(reinterpret_cast<float*>(p.C) + idx + c, v[c]);
+        } else if (EPI == EPI_ACC) {
+          st4(reinterpret_cast<float*>(p.C) + idx, pre[i][j] + v);
+        } else if (EPI == EPI_RESID) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            float e = v[c];
+            if (p.thr_drop) e = dropout_keep(salt_drop, (uint32_t)(idx + c), p.thr_drop) ? e * p.scale_drop : 0.f;
+            if (p.thr_dp) e = keep_row ? e * p.scale_dp : 0.f;
+            v[c] = pre[i][j][c] + e;
+          }
+          st4(reinterpret_cast<float*>(p.C) + idx, v);
+        } else if (EPI == EPI_GELU) {
+          st4bf(reinterpret_cast<bf16*>(p.C) + idx, v);
+          f32x4 h;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            float e = gelu_f(v[c]);
+            if (p.thr_drop) e = dropout_keep(salt_drop, (uint32_t)(idx + c), p.thr_drop) ? e * p.scale_drop : 0.f;
+            h[c] = e;
+          }
+          st4bf(reinterpret_cast<bf16*>(p.C2) + idx, h);
+        } else if (EPI == EPI_DGELU) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            float e = v[c];
+            if (p.thr_drop) e = dropout_keep(salt_drop, (uint32_t)(idx + c), p.thr_drop) ? e * p.scale_drop : 0.f;
+            v[c] = e * gelu_grad_f(pre[i][j][c]);
+          }
+          st4bf(reinterpret_cast<bf16*>(p.C) + idx, v);
+        } else if (EPI == EPI_EMBED) {
+          v += pre[i][j];
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if (p.thr_drop) v[c] = dropout_keep(salt_drop, (uint32_t)(idx + c), p.thr_drop) ? v[c] * p.scale_drop : 0.f;
+          st4(reinterpret_cast<float*>(p.C) + idx, v);
         }
-        st4bf(reinterpret_cast<bf16*>(p.C2) + idx, h);
-      } else if (EPI == EPI_DGELU) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          float e = v[c];
-          if (p.thr_drop) e = dropout_keep(salt_drop, (uint32_t)(idx + c), p.thr_drop) ? e * p.scale_drop : 0.f;
-          v[c] = e * gelu_grad_f(pre[i][j][c]);
-        }
-        st4bf(reinterpret_cast<bf16*>(p.C) + idx, v);
-      } else if (EPI == EPI_EMBED) {
-        v += pre[i][j];
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (p.thr_drop) v[c] = dropout_keep(salt_drop, (uint32_t)(idx + c), p.thr_drop) ? v[c] * p.scale_drop : 0.f;
-        st4(reinterpret_cast<float*>(p.C) + idx, v);
       }
     }
   }
+};
+
+template <int EPI, int FM, int FN>
+__device__ __forceinline__ void run_epilogue_vec(const GemmParams& p, const f32x4 (&acc)[FM][FN], int mb, int nb,
+                                                 int g, int li) {
+  VecEpi<EPI, FM, FN> ep;
+  ep.prefetch(p, mb, nb, g, li);
+  ep.finish(p, acc, li);
 }
+
+// epilogues that take the quad-transposed vector path
+template <int EPI>
+struct UsesVecEpi {
+  // HEAD: columns not contiguous.  ATOMIC: in the accumulator layout one atomic
+  // instruction covers 4 rows x 64 B; after the quad transpose it would touch 16
+  // rows (4x the cache lines per instruction) - measured 10% slower per step.
+  static constexpr bool value = EPI != EPI_HEAD && EPI != EPI_ATOMIC;
+};
 
 template <int EPI, int FM, int FN>
 __device__ __forceinline__ void run_epilogue(const GemmParams& p, const f32x4 (&acc)[FM][FN], int mb, int nb,
                                              int g, int li) {
-  // HEAD: columns not contiguous.  ATOMIC: in the accumulator layout one atomic
-  // instruction covers 4 rows x 64 B; after the quad transpose it would touch 16
-  // rows (4x the cache lines per instruction) - measured 10% slower per step.
-  if (EPI == EPI_HEAD || EPI == EPI_ATOMIC || p.debug == 3) run_epilogue_scalar<EPI, FM, FN>(p, acc, mb, nb, g, li);
+  if (!UsesVecEpi<EPI>::value || p.debug == 3) run_epilogue_scalar<EPI, FM, FN>(p, acc, mb, nb, g, li);
   else run_epilogue_vec<EPI, FM, FN>(p, acc, mb, nb, g, li);
 }
 
@@ -619,6 +647,10 @@ __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int t
       oa.issue(smem + s * STAGE, kt0 + s, wave);
       ob.issue(smem + s * STAGE + OA::BYTES, kt0 + s, wave);
     }
+  // epilogue operands in flight behind the first operand tiles (see VecEpi)
+  constexpr bool VEC = UsesVecEpi<EPI>::value;
+  VecEpi<EPI, FM, FN> ep;
+  if (VEC && p.debug != 3) ep.prefetch(p, m0 + wm * TM, n0 + wn * TN, g, li);
 
   for (int kt = 0; kt < (p.debug == 2 ? 0 : nk); ++kt) {
     const int rem = min(S - 2, nk - 1 - kt);
@@ -690,7 +722,8 @@ __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int t
       }
   }
 
-  run_epilogue<EPI, FM, FN>(p, acc, m0 + wm * TM, n0 + wn * TN, g, li);
+  if (VEC && p.debug != 3) ep.finish(p, acc, li);
+  else run_epilogue_scalar<EPI, FM, FN>(p, acc, m0 + wm * TM, n0 + wn * TN, g, li);
 }
 
 template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EPI, int S>
@@ -722,14 +755,21 @@ __global__ __launch_bounds__(256) void gemm_wgrad_group_kernel(WgradGroup gp) {
 
 template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EPI>
 static void launch_dma(GemmParams p, int splits, hipStream_t stream) {
-  constexpr int S = 4;
-  constexpr int lds = S * (BM * 128 + BN * 128);
   const int total_kt = (p.K + BK - 1) / BK;
   p.ktiles_per_split = (total_kt + splits - 1) / splits;
   splits = (total_kt + p.ktiles_per_split - 1) / p.ktiles_per_split;
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, WM, WN, AT, BT, EPI, S>), dim3(tiles, 1, splits), dim3(256), lds,
-                     stream, p);
+  // keep every workgroup of the grid co-resident (one round): a 4-stage ring
+  // allows 160 KiB / (4 x stage) workgroups per CU, a 3-stage ring 4/3 of that
+  constexpr int stage = BM * 128 + BN * 128;
+  constexpr int per_cu4 = (160 * 1024) / (4 * stage);
+  static const bool force_s4 = getenv_flag("DDIM_COLD_GEMM_S4");
+  if (tiles * splits > 256 * per_cu4 && p.ktiles_per_split <= 8 && !force_s4)
+    hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, WM, WN, AT, BT, EPI, 3>), dim3(tiles, 1, splits), dim3(256),
+                       3 * stage, stream, p);
+  else
+    hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, WM, WN, AT, BT, EPI, 4>), dim3(tiles, 1, splits), dim3(256),
+                       4 * stage, stream, p);
 }
 
 template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EPI>
@@ -780,7 +820,9 @@ static void launch_auto(GemmParams p, int splits, hipStream_t stream) {
 // Explicit instantiations: hipcc 7.2 intermittently fails to emit host launch
 // stubs for implicitly instantiated kernel templates (undefined
 // __device_stub__ at dlopen); build.py also checks the .so for that.
-#define DC_INST_DMA(BM, AT, BT, EPI) template __global__ void gemm_dma_kernel<BM, 64, 2, 2, AT, BT, EPI, 4>(GemmParams);
+#define DC_INST_DMA(BM, AT, BT, EPI)                                                   \
+  template __global__ void gemm_dma_kernel<BM, 64, 2, 2, AT, BT, EPI, 4>(GemmParams); \
+  template __global__ void gemm_dma_kernel<BM, 64, 2, 2, AT, BT, EPI, 3>(GemmParams);
 #define DC_INST_DMA2(AT, BT, EPI) DC_INST_DMA(64, AT, BT, EPI) DC_INST_DMA(32, AT, BT, EPI)
 DC_INST_DMA2(false, false, EPI_BF16)
 DC_INST_DMA2(false, false, EPI_F32)

@@ -50,6 +50,13 @@ def layernorm_fwd(x, gamma, beta, eps: float = 1e-5):
     return ref.layernorm_fwd(x, gamma, beta, eps)
 
 
+def linear_fwd(a, w, b=None, out_fp32: bool = False):
+    """Plain ``a @ w.T + b`` on the MFMA GEMM (bf16 or fp32 output)."""
+    if _hip(a):
+        return _ops().linear_fwd(a, w, b, bool(out_fp32))
+    return ref.linear_fwd(a, w, b, out_fp32)
+
+
 def qkv_fwd(a, w, b, B: int, N: int, H: int):
     if _hip(a):
         return _ops().qkv_fwd(a, w, b, B, N, H)

@@ -137,6 +137,13 @@ def layernorm_fwd(x, gamma, beta, eps: float = 1e-5):
     return bf16(y), mean, rstd
 
 
+def linear_fwd(a, w, b, out_fp32: bool):
+    y = _mm(a.reshape(-1, a.shape[-1]), w)
+    if b is not None:
+        y = y + b.float()
+    return y if out_fp32 else bf16(y)
+
+
 def qkv_fwd(a, w, b, B: int, N: int, H: int):
     """QKV projection written head-major: [3, B, H, N, hd] bf16."""
     D3 = w.shape[0]

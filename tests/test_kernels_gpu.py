@@ -183,6 +183,16 @@ def test_wgrad(M, Nout, K):
     close(db1, db2, 2e-2, 1e-4, "db")
 
 
+@pytest.mark.parametrize("M,N,K,f32,bias", [(2080, 1152, 384, False, True), (100, 192, 64, True, False),
+                                            (4160, 384, 384, True, True)])
+def test_linear_fwd(M, N, K, f32, bias):
+    a, w = bf(M, K), bf(N, K, scale=0.05)
+    b = torch.randn(N, device=DEV) if bias else None
+    y = ops.linear_fwd(a, w, b, f32)
+    yr = ref.linear_fwd(a, w, b, f32)
+    close(y.float(), yr.float(), 3e-2, 2e-2, "y")
+
+
 @pytest.mark.parametrize("M,D,K,N,pd,pdp", [(2080, 384, 384, 65, 0.1, 0.1), (130, 256, 256, 65, 0.0, 0.0),
                                              (4160, 384, 384, 65, 0.0, 0.0), (100, 512, 128, 50, 0.2, 0.3)])
 def test_linear_residual_ln(M, D, K, N, pd, pdp):

@@ -15,6 +15,9 @@ dqkv = bf(M, 3 * D)
 res = {
  "resid": t(lambda: ops.linear_residual_fwd(a, w, b, x, N, r, 3, 0.0, 4, 0.0)),
  "qkv": t(lambda: ops.qkv_fwd(a, w3, b3, B, N, H)),
+ "plain nt bf16 2080x1152": t(lambda: ops.linear_fwd(a, w3, b3, False)),
+ "plain nt f32 2080x1152": t(lambda: ops.linear_fwd(a, w3, b3, True)),
+ "plain nt bf16 2080x384": t(lambda: ops.linear_fwd(a, w, b, False)),
  "gelu": t(lambda: ops.linear_gelu_fwd(a, w, b, r, 5, 0.0)),
  "dgrad f32": t(lambda: ops.linear_dgrad(a, w, True)),
  "dgrad qkv": t(lambda: ops.linear_dgrad(dqkv, w3, True)),
