@@ -787,32 +787,80 @@ static void launch_cfg(GemmParams p, int splits, hipStream_t stream) {
 
 // (tag dispatch instead of `if constexpr`: hipcc 7.2 silently drops the host
 // stub of a kernel template first referenced inside an if-constexpr branch)
+// tile configs: 0 = 32x64, 1 = 64x64, 2 = 128x64, 3 = 128x128 (4 waves, 2x2)
 template <bool AT, bool BT, int EPI>
-struct DmaSmall {
-  static void launch(GemmParams p, int splits, hipStream_t stream, bool big) {
-    if (big) launch_dma<64, 64, 2, 2, AT, BT, EPI>(p, splits, stream);
-    else launch_dma<32, 64, 2, 2, AT, BT, EPI>(p, splits, stream);
+struct DmaTiles {
+  static void launch(GemmParams p, int splits, hipStream_t stream, int cfg) {
+    switch (cfg) {
+      case 0: launch_dma<32, 64, 2, 2, AT, BT, EPI>(p, splits, stream); break;
+      case 1: launch_dma<64, 64, 2, 2, AT, BT, EPI>(p, splits, stream); break;
+      case 2: launch_dma<128, 64, 2, 2, AT, BT, EPI>(p, splits, stream); break;
+      default: launch_dma<128, 128, 2, 2, AT, BT, EPI>(p, splits, stream); break;
+    }
+  }
+};
+template <int EPI>
+struct DmaTiles<false, true, EPI> {  // transposed B (dgrad): BN = 64
+  static void launch(GemmParams p, int splits, hipStream_t stream, int cfg) {
+    switch (cfg) {
+      case 0: launch_dma<32, 64, 2, 2, false, true, EPI>(p, splits, stream); break;
+      case 1: launch_dma<64, 64, 2, 2, false, true, EPI>(p, splits, stream); break;
+      default: launch_dma<128, 64, 2, 2, false, true, EPI>(p, splits, stream); break;
+    }
   }
 };
 template <bool BT, int EPI>
-struct DmaSmall<true, BT, EPI> {
-  static void launch(GemmParams p, int splits, hipStream_t stream, bool) {
+struct DmaTiles<true, BT, EPI> {  // transposed A (wgrad): 64x64
+  static void launch(GemmParams p, int splits, hipStream_t stream, int) {
     launch_dma<64, 64, 2, 2, true, BT, EPI>(p, splits, stream);
   }
 };
 
-// tile choice: 64x64 when it yields >= ~1 wave of workgroups per CU, else 32x64.
-// The LDS-DMA ring kernel needs K % 64 == 0 for k-contiguous operands (transposed
-// operands get zero rows past K from the buffer bounds check).
+// Tile choice: 64x64 when that alone gives ~1 workgroup per CU, else 32x64.
+// A cost model "operand bytes per CU" (one CU ingests ~80 GB/s of operand tiles,
+// tools/ub_stream.hip) that picks 128x64 / 128x128 for the big shapes measured
+// SLOWER everywhere (qkv 2080x1152x384: 11.9 us at 128x128 vs 7.5 at 64x64;
+// train step -10%): more, smaller workgroups hide latency better than fewer
+// bytes help.  It stays available as DDIM_COLD_GEMM_TILE_MODEL=1, and
+// DDIM_COLD_GEMM_TILE=0..3 forces a tile.  The LDS-DMA ring needs K % 64 == 0
+// for k-contiguous operands (transposed operands get zero rows past K from the
+// buffer bounds check).
+static int pick_tiles(int M, int N, int K, int splits, bool at, bool bt) {
+  static const int forced = [] {
+    const char* e = getenv("DDIM_COLD_GEMM_TILE");
+    return e ? atoi(e) : -1;
+  }();
+  static const bool model = getenv_flag("DDIM_COLD_GEMM_TILE_MODEL");
+  if (at) return 1;
+  if (forced >= 0) return bt && forced > 2 ? 2 : forced;
+  if (!model) return ((M + 63) / 64) * ((N + 63) / 64) * splits >= 240 ? 1 : 0;
+  const int nk = ((K + 63) / 64 + splits - 1) / splits;
+  const int bms[4] = {32, 64, 128, 128}, bns[4] = {64, 64, 64, 128};
+  const int ncfg = bt ? 3 : 4;
+  int best = 0;
+  long long best_cost = -1, best_tiles = 0;
+  for (int c = 0; c < ncfg; ++c) {
+    const long long tiles = (long long)((M + bms[c] - 1) / bms[c]) * ((N + bns[c] - 1) / bns[c]) * splits;
+    const long long per_cu = (tiles + 255) / 256;
+    const long long cost = per_cu * (bms[c] + bns[c]) * 128LL * nk;
+    if (best_cost < 0 || cost < best_cost || (cost == best_cost && tiles > best_tiles)) {
+      best = c;
+      best_cost = cost;
+      best_tiles = tiles;
+    }
+  }
+  return best;
+}
+
 template <bool AT, bool BT, int EPI>
 static void launch_auto(GemmParams p, int splits, hipStream_t stream) {
-  const int tiles64 = ((p.M + 63) / 64) * ((p.N + 63) / 64);
-  const bool big = tiles64 * splits >= 240 || AT;
   const bool dma_ok = (AT || BT || p.K % 64 == 0) && (AT || p.K % 64 == 0) && !dma_disabled();
   if (dma_ok) {
-    DmaSmall<AT, BT, EPI>::launch(p, splits, stream, big);
+    DmaTiles<AT, BT, EPI>::launch(p, splits, stream, pick_tiles(p.M, p.N, p.K, splits, AT, BT));
     return;
   }
+  const int tiles64 = ((p.M + 63) / 64) * ((p.N + 63) / 64);
+  const bool big = tiles64 * splits >= 240 || AT;
   if (big) launch_cfg<64, 64, 2, 2, AT, BT, EPI>(p, splits, stream);
   else launch_cfg<32, 64, 2, 2, AT, BT, EPI>(p, splits, stream);
 }
@@ -820,17 +868,20 @@ static void launch_auto(GemmParams p, int splits, hipStream_t stream) {
 // Explicit instantiations: hipcc 7.2 intermittently fails to emit host launch
 // stubs for implicitly instantiated kernel templates (undefined
 // __device_stub__ at dlopen); build.py also checks the .so for that.
-#define DC_INST_DMA(BM, AT, BT, EPI)                                                   \
-  template __global__ void gemm_dma_kernel<BM, 64, 2, 2, AT, BT, EPI, 4>(GemmParams); \
-  template __global__ void gemm_dma_kernel<BM, 64, 2, 2, AT, BT, EPI, 3>(GemmParams);
-#define DC_INST_DMA2(AT, BT, EPI) DC_INST_DMA(64, AT, BT, EPI) DC_INST_DMA(32, AT, BT, EPI)
-DC_INST_DMA2(false, false, EPI_BF16)
-DC_INST_DMA2(false, false, EPI_F32)
-DC_INST_DMA2(false, false, EPI_QKV)
-DC_INST_DMA2(false, false, EPI_RESID)
-DC_INST_DMA2(false, false, EPI_GELU)
-DC_INST_DMA2(false, false, EPI_HEAD)
-DC_INST_DMA2(false, false, EPI_EMBED)
+#define DC_INST_DMAT(BM, BN, AT, BT, EPI)                                               \
+  template __global__ void gemm_dma_kernel<BM, BN, 2, 2, AT, BT, EPI, 4>(GemmParams); \
+  template __global__ void gemm_dma_kernel<BM, BN, 2, 2, AT, BT, EPI, 3>(GemmParams);
+#define DC_INST_DMA(BM, AT, BT, EPI) DC_INST_DMAT(BM, 64, AT, BT, EPI)
+#define DC_INST_DMA2(AT, BT, EPI) \
+  DC_INST_DMA(64, AT, BT, EPI) DC_INST_DMA(32, AT, BT, EPI) DC_INST_DMA(128, AT, BT, EPI)
+#define DC_INST_DMA3(EPI) DC_INST_DMA2(false, false, EPI) DC_INST_DMAT(128, 128, false, false, EPI)
+DC_INST_DMA3(EPI_BF16)
+DC_INST_DMA3(EPI_F32)
+DC_INST_DMA3(EPI_QKV)
+DC_INST_DMA3(EPI_RESID)
+DC_INST_DMA3(EPI_GELU)
+DC_INST_DMA3(EPI_HEAD)
+DC_INST_DMA3(EPI_EMBED)
 DC_INST_DMA2(false, true, EPI_BF16)
 DC_INST_DMA2(false, true, EPI_F32)
 DC_INST_DMA2(false, true, EPI_DGELU)
