@@ -168,6 +168,172 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
   }
 }
 
+// ============================================================================ forward, long sequences
+// Flash forward v2 (N > 128): 128 queries per workgroup (4 waves x 32 queries =
+// two 16-query MFMA column tiles per wave, so every K / V fragment read from
+// LDS feeds two MFMAs), KV tiles of 64 keys DOUBLE-BUFFERED: the next tile's
+// global loads are issued before the current tile's MFMAs and land in
+// registers, then go to the other LDS buffer — one barrier per tile and no
+// exposed load latency.  Dropout is a template flag (branch-free softmax).
+template <int HD>
+struct KvStage {  // one 64-row K tile + one 64-row V tile, register-staged
+  static constexpr int CPR = HD / 8;
+  static constexpr int PER = 64 * CPR / 256;  // 16-B chunks per thread per matrix
+  u32x4 k[PER], v[PER];
+  __device__ __forceinline__ void load(const bf16* __restrict__ kb, const bf16* __restrict__ vb, int r0, int N) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = threadIdx.x + i * 256;
+      const int r = c / CPR, cc = c - r * CPR;
+      const int rr = r0 + r < N ? r0 + r : N - 1;
+      const u32x4 z = {0u, 0u, 0u, 0u};
+      const u32x4 kv = *reinterpret_cast<const u32x4*>(kb + (size_t)rr * HD + cc * 8);
+      const u32x4 vv = *reinterpret_cast<const u32x4*>(vb + (size_t)rr * HD + cc * 8);
+      k[i] = r0 + r < N ? kv : z;
+      v[i] = r0 + r < N ? vv : z;
+    }
+  }
+  __device__ __forceinline__ void store(char* kl, char* vl) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = threadIdx.x + i * 256;
+      const int r = c / CPR, cc = c - r * CPR;
+      *reinterpret_cast<u32x4*>(kl + r * AC<HD>::S + cc * 16) = k[i];
+      *reinterpret_cast<u32x4*>(vl + r * AC<HD>::S + cc * 16) = v[i];
+    }
+  }
+};
+
+template <int HD, bool DROP>
+__global__ __launch_bounds__(256) void attn_fwd_flash2_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                              float* __restrict__ lse, int B, int H, int N,
+                                                              float scale, const int64_t* __restrict__ rng, int site,
+                                                              uint32_t thr, float dsc) {
+  using C = AC<HD>;
+  __shared__ __attribute__((aligned(16))) char lds[4 * C::TILE];  // [buf][K | V]
+  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const size_t mat = (size_t)N * HD;
+  const bf16* qb = qkv + (size_t)bh * mat;
+  const bf16* kb = qkv + ((size_t)B * H + bh) * mat;
+  const bf16* vb = qkv + ((size_t)2 * B * H + bh) * mat;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
+  const int qbase = blockIdx.x * 128 + wave * 32;
+  const float sl2 = scale * LOG2E;
+  const uint32_t salt = DROP ? site_salt(rng, site) : 0u;
+
+  KvStage<HD> stg;
+  stg.load(kb, vb, 0, N);
+  bf16x8 qf[2][C::KS];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) qf[u][s] = frag_glb<HD>(qb, qbase + 16 * u + li, N, s, g);
+  stg.store(lds, lds + C::TILE);
+  __syncthreads();
+
+  f32x4 o[2][C::DT];
+  float m_run[2], l_run[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    m_run[u] = -INFINITY;
+    l_run[u] = 0.f;
+#pragma unroll
+    for (int d = 0; d < C::DT; ++d) o[u][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int ntiles = (N + 63) / 64;
+  for (int it = 0; it < ntiles; ++it) {
+    const int kv0 = it * 64;
+    const bool more = it + 1 < ntiles;
+    if (more) stg.load(kb, vb, kv0 + 64, N);  // lands during this tile's MFMAs
+    const char* Kl = lds + (it & 1) * 2 * C::TILE;
+    const char* Vl = Kl + C::TILE;
+    f32x4 st[2][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      st[0][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      st[1][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) {
+        const bf16x8 kf = frag_row<HD>(Kl, 16 * t + li, s, g);
+        st[0][t] = mfma16(kf, qf[0][s], st[0][t]);
+        st[1][t] = mfma16(kf, qf[1][s], st[1][t]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = qbase + 16 * u + li;
+      float mt = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = (kv0 + 16 * t + 4 * g + r) < N ? st[u][t][r] * sl2 : -INFINITY;
+          st[u][t][r] = v;
+          mt = fmaxf(mt, v);
+        }
+      mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float m_new = fmaxf(m_run[u], mt);
+      const float alpha = exp2f(m_run[u] - m_new);
+      const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * N + kv0);
+      float ls = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float pv = exp2f(st[u][t][r] - m_new);
+          ls += pv;
+          if (DROP) pv = dropout_keep(salt, rowidx + (uint32_t)(16 * t + 4 * g + r), thr) ? pv * dsc : 0.f;
+          st[u][t][r] = pv;
+        }
+      ls += __shfl_xor(ls, 16, 64);
+      ls += __shfl_xor(ls, 32, 64);
+      l_run[u] = l_run[u] * alpha + ls;
+      m_run[u] = m_new;
+#pragma unroll
+      for (int d = 0; d < C::DT; ++d) o[u][d] *= alpha;
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 pb0 = pack8(st[0][2 * s2], st[0][2 * s2 + 1]);
+      const bf16x8 pb1 = pack8(st[1][2 * s2], st[1][2 * s2 + 1]);
+#pragma unroll
+      for (int d = 0; d < C::DT; ++d) {
+        const bf16x8 vf = frag_t<C::S>(Vl, 16 * d, s2, lane);
+        o[0][d] = mfma16(vf, pb0, o[0][d]);
+        o[1][d] = mfma16(vf, pb1, o[1][d]);
+      }
+    }
+    if (more) stg.store(lds + ((it + 1) & 1) * 2 * C::TILE, lds + ((it + 1) & 1) * 2 * C::TILE + C::TILE);
+    __syncthreads();
+  }
+  const int D = H * HD;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int q = qbase + 16 * u + li;
+    if (q < N) {
+      const float inv = 1.f / l_run[u];
+      bf16* orow = out + ((size_t)b * N + q) * D + h * HD;
+#pragma unroll
+      for (int d = 0; d < C::DT; ++d) {
+        bf16x4 v;
+        v[0] = f2bf(o[u][d][0] * inv); v[1] = f2bf(o[u][d][1] * inv);
+        v[2] = f2bf(o[u][d][2] * inv); v[3] = f2bf(o[u][d][3] * inv);
+        *reinterpret_cast<bf16x4*>(orow + 16 * d + 4 * g) = v;
+      }
+      if (g == 0) lse[(size_t)bh * N + q] = (m_run[u] + log2f(l_run[u])) * LN2;
+    }
+  }
+}
+template __global__ void attn_fwd_flash2_kernel<32, true>(const bf16*, bf16*, float*, int, int, int, float,
+                                                          const int64_t*, int, uint32_t, float);
+template __global__ void attn_fwd_flash2_kernel<32, false>(const bf16*, bf16*, float*, int, int, int, float,
+                                                           const int64_t*, int, uint32_t, float);
+template __global__ void attn_fwd_flash2_kernel<64, true>(const bf16*, bf16*, float*, int, int, int, float,
+                                                          const int64_t*, int, uint32_t, float);
+template __global__ void attn_fwd_flash2_kernel<64, false>(const bf16*, bf16*, float*, int, int, int, float,
+                                                           const int64_t*, int, uint32_t, float);
+
 // ============================================================================ backward: dQ (+delta)
 template <int HD>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ qkv,
@@ -696,7 +862,21 @@ void attn_fwd_launch(const void* qkv, void* o, float* lse, int B, int H, int N, 
     else dispatch_short<64>(false, nullptr, q, nullptr, lse, nullptr, out, B, H, N, scale, rng, site, thr, dsc, stream);
     return;
   }
-  if (hd == 32)
+  static const bool v1 = [] {
+    const char* e = getenv("DDIM_COLD_ATTN_FLASH_V1");
+    return e && e[0] == '1';
+  }();
+  // v2 has half the workgroups of v1: measured better from ~600 tokens (N=626:
+  // 63 vs 71 us without dropout), worse at N=257 with dropout (25 vs 22 us)
+  const bool use_v2 = !v1 && N >= 384;
+  const dim3 grid2((N + 127) / 128, B * H);
+  if (use_v2 && hd == 32) {
+    if (thr) hipLaunchKernelGGL((attn_fwd_flash2_kernel<32, true>), grid2, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc);
+    else hipLaunchKernelGGL((attn_fwd_flash2_kernel<32, false>), grid2, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc);
+  } else if (use_v2 && hd == 64) {
+    if (thr) hipLaunchKernelGGL((attn_fwd_flash2_kernel<64, true>), grid2, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc);
+    else hipLaunchKernelGGL((attn_fwd_flash2_kernel<64, false>), grid2, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc);
+  } else if (hd == 32)
     hipLaunchKernelGGL(attn_fwd_kernel<32>, grid, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc);
   else if (hd == 64)
     hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc);

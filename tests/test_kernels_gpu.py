@@ -238,7 +238,9 @@ def test_linear_wgrad_group(big):
                                         (1, 2, 17, 32, 0.0), (1, 6, 626, 64, 0.0), (2, 3, 130, 64, 0.2),
                                         # short-sequence path (N <= 128): every padded size, both head dims
                                         (2, 3, 100, 64, 0.1), (3, 5, 128, 32, 0.1), (2, 2, 64, 64, 0.0),
-                                        (2, 4, 32, 32, 0.1), (2, 4, 33, 64, 0.0), (8, 4, 97, 32, 0.0)])
+                                        (2, 4, 32, 32, 0.1), (2, 4, 33, 64, 0.0), (8, 4, 97, 32, 0.0),
+                                        # flash v2 (N >= 384)
+                                        (1, 2, 400, 32, 0.1), (2, 3, 513, 64, 0.0)])
 def test_attention_fwd_bwd(B, H, N, hd, p):
     qkv = bf(3, B, H, N, hd)
     r = rng()

@@ -1,0 +1,21 @@
+"""Attention fwd/bwd timings on the model shapes (graph-timed)."""
+import os, sys, json
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from ddim_cold_amd import ops
+from tools.ubench import t
+dev = "cuda"
+r = torch.tensor([1, 2], dtype=torch.int64, device=dev)
+res = {}
+for (B, H, N, hd) in [(32, 12, 65, 32), (32, 4, 257, 64), (32, 6, 626, 64)]:
+    qkv = (torch.randn(3, B, H, N, hd, device=dev) * 0.5).to(torch.bfloat16)
+    do = (torch.randn(B, N, H * hd, device=dev)).to(torch.bfloat16)
+    for p in (0.0, 0.1):
+        o, lse = ops.attn_fwd(qkv, hd ** -0.5, r, 5, p)
+        f = t(lambda: ops.attn_fwd(qkv, hd ** -0.5, r, 5, p), reps=20)
+        b = t(lambda: ops.attn_bwd(do, qkv, o, lse, hd ** -0.5, r, 5, p), reps=20)
+        fl = 4 * B * H * N * N * hd
+        res[f"B{B} H{H} N{N} hd{hd} p{p}"] = {"fwd_us": round(f, 1), "bwd_us": round(b, 1),
+                                             "fwd_TFLOPs": round(fl / f / 1e6, 1), "bwd_TFLOPs": round(2.5 * fl / b / 1e6, 1)}
+for k, v in res.items():
+    print(k, v)
