@@ -168,7 +168,7 @@ def main():
                                 f"{model.img_size[0]}x{model.img_size[1]})", "global_batch": args.batch * n,
                        "per_gpu_batch": args.batch, "seq_len": model.num_tokens, "parallelism": f"dp{n}",
                        "graph": not args.no_graph, "bucket_blocks": args.bucket_blocks,
-                       "allreduce": ("none" if not engine.segmented else
+                       "allreduce": ("none" if not engine.segmented else "eager" if dev.type != "cuda" else
                                      "segmented" if (args.segmented_comm or getattr(engine, "_graph_comm_failed", False))
                                      else "captured-in-graph"),
                        "optimizer": "AdamW(wd=0.05)+clip1.0+cosine", "final_loss": round(loss, 5)},
