@@ -212,7 +212,7 @@ class ViTProgram:
     # ------------------------------------------------------------------ backward
     def backward_iter(self, P: ModelTensors, G: ModelTensors, S: Saved, dtok: torch.Tensor, rng: torch.Tensor,
                       training: bool = True, wgrad: Optional[Callable] = None,
-                      ln_ws: Optional[torch.Tensor] = None) -> Iterator[int]:
+                      ln_ws: Optional[torch.Tensor] = None, wgrad_stream=None) -> Iterator[int]:
         """Hand-written backward; yields the block index after each block's grads
         are issued (L-1 first, then ..., 0) and -1 after the embedding grads.
 
@@ -229,7 +229,7 @@ class ViTProgram:
             return None if ln_ws is None else ln_ws[k]
         batch = None
         if wgrad is None:
-            batch = wgrad = ops.WgradBatch()
+            batch = wgrad = ops.WgradBatch(wgrad_stream)
 
         def flush():
             if batch is not None:
@@ -278,6 +278,8 @@ class ViTProgram:
         wgrad(gpatch, S.patches, G.pe_w, G.pe_b)
         flush()
         keep.append(gpatch)
+        if batch is not None:
+            keep.append(batch.keep)
         self._keep = keep  # holds side-stream operands alive until the caller joins
         yield -1
 

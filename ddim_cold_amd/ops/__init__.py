@@ -147,17 +147,33 @@ def linear_wgrad_group(jobs):
 
 
 class WgradBatch:
-    """Collects weight-gradient GEMMs and issues them as one grouped launch on ``flush``."""
+    """Collects weight-gradient GEMMs and issues them as one grouped launch on ``flush``.
 
-    def __init__(self):
+    With ``stream`` the launch goes to that stream (forked from the current one),
+    so it can run beside the rest of the backward; the caller joins the stream
+    before anything reads the gradients.  Operands are kept referenced in
+    ``self.keep`` until the caller drops the batch.
+    """
+
+    def __init__(self, stream=None):
         self.jobs = []
+        self.stream = stream
+        self.keep = []
 
     def __call__(self, dy, x, dw, db):
         self.jobs.append((dy, x, dw, db))
 
     def flush(self):
         jobs, self.jobs = self.jobs, []
-        linear_wgrad_group(jobs)
+        if not jobs:
+            return
+        if self.stream is None:
+            linear_wgrad_group(jobs)
+            return
+        self.stream.wait_stream(torch.cuda.current_stream(self.stream.device))
+        with torch.cuda.stream(self.stream):
+            linear_wgrad_group(jobs)
+        self.keep.append(jobs)
 
 
 LN_REPLICAS = 16  # csrc/layernorm.hip LN_REPLICAS

@@ -57,7 +57,11 @@ class EngineConfig:
     use_graph: bool = True
     graph_warmup: int = 3     # eager steps before capture
     bucket_blocks: int = 2    # transformer blocks per all-reduce bucket
-    wgrad_stream: bool = False  # measured: side-stream wgrad overlap is slower on MI355X (1.79 vs 1.53 ms)
+    # grouped weight-gradient launches on a second stream (a parallel graph
+    # branch), joined only by the all-reduce and the optimizer.  Measured on
+    # MI355X: 28.2k img/s with vs 33.1k without (graph branches of these
+    # latency-bound kernels interfere more than they overlap) -> off.
+    wgrad_stream: bool = False
     seed: int = 42
     loss_beta: float = 1.0
     ema_decay: float = 0.99
@@ -109,6 +113,7 @@ class TrainEngine:
         self._graphs: Optional[List[torch.cuda.CUDAGraph]] = None
         self._eager_steps = 0
         self.batch_fn: Optional[Callable] = None
+        self._segment_capture = False
         self._static = None
         self.steps_done = 0
         if self.world > 1:
@@ -223,12 +228,6 @@ class TrainEngine:
         self.batch_fn = fn
         self._graphs = None
 
-    def _wgrad(self, dy, x, dw, db):
-        cur = torch.cuda.current_stream(self.device)
-        self.side.wait_stream(cur)
-        with torch.cuda.stream(self.side):
-            ops.linear_wgrad(dy, x, dw, db)
-
     def _join_side(self):
         if self.side is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.side)
@@ -243,23 +242,25 @@ class TrainEngine:
         del out
         ln_lo = 0
         for i in self.prog.backward_iter(self.param_tensors, self.grad_tensors, S, dtok, self.rng, True,
-                                         wgrad=self._wgrad if self.side is not None else None, ln_ws=self.ln_ws):
+                                         ln_ws=self.ln_ws, wgrad_stream=self.side):
             if i in self.bucket_after and (self.segmented or i == -1):
                 hi = self.ln_done_at[i]
                 if hi > ln_lo:
                     ops.replica_reduce_(self.ln_ws[ln_lo:hi], None if self.ln_ptrs is None else self.ln_ptrs[ln_lo:hi],
                                         2 * c.dim, dsts=self.ln_dsts[ln_lo:hi])
                     ln_lo = hi
-                self._join_side()
+                if self._segment_capture:
+                    self._join_side()  # a captured segment must rejoin every stream it forked
                 yield ("bucket", self.bucket_after[i])
         S = None
-        self.prog._keep = None
+        self._join_side()  # all weight gradients final before the norm / optimizer
         # optimizer: grads are SUM-reduced over ranks -> average via grad_scale
         gs = 1.0 / self.world
         ops.sqnorm(self.flat_g, self.sqnorm, gs)
         ops.adamw_step(self.flat_p, self.flat_g, self.flat_m, self.flat_v, self.flat_pb, self.sqnorm,
                        self.step_ctr, self.hyper, gs)
         ops.advance_counters(self.step_ctr, self.rng, self.sqnorm)
+        self.prog._keep = None
         yield ("done", -1)
 
     def _allreduce(self, k: int):
@@ -268,6 +269,8 @@ class TrainEngine:
         views = [self.flat_g[a:b] for a, b in self.bucket_ranges[k]]
         if self.comm is not None:
             self.comm.wait_stream(torch.cuda.current_stream(self.device))
+            if self.side is not None:  # the bucket's weight gradients come from the side stream
+                self.comm.wait_stream(self.side)
             with torch.cuda.stream(self.comm):
                 for v in views:
                     dist.all_reduce(v, group=self.pg)
@@ -319,11 +322,15 @@ class TrainEngine:
                         pass
             graphs.append(g)
         else:
-            for _ in range(nseg):
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=pool):
-                    next(gen)
-                graphs.append(g)
+            self._segment_capture = True
+            try:
+                for _ in range(nseg):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, pool=pool):
+                        next(gen)
+                    graphs.append(g)
+            finally:
+                self._segment_capture = False
         self._graphs = graphs
 
     def _replay(self):
