@@ -234,6 +234,35 @@ Tensor head_fwd(Tensor a, Tensor w, Tensor b, int64_t B, int64_t C, int64_t H, i
   return img;
 }
 
+// Head GEMM with the sampler step fused into its unpatchify epilogue:
+//   mode 1 (DDIM): x0 = clamp(head(a), -1, 1); x <- sqrt(a_tk) x0 + sqrt(1-a_tk) (x - sqrt(a_t) x0)/sqrt(1-a_t)
+//                  in place, x0 written to x0_out; coef = device row {sqrt a_t, sqrt 1-a_t, sqrt a_tk, sqrt 1-a_tk}
+//   mode 2 (cold): x <- clamp(head(a), -1, 1)
+void head_step_(Tensor a, Tensor w, Tensor b, Tensor x, c10::optional<Tensor> x0_out, c10::optional<Tensor> coef,
+                int64_t patch, int64_t mode) {
+  CHECK_IN(a, BF16); CHECK_IN(w, BF16); CHECK_IN(b, F32); CHECK_IN(x, F32);
+  const c10::DeviceGuard guard(a.device());
+  TORCH_CHECK(x.dim() == 4, "x must be [B, C, H, W]");
+  const int B = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int K = a.size(-1);
+  auto a2 = a.view({-1, K});
+  check_linear(a2, w, K);
+  const int N = (H / patch) * (W / patch) + 1;
+  TORCH_CHECK(a2.size(0) == B * N && w.size(0) == C * patch * patch && b.numel() == w.size(0), "head shapes");
+  TORCH_CHECK(mode == 1 || mode == 2, "head_step_: mode 1 (ddim) or 2 (clamp)");
+  GemmArgs g = nt_args(a2, w);
+  g.C = x.data_ptr(); g.bias = b.data_ptr<float>();
+  g.tokens = N; g.batch = B; g.chans = C; g.img_h = H; g.img_w = W; g.patch = patch;
+  g.head_mode = (int)mode;
+  if (mode == 1) {
+    TORCH_CHECK(x0_out.has_value() && coef.has_value(), "ddim mode needs x0_out and coef");
+    CHECK_IN((*x0_out), F32); CHECK_IN((*coef), F32);
+    TORCH_CHECK(x0_out->sizes() == x.sizes() && coef->numel() >= 4, "x0_out / coef shapes");
+    g.res = x.data_ptr<float>(); g.C2 = x0_out->data_ptr(); g.coef = coef->data_ptr<float>();
+  }
+  gemm_nt(g, EPI_HEAD, cur_stream());
+}
+
 std::tuple<Tensor, Tensor> smooth_l1_fwd_bwd(Tensor pred, Tensor target, int64_t N, int64_t patch, double beta) {
   CHECK_IN(pred, F32); CHECK_IN(target, F32);
   const c10::DeviceGuard guard(pred.device());
@@ -572,6 +601,8 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("linear_residual_ln_fwd(Tensor a, Tensor w, Tensor b, Tensor x, Tensor gamma, Tensor beta, float eps, "
         "int N, Tensor rng, int site_drop, float p_drop, int site_dp, float p_dp) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("head_fwd(Tensor a, Tensor w, Tensor b, int B, int C, int H, int W, int patch) -> Tensor");
+  m.def("head_step_(Tensor a, Tensor w, Tensor b, Tensor(a!) x, Tensor(b!)? x0_out, Tensor? coef, int patch, "
+        "int mode) -> ()");
   m.def("smooth_l1_fwd_bwd(Tensor pred, Tensor target, int N, int patch, float beta) -> (Tensor, Tensor)");
   m.def("img_to_tokgrad(Tensor dimg, int N, int patch) -> Tensor");
   m.def("linear_dgrad(Tensor dy, Tensor w, bool out_fp32) -> Tensor");
@@ -611,6 +642,7 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("linear_dgrad", &linear_dgrad);
   m.impl("linear_dgrad_gelu", &linear_dgrad_gelu);
   m.impl("linear_wgrad", &linear_wgrad);
+  m.impl("head_step_", &head_step_);
   m.impl("linear_fwd", &linear_fwd);
   m.impl("linear_residual_ln_fwd", &linear_residual_ln_fwd);
   m.impl("linear_wgrad_group", &linear_wgrad_group);

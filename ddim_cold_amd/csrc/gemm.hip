@@ -59,6 +59,8 @@ struct GemmParams {
   const int64_t* tsteps;
   int emb_dim;
   int ktiles_per_split;
+  const float* coef;     // HEAD mode 1: {sqrt a_t, sqrt(1-a_t), sqrt a_tk, sqrt(1-a_tk)} (device)
+  int head_mode;         // HEAD: 0 image, 1 fused DDIM step (res = x_t in, C = x_next, C2 = x0), 2 clamp
   int debug;  // profiling aid (DDIM_COLD_GEMM_DEBUG): 1 = skip the epilogue, 2 = skip the main loop,
               // 3 = scalar (untransposed) epilogue
 };
@@ -193,7 +195,7 @@ __device__ __forceinline__ long long epi_col(const GemmParams& p, int n) {
 
 template <int EPI>
 __device__ __forceinline__ void epilogue(const GemmParams& p, long long idx, int rb, float v, float pre,
-                                         uint32_t salt_drop, uint32_t salt_dp) {
+                                         uint32_t salt_drop, uint32_t salt_dp, const f32x4& cf) {
   if (EPI == EPI_BF16) {
     reinterpret_cast<bf16*>(p.C)[idx] = f2bf(v);
   } else if (EPI == EPI_F32) {
@@ -217,7 +219,20 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, long long idx, int
     if (p.thr_drop) v = dropout_keep(salt_drop, (uint32_t)idx, p.thr_drop) ? v * p.scale_drop : 0.f;
     reinterpret_cast<bf16*>(p.C)[idx] = f2bf(v * gelu_grad_f(pre));
   } else if (EPI == EPI_HEAD) {
-    reinterpret_cast<float*>(p.C)[idx] = v;
+    if (p.head_mode == 0) {
+      reinterpret_cast<float*>(p.C)[idx] = v;
+    } else {
+      // the sampler's x0-hat clamp (ViT.py:229, ViT_draft2drawing.py:280), and for
+      // mode 1 the whole DDIM update (ViT.py:230-234) with x_t preloaded in `pre`
+      const float x0 = fminf(fmaxf(v, -1.f), 1.f);
+      if (p.head_mode == 2) {
+        reinterpret_cast<float*>(p.C)[idx] = x0;
+      } else {
+        const float eps = (pre - cf[0] * x0) / cf[1];
+        reinterpret_cast<float*>(p.C)[idx] = cf[2] * x0 + cf[3] * eps;
+        reinterpret_cast<float*>(p.C2)[idx] = x0;
+      }
+    }
   } else if (EPI == EPI_EMBED) {
     v += pre;
     if (p.thr_drop) v = dropout_keep(salt_drop, (uint32_t)idx, p.thr_drop) ? v * p.scale_drop : 0.f;
@@ -231,6 +246,7 @@ template <int EPI, int FM, int FN>
 __device__ __forceinline__ void run_epilogue_scalar(const GemmParams& p, const f32x4 (&acc)[FM][FN], int mb, int nb,
                                              int g, int li) {
   constexpr bool ELEM = EPI == EPI_RESID || EPI == EPI_DGELU || EPI == EPI_EMBED || EPI == EPI_ACC;
+  const bool head_ddim = EPI == EPI_HEAD && p.head_mode == 1;
   RowInfo rows[FM][4];
   long long cols[FN];
   bool colok[FN];
@@ -260,6 +276,7 @@ __device__ __forceinline__ void run_epilogue_scalar(const GemmParams& p, const f
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float v = 0.f;
+        if (head_ddim && rows[i][r].off >= 0 && colok[j]) v = p.res[rows[i][r].off + cols[j]];
         if (ELEM && rows[i][r].off >= 0 && colok[j]) {
           const int n = nb + j * 16 + li;
           if (EPI == EPI_RESID) v = p.res[rows[i][r].off + n];
@@ -277,6 +294,8 @@ __device__ __forceinline__ void run_epilogue_scalar(const GemmParams& p, const f
   uint32_t salt_drop = 0, salt_dp = 0;
   if (p.thr_drop) salt_drop = site_salt(p.rng, p.site_drop);
   if (p.thr_dp) salt_dp = site_salt(p.rng, p.site_dp);
+  f32x4 cf = f32x4{0.f, 1.f, 0.f, 0.f};
+  if (head_ddim) cf = f32x4{p.coef[0], p.coef[1], p.coef[2], p.coef[3]};
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -285,7 +304,7 @@ __device__ __forceinline__ void run_epilogue_scalar(const GemmParams& p, const f
       for (int r = 0; r < 4; ++r)
         if (rows[i][r].off >= 0 && colok[j])
           epilogue<EPI>(p, rows[i][r].off + cols[j], rows[i][r].b, acc[i][j][r] + colb[j], pre[i][j][r], salt_drop,
-                        salt_dp);
+                        salt_dp, cf);
 }
 
 
@@ -919,6 +938,7 @@ static GemmParams base_params(const GemmArgs& a) {
   p.tokens = a.tokens; p.batch = a.batch; p.heads = a.heads; p.hd = a.hd;
   p.chans = a.chans; p.img_h = a.img_h; p.img_w = a.img_w; p.patch = a.patch;
   p.pos = a.pos; p.temb = a.temb; p.tsteps = a.tsteps; p.emb_dim = a.emb_dim;
+  p.coef = a.coef; p.head_mode = a.head_mode;
   return p;
 }
 

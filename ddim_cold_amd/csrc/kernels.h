@@ -39,6 +39,8 @@ struct GemmArgs {
   const float* temb = nullptr;
   const int64_t* tsteps = nullptr;
   int emb_dim = 0;
+  const float* coef = nullptr;  // EPI_HEAD head_mode 1
+  int head_mode = 0;            // EPI_HEAD: 0 image, 1 fused DDIM step, 2 clamp
 };
 
 void gemm_nt(const GemmArgs& a, int epi, hipStream_t stream);

@@ -62,6 +62,18 @@ class _Denoiser:
             return ("engine", id(eng))
         return tuple((p.data_ptr(), p._version) for p in self.model.parameters())
 
+    def step_(self, x, t, mode: int, x0_out=None, coef=None):
+        """In-place sampler step on ``x`` with the update fused into the head GEMM
+        (mode 1: DDIM with ``coef``, x0-hat into ``x0_out``; mode 2: clamp)."""
+        if self.fused and FUSED_HEAD:
+            self.prog.forward(self.P, x, t, self.rng, False, save=False, head_step=(mode, x0_out, coef))
+            return
+        x0_raw = self(x, t)
+        if mode == 2:
+            torch.clamp(x0_raw, -1.0, 1.0, out=x)
+        else:
+            ops.ddim_step_(x, x0_raw, x0_out, coef)
+
     def __call__(self, x, t):
         if self.fused:
             out, _ = self.prog.forward(self.P, x, t, self.rng, False, save=False)
@@ -72,6 +84,9 @@ class _Denoiser:
             return self.model.forward_reference(x, t)
         finally:
             self.model.train(was)
+
+
+FUSED_HEAD = os.environ.get("DDIM_COLD_SAMPLER_FUSED_HEAD", "1") == "1"
 
 
 def default_streams(N: int, device) -> int:
@@ -168,8 +183,7 @@ class DDIMSampler:
         def chain(sl):
             xs, x0s = x[sl], x0[sl]
             for i in range(len(self.ts)):
-                x0_raw = den(xs, tt[i][sl])
-                ops.ddim_step_(xs, x0_raw, x0s, coef[i])
+                den.step_(xs, tt[i][sl], 1, x0s, coef[i])  # forward + clamp + DDIM update, one head epilogue
                 if traj is not None:
                     traj[i][sl].copy_(x0s)
 
@@ -235,8 +249,7 @@ class ColdSampler:
         def chain(sl):
             xs = x[sl]
             for i in range(len(ts)):
-                x0_raw = den(xs, tt[i][sl])
-                torch.clamp(x0_raw, -1.0, 1.0, out=xs)
+                den.step_(xs, tt[i][sl], 2)  # forward + clamp in the head epilogue
                 traj[i][sl].copy_(xs)
 
         st = {"key": den.key(), "x": x, "traj": traj, "loop": _GraphLoop(lambda: chains.run(chain), dev)}

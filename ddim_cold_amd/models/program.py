@@ -161,7 +161,10 @@ class ViTProgram:
 
     # ------------------------------------------------------------------ forward
     def forward(self, P: ModelTensors, img: torch.Tensor, t: torch.Tensor, rng: torch.Tensor, training: bool,
-                save: bool = True):
+                save: bool = True, head_step=None):
+        """``head_step = (mode, x0_out, coef)`` fuses the sampler update into the head
+        GEMM (``ops.head_step_``): ``img`` (the current x_t) is updated in place and
+        returned; mode 1 = DDIM step, mode 2 = clamp (cold sampler)."""
         c = self.cfg
         B = img.shape[0]
         N, D, M = c.tokens, c.dim, B * c.tokens
@@ -204,6 +207,10 @@ class ViTProgram:
                 S.blocks.append((x0, l1, m1, r1, qkv, o, lse, x1, l2, m2, r2, u, h))
             l1, m1, r1 = ln_n, m_n, r_n
         lf, mf, rf = l1, m1, r1
+        if head_step is not None:
+            mode, x0_out, coef = head_step
+            ops.head_step_(lf, P.head_w, P.head_b, img, x0_out, coef, c.patch, mode)
+            return img, S
         out = ops.head_fwd(lf, P.head_w, P.head_b, B, c.chans, c.img_h, c.img_w, c.patch)
         if save:
             S.xL, S.lf, S.mf, S.rf = x, lf, mf, rf

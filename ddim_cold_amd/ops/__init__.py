@@ -96,6 +96,22 @@ def linear_gelu_fwd(a, w, b, rng, site: int, p: float):
     return ref.linear_gelu_fwd(a, w, b, rng, site, p)
 
 
+def head_step_(a, w, b, x, x0_out, coef, patch: int, mode: int):
+    """Head GEMM + sampler step in its epilogue (in place on ``x``): mode 1 = clamp +
+    DDIM update (``x0_out`` gets the clamped x0-hat; ``coef`` a device row of
+    ``ddim_coefficients``), mode 2 = clamp only (cold sampler)."""
+    if _hip(a):
+        return _ops().head_step_(a, w, b, x, x0_out, coef, patch, mode)
+    B, C, H, W = x.shape
+    x0_raw = ref.head_fwd(a, w, b, B, C, H, W, patch)
+    if mode == 2:
+        x.copy_(torch.clamp(x0_raw, -1.0, 1.0))
+        return
+    xn, x0 = ref.ddim_step(x, x0_raw, [float(v) for v in coef.tolist()[:4]])
+    x.copy_(xn)
+    x0_out.copy_(x0)
+
+
 def head_fwd(a, w, b, B: int, C: int, H: int, W: int, patch: int):
     if _hip(a):
         return _ops().head_fwd(a, w, b, B, C, H, W, patch)

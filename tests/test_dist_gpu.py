@@ -14,5 +14,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_rccl_engine_paths_match_single_process():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "dist_parity.py")], capture_output=True,
                        text=True, timeout=600, env=dict(os.environ, PYTHONPATH=ROOT))
-    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    assert r.returncode == 0, "\n".join(l for l in (r.stdout + r.stderr).splitlines()
+                                        if not l.startswith("[W") and "amdgpu.ids" not in l)[-3000:]
     assert "dist-parity ok" in r.stdout

@@ -134,6 +134,29 @@ def test_head_fwd(B, C, H, W, p, D):
     close(img, imgr, 1e-3, 1e-3, "head")
 
 
+@pytest.mark.parametrize("mode", [1, 2])
+def test_head_step_fused_sampler_update(mode):
+    """Head GEMM with the DDIM update (mode 1) / clamp (mode 2) in its epilogue."""
+    from ddim_cold_amd.diffusion.schedule import ddim_coefficients
+    B, C, H, W, p, D = 4, 3, 64, 64, 8, 384
+    N = (H // p) * (W // p) + 1
+    a = bf(B * N, D)
+    w = bf(C * p * p, D, scale=0.05)
+    b = torch.randn(C * p * p, device=DEV)
+    x = torch.randn(B, C, H, W, device=DEV)
+    coef = torch.tensor(ddim_coefficients(2000, 999, 20), device=DEV)
+    x0 = torch.empty_like(x)
+    xk = x.clone()
+    ops.head_step_(a, w, b, xk, x0 if mode == 1 else None, coef if mode == 1 else None, p, mode)
+    raw = ref.head_fwd(a, w, b, B, C, H, W, p)
+    if mode == 2:
+        close(xk, raw.clamp(-1, 1), 1e-3, 1e-3, "clamp")
+    else:
+        xn, x0r = ref.ddim_step(x, raw, coef.tolist())
+        close(x0, x0r, 1e-3, 1e-3, "x0")
+        close(xk, xn, 2e-3, 1e-3, "x_next")
+
+
 @pytest.mark.parametrize("B,C,H,W,p,D,pd", [(4, 3, 64, 64, 8, 384, 0.1), (2, 3, 64, 64, 4, 256, 0.0)])
 def test_patch_embed(B, C, H, W, p, D, pd):
     N = (H // p) * (W // p) + 1

@@ -28,8 +28,9 @@ def run(dist_mode):
 
 
 if __name__ == "__main__":
+    from ddim_cold_amd.parallel.dist import free_port
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", "29541")
+    os.environ.setdefault("MASTER_PORT", str(free_port()))
     torch.cuda.set_device(0)
     ref, loss0, _, _ = run(None)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
