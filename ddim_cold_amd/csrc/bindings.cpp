@@ -263,8 +263,14 @@ void head_step_(Tensor a, Tensor w, Tensor b, Tensor x, c10::optional<Tensor> x0
   gemm_nt(g, EPI_HEAD, cur_stream());
 }
 
-std::tuple<Tensor, Tensor> smooth_l1_fwd_bwd(Tensor pred, Tensor target, int64_t N, int64_t patch, double beta) {
+std::tuple<Tensor, Tensor> smooth_l1_fwd_bwd(Tensor pred, Tensor target, int64_t N, int64_t patch, double beta,
+                                             c10::optional<Tensor> loss_last, c10::optional<Tensor> loss_ema,
+                                             double ema_decay) {
   CHECK_IN(pred, F32); CHECK_IN(target, F32);
+  float* ll = nullptr;
+  float* le = nullptr;
+  if (loss_last.has_value() && loss_last->defined()) { CHECK_IN((*loss_last), F32); ll = loss_last->data_ptr<float>(); }
+  if (loss_ema.has_value() && loss_ema->defined()) { CHECK_IN((*loss_ema), F32); le = loss_ema->data_ptr<float>(); }
   const c10::DeviceGuard guard(pred.device());
   TORCH_CHECK(pred.sizes() == target.sizes() && pred.dim() == 4, "pred/target shape");
   const int B = pred.size(0), C = pred.size(1), H = pred.size(2), W = pred.size(3);
@@ -273,7 +279,7 @@ std::tuple<Tensor, Tensor> smooth_l1_fwd_bwd(Tensor pred, Tensor target, int64_t
   auto parts = at::empty({L1_PARTS}, pred.options());
   auto dtok = at::empty({(int64_t)B * N, C * patch * patch}, pred.options().dtype(BF16));
   smooth_l1_launch(pred.data_ptr<float>(), target.data_ptr<float>(), loss.data_ptr<float>(), parts.data_ptr<float>(),
-                   dtok.data_ptr(), B, C, H, W, patch, (float)beta, cur_stream());
+                   dtok.data_ptr(), B, C, H, W, patch, (float)beta, ll, le, (float)ema_decay, cur_stream());
   return {loss, dtok};
 }
 
@@ -603,7 +609,8 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("head_fwd(Tensor a, Tensor w, Tensor b, int B, int C, int H, int W, int patch) -> Tensor");
   m.def("head_step_(Tensor a, Tensor w, Tensor b, Tensor(a!) x, Tensor(b!)? x0_out, Tensor? coef, int patch, "
         "int mode) -> ()");
-  m.def("smooth_l1_fwd_bwd(Tensor pred, Tensor target, int N, int patch, float beta) -> (Tensor, Tensor)");
+  m.def("smooth_l1_fwd_bwd(Tensor pred, Tensor target, int N, int patch, float beta, Tensor(a!)? loss_last=None, "
+        "Tensor(b!)? loss_ema=None, float ema_decay=0.99) -> (Tensor, Tensor)");
   m.def("img_to_tokgrad(Tensor dimg, int N, int patch) -> Tensor");
   m.def("linear_dgrad(Tensor dy, Tensor w, bool out_fp32) -> Tensor");
   m.def("linear_dgrad_gelu(Tensor dy, Tensor w, Tensor u, Tensor rng, int site, float p) -> Tensor");

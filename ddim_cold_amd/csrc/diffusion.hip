@@ -98,6 +98,38 @@ __global__ void cold_draw_kernel(const int64_t* __restrict__ rng, int site, int 
   }
 }
 
+// cold_draw + pixelate_pair in ONE launch: every element recomputes its sample's
+// (pool index, t) from the counter hash (two mix32, cheaper than a dependent
+// launch); the first element of each sample also stores them for the model.
+__global__ __launch_bounds__(256) void cold_batch_kernel(const float* __restrict__ pool, int pool_n,
+                                                         const int64_t* __restrict__ rng, int site, int max_t,
+                                                         int64_t* __restrict__ idx, int64_t* __restrict__ t,
+                                                         int draw_idx, float* __restrict__ xt, float* __restrict__ xtm1,
+                                                         int B, int C, int H, int W) {
+  const uint32_t salt = site_salt(rng, site);
+  const int64_t per = (int64_t)C * H * W;
+  const int64_t n = (int64_t)B * per;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    const int b = (int)(e / per);
+    const int64_t rem = e - (int64_t)b * per;
+    const int64_t src = draw_idx ? (int64_t)(mix32(((uint32_t)(2 * b) * 0x9E3779B1u) ^ salt) % (uint32_t)pool_n)
+                                 : idx[b];
+    const int tt = 1 + (int)(mix32(((uint32_t)(2 * b + 1) * 0x9E3779B1u) ^ salt) % (uint32_t)max_t);
+    if (rem == 0) {
+      if (draw_idx) idx[b] = src;
+      t[b] = tt;
+    }
+    const int x = (int)(rem % W);
+    const int64_t r = rem / W;
+    const int y = (int)(r % H);
+    const int c = (int)(r / H);
+    const float* im = pool + ((size_t)src * C + c) * H * W;
+    const int f1 = 1 << tt, f0 = 1 << (tt - 1);
+    xt[e] = im[(size_t)pix_src(y, H, f1) * W + pix_src(x, W, f1)];
+    xtm1[e] = im[(size_t)pix_src(y, H, f0) * W + pix_src(x, W, f0)];
+  }
+}
+
 static int g_grid(int64_t n) {
   int64_t g = (n + 255) / 256;
   if (g > 4096) g = 4096;
@@ -133,7 +165,6 @@ void pixelate_pair_launch(const float* img, const int64_t* idx, const int64_t* t
 void cold_batch_launch(const float* pool, int pool_n, const int64_t* rng, int site, float* x_t, float* x_tm1,
                        int64_t* t, int64_t* idx_ws, int B, int C, int H, int W, int max_t, bool draw_idx,
                        hipStream_t stream) {
-  hipLaunchKernelGGL(cold_draw_kernel, dim3(1), dim3(256), 0, stream, rng, site, pool_n, max_t, B, idx_ws, t,
-                     draw_idx ? 1 : 0);
-  pixelate_pair_launch(pool, idx_ws, t, x_t, x_tm1, B, C, H, W, stream);
+  hipLaunchKernelGGL(cold_batch_kernel, dim3(g_grid((int64_t)B * C * H * W)), dim3(256), 0, stream, pool, pool_n, rng,
+                     site, max_t, idx_ws, t, draw_idx ? 1 : 0, x_t, x_tm1, B, C, H, W);
 }

@@ -146,14 +146,24 @@ __global__ __launch_bounds__(256) void tokgrad_kernel(const float* __restrict__ 
   }
 }
 
-__global__ __launch_bounds__(256) void sum_parts_kernel(const float* __restrict__ parts, int n, float* __restrict__ out) {
+// loss = sum of the per-block partials; optionally also the trainer's loss
+// bookkeeping (multi_gpu_trainer.py:125-126: last loss + EMA 0.99/0.01) so the
+// training step needs no extra copy / elementwise launches for it
+__global__ __launch_bounds__(256) void sum_parts_kernel(const float* __restrict__ parts, int n, float* __restrict__ out,
+                                                        float* __restrict__ loss_last, float* __restrict__ loss_ema,
+                                                        float decay) {
   __shared__ float red[4];
   float v = 0.f;
   for (int i = threadIdx.x; i < n; i += 256) v += parts[i];
   v = wave_sum(v);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
-  if (threadIdx.x == 0) out[0] = red[0] + red[1] + red[2] + red[3];
+  if (threadIdx.x == 0) {
+    const float l = red[0] + red[1] + red[2] + red[3];
+    out[0] = l;
+    if (loss_last) loss_last[0] = l;
+    if (loss_ema) loss_ema[0] = loss_ema[0] * decay + l * (1.f - decay);
+  }
 }
 
 static int grid_for(size_t n) {
@@ -188,14 +198,16 @@ void embed_bwd_launch(const float* g, const int64_t* t, float* dcls, float* dpos
 }
 
 void smooth_l1_launch(const float* pred, const float* target, float* loss, float* partials, void* dtok, int B,
-                      int C, int H, int W, int patch, float beta, hipStream_t stream) {
+                      int C, int H, int W, int patch, float beta, float* loss_last, float* loss_ema, float ema_decay,
+                      hipStream_t stream) {
   const size_t n_img = (size_t)B * C * H * W;
   const size_t n = n_img + (size_t)B * C * patch * patch;
   int grid = grid_for(n);
   if (grid > L1_PARTS) grid = L1_PARTS;
   hipLaunchKernelGGL(tokgrad_kernel<true>, dim3(grid), dim3(256), 0, stream, pred, target, partials,
                      reinterpret_cast<bf16*>(dtok), B, C, H, W, patch, beta, 1.0f / (float)n_img);
-  hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(256), 0, stream, partials, grid, loss);
+  hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(256), 0, stream, partials, grid, loss, loss_last, loss_ema,
+                     ema_decay);
 }
 
 void img_to_tokgrad_launch(const float* dimg, void* dtok, int B, int C, int H, int W, int patch, hipStream_t stream) {

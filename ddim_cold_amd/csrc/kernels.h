@@ -101,7 +101,8 @@ void patchify_cls_launch(const float* img, const int64_t* t, const float* cls, c
 void embed_bwd_launch(const float* g, const int64_t* t, float* dcls, float* dpos, float* dtemb, void* gpatch,
                       int B, int N, int D, const int64_t* rng, int site, double p, hipStream_t stream);
 void smooth_l1_launch(const float* pred, const float* target, float* loss, float* partials, void* dtok, int B,
-                      int C, int H, int W, int patch, float beta, hipStream_t stream);
+                      int C, int H, int W, int patch, float beta, float* loss_last, float* loss_ema, float ema_decay,
+                      hipStream_t stream);
 constexpr int L1_PARTS = 512;
 void img_to_tokgrad_launch(const float* dimg, void* dtok, int B, int C, int H, int W, int patch,
                            hipStream_t stream);

@@ -118,10 +118,18 @@ def head_fwd(a, w, b, B: int, C: int, H: int, W: int, patch: int):
     return ref.head_fwd(a, w, b, B, C, H, W, patch)
 
 
-def smooth_l1_fwd_bwd(pred, target, N: int, patch: int, beta: float = 1.0):
+def smooth_l1_fwd_bwd(pred, target, N: int, patch: int, beta: float = 1.0, loss_last=None, loss_ema=None,
+                      ema_decay: float = 0.99):
+    """Mean smooth-L1 loss and its token-layout gradient; optionally also writes
+    ``loss_last`` and updates ``loss_ema`` (decay) in the same launch."""
     if _hip(pred):
-        return _ops().smooth_l1_fwd_bwd(pred, target, N, patch, float(beta))
-    return ref.smooth_l1_fwd_bwd(pred, target, N, patch, beta)
+        return _ops().smooth_l1_fwd_bwd(pred, target, N, patch, float(beta), loss_last, loss_ema, float(ema_decay))
+    loss, dtok = ref.smooth_l1_fwd_bwd(pred, target, N, patch, beta)
+    if loss_last is not None:
+        loss_last.copy_(loss.reshape(loss_last.shape))
+    if loss_ema is not None:
+        loss_ema.mul_(ema_decay).add_(loss.reshape(loss_ema.shape), alpha=1.0 - ema_decay)
+    return loss, dtok
 
 
 def img_to_tokgrad(dimg, N: int, patch: int):

@@ -236,9 +236,8 @@ class TrainEngine:
         c = self.prog.cfg
         img, tgt, t = self.batch_fn()
         out, S = self.prog.forward(self.param_tensors, img, t, self.rng, True)
-        loss, dtok = ops.smooth_l1_fwd_bwd(out, tgt, c.tokens, c.patch, self.cfg.loss_beta)
-        self.loss_last.copy_(loss)
-        self.loss_ema.mul_(self.cfg.ema_decay).add_(loss, alpha=1.0 - self.cfg.ema_decay)
+        _, dtok = ops.smooth_l1_fwd_bwd(out, tgt, c.tokens, c.patch, self.cfg.loss_beta, self.loss_last,
+                                        self.loss_ema, self.cfg.ema_decay)
         del out
         ln_lo = 0
         for i in self.prog.backward_iter(self.param_tensors, self.grad_tensors, S, dtok, self.rng, True,
