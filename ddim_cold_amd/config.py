@@ -77,6 +77,7 @@ class ExperimentConfig:
     timestep_embedding: str = "learned"
     max_steps: int = 0
     backend: Optional[str] = None
+    grad_accum: int = 1           # micro-batches of per_gpu_batch per optimizer step
 
     # ------------------------------------------------------------------ derived
     @property
@@ -93,6 +94,8 @@ class ExperimentConfig:
                     timestep_embedding=self.timestep_embedding)
 
     def validate(self):
+        if self.grad_accum < 1:
+            raise ValueError("grad_accum must be >= 1")
         if len(self.epoch) != 2 or self.epoch[0] > self.epoch[1]:
             raise ValueError(f"epoch must be [start, end], got {self.epoch}")
         if self.image_size[0] % self.patch_size or self.image_size[1] % self.patch_size:

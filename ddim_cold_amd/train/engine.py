@@ -79,6 +79,10 @@ class EngineConfig:
     # 1.125 segmented (each extra graph launch + stream join costs ~30 us).
     # Falls back to segments if the capture raises.
     graph_comm: bool = True
+    # micro-batches per optimizer step (batch_fn is called grad_accum times per
+    # step; gradients accumulate in the arena, averaged in the optimizer; the
+    # all-reduce runs once, after the last micro-batch's backward)
+    grad_accum: int = 1
 
 
 def _align(n: int) -> int:
@@ -234,27 +238,35 @@ class TrainEngine:
 
     def _step_iter(self):
         c = self.prog.cfg
-        img, tgt, t = self.batch_fn()
-        out, S = self.prog.forward(self.param_tensors, img, t, self.rng, True)
-        _, dtok = ops.smooth_l1_fwd_bwd(out, tgt, c.tokens, c.patch, self.cfg.loss_beta, self.loss_last,
-                                        self.loss_ema, self.cfg.ema_decay)
-        del out
-        ln_lo = 0
-        for i in self.prog.backward_iter(self.param_tensors, self.grad_tensors, S, dtok, self.rng, True,
-                                         ln_ws=self.ln_ws, wgrad_stream=self.side):
-            if i in self.bucket_after and (self.segmented or i == -1):
-                hi = self.ln_done_at[i]
-                if hi > ln_lo:
-                    ops.replica_reduce_(self.ln_ws[ln_lo:hi], None if self.ln_ptrs is None else self.ln_ptrs[ln_lo:hi],
-                                        2 * c.dim, dsts=self.ln_dsts[ln_lo:hi])
-                    ln_lo = hi
-                if self._segment_capture:
-                    self._join_side()  # a captured segment must rejoin every stream it forked
-                yield ("bucket", self.bucket_after[i])
-        S = None
+        k_acc = max(1, int(self.cfg.grad_accum))
+        for micro in range(k_acc):
+            last = micro == k_acc - 1
+            if micro > 0:
+                self.rng[1:].add_(1)  # fresh dropout masks and batch draws per micro-batch
+            img, tgt, t = self.batch_fn()
+            out, S = self.prog.forward(self.param_tensors, img, t, self.rng, True)
+            _, dtok = ops.smooth_l1_fwd_bwd(out, tgt, c.tokens, c.patch, self.cfg.loss_beta, self.loss_last,
+                                            self.loss_ema, self.cfg.ema_decay)
+            del out
+            ln_lo = 0
+            for i in self.prog.backward_iter(self.param_tensors, self.grad_tensors, S, dtok, self.rng, True,
+                                             ln_ws=self.ln_ws, wgrad_stream=self.side):
+                if i in self.bucket_after and (self.segmented or i == -1):
+                    hi = self.ln_done_at[i]
+                    if hi > ln_lo:
+                        ops.replica_reduce_(self.ln_ws[ln_lo:hi],
+                                            None if self.ln_ptrs is None else self.ln_ptrs[ln_lo:hi],
+                                            2 * c.dim, dsts=self.ln_dsts[ln_lo:hi])
+                        ln_lo = hi
+                    if last:
+                        if self._segment_capture:
+                            self._join_side()  # a captured segment must rejoin every stream it forked
+                        yield ("bucket", self.bucket_after[i])
+            S = None
         self._join_side()  # all weight gradients final before the norm / optimizer
-        # optimizer: grads are SUM-reduced over ranks -> average via grad_scale
-        gs = 1.0 / self.world
+        # optimizer: grads are SUM-reduced over ranks and summed over micro-batches
+        # -> average via grad_scale
+        gs = 1.0 / (self.world * k_acc)
         ops.sqnorm(self.flat_g, self.sqnorm, gs)
         ops.adamw_step(self.flat_p, self.flat_g, self.flat_m, self.flat_v, self.flat_pb, self.sqnorm,
                        self.step_ctr, self.hyper, gs)

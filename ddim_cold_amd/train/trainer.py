@@ -122,12 +122,13 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
 
     train_pool, val_pool = _pools(cfg, device, rank)
     B = cfg.per_gpu_batch
+    A = int(cfg.grad_accum)
     n_train, n_val = train_pool.shape[0], val_pool.shape[0]
-    steps_per_epoch = len(shard_indices(n_train, world, rank, 0, cfg.seed)) // B
+    steps_per_epoch = len(shard_indices(n_train, world, rank, 0, cfg.seed)) // (B * A)
     if cfg.max_steps:
         steps_per_epoch = min(steps_per_epoch, cfg.max_steps)
     if steps_per_epoch < 1:
-        raise ValueError(f"dataset too small: {n_train} images for batch {B} x {world} ranks")
+        raise ValueError(f"dataset too small: {n_train} images for batch {B} x {A} micro-batches x {world} ranks")
     val_idx0 = shard_indices(n_val, world, rank, 0, cfg.seed, shuffle=False, drop_last=False)
     val_batches = math.ceil(val_idx0.numel() / B)
 
@@ -145,10 +146,22 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
 
     temb_rows = int(math.log2(cfg.image_size[1])) + 1 if cfg.dataset.startswith("cold") else None
     ecfg = EngineConfig(lr=cfg.lr, t_max=steps_per_epoch * cfg.epoch[1], use_graph=cfg.graph,
-                        bucket_blocks=cfg.bucket_blocks, seed=cfg.seed * 1000 + rank, temb_rows=temb_rows)
+                        bucket_blocks=cfg.bucket_blocks, seed=cfg.seed * 1000 + rank, temb_rows=temb_rows,
+                        grad_accum=A)
     engine = TrainEngine(model, ecfg, device=device)
-    idx_dev = torch.zeros(B, dtype=torch.int64, device=device)
-    engine.set_batch_fn(make_batcher(cfg.dataset, train_pool, B, engine.rng, cfg.total_steps, idx=idx_dev))
+    # one static index row per micro-batch; the engine calls the batch source A
+    # times per step in order (also while capturing), so call j reads row j
+    idx_dev = torch.zeros(A, B, dtype=torch.int64, device=device)
+    batchers = [make_batcher(cfg.dataset, train_pool, B, engine.rng, cfg.total_steps, idx=idx_dev[j])
+                for j in range(A)]
+    calls = [0]
+
+    def batch_fn():
+        j = calls[0] % A
+        calls[0] += 1
+        return batchers[j]()
+
+    engine.set_batch_fn(batch_fn)
 
     start_epoch, end_epoch = int(cfg.epoch[0]), int(cfg.epoch[1])
     loss_rec, steps, best_loss = 5.0, 0, 5.0
@@ -169,8 +182,8 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
     t_start = time.time()
     for epoch in range(start_epoch, end_epoch):
         model.train()
-        table = shard_indices(n_train, world, rank, epoch, cfg.seed)[: steps_per_epoch * B]
-        table = table.view(steps_per_epoch, B).to(device)
+        table = shard_indices(n_train, world, rank, epoch, cfg.seed)[: steps_per_epoch * A * B]
+        table = table.view(steps_per_epoch, A, B).to(device)
         for s in range(steps_per_epoch):
             idx_dev.copy_(table[s])
             engine.train_step()

@@ -153,3 +153,18 @@ def test_data_parallel_gloo_matches_single_process():
     # exp_avg after one step = (1-b1) * mean-gradient
     err = (r["m"] - m1).abs().max().item() / m1.abs().max().item()
     assert err < 1e-4, err
+
+
+def test_grad_accumulation_matches_full_batch():
+    """grad_accum=2 over two half batches == one step on the full batch (no dropout)."""
+    x, y, t = _batch(4, seed=9)
+    full = TrainEngine(_model(drop=False), EngineConfig(lr=1e-3, weight_decay=0.0, max_grad_norm=0.0), device="cpu")
+    full.step(x, y, t)
+    acc = TrainEngine(_model(drop=False), EngineConfig(lr=1e-3, weight_decay=0.0, max_grad_norm=0.0, grad_accum=2),
+                      device="cpu")
+    halves = iter([(x[:2], y[:2], t[:2]), (x[2:], y[2:], t[2:])])
+    acc.set_batch_fn(lambda: next(halves))
+    acc.train_step()
+    err = (acc.flat_m - full.flat_m).abs().max().item() / full.flat_m.abs().max().item()
+    assert err < 1e-4, err
+    assert int(acc.step_ctr[0]) == 1 and int(acc.rng[1]) == 2

@@ -80,6 +80,15 @@ def test_trainer_log_checkpoints_and_resume(tmp_path):
     assert float(last2["optimizer"]["state"][0]["step"]) == 3 * spe
 
 
+def test_trainer_grad_accum(tmp_path):
+    cfg = _tiny_cfg(grad_accum=2, epoch=[0, 1], ckpt_dir=str(tmp_path / "Saved_Models"))
+    paths = Paths.make(cfg, "acc", root=str(tmp_path))
+    res = launch(cfg, "acc", paths, backend="gloo")
+    assert res["steps"] == 64 // (8 * 2)
+    last = torch.load(os.path.join(paths.ckpt_dir, "lastepoch.pkl"), weights_only=True)
+    assert float(last["optimizer"]["state"][0]["step"]) == res["steps"]
+
+
 def test_checkpoint_weights_roundtrip(tmp_path):
     from ddim_cold_amd.models import DiffusionVisionTransformer
     m = DiffusionVisionTransformer(img_size=[16, 16], patch_size=4, embed_dim=32, depth=1, num_heads=2)
