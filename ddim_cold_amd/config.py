@@ -78,6 +78,10 @@ class ExperimentConfig:
     max_steps: int = 0
     backend: Optional[str] = None
     grad_accum: int = 1           # micro-batches of per_gpu_batch per optimizer step
+    use_diff_step: bool = False   # True: the model's total_steps = diff_step (reference parses it but keeps 2000)
+    sync_check_every: int = 0     # debug: cross-rank parameter checksum every N steps (0 = only after init)
+    fault_inject_step: int = 0    # testing: raise after this many steps (after logging), to exercise resume
+    perf_log: bool = True         # extra '# perf' lines (img/s, device ms/step) next to the reference lines
 
     # ------------------------------------------------------------------ derived
     @property
@@ -88,9 +92,13 @@ class ExperimentConfig:
     def lr(self) -> float:
         return self.base_lr * self.per_gpu_batch * self.num_gpus / 512
 
+    @property
+    def model_total_steps(self) -> int:
+        return int(self.diff_step) if self.use_diff_step else int(self.total_steps)
+
     def model_kwargs(self) -> dict:
         return dict(img_size=list(self.image_size), patch_size=self.patch_size, embed_dim=self.embed_dim,
-                    depth=self.depth, num_heads=self.head, total_steps=self.total_steps,
+                    depth=self.depth, num_heads=self.head, total_steps=self.model_total_steps,
                     timestep_embedding=self.timestep_embedding)
 
     def validate(self):

@@ -10,7 +10,8 @@ Reference (multi_gpu_trainer.py:71-80, 94-106, 152-163):
 All written with ``torch.save``; optimizer / scheduler entries are standard
 ``torch.optim.AdamW`` / ``CosineAnnealingLR`` state dicts so files move freely
 between this framework and the reference.  Extra keys we add (ignored by the
-reference): ``'rng'`` (device RNG seed/step), ``'engine_steps'``.
+reference): ``'rng'`` (device RNG seed/step), ``'engine_steps'``, ``'scaler'`` (GradScaler
+layout, scale 1: bf16 training needs no loss scaling).
 
 Loading uses ``weights_only=True`` (no arbitrary unpickling).
 """
@@ -71,6 +72,10 @@ def save_lastepoch(path: str, model, engine, epoch: int, steps: int, loss_rec: f
         "optimizer": _to_cpu(engine.optimizer_state_dict()),
         "rng": engine.rng.detach().cpu().clone(),
         "engine_steps": int(engine.steps_done),
+        # torch.cuda.amp.GradScaler state_dict layout (the reference does not save it,
+        # SURVEY §7.4 D15); bf16 needs no loss scaling, so the scale is fixed at 1
+        "scaler": {"scale": 1.0, "growth_factor": 2.0, "backoff_factor": 0.5, "growth_interval": 2000,
+                   "_growth_tracker": 0},
     }
     _atomic_save(ckpt, path)
 

@@ -40,6 +40,7 @@ from ..models.program import model_tensors
 from ..models.vit import DiffusionVisionTransformer
 from ..parallel import dist as pdist
 from ..utils.logging import ScalarWriter, asctime, fmt_epoch, fmt_steps, printLog
+from ..utils.observe import FaultInjected, StepClock, check_param_sync, phase, torch_profiler
 from . import checkpoint as ckpt
 from .engine import EngineConfig, TrainEngine
 
@@ -152,7 +153,7 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
     # one static index row per micro-batch; the engine calls the batch source A
     # times per step in order (also while capturing), so call j reads row j
     idx_dev = torch.zeros(A, B, dtype=torch.int64, device=device)
-    batchers = [make_batcher(cfg.dataset, train_pool, B, engine.rng, cfg.total_steps, idx=idx_dev[j])
+    batchers = [make_batcher(cfg.dataset, train_pool, B, engine.rng, cfg.model_total_steps, idx=idx_dev[j])
                 for j in range(A)]
     calls = [0]
 
@@ -175,7 +176,13 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
             printLog(f"resuming from epoch {start_epoch:8d} of " + cfg.resume, paths.log)
             printLog(f"recovering best_loss {best_loss:4f}", paths.log)
     engine.loss_ema.fill_(loss_rec)
+    check_param_sync(engine.flat_p, step=steps)  # replicas start identical
     writer = ScalarWriter(paths.ckpt_dir, enabled=(rank == 0))
+    clock = StepClock(device)
+    clock.mark(steps)
+    prof = torch_profiler(rank)
+    if prof is not None:
+        prof.__enter__()
     eval_rng = torch.tensor([cfg.seed + 7919, 0], dtype=torch.int64, device=device)
 
     history = []
@@ -186,11 +193,15 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
         table = table.view(steps_per_epoch, A, B).to(device)
         for s in range(steps_per_epoch):
             idx_dev.copy_(table[s])
-            engine.train_step()
+            with phase("train_step"):
+                engine.train_step()
+            if prof is not None:
+                prof.step()
             steps += 1
+            if cfg.sync_check_every and steps % cfg.sync_check_every == 0:
+                check_param_sync(engine.flat_p, step=steps)
             if steps % cfg.log_every == 0:
-                if device.type == "cuda":
-                    torch.cuda.synchronize()
+                window = clock.mark(steps)  # device events: the only sync of the window
                 loss_rec = float(engine.loss_ema.item())
                 if verbose:
                     print(f"[rank {rank}] step {steps} loss_ema {loss_rec:.4f}", flush=True)
@@ -198,11 +209,18 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
                     now = time.time()
                     printLog(fmt_steps(steps, loss_rec, now - t_start), paths.log)
                     t_start = now
+                    if cfg.perf_log and window is not None and window[1] > 0:
+                        sec, n = window
+                        printLog(f"# perf: {n * B * A * world / sec:.1f} img/s  {1e3 * sec / n:.3f} ms/step "
+                                 f"(device, {world} rank(s))", paths.log)
+            if cfg.fault_inject_step and steps >= cfg.fault_inject_step:
+                raise FaultInjected(f"fault injected at step {steps} (fault_inject_step)")
         loss_rec = float(engine.loss_ema.item())
         if (epoch - start_epoch + 1) % max(cfg.eval_every, 1) == 0 or epoch == end_epoch - 1:
             model.eval()
             vidx = shard_indices(n_val, world, rank, epoch, cfg.seed, shuffle=False, drop_last=False)
-            vloss = evaluate(model, engine, val_pool, vidx, B, cfg.dataset, cfg.total_steps, eval_rng)
+            with phase("evaluate"):
+                vloss = evaluate(model, engine, val_pool, vidx, B, cfg.dataset, cfg.model_total_steps, eval_rng)
             vloss = pdist.all_reduce_mean(vloss, device)
             model.train()
             history.append((epoch, vloss))
@@ -215,6 +233,8 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
                 ckpt.save_lastepoch(os.path.join(paths.ckpt_dir, "lastepoch.pkl"), model, engine, epoch, steps,
                                     loss_rec, best_loss)
             pdist.barrier()
+    if prof is not None:
+        prof.__exit__(None, None, None)
     writer.close()
     result = {"steps": steps, "loss_rec": loss_rec, "best_loss": best_loss, "history": history,
               "final_lr": engine.current_lr()}

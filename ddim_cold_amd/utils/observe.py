@@ -1,0 +1,111 @@
+"""Observability / debugging aids of the trainer.
+
+* :class:`StepClock` — device-side (HIP event) timing of log windows: no host
+  synchronisation inside the step loop, read only at log points.
+* :func:`range_push` / :func:`range_pop` — roctx ranges (through
+  ``torch.cuda.nvtx``, which ROCm builds route to roctx) around trainer phases,
+  visible in ``rocprofv3 --marker-trace``; no-ops where unavailable.
+* :func:`torch_profiler` — optional ``torch.profiler`` capture of a step window
+  (``DDIM_COLD_TORCH_PROFILE=<dir>``, ``DDIM_COLD_TORCH_PROFILE_STEPS=a,b``).
+* :func:`check_param_sync` — cross-rank parameter checksum (debug mode
+  ``sync_check_every``): raises if data-parallel replicas diverged.
+* :class:`FaultInjected` — raised by ``fault_inject_step`` to test resume.
+"""
+from __future__ import annotations
+
+import contextlib
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+class FaultInjected(RuntimeError):
+    pass
+
+
+class StepClock:
+    """HIP-event clock over log windows (falls back to host time on CPU)."""
+
+    def __init__(self, device: torch.device):
+        self.cuda = torch.device(device).type == "cuda"
+        self.last = None
+        self.last_steps = 0
+        if not self.cuda:
+            import time
+            self._now = time.perf_counter
+
+    def mark(self, steps: int):
+        """Returns (seconds, steps) since the previous mark (None on the first call)."""
+        if self.cuda:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            ev.synchronize()
+            out = None
+            if self.last is not None:
+                out = (self.last.elapsed_time(ev) / 1e3, steps - self.last_steps)
+            self.last, self.last_steps = ev, steps
+            return out
+        now = self._now()
+        out = None if self.last is None else (now - self.last, steps - self.last_steps)
+        self.last, self.last_steps = now, steps
+        return out
+
+
+def range_push(name: str):
+    try:
+        torch.cuda.nvtx.range_push(name)
+    except Exception:
+        pass
+
+
+def range_pop():
+    try:
+        torch.cuda.nvtx.range_pop()
+    except Exception:
+        pass
+
+
+@contextlib.contextmanager
+def phase(name: str):
+    range_push(name)
+    try:
+        yield
+    finally:
+        range_pop()
+
+
+def torch_profiler(rank: int):
+    """A ``torch.profiler.profile`` (entered by the caller) when DDIM_COLD_TORCH_PROFILE is set, else None."""
+    out = os.environ.get("DDIM_COLD_TORCH_PROFILE")
+    if not out:
+        return None
+    a, b = (int(v) for v in os.environ.get("DDIM_COLD_TORCH_PROFILE_STEPS", "10,15").split(","))
+    from torch.profiler import ProfilerActivity, profile, schedule
+    acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if torch.cuda.is_available() else [])
+    os.makedirs(out, exist_ok=True)
+
+    def handler(p):
+        p.export_chrome_trace(os.path.join(out, f"trace_rank{rank}.json"))
+
+    return profile(activities=acts, schedule=schedule(wait=a, warmup=0, active=max(1, b - a), repeat=1),
+                   on_trace_ready=handler)
+
+
+def param_checksum(flat: torch.Tensor) -> torch.Tensor:
+    f = flat.double()
+    return torch.stack([f.sum(), (f * f).sum(), f.abs().max()])
+
+
+def check_param_sync(flat: torch.Tensor, group=None, step: Optional[int] = None, rtol: float = 0.0):
+    """All ranks must hold identical parameters: compare checksums via MAX / MIN all-reduce."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return
+    cs = param_checksum(flat)
+    hi, lo = cs.clone(), cs.clone()
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    if not torch.all((hi - lo).abs() <= rtol * hi.abs()):
+        raise RuntimeError(f"data-parallel replicas diverged at step {step}: checksum max {hi.tolist()} "
+                           f"min {lo.tolist()}")

@@ -168,3 +168,28 @@ def test_grad_accumulation_matches_full_batch():
     err = (acc.flat_m - full.flat_m).abs().max().item() / full.flat_m.abs().max().item()
     assert err < 1e-4, err
     assert int(acc.step_ctr[0]) == 1 and int(acc.rng[1]) == 2
+
+
+def _sync_worker(rank, world, port, out_path):
+    from ddim_cold_amd.utils.observe import check_param_sync
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        same = torch.arange(10.0)
+        check_param_sync(same)  # identical: passes
+        try:
+            check_param_sync(same + rank)  # diverged replicas
+            ok = False
+        except RuntimeError:
+            ok = True
+        if rank == 0:
+            torch.save({"detected": ok}, out_path)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_param_sync_check_detects_divergence():
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "r.pt")
+        mp.start_processes(_sync_worker, args=(2, free_port(), out), nprocs=2, join=True, start_method="spawn")
+        assert torch.load(out, weights_only=True)["detected"]

@@ -89,6 +89,21 @@ def test_trainer_grad_accum(tmp_path):
     assert float(last["optimizer"]["state"][0]["step"]) == res["steps"]
 
 
+def test_fault_injection_and_resume(tmp_path):
+    from ddim_cold_amd.utils.observe import FaultInjected
+    cfg = _tiny_cfg(ckpt_dir=str(tmp_path / "Saved_Models"), fault_inject_step=10, sync_check_every=3)
+    paths = Paths.make(cfg, "flt", root=str(tmp_path))
+    with pytest.raises(FaultInjected):
+        launch(cfg, "flt", paths, backend="gloo")
+    last = torch.load(os.path.join(paths.ckpt_dir, "lastepoch.pkl"), weights_only=True)
+    assert last["epoch"] == 0 and last["steps"] == 8 and last["scaler"]["scale"] == 1.0
+    cfg2 = dataclasses.replace(cfg, fault_inject_step=0, resume=os.path.join(paths.ckpt_dir, "lastepoch.pkl"))
+    res = launch(cfg2, "flt", paths, backend="gloo")
+    assert res["steps"] == 16 and [e for e, _ in res["history"]] == [1]
+    with open(paths.log) as f:
+        assert "# perf:" in f.read()
+
+
 def test_checkpoint_weights_roundtrip(tmp_path):
     from ddim_cold_amd.models import DiffusionVisionTransformer
     m = DiffusionVisionTransformer(img_size=[16, 16], patch_size=4, embed_dim=32, depth=1, num_heads=2)
@@ -103,7 +118,7 @@ def test_checkpoint_weights_roundtrip(tmp_path):
 
 
 def test_trainer_two_ranks_gloo(tmp_path):
-    cfg = _tiny_cfg(num_gpus=2, epoch=[0, 1], ckpt_dir=str(tmp_path / "Saved_Models"))
+    cfg = _tiny_cfg(num_gpus=2, epoch=[0, 1], ckpt_dir=str(tmp_path / "Saved_Models"), sync_check_every=2)
     paths = Paths.make(cfg, "exp2", root=str(tmp_path))
     res = launch(cfg, "exp2", paths, backend="gloo")
     assert res["steps"] == 64 // 2 // 8
