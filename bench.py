@@ -61,6 +61,8 @@ def main():
                     help="init the RCCL process group and run segmented graphs + collectives even with 1 rank")
     ap.add_argument("--segmented-comm", action="store_true",
                     help="host-issued all-reduces between graph segments instead of capturing them in the step graph")
+    ap.add_argument("--grad-wire", default="fp32", choices=["fp32", "bf16"],
+                    help="gradient all-reduce wire format (bf16 halves the xGMI bytes)")
     ap.add_argument("--sampler-k", type=int, default=20)
     ap.add_argument("--sampler-n", type=int, default=64)
     ap.add_argument("--no-eager-baseline", action="store_true",
@@ -90,7 +92,7 @@ def main():
                        seed=42, force_segments=args.force_dist,
                        wgrad_stream=args.wgrad_stream,
                        temb_rows=int(math.log2(model.img_size[1])) + 1,  # cold t in 1..log2(W)
-                       graph_comm=not args.segmented_comm)
+                       graph_comm=not args.segmented_comm, grad_wire=args.grad_wire)
     engine = TrainEngine(model, cfg, device=dev)
     pool = synthetic_pool(1024, tuple(model.img_size), seed=7 + rank, device=dev)
     engine.set_batch_fn(ColdBatcher(pool, args.batch, engine.rng))
@@ -171,6 +173,7 @@ def main():
                        "allreduce": ("none" if not engine.segmented else "eager" if dev.type != "cuda" else
                                      "segmented" if (args.segmented_comm or getattr(engine, "_graph_comm_failed", False))
                                      else "captured-in-graph"),
+                       "grad_wire": args.grad_wire,
                        "optimizer": "AdamW(wd=0.05)+clip1.0+cosine", "final_loss": round(loss, 5)},
         }
         out.update(extra)

@@ -83,6 +83,9 @@ class EngineConfig:
     # step; gradients accumulate in the arena, averaged in the optimizer; the
     # all-reduce runs once, after the last micro-batch's backward)
     grad_accum: int = 1
+    # gradient all-reduce wire format: "fp32" (reference DDP semantics) or "bf16"
+    # (halves the xGMI bytes; the sum is accumulated in bf16 by RCCL)
+    grad_wire: str = "fp32"
 
 
 def _align(n: int) -> int:
@@ -149,6 +152,9 @@ class TrainEngine:
         self.flat_m = torch.zeros(off, dtype=torch.float32, device=dev)
         self.flat_v = torch.zeros(off, dtype=torch.float32, device=dev)
         self.flat_pb = torch.zeros(off, dtype=torch.bfloat16, device=dev)
+        if self.cfg.grad_wire not in ("fp32", "bf16"):
+            raise ValueError(f"grad_wire must be 'fp32' or 'bf16', got {self.cfg.grad_wire!r}")
+        self.flat_gw = torch.zeros(off, dtype=torch.bfloat16, device=dev) if self.cfg.grad_wire == "bf16" else None
         views_p, views_g = {}, {}
         for n, p in named:
             o, k = self.offsets[n]
@@ -277,17 +283,26 @@ class TrainEngine:
     def _allreduce(self, k: int):
         if not self.dist_on or (self.world <= 1 and not self.cfg.force_segments):
             return
-        views = [self.flat_g[a:b] for a, b in self.bucket_ranges[k]]
+        ranges = self.bucket_ranges[k]
+
+        def reduce():
+            for a, b in ranges:
+                if self.flat_gw is None:
+                    dist.all_reduce(self.flat_g[a:b], group=self.pg)
+                else:  # bf16 wire: cast, reduce, cast back (on the comm stream)
+                    w = self.flat_gw[a:b]
+                    w.copy_(self.flat_g[a:b])
+                    dist.all_reduce(w, group=self.pg)
+                    self.flat_g[a:b].copy_(w)
+
         if self.comm is not None:
             self.comm.wait_stream(torch.cuda.current_stream(self.device))
             if self.side is not None:  # the bucket's weight gradients come from the side stream
                 self.comm.wait_stream(self.side)
             with torch.cuda.stream(self.comm):
-                for v in views:
-                    dist.all_reduce(v, group=self.pg)
+                reduce()
         else:
-            for v in views:
-                dist.all_reduce(v, group=self.pg)
+            reduce()
 
     def _join_comm(self):
         if self.comm is not None:
