@@ -28,6 +28,7 @@
 #include "kernels.h"
 #include "gemm_common.h"
 #include <cstdlib>
+#include <algorithm>
 
 namespace dc {
 
@@ -772,6 +773,139 @@ __global__ __launch_bounds__(256) void gemm_wgrad_group_kernel(WgradGroup gp) {
   gemm_dma_body<64, 64, 2, 2, true, true, EPI, 4>(p, tm, local - tm * tiles_n);
 }
 
+// Grouped weight gradient, 8 waves: the two halves of the workgroup (waves 0-3
+// and 4-7) reduce the two halves of the token range of the SAME 64x64 output
+// tile through their own LDS-DMA rings (2 x 64 KiB), then half 1 hands its
+// accumulators to half 0 through LDS and half 0 writes the tile with a plain
+// read-add-write epilogue.  Twice the operand bytes in flight per CU (what the
+// 2-way atomic split bought) without fp32 atomics.
+template <int S>
+__global__ __launch_bounds__(512) void gemm_wgrad_group8_kernel(WgradGroup gp) {
+  constexpr int BMN = 64, FM = 2, FN = 2;
+  using OP = DmaOperand<64, true>;
+  constexpr int STAGE = 2 * OP::BYTES;
+  constexpr int LPT = 2 * OP::PER_WAVE;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int bid = xcd_remap(blockIdx.x, gp.tile_start[gp.n]);
+  int pi = 0;
+#pragma unroll
+  for (int j = 1; j < WG_MAX; ++j)
+    if (j < gp.n && bid >= gp.tile_start[j]) pi = j;
+  const GemmParams& p = gp.p[pi];
+  const int tiles_n = (p.N + 63) / 64;
+  const int local = bid - gp.tile_start[pi];
+  const int tm = local / tiles_n, tn = local - tm * tiles_n;
+  const int m0 = tm * BMN, n0 = tn * BMN;
+
+  const int half = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & 3);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int g = lane >> 4, li = lane & 15;
+  char* ring = smem + half * S * STAGE;
+
+  const int total_kt = (p.K + BK - 1) / BK;
+  const int h0 = (total_kt + 1) / 2;
+  const int kt0 = half ? h0 : 0;
+  const int nk = half ? total_kt - h0 : h0;
+  const int niter = h0;  // both halves run the same number of barriers
+
+  OP oa, ob;
+  oa.init(p.A, p.lda, p.K, m0, wave, lane);
+  ob.init(p.B, p.ldb, p.K, n0, wave, lane);
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool do_db = (p.bias != nullptr) && (tn == 0) && (wn == 0);
+  f32x4 dbacc[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) dbacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = f2bf(1.f);
+
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nk) {
+      oa.issue(ring + s * STAGE, kt0 + s, wave);
+      ob.issue(ring + s * STAGE + OP::BYTES, kt0 + s, wave);
+    }
+  for (int kt = 0; kt < niter; ++kt) {
+    const bool active = kt < nk;
+    if (active) vm_wait_rem<LPT>(min(S - 2, nk - 1 - kt));
+    raw_barrier();
+    if (!active) continue;
+    if (kt + S - 1 < nk) {
+      const int st = (kt + S - 1) % S;
+      oa.issue(ring + st * STAGE, kt0 + kt + S - 1, wave);
+      ob.issue(ring + st * STAGE + OP::BYTES, kt0 + kt + S - 1, wave);
+    }
+    const char* la = ring + (kt % S) * STAGE;
+    const char* lb = la + OP::BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = frag_t_swz(la, wm * 32 + i * 16, s, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = frag_t_swz(lb, wn * 32 + j * 16, s, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+      if (do_db) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) dbacc[i] = mfma16(af[i], ones, dbacc[i]);
+      }
+    }
+  }
+  // hand half 1's partial tile to half 0 through LDS (rings are done)
+  __syncthreads();
+  f32x4* xch = reinterpret_cast<f32x4*>(smem);  // [FM*FN + FM][256 lanes]
+  const int t = threadIdx.x & 255;
+  if (half == 1) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) xch[(i * FN + j) * 256 + t] = acc[i][j];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) xch[(FM * FN + i) * 256 + t] = dbacc[i];
+  }
+  __syncthreads();
+  if (half == 1) return;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] += xch[(i * FN + j) * 256 + t];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) dbacc[i] += xch[(FM * FN + i) * 256 + t];
+
+  if (do_db && li == 0) {
+    float* db = const_cast<float*>(p.bias);
+    float old[FM][4];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 32 + i * 16 + 4 * g + r;
+        old[i][r] = m < p.M ? db[m] : 0.f;
+      }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 32 + i * 16 + 4 * g + r;
+        if (m < p.M) db[m] = old[i][r] + dbacc[i][r];
+      }
+  }
+  run_epilogue_vec<EPI_ACC, FM, FN>(p, acc, m0 + wm * 32, n0 + wn * 32, g, li);
+}
+template __global__ void gemm_wgrad_group8_kernel<4>(WgradGroup);
+
 template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EPI>
 static void launch_dma(GemmParams p, int splits, hipStream_t stream) {
   const int total_kt = (p.K + BK - 1) / BK;
@@ -989,12 +1123,19 @@ void gemm_wgrad_group(const GemmArgs* probs, int n, int splits, hipStream_t stre
     gp.p[i] = base_params(probs[i]);
     check_vec(gp.p[i], EPI_ATOMIC);
     const int kt = (gp.p[i].K + BK - 1) / BK;
-    gp.p[i].ktiles_per_split = (kt + splits - 1) / splits;
+    gp.p[i].ktiles_per_split = (kt + std::max(splits, 1) - 1) / std::max(splits, 1);
     gp.tile_start[i] = tiles;
     tiles += ((gp.p[i].M + 63) / 64) * ((gp.p[i].N + 63) / 64);
   }
   for (int i = n; i <= WG_MAX; ++i) gp.tile_start[i] = tiles;
   constexpr int lds = 4 * (64 * 128 + 64 * 128);
+  if (splits == 0) {  // 8-wave two-half kernel (no atomics)
+    static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_wgrad_group8_kernel<4>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 2 * lds) == hipSuccess;
+    (void)attr;
+    hipLaunchKernelGGL(gemm_wgrad_group8_kernel<4>, dim3(tiles), dim3(512), 2 * lds, stream, gp);
+    return;
+  }
   if (splits == 1)
     hipLaunchKernelGGL(gemm_wgrad_group_kernel<EPI_ACC>, dim3(tiles, 1, 1), dim3(256), lds, stream, gp);
   else
