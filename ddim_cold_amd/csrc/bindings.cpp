@@ -397,14 +397,17 @@ void linear_wgrad_group(std::vector<Tensor> dys, std::vector<Tensor> xs, std::ve
   }();
   // measured (graph-timed, block group 216 tiles): unsplit 25.8 us, 2-way 14.9, 3-way 20.6, 4-way 19.6:
   // one 64 KiB-LDS workgroup per CU cannot keep enough K tiles in flight, two can
+  // measured: 18.1 us (8-wave) vs 15.0 us (2-way atomic split) per block group ->
+  // opt-in (DDIM_COLD_WGRAD_GROUP8=1): two independently scheduled workgroups per CU
+  // hide latency better than one 8-wave workgroup whose halves share every barrier
   static const bool eight = [] {
     const char* e = getenv("DDIM_COLD_WGRAD_GROUP8");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   int splits = forced > 0 ? forced : (tiles >= 160 ? 2 : std::min(8, (256 + tiles - 1) / tiles));
   splits = std::max(1, std::min(splits, min_kt));
-  // full block groups: the 8-wave two-half kernel (same in-flight bytes as the
-  // 2-way split, no atomics); splits = 0 selects it
+  // full block groups, opt-in: the 8-wave two-half kernel (same in-flight bytes
+  // as the 2-way split, no atomics); splits = 0 selects it
   if (eight && forced <= 0 && tiles >= 160 && min_kt >= 2) splits = 0;
   for (size_t i0 = 0; i0 < n; i0 += 6) {
     const int cnt = (int)std::min<size_t>(6, n - i0);

@@ -235,6 +235,20 @@ def test_linear_residual_ln(M, D, K, N, pd, pdp):
 
 @pytest.mark.parametrize("big", [True, False])
 def test_linear_wgrad_group(big):
+    _wgrad_group_check(big)
+
+
+def test_linear_wgrad_group_8wave():
+    """The opt-in 8-wave two-half kernel, in a child process (the switch is read once)."""
+    import subprocess, sys, os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", __file__, "-k",
+                        "test_linear_wgrad_group and not 8wave"], capture_output=True, text=True, timeout=600,
+                       cwd=root, env=dict(os.environ, DDIM_COLD_WGRAD_GROUP8="1", PYTHONPATH=root))
+    assert r.returncode == 0, r.stdout[-3000:]
+
+
+def _wgrad_group_check(big):
     """Grouped launch == per-problem reference (unsplit read-add-write and split atomic paths)."""
     M = 2080
     shapes = [(1152, 384), (384, 384), (384, 384), (384, 384), (192, 384)] if big else [(384, 192), (64, 96)]
