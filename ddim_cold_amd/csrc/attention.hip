@@ -334,6 +334,183 @@ template __global__ void attn_fwd_flash2_kernel<64, true>(const bf16*, bf16*, fl
 template __global__ void attn_fwd_flash2_kernel<64, false>(const bf16*, bf16*, float*, int, int, int, float,
                                                            const int64_t*, int, uint32_t, float);
 
+// ============================================================================ forward, medium sequences
+// Resident-KV forward (128 < N <= 320, e.g. the 257-token OxfordFlower config):
+// one workgroup per (b, h) stages the head's WHOLE K and V once (dynamic LDS,
+// padded rows), then each of ceil(N/32) waves runs an online softmax over
+// 64-key chunks for its 32 queries with no barrier in the loop.  B*H
+// workgroups (one round on 256 CUs for B*H <= 256) instead of ceil(N/64)*B*H
+// tiles that re-stage K/V per 64 keys.
+template <int HD, bool DROP>
+__global__ __launch_bounds__(640) void attn_fwd_resident_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                                float* __restrict__ lse, int B, int H, int N,
+                                                                float scale, const int64_t* __restrict__ rng,
+                                                                int site, uint32_t thr, float dsc) {
+  using C = AC<HD>;
+  extern __shared__ __attribute__((aligned(16))) char dyn[];
+  const int NP = (N + 63) / 64 * 64;  // keys padded to whole 64-key chunks
+  char* Kl = dyn;
+  char* Vl = dyn + NP * C::S;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const size_t mat = (size_t)N * HD;
+  const bf16* qb = qkv + (size_t)bh * mat;
+  const bf16* kb = qkv + ((size_t)B * H + bh) * mat;
+  const bf16* vb = qkv + ((size_t)2 * B * H + bh) * mat;
+  const int nt = blockDim.x;
+  // stage K and V: 8 chunks of 16 B in flight per thread per batch
+  const int total = NP * C::CPR;
+  for (int c0 = threadIdx.x; c0 < total; c0 += 8 * nt) {
+    u32x4 kv[8], vv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int c = c0 + u * nt;
+      const int r = c / C::CPR, cc = c - r * C::CPR;
+      const int rr = r < N ? r : N - 1;
+      const u32x4 z = {0u, 0u, 0u, 0u};
+      const bool ok = c < total && r < N;
+      kv[u] = ok ? *reinterpret_cast<const u32x4*>(kb + (size_t)rr * HD + cc * 8) : z;
+      vv[u] = ok ? *reinterpret_cast<const u32x4*>(vb + (size_t)rr * HD + cc * 8) : z;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int c = c0 + u * nt;
+      if (c < total) {
+        const int r = c / C::CPR, cc = c - r * C::CPR;
+        *reinterpret_cast<u32x4*>(Kl + r * C::S + cc * 16) = kv[u];
+        *reinterpret_cast<u32x4*>(Vl + r * C::S + cc * 16) = vv[u];
+      }
+    }
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
+  const int qbase = wave * 32;
+  bf16x8 qf[2][C::KS];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) qf[u][s] = frag_glb<HD>(qb, qbase + 16 * u + li, N, s, g);
+  const uint32_t salt = DROP ? site_salt(rng, site) : 0u;
+  const float sl2 = scale * LOG2E;
+  __syncthreads();
+
+  f32x4 o[2][C::DT];
+  float m_run[2], l_run[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    m_run[u] = -INFINITY;
+    l_run[u] = 0.f;
+#pragma unroll
+    for (int d = 0; d < C::DT; ++d) o[u][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int kv0 = 0; kv0 < N; kv0 += 64) {
+    const char* Kc = Kl + kv0 * C::S;
+    const char* Vc = Vl + kv0 * C::S;
+    f32x4 st[2][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      st[0][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      st[1][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) {
+        const bf16x8 kf = frag_row<HD>(Kc, 16 * t + li, s, g);
+        st[0][t] = mfma16(kf, qf[0][s], st[0][t]);
+        st[1][t] = mfma16(kf, qf[1][s], st[1][t]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = qbase + 16 * u + li;
+      float mt = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = (kv0 + 16 * t + 4 * g + r) < N ? st[u][t][r] * sl2 : -INFINITY;
+          st[u][t][r] = v;
+          mt = fmaxf(mt, v);
+        }
+      mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float m_new = fmaxf(m_run[u], mt);
+      const float alpha = exp2f(m_run[u] - m_new);
+      const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * N + kv0);
+      float ls = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float pv = exp2f(st[u][t][r] - m_new);
+          ls += pv;
+          if (DROP) pv = dropout_keep(salt, rowidx + (uint32_t)(16 * t + 4 * g + r), thr) ? pv * dsc : 0.f;
+          st[u][t][r] = pv;
+        }
+      ls += __shfl_xor(ls, 16, 64);
+      ls += __shfl_xor(ls, 32, 64);
+      l_run[u] = l_run[u] * alpha + ls;
+      m_run[u] = m_new;
+#pragma unroll
+      for (int d = 0; d < C::DT; ++d) o[u][d] *= alpha;
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 pb0 = pack8(st[0][2 * s2], st[0][2 * s2 + 1]);
+      const bf16x8 pb1 = pack8(st[1][2 * s2], st[1][2 * s2 + 1]);
+#pragma unroll
+      for (int d = 0; d < C::DT; ++d) {
+        const bf16x8 vf = frag_t<C::S>(Vc, 16 * d, s2, lane);
+        o[0][d] = mfma16(vf, pb0, o[0][d]);
+        o[1][d] = mfma16(vf, pb1, o[1][d]);
+      }
+    }
+  }
+  const int D = H * HD;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int q = qbase + 16 * u + li;
+    if (q < N) {
+      const float inv = 1.f / l_run[u];
+      bf16* orow = out + ((size_t)b * N + q) * D + h * HD;
+#pragma unroll
+      for (int d = 0; d < C::DT; ++d) {
+        bf16x4 v;
+        v[0] = f2bf(o[u][d][0] * inv); v[1] = f2bf(o[u][d][1] * inv);
+        v[2] = f2bf(o[u][d][2] * inv); v[3] = f2bf(o[u][d][3] * inv);
+        *reinterpret_cast<bf16x4*>(orow + 16 * d + 4 * g) = v;
+      }
+      if (g == 0) lse[(size_t)bh * N + q] = (m_run[u] + log2f(l_run[u])) * LN2;
+    }
+  }
+}
+template __global__ void attn_fwd_resident_kernel<32, true>(const bf16*, bf16*, float*, int, int, int, float,
+                                                            const int64_t*, int, uint32_t, float);
+template __global__ void attn_fwd_resident_kernel<32, false>(const bf16*, bf16*, float*, int, int, int, float,
+                                                             const int64_t*, int, uint32_t, float);
+template __global__ void attn_fwd_resident_kernel<64, true>(const bf16*, bf16*, float*, int, int, int, float,
+                                                            const int64_t*, int, uint32_t, float);
+template __global__ void attn_fwd_resident_kernel<64, false>(const bf16*, bf16*, float*, int, int, int, float,
+                                                             const int64_t*, int, uint32_t, float);
+
+template <int HD>
+static void launch_resident(const bf16* q, bf16* out, float* lse, int B, int H, int N, float scale,
+                            const int64_t* rng, int site, uint32_t thr, float dsc, hipStream_t stream) {
+  const int waves = (N + 31) / 32;
+  const int NP = (N + 63) / 64 * 64;
+  const int lds = 2 * NP * AC<HD>::S;
+  static bool attr = [] {
+    bool ok = true;
+    for (const void* f : {reinterpret_cast<const void*>(&attn_fwd_resident_kernel<HD, true>),
+                          reinterpret_cast<const void*>(&attn_fwd_resident_kernel<HD, false>)})
+      ok = ok && hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+    return ok;
+  }();
+  (void)attr;
+  if (thr)
+    hipLaunchKernelGGL((attn_fwd_resident_kernel<HD, true>), dim3(B * H), dim3(64 * waves), lds, stream, q, out, lse,
+                       B, H, N, scale, rng, site, thr, dsc);
+  else
+    hipLaunchKernelGGL((attn_fwd_resident_kernel<HD, false>), dim3(B * H), dim3(64 * waves), lds, stream, q, out, lse,
+                       B, H, N, scale, rng, site, thr, dsc);
+}
+
 // ============================================================================ backward: dQ (+delta)
 template <int HD>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ qkv,
@@ -866,6 +1043,17 @@ void attn_fwd_launch(const void* qkv, void* o, float* lse, int B, int H, int N, 
     const char* e = getenv("DDIM_COLD_ATTN_FLASH_V1");
     return e && e[0] == '1';
   }();
+  static const bool no_resident = [] {
+    const char* e = getenv("DDIM_COLD_ATTN_NO_RESIDENT");
+    return e && e[0] == '1';
+  }();
+  // one workgroup per head: needs ~a workgroup per CU to pay off.  Measured N=257
+  // hd=64: B*H=256 20.1 vs 31.9 us (v1); B*H=128 equal without dropout, 27 vs 22 with
+  if (!v1 && !no_resident && N <= 320 && B * H >= 192 && (hd == 32 || hd == 64)) {
+    if (hd == 32) launch_resident<32>(q, out, lse, B, H, N, scale, rng, site, thr, dsc, stream);
+    else launch_resident<64>(q, out, lse, B, H, N, scale, rng, site, thr, dsc, stream);
+    return;
+  }
   // v2 has half the workgroups of v1: measured better from ~600 tokens (N=626:
   // 63 vs 71 us without dropout), worse at N=257 with dropout (25 vs 22 us)
   const bool use_v2 = !v1 && N >= 384;

@@ -276,6 +276,8 @@ def _wgrad_group_check(big):
                                         # short-sequence path (N <= 128): every padded size, both head dims
                                         (2, 3, 100, 64, 0.1), (3, 5, 128, 32, 0.1), (2, 2, 64, 64, 0.0),
                                         (2, 4, 32, 32, 0.1), (2, 4, 33, 64, 0.0), (8, 4, 97, 32, 0.0),
+                                        # resident-KV forward (128 < N <= 320, B*H >= 192)
+                                        (48, 4, 257, 64, 0.1), (16, 12, 200, 32, 0.0),
                                         # flash v2 (N >= 384)
                                         (1, 2, 400, 32, 0.1), (2, 3, 513, 64, 0.0)])
 def test_attention_fwd_bwd(B, H, N, hd, p):

@@ -7,7 +7,7 @@ from tools.ubench import t
 dev = "cuda"
 r = torch.tensor([1, 2], dtype=torch.int64, device=dev)
 res = {}
-for (B, H, N, hd) in [(32, 12, 65, 32), (32, 4, 257, 64), (32, 6, 626, 64)]:
+for (B, H, N, hd) in [(32, 12, 65, 32), (32, 4, 257, 64), (64, 4, 257, 64), (32, 6, 626, 64)]:
     qkv = (torch.randn(3, B, H, N, hd, device=dev) * 0.5).to(torch.bfloat16)
     do = (torch.randn(B, N, H * hd, device=dev)).to(torch.bfloat16)
     for p in (0.0, 0.1):
