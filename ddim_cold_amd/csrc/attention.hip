@@ -519,9 +519,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
                                                           int H, int N, float scale, const int64_t* __restrict__ rng,
                                                           int site, uint32_t thr, float dsc) {
   using C = AC<HD>;
-  __shared__ __attribute__((aligned(16))) char lds[2 * C::TILE];
-  char* Kl = lds;
-  char* Vl = lds + C::TILE;
+  __shared__ __attribute__((aligned(16))) char lds[4 * C::TILE];  // [buf][K | V], double-buffered
   const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
   const int D = H * HD;
   const size_t mat = (size_t)N * HD;
@@ -531,6 +529,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
   const int q = blockIdx.x * 64 + wave * 16 + li;
   const bool qv = q < N;
+  KvStage<HD> stg;
+  stg.load(kb, vb, 0, N);
   const float sl2 = scale * LOG2E;
   const uint32_t salt = thr ? site_salt(rng, site) : 0u;
 
@@ -563,11 +563,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
 #pragma unroll
   for (int d = 0; d < C::DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int kv0 = 0; kv0 < N; kv0 += 64) {
-    __syncthreads();
-    stage64<HD>(Kl, kb, kv0, N);
-    stage64<HD>(Vl, vb, kv0, N);
-    __syncthreads();
+  stg.store(lds, lds + C::TILE);
+  __syncthreads();
+  const int ntiles = (N + 63) / 64;
+  for (int it = 0; it < ntiles; ++it) {
+    const int kv0 = it * 64;
+    const bool more = it + 1 < ntiles;
+    if (more) stg.load(kb, vb, kv0 + 64, N);  // next tile lands during this tile's MFMAs
+    const char* Kl = lds + (it & 1) * 2 * C::TILE;
+    const char* Vl = Kl + C::TILE;
     f32x4 ds[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -595,6 +599,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
 #pragma unroll
       for (int d = 0; d < C::DT; ++d) dq[d] = mfma16(frag_t<C::S>(Kl, 16 * d, s2, lane), sb, dq[d]);
     }
+    if (more) stg.store(lds + ((it + 1) & 1) * 2 * C::TILE, lds + ((it + 1) & 1) * 2 * C::TILE + C::TILE);
+    __syncthreads();
   }
   if (qv) {
     bf16* row = dqkv + ((size_t)b * N + q) * (3 * D) + h * HD;
@@ -618,10 +624,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
                                                            const int64_t* __restrict__ rng, int site, uint32_t thr,
                                                            float dsc) {
   using C = AC<HD>;
-  __shared__ __attribute__((aligned(16))) char lds[2 * C::TILE];
-  __shared__ float s_lse[64], s_del[64];
-  char* Ql = lds;
-  char* Dl = lds + C::TILE;
+  __shared__ __attribute__((aligned(16))) char lds[4 * C::TILE];  // [buf][Q | dO], double-buffered
+  __shared__ float s_lse[2][64], s_del[2][64];
   const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
   const int D = H * HD;
   const size_t mat = (size_t)N * HD;
@@ -646,22 +650,59 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
     dv[d] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
-  for (int q0 = 0; q0 < N; q0 += 64) {
-    __syncthreads();
-    stage64<HD>(Ql, qb, q0, N);
-    // dO rows (token-major, head slice) into the padded image
-    for (int c = threadIdx.x; c < 64 * C::CPR; c += 256) {
-      const int r = c / C::CPR, cc = c % C::CPR;
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (q0 + r < N) v = *reinterpret_cast<const u32x4*>(dout + ((size_t)b * N + q0 + r) * D + h * HD + cc * 8);
-      *reinterpret_cast<u32x4*>(Dl + r * C::S + cc * 16) = v;
+  // register-staged prefetch of the next query tile: Q rows (head-major), dO rows
+  // (token-major, head slice), LSE and delta
+  constexpr int PER = 64 * C::CPR / 256;
+  u32x4 rq[PER], rd[PER];
+  float rl = INFINITY, rdl = 0.f;
+  auto load_tile = [&](int q0) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = threadIdx.x + i * 256;
+      const int r = c / C::CPR, cc = c - r * C::CPR;
+      const int rr = q0 + r < N ? q0 + r : N - 1;
+      const u32x4 z = {0u, 0u, 0u, 0u};
+      const u32x4 qv4 = *reinterpret_cast<const u32x4*>(qb + (size_t)rr * HD + cc * 8);
+      const u32x4 dv4 = *reinterpret_cast<const u32x4*>(dout + ((size_t)b * N + rr) * D + h * HD + cc * 8);
+      rq[i] = q0 + r < N ? qv4 : z;
+      rd[i] = q0 + r < N ? dv4 : z;
     }
     if (threadIdx.x < 64) {
       const int qq = q0 + threadIdx.x;
-      s_lse[threadIdx.x] = qq < N ? lse[(size_t)bh * N + qq] * LOG2E : INFINITY;
-      s_del[threadIdx.x] = qq < N ? delta[(size_t)bh * N + qq] : 0.f;
+      const int qc = qq < N ? qq : N - 1;
+      const float l = lse[(size_t)bh * N + qc], dd = delta[(size_t)bh * N + qc];
+      rl = qq < N ? l * LOG2E : INFINITY;
+      rdl = qq < N ? dd : 0.f;
     }
-    __syncthreads();
+  };
+  auto store_tile = [&](int buf) {
+    char* ql = lds + buf * 2 * C::TILE;
+    char* dl = ql + C::TILE;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = threadIdx.x + i * 256;
+      const int r = c / C::CPR, cc = c - r * C::CPR;
+      *reinterpret_cast<u32x4*>(ql + r * C::S + cc * 16) = rq[i];
+      *reinterpret_cast<u32x4*>(dl + r * C::S + cc * 16) = rd[i];
+    }
+    if (threadIdx.x < 64) {
+      s_lse[buf][threadIdx.x] = rl;
+      s_del[buf][threadIdx.x] = rdl;
+    }
+  };
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  const int ntiles = (N + 63) / 64;
+  for (int it = 0; it < ntiles; ++it) {
+    const int q0 = it * 64;
+    const bool more = it + 1 < ntiles;
+    if (more) load_tile(q0 + 64);
+    const int buf = it & 1;
+    const char* Ql = lds + buf * 2 * C::TILE;
+    const char* Dl = Ql + C::TILE;
+    const float* sl = s_lse[buf];
+    const float* sd = s_del[buf];
     f32x4 pm[4], ds[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -675,7 +716,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
       for (int r = 0; r < 4; ++r) {
         const int qr = 16 * t + 4 * g + r;
         const int qq = q0 + qr;
-        const float pr = exp2f(st[r] * sl2 - s_lse[qr]);
+        const float pr = exp2f(st[r] * sl2 - sl[qr]);
         float pd = pr, dpv = dp[r];
         if (thr) {
           const uint32_t idx = (uint32_t)(((size_t)bh * N + qq) * N + key);
@@ -684,7 +725,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
           dpv = kp ? dpv * dsc : 0.f;
         }
         pm[t][r] = pd;
-        ds[t][r] = pr * (dpv - s_del[qr]);
+        ds[t][r] = pr * (dpv - sd[qr]);
       }
     }
 #pragma unroll
@@ -697,6 +738,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
         dk[d] = mfma16(frag_t<C::S>(Ql, 16 * d, s2, lane), sb, dk[d]);
       }
     }
+    if (more) store_tile(buf ^ 1);
+    __syncthreads();
   }
   if (key < N) {
     bf16* row = dqkv + ((size_t)b * N + key) * (3 * D) + h * HD;
