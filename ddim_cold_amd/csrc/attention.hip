@@ -778,11 +778,25 @@ struct ShortImg {
   static constexpr int PER = NP * CPR / NT;  // chunks per thread (= HD / 32)
   static constexpr int RS = 2 * HD + 32;   // padded LDS row stride (bytes)
   u32x4 v[PER];
+  // chunk c -> (row, 16-B chunk).  64-B rows (hd 32): an 8-lane ds_write_b128
+  // group takes rows r and r+2 (48 dwords apart, disjoint banks mod 32) instead
+  // of r and r+1 (2-way conflict at the 96-B stride)
+  __device__ __forceinline__ static void rc(int c, int& r, int& cc) {
+    if (CPR == 4) {
+      const int grp = c >> 3, j = c & 7;
+      r = (grp >> 1) * 4 + (grp & 1) + 2 * (j >> 2);
+      cc = j & 3;
+    } else {
+      r = c / CPR;
+      cc = c - r * CPR;
+    }
+  }
   __device__ __forceinline__ void load(const bf16* __restrict__ base, size_t ld, int N) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = threadIdx.x + i * NT;
-      const int r = c / CPR, cc = c - r * CPR;
+      int r, cc;
+      rc(c, r, cc);
       const int rr = r < N ? r : N - 1;
       const u32x4 x = *reinterpret_cast<const u32x4*>(base + (size_t)rr * ld + cc * 8);
       const u32x4 z = {0u, 0u, 0u, 0u};
@@ -793,11 +807,32 @@ struct ShortImg {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = threadIdx.x + i * NT;
-      const int r = c / CPR, cc = c - r * CPR;
+      int r, cc;
+      rc(c, r, cc);
       *reinterpret_cast<u32x4*>(img + r * RS + cc * 16) = v[i];
     }
   }
 };
+
+// [query][key] P / dS images of the short backward: 8-B column pieces XOR-ed by
+// ((row >> 2) & 3) so the 16 rows of a ds_write_b64 lane group land on distinct
+// banks; the transposed reads (4 rows sharing one XOR) stay conflict-free
+__device__ __forceinline__ int pimg_off(int row, int byte, int stride) {
+  return row * stride + (byte ^ (((row >> 2) & 3) << 3));
+}
+
+template <int STRIDE>
+__device__ __forceinline__ bf16x8 frag_t_pimg(const char* lds, int c0, int s, int lane) {
+  const int i = lane & 15, g = lane >> 4, q = i >> 2, p = i & 3;
+  const int ra = 32 * s + 4 * g + q;  // ra + 16 has the same XOR
+  const char* pa = lds + pimg_off(ra, (c0 + 4 * p) * 2, STRIDE);
+  const bf16x4 lo = lds_read_tr(reinterpret_cast<const bf16*>(pa));
+  const bf16x4 hi = lds_read_tr(reinterpret_cast<const bf16*>(pa + 16 * STRIDE));
+  bf16x8 v;
+  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  return v;
+}
 
 __device__ __forceinline__ bf16x4 pack4(const f32x4& a) {
   bf16x4 v;
@@ -965,8 +1000,8 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
       pm[r] = pd;
       ds[t][r] = pr * (dpv - dl);
     }
-    *reinterpret_cast<bf16x4*>(Pl + q * PS + (16 * t + 4 * g) * 2) = pack4(pm);
-    *reinterpret_cast<bf16x4*>(Sl + q * PS + (16 * t + 4 * g) * 2) = pack4(ds[t]);
+    *reinterpret_cast<bf16x4*>(Pl + pimg_off(q, (16 * t + 4 * g) * 2, PS)) = pack4(pm);
+    *reinterpret_cast<bf16x4*>(Sl + pimg_off(q, (16 * t + 4 * g) * 2, PS)) = pack4(ds[t]);
   }
   f32x4 dq[DT];
 #pragma unroll
@@ -994,8 +1029,8 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
   }
 #pragma unroll
   for (int s = 0; s < NP / 32; ++s) {
-    const bf16x8 pb = frag_t<PS>(Pl, 16 * wave, s, lane);
-    const bf16x8 sb = frag_t<PS>(Sl, 16 * wave, s, lane);
+    const bf16x8 pb = frag_t_pimg<PS>(Pl, 16 * wave, s, lane);
+    const bf16x8 sb = frag_t_pimg<PS>(Sl, 16 * wave, s, lane);
 #pragma unroll
     for (int d = 0; d < DT; ++d) {
       dv[d] = mfma16(frag_t<RS>(Dl, 16 * d, s, lane), pb, dv[d]);
