@@ -293,17 +293,22 @@ Tensor img_to_tokgrad(Tensor dimg, int64_t N, int64_t patch) {
   return dtok;
 }
 
-Tensor linear_dgrad(Tensor dy, Tensor w, bool out_fp32) {
+// splits > 1 (fp32 only): [splits, M, K] partial products over K slices
+Tensor linear_dgrad(Tensor dy, Tensor w, bool out_fp32, int64_t splits) {
   CHECK_IN(dy, BF16); CHECK_IN(w, BF16);
   const c10::DeviceGuard guard(dy.device());
   TORCH_CHECK(dy.dim() == 2 && w.dim() == 2 && dy.size(1) == w.size(0), "dgrad shapes");
   const int M = dy.size(0), Nout = w.size(0), K = w.size(1);
   TORCH_CHECK(Nout % 8 == 0 && K % 8 == 0, "dgrad dims must be multiples of 8");
-  auto dx = at::empty({M, K}, dy.options().dtype(out_fp32 ? F32 : BF16));
+  TORCH_CHECK(splits >= 1 && (splits == 1 || out_fp32), "dgrad K split needs fp32 output");
+  auto dx = splits > 1 ? at::empty({splits, M, K}, dy.options().dtype(F32))
+                       : at::empty({M, K}, dy.options().dtype(out_fp32 ? F32 : BF16));
   GemmArgs g;
   g.A = dy.data_ptr(); g.B = w.data_ptr();
   g.M = M; g.N = K; g.K = Nout; g.lda = Nout; g.ldb = K;
   g.C = dx.data_ptr(); g.ldc = K;
+  g.splits = (int)splits;
+  g.split_stride = (long long)M * K;
   gemm_dgrad(g, out_fp32 ? EPI_F32 : EPI_BF16, cur_stream());
   return dx;
 }
@@ -423,8 +428,10 @@ std::tuple<Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tenso
   CHECK_IN(dgamma, F32); CHECK_IN(dbeta, F32); check_rng(rng);
   const c10::DeviceGuard guard(x.device());
   const int D = x.size(-1), M = x.numel() / D;
-  TORCH_CHECK(dy.numel() == x.numel() && mean.numel() == M && rstd.numel() == M && gamma.numel() == D &&
-                  dgamma.numel() == D && dbeta.numel() == D && M % N == 0,
+  // dy may be [P, M, D]: P partial products (K-split dgrad) summed on load
+  const int parts = x.numel() > 0 ? (int)(dy.numel() / x.numel()) : 1;
+  TORCH_CHECK(dy.numel() == (int64_t)parts * x.numel() && mean.numel() == M && rstd.numel() == M &&
+                  gamma.numel() == D && dgamma.numel() == D && dbeta.numel() == D && M % N == 0 && parts <= 4,
               "layernorm_bwd shapes");
   const float* gr = nullptr;
   if (g_res.has_value() && g_res->defined()) {
@@ -444,7 +451,7 @@ std::tuple<Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tenso
   layernorm_bwd_launch(dy.data_ptr<float>(), x.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                        gamma.data_ptr<float>(), gr, g_out.data_ptr<float>(), emit_gy ? gy.data_ptr() : nullptr,
                        w.data_ptr<float>(), M, D, N, rng.data_ptr<int64_t>(), site_drop, p_drop, site_dp, p_dp,
-                       cur_stream());
+                       parts, cur_stream());
   if (own_ws) {
     auto s = w.sum(0);
     dgamma.add_(s.narrow(0, 0, D));
@@ -622,7 +629,7 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("smooth_l1_fwd_bwd(Tensor pred, Tensor target, int N, int patch, float beta, Tensor(a!)? loss_last=None, "
         "Tensor(b!)? loss_ema=None, float ema_decay=0.99) -> (Tensor, Tensor)");
   m.def("img_to_tokgrad(Tensor dimg, int N, int patch) -> Tensor");
-  m.def("linear_dgrad(Tensor dy, Tensor w, bool out_fp32) -> Tensor");
+  m.def("linear_dgrad(Tensor dy, Tensor w, bool out_fp32, int splits=1) -> Tensor");
   m.def("linear_dgrad_gelu(Tensor dy, Tensor w, Tensor u, Tensor rng, int site, float p) -> Tensor");
   m.def("linear_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, Tensor(b!)? db) -> ()");
   m.def("linear_wgrad_group(Tensor[] dys, Tensor[] xs, Tensor(a!)[] dws, Tensor(b!)?[] dbs) -> ()");

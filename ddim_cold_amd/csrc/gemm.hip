@@ -61,6 +61,7 @@ struct GemmParams {
   int emb_dim;
   int ktiles_per_split;
   const float* coef;     // HEAD mode 1: {sqrt a_t, sqrt(1-a_t), sqrt a_tk, sqrt(1-a_tk)} (device)
+  long long split_stride;  // EPI_F32: elements between the K-split output slices
   int head_mode;         // HEAD: 0 image, 1 fused DDIM step (res = x_t in, C = x_next, C2 = x0), 2 clamp
   int debug;  // profiling aid (DDIM_COLD_GEMM_DEBUG): 1 = skip the epilogue, 2 = skip the main loop,
               // 3 = scalar (untransposed) epilogue
@@ -200,7 +201,7 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, long long idx, int
   if (EPI == EPI_BF16) {
     reinterpret_cast<bf16*>(p.C)[idx] = f2bf(v);
   } else if (EPI == EPI_F32) {
-    reinterpret_cast<float*>(p.C)[idx] = v;
+    reinterpret_cast<float*>(p.C)[idx + blockIdx.z * p.split_stride] = v;
   } else if (EPI == EPI_ATOMIC) {
     atomicAdd(reinterpret_cast<float*>(p.C) + idx, v);
   } else if (EPI == EPI_ACC) {
@@ -424,7 +425,7 @@ struct VecEpi {
         if (EPI == EPI_BF16 || EPI == EPI_QKV) {
           st4bf(reinterpret_cast<bf16*>(p.C) + idx, v);
         } else if (EPI == EPI_F32) {
-          st4(reinterpret_cast<float*>(p.C) + idx, v);
+          st4(reinterpret_cast<float*>(p.C) + idx + blockIdx.z * p.split_stride, v);
         } else if (EPI == EPI_ATOMIC) {
 #pragma unroll
           for (int c = 0; c < 4; ++c) atomicAdd(reinterpret_cast<float*>(p.C) + idx + c, v[c]);
@@ -1074,6 +1075,7 @@ static GemmParams base_params(const GemmArgs& a) {
   p.chans = a.chans; p.img_h = a.img_h; p.img_w = a.img_w; p.patch = a.patch;
   p.pos = a.pos; p.temb = a.temb; p.tsteps = a.tsteps; p.emb_dim = a.emb_dim;
   p.coef = a.coef; p.head_mode = a.head_mode;
+  p.split_stride = a.split_stride;
   return p;
 }
 
@@ -1103,7 +1105,13 @@ void gemm_dgrad(const GemmArgs& a, int epi, hipStream_t stream) {
   check_vec(p, epi);
   switch (epi) {
     case EPI_BF16: launch_auto<false, true, EPI_BF16>(p, 1, stream); break;
-    case EPI_F32: launch_auto<false, true, EPI_F32>(p, 1, stream); break;
+    case EPI_F32: {
+      const int kt = (p.K + 63) / 64;
+      const int splits = std::max(1, std::min(a.splits, kt));
+      if (splits > 1 && (p.bias || (kt + splits - 1) / splits * (splits - 1) >= kt))
+        throw std::runtime_error("gemm_dgrad: K split needs no bias and a non-empty last slice");
+      launch_auto<false, true, EPI_F32>(p, splits, stream);
+    } break;
     case EPI_DGELU: launch_auto<false, true, EPI_DGELU>(p, 1, stream); break;
     default: throw std::runtime_error("gemm_dgrad: unsupported epilogue");
   }

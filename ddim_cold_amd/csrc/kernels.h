@@ -41,6 +41,10 @@ struct GemmArgs {
   int emb_dim = 0;
   const float* coef = nullptr;  // EPI_HEAD head_mode 1
   int head_mode = 0;            // EPI_HEAD: 0 image, 1 fused DDIM step, 2 clamp
+  // EPI_F32 dgrad split over K: slice z of `splits` writes its partial product to
+  // C + z * split_stride (no atomics, no zeroing; the consumer sums the slices)
+  int splits = 1;
+  long long split_stride = 0;
 };
 
 void gemm_nt(const GemmArgs& a, int epi, hipStream_t stream);
@@ -83,7 +87,7 @@ void layernorm_fwd_launch(const float* x, const float* gamma, const float* beta,
 void layernorm_bwd_launch(const float* dy, const float* x, const float* mean, const float* rstd,
                           const float* gamma, const float* g_res, float* g_out, void* gy_bf16, float* dgb_ws, int M,
                           int D, int tokens, const int64_t* rng, int site_drop, double p_drop, int site_dp,
-                          double p_dp, hipStream_t stream);
+                          double p_dp, int dy_parts, hipStream_t stream);
 int ln_replicas();
 void replica_reduce_launch(float* ws, float* const* dsts_dev, int G, int C, hipStream_t stream);
 

@@ -74,7 +74,7 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const float* __restrict
                                                      float* __restrict__ dgb_ws, int M,
                                                      int tokens, const int64_t* __restrict__ rng, int site_drop,
                                                      uint32_t thr_drop, float sc_drop, int site_dp, uint32_t thr_dp,
-                                                     float sc_dp) {
+                                                     float sc_dp, int dy_parts) {
   constexpr int D = VEC * 128;
   __shared__ float red[NW][2 * D];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -107,6 +107,15 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const float* __restrict
       xv[j][i] = xr[lane + 64 * i];
       dv[j][i] = dr[lane + 64 * i];
       rv[j][i] = g_res ? gr[lane + 64 * i] : make_float2(0.f, 0.f);
+    }
+    for (int pt = 1; pt < dy_parts; ++pt) {  // K-split dgrad partials
+      const float2* dp = dr + (size_t)pt * M * (D / 2);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        const float2 e = dp[lane + 64 * i];
+        dv[j][i].x += e.x;
+        dv[j][i].y += e.y;
+      }
     }
     muv[j] = mean[row];
     rsv[j] = rstd[row];
@@ -232,7 +241,7 @@ void layernorm_fwd_launch(const float* x, const float* gamma, const float* beta,
 void layernorm_bwd_launch(const float* dy, const float* x, const float* mean, const float* rstd,
                           const float* gamma, const float* g_res, float* g_out, void* gy_bf16, float* dgb_ws, int M,
                           int D, int tokens, const int64_t* rng, int site_drop, double p_drop, int site_dp,
-                          double p_dp, hipStream_t stream) {
+                          double p_dp, int dy_parts, hipStream_t stream) {
   if (D % 128) throw std::runtime_error("layernorm: D % 128 != 0");
   const uint32_t td = drop_threshold_host(p_drop), tp = drop_threshold_host(p_dp);
   const float sd = p_drop > 0 ? 1.f / (1.f - (float)p_drop) : 1.f;
@@ -246,7 +255,7 @@ void layernorm_bwd_launch(const float* dy, const float* x, const float* mean, co
   LN_DISPATCH(D, hipLaunchKernelGGL((ln_bwd_kernel<VEC, R, W>), dim3((M + R * W - 1) / (R * W)), dim3(W * 64), 0, \
                                     stream, dy, x, mean, rstd, gamma, g_res, g_out,                           \
                                     reinterpret_cast<bf16*>(gy_bf16), dgb_ws, M, tokens, rng, site_drop, td,   \
-                                    sd, site_dp, tp, sp))
+                                    sd, site_dp, tp, sp, dy_parts))
   // measured on the ViT-tiny shape (M 2080, D 384, dropout on): 1 row x 8 waves
   // 5.0 us, 2 x 4 5.9, 1 x 4 5.2, 1 x 16 5.1, 2 x 16 7.2
   switch (cfg) {

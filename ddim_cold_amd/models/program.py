@@ -31,6 +31,9 @@ from .. import ops
 
 SITE_EMBED = 1
 FUSE_LN = os.environ.get("DDIM_COLD_FUSE_LN", "0") == "1"  # residual GEMM + LayerNorm in one kernel
+# K split of the QKV input-gradient GEMM (reduction dim 3D): the partial products
+# go to separate buffers that the LayerNorm backward sums on load
+QKV_DGRAD_SPLITS = int(os.environ.get("DDIM_COLD_QKV_DGRAD_SPLITS", "2"))
 
 
 def block_sites(i: int):
@@ -268,7 +271,7 @@ class ViTProgram:
             do = ops.linear_dgrad(gy1, bp.proj_w, False)
             dqkv = ops.attn_bwd(do, qkv, o, lse, c.scale, rng, sa, ad)
             wgrad(dqkv, l1, bg.qkv_w, bg.qkv_b)
-            dl1 = ops.linear_dgrad(dqkv, bp.qkv_w, True)
+            dl1 = ops.linear_dgrad(dqkv, bp.qkv_w, True, QKV_DGRAD_SPLITS if 3 * D >= 768 else 1)
             if i > 0:
                 _, _, _, _, psf2, psd2 = block_sites(i - 1)
                 g, gy = ops.layernorm_bwd(dl1, x0, m1, r1, bp.n1w, g1, bg.n1w, bg.n1b, N, rng, psf2, pd, psd2,

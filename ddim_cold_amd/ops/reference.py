@@ -222,8 +222,15 @@ def smooth_l1_fwd_bwd(pred, target, N: int, patch: int, beta: float = 1.0):
 
 
 # ----------------------------------------------------------------------------- backward ops
-def linear_dgrad(dy, w, out_fp32: bool):
-    """dx = dy @ W  (W in nn.Linear layout [N_out, K])."""
+def linear_dgrad(dy, w, out_fp32: bool, splits: int = 1):
+    """dx = dy @ W  (W in nn.Linear layout [N_out, K]).  ``splits`` > 1: the
+    [splits, M, K] partial products over 64-aligned slices of N_out, as the
+    K-split kernel writes them (their sum is dx)."""
+    if splits > 1:
+        kt = (dy.shape[1] + 63) // 64
+        step = (kt + splits - 1) // splits * 64
+        return torch.stack([dy[:, z * step:(z + 1) * step].float() @ w[z * step:(z + 1) * step].float()
+                            for z in range(splits)])
     dx = dy.float() @ w.float()
     return dx if out_fp32 else bf16(dx)
 
@@ -247,7 +254,7 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dgamma, dbeta, N: int, rng,
     """g_out = g_res + LN^T(dy);  dgamma/dbeta += ...;  gy = bf16(g_out * branch masks)."""
     M, D = x.shape[0] * (x.shape[1] if x.dim() == 3 else 1), x.shape[-1]
     xf = x.reshape(M, D).float()
-    dyf = dy.reshape(M, D).float()
+    dyf = dy.reshape(-1, M, D).float().sum(0)  # K-split dgrad partials summed
     xhat = (xf - mean.reshape(M, 1)) * rstd.reshape(M, 1)
     dgamma.add_((dyf * xhat).sum(0))
     dbeta.add_(dyf.sum(0))

@@ -194,3 +194,24 @@ def test_param_sync_check_detects_divergence():
         out = os.path.join(d, "r.pt")
         mp.start_processes(_sync_worker, args=(2, free_port(), out), nprocs=2, join=True, start_method="spawn")
         assert torch.load(out, weights_only=True)["detected"]
+
+
+def test_reference_ksplit_dgrad_and_ln_partials():
+    """K-split dgrad partials (64-aligned slices of the reduction dim) sum to the
+    full product, and the LayerNorm backward accepts the stacked partials."""
+    from ddim_cold_amd.ops import reference as ref
+    torch.manual_seed(0)
+    dy = torch.randn(40, 200).to(torch.bfloat16)
+    w = torch.randn(200, 128).to(torch.bfloat16)
+    parts = ref.linear_dgrad(dy, w, True, 3)
+    assert parts.shape == (3, 40, 128)
+    torch.testing.assert_close(parts.sum(0), ref.linear_dgrad(dy, w, True), rtol=1e-5, atol=1e-4)
+    x = torch.randn(40, 128)
+    g, b = torch.randn(128), torch.randn(128)
+    _, mu, rs = ref.layernorm_fwd(x, g, b)
+    r = torch.tensor([1, 2], dtype=torch.int64)
+    z = [torch.zeros(128) for _ in range(4)]
+    a, _ = ref.layernorm_bwd(parts, x, mu, rs, g, None, z[0], z[1], 40, r, 0, 0.0, 0, 0.0, False)
+    e, _ = ref.layernorm_bwd(parts.sum(0), x, mu, rs, g, None, z[2], z[3], 40, r, 0, 0.0, 0, 0.0, False)
+    torch.testing.assert_close(a, e)
+    torch.testing.assert_close(z[0], z[2])

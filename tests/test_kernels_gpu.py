@@ -183,6 +183,29 @@ def test_dgrad(M, Nout, K):
         close(dx, dxr, 2e-2 if not fp32 else 1e-3, 1e-2, f"dgrad fp32={fp32}")
 
 
+@pytest.mark.parametrize("M,Nout,K,splits", [(2080, 1152, 384, 2), (2080, 1152, 384, 3), (300, 768, 256, 4),
+                                             (100, 200, 48, 2)])
+def test_dgrad_ksplit(M, Nout, K, splits):
+    """K-split dgrad: per-slice partial products (no atomics) and the LayerNorm
+    backward summing them on load."""
+    dy = bf(M, Nout)
+    w = bf(Nout, K, scale=0.05)
+    dx = ops.linear_dgrad(dy, w, True, splits)
+    dxr = ref.linear_dgrad(dy, w, True, splits)
+    assert dx.shape == (splits, M, K)
+    close(dx, dxr, 1e-3, 1e-2, "dgrad slices")
+    close(dx.sum(0), ref.linear_dgrad(dy, w, True), 1e-3, 1e-2, "dgrad sum")
+    if K % 128 == 0:
+        x = torch.randn(M, K, device=DEV)
+        g, b = torch.randn(K, device=DEV), torch.randn(K, device=DEV)
+        _, mu, rs = ref.layernorm_fwd(x, g, b)
+        dg1, db1, dg2, db2 = (torch.zeros(K, device=DEV) for _ in range(4))
+        go, _ = ops.layernorm_bwd(dx, x, mu, rs, g, None, dg1, db1, M, rng(), 0, 0.0, 0, 0.0, False)
+        gor, _ = ref.layernorm_bwd(dx.sum(0), x, mu, rs, g, None, dg2, db2, M, rng(), 0, 0.0, 0, 0.0, False)
+        close(go, gor, 1e-4, 1e-4, "ln g_out (summed partials)")
+        close(dg1, dg2, 1e-2, 1e-4, "ln dgamma (summed partials)")
+
+
 def test_dgrad_gelu():
     M, N, K = 2080, 384, 384
     dy, w, u = bf(M, N), bf(N, K, scale=0.05), bf(M, K)
