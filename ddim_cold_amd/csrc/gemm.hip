@@ -687,19 +687,28 @@ __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int t
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       bf16x8 af[FM], bfr[FN];
+      TrFrag ta[FM], tb[FN];  // transposed reads: all issued, then one wait
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int r = wm * TM + i * 16;
-        if (AT) af[i] = frag_t_swz(la, r, s, lane);
+        if (AT) ta[i] = frag_t_swz_issue(la, r, s, lane);
         else if (PERM) af[i] = frag_k_perm(la, r + li, s, g);
         else af[i] = frag_k(la, r + li, s, g);
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int r = wn * TN + j * 16;
-        if (BT) bfr[j] = frag_t_swz(lb, r, s, lane);
+        if (BT) tb[j] = frag_t_swz_issue(lb, r, s, lane);
         else if (PERM) bfr[j] = frag_k_perm(lb, r + li, s, g);
         else bfr[j] = frag_k(lb, r + li, s, g);
+      }
+      if (AT) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[i] = frag_t_fence(ta[i]);
+      }
+      if (BT) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bfr[j] = frag_t_fence(tb[j]);
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
@@ -760,7 +769,7 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(GemmParams p) {
 // (the four linears of a transformer block, plus the head / patch embedding)
 // in ONE launch.  Tiles of all problems share the grid (XCD-aware), blockIdx.z
 // is the token (K) split of every problem.
-template <int EPI>
+template <int EPI, int S>
 __global__ __launch_bounds__(256) void gemm_wgrad_group_kernel(WgradGroup gp) {
   const int bid = xcd_remap(blockIdx.x, gp.tile_start[gp.n]);
   int i = 0;
@@ -771,7 +780,7 @@ __global__ __launch_bounds__(256) void gemm_wgrad_group_kernel(WgradGroup gp) {
   const int tiles_n = (p.N + 63) / 64;
   const int local = bid - gp.tile_start[i];
   const int tm = local / tiles_n;
-  gemm_dma_body<64, 64, 2, 2, true, true, EPI, 4>(p, tm, local - tm * tiles_n);
+  gemm_dma_body<64, 64, 2, 2, true, true, EPI, S>(p, tm, local - tm * tiles_n);
 }
 
 // Grouped weight gradient, 8 waves: the two halves of the workgroup (waves 0-3
@@ -1041,8 +1050,12 @@ DC_INST_DMA2(false, true, EPI_BF16)
 DC_INST_DMA2(false, true, EPI_F32)
 DC_INST_DMA2(false, true, EPI_DGELU)
 DC_INST_DMA(64, true, true, EPI_ATOMIC)
-template __global__ void gemm_wgrad_group_kernel<EPI_ATOMIC>(WgradGroup);
-template __global__ void gemm_wgrad_group_kernel<EPI_ACC>(WgradGroup);
+template __global__ void gemm_wgrad_group_kernel<EPI_ATOMIC, 4>(WgradGroup);
+template __global__ void gemm_wgrad_group_kernel<EPI_ACC, 4>(WgradGroup);
+template __global__ void gemm_wgrad_group_kernel<EPI_ATOMIC, 6>(WgradGroup);
+template __global__ void gemm_wgrad_group_kernel<EPI_ACC, 6>(WgradGroup);
+template __global__ void gemm_wgrad_group_kernel<EPI_ATOMIC, 8>(WgradGroup);
+template __global__ void gemm_wgrad_group_kernel<EPI_ACC, 8>(WgradGroup);
 
 }  // namespace dc
 
@@ -1145,8 +1158,27 @@ void gemm_wgrad_group(const GemmArgs* probs, int n, int splits, hipStream_t stre
     hipLaunchKernelGGL(gemm_wgrad_group8_kernel<4>, dim3(tiles), dim3(512), 2 * lds, stream, gp);
     return;
   }
-  if (splits == 1)
-    hipLaunchKernelGGL(gemm_wgrad_group_kernel<EPI_ACC>, dim3(tiles, 1, 1), dim3(256), lds, stream, gp);
-  else
-    hipLaunchKernelGGL(gemm_wgrad_group_kernel<EPI_ATOMIC>, dim3(tiles, 1, splits), dim3(256), lds, stream, gp);
+  // LDS-DMA ring depth (DDIM_COLD_WGRAD_S = 4 / 6 / 8): the token-reduction loop
+  // is bound by operand bytes in flight per CU
+  static const int ring = [] {
+    const char* e = getenv("DDIM_COLD_WGRAD_S");
+    const int v = e ? atoi(e) : 4;
+    return v >= 8 ? 8 : v >= 6 ? 6 : 4;
+  }();
+  const int slds = ring * (64 * 128 + 64 * 128);
+  auto go = [&](auto kern) {
+    static_assert(true, "");
+    if (slds > 65536)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, slds);
+    hipLaunchKernelGGL(kern, dim3(tiles, 1, std::max(splits, 1)), dim3(256), slds, stream, gp);
+  };
+  if (splits == 1) {
+    if (ring == 8) go(gemm_wgrad_group_kernel<EPI_ACC, 8>);
+    else if (ring == 6) go(gemm_wgrad_group_kernel<EPI_ACC, 6>);
+    else go(gemm_wgrad_group_kernel<EPI_ACC, 4>);
+  } else {
+    if (ring == 8) go(gemm_wgrad_group_kernel<EPI_ATOMIC, 8>);
+    else if (ring == 6) go(gemm_wgrad_group_kernel<EPI_ATOMIC, 6>);
+    else go(gemm_wgrad_group_kernel<EPI_ATOMIC, 4>);
+  }
 }

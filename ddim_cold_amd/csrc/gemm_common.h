@@ -25,9 +25,11 @@ __device__ __forceinline__ bf16x8 frag_k_perm(const char* lds, int r, int s, int
   u32x4 v = {lo[0], lo[1], hi[0], hi[1]};
   return __builtin_bit_cast(bf16x8, v);
 }
+// wait until at most N vector-memory ops are outstanding (clamped to the
+// 6-bit vmcnt field: waiting for fewer is still correct, just stricter)
 template <int N>
 __device__ __forceinline__ void vm_wait() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N < 63 ? N : 63) : "memory");
 }
 template <int LPT>
 __device__ __forceinline__ void vm_wait_rem(int rem) {
@@ -36,7 +38,9 @@ __device__ __forceinline__ void vm_wait_rem(int rem) {
     case 1: vm_wait<LPT>(); break;
     case 2: vm_wait<2 * LPT>(); break;
     case 3: vm_wait<3 * LPT>(); break;
-    default: vm_wait<4 * LPT>(); break;
+    case 4: vm_wait<4 * LPT>(); break;
+    case 5: vm_wait<5 * LPT>(); break;
+    default: vm_wait<6 * LPT>(); break;
   }
 }
 __device__ __forceinline__ void raw_barrier() {
@@ -44,17 +48,42 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
-__device__ __forceinline__ bf16x8 frag_t_swz(const char* lds, int c0, int s, int lane) {
+// Transposed-image fragment reads for the LDS-DMA GEMMs.  ds_read_b64_tr_b16 is
+// issued from inline asm: through the builtin, hipcc (ROCm 7.2) treats the read
+// as aliasing every in-flight LDS-DMA and emits s_waitcnt vmcnt(0) before it,
+// draining the whole ring each k-step (found in the .s of every transposed-
+// operand GEMM).  The asm read is invisible to the compiler's counters, so the
+// caller waits explicitly: issue the reads (frag_t_swz_issue), then
+// frag_t_fence() on every fragment before its first use.
+struct TrFrag {
+  bf16x4 lo, hi;
+};
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const DC_LDS char*)(p);
+}
+__device__ __forceinline__ TrFrag frag_t_swz_issue(const char* lds, int c0, int s, int lane) {
   const int i = lane & 15, g = lane >> 4, q = i >> 2, p = i & 3;
   const int ra = 32 * s + 4 * g + q;
   const int chunk = (c0 >> 3) + (p >> 1);
   const int off = ra * 128 + 16 * (chunk ^ (ra & 6)) + 8 * (p & 1);
-  const bf16x4 lo = lds_read_tr(reinterpret_cast<const bf16*>(lds + off));
-  const bf16x4 hi = lds_read_tr(reinterpret_cast<const bf16*>(lds + off + 16 * 128));
+  TrFrag f;
+  const uint32_t a = lds_addr(lds + off);
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(f.lo) : "v"(a));
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:2048" : "=v"(f.hi) : "v"(a));
+  return f;
+}
+// wait for every outstanding LDS read, tied to the fragment so no use of it can
+// be scheduled above the wait
+__device__ __forceinline__ bf16x8 frag_t_fence(TrFrag& f) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f.lo), "+v"(f.hi));
   bf16x8 v;
-  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
-  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  v[0] = f.lo[0]; v[1] = f.lo[1]; v[2] = f.lo[2]; v[3] = f.lo[3];
+  v[4] = f.hi[0]; v[5] = f.hi[1]; v[6] = f.hi[2]; v[7] = f.hi[3];
   return v;
+}
+__device__ __forceinline__ bf16x8 frag_t_swz(const char* lds, int c0, int s, int lane) {
+  TrFrag f = frag_t_swz_issue(lds, c0, s, lane);
+  return frag_t_fence(f);
 }
 
 template <int R, bool T>

@@ -261,13 +261,18 @@ def test_linear_wgrad_group(big):
     _wgrad_group_check(big)
 
 
-def test_linear_wgrad_group_8wave():
-    """The opt-in 8-wave two-half kernel, in a child process (the switch is read once)."""
+@pytest.mark.parametrize("env", [{"DDIM_COLD_WGRAD_GROUP8": "1"},
+                                 {"DDIM_COLD_WGRAD_S": "8", "DDIM_COLD_WGRAD_GROUP_SPLITS": "1"},
+                                 {"DDIM_COLD_WGRAD_S": "8", "DDIM_COLD_WGRAD_GROUP_SPLITS": "2"},
+                                 {"DDIM_COLD_WGRAD_S": "6", "DDIM_COLD_WGRAD_GROUP_SPLITS": "3"}])
+def test_linear_wgrad_group_variants(env):
+    """Opt-in grouped weight-gradient variants (8-wave two-half kernel, deeper
+    LDS-DMA rings, forced token splits) in a child process (switches are read once)."""
     import subprocess, sys, os
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", __file__, "-k",
-                        "test_linear_wgrad_group and not 8wave"], capture_output=True, text=True, timeout=600,
-                       cwd=root, env=dict(os.environ, DDIM_COLD_WGRAD_GROUP8="1", PYTHONPATH=root))
+                        "test_linear_wgrad_group and not variants"], capture_output=True, text=True, timeout=600,
+                       cwd=root, env=dict(os.environ, PYTHONPATH=root, **env))
     assert r.returncode == 0, r.stdout[-3000:]
 
 
