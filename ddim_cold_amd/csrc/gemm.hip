@@ -29,6 +29,7 @@
 #include "gemm_common.h"
 #include <cstdlib>
 #include <algorithm>
+#include <type_traits>
 
 namespace dc {
 
@@ -673,53 +674,84 @@ __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int t
   VecEpi<EPI, FM, FN> ep;
   if (VEC && p.debug != 3) ep.prefetch(p, m0 + wm * TM, n0 + wn * TN, g, li);
 
-  for (int kt = 0; kt < (p.debug == 2 ? 0 : nk); ++kt) {
-    const int rem = min(S - 2, nk - 1 - kt);
-    vm_wait_rem<LPT>(rem);
-    raw_barrier();
-    if (kt + S - 1 < nk) {
-      const int st = (kt + S - 1) % S;
-      oa.issue(smem + st * STAGE, kt0 + kt + S - 1, wave);
-      ob.issue(smem + st * STAGE + OA::BYTES, kt0 + kt + S - 1, wave);
+  // main loop; the bias-gradient MFMA variant is a separate instantiation so the
+  // loop carries no per-k-step branch (one made hipcc shuffle the accumulators
+  // between AGPRs and VGPRs every iteration)
+  auto mainloop = [&](auto db_tag) {
+    constexpr bool DB = decltype(db_tag)::value;
+    for (int kt = 0; kt < (p.debug == 2 ? 0 : nk); ++kt) {
+      const int rem = min(S - 2, nk - 1 - kt);
+      vm_wait_rem<LPT>(rem);
+      raw_barrier();
+      if (kt + S - 1 < nk) {
+        const int st = (kt + S - 1) % S;
+        oa.issue(smem + st * STAGE, kt0 + kt + S - 1, wave);
+        ob.issue(smem + st * STAGE + OA::BYTES, kt0 + kt + S - 1, wave);
+      }
+      const char* la = smem + (kt % S) * STAGE;
+      const char* lb = la + OA::BYTES;
+      // transposed operands: the reads of BOTH 32-deep k-steps are issued up
+      // front (inline asm, see frag_t_swz_issue); k-step 0 waits only for its own
+      TrFrag ta[2][FM], tb[2][FN];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          if (AT) ta[s][i] = frag_t_swz_issue(la, wm * TM + i * 16, s, lane);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          if (BT) tb[s][j] = frag_t_swz_issue(lb, wn * TN + j * 16, s, lane);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 af[FM], bfr[FN];
+        if (AT || BT) {
+          if (s == 0) {
+            // reads issued after k-step 0's: 2 per transposed fragment
+            constexpr int LATER = 2 * ((AT ? FM : 0) + (BT ? FN : 0));
+            static_assert(LATER < 16, "lgkmcnt is 4 bits");
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+              if (AT) af[i] = frag_t_fence_n<LATER>(ta[0][i]);
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              if (BT) bfr[j] = frag_t_fence_n<LATER>(tb[0][j]);
+          } else {
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+              if (AT) af[i] = frag_t_fence_n<0>(ta[1][i]);
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              if (BT) bfr[j] = frag_t_fence_n<0>(tb[1][j]);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int r = wm * TM + i * 16;
+          if (AT) continue;
+          if (PERM) af[i] = frag_k_perm(la, r + li, s, g);
+          else af[i] = frag_k(la, r + li, s, g);
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int r = wn * TN + j * 16;
+          if (BT) continue;
+          if (PERM) bfr[j] = frag_k_perm(lb, r + li, s, g);
+          else bfr[j] = frag_k(lb, r + li, s, g);
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+        if (DB) {
+#pragma unroll
+          for (int i = 0; i < FM; ++i) dbacc[i] = mfma16(af[i], ones, dbacc[i]);
+        }
+      }
     }
-    const char* la = smem + (kt % S) * STAGE;
-    const char* lb = la + OA::BYTES;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 af[FM], bfr[FN];
-      TrFrag ta[FM], tb[FN];  // transposed reads: all issued, then one wait
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int r = wm * TM + i * 16;
-        if (AT) ta[i] = frag_t_swz_issue(la, r, s, lane);
-        else if (PERM) af[i] = frag_k_perm(la, r + li, s, g);
-        else af[i] = frag_k(la, r + li, s, g);
-      }
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int r = wn * TN + j * 16;
-        if (BT) tb[j] = frag_t_swz_issue(lb, r, s, lane);
-        else if (PERM) bfr[j] = frag_k_perm(lb, r + li, s, g);
-        else bfr[j] = frag_k(lb, r + li, s, g);
-      }
-      if (AT) {
-#pragma unroll
-        for (int i = 0; i < FM; ++i) af[i] = frag_t_fence(ta[i]);
-      }
-      if (BT) {
-#pragma unroll
-        for (int j = 0; j < FN; ++j) bfr[j] = frag_t_fence(tb[j]);
-      }
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
-      if (WG && do_db) {
-#pragma unroll
-        for (int i = 0; i < FM; ++i) dbacc[i] = mfma16(af[i], ones, dbacc[i]);
-      }
-    }
-  }
+  };
+  if (WG && do_db) mainloop(std::true_type{});
+  else mainloop(std::false_type{});
 
   if (p.debug == 1) {
     float t = 0.f;

@@ -81,6 +81,16 @@ __device__ __forceinline__ bf16x8 frag_t_fence(TrFrag& f) {
   v[4] = f.hi[0]; v[5] = f.hi[1]; v[6] = f.hi[2]; v[7] = f.hi[3];
   return v;
 }
+// counted variant: wait until at most N LDS reads are outstanding (the N issued
+// after this fragment's)
+template <int N>
+__device__ __forceinline__ bf16x8 frag_t_fence_n(TrFrag& f) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(f.lo), "+v"(f.hi) : "n"(N));
+  bf16x8 v;
+  v[0] = f.lo[0]; v[1] = f.lo[1]; v[2] = f.lo[2]; v[3] = f.lo[3];
+  v[4] = f.hi[0]; v[5] = f.hi[1]; v[6] = f.hi[2]; v[7] = f.hi[3];
+  return v;
+}
 __device__ __forceinline__ bf16x8 frag_t_swz(const char* lds, int c0, int s, int lane) {
   TrFrag f = frag_t_swz_issue(lds, c0, s, lane);
   return frag_t_fence(f);
