@@ -63,6 +63,8 @@ def main():
                     help="host-issued all-reduces between graph segments instead of capturing them in the step graph")
     ap.add_argument("--grad-wire", default="fp32", choices=["fp32", "bf16"],
                     help="gradient all-reduce wire format (bf16 halves the xGMI bytes)")
+    ap.add_argument("--comm", default="torch", choices=["torch", "native"],
+                    help="gradient collectives through torch.distributed (RCCL) or the native RCCL communicator")
     ap.add_argument("--sampler-k", type=int, default=20)
     ap.add_argument("--sampler-n", type=int, default=64)
     ap.add_argument("--no-eager-baseline", action="store_true",
@@ -92,7 +94,8 @@ def main():
                        seed=42, force_segments=args.force_dist,
                        wgrad_stream=args.wgrad_stream,
                        temb_rows=int(math.log2(model.img_size[1])) + 1,  # cold t in 1..log2(W)
-                       graph_comm=not args.segmented_comm, grad_wire=args.grad_wire)
+                       graph_comm=not args.segmented_comm, grad_wire=args.grad_wire,
+                       comm=args.comm)
     engine = TrainEngine(model, cfg, device=dev)
     pool = synthetic_pool(1024, tuple(model.img_size), seed=7 + rank, device=dev)
     engine.set_batch_fn(ColdBatcher(pool, args.batch, engine.rng))
@@ -121,7 +124,8 @@ def main():
     ms = elapsed / args.steps * 1e3
     value = n * args.batch * args.steps / elapsed
     extra = {}
-    if rank == 0 and not args.no_sampler and dev.type == "cuda":
+    # the sampler metric is a 1-GPU number (BASELINE.json config 5): multi-rank runs skip it
+    if rank == 0 and n == 1 and not args.no_sampler and dev.type == "cuda":
         from ddim_cold_amd.diffusion.samplers import DDIMSampler
         model.eval()
         s = DDIMSampler(model, dev, k=args.sampler_k)
@@ -173,7 +177,7 @@ def main():
                        "allreduce": ("none" if not engine.segmented else "eager" if dev.type != "cuda" else
                                      "segmented" if (args.segmented_comm or getattr(engine, "_graph_comm_failed", False))
                                      else "captured-in-graph"),
-                       "grad_wire": args.grad_wire,
+                       "grad_wire": args.grad_wire, "comm": args.comm,
                        "optimizer": "AdamW(wd=0.05)+clip1.0+cosine", "final_loss": round(loss, 5)},
         }
         out.update(extra)

@@ -50,7 +50,7 @@ def _flags(inc, abi, resource_usage=False):
     ]
     if resource_usage:
         f.append("-Rpass-analysis=kernel-resource-usage")
-    for d in inc + [py_inc, CSRC]:
+    for d in inc + [py_inc, CSRC, "/opt/rocm/include"]:
         f += ["-I", d]
     return f
 
@@ -104,6 +104,9 @@ def build(force: bool = False, jobs: int | None = None, resource_usage: bool = F
     if force or not os.path.isfile(OUT) or os.path.getmtime(OUT) < newest or _stale_link(objs):
         cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", OUT + ".tmp"] + objs + [
             "-L", libdir, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+            # RCCL: torch's own librccl.so by path (no SONAME; the loader matches the
+            # file PyTorch already loaded, so the process keeps ONE RCCL instance)
+            os.path.join(libdir, "librccl.so"),
             f"-Wl,-rpath,{libdir}",
         ]
         r = subprocess.run(cmd, capture_output=True, text=True)

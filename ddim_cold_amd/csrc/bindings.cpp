@@ -54,8 +54,48 @@ GemmArgs nt_args(const Tensor& a, const Tensor& w) {
   return g;
 }
 
+bool ln_fold_width_ok(int64_t D) { return D % 32 == 0 && D / 32 <= 16; }
+
+// LayerNorm fold, consumer side (gemm.hip): A = bf16(x), w = bf16(gamma o W),
+// b = bias + W beta; ln_st [M][2] row {sum, sum^2} of x; ln_c [N] row sums of w
+void apply_fold(GemmArgs& g, int M, int N, const c10::optional<Tensor>& ln_st, const c10::optional<Tensor>& ln_c,
+                double eps, const c10::optional<Tensor>& ln_mean, const c10::optional<Tensor>& ln_rstd) {
+  if (!ln_st.has_value() || !ln_st->defined()) return;
+  CHECK_IN((*ln_st), F32);
+  TORCH_CHECK(ln_c.has_value() && ln_c->defined(), "LayerNorm fold needs ln_c");
+  CHECK_IN((*ln_c), F32);
+  TORCH_CHECK(ln_fold_width_ok(g.K), "LayerNorm fold: width must be a multiple of 32, <= 512");
+  TORCH_CHECK(ln_st->numel() == 2 * (int64_t)M * (g.K / 32) && ln_c->numel() == N, "LayerNorm fold shapes");
+  g.ln_st = ln_st->data_ptr<float>();
+  g.ln_c = ln_c->data_ptr<float>();
+  g.ln_eps = (float)eps;
+  if (ln_mean.has_value() && ln_mean->defined()) {
+    TORCH_CHECK(ln_rstd.has_value() && ln_rstd->defined(), "ln_mean needs ln_rstd");
+    CHECK_IN((*ln_mean), F32); CHECK_IN((*ln_rstd), F32);
+    TORCH_CHECK(ln_mean->numel() == M && ln_rstd->numel() == M, "ln_mean / ln_rstd shapes");
+    g.ln_mean = ln_mean->data_ptr<float>();
+    g.ln_rstd = ln_rstd->data_ptr<float>();
+  }
+}
+
+// LayerNorm fold, producer side: row statistics (accumulated, zeroed beforehand) + bf16 copy
+void apply_prod(GemmArgs& g, int64_t rows, int64_t D, const c10::optional<Tensor>& st_out,
+                const c10::optional<Tensor>& xb_out) {
+  if (!st_out.has_value() || !st_out->defined()) return;
+  CHECK_IN((*st_out), F32);
+  TORCH_CHECK(xb_out.has_value() && xb_out->defined(), "row statistics need the bf16 copy output");
+  CHECK_IN((*xb_out), BF16);
+  TORCH_CHECK(ln_fold_width_ok(D), "LayerNorm fold: width must be a multiple of 32, <= 512");
+  TORCH_CHECK(st_out->numel() == 2 * rows * (D / 32) && xb_out->numel() == rows * D, "LayerNorm-fold producer shapes");
+  g.st_out = st_out->data_ptr<float>();
+  g.xb_out = xb_out->data_ptr();
+}
+
+// ln_st: [B*N][D/32][2] row statistics of the tokens (the first LayerNorm's
+// input; LayerNorm fold), filled together with the tokens' bf16 copy xb_out.
 std::tuple<Tensor, Tensor> patch_embed_fwd(Tensor img, Tensor t, Tensor w_pe, Tensor b_pe, Tensor cls, Tensor pos,
-                                           Tensor temb, Tensor rng, int64_t site, double p, int64_t patch) {
+                                           Tensor temb, Tensor rng, int64_t site, double p, int64_t patch,
+                                           c10::optional<Tensor> ln_st, c10::optional<Tensor> xb_out) {
   CHECK_IN(img, F32); CHECK_IN(t, I64); CHECK_IN(w_pe, BF16); CHECK_IN(b_pe, F32);
   CHECK_IN(cls, F32); CHECK_IN(pos, F32); CHECK_IN(temb, F32); check_rng(rng);
   const c10::DeviceGuard guard(img.device());
@@ -71,9 +111,21 @@ std::tuple<Tensor, Tensor> patch_embed_fwd(Tensor img, Tensor t, Tensor w_pe, Te
   TORCH_CHECK(t.numel() == B, "t must be [B]");
   auto x = at::empty({B, N, D}, img.options());
   auto patches = at::empty({(int64_t)B * NP, F}, img.options().dtype(BF16));
+  float* st = nullptr;
+  void* xb = nullptr;
+  if (ln_st.has_value() && ln_st->defined()) {
+    CHECK_IN((*ln_st), F32);
+    TORCH_CHECK(ln_fold_width_ok(D), "LayerNorm fold: width must be a multiple of 32, <= 512");
+    TORCH_CHECK(ln_st->numel() == (int64_t)B * N * (D / 32) * 2, "ln_st must be [B*N, D/32, 2]");
+    TORCH_CHECK(xb_out.has_value() && xb_out->defined(), "ln_st needs xb_out");
+    CHECK_IN((*xb_out), BF16);
+    TORCH_CHECK(xb_out->numel() == (int64_t)B * N * D, "xb_out shape");
+    st = ln_st->data_ptr<float>();
+    xb = xb_out->data_ptr();
+  }
   patchify_cls_launch(img.data_ptr<float>(), t.data_ptr<int64_t>(), cls.data_ptr<float>(), pos.data_ptr<float>(),
                       temb.data_ptr<float>(), patches.data_ptr(), x.data_ptr<float>(), B, C, H, W, P, D,
-                      rng.data_ptr<int64_t>(), site, p, cur_stream());
+                      rng.data_ptr<int64_t>(), site, p, st, xb, cur_stream());
   GemmArgs g;
   g.A = patches.data_ptr();
   g.B = w_pe.data_ptr();
@@ -83,6 +135,8 @@ std::tuple<Tensor, Tensor> patch_embed_fwd(Tensor img, Tensor t, Tensor w_pe, Te
   g.rng = rng.data_ptr<int64_t>(); g.site_drop = site; g.p_drop = p;
   g.tokens = NP; g.batch = B;
   g.pos = pos.data_ptr<float>(); g.temb = temb.data_ptr<float>(); g.tsteps = t.data_ptr<int64_t>(); g.emb_dim = D;
+  g.st_out = st;  // slice 0, indexed by token row
+  g.xb_out = xb;
   gemm_nt(g, EPI_EMBED, cur_stream());
   return {x, patches};
 }
@@ -102,7 +156,7 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_fwd(Tensor x, Tensor gamma, Tensor 
 }
 
 // y = a w^T (+ b): plain nn.Linear, bf16 or fp32 output
-Tensor linear_fwd(Tensor a, Tensor w, c10::optional<Tensor> b, bool out_fp32) {
+Tensor linear_fwd(Tensor a, Tensor w, c10::optional<Tensor> b, bool out_fp32, c10::optional<Tensor> ln_st, c10::optional<Tensor> ln_c, double ln_eps) {
   CHECK_IN(a, BF16); CHECK_IN(w, BF16);
   const c10::DeviceGuard guard(a.device());
   const int K = a.size(-1);
@@ -117,11 +171,13 @@ Tensor linear_fwd(Tensor a, Tensor w, c10::optional<Tensor> b, bool out_fp32) {
     TORCH_CHECK(b->numel() == Dout, "bias shape");
     g.bias = b->data_ptr<float>();
   }
+  apply_fold(g, M, Dout, ln_st, ln_c, ln_eps, c10::nullopt, c10::nullopt);
   gemm_nt(g, out_fp32 ? EPI_F32 : EPI_BF16, cur_stream());
   return out;
 }
 
-Tensor qkv_fwd(Tensor a, Tensor w, Tensor b, int64_t B, int64_t N, int64_t H) {
+Tensor qkv_fwd(Tensor a, Tensor w, Tensor b, int64_t B, int64_t N, int64_t H, c10::optional<Tensor> ln_st, c10::optional<Tensor> ln_c, double ln_eps,
+               c10::optional<Tensor> ln_mean, c10::optional<Tensor> ln_rstd) {
   CHECK_IN(a, BF16); CHECK_IN(w, BF16); CHECK_IN(b, F32);
   const c10::DeviceGuard guard(a.device());
   const int D = a.size(1);
@@ -131,6 +187,7 @@ Tensor qkv_fwd(Tensor a, Tensor w, Tensor b, int64_t B, int64_t N, int64_t H) {
   GemmArgs g = nt_args(a, w);
   g.C = out.data_ptr(); g.ldc = 3 * D; g.bias = b.data_ptr<float>();
   g.tokens = N; g.batch = B; g.heads = H; g.hd = D / H;
+  apply_fold(g, B * N, 3 * D, ln_st, ln_c, ln_eps, ln_mean, ln_rstd);
   gemm_nt(g, EPI_QKV, cur_stream());
   return out;
 }
@@ -149,7 +206,7 @@ std::tuple<Tensor, Tensor> attn_fwd(Tensor qkv, double scale, Tensor rng, int64_
 }
 
 Tensor linear_residual_fwd(Tensor a, Tensor w, Tensor b, Tensor x, int64_t N, Tensor rng, int64_t site_drop,
-                           double p_drop, int64_t site_dp, double p_dp) {
+                           double p_drop, int64_t site_dp, double p_dp, c10::optional<Tensor> st_out, c10::optional<Tensor> xb_out) {
   CHECK_IN(a, BF16); CHECK_IN(w, BF16); CHECK_IN(b, F32); CHECK_IN(x, F32); check_rng(rng);
   const c10::DeviceGuard guard(a.device());
   const int K = a.size(-1);
@@ -162,6 +219,7 @@ Tensor linear_residual_fwd(Tensor a, Tensor w, Tensor b, Tensor x, int64_t N, Te
   g.C = out.data_ptr(); g.ldc = Dout; g.bias = b.data_ptr<float>(); g.res = x.data_ptr<float>();
   g.rng = rng.data_ptr<int64_t>(); g.site_drop = site_drop; g.p_drop = p_drop; g.site_dp = site_dp; g.p_dp = p_dp;
   g.tokens = N;
+  apply_prod(g, M, Dout, st_out, xb_out);
   gemm_nt(g, EPI_RESID, cur_stream());
   return out;
 }
@@ -201,7 +259,9 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> linear_residual_ln_fwd(Tensor a, Tens
   return {x_out, ln, mean, rstd};
 }
 
-std::tuple<Tensor, Tensor> linear_gelu_fwd(Tensor a, Tensor w, Tensor b, Tensor rng, int64_t site, double p) {
+std::tuple<Tensor, Tensor> linear_gelu_fwd(Tensor a, Tensor w, Tensor b, Tensor rng, int64_t site, double p,
+                                           c10::optional<Tensor> ln_st, c10::optional<Tensor> ln_c, double ln_eps, c10::optional<Tensor> ln_mean,
+                                           c10::optional<Tensor> ln_rstd) {
   CHECK_IN(a, BF16); CHECK_IN(w, BF16); CHECK_IN(b, F32); check_rng(rng);
   const c10::DeviceGuard guard(a.device());
   const int K = a.size(-1);
@@ -214,11 +274,13 @@ std::tuple<Tensor, Tensor> linear_gelu_fwd(Tensor a, Tensor w, Tensor b, Tensor 
   GemmArgs g = nt_args(a2, w);
   g.C = u.data_ptr(); g.ldc = Hm; g.C2 = h.data_ptr(); g.bias = b.data_ptr<float>();
   g.rng = rng.data_ptr<int64_t>(); g.site_drop = site; g.p_drop = p;
+  apply_fold(g, M, Hm, ln_st, ln_c, ln_eps, ln_mean, ln_rstd);
   gemm_nt(g, EPI_GELU, cur_stream());
   return {u, h};
 }
 
-Tensor head_fwd(Tensor a, Tensor w, Tensor b, int64_t B, int64_t C, int64_t H, int64_t W, int64_t patch) {
+Tensor head_fwd(Tensor a, Tensor w, Tensor b, int64_t B, int64_t C, int64_t H, int64_t W, int64_t patch,
+                c10::optional<Tensor> ln_st, c10::optional<Tensor> ln_c, double ln_eps, c10::optional<Tensor> ln_mean, c10::optional<Tensor> ln_rstd) {
   CHECK_IN(a, BF16); CHECK_IN(w, BF16); CHECK_IN(b, F32);
   const c10::DeviceGuard guard(a.device());
   const int K = a.size(-1);
@@ -230,6 +292,7 @@ Tensor head_fwd(Tensor a, Tensor w, Tensor b, int64_t B, int64_t C, int64_t H, i
   GemmArgs g = nt_args(a2, w);
   g.C = img.data_ptr(); g.bias = b.data_ptr<float>();
   g.tokens = N; g.batch = B; g.chans = C; g.img_h = H; g.img_w = W; g.patch = patch;
+  apply_fold(g, B * N, w.size(0), ln_st, ln_c, ln_eps, ln_mean, ln_rstd);
   gemm_nt(g, EPI_HEAD, cur_stream());
   return img;
 }
@@ -239,7 +302,7 @@ Tensor head_fwd(Tensor a, Tensor w, Tensor b, int64_t B, int64_t C, int64_t H, i
 //                  in place, x0 written to x0_out; coef = device row {sqrt a_t, sqrt 1-a_t, sqrt a_tk, sqrt 1-a_tk}
 //   mode 2 (cold): x <- clamp(head(a), -1, 1)
 void head_step_(Tensor a, Tensor w, Tensor b, Tensor x, c10::optional<Tensor> x0_out, c10::optional<Tensor> coef,
-                int64_t patch, int64_t mode) {
+                int64_t patch, int64_t mode, c10::optional<Tensor> ln_st, c10::optional<Tensor> ln_c, double ln_eps) {
   CHECK_IN(a, BF16); CHECK_IN(w, BF16); CHECK_IN(b, F32); CHECK_IN(x, F32);
   const c10::DeviceGuard guard(a.device());
   TORCH_CHECK(x.dim() == 4, "x must be [B, C, H, W]");
@@ -260,6 +323,7 @@ void head_step_(Tensor a, Tensor w, Tensor b, Tensor x, c10::optional<Tensor> x0
     TORCH_CHECK(x0_out->sizes() == x.sizes() && coef->numel() >= 4, "x0_out / coef shapes");
     g.res = x.data_ptr<float>(); g.C2 = x0_out->data_ptr(); g.coef = coef->data_ptr<float>();
   }
+  apply_fold(g, B * N, w.size(0), ln_st, ln_c, ln_eps, c10::nullopt, c10::nullopt);
   gemm_nt(g, EPI_HEAD, cur_stream());
 }
 
@@ -423,7 +487,7 @@ void linear_wgrad_group(std::vector<Tensor> dys, std::vector<Tensor> xs, std::ve
 std::tuple<Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma,
                                          c10::optional<Tensor> g_res, Tensor dgamma, Tensor dbeta, int64_t N,
                                          Tensor rng, int64_t site_drop, double p_drop, int64_t site_dp, double p_dp,
-                                         bool emit_gy, c10::optional<Tensor> ws) {
+                                         bool emit_gy, c10::optional<Tensor> ws, c10::optional<Tensor> beta, c10::optional<Tensor> y_out) {
   CHECK_IN(dy, F32); CHECK_IN(x, F32); CHECK_IN(mean, F32); CHECK_IN(rstd, F32); CHECK_IN(gamma, F32);
   CHECK_IN(dgamma, F32); CHECK_IN(dbeta, F32); check_rng(rng);
   const c10::DeviceGuard guard(x.device());
@@ -446,11 +510,22 @@ std::tuple<Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tenso
     CHECK_IN(w, F32);
     TORCH_CHECK(w.numel() == (int64_t)R * 2 * D, "ln ws must hold ln_replicas x 2D floats");
   }
+  // y_out: also emit the LayerNorm output bf16 (x_hat gamma + beta) for the weight
+  // gradient of the GEMM that consumed it through the LayerNorm fold
+  const float* bp = nullptr;
+  void* yp = nullptr;
+  if (y_out.has_value() && y_out->defined()) {
+    TORCH_CHECK(beta.has_value() && beta->defined(), "y_out needs beta");
+    CHECK_IN((*beta), F32); CHECK_IN((*y_out), BF16);
+    TORCH_CHECK(beta->numel() == D && y_out->numel() == x.numel(), "beta / y_out shapes");
+    bp = beta->data_ptr<float>();
+    yp = y_out->data_ptr();
+  }
   auto g_out = at::empty(x.sizes(), x.options());
   Tensor gy = emit_gy ? at::empty({M, D}, x.options().dtype(BF16)) : at::empty({0}, x.options().dtype(BF16));
   layernorm_bwd_launch(dy.data_ptr<float>(), x.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
-                       gamma.data_ptr<float>(), gr, g_out.data_ptr<float>(), emit_gy ? gy.data_ptr() : nullptr,
-                       w.data_ptr<float>(), M, D, N, rng.data_ptr<int64_t>(), site_drop, p_drop, site_dp, p_dp,
+                       gamma.data_ptr<float>(), bp, gr, g_out.data_ptr<float>(), emit_gy ? gy.data_ptr() : nullptr,
+                       yp, w.data_ptr<float>(), M, D, N, rng.data_ptr<int64_t>(), site_drop, p_drop, site_dp, p_dp,
                        parts, cur_stream());
   if (own_ws) {
     auto s = w.sum(0);
@@ -609,23 +684,67 @@ void cold_batch(Tensor pool, Tensor rng, int64_t site, Tensor x_t, Tensor x_tm1,
                     draw_idx, cur_stream());
 }
 
+
+// LayerNorm fold weights for a list of GEMMs consuming a LayerNorm (one launch)
+void ln_fold_(std::vector<Tensor> ws, std::vector<Tensor> gammas, std::vector<Tensor> betas,
+              std::vector<c10::optional<Tensor>> biases, std::vector<Tensor> wfs, std::vector<Tensor> cs,
+              std::vector<Tensor> bfs) {
+  const size_t n = ws.size();
+  TORCH_CHECK(n > 0 && n <= (size_t)FOLD_MAX, "ln_fold_: 1..", FOLD_MAX, " GEMMs per launch");
+  TORCH_CHECK(gammas.size() == n && betas.size() == n && biases.size() == n && wfs.size() == n && cs.size() == n &&
+                  bfs.size() == n, "ln_fold_: list lengths");
+  const c10::DeviceGuard guard(ws[0].device());
+  FoldTable tb{};
+  tb.n = (int)n;
+  tb.K = ws[0].size(-1);
+  TORCH_CHECK(tb.K % 4 == 0, "ln_fold_: K % 4");
+  int rows = 0;
+  for (size_t i = 0; i < n; ++i) {
+    CHECK_IN(ws[i], F32); CHECK_IN(gammas[i], F32); CHECK_IN(betas[i], F32);
+    CHECK_IN(wfs[i], BF16); CHECK_IN(cs[i], F32); CHECK_IN(bfs[i], F32);
+    TORCH_CHECK(ws[i].dim() == 2 && ws[i].size(1) == tb.K, "ln_fold_: weights must be [rows, K] with one K");
+    const int R = ws[i].size(0);
+    TORCH_CHECK(gammas[i].numel() == tb.K && betas[i].numel() == tb.K && wfs[i].numel() == (int64_t)R * tb.K &&
+                    cs[i].numel() == R && bfs[i].numel() == R, "ln_fold_: shapes");
+    for (const Tensor* t : {&ws[i], &gammas[i], &betas[i]})
+      TORCH_CHECK(((uintptr_t)t->data_ptr() & 15) == 0, "ln_fold_: 16-B aligned fp32 operands");
+    TORCH_CHECK(((uintptr_t)wfs[i].data_ptr() & 7) == 0, "ln_fold_: 8-B aligned output");
+    FoldJob& j = tb.j[i];
+    j.w = ws[i].data_ptr<float>(); j.gamma = gammas[i].data_ptr<float>(); j.beta = betas[i].data_ptr<float>();
+    j.bias = nullptr;
+    if (biases[i].has_value() && biases[i]->defined()) {
+      CHECK_IN((*biases[i]), F32);
+      TORCH_CHECK(biases[i]->numel() == R, "ln_fold_: bias shape");
+      j.bias = biases[i]->data_ptr<float>();
+    }
+    j.wf = wfs[i].data_ptr(); j.c = cs[i].data_ptr<float>(); j.bf = bfs[i].data_ptr<float>();
+    tb.start[i] = rows;
+    rows += R;
+  }
+  tb.start[n] = rows;
+  ln_fold_launch(tb, cur_stream());
+}
 }  // namespace
 
 TORCH_LIBRARY(ddim_cold, m) {
   m.def("patch_embed_fwd(Tensor img, Tensor t, Tensor w_pe, Tensor b_pe, Tensor cls, Tensor pos, Tensor temb, "
-        "Tensor rng, int site, float p, int patch) -> (Tensor, Tensor)");
+        "Tensor rng, int site, float p, int patch, Tensor(a!)? ln_st=None, Tensor(b!)? xb_out=None) -> (Tensor, Tensor)");
   m.def("layernorm_fwd(Tensor x, Tensor gamma, Tensor beta, float eps) -> (Tensor, Tensor, Tensor)");
-  m.def("qkv_fwd(Tensor a, Tensor w, Tensor b, int B, int N, int H) -> Tensor");
+  m.def("qkv_fwd(Tensor a, Tensor w, Tensor b, int B, int N, int H, Tensor? ln_st=None, Tensor? ln_c=None, "
+        "float ln_eps=1e-5, Tensor(a!)? ln_mean=None, Tensor(b!)? ln_rstd=None) -> Tensor");
   m.def("attn_fwd(Tensor qkv, float scale, Tensor rng, int site, float p) -> (Tensor, Tensor)");
   m.def("linear_residual_fwd(Tensor a, Tensor w, Tensor b, Tensor x, int N, Tensor rng, int site_drop, "
-        "float p_drop, int site_dp, float p_dp) -> Tensor");
-  m.def("linear_gelu_fwd(Tensor a, Tensor w, Tensor b, Tensor rng, int site, float p) -> (Tensor, Tensor)");
-  m.def("linear_fwd(Tensor a, Tensor w, Tensor? b, bool out_fp32) -> Tensor");
+        "float p_drop, int site_dp, float p_dp, Tensor(a!)? st_out=None, Tensor(b!)? xb_out=None) -> Tensor");
+  m.def("linear_gelu_fwd(Tensor a, Tensor w, Tensor b, Tensor rng, int site, float p, Tensor? ln_st=None, "
+        "Tensor? ln_c=None, float ln_eps=1e-5, Tensor(a!)? ln_mean=None, Tensor(b!)? ln_rstd=None) -> (Tensor, Tensor)");
+  m.def("linear_fwd(Tensor a, Tensor w, Tensor? b, bool out_fp32, Tensor? ln_st=None, Tensor? ln_c=None, "
+        "float ln_eps=1e-5) -> Tensor");
   m.def("linear_residual_ln_fwd(Tensor a, Tensor w, Tensor b, Tensor x, Tensor gamma, Tensor beta, float eps, "
         "int N, Tensor rng, int site_drop, float p_drop, int site_dp, float p_dp) -> (Tensor, Tensor, Tensor, Tensor)");
-  m.def("head_fwd(Tensor a, Tensor w, Tensor b, int B, int C, int H, int W, int patch) -> Tensor");
+  m.def("head_fwd(Tensor a, Tensor w, Tensor b, int B, int C, int H, int W, int patch, Tensor? ln_st=None, "
+        "Tensor? ln_c=None, float ln_eps=1e-5, Tensor(a!)? ln_mean=None, Tensor(b!)? ln_rstd=None) -> Tensor");
   m.def("head_step_(Tensor a, Tensor w, Tensor b, Tensor(a!) x, Tensor(b!)? x0_out, Tensor? coef, int patch, "
-        "int mode) -> ()");
+        "int mode, Tensor? ln_st=None, Tensor? ln_c=None, float ln_eps=1e-5) -> ()");
   m.def("smooth_l1_fwd_bwd(Tensor pred, Tensor target, int N, int patch, float beta, Tensor(a!)? loss_last=None, "
         "Tensor(b!)? loss_ema=None, float ema_decay=0.99) -> (Tensor, Tensor)");
   m.def("img_to_tokgrad(Tensor dimg, int N, int patch) -> Tensor");
@@ -635,8 +754,10 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("linear_wgrad_group(Tensor[] dys, Tensor[] xs, Tensor(a!)[] dws, Tensor(b!)?[] dbs) -> ()");
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor? g_res, "
         "Tensor(a!) dgamma, Tensor(b!) dbeta, int N, Tensor rng, int site_drop, float p_drop, int site_dp, "
-        "float p_dp, bool emit_gy, Tensor(c!)? ws=None) -> (Tensor, Tensor)");
+        "float p_dp, bool emit_gy, Tensor(c!)? ws=None, Tensor? beta=None, Tensor(d!)? y_out=None) -> (Tensor, Tensor)");
   m.def("replica_reduce_(Tensor(a!) ws, Tensor dst_ptrs, int C) -> ()");
+  m.def("ln_fold_(Tensor[] ws, Tensor[] gammas, Tensor[] betas, Tensor?[] biases, Tensor(a!)[] wfs, Tensor(b!)[] cs, "
+        "Tensor(c!)[] bfs) -> ()");
   m.def("attn_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, float scale, Tensor rng, int site, float p) -> Tensor");
   m.def("embed_bwd(Tensor g, Tensor t, Tensor rng, int site, float p, Tensor(a!) dcls, Tensor(b!) dpos, "
         "Tensor(c!) dtemb) -> Tensor");
@@ -672,6 +793,7 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("linear_wgrad_group", &linear_wgrad_group);
   m.impl("layernorm_bwd", &layernorm_bwd);
   m.impl("replica_reduce_", &replica_reduce_);
+  m.impl("ln_fold_", &ln_fold_);
   m.impl("attn_bwd", &attn_bwd);
   m.impl("embed_bwd", &embed_bwd);
   m.impl("sqnorm", &sqnorm);

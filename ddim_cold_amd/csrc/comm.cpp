@@ -1,0 +1,162 @@
+// Native RCCL communicator for the bucketed gradient reducer.
+//
+// Reference: the reference reduces gradients through DDP's NCCL reducer
+// (multi_gpu_trainer.py:88 DistributedDataParallel, :128 backward hooks) and
+// broadcasts the initial weights through DDP's constructor (X2 in SURVEY §2.5).
+// Here the train engine (train/engine.py) owns one ncclComm_t per process:
+//
+// * bootstrap: rank 0 draws the ncclUniqueId (comm_unique_id), the Python
+//   side ships its 128 bytes through the torch.distributed TCPStore, every rank
+//   calls comm_init (ncclCommInitRank on its own device);
+// * collectives are enqueued directly on the CALLER's current HIP stream (the
+//   engine's communication stream), so they are captured into the step's
+//   hipGraph like any kernel, with no ProcessGroup work objects, internal
+//   streams or cross-stream events in between;
+// * the bf16 wire format packs the fp32 gradient range into a bf16 scratch
+//   range (comm_wire.hip), all-reduces ncclBfloat16 in place and unpacks back:
+//   three graph nodes per bucket instead of the cast/copy chain, half the xGMI
+//   bytes.
+//
+// RCCL is the one PyTorch already loaded (torch/lib/librccl.so, linked by the
+// same name), so there is a single RCCL instance in the process.
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/core/DeviceGuard.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "kernels.h"
+
+using at::Tensor;
+
+namespace {
+
+std::mutex g_mu;
+std::vector<ncclComm_t> g_comms;  // handle -> communicator (nullptr once destroyed)
+
+#define NCCL_CHECK(cmd)                                                                         \
+  do {                                                                                          \
+    ncclResult_t r_ = (cmd);                                                                    \
+    TORCH_CHECK(r_ == ncclSuccess, "RCCL error ", (int)r_, " (", ncclGetErrorString(r_), ") at ", \
+                #cmd);                                                                          \
+  } while (0)
+
+ncclComm_t get_comm(int64_t h) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  TORCH_CHECK(h >= 0 && h < (int64_t)g_comms.size() && g_comms[h] != nullptr, "invalid communicator handle ", h);
+  return g_comms[h];
+}
+
+ncclDataType_t nccl_dtype(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return ncclFloat32;
+    case at::kBFloat16: return ncclBfloat16;
+    case at::kHalf: return ncclFloat16;
+    case at::kDouble: return ncclFloat64;
+    case at::kLong: return ncclInt64;
+    case at::kInt: return ncclInt32;
+    default: TORCH_CHECK(false, "unsupported dtype for RCCL: ", t.scalar_type());
+  }
+}
+
+ncclRedOp_t nccl_op(int64_t op) {
+  switch (op) {
+    case 0: return ncclSum;
+    case 1: return ncclMax;
+    case 2: return ncclMin;
+    default: TORCH_CHECK(false, "reduce op must be 0 (sum), 1 (max) or 2 (min)");
+  }
+}
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_buf(const Tensor& t) {
+  TORCH_CHECK(t.is_cuda(), "communicator buffers must be GPU tensors");
+  TORCH_CHECK(t.is_contiguous(), "communicator buffers must be contiguous");
+}
+
+Tensor comm_unique_id() {
+  ncclUniqueId id;
+  NCCL_CHECK(ncclGetUniqueId(&id));
+  auto out = at::empty({(int64_t)sizeof(id.internal)}, at::TensorOptions().dtype(at::kByte));
+  std::memcpy(out.data_ptr<uint8_t>(), id.internal, sizeof(id.internal));
+  return out;
+}
+
+int64_t comm_init(Tensor uid, int64_t world, int64_t rank, int64_t device) {
+  TORCH_CHECK(!uid.is_cuda() && uid.scalar_type() == at::kByte && uid.numel() == NCCL_UNIQUE_ID_BYTES,
+              "uid must be a CPU uint8 tensor of ", NCCL_UNIQUE_ID_BYTES, " bytes");
+  TORCH_CHECK(world >= 1 && rank >= 0 && rank < world, "bad world/rank");
+  ncclUniqueId id;
+  std::memcpy(id.internal, uid.contiguous().data_ptr<uint8_t>(), sizeof(id.internal));
+  const c10::DeviceGuard guard(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
+  ncclComm_t comm;
+  NCCL_CHECK(ncclCommInitRank(&comm, (int)world, id, (int)rank));
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_comms.push_back(comm);
+  return (int64_t)g_comms.size() - 1;
+}
+
+// In-place all-reduce of a contiguous GPU buffer on the current stream.
+void comm_all_reduce_(Tensor buf, int64_t h, int64_t op) {
+  check_buf(buf);
+  const c10::DeviceGuard guard(buf.device());
+  NCCL_CHECK(ncclAllReduce(buf.data_ptr(), buf.data_ptr(), (size_t)buf.numel(), nccl_dtype(buf), nccl_op(op),
+                           get_comm(h), cur_stream()));
+}
+
+// In-place SUM all-reduce of an fp32 range over a bf16 wire:
+// pack fp32 -> bf16 scratch, all-reduce bf16, unpack back into the fp32 range.
+void comm_all_reduce_bf16_wire_(Tensor buf, Tensor scratch, int64_t h) {
+  check_buf(buf);
+  check_buf(scratch);
+  TORCH_CHECK(buf.scalar_type() == at::kFloat && scratch.scalar_type() == at::kBFloat16, "fp32 buf, bf16 scratch");
+  TORCH_CHECK(scratch.numel() >= buf.numel(), "scratch too small");
+  TORCH_CHECK(((uintptr_t)buf.data_ptr() % 16) == 0 && ((uintptr_t)scratch.data_ptr() % 16) == 0,
+              "wire buffers must be 16-B aligned");
+  const c10::DeviceGuard guard(buf.device());
+  const int64_t n = buf.numel();
+  hipStream_t s = cur_stream();
+  wire_pack_launch(buf.data_ptr<float>(), scratch.data_ptr(), n, s);
+  NCCL_CHECK(ncclAllReduce(scratch.data_ptr(), scratch.data_ptr(), (size_t)n, ncclBfloat16, ncclSum, get_comm(h), s));
+  wire_unpack_launch(scratch.data_ptr(), buf.data_ptr<float>(), n, s);
+}
+
+void comm_broadcast_(Tensor buf, int64_t h, int64_t root) {
+  check_buf(buf);
+  const c10::DeviceGuard guard(buf.device());
+  NCCL_CHECK(ncclBroadcast(buf.data_ptr(), buf.data_ptr(), (size_t)buf.numel(), nccl_dtype(buf), (int)root,
+                           get_comm(h), cur_stream()));
+}
+
+std::tuple<int64_t, int64_t> comm_info(int64_t h) {
+  int n = 0, r = 0;
+  ncclComm_t c = get_comm(h);
+  NCCL_CHECK(ncclCommCount(c, &n));
+  NCCL_CHECK(ncclCommUserRank(c, &r));
+  return {n, r};
+}
+
+void comm_destroy(int64_t h) {
+  ncclComm_t c = get_comm(h);
+  NCCL_CHECK(ncclCommDestroy(c));
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_comms[h] = nullptr;
+}
+
+}  // namespace
+
+TORCH_LIBRARY_FRAGMENT(ddim_cold, m) {
+  m.def("comm_unique_id() -> Tensor", &comm_unique_id);
+  m.def("comm_init(Tensor uid, int world, int rank, int device) -> int", &comm_init);
+  m.def("comm_all_reduce_(Tensor(a!) buf, int handle, int op=0) -> ()", &comm_all_reduce_);
+  m.def("comm_all_reduce_bf16_wire_(Tensor(a!) buf, Tensor(b!) scratch, int handle) -> ()",
+        &comm_all_reduce_bf16_wire_);
+  m.def("comm_broadcast_(Tensor(a!) buf, int handle, int root=0) -> ()", &comm_broadcast_);
+  m.def("comm_info(int handle) -> (int, int)", &comm_info);
+  m.def("comm_destroy(int handle) -> ()", &comm_destroy);
+}

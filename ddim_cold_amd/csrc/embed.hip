@@ -15,32 +15,61 @@
 
 namespace dc {
 
+// LayerNorm fold (gemm.hip): with `st` (the first LayerNorm's row statistics,
+// [B*N][D/32][2] slots) the cls-row blocks write their rows' complete
+// {sum, sum^2} into slot 0 (the other slots zero) plus the rows' bf16 copy; the
+// patch rows' slots come from the patch-embed GEMM epilogue.
 __global__ __launch_bounds__(256) void patchify_cls_kernel(const float* __restrict__ img, const int64_t* __restrict__ t,
                                                            const float* __restrict__ cls, const float* __restrict__ pos,
                                                            const float* __restrict__ temb, bf16* __restrict__ patches,
                                                            float* __restrict__ x, int B, int C, int H, int W, int P,
                                                            int D, const int64_t* __restrict__ rng, int site,
-                                                           uint32_t thr, float dsc) {
-  const int Hp = H / P, Wp = W / P, NP = Hp * Wp, F = C * P * P;
-  const size_t n_patch = (size_t)B * NP * F;
-  const size_t n_cls = (size_t)B * D;
-  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < n_patch + n_cls;
-       e += (size_t)gridDim.x * blockDim.x) {
-    if (e < n_patch) {
-      const int k = (int)(e % F);
-      const size_t row = e / F;
-      const int b = (int)(row / NP), pidx = (int)(row % NP);
-      const int hp = pidx / Wp, wp = pidx - hp * Wp;
-      const int c = k / (P * P), ij = k - c * P * P, i = ij / P, j = ij - i * P;
-      patches[e] = f2bf(img[(((size_t)b * C + c) * H + hp * P + i) * W + wp * P + j]);
-    } else {
-      const size_t e2 = e - n_patch;
-      const int b = (int)(e2 / D), d = (int)(e2 % D);
+                                                           uint32_t thr, float dsc, float* __restrict__ st,
+                                                           bf16* __restrict__ xb, int patch_blocks) {
+  const int Hp = H / P, Wp = W / P, NP = Hp * Wp, F = C * P * P, N = NP + 1;
+  if ((int)blockIdx.x >= patch_blocks) {
+    // cls row of sample b
+    const int b = blockIdx.x - patch_blocks;
+    const size_t row = (size_t)b * N;
+    const uint32_t salt = thr ? site_salt(rng, site) : 0u;
+    float s = 0.f, q = 0.f;
+    for (int d = threadIdx.x; d < D; d += 256) {
       float v = cls[d] + pos[d] + temb[(size_t)t[b] * D + d];
-      const size_t idx = (size_t)b * (NP + 1) * D + d;
-      if (thr) v = dropout_keep(site_salt(rng, site), (uint32_t)idx, thr) ? v * dsc : 0.f;
+      const size_t idx = row * D + d;
+      if (thr) v = dropout_keep(salt, (uint32_t)idx, thr) ? v * dsc : 0.f;
       x[idx] = v;
+      if (st) {
+        xb[idx] = f2bf(v);
+        s += v;
+        q += v * v;
+      }
     }
+    if (st) {
+      __shared__ float red[2][4];
+      s = wave_sum(s);
+      q = wave_sum(q);
+      if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = s;
+        red[1][threadIdx.x >> 6] = q;
+      }
+      __syncthreads();
+      const int np = D / 32;
+      float* sr = st + 2 * row * np;
+      for (int k = threadIdx.x; k < 2 * np; k += 256)
+        sr[k] = k == 0 ? (red[0][0] + red[0][1]) + (red[0][2] + red[0][3])
+                       : k == 1 ? (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]) : 0.f;
+    }
+    return;
+  }
+  const size_t n_patch = (size_t)B * NP * F;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < n_patch;
+       e += (size_t)patch_blocks * blockDim.x) {
+    const int k = (int)(e % F);
+    const size_t row = e / F;
+    const int b = (int)(row / NP), pidx = (int)(row % NP);
+    const int hp = pidx / Wp, wp = pidx - hp * Wp;
+    const int c = k / (P * P), ij = k - c * P * P, i = ij / P, j = ij - i * P;
+    patches[e] = f2bf(img[(((size_t)b * C + c) * H + hp * P + i) * W + wp * P + j]);
   }
 }
 
@@ -179,12 +208,14 @@ using namespace dc;
 
 void patchify_cls_launch(const float* img, const int64_t* t, const float* cls, const float* pos, const float* temb,
                          void* patches, float* x, int B, int C, int H, int W, int patch, int D, const int64_t* rng,
-                         int site, double p, hipStream_t stream) {
-  const size_t n = (size_t)B * (H / patch) * (W / patch) * C * patch * patch + (size_t)B * D;
+                         int site, double p, float* st, void* xb, hipStream_t stream) {
+  const size_t n = (size_t)B * (H / patch) * (W / patch) * C * patch * patch;
   const uint32_t thr = drop_threshold_host(p);
   const float dsc = p > 0 ? 1.f / (1.f - (float)p) : 1.f;
-  hipLaunchKernelGGL(patchify_cls_kernel, dim3(grid_for(n)), dim3(256), 0, stream, img, t, cls, pos, temb,
-                     reinterpret_cast<bf16*>(patches), x, B, C, H, W, patch, D, rng, site, thr, dsc);
+  const int pb = grid_for(n);
+  hipLaunchKernelGGL(patchify_cls_kernel, dim3(pb + B), dim3(256), 0, stream, img, t, cls, pos, temb,
+                     reinterpret_cast<bf16*>(patches), x, B, C, H, W, patch, D, rng, site, thr, dsc, st,
+                     reinterpret_cast<bf16*>(xb), pb);
 }
 
 void embed_bwd_launch(const float* g, const int64_t* t, float* dcls, float* dpos, float* dtemb, void* gpatch, int B,

@@ -64,6 +64,15 @@ struct GemmParams {
   const float* coef;     // HEAD mode 1: {sqrt a_t, sqrt(1-a_t), sqrt a_tk, sqrt(1-a_tk)} (device)
   long long split_stride;  // EPI_F32: elements between the K-split output slices
   int head_mode;         // HEAD: 0 image, 1 fused DDIM step (res = x_t in, C = x_next, C2 = x0), 2 clamp
+  // LayerNorm fold (GemmArgs): consumer side
+  const float* ln_st;
+  const float* ln_c;
+  float ln_eps;
+  float* ln_mean;
+  float* ln_rstd;
+  // producer side
+  float* st_out;
+  bf16* xb_out;
   int debug;  // profiling aid (DDIM_COLD_GEMM_DEBUG): 1 = skip the epilogue, 2 = skip the main loop,
               // 3 = scalar (untransposed) epilogue
 };
@@ -196,9 +205,54 @@ __device__ __forceinline__ long long epi_col(const GemmParams& p, int n) {
   return n;
 }
 
+// ---- LayerNorm fold.  LN(x) W^T + b = rstd * (x (gamma o W)^T - mean * c) + (b + W beta)
+// with c[n] = sum_k bf16(gamma_k W[n][k]) (ln_fold_prep in layernorm.hip), so the
+// GEMM consuming a LayerNorm reads the raw residual stream (its bf16 copy) and
+// the LayerNorm launch disappears.  The row statistics {sum x, sum x^2} come from
+// the epilogue of the GEMM that PRODUCED x (residual / patch-embed epilogue:
+// per-row partial sums over its columns, fp32 atomics).
 template <int EPI>
-__device__ __forceinline__ void epilogue(const GemmParams& p, long long idx, int rb, float v, float pre,
-                                         uint32_t salt_drop, uint32_t salt_dp, const f32x4& cf) {
+struct FoldEpi {
+  static constexpr bool CONSUMER =
+      EPI == EPI_QKV || EPI == EPI_GELU || EPI == EPI_BF16 || EPI == EPI_F32 || EPI == EPI_HEAD;
+  static constexpr bool PRODUCER = EPI == EPI_RESID || EPI == EPI_EMBED;
+};
+
+// Row statistics layout: st[row][NP][2], NP = D / 32 slots; slot s holds
+// {sum, sum^2} of the row's columns 32s..32s+31, written exactly once by the
+// wave of the producing epilogue that owns those columns (no atomics, no
+// zeroing: deterministic).  Consumers add the slots in a fixed butterfly order.
+constexpr int LN_SLOT = 32;
+constexpr int LN_MAX_SLOTS = 16;
+
+// (mean, rstd) of a row from its {sum, sum^2} over D = K columns
+__device__ __forceinline__ float2 ln_row_stats(const GemmParams& p, float2 st) {
+  const float invd = 1.0f / (float)p.K;
+  const float mu = st.x * invd;
+  const float var = fmaxf(st.y * invd - mu * mu, 0.f);
+  return make_float2(mu, rsqrtf(var + p.ln_eps));
+}
+
+__device__ __forceinline__ float2 f2add(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+template <int MASK>
+__device__ __forceinline__ float2 f2xor(float2 a) {
+  return make_float2(__shfl_xor(a.x, MASK), __shfl_xor(a.y, MASK));
+}
+
+// destination token row of a producer epilogue row (statistics index)
+template <int EPI>
+__device__ __forceinline__ int fold_token_row(const GemmParams& p, int m) {
+  if (EPI == EPI_EMBED) {
+    const int b = m / p.tokens;
+    return m + b + 1;  // b*(P+1) + patch + 1
+  }
+  return m;
+}
+
+// returns the stored fp32 value of the residual / embedding epilogues (LayerNorm statistics)
+template <int EPI>
+__device__ __forceinline__ float epilogue(const GemmParams& p, long long idx, int rb, float v, float pre,
+                                          uint32_t salt_drop, uint32_t salt_dp, const f32x4& cf) {
   if (EPI == EPI_BF16) {
     reinterpret_cast<bf16*>(p.C)[idx] = f2bf(v);
   } else if (EPI == EPI_F32) {
@@ -213,6 +267,7 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, long long idx, int
     if (p.thr_drop) v = dropout_keep(salt_drop, (uint32_t)idx, p.thr_drop) ? v * p.scale_drop : 0.f;
     if (p.thr_dp) v = dropout_keep(salt_dp, (uint32_t)rb, p.thr_dp) ? v * p.scale_dp : 0.f;
     reinterpret_cast<float*>(p.C)[idx] = pre + v;
+    return pre + v;
   } else if (EPI == EPI_GELU) {
     reinterpret_cast<bf16*>(p.C)[idx] = f2bf(v);
     float h = gelu_f(v);
@@ -240,7 +295,9 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, long long idx, int
     v += pre;
     if (p.thr_drop) v = dropout_keep(salt_drop, (uint32_t)idx, p.thr_drop) ? v * p.scale_drop : 0.f;
     reinterpret_cast<float*>(p.C)[idx] = v;
+    return v;
   }
+  return 0.f;
 }
 
 // scalar whole-tile epilogue (HEAD: output columns are not contiguous in memory):
@@ -269,6 +326,24 @@ __device__ __forceinline__ void run_epilogue_scalar(const GemmParams& p, const f
       const int m = mb + i * 16 + 4 * g + r;
       rows[i][r] = epi_row<EPI>(p, m < p.M ? m : p.M - 1);
       if (m >= p.M) rows[i][r].off = -1;
+    }
+  // LayerNorm fold, consumer side: per-row statistics and per-column c
+  constexpr bool FC = FoldEpi<EPI>::CONSUMER, FP = FoldEpi<EPI>::PRODUCER;
+  const bool fold = FC && p.ln_st != nullptr;
+  // slot li of each of the lane's rows (the 16 lanes of a row group hold all <= 16 slots)
+  const int np_in = p.K / LN_SLOT;
+  float2 lnst[FM][4];
+  float colc[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) colc[j] = (fold && colok[j]) ? p.ln_c[nb + j * 16 + li] : 0.f;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = mb + i * 16 + 4 * g + r;
+      lnst[i][r] = (fold && m < p.M && li < np_in)
+                       ? *reinterpret_cast<const float2*>(p.ln_st + 2 * ((size_t)m * np_in + li))
+                       : make_float2(0.f, 0.f);
     }
   // phase 1: element loads
   float pre[FM][FN][4];
@@ -299,15 +374,69 @@ __device__ __forceinline__ void run_epilogue_scalar(const GemmParams& p, const f
   if (p.thr_dp) salt_dp = site_salt(p.rng, p.site_dp);
   f32x4 cf = f32x4{0.f, 1.f, 0.f, 0.f};
   if (head_ddim) cf = f32x4{p.coef[0], p.coef[1], p.coef[2], p.coef[3]};
+  float2 ms[FM][4];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (fold) {  // sum the slots across the 16 lanes (fixed butterfly order: identical on every lane)
+        float2 t = lnst[i][r];
+        t = f2add(t, f2xor<1>(t));
+        t = f2add(t, f2xor<2>(t));
+        t = f2add(t, f2xor<4>(t));
+        t = f2add(t, f2xor<8>(t));
+        lnst[i][r] = t;
+      }
+      ms[i][r] = fold ? ln_row_stats(p, lnst[i][r]) : make_float2(0.f, 1.f);
+      const int m = mb + i * 16 + 4 * g + r;
+      // every row's (mean, rstd) for the LayerNorm backward, also rows the epilogue skips
+      if (fold && p.ln_mean != nullptr && nb == 0 && li == 0 && m < p.M) {
+        p.ln_mean[m] = ms[i][r].x;
+        p.ln_rstd[m] = ms[i][r].y;
+      }
+    }
+  const bool prod = FP && p.st_out != nullptr;
+  float2 part[FM][4][(FN + 1) / 2];  // producer (debug path): per-slot partials of the lane's rows
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int sl = 0; sl < (FN + 1) / 2; ++sl) part[i][r][sl] = make_float2(0.f, 0.f);
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        if (rows[i][r].off >= 0 && colok[j])
-          epilogue<EPI>(p, rows[i][r].off + cols[j], rows[i][r].b, acc[i][j][r] + colb[j], pre[i][j][r], salt_drop,
-                        salt_dp, cf);
+        if (rows[i][r].off >= 0 && colok[j]) {
+          const float a = fold ? (acc[i][j][r] - ms[i][r].x * colc[j]) * ms[i][r].y : acc[i][j][r];
+          const float o = epilogue<EPI>(p, rows[i][r].off + cols[j], rows[i][r].b, a + colb[j], pre[i][j][r],
+                                        salt_drop, salt_dp, cf);
+          if (prod) {
+            part[i][r][j / 2] = f2add(part[i][r][j / 2], make_float2(o, o * o));
+            p.xb_out[rows[i][r].off + cols[j]] = f2bf(o);
+          }
+        }
+  if (prod) {
+    const int np_out = p.N / LN_SLOT;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int sl = 0; sl < (FN + 1) / 2; ++sl) {
+          float2 t = part[i][r][sl];
+          t = f2add(t, f2xor<1>(t));
+          t = f2add(t, f2xor<2>(t));
+          t = f2add(t, f2xor<4>(t));
+          t = f2add(t, f2xor<8>(t));
+          const int m = mb + i * 16 + 4 * g + r;
+          if (li == 0 && m < p.M)
+            *reinterpret_cast<float2*>(p.st_out + 2 * ((size_t)fold_token_row<EPI>(p, m) * np_out + nb / LN_SLOT +
+                                                       sl)) = t;
+        }
+  }
 }
 
 
@@ -360,14 +489,23 @@ __device__ __forceinline__ f32x4 ld4bf(const bf16* p) {
 template <int EPI, int FM, int FN>
 struct VecEpi {
   static constexpr bool PRE = EPI == EPI_RESID || EPI == EPI_DGELU || EPI == EPI_EMBED || EPI == EPI_ACC;
+  static constexpr bool FC = FoldEpi<EPI>::CONSUMER, FP = FoldEpi<EPI>::PRODUCER;
   RowInfo rows[FM];
   long long cols[FN];
   bool colok[FN];
   f32x4 colb[FN];
   f32x4 pre[FM][FN];
+  int rowm[FM];     // GEMM row of the lane's fragment row (-1: out of range)
+  float2 lnst[FM][LN_MAX_SLOTS / 4];  // fold consumer: statistics slots q, q+4, .. of the row
+  f32x4 lnc[FN];    // fold consumer: c of the lane's 4 columns
+  bool first_col;   // lane holds column 0 (writes the row's mean / rstd)
+  int colbase;      // first column of the wave's tile
 
   __device__ __forceinline__ void prefetch(const GemmParams& p, int mb, int nb, int g, int li) {
     const int x = li & 3, q = li >> 2;
+    const bool fold = FC && p.ln_st != nullptr;
+    first_col = nb == 0 && q == 0;
+    colbase = nb;
     const bool has_bias = (EPI != EPI_ATOMIC) && (EPI != EPI_ACC) && p.bias != nullptr;
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -381,6 +519,20 @@ struct VecEpi {
       const int m = mb + i * 16 + 4 * g + x;
       rows[i] = epi_row<EPI>(p, m < p.M ? m : p.M - 1);
       if (m >= p.M) rows[i].off = -1;
+      rowm[i] = m < p.M ? m : -1;
+      const int np_in = p.K / LN_SLOT;
+#pragma unroll
+      for (int k = 0; k < LN_MAX_SLOTS / 4; ++k) {
+        const int sl = q + 4 * k;
+        lnst[i][k] = (fold && m < p.M && sl < np_in)
+                         ? *reinterpret_cast<const float2*>(p.ln_st + 2 * ((size_t)m * np_in + sl))
+                         : make_float2(0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = nb + j * 16 + 4 * q;
+      lnc[j] = (fold && colok[j]) ? ld4(p.ln_c + n) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -413,6 +565,30 @@ struct VecEpi {
     uint32_t salt_drop = 0, salt_dp = 0;
     if (p.thr_drop) salt_drop = site_salt(p.rng, p.site_drop);
     if (p.thr_dp) salt_dp = site_salt(p.rng, p.site_dp);
+    const bool fold = FC && p.ln_st != nullptr;
+    const bool prod = FP && p.st_out != nullptr;
+    float2 ms[FM];
+    constexpr int SL = FN / 2;  // 32-column statistics slots per wave
+    float2 part[FM][SL];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      if (fold) {  // the row's slots: lane-local, then across the 4 lanes of the row (fixed order)
+        float2 t = lnst[i][0];
+#pragma unroll
+        for (int k = 1; k < LN_MAX_SLOTS / 4; ++k) t = f2add(t, lnst[i][k]);
+        t = f2add(t, f2xor<4>(t));
+        t = f2add(t, f2xor<8>(t));
+        ms[i] = ln_row_stats(p, t);
+      } else {
+        ms[i] = make_float2(0.f, 1.f);
+      }
+#pragma unroll
+      for (int sl = 0; sl < SL; ++sl) part[i][sl] = make_float2(0.f, 0.f);
+      if (fold && p.ln_mean != nullptr && first_col && rowm[i] >= 0) {
+        p.ln_mean[rowm[i]] = ms[i].x;
+        p.ln_rstd[rowm[i]] = ms[i].y;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       if (rows[i].off < 0) continue;
@@ -422,7 +598,7 @@ struct VecEpi {
       for (int j = 0; j < FN; ++j) {
         if (!colok[j]) continue;
         const long long idx = rows[i].off + cols[j];
-        f32x4 v = acc[i][j] + colb[j];
+        f32x4 v = fold ? (acc[i][j] - ms[i].x * lnc[j]) * ms[i].y + colb[j] : acc[i][j] + colb[j];
         if (EPI == EPI_BF16 || EPI == EPI_QKV) {
           st4bf(reinterpret_cast<bf16*>(p.C) + idx, v);
         } else if (EPI == EPI_F32) {
@@ -441,6 +617,11 @@ struct VecEpi {
             v[c] = pre[i][j][c] + e;
           }
           st4(reinterpret_cast<float*>(p.C) + idx, v);
+          if (prod) {
+            part[i][j / 2] = f2add(part[i][j / 2], make_float2((v[0] + v[1]) + (v[2] + v[3]),
+                                                               (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3])));
+            st4bf(p.xb_out + idx, v);
+          }
         } else if (EPI == EPI_GELU) {
           st4bf(reinterpret_cast<bf16*>(p.C) + idx, v);
           f32x4 h;
@@ -465,8 +646,30 @@ struct VecEpi {
           for (int c = 0; c < 4; ++c)
             if (p.thr_drop) v[c] = dropout_keep(salt_drop, (uint32_t)(idx + c), p.thr_drop) ? v[c] * p.scale_drop : 0.f;
           st4(reinterpret_cast<float*>(p.C) + idx, v);
+          if (prod) {
+            part[i][j / 2] = f2add(part[i][j / 2], make_float2((v[0] + v[1]) + (v[2] + v[3]),
+                                                               (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3])));
+            st4bf(p.xb_out + idx, v);
+          }
         }
       }
+    }
+    if (prod) {
+      // the 4 lanes of a row (q = 0..3: lanes x, x+4, x+8, x+12 of the 16-lane
+      // group) hold 32 consecutive columns per slot: reduce, one float2 store per
+      // (row, slot)
+      const int np_out = p.N / LN_SLOT;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int sl = 0; sl < SL; ++sl) {
+          float2 t = part[i][sl];
+          t = f2add(t, f2xor<4>(t));
+          t = f2add(t, f2xor<8>(t));
+          if ((li >> 2) == 0 && rowm[i] >= 0)
+            *reinterpret_cast<float2*>(p.st_out + 2 * ((size_t)fold_token_row<EPI>(p, rowm[i]) * np_out +
+                                                       colbase / LN_SLOT + sl)) = t;
+        }
     }
   }
 };
@@ -1121,6 +1324,8 @@ static GemmParams base_params(const GemmArgs& a) {
   p.pos = a.pos; p.temb = a.temb; p.tsteps = a.tsteps; p.emb_dim = a.emb_dim;
   p.coef = a.coef; p.head_mode = a.head_mode;
   p.split_stride = a.split_stride;
+  p.ln_st = a.ln_st; p.ln_c = a.ln_c; p.ln_eps = a.ln_eps; p.ln_mean = a.ln_mean; p.ln_rstd = a.ln_rstd;
+  p.st_out = a.st_out; p.xb_out = reinterpret_cast<bf16*>(a.xb_out);
   return p;
 }
 

@@ -45,6 +45,21 @@ struct GemmArgs {
   // C + z * split_stride (no atomics, no zeroing; the consumer sums the slices)
   int splits = 1;
   long long split_stride = 0;
+  // LayerNorm folded into the GEMM (see gemm.hip "LayerNorm fold"):
+  // consumer (QKV / GELU / HEAD / BF16 / F32): A = bf16(x), B = bf16(gamma o W),
+  //   bias = b + W beta, y = rstd*(acc - mean*ln_c) + bias with (mean, rstd)
+  //   from the row statistics ln_st[m][K/32] = {sum x, sum x^2} per 32-column
+  //   slot; optional mean/rstd out
+  const float* ln_st = nullptr;
+  const float* ln_c = nullptr;
+  float ln_eps = 1e-5f;
+  float* ln_mean = nullptr;
+  float* ln_rstd = nullptr;
+  // producer (RESID / EMBED): write {sum, sum^2} of every output row's 32-column
+  // slots into st_out[row][N/32] (each slot written once: deterministic, no
+  // zeroing) and a bf16 copy of the output to xb_out
+  float* st_out = nullptr;
+  void* xb_out = nullptr;
 };
 
 void gemm_nt(const GemmArgs& a, int epi, hipStream_t stream);
@@ -85,10 +100,30 @@ void layernorm_fwd_launch(const float* x, const float* gamma, const float* beta,
 // dgamma||dbeta partials go into ws [ln_replicas()][2D] (must be zero on entry);
 // replica_reduce_launch adds them into the destinations and re-zeroes ws.
 void layernorm_bwd_launch(const float* dy, const float* x, const float* mean, const float* rstd,
-                          const float* gamma, const float* g_res, float* g_out, void* gy_bf16, float* dgb_ws, int M,
+                          const float* gamma, const float* beta, const float* g_res, float* g_out, void* gy_bf16,
+                          void* y_bf16, float* dgb_ws, int M,
                           int D, int tokens, const int64_t* rng, int site_drop, double p_drop, int site_dp,
                           double p_dp, int dy_parts, hipStream_t stream);
 int ln_replicas();
+
+// LayerNorm fold weights for the GEMMs that consume a LayerNorm (layernorm.hip)
+constexpr int FOLD_MAX = 16;
+struct FoldJob {
+  const float* w;      // [rows][K] fp32 master weight
+  const float* gamma;  // [K]
+  const float* beta;   // [K]
+  const float* bias;   // [rows] or null
+  void* wf;            // [rows][K] bf16 out: gamma o W
+  float* c;            // [rows] out: row sums of wf
+  float* bf;           // [rows] out: bias + W beta
+};
+struct FoldTable {
+  FoldJob j[FOLD_MAX];
+  int start[FOLD_MAX + 1];
+  int n;
+  int K;
+};
+void ln_fold_launch(const FoldTable& tb, hipStream_t stream);
 void replica_reduce_launch(float* ws, float* const* dsts_dev, int G, int C, hipStream_t stream);
 
 // Attention (attention.hip)
@@ -101,7 +136,7 @@ void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const flo
 // Embedding / head / loss (embed.hip)
 void patchify_cls_launch(const float* img, const int64_t* t, const float* cls, const float* pos,
                          const float* temb, void* patches, float* x, int B, int C, int H, int W, int patch,
-                         int D, const int64_t* rng, int site, double p, hipStream_t stream);
+                         int D, const int64_t* rng, int site, double p, float* st, void* xb, hipStream_t stream);
 void embed_bwd_launch(const float* g, const int64_t* t, float* dcls, float* dpos, float* dtemb, void* gpatch,
                       int B, int N, int D, const int64_t* rng, int site, double p, hipStream_t stream);
 void smooth_l1_launch(const float* pred, const float* target, float* loss, float* partials, void* dtok, int B,
@@ -131,3 +166,7 @@ void q_sample_launch(const float* x0, const int64_t* t, const float* eps, float*
 void cold_batch_launch(const float* pool, int pool_n, const int64_t* rng, int site, float* x_t, float* x_tm1,
                        int64_t* t, int64_t* idx_ws, int B, int C, int H, int W, int max_t, bool draw_idx,
                        hipStream_t stream);
+
+// gradient wire format (comm_wire.hip): fp32 <-> bf16 (RNE), 16-B aligned buffers
+void wire_pack_launch(const float* src, void* dst, int64_t n, hipStream_t stream);
+void wire_unpack_launch(const void* src, float* dst, int64_t n, hipStream_t stream);

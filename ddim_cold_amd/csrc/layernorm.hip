@@ -69,9 +69,10 @@ __global__ __launch_bounds__(NW * 64) void ln_fwd_kernel(const float* __restrict
 template <int VEC, int RPW, int NW>
 __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                     const float* __restrict__ gamma, const float* __restrict__ g_res,
+                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                     const float* __restrict__ g_res,
                                                      float* __restrict__ g_out, bf16* __restrict__ gy,
-                                                     float* __restrict__ dgb_ws, int M,
+                                                     bf16* __restrict__ y_out, float* __restrict__ dgb_ws, int M,
                                                      int tokens, const int64_t* __restrict__ rng, int site_drop,
                                                      uint32_t thr_drop, float sc_drop, int site_dp, uint32_t thr_dp,
                                                      float sc_dp, int dy_parts) {
@@ -79,12 +80,13 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const float* __restrict
   __shared__ float red[NW][2 * D];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float2* g2 = reinterpret_cast<const float2*>(gamma);
-  float2 dgam[VEC], dbet[VEC], gm[VEC];
+  float2 dgam[VEC], dbet[VEC], gm[VEC], bt[VEC];
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
     dgam[i] = make_float2(0.f, 0.f);
     dbet[i] = make_float2(0.f, 0.f);
     gm[i] = g2[lane + 64 * i];
+    bt[i] = y_out ? reinterpret_cast<const float2*>(beta)[lane + 64 * i] : make_float2(0.f, 0.f);
   }
   uint32_t salt_drop = 0, salt_dp = 0;
   if (gy) {
@@ -149,6 +151,14 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const float* __restrict
       float2 o = make_float2((dxh[i].x - c1 - xh[i].x * c2) * rs + rv[j][i].x,
                              (dxh[i].y - c1 - xh[i].y * c2) * rs + rv[j][i].y);
       reinterpret_cast<float2*>(g_out + (size_t)row * D)[c] = o;
+      if (y_out) {
+        // the LayerNorm output itself (bf16), for the weight gradient of the GEMM
+        // that consumed it with the LayerNorm folded in (no forward LayerNorm launch)
+        bf16x2 yv;
+        yv[0] = f2bf(xh[i].x * gm[i].x + bt[i].x);
+        yv[1] = f2bf(xh[i].y * gm[i].y + bt[i].y);
+        reinterpret_cast<bf16x2*>(y_out + (size_t)row * D)[c] = yv;
+      }
       if (gy) {
         float a = o.x * dpsc, b = o.y * dpsc;
         if (thr_drop) {
@@ -203,9 +213,70 @@ __global__ __launch_bounds__(256) void replica_reduce_kernel(float* __restrict__
   dsts[gi][c] += s;
 }
 
+// LayerNorm fold weights (see gemm.hip "LayerNorm fold"): for each GEMM that
+// consumes a LayerNorm, wf[n][k] = bf16(gamma_k W[n][k]), c[n] = sum_k wf[n][k]
+// (the bf16 values the MFMA multiplies, so the mean term cancels exactly what
+// the GEMM accumulated), bf[n] = b[n] + sum_k beta_k W[n][k].  One wave per
+// output row, all folded GEMMs of the model in one launch (after each
+// optimizer step; once per sampling run).
+__global__ __launch_bounds__(256) void ln_fold_kernel(FoldTable tb) {
+  // two rows per wave (32 lanes each), every load of the row issued before use
+  constexpr int IT = 4;  // float4 per lane: K <= 32 * 4 * IT = 512
+  const int hl = threadIdx.x & 31;
+  const int r = blockIdx.x * 8 + (threadIdx.x >> 5);
+  const bool live = r < tb.start[tb.n];
+  const int rr = live ? r : tb.start[tb.n] - 1;
+  int ji = 0;
+#pragma unroll
+  for (int j = 1; j < FOLD_MAX; ++j)
+    if (j < tb.n && rr >= tb.start[j]) ji = j;
+  const FoldJob& jb = tb.j[ji];
+  const int n = rr - tb.start[ji], K4 = tb.K / 4;
+  const float4* w = reinterpret_cast<const float4*>(jb.w + (size_t)n * tb.K);
+  const float4* g = reinterpret_cast<const float4*>(jb.gamma);
+  const float4* b = reinterpret_cast<const float4*>(jb.beta);
+  bf16x4* o = reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(jb.wf) + (size_t)n * tb.K);
+  float4 wv[IT], gv[IT], bv[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int k = hl + 32 * i;
+    const bool ok = k < K4;
+    wv[i] = ok ? w[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+    gv[i] = ok ? g[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+    bv[i] = ok ? b[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float cs = 0.f, bs = 0.f;
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int k = hl + 32 * i;
+    bf16x4 q;
+    q[0] = f2bf(gv[i].x * wv[i].x); q[1] = f2bf(gv[i].y * wv[i].y);
+    q[2] = f2bf(gv[i].z * wv[i].z); q[3] = f2bf(gv[i].w * wv[i].w);
+    if (live && k < K4) o[k] = q;
+    cs += (bf2f(q[0]) + bf2f(q[1])) + (bf2f(q[2]) + bf2f(q[3]));
+    bs += (bv[i].x * wv[i].x + bv[i].y * wv[i].y) + (bv[i].z * wv[i].z + bv[i].w * wv[i].w);
+  }
+#pragma unroll
+  for (int m = 16; m > 0; m >>= 1) {
+    cs += __shfl_xor(cs, m, 32);
+    bs += __shfl_xor(bs, m, 32);
+  }
+  if (live && hl == 0) {
+    jb.c[n] = cs;
+    jb.bf[n] = bs + (jb.bias ? jb.bias[n] : 0.f);
+  }
+}
+
 }  // namespace dc
 
 using namespace dc;
+
+void ln_fold_launch(const FoldTable& tb, hipStream_t stream) {
+  if (tb.n <= 0) return;
+  if (tb.n > FOLD_MAX || tb.K % 4 || tb.K > 512) throw std::runtime_error("ln_fold: bad table (K % 4, K <= 512)");
+  const int rows = tb.start[tb.n];
+  hipLaunchKernelGGL(ln_fold_kernel, dim3((rows + 7) / 8), dim3(256), 0, stream, tb);
+}
 
 #define LN_DISPATCH(D, ...)                                                   \
   switch ((D) / 128) {                                                        \
@@ -239,7 +310,8 @@ void layernorm_fwd_launch(const float* x, const float* gamma, const float* beta,
 }
 
 void layernorm_bwd_launch(const float* dy, const float* x, const float* mean, const float* rstd,
-                          const float* gamma, const float* g_res, float* g_out, void* gy_bf16, float* dgb_ws, int M,
+                          const float* gamma, const float* beta, const float* g_res, float* g_out, void* gy_bf16,
+                          void* y_bf16, float* dgb_ws, int M,
                           int D, int tokens, const int64_t* rng, int site_drop, double p_drop, int site_dp,
                           double p_dp, int dy_parts, hipStream_t stream) {
   if (D % 128) throw std::runtime_error("layernorm: D % 128 != 0");
@@ -253,8 +325,9 @@ void layernorm_bwd_launch(const float* dy, const float* x, const float* mean, co
   }();
 #define LN_BWD_GO(R, W)                                                                                      \
   LN_DISPATCH(D, hipLaunchKernelGGL((ln_bwd_kernel<VEC, R, W>), dim3((M + R * W - 1) / (R * W)), dim3(W * 64), 0, \
-                                    stream, dy, x, mean, rstd, gamma, g_res, g_out,                           \
-                                    reinterpret_cast<bf16*>(gy_bf16), dgb_ws, M, tokens, rng, site_drop, td,   \
+                                    stream, dy, x, mean, rstd, gamma, beta, g_res, g_out,                     \
+                                    reinterpret_cast<bf16*>(gy_bf16), reinterpret_cast<bf16*>(y_bf16), dgb_ws,  \
+                                    M, tokens, rng, site_drop, td,                                              \
                                     sd, site_dp, tp, sp, dy_parts))
   // measured on the ViT-tiny shape (M 2080, D 384, dropout on): 1 row x 8 waves
   // 5.0 us, 2 x 4 5.9, 1 x 4 5.2, 1 x 16 5.1, 2 x 16 7.2

@@ -34,6 +34,19 @@ FUSE_LN = os.environ.get("DDIM_COLD_FUSE_LN", "0") == "1"  # residual GEMM + Lay
 # K split of the QKV input-gradient GEMM (reduction dim 3D): the partial products
 # go to separate buffers that the LayerNorm backward sums on load
 QKV_DGRAD_SPLITS = int(os.environ.get("DDIM_COLD_QKV_DGRAD_SPLITS", "2"))
+# LayerNorm fold (csrc/gemm.hip): every LayerNorm is folded into the GEMM that
+# consumes it (QKV, fc1, head) -- no LayerNorm launch in the forward.  The
+# producing GEMM's epilogue accumulates the row statistics; the LayerNorm
+# backward re-emits the normalised rows for the weight gradients.
+FOLD_LN = os.environ.get("DDIM_COLD_LN_FOLD", "1") == "1"
+# dtype of the bf16 activation copies / folded weights the program allocates
+# (tests on CPU switch it to fp32 to isolate the program logic from rounding)
+ACT_DTYPE = torch.bfloat16
+
+
+def fold_width_ok(D: int) -> bool:
+    """Widths the LayerNorm fold supports (csrc/gemm.hip: 32-column statistics slots, <= 16)."""
+    return D % 32 == 0 and D // 32 <= 16
 
 
 def block_sites(i: int):
@@ -56,6 +69,13 @@ class BlockTensors:
     fc1_b: torch.Tensor
     fc2_w: torch.Tensor
     fc2_b: torch.Tensor
+    # LayerNorm fold (LnFold.attach): gamma-scaled bf16 weight, its row sums, folded bias
+    qkv_wf: Optional[torch.Tensor] = None
+    qkv_c: Optional[torch.Tensor] = None
+    qkv_bf: Optional[torch.Tensor] = None
+    fc1_wf: Optional[torch.Tensor] = None
+    fc1_c: Optional[torch.Tensor] = None
+    fc1_bf: Optional[torch.Tensor] = None
 
 
 @dataclass
@@ -71,6 +91,13 @@ class ModelTensors:
     nb: torch.Tensor
     head_w: torch.Tensor
     head_b: torch.Tensor
+    head_wf: Optional[torch.Tensor] = None
+    head_c: Optional[torch.Tensor] = None
+    head_bf: Optional[torch.Tensor] = None
+
+    @property
+    def folded(self) -> bool:
+        return self.head_wf is not None
 
 
 MATRIX_SUFFIXES = ("attn.qkv.weight", "attn.proj.weight", "mlp.fc1.weight", "mlp.fc2.weight")
@@ -97,6 +124,67 @@ def collect(named: Dict[str, torch.Tensor], depth: int, D: int) -> ModelTensors:
         pe_w=pe_w.reshape(pe_w.shape[0], -1) if pe_w is not None else None,
         pe_b=g("patch_embed.proj.bias"), temb=g("time_embed.weight"), blocks=blocks,
         nw=g("norm.weight"), nb=g("norm.bias"), head_w=g("head.weight"), head_b=g("head.bias"))
+
+
+class LnFold:
+    """Folded weights of every GEMM that consumes a LayerNorm (QKV <- norm1,
+    fc1 <- norm2, head <- norm), in three flat arenas; :meth:`refresh` recomputes
+    them from the fp32 masters in one ``ln_fold_`` launch per 16 GEMMs (after
+    every optimizer step in the train engine; once per weight version for
+    inference)."""
+
+    @staticmethod
+    def jobs(depth: int):
+        """(key, weight, gamma, beta, bias) parameter names of every folded GEMM."""
+        jobs = []
+        for i in range(depth):
+            p = f"blocks.{i}."
+            jobs.append((("qkv", i), p + "attn.qkv.weight", p + "norm1.weight", p + "norm1.bias", p + "attn.qkv.bias"))
+            jobs.append((("fc1", i), p + "mlp.fc1.weight", p + "norm2.weight", p + "norm2.bias", p + "mlp.fc1.bias"))
+        jobs.append((("head",), "head.weight", "norm.weight", "norm.bias", "head.bias"))
+        return jobs
+
+    @staticmethod
+    def names(depth: int):
+        return [n for j in LnFold.jobs(depth) for n in j[1:]]
+
+    def __init__(self, named32: Dict[str, torch.Tensor], depth: int):
+        jobs = self.jobs(depth)
+        self.keys = [j[0] for j in jobs]
+        self.src = [tuple(named32[n] for n in j[1:]) for j in jobs]
+        w0 = self.src[0][0]
+        dev, K = w0.device, w0.shape[1]
+        rows = [w.shape[0] for w, _, _, _ in self.src]
+        # 16-B aligned sub-ranges (vector loads/stores in the GEMMs)
+        offs, o = [], 0
+        for r in rows:
+            offs.append(o)
+            o += (r + 7) // 8 * 8
+        self.wf_arena = torch.zeros(o * K, dtype=ACT_DTYPE, device=dev)
+        self.c_arena = torch.zeros(o, dtype=torch.float32, device=dev)
+        self.bf_arena = torch.zeros(o, dtype=torch.float32, device=dev)
+        self.out = {}
+        for key, r, off in zip(self.keys, rows, offs):
+            self.out[key] = (self.wf_arena[off * K:(off + r) * K].view(r, K), self.c_arena[off:off + r],
+                             self.bf_arena[off:off + r])
+
+    def tensors(self):
+        return [t for w, g, b, bias in self.src for t in (w, g, b, bias)]
+
+    def refresh(self):
+        for a in range(0, len(self.keys), 16):
+            ks = self.keys[a:a + 16]
+            src = self.src[a:a + 16]
+            ops.ln_fold_([w.reshape(w.shape[0], -1) for w, _, _, _ in src], [g for _, g, _, _ in src],
+                         [b for _, _, b, _ in src], [bias for _, _, _, bias in src],
+                         [self.out[k][0] for k in ks], [self.out[k][1] for k in ks], [self.out[k][2] for k in ks])
+
+    def attach(self, P: "ModelTensors") -> "ModelTensors":
+        for i, bp in enumerate(P.blocks):
+            bp.qkv_wf, bp.qkv_c, bp.qkv_bf = self.out[("qkv", i)]
+            bp.fc1_wf, bp.fc1_c, bp.fc1_bf = self.out[("fc1", i)]
+        P.head_wf, P.head_c, P.head_bf = self.out[("head",)]
+        return P
 
 
 @dataclass
@@ -168,6 +256,8 @@ class ViTProgram:
         """``head_step = (mode, x0_out, coef)`` fuses the sampler update into the head
         GEMM (``ops.head_step_``): ``img`` (the current x_t) is updated in place and
         returned; mode 1 = DDIM step, mode 2 = clamp (cold sampler)."""
+        if P.folded and fold_width_ok(self.cfg.dim):
+            return self._forward_folded(P, img, t, rng, training, save, head_step)
         c = self.cfg
         B = img.shape[0]
         N, D, M = c.tokens, c.dim, B * c.tokens
@@ -219,6 +309,63 @@ class ViTProgram:
             S.xL, S.lf, S.mf, S.rf = x, lf, mf, rf
         return out, S
 
+    def _forward_folded(self, P: ModelTensors, img, t, rng, training: bool, save: bool, head_step):
+        """Forward with every LayerNorm folded into its consumer GEMM: 5 launches
+        per block (QKV, attention, proj+residual, fc1+GELU, fc2+residual).  The
+        residual GEMMs (and the patch embedding) emit each new residual row's
+        {sum, sum^2} and bf16 copy; QKV / fc1 / head read that copy with
+        gamma-scaled weights and apply mean / rstd in their epilogue.  Saved
+        tensors match the unfolded forward except the LayerNorm outputs (None:
+        the backward re-emits them)."""
+        c = self.cfg
+        B = img.shape[0]
+        N, D, M, L = c.tokens, c.dim, B * c.tokens, c.depth
+        pd = c.drop if training else 0.0
+        ad = c.attn_drop if training else 0.0
+        dpr = c.dpr if training else [0.0] * c.depth
+        dev = img.device
+        # row statistics of every LayerNorm input ({sum, sum^2} per 32-column slot),
+        # each slot written once by the producing epilogue
+        st = torch.empty(2 * L + 1, M, D // 32, 2, dtype=torch.float32, device=dev)
+        xb = torch.empty(M, D, dtype=ACT_DTYPE, device=dev)
+        x, patches = ops.patch_embed_fwd(img, t, P.pe_w, P.pe_b, P.cls, P.pos, P.temb, rng, SITE_EMBED, pd,
+                                         c.patch, ln_st=st[0], xb_out=xb)
+        x = x.view(M, D)
+        S = Saved(t=t, patches=patches) if save else None
+
+        def stats():
+            return (torch.empty(M, dtype=torch.float32, device=dev),
+                    torch.empty(M, dtype=torch.float32, device=dev)) if save else (None, None)
+        for i, bp in enumerate(P.blocks):
+            sa, sp, sd1, sf1, sf2, sd2 = block_sites(i)
+            x0 = x
+            m1, r1 = stats()
+            qkv = ops.qkv_fwd(xb, bp.qkv_wf, bp.qkv_bf, B, N, c.heads, fold=(st[2 * i], bp.qkv_c, c.eps, m1, r1))
+            o, lse = ops.attn_fwd(qkv, c.scale, rng, sa, ad)
+            o = o.view(M, D)
+            x1b = torch.empty(M, D, dtype=ACT_DTYPE, device=dev)
+            x1 = ops.linear_residual_fwd(o, bp.proj_w, bp.proj_b, x0, N, rng, sp, pd, sd1, dpr[i],
+                                         st_out=st[2 * i + 1], xb_out=x1b)
+            m2, r2 = stats()
+            u, h = ops.linear_gelu_fwd(x1b, bp.fc1_wf, bp.fc1_bf, rng, sf1, pd,
+                                       fold=(st[2 * i + 1], bp.fc1_c, c.eps, m2, r2))
+            xb = torch.empty(M, D, dtype=ACT_DTYPE, device=dev)
+            x = ops.linear_residual_fwd(h, bp.fc2_w, bp.fc2_b, x1, N, rng, sf2, pd, sd2, dpr[i],
+                                        st_out=st[2 * i + 2], xb_out=xb)
+            if save:
+                S.blocks.append((x0, None, m1, r1, qkv, o, lse, x1, None, m2, r2, u, h))
+        if head_step is not None:
+            mode, x0_out, coef = head_step
+            ops.head_step_(xb, P.head_wf, P.head_bf, img, x0_out, coef, c.patch, mode,
+                           fold=(st[2 * L], P.head_c, c.eps))
+            return img, S
+        mf, rf = stats()
+        out = ops.head_fwd(xb, P.head_wf, P.head_bf, B, c.chans, c.img_h, c.img_w, c.patch,
+                           fold=(st[2 * L], P.head_c, c.eps, mf, rf))
+        if save:
+            S.xL, S.lf, S.mf, S.rf = x, None, mf, rf
+        return out, S
+
     # ------------------------------------------------------------------ backward
     def backward_iter(self, P: ModelTensors, G: ModelTensors, S: Saved, dtok: torch.Tensor, rng: torch.Tensor,
                       training: bool = True, wgrad: Optional[Callable] = None,
@@ -250,11 +397,20 @@ class ViTProgram:
         ad = c.attn_drop if training else 0.0
         dpr = c.dpr if training else [0.0] * c.depth
         L = c.depth
+        M = dtok.shape[0]
+        # LayerNorm fold: the forward never materialised the LayerNorm outputs;
+        # each LayerNorm backward re-emits its output (bf16) for the weight
+        # gradient queued right after it
+        fold = S.lf is None
+
+        def ln_out(lo):
+            return torch.empty(M, D, dtype=ACT_DTYPE, device=dtok.device) if fold else lo
         dlf = ops.linear_dgrad(dtok, P.head_w, True)
-        wgrad(dtok, S.lf, G.head_w, G.head_b)
+        lf = ln_out(S.lf)
         _, _, _, _, sf2, sd2 = block_sites(L - 1)
         g, gy = ops.layernorm_bwd(dlf, S.xL, S.mf, S.rf, P.nw, None, G.nw, G.nb, N, rng, sf2, pd, sd2,
-                                  dpr[L - 1], True, ws(0))
+                                  dpr[L - 1], True, ws(0), beta=P.nb if fold else None, y_out=lf if fold else None)
+        wgrad(dtok, lf, G.head_w, G.head_b)
         keep = []
         for i in range(L - 1, -1, -1):
             x0, l1, m1, r1, qkv, o, lse, x1, l2, m2, r2, u, h = S.blocks[i]
@@ -262,24 +418,27 @@ class ViTProgram:
             sa, sp, sd1, sf1, _, _ = block_sites(i)
             wgrad(gy, h, bg.fc2_w, bg.fc2_b)
             du = ops.linear_dgrad_gelu(gy, bp.fc2_w, u, rng, sf1, pd)
-            wgrad(du, l2, bg.fc1_w, bg.fc1_b)
             dl2 = ops.linear_dgrad(du, bp.fc1_w, True)
             k2 = 1 + 2 * (L - 1 - i)
+            l2 = ln_out(l2)
             g1, gy1 = ops.layernorm_bwd(dl2, x1, m2, r2, bp.n2w, g, bg.n2w, bg.n2b, N, rng, sp, pd, sd1, dpr[i],
-                                        True, ws(k2))
+                                        True, ws(k2), beta=bp.n2b if fold else None, y_out=l2 if fold else None)
+            wgrad(du, l2, bg.fc1_w, bg.fc1_b)
             wgrad(gy1, o, bg.proj_w, bg.proj_b)
             do = ops.linear_dgrad(gy1, bp.proj_w, False)
             dqkv = ops.attn_bwd(do, qkv, o, lse, c.scale, rng, sa, ad)
-            wgrad(dqkv, l1, bg.qkv_w, bg.qkv_b)
             dl1 = ops.linear_dgrad(dqkv, bp.qkv_w, True, QKV_DGRAD_SPLITS if 3 * D >= 768 else 1)
+            l1 = ln_out(l1)
+            fk = dict(beta=bp.n1b, y_out=l1) if fold else {}
             if i > 0:
                 _, _, _, _, psf2, psd2 = block_sites(i - 1)
                 g, gy = ops.layernorm_bwd(dl1, x0, m1, r1, bp.n1w, g1, bg.n1w, bg.n1b, N, rng, psf2, pd, psd2,
-                                          dpr[i - 1], True, ws(k2 + 1))
+                                          dpr[i - 1], True, ws(k2 + 1), **fk)
             else:
                 g, gy = ops.layernorm_bwd(dl1, x0, m1, r1, bp.n1w, g1, bg.n1w, bg.n1b, N, rng, 0, 0.0, 0, 0.0,
-                                          False, ws(k2 + 1))
-            keep.append((gy1, du, dqkv))
+                                          False, ws(k2 + 1), **fk)
+            wgrad(dqkv, l1, bg.qkv_w, bg.qkv_b)
+            keep.append((gy1, du, dqkv, l1, l2))
             flush()
             yield i
         B = S.t.shape[0]
@@ -287,7 +446,7 @@ class ViTProgram:
         gpatch = ops.embed_bwd(g.view(B, N, D), S.t, rng, SITE_EMBED, pd, G.cls, G.pos, temb_g)
         wgrad(gpatch, S.patches, G.pe_w, G.pe_b)
         flush()
-        keep.append(gpatch)
+        keep.append((gpatch, lf))
         if batch is not None:
             keep.append(batch.keep)
         self._keep = keep  # holds side-stream operands alive until the caller joins
@@ -324,7 +483,23 @@ def model_tensors(model, named: Optional[Dict[str, torch.Tensor]] = None) -> Mod
     conv = {}
     for n, p in named.items():
         conv[n] = _bf16_cached(model, n, p) if is_matrix_param(n) else p.detach()
-    return collect(conv, len(model.blocks), model.embed_dim)
+    P = collect(conv, len(model.blocks), model.embed_dim)
+    if FOLD_LN:
+        _fold_cached(model, named).attach(P)
+    return P
+
+
+def _fold_cached(model, named: Dict[str, torch.Tensor]) -> LnFold:
+    """LnFold of the given fp32 parameters, recomputed when any input changes version."""
+    depth = len(model.blocks)
+    key = tuple((named[n].data_ptr(), named[n]._version, named[n].device) for n in LnFold.names(depth))
+    cache = model.__dict__.get("_ln_fold")
+    if cache is not None and cache[0] == key:
+        return cache[1]
+    fold = LnFold({n: p.detach() for n, p in named.items()}, depth)
+    fold.refresh()
+    model.__dict__["_ln_fold"] = (key, fold)
+    return fold
 
 
 def rng_state(model, device) -> torch.Tensor:

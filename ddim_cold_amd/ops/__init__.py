@@ -21,7 +21,7 @@ __all__ = [
     "linear_residual_fwd", "linear_gelu_fwd", "head_fwd", "smooth_l1_fwd_bwd", "img_to_tokgrad",
     "linear_dgrad", "linear_dgrad_gelu", "linear_wgrad", "layernorm_bwd", "attn_bwd", "embed_bwd",
     "sqnorm", "adamw_step", "advance_counters", "ddim_step", "ddim_step_", "randn_", "q_sample",
-    "pixelate_pair", "cold_batch",
+    "pixelate_pair", "cold_batch", "ln_fold_",
 ]
 
 
@@ -38,10 +38,14 @@ def _ops():
 
 
 # ----------------------------------------------------------------------------- forward
-def patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site: int, p: float, patch: int):
+def patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site: int, p: float, patch: int, ln_st=None,
+                    xb_out=None):
+    """Tokens + bf16 patches.  LayerNorm fold: ``ln_st`` ([B*N, D/32, 2]) gets the
+    tokens' row statistics ({sum, sum^2} per 32-column slot); ``xb_out`` their
+    bf16 copy (the A operand of the first QKV GEMM)."""
     if _hip(img):
-        return _ops().patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site, float(p), patch)
-    return ref.patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site, p, patch)
+        return _ops().patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site, float(p), patch, ln_st, xb_out)
+    return ref.patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site, p, patch, ln_st, xb_out)
 
 
 def layernorm_fwd(x, gamma, beta, eps: float = 1e-5):
@@ -50,17 +54,32 @@ def layernorm_fwd(x, gamma, beta, eps: float = 1e-5):
     return ref.layernorm_fwd(x, gamma, beta, eps)
 
 
-def linear_fwd(a, w, b=None, out_fp32: bool = False):
-    """Plain ``a @ w.T + b`` on the MFMA GEMM (bf16 or fp32 output)."""
+def linear_fwd(a, w, b=None, out_fp32: bool = False, fold=None):
+    """Plain ``a @ w.T + b`` on the MFMA GEMM (bf16 or fp32 output).  ``fold =
+    (ln_st, ln_c, eps)``: LayerNorm folded in (``a`` = raw rows, ``w``/``b`` folded)."""
+    st, c, eps = fold if fold is not None else (None, None, 1e-5)
     if _hip(a):
-        return _ops().linear_fwd(a, w, b, bool(out_fp32))
-    return ref.linear_fwd(a, w, b, out_fp32)
+        return _ops().linear_fwd(a, w, b, bool(out_fp32), st, c, float(eps))
+    return ref.linear_fwd(a, w, b, out_fp32, st, c, eps)
 
 
-def qkv_fwd(a, w, b, B: int, N: int, H: int):
+def _fold_args(fold):
+    """``fold = (ln_st, ln_c, eps[, mean_out, rstd_out])`` -> op keyword tuple."""
+    if fold is None:
+        return None, None, 1e-5, None, None
+    st, c, eps = fold[:3]
+    mean, rstd = (fold[3], fold[4]) if len(fold) > 3 else (None, None)
+    return st, c, float(eps), mean, rstd
+
+
+def qkv_fwd(a, w, b, B: int, N: int, H: int, fold=None):
+    """QKV projection, head-major [3,B,H,N,hd].  ``fold = (ln_st, ln_c, eps, mean_out,
+    rstd_out)``: the preceding LayerNorm folded in (``a`` = bf16 residual rows,
+    ``w``/``b`` from :func:`ln_fold_`); mean/rstd of the rows written for the backward."""
+    st, c, eps, mean, rstd = _fold_args(fold)
     if _hip(a):
-        return _ops().qkv_fwd(a, w, b, B, N, H)
-    return ref.qkv_fwd(a, w, b, B, N, H)
+        return _ops().qkv_fwd(a, w, b, B, N, H, st, c, eps, mean, rstd)
+    return ref.qkv_fwd(a, w, b, B, N, H, st, c, eps, mean, rstd)
 
 
 def attn_fwd(qkv, scale: float, rng, site: int, p: float):
@@ -69,10 +88,14 @@ def attn_fwd(qkv, scale: float, rng, site: int, p: float):
     return ref.attn_fwd(qkv, scale, rng, site, p)
 
 
-def linear_residual_fwd(a, w, b, x, N: int, rng, site_drop: int, p_drop: float, site_dp: int, p_dp: float):
+def linear_residual_fwd(a, w, b, x, N: int, rng, site_drop: int, p_drop: float, site_dp: int, p_dp: float,
+                        st_out=None, xb_out=None):
+    """x + DropPath(Dropout(a w^T + b)).  LayerNorm fold producer: ``st_out`` ([M, D/32, 2])
+    gets the new rows' {sum, sum^2} per 32-column slot, ``xb_out`` their bf16 copy."""
     if _hip(a):
-        return _ops().linear_residual_fwd(a, w, b, x, N, rng, site_drop, float(p_drop), site_dp, float(p_dp))
-    return ref.linear_residual_fwd(a, w, b, x, N, rng, site_drop, p_drop, site_dp, p_dp)
+        return _ops().linear_residual_fwd(a, w, b, x, N, rng, site_drop, float(p_drop), site_dp, float(p_dp),
+                                          st_out, xb_out)
+    return ref.linear_residual_fwd(a, w, b, x, N, rng, site_drop, p_drop, site_dp, p_dp, st_out, xb_out)
 
 
 def residual_ln_fusable(D: int, K: int) -> bool:
@@ -90,20 +113,22 @@ def linear_residual_ln_fwd(a, w, b, x, gamma, beta, eps: float, N: int, rng, sit
     return ref.linear_residual_ln_fwd(a, w, b, x, gamma, beta, eps, N, rng, site_drop, p_drop, site_dp, p_dp)
 
 
-def linear_gelu_fwd(a, w, b, rng, site: int, p: float):
+def linear_gelu_fwd(a, w, b, rng, site: int, p: float, fold=None):
+    st, c, eps, mean, rstd = _fold_args(fold)
     if _hip(a):
-        return _ops().linear_gelu_fwd(a, w, b, rng, site, float(p))
-    return ref.linear_gelu_fwd(a, w, b, rng, site, p)
+        return _ops().linear_gelu_fwd(a, w, b, rng, site, float(p), st, c, eps, mean, rstd)
+    return ref.linear_gelu_fwd(a, w, b, rng, site, p, st, c, eps, mean, rstd)
 
 
-def head_step_(a, w, b, x, x0_out, coef, patch: int, mode: int):
+def head_step_(a, w, b, x, x0_out, coef, patch: int, mode: int, fold=None):
     """Head GEMM + sampler step in its epilogue (in place on ``x``): mode 1 = clamp +
     DDIM update (``x0_out`` gets the clamped x0-hat; ``coef`` a device row of
     ``ddim_coefficients``), mode 2 = clamp only (cold sampler)."""
+    st, c, eps, _, _ = _fold_args(fold)
     if _hip(a):
-        return _ops().head_step_(a, w, b, x, x0_out, coef, patch, mode)
+        return _ops().head_step_(a, w, b, x, x0_out, coef, patch, mode, st, c, eps)
     B, C, H, W = x.shape
-    x0_raw = ref.head_fwd(a, w, b, B, C, H, W, patch)
+    x0_raw = ref.head_fwd(a, w, b, B, C, H, W, patch, st, c, eps)
     if mode == 2:
         x.copy_(torch.clamp(x0_raw, -1.0, 1.0))
         return
@@ -112,10 +137,11 @@ def head_step_(a, w, b, x, x0_out, coef, patch: int, mode: int):
     x0_out.copy_(x0)
 
 
-def head_fwd(a, w, b, B: int, C: int, H: int, W: int, patch: int):
+def head_fwd(a, w, b, B: int, C: int, H: int, W: int, patch: int, fold=None):
+    st, c, eps, mean, rstd = _fold_args(fold)
     if _hip(a):
-        return _ops().head_fwd(a, w, b, B, C, H, W, patch)
-    return ref.head_fwd(a, w, b, B, C, H, W, patch)
+        return _ops().head_fwd(a, w, b, B, C, H, W, patch, st, c, eps, mean, rstd)
+    return ref.head_fwd(a, w, b, B, C, H, W, patch, st, c, eps, mean, rstd)
 
 
 def smooth_l1_fwd_bwd(pred, target, N: int, patch: int, beta: float = 1.0, loss_last=None, loss_ema=None,
@@ -207,21 +233,35 @@ LN_REPLICAS = 16  # csrc/layernorm.hip LN_REPLICAS
 
 
 def layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dgamma, dbeta, N: int, rng, site_drop: int, p_drop: float,
-                  site_dp: int, p_dp: float, emit_gy: bool, ws: Optional[torch.Tensor] = None):
+                  site_dp: int, p_dp: float, emit_gy: bool, ws: Optional[torch.Tensor] = None, beta=None,
+                  y_out=None):
     """LayerNorm backward.  With ``ws`` ([LN_REPLICAS, 2D], zero on entry) the
     dgamma||dbeta partials stay in the replica workspace (finalise later with
-    :func:`replica_reduce_`); otherwise they are added into dgamma / dbeta."""
+    :func:`replica_reduce_`); otherwise they are added into dgamma / dbeta.
+    ``y_out`` (with ``beta``): also write the LayerNorm output (bf16) — the
+    forward folded the LayerNorm into the next GEMM and never stored it."""
     if _hip(x):
         g_out, gy = _ops().layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dgamma, dbeta, N, rng, site_drop,
-                                         float(p_drop), site_dp, float(p_dp), bool(emit_gy), ws)
+                                         float(p_drop), site_dp, float(p_dp), bool(emit_gy), ws, beta, y_out)
         return g_out, (gy if emit_gy else None)
     if ws is not None:
         D = x.shape[-1]
-        dg, db = ws[0, :D], ws[0, D:]
-        return ref.layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dg, db, N, rng, site_drop, p_drop,
-                                 site_dp, p_dp, emit_gy)
+        dgamma, dbeta = ws[0, :D], ws[0, D:]
+    if y_out is not None:
+        ref.layernorm_out_(x, mean, rstd, gamma, beta, y_out)
     return ref.layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dgamma, dbeta, N, rng, site_drop, p_drop,
                              site_dp, p_dp, emit_gy)
+
+
+def ln_fold_(ws, gammas, betas, biases, wfs, cs, bfs):
+    """LayerNorm fold weights for GEMMs that consume a LayerNorm (one launch on GPU):
+    ``wf = bf16(gamma o W)``, ``c = rowsum(wf)``, ``bf = b + W beta``."""
+    if not ws:
+        return
+    if _hip(ws[0]):
+        return _ops().ln_fold_(list(ws), list(gammas), list(betas), list(biases), list(wfs), list(cs), list(bfs))
+    for w, g, be, b, wf, c, bf in zip(ws, gammas, betas, biases, wfs, cs, bfs):
+        ref.ln_fold(w, g, be, b, wf, c, bf)
 
 
 def replica_reduce_(ws, dst_ptrs, C: int, dsts=None):

@@ -116,8 +116,26 @@ def patchify_bf16(img: torch.Tensor, patch: int) -> torch.Tensor:
     return bf16(t.reshape(B * Hp * Wp, C * patch * patch))
 
 
-def patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site: int, p: float, patch: int):
-    """tokens x[B,N,D] fp32 = pos_drop(cat(cls, conv(img)) + pos + temb[t]); also the bf16 patches."""
+LN_SLOT = 32  # csrc/gemm.hip: row statistics per 32-column slot
+
+
+def row_stats(x: torch.Tensor) -> torch.Tensor:
+    """LayerNorm-fold row statistics [M, D/32, 2]: {sum, sum^2} of each row's 32-column slots."""
+    D = x.shape[-1]
+    xf = x.reshape(-1, D // LN_SLOT, LN_SLOT).float()
+    return torch.stack((xf.sum(-1), (xf * xf).sum(-1)), dim=-1)
+
+
+def _row_stats_add_(st: torch.Tensor, x: torch.Tensor):
+    """Write the LayerNorm-fold producer statistics of ``x`` into ``st`` ([M, D/32, 2])."""
+    st.copy_(row_stats(x).view(st.shape))
+
+
+def patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site: int, p: float, patch: int, ln_st=None,
+                    xb_out=None):
+    """tokens x[B,N,D] fp32 = pos_drop(cat(cls, conv(img)) + pos + temb[t]); also the bf16 patches.
+    LayerNorm fold: ``ln_st`` [B*N, D/32, 2] = the tokens' row statistics
+    (:func:`row_stats`); ``xb_out`` = the tokens in bf16."""
     B = img.shape[0]
     D = w_pe.shape[0]
     patches = patchify_bf16(img, patch)
@@ -125,7 +143,11 @@ def patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site: int, p: float
     proj = proj.view(B, -1, D)
     tok = torch.cat((cls.float().reshape(1, 1, D).expand(B, 1, D), proj), dim=1)
     tok = tok + pos.float().reshape(1, -1, D) + temb.float()[t].unsqueeze(1)
-    return _dropout(tok, rng, site, p).contiguous(), patches
+    tok = _dropout(tok, rng, site, p).contiguous()
+    if ln_st is not None:
+        _row_stats_add_(ln_st, tok)
+        xb_out.copy_(bf16(tok).view(xb_out.shape))
+    return tok, patches
 
 
 def layernorm_fwd(x, gamma, beta, eps: float = 1e-5):
@@ -137,18 +159,41 @@ def layernorm_fwd(x, gamma, beta, eps: float = 1e-5):
     return bf16(y), mean, rstd
 
 
-def linear_fwd(a, w, b, out_fp32: bool):
-    y = _mm(a.reshape(-1, a.shape[-1]), w)
+def ln_row_stats(st: torch.Tensor, K: int, eps: float):
+    """(mean, rstd) of rows from their per-slot {sum, sum^2} ([M, K/32, 2]; LayerNorm fold)."""
+    tot = st.reshape(st.shape[0], -1, 2).sum(1)
+    mu = tot[:, 0] / K
+    var = torch.clamp(tot[:, 1] / K - mu * mu, min=0.0)
+    return mu, torch.rsqrt(var + eps)
+
+
+def _lin(a, w, b, st=None, c=None, eps: float = 1e-5, mean_out=None, rstd_out=None):
+    """fp32 ``a @ w.T + b``; with the LayerNorm fold (``st`` = row {sum, sum^2} of the
+    raw rows ``a``, ``w``/``b``/``c`` from :func:`ln_fold`):
+    ``rstd * (a @ w.T - mean * c) + b`` = LayerNorm(a) @ W.T + bias."""
+    a2 = a.reshape(-1, a.shape[-1])
+    y = _mm(a2, w)
+    if st is not None:
+        mu, rs = ln_row_stats(st.reshape(a2.shape[0], -1, 2), a2.shape[1], eps)
+        y = (y - mu.unsqueeze(1) * c.float().unsqueeze(0)) * rs.unsqueeze(1)
+        if mean_out is not None:
+            mean_out.copy_(mu.view(mean_out.shape))
+            rstd_out.copy_(rs.view(rstd_out.shape))
     if b is not None:
         y = y + b.float()
+    return y
+
+
+def linear_fwd(a, w, b, out_fp32: bool, st=None, c=None, eps: float = 1e-5):
+    y = _lin(a, w, b, st, c, eps)
     return y if out_fp32 else bf16(y)
 
 
-def qkv_fwd(a, w, b, B: int, N: int, H: int):
+def qkv_fwd(a, w, b, B: int, N: int, H: int, st=None, c=None, eps: float = 1e-5, mean_out=None, rstd_out=None):
     """QKV projection written head-major: [3, B, H, N, hd] bf16."""
     D3 = w.shape[0]
     D = D3 // 3
-    y = bf16(_mm(a, w) + b.float())
+    y = bf16(_lin(a, w, b, st, c, eps, mean_out, rstd_out))
     return y.view(B, N, 3, H, D // H).permute(2, 0, 3, 1, 4).contiguous()
 
 
@@ -166,14 +211,19 @@ def attn_fwd(qkv, scale: float, rng, site: int, p: float):
 
 
 def linear_residual_fwd(a, w, b, x, N: int, rng, site_drop: int, p_drop: float,
-                        site_dp: int, p_dp: float):
-    """x_new = x + DropPath(Dropout(a @ w.T + b)) (fp32 residual stream)."""
+                        site_dp: int, p_dp: float, st_out=None, xb_out=None):
+    """x_new = x + DropPath(Dropout(a @ w.T + b)) (fp32 residual stream); LayerNorm-fold
+    producer: st_out = row statistics of x_new (:func:`row_stats`), xb_out = bf16(x_new)."""
     M, Dout = x.shape[0] * (x.shape[1] if x.dim() == 3 else 1), w.shape[0]
     y = _mm(a.reshape(-1, a.shape[-1]), w) + b.float()
     y = _dropout(y, rng, site_drop, p_drop)
     B = M // N
     sc = _sample_scale(B, rng, site_dp, p_dp, x.device).repeat_interleave(N)
-    return (x.reshape(M, Dout).float() + y * sc.unsqueeze(1)).view(x.shape)
+    out = (x.reshape(M, Dout).float() + y * sc.unsqueeze(1)).view(x.shape)
+    if st_out is not None:
+        _row_stats_add_(st_out, out)
+        xb_out.copy_(bf16(out).view(xb_out.shape))
+    return out
 
 
 def linear_residual_ln_fwd(a, w, b, x, gamma, beta, eps: float, N: int, rng, site_drop: int, p_drop: float,
@@ -184,18 +234,20 @@ def linear_residual_ln_fwd(a, w, b, x, gamma, beta, eps: float, N: int, rng, sit
     return xn, ln, mean, rstd
 
 
-def linear_gelu_fwd(a, w, b, rng, site: int, p: float):
+def linear_gelu_fwd(a, w, b, rng, site: int, p: float, st=None, c=None, eps: float = 1e-5, mean_out=None,
+                    rstd_out=None):
     """u = a @ w.T + b (bf16, saved); h = Dropout(GELU(u)) (bf16)."""
-    u = _mm(a, w) + b.float()
+    u = _lin(a, w, b, st, c, eps, mean_out, rstd_out)
     u16 = bf16(u)
     h = _dropout(gelu(u), rng, site, p)
     return u16, bf16(h)
 
 
-def head_fwd(a, w, b, B: int, C: int, H: int, W: int, patch: int):
+def head_fwd(a, w, b, B: int, C: int, H: int, W: int, patch: int, st=None, c=None, eps: float = 1e-5,
+             mean_out=None, rstd_out=None):
     """Head linear on patch tokens, unpatchified straight to [B,C,H,W] fp32."""
     N = a.shape[0] // B
-    y = (_mm(a, w) + b.float()).view(B, N, -1)[:, 1:, :]
+    y = _lin(a, w, b, st, c, eps, mean_out, rstd_out).view(B, N, -1)[:, 1:, :]
     Hp, Wp = H // patch, W // patch
     img = y.reshape(B, Hp, Wp, patch, patch, C).permute(0, 5, 1, 3, 2, 4)
     return img.reshape(B, C, H, W).contiguous()
@@ -247,6 +299,26 @@ def linear_wgrad(dy, x, dw, db: Optional[torch.Tensor]):
     dw.add_((dy.float().t() @ x.float()).view_as(dw))
     if db is not None:
         db.add_(dy.float().sum(0))
+
+
+def layernorm_out_(x, mean, rstd, gamma, beta, y_out):
+    """y_out = bf16((x - mean) * rstd * gamma + beta) (LayerNorm output from saved statistics)."""
+    D = x.shape[-1]
+    xf = x.reshape(-1, D).float()
+    y = (xf - mean.reshape(-1, 1)) * rstd.reshape(-1, 1) * gamma.float() + beta.float()
+    y_out.copy_(bf16(y).view(y_out.shape))
+
+
+def ln_fold(w, gamma, beta, bias, wf, c, bf):
+    """LayerNorm fold weights: wf = bf16(gamma o W); c = rowsum(wf) (of the bf16
+    values); bf = bias + W beta."""
+    wq = bf16(w.float() * gamma.float().unsqueeze(0))
+    wf.copy_(wq.view(wf.shape))
+    c.copy_(wq.float().sum(1).view(c.shape))
+    bb = w.float() @ beta.float()
+    if bias is not None:
+        bb = bb + bias.float()
+    bf.copy_(bb.view(bf.shape))
 
 
 def layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dgamma, dbeta, N: int, rng,

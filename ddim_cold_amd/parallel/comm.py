@@ -1,0 +1,70 @@
+"""Native RCCL communicator (``csrc/comm.cpp``) for the gradient reducer.
+
+The reference's only hot collective is DDP's bucketed gradient all-reduce
+(``multi_gpu_trainer.py:88``, ``:128``) plus the initial parameter broadcast
+of the DDP constructor.  ``NativeComm`` is the MI355X-side owner of that
+traffic: one ``ncclComm_t`` per process, bootstrapped through the
+``torch.distributed`` TCPStore (rank 0 publishes the 128-byte
+``ncclUniqueId``), whose collectives go straight onto the caller's current
+HIP stream — the train engine's communication stream — so they are captured
+into the step hipGraph as plain graph nodes.  ``torch.distributed`` (backend
+``nccl`` = RCCL) stays the control plane: rendezvous, barriers, metric
+reductions.
+"""
+from __future__ import annotations
+
+import itertools
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _ext
+
+_SEQ = itertools.count()
+
+SUM, MAX, MIN = 0, 1, 2
+
+
+def _store():
+    return dist.distributed_c10d._get_default_store()
+
+
+class NativeComm:
+    """One RCCL communicator over the ranks of the default process group."""
+
+    def __init__(self, device: torch.device, key: Optional[str] = None):
+        if not dist.is_initialized():
+            raise RuntimeError("NativeComm needs an initialised torch.distributed process group (rendezvous)")
+        _ext.load(raise_on_error=True)
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("NativeComm is GPU-only (RCCL); use torch.distributed on CPU")
+        self.world = dist.get_world_size()
+        self.rank = dist.get_rank()
+        store = _store()
+        key = key or f"ddim_cold/native_comm/{next(_SEQ)}"
+        if self.rank == 0:
+            uid = torch.ops.ddim_cold.comm_unique_id()
+            store.set(key, bytes(uid.tolist()))
+        raw = store.get(key)  # blocks until rank 0 has published the id
+        uid = torch.tensor(list(raw), dtype=torch.uint8)
+        idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self.handle = int(torch.ops.ddim_cold.comm_init(uid, self.world, self.rank, idx))
+        n, r = torch.ops.ddim_cold.comm_info(self.handle)
+        assert (n, r) == (self.world, self.rank), (n, r, self.world, self.rank)
+
+    def all_reduce_(self, buf: torch.Tensor, op: int = SUM):
+        torch.ops.ddim_cold.comm_all_reduce_(buf, self.handle, op)
+
+    def all_reduce_bf16_wire_(self, buf: torch.Tensor, scratch: torch.Tensor):
+        """SUM all-reduce of an fp32 range over a bf16 wire (pack, reduce, unpack)."""
+        torch.ops.ddim_cold.comm_all_reduce_bf16_wire_(buf, scratch, self.handle)
+
+    def broadcast_(self, buf: torch.Tensor, root: int = 0):
+        torch.ops.ddim_cold.comm_broadcast_(buf, self.handle, root)
+
+    def destroy(self):
+        if self.handle is not None:
+            torch.ops.ddim_cold.comm_destroy(self.handle)
+            self.handle = None

@@ -40,7 +40,8 @@ import torch
 import torch.distributed as dist
 
 from .. import ops
-from ..models.program import ModelTensors, ViTProgram, collect, is_matrix_param
+from ..models import program as _program
+from ..models.program import LnFold, ModelTensors, ViTProgram, collect, is_matrix_param
 
 ALIGN = 64  # elements (256 B fp32)
 
@@ -86,6 +87,12 @@ class EngineConfig:
     # gradient all-reduce wire format: "fp32" (reference DDP semantics) or "bf16"
     # (halves the xGMI bytes; the sum is accumulated in bf16 by RCCL)
     grad_wire: str = "fp32"
+    # who issues the gradient collectives: "torch" (torch.distributed 'nccl' =
+    # RCCL through ProcessGroupNCCL) or "native" (csrc/comm.cpp: our own
+    # ncclComm_t, collectives enqueued directly on the comm stream, bf16 wire
+    # pack/unpack as two fused kernels).  torch.distributed stays the control
+    # plane (rendezvous, barriers, metrics) either way.
+    comm: str = "torch"
 
 
 def _align(n: int) -> int:
@@ -117,6 +124,14 @@ class TrainEngine:
         self.loss_ema = torch.full((1,), cfg.ema_init, dtype=torch.float32, device=dev)
         self.side = torch.cuda.Stream(device=dev) if (self.is_cuda and cfg.wgrad_stream) else None
         self.comm = torch.cuda.Stream(device=dev) if (self.is_cuda and self.segmented) else None
+        if cfg.comm not in ("torch", "native"):
+            raise ValueError(f"comm must be 'torch' or 'native', got {cfg.comm!r}")
+        self.ncomm = None
+        if cfg.comm == "native" and self.dist_on and self.is_cuda:
+            if process_group is not None and process_group is not dist.group.WORLD:
+                raise ValueError("comm='native' spans the default process group only")
+            from ..parallel.comm import NativeComm
+            self.ncomm = NativeComm(dev)
         self._graphs: Optional[List[torch.cuda.CUDAGraph]] = None
         self._eager_steps = 0
         self.batch_fn: Optional[Callable] = None
@@ -124,7 +139,10 @@ class TrainEngine:
         self._static = None
         self.steps_done = 0
         if self.world > 1:
-            dist.broadcast(self.flat_p, src=0, group=self.pg)
+            if self.ncomm is not None:
+                self.ncomm.broadcast_(self.flat_p, 0)
+            else:
+                dist.broadcast(self.flat_p, src=0, group=self.pg)
             self._refresh_shadow()
         model._engine = self
 
@@ -164,12 +182,18 @@ class TrainEngine:
             vg = self.flat_g[o:o + k].view_as(p)
             p.grad = vg
             views_g[n] = vg
+        c = self.prog.cfg
+        # LayerNorm fold: gamma-scaled bf16 weights / row sums / folded biases of
+        # the QKV, fc1 and head GEMMs, recomputed from the fp32 masters after
+        # every optimizer step (inside the step graph)
+        self.lnfold = LnFold({n: p.data for n, p in named}, c.depth) if _program.FOLD_LN else None
         self._refresh_shadow()
         for n, p in named:
             o, k = self.offsets[n]
             views_p[n] = self.flat_pb[o:o + k].view(p.shape) if is_matrix_param(n) else p.data
-        c = self.prog.cfg
         self.param_tensors: ModelTensors = collect(views_p, c.depth, c.dim)
+        if self.lnfold is not None:
+            self.lnfold.attach(self.param_tensors)
         self.grad_tensors: ModelTensors = collect(views_g, c.depth, c.dim)
         if not c.learn_temb:
             self.grad_tensors.temb = None
@@ -231,6 +255,8 @@ class TrainEngine:
 
     def _refresh_shadow(self):
         self.flat_pb.copy_(self.flat_p.to(torch.bfloat16))
+        if getattr(self, "lnfold", None) is not None:
+            self.lnfold.refresh()
 
     # ------------------------------------------------------------------ step program
     def set_batch_fn(self, fn: Callable):
@@ -276,6 +302,8 @@ class TrainEngine:
         ops.sqnorm(self.flat_g, self.sqnorm, gs)
         ops.adamw_step(self.flat_p, self.flat_g, self.flat_m, self.flat_v, self.flat_pb, self.sqnorm,
                        self.step_ctr, self.hyper, gs)
+        if self.lnfold is not None:
+            self.lnfold.refresh()
         ops.advance_counters(self.step_ctr, self.rng, self.sqnorm)
         self.prog._keep = None
         yield ("done", -1)
@@ -287,7 +315,12 @@ class TrainEngine:
 
         def reduce():
             for a, b in ranges:
-                if self.flat_gw is None:
+                if self.ncomm is not None:
+                    if self.flat_gw is None:
+                        self.ncomm.all_reduce_(self.flat_g[a:b])
+                    else:
+                        self.ncomm.all_reduce_bf16_wire_(self.flat_g[a:b], self.flat_gw[a:b])
+                elif self.flat_gw is None:
                     dist.all_reduce(self.flat_g[a:b], group=self.pg)
                 else:  # bf16 wire: cast, reduce, cast back (on the comm stream)
                     w = self.flat_gw[a:b]

@@ -40,6 +40,11 @@ def _grads(model, x, y, t, rng):
              for n, p in model.named_parameters()}
     grads = {n: torch.zeros_like(p) for n, p in model.named_parameters()}
     P = collect(views, c.depth, c.dim)
+    from ddim_cold_amd.models import program as pr
+    if pr.FOLD_LN:  # the engine folds every LayerNorm into its consumer GEMM
+        fold = pr.LnFold({n: p.detach() for n, p in model.named_parameters()}, c.depth)
+        fold.refresh()
+        fold.attach(P)
     G = collect(grads, c.depth, c.dim)
     out, S = prog.forward(P, x, t, rng, True)
     loss, dtok = ref.smooth_l1_fwd_bwd(out, y, c.tokens, c.patch)

@@ -116,7 +116,9 @@ def test_positional_encoding():
 @pytest.fixture
 def fp32_reference(monkeypatch):
     """Run the reference ops without bf16 rounding: isolates the program's logic."""
+    from ddim_cold_amd.models import program
     monkeypatch.setattr(ref, "bf16", lambda x: x.float() if x.dtype == torch.bfloat16 else x)
+    monkeypatch.setattr(program, "ACT_DTYPE", torch.float32)
 
 
 @pytest.mark.parametrize("cfg", [dict(img_size=[32, 32], patch_size=8, embed_dim=128, depth=3, num_heads=4),
@@ -160,3 +162,66 @@ def test_program_eval_matches_plain_model(fp32_reference):
         a = m.forward_reference(x, t)
         b, _ = prog.forward(P, x, t, torch.tensor([0, 0]), False, save=False)
     assert (a - b).abs().max() < 1e-5
+
+
+def _folded(m, named):
+    from ddim_cold_amd.models.program import LnFold
+    c = ViTProgram.from_model(m).cfg
+    P = collect(dict(named), c.depth, c.dim)
+    fold = LnFold(dict(named), c.depth)
+    fold.refresh()
+    return fold.attach(P)
+
+
+@pytest.mark.parametrize("cfg", [dict(img_size=[32, 32], patch_size=8, embed_dim=128, depth=3, num_heads=4),
+                                 dict(img_size=[16, 16], patch_size=4, embed_dim=64, depth=2, num_heads=2)])
+def test_program_layernorm_fold_matches_autograd(fp32_reference, cfg):
+    """LayerNorm fold (forward without LayerNorm launches: statistics from the producing
+    epilogue, gamma/beta folded into the consumer GEMM, LayerNorm outputs re-emitted
+    by the backward) == autograd of the unfolded forward, all dropout sites active."""
+    torch.manual_seed(0)
+    m = DiffusionVisionTransformer(drop_rate=0.1, attn_drop_rate=0.1, drop_path_rate=0.2, **cfg).train()
+    with torch.no_grad():  # non-trivial LayerNorm affine parameters
+        for n, p in m.named_parameters():
+            if "norm" in n:
+                p.add_(0.3 * torch.randn_like(p))
+    prog = ViTProgram.from_model(m)
+    named = {n: p.detach().clone().requires_grad_(True) for n, p in m.named_parameters()}
+    P = collect(named, prog.cfg.depth, prog.cfg.dim)
+    B, H = 3, cfg["img_size"][0]
+    img = torch.randn(B, 3, H, H)
+    tgt = torch.randn(B, 3, H, H).clamp(-1, 1)
+    t = torch.randint(0, 2000, (B,))
+    rng = torch.tensor([12345, 7])
+    out, _ = prog.forward(P, img, t, rng, True)
+    loss, dtok = ref.smooth_l1_fwd_bwd(out, tgt, prog.cfg.tokens, prog.cfg.patch)
+    loss.backward()
+    Pf = _folded(m, {n: p.detach() for n, p in named.items()})
+    assert Pf.folded
+    out2, S = prog.forward(Pf, img, t, rng, True)
+    assert (out2 - out.detach()).abs().max() < 1e-4
+    assert S.lf is None and all(b[1] is None and b[8] is None for b in S.blocks)
+    grads = {n: torch.zeros_like(p) for n, p in named.items()}
+    G = collect(grads, prog.cfg.depth, prog.cfg.dim)
+    prog.backward(Pf, G, S, dtok, rng, True)
+    for n, p in named.items():
+        a, b = p.grad, grads[n]
+        rel = (a - b).abs().max().item() / (a.abs().max().item() + 1e-12)
+        assert rel < 1e-3, (n, rel)
+
+
+def test_layernorm_fold_reference_identity():
+    """rstd*(x (gamma o W)^T - mean*c) + (b + W beta) == LayerNorm(x) W^T + b."""
+    torch.manual_seed(0)
+    x = torch.randn(37, 64) * 3 + 0.5
+    w, b = torch.randn(48, 64), torch.randn(48)
+    g, be = torch.randn(64), torch.randn(64)
+    wf, c, bf = torch.empty(48, 64), torch.empty(48), torch.empty(48)
+    ref.ln_fold(w, g, be, b, wf, c, bf)
+    st = ref.row_stats(x)
+    mean, rstd = torch.empty(37), torch.empty(37)
+    y = ref._lin(x, wf, bf, st, c, 1e-5, mean, rstd)
+    expect = torch.nn.functional.layer_norm(x, (64,), g, be, 1e-5) @ w.t() + b
+    # the fold multiplies bf16-rounded (gamma o W); compare against that rounding
+    assert (y - expect).abs().max() < 0.05 * expect.abs().max()
+    torch.testing.assert_close(mean, x.mean(-1), rtol=1e-5, atol=1e-5)
