@@ -724,6 +724,51 @@ void ln_fold_(std::vector<Tensor> ws, std::vector<Tensor> gammas, std::vector<Te
   tb.start[n] = rows;
   ln_fold_launch(tb, cur_stream());
 }
+
+// Fused QKV projection + short attention (one workgroup per head): returns
+// (o [B,N,D] bf16, lse [B,H,N] fp32, qkv [3,B,H,N,hd] bf16 or empty).  With
+// ln_st / ln_c the preceding LayerNorm is folded in (a = raw rows, w/b folded).
+std::tuple<Tensor, Tensor, Tensor> qkv_attn_fwd(Tensor a, Tensor w, Tensor b, c10::optional<Tensor> ln_st,
+                                                c10::optional<Tensor> ln_c, double ln_eps, int64_t B, int64_t N,
+                                                int64_t H, double scale, Tensor rng, int64_t site, double p,
+                                                bool save_qkv, c10::optional<Tensor> ln_mean,
+                                                c10::optional<Tensor> ln_rstd) {
+  CHECK_IN(a, BF16); CHECK_IN(w, BF16); CHECK_IN(b, F32); check_rng(rng);
+  const c10::DeviceGuard guard(a.device());
+  const int D = a.size(-1);
+  TORCH_CHECK(a.numel() == B * N * D && w.size(0) == 3 * D && w.size(1) == D && b.numel() == 3 * D && D % H == 0,
+              "qkv_attn_fwd shapes");
+  const int hd = D / H;
+  TORCH_CHECK(qkv_attn_supported(N, hd, D), "qkv_attn_fwd: needs hd 32, 64 < N <= 128, D in {256,384,512}");
+  QkvArgs q;
+  q.x = a.data_ptr(); q.w = w.data_ptr(); q.bias = b.data_ptr<float>();
+  if (ln_st.has_value() && ln_st->defined()) {
+    CHECK_IN((*ln_st), F32);
+    TORCH_CHECK(ln_c.has_value() && ln_c->defined(), "LayerNorm fold needs ln_c");
+    CHECK_IN((*ln_c), F32);
+    TORCH_CHECK(ln_st->numel() == 2 * B * N * (D / 32) && ln_c->numel() == 3 * D, "LayerNorm fold shapes");
+    q.st = ln_st->data_ptr<float>();
+    q.c = ln_c->data_ptr<float>();
+    if (ln_mean.has_value() && ln_mean->defined()) {
+      CHECK_IN((*ln_mean), F32); CHECK_IN((*ln_rstd), F32);
+      TORCH_CHECK(ln_mean->numel() == B * N && ln_rstd->numel() == B * N, "ln_mean / ln_rstd shapes");
+      q.mean = ln_mean->data_ptr<float>();
+      q.rstd = ln_rstd->data_ptr<float>();
+    }
+  }
+  q.eps = (float)ln_eps;
+  auto o = at::empty({B, N, D}, a.options());
+  auto lse = at::empty({B, H, N}, a.options().dtype(F32));
+  Tensor qkv = save_qkv ? at::empty({3, B, H, N, hd}, a.options()) : at::empty({0}, a.options());
+  q.qkv = save_qkv ? qkv.data_ptr() : nullptr;
+  q.out = o.data_ptr(); q.lse = lse.data_ptr<float>();
+  q.B = B; q.H = H; q.N = N; q.hd = hd; q.D = D; q.scale = (float)scale;
+  q.rng = rng.data_ptr<int64_t>(); q.site = site; q.p = p;
+  qkv_attn_fwd_launch(q, cur_stream());
+  return {o, lse, qkv};
+}
+
+bool qkv_attn_ok(int64_t N, int64_t hd, int64_t D) { return qkv_attn_supported(N, hd, D); }
 }  // namespace
 
 TORCH_LIBRARY(ddim_cold, m) {
@@ -733,6 +778,10 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("qkv_fwd(Tensor a, Tensor w, Tensor b, int B, int N, int H, Tensor? ln_st=None, Tensor? ln_c=None, "
         "float ln_eps=1e-5, Tensor(a!)? ln_mean=None, Tensor(b!)? ln_rstd=None) -> Tensor");
   m.def("attn_fwd(Tensor qkv, float scale, Tensor rng, int site, float p) -> (Tensor, Tensor)");
+  m.def("qkv_attn_fwd(Tensor a, Tensor w, Tensor b, Tensor? ln_st, Tensor? ln_c, float ln_eps, int B, int N, int H, "
+        "float scale, Tensor rng, int site, float p, bool save_qkv, Tensor(a!)? ln_mean=None, "
+        "Tensor(b!)? ln_rstd=None) -> (Tensor, Tensor, Tensor)");
+  m.def("qkv_attn_ok(int N, int hd, int D) -> bool", &qkv_attn_ok);
   m.def("linear_residual_fwd(Tensor a, Tensor w, Tensor b, Tensor x, int N, Tensor rng, int site_drop, "
         "float p_drop, int site_dp, float p_dp, Tensor(a!)? st_out=None, Tensor(b!)? xb_out=None) -> Tensor");
   m.def("linear_gelu_fwd(Tensor a, Tensor w, Tensor b, Tensor rng, int site, float p, Tensor? ln_st=None, "
@@ -779,6 +828,7 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("layernorm_fwd", &layernorm_fwd);
   m.impl("qkv_fwd", &qkv_fwd);
   m.impl("attn_fwd", &attn_fwd);
+  m.impl("qkv_attn_fwd", &qkv_attn_fwd);
   m.impl("linear_residual_fwd", &linear_residual_fwd);
   m.impl("linear_gelu_fwd", &linear_gelu_fwd);
   m.impl("head_fwd", &head_fwd);

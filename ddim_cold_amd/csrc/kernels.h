@@ -170,3 +170,25 @@ void cold_batch_launch(const float* pool, int pool_n, const int64_t* rng, int si
 // gradient wire format (comm_wire.hip): fp32 <-> bf16 (RNE), 16-B aligned buffers
 void wire_pack_launch(const float* src, void* dst, int64_t n, hipStream_t stream);
 void wire_unpack_launch(const void* src, float* dst, int64_t n, hipStream_t stream);
+
+// fused QKV projection + short-sequence attention (attention.hip), hd 32, 64 < N <= 128
+struct QkvArgs {
+  const void* x = nullptr;      // [B*N][D] bf16
+  const void* w = nullptr;      // [3D][D] bf16
+  const float* bias = nullptr;  // [3D]
+  const float* c = nullptr;     // [3D] (LayerNorm fold) or null
+  const float* st = nullptr;    // [B*N][D/32][2] (LayerNorm fold) or null
+  float eps = 1e-5f;
+  float* mean = nullptr;
+  float* rstd = nullptr;
+  void* qkv = nullptr;          // [3][B][H][N][hd] or null
+  void* out = nullptr;          // [B][N][D]
+  float* lse = nullptr;         // [B][H][N] or null
+  int B = 0, H = 0, N = 0, hd = 0, D = 0;
+  float scale = 1.f;
+  const int64_t* rng = nullptr;
+  int site = 0;
+  double p = 0.0;
+};
+bool qkv_attn_supported(int N, int hd, int D);
+void qkv_attn_fwd_launch(const QkvArgs& a, hipStream_t stream);

@@ -39,6 +39,12 @@ QKV_DGRAD_SPLITS = int(os.environ.get("DDIM_COLD_QKV_DGRAD_SPLITS", "2"))
 # producing GEMM's epilogue accumulates the row statistics; the LayerNorm
 # backward re-emits the normalised rows for the weight gradients.
 FOLD_LN = os.environ.get("DDIM_COLD_LN_FOLD", "1") == "1"
+# QKV projection + attention of a head in one kernel for 64 < N <= 128, hd 32
+# (csrc/attention.hip qkv_attn_fwd_kernel).  Measured on MI355X (ViT-tiny):
+# 19.4 us vs 12.3 + 6.4 us for QKV GEMM + attention at B=32 and 22.9 vs
+# 15.3 + 6.1 at the sampler's N=64 -- no better as a kernel, and the step /
+# sampler graphs get 1.5 % slower -> opt-in (DDIM_COLD_QKV_ATTN=1).
+FUSE_QKV_ATTN = os.environ.get("DDIM_COLD_QKV_ATTN", "0") == "1"
 # dtype of the bf16 activation copies / folded weights the program allocates
 # (tests on CPU switch it to fp32 to isolate the program logic from rounding)
 ACT_DTYPE = torch.bfloat16
@@ -336,12 +342,18 @@ class ViTProgram:
         def stats():
             return (torch.empty(M, dtype=torch.float32, device=dev),
                     torch.empty(M, dtype=torch.float32, device=dev)) if save else (None, None)
+        fused = FUSE_QKV_ATTN and ops.qkv_attn_supported(N, D // c.heads, D)
         for i, bp in enumerate(P.blocks):
             sa, sp, sd1, sf1, sf2, sd2 = block_sites(i)
             x0 = x
             m1, r1 = stats()
-            qkv = ops.qkv_fwd(xb, bp.qkv_wf, bp.qkv_bf, B, N, c.heads, fold=(st[2 * i], bp.qkv_c, c.eps, m1, r1))
-            o, lse = ops.attn_fwd(qkv, c.scale, rng, sa, ad)
+            fold = (st[2 * i], bp.qkv_c, c.eps, m1, r1)
+            if fused:
+                o, lse, qkv = ops.qkv_attn_fwd(xb, bp.qkv_wf, bp.qkv_bf, B, N, c.heads, c.scale, rng, sa, ad, save,
+                                               fold=fold)
+            else:
+                qkv = ops.qkv_fwd(xb, bp.qkv_wf, bp.qkv_bf, B, N, c.heads, fold=fold)
+                o, lse = ops.attn_fwd(qkv, c.scale, rng, sa, ad)
             o = o.view(M, D)
             x1b = torch.empty(M, D, dtype=ACT_DTYPE, device=dev)
             x1 = ops.linear_residual_fwd(o, bp.proj_w, bp.proj_b, x0, N, rng, sp, pd, sd1, dpr[i],

@@ -82,6 +82,26 @@ def qkv_fwd(a, w, b, B: int, N: int, H: int, fold=None):
     return ref.qkv_fwd(a, w, b, B, N, H, st, c, eps, mean, rstd)
 
 
+def qkv_attn_supported(N: int, hd: int, D: int) -> bool:
+    """Shapes the fused QKV + attention kernel covers (csrc/attention.hip)."""
+    return hd == 32 and 64 < N <= 128 and D in (256, 384, 512)
+
+
+def qkv_attn_fwd(a, w, b, B: int, N: int, H: int, scale: float, rng, site: int, p: float, save_qkv: bool,
+                 fold=None):
+    """Fused QKV projection + short attention, one workgroup per head:
+    ``(o [B,N,D], lse [B,H,N], qkv [3,B,H,N,hd] or None)``; ``fold = (ln_st, ln_c,
+    eps[, mean_out, rstd_out])`` folds the preceding LayerNorm in (see :func:`qkv_fwd`)."""
+    st, c, eps, mean, rstd = _fold_args(fold)
+    if _hip(a):
+        o, lse, qkv = _ops().qkv_attn_fwd(a, w, b, st, c, eps, B, N, H, float(scale), rng, site, float(p),
+                                          bool(save_qkv), mean, rstd)
+        return o, lse, (qkv if save_qkv else None)
+    qkv = ref.qkv_fwd(a, w, b, B, N, H, st, c, eps, mean, rstd)
+    o, lse = ref.attn_fwd(qkv, scale, rng, site, p)
+    return o, lse, (qkv if save_qkv else None)
+
+
 def attn_fwd(qkv, scale: float, rng, site: int, p: float):
     if _hip(qkv):
         return _ops().attn_fwd(qkv, float(scale), rng, site, float(p))

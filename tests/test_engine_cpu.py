@@ -128,7 +128,10 @@ def _ddp_worker(rank, world, port, out_path, wire="fp32"):
         model = _model(drop=False, seed=rank)  # different init per rank: engine must broadcast rank 0's
         eng = TrainEngine(model, EngineConfig(lr=1e-3, weight_decay=0.0, max_grad_norm=0.0, bucket_blocks=1,
                                               temb_rows=7, grad_wire=wire), device="cpu")
-        assert len(eng.bucket_ranges[-1]) == 2  # inactive time_embed rows skipped
+        # inactive time_embed rows skipped; the embeddings have their own last bucket
+        reduced = sum(b - a for rs in eng.bucket_ranges for a, b in rs)
+        assert reduced == eng.numel - (2000 - 7) * model.embed_dim
+        assert eng.bucket_ranges[-1][-1][1] <= eng.offsets["blocks.0.norm1.weight"][0]
         x, y, t = _batch(4, seed=5)
         t = t % 6 + 1  # cold-diffusion timesteps
         b = 4 // world
