@@ -364,8 +364,8 @@ Tensor linear_dgrad(Tensor dy, Tensor w, bool out_fp32, int64_t splits) {
   TORCH_CHECK(dy.dim() == 2 && w.dim() == 2 && dy.size(1) == w.size(0), "dgrad shapes");
   const int M = dy.size(0), Nout = w.size(0), K = w.size(1);
   TORCH_CHECK(Nout % 8 == 0 && K % 8 == 0, "dgrad dims must be multiples of 8");
-  TORCH_CHECK(splits >= 1 && (splits == 1 || out_fp32), "dgrad K split needs fp32 output");
-  auto dx = splits > 1 ? at::empty({splits, M, K}, dy.options().dtype(F32))
+  TORCH_CHECK(splits >= 1 && splits <= 4, "dgrad K split: 1..4");
+  auto dx = splits > 1 ? at::empty({splits, M, K}, dy.options().dtype(out_fp32 ? F32 : BF16))
                        : at::empty({M, K}, dy.options().dtype(out_fp32 ? F32 : BF16));
   GemmArgs g;
   g.A = dy.data_ptr(); g.B = w.data_ptr();
@@ -488,7 +488,9 @@ std::tuple<Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tenso
                                          c10::optional<Tensor> g_res, Tensor dgamma, Tensor dbeta, int64_t N,
                                          Tensor rng, int64_t site_drop, double p_drop, int64_t site_dp, double p_dp,
                                          bool emit_gy, c10::optional<Tensor> ws, c10::optional<Tensor> beta, c10::optional<Tensor> y_out) {
-  CHECK_IN(dy, F32); CHECK_IN(x, F32); CHECK_IN(mean, F32); CHECK_IN(rstd, F32); CHECK_IN(gamma, F32);
+  CHECK_CUDA(dy); CHECK_CONTIG(dy);
+  TORCH_CHECK(dy.scalar_type() == F32 || dy.scalar_type() == BF16, "dy must be fp32 or bf16");
+  CHECK_IN(x, F32); CHECK_IN(mean, F32); CHECK_IN(rstd, F32); CHECK_IN(gamma, F32);
   CHECK_IN(dgamma, F32); CHECK_IN(dbeta, F32); check_rng(rng);
   const c10::DeviceGuard guard(x.device());
   const int D = x.size(-1), M = x.numel() / D;
@@ -523,7 +525,7 @@ std::tuple<Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tenso
   }
   auto g_out = at::empty(x.sizes(), x.options());
   Tensor gy = emit_gy ? at::empty({M, D}, x.options().dtype(BF16)) : at::empty({0}, x.options().dtype(BF16));
-  layernorm_bwd_launch(dy.data_ptr<float>(), x.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+  layernorm_bwd_launch(dy.data_ptr(), dy.scalar_type() == BF16, x.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                        gamma.data_ptr<float>(), bp, gr, g_out.data_ptr<float>(), emit_gy ? gy.data_ptr() : nullptr,
                        yp, w.data_ptr<float>(), M, D, N, rng.data_ptr<int64_t>(), site_drop, p_drop, site_dp, p_dp,
                        parts, cur_stream());

@@ -254,7 +254,7 @@ template <int EPI>
 __device__ __forceinline__ float epilogue(const GemmParams& p, long long idx, int rb, float v, float pre,
                                           uint32_t salt_drop, uint32_t salt_dp, const f32x4& cf) {
   if (EPI == EPI_BF16) {
-    reinterpret_cast<bf16*>(p.C)[idx] = f2bf(v);
+    reinterpret_cast<bf16*>(p.C)[idx + blockIdx.z * p.split_stride] = f2bf(v);
   } else if (EPI == EPI_F32) {
     reinterpret_cast<float*>(p.C)[idx + blockIdx.z * p.split_stride] = v;
   } else if (EPI == EPI_ATOMIC) {
@@ -599,7 +599,9 @@ struct VecEpi {
         if (!colok[j]) continue;
         const long long idx = rows[i].off + cols[j];
         f32x4 v = fold ? (acc[i][j] - ms[i].x * lnc[j]) * ms[i].y + colb[j] : acc[i][j] + colb[j];
-        if (EPI == EPI_BF16 || EPI == EPI_QKV) {
+        if (EPI == EPI_BF16) {
+          st4bf(reinterpret_cast<bf16*>(p.C) + idx + blockIdx.z * p.split_stride, v);
+        } else if (EPI == EPI_QKV) {
           st4bf(reinterpret_cast<bf16*>(p.C) + idx, v);
         } else if (EPI == EPI_F32) {
           st4(reinterpret_cast<float*>(p.C) + idx + blockIdx.z * p.split_stride, v);
@@ -1354,13 +1356,17 @@ void gemm_dgrad(const GemmArgs& a, int epi, hipStream_t stream) {
   GemmParams p = base_params(a);
   check_vec(p, epi);
   switch (epi) {
-    case EPI_BF16: launch_auto<false, true, EPI_BF16>(p, 1, stream); break;
+    case EPI_BF16:
     case EPI_F32: {
+      // K split: slice z writes its partial product to C + z * split_stride
+      // (every slice non-empty; the consumer sums the slices)
       const int kt = (p.K + 63) / 64;
       const int splits = std::max(1, std::min(a.splits, kt));
+      if (splits != a.splits && a.splits > 1) throw std::runtime_error("gemm_dgrad: more K slices than k-tiles");
       if (splits > 1 && (p.bias || (kt + splits - 1) / splits * (splits - 1) >= kt))
         throw std::runtime_error("gemm_dgrad: K split needs no bias and a non-empty last slice");
-      launch_auto<false, true, EPI_F32>(p, splits, stream);
+      if (epi == EPI_BF16) launch_auto<false, true, EPI_BF16>(p, splits, stream);
+      else launch_auto<false, true, EPI_F32>(p, splits, stream);
     } break;
     case EPI_DGELU: launch_auto<false, true, EPI_DGELU>(p, 1, stream); break;
     default: throw std::runtime_error("gemm_dgrad: unsupported epilogue");

@@ -66,8 +66,9 @@ __global__ __launch_bounds__(NW * 64) void ln_fwd_kernel(const float* __restrict
   }
 }
 
-template <int VEC, int RPW, int NW>
-__global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+// DYB: dy (and its K-split partials) in bf16 -- the dgrad GEMMs write half the bytes
+template <int VEC, int RPW, int NW, bool DYB>
+__global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict__ dyv, const float* __restrict__ x,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
                                                      const float* __restrict__ g_res,
@@ -102,19 +103,25 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const float* __restrict
     rows[j] = (blockIdx.x * NW + wave) * RPW + j;
     const int row = rows[j] < M ? rows[j] : M - 1;
     const float2* xr = reinterpret_cast<const float2*>(x + (size_t)row * D);
-    const float2* dr = reinterpret_cast<const float2*>(dy + (size_t)row * D);
     const float2* gr = reinterpret_cast<const float2*>(g_res + (size_t)row * D);
+    auto ldy = [&](int pt, int i) -> float2 {
+      const size_t off = (size_t)pt * M * D + (size_t)row * D;
+      if (DYB) {
+        const bf16x2 e = reinterpret_cast<const bf16x2*>(reinterpret_cast<const bf16*>(dyv) + off)[lane + 64 * i];
+        return make_float2(bf2f(e[0]), bf2f(e[1]));
+      }
+      return reinterpret_cast<const float2*>(reinterpret_cast<const float*>(dyv) + off)[lane + 64 * i];
+    };
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
       xv[j][i] = xr[lane + 64 * i];
-      dv[j][i] = dr[lane + 64 * i];
+      dv[j][i] = ldy(0, i);
       rv[j][i] = g_res ? gr[lane + 64 * i] : make_float2(0.f, 0.f);
     }
     for (int pt = 1; pt < dy_parts; ++pt) {  // K-split dgrad partials
-      const float2* dp = dr + (size_t)pt * M * (D / 2);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) {
-        const float2 e = dp[lane + 64 * i];
+        const float2 e = ldy(pt, i);
         dv[j][i].x += e.x;
         dv[j][i].y += e.y;
       }
@@ -309,7 +316,7 @@ void layernorm_fwd_launch(const float* x, const float* gamma, const float* beta,
 #undef LN_FWD_GO
 }
 
-void layernorm_bwd_launch(const float* dy, const float* x, const float* mean, const float* rstd,
+void layernorm_bwd_launch(const void* dy, bool dy_bf16, const float* x, const float* mean, const float* rstd,
                           const float* gamma, const float* beta, const float* g_res, float* g_out, void* gy_bf16,
                           void* y_bf16, float* dgb_ws, int M,
                           int D, int tokens, const int64_t* rng, int site_drop, double p_drop, int site_dp,
@@ -323,12 +330,15 @@ void layernorm_bwd_launch(const float* dy, const float* x, const float* mean, co
     const char* e = getenv("DDIM_COLD_LN_BWD_CFG");
     return e ? atoi(e) : 0;
   }();
-#define LN_BWD_GO(R, W)                                                                                      \
-  LN_DISPATCH(D, hipLaunchKernelGGL((ln_bwd_kernel<VEC, R, W>), dim3((M + R * W - 1) / (R * W)), dim3(W * 64), 0, \
-                                    stream, dy, x, mean, rstd, gamma, beta, g_res, g_out,                     \
+#define LN_BWD_GO1(R, W, DYB)                                                                                 \
+  LN_DISPATCH(D, hipLaunchKernelGGL((ln_bwd_kernel<VEC, R, W, DYB>), dim3((M + R * W - 1) / (R * W)), dim3(W * 64), \
+                                    0, stream, dy, x, mean, rstd, gamma, beta, g_res, g_out,                   \
                                     reinterpret_cast<bf16*>(gy_bf16), reinterpret_cast<bf16*>(y_bf16), dgb_ws,  \
                                     M, tokens, rng, site_drop, td,                                              \
                                     sd, site_dp, tp, sp, dy_parts))
+#define LN_BWD_GO(R, W)           \
+  if (dy_bf16) LN_BWD_GO1(R, W, true) \
+  else LN_BWD_GO1(R, W, false)
   // measured on the ViT-tiny shape (M 2080, D 384, dropout on): 1 row x 8 waves
   // 5.0 us, 2 x 4 5.9, 1 x 4 5.2, 1 x 16 5.1, 2 x 16 7.2
   switch (cfg) {
@@ -338,6 +348,7 @@ void layernorm_bwd_launch(const float* dy, const float* x, const float* mean, co
     default: LN_BWD_GO(1, 8); break;
   }
 #undef LN_BWD_GO
+#undef LN_BWD_GO1
 }
 
 int ln_replicas() { return LN_REPLICAS; }

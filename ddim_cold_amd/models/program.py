@@ -34,6 +34,11 @@ FUSE_LN = os.environ.get("DDIM_COLD_FUSE_LN", "0") == "1"  # residual GEMM + Lay
 # K split of the QKV input-gradient GEMM (reduction dim 3D): the partial products
 # go to separate buffers that the LayerNorm backward sums on load
 QKV_DGRAD_SPLITS = int(os.environ.get("DDIM_COLD_QKV_DGRAD_SPLITS", "2"))
+# the input-gradient GEMMs feeding a LayerNorm backward (head, fc1, QKV) write
+# bf16 (the K-split partials too) instead of fp32: half the bytes on both sides
+# of the dgrad -> LayerNorm-backward hand-off; the LayerNorm backward sums and
+# computes in fp32 (the reference's fp16 autocast hands it fp16 gradients)
+DGRAD_BF16 = os.environ.get("DDIM_COLD_DGRAD_BF16", "1") == "1"
 # LayerNorm fold (csrc/gemm.hip): every LayerNorm is folded into the GEMM that
 # consumes it (QKV, fc1, head) -- no LayerNorm launch in the forward.  The
 # producing GEMM's epilogue accumulates the row statistics; the LayerNorm
@@ -417,7 +422,8 @@ class ViTProgram:
 
         def ln_out(lo):
             return torch.empty(M, D, dtype=ACT_DTYPE, device=dtok.device) if fold else lo
-        dlf = ops.linear_dgrad(dtok, P.head_w, True)
+        f32 = not DGRAD_BF16
+        dlf = ops.linear_dgrad(dtok, P.head_w, f32)
         lf = ln_out(S.lf)
         _, _, _, _, sf2, sd2 = block_sites(L - 1)
         g, gy = ops.layernorm_bwd(dlf, S.xL, S.mf, S.rf, P.nw, None, G.nw, G.nb, N, rng, sf2, pd, sd2,
@@ -430,7 +436,7 @@ class ViTProgram:
             sa, sp, sd1, sf1, _, _ = block_sites(i)
             wgrad(gy, h, bg.fc2_w, bg.fc2_b)
             du = ops.linear_dgrad_gelu(gy, bp.fc2_w, u, rng, sf1, pd)
-            dl2 = ops.linear_dgrad(du, bp.fc1_w, True)
+            dl2 = ops.linear_dgrad(du, bp.fc1_w, f32)
             k2 = 1 + 2 * (L - 1 - i)
             l2 = ln_out(l2)
             g1, gy1 = ops.layernorm_bwd(dl2, x1, m2, r2, bp.n2w, g, bg.n2w, bg.n2b, N, rng, sp, pd, sd1, dpr[i],
@@ -439,7 +445,7 @@ class ViTProgram:
             wgrad(gy1, o, bg.proj_w, bg.proj_b)
             do = ops.linear_dgrad(gy1, bp.proj_w, False)
             dqkv = ops.attn_bwd(do, qkv, o, lse, c.scale, rng, sa, ad)
-            dl1 = ops.linear_dgrad(dqkv, bp.qkv_w, True, QKV_DGRAD_SPLITS if 3 * D >= 768 else 1)
+            dl1 = ops.linear_dgrad(dqkv, bp.qkv_w, f32, QKV_DGRAD_SPLITS if 3 * D >= 768 else 1)
             l1 = ln_out(l1)
             fk = dict(beta=bp.n1b, y_out=l1) if fold else {}
             if i > 0:

@@ -186,9 +186,9 @@ def img_to_tokgrad(dimg, N: int, patch: int):
 
 # ----------------------------------------------------------------------------- backward
 def linear_dgrad(dy, w, out_fp32: bool, splits: int = 1):
-    """``dy @ W``.  ``splits`` > 1 (fp32): ``[splits, M, K]`` partial products
-    over slices of the reduction dim, written without atomics or zeroing;
-    :func:`layernorm_bwd` sums them as it loads ``dy``."""
+    """``dy @ W``.  ``splits`` > 1: ``[splits, M, K]`` partial products (fp32 or
+    bf16) over slices of the reduction dim, written without atomics or zeroing;
+    :func:`layernorm_bwd` sums them (in fp32) as it loads ``dy``."""
     if _hip(dy):
         return _ops().linear_dgrad(dy, w, bool(out_fp32), int(splits))
     return ref.linear_dgrad(dy, w, out_fp32, splits)

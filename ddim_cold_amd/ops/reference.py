@@ -277,12 +277,13 @@ def smooth_l1_fwd_bwd(pred, target, N: int, patch: int, beta: float = 1.0):
 def linear_dgrad(dy, w, out_fp32: bool, splits: int = 1):
     """dx = dy @ W  (W in nn.Linear layout [N_out, K]).  ``splits`` > 1: the
     [splits, M, K] partial products over 64-aligned slices of N_out, as the
-    K-split kernel writes them (their sum is dx)."""
+    K-split kernel writes them (their sum is dx; fp32 or bf16 each)."""
     if splits > 1:
         kt = (dy.shape[1] + 63) // 64
         step = (kt + splits - 1) // splits * 64
-        return torch.stack([dy[:, z * step:(z + 1) * step].float() @ w[z * step:(z + 1) * step].float()
-                            for z in range(splits)])
+        parts = torch.stack([dy[:, z * step:(z + 1) * step].float() @ w[z * step:(z + 1) * step].float()
+                             for z in range(splits)])
+        return parts if out_fp32 else bf16(parts)
     dx = dy.float() @ w.float()
     return dx if out_fp32 else bf16(dx)
 

@@ -235,3 +235,26 @@ def test_fused_qkv_attention(B, N, H, D, p, fold):
     # eval-mode call: no qkv saved, same output
     o2, _, q2 = ops.qkv_attn_fwd(a, wq, bq, B, N, H, scale, r, 11, p, False, fold=fk(None, None)[:3] if fold else None)
     assert q2 is None and torch.equal(o2, o)
+
+
+@pytest.mark.parametrize("splits", [1, 2, 3])
+def test_bf16_dgrad_into_layernorm_bwd(splits):
+    """bf16 input-gradient GEMM (optionally K-split into bf16 partials) feeding the
+    LayerNorm backward, which sums the partials in fp32."""
+    M, Nout, K, N = 2080, 1152, 384, 65
+    dy = (torch.randn(M, Nout, device=DEV)).to(torch.bfloat16)
+    w = (torch.randn(Nout, K, device=DEV) * 0.05).to(torch.bfloat16)
+    parts = ops.linear_dgrad(dy, w, False, splits)
+    pr = ref.linear_dgrad(dy, w, False, splits)
+    assert parts.dtype == torch.bfloat16 and parts.shape == pr.shape
+    close(parts, pr, 2e-2, 1e-2, "bf16 dgrad partials")
+    x = torch.randn(M, K, device=DEV) * 2 + 0.3
+    g, be = torch.randn(K, device=DEV), torch.randn(K, device=DEV)
+    _, mu, rs = ref.layernorm_fwd(x, g, be)
+    dg1, db1, dg2, db2 = (torch.zeros(K, device=DEV) for _ in range(4))
+    go, gy = ops.layernorm_bwd(parts, x, mu, rs, g, None, dg1, db1, N, rng(), 7, 0.1, 8, 0.1, True)
+    gor, gyr = ref.layernorm_bwd(parts, x, mu, rs, g, None, dg2, db2, N, rng(), 7, 0.1, 8, 0.1, True)
+    close(go, gor, 1e-4, 1e-4, "g_out")
+    close(dg1, dg2, 1e-2, 1e-4, "dgamma")
+    close(db1, db2, 1e-2, 1e-4, "dbeta")
+    close(gy, gyr, 1e-2, 1e-2, "gy")
