@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
         ls += pv;
         if (thr) {
           const int key = kv0 + 16 * t + 4 * g + r;
-          const uint32_t idx = (uint32_t)(((size_t)bh * N + q) * N + key);
+          const uint32_t idx = (uint32_t)(((size_t)bh * N + q) * attn_mask_ld(N) + key);
           pv = dropout_keep(salt, idx, thr) ? pv * dsc : 0.f;
         }
         st[t][r] = pv;
@@ -275,17 +275,20 @@ __global__ __launch_bounds__(256) void attn_fwd_flash2_kernel(const bf16* __rest
       mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
       const float m_new = fmaxf(m_run[u], mt);
       const float alpha = exp2f(m_run[u] - m_new);
-      const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * N + kv0);
+      const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * attn_mask_ld(N) + kv0);
       float ls = 0.f;
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+      for (int t = 0; t < 4; ++t) {
+        bool kp[4] = {true, true, true, true};
+        if (DROP) dropout_keep4(salt, rowidx + (uint32_t)(16 * t + 4 * g), thr, kp);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float pv = exp2f(st[u][t][r] - m_new);
           ls += pv;
-          if (DROP) pv = dropout_keep(salt, rowidx + (uint32_t)(16 * t + 4 * g + r), thr) ? pv * dsc : 0.f;
+          if (DROP) pv = kp[r] ? pv * dsc : 0.f;
           st[u][t][r] = pv;
         }
+      }
       ls += __shfl_xor(ls, 16, 64);
       ls += __shfl_xor(ls, 32, 64);
       l_run[u] = l_run[u] * alpha + ls;
@@ -432,17 +435,20 @@ __global__ __launch_bounds__(640) void attn_fwd_resident_kernel(const bf16* __re
       mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
       const float m_new = fmaxf(m_run[u], mt);
       const float alpha = exp2f(m_run[u] - m_new);
-      const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * N + kv0);
+      const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * attn_mask_ld(N) + kv0);
       float ls = 0.f;
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+      for (int t = 0; t < 4; ++t) {
+        bool kp[4] = {true, true, true, true};
+        if (DROP) dropout_keep4(salt, rowidx + (uint32_t)(16 * t + 4 * g), thr, kp);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float pv = exp2f(st[u][t][r] - m_new);
           ls += pv;
-          if (DROP) pv = dropout_keep(salt, rowidx + (uint32_t)(16 * t + 4 * g + r), thr) ? pv * dsc : 0.f;
+          if (DROP) pv = kp[r] ? pv * dsc : 0.f;
           st[u][t][r] = pv;
         }
+      }
       ls += __shfl_xor(ls, 16, 64);
       ls += __shfl_xor(ls, 32, 64);
       l_run[u] = l_run[u] * alpha + ls;
@@ -587,7 +593,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
         const float pr = key < N ? exp2f(st[r] * sl2 - lse2) : 0.f;
         float dpv = dp[r];
         if (thr) {
-          const uint32_t idx = (uint32_t)(((size_t)bh * N + q) * N + key);
+          const uint32_t idx = (uint32_t)(((size_t)bh * N + q) * attn_mask_ld(N) + key);
           dpv = dropout_keep(salt, idx, thr) ? dpv * dsc : 0.f;
         }
         ds[t][r] = pr * (dpv - dl);
@@ -719,7 +725,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
         const float pr = exp2f(st[r] * sl2 - sl[qr]);
         float pd = pr, dpv = dp[r];
         if (thr) {
-          const uint32_t idx = (uint32_t)(((size_t)bh * N + qq) * N + key);
+          const uint32_t idx = (uint32_t)(((size_t)bh * N + qq) * attn_mask_ld(N) + key);
           const bool kp = dropout_keep(salt, idx, thr);
           pd = kp ? pr * dsc : 0.f;
           dpv = kp ? dpv * dsc : 0.f;
@@ -888,16 +894,19 @@ __global__ __launch_bounds__(NP * 4) void attn_fwd_short_kernel(const bf16* __re
   mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
   float l = 0.f;
-  const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * N);
+  const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * attn_mask_ld(N));
 #pragma unroll
-  for (int t = 0; t < KT; ++t)
+  for (int t = 0; t < KT; ++t) {
+    bool kp[4] = {true, true, true, true};
+    if (DROP) dropout_keep4(salt, rowidx + (uint32_t)(16 * t + 4 * g), thr, kp);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float pv = exp2f(st[t][r] - mx);
       l += pv;
-      if (DROP) pv = dropout_keep(salt, rowidx + (uint32_t)(16 * t + 4 * g + r), thr) ? pv * dsc : 0.f;
+      if (DROP) pv = kp[r] ? pv * dsc : 0.f;
       st[t][r] = pv;
     }
+  }
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
   f32x4 o[DT];
@@ -976,7 +985,7 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
   }
   dl += __shfl_xor(dl, 16, 64);
   dl += __shfl_xor(dl, 32, 64);
-  const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * N);
+  const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * attn_mask_ld(N));
   f32x4 ds[KT];
 #pragma unroll
   for (int t = 0; t < KT; ++t) {
@@ -987,13 +996,15 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
       dp = mfma16(frag_row<HD>(Vl, 16 * t + li, s, g), df[s], dp);
     }
     f32x4 pm;
+    bool kq[4] = {true, true, true, true};
+    if (DROP) dropout_keep4(salt, rowidx + (uint32_t)(16 * t + 4 * g), thr, kq);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int key = 16 * t + 4 * g + r;
       const float pr = key < N ? exp2f(st[r] * sl2 - lse2) : 0.f;
       float pd = pr, dpv = dp[r];
       if (DROP) {
-        const bool kp = dropout_keep(salt, rowidx + (uint32_t)key, thr);
+        const bool kp = kq[r];
         pd = kp ? pr * dsc : 0.f;
         dpv = kp ? dpv * dsc : 0.f;
       }
@@ -1271,16 +1282,19 @@ __global__ __launch_bounds__(NP * 4) void qkv_attn_fwd_kernel(QkvAttnArgs a) {
   mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
   float l = 0.f;
-  const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * N);
+  const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * attn_mask_ld(N));
 #pragma unroll
-  for (int t = 0; t < KT; ++t)
+  for (int t = 0; t < KT; ++t) {
+    bool kp[4] = {true, true, true, true};
+    if (DROP) dropout_keep4(salt, rowidx + (uint32_t)(16 * t + 4 * g), a.thr, kp);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float pv = exp2f(st[t][r] - mx);
       l += pv;
-      if (DROP) pv = dropout_keep(salt, rowidx + (uint32_t)(16 * t + 4 * g + r), a.thr) ? pv * a.dsc : 0.f;
+      if (DROP) pv = kp[r] ? pv * a.dsc : 0.f;
       st[t][r] = pv;
     }
+  }
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
   f32x4 o[DT];

@@ -74,13 +74,35 @@ __device__ __forceinline__ uint32_t site_salt(const int64_t* rng, int site) {
   return mix32(b + (uint32_t)site * 0x85EBCA6Bu);
 }
 
-__device__ __forceinline__ bool dropout_keep(uint32_t salt, uint32_t idx, uint32_t thresh) {
-  return mix32((idx * 0x9E3779B1u) ^ salt) >= thresh;
+// Dropout masks (counter-based, regenerated in backward): element i of a site
+// keeps iff the 16-bit half (i & 1) of mix32(((i >> 1) * golden) ^ salt) is
+// >= thr, thr = round(p * 2^16).  One hash serves an aligned pair of elements
+// (v_mul_lo_u32 is quarter rate: the hash dominated the dropout cost).
+__device__ __forceinline__ uint32_t drop_hash(uint32_t salt, uint32_t pair) {
+  return mix32((pair * 0x9E3779B1u) ^ salt);
 }
 
+__device__ __forceinline__ bool dropout_keep(uint32_t salt, uint32_t idx, uint32_t thresh) {
+  const uint32_t h = drop_hash(salt, idx >> 1);
+  return ((idx & 1u) ? (h >> 16) : (h & 0xFFFFu)) >= thresh;
+}
+
+// keep flags of the 4 consecutive elements idx..idx+3 (idx even): two hashes
+__device__ __forceinline__ void dropout_keep4(uint32_t salt, uint32_t idx, uint32_t thresh, bool (&k)[4]) {
+  const uint32_t h0 = drop_hash(salt, idx >> 1), h1 = drop_hash(salt, (idx >> 1) + 1u);
+  k[0] = (h0 & 0xFFFFu) >= thresh;
+  k[1] = (h0 >> 16) >= thresh;
+  k[2] = (h1 & 0xFFFFu) >= thresh;
+  k[3] = (h1 >> 16) >= thresh;
+}
+
+// attention-probability masks index (b, h, q, key) as (bh * N + q) * ld + key
+// with the row stride padded to 4 (aligned pairs / quads within a row)
+__host__ __device__ __forceinline__ int attn_mask_ld(int N) { return (N + 3) & ~3; }
+
 inline uint32_t drop_threshold_host(double p) {
-  double v = p * 4294967296.0 + 0.5;
-  if (v >= 4294967295.0) return 0xFFFFFFFFu;
+  double v = p * 65536.0 + 0.5;
+  if (v >= 65536.0) return 65536u;  // drop everything
   if (v <= 0.0) return 0u;
   return (uint32_t)v;
 }

@@ -611,10 +611,12 @@ struct VecEpi {
         } else if (EPI == EPI_ACC) {
           st4(reinterpret_cast<float*>(p.C) + idx, pre[i][j] + v);
         } else if (EPI == EPI_RESID) {
+          bool kp[4] = {true, true, true, true};
+          if (p.thr_drop) dropout_keep4(salt_drop, (uint32_t)idx, p.thr_drop, kp);
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             float e = v[c];
-            if (p.thr_drop) e = dropout_keep(salt_drop, (uint32_t)(idx + c), p.thr_drop) ? e * p.scale_drop : 0.f;
+            if (p.thr_drop) e = kp[c] ? e * p.scale_drop : 0.f;
             if (p.thr_dp) e = keep_row ? e * p.scale_dp : 0.f;
             v[c] = pre[i][j][c] + e;
           }
@@ -627,26 +629,33 @@ struct VecEpi {
         } else if (EPI == EPI_GELU) {
           st4bf(reinterpret_cast<bf16*>(p.C) + idx, v);
           f32x4 h;
+          bool kp[4] = {true, true, true, true};
+          if (p.thr_drop) dropout_keep4(salt_drop, (uint32_t)idx, p.thr_drop, kp);
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             float e = gelu_f(v[c]);
-            if (p.thr_drop) e = dropout_keep(salt_drop, (uint32_t)(idx + c), p.thr_drop) ? e * p.scale_drop : 0.f;
+            if (p.thr_drop) e = kp[c] ? e * p.scale_drop : 0.f;
             h[c] = e;
           }
           st4bf(reinterpret_cast<bf16*>(p.C2) + idx, h);
         } else if (EPI == EPI_DGELU) {
+          bool kp[4] = {true, true, true, true};
+          if (p.thr_drop) dropout_keep4(salt_drop, (uint32_t)idx, p.thr_drop, kp);
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             float e = v[c];
-            if (p.thr_drop) e = dropout_keep(salt_drop, (uint32_t)(idx + c), p.thr_drop) ? e * p.scale_drop : 0.f;
+            if (p.thr_drop) e = kp[c] ? e * p.scale_drop : 0.f;
             v[c] = e * gelu_grad_f(pre[i][j][c]);
           }
           st4bf(reinterpret_cast<bf16*>(p.C) + idx, v);
         } else if (EPI == EPI_EMBED) {
           v += pre[i][j];
+          if (p.thr_drop) {
+            bool kp[4];
+            dropout_keep4(salt_drop, (uint32_t)idx, p.thr_drop, kp);
 #pragma unroll
-          for (int c = 0; c < 4; ++c)
-            if (p.thr_drop) v[c] = dropout_keep(salt_drop, (uint32_t)(idx + c), p.thr_drop) ? v[c] * p.scale_drop : 0.f;
+            for (int c = 0; c < 4; ++c) v[c] = kp[c] ? v[c] * p.scale_drop : 0.f;
+          }
           st4(reinterpret_cast<float*>(p.C) + idx, v);
           if (prod) {
             part[i][j / 2] = f2add(part[i][j / 2], make_float2((v[0] + v[1]) + (v[2] + v[3]),

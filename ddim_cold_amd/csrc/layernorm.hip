@@ -170,8 +170,9 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict_
         float a = o.x * dpsc, b = o.y * dpsc;
         if (thr_drop) {
           const uint32_t idx = (uint32_t)((size_t)row * D + 2 * c);
-          a = dropout_keep(salt_drop, idx, thr_drop) ? a * sc_drop : 0.f;
-          b = dropout_keep(salt_drop, idx + 1, thr_drop) ? b * sc_drop : 0.f;
+          const uint32_t hh = drop_hash(salt_drop, idx >> 1);  // idx even: one hash for the pair
+          a = (hh & 0xFFFFu) >= thr_drop ? a * sc_drop : 0.f;
+          b = (hh >> 16) >= thr_drop ? b * sc_drop : 0.f;
         }
         bf16x2 h;
         h[0] = f2bf(a);

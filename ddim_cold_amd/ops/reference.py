@@ -61,16 +61,30 @@ def site_salt(rng: torch.Tensor, site: int) -> int:
 
 
 def drop_threshold(p: float) -> int:
-    """Drop iff hash < threshold; threshold = round(p * 2^32) clamped to uint32."""
-    return min(int(p * 4294967296.0 + 0.5), MASK32)
+    """Drop iff the element's 16-bit hash half < threshold; threshold = round(p * 2^16)."""
+    return min(int(p * 65536.0 + 0.5), 65536)
 
 
 def keep_mask(numel: int, rng: torch.Tensor, site: int, p: float, device=None) -> torch.Tensor:
-    """Boolean keep-mask over a flat index space [0, numel) (bit-exact with the HIP kernels)."""
+    """Boolean keep-mask over a flat index space [0, numel) (bit-exact with ``dropout_keep``
+    in csrc/common.h): element i uses the 16-bit half (i & 1) of the hash of pair i >> 1."""
     salt = site_salt(rng, site)
     idx = torch.arange(numel, dtype=torch.int64, device=device) & MASK32
-    h = mix32(_mul32(idx, GOLDEN) ^ salt)
-    return h >= drop_threshold(p)
+    h = mix32(_mul32(idx >> 1, GOLDEN) ^ salt)
+    half = torch.where((idx & 1) == 1, h >> 16, h & 0xFFFF)
+    return half >= drop_threshold(p)
+
+
+def attn_mask_ld(N: int) -> int:
+    """Row stride of the attention-probability mask index (csrc/common.h attn_mask_ld)."""
+    return (N + 3) // 4 * 4
+
+
+def attn_keep_mask(B: int, H: int, N: int, rng, site: int, p: float, device=None) -> torch.Tensor:
+    """[B, H, N, N] keep-mask of the attention probabilities; element (b, h, q, key) has
+    flat index ((b*H + h)*N + q) * attn_mask_ld(N) + key."""
+    ld = attn_mask_ld(N)
+    return keep_mask(B * H * N * ld, rng, site, p, device).view(B, H, N, ld)[..., :N]
 
 
 def _dropout(x: torch.Tensor, rng, site, p) -> torch.Tensor:
@@ -204,7 +218,9 @@ def attn_fwd(qkv, scale: float, rng, site: int, p: float):
     s = (q @ k.transpose(-1, -2)) * scale
     lse = torch.logsumexp(s, dim=-1)
     pr = torch.exp(s - lse.unsqueeze(-1))
-    pr = _dropout(pr, rng, site, p)
+    if p > 0.0:
+        pr = torch.where(attn_keep_mask(B, H, N, rng, site, p, pr.device), pr / (1.0 - p),
+                         torch.zeros((), dtype=pr.dtype, device=pr.device))
     # P is rounded to bf16 before the PV product (as the MFMA kernel does)
     o = bf16(pr).float() @ v
     return bf16(o.transpose(1, 2).reshape(B, N, H * hd)), lse
@@ -352,7 +368,7 @@ def attn_bwd(do, qkv, o, lse, scale: float, rng, site: int, p: float):
     s = (q @ k.transpose(-1, -2)) * scale
     pr = torch.exp(s - lse.unsqueeze(-1))
     if p > 0:
-        m = keep_mask(pr.numel(), rng, site, p, pr.device).view(pr.shape).float() / (1.0 - p)
+        m = attn_keep_mask(B, H, N, rng, site, p, pr.device).float() / (1.0 - p)
     else:
         m = torch.ones_like(pr)
     pd = pr * m
