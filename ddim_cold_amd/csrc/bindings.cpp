@@ -329,7 +329,7 @@ void head_step_(Tensor a, Tensor w, Tensor b, Tensor x, c10::optional<Tensor> x0
 
 std::tuple<Tensor, Tensor> smooth_l1_fwd_bwd(Tensor pred, Tensor target, int64_t N, int64_t patch, double beta,
                                              c10::optional<Tensor> loss_last, c10::optional<Tensor> loss_ema,
-                                             double ema_decay) {
+                                             double ema_decay, bool finish) {
   CHECK_IN(pred, F32); CHECK_IN(target, F32);
   float* ll = nullptr;
   float* le = nullptr;
@@ -342,9 +342,11 @@ std::tuple<Tensor, Tensor> smooth_l1_fwd_bwd(Tensor pred, Tensor target, int64_t
   auto loss = at::empty({1}, pred.options());
   auto parts = at::empty({L1_PARTS}, pred.options());
   auto dtok = at::empty({(int64_t)B * N, C * patch * patch}, pred.options().dtype(BF16));
-  smooth_l1_launch(pred.data_ptr<float>(), target.data_ptr<float>(), loss.data_ptr<float>(), parts.data_ptr<float>(),
-                   dtok.data_ptr(), B, C, H, W, patch, (float)beta, ll, le, (float)ema_decay, cur_stream());
-  return {loss, dtok};
+  const int np = smooth_l1_launch(pred.data_ptr<float>(), target.data_ptr<float>(), loss.data_ptr<float>(),
+                                  parts.data_ptr<float>(), dtok.data_ptr(), B, C, H, W, patch, (float)beta, ll, le,
+                                  (float)ema_decay, finish, cur_stream());
+  // finish = false: the per-block partials (their sum is the loss) instead of the loss
+  return {finish ? loss : parts.narrow(0, 0, np), dtok};
 }
 
 Tensor img_to_tokgrad(Tensor dimg, int64_t N, int64_t patch) {
@@ -690,7 +692,9 @@ void cold_batch(Tensor pool, Tensor rng, int64_t site, Tensor x_t, Tensor x_tm1,
 // LayerNorm fold weights for a list of GEMMs consuming a LayerNorm (one launch)
 void ln_fold_(std::vector<Tensor> ws, std::vector<Tensor> gammas, std::vector<Tensor> betas,
               std::vector<c10::optional<Tensor>> biases, std::vector<Tensor> wfs, std::vector<Tensor> cs,
-              std::vector<Tensor> bfs) {
+              std::vector<Tensor> bfs, c10::optional<Tensor> loss_parts, c10::optional<Tensor> loss_last,
+              c10::optional<Tensor> loss_ema, double ema_decay, c10::optional<Tensor> step,
+              c10::optional<Tensor> rng, c10::optional<Tensor> sq) {
   const size_t n = ws.size();
   TORCH_CHECK(n > 0 && n <= (size_t)FOLD_MAX, "ln_fold_: 1..", FOLD_MAX, " GEMMs per launch");
   TORCH_CHECK(gammas.size() == n && betas.size() == n && biases.size() == n && wfs.size() == n && cs.size() == n &&
@@ -724,6 +728,22 @@ void ln_fold_(std::vector<Tensor> ws, std::vector<Tensor> gammas, std::vector<Te
     rows += R;
   }
   tb.start[n] = rows;
+  if (step.has_value() && step->defined()) {  // training-step tail in the same launch
+    CHECK_IN((*step), I64); check_rng(*rng);
+    TORCH_CHECK(loss_parts.has_value() && loss_parts->defined() && sq.has_value() && sq->defined(),
+                "step tail needs loss_parts and sq");
+    CHECK_IN((*loss_parts), F32); CHECK_IN((*sq), F32);
+    TORCH_CHECK(sq->numel() >= SQ_PARTS, "sq must hold SQ_PARTS partials");
+    tb.tail = 1;
+    tb.loss_parts = loss_parts->data_ptr<float>();
+    tb.loss_nparts = (int)loss_parts->numel();
+    if (loss_last.has_value() && loss_last->defined()) { CHECK_IN((*loss_last), F32); tb.loss_last = loss_last->data_ptr<float>(); }
+    if (loss_ema.has_value() && loss_ema->defined()) { CHECK_IN((*loss_ema), F32); tb.loss_ema = loss_ema->data_ptr<float>(); }
+    tb.ema_decay = (float)ema_decay;
+    tb.step = step->data_ptr<int64_t>();
+    tb.rng = rng->data_ptr<int64_t>();
+    tb.sq = sq->data_ptr<float>();
+  }
   ln_fold_launch(tb, cur_stream());
 }
 
@@ -797,7 +817,7 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("head_step_(Tensor a, Tensor w, Tensor b, Tensor(a!) x, Tensor(b!)? x0_out, Tensor? coef, int patch, "
         "int mode, Tensor? ln_st=None, Tensor? ln_c=None, float ln_eps=1e-5) -> ()");
   m.def("smooth_l1_fwd_bwd(Tensor pred, Tensor target, int N, int patch, float beta, Tensor(a!)? loss_last=None, "
-        "Tensor(b!)? loss_ema=None, float ema_decay=0.99) -> (Tensor, Tensor)");
+        "Tensor(b!)? loss_ema=None, float ema_decay=0.99, bool finish=True) -> (Tensor, Tensor)");
   m.def("img_to_tokgrad(Tensor dimg, int N, int patch) -> Tensor");
   m.def("linear_dgrad(Tensor dy, Tensor w, bool out_fp32, int splits=1) -> Tensor");
   m.def("linear_dgrad_gelu(Tensor dy, Tensor w, Tensor u, Tensor rng, int site, float p) -> Tensor");
@@ -808,7 +828,8 @@ TORCH_LIBRARY(ddim_cold, m) {
         "float p_dp, bool emit_gy, Tensor(c!)? ws=None, Tensor? beta=None, Tensor(d!)? y_out=None) -> (Tensor, Tensor)");
   m.def("replica_reduce_(Tensor(a!) ws, Tensor dst_ptrs, int C) -> ()");
   m.def("ln_fold_(Tensor[] ws, Tensor[] gammas, Tensor[] betas, Tensor?[] biases, Tensor(a!)[] wfs, Tensor(b!)[] cs, "
-        "Tensor(c!)[] bfs) -> ()");
+        "Tensor(c!)[] bfs, Tensor? loss_parts=None, Tensor(d!)? loss_last=None, Tensor(e!)? loss_ema=None, "
+        "float ema_decay=0.99, Tensor(f!)? step=None, Tensor(g!)? rng=None, Tensor? sq=None) -> ()");
   m.def("attn_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, float scale, Tensor rng, int site, float p) -> Tensor");
   m.def("embed_bwd(Tensor g, Tensor t, Tensor rng, int site, float p, Tensor(a!) dcls, Tensor(b!) dpos, "
         "Tensor(c!) dtemb) -> Tensor");

@@ -228,17 +228,19 @@ void embed_bwd_launch(const float* g, const int64_t* t, float* dcls, float* dpos
                      dtemb, reinterpret_cast<bf16*>(gpatch), B, N, D, rng, site, thr, dsc, blocksA, blocksB);
 }
 
-void smooth_l1_launch(const float* pred, const float* target, float* loss, float* partials, void* dtok, int B,
-                      int C, int H, int W, int patch, float beta, float* loss_last, float* loss_ema, float ema_decay,
-                      hipStream_t stream) {
+int smooth_l1_launch(const float* pred, const float* target, float* loss, float* partials, void* dtok, int B,
+                     int C, int H, int W, int patch, float beta, float* loss_last, float* loss_ema, float ema_decay,
+                     bool finish, hipStream_t stream) {
   const size_t n_img = (size_t)B * C * H * W;
   const size_t n = n_img + (size_t)B * C * patch * patch;
   int grid = grid_for(n);
   if (grid > L1_PARTS) grid = L1_PARTS;
   hipLaunchKernelGGL(tokgrad_kernel<true>, dim3(grid), dim3(256), 0, stream, pred, target, partials,
                      reinterpret_cast<bf16*>(dtok), B, C, H, W, patch, beta, 1.0f / (float)n_img);
-  hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(256), 0, stream, partials, grid, loss, loss_last, loss_ema,
-                     ema_decay);
+  if (finish)
+    hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(256), 0, stream, partials, grid, loss, loss_last, loss_ema,
+                       ema_decay);
+  return grid;
 }
 
 void img_to_tokgrad_launch(const float* dimg, void* dtok, int B, int C, int H, int W, int patch, hipStream_t stream) {

@@ -122,6 +122,18 @@ struct FoldTable {
   int start[FOLD_MAX + 1];
   int n;
   int K;
+  // optional training-step tail run by one extra workgroup of the same launch
+  // (the fold runs right after the optimizer): finish the smooth-L1 loss from its
+  // per-block partials (loss_last, EMA) and advance the step / RNG counters
+  int tail = 0;
+  const float* loss_parts = nullptr;
+  int loss_nparts = 0;
+  float* loss_last = nullptr;
+  float* loss_ema = nullptr;
+  float ema_decay = 0.99f;
+  int64_t* step = nullptr;
+  int64_t* rng = nullptr;
+  const float* sq = nullptr;  // SQ_PARTS grad-norm partials (non-finite -> optimizer step skipped)
 };
 void ln_fold_launch(const FoldTable& tb, hipStream_t stream);
 void replica_reduce_launch(float* ws, float* const* dsts_dev, int G, int C, hipStream_t stream);
@@ -139,9 +151,11 @@ void patchify_cls_launch(const float* img, const int64_t* t, const float* cls, c
                          int D, const int64_t* rng, int site, double p, float* st, void* xb, hipStream_t stream);
 void embed_bwd_launch(const float* g, const int64_t* t, float* dcls, float* dpos, float* dtemb, void* gpatch,
                       int B, int N, int D, const int64_t* rng, int site, double p, hipStream_t stream);
-void smooth_l1_launch(const float* pred, const float* target, float* loss, float* partials, void* dtok, int B,
-                      int C, int H, int W, int patch, float beta, float* loss_last, float* loss_ema, float ema_decay,
-                      hipStream_t stream);
+// returns the number of per-block loss partials written; finish = false leaves
+// summing them (loss, loss_last, EMA) to a later kernel (the step tail of ln_fold)
+int smooth_l1_launch(const float* pred, const float* target, float* loss, float* partials, void* dtok, int B,
+                     int C, int H, int W, int patch, float beta, float* loss_last, float* loss_ema, float ema_decay,
+                     bool finish, hipStream_t stream);
 constexpr int L1_PARTS = 512;
 void img_to_tokgrad_launch(const float* dimg, void* dtok, int B, int C, int H, int W, int patch,
                            hipStream_t stream);

@@ -228,6 +228,30 @@ __global__ __launch_bounds__(256) void replica_reduce_kernel(float* __restrict__
 // output row, all folded GEMMs of the model in one launch (after each
 // optimizer step; once per sampling run).
 __global__ __launch_bounds__(256) void ln_fold_kernel(FoldTable tb) {
+  if (tb.tail && blockIdx.x == gridDim.x - 1) {
+    // training-step tail (one workgroup): loss from its partials, counters
+    __shared__ float red[2][4];
+    float lv = 0.f, sv = 0.f;
+    for (int i = threadIdx.x; i < tb.loss_nparts; i += 256) lv += tb.loss_parts[i];
+    for (int i = threadIdx.x; i < SQ_PARTS; i += 256) sv += tb.sq[i];
+    lv = wave_sum(lv);
+    sv = wave_sum(sv);
+    if ((threadIdx.x & 63) == 0) {
+      red[0][threadIdx.x >> 6] = lv;
+      red[1][threadIdx.x >> 6] = sv;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float l = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+      const float sq = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+      if (tb.loss_last) tb.loss_last[0] = l;
+      if (tb.loss_ema) tb.loss_ema[0] = tb.loss_ema[0] * tb.ema_decay + l * (1.f - tb.ema_decay);
+      if (isfinite(sq)) tb.step[0] += 1;  // a non-finite step was skipped by the optimizer
+      tb.step[1] += 1;
+      tb.rng[1] += 1;
+    }
+    return;
+  }
   // two rows per wave (32 lanes each), every load of the row issued before use
   constexpr int IT = 4;  // float4 per lane: K <= 32 * 4 * IT = 512
   const int hl = threadIdx.x & 31;
@@ -283,7 +307,7 @@ void ln_fold_launch(const FoldTable& tb, hipStream_t stream) {
   if (tb.n <= 0) return;
   if (tb.n > FOLD_MAX || tb.K % 4 || tb.K > 512) throw std::runtime_error("ln_fold: bad table (K % 4, K <= 512)");
   const int rows = tb.start[tb.n];
-  hipLaunchKernelGGL(ln_fold_kernel, dim3((rows + 7) / 8), dim3(256), 0, stream, tb);
+  hipLaunchKernelGGL(ln_fold_kernel, dim3((rows + 7) / 8 + (tb.tail ? 1 : 0)), dim3(256), 0, stream, tb);
 }
 
 #define LN_DISPATCH(D, ...)                                                   \

@@ -182,13 +182,17 @@ class LnFold:
     def tensors(self):
         return [t for w, g, b, bias in self.src for t in (w, g, b, bias)]
 
-    def refresh(self):
+    def refresh(self, tail=None):
+        """Recompute the folded weights; ``tail`` (see :func:`ops.ln_fold_`) rides
+        along in the last launch."""
         for a in range(0, len(self.keys), 16):
             ks = self.keys[a:a + 16]
             src = self.src[a:a + 16]
+            last = a + 16 >= len(self.keys)
             ops.ln_fold_([w.reshape(w.shape[0], -1) for w, _, _, _ in src], [g for _, g, _, _ in src],
                          [b for _, _, b, _ in src], [bias for _, _, _, bias in src],
-                         [self.out[k][0] for k in ks], [self.out[k][1] for k in ks], [self.out[k][2] for k in ks])
+                         [self.out[k][0] for k in ks], [self.out[k][1] for k in ks], [self.out[k][2] for k in ks],
+                         tail=tail if last else None)
 
     def attach(self, P: "ModelTensors") -> "ModelTensors":
         for i, bp in enumerate(P.blocks):

@@ -165,12 +165,17 @@ def head_fwd(a, w, b, B: int, C: int, H: int, W: int, patch: int, fold=None):
 
 
 def smooth_l1_fwd_bwd(pred, target, N: int, patch: int, beta: float = 1.0, loss_last=None, loss_ema=None,
-                      ema_decay: float = 0.99):
+                      ema_decay: float = 0.99, finish: bool = True):
     """Mean smooth-L1 loss and its token-layout gradient; optionally also writes
-    ``loss_last`` and updates ``loss_ema`` (decay) in the same launch."""
+    ``loss_last`` and updates ``loss_ema`` (decay) in the same launch.  ``finish=False``
+    returns the loss as per-block partials (summed later by the step tail of
+    :func:`ln_fold_`) instead of launching the finishing reduction."""
     if _hip(pred):
-        return _ops().smooth_l1_fwd_bwd(pred, target, N, patch, float(beta), loss_last, loss_ema, float(ema_decay))
+        return _ops().smooth_l1_fwd_bwd(pred, target, N, patch, float(beta), loss_last, loss_ema, float(ema_decay),
+                                        bool(finish))
     loss, dtok = ref.smooth_l1_fwd_bwd(pred, target, N, patch, beta)
+    if not finish:
+        return loss.reshape(1), dtok
     if loss_last is not None:
         loss_last.copy_(loss.reshape(loss_last.shape))
     if loss_ema is not None:
@@ -273,15 +278,30 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dgamma, dbeta, N: int, rng, s
                              site_dp, p_dp, emit_gy)
 
 
-def ln_fold_(ws, gammas, betas, biases, wfs, cs, bfs):
+def ln_fold_(ws, gammas, betas, biases, wfs, cs, bfs, tail=None):
     """LayerNorm fold weights for GEMMs that consume a LayerNorm (one launch on GPU):
-    ``wf = bf16(gamma o W)``, ``c = rowsum(wf)``, ``bf = b + W beta``."""
+    ``wf = bf16(gamma o W)``, ``c = rowsum(wf)``, ``bf = b + W beta``.
+
+    ``tail = (loss_parts, loss_last, loss_ema, ema_decay, step, rng, sq)``: the
+    training step's tail rides in the same launch -- loss from the smooth-L1
+    partials (``loss_last``, EMA) and the counter advance of
+    :func:`advance_counters` (optimizer step only if the grad norm ``sq`` is finite)."""
     if not ws:
         return
     if _hip(ws[0]):
-        return _ops().ln_fold_(list(ws), list(gammas), list(betas), list(biases), list(wfs), list(cs), list(bfs))
+        t = tail if tail is not None else (None, None, None, 0.99, None, None, None)
+        return _ops().ln_fold_(list(ws), list(gammas), list(betas), list(biases), list(wfs), list(cs), list(bfs),
+                               t[0], t[1], t[2], float(t[3]), t[4], t[5], t[6])
     for w, g, be, b, wf, c, bf in zip(ws, gammas, betas, biases, wfs, cs, bfs):
         ref.ln_fold(w, g, be, b, wf, c, bf)
+    if tail is not None:
+        parts, loss_last, loss_ema, decay, step, rng, sq = tail
+        loss = parts.float().sum().reshape(1)
+        if loss_last is not None:
+            loss_last.copy_(loss.reshape(loss_last.shape))
+        if loss_ema is not None:
+            loss_ema.mul_(decay).add_(loss.reshape(loss_ema.shape), alpha=1.0 - decay)
+        advance_counters(step, rng, sq)
 
 
 def replica_reduce_(ws, dst_ptrs, C: int, dsts=None):

@@ -276,14 +276,21 @@ class TrainEngine:
     def _step_iter(self):
         c = self.prog.cfg
         k_acc = max(1, int(self.cfg.grad_accum))
+        # loss bookkeeping + counter advance ride in the LayerNorm-fold launch after
+        # the optimizer (one workgroup of it) instead of two extra tiny launches
+        tail = self.lnfold is not None and k_acc == 1
         for micro in range(k_acc):
             last = micro == k_acc - 1
             if micro > 0:
                 self.rng[1:].add_(1)  # fresh dropout masks and batch draws per micro-batch
             img, tgt, t = self.batch_fn()
             out, S = self.prog.forward(self.param_tensors, img, t, self.rng, True)
-            _, dtok = ops.smooth_l1_fwd_bwd(out, tgt, c.tokens, c.patch, self.cfg.loss_beta, self.loss_last,
-                                            self.loss_ema, self.cfg.ema_decay)
+            if tail:
+                loss_parts, dtok = ops.smooth_l1_fwd_bwd(out, tgt, c.tokens, c.patch, self.cfg.loss_beta,
+                                                         finish=False)
+            else:
+                _, dtok = ops.smooth_l1_fwd_bwd(out, tgt, c.tokens, c.patch, self.cfg.loss_beta, self.loss_last,
+                                                self.loss_ema, self.cfg.ema_decay)
             del out
             ln_lo = 0
             for i in self.prog.backward_iter(self.param_tensors, self.grad_tensors, S, dtok, self.rng, True,
@@ -307,9 +314,13 @@ class TrainEngine:
         ops.sqnorm(self.flat_g, self.sqnorm, gs)
         ops.adamw_step(self.flat_p, self.flat_g, self.flat_m, self.flat_v, self.flat_pb, self.sqnorm,
                        self.step_ctr, self.hyper, gs)
-        if self.lnfold is not None:
-            self.lnfold.refresh()
-        ops.advance_counters(self.step_ctr, self.rng, self.sqnorm)
+        if tail:
+            self.lnfold.refresh(tail=(loss_parts, self.loss_last, self.loss_ema, self.cfg.ema_decay, self.step_ctr,
+                                      self.rng, self.sqnorm))
+        else:
+            if self.lnfold is not None:
+                self.lnfold.refresh()
+            ops.advance_counters(self.step_ctr, self.rng, self.sqnorm)
         self.prog._keep = None
         yield ("done", -1)
 

@@ -1,0 +1,7 @@
+#!/bin/bash
+cd "$(dirname "$0")/.." 2>/dev/null || cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+rm -rf gpurun_out/prof_graph
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_graph -o run -- python3 bench.py --steps 30 --warmup 10 --no-sampler > gpurun_out/prof_graph.log 2>&1
+rc=$?; tail -2 gpurun_out/prof_graph.log; exit $rc
