@@ -390,7 +390,8 @@ class ViTProgram:
     # ------------------------------------------------------------------ backward
     def backward_iter(self, P: ModelTensors, G: ModelTensors, S: Saved, dtok: torch.Tensor, rng: torch.Tensor,
                       training: bool = True, wgrad: Optional[Callable] = None,
-                      ln_ws: Optional[torch.Tensor] = None, wgrad_stream=None) -> Iterator[int]:
+                      ln_ws: Optional[torch.Tensor] = None, wgrad_stream=None,
+                      embed_with_block0: bool = False) -> Iterator[int]:
         """Hand-written backward; yields the block index after each block's grads
         are issued (L-1 first, then ..., 0) and -1 after the embedding grads.
 
@@ -401,7 +402,10 @@ class ViTProgram:
         each one immediately (e.g. on a side stream).  ``ln_ws`` ([2L+1, R, 2D],
         zero) collects LayerNorm dgamma/dbeta replicas in backward order (final
         norm, then norm2/norm1 of blocks L-1..0); the caller finalises them
-        with ``ops.replica_reduce_``.
+        with ``ops.replica_reduce_``.  ``embed_with_block0``: the embedding
+        backward runs before block 0's weight gradients are issued, so the
+        patch-embedding weight gradient joins block 0's grouped launch (one
+        launch fewer; no separate gradient bucket for the embeddings then).
         """
         def ws(k):
             return None if ln_ws is None else ln_ws[k]
@@ -461,18 +465,27 @@ class ViTProgram:
                                           False, ws(k2 + 1), **fk)
             wgrad(dqkv, l1, bg.qkv_w, bg.qkv_b)
             keep.append((gy1, du, dqkv, l1, l2))
+            if i == 0 and embed_with_block0:
+                gpatch = self._embed_backward(P, G, S, g, rng, pd, wgrad)
             flush()
             yield i
-        B = S.t.shape[0]
-        temb_g = G.temb if G.temb is not None else torch.zeros_like(P.temb)
-        gpatch = ops.embed_bwd(g.view(B, N, D), S.t, rng, SITE_EMBED, pd, G.cls, G.pos, temb_g)
-        wgrad(gpatch, S.patches, G.pe_w, G.pe_b)
-        flush()
+        if not embed_with_block0:
+            gpatch = self._embed_backward(P, G, S, g, rng, pd, wgrad)
+            flush()
         keep.append((gpatch, lf))
         if batch is not None:
             keep.append(batch.keep)
         self._keep = keep  # holds side-stream operands alive until the caller joins
         yield -1
+
+    def _embed_backward(self, P, G, S, g, rng, pd, wgrad):
+        """cls / pos / time-embedding gradients and the patch-embedding weight gradient (queued)."""
+        c = self.cfg
+        B = S.t.shape[0]
+        temb_g = G.temb if G.temb is not None else torch.zeros_like(P.temb)
+        gpatch = ops.embed_bwd(g.view(B, c.tokens, c.dim), S.t, rng, SITE_EMBED, pd, G.cls, G.pos, temb_g)
+        wgrad(gpatch, S.patches, G.pe_w, G.pe_b)
+        return gpatch
 
     def backward(self, P, G, S, dtok, rng, training=True, wgrad=None):
         for _ in self.backward_iter(P, G, S, dtok, rng, training, wgrad):

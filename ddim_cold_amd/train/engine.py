@@ -293,8 +293,11 @@ class TrainEngine:
                                                 self.loss_ema, self.cfg.ema_decay)
             del out
             ln_lo = 0
+            # without a separate embedding bucket (single process) the patch-embedding
+            # weight gradient joins block 0's grouped launch
+            merge = not (self.segmented and self.cfg.embed_bucket)
             for i in self.prog.backward_iter(self.param_tensors, self.grad_tensors, S, dtok, self.rng, True,
-                                             ln_ws=self.ln_ws, wgrad_stream=self.side):
+                                             ln_ws=self.ln_ws, wgrad_stream=self.side, embed_with_block0=merge):
                 if i in self.bucket_after and (self.segmented or i == -1):
                     hi = self.ln_done_at[i]
                     if hi > ln_lo:
