@@ -327,6 +327,38 @@ void head_step_(Tensor a, Tensor w, Tensor b, Tensor x, c10::optional<Tensor> x0
   gemm_nt(g, EPI_HEAD, cur_stream());
 }
 
+// Head GEMM with the training loss in its epilogue (head_mode 3): the smooth-L1
+// of the unpatchified prediction vs `target` (multi_gpu_trainer.py:124) as one
+// partial per workgroup, and its gradient written straight into the token
+// layout the head backward consumes (cls rows zero).  Returns (partials, dtok).
+std::tuple<Tensor, Tensor> head_loss(Tensor a, Tensor w, Tensor b, Tensor target, int64_t patch, double beta,
+                                     c10::optional<Tensor> ln_st, c10::optional<Tensor> ln_c, double ln_eps,
+                                     c10::optional<Tensor> ln_mean, c10::optional<Tensor> ln_rstd) {
+  CHECK_IN(a, BF16); CHECK_IN(w, BF16); CHECK_IN(b, F32); CHECK_IN(target, F32);
+  const c10::DeviceGuard guard(a.device());
+  TORCH_CHECK(target.dim() == 4, "target must be [B, C, H, W]");
+  const int B = target.size(0), C = target.size(1), H = target.size(2), W = target.size(3);
+  const int K = a.size(-1);
+  auto a2 = a.view({-1, K});
+  check_linear(a2, w, K);
+  const int N = (H / patch) * (W / patch) + 1, F = C * patch * patch;
+  TORCH_CHECK(a2.size(0) == (int64_t)B * N && w.size(0) == F && b.numel() == F, "head_loss shapes");
+  TORCH_CHECK(beta > 0, "smooth-L1 beta must be > 0");
+  const int M = B * N;
+  auto dtok = at::empty({M, F}, a.options());
+  auto parts = at::empty({gemm_nt_grid(M, F, K)}, a.options().dtype(F32));
+  GemmArgs g = nt_args(a2, w);
+  g.C = dtok.data_ptr(); g.C2 = dtok.data_ptr(); g.bias = b.data_ptr<float>(); g.res = target.data_ptr<float>();
+  g.tokens = N; g.batch = B; g.chans = C; g.img_h = H; g.img_w = W; g.patch = patch;
+  g.head_mode = 3;
+  g.loss_beta = (float)beta;
+  g.loss_inv_n = 1.0f / (float)((int64_t)B * C * H * W);
+  g.loss_parts = parts.data_ptr<float>();
+  apply_fold(g, M, F, ln_st, ln_c, ln_eps, ln_mean, ln_rstd);
+  gemm_nt(g, EPI_HEAD, cur_stream());
+  return {parts, dtok};
+}
+
 std::tuple<Tensor, Tensor> smooth_l1_fwd_bwd(Tensor pred, Tensor target, int64_t N, int64_t patch, double beta,
                                              c10::optional<Tensor> loss_last, c10::optional<Tensor> loss_ema,
                                              double ema_decay, bool finish) {
@@ -816,6 +848,8 @@ TORCH_LIBRARY(ddim_cold, m) {
         "Tensor? ln_c=None, float ln_eps=1e-5, Tensor(a!)? ln_mean=None, Tensor(b!)? ln_rstd=None) -> Tensor");
   m.def("head_step_(Tensor a, Tensor w, Tensor b, Tensor(a!) x, Tensor(b!)? x0_out, Tensor? coef, int patch, "
         "int mode, Tensor? ln_st=None, Tensor? ln_c=None, float ln_eps=1e-5) -> ()");
+  m.def("head_loss(Tensor a, Tensor w, Tensor b, Tensor target, int patch, float beta, Tensor? ln_st=None, "
+        "Tensor? ln_c=None, float ln_eps=1e-5, Tensor(a!)? ln_mean=None, Tensor(b!)? ln_rstd=None) -> (Tensor, Tensor)");
   m.def("smooth_l1_fwd_bwd(Tensor pred, Tensor target, int N, int patch, float beta, Tensor(a!)? loss_last=None, "
         "Tensor(b!)? loss_ema=None, float ema_decay=0.99, bool finish=True) -> (Tensor, Tensor)");
   m.def("img_to_tokgrad(Tensor dimg, int N, int patch) -> Tensor");
@@ -856,6 +890,7 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("linear_gelu_fwd", &linear_gelu_fwd);
   m.impl("head_fwd", &head_fwd);
   m.impl("smooth_l1_fwd_bwd", &smooth_l1_fwd_bwd);
+  m.impl("head_loss", &head_loss);
   m.impl("img_to_tokgrad", &img_to_tokgrad);
   m.impl("linear_dgrad", &linear_dgrad);
   m.impl("linear_dgrad_gelu", &linear_dgrad_gelu);

@@ -63,7 +63,11 @@ struct GemmParams {
   int ktiles_per_split;
   const float* coef;     // HEAD mode 1: {sqrt a_t, sqrt(1-a_t), sqrt a_tk, sqrt(1-a_tk)} (device)
   long long split_stride;  // EPI_F32: elements between the K-split output slices
-  int head_mode;         // HEAD: 0 image, 1 fused DDIM step (res = x_t in, C = x_next, C2 = x0), 2 clamp
+  int head_mode;         // HEAD: 0 image, 1 fused DDIM step (res = x_t in, C = x_next, C2 = x0), 2 clamp,
+                         //   3 training loss (res = target image, C2 = token-layout grad, loss_parts)
+  float loss_beta;       // HEAD mode 3: smooth-L1 beta and 1/numel
+  float loss_inv_n;
+  float* loss_parts;     // HEAD mode 3: one loss partial per workgroup (gridDim.x entries)
   // LayerNorm fold (GemmArgs): consumer side
   const float* ln_st;
   const float* ln_c;
@@ -279,6 +283,12 @@ __device__ __forceinline__ float epilogue(const GemmParams& p, long long idx, in
   } else if (EPI == EPI_HEAD) {
     if (p.head_mode == 0) {
       reinterpret_cast<float*>(p.C)[idx] = v;
+    } else if (p.head_mode == 3) {
+      // smooth-L1 vs the target pixel (`pre`), multi_gpu_trainer.py:124: the image
+      // is never written; returns the element's loss / numel (the gradient is
+      // stored by the caller in the token layout)
+      const float d = v - pre, ad = fabsf(d), b = p.loss_beta;
+      return (ad < b ? 0.5f * d * d / b : ad - 0.5f * b) * p.loss_inv_n;
     } else {
       // the sampler's x0-hat clamp (ViT.py:229, ViT_draft2drawing.py:280), and for
       // mode 1 the whole DDIM update (ViT.py:230-234) with x_t preloaded in `pre`
@@ -307,6 +317,7 @@ __device__ __forceinline__ void run_epilogue_scalar(const GemmParams& p, const f
                                              int g, int li) {
   constexpr bool ELEM = EPI == EPI_RESID || EPI == EPI_DGELU || EPI == EPI_EMBED || EPI == EPI_ACC;
   const bool head_ddim = EPI == EPI_HEAD && p.head_mode == 1;
+  const bool head_loss = EPI == EPI_HEAD && p.head_mode == 3;
   RowInfo rows[FM][4];
   long long cols[FN];
   bool colok[FN];
@@ -354,7 +365,7 @@ __device__ __forceinline__ void run_epilogue_scalar(const GemmParams& p, const f
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float v = 0.f;
-        if (head_ddim && rows[i][r].off >= 0 && colok[j]) v = p.res[rows[i][r].off + cols[j]];
+        if ((head_ddim || head_loss) && rows[i][r].off >= 0 && colok[j]) v = p.res[rows[i][r].off + cols[j]];
         if (ELEM && rows[i][r].off >= 0 && colok[j]) {
           const int n = nb + j * 16 + li;
           if (EPI == EPI_RESID) v = p.res[rows[i][r].off + n];
@@ -396,6 +407,7 @@ __device__ __forceinline__ void run_epilogue_scalar(const GemmParams& p, const f
       }
     }
   const bool prod = FP && p.st_out != nullptr;
+  float lsum = 0.f;  // HEAD mode 3: this lane's loss contributions
   float2 part[FM][4][(FN + 1) / 2];  // producer (debug path): per-slot partials of the lane's rows
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -417,6 +429,14 @@ __device__ __forceinline__ void run_epilogue_scalar(const GemmParams& p, const f
             part[i][r][j / 2] = f2add(part[i][r][j / 2], make_float2(o, o * o));
             p.xb_out[rows[i][r].off + cols[j]] = f2bf(o);
           }
+          if (head_loss) {  // gradient of the mean smooth-L1, straight into the token layout
+            const int m = mb + i * 16 + 4 * g + r, n = nb + j * 16 + li;
+            const float d = (a + colb[j] - pre[i][j][r]) / p.loss_beta;
+            reinterpret_cast<bf16*>(p.C2)[(size_t)m * p.N + n] = f2bf(fminf(fmaxf(d, -1.f), 1.f) * p.loss_inv_n);
+            lsum += o;
+          }
+        } else if (head_loss && colok[j] && mb + i * 16 + 4 * g + r < p.M) {  // cls rows: zero gradient
+          reinterpret_cast<bf16*>(p.C2)[(size_t)(mb + i * 16 + 4 * g + r) * p.N + nb + j * 16 + li] = f2bf(0.f);
         }
   if (prod) {
     const int np_out = p.N / LN_SLOT;
@@ -436,6 +456,13 @@ __device__ __forceinline__ void run_epilogue_scalar(const GemmParams& p, const f
             *reinterpret_cast<float2*>(p.st_out + 2 * ((size_t)fold_token_row<EPI>(p, m) * np_out + nb / LN_SLOT +
                                                        sl)) = t;
         }
+  }
+  if (head_loss) {  // one deterministic partial per workgroup (summed by the step tail)
+    __shared__ float lred[4];
+    lsum = wave_sum(lsum);
+    if ((threadIdx.x & 63) == 0) lred[threadIdx.x >> 6] = lsum;
+    __syncthreads();
+    if (threadIdx.x == 0) p.loss_parts[blockIdx.x] = (lred[0] + lred[1]) + (lred[2] + lred[3]);
   }
 }
 
@@ -1334,6 +1361,7 @@ static GemmParams base_params(const GemmArgs& a) {
   p.chans = a.chans; p.img_h = a.img_h; p.img_w = a.img_w; p.patch = a.patch;
   p.pos = a.pos; p.temb = a.temb; p.tsteps = a.tsteps; p.emb_dim = a.emb_dim;
   p.coef = a.coef; p.head_mode = a.head_mode;
+  p.loss_beta = a.loss_beta; p.loss_inv_n = a.loss_inv_n; p.loss_parts = a.loss_parts;
   p.split_stride = a.split_stride;
   p.ln_st = a.ln_st; p.ln_c = a.ln_c; p.ln_eps = a.ln_eps; p.ln_mean = a.ln_mean; p.ln_rstd = a.ln_rstd;
   p.st_out = a.st_out; p.xb_out = reinterpret_cast<bf16*>(a.xb_out);
@@ -1359,6 +1387,21 @@ void gemm_nt(const GemmArgs& a, int epi, hipStream_t stream) {
     case EPI_EMBED: launch_auto<false, false, EPI_EMBED>(p, 1, stream); break;
     default: throw std::runtime_error("gemm_nt: unsupported epilogue");
   }
+}
+
+int gemm_nt_grid(int M, int N, int K) {
+  // mirrors launch_auto<false, false, *> (one split)
+  const bool dma_ok = K % 64 == 0 && !dma_disabled();
+  int bm = 64, bn = 64;
+  if (dma_ok) {
+    const int cfg = pick_tiles(M, N, K, 1, false, false);
+    const int bms[4] = {32, 64, 128, 128}, bns[4] = {64, 64, 64, 128};
+    bm = bms[cfg < 0 ? 0 : (cfg > 3 ? 3 : cfg)];
+    bn = bns[cfg < 0 ? 0 : (cfg > 3 ? 3 : cfg)];
+  } else if (((M + 63) / 64) * ((N + 63) / 64) < 240) {
+    bm = 32;
+  }
+  return ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
 }
 
 void gemm_dgrad(const GemmArgs& a, int epi, hipStream_t stream) {

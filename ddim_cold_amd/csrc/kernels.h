@@ -40,7 +40,10 @@ struct GemmArgs {
   const int64_t* tsteps = nullptr;
   int emb_dim = 0;
   const float* coef = nullptr;  // EPI_HEAD head_mode 1
-  int head_mode = 0;            // EPI_HEAD: 0 image, 1 fused DDIM step, 2 clamp
+  int head_mode = 0;            // EPI_HEAD: 0 image, 1 fused DDIM step, 2 clamp, 3 smooth-L1 loss + grad
+  float loss_beta = 1.f;        // EPI_HEAD mode 3
+  float loss_inv_n = 1.f;
+  float* loss_parts = nullptr;  // EPI_HEAD mode 3: one partial per workgroup (gemm_nt_grid entries)
   // EPI_F32 dgrad split over K: slice z of `splits` writes its partial product to
   // C + z * split_stride (no atomics, no zeroing; the consumer sums the slices)
   int splits = 1;
@@ -63,6 +66,8 @@ struct GemmArgs {
 };
 
 void gemm_nt(const GemmArgs& a, int epi, hipStream_t stream);
+// workgroups gemm_nt launches for an [M x N x K] problem (one split)
+int gemm_nt_grid(int M, int N, int K);
 void gemm_dgrad(const GemmArgs& a, int epi, hipStream_t stream);
 void gemm_wgrad(const GemmArgs& a, int splits, hipStream_t stream);
 // grouped dW += dy^T x for n <= 6 problems in one launch; splits == 1 -> plain

@@ -267,12 +267,16 @@ class ViTProgram:
 
     # ------------------------------------------------------------------ forward
     def forward(self, P: ModelTensors, img: torch.Tensor, t: torch.Tensor, rng: torch.Tensor, training: bool,
-                save: bool = True, head_step=None):
+                save: bool = True, head_step=None, loss=None):
         """``head_step = (mode, x0_out, coef)`` fuses the sampler update into the head
         GEMM (``ops.head_step_``): ``img`` (the current x_t) is updated in place and
-        returned; mode 1 = DDIM step, mode 2 = clamp (cold sampler)."""
+        returned; mode 1 = DDIM step, mode 2 = clamp (cold sampler).  ``loss =
+        (target, beta)`` (LayerNorm-folded program only, see :meth:`supports_fused_loss`)
+        returns ``(loss_parts, dtok)`` from :func:`ops.head_loss` instead of the image."""
         if P.folded and fold_width_ok(self.cfg.dim):
-            return self._forward_folded(P, img, t, rng, training, save, head_step)
+            return self._forward_folded(P, img, t, rng, training, save, head_step, loss)
+        if loss is not None:
+            raise ValueError("the fused head loss needs the LayerNorm-folded program")
         c = self.cfg
         B = img.shape[0]
         N, D, M = c.tokens, c.dim, B * c.tokens
@@ -324,7 +328,7 @@ class ViTProgram:
             S.xL, S.lf, S.mf, S.rf = x, lf, mf, rf
         return out, S
 
-    def _forward_folded(self, P: ModelTensors, img, t, rng, training: bool, save: bool, head_step):
+    def _forward_folded(self, P: ModelTensors, img, t, rng, training: bool, save: bool, head_step, loss=None):
         """Forward with every LayerNorm folded into its consumer GEMM: 5 launches
         per block (QKV, attention, proj+residual, fc1+GELU, fc2+residual).  The
         residual GEMMs (and the patch embedding) emit each new residual row's
@@ -381,11 +385,19 @@ class ViTProgram:
                            fold=(st[2 * L], P.head_c, c.eps))
             return img, S
         mf, rf = stats()
-        out = ops.head_fwd(xb, P.head_wf, P.head_bf, B, c.chans, c.img_h, c.img_w, c.patch,
-                           fold=(st[2 * L], P.head_c, c.eps, mf, rf))
+        if loss is not None:  # training: the loss and its token-layout gradient from the head GEMM
+            target, beta = loss
+            out = ops.head_loss(xb, P.head_wf, P.head_bf, target, c.patch, beta,
+                                fold=(st[2 * L], P.head_c, c.eps, mf, rf))
+        else:
+            out = ops.head_fwd(xb, P.head_wf, P.head_bf, B, c.chans, c.img_h, c.img_w, c.patch,
+                               fold=(st[2 * L], P.head_c, c.eps, mf, rf))
         if save:
             S.xL, S.lf, S.mf, S.rf = x, None, mf, rf
         return out, S
+
+    def supports_fused_loss(self, P: ModelTensors) -> bool:
+        return P.folded and fold_width_ok(self.cfg.dim)
 
     # ------------------------------------------------------------------ backward
     def backward_iter(self, P: ModelTensors, G: ModelTensors, S: Saved, dtok: torch.Tensor, rng: torch.Tensor,

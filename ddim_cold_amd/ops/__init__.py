@@ -164,6 +164,20 @@ def head_fwd(a, w, b, B: int, C: int, H: int, W: int, patch: int, fold=None):
     return ref.head_fwd(a, w, b, B, C, H, W, patch, st, c, eps, mean, rstd)
 
 
+def head_loss(a, w, b, target, patch: int, beta: float = 1.0, fold=None):
+    """Head GEMM + mean smooth-L1 vs ``target`` + its gradient in the token layout, in
+    one launch: ``(loss_parts, dtok)`` -- the loss is ``loss_parts.sum()`` (finished by
+    the step tail of :func:`ln_fold_`); the predicted image is never materialised."""
+    st, c, eps, mean, rstd = _fold_args(fold)
+    if _hip(a):
+        return _ops().head_loss(a, w, b, target, patch, float(beta), st, c, eps, mean, rstd)
+    B, C, H, W = target.shape
+    out = ref.head_fwd(a, w, b, B, C, H, W, patch, st, c, eps, mean, rstd)
+    N = a.shape[0] // B
+    loss, dtok = ref.smooth_l1_fwd_bwd(out, target, N, patch, beta)
+    return loss.reshape(1), dtok
+
+
 def smooth_l1_fwd_bwd(pred, target, N: int, patch: int, beta: float = 1.0, loss_last=None, loss_ema=None,
                       ema_decay: float = 0.99, finish: bool = True):
     """Mean smooth-L1 loss and its token-layout gradient; optionally also writes

@@ -284,8 +284,16 @@ class TrainEngine:
             if micro > 0:
                 self.rng[1:].add_(1)  # fresh dropout masks and batch draws per micro-batch
             img, tgt, t = self.batch_fn()
-            out, S = self.prog.forward(self.param_tensors, img, t, self.rng, True)
-            if tail:
+            if tail and self.prog.supports_fused_loss(self.param_tensors):
+                # head GEMM epilogue computes the loss partials and the token-layout gradient
+                (loss_parts, dtok), S = self.prog.forward(self.param_tensors, img, t, self.rng, True,
+                                                          loss=(tgt, self.cfg.loss_beta))
+                out = None
+            else:
+                out, S = self.prog.forward(self.param_tensors, img, t, self.rng, True)
+            if out is None:
+                pass
+            elif tail:
                 loss_parts, dtok = ops.smooth_l1_fwd_bwd(out, tgt, c.tokens, c.patch, self.cfg.loss_beta,
                                                          finish=False)
             else:

@@ -258,3 +258,28 @@ def test_bf16_dgrad_into_layernorm_bwd(splits):
     close(dg1, dg2, 1e-2, 1e-4, "dgamma")
     close(db1, db2, 1e-2, 1e-4, "dbeta")
     close(gy, gyr, 1e-2, 1e-2, "gy")
+
+
+@pytest.mark.parametrize("B,C,H,W,p,D,fold", [(32, 3, 64, 64, 8, 384, True), (4, 3, 64, 64, 4, 256, False),
+                                              (3, 3, 32, 32, 8, 128, True)])
+def test_head_loss_fused(B, C, H, W, p, D, fold):
+    """Head GEMM with the smooth-L1 loss + token-layout gradient in its epilogue ==
+    head_fwd + smooth_l1_fwd_bwd."""
+    N = (H // p) * (W // p) + 1
+    M = B * N
+    F = C * p * p
+    if fold:
+        x, a, st, w, g, be, b, wf, c, bf = folded(F, D, M)
+        fk = (st, c, 1e-5)
+    else:
+        a = torch.randn(M, D, device=DEV).to(torch.bfloat16)
+        wf = (torch.randn(F, D, device=DEV) * 0.05).to(torch.bfloat16)
+        bf = torch.randn(F, device=DEV) * 0.1
+        fk = None
+    target = torch.randn(B, C, H, W, device=DEV).clamp(-1, 1)
+    parts, dtok = ops.head_loss(a, wf, bf, target, p, 1.0, fold=fk)
+    img = ops.head_fwd(a, wf, bf, B, C, H, W, p, fold=fk)
+    loss_r, dtok_r = ops.smooth_l1_fwd_bwd(img, target, N, p, 1.0)
+    torch.testing.assert_close(parts.sum(), loss_r.reshape(()), rtol=1e-4, atol=1e-6)
+    close(dtok, dtok_r, 1e-6, 1e-2, "token-layout gradient")
+    assert torch.count_nonzero(dtok.view(B, N, F)[:, 0]) == 0
