@@ -737,18 +737,19 @@ void ln_fold_(std::vector<Tensor> ws, std::vector<Tensor> gammas, std::vector<Te
   tb.K = ws[0].size(-1);
   TORCH_CHECK(tb.K % 4 == 0, "ln_fold_: K % 4");
   int rows = 0;
+  tb.w_bf16 = ws[0].scalar_type() == BF16 ? 1 : 0;
   for (size_t i = 0; i < n; ++i) {
-    CHECK_IN(ws[i], F32); CHECK_IN(gammas[i], F32); CHECK_IN(betas[i], F32);
+    CHECK_IN(ws[i], (tb.w_bf16 ? BF16 : F32)); CHECK_IN(gammas[i], F32); CHECK_IN(betas[i], F32);
     CHECK_IN(wfs[i], BF16); CHECK_IN(cs[i], F32); CHECK_IN(bfs[i], F32);
     TORCH_CHECK(ws[i].dim() == 2 && ws[i].size(1) == tb.K, "ln_fold_: weights must be [rows, K] with one K");
     const int R = ws[i].size(0);
     TORCH_CHECK(gammas[i].numel() == tb.K && betas[i].numel() == tb.K && wfs[i].numel() == (int64_t)R * tb.K &&
                     cs[i].numel() == R && bfs[i].numel() == R, "ln_fold_: shapes");
     for (const Tensor* t : {&ws[i], &gammas[i], &betas[i]})
-      TORCH_CHECK(((uintptr_t)t->data_ptr() & 15) == 0, "ln_fold_: 16-B aligned fp32 operands");
+      TORCH_CHECK(((uintptr_t)t->data_ptr() & 15) == 0, "ln_fold_: 16-B aligned operands");
     TORCH_CHECK(((uintptr_t)wfs[i].data_ptr() & 7) == 0, "ln_fold_: 8-B aligned output");
     FoldJob& j = tb.j[i];
-    j.w = ws[i].data_ptr<float>(); j.gamma = gammas[i].data_ptr<float>(); j.beta = betas[i].data_ptr<float>();
+    j.w = ws[i].data_ptr(); j.gamma = gammas[i].data_ptr<float>(); j.beta = betas[i].data_ptr<float>();
     j.bias = nullptr;
     if (biases[i].has_value() && biases[i]->defined()) {
       CHECK_IN((*biases[i]), F32);

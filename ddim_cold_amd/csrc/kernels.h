@@ -114,7 +114,7 @@ int ln_replicas();
 // LayerNorm fold weights for the GEMMs that consume a LayerNorm (layernorm.hip)
 constexpr int FOLD_MAX = 16;
 struct FoldJob {
-  const float* w;      // [rows][K] fp32 master weight
+  const void* w;       // [rows][K] weight: fp32 master, or its bf16 shadow (FoldTable::w_bf16)
   const float* gamma;  // [K]
   const float* beta;   // [K]
   const float* bias;   // [rows] or null
@@ -127,6 +127,7 @@ struct FoldTable {
   int start[FOLD_MAX + 1];
   int n;
   int K;
+  int w_bf16 = 0;  // weights given as bf16 (the optimizer's shadow copy: half the bytes)
   // optional training-step tail run by one extra workgroup of the same launch
   // (the fold runs right after the optimizer): finish the smooth-L1 loss from its
   // per-block partials (loss_last, EMA) and advance the step / RNG counters

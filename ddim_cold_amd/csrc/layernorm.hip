@@ -264,7 +264,8 @@ __global__ __launch_bounds__(256) void ln_fold_kernel(FoldTable tb) {
     if (j < tb.n && rr >= tb.start[j]) ji = j;
   const FoldJob& jb = tb.j[ji];
   const int n = rr - tb.start[ji], K4 = tb.K / 4;
-  const float4* w = reinterpret_cast<const float4*>(jb.w + (size_t)n * tb.K);
+  const float4* w = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(jb.w) + (size_t)n * tb.K);
+  const bf16x4* wb = reinterpret_cast<const bf16x4*>(reinterpret_cast<const bf16*>(jb.w) + (size_t)n * tb.K);
   const float4* g = reinterpret_cast<const float4*>(jb.gamma);
   const float4* b = reinterpret_cast<const float4*>(jb.beta);
   bf16x4* o = reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(jb.wf) + (size_t)n * tb.K);
@@ -273,7 +274,12 @@ __global__ __launch_bounds__(256) void ln_fold_kernel(FoldTable tb) {
   for (int i = 0; i < IT; ++i) {
     const int k = hl + 32 * i;
     const bool ok = k < K4;
-    wv[i] = ok ? w[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tb.w_bf16) {
+      const bf16x4 q = ok ? wb[k] : bf16x4{};
+      wv[i] = ok ? make_float4(bf2f(q[0]), bf2f(q[1]), bf2f(q[2]), bf2f(q[3])) : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      wv[i] = ok ? w[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     gv[i] = ok ? g[k] : make_float4(0.f, 0.f, 0.f, 0.f);
     bv[i] = ok ? b[k] : make_float4(0.f, 0.f, 0.f, 0.f);
   }

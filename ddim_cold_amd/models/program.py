@@ -159,10 +159,14 @@ class LnFold:
     def names(depth: int):
         return [n for j in LnFold.jobs(depth) for n in j[1:]]
 
-    def __init__(self, named32: Dict[str, torch.Tensor], depth: int):
+    def __init__(self, named32: Dict[str, torch.Tensor], depth: int,
+                 weights: Optional[Dict[str, torch.Tensor]] = None):
+        """``weights``: optional replacement tensors for the matrix weights (the
+        engine passes its bf16 shadow copies: the fold then reads half the bytes)."""
         jobs = self.jobs(depth)
         self.keys = [j[0] for j in jobs]
-        self.src = [tuple(named32[n] for n in j[1:]) for j in jobs]
+        self.src = [tuple((weights[n] if (weights is not None and k == 0) else named32[n])
+                          for k, n in enumerate(j[1:])) for j in jobs]
         w0 = self.src[0][0]
         dev, K = w0.device, w0.shape[1]
         rows = [w.shape[0] for w, _, _, _ in self.src]

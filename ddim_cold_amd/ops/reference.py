@@ -328,7 +328,7 @@ def layernorm_out_(x, mean, rstd, gamma, beta, y_out):
 
 def ln_fold(w, gamma, beta, bias, wf, c, bf):
     """LayerNorm fold weights: wf = bf16(gamma o W); c = rowsum(wf) (of the bf16
-    values); bf = bias + W beta."""
+    values); bf = bias + W beta.  ``w`` fp32, or its bf16 copy (then used as is)."""
     wq = bf16(w.float() * gamma.float().unsqueeze(0))
     wf.copy_(wq.view(wf.shape))
     c.copy_(wq.float().sum(1).view(c.shape))

@@ -191,7 +191,11 @@ class TrainEngine:
         # LayerNorm fold: gamma-scaled bf16 weights / row sums / folded biases of
         # the QKV, fc1 and head GEMMs, recomputed from the fp32 masters after
         # every optimizer step (inside the step graph)
-        self.lnfold = LnFold({n: p.data for n, p in named}, c.depth) if _program.FOLD_LN else None
+        # (reads the bf16 shadow the optimizer just wrote: half the bytes of the fp32 masters)
+        self.lnfold = LnFold({n: p.data for n, p in named}, c.depth,
+                             weights={n: self.flat_pb[o:o + k].view(p.shape)
+                                      for n, p in named for o, k in [self.offsets[n]] if is_matrix_param(n)}) \
+            if _program.FOLD_LN else None
         self._refresh_shadow()
         for n, p in named:
             o, k = self.offsets[n]

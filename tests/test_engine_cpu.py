@@ -42,7 +42,8 @@ def _grads(model, x, y, t, rng):
     P = collect(views, c.depth, c.dim)
     from ddim_cold_amd.models import program as pr
     if pr.FOLD_LN:  # the engine folds every LayerNorm into its consumer GEMM
-        fold = pr.LnFold({n: p.detach() for n, p in model.named_parameters()}, c.depth)
+        fold = pr.LnFold({n: p.detach() for n, p in model.named_parameters()}, c.depth,
+                         weights={n: v for n, v in views.items() if is_matrix_param(n)})
         fold.refresh()
         fold.attach(P)
     G = collect(grads, c.depth, c.dim)

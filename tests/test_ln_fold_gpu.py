@@ -283,3 +283,18 @@ def test_head_loss_fused(B, C, H, W, p, D, fold):
     torch.testing.assert_close(parts.sum(), loss_r.reshape(()), rtol=1e-4, atol=1e-6)
     close(dtok, dtok_r, 1e-6, 1e-2, "token-layout gradient")
     assert torch.count_nonzero(dtok.view(B, N, F)[:, 0]) == 0
+
+
+def test_ln_fold_kernel_bf16_weights():
+    """Fold from the optimizer's bf16 weight shadow (what the train engine does)."""
+    rows, K = 1152, 384
+    w = (torch.randn(rows, K, device=DEV)).to(torch.bfloat16)
+    g, be, b = torch.randn(K, device=DEV), torch.randn(K, device=DEV), torch.randn(rows, device=DEV)
+    outs = [torch.empty(rows, K, dtype=torch.bfloat16, device=DEV), torch.empty(rows, device=DEV),
+            torch.empty(rows, device=DEV)]
+    ops.ln_fold_([w], [g], [be], [b], *[[o] for o in outs])
+    exp = [torch.empty_like(o) for o in outs]
+    ref.ln_fold(w.float(), g, be, b, *exp)
+    close(outs[0], exp[0], 0, 0, "wf")
+    close(outs[1], exp[1], 1e-3, 1e-5, "c")
+    close(outs[2], exp[2], 1e-3, 1e-5, "bf")
