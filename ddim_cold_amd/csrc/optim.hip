@@ -46,12 +46,21 @@ __global__ __launch_bounds__(256) void sqnorm_kernel(const float* __restrict__ g
   if (threadIdx.x == 0) out[blockIdx.x] = (red[0] + red[1] + red[2] + red[3]) * scale * scale;
 }
 
+__device__ __forceinline__ void adamw_elem(float& p, float g, float& m, float& v, float coef, float decay, float b1,
+                                           float b2, float step_size, float inv_sbc2, float eps) {
+  const float gi = g * coef;
+  p *= decay;
+  m = b1 * m + (1.f - b1) * gi;
+  v = b2 * v + (1.f - b2) * gi * gi;
+  p -= step_size * m / (sqrtf(v) * inv_sbc2 + eps);
+}
+
 // hyper = {base_lr, beta1, beta2, eps, weight_decay, max_norm, T_max, eta_min}
 // step  = {adam_step, sched_step}
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                                                     float* __restrict__ v, bf16* __restrict__ pb, int64_t n,
                                                     const float* __restrict__ sqnorm, const int64_t* __restrict__ step,
-                                                    const float* __restrict__ hyper, float grad_scale) {
+                                                    const float* __restrict__ hyper, float grad_scale, bool vec) {
   const float sq = sum_parts(sqnorm);
   const bool skip = !isfinite(sq);
   const float base_lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
@@ -66,14 +75,36 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, float
   const float step_size = lr / bc1;
   const float inv_sbc2 = 1.f / sqrtf(bc2);
   const float decay = 1.f - lr * wd;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const float gi = g[i] * coef;
+  // 16-byte vectors (the arenas are allocator-aligned; `vec` is checked on the host),
+  // scalar tail.  Same math per element as the scalar path.
+  const int64_t nv = vec ? n / 4 : 0;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += stride) {
+    float4 gv = reinterpret_cast<float4*>(g)[i];
+    reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (skip) continue;
+    float4 pv = reinterpret_cast<const float4*>(p)[i];
+    float4 mv = reinterpret_cast<const float4*>(m)[i];
+    float4 vv = reinterpret_cast<const float4*>(v)[i];
+    adamw_elem(pv.x, gv.x, mv.x, vv.x, coef, decay, b1, b2, step_size, inv_sbc2, eps);
+    adamw_elem(pv.y, gv.y, mv.y, vv.y, coef, decay, b1, b2, step_size, inv_sbc2, eps);
+    adamw_elem(pv.z, gv.z, mv.z, vv.z, coef, decay, b1, b2, step_size, inv_sbc2, eps);
+    adamw_elem(pv.w, gv.w, mv.w, vv.w, coef, decay, b1, b2, step_size, inv_sbc2, eps);
+    reinterpret_cast<float4*>(m)[i] = mv;
+    reinterpret_cast<float4*>(v)[i] = vv;
+    reinterpret_cast<float4*>(p)[i] = pv;
+    if (pb) {
+      bf16x4 o;
+      o[0] = f2bf(pv.x); o[1] = f2bf(pv.y); o[2] = f2bf(pv.z); o[3] = f2bf(pv.w);
+      reinterpret_cast<bf16x4*>(pb)[i] = o;
+    }
+  }
+  for (int64_t i = nv * 4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    float gi = g[i];
     g[i] = 0.f;
     if (skip) continue;
-    float pi = p[i] * decay;
-    const float mi = b1 * m[i] + (1.f - b1) * gi;
-    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
-    pi -= step_size * mi / (sqrtf(vi) * inv_sbc2 + eps);
+    float pi = p[i], mi = m[i], vi = v[i];
+    adamw_elem(pi, gi, mi, vi, coef, decay, b1, b2, step_size, inv_sbc2, eps);
     m[i] = mi;
     v[i] = vi;
     p[i] = pi;
@@ -95,7 +126,7 @@ __global__ __launch_bounds__(256) void advance_kernel(int64_t* step, int64_t* rn
 using namespace dc;
 
 static int opt_grid(int64_t n) {
-  int64_t g = (n + 255) / 256;
+  int64_t g = (n / 4 + 255) / 256;
   if (g > 2048) g = 2048;
   if (g < 1) g = 1;
   return (int)g;
@@ -107,8 +138,10 @@ void sqnorm_launch(const float* g, int64_t n, float* out, float scale, hipStream
 
 void adamw_launch(float* p, float* g, float* m, float* v, void* p_bf16, int64_t n, const float* sqnorm,
                   const int64_t* step, const float* hyper, float grad_scale, hipStream_t stream) {
+  auto al = [](const void* q, uintptr_t a) { return (reinterpret_cast<uintptr_t>(q) & (a - 1)) == 0; };
+  const bool vec = al(p, 16) && al(g, 16) && al(m, 16) && al(v, 16) && (p_bf16 == nullptr || al(p_bf16, 8));
   hipLaunchKernelGGL(adamw_kernel, dim3(opt_grid(n)), dim3(256), 0, stream, p, g, m, v,
-                     reinterpret_cast<bf16*>(p_bf16), n, sqnorm, step, hyper, grad_scale);
+                     reinterpret_cast<bf16*>(p_bf16), n, sqnorm, step, hyper, grad_scale, vec);
 }
 
 void advance_counters_launch(int64_t* step, int64_t* rng, const float* sqnorm, hipStream_t stream) {
