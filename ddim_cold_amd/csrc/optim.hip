@@ -34,7 +34,17 @@ __global__ __launch_bounds__(256) void sqnorm_kernel(const float* __restrict__ g
   float acc = 0.f;
   const int64_t n4 = n / 4;
   const float4* g4 = reinterpret_cast<const float4*>(g);
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+  // four independent 16-byte loads in flight per thread before any use
+  const int64_t st = (int64_t)gridDim.x * 256;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * st < n4; i += 4 * st) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = g4[i + u * st];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
+  }
+  for (; i < n4; i += st) {
     const float4 v = g4[i];
     acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
   }
