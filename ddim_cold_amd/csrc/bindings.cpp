@@ -93,9 +93,10 @@ void apply_prod(GemmArgs& g, int64_t rows, int64_t D, const c10::optional<Tensor
 
 // ln_st: [B*N][D/32][2] row statistics of the tokens (the first LayerNorm's
 // input; LayerNorm fold), filled together with the tokens' bf16 copy xb_out.
-std::tuple<Tensor, Tensor> patch_embed_fwd(Tensor img, Tensor t, Tensor w_pe, Tensor b_pe, Tensor cls, Tensor pos,
-                                           Tensor temb, Tensor rng, int64_t site, double p, int64_t patch,
-                                           c10::optional<Tensor> ln_st, c10::optional<Tensor> xb_out) {
+static std::tuple<Tensor, Tensor> patch_embed_impl(Tensor img, Tensor t, Tensor w_pe, Tensor b_pe, Tensor cls,
+                                                   Tensor pos, Tensor temb, Tensor rng, int64_t site, double p,
+                                                   int64_t patch, c10::optional<Tensor> ln_st,
+                                                   c10::optional<Tensor> xb_out, ColdSrc cs) {
   CHECK_IN(img, F32); CHECK_IN(t, I64); CHECK_IN(w_pe, BF16); CHECK_IN(b_pe, F32);
   CHECK_IN(cls, F32); CHECK_IN(pos, F32); CHECK_IN(temb, F32); check_rng(rng);
   const c10::DeviceGuard guard(img.device());
@@ -125,7 +126,7 @@ std::tuple<Tensor, Tensor> patch_embed_fwd(Tensor img, Tensor t, Tensor w_pe, Te
   }
   patchify_cls_launch(img.data_ptr<float>(), t.data_ptr<int64_t>(), cls.data_ptr<float>(), pos.data_ptr<float>(),
                       temb.data_ptr<float>(), patches.data_ptr(), x.data_ptr<float>(), B, C, H, W, P, D,
-                      rng.data_ptr<int64_t>(), site, p, st, xb, cur_stream());
+                      rng.data_ptr<int64_t>(), site, p, st, xb, cur_stream(), cs);
   GemmArgs g;
   g.A = patches.data_ptr();
   g.B = w_pe.data_ptr();
@@ -139,6 +140,41 @@ std::tuple<Tensor, Tensor> patch_embed_fwd(Tensor img, Tensor t, Tensor w_pe, Te
   g.xb_out = xb;
   gemm_nt(g, EPI_EMBED, cur_stream());
   return {x, patches};
+}
+
+std::tuple<Tensor, Tensor> patch_embed_fwd(Tensor img, Tensor t, Tensor w_pe, Tensor b_pe, Tensor cls, Tensor pos,
+                                           Tensor temb, Tensor rng, int64_t site, double p, int64_t patch,
+                                           c10::optional<Tensor> ln_st, c10::optional<Tensor> xb_out) {
+  return patch_embed_impl(img, t, w_pe, b_pe, cls, pos, temb, rng, site, p, patch, ln_st, xb_out, ColdSrc());
+}
+
+// patch_embed_fwd with the cold-diffusion batch draw fused into the patchify launch
+// (cold_batch + patch_embed_fwd in one launch fewer): `img` is the x_t buffer (its
+// shape drives the launch; written only if write_xt), `target`, `t` and `idx` are outputs
+// (idx is an input when !draw_idx).  Same values as ops.cold_batch followed by
+// patch_embed_fwd on its x_t.
+std::tuple<Tensor, Tensor> patch_embed_cold_fwd(Tensor pool, int64_t data_site, int64_t max_t, bool draw_idx,
+                                                bool target_x0, Tensor img, Tensor target, Tensor t, Tensor idx,
+                                                bool write_xt, Tensor w_pe, Tensor b_pe, Tensor cls, Tensor pos,
+                                                Tensor temb, Tensor rng, int64_t site, double p, int64_t patch,
+                                                c10::optional<Tensor> ln_st, c10::optional<Tensor> xb_out) {
+  CHECK_IN(pool, F32); CHECK_IN(img, F32); CHECK_IN(target, F32); CHECK_IN(t, I64); CHECK_IN(idx, I64);
+  const int B = img.size(0), C = img.size(1), H = img.size(2), W = img.size(3);
+  TORCH_CHECK(pool.dim() == 4 && pool.size(1) == C && pool.size(2) == H && pool.size(3) == W, "pool shape");
+  TORCH_CHECK(target.sizes() == img.sizes() && t.numel() == B && idx.numel() == B, "cold patch-embed shapes");
+  TORCH_CHECK(max_t >= 1 && (1 << max_t) <= W && (1 << max_t) <= H, "max_t");
+  ColdSrc cs;
+  cs.pool = pool.data_ptr<float>();
+  cs.pool_n = pool.size(0);
+  cs.site = data_site;
+  cs.max_t = max_t;
+  cs.draw_idx = draw_idx;
+  cs.target_x0 = target_x0;
+  cs.idx = idx.data_ptr<int64_t>();
+  cs.t_out = t.data_ptr<int64_t>();
+  cs.target = target.data_ptr<float>();
+  cs.x_t = write_xt ? img.data_ptr<float>() : nullptr;
+  return patch_embed_impl(img, t, w_pe, b_pe, cls, pos, temb, rng, site, p, patch, ln_st, xb_out, cs);
 }
 
 std::tuple<Tensor, Tensor, Tensor> layernorm_fwd(Tensor x, Tensor gamma, Tensor beta, double eps) {
@@ -879,10 +915,15 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("pixelate_pair(Tensor img, Tensor? idx, Tensor t, int B) -> (Tensor, Tensor)");
   m.def("cold_batch(Tensor pool, Tensor rng, int site, Tensor(a!) x_t, Tensor(b!) x_tm1, Tensor(c!) t, "
         "Tensor(d!) idx_ws, int max_t, bool draw_idx=True) -> ()");
+  m.def("patch_embed_cold_fwd(Tensor pool, int data_site, int max_t, bool draw_idx, bool target_x0, "
+        "Tensor(a!) img, Tensor(b!) target, Tensor(c!) t, Tensor(d!) idx, bool write_xt, Tensor w_pe, Tensor b_pe, "
+        "Tensor cls, Tensor pos, Tensor temb, Tensor rng, int site, float p, int patch, Tensor(e!)? ln_st=None, "
+        "Tensor(f!)? xb_out=None) -> (Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("patch_embed_fwd", &patch_embed_fwd);
+  m.impl("patch_embed_cold_fwd", &patch_embed_cold_fwd);
   m.impl("layernorm_fwd", &layernorm_fwd);
   m.impl("qkv_fwd", &qkv_fwd);
   m.impl("attn_fwd", &attn_fwd);

@@ -130,4 +130,27 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
 
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
+// Cold-diffusion pixelation (diffusion_loader.py:79-83, NEAREST down to W/f then
+// NEAREST back up): source row/column of output pixel y.
+// torch 'nearest' index: min(floor(dst * in/out), in-1)
+__device__ __forceinline__ int nearest_src(int dst, int in, int out) {
+  const float scale = (float)in / (float)out;
+  const int s = (int)floorf((float)dst * scale);
+  return s < in - 1 ? s : in - 1;
+}
+__device__ __forceinline__ int pix_src(int y, int H, int f) {
+  int ts = H / f;
+  if (ts < 1) ts = 1;
+  return nearest_src(nearest_src(y, ts, H), H, ts);
+}
+
+// Per-sample cold-batch draw (pool index, t in 1..max_t) from the data site's
+// counter hash: cold_batch_kernel and the fused cold patchify derive the same pair.
+__device__ __forceinline__ int cold_draw_idx(uint32_t salt, int b, int pool_n) {
+  return (int)(mix32(((uint32_t)(2 * b) * 0x9E3779B1u) ^ salt) % (uint32_t)pool_n);
+}
+__device__ __forceinline__ int cold_draw_t(uint32_t salt, int b, int max_t) {
+  return 1 + (int)(mix32(((uint32_t)(2 * b + 1) * 0x9E3779B1u) ^ salt) % (uint32_t)max_t);
+}
+
 }  // namespace dc

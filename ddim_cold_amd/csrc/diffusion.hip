@@ -57,17 +57,6 @@ __global__ __launch_bounds__(256) void q_sample_kernel(const float* __restrict__
   }
 }
 
-// torch 'nearest' index: min(floor(dst * in/out), in-1)
-__device__ __forceinline__ int nearest_src(int dst, int in, int out) {
-  const float scale = (float)in / (float)out;
-  const int s = (int)floorf((float)dst * scale);
-  return s < in - 1 ? s : in - 1;
-}
-__device__ __forceinline__ int pix_src(int y, int H, int f) {
-  int ts = H / f;
-  if (ts < 1) ts = 1;
-  return nearest_src(nearest_src(y, ts, H), H, ts);
-}
 
 __global__ __launch_bounds__(256) void pixelate_pair_kernel(const float* __restrict__ img, const int64_t* __restrict__ idx,
                                                             const int64_t* __restrict__ t, float* __restrict__ xt,

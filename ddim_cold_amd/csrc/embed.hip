@@ -25,16 +25,27 @@ __global__ __launch_bounds__(256) void patchify_cls_kernel(const float* __restri
                                                            float* __restrict__ x, int B, int C, int H, int W, int P,
                                                            int D, const int64_t* __restrict__ rng, int site,
                                                            uint32_t thr, float dsc, float* __restrict__ st,
-                                                           bf16* __restrict__ xb, int patch_blocks) {
+                                                           bf16* __restrict__ xb, int patch_blocks, ColdSrc cs) {
   const int Hp = H / P, Wp = W / P, NP = Hp * Wp, F = C * P * P, N = NP + 1;
+  const uint32_t csalt = cs.pool ? site_salt(rng, cs.site) : 0u;
   if ((int)blockIdx.x >= patch_blocks) {
     // cls row of sample b
     const int b = blockIdx.x - patch_blocks;
     const size_t row = (size_t)b * N;
     const uint32_t salt = thr ? site_salt(rng, site) : 0u;
+    int64_t tb;
+    if (cs.pool) {  // this block owns sample b's draw: publish (t, pool index) for the model
+      tb = cold_draw_t(csalt, b, cs.max_t);
+      if (threadIdx.x == 0) {
+        cs.t_out[b] = tb;
+        if (cs.draw_idx) cs.idx[b] = cold_draw_idx(csalt, b, cs.pool_n);
+      }
+    } else {
+      tb = t[b];
+    }
     float s = 0.f, q = 0.f;
     for (int d = threadIdx.x; d < D; d += 256) {
-      float v = cls[d] + pos[d] + temb[(size_t)t[b] * D + d];
+      float v = cls[d] + pos[d] + temb[(size_t)tb * D + d];
       const size_t idx = row * D + d;
       if (thr) v = dropout_keep(salt, (uint32_t)idx, thr) ? v * dsc : 0.f;
       x[idx] = v;
@@ -69,7 +80,23 @@ __global__ __launch_bounds__(256) void patchify_cls_kernel(const float* __restri
     const int b = (int)(row / NP), pidx = (int)(row % NP);
     const int hp = pidx / Wp, wp = pidx - hp * Wp;
     const int c = k / (P * P), ij = k - c * P * P, i = ij / P, j = ij - i * P;
-    patches[e] = f2bf(img[(((size_t)b * C + c) * H + hp * P + i) * W + wp * P + j]);
+    const int y = hp * P + i, xx = wp * P + j;
+    if (cs.pool) {
+      // cold batch fused in: pixelate the pool image straight into the patch row
+      // (x_t) and write the target image (x_{t-1}, or x0) -- same values as
+      // cold_batch_kernel + this kernel's image path, one launch fewer
+      const int src = cs.draw_idx ? cold_draw_idx(csalt, b, cs.pool_n) : (int)cs.idx[b];
+      const int tt = cold_draw_t(csalt, b, cs.max_t);
+      const float* im = cs.pool + ((size_t)src * C + c) * H * W;
+      const int f1 = 1 << tt, f0 = cs.target_x0 ? 1 : 1 << (tt - 1);
+      const float xt = im[(size_t)pix_src(y, H, f1) * W + pix_src(xx, W, f1)];
+      const size_t o = (((size_t)b * C + c) * H + y) * W + xx;
+      cs.target[o] = cs.target_x0 ? im[(size_t)y * W + xx] : im[(size_t)pix_src(y, H, f0) * W + pix_src(xx, W, f0)];
+      if (cs.x_t) cs.x_t[o] = xt;
+      patches[e] = f2bf(xt);
+    } else {
+      patches[e] = f2bf(img[(((size_t)b * C + c) * H + y) * W + xx]);
+    }
   }
 }
 
@@ -208,14 +235,14 @@ using namespace dc;
 
 void patchify_cls_launch(const float* img, const int64_t* t, const float* cls, const float* pos, const float* temb,
                          void* patches, float* x, int B, int C, int H, int W, int patch, int D, const int64_t* rng,
-                         int site, double p, float* st, void* xb, hipStream_t stream) {
+                         int site, double p, float* st, void* xb, hipStream_t stream, ColdSrc cs) {
   const size_t n = (size_t)B * (H / patch) * (W / patch) * C * patch * patch;
   const uint32_t thr = drop_threshold_host(p);
   const float dsc = p > 0 ? 1.f / (1.f - (float)p) : 1.f;
   const int pb = grid_for(n);
   hipLaunchKernelGGL(patchify_cls_kernel, dim3(pb + B), dim3(256), 0, stream, img, t, cls, pos, temb,
                      reinterpret_cast<bf16*>(patches), x, B, C, H, W, patch, D, rng, site, thr, dsc, st,
-                     reinterpret_cast<bf16*>(xb), pb);
+                     reinterpret_cast<bf16*>(xb), pb, cs);
 }
 
 void embed_bwd_launch(const float* g, const int64_t* t, float* dcls, float* dpos, float* dtemb, void* gpatch, int B,

@@ -152,9 +152,22 @@ void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const flo
                      double p, hipStream_t stream);
 
 // Embedding / head / loss (embed.hip)
+// Optional cold-diffusion batch source fused into patchify (pool != nullptr): the
+// patch rows are pixelated straight from the pool (cold_batch_kernel's draw), the
+// target image and (t, pool index) are written by the same launch; `img` is unused.
+struct ColdSrc {
+  const float* pool = nullptr;
+  int pool_n = 0, site = 0, max_t = 1;
+  bool draw_idx = true, target_x0 = false;
+  int64_t* idx = nullptr;    // [B] pool indices (written if draw_idx, else read)
+  int64_t* t_out = nullptr;  // [B] t (== the `t` the GEMM epilogue reads)
+  float* target = nullptr;   // [B,C,H,W] x_{t-1} (or x0)
+  float* x_t = nullptr;      // optional [B,C,H,W] x_t image
+};
 void patchify_cls_launch(const float* img, const int64_t* t, const float* cls, const float* pos,
                          const float* temb, void* patches, float* x, int B, int C, int H, int W, int patch,
-                         int D, const int64_t* rng, int site, double p, float* st, void* xb, hipStream_t stream);
+                         int D, const int64_t* rng, int site, double p, float* st, void* xb, hipStream_t stream,
+                         ColdSrc cs = ColdSrc());
 void embed_bwd_launch(const float* g, const int64_t* t, float* dcls, float* dpos, float* dtemb, void* gpatch,
                       int B, int N, int D, const int64_t* rng, int site, double p, hipStream_t stream);
 // returns the number of per-block loss partials written; finish = false leaves

@@ -63,6 +63,13 @@ class ColdBatcher:
         self.rng = rng
         self.target = target
 
+    def fused_spec(self):
+        """Deferred form for a consumer that fuses the draw into its patch embedding
+        (:func:`ops.patch_embed_cold_fwd`): ``((x_t, target, t), cold)`` without launching
+        anything; x_t is not materialised (the patch rows are pixelated from the pool)."""
+        cold = (self.pool, SITE_DATA, self.max_t, self.draw, self.target == "x0", self.x_tm1, self.idx, False)
+        return (self.x_t, self.x_tm1, self.t), cold
+
     def __call__(self):
         ops.cold_batch(self.pool, self.rng, SITE_DATA, self.x_t, self.x_tm1, self.t, self.idx, self.max_t,
                        self.draw)

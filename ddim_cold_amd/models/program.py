@@ -271,16 +271,18 @@ class ViTProgram:
 
     # ------------------------------------------------------------------ forward
     def forward(self, P: ModelTensors, img: torch.Tensor, t: torch.Tensor, rng: torch.Tensor, training: bool,
-                save: bool = True, head_step=None, loss=None):
+                save: bool = True, head_step=None, loss=None, cold=None):
         """``head_step = (mode, x0_out, coef)`` fuses the sampler update into the head
         GEMM (``ops.head_step_``): ``img`` (the current x_t) is updated in place and
         returned; mode 1 = DDIM step, mode 2 = clamp (cold sampler).  ``loss =
         (target, beta)`` (LayerNorm-folded program only, see :meth:`supports_fused_loss`)
-        returns ``(loss_parts, dtok)`` from :func:`ops.head_loss` instead of the image."""
+        returns ``(loss_parts, dtok)`` from :func:`ops.head_loss` instead of the image.
+        ``cold`` (LayerNorm-folded program only): the cold batch draw fused into the
+        patch embedding (:func:`ops.patch_embed_cold_fwd`); ``img``/``t`` are its outputs."""
         if P.folded and fold_width_ok(self.cfg.dim):
-            return self._forward_folded(P, img, t, rng, training, save, head_step, loss)
-        if loss is not None:
-            raise ValueError("the fused head loss needs the LayerNorm-folded program")
+            return self._forward_folded(P, img, t, rng, training, save, head_step, loss, cold)
+        if loss is not None or cold is not None:
+            raise ValueError("the fused head loss / cold batch need the LayerNorm-folded program")
         c = self.cfg
         B = img.shape[0]
         N, D, M = c.tokens, c.dim, B * c.tokens
@@ -332,7 +334,8 @@ class ViTProgram:
             S.xL, S.lf, S.mf, S.rf = x, lf, mf, rf
         return out, S
 
-    def _forward_folded(self, P: ModelTensors, img, t, rng, training: bool, save: bool, head_step, loss=None):
+    def _forward_folded(self, P: ModelTensors, img, t, rng, training: bool, save: bool, head_step, loss=None,
+                        cold=None):
         """Forward with every LayerNorm folded into its consumer GEMM: 5 launches
         per block (QKV, attention, proj+residual, fc1+GELU, fc2+residual).  The
         residual GEMMs (and the patch embedding) emit each new residual row's
@@ -351,8 +354,12 @@ class ViTProgram:
         # each slot written once by the producing epilogue
         st = torch.empty(2 * L + 1, M, D // 32, 2, dtype=torch.float32, device=dev)
         xb = torch.empty(M, D, dtype=ACT_DTYPE, device=dev)
-        x, patches = ops.patch_embed_fwd(img, t, P.pe_w, P.pe_b, P.cls, P.pos, P.temb, rng, SITE_EMBED, pd,
-                                         c.patch, ln_st=st[0], xb_out=xb)
+        if cold is not None:
+            x, patches = ops.patch_embed_cold_fwd(cold, img, t, P.pe_w, P.pe_b, P.cls, P.pos, P.temb, rng,
+                                                  SITE_EMBED, pd, c.patch, ln_st=st[0], xb_out=xb)
+        else:
+            x, patches = ops.patch_embed_fwd(img, t, P.pe_w, P.pe_b, P.cls, P.pos, P.temb, rng, SITE_EMBED, pd,
+                                             c.patch, ln_st=st[0], xb_out=xb)
         x = x.view(M, D)
         S = Saved(t=t, patches=patches) if save else None
 

@@ -21,7 +21,7 @@ __all__ = [
     "linear_residual_fwd", "linear_gelu_fwd", "head_fwd", "smooth_l1_fwd_bwd", "img_to_tokgrad",
     "linear_dgrad", "linear_dgrad_gelu", "linear_wgrad", "layernorm_bwd", "attn_bwd", "embed_bwd",
     "sqnorm", "adamw_step", "advance_counters", "ddim_step", "ddim_step_", "randn_", "q_sample",
-    "pixelate_pair", "cold_batch", "ln_fold_",
+    "pixelate_pair", "cold_batch", "patch_embed_cold_fwd", "ln_fold_",
 ]
 
 
@@ -46,6 +46,24 @@ def patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site: int, p: float
     if _hip(img):
         return _ops().patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site, float(p), patch, ln_st, xb_out)
     return ref.patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site, p, patch, ln_st, xb_out)
+
+
+def patch_embed_cold_fwd(cold, img, t, w_pe, b_pe, cls, pos, temb, rng, site: int, p: float, patch: int,
+                         ln_st=None, xb_out=None):
+    """:func:`cold_batch` fused into :func:`patch_embed_fwd` (one launch fewer per
+    training step): ``cold = (pool, data_site, max_t, draw_idx, target_x0, target,
+    idx, write_xt)``; the patch rows are pixelated straight from the pool, ``target``,
+    ``t`` and (if ``draw_idx``) ``idx`` are written, ``img`` (x_t) only if ``write_xt``.
+    Same values as ``cold_batch`` then ``patch_embed_fwd``."""
+    pool, dsite, max_t, draw, tx0, target, idx, write_xt = cold
+    if _hip(img):
+        return _ops().patch_embed_cold_fwd(pool, int(dsite), int(max_t), bool(draw), bool(tx0), img, target, t, idx,
+                                           bool(write_xt), w_pe, b_pe, cls, pos, temb, rng, site, float(p), patch,
+                                           ln_st, xb_out)
+    cold_batch(pool, rng, dsite, img, target, t, idx, max_t, draw)
+    if tx0:
+        torch.index_select(pool, 0, idx, out=target)
+    return patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site, p, patch, ln_st, xb_out)
 
 
 def layernorm_fwd(x, gamma, beta, eps: float = 1e-5):

@@ -33,6 +33,7 @@ AdamW step, cosine LR step, zero_grad) re-designed for a latency-bound
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Tuple
 
@@ -98,6 +99,11 @@ class EngineConfig:
     # pack/unpack as two fused kernels).  torch.distributed stays the control
     # plane (rendezvous, barriers, metrics) either way.
     comm: str = "torch"
+    # a batch source with ``fused_spec()`` (data.synthetic.ColdBatcher) has its draw
+    # fused into the patch-embedding launch (ops.patch_embed_cold_fwd: the patch rows
+    # pixelated straight from the pool, x_t never materialised): one launch fewer
+    # per step, identical values.  DDIM_COLD_FUSE_BATCH=0 turns it off.
+    fuse_batch: bool = os.environ.get("DDIM_COLD_FUSE_BATCH", "1") != "0"
 
 
 def _align(n: int) -> int:
@@ -287,11 +293,17 @@ class TrainEngine:
             last = micro == k_acc - 1
             if micro > 0:
                 self.rng[1:].add_(1)  # fresh dropout masks and batch draws per micro-batch
-            img, tgt, t = self.batch_fn()
-            if tail and self.prog.supports_fused_loss(self.param_tensors):
+            fused_loss = tail and self.prog.supports_fused_loss(self.param_tensors)
+            spec = getattr(self.batch_fn, "fused_spec", None)
+            cold = None
+            if fused_loss and self.cfg.fuse_batch and spec is not None:
+                (img, tgt, t), cold = spec()  # drawn inside the patch-embedding launch
+            else:
+                img, tgt, t = self.batch_fn()
+            if fused_loss:
                 # head GEMM epilogue computes the loss partials and the token-layout gradient
                 (loss_parts, dtok), S = self.prog.forward(self.param_tensors, img, t, self.rng, True,
-                                                          loss=(tgt, self.cfg.loss_beta))
+                                                          loss=(tgt, self.cfg.loss_beta), cold=cold)
                 out = None
             else:
                 out, S = self.prog.forward(self.param_tensors, img, t, self.rng, True)

@@ -224,3 +224,24 @@ def test_reference_ksplit_dgrad_and_ln_partials():
     e, _ = ref.layernorm_bwd(parts.sum(0), x, mu, rs, g, None, z[2], z[3], 40, r, 0, 0.0, 0, 0.0, False)
     torch.testing.assert_close(a, e)
     torch.testing.assert_close(z[0], z[2])
+
+
+def test_engine_fused_cold_batch_matches_unfused_cpu():
+    """ColdBatcher.fused_spec path (draw fused into the patch embedding) == the plain batch_fn path."""
+    from ddim_cold_amd.data.synthetic import ColdBatcher, synthetic_pool
+
+    def run(fuse):
+        model = _model()
+        eng = TrainEngine(model, EngineConfig(lr=1e-3, t_max=10, use_graph=False, seed=5, fuse_batch=fuse))
+        bat = ColdBatcher(synthetic_pool(16, size=(16, 16), seed=1), 4, eng.rng)
+        calls = []
+        if fuse:
+            spec = bat.fused_spec
+            bat.fused_spec = lambda: (calls.append(1), spec())[1]
+        eng.set_batch_fn(bat)
+        losses = [float(eng.train_step()) for _ in range(3)]
+        return eng.flat_p.clone(), losses, len(calls), bat.t.clone(), bat.x_tm1.clone()
+    pf, lf, nf, tf, yf = run(True)
+    pu, lu, _, tu, yu = run(False)
+    assert nf == 3  # the fused path really ran
+    assert lf == lu and torch.equal(pf, pu) and torch.equal(tf, tu) and torch.equal(yf, yu)

@@ -31,3 +31,59 @@ def test_graph_step_matches_eager(grad_accum):
     # AdamW turns last-bit differences of near-zero grads (fp32 atomics) into <= 2*lr per step
     assert (pg - pe).abs().max().item() <= 2 * 1e-3 * 5
     assert int(eng.rng[1]) == 5 * grad_accum and int(eng.step_ctr[0]) == 5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("target", ["prev", "x0"])
+@pytest.mark.parametrize("draw", [True, False])
+def test_patch_embed_cold_matches_cold_batch_then_embed(target, draw):
+    """ops.patch_embed_cold_fwd (batch draw fused into the patchify launch) == cold_batch
+    followed by patch_embed_fwd, bit for bit (tokens, patch rows, target, t, idx, LN stats)."""
+    from ddim_cold_amd import ops
+    from ddim_cold_amd.data.synthetic import SITE_DATA
+    from ddim_cold_amd.models.program import SITE_EMBED
+    torch.manual_seed(0)
+    model = build_model("vit_tiny").cuda().train()
+    B, D = 8, model.embed_dim
+    N = model.patch_embed.num_patches + 1
+    pool = synthetic_pool(32, seed=2, device="cuda")
+    rng = torch.tensor([11, 5], dtype=torch.int64, device="cuda")
+    idx0 = torch.randint(0, 32, (B,), device="cuda")
+    pe_w = model.patch_embed.proj.weight.detach().reshape(D, -1).to(torch.bfloat16).contiguous()
+    args = (pe_w, model.patch_embed.proj.bias.detach(), model.cls_token.detach(), model.pos_embed.detach(),
+            model.time_embed.weight.detach(), rng, SITE_EMBED, 0.1, model.patch_size)
+
+    def bufs():
+        return (torch.empty(B, 3, 64, 64, device="cuda"), torch.empty(B, 3, 64, 64, device="cuda"),
+                torch.empty(B, dtype=torch.int64, device="cuda"), idx0.clone(),
+                torch.empty(B * N, D // 32, 2, device="cuda"), torch.empty(B * N, D, dtype=torch.bfloat16, device="cuda"))
+
+    xt, tg, t, idx, st, xb = bufs()
+    ops.cold_batch(pool, rng, SITE_DATA, xt, tg, t, idx, 6, draw)
+    if target == "x0":
+        torch.index_select(pool, 0, idx, out=tg)
+    x_ref, p_ref = ops.patch_embed_fwd(xt, t, *args, ln_st=st, xb_out=xb)
+    xt2, tg2, t2, idx2, st2, xb2 = bufs()
+    cold = (pool, SITE_DATA, 6, draw, target == "x0", tg2, idx2, True)
+    x, p = ops.patch_embed_cold_fwd(cold, xt2, t2, *args, ln_st=st2, xb_out=xb2)
+    torch.cuda.synchronize()
+    assert torch.equal(t2, t) and torch.equal(idx2, idx)
+    assert torch.equal(xt2, xt) and torch.equal(tg2, tg)
+    assert torch.equal(p, p_ref) and torch.equal(x, x_ref) and torch.equal(xb2, xb) and torch.equal(st2, st)
+
+
+@pytest.mark.gpu
+def test_engine_fused_batch_matches_unfused():
+    def run(fuse):
+        torch.manual_seed(0)
+        model = build_model("vit_tiny").cuda().train()
+        eng = TrainEngine(model, EngineConfig(lr=1e-3, t_max=100, seed=3, use_graph=True, graph_warmup=1,
+                                              temb_rows=7, fuse_batch=fuse))
+        eng.set_batch_fn(ColdBatcher(synthetic_pool(64, seed=1, device="cuda"), 8, eng.rng))
+        losses = [float(eng.train_step()) for _ in range(4)]
+        torch.cuda.synchronize()
+        return eng.flat_p.clone(), losses
+    pf, lf = run(True)
+    pu, lu = run(False)
+    assert all(abs(a - b) <= 1e-4 * abs(b) for a, b in zip(lf, lu)), (lf, lu)
+    assert (pf - pu).abs().max().item() <= 2 * 1e-3 * 4
