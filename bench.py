@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--model", default="vit_tiny")
     ap.add_argument("--batch", type=int, default=32, help="per-GPU batch (yaml batch_size 16 x2 for AMP)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--graph-steps", type=int, default=4,
+                    help="optimizer steps per hipGraph replay (TrainEngine.train_steps; every step fully executed)")
     ap.add_argument("--bucket-blocks", type=int, default=2)
     ap.add_argument("--no-sampler", action="store_true")
     ap.add_argument("--wgrad-stream", action="store_true")
@@ -95,21 +97,19 @@ def main():
                        wgrad_stream=args.wgrad_stream,
                        temb_rows=int(math.log2(model.img_size[1])) + 1,  # cold t in 1..log2(W)
                        graph_comm=not args.segmented_comm, grad_wire=args.grad_wire,
-                       comm=args.comm)
+                       comm=args.comm, graph_steps=args.graph_steps)
     engine = TrainEngine(model, cfg, device=dev)
     pool = synthetic_pool(1024, tuple(model.img_size), seed=7 + rank, device=dev)
     engine.set_batch_fn(ColdBatcher(pool, args.batch, engine.rng))
 
-    for _ in range(args.warmup):
-        engine.train_step()
+    engine.train_steps(args.warmup)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        engine.train_step()
+    engine.train_steps(args.steps)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     barrier()
@@ -173,7 +173,7 @@ def main():
                                 f"heads={model.blocks[0].attn.num_heads}, patch={model.patch_size}, "
                                 f"{model.img_size[0]}x{model.img_size[1]})", "global_batch": args.batch * n,
                        "per_gpu_batch": args.batch, "seq_len": model.num_tokens, "parallelism": f"dp{n}",
-                       "graph": not args.no_graph, "bucket_blocks": args.bucket_blocks,
+                       "graph": not args.no_graph, "graph_steps": args.graph_steps, "bucket_blocks": args.bucket_blocks,
                        "allreduce": ("none" if not engine.segmented else "eager" if dev.type != "cuda" else
                                      "segmented" if (args.segmented_comm or getattr(engine, "_graph_comm_failed", False))
                                      else "captured-in-graph"),

@@ -104,6 +104,11 @@ class EngineConfig:
     # pixelated straight from the pool, x_t never materialised): one launch fewer
     # per step, identical values.  DDIM_COLD_FUSE_BATCH=0 turns it off.
     fuse_batch: bool = os.environ.get("DDIM_COLD_FUSE_BATCH", "1") != "0"
+    # optimizer steps per hipGraph replay for train_steps(n) (one graph holding K
+    # complete steps, every counter on the device): the inter-replay dispatch gap
+    # (~8 us before each step's first kernel in the graph-mode trace) is paid once
+    # per K steps.  train_step() keeps replaying the one-step graph.
+    graph_steps: int = 1
 
 
 def _align(n: int) -> int:
@@ -144,6 +149,7 @@ class TrainEngine:
             from ..parallel.comm import NativeComm
             self.ncomm = NativeComm(dev)
         self._graphs: Optional[List[torch.cuda.CUDAGraph]] = None
+        self._multi = None  # (K-step graph, K) for train_steps
         self._eager_steps = 0
         self.batch_fn: Optional[Callable] = None
         self._segment_capture = False
@@ -278,6 +284,7 @@ class TrainEngine:
         """``fn() -> (x_t, target, t)`` device tensors; called inside the captured region."""
         self.batch_fn = fn
         self._graphs = None
+        self._multi = None
 
     def _join_side(self):
         if self.side is not None:
@@ -405,24 +412,32 @@ class TrainEngine:
                 torch.cuda.synchronize(self.device)
         self._capture_impl(graph_comm=False)
 
+    def _captured_step_body(self):
+        """One whole step issued on the capturing stream (collectives as graph nodes)."""
+        for kind, k in self._step_iter():
+            if kind == "bucket":
+                self._allreduce(k)
+                if k == len(self.buckets) - 1:
+                    self._join_comm()
+
     def _capture_impl(self, graph_comm: bool):
         pool = torch.cuda.graph_pool_handle()
         graphs = []
+        self._multi = None
         gen = self._step_iter()
         nseg = len(self.buckets) + 1 if (self.segmented and not graph_comm) else 1
         if nseg == 1:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool):
-                if self.segmented:  # graph_comm: the collectives become graph nodes
-                    for kind, k in gen:
-                        if kind == "bucket":
-                            self._allreduce(k)
-                            if k == len(self.buckets) - 1:
-                                self._join_comm()
-                else:
-                    for _ in gen:
-                        pass
+                self._captured_step_body()
             graphs.append(g)
+            K = max(1, int(self.cfg.graph_steps))
+            if K > 1:  # K steps in one graph, own memory pool
+                gm = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gm, pool=torch.cuda.graph_pool_handle()):
+                    for _ in range(K):
+                        self._captured_step_body()
+                self._multi = (gm, K)
         else:
             self._segment_capture = True
             try:
@@ -446,6 +461,23 @@ class TrainEngine:
             self._allreduce(k)
         self._join_comm()
         gs[nb].replay()
+
+    def train_steps(self, n: int):
+        """Run ``n`` optimizer steps (``batch_fn`` draws each step's batch on the device).
+        With ``graph_steps = K > 1`` every run of K steps is ONE replay of a K-step
+        graph; the remainder (and the eager warm-up) goes through :meth:`train_step`.
+        Returns the device loss tensor of the last step (no host sync)."""
+        done = 0
+        while done < n:
+            multi = getattr(self, "_multi", None)
+            if multi is not None and n - done >= multi[1]:
+                multi[0].replay()
+                self.steps_done += multi[1]
+                done += multi[1]
+            else:
+                self.train_step()
+                done += 1
+        return self.loss_last
 
     def train_step(self):
         """Run one optimizer step on the batch produced by ``batch_fn``.

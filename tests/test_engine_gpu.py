@@ -87,3 +87,23 @@ def test_engine_fused_batch_matches_unfused():
     pu, lu = run(False)
     assert all(abs(a - b) <= 1e-4 * abs(b) for a, b in zip(lf, lu)), (lf, lu)
     assert (pf - pu).abs().max().item() <= 2 * 1e-3 * 4
+
+
+@pytest.mark.gpu
+def test_multi_step_graph_matches_single_step_graph():
+    """train_steps with a 4-step graph == 9 single-step replays (every counter on the device)."""
+    def run(K):
+        torch.manual_seed(0)
+        model = build_model("vit_tiny").cuda().train()
+        eng = TrainEngine(model, EngineConfig(lr=1e-3, t_max=100, seed=3, use_graph=True, graph_warmup=1,
+                                              temb_rows=7, graph_steps=K))
+        eng.set_batch_fn(ColdBatcher(synthetic_pool(64, seed=1, device="cuda"), 8, eng.rng))
+        eng.train_steps(9)  # 1 eager + capture, then (K=4) two 4-step replays
+        torch.cuda.synchronize()
+        return eng.flat_p.clone(), float(eng.loss_ema), eng
+    pm, em, eng = run(4)
+    ps, es, _ = run(1)
+    assert eng._multi is not None and eng._multi[1] == 4 and eng.steps_done == 9
+    assert int(eng.step_ctr[0]) == 9 and int(eng.rng[1]) == 9
+    assert abs(em - es) <= 1e-4 * abs(es), (em, es)
+    assert (pm - ps).abs().max().item() <= 2 * 1e-3 * 9
