@@ -633,7 +633,8 @@ Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, double scale, Ten
   return dqkv;
 }
 
-Tensor embed_bwd(Tensor g, Tensor t, Tensor rng, int64_t site, double p, Tensor dcls, Tensor dpos, Tensor dtemb) {
+Tensor embed_bwd(Tensor g, Tensor t, Tensor rng, int64_t site, double p, Tensor dcls, Tensor dpos, Tensor dtemb,
+                 c10::optional<Tensor> ln_ws, c10::optional<Tensor> ln_ptrs, int64_t ln_C) {
   CHECK_IN(g, F32); CHECK_IN(t, I64); check_rng(rng); CHECK_IN(dcls, F32); CHECK_IN(dpos, F32); CHECK_IN(dtemb, F32);
   const c10::DeviceGuard guard(g.device());
   TORCH_CHECK(g.dim() == 3, "g must be [B,N,D]");
@@ -641,9 +642,21 @@ Tensor embed_bwd(Tensor g, Tensor t, Tensor rng, int64_t site, double p, Tensor 
   TORCH_CHECK(t.numel() == B && dcls.numel() == D && dpos.numel() == (int64_t)N * D && dtemb.size(-1) == D,
               "embed_bwd shapes");
   auto gpatch = at::empty({(int64_t)B * (N - 1), D}, g.options().dtype(BF16));
+  ReplicaFinal rf;
+  if (ln_ws.has_value() && ln_ws->defined()) {  // replica_reduce_ folded into this launch
+    CHECK_IN((*ln_ws), F32);
+    TORCH_CHECK(ln_ptrs.has_value() && ln_ptrs->defined(), "ln_ws needs ln_ptrs");
+    CHECK_IN((*ln_ptrs), I64);
+    rf.G = ln_ptrs->numel();
+    rf.R = ln_replicas();
+    rf.C = ln_C;
+    TORCH_CHECK(ln_C > 0 && ln_ws->numel() == (int64_t)rf.G * rf.R * ln_C, "replica ws shape");
+    rf.ws = ln_ws->data_ptr<float>();
+    rf.dsts = reinterpret_cast<float* const*>(ln_ptrs->data_ptr<int64_t>());
+  }
   embed_bwd_launch(g.data_ptr<float>(), t.data_ptr<int64_t>(), dcls.data_ptr<float>(), dpos.data_ptr<float>(),
                    dtemb.data_ptr<float>(), gpatch.data_ptr(), B, N, D, rng.data_ptr<int64_t>(), site, p,
-                   cur_stream());
+                   cur_stream(), rf);
   return gpatch;
 }
 
@@ -903,7 +916,7 @@ TORCH_LIBRARY(ddim_cold, m) {
         "float ema_decay=0.99, Tensor(f!)? step=None, Tensor(g!)? rng=None, Tensor? sq=None) -> ()");
   m.def("attn_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, float scale, Tensor rng, int site, float p) -> Tensor");
   m.def("embed_bwd(Tensor g, Tensor t, Tensor rng, int site, float p, Tensor(a!) dcls, Tensor(b!) dpos, "
-        "Tensor(c!) dtemb) -> Tensor");
+        "Tensor(c!) dtemb, Tensor(d!)? ln_ws=None, Tensor? ln_ptrs=None, int ln_C=0) -> Tensor");
   m.def("sqnorm(Tensor g, Tensor(a!) out, float scale) -> ()");
   m.def("adamw_step(Tensor(a!) p, Tensor(b!) g, Tensor(c!) m, Tensor(d!) v, Tensor(e!)? pbf, Tensor sq, "
         "Tensor step, Tensor hyper, float grad_scale) -> ()");

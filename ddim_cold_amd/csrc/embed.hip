@@ -105,7 +105,8 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const float* __restrict_
                                                         float* __restrict__ dcls, float* __restrict__ dpos,
                                                         float* __restrict__ dtemb, bf16* __restrict__ gpatch, int B,
                                                         int N, int D, const int64_t* __restrict__ rng, int site,
-                                                        uint32_t thr, float dsc, int blocksA, int blocksB) {
+                                                        uint32_t thr, float dsc, int blocksA, int blocksB,
+                                                        int blocksC, ReplicaFinal rf) {
   const uint32_t salt = thr ? site_salt(rng, site) : 0u;
   auto gm = [&](size_t idx) -> float {
     const float v = g[idx];
@@ -145,10 +146,23 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const float* __restrict_
     for (; n < N; ++n) s += gm(((size_t)b * N + n) * D + d);
     const int64_t tb = t[b];
     atomicAdd(dtemb + (size_t)tb * D + d, s);
+  } else if (bid >= blocksA + blocksB + blocksC) {
+    // part D: LayerNorm dgamma/dbeta replica finalize (replica_reduce_kernel's work;
+    // every LayerNorm backward has run before the embedding backward)
+    const int rb = bid - blocksA - blocksB - blocksC, cb = (rf.C + 255) / 256;
+    const int gi = rb / cb, c = (rb - gi * cb) * 256 + threadIdx.x;
+    if (c >= rf.C) return;
+    float* w = rf.ws + (size_t)gi * rf.R * rf.C + c;
+    float s = 0.f;
+    for (int r = 0; r < rf.R; ++r) {
+      s += w[(size_t)r * rf.C];
+      w[(size_t)r * rf.C] = 0.f;
+    }
+    rf.dsts[gi][c] += s;
   } else {
     const size_t total = (size_t)B * (N - 1) * D;
     for (size_t e = (size_t)(bid - blocksA - blocksB) * 256 + threadIdx.x; e < total;
-         e += (size_t)(gridDim.x - blocksA - blocksB) * 256) {
+         e += (size_t)blocksC * 256) {
       const size_t row = e / D;
       const int d = (int)(e - row * D);
       const int b = (int)(row / (N - 1)), i = (int)(row % (N - 1));
@@ -246,13 +260,15 @@ void patchify_cls_launch(const float* img, const int64_t* t, const float* cls, c
 }
 
 void embed_bwd_launch(const float* g, const int64_t* t, float* dcls, float* dpos, float* dtemb, void* gpatch, int B,
-                      int N, int D, const int64_t* rng, int site, double p, hipStream_t stream) {
+                      int N, int D, const int64_t* rng, int site, double p, hipStream_t stream, ReplicaFinal rf) {
   const int blocksA = cdiv(N * D, 256), blocksB = cdiv(B * D, 256);
   const int blocksC = grid_for((size_t)B * (N - 1) * D);
+  const int blocksD = rf.ws ? rf.G * cdiv(rf.C, 256) : 0;
   const uint32_t thr = drop_threshold_host(p);
   const float dsc = p > 0 ? 1.f / (1.f - (float)p) : 1.f;
-  hipLaunchKernelGGL(embed_bwd_kernel, dim3(blocksA + blocksB + blocksC), dim3(256), 0, stream, g, t, dcls, dpos,
-                     dtemb, reinterpret_cast<bf16*>(gpatch), B, N, D, rng, site, thr, dsc, blocksA, blocksB);
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3(blocksA + blocksB + blocksC + blocksD), dim3(256), 0, stream, g, t, dcls,
+                     dpos, dtemb, reinterpret_cast<bf16*>(gpatch), B, N, D, rng, site, thr, dsc, blocksA, blocksB,
+                     blocksC, rf);
 }
 
 int smooth_l1_launch(const float* pred, const float* target, float* loss, float* partials, void* dtok, int B,

@@ -168,8 +168,14 @@ void patchify_cls_launch(const float* img, const int64_t* t, const float* cls, c
                          const float* temb, void* patches, float* x, int B, int C, int H, int W, int patch,
                          int D, const int64_t* rng, int site, double p, float* st, void* xb, hipStream_t stream,
                          ColdSrc cs = ColdSrc());
+// optional LayerNorm replica finalize carried by the embedding-backward launch
+struct ReplicaFinal {
+  float* ws = nullptr;          // [G][R][C] replicas (re-zeroed)
+  float* const* dsts = nullptr; // [G] device pointers to the [C] grad ranges (+=)
+  int G = 0, R = 0, C = 0;
+};
 void embed_bwd_launch(const float* g, const int64_t* t, float* dcls, float* dpos, float* dtemb, void* gpatch,
-                      int B, int N, int D, const int64_t* rng, int site, double p, hipStream_t stream);
+                      int B, int N, int D, const int64_t* rng, int site, double p, hipStream_t stream, ReplicaFinal rf = ReplicaFinal());
 // returns the number of per-block loss partials written; finish = false leaves
 // summing them (loss, loss_last, EMA) to a later kernel (the step tail of ln_fold)
 int smooth_l1_launch(const float* pred, const float* target, float* loss, float* partials, void* dtok, int B,

@@ -414,7 +414,7 @@ class ViTProgram:
     def backward_iter(self, P: ModelTensors, G: ModelTensors, S: Saved, dtok: torch.Tensor, rng: torch.Tensor,
                       training: bool = True, wgrad: Optional[Callable] = None,
                       ln_ws: Optional[torch.Tensor] = None, wgrad_stream=None,
-                      embed_with_block0: bool = False) -> Iterator[int]:
+                      embed_with_block0: bool = False, ln_final=None) -> Iterator[int]:
         """Hand-written backward; yields the block index after each block's grads
         are issued (L-1 first, then ..., 0) and -1 after the embedding grads.
 
@@ -489,11 +489,11 @@ class ViTProgram:
             wgrad(dqkv, l1, bg.qkv_w, bg.qkv_b)
             keep.append((gy1, du, dqkv, l1, l2))
             if i == 0 and embed_with_block0:
-                gpatch = self._embed_backward(P, G, S, g, rng, pd, wgrad)
+                gpatch = self._embed_backward(P, G, S, g, rng, pd, wgrad, ln_final)
             flush()
             yield i
         if not embed_with_block0:
-            gpatch = self._embed_backward(P, G, S, g, rng, pd, wgrad)
+            gpatch = self._embed_backward(P, G, S, g, rng, pd, wgrad, ln_final)
             flush()
         keep.append((gpatch, lf))
         if batch is not None:
@@ -501,12 +501,13 @@ class ViTProgram:
         self._keep = keep  # holds side-stream operands alive until the caller joins
         yield -1
 
-    def _embed_backward(self, P, G, S, g, rng, pd, wgrad):
+    def _embed_backward(self, P, G, S, g, rng, pd, wgrad, ln_final=None):
         """cls / pos / time-embedding gradients and the patch-embedding weight gradient (queued)."""
         c = self.cfg
         B = S.t.shape[0]
         temb_g = G.temb if G.temb is not None else torch.zeros_like(P.temb)
-        gpatch = ops.embed_bwd(g.view(B, c.tokens, c.dim), S.t, rng, SITE_EMBED, pd, G.cls, G.pos, temb_g)
+        gpatch = ops.embed_bwd(g.view(B, c.tokens, c.dim), S.t, rng, SITE_EMBED, pd, G.cls, G.pos, temb_g,
+                               ln_final=ln_final)
         wgrad(gpatch, S.patches, G.pe_w, G.pe_b)
         return gpatch
 

@@ -354,9 +354,14 @@ def attn_bwd(do, qkv, o, lse, scale: float, rng, site: int, p: float):
     return ref.attn_bwd(do, qkv, o, lse, scale, rng, site, p)
 
 
-def embed_bwd(g, t, rng, site: int, p: float, dcls, dpos, dtemb):
+def embed_bwd(g, t, rng, site: int, p: float, dcls, dpos, dtemb, ln_final=None):
+    """``ln_final = (ws, dst_ptrs, C)``: the LayerNorm replica finalize
+    (:func:`replica_reduce_`) rides in the same launch (GPU only)."""
     if _hip(g):
-        return _ops().embed_bwd(g, t, rng, site, float(p), dcls, dpos, dtemb)
+        ws, ptrs, C = ln_final if ln_final is not None else (None, None, 0)
+        return _ops().embed_bwd(g, t, rng, site, float(p), dcls, dpos, dtemb, ws, ptrs, int(C))
+    if ln_final is not None:
+        raise ValueError("ln_final needs the HIP extension (use replica_reduce_ on CPU)")
     return ref.embed_bwd(g, t, rng, site, p, dcls, dpos, dtemb)
 
 

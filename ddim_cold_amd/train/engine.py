@@ -327,10 +327,18 @@ class TrainEngine:
             # without a separate embedding bucket (single process) the patch-embedding
             # weight gradient joins block 0's grouped launch
             merge = not (self.segmented and self.cfg.embed_bucket)
+            # single process: the LayerNorm replica finalize rides in the embedding-backward launch
+            ln_final = None
+            if not self.segmented and self.ln_ptrs is not None and os.environ.get("DDIM_COLD_FUSE_LNFINAL", "1") != "0":
+                hi = self.ln_done_at[-1]
+                ln_final = (self.ln_ws[:hi], self.ln_ptrs[:hi], 2 * c.dim)
             for i in self.prog.backward_iter(self.param_tensors, self.grad_tensors, S, dtok, self.rng, True,
-                                             ln_ws=self.ln_ws, wgrad_stream=self.side, embed_with_block0=merge):
+                                             ln_ws=self.ln_ws, wgrad_stream=self.side, embed_with_block0=merge,
+                                             ln_final=ln_final):
                 if i in self.bucket_after and (self.segmented or i == -1):
                     hi = self.ln_done_at[i]
+                    if ln_final is not None:
+                        ln_lo = hi  # already finalized by the embedding backward
                     if hi > ln_lo:
                         ops.replica_reduce_(self.ln_ws[ln_lo:hi],
                                             None if self.ln_ptrs is None else self.ln_ptrs[ln_lo:hi],
