@@ -10,7 +10,8 @@ Reference (multi_gpu_trainer.py:71-80, 94-106, 152-163):
 All written with ``torch.save``; optimizer / scheduler entries are standard
 ``torch.optim.AdamW`` / ``CosineAnnealingLR`` state dicts so files move freely
 between this framework and the reference.  Extra keys we add (ignored by the
-reference): ``'rng'`` (device RNG seed/step), ``'engine_steps'``, ``'scaler'`` (GradScaler
+reference): ``'rng'`` (device RNG seed/step; a resume restores only the
+step, each rank keeps its own seed), ``'engine_steps'``, ``'scaler'`` (GradScaler
 layout, scale 1: bf16 training needs no loss scaling).
 
 Loading uses ``weights_only=True`` (no arbitrary unpickling).
@@ -90,7 +91,10 @@ def load_lastepoch(path: str, model, engine) -> dict:
         if ckpt.get("scheduler"):
             engine.load_scheduler_state_dict(ckpt["scheduler"])
         if ckpt.get("rng") is not None:
-            engine.rng.copy_(ckpt["rng"].to(engine.rng.device))
+            # only the step counter: lastepoch.pkl is written by rank 0, and every
+            # rank keeps its own seed (cfg.seed * 1000 + rank) so the ranks' cold
+            # timesteps / dropout masks stay independent after a resume
+            engine.rng[1:].copy_(ckpt["rng"][1:].to(engine.rng.device))
     return ckpt
 
 

@@ -294,8 +294,11 @@ class TrainEngine:
         c = self.prog.cfg
         k_acc = max(1, int(self.cfg.grad_accum))
         # loss bookkeeping + counter advance ride in the LayerNorm-fold launch after
-        # the optimizer (one workgroup of it) instead of two extra tiny launches
-        tail = self.lnfold is not None and k_acc == 1
+        # the optimizer (one workgroup of it) instead of two extra tiny launches.
+        # With grad_accum > 1 the micro-batch loss partials are averaged first, so the
+        # EMA moves once per optimizer step (multi_gpu_trainer.py:126 semantics).
+        tail = self.lnfold is not None
+        loss_acc = None
         for micro in range(k_acc):
             last = micro == k_acc - 1
             if micro > 0:
@@ -316,13 +319,16 @@ class TrainEngine:
                 out, S = self.prog.forward(self.param_tensors, img, t, self.rng, True)
             if out is None:
                 pass
-            elif tail:
+            elif tail or k_acc > 1:
                 loss_parts, dtok = ops.smooth_l1_fwd_bwd(out, tgt, c.tokens, c.patch, self.cfg.loss_beta,
                                                          finish=False)
             else:
                 _, dtok = ops.smooth_l1_fwd_bwd(out, tgt, c.tokens, c.patch, self.cfg.loss_beta, self.loss_last,
                                                 self.loss_ema, self.cfg.ema_decay)
             del out
+            if k_acc > 1:  # mean over micro-batches (partials sum to each micro-batch's loss)
+                lp = loss_parts.float() * (1.0 / k_acc)
+                loss_acc = lp if loss_acc is None else loss_acc + lp
             ln_lo = 0
             # without a separate embedding bucket (single process) the patch-embedding
             # weight gradient joins block 0's grouped launch
@@ -356,10 +362,16 @@ class TrainEngine:
         ops.sqnorm(self.flat_g, self.sqnorm, gs)
         ops.adamw_step(self.flat_p, self.flat_g, self.flat_m, self.flat_v, self.flat_pb, self.sqnorm,
                        self.step_ctr, self.hyper, gs)
+        if loss_acc is not None:
+            loss_parts = loss_acc
         if tail:
             self.lnfold.refresh(tail=(loss_parts, self.loss_last, self.loss_ema, self.cfg.ema_decay, self.step_ctr,
                                       self.rng, self.sqnorm))
         else:
+            if k_acc > 1:  # one EMA update per optimizer step
+                loss = loss_parts.sum().reshape(self.loss_last.shape)
+                self.loss_last.copy_(loss)
+                self.loss_ema.mul_(self.cfg.ema_decay).add_(loss, alpha=1.0 - self.cfg.ema_decay)
             if self.lnfold is not None:
                 self.lnfold.refresh()
             ops.advance_counters(self.step_ctr, self.rng, self.sqnorm)

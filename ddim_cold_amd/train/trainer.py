@@ -183,7 +183,10 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
     prof = torch_profiler(rank)
     if prof is not None:
         prof.__enter__()
-    eval_rng = torch.tensor([cfg.seed + 7919, 0], dtype=torch.int64, device=device)
+    # eval draws (cold t per sample): independent per rank, like each rank's DataLoader
+    # in the reference; the counter is derived from the epoch, so a resumed run
+    # evaluates epoch e with the same draws as an uninterrupted one
+    eval_rng = torch.tensor([cfg.seed + 7919 + 1000003 * rank, 0], dtype=torch.int64, device=device)
 
     history = []
     t_start = time.time()
@@ -219,6 +222,7 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
         if (epoch - start_epoch + 1) % max(cfg.eval_every, 1) == 0 or epoch == end_epoch - 1:
             model.eval()
             vidx = shard_indices(n_val, world, rank, epoch, cfg.seed, shuffle=False, drop_last=False)
+            eval_rng[1] = epoch * val_batches
             with phase("evaluate"):
                 vloss = evaluate(model, engine, val_pool, vidx, B, cfg.dataset, cfg.model_total_steps, eval_rng)
             vloss = pdist.all_reduce_mean(vloss, device)
@@ -237,7 +241,8 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
         prof.__exit__(None, None, None)
     writer.close()
     result = {"steps": steps, "loss_rec": loss_rec, "best_loss": best_loss, "history": history,
-              "final_lr": engine.current_lr()}
+              "final_lr": engine.current_lr(), "rng": [int(v) for v in engine.rng.tolist()],
+              "eval_rng": [int(v) for v in eval_rng.tolist()]}
     pdist.cleanup()
     return result
 
@@ -249,8 +254,8 @@ def _spawn_entry(rank, world, cfg, exp_name, paths, backend, port, queue):
     os.environ["WORLD_SIZE"] = str(world)
     os.environ["LOCAL_RANK"] = str(rank)
     res = train_worker(rank, world, cfg, exp_name, paths, local_rank=rank, backend=backend)
-    if queue is not None and rank == 0:
-        queue.put(res)
+    if queue is not None:
+        queue.put((rank, res))
 
 
 def launch(cfg: ExperimentConfig, exp_name: str, paths: Paths, backend: Optional[str] = None) -> dict:
@@ -287,4 +292,10 @@ def launch(cfg: ExperimentConfig, exp_name: str, paths: Paths, backend: Optional
     bad = [p.exitcode for p in procs if p.exitcode != 0]
     if bad:
         raise RuntimeError(f"rank processes failed with exit codes {bad}")
-    return q.get() if not q.empty() else {}
+    per_rank = {}
+    while not q.empty():
+        r, res = q.get()
+        per_rank[r] = res
+    out = dict(per_rank.get(0, {}))
+    out["per_rank"] = per_rank  # every rank's result (rank 0's is also the top level)
+    return out

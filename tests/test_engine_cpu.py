@@ -178,6 +178,23 @@ def test_grad_accumulation_matches_full_batch():
     err = (acc.flat_m - full.flat_m).abs().max().item() / full.flat_m.abs().max().item()
     assert err < 1e-4, err
     assert int(acc.step_ctr[0]) == 1 and int(acc.rng[1]) == 2
+    # one EMA update per optimizer step with the mean micro-batch loss
+    # (multi_gpu_trainer.py:126: loss_rec = 0.99 loss_rec + 0.01 loss)
+    torch.testing.assert_close(acc.loss_last, full.loss_last, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(acc.loss_ema, 0.99 * 5.0 + 0.01 * full.loss_last, rtol=1e-5, atol=1e-6)
+
+
+def test_grad_accumulation_ema_once_per_step_without_fold(monkeypatch):
+    """Same EMA semantics on the unfolded path (no step tail)."""
+    x, y, t = _batch(4, seed=9)
+    acc = TrainEngine(_model(drop=False), EngineConfig(lr=1e-3, weight_decay=0.0, max_grad_norm=0.0, grad_accum=2),
+                      device="cpu")
+    acc.lnfold = None
+    halves = iter([(x[:2], y[:2], t[:2]), (x[2:], y[2:], t[2:])])
+    acc.set_batch_fn(lambda: next(halves))
+    acc.train_step()
+    assert int(acc.step_ctr[0]) == 1 and int(acc.rng[1]) == 2
+    torch.testing.assert_close(acc.loss_ema, 0.99 * 5.0 + 0.01 * acc.loss_last, rtol=1e-5, atol=1e-6)
 
 
 def _sync_worker(rank, world, port, out_path):

@@ -107,3 +107,30 @@ def test_multi_step_graph_matches_single_step_graph():
     assert int(eng.step_ctr[0]) == 9 and int(eng.rng[1]) == 9
     assert abs(em - es) <= 1e-4 * abs(es), (em, es)
     assert (pm - ps).abs().max().item() <= 2 * 1e-3 * 9
+
+
+@pytest.mark.gpu
+def test_ln_replica_finalize_fused_matches_separate(monkeypatch):
+    """LayerNorm dgamma/dbeta replica finalize carried by the embedding-backward launch
+    (DDIM_COLD_FUSE_LNFINAL=1, default) == the separate replica_reduce_ launch (=0):
+    same LayerNorm parameters after the step, replica workspace re-zeroed."""
+    def run(flag):
+        monkeypatch.setenv("DDIM_COLD_FUSE_LNFINAL", flag)
+        torch.manual_seed(0)
+        model = build_model("vit_tiny").cuda().train()
+        # no clipping: LayerNorm params after one AdamW step depend only on their own grads
+        eng = TrainEngine(model, EngineConfig(lr=1e-3, t_max=100, seed=3, use_graph=False, temb_rows=7,
+                                              max_grad_norm=0.0))
+        eng.set_batch_fn(ColdBatcher(synthetic_pool(64, seed=1, device="cuda"), 8, eng.rng))
+        eng.train_step()
+        torch.cuda.synchronize()
+        ln = torch.cat([eng.flat_p[eng.offsets[n + ".weight"][0]:eng.offsets[n + ".weight"][0] + 2 * model.embed_dim]
+                        for n in eng.ln_order])
+        # the step must have touched every LayerNorm parameter
+        return ln.clone(), float(eng.ln_ws.abs().max()), eng.flat_m.clone()
+    lf, wf, mf = run("1")
+    lu, wu, mu = run("0")
+    assert wf == 0.0 and wu == 0.0
+    init = torch.cat([torch.ones(384), torch.zeros(384)]).cuda().repeat(15)
+    assert (lf - init).abs().max() > 0
+    torch.testing.assert_close(lf, lu, rtol=0, atol=1e-6)

@@ -126,6 +126,26 @@ def test_trainer_two_ranks_gloo(tmp_path):
     assert len(epochs) == 1 and epochs[0][1] > 0
 
 
+def test_two_rank_resume_keeps_per_rank_seeds(tmp_path):
+    """lastepoch.pkl is written by rank 0; a 2-rank resume must keep each rank's own
+    RNG seed (independent cold t / dropout draws) and restore only the step counter."""
+    cfg = _tiny_cfg(num_gpus=2, epoch=[0, 1], ckpt_dir=str(tmp_path / "Saved_Models"))
+    paths = Paths.make(cfg, "res2", root=str(tmp_path))
+    res = launch(cfg, "res2", paths, backend="gloo")
+    seeds = {r: v["rng"][0] for r, v in res["per_rank"].items()}
+    assert len(seeds) == 2 and seeds[0] != seeds[1]
+    cfg2 = dataclasses.replace(cfg, resume=os.path.join(paths.ckpt_dir, "lastepoch.pkl"), epoch=[0, 2])
+    res2 = launch(cfg2, "res2", paths, backend="gloo")
+    pr = res2["per_rank"]
+    assert {r: v["rng"][0] for r, v in pr.items()} == seeds
+    # step counter continued from the checkpoint on every rank
+    assert pr[0]["rng"][1] == pr[1]["rng"][1] == 2 * res["per_rank"][0]["rng"][1]
+    # eval draws differ per rank and follow the epoch
+    assert pr[0]["eval_rng"][0] != pr[1]["eval_rng"][0]
+    nvb = res["per_rank"][0]["eval_rng"][1]  # val batches per rank (epoch 0 evaluated)
+    assert nvb >= 1 and pr[0]["eval_rng"][1] == pr[1]["eval_rng"][1] == 2 * nvb
+
+
 def test_cli_entry_points(tmp_path):
     cfg = dict(initializing="init.pkl", framework="_cli", num_gpus=1, batch_size=4, epoch=[0, 1],
                image_size=[16, 16], patch_size=4, embed_dim=32, depth=1, head=2, synthetic=True,
