@@ -501,11 +501,12 @@ void linear_wgrad(Tensor dy, Tensor x, Tensor dw, c10::optional<Tensor> db) {
 // (db_i += colsum dy_i).  The token reduction is split over fp32 atomics (2-way
 // for a full block group, more for small groups); splits == 1 would use a plain
 // read-add-write epilogue.
-void linear_wgrad_group(std::vector<Tensor> dys, std::vector<Tensor> xs, std::vector<Tensor> dws,
-                        std::vector<c10::optional<Tensor>> dbs) {
+static std::vector<GemmArgs> wgrad_probs(const std::vector<Tensor>& dys, const std::vector<Tensor>& xs,
+                                         const std::vector<Tensor>& dws,
+                                         const std::vector<c10::optional<Tensor>>& dbs, int* tiles_out,
+                                         int* min_kt_out) {
   const size_t n = dys.size();
-  TORCH_CHECK(n >= 1 && xs.size() == n && dws.size() == n && dbs.size() == n, "wgrad_group: list sizes");
-  const c10::DeviceGuard guard(dys[0].device());
+  TORCH_CHECK(xs.size() == n && dws.size() == n && dbs.size() == n, "wgrad_group: list sizes");
   std::vector<GemmArgs> probs;
   int tiles = 0, min_kt = 1 << 30;
   for (size_t i = 0; i < n; ++i) {
@@ -530,6 +531,22 @@ void linear_wgrad_group(std::vector<Tensor> dys, std::vector<Tensor> xs, std::ve
     tiles += ((Nout + 63) / 64) * ((K + 63) / 64);
     min_kt = std::min(min_kt, (M + 63) / 64);
   }
+  if (tiles_out) *tiles_out = tiles;
+  if (min_kt_out) *min_kt_out = min_kt;
+  return probs;
+}
+
+// Grouped weight gradients: one launch for all (dy_i, x_i) -> dW_i += dy_i^T x_i
+// (db_i += colsum dy_i).  The token reduction is split over fp32 atomics (2-way
+// for a full block group, more for small groups); splits == 1 would use a plain
+// read-add-write epilogue.
+void linear_wgrad_group(std::vector<Tensor> dys, std::vector<Tensor> xs, std::vector<Tensor> dws,
+                        std::vector<c10::optional<Tensor>> dbs) {
+  const size_t n = dys.size();
+  TORCH_CHECK(n >= 1, "wgrad_group: empty");
+  const c10::DeviceGuard guard(dys[0].device());
+  int tiles = 0, min_kt = 0;
+  std::vector<GemmArgs> probs = wgrad_probs(dys, xs, dws, dbs, &tiles, &min_kt);
   static const int forced = [] {
     const char* e = getenv("DDIM_COLD_WGRAD_GROUP_SPLITS");
     return e ? atoi(e) : 0;
@@ -552,6 +569,65 @@ void linear_wgrad_group(std::vector<Tensor> dys, std::vector<Tensor> xs, std::ve
     const int cnt = (int)std::min<size_t>(6, n - i0);
     gemm_wgrad_group(probs.data() + i0, cnt, splits, cur_stream());  // splits 0: 8-wave kernel
   }
+}
+
+// Token split of weight-gradient riders: enough slices that the riders' tiles
+// number about `target` workgroups (DDIM_COLD_RIDE_WG, default 160), >= 2
+static int ride_splits(int tiles, int min_kt) {
+  static const int target = [] {
+    const char* e = getenv("DDIM_COLD_RIDE_WG");
+    return e ? std::max(16, atoi(e)) : 160;
+  }();
+  int s = (target + tiles - 1) / tiles;
+  s = std::max(2, std::min(s, 8));
+  return std::min(s, std::max(2, min_kt));
+}
+
+// dy @ W (linear_dgrad / linear_dgrad_gelu semantics) with the listed weight
+// gradients riding in the same launch (csrc/gemm.hip gemm_dgrad_ride_kernel).
+// mode 0: plain dgrad (out_fp32, splits as linear_dgrad); mode 1: GELU' dgrad
+// (u, rng, site, p as linear_dgrad_gelu).
+Tensor linear_dgrad_ride(Tensor dy, Tensor w, int64_t mode, bool out_fp32, int64_t splits,
+                         c10::optional<Tensor> u, c10::optional<Tensor> rng, int64_t site, double p,
+                         std::vector<Tensor> dys, std::vector<Tensor> xs, std::vector<Tensor> dws,
+                         std::vector<c10::optional<Tensor>> dbs) {
+  CHECK_IN(dy, BF16); CHECK_IN(w, BF16);
+  const c10::DeviceGuard guard(dy.device());
+  TORCH_CHECK(dy.dim() == 2 && w.dim() == 2 && dy.size(1) == w.size(0), "dgrad shapes");
+  TORCH_CHECK(mode == 0 || mode == 1, "dgrad_ride: mode 0 (plain) or 1 (GELU')");
+  const int M = dy.size(0), Nout = w.size(0), K = w.size(1);
+  TORCH_CHECK(Nout % 8 == 0 && K % 8 == 0, "dgrad dims must be multiples of 8");
+  TORCH_CHECK(dys.size() <= 6, "dgrad_ride: at most 6 riders");
+  GemmArgs g;
+  g.A = dy.data_ptr(); g.B = w.data_ptr();
+  g.M = M; g.N = K; g.K = Nout; g.lda = Nout; g.ldb = K;
+  Tensor dx;
+  int epi;
+  if (mode == 1) {
+    TORCH_CHECK(u.has_value() && rng.has_value(), "dgrad_ride: GELU' needs u and rng");
+    CHECK_IN((*u), BF16); check_rng(*rng);
+    TORCH_CHECK(u->numel() == (int64_t)M * K, "u shape");
+    dx = at::empty({M, K}, dy.options());
+    g.aux = u->data_ptr(); g.rng = rng->data_ptr<int64_t>(); g.site_drop = site; g.p_drop = p;
+    epi = EPI_DGELU;
+  } else {
+    TORCH_CHECK(splits >= 1 && splits <= 4, "dgrad K split: 1..4");
+    dx = splits > 1 ? at::empty({splits, M, K}, dy.options().dtype(out_fp32 ? F32 : BF16))
+                    : at::empty({M, K}, dy.options().dtype(out_fp32 ? F32 : BF16));
+    g.splits = (int)splits;
+    g.split_stride = (long long)M * K;
+    epi = out_fp32 ? EPI_F32 : EPI_BF16;
+  }
+  g.C = dx.data_ptr(); g.ldc = K;
+  int tiles = 0, min_kt = 1;
+  std::vector<GemmArgs> probs;
+  if (!dys.empty()) {
+    probs = wgrad_probs(dys, xs, dws, dbs, &tiles, &min_kt);
+    for (auto& t : dys) TORCH_CHECK(t.device() == dy.device(), "dgrad_ride: riders on another device");
+  }
+  const int ws = probs.empty() ? 2 : ride_splits(tiles, min_kt);
+  gemm_dgrad_ride(g, epi, probs.data(), (int)probs.size(), ws, cur_stream());
+  return dx;
 }
 
 std::tuple<Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma,
@@ -907,6 +983,8 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("linear_dgrad_gelu(Tensor dy, Tensor w, Tensor u, Tensor rng, int site, float p) -> Tensor");
   m.def("linear_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, Tensor(b!)? db) -> ()");
   m.def("linear_wgrad_group(Tensor[] dys, Tensor[] xs, Tensor(a!)[] dws, Tensor(b!)?[] dbs) -> ()");
+  m.def("linear_dgrad_ride(Tensor dy, Tensor w, int mode, bool out_fp32, int splits, Tensor? u, Tensor? rng, "
+        "int site, float p, Tensor[] dys, Tensor[] xs, Tensor(a!)[] dws, Tensor(b!)?[] dbs) -> Tensor");
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor? g_res, "
         "Tensor(a!) dgamma, Tensor(b!) dbeta, int N, Tensor rng, int site_drop, float p_drop, int site_dp, "
         "float p_dp, bool emit_gy, Tensor(c!)? ws=None, Tensor? beta=None, Tensor(d!)? y_out=None) -> (Tensor, Tensor)");
@@ -954,6 +1032,7 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("linear_fwd", &linear_fwd);
   m.impl("linear_residual_ln_fwd", &linear_residual_ln_fwd);
   m.impl("linear_wgrad_group", &linear_wgrad_group);
+  m.impl("linear_dgrad_ride", &linear_dgrad_ride);
   m.impl("layernorm_bwd", &layernorm_bwd);
   m.impl("replica_reduce_", &replica_reduce_);
   m.impl("ln_fold_", &ln_fold_);

@@ -1,0 +1,690 @@
+// GEMM parameter block and the fused epilogue family (bias, LayerNorm fold
+// consumer/producer, QKV head-major scatter, residual + dropout + drop-path,
+// GELU, head / unpatchify / loss / DDIM update, patch embedding, gradient
+// accumulate), shared by the GEMM kernels (gemm.hip) and the image-group
+// persistent forward (vit_group.hip), so both produce bit-identical outputs.
+//
+// ``PUB`` (VecEpi): the epilogue's hand-off outputs (bf16 residual copy,
+// LayerNorm statistics, GELU output) are stored write-through (sc1) and the
+// statistics it consumes are loaded sc1, for a consumer workgroup of the SAME
+// launch on another XCD (MI355X_MICROARCH.md, inter-workgroup visibility).
+#pragma once
+#include "common.h"
+#include "kernels.h"
+
+namespace dc {
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned int gu32;
+
+// write-through 8-B store / L1-bypassing 8-B load (agent-scope relaxed atomics:
+// global_store_dwordx2 sc1 / global_load_dwordx2 sc1)
+__device__ __forceinline__ void st8_sc1(void* p, uint64_t v) {
+  __hip_atomic_store((gu64*)p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld8_sc1(const void* p) {
+  return __hip_atomic_load((gu64*)const_cast<void*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+struct GemmParams {
+  const bf16* A;
+  const bf16* B;
+  int M, N, K;
+  int lda, ldb;
+  void* C;
+  int ldc;
+  const float* bias;
+  // epilogue extras
+  const float* res;      // residual stream in (RESID)
+  void* C2;              // second output (GELU: h)
+  const bf16* aux;       // saved pre-activation u (DGELU)
+  const int64_t* rng;    // {seed, step}
+  int site_drop;
+  uint32_t thr_drop;
+  float scale_drop;
+  int site_dp;
+  uint32_t thr_dp;
+  float scale_dp;
+  int tokens;            // tokens per sample (N = P+1), or patches per sample (EMBED)
+  int batch;
+  int heads, hd;         // QKV scatter
+  int chans, img_h, img_w, patch;  // HEAD
+  const float* pos;      // EMBED
+  const float* temb;
+  const int64_t* tsteps;
+  int emb_dim;
+  int ktiles_per_split;
+  const float* coef;     // HEAD mode 1: {sqrt a_t, sqrt(1-a_t), sqrt a_tk, sqrt(1-a_tk)} (device)
+  long long split_stride;  // EPI_F32: elements between the K-split output slices
+  int head_mode;         // HEAD: 0 image, 1 fused DDIM step (res = x_t in, C = x_next, C2 = x0), 2 clamp,
+                         //   3 training loss (res = target image, C2 = token-layout grad, loss_parts)
+  float loss_beta;       // HEAD mode 3: smooth-L1 beta and 1/numel
+  float loss_inv_n;
+  float* loss_parts;     // HEAD mode 3: one loss partial per workgroup (gridDim.x entries)
+  // LayerNorm fold (GemmArgs): consumer side
+  const float* ln_st;
+  const float* ln_c;
+  float ln_eps;
+  float* ln_mean;
+  float* ln_rstd;
+  // producer side
+  float* st_out;
+  bf16* xb_out;
+  int debug;  // profiling aid (DDIM_COLD_GEMM_DEBUG): 1 = skip the epilogue, 2 = skip the main loop,
+              // 3 = scalar (untransposed) epilogue
+};
+
+
+// Epilogue in two phases: (1) every global load the epilogue needs (bias per
+// column, residual / saved pre-activation / pos+time embedding per element) is
+// issued for the whole fragment tile, (2) compute + store.  Interleaving them
+// per element serialises the tile on memory latency (the loads may alias the
+// stores through GemmParams, so the compiler cannot hoist them).
+// The epilogue is "load everything, then compute + store": interleaving per-element
+// loads (bias / residual / saved pre-activation / embeddings, which may alias the
+// stores through GemmParams) with stores serialises the tile on memory latency.
+// Every output index is separable, idx = rowoff(m) + coloff(n), so the integer
+// divisions (token -> sample, column -> head / pixel) are done once per row and
+// once per column of the lane's fragment, not per element.
+struct RowInfo {
+  long long off;  // row part of the destination index (-1: skip row)
+  int b;          // sample index (drop-path) / helper
+};
+
+template <int EPI>
+__device__ __forceinline__ RowInfo epi_row(const GemmParams& p, int m) {
+  RowInfo ri;
+  ri.b = 0;
+  if (EPI == EPI_QKV) {
+    const int b = m / p.tokens, tok = m - b * p.tokens;
+    ri.off = ((long long)b * p.heads * p.tokens + tok) * p.hd;
+  } else if (EPI == EPI_RESID) {
+    ri.off = (long long)m * p.N;
+    ri.b = m / p.tokens;
+  } else if (EPI == EPI_GELU || EPI == EPI_DGELU) {
+    ri.off = (long long)m * p.N;
+  } else if (EPI == EPI_HEAD) {
+    const int b = m / p.tokens, tok = m - b * p.tokens;
+    if (tok == 0) {
+      ri.off = -1;
+    } else {
+      const int P = p.patch, Wp = p.img_w / P;
+      const int patch = tok - 1, hp = patch / Wp, wp = patch - hp * Wp;
+      ri.off = (long long)b * p.chans * p.img_h * p.img_w + (long long)hp * P * p.img_w + wp * P;
+    }
+  } else if (EPI == EPI_EMBED) {
+    const int Pn = p.tokens;
+    const int b = m / Pn, patch = m - b * Pn;
+    ri.off = ((long long)b * (Pn + 1) + patch + 1) * p.emb_dim;
+    ri.b = b;
+  } else {
+    ri.off = (long long)m * p.ldc;
+  }
+  return ri;
+}
+
+template <int EPI>
+__device__ __forceinline__ long long epi_col(const GemmParams& p, int n) {
+  if (EPI == EPI_QKV) {
+    const int D = p.heads * p.hd;
+    const int s = n / D, rem = n - s * D;
+    const int h = rem / p.hd, d = rem - h * p.hd;
+    return (long long)s * p.batch * p.heads * p.tokens * p.hd + (long long)h * p.tokens * p.hd + d;
+  }
+  if (EPI == EPI_HEAD) {
+    const int P = p.patch;
+    const int c = n % p.chans, ab = n / p.chans, a = ab / P, bb = ab - a * P;
+    return (long long)c * p.img_h * p.img_w + (long long)a * p.img_w + bb;
+  }
+  return n;
+}
+
+// ---- LayerNorm fold.  LN(x) W^T + b = rstd * (x (gamma o W)^T - mean * c) + (b + W beta)
+// with c[n] = sum_k bf16(gamma_k W[n][k]) (ln_fold_prep in layernorm.hip), so the
+// GEMM consuming a LayerNorm reads the raw residual stream (its bf16 copy) and
+// the LayerNorm launch disappears.  The row statistics {sum x, sum x^2} come from
+// the epilogue of the GEMM that PRODUCED x (residual / patch-embed epilogue:
+// per-row partial sums over its columns, fp32 atomics).
+template <int EPI>
+struct FoldEpi {
+  static constexpr bool CONSUMER =
+      EPI == EPI_QKV || EPI == EPI_GELU || EPI == EPI_BF16 || EPI == EPI_F32 || EPI == EPI_HEAD;
+  static constexpr bool PRODUCER = EPI == EPI_RESID || EPI == EPI_EMBED;
+};
+
+// Row statistics layout: st[row][NP][2], NP = D / 32 slots; slot s holds
+// {sum, sum^2} of the row's columns 32s..32s+31, written exactly once by the
+// wave of the producing epilogue that owns those columns (no atomics, no
+// zeroing: deterministic).  Consumers add the slots in a fixed butterfly order.
+constexpr int LN_SLOT = 32;
+constexpr int LN_MAX_SLOTS = 16;
+
+// (mean, rstd) of a row from its {sum, sum^2} over D = K columns
+__device__ __forceinline__ float2 ln_row_stats(const GemmParams& p, float2 st) {
+  const float invd = 1.0f / (float)p.K;
+  const float mu = st.x * invd;
+  const float var = fmaxf(st.y * invd - mu * mu, 0.f);
+  return make_float2(mu, rsqrtf(var + p.ln_eps));
+}
+
+__device__ __forceinline__ float2 f2add(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+template <int MASK>
+__device__ __forceinline__ float2 f2xor(float2 a) {
+  return make_float2(__shfl_xor(a.x, MASK), __shfl_xor(a.y, MASK));
+}
+
+// destination token row of a producer epilogue row (statistics index)
+template <int EPI>
+__device__ __forceinline__ int fold_token_row(const GemmParams& p, int m) {
+  if (EPI == EPI_EMBED) {
+    const int b = m / p.tokens;
+    return m + b + 1;  // b*(P+1) + patch + 1
+  }
+  return m;
+}
+
+// returns the stored fp32 value of the residual / embedding epilogues (LayerNorm statistics)
+template <int EPI>
+__device__ __forceinline__ float epilogue(const GemmParams& p, long long idx, int rb, float v, float pre,
+                                          uint32_t salt_drop, uint32_t salt_dp, const f32x4& cf) {
+  if (EPI == EPI_BF16) {
+    reinterpret_cast<bf16*>(p.C)[idx + blockIdx.z * p.split_stride] = f2bf(v);
+  } else if (EPI == EPI_F32) {
+    reinterpret_cast<float*>(p.C)[idx + blockIdx.z * p.split_stride] = v;
+  } else if (EPI == EPI_ATOMIC) {
+    atomicAdd(reinterpret_cast<float*>(p.C) + idx, v);
+  } else if (EPI == EPI_ACC) {
+    reinterpret_cast<float*>(p.C)[idx] = pre + v;  // pre = old C (loaded in phase 1)
+  } else if (EPI == EPI_QKV) {
+    reinterpret_cast<bf16*>(p.C)[idx] = f2bf(v);
+  } else if (EPI == EPI_RESID) {
+    if (p.thr_drop) v = dropout_keep(salt_drop, (uint32_t)idx, p.thr_drop) ? v * p.scale_drop : 0.f;
+    if (p.thr_dp) v = dropout_keep(salt_dp, (uint32_t)rb, p.thr_dp) ? v * p.scale_dp : 0.f;
+    reinterpret_cast<float*>(p.C)[idx] = pre + v;
+    return pre + v;
+  } else if (EPI == EPI_GELU) {
+    reinterpret_cast<bf16*>(p.C)[idx] = f2bf(v);
+    float h = gelu_f(v);
+    if (p.thr_drop) h = dropout_keep(salt_drop, (uint32_t)idx, p.thr_drop) ? h * p.scale_drop : 0.f;
+    reinterpret_cast<bf16*>(p.C2)[idx] = f2bf(h);
+  } else if (EPI == EPI_DGELU) {
+    if (p.thr_drop) v = dropout_keep(salt_drop, (uint32_t)idx, p.thr_drop) ? v * p.scale_drop : 0.f;
+    reinterpret_cast<bf16*>(p.C)[idx] = f2bf(v * gelu_grad_f(pre));
+  } else if (EPI == EPI_HEAD) {
+    if (p.head_mode == 0) {
+      reinterpret_cast<float*>(p.C)[idx] = v;
+    } else if (p.head_mode == 3) {
+      // smooth-L1 vs the target pixel (`pre`), multi_gpu_trainer.py:124: the image
+      // is never written; returns the element's loss / numel (the gradient is
+      // stored by the caller in the token layout)
+      const float d = v - pre, ad = fabsf(d), b = p.loss_beta;
+      return (ad < b ? 0.5f * d * d / b : ad - 0.5f * b) * p.loss_inv_n;
+    } else {
+      // the sampler's x0-hat clamp (ViT.py:229, ViT_draft2drawing.py:280), and for
+      // mode 1 the whole DDIM update (ViT.py:230-234) with x_t preloaded in `pre`
+      const float x0 = fminf(fmaxf(v, -1.f), 1.f);
+      if (p.head_mode == 2) {
+        reinterpret_cast<float*>(p.C)[idx] = x0;
+      } else {
+        const float eps = (pre - cf[0] * x0) / cf[1];
+        reinterpret_cast<float*>(p.C)[idx] = cf[2] * x0 + cf[3] * eps;
+        reinterpret_cast<float*>(p.C2)[idx] = x0;
+      }
+    }
+  } else if (EPI == EPI_EMBED) {
+    v += pre;
+    if (p.thr_drop) v = dropout_keep(salt_drop, (uint32_t)idx, p.thr_drop) ? v * p.scale_drop : 0.f;
+    reinterpret_cast<float*>(p.C)[idx] = v;
+    return v;
+  }
+  return 0.f;
+}
+
+// scalar whole-tile epilogue (HEAD: output columns are not contiguous in memory):
+// acc[FM][FN] fragment tiles at (mb + i*16 + 4g + r, nb + j*16 + li)
+template <int EPI, int FM, int FN>
+__device__ __forceinline__ void run_epilogue_scalar(const GemmParams& p, const f32x4 (&acc)[FM][FN], int mb, int nb,
+                                             int g, int li) {
+  constexpr bool ELEM = EPI == EPI_RESID || EPI == EPI_DGELU || EPI == EPI_EMBED || EPI == EPI_ACC;
+  const bool head_ddim = EPI == EPI_HEAD && p.head_mode == 1;
+  const bool head_loss = EPI == EPI_HEAD && p.head_mode == 3;
+  RowInfo rows[FM][4];
+  long long cols[FN];
+  bool colok[FN];
+  float colb[FN];
+  const bool has_bias = (EPI != EPI_ATOMIC) && (EPI != EPI_ACC) && p.bias != nullptr;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = nb + j * 16 + li;
+    colok[j] = n < p.N;
+    cols[j] = epi_col<EPI>(p, n);
+    colb[j] = (has_bias && colok[j]) ? p.bias[n] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = mb + i * 16 + 4 * g + r;
+      rows[i][r] = epi_row<EPI>(p, m < p.M ? m : p.M - 1);
+      if (m >= p.M) rows[i][r].off = -1;
+    }
+  // LayerNorm fold, consumer side: per-row statistics and per-column c
+  constexpr bool FC = FoldEpi<EPI>::CONSUMER, FP = FoldEpi<EPI>::PRODUCER;
+  const bool fold = FC && p.ln_st != nullptr;
+  // slot li of each of the lane's rows (the 16 lanes of a row group hold all <= 16 slots)
+  const int np_in = p.K / LN_SLOT;
+  float2 lnst[FM][4];
+  float colc[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) colc[j] = (fold && colok[j]) ? p.ln_c[nb + j * 16 + li] : 0.f;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = mb + i * 16 + 4 * g + r;
+      lnst[i][r] = (fold && m < p.M && li < np_in)
+                       ? *reinterpret_cast<const float2*>(p.ln_st + 2 * ((size_t)m * np_in + li))
+                       : make_float2(0.f, 0.f);
+    }
+  // phase 1: element loads
+  float pre[FM][FN][4];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = 0.f;
+        if ((head_ddim || head_loss) && rows[i][r].off >= 0 && colok[j]) v = p.res[rows[i][r].off + cols[j]];
+        if (ELEM && rows[i][r].off >= 0 && colok[j]) {
+          const int n = nb + j * 16 + li;
+          if (EPI == EPI_RESID) v = p.res[rows[i][r].off + n];
+          if (EPI == EPI_ACC) v = reinterpret_cast<const float*>(p.C)[rows[i][r].off + n];
+          if (EPI == EPI_DGELU) v = bf2f(p.aux[rows[i][r].off + n]);
+          if (EPI == EPI_EMBED) {
+            const int m = mb + i * 16 + 4 * g + r;
+            const int patch = m - rows[i][r].b * p.tokens;
+            v = p.pos[(size_t)(patch + 1) * p.emb_dim + n] + p.temb[(size_t)p.tsteps[rows[i][r].b] * p.emb_dim + n];
+          }
+        }
+        pre[i][j][r] = v;
+      }
+  // phase 2: compute + store
+  uint32_t salt_drop = 0, salt_dp = 0;
+  if (p.thr_drop) salt_drop = site_salt(p.rng, p.site_drop);
+  if (p.thr_dp) salt_dp = site_salt(p.rng, p.site_dp);
+  f32x4 cf = f32x4{0.f, 1.f, 0.f, 0.f};
+  if (head_ddim) cf = f32x4{p.coef[0], p.coef[1], p.coef[2], p.coef[3]};
+  float2 ms[FM][4];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (fold) {  // sum the slots across the 16 lanes (fixed butterfly order: identical on every lane)
+        float2 t = lnst[i][r];
+        t = f2add(t, f2xor<1>(t));
+        t = f2add(t, f2xor<2>(t));
+        t = f2add(t, f2xor<4>(t));
+        t = f2add(t, f2xor<8>(t));
+        lnst[i][r] = t;
+      }
+      ms[i][r] = fold ? ln_row_stats(p, lnst[i][r]) : make_float2(0.f, 1.f);
+      const int m = mb + i * 16 + 4 * g + r;
+      // every row's (mean, rstd) for the LayerNorm backward, also rows the epilogue skips
+      if (fold && p.ln_mean != nullptr && nb == 0 && li == 0 && m < p.M) {
+        p.ln_mean[m] = ms[i][r].x;
+        p.ln_rstd[m] = ms[i][r].y;
+      }
+    }
+  const bool prod = FP && p.st_out != nullptr;
+  float lsum = 0.f;  // HEAD mode 3: this lane's loss contributions
+  float2 part[FM][4][(FN + 1) / 2];  // producer (debug path): per-slot partials of the lane's rows
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int sl = 0; sl < (FN + 1) / 2; ++sl) part[i][r][sl] = make_float2(0.f, 0.f);
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (rows[i][r].off >= 0 && colok[j]) {
+          const float a = fold ? (acc[i][j][r] - ms[i][r].x * colc[j]) * ms[i][r].y : acc[i][j][r];
+          const float o = epilogue<EPI>(p, rows[i][r].off + cols[j], rows[i][r].b, a + colb[j], pre[i][j][r],
+                                        salt_drop, salt_dp, cf);
+          if (prod) {
+            part[i][r][j / 2] = f2add(part[i][r][j / 2], make_float2(o, o * o));
+            p.xb_out[rows[i][r].off + cols[j]] = f2bf(o);
+          }
+          if (head_loss) {  // gradient of the mean smooth-L1, straight into the token layout
+            const int m = mb + i * 16 + 4 * g + r, n = nb + j * 16 + li;
+            const float d = (a + colb[j] - pre[i][j][r]) / p.loss_beta;
+            reinterpret_cast<bf16*>(p.C2)[(size_t)m * p.N + n] = f2bf(fminf(fmaxf(d, -1.f), 1.f) * p.loss_inv_n);
+            lsum += o;
+          }
+        } else if (head_loss && colok[j] && mb + i * 16 + 4 * g + r < p.M) {  // cls rows: zero gradient
+          reinterpret_cast<bf16*>(p.C2)[(size_t)(mb + i * 16 + 4 * g + r) * p.N + nb + j * 16 + li] = f2bf(0.f);
+        }
+  if (prod) {
+    const int np_out = p.N / LN_SLOT;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int sl = 0; sl < (FN + 1) / 2; ++sl) {
+          float2 t = part[i][r][sl];
+          t = f2add(t, f2xor<1>(t));
+          t = f2add(t, f2xor<2>(t));
+          t = f2add(t, f2xor<4>(t));
+          t = f2add(t, f2xor<8>(t));
+          const int m = mb + i * 16 + 4 * g + r;
+          if (li == 0 && m < p.M)
+            *reinterpret_cast<float2*>(p.st_out + 2 * ((size_t)fold_token_row<EPI>(p, m) * np_out + nb / LN_SLOT +
+                                                       sl)) = t;
+        }
+  }
+  if (head_loss) {  // one deterministic partial per workgroup (summed by the step tail)
+    __shared__ float lred[4];
+    lsum = wave_sum(lsum);
+    if ((threadIdx.x & 63) == 0) lred[threadIdx.x >> 6] = lsum;
+    __syncthreads();
+    if (threadIdx.x == 0) p.loss_parts[blockIdx.x] = (lred[0] + lred[1]) + (lred[2] + lred[3]);
+  }
+}
+
+
+// ---- 4x4 transpose inside each quad of lanes (DPP quad_perm, no LDS):
+// in:  a[r] = element (row r, column x) of a 4x4 block, x = lane's quad position
+// out: o[c] = element (row x, column c)
+__device__ __forceinline__ float sel4(const f32x4& a, int i) {
+  return i == 0 ? a[0] : i == 1 ? a[1] : i == 2 ? a[2] : a[3];
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ f32x4 quad_transpose(const f32x4& a, int x) {
+  const float r0 = sel4(a, x);
+  const float r1 = dpp_f<0x93>(sel4(a, (x + 1) & 3));  // from quad lane (x-1)&3: (row x, col (x-1)&3)
+  const float r2 = dpp_f<0x4E>(sel4(a, (x + 2) & 3));  // (row x, col (x-2)&3)
+  const float r3 = dpp_f<0x39>(sel4(a, (x + 3) & 3));  // (row x, col (x-3)&3)
+  f32x4 o;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int d = (x - c) & 3;
+    o[c] = d == 0 ? r0 : d == 1 ? r1 : d == 2 ? r2 : r3;
+  }
+  return o;
+}
+
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ void st4(float* p, const f32x4& v) { *reinterpret_cast<f32x4*>(p) = v; }
+__device__ __forceinline__ void st4bf(bf16* p, const f32x4& v) {
+  bf16x4 b;
+  b[0] = f2bf(v[0]); b[1] = f2bf(v[1]); b[2] = f2bf(v[2]); b[3] = f2bf(v[3]);
+  *reinterpret_cast<bf16x4*>(p) = b;
+}
+// bf16x4 store, write-through (sc1) when the bytes are handed to another workgroup of the launch
+template <bool PUB>
+__device__ __forceinline__ void st4bf_pub(bf16* p, const f32x4& v) {
+  if (!PUB) {
+    st4bf(p, v);
+  } else {
+    bf16x4 b;
+    b[0] = f2bf(v[0]); b[1] = f2bf(v[1]); b[2] = f2bf(v[2]); b[3] = f2bf(v[3]);
+    st8_sc1(p, __builtin_bit_cast(uint64_t, b));
+  }
+}
+template <bool PUB>
+__device__ __forceinline__ void st2f_pub(float* p, float2 v) {
+  if (!PUB) *reinterpret_cast<float2*>(p) = v;
+  else st8_sc1(p, __builtin_bit_cast(uint64_t, v));
+}
+template <bool PUB>
+__device__ __forceinline__ float2 ld2f_pub(const float* p) {
+  if (!PUB) return *reinterpret_cast<const float2*>(p);
+  return __builtin_bit_cast(float2, ld8_sc1(p));
+}
+__device__ __forceinline__ f32x4 ld4bf(const bf16* p) {
+  const bf16x4 b = *reinterpret_cast<const bf16x4*>(p);
+  return f32x4{bf2f(b[0]), bf2f(b[1]), bf2f(b[2]), bf2f(b[3])};
+}
+
+// Vector epilogue: the MFMA accumulator layout (lane = column, 4 registers =
+// 4 rows) is transposed inside lane quads so each lane owns 4 CONSECUTIVE
+// columns of one row; every load/store of the epilogue is then one 8-/16-byte
+// vector access instead of four 2-/4-byte scalar ones.  Requires N % 4 == 0 and
+// output columns contiguous in groups of 4 (all epilogues except HEAD).
+//
+// Split in two so the epilogue's global loads (bias, residual, saved
+// pre-activation, embeddings, accumulate target) can be issued BEFORE the main
+// loop (`prefetch`) and land while the MFMAs run: at these sizes a GEMM is a
+// chain of ~3 dependent memory round trips and this removes one of them.
+template <int EPI, int FM, int FN, bool PUB = false>
+struct VecEpi {
+  static constexpr bool PRE = EPI == EPI_RESID || EPI == EPI_DGELU || EPI == EPI_EMBED || EPI == EPI_ACC;
+  static constexpr bool FC = FoldEpi<EPI>::CONSUMER, FP = FoldEpi<EPI>::PRODUCER;
+  RowInfo rows[FM];
+  long long cols[FN];
+  bool colok[FN];
+  f32x4 colb[FN];
+  f32x4 pre[FM][FN];
+  int rowm[FM];     // GEMM row of the lane's fragment row (-1: out of range)
+  float2 lnst[FM][LN_MAX_SLOTS / 4];  // fold consumer: statistics slots q, q+4, .. of the row
+  f32x4 lnc[FN];    // fold consumer: c of the lane's 4 columns
+  bool first_col;   // lane holds column 0 (writes the row's mean / rstd)
+  int colbase;      // first column of the wave's tile
+
+  __device__ __forceinline__ void prefetch(const GemmParams& p, int mb, int nb, int g, int li) {
+    const int x = li & 3, q = li >> 2;
+    const bool fold = FC && p.ln_st != nullptr;
+    first_col = nb == 0 && q == 0;
+    colbase = nb;
+    const bool has_bias = (EPI != EPI_ATOMIC) && (EPI != EPI_ACC) && p.bias != nullptr;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = nb + j * 16 + 4 * q;
+      colok[j] = n < p.N;
+      cols[j] = epi_col<EPI>(p, n);
+      colb[j] = (has_bias && colok[j]) ? ld4(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = mb + i * 16 + 4 * g + x;
+      rows[i] = epi_row<EPI>(p, m < p.M ? m : p.M - 1);
+      if (m >= p.M) rows[i].off = -1;
+      rowm[i] = m < p.M ? m : -1;
+      const int np_in = p.K / LN_SLOT;
+#pragma unroll
+      for (int k = 0; k < LN_MAX_SLOTS / 4; ++k) {
+        const int sl = q + 4 * k;
+        lnst[i][k] = (fold && m < p.M && sl < np_in) ? ld2f_pub<PUB>(p.ln_st + 2 * ((size_t)m * np_in + sl))
+                                                     : make_float2(0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = nb + j * 16 + 4 * q;
+      lnc[j] = (fold && colok[j]) ? ld4(p.ln_c + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (PRE && rows[i].off >= 0 && colok[j]) {
+          const int n = nb + j * 16 + 4 * q;
+          if (EPI == EPI_RESID) v = ld4(p.res + rows[i].off + n);
+          if (EPI == EPI_DGELU) v = ld4bf(p.aux + rows[i].off + n);
+          if (EPI == EPI_ACC) v = ld4(reinterpret_cast<const float*>(p.C) + rows[i].off + n);
+          if (EPI == EPI_EMBED) {
+            const int m = mb + i * 16 + 4 * g + x;
+            const int patch = m - rows[i].b * p.tokens;
+            v = ld4(p.pos + (size_t)(patch + 1) * p.emb_dim + n) +
+                ld4(p.temb + (size_t)p.tsteps[rows[i].b] * p.emb_dim + n);
+          }
+        }
+        pre[i][j] = v;
+      }
+  }
+
+  __device__ __forceinline__ void finish(const GemmParams& p, const f32x4 (&acc_in)[FM][FN], int li) {
+    const int x = li & 3;
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = quad_transpose(acc_in[i][j], x);
+    uint32_t salt_drop = 0, salt_dp = 0;
+    if (p.thr_drop) salt_drop = site_salt(p.rng, p.site_drop);
+    if (p.thr_dp) salt_dp = site_salt(p.rng, p.site_dp);
+    const bool fold = FC && p.ln_st != nullptr;
+    const bool prod = FP && p.st_out != nullptr;
+    float2 ms[FM];
+    constexpr int SL = FN / 2;  // 32-column statistics slots per wave
+    float2 part[FM][SL];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      if (fold) {  // the row's slots: lane-local, then across the 4 lanes of the row (fixed order)
+        float2 t = lnst[i][0];
+#pragma unroll
+        for (int k = 1; k < LN_MAX_SLOTS / 4; ++k) t = f2add(t, lnst[i][k]);
+        t = f2add(t, f2xor<4>(t));
+        t = f2add(t, f2xor<8>(t));
+        ms[i] = ln_row_stats(p, t);
+      } else {
+        ms[i] = make_float2(0.f, 1.f);
+      }
+#pragma unroll
+      for (int sl = 0; sl < SL; ++sl) part[i][sl] = make_float2(0.f, 0.f);
+      if (fold && p.ln_mean != nullptr && first_col && rowm[i] >= 0) {
+        p.ln_mean[rowm[i]] = ms[i].x;
+        p.ln_rstd[rowm[i]] = ms[i].y;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      if (rows[i].off < 0) continue;
+      const bool keep_row =
+          (EPI == EPI_RESID && p.thr_dp) ? dropout_keep(salt_dp, (uint32_t)rows[i].b, p.thr_dp) : true;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        if (!colok[j]) continue;
+        const long long idx = rows[i].off + cols[j];
+        f32x4 v = fold ? (acc[i][j] - ms[i].x * lnc[j]) * ms[i].y + colb[j] : acc[i][j] + colb[j];
+        if (EPI == EPI_BF16) {
+          st4bf(reinterpret_cast<bf16*>(p.C) + idx + blockIdx.z * p.split_stride, v);
+        } else if (EPI == EPI_QKV) {
+          st4bf(reinterpret_cast<bf16*>(p.C) + idx, v);
+        } else if (EPI == EPI_F32) {
+          st4(reinterpret_cast<float*>(p.C) + idx + blockIdx.z * p.split_stride, v);
+        } else if (EPI == EPI_ATOMIC) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) atomicAdd(reinterpret_cast<float*>(p.C) + idx + c, v[c]);
+        } else if (EPI == EPI_ACC) {
+          st4(reinterpret_cast<float*>(p.C) + idx, pre[i][j] + v);
+        } else if (EPI == EPI_RESID) {
+          bool kp[4] = {true, true, true, true};
+          if (p.thr_drop) dropout_keep4(salt_drop, (uint32_t)idx, p.thr_drop, kp);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            float e = v[c];
+            if (p.thr_drop) e = kp[c] ? e * p.scale_drop : 0.f;
+            if (p.thr_dp) e = keep_row ? e * p.scale_dp : 0.f;
+            v[c] = pre[i][j][c] + e;
+          }
+          st4(reinterpret_cast<float*>(p.C) + idx, v);
+          if (prod) {
+            part[i][j / 2] = f2add(part[i][j / 2], make_float2((v[0] + v[1]) + (v[2] + v[3]),
+                                                               (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3])));
+            st4bf_pub<PUB>(p.xb_out + idx, v);
+          }
+        } else if (EPI == EPI_GELU) {
+          st4bf(reinterpret_cast<bf16*>(p.C) + idx, v);
+          f32x4 h;
+          bool kp[4] = {true, true, true, true};
+          if (p.thr_drop) dropout_keep4(salt_drop, (uint32_t)idx, p.thr_drop, kp);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            float e = gelu_f(v[c]);
+            if (p.thr_drop) e = kp[c] ? e * p.scale_drop : 0.f;
+            h[c] = e;
+          }
+          st4bf_pub<PUB>(reinterpret_cast<bf16*>(p.C2) + idx, h);
+        } else if (EPI == EPI_DGELU) {
+          bool kp[4] = {true, true, true, true};
+          if (p.thr_drop) dropout_keep4(salt_drop, (uint32_t)idx, p.thr_drop, kp);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            float e = v[c];
+            if (p.thr_drop) e = kp[c] ? e * p.scale_drop : 0.f;
+            v[c] = e * gelu_grad_f(pre[i][j][c]);
+          }
+          st4bf(reinterpret_cast<bf16*>(p.C) + idx, v);
+        } else if (EPI == EPI_EMBED) {
+          v += pre[i][j];
+          if (p.thr_drop) {
+            bool kp[4];
+            dropout_keep4(salt_drop, (uint32_t)idx, p.thr_drop, kp);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[c] = kp[c] ? v[c] * p.scale_drop : 0.f;
+          }
+          st4(reinterpret_cast<float*>(p.C) + idx, v);
+          if (prod) {
+            part[i][j / 2] = f2add(part[i][j / 2], make_float2((v[0] + v[1]) + (v[2] + v[3]),
+                                                               (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3])));
+            st4bf_pub<PUB>(p.xb_out + idx, v);
+          }
+        }
+      }
+    }
+    if (prod) {
+      // the 4 lanes of a row (q = 0..3: lanes x, x+4, x+8, x+12 of the 16-lane
+      // group) hold 32 consecutive columns per slot: reduce, one float2 store per
+      // (row, slot)
+      const int np_out = p.N / LN_SLOT;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int sl = 0; sl < SL; ++sl) {
+          float2 t = part[i][sl];
+          t = f2add(t, f2xor<4>(t));
+          t = f2add(t, f2xor<8>(t));
+          if ((li >> 2) == 0 && rowm[i] >= 0)
+            st2f_pub<PUB>(p.st_out + 2 * ((size_t)fold_token_row<EPI>(p, rowm[i]) * np_out + colbase / LN_SLOT + sl),
+                          t);
+        }
+    }
+  }
+};
+
+template <int EPI, int FM, int FN>
+__device__ __forceinline__ void run_epilogue_vec(const GemmParams& p, const f32x4 (&acc)[FM][FN], int mb, int nb,
+                                                 int g, int li) {
+  VecEpi<EPI, FM, FN> ep;
+  ep.prefetch(p, mb, nb, g, li);
+  ep.finish(p, acc, li);
+}
+
+// epilogues that take the quad-transposed vector path
+template <int EPI>
+struct UsesVecEpi {
+  // HEAD: columns not contiguous.  ATOMIC: in the accumulator layout one atomic
+  // instruction covers 4 rows x 64 B; after the quad transpose it would touch 16
+  // rows (4x the cache lines per instruction) - measured 10% slower per step.
+  static constexpr bool value = EPI != EPI_HEAD && EPI != EPI_ATOMIC;
+};
+
+template <int EPI, int FM, int FN>
+__device__ __forceinline__ void run_epilogue(const GemmParams& p, const f32x4 (&acc)[FM][FN], int mb, int nb,
+                                             int g, int li) {
+  if (!UsesVecEpi<EPI>::value || p.debug == 3) run_epilogue_scalar<EPI, FM, FN>(p, acc, mb, nb, g, li);
+  else run_epilogue_vec<EPI, FM, FN>(p, acc, mb, nb, g, li);
+}
+
+
+}  // namespace dc

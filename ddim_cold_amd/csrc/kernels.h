@@ -73,6 +73,10 @@ void gemm_wgrad(const GemmArgs& a, int splits, hipStream_t stream);
 // grouped dW += dy^T x for n <= 6 problems in one launch; splits == 1 -> plain
 // read-add-write (one writer per element), else fp32 atomics over token slices
 void gemm_wgrad_group(const GemmArgs* probs, int n, int splits, hipStream_t stream);
+// dgrad (EPI_BF16 / EPI_F32 with a.splits K slices, or EPI_DGELU) carrying n <= 6
+// weight-gradient problems (dW += dy^T x, fp32 atomics over wsplits token slices)
+// as extra workgroups of the same launch
+void gemm_dgrad_ride(const GemmArgs& a, int epi, const GemmArgs* probs, int n, int wsplits, hipStream_t stream);
 
 // Row-panel GEMM + residual + LayerNorm epilogue (gemm_ln.hip)
 struct GemmLnArgs {

@@ -50,6 +50,11 @@ FOLD_LN = os.environ.get("DDIM_COLD_LN_FOLD", "1") == "1"
 # 15.3 + 6.1 at the sampler's N=64 -- no better as a kernel, and the step /
 # sampler graphs get 1.5 % slower -> opt-in (DDIM_COLD_QKV_ATTN=1).
 FUSE_QKV_ATTN = os.environ.get("DDIM_COLD_QKV_ATTN", "0") == "1"
+# Weight gradients ride in the input-gradient launches (csrc/gemm.hip
+# gemm_dgrad_ride_kernel): fc2 (+ head) with the GELU' dgrad, the next block's
+# QKV with the fc1 dgrad, fc1 with the proj dgrad, proj with the QKV dgrad; only
+# block 0's QKV (+ patch embedding) keeps a grouped launch of its own.
+WGRAD_RIDE = os.environ.get("DDIM_COLD_WGRAD_RIDE", "1") == "1"
 # dtype of the bf16 activation copies / folded weights the program allocates
 # (tests on CPU switch it to fp32 to isolate the program logic from rounding)
 ACT_DTYPE = torch.bfloat16
@@ -432,6 +437,9 @@ class ViTProgram:
         """
         def ws(k):
             return None if ln_ws is None else ln_ws[k]
+        # weight gradients ride in the next input-gradient launch (default), unless
+        # the caller supplies its own wgrad callable or a side stream
+        ride = WGRAD_RIDE and wgrad is None and wgrad_stream is None
         batch = None
         if wgrad is None:
             batch = wgrad = ops.WgradBatch(wgrad_stream)
@@ -454,29 +462,48 @@ class ViTProgram:
         def ln_out(lo):
             return torch.empty(M, D, dtype=ACT_DTYPE, device=dtok.device) if fold else lo
         f32 = not DGRAD_BF16
+        keep = []
         dlf = ops.linear_dgrad(dtok, P.head_w, f32)
         lf = ln_out(S.lf)
         _, _, _, _, sf2, sd2 = block_sites(L - 1)
         g, gy = ops.layernorm_bwd(dlf, S.xL, S.mf, S.rf, P.nw, None, G.nw, G.nb, N, rng, sf2, pd, sd2,
                                   dpr[L - 1], True, ws(0), beta=P.nb if fold else None, y_out=lf if fold else None)
-        wgrad(dtok, lf, G.head_w, G.head_b)
-        keep = []
+        if ride:
+            riders = [(dtok, lf, G.head_w, G.head_b)]  # joins block L-1's first launch
+            qkv_job = None  # the previous block's QKV weight gradient (rides on the fc1 dgrad)
+        else:
+            wgrad(dtok, lf, G.head_w, G.head_b)
         for i in range(L - 1, -1, -1):
             x0, l1, m1, r1, qkv, o, lse, x1, l2, m2, r2, u, h = S.blocks[i]
             bp, bg = P.blocks[i], G.blocks[i]
             sa, sp, sd1, sf1, _, _ = block_sites(i)
-            wgrad(gy, h, bg.fc2_w, bg.fc2_b)
-            du = ops.linear_dgrad_gelu(gy, bp.fc2_w, u, rng, sf1, pd)
-            dl2 = ops.linear_dgrad(du, bp.fc1_w, f32)
+            if ride:
+                du = ops.linear_dgrad_ride(gy, bp.fc2_w, riders + [(gy, h, bg.fc2_w, bg.fc2_b)],
+                                           gelu=(u, rng, sf1, pd))
+                dl2 = ops.linear_dgrad_ride(du, bp.fc1_w, [qkv_job] if qkv_job else [], f32)
+                if qkv_job is not None:
+                    yield i + 1  # block i+1's last weight gradient is issued
+                riders, qkv_job = [], None
+            else:
+                wgrad(gy, h, bg.fc2_w, bg.fc2_b)
+                du = ops.linear_dgrad_gelu(gy, bp.fc2_w, u, rng, sf1, pd)
+                dl2 = ops.linear_dgrad(du, bp.fc1_w, f32)
             k2 = 1 + 2 * (L - 1 - i)
             l2 = ln_out(l2)
             g1, gy1 = ops.layernorm_bwd(dl2, x1, m2, r2, bp.n2w, g, bg.n2w, bg.n2b, N, rng, sp, pd, sd1, dpr[i],
                                         True, ws(k2), beta=bp.n2b if fold else None, y_out=l2 if fold else None)
-            wgrad(du, l2, bg.fc1_w, bg.fc1_b)
-            wgrad(gy1, o, bg.proj_w, bg.proj_b)
-            do = ops.linear_dgrad(gy1, bp.proj_w, False)
+            if ride:
+                do = ops.linear_dgrad_ride(gy1, bp.proj_w, [(du, l2, bg.fc1_w, bg.fc1_b)])
+            else:
+                wgrad(du, l2, bg.fc1_w, bg.fc1_b)
+                wgrad(gy1, o, bg.proj_w, bg.proj_b)
+                do = ops.linear_dgrad(gy1, bp.proj_w, False)
             dqkv = ops.attn_bwd(do, qkv, o, lse, c.scale, rng, sa, ad)
-            dl1 = ops.linear_dgrad(dqkv, bp.qkv_w, f32, QKV_DGRAD_SPLITS if 3 * D >= 768 else 1)
+            qs = QKV_DGRAD_SPLITS if 3 * D >= 768 else 1
+            if ride:
+                dl1 = ops.linear_dgrad_ride(dqkv, bp.qkv_w, [(gy1, o, bg.proj_w, bg.proj_b)], f32, qs)
+            else:
+                dl1 = ops.linear_dgrad(dqkv, bp.qkv_w, f32, qs)
             l1 = ln_out(l1)
             fk = dict(beta=bp.n1b, y_out=l1) if fold else {}
             if i > 0:
@@ -486,8 +513,11 @@ class ViTProgram:
             else:
                 g, gy = ops.layernorm_bwd(dl1, x0, m1, r1, bp.n1w, g1, bg.n1w, bg.n1b, N, rng, 0, 0.0, 0, 0.0,
                                           False, ws(k2 + 1), **fk)
-            wgrad(dqkv, l1, bg.qkv_w, bg.qkv_b)
             keep.append((gy1, du, dqkv, l1, l2))
+            if ride and i > 0:
+                qkv_job = (dqkv, l1, bg.qkv_w, bg.qkv_b)
+                continue
+            wgrad(dqkv, l1, bg.qkv_w, bg.qkv_b)
             if i == 0 and embed_with_block0:
                 gpatch = self._embed_backward(P, G, S, g, rng, pd, wgrad, ln_final)
             flush()

@@ -256,6 +256,24 @@ def linear_wgrad_group(jobs):
         ref.linear_wgrad(dy, x, dw, db)
 
 
+def linear_dgrad_ride(dy, w, jobs, out_fp32: bool = False, splits: int = 1, gelu=None):
+    """:func:`linear_dgrad` (or, with ``gelu = (u, rng, site, p)``,
+    :func:`linear_dgrad_gelu`) with the weight-gradient ``jobs`` (``(dy, x, dw,
+    db)`` as :func:`linear_wgrad_group`) riding in the SAME launch as extra
+    workgroups (csrc/gemm.hip ``gemm_dgrad_ride_kernel``)."""
+    if _hip(dy):
+        dys, xs, dws, dbs = (list(z) for z in zip(*jobs)) if jobs else ([], [], [], [])
+        if gelu is not None:
+            u, rng, site, p = gelu
+            return _ops().linear_dgrad_ride(dy, w, 1, False, 1, u, rng, int(site), float(p), dys, xs, dws, dbs)
+        return _ops().linear_dgrad_ride(dy, w, 0, bool(out_fp32), int(splits), None, None, 0, 0.0,
+                                        dys, xs, dws, dbs)
+    out = ref.linear_dgrad_gelu(dy, w, *gelu) if gelu is not None else ref.linear_dgrad(dy, w, out_fp32, splits)
+    for j in jobs:
+        ref.linear_wgrad(*j)
+    return out
+
+
 class WgradBatch:
     """Collects weight-gradient GEMMs and issues them as one grouped launch on ``flush``.
 

@@ -276,6 +276,45 @@ def test_linear_wgrad_group_variants(env):
     assert r.returncode == 0, r.stdout[-3000:]
 
 
+@pytest.mark.parametrize("mode,M,Nout,K,splits,riders", [
+    ("bf16", 2080, 384, 384, 1, [(384, 384)]),               # fc1 dgrad + fc1 wgrad
+    ("bf16", 2080, 1152, 384, 2, [(1152, 384)]),             # QKV dgrad (K split) + next QKV wgrad
+    ("f32", 2080, 384, 384, 1, [(384, 384), (192, 384)]),    # fp32 out, two riders
+    ("gelu", 2080, 384, 384, 1, [(192, 384), (384, 384)]),   # GELU' dgrad + head + fc2 wgrad
+    ("bf16", 4160, 384, 384, 1, [(384, 384)]),               # 64x64 dgrad tiles
+    ("bf16", 300, 256, 128, 1, [(256, 128), (64, 96), (128, 64)]),
+    ("gelu", 130, 256, 256, 1, []),                          # no riders: plain dgrad
+])
+def test_dgrad_ride(mode, M, Nout, K, splits, riders):
+    """dgrad with weight-gradient riders in the same launch == dgrad + reference wgrads."""
+    dy, w = bf(M, Nout), bf(Nout, K, scale=0.05)
+    r = rng()
+    u = bf(M, K)
+    jobs, refs = [], []
+    for i, (nout, k) in enumerate(riders):
+        gy, x = bf(M, nout), bf(M, k)
+        dw0 = torch.randn(nout, k, device=DEV) * 0.1
+        db0 = torch.randn(nout, device=DEV) if i % 2 == 0 else None
+        jobs.append((gy, x, dw0.clone(), db0.clone() if db0 is not None else None))
+        dw2, db2 = dw0.clone(), (db0.clone() if db0 is not None else None)
+        ref.linear_wgrad(gy, x, dw2, db2)
+        refs.append((dw2, db2))
+    if mode == "gelu":
+        dx = ops.linear_dgrad_ride(dy, w, jobs, gelu=(u, r, 11, 0.1))
+        dxr = ref.linear_dgrad_gelu(dy, w, u, r, 11, 0.1)
+        close(dx, dxr, 2e-2, 1e-2, "dgelu")
+    else:
+        f32 = mode == "f32"
+        dx = ops.linear_dgrad_ride(dy, w, jobs, f32, splits)
+        dxr = ref.linear_dgrad(dy, w, f32, splits)
+        assert dx.shape == dxr.shape
+        close(dx, dxr, 1e-3 if f32 else 2e-2, 1e-2, "dgrad")
+    for (_, _, dw, db), (dw2, db2) in zip(jobs, refs):
+        close(dw, dw2, 2e-2, 1e-4, "rider dw")
+        if db is not None:
+            close(db, db2, 2e-2, 1e-4, "rider db")
+
+
 def _wgrad_group_check(big):
     """Grouped launch == per-problem reference (unsplit read-add-write and split atomic paths)."""
     M = 2080

@@ -46,6 +46,41 @@ def test_program_fwd_bwd_vs_reference_ops(name):
         assert _rel(g1[n], g2[n]) < 8e-2, n
 
 
+@pytest.mark.parametrize("name", ["vit_tiny", "oxford_flower"])
+@pytest.mark.parametrize("embed_with_block0", [True, False])
+def test_backward_wgrad_ride_matches_grouped(name, embed_with_block0, monkeypatch):
+    """Weight gradients riding in the dgrad launches == one grouped launch per block
+    (same backward otherwise; fp32 atomics -> summation order differs slightly), and
+    the block yields keep their order (L-1 .. 0, -1)."""
+    from ddim_cold_amd.models import program as pm
+    torch.manual_seed(0)
+    m = build_model(name).to(DEV).train()
+    prog = ViTProgram.from_model(m)
+    P = model_tensors(m)
+    B = 8
+    img = torch.randn(B, 3, 64, 64, device=DEV).clamp(-1, 1)
+    tgt = torch.randn_like(img).clamp(-1, 1)
+    t = torch.randint(0, 2000, (B,), device=DEV)
+    r = torch.tensor([77, 3], dtype=torch.int64, device=DEV)
+    with torch.no_grad():
+        out, S = prog.forward(P, img, t, r, True)
+        _, dtok = ops.smooth_l1_fwd_bwd(out, tgt, prog.cfg.tokens, prog.cfg.patch)
+    results = []
+    for ride in (True, False):
+        monkeypatch.setattr(pm, "WGRAD_RIDE", ride)
+        grads = {n: torch.zeros_like(p) for n, p in m.named_parameters()}
+        G = collect(grads, prog.cfg.depth, prog.cfg.dim)
+        with torch.no_grad():
+            order = list(prog.backward_iter(P, G, S, dtok, r, True, embed_with_block0=embed_with_block0))
+        torch.cuda.synchronize()
+        assert order == list(range(prog.cfg.depth - 1, -1, -1)) + [-1]
+        results.append(grads)
+    g1, g2 = results
+    for n in g1:
+        assert g1[n].abs().max() > 0 or g2[n].abs().max() == 0, n
+        assert _rel(g1[n], g2[n]) < 1e-4, n
+
+
 def test_autograd_wrapper_matches_plain_model():
     torch.manual_seed(0)
     m = build_model("vit_tiny").to(DEV).eval()  # eval: no dropout -> deterministic comparison
