@@ -630,6 +630,79 @@ Tensor linear_dgrad_ride(Tensor dy, Tensor w, int64_t mode, bool out_fp32, int64
   return dx;
 }
 
+// Image-group persistent forward of all transformer blocks (csrc/vit_group.hip).
+// ts: VG_TS tensors per block in the order below (None for the optional ones).
+constexpr int VG_TS = 28;
+bool vit_group_ok(int64_t D, int64_t H, int64_t hd, int64_t N, int64_t L) {
+  return vit_group_supported((int)D, (int)H, (int)hd, (int)N, (int)L);
+}
+void vit_group_fwd(std::vector<c10::optional<Tensor>> ts, int64_t L, int64_t B, int64_t N, std::vector<int64_t> sites,
+                   std::vector<double> p_dp, Tensor rng, double p_drop, double p_attn, double scale, double eps,
+                   Tensor ctr, Tensor err, c10::optional<Tensor> stamps) {
+  TORCH_CHECK(L >= 1 && L <= VG_MAXL && (int64_t)ts.size() == L * VG_TS, "vit_group_fwd: tensor list size");
+  TORCH_CHECK((int64_t)sites.size() == 6 * L && (int64_t)p_dp.size() == L, "vit_group_fwd: sites / drop-path list");
+  check_rng(rng);
+  CHECK_IN(ctr, at::kInt); CHECK_IN(err, at::kInt);
+  TORCH_CHECK(ctr.numel() >= B * 16, "vit_group_fwd: counter buffer too small");
+  const int D = 384, M = (int)(B * N);
+  const c10::DeviceGuard guard(rng.device());
+  VgArgs a;
+  a.L = (int)L; a.B = (int)B; a.N = (int)N; a.D = D; a.H = 12; a.hd = 32;
+  TORCH_CHECK(vit_group_supported(a.D, a.H, a.hd, a.N, a.L), "vit_group_fwd: unsupported shape");
+  // (required?, dtype, elements) per slot
+  struct Slot { bool req; c10::ScalarType dt; int64_t n; };
+  const int64_t MD = (int64_t)M * D;
+  const Slot slots[VG_TS] = {
+      {true, BF16, 3 * D * D}, {true, F32, 3 * D}, {true, F32, 3 * D}, {true, BF16, D * D}, {true, F32, D},
+      {true, BF16, D * D}, {true, F32, D}, {true, F32, D}, {true, BF16, D * D}, {true, F32, D},
+      {true, BF16, MD}, {true, F32, (int64_t)M * (D / 32) * 2}, {true, F32, MD},
+      {false, BF16, 3 * MD}, {true, BF16, MD}, {false, F32, B * 12 * N}, {true, F32, MD}, {true, BF16, MD},
+      {true, F32, (int64_t)M * (D / 32) * 2}, {true, BF16, MD}, {true, BF16, MD}, {true, F32, MD}, {true, BF16, MD},
+      {true, F32, (int64_t)M * (D / 32) * 2}, {false, F32, M}, {false, F32, M}, {false, F32, M}, {false, F32, M}};
+  std::vector<void*> ptr(ts.size(), nullptr);
+  for (size_t i = 0; i < ts.size(); ++i) {
+    const Slot& sl = slots[i % VG_TS];
+    if (!ts[i].has_value() || !ts[i]->defined()) {
+      TORCH_CHECK(!sl.req, "vit_group_fwd: tensor ", i % VG_TS, " of block ", i / VG_TS, " is required");
+      continue;
+    }
+    const Tensor& t = *ts[i];
+    CHECK_IN(t, sl.dt);
+    TORCH_CHECK(t.device() == rng.device(), "vit_group_fwd: tensors on different devices");
+    TORCH_CHECK(t.numel() == sl.n, "vit_group_fwd: tensor ", i % VG_TS, " of block ", i / VG_TS, " has ", t.numel(),
+                " elements, expected ", sl.n);
+    ptr[i] = t.data_ptr();
+  }
+  for (int l = 0; l < L; ++l) {
+    void** q = ptr.data() + (size_t)l * VG_TS;
+    VgBlock& b = a.blk[l];
+    b.qkv_wf = q[0]; b.qkv_bf = (const float*)q[1]; b.qkv_c = (const float*)q[2];
+    b.proj_w = q[3]; b.proj_b = (const float*)q[4];
+    b.fc1_wf = q[5]; b.fc1_bf = (const float*)q[6]; b.fc1_c = (const float*)q[7];
+    b.fc2_w = q[8]; b.fc2_b = (const float*)q[9];
+    b.xb_in = q[10]; b.st_in = (const float*)q[11]; b.x_in = (const float*)q[12];
+    b.qkv = q[13]; b.o = q[14]; b.lse = (float*)q[15]; b.x1 = (float*)q[16]; b.x1b = q[17]; b.st1 = (float*)q[18];
+    b.u = q[19]; b.h = q[20]; b.x_out = (float*)q[21]; b.xb_out = q[22]; b.st_out = (float*)q[23];
+    b.m1 = (float*)q[24]; b.r1 = (float*)q[25]; b.m2 = (float*)q[26]; b.r2 = (float*)q[27];
+    const int64_t* s6 = sites.data() + 6 * l;
+    b.site_a = (int)s6[0]; b.site_p = (int)s6[1]; b.site_d1 = (int)s6[2];
+    b.site_f1 = (int)s6[3]; b.site_f2 = (int)s6[4]; b.site_d2 = (int)s6[5];
+    b.p_dp = p_dp[l];
+    TORCH_CHECK((b.m1 == nullptr) == (b.r1 == nullptr) && (b.m2 == nullptr) == (b.r2 == nullptr),
+                "vit_group_fwd: mean / rstd outputs come in pairs");
+  }
+  a.rng = rng.data_ptr<int64_t>();
+  a.p_drop = p_drop; a.p_attn = p_attn; a.scale = (float)scale; a.eps = (float)eps;
+  a.ctr = reinterpret_cast<unsigned*>(ctr.data_ptr<int>());
+  a.err = reinterpret_cast<unsigned*>(err.data_ptr<int>());
+  if (stamps.has_value() && stamps->defined()) {
+    CHECK_IN((*stamps), at::kLong);
+    TORCH_CHECK(stamps->numel() >= B * 6 * VG_MAXL * 32, "vit_group_fwd: stamps buffer too small");
+    a.stamps = stamps->data_ptr();
+  }
+  vit_group_fwd_launch(a, cur_stream());
+}
+
 std::tuple<Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma,
                                          c10::optional<Tensor> g_res, Tensor dgamma, Tensor dbeta, int64_t N,
                                          Tensor rng, int64_t site_drop, double p_drop, int64_t site_dp, double p_dp,
@@ -983,6 +1056,9 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("linear_dgrad_gelu(Tensor dy, Tensor w, Tensor u, Tensor rng, int site, float p) -> Tensor");
   m.def("linear_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, Tensor(b!)? db) -> ()");
   m.def("linear_wgrad_group(Tensor[] dys, Tensor[] xs, Tensor(a!)[] dws, Tensor(b!)?[] dbs) -> ()");
+  m.def("vit_group_ok(int D, int H, int hd, int N, int L) -> bool", &vit_group_ok);
+  m.def("vit_group_fwd(Tensor?[] ts, int L, int B, int N, int[] sites, float[] p_dp, Tensor rng, float p_drop, "
+        "float p_attn, float scale, float eps, Tensor(a!) ctr, Tensor(b!) err, Tensor(c!)? stamps=None) -> ()");
   m.def("linear_dgrad_ride(Tensor dy, Tensor w, int mode, bool out_fp32, int splits, Tensor? u, Tensor? rng, "
         "int site, float p, Tensor[] dys, Tensor[] xs, Tensor(a!)[] dws, Tensor(b!)?[] dbs) -> Tensor");
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor? g_res, "
@@ -1033,6 +1109,7 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("linear_residual_ln_fwd", &linear_residual_ln_fwd);
   m.impl("linear_wgrad_group", &linear_wgrad_group);
   m.impl("linear_dgrad_ride", &linear_dgrad_ride);
+  m.impl("vit_group_fwd", &vit_group_fwd);
   m.impl("layernorm_bwd", &layernorm_bwd);
   m.impl("replica_reduce_", &replica_reduce_);
   m.impl("ln_fold_", &ln_fold_);

@@ -428,6 +428,14 @@ __device__ __forceinline__ void st4bf(bf16* p, const f32x4& v) {
   b[0] = f2bf(v[0]); b[1] = f2bf(v[1]); b[2] = f2bf(v[2]); b[3] = f2bf(v[3]);
   *reinterpret_cast<bf16x4*>(p) = b;
 }
+// {sum, sum of squares} of 4 consecutive outputs (LayerNorm statistics
+// producer).  Explicit fma so every kernel that produces statistics rounds
+// identically, whatever the compiler's contraction choice in its context.
+__device__ __forceinline__ float2 stat4(const f32x4& v) {
+  return make_float2((v[0] + v[1]) + (v[2] + v[3]),
+                     __builtin_fmaf(v[0], v[0], v[1] * v[1]) + __builtin_fmaf(v[2], v[2], v[3] * v[3]));
+}
+
 // bf16x4 store, write-through (sc1) when the bytes are handed to another workgroup of the launch
 template <bool PUB>
 __device__ __forceinline__ void st4bf_pub(bf16* p, const f32x4& v) {
@@ -599,8 +607,7 @@ struct VecEpi {
           }
           st4(reinterpret_cast<float*>(p.C) + idx, v);
           if (prod) {
-            part[i][j / 2] = f2add(part[i][j / 2], make_float2((v[0] + v[1]) + (v[2] + v[3]),
-                                                               (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3])));
+            part[i][j / 2] = f2add(part[i][j / 2], stat4(v));
             st4bf_pub<PUB>(p.xb_out + idx, v);
           }
         } else if (EPI == EPI_GELU) {
@@ -635,8 +642,7 @@ struct VecEpi {
           }
           st4(reinterpret_cast<float*>(p.C) + idx, v);
           if (prod) {
-            part[i][j / 2] = f2add(part[i][j / 2], make_float2((v[0] + v[1]) + (v[2] + v[3]),
-                                                               (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3])));
+            part[i][j / 2] = f2add(part[i][j / 2], stat4(v));
             st4bf_pub<PUB>(p.xb_out + idx, v);
           }
         }

@@ -235,3 +235,33 @@ struct QkvArgs {
 };
 bool qkv_attn_supported(int N, int hd, int D);
 void qkv_attn_fwd_launch(const QkvArgs& a, hipStream_t stream);
+
+// Image-group persistent forward of all transformer blocks (vit_group.hip):
+// D = 384, 12 heads of 32, N <= 80 tokens, LayerNorm-folded weights; one
+// launch (per <= CUs/6 images) replaces the 5 launches per block.
+constexpr int VG_MAXL = 8;
+struct VgBlock {
+  const void *qkv_wf = nullptr, *proj_w = nullptr, *fc1_wf = nullptr, *fc2_w = nullptr;  // bf16
+  const float *qkv_bf = nullptr, *qkv_c = nullptr, *proj_b = nullptr, *fc1_bf = nullptr, *fc1_c = nullptr,
+              *fc2_b = nullptr;
+  const void* xb_in = nullptr;      // [M][D] bf16 residual copy (block input)
+  const float* st_in = nullptr;     // [M][D/32][2] its LayerNorm statistics slots
+  const float* x_in = nullptr;      // [M][D] fp32 residual stream (block input)
+  void *qkv = nullptr, *o = nullptr, *x1b = nullptr, *u = nullptr, *h = nullptr, *xb_out = nullptr;  // bf16
+  float *lse = nullptr, *x1 = nullptr, *st1 = nullptr, *x_out = nullptr, *st_out = nullptr;
+  float *m1 = nullptr, *r1 = nullptr, *m2 = nullptr, *r2 = nullptr;  // optional (saved for the backward)
+  int site_a = 0, site_p = 0, site_d1 = 0, site_f1 = 0, site_f2 = 0, site_d2 = 0;
+  double p_dp = 0.0;
+};
+struct VgArgs {
+  VgBlock blk[VG_MAXL];
+  int L = 0, B = 0, N = 0, D = 0, H = 0, hd = 0;
+  const int64_t* rng = nullptr;
+  double p_drop = 0.0, p_attn = 0.0;
+  float scale = 1.f, eps = 1e-5f;
+  unsigned* ctr = nullptr;  // [B * 16] hand-off counters (zeroed by the launcher)
+  unsigned* err = nullptr;  // set to nonzero if a hand-off wait gave up
+  void* stamps = nullptr;   // optional int64 [grid][VG_MAXL][16] phase timestamps (profiling)
+};
+bool vit_group_supported(int D, int H, int hd, int N, int L);
+void vit_group_fwd_launch(const VgArgs& a, hipStream_t stream);

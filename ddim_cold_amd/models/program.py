@@ -55,6 +55,16 @@ FUSE_QKV_ATTN = os.environ.get("DDIM_COLD_QKV_ATTN", "0") == "1"
 # QKV with the fc1 dgrad, fc1 with the proj dgrad, proj with the QKV dgrad; only
 # block 0's QKV (+ patch embedding) keeps a grouped launch of its own.
 WGRAD_RIDE = os.environ.get("DDIM_COLD_WGRAD_RIDE", "1") == "1"
+# All transformer blocks of the LayerNorm-folded forward as ONE persistent
+# launch of image groups (csrc/vit_group.hip; ViT-tiny shape) instead of 5
+# launches per block.  Same math, bit-identical outputs (tests/test_group_fwd_gpu.py).
+# Measured on MI355X (tools/vg_stamps.py, tools/gpu_group_ab.sh): ~40 us per
+# block at B=32 -- each of the 4 hand-offs per block costs ~1 us wait + ~2.8 us
+# gather of the 50 KB activation panel through memory + the write-through
+# drain, which eats the launch overhead it removes -- so the train step is
+# 0.890 vs 0.871 ms/step and the B=64 sampler (two launches: one 156 KiB-LDS
+# workgroup per CU) is slower too: opt-in (DDIM_COLD_GROUP_FWD=1).
+GROUP_FWD = os.environ.get("DDIM_COLD_GROUP_FWD", "0") == "1"
 # dtype of the bf16 activation copies / folded weights the program allocates
 # (tests on CPU switch it to fp32 to isolate the program logic from rounding)
 ACT_DTYPE = torch.bfloat16
@@ -372,7 +382,13 @@ class ViTProgram:
             return (torch.empty(M, dtype=torch.float32, device=dev),
                     torch.empty(M, dtype=torch.float32, device=dev)) if save else (None, None)
         fused = FUSE_QKV_ATTN and ops.qkv_attn_supported(N, D // c.heads, D)
-        for i, bp in enumerate(P.blocks):
+        if (GROUP_FWD and not fused and dev.type == "cuda" and P.blocks[0].qkv_wf.dtype == torch.bfloat16
+                and c.hidden == D and ops.vit_group_ok(D, c.heads, D // c.heads, N, L)):
+            x, xb = self._blocks_group(P, x, xb, st, rng, B, pd, ad, dpr, S, stats)
+            blocks = ()
+        else:
+            blocks = enumerate(P.blocks)
+        for i, bp in blocks:
             sa, sp, sd1, sf1, sf2, sd2 = block_sites(i)
             x0 = x
             m1, r1 = stats()
@@ -411,6 +427,48 @@ class ViTProgram:
         if save:
             S.xL, S.lf, S.mf, S.rf = x, None, mf, rf
         return out, S
+
+    def _blocks_group(self, P: ModelTensors, x, xb, st, rng, B: int, pd: float, ad: float, dpr, S, stats):
+        """Every transformer block of the folded forward in ONE persistent launch
+        (:func:`ops.vit_group_fwd`, csrc/vit_group.hip): same tensors, same values
+        as the per-op sequence of :meth:`_forward_folded`.  Returns the last
+        block's (fp32 residual stream, bf16 copy)."""
+        c = self.cfg
+        N, D, L = c.tokens, c.dim, c.depth
+        M, dev = B * N, x.device
+        save = S is not None
+
+        def bf16(*shape):
+            return torch.empty(*shape, dtype=ACT_DTYPE, device=dev)
+
+        def f32(*shape):
+            return torch.empty(*shape, dtype=torch.float32, device=dev)
+        ts, sites, dps, saved = [], [], [], []
+        for i, bp in enumerate(P.blocks):
+            x0 = x
+            m1, r1 = stats()
+            m2, r2 = stats()
+            qkv = bf16(3, B, c.heads, N, D // c.heads)
+            o, lse = bf16(B, N, D), (f32(B, c.heads, N) if save else None)
+            x1, x1b, u, h = f32(M, D), bf16(M, D), bf16(M, c.hidden), bf16(M, c.hidden)
+            x, xb_new = f32(M, D), bf16(M, D)
+            ts += [bp.qkv_wf, bp.qkv_bf, bp.qkv_c, bp.proj_w, bp.proj_b, bp.fc1_wf, bp.fc1_bf, bp.fc1_c,
+                   bp.fc2_w, bp.fc2_b, xb, st[2 * i], x0,
+                   qkv if save else None, o, lse, x1, x1b, st[2 * i + 1], u, h, x, xb_new, st[2 * i + 2],
+                   m1, r1, m2, r2]
+            sites += list(block_sites(i))
+            dps.append(dpr[i])
+            if save:
+                saved.append((x0, None, m1, r1, qkv, o.view(M, D), lse, x1, None, m2, r2, u, h))
+            xb = xb_new
+        if getattr(self, "_vg_err", None) is None or self._vg_err.device != dev:
+            self._vg_err = torch.zeros(1, dtype=torch.int32, device=dev)
+        ctr = torch.empty(B * 16, dtype=torch.int32, device=dev)
+        ops.vit_group_fwd(ts, L, B, N, sites, dps, rng, pd, ad, c.scale, c.eps, ctr, self._vg_err,
+                          getattr(self, "vg_stamps", None))
+        if save:
+            S.blocks.extend(saved)
+        return x, xb
 
     def supports_fused_loss(self, P: ModelTensors) -> bool:
         return P.folded and fold_width_ok(self.cfg.dim)

@@ -256,6 +256,20 @@ def linear_wgrad_group(jobs):
         ref.linear_wgrad(dy, x, dw, db)
 
 
+def vit_group_ok(D: int, H: int, hd: int, N: int, L: int) -> bool:
+    """Shapes the image-group persistent block forward covers (csrc/vit_group.hip)."""
+    return _ext.available() and bool(_ops().vit_group_ok(D, H, hd, N, L))
+
+
+def vit_group_fwd(ts, L: int, B: int, N: int, sites, p_dp, rng, p_drop: float, p_attn: float, scale: float,
+                  eps: float, ctr, err, stamps=None):
+    """All transformer blocks of the LayerNorm-folded forward in one persistent
+    launch (GPU only; ``ts``: 28 tensors per block, see csrc/bindings.cpp).
+    ``stamps`` (int64 [B*6, 8, 16], optional): per-workgroup phase timestamps."""
+    _ops().vit_group_fwd(ts, L, B, N, [int(v) for v in sites], [float(v) for v in p_dp], rng, float(p_drop),
+                         float(p_attn), float(scale), float(eps), ctr, err, stamps)
+
+
 def linear_dgrad_ride(dy, w, jobs, out_fp32: bool = False, splits: int = 1, gelu=None):
     """:func:`linear_dgrad` (or, with ``gelu = (u, rng, site, p)``,
     :func:`linear_dgrad_gelu`) with the weight-gradient ``jobs`` (``(dy, x, dw,
