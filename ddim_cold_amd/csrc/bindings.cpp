@@ -630,6 +630,21 @@ Tensor linear_dgrad_ride(Tensor dy, Tensor w, int64_t mode, bool out_fp32, int64
   return dx;
 }
 
+// fp32 <-> bf16 gradient wire (csrc/comm_wire.hip): one fused 16-B-vector
+// kernel each way (the torch-collective bf16 wire path of the train engine)
+void wire_pack(Tensor src, Tensor dst) {
+  CHECK_IN(src, F32); CHECK_IN(dst, BF16);
+  TORCH_CHECK(src.numel() == dst.numel(), "wire_pack: sizes");
+  const c10::DeviceGuard guard(src.device());
+  wire_pack_launch(src.data_ptr<float>(), dst.data_ptr(), src.numel(), cur_stream());
+}
+void wire_unpack(Tensor src, Tensor dst) {
+  CHECK_IN(src, BF16); CHECK_IN(dst, F32);
+  TORCH_CHECK(src.numel() == dst.numel(), "wire_unpack: sizes");
+  const c10::DeviceGuard guard(src.device());
+  wire_unpack_launch(src.data_ptr(), dst.data_ptr<float>(), src.numel(), cur_stream());
+}
+
 // Image-group persistent forward of all transformer blocks (csrc/vit_group.hip).
 // ts: VG_TS tensors per block in the order below (None for the optional ones).
 constexpr int VG_TS = 28;
@@ -1056,6 +1071,8 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("linear_dgrad_gelu(Tensor dy, Tensor w, Tensor u, Tensor rng, int site, float p) -> Tensor");
   m.def("linear_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, Tensor(b!)? db) -> ()");
   m.def("linear_wgrad_group(Tensor[] dys, Tensor[] xs, Tensor(a!)[] dws, Tensor(b!)?[] dbs) -> ()");
+  m.def("wire_pack(Tensor src, Tensor(a!) dst) -> ()");
+  m.def("wire_unpack(Tensor src, Tensor(a!) dst) -> ()");
   m.def("vit_group_ok(int D, int H, int hd, int N, int L) -> bool", &vit_group_ok);
   m.def("vit_group_fwd(Tensor?[] ts, int L, int B, int N, int[] sites, float[] p_dp, Tensor rng, float p_drop, "
         "float p_attn, float scale, float eps, Tensor(a!) ctr, Tensor(b!) err, Tensor(c!)? stamps=None) -> ()");
@@ -1110,6 +1127,8 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("linear_wgrad_group", &linear_wgrad_group);
   m.impl("linear_dgrad_ride", &linear_dgrad_ride);
   m.impl("vit_group_fwd", &vit_group_fwd);
+  m.impl("wire_pack", &wire_pack);
+  m.impl("wire_unpack", &wire_unpack);
   m.impl("layernorm_bwd", &layernorm_bwd);
   m.impl("replica_reduce_", &replica_reduce_);
   m.impl("ln_fold_", &ln_fold_);

@@ -256,6 +256,20 @@ def linear_wgrad_group(jobs):
         ref.linear_wgrad(dy, x, dw, db)
 
 
+def wire_pack(src, dst):
+    """fp32 -> bf16 (round to nearest even) into ``dst`` (gradient wire format)."""
+    if _hip(src):
+        return _ops().wire_pack(src, dst)
+    dst.copy_(src)
+
+
+def wire_unpack(src, dst):
+    """bf16 -> fp32 into ``dst``."""
+    if _hip(src):
+        return _ops().wire_unpack(src, dst)
+    dst.copy_(src)
+
+
 def vit_group_ok(D: int, H: int, hd: int, N: int, L: int) -> bool:
     """Shapes the image-group persistent block forward covers (csrc/vit_group.hip)."""
     return _ext.available() and bool(_ops().vit_group_ok(D, H, hd, N, L))

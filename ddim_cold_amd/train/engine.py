@@ -392,11 +392,11 @@ class TrainEngine:
                         self.ncomm.all_reduce_bf16_wire_(self.flat_g[a:b], self.flat_gw[a:b])
                 elif self.flat_gw is None:
                     dist.all_reduce(self.flat_g[a:b], group=self.pg)
-                else:  # bf16 wire: cast, reduce, cast back (on the comm stream)
+                else:  # bf16 wire: fused pack, reduce, fused unpack (on the comm stream)
                     w = self.flat_gw[a:b]
-                    w.copy_(self.flat_g[a:b])
+                    ops.wire_pack(self.flat_g[a:b], w)
                     dist.all_reduce(w, group=self.pg)
-                    self.flat_g[a:b].copy_(w)
+                    ops.wire_unpack(w, self.flat_g[a:b])
 
         if self.comm is not None:
             self.comm.wait_stream(torch.cuda.current_stream(self.device))
