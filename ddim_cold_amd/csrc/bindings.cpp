@@ -571,6 +571,15 @@ void linear_wgrad_group(std::vector<Tensor> dys, std::vector<Tensor> xs, std::ve
   }
 }
 
+// Every weight gradient of a training step in ONE launch (gemm_wgrad_multi_kernel)
+void linear_wgrad_multi(std::vector<Tensor> dys, std::vector<Tensor> xs, std::vector<Tensor> dws,
+                        std::vector<c10::optional<Tensor>> dbs) {
+  TORCH_CHECK(!dys.empty() && dys.size() <= 32, "wgrad_multi: 1..32 problems");
+  const c10::DeviceGuard guard(dys[0].device());
+  std::vector<GemmArgs> probs = wgrad_probs(dys, xs, dws, dbs, nullptr, nullptr);
+  gemm_wgrad_multi(probs.data(), (int)probs.size(), cur_stream());
+}
+
 // Token split of weight-gradient riders: enough slices that the riders' tiles
 // number about `target` workgroups (DDIM_COLD_RIDE_WG, default 160), >= 2
 static int ride_splits(int tiles, int min_kt) {
@@ -1076,6 +1085,7 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("vit_group_ok(int D, int H, int hd, int N, int L) -> bool", &vit_group_ok);
   m.def("vit_group_fwd(Tensor?[] ts, int L, int B, int N, int[] sites, float[] p_dp, Tensor rng, float p_drop, "
         "float p_attn, float scale, float eps, Tensor(a!) ctr, Tensor(b!) err, Tensor(c!)? stamps=None) -> ()");
+  m.def("linear_wgrad_multi(Tensor[] dys, Tensor[] xs, Tensor(a!)[] dws, Tensor(b!)?[] dbs) -> ()");
   m.def("linear_dgrad_ride(Tensor dy, Tensor w, int mode, bool out_fp32, int splits, Tensor? u, Tensor? rng, "
         "int site, float p, Tensor[] dys, Tensor[] xs, Tensor(a!)[] dws, Tensor(b!)?[] dbs) -> Tensor");
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor? g_res, "
@@ -1126,6 +1136,7 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("linear_residual_ln_fwd", &linear_residual_ln_fwd);
   m.impl("linear_wgrad_group", &linear_wgrad_group);
   m.impl("linear_dgrad_ride", &linear_dgrad_ride);
+  m.impl("linear_wgrad_multi", &linear_wgrad_multi);
   m.impl("vit_group_fwd", &vit_group_fwd);
   m.impl("wire_pack", &wire_pack);
   m.impl("wire_unpack", &wire_unpack);

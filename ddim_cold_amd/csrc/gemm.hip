@@ -739,6 +739,48 @@ DC_INST_DMA2(false, true, EPI_DGELU)
 DC_INST_DMA(64, true, true, EPI_ATOMIC)
 template __global__ void gemm_wgrad_group_kernel<EPI_ATOMIC, 4>(WgradGroup);
 template __global__ void gemm_wgrad_group_kernel<EPI_ACC, 4>(WgradGroup);
+
+// Whole-backward weight gradient: every dW += dy^T x of a training step (all
+// blocks, head, patch embedding; up to WM_MAX problems) in ONE launch after the
+// backward.  Per-block launches of ~400 workgroups are latency-bound (~15 us
+// for 3.7 GFLOP); one launch of ~1,500 workgroups keeps every CU streaming
+// operand tiles.  Problems are compact descriptors (the kernel-argument block
+// must stay under 4 KiB); one token split, so the epilogue is a plain
+// read-add-write (EPI_ACC: deterministic, no fp32 atomics).
+constexpr int WM_MAX = 32;
+struct WgDesc {
+  const bf16* A;
+  const bf16* B;
+  float* C;
+  float* bias;
+  int M, N, K, lda, ldb, ldc;
+};
+struct WgradMulti {
+  WgDesc d[WM_MAX];
+  int tile_start[WM_MAX + 1];
+  int n;
+};
+template <int S>
+__global__ __launch_bounds__(256) void gemm_wgrad_multi_kernel(WgradMulti gm) {
+  const int bid = xcd_remap(blockIdx.x, gm.tile_start[gm.n]);
+  int lo = 0, hi = gm.n - 1;  // problem owning tile `bid`: binary search over tile_start
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (bid >= gm.tile_start[mid]) lo = mid;
+    else hi = mid - 1;
+  }
+  const WgDesc& d = gm.d[lo];
+  GemmParams p{};
+  p.A = d.A; p.B = d.B; p.C = d.C; p.bias = d.bias;
+  p.M = d.M; p.N = d.N; p.K = d.K; p.lda = d.lda; p.ldb = d.ldb; p.ldc = d.ldc;
+  p.ktiles_per_split = (d.K + BK - 1) / BK;
+  const int tiles_n = (d.N + 63) / 64;
+  const int local = bid - gm.tile_start[lo];
+  const int tm = local / tiles_n;
+  gemm_dma_body<64, 64, 2, 2, true, true, EPI_ACC, S>(p, tm, local - tm * tiles_n, 0);
+}
+template __global__ void gemm_wgrad_multi_kernel<3>(WgradMulti);
+template __global__ void gemm_wgrad_multi_kernel<4>(WgradMulti);
 template __global__ void gemm_wgrad_group_kernel<EPI_ATOMIC, 6>(WgradGroup);
 template __global__ void gemm_wgrad_group_kernel<EPI_ACC, 6>(WgradGroup);
 template __global__ void gemm_wgrad_group_kernel<EPI_ATOMIC, 8>(WgradGroup);
@@ -918,6 +960,33 @@ void gemm_dgrad_ride(const GemmArgs& a, int epi, const GemmArgs* probs, int n, i
     case EPI_F32: RideTiles<EPI_F32>::launch(p, gp, dsplits, wsplits, bm, stream); break;
     default: RideTiles<EPI_DGELU>::launch(p, gp, dsplits, wsplits, bm, stream); break;
   }
+}
+
+void gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream) {
+  if (n < 1 || n > WM_MAX) throw std::runtime_error("gemm_wgrad_multi: 1..32 problems per launch");
+  WgradMulti gm{};
+  gm.n = n;
+  int tiles = 0;
+  for (int i = 0; i < n; ++i) {
+    const GemmArgs& a = probs[i];
+    if (a.N % 4 != 0) throw std::runtime_error("gemm_wgrad_multi: output width must be a multiple of 4");
+    WgDesc& d = gm.d[i];
+    d.A = reinterpret_cast<const bf16*>(a.A); d.B = reinterpret_cast<const bf16*>(a.B);
+    d.C = reinterpret_cast<float*>(a.C); d.bias = const_cast<float*>(a.bias);
+    d.M = a.M; d.N = a.N; d.K = a.K; d.lda = a.lda; d.ldb = a.ldb; d.ldc = a.ldc;
+    gm.tile_start[i] = tiles;
+    tiles += ((a.M + 63) / 64) * ((a.N + 63) / 64);
+  }
+  for (int i = n; i <= WM_MAX; ++i) gm.tile_start[i] = tiles;
+  // ring depth: 3 stages (48 KiB) -> 3 workgroups per CU, 4 (64 KiB) -> 2
+  static const int ring = [] {
+    const char* e = getenv("DDIM_COLD_WGRAD_MULTI_S");
+    return (e && atoi(e) == 4) ? 4 : 3;
+  }();
+  if (ring == 4)
+    hipLaunchKernelGGL(gemm_wgrad_multi_kernel<4>, dim3(tiles), dim3(256), 4 * (64 * 128 + 64 * 128), stream, gm);
+  else
+    hipLaunchKernelGGL(gemm_wgrad_multi_kernel<3>, dim3(tiles), dim3(256), 3 * (64 * 128 + 64 * 128), stream, gm);
 }
 
 void gemm_wgrad_group(const GemmArgs* probs, int n, int splits, hipStream_t stream) {

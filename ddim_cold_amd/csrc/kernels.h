@@ -77,6 +77,8 @@ void gemm_wgrad_group(const GemmArgs* probs, int n, int splits, hipStream_t stre
 // weight-gradient problems (dW += dy^T x, fp32 atomics over wsplits token slices)
 // as extra workgroups of the same launch
 void gemm_dgrad_ride(const GemmArgs& a, int epi, const GemmArgs* probs, int n, int wsplits, hipStream_t stream);
+// every weight gradient of a step (n <= 32 problems) in one launch, unsplit (plain read-add-write)
+void gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream);
 
 // Row-panel GEMM + residual + LayerNorm epilogue (gemm_ln.hip)
 struct GemmLnArgs {

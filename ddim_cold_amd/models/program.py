@@ -477,7 +477,7 @@ class ViTProgram:
     def backward_iter(self, P: ModelTensors, G: ModelTensors, S: Saved, dtok: torch.Tensor, rng: torch.Tensor,
                       training: bool = True, wgrad: Optional[Callable] = None,
                       ln_ws: Optional[torch.Tensor] = None, wgrad_stream=None,
-                      embed_with_block0: bool = False, ln_final=None) -> Iterator[int]:
+                      embed_with_block0: bool = False, ln_final=None, wgrad_tail: bool = False) -> Iterator[int]:
         """Hand-written backward; yields the block index after each block's grads
         are issued (L-1 first, then ..., 0) and -1 after the embedding grads.
 
@@ -492,14 +492,22 @@ class ViTProgram:
         backward runs before block 0's weight gradients are issued, so the
         patch-embedding weight gradient joins block 0's grouped launch (one
         launch fewer; no separate gradient bucket for the embeddings then).
+        ``wgrad_tail`` (single process: nothing consumes a block's gradients
+        before the optimizer): EVERY weight gradient is queued and issued as one
+        launch after the embedding backward (:func:`ops.linear_wgrad_multi`), so
+        the block yields then only mark the order, not finished gradients.
         """
         def ws(k):
             return None if ln_ws is None else ln_ws[k]
         # weight gradients ride in the next input-gradient launch (default), unless
         # the caller supplies its own wgrad callable or a side stream
-        ride = WGRAD_RIDE and wgrad is None and wgrad_stream is None
+        tail = wgrad_tail and wgrad is None and wgrad_stream is None
+        ride = WGRAD_RIDE and wgrad is None and wgrad_stream is None and not tail
         batch = None
-        if wgrad is None:
+        tail_jobs = []
+        if tail:
+            wgrad = lambda dy, x, dw, db: tail_jobs.append((dy, x, dw, db))  # noqa: E731
+        elif wgrad is None:
             batch = wgrad = ops.WgradBatch(wgrad_stream)
 
         def flush():
@@ -583,6 +591,9 @@ class ViTProgram:
         if not embed_with_block0:
             gpatch = self._embed_backward(P, G, S, g, rng, pd, wgrad, ln_final)
             flush()
+        if tail:
+            ops.linear_wgrad_multi(tail_jobs)
+            keep.append(tail_jobs)
         keep.append((gpatch, lf))
         if batch is not None:
             keep.append(batch.keep)

@@ -302,6 +302,20 @@ def linear_dgrad_ride(dy, w, jobs, out_fp32: bool = False, splits: int = 1, gelu
     return out
 
 
+def linear_wgrad_multi(jobs):
+    """Every ``(dy, x, dw, db)`` weight-gradient job of a step (<= 32) in ONE launch
+    (csrc/gemm.hip ``gemm_wgrad_multi_kernel``; unsplit, deterministic)."""
+    if not jobs:
+        return
+    if _hip(jobs[0][0]):
+        for a in range(0, len(jobs), 32):
+            dys, xs, dws, dbs = (list(z) for z in zip(*jobs[a:a + 32]))
+            _ops().linear_wgrad_multi(dys, xs, dws, dbs)
+        return
+    for dy, x, dw, db in jobs:
+        ref.linear_wgrad(dy, x, dw, db)
+
+
 class WgradBatch:
     """Collects weight-gradient GEMMs and issues them as one grouped launch on ``flush``.
 

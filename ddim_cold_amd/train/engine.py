@@ -338,9 +338,12 @@ class TrainEngine:
             if not self.segmented and self.ln_ptrs is not None and os.environ.get("DDIM_COLD_FUSE_LNFINAL", "1") != "0":
                 hi = self.ln_done_at[-1]
                 ln_final = (self.ln_ws[:hi], self.ln_ptrs[:hi], 2 * c.dim)
+            # single process: every weight gradient in one launch after the backward
+            # (no bucket needs a block's gradients early)
+            tail_w = not self.segmented and os.environ.get("DDIM_COLD_WGRAD_TAIL", "1") != "0"
             for i in self.prog.backward_iter(self.param_tensors, self.grad_tensors, S, dtok, self.rng, True,
                                              ln_ws=self.ln_ws, wgrad_stream=self.side, embed_with_block0=merge,
-                                             ln_final=ln_final):
+                                             ln_final=ln_final, wgrad_tail=tail_w):
                 if i in self.bucket_after and (self.segmented or i == -1):
                     hi = self.ln_done_at[i]
                     if ln_final is not None:

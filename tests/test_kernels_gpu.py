@@ -315,6 +315,28 @@ def test_dgrad_ride(mode, M, Nout, K, splits, riders):
             close(db, db2, 2e-2, 1e-4, "rider db")
 
 
+@pytest.mark.parametrize("n", [1, 7, 30])
+def test_linear_wgrad_multi(n):
+    """Every weight gradient of a step in one launch == per-problem reference (bias or not, odd shapes)."""
+    shapes = [(1152, 384), (384, 384), (384, 384), (384, 384), (192, 384), (384, 192), (64, 96), (256, 128)]
+    jobs, refs = [], []
+    for i in range(n):
+        nout, k = shapes[i % len(shapes)]
+        m = 2080 if i % 3 else 300
+        dy, x = bf(m, nout), bf(m, k)
+        dw0 = torch.randn(nout, k, device=DEV) * 0.1
+        db0 = torch.randn(nout, device=DEV) if i % 2 == 0 else None
+        jobs.append((dy, x, dw0.clone(), db0.clone() if db0 is not None else None))
+        dw2, db2 = dw0.clone(), (db0.clone() if db0 is not None else None)
+        ref.linear_wgrad(dy, x, dw2, db2)
+        refs.append((dw2, db2))
+    ops.linear_wgrad_multi(jobs)
+    for (_, _, dw, db), (dw2, db2) in zip(jobs, refs):
+        close(dw, dw2, 2e-2, 1e-4, "dw")
+        if db is not None:
+            close(db, db2, 2e-2, 1e-4, "db")
+
+
 def _wgrad_group_check(big):
     """Grouped launch == per-problem reference (unsplit read-add-write and split atomic paths)."""
     M = 2080

@@ -48,7 +48,8 @@ def test_program_fwd_bwd_vs_reference_ops(name):
 
 @pytest.mark.parametrize("name", ["vit_tiny", "oxford_flower"])
 @pytest.mark.parametrize("embed_with_block0", [True, False])
-def test_backward_wgrad_ride_matches_grouped(name, embed_with_block0, monkeypatch):
+@pytest.mark.parametrize("mode", ["ride", "tail"])
+def test_backward_wgrad_ride_matches_grouped(name, embed_with_block0, mode, monkeypatch):
     """Weight gradients riding in the dgrad launches == one grouped launch per block
     (same backward otherwise; fp32 atomics -> summation order differs slightly), and
     the block yields keep their order (L-1 .. 0, -1)."""
@@ -66,12 +67,13 @@ def test_backward_wgrad_ride_matches_grouped(name, embed_with_block0, monkeypatc
         out, S = prog.forward(P, img, t, r, True)
         _, dtok = ops.smooth_l1_fwd_bwd(out, tgt, prog.cfg.tokens, prog.cfg.patch)
     results = []
-    for ride in (True, False):
-        monkeypatch.setattr(pm, "WGRAD_RIDE", ride)
+    for new in (True, False):
+        monkeypatch.setattr(pm, "WGRAD_RIDE", new and mode == "ride")
         grads = {n: torch.zeros_like(p) for n, p in m.named_parameters()}
         G = collect(grads, prog.cfg.depth, prog.cfg.dim)
         with torch.no_grad():
-            order = list(prog.backward_iter(P, G, S, dtok, r, True, embed_with_block0=embed_with_block0))
+            order = list(prog.backward_iter(P, G, S, dtok, r, True, embed_with_block0=embed_with_block0,
+                                            wgrad_tail=new and mode == "tail"))
         torch.cuda.synchronize()
         assert order == list(range(prog.cfg.depth - 1, -1, -1)) + [-1]
         results.append(grads)
