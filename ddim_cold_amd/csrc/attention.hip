@@ -927,14 +927,21 @@ __global__ __launch_bounds__(NP * 4) void attn_fwd_short_kernel(const bf16* __re
   }
 }
 
-template <int HD, int NP, bool DROP>
+// Fused projection input-gradient (FUSE): dO of the head is computed in the
+// kernel, dO[b, :, h] = gy[b rows, :] @ Wp[:, h*hd : (h+1)*hd] (the proj
+// Linear's dgrad restricted to this head's columns; `dout` is then gy [B*N][Dm]
+// and `wp` the proj weight [Dm][Dm]), instead of being read from a separate
+// dgrad launch's output.  Same permuted-k MFMA order as the dgrad GEMM (tr
+// reads of the weight slice staged in the P/dS region), bf16-rounded like it.
+template <int HD, int NP, bool DROP, bool FUSE>
 __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __restrict__ dout,
                                                                 const bf16* __restrict__ qkv,
                                                                 const bf16* __restrict__ out,
                                                                 const float* __restrict__ lse,
                                                                 bf16* __restrict__ dqkv, int B, int H, int N,
                                                                 float scale, const int64_t* __restrict__ rng,
-                                                                int site, uint32_t thr, float dsc) {
+                                                                int site, uint32_t thr, float dsc,
+                                                                const bf16* __restrict__ wp, int Dm) {
   using I = ShortImg<HD, NP>;
   constexpr int RS = I::RS, PS = 2 * NP + 32, KS = HD / 32, DT = HD / 16, KT = NP / 16;
   __shared__ __attribute__((aligned(16))) char lds[4 * NP * RS + 2 * NP * PS];
@@ -956,7 +963,37 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
   iq.load(qkv + (size_t)bh * mat, HD, N);
   ik.load(qkv + ((size_t)B * H + bh) * mat, HD, N);
   iv.load(qkv + ((size_t)2 * B * H + bh) * mat, HD, N);
-  id.load(dout + (size_t)b * N * D + h * HD, D, N);
+  // FUSE: the weight slice Wp[:, h*HD..] ([Dm k-rows][HD], BS-byte rows) goes to the
+  // P/dS region; each wave's gy rows load as permuted-k A fragments
+  constexpr int BS = 2 * HD + 32;
+  constexpr int WCH = HD / 8;  // 16-B chunks per weight-slice row
+  constexpr int WPER = FUSE ? (512 * WCH + NP * 4 - 1) / (NP * 4) : 1;  // Dm <= 512
+  u32x4 wv[WPER];
+  if (FUSE) {
+#pragma unroll
+    for (int i = 0; i < WPER; ++i) {
+      const int c = threadIdx.x + i * NP * 4;
+      const int k = c / WCH, cc = c - k * WCH;
+      wv[i] = k < Dm ? *reinterpret_cast<const u32x4*>(wp + (size_t)k * Dm + h * HD + cc * 8) : u32x4{0u, 0u, 0u, 0u};
+    }
+  } else {
+    id.load(dout + (size_t)b * N * D + h * HD, D, N);
+  }
+  // FUSE: this wave's gy rows as permuted-k A fragments, every 32-deep step's
+  // loads issued up front (Dm <= 512: 16 steps)
+  u32x4 gfr[FUSE ? 16 : 1];
+  if (FUSE) {
+    const int r = wave * 16 + li;
+    const bf16* grow = dout + ((size_t)b * N + (r < N ? r : N - 1)) * Dm;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if (32 * s < Dm) {
+        const u32x2 lo = *reinterpret_cast<const u32x2*>(grow + 32 * s + 4 * g);
+        const u32x2 hi = *reinterpret_cast<const u32x2*>(grow + 32 * s + 16 + 4 * g);
+        gfr[s] = u32x4{lo[0], lo[1], hi[0], hi[1]};
+      }
+    }
+  }
   bf16x8 of[KS];
   {
     const bf16* orow = out + ((size_t)b * N + qc) * D + h * HD;
@@ -968,7 +1005,39 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
   iq.store(Ql);
   ik.store(Kl);
   iv.store(Vl);
-  id.store(Dl);
+  if (FUSE) {
+#pragma unroll
+    for (int i = 0; i < WPER; ++i) {
+      const int c = threadIdx.x + i * NP * 4;
+      const int k = c / WCH, cc = c - k * WCH;
+      if (k < Dm) *reinterpret_cast<u32x4*>(Pl + k * BS + cc * 16) = wv[i];
+    }
+    __syncthreads();
+    // dO rows 16w..16w+15 of this head: transposed accumulators (lane: row 16w+li,
+    // columns 16ct + 4g..+3), K = Dm in 32-deep steps, permuted k order
+    const int r = wave * 16 + li;
+    f32x4 acc[HD / 16];
+#pragma unroll
+    for (int ct = 0; ct < HD / 16; ++ct) acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if (32 * s < Dm) {
+        const bf16x8 af = __builtin_bit_cast(bf16x8, gfr[s]);
+#pragma unroll
+        for (int ct = 0; ct < HD / 16; ++ct) acc[ct] = mfma16(frag_t<BS>(Pl, 16 * ct, s, lane), af, acc[ct]);
+      }
+    }
+    if (r < N) {
+#pragma unroll
+      for (int ct = 0; ct < HD / 16; ++ct) *reinterpret_cast<bf16x4*>(Dl + r * RS + (16 * ct + 4 * g) * 2) = pack4(acc[ct]);
+    } else if (r < NP) {
+#pragma unroll
+      for (int ct = 0; ct < HD / 16; ++ct)
+        *reinterpret_cast<bf16x4*>(Dl + r * RS + (16 * ct + 4 * g) * 2) = pack4(f32x4{0.f, 0.f, 0.f, 0.f});
+    }
+  } else {
+    id.store(Dl);
+  }
   __syncthreads();
 
   // ---- phase A: this wave's 16 queries against all keys
@@ -1062,42 +1131,53 @@ template <int HD, int NP, bool DROP>
 struct ShortLaunch {
   static void run(bool bwd, const bf16* d, const bf16* q, const bf16* o, float* lse, const float* lse_in,
                   bf16* outp, int B, int H, int N, float scale, const int64_t* rng, int site, uint32_t thr,
-                  float dsc, hipStream_t stream) {
+                  float dsc, hipStream_t stream, const bf16* wp, int Dm) {
     if (!bwd)
       hipLaunchKernelGGL((attn_fwd_short_kernel<HD, NP, DROP>), dim3(B * H), dim3(NP * 4), 0, stream, q, outp, lse,
                          B, H, N, scale, rng, site, thr, dsc);
+    else if (wp != nullptr)
+      hipLaunchKernelGGL((attn_bwd_short_kernel<HD, NP, DROP, true>), dim3(B * H), dim3(NP * 4), 0, stream, d, q, o,
+                         lse_in, outp, B, H, N, scale, rng, site, thr, dsc, wp, Dm);
     else
-      hipLaunchKernelGGL((attn_bwd_short_kernel<HD, NP, DROP>), dim3(B * H), dim3(NP * 4), 0, stream, d, q, o,
-                         lse_in, outp, B, H, N, scale, rng, site, thr, dsc);
+      hipLaunchKernelGGL((attn_bwd_short_kernel<HD, NP, DROP, false>), dim3(B * H), dim3(NP * 4), 0, stream, d, q, o,
+                         lse_in, outp, B, H, N, scale, rng, site, thr, dsc, wp, Dm);
   }
 };
 
 template <int HD, int NP>
 static void launch_short(bool bwd, const bf16* d, const bf16* q, const bf16* o, float* lse, const float* lse_in,
                          bf16* outp, int B, int H, int N, float scale, const int64_t* rng, int site, uint32_t thr,
-                         float dsc, hipStream_t stream) {
-  if (thr) ShortLaunch<HD, NP, true>::run(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream);
-  else ShortLaunch<HD, NP, false>::run(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream);
+                         float dsc, hipStream_t stream, const bf16* wp = nullptr, int Dm = 0) {
+  if (thr)
+    ShortLaunch<HD, NP, true>::run(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, wp, Dm);
+  else
+    ShortLaunch<HD, NP, false>::run(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, wp,
+                                    Dm);
 }
 
 template <int HD>
 static void dispatch_short(bool bwd, const bf16* d, const bf16* q, const bf16* o, float* lse, const float* lse_in,
                            bf16* outp, int B, int H, int N, float scale, const int64_t* rng, int site, uint32_t thr,
-                           float dsc, hipStream_t stream) {
+                           float dsc, hipStream_t stream, const bf16* wp = nullptr, int Dm = 0) {
   switch ((N + 31) / 32) {
-    case 1: launch_short<HD, 32>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream); break;
-    case 2: launch_short<HD, 64>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream); break;
-    case 3: launch_short<HD, 96>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream); break;
-    default: launch_short<HD, 128>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream); break;
+    case 1: launch_short<HD, 32>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, wp, Dm); break;
+    case 2: launch_short<HD, 64>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, wp, Dm); break;
+    case 3: launch_short<HD, 96>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, wp, Dm); break;
+    default: launch_short<HD, 128>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, wp, Dm); break;
   }
 }
 
 #define DC_INST_SHORT1(HD, NP, DR)                                                                                 \
   template __global__ void attn_fwd_short_kernel<HD, NP, DR>(const bf16*, bf16*, float*, int, int, int, float,    \
                                                              const int64_t*, int, uint32_t, float);               \
-  template __global__ void attn_bwd_short_kernel<HD, NP, DR>(const bf16*, const bf16*, const bf16*, const float*, \
-                                                             bf16*, int, int, int, float, const int64_t*, int,    \
-                                                             uint32_t, float);
+  template __global__ void attn_bwd_short_kernel<HD, NP, DR, false>(const bf16*, const bf16*, const bf16*,        \
+                                                                    const float*, bf16*, int, int, int, float,    \
+                                                                    const int64_t*, int, uint32_t, float,         \
+                                                                    const bf16*, int);                            \
+  template __global__ void attn_bwd_short_kernel<HD, NP, DR, true>(const bf16*, const bf16*, const bf16*,         \
+                                                                   const float*, bf16*, int, int, int, float,     \
+                                                                   const int64_t*, int, uint32_t, float,          \
+                                                                   const bf16*, int);
 #define DC_INST_SHORT(HD, NP) DC_INST_SHORT1(HD, NP, true) DC_INST_SHORT1(HD, NP, false)
 DC_INST_SHORT(32, 32) DC_INST_SHORT(32, 64) DC_INST_SHORT(32, 96) DC_INST_SHORT(32, 128)
 DC_INST_SHORT(64, 32) DC_INST_SHORT(64, 64) DC_INST_SHORT(64, 96) DC_INST_SHORT(64, 128)
@@ -1416,6 +1496,29 @@ void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const flo
   } else {
     throw std::runtime_error("attention: head dim must be 32 or 64");
   }
+}
+
+// LDS the fused kernel needs for the weight slice (P/dS region: 2 NP (2 NP + 32) bytes)
+bool attn_bwd_proj_supported(int N, int hd, int Dm) {
+  if (N > SHORT_MAX_N || short_disabled() || (hd != 32 && hd != 64) || Dm % 32 != 0 || Dm > 512) return false;
+  const int NP = 32 * ((N + 31) / 32);
+  return Dm * (2 * hd + 32) <= 2 * NP * (2 * NP + 32);
+}
+
+void attn_bwd_proj_launch(const void* gy, const void* wp, int Dm, const void* qkv, const void* o, const float* lse,
+                          void* dqkv, int B, int H, int N, int hd, float scale, const int64_t* rng, int site,
+                          double p, hipStream_t stream) {
+  if (!attn_bwd_proj_supported(N, hd, Dm) || Dm != H * hd)
+    throw std::runtime_error("attn_bwd_proj: unsupported shape");
+  const uint32_t thr = drop_threshold_host(p);
+  const float dsc = p > 0 ? 1.f / (1.f - (float)p) : 1.f;
+  const bf16* d = reinterpret_cast<const bf16*>(gy);
+  const bf16* q = reinterpret_cast<const bf16*>(qkv);
+  const bf16* oo = reinterpret_cast<const bf16*>(o);
+  const bf16* w = reinterpret_cast<const bf16*>(wp);
+  bf16* dq = reinterpret_cast<bf16*>(dqkv);
+  if (hd == 32) dispatch_short<32>(true, d, q, oo, nullptr, lse, dq, B, H, N, scale, rng, site, thr, dsc, stream, w, Dm);
+  else dispatch_short<64>(true, d, q, oo, nullptr, lse, dq, B, H, N, scale, rng, site, thr, dsc, stream, w, Dm);
 }
 
 bool qkv_attn_supported(int N, int hd, int D) {

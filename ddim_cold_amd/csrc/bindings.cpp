@@ -806,6 +806,26 @@ Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, double scale, Ten
   return dqkv;
 }
 
+bool attn_bwd_proj_ok(int64_t N, int64_t hd, int64_t D) { return attn_bwd_proj_supported((int)N, (int)hd, (int)D); }
+
+// attention backward with the proj input gradient fused in: gy [B*N][D] (the
+// gradient at the proj output), wp = proj weight [D][D]
+Tensor attn_bwd_proj(Tensor gy, Tensor wp, Tensor qkv, Tensor o, Tensor lse, double scale, Tensor rng, int64_t site,
+                     double p) {
+  CHECK_IN(gy, BF16); CHECK_IN(wp, BF16); CHECK_IN(qkv, BF16); CHECK_IN(o, BF16); CHECK_IN(lse, F32); check_rng(rng);
+  const c10::DeviceGuard guard(qkv.device());
+  TORCH_CHECK(qkv.dim() == 5 && qkv.size(0) == 3, "qkv must be [3,B,H,N,hd]");
+  const int B = qkv.size(1), H = qkv.size(2), N = qkv.size(3), hd = qkv.size(4), D = H * hd;
+  TORCH_CHECK(gy.numel() == (int64_t)B * N * D && wp.numel() == (int64_t)D * D && o.numel() == gy.numel() &&
+                  lse.numel() == (int64_t)B * H * N,
+              "attn_bwd_proj shapes");
+  TORCH_CHECK(attn_bwd_proj_supported(N, hd, D), "attn_bwd_proj: unsupported shape");
+  auto dqkv = at::empty({(int64_t)B * N, 3 * D}, qkv.options());
+  attn_bwd_proj_launch(gy.data_ptr(), wp.data_ptr(), D, qkv.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
+                       dqkv.data_ptr(), B, H, N, hd, (float)scale, rng.data_ptr<int64_t>(), site, p, cur_stream());
+  return dqkv;
+}
+
 Tensor embed_bwd(Tensor g, Tensor t, Tensor rng, int64_t site, double p, Tensor dcls, Tensor dpos, Tensor dtemb,
                  c10::optional<Tensor> ln_ws, c10::optional<Tensor> ln_ptrs, int64_t ln_C) {
   CHECK_IN(g, F32); CHECK_IN(t, I64); check_rng(rng); CHECK_IN(dcls, F32); CHECK_IN(dpos, F32); CHECK_IN(dtemb, F32);
@@ -1082,6 +1102,9 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("linear_wgrad_group(Tensor[] dys, Tensor[] xs, Tensor(a!)[] dws, Tensor(b!)?[] dbs) -> ()");
   m.def("wire_pack(Tensor src, Tensor(a!) dst) -> ()");
   m.def("wire_unpack(Tensor src, Tensor(a!) dst) -> ()");
+  m.def("attn_bwd_proj_ok(int N, int hd, int D) -> bool", &attn_bwd_proj_ok);
+  m.def("attn_bwd_proj(Tensor gy, Tensor wp, Tensor qkv, Tensor o, Tensor lse, float scale, Tensor rng, int site, "
+        "float p) -> Tensor");
   m.def("vit_group_ok(int D, int H, int hd, int N, int L) -> bool", &vit_group_ok);
   m.def("vit_group_fwd(Tensor?[] ts, int L, int B, int N, int[] sites, float[] p_dp, Tensor rng, float p_drop, "
         "float p_attn, float scale, float eps, Tensor(a!) ctr, Tensor(b!) err, Tensor(c!)? stamps=None) -> ()");
@@ -1139,6 +1162,7 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("linear_wgrad_multi", &linear_wgrad_multi);
   m.impl("vit_group_fwd", &vit_group_fwd);
   m.impl("wire_pack", &wire_pack);
+  m.impl("attn_bwd_proj", &attn_bwd_proj);
   m.impl("wire_unpack", &wire_unpack);
   m.impl("layernorm_bwd", &layernorm_bwd);
   m.impl("replica_reduce_", &replica_reduce_);

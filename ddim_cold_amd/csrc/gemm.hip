@@ -221,13 +221,13 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
 template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EPI, int S>
 __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int tn, int kz) {
   static_assert(WM * WN == 4, "4 waves");
-  static_assert(!AT || BM == 64, "transposed A needs BM == 64");
-  static_assert(!BT || BN == 64, "transposed B needs BN == 64");
+  static_assert(!AT || BM == 64 || BM == 128, "transposed A: BM 64 or 128 (two half images)");
+  static_assert(!BT || BN == 64 || BN == 128, "transposed B: BN 64 or 128 (two half images)");
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
   constexpr bool PERM = AT || BT;
-  using OA = DmaOperand<BM, AT>;
-  using OB = DmaOperand<BN, BT>;
+  using OA = typename DmaOp<BM, AT>::type;
+  using OB = typename DmaOp<BN, BT>::type;
   constexpr int STAGE = OA::BYTES + OB::BYTES;
   constexpr int LPT = OA::PER_WAVE + OB::PER_WAVE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -299,10 +299,10 @@ __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int t
       for (int s = 0; s < 2; ++s) {
 #pragma unroll
         for (int i = 0; i < FM; ++i)
-          if (AT) ta[s][i] = frag_t_swz_issue(la, wm * TM + i * 16, s, lane);
+          if (AT) ta[s][i] = frag_t_half(la, wm * TM + i * 16, s, lane);
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          if (BT) tb[s][j] = frag_t_swz_issue(lb, wn * TN + j * 16, s, lane);
+          if (BT) tb[s][j] = frag_t_half(lb, wn * TN + j * 16, s, lane);
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -310,8 +310,9 @@ __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int t
         if (AT || BT) {
           if (s == 0) {
             // reads issued after k-step 0's: 2 per transposed fragment
-            constexpr int LATER = 2 * ((AT ? FM : 0) + (BT ? FN : 0));
-            static_assert(LATER < 16, "lgkmcnt is 4 bits");
+            // (clamped to the 4-bit lgkmcnt field: waiting for fewer is correct, just stricter)
+            constexpr int LATER0 = 2 * ((AT ? FM : 0) + (BT ? FN : 0));
+            constexpr int LATER = LATER0 < 16 ? LATER0 : 15;
 #pragma unroll
             for (int i = 0; i < FM; ++i)
               if (AT) af[i] = frag_t_fence_n<LATER>(ta[0][i]);
@@ -760,7 +761,7 @@ struct WgradMulti {
   int tile_start[WM_MAX + 1];
   int n;
 };
-template <int S>
+template <int T, int S>
 __global__ __launch_bounds__(256) void gemm_wgrad_multi_kernel(WgradMulti gm) {
   const int bid = xcd_remap(blockIdx.x, gm.tile_start[gm.n]);
   int lo = 0, hi = gm.n - 1;  // problem owning tile `bid`: binary search over tile_start
@@ -774,13 +775,14 @@ __global__ __launch_bounds__(256) void gemm_wgrad_multi_kernel(WgradMulti gm) {
   p.A = d.A; p.B = d.B; p.C = d.C; p.bias = d.bias;
   p.M = d.M; p.N = d.N; p.K = d.K; p.lda = d.lda; p.ldb = d.ldb; p.ldc = d.ldc;
   p.ktiles_per_split = (d.K + BK - 1) / BK;
-  const int tiles_n = (d.N + 63) / 64;
+  const int tiles_n = (d.N + T - 1) / T;
   const int local = bid - gm.tile_start[lo];
   const int tm = local / tiles_n;
-  gemm_dma_body<64, 64, 2, 2, true, true, EPI_ACC, S>(p, tm, local - tm * tiles_n, 0);
+  gemm_dma_body<T, T, 2, 2, true, true, EPI_ACC, S>(p, tm, local - tm * tiles_n, 0);
 }
-template __global__ void gemm_wgrad_multi_kernel<3>(WgradMulti);
-template __global__ void gemm_wgrad_multi_kernel<4>(WgradMulti);
+template __global__ void gemm_wgrad_multi_kernel<64, 3>(WgradMulti);
+template __global__ void gemm_wgrad_multi_kernel<64, 4>(WgradMulti);
+template __global__ void gemm_wgrad_multi_kernel<128, 3>(WgradMulti);
 template __global__ void gemm_wgrad_group_kernel<EPI_ATOMIC, 6>(WgradGroup);
 template __global__ void gemm_wgrad_group_kernel<EPI_ACC, 6>(WgradGroup);
 template __global__ void gemm_wgrad_group_kernel<EPI_ATOMIC, 8>(WgradGroup);
@@ -967,6 +969,13 @@ void gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream) {
   WgradMulti gm{};
   gm.n = n;
   int tiles = 0;
+  // tile: 64 x 64 (three 48 KiB workgroups per CU).  128 x 128 (DDIM_COLD_WGRAD_MULTI_TILE=128:
+  // half the operand bytes per output, one 96 KiB workgroup per CU, ~390 workgroups
+  // in 1.5 rounds) measured 14 us/step slower (0.838 vs 0.824 ms/step, interleaved A/B)
+  static const int T = [] {
+    const char* e = getenv("DDIM_COLD_WGRAD_MULTI_TILE");
+    return (e && atoi(e) == 128) ? 128 : 64;
+  }();
   for (int i = 0; i < n; ++i) {
     const GemmArgs& a = probs[i];
     if (a.N % 4 != 0) throw std::runtime_error("gemm_wgrad_multi: output width must be a multiple of 4");
@@ -975,18 +984,26 @@ void gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream) {
     d.C = reinterpret_cast<float*>(a.C); d.bias = const_cast<float*>(a.bias);
     d.M = a.M; d.N = a.N; d.K = a.K; d.lda = a.lda; d.ldb = a.ldb; d.ldc = a.ldc;
     gm.tile_start[i] = tiles;
-    tiles += ((a.M + 63) / 64) * ((a.N + 63) / 64);
+    tiles += ((a.M + T - 1) / T) * ((a.N + T - 1) / T);
   }
   for (int i = n; i <= WM_MAX; ++i) gm.tile_start[i] = tiles;
-  // ring depth: 3 stages (48 KiB) -> 3 workgroups per CU, 4 (64 KiB) -> 2
+  if (T == 128) {
+    constexpr int lds = 3 * (128 * 128 + 128 * 128);
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_wgrad_multi_kernel<128, 3>),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+    (void)attr;
+    hipLaunchKernelGGL((gemm_wgrad_multi_kernel<128, 3>), dim3(tiles), dim3(256), lds, stream, gm);
+    return;
+  }
+  // 64 x 64: ring depth 3 stages (48 KiB) -> 3 workgroups per CU, 4 (64 KiB) -> 2
   static const int ring = [] {
     const char* e = getenv("DDIM_COLD_WGRAD_MULTI_S");
     return (e && atoi(e) == 4) ? 4 : 3;
   }();
   if (ring == 4)
-    hipLaunchKernelGGL(gemm_wgrad_multi_kernel<4>, dim3(tiles), dim3(256), 4 * (64 * 128 + 64 * 128), stream, gm);
+    hipLaunchKernelGGL((gemm_wgrad_multi_kernel<64, 4>), dim3(tiles), dim3(256), 4 * (64 * 128 + 64 * 128), stream, gm);
   else
-    hipLaunchKernelGGL(gemm_wgrad_multi_kernel<3>, dim3(tiles), dim3(256), 3 * (64 * 128 + 64 * 128), stream, gm);
+    hipLaunchKernelGGL((gemm_wgrad_multi_kernel<64, 3>), dim3(tiles), dim3(256), 3 * (64 * 128 + 64 * 128), stream, gm);
 }
 
 void gemm_wgrad_group(const GemmArgs* probs, int n, int splits, hipStream_t stream) {

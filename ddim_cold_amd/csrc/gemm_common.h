@@ -133,6 +133,34 @@ struct DmaOperand {
   }
 };
 
+// A transposed operand 128 columns wide is staged as TWO 64-column half images
+// (the transposed-read swizzle and the DMA piece map assume 128-B image rows).
+struct DmaOperandT128 {
+  static constexpr int BYTES = 2 * 64 * 128;  // one 64-deep K tile, both halves
+  static constexpr int PER_WAVE = 4;
+  DmaOperand<64, true> h0, h1;
+  __device__ __forceinline__ void init(const bf16* base, int ld, int rows_total, int row0, int wave, int lane) {
+    h0.init(base, ld, rows_total, row0, wave, lane);
+    h1.init(base, ld, rows_total, row0 + 64, wave, lane);
+  }
+  __device__ __forceinline__ void issue(char* lds_tile, int kt, int wave) const {
+    h0.issue(lds_tile, kt, wave);
+    h1.issue(lds_tile + 64 * 128, kt, wave);
+  }
+};
+template <int R, bool T>
+struct DmaOp {
+  using type = DmaOperand<R, T>;
+};
+template <>
+struct DmaOp<128, true> {
+  using type = DmaOperandT128;
+};
+// transposed fragment (operand columns c0..c0+15) of a [64 k][64]-per-half image
+__device__ __forceinline__ TrFrag frag_t_half(const char* lds, int c0, int s, int lane) {
+  return frag_t_swz_issue(lds + (c0 >> 6) * (64 * 128), c0 & 63, s, lane);
+}
+
 // bijective XCD-aware remap: consecutive block ids land on different XCDs
 // (round robin); give each XCD a contiguous range of tiles instead
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {

@@ -216,6 +216,13 @@ void cold_batch_launch(const float* pool, int pool_n, const int64_t* rng, int si
 void wire_pack_launch(const float* src, void* dst, int64_t n, hipStream_t stream);
 void wire_unpack_launch(const void* src, float* dst, int64_t n, hipStream_t stream);
 
+// attention backward with the proj Linear's input gradient fused in (short path):
+// dO = gy @ Wp computed per head inside the kernel (gy [B*N][Dm], Wp [Dm][Dm])
+bool attn_bwd_proj_supported(int N, int hd, int Dm);
+void attn_bwd_proj_launch(const void* gy, const void* wp, int Dm, const void* qkv, const void* o, const float* lse,
+                          void* dqkv, int B, int H, int N, int hd, float scale, const int64_t* rng, int site,
+                          double p, hipStream_t stream);
+
 // fused QKV projection + short-sequence attention (attention.hip), hd 32, 64 < N <= 128
 struct QkvArgs {
   const void* x = nullptr;      // [B*N][D] bf16

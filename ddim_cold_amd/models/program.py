@@ -65,6 +65,12 @@ WGRAD_RIDE = os.environ.get("DDIM_COLD_WGRAD_RIDE", "1") == "1"
 # 0.890 vs 0.871 ms/step and the B=64 sampler (two launches: one 156 KiB-LDS
 # workgroup per CU) is slower too: opt-in (DDIM_COLD_GROUP_FWD=1).
 GROUP_FWD = os.environ.get("DDIM_COLD_GROUP_FWD", "0") == "1"
+# proj input gradient computed per head inside the short attention backward
+# (ops.attn_bwd_proj): one launch fewer per block, but each (b, h) workgroup
+# then runs a K = D GEMM before its attention math; measured slower than the
+# 390-workgroup dgrad + attention backward (0.836 vs 0.823 ms/step, 3
+# interleaved 1000-step pairs, tools/gpu_ap.sh): opt-in (DDIM_COLD_ATTN_PROJ=1)
+ATTN_PROJ = os.environ.get("DDIM_COLD_ATTN_PROJ", "0") == "1"
 # dtype of the bf16 activation copies / folded weights the program allocates
 # (tests on CPU switch it to fp32 to isolate the program logic from rounding)
 ACT_DTYPE = torch.bfloat16
@@ -558,16 +564,24 @@ class ViTProgram:
             l2 = ln_out(l2)
             g1, gy1 = ops.layernorm_bwd(dl2, x1, m2, r2, bp.n2w, g, bg.n2w, bg.n2b, N, rng, sp, pd, sd1, dpr[i],
                                         True, ws(k2), beta=bp.n2b if fold else None, y_out=l2 if fold else None)
-            if ride:
+            fuse_ap = ATTN_PROJ and dtok.is_cuda and ops.attn_bwd_proj_ok(N, D // c.heads, D)
+            riders_q = [(gy1, o, bg.proj_w, bg.proj_b)]
+            if ride and not fuse_ap:
                 do = ops.linear_dgrad_ride(gy1, bp.proj_w, [(du, l2, bg.fc1_w, bg.fc1_b)])
+            elif ride:
+                riders_q.append((du, l2, bg.fc1_w, bg.fc1_b))  # the proj dgrad launch is gone
             else:
                 wgrad(du, l2, bg.fc1_w, bg.fc1_b)
                 wgrad(gy1, o, bg.proj_w, bg.proj_b)
-                do = ops.linear_dgrad(gy1, bp.proj_w, False)
-            dqkv = ops.attn_bwd(do, qkv, o, lse, c.scale, rng, sa, ad)
+                if not fuse_ap:
+                    do = ops.linear_dgrad(gy1, bp.proj_w, False)
+            if fuse_ap:
+                dqkv = ops.attn_bwd_proj(gy1, bp.proj_w, qkv, o, lse, c.scale, rng, sa, ad)
+            else:
+                dqkv = ops.attn_bwd(do, qkv, o, lse, c.scale, rng, sa, ad)
             qs = QKV_DGRAD_SPLITS if 3 * D >= 768 else 1
             if ride:
-                dl1 = ops.linear_dgrad_ride(dqkv, bp.qkv_w, [(gy1, o, bg.proj_w, bg.proj_b)], f32, qs)
+                dl1 = ops.linear_dgrad_ride(dqkv, bp.qkv_w, riders_q, f32, qs)
             else:
                 dl1 = ops.linear_dgrad(dqkv, bp.qkv_w, f32, qs)
             l1 = ln_out(l1)

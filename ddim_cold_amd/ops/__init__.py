@@ -256,6 +256,22 @@ def linear_wgrad_group(jobs):
         ref.linear_wgrad(dy, x, dw, db)
 
 
+def attn_bwd_proj_ok(N: int, hd: int, D: int) -> bool:
+    """Shapes the fused proj-dgrad + short attention backward covers (csrc/attention.hip)."""
+    return _ext.available() and bool(_ops().attn_bwd_proj_ok(N, hd, D))
+
+
+def attn_bwd_proj(gy, wp, qkv, o, lse, scale: float, rng, site: int, p: float):
+    """:func:`attn_bwd` of ``dO = gy @ wp`` (the proj Linear's input gradient)
+    with that GEMM computed per head inside the attention-backward kernel on a
+    GPU (one launch fewer); elsewhere the two ops in sequence."""
+    B, H, N, hd = qkv.shape[1], qkv.shape[2], qkv.shape[3], qkv.shape[4]
+    if _hip(gy) and attn_bwd_proj_ok(N, hd, H * hd):
+        return _ops().attn_bwd_proj(gy, wp, qkv, o, lse, float(scale), rng, int(site), float(p))
+    do = linear_dgrad(gy, wp, False)
+    return attn_bwd(do, qkv, o, lse, scale, rng, site, p)
+
+
 def wire_pack(src, dst):
     """fp32 -> bf16 (round to nearest even) into ``dst`` (gradient wire format)."""
     if _hip(src):

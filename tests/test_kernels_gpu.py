@@ -510,3 +510,21 @@ def test_cold_batch_and_q_sample():
     eps = torch.randn_like(x0)
     tt = torch.randint(0, 2000, (B,), device=DEV)
     close(ops.q_sample(x0, tt, eps, 2000), ref.q_sample(x0, tt, eps, 2000), 1e-5, 1e-5, "q_sample")
+
+
+@pytest.mark.parametrize("B,H,N,hd,p", [(32, 12, 65, 32, 0.1), (4, 12, 65, 32, 0.0), (3, 4, 100, 64, 0.1),
+                                        (2, 8, 17, 32, 0.0), (2, 4, 128, 64, 0.0)])
+def test_attn_bwd_proj_fused(B, H, N, hd, p):
+    """Short attention backward with the proj input gradient computed per head in the
+    kernel == proj dgrad (bf16) followed by the attention backward."""
+    D = H * hd
+    if not ops.attn_bwd_proj_ok(N, hd, D):
+        pytest.skip("shape not covered by the fused kernel")
+    qkv = bf(3, B, H, N, hd)
+    gy, wp = bf(B * N, D), bf(D, D, scale=0.05)
+    r = rng()
+    o, lse = ops.attn_fwd(qkv, hd ** -0.5, r, 5, p)
+    fused = ops.attn_bwd_proj(gy, wp, qkv, o, lse, hd ** -0.5, r, 5, p)
+    do = ops.linear_dgrad(gy, wp, False)
+    sep = ops.attn_bwd(do, qkv, o, lse, hd ** -0.5, r, 5, p)
+    close(fused, sep, 2e-3, 1e-2, "dqkv")
