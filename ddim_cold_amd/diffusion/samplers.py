@@ -143,8 +143,9 @@ class _GraphLoop:
             with torch.cuda.stream(s):
                 self.body()  # warm-up (allocator, kernels); also produces this call's result
             torch.cuda.current_stream(self.device).wait_stream(s)
+            from ..utils.observe import no_gc
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with no_gc(), torch.cuda.graph(g):
                 self.body()
             self.graph = g
             return

@@ -444,6 +444,11 @@ class TrainEngine:
                     self._join_comm()
 
     def _capture_impl(self, graph_comm: bool):
+        from ..utils.observe import no_gc
+        with no_gc():
+            self._capture_graphs(graph_comm)
+
+    def _capture_graphs(self, graph_comm: bool):
         pool = torch.cuda.graph_pool_handle()
         graphs = []
         self._multi = None

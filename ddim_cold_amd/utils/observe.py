@@ -109,3 +109,21 @@ def check_param_sync(flat: torch.Tensor, group=None, step: Optional[int] = None,
     if not torch.all((hi - lo).abs() <= rtol * hi.abs()):
         raise RuntimeError(f"data-parallel replicas diverged at step {step}: checksum max {hi.tolist()} "
                            f"min {lo.tolist()}")
+
+
+@contextlib.contextmanager
+def no_gc():
+    """Collect, then keep Python's cyclic GC off for the block (hipGraph stream
+    capture): a collection during capture can run destructors of an earlier,
+    unreferenced graph or of tensors tied to another stream -- HIP calls that
+    are illegal while a stream is being captured (seen as an abort inside a
+    captured op)."""
+    import gc
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
