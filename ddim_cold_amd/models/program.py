@@ -483,7 +483,8 @@ class ViTProgram:
     def backward_iter(self, P: ModelTensors, G: ModelTensors, S: Saved, dtok: torch.Tensor, rng: torch.Tensor,
                       training: bool = True, wgrad: Optional[Callable] = None,
                       ln_ws: Optional[torch.Tensor] = None, wgrad_stream=None,
-                      embed_with_block0: bool = False, ln_final=None, wgrad_tail: bool = False) -> Iterator[int]:
+                      embed_with_block0: bool = False, ln_final=None, wgrad_tail: bool = False,
+                      wgrad_flush=None) -> Iterator[int]:
         """Hand-written backward; yields the block index after each block's grads
         are issued (L-1 first, then ..., 0) and -1 after the embedding grads.
 
@@ -502,12 +503,17 @@ class ViTProgram:
         before the optimizer): EVERY weight gradient is queued and issued as one
         launch after the embedding backward (:func:`ops.linear_wgrad_multi`), so
         the block yields then only mark the order, not finished gradients.
+        ``wgrad_flush`` (a set of block indices; data parallel): weight
+        gradients are queued and issued as one launch per gradient bucket --
+        after each listed block (and after the embedding backward) -- so the
+        bucket's all-reduce can start while the rest of the backward runs.
         """
         def ws(k):
             return None if ln_ws is None else ln_ws[k]
         # weight gradients ride in the next input-gradient launch (default), unless
         # the caller supplies its own wgrad callable or a side stream
-        tail = wgrad_tail and wgrad is None and wgrad_stream is None
+        bucketed = wgrad_flush is not None and wgrad is None and wgrad_stream is None and not wgrad_tail
+        tail = (wgrad_tail or bucketed) and wgrad is None and wgrad_stream is None
         ride = WGRAD_RIDE and wgrad is None and wgrad_stream is None and not tail
         batch = None
         tail_jobs = []
@@ -601,11 +607,15 @@ class ViTProgram:
             if i == 0 and embed_with_block0:
                 gpatch = self._embed_backward(P, G, S, g, rng, pd, wgrad, ln_final)
             flush()
+            if bucketed and (i in wgrad_flush or (i == 0 and embed_with_block0)) and tail_jobs:
+                ops.linear_wgrad_multi(tail_jobs)  # this bucket's weight gradients: final now
+                keep.append(tail_jobs)
+                tail_jobs = []
             yield i
         if not embed_with_block0:
             gpatch = self._embed_backward(P, G, S, g, rng, pd, wgrad, ln_final)
             flush()
-        if tail:
+        if tail and tail_jobs:
             ops.linear_wgrad_multi(tail_jobs)
             keep.append(tail_jobs)
         keep.append((gpatch, lf))

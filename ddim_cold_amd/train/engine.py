@@ -341,9 +341,13 @@ class TrainEngine:
             # single process: every weight gradient in one launch after the backward
             # (no bucket needs a block's gradients early)
             tail_w = not self.segmented and os.environ.get("DDIM_COLD_WGRAD_TAIL", "1") != "0"
+            # data parallel: one weight-gradient launch per gradient bucket
+            # (DDIM_COLD_WGRAD_BUCKET=0: riders in the input-gradient launches)
+            flush_at = set(k for k in self.bucket_after if k >= 0) \
+                if (self.segmented and os.environ.get("DDIM_COLD_WGRAD_BUCKET", "1") != "0") else None
             for i in self.prog.backward_iter(self.param_tensors, self.grad_tensors, S, dtok, self.rng, True,
                                              ln_ws=self.ln_ws, wgrad_stream=self.side, embed_with_block0=merge,
-                                             ln_final=ln_final, wgrad_tail=tail_w):
+                                             ln_final=ln_final, wgrad_tail=tail_w, wgrad_flush=flush_at):
                 if i in self.bucket_after and (self.segmented or i == -1):
                     hi = self.ln_done_at[i]
                     if ln_final is not None:

@@ -48,7 +48,7 @@ def test_program_fwd_bwd_vs_reference_ops(name):
 
 @pytest.mark.parametrize("name", ["vit_tiny", "oxford_flower"])
 @pytest.mark.parametrize("embed_with_block0", [True, False])
-@pytest.mark.parametrize("mode", ["ride", "tail"])
+@pytest.mark.parametrize("mode", ["ride", "tail", "bucket"])
 def test_backward_wgrad_ride_matches_grouped(name, embed_with_block0, mode, monkeypatch):
     """Weight gradients riding in the dgrad launches == one grouped launch per block
     (same backward otherwise; fp32 atomics -> summation order differs slightly), and
@@ -73,7 +73,8 @@ def test_backward_wgrad_ride_matches_grouped(name, embed_with_block0, mode, monk
         G = collect(grads, prog.cfg.depth, prog.cfg.dim)
         with torch.no_grad():
             order = list(prog.backward_iter(P, G, S, dtok, r, True, embed_with_block0=embed_with_block0,
-                                            wgrad_tail=new and mode == "tail"))
+                                            wgrad_tail=new and mode == "tail",
+                                            wgrad_flush={3, 1, 0} if new and mode == "bucket" else None))
         torch.cuda.synchronize()
         assert order == list(range(prog.cfg.depth - 1, -1, -1)) + [-1]
         results.append(grads)
