@@ -117,6 +117,23 @@ def test_checkpoint_weights_roundtrip(tmp_path):
     ckpt.load_weights(m2, p)
 
 
+def test_plumbing_config_gaussian32(tmp_path):
+    """BASELINE.json config #1: full-size ViT-tiny on 32x32 synthetic Gaussian-diffusion
+    images, batch 8, one gloo rank on the CPU, from the shipped YAML."""
+    cfg = load_config(os.path.join(ROOT, "configs", "plumbing_gaussian32.yaml")).validate()
+    assert (cfg.dataset, cfg.image_size, cfg.per_gpu_batch, cfg.embed_dim, cfg.depth) == \
+        ("gaussian", [32, 32], 8, 384, 7)
+    cfg = dataclasses.replace(cfg, ckpt_dir=str(tmp_path / "Saved_Models"))
+    paths = Paths.make(cfg, "plumbing_gaussian32", root=str(tmp_path))
+    res = launch(cfg, "plumbing_gaussian32", paths, backend="gloo")
+    assert res["steps"] == 64 // 8
+    steps, epochs = parse_log(paths.log)
+    assert len(epochs) == 1 and 0 < epochs[0][1] < 10
+    assert all(loss == loss for _, loss, _ in steps)  # finite EMA losses
+    last = torch.load(os.path.join(paths.ckpt_dir, "lastepoch.pkl"), weights_only=True)
+    assert last["state_dict"]["module.pos_embed"].shape[1] == (32 // 8) ** 2 + 1
+
+
 def test_trainer_two_ranks_gloo(tmp_path):
     cfg = _tiny_cfg(num_gpus=2, epoch=[0, 1], ckpt_dir=str(tmp_path / "Saved_Models"), sync_check_every=2)
     paths = Paths.make(cfg, "exp2", root=str(tmp_path))
