@@ -79,6 +79,12 @@ class EngineConfig:
     # Cold diffusion draws t in 1..log2(W) (7 rows), so for ViT-tiny this drops
     # 3.1 MB of the 28.7 MB gradient all-reduce.  None: all rows.
     temb_rows: Optional[int] = None
+    # data parallel with t drawn from the whole table (Gaussian diffusion, temb_rows
+    # None): only the <= world x batch rows indexed by this step's timesteps carry
+    # gradient, so the time_embed gradient is exchanged as all-gathered (t, row)
+    # pairs (49 KB per rank for ViT-tiny at batch 32) instead of all-reducing the
+    # dense [2000, 384] table (3.1 MB).  SURVEY.md §5.8 option 4.
+    temb_sparse: bool = True
     # capture the bucketed all-reduces INTO the step's hipGraph (RCCL kernels on a
     # comm-stream branch joined before the optimizer) instead of replaying one
     # graph segment per bucket with host-issued collectives in between.
@@ -247,6 +253,15 @@ class TrainEngine:
                 self.bucket_ranges.append([r for r in ((a, skip[0]), (skip[1], b)) if r[1] > r[0]])
             else:
                 self.bucket_ranges.append([(a, b)])
+        self.temb_bucket = None
+        if (self.cfg.temb_sparse and self.segmented and self.grad_tensors.temb is not None
+                and (rows is None or rows >= self.prog.cfg.total_steps)):
+            for k, (a, b) in enumerate(bounds):
+                if a <= to and to + tn <= b:
+                    self.temb_bucket = k
+                    self.bucket_ranges[k] = [r for a2, b2 in self.bucket_ranges[k]
+                                             for r in ((a2, min(b2, to)), (max(a2, to + tn), b2)) if r[1] > r[0]]
+        self._temb_t: List[torch.Tensor] = []
         # LayerNorm dgamma/dbeta replica workspace in backward order: final norm,
         # then norm2, norm1 of blocks L-1 .. 0; destinations = grad-arena views
         # (weight and bias of one LayerNorm are adjacent: one [2D] range).
@@ -299,6 +314,7 @@ class TrainEngine:
         # EMA moves once per optimizer step (multi_gpu_trainer.py:126 semantics).
         tail = self.lnfold is not None
         loss_acc = None
+        self._temb_t = []
         for micro in range(k_acc):
             last = micro == k_acc - 1
             if micro > 0:
@@ -310,6 +326,7 @@ class TrainEngine:
                 (img, tgt, t), cold = spec()  # drawn inside the patch-embedding launch
             else:
                 img, tgt, t = self.batch_fn()
+            self._temb_t.append(t)
             if fused_loss:
                 # head GEMM epilogue computes the loss partials and the token-layout gradient
                 (loss_parts, dtok), S = self.prog.forward(self.param_tensors, img, t, self.rng, True,
@@ -404,6 +421,8 @@ class TrainEngine:
                     ops.wire_pack(self.flat_g[a:b], w)
                     dist.all_reduce(w, group=self.pg)
                     ops.wire_unpack(w, self.flat_g[a:b])
+            if k == self.temb_bucket:
+                self._temb_exchange()
 
         if self.comm is not None:
             self.comm.wait_stream(torch.cuda.current_stream(self.device))
@@ -413,6 +432,29 @@ class TrainEngine:
                 reduce()
         else:
             reduce()
+
+    def _temb_exchange(self):
+        """Sum the time_embed gradient over ranks from its non-zero rows only.
+
+        Each rank contributes (t, row) for the distinct timesteps of its micro-batches
+        (a repeated t keeps its first row, which already holds every sample's
+        contribution), all-gathered; every rank then forms each gathered row's total
+        with one [W*n, W*n] 0/1 matrix product over the gathered rows -- the same
+        inputs and the same kernel on every rank, so the replicas stay bit-identical
+        (a scatter-add with atomics would round differently per rank) -- and writes it
+        back to those rows.  Rows no rank touched are zero everywhere already."""
+        g = self.grad_tensors.temb
+        idx = torch.cat([t.reshape(-1) for t in self._temb_t]).to(torch.int64)
+        n = idx.numel()
+        rows = g.index_select(0, idx)
+        first = ~(idx[:, None] == idx[None, :]).tril(-1).any(1)
+        rows.mul_(first[:, None].to(rows.dtype))
+        idx_all = idx.new_empty(self.world * n)
+        rows_all = rows.new_empty(self.world * n, g.shape[1])
+        dist.all_gather_into_tensor(idx_all, idx, group=self.pg)
+        dist.all_gather_into_tensor(rows_all, rows, group=self.pg)
+        same = (idx_all[:, None] == idx_all[None, :]).to(rows.dtype)
+        g.index_copy_(0, idx_all, same @ rows_all)
 
     def _join_comm(self):
         if self.comm is not None:

@@ -122,19 +122,21 @@ def test_nonfinite_grad_skips_update():
     assert int(eng.step_ctr[0]) == 0 and int(eng.step_ctr[1]) == 1
 
 
-def _ddp_worker(rank, world, port, out_path, wire="fp32"):
+def _ddp_worker(rank, world, port, out_path, wire="fp32", gauss=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         model = _model(drop=False, seed=rank)  # different init per rank: engine must broadcast rank 0's
         eng = TrainEngine(model, EngineConfig(lr=1e-3, weight_decay=0.0, max_grad_norm=0.0, bucket_blocks=1,
-                                              temb_rows=7, grad_wire=wire), device="cpu")
-        # inactive time_embed rows skipped; the embeddings have their own last bucket
+                                              temb_rows=None if gauss else 7, grad_wire=wire), device="cpu")
+        # inactive time_embed rows skipped (cold) or the whole table exchanged as
+        # all-gathered rows (Gaussian); the embeddings have their own last bucket
         reduced = sum(b - a for rs in eng.bucket_ranges for a, b in rs)
-        assert reduced == eng.numel - (2000 - 7) * model.embed_dim
+        assert reduced == eng.numel - (2000 - (0 if gauss else 7)) * model.embed_dim
+        assert (eng.temb_bucket is not None) == gauss
         assert eng.bucket_ranges[-1][-1][1] <= eng.offsets["blocks.0.norm1.weight"][0]
         x, y, t = _batch(4, seed=5)
-        t = t % 6 + 1  # cold-diffusion timesteps
+        t = t % 6 + 1 if not gauss else t[[0, 0, 1, 0]]  # cold timesteps / repeats across and within ranks
         b = 4 // world
         eng.step(x[rank * b:(rank + 1) * b], y[rank * b:(rank + 1) * b], t[rank * b:(rank + 1) * b])
         m = eng.flat_m.clone()
@@ -147,22 +149,27 @@ def _ddp_worker(rank, world, port, out_path, wire="fp32"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("wire,tol", [("fp32", 1e-4), ("bf16", 2e-2)])
-def test_data_parallel_gloo_matches_single_process(wire, tol):
-    """Bucketed all-reduce over 2 ranks == one process on the full batch (no dropout)."""
+@pytest.mark.parametrize("wire,tol,gauss", [("fp32", 1e-4, False), ("bf16", 2e-2, False), ("fp32", 1e-4, True)])
+def test_data_parallel_gloo_matches_single_process(wire, tol, gauss):
+    """Bucketed all-reduce over 2 ranks == one process on the full batch (no dropout);
+    gauss: sparse time_embed row exchange, with a t repeated inside and across ranks."""
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "r.pt")
-        mp.start_processes(_ddp_worker, args=(2, free_port(), out, wire), nprocs=2, join=True, start_method="spawn")
+        mp.start_processes(_ddp_worker, args=(2, free_port(), out, wire, gauss), nprocs=2, join=True,
+                           start_method="spawn")
         r = torch.load(out, weights_only=True)
     assert r["same"]
     model = _model(drop=False, seed=0)
     eng = TrainEngine(model, EngineConfig(lr=1e-3, weight_decay=0.0, max_grad_norm=0.0), device="cpu")
     x, y, t = _batch(4, seed=5)
-    eng.step(x, y, t % 6 + 1)
+    eng.step(x, y, t[[0, 0, 1, 0]] if gauss else t % 6 + 1)
     m1 = eng.flat_m
     # exp_avg after one step = (1-b1) * mean-gradient
     err = (r["m"] - m1).abs().max().item() / m1.abs().max().item()
     assert err < tol, err
+    o, k = eng.offsets["time_embed.weight"]
+    te, te1 = r["m"][o:o + k], m1[o:o + k]
+    assert te1.abs().max() > 0 and (te - te1).abs().max().item() < tol * te1.abs().max().item()
 
 
 def test_grad_accumulation_matches_full_batch():

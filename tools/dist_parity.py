@@ -11,16 +11,20 @@ import torch
 import torch.distributed as dist
 from ddim_cold_amd.models import build_model
 from ddim_cold_amd.train.engine import EngineConfig, TrainEngine
-from ddim_cold_amd.data.synthetic import ColdBatcher, synthetic_pool
+from ddim_cold_amd.data.synthetic import ColdBatcher, GaussianBatcher, synthetic_pool
 
 
-def run(dist_mode, comm="torch", wire="fp32"):
+def run(dist_mode, comm="torch", wire="fp32", gauss=False):
     torch.manual_seed(0)
     model = build_model("vit_tiny").cuda().train()
-    cfg = EngineConfig(lr=1e-3, t_max=100, seed=5, temb_rows=7, force_segments=dist_mode is not None,
+    cfg = EngineConfig(lr=1e-3, t_max=100, seed=5, temb_rows=None if gauss else 7,
+                       force_segments=dist_mode is not None,
                        graph_comm=dist_mode == "captured", graph_warmup=2, comm=comm, grad_wire=wire)
     eng = TrainEngine(model, cfg)
-    eng.set_batch_fn(ColdBatcher(synthetic_pool(64, seed=3, device="cuda"), 16, eng.rng))
+    pool = synthetic_pool(64, seed=3, device="cuda")
+    # Gaussian diffusion (t over the whole table): sparse time_embed row exchange
+    eng.set_batch_fn(GaussianBatcher(pool, 16, eng.rng, 2000) if gauss else ColdBatcher(pool, 16, eng.rng))
+    assert (eng.temb_bucket is not None) == (gauss and dist_mode is not None)
     for _ in range(6):
         eng.train_step()
     torch.cuda.synchronize()
@@ -57,7 +61,11 @@ if __name__ == "__main__":
     # native RCCL communicator (csrc/comm.cpp): captured in the step graph, fp32 and bf16 wire
     nat, loss3, failed3, ng3 = run("captured", comm="native")
     natb, loss4, failed4, ng4 = run("captured", comm="native", wire="bf16")
+    gref, gl0, _, _ = run(None, gauss=True)
+    gcap, gl1, gfailed, gng = run("captured", gauss=True)
     dist.destroy_process_group()
+    assert not gfailed and gng == 1, "sparse time_embed exchange not captured"
+    assert (gref - gcap).abs().max().item() <= 2 * 1e-3 * 6 and abs(gl1 - gl0) <= 1e-4 * abs(gl0), (gl0, gl1)
     print(f"losses {loss0:.6f} {loss1:.6f} {loss2:.6f} native {loss3:.6f} native-bf16 {loss4:.6f}; "
           f"graphs captured={ng1} segmented={ng2} native={ng3}/{ng4}; fallback={failed} {failed3} {failed4}")
     assert not (failed or failed3 or failed4), "graph capture of collectives fell back"
