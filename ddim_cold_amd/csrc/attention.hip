@@ -850,9 +850,11 @@ template <int HD, int NP, bool DROP>
 __global__ __launch_bounds__(NP * 4) void attn_fwd_short_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                                 float* __restrict__ lse, int B, int H, int N,
                                                                 float scale, const int64_t* __restrict__ rng,
-                                                                int site, uint32_t thr, float dsc) {
+                                                                int site, uint32_t thr, float dsc,
+                                                                uint32_t* __restrict__ keep_bits) {
   using I = ShortImg<HD, NP>;
   constexpr int RS = I::RS, KS = HD / 32, DT = HD / 16, KT = NP / 16;
+  static_assert(KT * 4 <= 32, "one 32-bit keep word per lane");
   __shared__ __attribute__((aligned(16))) char lds[2 * NP * RS];
   char* Kl = lds;
   char* Vl = lds + NP * RS;
@@ -895,6 +897,7 @@ __global__ __launch_bounds__(NP * 4) void attn_fwd_short_kernel(const bf16* __re
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
   float l = 0.f;
   const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * attn_mask_ld(N));
+  uint32_t kbits = 0u;
 #pragma unroll
   for (int t = 0; t < KT; ++t) {
     bool kp[4] = {true, true, true, true};
@@ -903,10 +906,16 @@ __global__ __launch_bounds__(NP * 4) void attn_fwd_short_kernel(const bf16* __re
     for (int r = 0; r < 4; ++r) {
       float pv = exp2f(st[t][r] - mx);
       l += pv;
-      if (DROP) pv = kp[r] ? pv * dsc : 0.f;
+      if (DROP) {
+        pv = kp[r] ? pv * dsc : 0.f;
+        kbits |= (kp[r] ? 1u : 0u) << (4 * t + r);
+      }
       st[t][r] = pv;
     }
   }
+  // the keep flags of this lane's (query, 16t + 4g + r) elements for the backward
+  // (same lane layout there): one word per lane instead of re-hashing KT*2 pairs
+  if (DROP && keep_bits != nullptr) keep_bits[((size_t)bh * NP + q) * 4 + g] = kbits;
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
   f32x4 o[DT];
@@ -941,7 +950,8 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
                                                                 bf16* __restrict__ dqkv, int B, int H, int N,
                                                                 float scale, const int64_t* __restrict__ rng,
                                                                 int site, uint32_t thr, float dsc,
-                                                                const bf16* __restrict__ wp, int Dm) {
+                                                                const bf16* __restrict__ wp, int Dm,
+                                                                const uint32_t* __restrict__ keep_bits) {
   using I = ShortImg<HD, NP>;
   constexpr int RS = I::RS, PS = 2 * NP + 32, KS = HD / 32, DT = HD / 16, KT = NP / 16;
   __shared__ __attribute__((aligned(16))) char lds[4 * NP * RS + 2 * NP * PS];
@@ -1001,6 +1011,9 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
     for (int s = 0; s < KS; ++s) of[s] = *reinterpret_cast<const bf16x8*>(orow + 32 * s + 8 * g);
   }
   const float lse_raw = lse[(size_t)bh * N + qc];
+  // the forward's keep flags (attn_fwd_short_kernel layout) when it stored them
+  const bool have_bits = DROP && keep_bits != nullptr;
+  const uint32_t kbits = have_bits ? keep_bits[((size_t)bh * NP + q) * 4 + g] : 0u;
   const uint32_t salt = DROP ? site_salt(rng, site) : 0u;
   iq.store(Ql);
   ik.store(Kl);
@@ -1066,7 +1079,14 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
     }
     f32x4 pm;
     bool kq[4] = {true, true, true, true};
-    if (DROP) dropout_keep4(salt, rowidx + (uint32_t)(16 * t + 4 * g), thr, kq);
+    if (DROP) {
+      if (have_bits) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) kq[r] = (kbits >> (4 * t + r)) & 1u;
+      } else {
+        dropout_keep4(salt, rowidx + (uint32_t)(16 * t + 4 * g), thr, kq);
+      }
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int key = 16 * t + 4 * g + r;
@@ -1131,53 +1151,55 @@ template <int HD, int NP, bool DROP>
 struct ShortLaunch {
   static void run(bool bwd, const bf16* d, const bf16* q, const bf16* o, float* lse, const float* lse_in,
                   bf16* outp, int B, int H, int N, float scale, const int64_t* rng, int site, uint32_t thr,
-                  float dsc, hipStream_t stream, const bf16* wp, int Dm) {
+                  float dsc, hipStream_t stream, const bf16* wp, int Dm, uint32_t* kb) {
     if (!bwd)
       hipLaunchKernelGGL((attn_fwd_short_kernel<HD, NP, DROP>), dim3(B * H), dim3(NP * 4), 0, stream, q, outp, lse,
-                         B, H, N, scale, rng, site, thr, dsc);
+                         B, H, N, scale, rng, site, thr, dsc, kb);
     else if (wp != nullptr)
       hipLaunchKernelGGL((attn_bwd_short_kernel<HD, NP, DROP, true>), dim3(B * H), dim3(NP * 4), 0, stream, d, q, o,
-                         lse_in, outp, B, H, N, scale, rng, site, thr, dsc, wp, Dm);
+                         lse_in, outp, B, H, N, scale, rng, site, thr, dsc, wp, Dm, kb);
     else
       hipLaunchKernelGGL((attn_bwd_short_kernel<HD, NP, DROP, false>), dim3(B * H), dim3(NP * 4), 0, stream, d, q, o,
-                         lse_in, outp, B, H, N, scale, rng, site, thr, dsc, wp, Dm);
+                         lse_in, outp, B, H, N, scale, rng, site, thr, dsc, wp, Dm, kb);
   }
 };
 
 template <int HD, int NP>
 static void launch_short(bool bwd, const bf16* d, const bf16* q, const bf16* o, float* lse, const float* lse_in,
                          bf16* outp, int B, int H, int N, float scale, const int64_t* rng, int site, uint32_t thr,
-                         float dsc, hipStream_t stream, const bf16* wp = nullptr, int Dm = 0) {
+                         float dsc, hipStream_t stream, const bf16* wp, int Dm, uint32_t* kb) {
   if (thr)
-    ShortLaunch<HD, NP, true>::run(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, wp, Dm);
+    ShortLaunch<HD, NP, true>::run(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, wp, Dm,
+                                   kb);
   else
     ShortLaunch<HD, NP, false>::run(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, wp,
-                                    Dm);
+                                    Dm, kb);
 }
 
 template <int HD>
 static void dispatch_short(bool bwd, const bf16* d, const bf16* q, const bf16* o, float* lse, const float* lse_in,
                            bf16* outp, int B, int H, int N, float scale, const int64_t* rng, int site, uint32_t thr,
-                           float dsc, hipStream_t stream, const bf16* wp = nullptr, int Dm = 0) {
+                           float dsc, hipStream_t stream, const bf16* wp = nullptr, int Dm = 0,
+                           uint32_t* kb = nullptr) {
   switch ((N + 31) / 32) {
-    case 1: launch_short<HD, 32>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, wp, Dm); break;
-    case 2: launch_short<HD, 64>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, wp, Dm); break;
-    case 3: launch_short<HD, 96>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, wp, Dm); break;
-    default: launch_short<HD, 128>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, wp, Dm); break;
+    case 1: launch_short<HD, 32>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, wp, Dm, kb); break;
+    case 2: launch_short<HD, 64>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, wp, Dm, kb); break;
+    case 3: launch_short<HD, 96>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, wp, Dm, kb); break;
+    default: launch_short<HD, 128>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, wp, Dm, kb); break;
   }
 }
 
 #define DC_INST_SHORT1(HD, NP, DR)                                                                                 \
   template __global__ void attn_fwd_short_kernel<HD, NP, DR>(const bf16*, bf16*, float*, int, int, int, float,    \
-                                                             const int64_t*, int, uint32_t, float);               \
+                                                             const int64_t*, int, uint32_t, float, uint32_t*);    \
   template __global__ void attn_bwd_short_kernel<HD, NP, DR, false>(const bf16*, const bf16*, const bf16*,        \
                                                                     const float*, bf16*, int, int, int, float,    \
                                                                     const int64_t*, int, uint32_t, float,         \
-                                                                    const bf16*, int);                            \
+                                                                    const bf16*, int, const uint32_t*);           \
   template __global__ void attn_bwd_short_kernel<HD, NP, DR, true>(const bf16*, const bf16*, const bf16*,         \
                                                                    const float*, bf16*, int, int, int, float,     \
                                                                    const int64_t*, int, uint32_t, float,          \
-                                                                   const bf16*, int);
+                                                                   const bf16*, int, const uint32_t*);
 #define DC_INST_SHORT(HD, NP) DC_INST_SHORT1(HD, NP, true) DC_INST_SHORT1(HD, NP, false)
 DC_INST_SHORT(32, 32) DC_INST_SHORT(32, 64) DC_INST_SHORT(32, 96) DC_INST_SHORT(32, 128)
 DC_INST_SHORT(64, 32) DC_INST_SHORT(64, 64) DC_INST_SHORT(64, 96) DC_INST_SHORT(64, 128)
@@ -1427,16 +1449,25 @@ static bool short_disabled() {
 
 using namespace dc;
 
+int64_t attn_keep_words(int B, int H, int N, int hd) {
+  if (N > SHORT_MAX_N || short_disabled() || (hd != 32 && hd != 64)) return 0;
+  return (int64_t)B * H * (32 * ((N + 31) / 32)) * 4;
+}
+
 void attn_fwd_launch(const void* qkv, void* o, float* lse, int B, int H, int N, int hd, float scale,
-                     const int64_t* rng, int site, double p, hipStream_t stream) {
+                     const int64_t* rng, int site, double p, hipStream_t stream, uint32_t* keep_bits) {
   const dim3 grid((N + 63) / 64, B * H);
   const uint32_t thr = drop_threshold_host(p);
   const float dsc = p > 0 ? 1.f / (1.f - (float)p) : 1.f;
   const bf16* q = reinterpret_cast<const bf16*>(qkv);
   bf16* out = reinterpret_cast<bf16*>(o);
   if (N <= SHORT_MAX_N && !short_disabled() && (hd == 32 || hd == 64)) {
-    if (hd == 32) dispatch_short<32>(false, nullptr, q, nullptr, lse, nullptr, out, B, H, N, scale, rng, site, thr, dsc, stream);
-    else dispatch_short<64>(false, nullptr, q, nullptr, lse, nullptr, out, B, H, N, scale, rng, site, thr, dsc, stream);
+    if (hd == 32)
+      dispatch_short<32>(false, nullptr, q, nullptr, lse, nullptr, out, B, H, N, scale, rng, site, thr, dsc, stream,
+                         nullptr, 0, keep_bits);
+    else
+      dispatch_short<64>(false, nullptr, q, nullptr, lse, nullptr, out, B, H, N, scale, rng, site, thr, dsc, stream,
+                         nullptr, 0, keep_bits);
     return;
   }
   static const bool v1 = [] {
@@ -1474,7 +1505,8 @@ void attn_fwd_launch(const void* qkv, void* o, float* lse, int B, int H, int N, 
 
 void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const float* lse, void* dqkv,
                         float* delta, int B, int H, int N, int hd, float scale, const int64_t* rng, int site,
-                        double p, hipStream_t stream) {
+                        double p, hipStream_t stream, const uint32_t* keep_bits) {
+  uint32_t* kb = const_cast<uint32_t*>(keep_bits);  // read-only in the backward kernel
   const dim3 grid((N + 63) / 64, B * H);
   const uint32_t thr = drop_threshold_host(p);
   const float dsc = p > 0 ? 1.f / (1.f - (float)p) : 1.f;
@@ -1483,8 +1515,8 @@ void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const flo
   const bf16* oo = reinterpret_cast<const bf16*>(o);
   bf16* dq = reinterpret_cast<bf16*>(dqkv);
   if (N <= SHORT_MAX_N && !short_disabled() && (hd == 32 || hd == 64)) {
-    if (hd == 32) dispatch_short<32>(true, d, q, oo, nullptr, lse, dq, B, H, N, scale, rng, site, thr, dsc, stream);
-    else dispatch_short<64>(true, d, q, oo, nullptr, lse, dq, B, H, N, scale, rng, site, thr, dsc, stream);
+    if (hd == 32) dispatch_short<32>(true, d, q, oo, nullptr, lse, dq, B, H, N, scale, rng, site, thr, dsc, stream, nullptr, 0, kb);
+    else dispatch_short<64>(true, d, q, oo, nullptr, lse, dq, B, H, N, scale, rng, site, thr, dsc, stream, nullptr, 0, kb);
     return;
   }
   if (hd == 32) {

@@ -228,7 +228,22 @@ Tensor qkv_fwd(Tensor a, Tensor w, Tensor b, int64_t B, int64_t N, int64_t H, c1
   return out;
 }
 
-std::tuple<Tensor, Tensor> attn_fwd(Tensor qkv, double scale, Tensor rng, int64_t site, double p) {
+// attention-dropout keep-flag words the short forward stores for the backward
+// (0: this shape takes the long-sequence kernels, which regenerate the masks)
+int64_t attn_keep_words_op(int64_t B, int64_t H, int64_t N, int64_t hd) {
+  return attn_keep_words((int)B, (int)H, (int)N, (int)hd);
+}
+
+static uint32_t* keep_ptr(const c10::optional<Tensor>& keep, int B, int H, int N, int hd) {
+  if (!keep.has_value()) return nullptr;
+  CHECK_IN(keep.value(), at::kInt);
+  const int64_t need = attn_keep_words(B, H, N, hd);
+  TORCH_CHECK(need > 0 && keep->numel() >= need, "attention keep-flag buffer: need ", need, " int32 words");
+  return reinterpret_cast<uint32_t*>(keep->data_ptr<int32_t>());
+}
+
+std::tuple<Tensor, Tensor> attn_fwd(Tensor qkv, double scale, Tensor rng, int64_t site, double p,
+                                    c10::optional<Tensor> keep_out) {
   CHECK_IN(qkv, BF16); check_rng(rng);
   const c10::DeviceGuard guard(qkv.device());
   TORCH_CHECK(qkv.dim() == 5 && qkv.size(0) == 3, "qkv must be [3,B,H,N,hd]");
@@ -237,7 +252,7 @@ std::tuple<Tensor, Tensor> attn_fwd(Tensor qkv, double scale, Tensor rng, int64_
   auto o = at::empty({B, N, H * hd}, qkv.options());
   auto lse = at::empty({B, H, N}, qkv.options().dtype(F32));
   attn_fwd_launch(qkv.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), B, H, N, hd, (float)scale,
-                  rng.data_ptr<int64_t>(), site, p, cur_stream());
+                  rng.data_ptr<int64_t>(), site, p, cur_stream(), keep_ptr(keep_out, B, H, N, hd));
   return {o, lse};
 }
 
@@ -789,7 +804,8 @@ void replica_reduce_(Tensor ws, Tensor dst_ptrs, int64_t C) {
                         cur_stream());
 }
 
-Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, double scale, Tensor rng, int64_t site, double p) {
+Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, double scale, Tensor rng, int64_t site, double p,
+                c10::optional<Tensor> keep) {
   CHECK_IN(dout, BF16); CHECK_IN(qkv, BF16); CHECK_IN(o, BF16); CHECK_IN(lse, F32); check_rng(rng);
   const c10::DeviceGuard guard(qkv.device());
   TORCH_CHECK(qkv.dim() == 5 && qkv.size(0) == 3, "qkv must be [3,B,H,N,hd]");
@@ -802,7 +818,7 @@ Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, double scale, Ten
   auto delta = at::empty({(int64_t)B * H * N}, lse.options());
   attn_bwd_launch(dout.data_ptr(), qkv.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), dqkv.data_ptr(),
                   delta.data_ptr<float>(), B, H, N, hd, (float)scale, rng.data_ptr<int64_t>(), site, p,
-                  cur_stream());
+                  cur_stream(), keep_ptr(keep, B, H, N, hd));
   return dqkv;
 }
 
@@ -1074,7 +1090,8 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("layernorm_fwd(Tensor x, Tensor gamma, Tensor beta, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("qkv_fwd(Tensor a, Tensor w, Tensor b, int B, int N, int H, Tensor? ln_st=None, Tensor? ln_c=None, "
         "float ln_eps=1e-5, Tensor(a!)? ln_mean=None, Tensor(b!)? ln_rstd=None) -> Tensor");
-  m.def("attn_fwd(Tensor qkv, float scale, Tensor rng, int site, float p) -> (Tensor, Tensor)");
+  m.def("attn_fwd(Tensor qkv, float scale, Tensor rng, int site, float p, Tensor? keep_out=None) -> (Tensor, Tensor)");
+  m.def("attn_keep_words(int B, int H, int N, int hd) -> int", &attn_keep_words_op);
   m.def("qkv_attn_fwd(Tensor a, Tensor w, Tensor b, Tensor? ln_st, Tensor? ln_c, float ln_eps, int B, int N, int H, "
         "float scale, Tensor rng, int site, float p, bool save_qkv, Tensor(a!)? ln_mean=None, "
         "Tensor(b!)? ln_rstd=None) -> (Tensor, Tensor, Tensor)");
@@ -1118,7 +1135,8 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("ln_fold_(Tensor[] ws, Tensor[] gammas, Tensor[] betas, Tensor?[] biases, Tensor(a!)[] wfs, Tensor(b!)[] cs, "
         "Tensor(c!)[] bfs, Tensor? loss_parts=None, Tensor(d!)? loss_last=None, Tensor(e!)? loss_ema=None, "
         "float ema_decay=0.99, Tensor(f!)? step=None, Tensor(g!)? rng=None, Tensor? sq=None) -> ()");
-  m.def("attn_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, float scale, Tensor rng, int site, float p) -> Tensor");
+  m.def("attn_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, float scale, Tensor rng, int site, float p, "
+        "Tensor? keep=None) -> Tensor");
   m.def("embed_bwd(Tensor g, Tensor t, Tensor rng, int site, float p, Tensor(a!) dcls, Tensor(b!) dpos, "
         "Tensor(c!) dtemb, Tensor(d!)? ln_ws=None, Tensor? ln_ptrs=None, int ln_C=0) -> Tensor");
   m.def("sqnorm(Tensor g, Tensor(a!) out, float scale) -> ()");

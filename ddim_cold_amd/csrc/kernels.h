@@ -151,11 +151,15 @@ void ln_fold_launch(const FoldTable& tb, hipStream_t stream);
 void replica_reduce_launch(float* ws, float* const* dsts_dev, int G, int C, hipStream_t stream);
 
 // Attention (attention.hip)
+// keep_bits: optional [attn_keep_words] attention-dropout keep flags, written by
+// the short-sequence forward and read by its backward instead of re-hashing
+// (ignored by the long-sequence kernels, which always regenerate)
+int64_t attn_keep_words(int B, int H, int N, int hd);
 void attn_fwd_launch(const void* qkv, void* o, float* lse, int B, int H, int N, int hd, float scale,
-                     const int64_t* rng, int site, double p, hipStream_t stream);
+                     const int64_t* rng, int site, double p, hipStream_t stream, uint32_t* keep_bits = nullptr);
 void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const float* lse, void* dqkv,
                      float* delta, int B, int H, int N, int hd, float scale, const int64_t* rng, int site,
-                     double p, hipStream_t stream);
+                     double p, hipStream_t stream, const uint32_t* keep_bits = nullptr);
 
 // Embedding / head / loss (embed.hip)
 // Optional cold-diffusion batch source fused into patchify (pool != nullptr): the

@@ -71,6 +71,11 @@ GROUP_FWD = os.environ.get("DDIM_COLD_GROUP_FWD", "0") == "1"
 # 390-workgroup dgrad + attention backward (0.836 vs 0.823 ms/step, 3
 # interleaved 1000-step pairs, tools/gpu_ap.sh): opt-in (DDIM_COLD_ATTN_PROJ=1)
 ATTN_PROJ = os.environ.get("DDIM_COLD_ATTN_PROJ", "0") == "1"
+# the short attention forward stores its dropout keep flags (one 32-bit word per
+# lane, 0.6 MB per block for ViT-tiny at B=32) and the backward reads them instead
+# of re-hashing 2 pairs per 4 probabilities (the mask hash was ~1.9 us of the
+# backward's ~11 us, tools/ub_drop.py).  Same masks either way.
+STORE_ATTN_KEEP = os.environ.get("DDIM_COLD_ATTN_KEEP", "1") != "0"
 # dtype of the bf16 activation copies / folded weights the program allocates
 # (tests on CPU switch it to fp32 to isolate the program logic from rounding)
 ACT_DTYPE = torch.bfloat16
@@ -259,6 +264,7 @@ class Saved:
     t: torch.Tensor
     patches: torch.Tensor
     blocks: list = field(default_factory=list)
+    keeps: list = field(default_factory=list)  # per block: stored attention keep flags or None
     xL: Optional[torch.Tensor] = None
     lf: Optional[torch.Tensor] = None
     mf: Optional[torch.Tensor] = None
@@ -404,7 +410,10 @@ class ViTProgram:
                                                fold=fold)
             else:
                 qkv = ops.qkv_fwd(xb, bp.qkv_wf, bp.qkv_bf, B, N, c.heads, fold=fold)
-                o, lse = ops.attn_fwd(qkv, c.scale, rng, sa, ad)
+                keep = ops.attn_keep_buffer(qkv, ad) if save and STORE_ATTN_KEEP else None
+                o, lse = ops.attn_fwd(qkv, c.scale, rng, sa, ad, keep_out=keep)
+                if save:
+                    S.keeps.append(keep)
             o = o.view(M, D)
             x1b = torch.empty(M, D, dtype=ACT_DTYPE, device=dev)
             x1 = ops.linear_residual_fwd(o, bp.proj_w, bp.proj_b, x0, N, rng, sp, pd, sd1, dpr[i],
@@ -584,7 +593,8 @@ class ViTProgram:
             if fuse_ap:
                 dqkv = ops.attn_bwd_proj(gy1, bp.proj_w, qkv, o, lse, c.scale, rng, sa, ad)
             else:
-                dqkv = ops.attn_bwd(do, qkv, o, lse, c.scale, rng, sa, ad)
+                dqkv = ops.attn_bwd(do, qkv, o, lse, c.scale, rng, sa, ad,
+                                    keep=S.keeps[i] if len(S.keeps) == L else None)
             qs = QKV_DGRAD_SPLITS if 3 * D >= 768 else 1
             if ride:
                 dl1 = ops.linear_dgrad_ride(dqkv, bp.qkv_w, riders_q, f32, qs)

@@ -17,7 +17,7 @@ from . import reference as ref
 from ._ext import force_reference
 
 __all__ = [
-    "native_available", "patch_embed_fwd", "layernorm_fwd", "qkv_fwd", "attn_fwd",
+    "native_available", "patch_embed_fwd", "layernorm_fwd", "qkv_fwd", "attn_fwd", "attn_keep_buffer",
     "linear_residual_fwd", "linear_gelu_fwd", "head_fwd", "smooth_l1_fwd_bwd", "img_to_tokgrad",
     "linear_dgrad", "linear_dgrad_gelu", "linear_wgrad", "layernorm_bwd", "attn_bwd", "embed_bwd",
     "sqnorm", "adamw_step", "advance_counters", "ddim_step", "ddim_step_", "randn_", "q_sample",
@@ -120,9 +120,21 @@ def qkv_attn_fwd(a, w, b, B: int, N: int, H: int, scale: float, rng, site: int, 
     return o, lse, (qkv if save_qkv else None)
 
 
-def attn_fwd(qkv, scale: float, rng, site: int, p: float):
+def attn_keep_buffer(qkv, p: float):
+    """int32 buffer for the attention-dropout keep flags the short-sequence forward
+    stores for its backward (one word per lane: no mask re-hashing there), or None
+    when there is nothing to store (p = 0, CPU, or a long sequence)."""
+    if p <= 0 or not _hip(qkv):
+        return None
+    _, B, H, N, hd = qkv.shape
+    n = int(_ops().attn_keep_words(B, H, N, hd))
+    return torch.empty(n, dtype=torch.int32, device=qkv.device) if n > 0 else None
+
+
+def attn_fwd(qkv, scale: float, rng, site: int, p: float, keep_out=None):
+    """``keep_out`` (:func:`attn_keep_buffer`): also store the dropout keep flags."""
     if _hip(qkv):
-        return _ops().attn_fwd(qkv, float(scale), rng, site, float(p))
+        return _ops().attn_fwd(qkv, float(scale), rng, site, float(p), keep_out)
     return ref.attn_fwd(qkv, scale, rng, site, p)
 
 
@@ -424,9 +436,10 @@ def replica_reduce_(ws, dst_ptrs, C: int, dsts=None):
     ws.zero_()
 
 
-def attn_bwd(do, qkv, o, lse, scale: float, rng, site: int, p: float):
+def attn_bwd(do, qkv, o, lse, scale: float, rng, site: int, p: float, keep=None):
+    """``keep``: the keep flags :func:`attn_fwd` stored (same masks as re-hashing)."""
     if _hip(qkv):
-        return _ops().attn_bwd(do, qkv, o, lse, float(scale), rng, site, float(p))
+        return _ops().attn_bwd(do, qkv, o, lse, float(scale), rng, site, float(p), keep)
     return ref.attn_bwd(do, qkv, o, lse, scale, rng, site, p)
 
 

@@ -382,6 +382,12 @@ def test_attention_fwd_bwd(B, H, N, hd, p):
     dqr = ref.attn_bwd(do, qkv, o, lse, scale, r, 5, p)
     assert dq.shape == (B * N, 3 * H * hd)
     close(dq, dqr, 3e-2, 3e-2, "dqkv")
+    # keep flags stored by the forward == masks re-hashed in the backward, bit for bit
+    keep = ops.attn_keep_buffer(qkv, p)
+    if keep is not None:
+        o2, lse2 = ops.attn_fwd(qkv, scale, r, 5, p, keep_out=keep)
+        assert torch.equal(o2, o) and torch.equal(lse2, lse)
+        assert torch.equal(ops.attn_bwd(do, qkv, o, lse, scale, r, 5, p, keep=keep), dq)
 
 
 def test_attention_spike_rescale():
