@@ -40,6 +40,8 @@ def _init_single(dev_index=0):
     backend = "nccl" if torch.cuda.is_available() else "gloo"
     kw = {}
     if backend == "nccl":
+        from ddim_cold_amd.parallel.dist import graph_safe_nccl_env
+        graph_safe_nccl_env()
         torch.cuda.set_device(dev_index)
         kw["device_id"] = torch.device("cuda", dev_index)
     dist.init_process_group(backend, rank=0, world_size=1, timeout=datetime.timedelta(seconds=300), **kw)

@@ -33,6 +33,18 @@ def env_world():
         int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
 
 
+def graph_safe_nccl_env():
+    """Environment for RCCL collectives captured in hipGraphs (call before the
+    process group exists).  ProcessGroupNCCL's watchdog thread polls the HIP
+    events of in-flight eager collectives; with its event cache on, an event of
+    a finished eager collective can be recycled into a collective recorded during
+    a capture and then polled -- seen on MI355X as the watchdog aborting the
+    process ("operation not permitted on an event last recorded in a capturing
+    stream").  Each collective then owns its events instead (the captured step
+    issues no eager collectives, so nothing is lost)."""
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+
+
 def init_distributed(backend: Optional[str] = None, rank: Optional[int] = None, world_size: Optional[int] = None,
                      master_addr: Optional[str] = None, master_port: Optional[int] = None,
                      timeout_s: int = 600) -> bool:
@@ -52,6 +64,7 @@ def init_distributed(backend: Optional[str] = None, rank: Optional[int] = None, 
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     kw = {}
     if backend == "nccl":
+        graph_safe_nccl_env()
         local = int(os.environ.get("LOCAL_RANK", rank % max(torch.cuda.device_count(), 1)))
         dev = torch.device("cuda", local)
         torch.cuda.set_device(dev)

@@ -13,11 +13,12 @@ AdamW step, cosine LR step, zero_grad) re-designed for a latency-bound
 * **Fused optimizer.**  3 launches per step (global grad-norm, AdamW + clip +
   cosine LR + bf16 shadow refresh + grad zeroing, counter bump); the LR /
   Adam step / RNG step live in device memory so the step is graph-replayable.
-* **Grouped weight gradients.**  The four weight-gradient GEMMs of a block
-  (and the head's, with the last block) are one grouped launch at the end of
-  the block's backward (``ops.WgradBatch``): 216 output tiles fill the chip
-  without a token split, so no atomics.  (Issuing them one by one on a side
-  stream, ``wgrad_stream=True``, measured slower.)
+* **Deferred weight gradients.**  Single process: every weight-gradient GEMM
+  of the step is ONE launch after the embedding backward
+  (``ops.linear_wgrad_multi``, 1,548 64x64 tiles, no token split, no atomics).
+  Data parallel: one such launch per gradient bucket, so each bucket's
+  all-reduce can start while the remaining blocks run backward.  (Issuing them
+  on a side stream, ``wgrad_stream=True``, measured slower.)
 * **One hipGraph per step, bucketed RCCL all-reduce inside it.**  Gradient
   buckets are contiguous arena ranges closed at transformer-block boundaries
   of the backward; as soon as a bucket's gradients are final its
@@ -45,6 +46,12 @@ from ..models import program as _program
 from ..models.program import LnFold, ModelTensors, ViTProgram, collect, is_matrix_param
 
 ALIGN = 64  # elements (256 B fp32)
+# Step graphs are captured in thread-local mode: other threads' HIP calls during a
+# capture (ProcessGroupNCCL's watchdog polling the events of eager collectives)
+# neither invalidate the capture nor fail in that thread.  In the default global
+# mode a watchdog poll inside the capture window was seen on MI355X to invalidate
+# the capture (fallback to segments) and abort the process from the watchdog.
+CAPTURE_MODE = "thread_local"
 
 
 @dataclass
@@ -491,6 +498,12 @@ class TrainEngine:
 
     def _capture_impl(self, graph_comm: bool):
         from ..utils.observe import no_gc
+        if self.dist_on and self.is_cuda:
+            # let the eager collectives of the warm-up finish and the process-group
+            # watchdog drop them (it polls every ~100 ms) before the capture opens
+            import time
+            torch.cuda.synchronize(self.device)
+            time.sleep(0.3)
         with no_gc():
             self._capture_graphs(graph_comm)
 
@@ -502,13 +515,13 @@ class TrainEngine:
         nseg = len(self.buckets) + 1 if (self.segmented and not graph_comm) else 1
         if nseg == 1:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
+            with torch.cuda.graph(g, pool=pool, capture_error_mode=CAPTURE_MODE):
                 self._captured_step_body()
             graphs.append(g)
             K = max(1, int(self.cfg.graph_steps))
             if K > 1:  # K steps in one graph, own memory pool
                 gm = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gm, pool=torch.cuda.graph_pool_handle()):
+                with torch.cuda.graph(gm, pool=torch.cuda.graph_pool_handle(), capture_error_mode=CAPTURE_MODE):
                     for _ in range(K):
                         self._captured_step_body()
                 self._multi = (gm, K)
@@ -517,7 +530,7 @@ class TrainEngine:
             try:
                 for _ in range(nseg):
                     g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, pool=pool):
+                    with torch.cuda.graph(g, pool=pool, capture_error_mode=CAPTURE_MODE):
                         next(gen)
                     graphs.append(g)
             finally:

@@ -41,6 +41,8 @@ if __name__ == "__main__":
     os.environ.setdefault("MASTER_PORT", str(free_port()))
     torch.cuda.set_device(0)
     ref, loss0, _, _ = run(None)
+    from ddim_cold_amd.parallel.dist import graph_safe_nccl_env
+    graph_safe_nccl_env()
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     from ddim_cold_amd.parallel.comm import NativeComm, MAX
     nc = NativeComm(torch.device("cuda", 0))
