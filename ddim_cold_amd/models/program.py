@@ -626,7 +626,15 @@ class ViTProgram:
             gpatch = self._embed_backward(P, G, S, g, rng, pd, wgrad, ln_final)
             flush()
         if tail and tail_jobs:
-            ops.linear_wgrad_multi(tail_jobs)
+            tiles = sum(-(-dy.shape[1] // 64) * -(-x.shape[1] // 64) for dy, x, _, _ in tail_jobs)
+            if bucketed and tiles < 64:
+                # the embedding bucket's patch-embedding gradient alone (18 tiles for
+                # ViT-tiny): unsplit, 18 workgroups walk all 2,048 tokens (~17 us on the
+                # step's critical path); the token-split kernel fills the chip
+                for job in tail_jobs:
+                    ops.linear_wgrad(*job)
+            else:
+                ops.linear_wgrad_multi(tail_jobs)
             keep.append(tail_jobs)
         keep.append((gpatch, lf))
         if batch is not None:

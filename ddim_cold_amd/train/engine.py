@@ -185,8 +185,20 @@ class TrainEngine:
         # replica finalize); every other tensor starts 256-B aligned.
         ln_prefixes = {n[: -len(".weight")] for n, p in named
                        if n.endswith(".weight") and p.dim() == 1 and (n.startswith("norm") or ".norm" in n)}
+        # arena order: embeddings, then EVERY LayerNorm, then the blocks' Linear
+        # weights, then the head.  The LayerNorm gradients are finalised once, in the
+        # embedding-backward launch (their dgamma/dbeta replicas are only complete
+        # then); placed here they fall in the last all-reduce bucket, so data
+        # parallel needs no replica finalize launch per bucket either.
+        def group(n):
+            if n.rsplit(".", 1)[0] in ln_prefixes:
+                return 1
+            if n.startswith("blocks."):
+                return 2
+            return 3 if n.startswith("head.") else 0
+        layout = sorted(named, key=lambda np_: group(np_[0]))  # stable: original order within a group
         off = 0
-        for n, p in named:
+        for n, p in layout:
             ln_bias = n.endswith(".bias") and n[: -len(".bias")] in ln_prefixes
             if not ln_bias:
                 off = _align(off)
@@ -233,7 +245,10 @@ class TrainEngine:
             self.grad_tensors.temb = None
         # all-reduce buckets: contiguous arena ranges, boundaries after block groups (backward order)
         L = c.depth
-        starts = [self.offsets[f"blocks.{i}.norm1.weight"][0] for i in range(L)]
+        # a block's arena range starts at its first Linear weight (LayerNorms live
+        # with the embeddings, see the layout above)
+        starts = [min(self.offsets[n][0] for n in self.names if n.startswith(f"blocks.{i}.")
+                      and n.rsplit(".", 1)[0] not in ln_prefixes) for i in range(L)]
         bb = max(1, self.cfg.bucket_blocks)
         self.bucket_after: Dict[int, int] = {}
         bounds = []
@@ -357,9 +372,10 @@ class TrainEngine:
             # without a separate embedding bucket (single process) the patch-embedding
             # weight gradient joins block 0's grouped launch
             merge = not (self.segmented and self.cfg.embed_bucket)
-            # single process: the LayerNorm replica finalize rides in the embedding-backward launch
+            # the LayerNorm replica finalize rides in the embedding-backward launch (data
+            # parallel too: every LayerNorm lives in the last bucket's arena range)
             ln_final = None
-            if not self.segmented and self.ln_ptrs is not None and os.environ.get("DDIM_COLD_FUSE_LNFINAL", "1") != "0":
+            if self.ln_ptrs is not None and os.environ.get("DDIM_COLD_FUSE_LNFINAL", "1") != "0":
                 hi = self.ln_done_at[-1]
                 ln_final = (self.ln_ws[:hi], self.ln_ptrs[:hi], 2 * c.dim)
             # single process: every weight gradient in one launch after the backward

@@ -134,7 +134,10 @@ def _ddp_worker(rank, world, port, out_path, wire="fp32", gauss=False):
         reduced = sum(b - a for rs in eng.bucket_ranges for a, b in rs)
         assert reduced == eng.numel - (2000 - (0 if gauss else 7)) * model.embed_dim
         assert (eng.temb_bucket is not None) == gauss
-        assert eng.bucket_ranges[-1][-1][1] <= eng.offsets["blocks.0.norm1.weight"][0]
+        assert eng.bucket_ranges[-1][-1][1] <= eng.offsets["blocks.0.attn.qkv.weight"][0]
+        # every LayerNorm sits in the last (embedding) bucket: finalised once, after block 0
+        last = eng.buckets[-1]
+        assert all(last[0] <= eng.offsets[n][0] < last[1] for n in eng.names if ".norm" in n or n.startswith("norm"))
         x, y, t = _batch(4, seed=5)
         t = t % 6 + 1 if not gauss else t[[0, 0, 1, 0]]  # cold timesteps / repeats across and within ranks
         b = 4 // world
