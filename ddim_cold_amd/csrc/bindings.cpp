@@ -96,7 +96,8 @@ void apply_prod(GemmArgs& g, int64_t rows, int64_t D, const c10::optional<Tensor
 static std::tuple<Tensor, Tensor> patch_embed_impl(Tensor img, Tensor t, Tensor w_pe, Tensor b_pe, Tensor cls,
                                                    Tensor pos, Tensor temb, Tensor rng, int64_t site, double p,
                                                    int64_t patch, c10::optional<Tensor> ln_st,
-                                                   c10::optional<Tensor> xb_out, ColdSrc cs) {
+                                                   c10::optional<Tensor> xb_out, ColdSrc cs,
+                                                   c10::optional<Tensor> patches_in = c10::nullopt) {
   CHECK_IN(img, F32); CHECK_IN(t, I64); CHECK_IN(w_pe, BF16); CHECK_IN(b_pe, F32);
   CHECK_IN(cls, F32); CHECK_IN(pos, F32); CHECK_IN(temb, F32); check_rng(rng);
   const c10::DeviceGuard guard(img.device());
@@ -111,7 +112,15 @@ static std::tuple<Tensor, Tensor> patch_embed_impl(Tensor img, Tensor t, Tensor 
   TORCH_CHECK(temb.dim() == 2 && temb.size(1) == D, "time embedding shape");
   TORCH_CHECK(t.numel() == B, "t must be [B]");
   auto x = at::empty({B, N, D}, img.options());
-  auto patches = at::empty({(int64_t)B * NP, F}, img.options().dtype(BF16));
+  // patches_in: the patch rows are already there (a sampler step's head wrote them);
+  // the GEMM epilogue then writes the cls rows and no patchify launch is needed
+  const bool have_patches = patches_in.has_value() && patches_in->defined();
+  if (have_patches) {
+    CHECK_IN((*patches_in), BF16);
+    TORCH_CHECK(patches_in->numel() == (int64_t)B * NP * F, "patches_in must be [B*P, C*p*p]");
+    TORCH_CHECK(!cs.pool, "patches_in excludes the fused cold batch draw");
+  }
+  auto patches = have_patches ? *patches_in : at::empty({(int64_t)B * NP, F}, img.options().dtype(BF16));
   float* st = nullptr;
   void* xb = nullptr;
   if (ln_st.has_value() && ln_st->defined()) {
@@ -124,9 +133,10 @@ static std::tuple<Tensor, Tensor> patch_embed_impl(Tensor img, Tensor t, Tensor 
     st = ln_st->data_ptr<float>();
     xb = xb_out->data_ptr();
   }
-  patchify_cls_launch(img.data_ptr<float>(), t.data_ptr<int64_t>(), cls.data_ptr<float>(), pos.data_ptr<float>(),
-                      temb.data_ptr<float>(), patches.data_ptr(), x.data_ptr<float>(), B, C, H, W, P, D,
-                      rng.data_ptr<int64_t>(), site, p, st, xb, cur_stream(), cs);
+  if (!have_patches)
+    patchify_cls_launch(img.data_ptr<float>(), t.data_ptr<int64_t>(), cls.data_ptr<float>(), pos.data_ptr<float>(),
+                        temb.data_ptr<float>(), patches.data_ptr(), x.data_ptr<float>(), B, C, H, W, P, D,
+                        rng.data_ptr<int64_t>(), site, p, st, xb, cur_stream(), cs);
   GemmArgs g;
   g.A = patches.data_ptr();
   g.B = w_pe.data_ptr();
@@ -138,14 +148,17 @@ static std::tuple<Tensor, Tensor> patch_embed_impl(Tensor img, Tensor t, Tensor 
   g.pos = pos.data_ptr<float>(); g.temb = temb.data_ptr<float>(); g.tsteps = t.data_ptr<int64_t>(); g.emb_dim = D;
   g.st_out = st;  // slice 0, indexed by token row
   g.xb_out = xb;
+  if (have_patches) g.cls_src = cls.data_ptr<float>();
   gemm_nt(g, EPI_EMBED, cur_stream());
   return {x, patches};
 }
 
 std::tuple<Tensor, Tensor> patch_embed_fwd(Tensor img, Tensor t, Tensor w_pe, Tensor b_pe, Tensor cls, Tensor pos,
                                            Tensor temb, Tensor rng, int64_t site, double p, int64_t patch,
-                                           c10::optional<Tensor> ln_st, c10::optional<Tensor> xb_out) {
-  return patch_embed_impl(img, t, w_pe, b_pe, cls, pos, temb, rng, site, p, patch, ln_st, xb_out, ColdSrc());
+                                           c10::optional<Tensor> ln_st, c10::optional<Tensor> xb_out,
+                                           c10::optional<Tensor> patches_in) {
+  return patch_embed_impl(img, t, w_pe, b_pe, cls, pos, temb, rng, site, p, patch, ln_st, xb_out, ColdSrc(),
+                          patches_in);
 }
 
 // patch_embed_fwd with the cold-diffusion batch draw fused into the patchify launch
@@ -353,7 +366,8 @@ Tensor head_fwd(Tensor a, Tensor w, Tensor b, int64_t B, int64_t C, int64_t H, i
 //                  in place, x0 written to x0_out; coef = device row {sqrt a_t, sqrt 1-a_t, sqrt a_tk, sqrt 1-a_tk}
 //   mode 2 (cold): x <- clamp(head(a), -1, 1)
 void head_step_(Tensor a, Tensor w, Tensor b, Tensor x, c10::optional<Tensor> x0_out, c10::optional<Tensor> coef,
-                int64_t patch, int64_t mode, c10::optional<Tensor> ln_st, c10::optional<Tensor> ln_c, double ln_eps) {
+                int64_t patch, int64_t mode, c10::optional<Tensor> ln_st, c10::optional<Tensor> ln_c, double ln_eps,
+                c10::optional<Tensor> patches_out) {
   CHECK_IN(a, BF16); CHECK_IN(w, BF16); CHECK_IN(b, F32); CHECK_IN(x, F32);
   const c10::DeviceGuard guard(a.device());
   TORCH_CHECK(x.dim() == 4, "x must be [B, C, H, W]");
@@ -373,6 +387,11 @@ void head_step_(Tensor a, Tensor w, Tensor b, Tensor x, c10::optional<Tensor> x0
     CHECK_IN((*x0_out), F32); CHECK_IN((*coef), F32);
     TORCH_CHECK(x0_out->sizes() == x.sizes() && coef->numel() >= 4, "x0_out / coef shapes");
     g.res = x.data_ptr<float>(); g.C2 = x0_out->data_ptr(); g.coef = coef->data_ptr<float>();
+  }
+  if (patches_out.has_value() && patches_out->defined()) {  // the next step's patch rows
+    CHECK_IN((*patches_out), BF16);
+    TORCH_CHECK(patches_out->numel() == (int64_t)B * (N - 1) * C * patch * patch, "patches_out must be [B*P, C*p*p]");
+    g.patch_out = patches_out->data_ptr();
   }
   apply_fold(g, B * N, w.size(0), ln_st, ln_c, ln_eps, c10::nullopt, c10::nullopt);
   gemm_nt(g, EPI_HEAD, cur_stream());
@@ -1086,7 +1105,8 @@ bool qkv_attn_ok(int64_t N, int64_t hd, int64_t D) { return qkv_attn_supported(N
 
 TORCH_LIBRARY(ddim_cold, m) {
   m.def("patch_embed_fwd(Tensor img, Tensor t, Tensor w_pe, Tensor b_pe, Tensor cls, Tensor pos, Tensor temb, "
-        "Tensor rng, int site, float p, int patch, Tensor(a!)? ln_st=None, Tensor(b!)? xb_out=None) -> (Tensor, Tensor)");
+        "Tensor rng, int site, float p, int patch, Tensor(a!)? ln_st=None, Tensor(b!)? xb_out=None, "
+        "Tensor? patches_in=None) -> (Tensor, Tensor)");
   m.def("layernorm_fwd(Tensor x, Tensor gamma, Tensor beta, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("qkv_fwd(Tensor a, Tensor w, Tensor b, int B, int N, int H, Tensor? ln_st=None, Tensor? ln_c=None, "
         "float ln_eps=1e-5, Tensor(a!)? ln_mean=None, Tensor(b!)? ln_rstd=None) -> Tensor");
@@ -1107,7 +1127,7 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("head_fwd(Tensor a, Tensor w, Tensor b, int B, int C, int H, int W, int patch, Tensor? ln_st=None, "
         "Tensor? ln_c=None, float ln_eps=1e-5, Tensor(a!)? ln_mean=None, Tensor(b!)? ln_rstd=None) -> Tensor");
   m.def("head_step_(Tensor a, Tensor w, Tensor b, Tensor(a!) x, Tensor(b!)? x0_out, Tensor? coef, int patch, "
-        "int mode, Tensor? ln_st=None, Tensor? ln_c=None, float ln_eps=1e-5) -> ()");
+        "int mode, Tensor? ln_st=None, Tensor? ln_c=None, float ln_eps=1e-5, Tensor(c!)? patches_out=None) -> ()");
   m.def("head_loss(Tensor a, Tensor w, Tensor b, Tensor target, int patch, float beta, Tensor? ln_st=None, "
         "Tensor? ln_c=None, float ln_eps=1e-5, Tensor(a!)? ln_mean=None, Tensor(b!)? ln_rstd=None) -> (Tensor, Tensor)");
   m.def("smooth_l1_fwd_bwd(Tensor pred, Tensor target, int N, int patch, float beta, Tensor(a!)? loss_last=None, "

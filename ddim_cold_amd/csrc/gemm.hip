@@ -823,6 +823,9 @@ static GemmParams base_params(const GemmArgs& a) {
   p.split_stride = a.split_stride;
   p.ln_st = a.ln_st; p.ln_c = a.ln_c; p.ln_eps = a.ln_eps; p.ln_mean = a.ln_mean; p.ln_rstd = a.ln_rstd;
   p.st_out = a.st_out; p.xb_out = reinterpret_cast<bf16*>(a.xb_out);
+  p.patch_out = reinterpret_cast<bf16*>(a.patch_out);
+  p.cls_src = a.cls_src;
+  if (p.cls_src != nullptr && p.debug == 3) p.debug = 0;  // the scalar epilogue writes no cls rows
   return p;
 }
 

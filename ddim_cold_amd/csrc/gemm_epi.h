@@ -70,6 +70,11 @@ struct GemmParams {
   // producer side
   float* st_out;
   bf16* xb_out;
+  // sampler steps: HEAD modes 1/2 also store the new image in the patch-row layout
+  // (bf16 [B*P][C*p*p], the next step's patch-embedding A operand: no patchify
+  // launch); EMBED with cls_src also writes the cls rows (cls + pos[0] + temb[t])
+  bf16* patch_out;
+  const float* cls_src;
   int debug;  // profiling aid (DDIM_COLD_GEMM_DEBUG): 1 = skip the epilogue, 2 = skip the main loop,
               // 3 = scalar (untransposed) epilogue
 };
@@ -225,10 +230,13 @@ __device__ __forceinline__ float epilogue(const GemmParams& p, long long idx, in
       const float x0 = fminf(fmaxf(v, -1.f), 1.f);
       if (p.head_mode == 2) {
         reinterpret_cast<float*>(p.C)[idx] = x0;
+        return x0;
       } else {
         const float eps = (pre - cf[0] * x0) / cf[1];
-        reinterpret_cast<float*>(p.C)[idx] = cf[2] * x0 + cf[3] * eps;
+        const float xn = cf[2] * x0 + cf[3] * eps;
+        reinterpret_cast<float*>(p.C)[idx] = xn;
         reinterpret_cast<float*>(p.C2)[idx] = x0;
+        return xn;
       }
     }
   } else if (EPI == EPI_EMBED) {
@@ -359,6 +367,12 @@ __device__ __forceinline__ void run_epilogue_scalar(const GemmParams& p, const f
             part[i][r][j / 2] = f2add(part[i][r][j / 2], make_float2(o, o * o));
             p.xb_out[rows[i][r].off + cols[j]] = f2bf(o);
           }
+          if (EPI == EPI_HEAD && p.patch_out != nullptr && (p.head_mode == 1 || p.head_mode == 2)) {
+            // the new image pixel (c, a, b) of patch row (sample, token - 1), conv-im2col order
+            const int m = mb + i * 16 + 4 * g + r, n = nb + j * 16 + li;
+            const int c = n % p.chans, ab = n / p.chans;
+            p.patch_out[(size_t)(m - m / p.tokens - 1) * p.N + c * p.patch * p.patch + ab] = f2bf(o);
+          }
           if (head_loss) {  // gradient of the mean smooth-L1, straight into the token layout
             const int m = mb + i * 16 + 4 * g + r, n = nb + j * 16 + li;
             const float d = (a + colb[j] - pre[i][j][r]) / p.loss_beta;
@@ -486,6 +500,8 @@ struct VecEpi {
   f32x4 lnc[FN];    // fold consumer: c of the lane's 4 columns
   bool first_col;   // lane holds column 0 (writes the row's mean / rstd)
   int colbase;      // first column of the wave's tile
+  int cls_i;        // EMBED with cls_src: fragment row that is a sample's first patch (-1: none)
+  f32x4 clsv[FN];   //   cls + pos[0] + temb[t] of that sample's cls row, the lane's columns
 
   __device__ __forceinline__ void prefetch(const GemmParams& p, int mb, int nb, int g, int li) {
     const int x = li & 3, q = li >> 2;
@@ -518,6 +534,21 @@ struct VecEpi {
     for (int j = 0; j < FN; ++j) {
       const int n = nb + j * 16 + 4 * q;
       lnc[j] = (fold && colok[j]) ? ld4(p.ln_c + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    cls_i = -1;
+    if (EPI == EPI_EMBED && p.cls_src != nullptr) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        if (rowm[i] >= 0 && rowm[i] % p.tokens == 0) cls_i = i;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = nb + j * 16 + 4 * q;
+        clsv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (cls_i >= 0 && colok[j]) {
+          const int b = rowm[cls_i] / p.tokens;
+          clsv[j] = ld4(p.cls_src + n) + ld4(p.pos + n) + ld4(p.temb + (size_t)p.tsteps[b] * p.emb_dim + n);
+        }
+      }
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -645,6 +676,43 @@ struct VecEpi {
             part[i][j / 2] = f2add(part[i][j / 2], stat4(v));
             st4bf_pub<PUB>(p.xb_out + idx, v);
           }
+        }
+      }
+    }
+    if (EPI == EPI_EMBED && p.cls_src != nullptr) {
+      // the cls row of a sample whose first patch row this lane holds (the same
+      // lanes of the row group, so the statistics reduce like the patch rows')
+      const int b = cls_i >= 0 ? rowm[cls_i] / p.tokens : 0;
+      const long long crow = (long long)b * (p.tokens + 1) * p.emb_dim;
+      float2 cpart[SL];
+#pragma unroll
+      for (int sl = 0; sl < SL; ++sl) cpart[sl] = make_float2(0.f, 0.f);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        if (cls_i < 0 || !colok[j]) continue;
+        const long long idx = crow + colbase + j * 16 + 4 * (li >> 2);
+        f32x4 v = clsv[j];
+        if (p.thr_drop) {
+          bool kp[4];
+          dropout_keep4(salt_drop, (uint32_t)idx, p.thr_drop, kp);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) v[c] = kp[c] ? v[c] * p.scale_drop : 0.f;
+        }
+        st4(reinterpret_cast<float*>(p.C) + idx, v);
+        if (prod) {
+          cpart[j / 2] = f2add(cpart[j / 2], stat4(v));
+          st4bf_pub<PUB>(p.xb_out + idx, v);
+        }
+      }
+      if (prod) {
+        const int np_out = p.N / LN_SLOT;
+#pragma unroll
+        for (int sl = 0; sl < SL; ++sl) {
+          float2 t = cpart[sl];
+          t = f2add(t, f2xor<4>(t));
+          t = f2add(t, f2xor<8>(t));
+          if ((li >> 2) == 0 && cls_i >= 0)
+            st2f_pub<PUB>(p.st_out + 2 * ((size_t)b * (p.tokens + 1) * np_out + colbase / LN_SLOT + sl), t);
         }
       }
     }

@@ -63,6 +63,10 @@ struct GemmArgs {
   // zeroing) and a bf16 copy of the output to xb_out
   float* st_out = nullptr;
   void* xb_out = nullptr;
+  // sampler steps (GemmParams::patch_out / cls_src): HEAD modes 1/2 also write the new
+  // image as bf16 patch rows; EMBED writes the cls rows itself (no patchify launch)
+  void* patch_out = nullptr;
+  const float* cls_src = nullptr;
 };
 
 void gemm_nt(const GemmArgs& a, int epi, hipStream_t stream);

@@ -62,11 +62,15 @@ class _Denoiser:
             return ("engine", id(eng))
         return tuple((p.data_ptr(), p._version) for p in self.model.parameters())
 
-    def step_(self, x, t, mode: int, x0_out=None, coef=None):
+    def step_(self, x, t, mode: int, x0_out=None, coef=None, patches=None):
         """In-place sampler step on ``x`` with the update fused into the head GEMM
-        (mode 1: DDIM with ``coef``, x0-hat into ``x0_out``; mode 2: clamp)."""
+        (mode 1: DDIM with ``coef``, x0-hat into ``x0_out``; mode 2: clamp).
+        ``patches = (patches_in, patches_out)``: bf16 patch rows of ``x`` handed from
+        one step's head epilogue to the next step's patch embedding (no patchify
+        launch per step; ``patches_in`` None on the first step)."""
         if self.fused and FUSED_HEAD:
-            self.prog.forward(self.P, x, t, self.rng, False, save=False, head_step=(mode, x0_out, coef))
+            hs = (mode, x0_out, coef) if patches is None else (mode, x0_out, coef) + tuple(patches)
+            self.prog.forward(self.P, x, t, self.rng, False, save=False, head_step=hs)
             return
         x0_raw = self(x, t)
         if mode == 2:
@@ -87,6 +91,25 @@ class _Denoiser:
 
 
 FUSED_HEAD = os.environ.get("DDIM_COLD_SAMPLER_FUSED_HEAD", "1") == "1"
+# the head epilogue of each step also writes the new x_t as the next step's bf16
+# patch rows, so every step after the first skips the patchify launch
+PATCH_CHAIN = os.environ.get("DDIM_COLD_SAMPLER_PATCH_CHAIN", "1") == "1"
+
+
+def _patch_rows(model, N: int, device, den) -> Optional[torch.Tensor]:
+    """bf16 [N*P, C*p*p] hand-off buffer for the patch-row chain (None: not used)."""
+    if not (PATCH_CHAIN and FUSED_HEAD and den.fused):
+        return None
+    p = model.patch_size
+    H, W = model.img_size
+    return torch.empty(N * (H // p) * (W // p), model.in_chans * p * p, dtype=torch.bfloat16, device=device)
+
+
+def _chain_patches(pbuf, sl, NP: int, first: bool):
+    if pbuf is None:
+        return None
+    rows = pbuf[(sl.start or 0) * NP:(sl.stop if sl.stop is not None else pbuf.shape[0] // NP) * NP]
+    return (None if first else rows, rows)
 
 
 def default_streams(N: int, device) -> int:
@@ -180,11 +203,14 @@ class DDIMSampler:
         traj = torch.zeros(len(self.ts), N, self.C, self.H, self.W, device=dev) if record else None
         coef = self.coef
         chains = _Chains(N, dev, nstreams)
+        pbuf = _patch_rows(self.model, N, dev, den)
+        NP = (self.H // self.model.patch_size) * (self.W // self.model.patch_size)
 
         def chain(sl):
             xs, x0s = x[sl], x0[sl]
             for i in range(len(self.ts)):
-                den.step_(xs, tt[i][sl], 1, x0s, coef[i])  # forward + clamp + DDIM update, one head epilogue
+                # forward + clamp + DDIM update, one head epilogue
+                den.step_(xs, tt[i][sl], 1, x0s, coef[i], patches=_chain_patches(pbuf, sl, NP, i == 0))
                 if traj is not None:
                     traj[i][sl].copy_(x0s)
 
@@ -246,11 +272,14 @@ class ColdSampler:
         tt = torch.tensor(ts, dtype=torch.int64, device=dev).unsqueeze(1).expand(-1, N).contiguous()
         traj = torch.zeros(len(ts), N, self.C, self.H, self.W, device=dev)
         chains = _Chains(N, dev, nstreams)
+        pbuf = _patch_rows(self.model, N, dev, den)
+        NP = (self.H // self.model.patch_size) * (self.W // self.model.patch_size)
 
         def chain(sl):
             xs = x[sl]
             for i in range(len(ts)):
-                den.step_(xs, tt[i][sl], 2)  # forward + clamp in the head epilogue
+                # forward + clamp in the head epilogue
+                den.step_(xs, tt[i][sl], 2, patches=_chain_patches(pbuf, sl, NP, i == 0))
                 traj[i][sl].copy_(xs)
 
         st = {"key": den.key(), "x": x, "traj": traj, "loop": _GraphLoop(lambda: chains.run(chain), dev)}

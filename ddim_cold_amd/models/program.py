@@ -353,7 +353,7 @@ class ViTProgram:
             l1, m1, r1 = ln_n, m_n, r_n
         lf, mf, rf = l1, m1, r1
         if head_step is not None:
-            mode, x0_out, coef = head_step
+            mode, x0_out, coef = head_step[:3]  # (patch-row hand-off: folded forward only)
             ops.head_step_(lf, P.head_w, P.head_b, img, x0_out, coef, c.patch, mode)
             return img, S
         out = ops.head_fwd(lf, P.head_w, P.head_b, B, c.chans, c.img_h, c.img_w, c.patch)
@@ -381,12 +381,15 @@ class ViTProgram:
         # each slot written once by the producing epilogue
         st = torch.empty(2 * L + 1, M, D // 32, 2, dtype=torch.float32, device=dev)
         xb = torch.empty(M, D, dtype=ACT_DTYPE, device=dev)
+        # sampler steps: head_step = (mode, x0_out, coef, patches_in, patches_out); the
+        # previous step's head left this step's bf16 patch rows in patches_in
+        patches_in = head_step[3] if head_step is not None and len(head_step) > 3 else None
         if cold is not None:
             x, patches = ops.patch_embed_cold_fwd(cold, img, t, P.pe_w, P.pe_b, P.cls, P.pos, P.temb, rng,
                                                   SITE_EMBED, pd, c.patch, ln_st=st[0], xb_out=xb)
         else:
             x, patches = ops.patch_embed_fwd(img, t, P.pe_w, P.pe_b, P.cls, P.pos, P.temb, rng, SITE_EMBED, pd,
-                                             c.patch, ln_st=st[0], xb_out=xb)
+                                             c.patch, ln_st=st[0], xb_out=xb, patches_in=patches_in)
         x = x.view(M, D)
         S = Saved(t=t, patches=patches) if save else None
 
@@ -427,8 +430,9 @@ class ViTProgram:
             if save:
                 S.blocks.append((x0, None, m1, r1, qkv, o, lse, x1, None, m2, r2, u, h))
         if head_step is not None:
-            mode, x0_out, coef = head_step
-            ops.head_step_(xb, P.head_wf, P.head_bf, img, x0_out, coef, c.patch, mode,
+            mode, x0_out, coef = head_step[:3]
+            patches_out = head_step[4] if len(head_step) > 4 else None
+            ops.head_step_(xb, P.head_wf, P.head_bf, img, x0_out, coef, c.patch, mode, patches_out=patches_out,
                            fold=(st[2 * L], P.head_c, c.eps))
             return img, S
         mf, rf = stats()

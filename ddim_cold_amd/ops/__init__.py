@@ -39,12 +39,15 @@ def _ops():
 
 # ----------------------------------------------------------------------------- forward
 def patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site: int, p: float, patch: int, ln_st=None,
-                    xb_out=None):
+                    xb_out=None, patches_in=None):
     """Tokens + bf16 patches.  LayerNorm fold: ``ln_st`` ([B*N, D/32, 2]) gets the
     tokens' row statistics ({sum, sum^2} per 32-column slot); ``xb_out`` their
-    bf16 copy (the A operand of the first QKV GEMM)."""
+    bf16 copy (the A operand of the first QKV GEMM).  ``patches_in``: the bf16
+    patch rows of ``img`` already exist (a sampler step's :func:`head_step_` wrote
+    them) -- on a GPU the patchify launch is skipped (the GEMM writes the cls rows)."""
     if _hip(img):
-        return _ops().patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site, float(p), patch, ln_st, xb_out)
+        return _ops().patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site, float(p), patch, ln_st, xb_out,
+                                      patches_in)
     return ref.patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site, p, patch, ln_st, xb_out)
 
 
@@ -170,13 +173,15 @@ def linear_gelu_fwd(a, w, b, rng, site: int, p: float, fold=None):
     return ref.linear_gelu_fwd(a, w, b, rng, site, p, st, c, eps, mean, rstd)
 
 
-def head_step_(a, w, b, x, x0_out, coef, patch: int, mode: int, fold=None):
+def head_step_(a, w, b, x, x0_out, coef, patch: int, mode: int, fold=None, patches_out=None):
     """Head GEMM + sampler step in its epilogue (in place on ``x``): mode 1 = clamp +
     DDIM update (``x0_out`` gets the clamped x0-hat; ``coef`` a device row of
-    ``ddim_coefficients``), mode 2 = clamp only (cold sampler)."""
+    ``ddim_coefficients``), mode 2 = clamp only (cold sampler).  ``patches_out``
+    (GPU): also the new ``x`` as bf16 patch rows, for the next step's
+    :func:`patch_embed_fwd` (``patches_in``)."""
     st, c, eps, _, _ = _fold_args(fold)
     if _hip(a):
-        return _ops().head_step_(a, w, b, x, x0_out, coef, patch, mode, st, c, eps)
+        return _ops().head_step_(a, w, b, x, x0_out, coef, patch, mode, st, c, eps, patches_out)
     B, C, H, W = x.shape
     x0_raw = ref.head_fwd(a, w, b, B, C, H, W, patch, st, c, eps)
     if mode == 2:

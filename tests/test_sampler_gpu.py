@@ -62,3 +62,42 @@ def test_img2img_gpu_batched(model):
     out = img2img(model, draft, [1199, 1599, 1999], k=400, device=DEV, generator=torch.Generator().manual_seed(3))
     assert out.shape == (3, 3, 64, 64) and torch.isfinite(out).all()
     assert out.min() >= 0 and out.max() <= 1
+
+
+@pytest.mark.gpu
+def test_patch_row_chain(model, monkeypatch):
+    """Head epilogue -> next step's patch rows: the patch embedding without its patchify
+    launch (cls rows from the GEMM epilogue) gives the same tokens, and the sampler
+    with the chain matches the sampler without it."""
+    from ddim_cold_amd import ops
+    from ddim_cold_amd.diffusion import samplers as smp
+    from ddim_cold_amd.models.program import model_tensors
+    P = model_tensors(model)
+    B, D = 6, model.embed_dim
+    img = torch.randn(B, 3, 64, 64, device=DEV)
+    t = torch.randint(0, 2000, (B,), device=DEV)
+    r = torch.zeros(2, dtype=torch.int64, device=DEV)
+    N = 65
+    outs = []
+    for chained in (False, True):
+        st = torch.full((B * N, D // 32, 2), float("nan"), device=DEV)
+        xb = torch.empty(B * N, D, dtype=torch.bfloat16, device=DEV)
+        pin = None
+        if chained:  # the bf16 patch rows a head epilogue would have written
+            _, pin = ops.patch_embed_fwd(img, t, P.pe_w, P.pe_b, P.cls, P.pos, P.temb, r, 0, 0.0, 8)
+        x, _ = ops.patch_embed_fwd(img, t, P.pe_w, P.pe_b, P.cls, P.pos, P.temb, r, 0, 0.0, 8, ln_st=st, xb_out=xb,
+                                   patches_in=pin)
+        outs.append((x.clone(), xb.clone(), st.sum(1)))
+    (x1, xb1, s1), (x2, xb2, s2) = outs
+    assert torch.equal(x1, x2) and torch.equal(xb1, xb2)
+    assert torch.allclose(s1, s2, rtol=1e-5, atol=1e-4)  # per-slot partials vs one sum in slot 0
+    noise = torch.randn(8, 3, 64, 64, generator=torch.Generator().manual_seed(4))
+    res = []
+    for on in (False, True):
+        monkeypatch.setattr(smp, "PATCH_CHAIN", on)
+        model.__dict__.pop("_sampler_graphs", None)
+        res.append(DDIMSampler(model, DEV, k=200).sample(8, noise=noise))
+        res.append(ColdSampler(model, DEV).sequence(4, generator=torch.Generator().manual_seed(5))[-1])
+    model.__dict__.pop("_sampler_graphs", None)
+    assert (res[0] - res[2]).abs().max() < 1e-3
+    assert (res[1] - res[3]).abs().max() < 1e-3
