@@ -501,6 +501,8 @@ struct VecEpi {
   bool first_col;   // lane holds column 0 (writes the row's mean / rstd)
   int colbase;      // first column of the wave's tile
   int cls_i;        // EMBED with cls_src: fragment row that is a sample's first patch (-1: none)
+  int cls_b;        //   and its sample (kept as a scalar: indexing rowm[cls_i] would put the
+                    //   epilogue's arrays in scratch memory)
   f32x4 clsv[FN];   //   cls + pos[0] + temb[t] of that sample's cls row, the lane's columns
 
   __device__ __forceinline__ void prefetch(const GemmParams& p, int mb, int nb, int g, int li) {
@@ -536,18 +538,20 @@ struct VecEpi {
       lnc[j] = (fold && colok[j]) ? ld4(p.ln_c + n) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
     cls_i = -1;
+    cls_b = 0;
     if (EPI == EPI_EMBED && p.cls_src != nullptr) {
 #pragma unroll
       for (int i = 0; i < FM; ++i)
-        if (rowm[i] >= 0 && rowm[i] % p.tokens == 0) cls_i = i;
+        if (rowm[i] >= 0 && rowm[i] % p.tokens == 0) {
+          cls_i = i;
+          cls_b = rowm[i] / p.tokens;
+        }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int n = nb + j * 16 + 4 * q;
         clsv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (cls_i >= 0 && colok[j]) {
-          const int b = rowm[cls_i] / p.tokens;
-          clsv[j] = ld4(p.cls_src + n) + ld4(p.pos + n) + ld4(p.temb + (size_t)p.tsteps[b] * p.emb_dim + n);
-        }
+        if (cls_i >= 0 && colok[j])
+          clsv[j] = ld4(p.cls_src + n) + ld4(p.pos + n) + ld4(p.temb + (size_t)p.tsteps[cls_b] * p.emb_dim + n);
       }
     }
 #pragma unroll
@@ -682,7 +686,7 @@ struct VecEpi {
     if (EPI == EPI_EMBED && p.cls_src != nullptr) {
       // the cls row of a sample whose first patch row this lane holds (the same
       // lanes of the row group, so the statistics reduce like the patch rows')
-      const int b = cls_i >= 0 ? rowm[cls_i] / p.tokens : 0;
+      const int b = cls_b;
       const long long crow = (long long)b * (p.tokens + 1) * p.emb_dim;
       float2 cpart[SL];
 #pragma unroll
