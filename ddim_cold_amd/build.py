@@ -18,6 +18,7 @@ import argparse
 import concurrent.futures as cf
 import hashlib
 import os
+import re
 import subprocess
 import sys
 import sysconfig
@@ -48,8 +49,9 @@ def _flags(inc, abi, resource_usage=False):
         "-Wno-unused-result", "-Wno-deprecated-declarations", "-Wno-unused-command-line-argument",
         "-fno-gpu-rdc", "-munsafe-fp-atomics",
     ]
-    if resource_usage:
-        f.append("-Rpass-analysis=kernel-resource-usage")
+    # per-kernel resource remarks (codegen unchanged): the build checks them for
+    # scratch memory, see _check_scratch
+    f.append("-Rpass-analysis=kernel-resource-usage")
     for d in inc + [py_inc, CSRC, "/opt/rocm/include"]:
         f += ["-I", d]
     return f
@@ -71,14 +73,37 @@ def _compile(src, flags, force):
     name = os.path.splitext(os.path.basename(src))[0]
     key = _hash(src, flags)
     obj = os.path.join(BUILD, f"{name}.{key}.o")
-    if os.path.isfile(obj) and not force:
-        return obj, None
+    if os.path.isfile(obj) and os.path.isfile(obj + ".log") and not force:
+        with open(obj + ".log") as fh:
+            return obj, fh.read()
     cmd = [HIPCC] + flags + ["-c", src, "-o", obj + ".tmp"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-8000:]}")
+    with open(obj + ".log", "w") as fh:
+        fh.write(r.stderr)
     os.replace(obj + ".tmp", obj)
     return obj, r.stderr
+
+
+def _check_scratch(logs):
+    """Fail the build if a GPU kernel uses scratch (private) memory: on gfx950 that
+    is a global-memory round trip per access -- a dynamically indexed register
+    array once put the patch-embedding epilogue there and cost ~4 us per launch.
+    DDIM_COLD_ALLOW_SCRATCH=1 downgrades this to a warning."""
+    bad = []
+    for log in logs:
+        for blk in (log or "").split("Function Name: ")[1:]:
+            m = re.search(r"ScratchSize \[bytes/lane\]: (\d+)", blk)
+            if m and int(m.group(1)) > 0:
+                bad.append(f"{blk.split()[0]} ({m.group(1)} B/lane)")
+    if not bad:
+        return
+    msg = "GPU kernels using scratch memory:\n  " + "\n  ".join(bad)
+    if os.environ.get("DDIM_COLD_ALLOW_SCRATCH") == "1":
+        print("[ddim_cold_amd.build] warning: " + msg)
+    else:
+        raise RuntimeError(msg)
 
 
 def sources():
@@ -91,14 +116,16 @@ def build(force: bool = False, jobs: int | None = None, resource_usage: bool = F
     flags = _flags(inc, abi, resource_usage)
     srcs = sources()
     jobs = jobs or min(len(srcs), max(1, min(8, (os.cpu_count() or 4))))
-    objs = []
+    objs, logs = [], []
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        futs = {ex.submit(_compile, s, flags, force or resource_usage): s for s in srcs}
+        futs = {ex.submit(_compile, s, flags, force): s for s in srcs}
         for fut in cf.as_completed(futs):
             obj, log = fut.result()
             objs.append(obj)
+            logs.append(log)
             if verbose and log and resource_usage:
                 print(log)
+    _check_scratch(logs)
     objs.sort()
     newest = max(os.path.getmtime(o) for o in objs)
     if force or not os.path.isfile(OUT) or os.path.getmtime(OUT) < newest or _stale_link(objs):
