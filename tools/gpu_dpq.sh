@@ -13,4 +13,6 @@ for rep in 1 2; do
   DPARGS="--force-dist" run dp-queues1 DEBUG_HIP_FORCE_GRAPH_QUEUES=1
   DPARGS="--force-dist" run dp-queues2 DEBUG_HIP_FORCE_GRAPH_QUEUES=2
   DPARGS="--force-dist --graph-steps 1" run dp-K1 X=1
+  DPARGS="--force-dist --bucket-blocks 4" run dp-bb4 X=1
+  DPARGS="--force-dist --bucket-blocks 7" run dp-bb7 X=1
 done
