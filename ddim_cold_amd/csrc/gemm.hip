@@ -761,7 +761,7 @@ struct WgradMulti {
   int tile_start[WM_MAX + 1];
   int n;
 };
-template <int T, int S>
+template <int T, int S, int TN = T>
 __global__ __launch_bounds__(256) void gemm_wgrad_multi_kernel(WgradMulti gm) {
   const int bid = xcd_remap(blockIdx.x, gm.tile_start[gm.n]);
   int lo = 0, hi = gm.n - 1;  // problem owning tile `bid`: binary search over tile_start
@@ -775,14 +775,16 @@ __global__ __launch_bounds__(256) void gemm_wgrad_multi_kernel(WgradMulti gm) {
   p.A = d.A; p.B = d.B; p.C = d.C; p.bias = d.bias;
   p.M = d.M; p.N = d.N; p.K = d.K; p.lda = d.lda; p.ldb = d.ldb; p.ldc = d.ldc;
   p.ktiles_per_split = (d.K + BK - 1) / BK;
-  const int tiles_n = (d.N + T - 1) / T;
+  const int tiles_n = (d.N + TN - 1) / TN;
   const int local = bid - gm.tile_start[lo];
   const int tm = local / tiles_n;
-  gemm_dma_body<T, T, 2, 2, true, true, EPI_ACC, S>(p, tm, local - tm * tiles_n, 0);
+  gemm_dma_body<T, TN, 2, 2, true, true, EPI_ACC, S>(p, tm, local - tm * tiles_n, 0);
 }
 template __global__ void gemm_wgrad_multi_kernel<64, 3>(WgradMulti);
 template __global__ void gemm_wgrad_multi_kernel<64, 4>(WgradMulti);
 template __global__ void gemm_wgrad_multi_kernel<128, 3>(WgradMulti);
+template __global__ void gemm_wgrad_multi_kernel<128, 3, 64>(WgradMulti);
+template __global__ void gemm_wgrad_multi_kernel<128, 2, 64>(WgradMulti);
 template __global__ void gemm_wgrad_group_kernel<EPI_ATOMIC, 6>(WgradGroup);
 template __global__ void gemm_wgrad_group_kernel<EPI_ACC, 6>(WgradGroup);
 template __global__ void gemm_wgrad_group_kernel<EPI_ATOMIC, 8>(WgradGroup);
@@ -975,10 +977,16 @@ void gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream) {
   // tile: 64 x 64 (three 48 KiB workgroups per CU).  128 x 128 (DDIM_COLD_WGRAD_MULTI_TILE=128:
   // half the operand bytes per output, one 96 KiB workgroup per CU, ~390 workgroups
   // in 1.5 rounds) measured 14 us/step slower (0.838 vs 0.824 ms/step, interleaved A/B)
-  static const int T = [] {
+  // DDIM_COLD_WGRAD_MULTI_TILE=12864 / 128642: 128 x 64 tiles (3 / 2 ring stages): 24 % fewer
+  // operand bytes, yet the step's launch takes the same time (60.8 / 60.1 vs 61.3 us,
+  // tools/gpu_wgm.sh: two workgroups per CU stream no faster than three) and a 1-block
+  // launch is slower (25 vs 17 us) -- opt-in
+  static const int cfg = [] {
     const char* e = getenv("DDIM_COLD_WGRAD_MULTI_TILE");
-    return (e && atoi(e) == 128) ? 128 : 64;
+    return e ? atoi(e) : 64;
   }();
+  const int T = cfg == 128 || cfg == 12864 || cfg == 128642 ? 128 : 64;
+  const int TNc = cfg == 128 ? 128 : 64;
   for (int i = 0; i < n; ++i) {
     const GemmArgs& a = probs[i];
     if (a.N % 4 != 0) throw std::runtime_error("gemm_wgrad_multi: output width must be a multiple of 4");
@@ -987,9 +995,21 @@ void gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream) {
     d.C = reinterpret_cast<float*>(a.C); d.bias = const_cast<float*>(a.bias);
     d.M = a.M; d.N = a.N; d.K = a.K; d.lda = a.lda; d.ldb = a.ldb; d.ldc = a.ldc;
     gm.tile_start[i] = tiles;
-    tiles += ((a.M + T - 1) / T) * ((a.N + T - 1) / T);
+    tiles += ((a.M + T - 1) / T) * ((a.N + TNc - 1) / TNc);
   }
   for (int i = n; i <= WM_MAX; ++i) gm.tile_start[i] = tiles;
+  if (T == 128 && TNc == 64) {
+    const int st = cfg == 128642 ? 2 : 3;
+    const int lds = st * (128 * 128 + 64 * 128);
+    static const bool attr3 = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_wgrad_multi_kernel<128, 3, 64>),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 3 * (128 * 128 + 64 * 128)) == hipSuccess;
+    (void)attr3;
+    if (st == 2)
+      hipLaunchKernelGGL((gemm_wgrad_multi_kernel<128, 2, 64>), dim3(tiles), dim3(256), lds, stream, gm);
+    else
+      hipLaunchKernelGGL((gemm_wgrad_multi_kernel<128, 3, 64>), dim3(tiles), dim3(256), lds, stream, gm);
+    return;
+  }
   if (T == 128) {
     constexpr int lds = 3 * (128 * 128 + 128 * 128);
     static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_wgrad_multi_kernel<128, 3>),
