@@ -607,11 +607,11 @@ void linear_wgrad_group(std::vector<Tensor> dys, std::vector<Tensor> xs, std::ve
 
 // Every weight gradient of a training step in ONE launch (gemm_wgrad_multi_kernel)
 void linear_wgrad_multi(std::vector<Tensor> dys, std::vector<Tensor> xs, std::vector<Tensor> dws,
-                        std::vector<c10::optional<Tensor>> dbs) {
+                        std::vector<c10::optional<Tensor>> dbs, bool store) {
   TORCH_CHECK(!dys.empty() && dys.size() <= 32, "wgrad_multi: 1..32 problems");
   const c10::DeviceGuard guard(dys[0].device());
   std::vector<GemmArgs> probs = wgrad_probs(dys, xs, dws, dbs, nullptr, nullptr);
-  gemm_wgrad_multi(probs.data(), (int)probs.size(), cur_stream());
+  gemm_wgrad_multi(probs.data(), (int)probs.size(), cur_stream(), store);
 }
 
 // Token split of weight-gradient riders: enough slices that the riders' tiles
@@ -862,7 +862,7 @@ Tensor attn_bwd_proj(Tensor gy, Tensor wp, Tensor qkv, Tensor o, Tensor lse, dou
 }
 
 Tensor embed_bwd(Tensor g, Tensor t, Tensor rng, int64_t site, double p, Tensor dcls, Tensor dpos, Tensor dtemb,
-                 c10::optional<Tensor> ln_ws, c10::optional<Tensor> ln_ptrs, int64_t ln_C) {
+                 c10::optional<Tensor> ln_ws, c10::optional<Tensor> ln_ptrs, int64_t ln_C, bool ln_store) {
   CHECK_IN(g, F32); CHECK_IN(t, I64); check_rng(rng); CHECK_IN(dcls, F32); CHECK_IN(dpos, F32); CHECK_IN(dtemb, F32);
   const c10::DeviceGuard guard(g.device());
   TORCH_CHECK(g.dim() == 3, "g must be [B,N,D]");
@@ -881,6 +881,7 @@ Tensor embed_bwd(Tensor g, Tensor t, Tensor rng, int64_t site, double p, Tensor 
     TORCH_CHECK(ln_C > 0 && ln_ws->numel() == (int64_t)rf.G * rf.R * ln_C, "replica ws shape");
     rf.ws = ln_ws->data_ptr<float>();
     rf.dsts = reinterpret_cast<float* const*>(ln_ptrs->data_ptr<int64_t>());
+    rf.store = ln_store ? 1 : 0;
   }
   embed_bwd_launch(g.data_ptr<float>(), t.data_ptr<int64_t>(), dcls.data_ptr<float>(), dpos.data_ptr<float>(),
                    dtemb.data_ptr<float>(), gpatch.data_ptr(), B, N, D, rng.data_ptr<int64_t>(), site, p,
@@ -896,7 +897,7 @@ void sqnorm(Tensor g, Tensor out, double scale) {
 }
 
 void adamw_step(Tensor p, Tensor g, Tensor m, Tensor v, c10::optional<Tensor> pbf, Tensor sq, Tensor step,
-                Tensor hyper, double grad_scale) {
+                Tensor hyper, double grad_scale, int64_t zero_hi) {
   CHECK_IN(p, F32); CHECK_IN(g, F32); CHECK_IN(m, F32); CHECK_IN(v, F32); CHECK_IN(sq, F32); CHECK_IN(step, I64);
   CHECK_IN(hyper, F32);
   const c10::DeviceGuard guard(p.device());
@@ -912,7 +913,7 @@ void adamw_step(Tensor p, Tensor g, Tensor m, Tensor v, c10::optional<Tensor> pb
   }
   adamw_launch(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), pb, n,
                sq.data_ptr<float>(), step.data_ptr<int64_t>(), hyper.data_ptr<float>(), (float)grad_scale,
-               cur_stream());
+               cur_stream(), zero_hi);
 }
 
 void advance_counters(Tensor step, Tensor rng, c10::optional<Tensor> sq) {
@@ -1145,7 +1146,7 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("vit_group_ok(int D, int H, int hd, int N, int L) -> bool", &vit_group_ok);
   m.def("vit_group_fwd(Tensor?[] ts, int L, int B, int N, int[] sites, float[] p_dp, Tensor rng, float p_drop, "
         "float p_attn, float scale, float eps, Tensor(a!) ctr, Tensor(b!) err, Tensor(c!)? stamps=None) -> ()");
-  m.def("linear_wgrad_multi(Tensor[] dys, Tensor[] xs, Tensor(a!)[] dws, Tensor(b!)?[] dbs) -> ()");
+  m.def("linear_wgrad_multi(Tensor[] dys, Tensor[] xs, Tensor(a!)[] dws, Tensor(b!)?[] dbs, bool store=False) -> ()");
   m.def("linear_dgrad_ride(Tensor dy, Tensor w, int mode, bool out_fp32, int splits, Tensor? u, Tensor? rng, "
         "int site, float p, Tensor[] dys, Tensor[] xs, Tensor(a!)[] dws, Tensor(b!)?[] dbs) -> Tensor");
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor? g_res, "
@@ -1158,10 +1159,10 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("attn_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, float scale, Tensor rng, int site, float p, "
         "Tensor? keep=None) -> Tensor");
   m.def("embed_bwd(Tensor g, Tensor t, Tensor rng, int site, float p, Tensor(a!) dcls, Tensor(b!) dpos, "
-        "Tensor(c!) dtemb, Tensor(d!)? ln_ws=None, Tensor? ln_ptrs=None, int ln_C=0) -> Tensor");
+        "Tensor(c!) dtemb, Tensor(d!)? ln_ws=None, Tensor? ln_ptrs=None, int ln_C=0, bool ln_store=False) -> Tensor");
   m.def("sqnorm(Tensor g, Tensor(a!) out, float scale) -> ()");
   m.def("adamw_step(Tensor(a!) p, Tensor(b!) g, Tensor(c!) m, Tensor(d!) v, Tensor(e!)? pbf, Tensor sq, "
-        "Tensor step, Tensor hyper, float grad_scale) -> ()");
+        "Tensor step, Tensor hyper, float grad_scale, int zero_hi=-1) -> ()");
   m.def("advance_counters(Tensor(a!) step, Tensor(b!) rng, Tensor? sq) -> ()");
   m.def("ddim_step(Tensor x_t, Tensor x0_raw, Tensor coef) -> (Tensor, Tensor)");
   m.def("ddim_step_(Tensor(a!) x, Tensor x0_raw, Tensor(b!) x0_out, Tensor coef) -> ()");

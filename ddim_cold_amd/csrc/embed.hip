@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const float* __restrict_
       s += w[(size_t)r * rf.C];
       w[(size_t)r * rf.C] = 0.f;
     }
-    rf.dsts[gi][c] += s;
+    rf.dsts[gi][c] = rf.store ? s : rf.dsts[gi][c] + s;
   } else {
     const size_t total = (size_t)B * (N - 1) * D;
     for (size_t e = (size_t)(bid - blocksA - blocksB) * 256 + threadIdx.x; e < total;

@@ -373,7 +373,7 @@ __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int t
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm * TM + i * 16 + 4 * g + r;
-        old[i][r] = (EPI == EPI_ACC && m < p.M) ? db[m] : 0.f;
+        old[i][r] = (EPI == EPI_ACC && m < p.M && !p.acc_store) ? db[m] : 0.f;
       }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -760,6 +760,7 @@ struct WgradMulti {
   WgDesc d[WM_MAX];
   int tile_start[WM_MAX + 1];
   int n;
+  int store;  // every target is zero: plain stores (no read-add)
 };
 template <int T, int S, int TN = T>
 __global__ __launch_bounds__(256) void gemm_wgrad_multi_kernel(WgradMulti gm) {
@@ -774,6 +775,7 @@ __global__ __launch_bounds__(256) void gemm_wgrad_multi_kernel(WgradMulti gm) {
   GemmParams p{};
   p.A = d.A; p.B = d.B; p.C = d.C; p.bias = d.bias;
   p.M = d.M; p.N = d.N; p.K = d.K; p.lda = d.lda; p.ldb = d.ldb; p.ldc = d.ldc;
+  p.acc_store = gm.store;
   p.ktiles_per_split = (d.K + BK - 1) / BK;
   const int tiles_n = (d.N + TN - 1) / TN;
   const int local = bid - gm.tile_start[lo];
@@ -969,10 +971,11 @@ void gemm_dgrad_ride(const GemmArgs& a, int epi, const GemmArgs* probs, int n, i
   }
 }
 
-void gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream) {
+void gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool store) {
   if (n < 1 || n > WM_MAX) throw std::runtime_error("gemm_wgrad_multi: 1..32 problems per launch");
   WgradMulti gm{};
   gm.n = n;
+  gm.store = store ? 1 : 0;
   int tiles = 0;
   // tile: 64 x 64 (three 48 KiB workgroups per CU).  128 x 128 (DDIM_COLD_WGRAD_MULTI_TILE=128:
   // half the operand bytes per output, one 96 KiB workgroup per CU, ~390 workgroups

@@ -75,6 +75,7 @@ struct GemmParams {
   // launch); EMBED with cls_src also writes the cls rows (cls + pos[0] + temb[t])
   bf16* patch_out;
   const float* cls_src;
+  int acc_store;  // EPI_ACC: the target is known to be zero -- store, don't read-add
   int debug;  // profiling aid (DDIM_COLD_GEMM_DEBUG): 1 = skip the epilogue, 2 = skip the main loop,
               // 3 = scalar (untransposed) epilogue
 };
@@ -307,7 +308,7 @@ __device__ __forceinline__ void run_epilogue_scalar(const GemmParams& p, const f
         if (ELEM && rows[i][r].off >= 0 && colok[j]) {
           const int n = nb + j * 16 + li;
           if (EPI == EPI_RESID) v = p.res[rows[i][r].off + n];
-          if (EPI == EPI_ACC) v = reinterpret_cast<const float*>(p.C)[rows[i][r].off + n];
+          if (EPI == EPI_ACC && !p.acc_store) v = reinterpret_cast<const float*>(p.C)[rows[i][r].off + n];
           if (EPI == EPI_DGELU) v = bf2f(p.aux[rows[i][r].off + n]);
           if (EPI == EPI_EMBED) {
             const int m = mb + i * 16 + 4 * g + r;
@@ -563,7 +564,7 @@ struct VecEpi {
           const int n = nb + j * 16 + 4 * q;
           if (EPI == EPI_RESID) v = ld4(p.res + rows[i].off + n);
           if (EPI == EPI_DGELU) v = ld4bf(p.aux + rows[i].off + n);
-          if (EPI == EPI_ACC) v = ld4(reinterpret_cast<const float*>(p.C) + rows[i].off + n);
+          if (EPI == EPI_ACC && !p.acc_store) v = ld4(reinterpret_cast<const float*>(p.C) + rows[i].off + n);
           if (EPI == EPI_EMBED) {
             const int m = mb + i * 16 + 4 * g + x;
             const int patch = m - rows[i].b * p.tokens;

@@ -82,7 +82,8 @@ void gemm_wgrad_group(const GemmArgs* probs, int n, int splits, hipStream_t stre
 // as extra workgroups of the same launch
 void gemm_dgrad_ride(const GemmArgs& a, int epi, const GemmArgs* probs, int n, int wsplits, hipStream_t stream);
 // every weight gradient of a step (n <= 32 problems) in one launch, unsplit (plain read-add-write)
-void gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream);
+// store: every target is zero on entry (plain stores instead of read-add-write)
+void gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool store = false);
 
 // Row-panel GEMM + residual + LayerNorm epilogue (gemm_ln.hip)
 struct GemmLnArgs {
@@ -185,8 +186,9 @@ void patchify_cls_launch(const float* img, const int64_t* t, const float* cls, c
 // optional LayerNorm replica finalize carried by the embedding-backward launch
 struct ReplicaFinal {
   float* ws = nullptr;          // [G][R][C] replicas (re-zeroed)
-  float* const* dsts = nullptr; // [G] device pointers to the [C] grad ranges (+=)
+  float* const* dsts = nullptr; // [G] device pointers to the [C] grad ranges (+=, or = with store)
   int G = 0, R = 0, C = 0;
+  int store = 0;
 };
 void embed_bwd_launch(const float* g, const int64_t* t, float* dcls, float* dpos, float* dtemb, void* gpatch,
                       int B, int N, int D, const int64_t* rng, int site, double p, hipStream_t stream, ReplicaFinal rf = ReplicaFinal());
@@ -204,8 +206,11 @@ void img_to_tokgrad_launch(const float* dimg, void* dtok, int B, int C, int H, i
 // adamw / advance sum the partials themselves.
 constexpr int SQ_PARTS = 1024;
 void sqnorm_launch(const float* g, int64_t n, float* partials, float scale, hipStream_t stream);
+// zero_hi: zero the gradient arena only below this element (the part that is
+// accumulated into; everything above is overwritten by its producer next step)
 void adamw_launch(float* p, float* g, float* m, float* v, void* p_bf16, int64_t n, const float* sqnorm,
-                  const int64_t* step, const float* hyper, float grad_scale, hipStream_t stream);
+                  const int64_t* step, const float* hyper, float grad_scale, hipStream_t stream,
+                  int64_t zero_hi = -1);
 void advance_counters_launch(int64_t* step, int64_t* rng, const float* sqnorm, hipStream_t stream);
 
 // Diffusion / data (diffusion.hip)

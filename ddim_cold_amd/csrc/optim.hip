@@ -70,7 +70,8 @@ __device__ __forceinline__ void adamw_elem(float& p, float g, float& m, float& v
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                                                     float* __restrict__ v, bf16* __restrict__ pb, int64_t n,
                                                     const float* __restrict__ sqnorm, const int64_t* __restrict__ step,
-                                                    const float* __restrict__ hyper, float grad_scale, bool vec) {
+                                                    const float* __restrict__ hyper, float grad_scale, bool vec,
+                                                    int64_t zero_hi) {
   const float sq = sum_parts(sqnorm);
   const bool skip = !isfinite(sq);
   const float base_lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
@@ -91,7 +92,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, float
   const int64_t stride = (int64_t)gridDim.x * 256;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += stride) {
     float4 gv = reinterpret_cast<float4*>(g)[i];
-    reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (4 * i < zero_hi) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (skip) continue;
     float4 pv = reinterpret_cast<const float4*>(p)[i];
     float4 mv = reinterpret_cast<const float4*>(m)[i];
@@ -111,7 +112,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, float
   }
   for (int64_t i = nv * 4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
     float gi = g[i];
-    g[i] = 0.f;
+    if (i < zero_hi) g[i] = 0.f;
     if (skip) continue;
     float pi = p[i], mi = m[i], vi = v[i];
     adamw_elem(pi, gi, mi, vi, coef, decay, b1, b2, step_size, inv_sbc2, eps);
@@ -147,11 +148,13 @@ void sqnorm_launch(const float* g, int64_t n, float* out, float scale, hipStream
 }
 
 void adamw_launch(float* p, float* g, float* m, float* v, void* p_bf16, int64_t n, const float* sqnorm,
-                  const int64_t* step, const float* hyper, float grad_scale, hipStream_t stream) {
+                  const int64_t* step, const float* hyper, float grad_scale, hipStream_t stream, int64_t zero_hi) {
+  if (zero_hi < 0 || zero_hi > n) zero_hi = n;
+  zero_hi = (zero_hi + 3) / 4 * 4 <= n ? (zero_hi + 3) / 4 * 4 : n;  // whole 16-B vectors
   auto al = [](const void* q, uintptr_t a) { return (reinterpret_cast<uintptr_t>(q) & (a - 1)) == 0; };
   const bool vec = al(p, 16) && al(g, 16) && al(m, 16) && al(v, 16) && (p_bf16 == nullptr || al(p_bf16, 8));
   hipLaunchKernelGGL(adamw_kernel, dim3(opt_grid(n)), dim3(256), 0, stream, p, g, m, v,
-                     reinterpret_cast<bf16*>(p_bf16), n, sqnorm, step, hyper, grad_scale, vec);
+                     reinterpret_cast<bf16*>(p_bf16), n, sqnorm, step, hyper, grad_scale, vec, zero_hi);
 }
 
 void advance_counters_launch(int64_t* step, int64_t* rng, const float* sqnorm, hipStream_t stream) {

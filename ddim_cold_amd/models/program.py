@@ -497,7 +497,7 @@ class ViTProgram:
                       training: bool = True, wgrad: Optional[Callable] = None,
                       ln_ws: Optional[torch.Tensor] = None, wgrad_stream=None,
                       embed_with_block0: bool = False, ln_final=None, wgrad_tail: bool = False,
-                      wgrad_flush=None) -> Iterator[int]:
+                      wgrad_flush=None, wgrad_store: bool = False) -> Iterator[int]:
         """Hand-written backward; yields the block index after each block's grads
         are issued (L-1 first, then ..., 0) and -1 after the embedding grads.
 
@@ -520,6 +520,8 @@ class ViTProgram:
         gradients are queued and issued as one launch per gradient bucket --
         after each listed block (and after the embedding backward) -- so the
         bucket's all-reduce can start while the rest of the backward runs.
+        ``wgrad_store`` (with ``wgrad_tail``): the weight-gradient targets are zero on
+        entry, so the tail launch writes instead of read-add-writing them.
         """
         def ws(k):
             return None if ln_ws is None else ln_ws[k]
@@ -638,7 +640,7 @@ class ViTProgram:
                 for job in tail_jobs:
                     ops.linear_wgrad(*job)
             else:
-                ops.linear_wgrad_multi(tail_jobs)
+                ops.linear_wgrad_multi(tail_jobs, store=wgrad_store and wgrad_tail)
             keep.append(tail_jobs)
         keep.append((gpatch, lf))
         if batch is not None:

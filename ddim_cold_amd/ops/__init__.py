@@ -335,17 +335,22 @@ def linear_dgrad_ride(dy, w, jobs, out_fp32: bool = False, splits: int = 1, gelu
     return out
 
 
-def linear_wgrad_multi(jobs):
+def linear_wgrad_multi(jobs, store: bool = False):
     """Every ``(dy, x, dw, db)`` weight-gradient job of a step (<= 32) in ONE launch
-    (csrc/gemm.hip ``gemm_wgrad_multi_kernel``; unsplit, deterministic)."""
+    (csrc/gemm.hip ``gemm_wgrad_multi_kernel``; unsplit, deterministic).  ``store``:
+    the targets are zero (``dW = dy^T x`` written, not added: no read of dW)."""
     if not jobs:
         return
     if _hip(jobs[0][0]):
         for a in range(0, len(jobs), 32):
             dys, xs, dws, dbs = (list(z) for z in zip(*jobs[a:a + 32]))
-            _ops().linear_wgrad_multi(dys, xs, dws, dbs)
+            _ops().linear_wgrad_multi(dys, xs, dws, dbs, bool(store))
         return
     for dy, x, dw, db in jobs:
+        if store:
+            dw.zero_()
+            if db is not None:
+                db.zero_()
         ref.linear_wgrad(dy, x, dw, db)
 
 
@@ -449,11 +454,13 @@ def attn_bwd(do, qkv, o, lse, scale: float, rng, site: int, p: float, keep=None)
 
 
 def embed_bwd(g, t, rng, site: int, p: float, dcls, dpos, dtemb, ln_final=None):
-    """``ln_final = (ws, dst_ptrs, C)``: the LayerNorm replica finalize
-    (:func:`replica_reduce_`) rides in the same launch (GPU only)."""
+    """``ln_final = (ws, dst_ptrs, C[, store])``: the LayerNorm replica finalize
+    (:func:`replica_reduce_`) rides in the same launch (GPU only); ``store``: the
+    destinations get the replica sum instead of having it added."""
     if _hip(g):
-        ws, ptrs, C = ln_final if ln_final is not None else (None, None, 0)
-        return _ops().embed_bwd(g, t, rng, site, float(p), dcls, dpos, dtemb, ws, ptrs, int(C))
+        ws, ptrs, C = ln_final[:3] if ln_final is not None else (None, None, 0)
+        store = bool(ln_final[3]) if ln_final is not None and len(ln_final) > 3 else False
+        return _ops().embed_bwd(g, t, rng, site, float(p), dcls, dpos, dtemb, ws, ptrs, int(C), store)
     if ln_final is not None:
         raise ValueError("ln_final needs the HIP extension (use replica_reduce_ on CPU)")
     return ref.embed_bwd(g, t, rng, site, p, dcls, dpos, dtemb)
@@ -471,10 +478,13 @@ def sqnorm(g, out, scale: float = 1.0):
     out[0] = (g.float() * scale).pow(2).sum()
 
 
-def adamw_step(p, g, m, v, pbf, sq, step, hyper, grad_scale: float = 1.0):
-    """Fused AdamW over a flat arena (see csrc/optim.hip for the exact math)."""
+def adamw_step(p, g, m, v, pbf, sq, step, hyper, grad_scale: float = 1.0, zero_hi: Optional[int] = None):
+    """Fused AdamW over a flat arena (see csrc/optim.hip for the exact math).
+    ``zero_hi``: zero the gradients only below this element (the producers of the
+    rest overwrite them next step); default: all."""
     if _hip(p):
-        return _ops().adamw_step(p, g, m, v, pbf, sq, step, hyper, float(grad_scale))
+        return _ops().adamw_step(p, g, m, v, pbf, sq, step, hyper, float(grad_scale),
+                                 -1 if zero_hi is None else int(zero_hi))
     import math
     sqv = float(sq.sum())
     base_lr, b1, b2, eps, wd, max_norm, tmax, eta_min = (float(x) for x in hyper.tolist()[:8])
@@ -482,7 +492,7 @@ def adamw_step(p, g, m, v, pbf, sq, step, hyper, grad_scale: float = 1.0):
     if max_norm > 0:
         coef *= min(1.0, max_norm / (math.sqrt(sqv) + 1e-6)) if math.isfinite(sqv) else 1.0
     gi = g * coef
-    g.zero_()
+    g[: (g.numel() if zero_hi is None else zero_hi)].zero_()
     if not math.isfinite(sqv):
         return
     t = int(step[0]) + 1

@@ -284,6 +284,9 @@ class TrainEngine:
                     self.bucket_ranges[k] = [r for a2, b2 in self.bucket_ranges[k]
                                              for r in ((a2, min(b2, to)), (max(a2, to + tn), b2)) if r[1] > r[0]]
         self._temb_t: List[torch.Tensor] = []
+        # gradient arena below this element is accumulated (embeddings: atomics in the
+        # embedding backward); above it every range has a single writer per step
+        self.acc_hi = min(self.offsets[n][0] for n in self.names if n.rsplit(".", 1)[0] in ln_prefixes)
         # LayerNorm dgamma/dbeta replica workspace in backward order: final norm,
         # then norm2, norm1 of blocks L-1 .. 0; destinations = grad-arena views
         # (weight and bias of one LayerNorm are adjacent: one [2D] range).
@@ -323,6 +326,16 @@ class TrainEngine:
         self._graphs = None
         self._multi = None
 
+    def _grad_overwrite(self, k_acc: int, tail_w: bool, ln_final) -> bool:
+        """Single process, one micro-batch, deferred weight gradients and the LayerNorm
+        finalize in the embedding launch: everything above ``acc_hi`` in the gradient
+        arena (LayerNorms, blocks, head) is written by exactly one producer per step,
+        which then stores instead of adding -- the optimizer zeroes only the
+        embeddings (accumulated by atomics) and the tail launch reads no gradients
+        (DDIM_COLD_GRAD_OVERWRITE=0: accumulate everywhere)."""
+        return (self.is_cuda and not self.segmented and k_acc == 1 and tail_w and ln_final is not None
+                and self.side is None and os.environ.get("DDIM_COLD_GRAD_OVERWRITE", "1") != "0")
+
     def _join_side(self):
         if self.side is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.side)
@@ -336,6 +349,7 @@ class TrainEngine:
         # EMA moves once per optimizer step (multi_gpu_trainer.py:126 semantics).
         tail = self.lnfold is not None
         loss_acc = None
+        overwrite = False
         self._temb_t = []
         for micro in range(k_acc):
             last = micro == k_acc - 1
@@ -381,13 +395,20 @@ class TrainEngine:
             # single process: every weight gradient in one launch after the backward
             # (no bucket needs a block's gradients early)
             tail_w = not self.segmented and os.environ.get("DDIM_COLD_WGRAD_TAIL", "1") != "0"
+            # single process, one micro-batch: every gradient above the embeddings has ONE
+            # producer per step (the tail weight-gradient launch, the LayerNorm finalize), so
+            # those write instead of accumulate and the optimizer zeroes only the embeddings
+            overwrite = self._grad_overwrite(k_acc, tail_w, ln_final)
+            if overwrite:
+                ln_final = ln_final + (True,)
             # data parallel: one weight-gradient launch per gradient bucket
             # (DDIM_COLD_WGRAD_BUCKET=0: riders in the input-gradient launches)
             flush_at = set(k for k in self.bucket_after if k >= 0) \
                 if (self.segmented and os.environ.get("DDIM_COLD_WGRAD_BUCKET", "1") != "0") else None
             for i in self.prog.backward_iter(self.param_tensors, self.grad_tensors, S, dtok, self.rng, True,
                                              ln_ws=self.ln_ws, wgrad_stream=self.side, embed_with_block0=merge,
-                                             ln_final=ln_final, wgrad_tail=tail_w, wgrad_flush=flush_at):
+                                             ln_final=ln_final, wgrad_tail=tail_w, wgrad_flush=flush_at,
+                                             wgrad_store=overwrite):
                 if i in self.bucket_after and (self.segmented or i == -1):
                     hi = self.ln_done_at[i]
                     if ln_final is not None:
@@ -408,7 +429,7 @@ class TrainEngine:
         gs = 1.0 / (self.world * k_acc)
         ops.sqnorm(self.flat_g, self.sqnorm, gs)
         ops.adamw_step(self.flat_p, self.flat_g, self.flat_m, self.flat_v, self.flat_pb, self.sqnorm,
-                       self.step_ctr, self.hyper, gs)
+                       self.step_ctr, self.hyper, gs, zero_hi=self.acc_hi if overwrite else None)
         if loss_acc is not None:
             loss_parts = loss_acc
         if tail:

@@ -134,3 +134,27 @@ def test_ln_replica_finalize_fused_matches_separate(monkeypatch):
     init = torch.cat([torch.ones(384), torch.zeros(384)]).cuda().repeat(15)
     assert (lf - init).abs().max() > 0
     torch.testing.assert_close(lf, lu, rtol=0, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_gradient_overwrite_matches_accumulate(monkeypatch):
+    """Single writer per gradient range (tail weight-gradient launch and LayerNorm finalize
+    store, AdamW zeroes only the embeddings) == accumulate + zero everything."""
+    def run(flag):
+        monkeypatch.setenv("DDIM_COLD_GRAD_OVERWRITE", flag)
+        torch.manual_seed(0)
+        model = build_model("vit_tiny").cuda().train()
+        eng = TrainEngine(model, EngineConfig(lr=1e-3, t_max=100, seed=3, use_graph=True, graph_warmup=1,
+                                              temb_rows=7))
+        eng.set_batch_fn(ColdBatcher(synthetic_pool(64, seed=1, device="cuda"), 8, eng.rng))
+        losses = [float(eng.train_step()) for _ in range(5)]
+        torch.cuda.synchronize()
+        return eng.flat_p.clone(), losses, eng
+    po, lo, eng = run("1")
+    pa, la, eng_a = run("0")
+    assert eng.acc_hi < eng.offsets["blocks.0.attn.qkv.weight"][0]
+    # overwrite mode leaves the last step's gradients above acc_hi in place; accumulate zeroes all
+    assert eng.flat_g[eng.acc_hi:].abs().max() > 0 and eng_a.flat_g.abs().max() == 0
+    assert eng.flat_g[:eng.acc_hi].abs().max() == 0
+    assert all(abs(a - b) <= 1e-4 * abs(b) for a, b in zip(lo, la)), (lo, la)
+    assert (po - pa).abs().max().item() <= 2 * 1e-3 * 5
