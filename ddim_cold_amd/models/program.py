@@ -520,8 +520,9 @@ class ViTProgram:
         gradients are queued and issued as one launch per gradient bucket --
         after each listed block (and after the embedding backward) -- so the
         bucket's all-reduce can start while the rest of the backward runs.
-        ``wgrad_store`` (with ``wgrad_tail``): the weight-gradient targets are zero on
-        entry, so the tail launch writes instead of read-add-writing them.
+        ``wgrad_store``: the block / head weight-gradient targets have no other writer
+        this step, so the deferred launches (tail or per bucket) write instead of
+        read-add-writing them (the embedding bucket's patch gradient still adds).
         """
         def ws(k):
             return None if ln_ws is None else ln_ws[k]
@@ -624,7 +625,7 @@ class ViTProgram:
                 gpatch = self._embed_backward(P, G, S, g, rng, pd, wgrad, ln_final)
             flush()
             if bucketed and (i in wgrad_flush or (i == 0 and embed_with_block0)) and tail_jobs:
-                ops.linear_wgrad_multi(tail_jobs)  # this bucket's weight gradients: final now
+                ops.linear_wgrad_multi(tail_jobs, store=wgrad_store)  # this bucket's weight gradients: final now
                 keep.append(tail_jobs)
                 tail_jobs = []
             yield i

@@ -326,14 +326,16 @@ class TrainEngine:
         self._graphs = None
         self._multi = None
 
-    def _grad_overwrite(self, k_acc: int, tail_w: bool, ln_final) -> bool:
-        """Single process, one micro-batch, deferred weight gradients and the LayerNorm
-        finalize in the embedding launch: everything above ``acc_hi`` in the gradient
-        arena (LayerNorms, blocks, head) is written by exactly one producer per step,
-        which then stores instead of adding -- the optimizer zeroes only the
-        embeddings (accumulated by atomics) and the tail launch reads no gradients
-        (DDIM_COLD_GRAD_OVERWRITE=0: accumulate everywhere)."""
-        return (self.is_cuda and not self.segmented and k_acc == 1 and tail_w and ln_final is not None
+    def _grad_overwrite(self, k_acc: int, deferred: bool, ln_final) -> bool:
+        """One micro-batch, deferred weight gradients (the single-process tail launch or
+        one launch per data-parallel bucket) and the LayerNorm finalize in the
+        embedding launch: everything above ``acc_hi`` in the gradient arena
+        (LayerNorms, blocks, head) is written by exactly one producer per step, which
+        then stores instead of adding -- the optimizer zeroes only the embeddings
+        (accumulated by atomics) and the deferred launches read no gradients.  The
+        all-reduce sums the fresh values in place.  DDIM_COLD_GRAD_OVERWRITE=0:
+        accumulate everywhere."""
+        return (self.is_cuda and k_acc == 1 and deferred and ln_final is not None
                 and self.side is None and os.environ.get("DDIM_COLD_GRAD_OVERWRITE", "1") != "0")
 
     def _join_side(self):
@@ -398,13 +400,13 @@ class TrainEngine:
             # single process, one micro-batch: every gradient above the embeddings has ONE
             # producer per step (the tail weight-gradient launch, the LayerNorm finalize), so
             # those write instead of accumulate and the optimizer zeroes only the embeddings
-            overwrite = self._grad_overwrite(k_acc, tail_w, ln_final)
-            if overwrite:
-                ln_final = ln_final + (True,)
-            # data parallel: one weight-gradient launch per gradient bucket
-            # (DDIM_COLD_WGRAD_BUCKET=0: riders in the input-gradient launches)
             flush_at = set(k for k in self.bucket_after if k >= 0) \
                 if (self.segmented and os.environ.get("DDIM_COLD_WGRAD_BUCKET", "1") != "0") else None
+            overwrite = self._grad_overwrite(k_acc, tail_w or flush_at is not None, ln_final)
+            if overwrite:
+                ln_final = ln_final + (True,)
+            # data parallel: one weight-gradient launch per gradient bucket (flush_at,
+            # above; DDIM_COLD_WGRAD_BUCKET=0: riders in the input-gradient launches)
             for i in self.prog.backward_iter(self.param_tensors, self.grad_tensors, S, dtok, self.rng, True,
                                              ln_ws=self.ln_ws, wgrad_stream=self.side, embed_with_block0=merge,
                                              ln_final=ln_final, wgrad_tail=tail_w, wgrad_flush=flush_at,
