@@ -28,6 +28,14 @@ namespace dc {
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
+// profiling aid (tools/ub_attn_stamps.py): when set, wave 0 of every short-backward
+// workgroup records s_memrealtime (100 MHz) at its phase boundaries, [grid][4]
+__device__ unsigned long long* g_attn_stamps = nullptr;
+__device__ __forceinline__ void attn_stamp(int k) {
+  unsigned long long* s = g_attn_stamps;
+  if (s != nullptr && threadIdx.x == 0) s[(size_t)blockIdx.x * 4 + k] = __builtin_amdgcn_s_memrealtime();
+}
+
 template <int HD>
 struct AC {
   static constexpr int S = 2 * HD + 32;   // LDS row stride in bytes
@@ -855,7 +863,9 @@ __global__ __launch_bounds__(NP * 4) void attn_fwd_short_kernel(const bf16* __re
   using I = ShortImg<HD, NP>;
   constexpr int RS = I::RS, KS = HD / 32, DT = HD / 16, KT = NP / 16;
   static_assert(KT * 4 <= 32, "one 32-bit keep word per lane");
-  __shared__ __attribute__((aligned(16))) char lds[2 * NP * RS];
+  // dynamic LDS (2 * NP * RS bytes, see short_lds): with static LDS, 384-thread
+  // workgroups were admitted one per CU from ~60 KB on (tools/ub_lds_census.hip)
+  extern __shared__ __attribute__((aligned(16))) char lds[];
   char* Kl = lds;
   char* Vl = lds + NP * RS;
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
@@ -954,7 +964,12 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
                                                                 const uint32_t* __restrict__ keep_bits) {
   using I = ShortImg<HD, NP>;
   constexpr int RS = I::RS, PS = 2 * NP + 32, KS = HD / 32, DT = HD / 16, KT = NP / 16;
-  __shared__ __attribute__((aligned(16))) char lds[4 * NP * RS + 2 * NP * PS];
+  // dynamic LDS (4 * NP * RS + 2 * NP * PS bytes, see short_lds): the same image as a
+  // static array (79,872 B at NP 96) got ONE 384-thread workgroup per CU instead of two
+  // -- 128 of the ViT-tiny step's 384 workgroups then waited for a second round
+  // (tools/ub_attn_stamps.py, tools/ub_lds_census.hip)
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  attn_stamp(0);
   char* Ql = lds;
   char* Kl = Ql + NP * RS;
   char* Vl = Kl + NP * RS;
@@ -1052,6 +1067,7 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
     id.store(Dl);
   }
   __syncthreads();
+  attn_stamp(1);
 
   // ---- phase A: this wave's 16 queries against all keys
   const float lse2 = qv ? lse_raw * LOG2E : INFINITY;
@@ -1117,6 +1133,7 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
 #pragma unroll
     for (int d = 0; d < DT; ++d) *reinterpret_cast<bf16x4*>(row + 16 * d + 4 * g) = pack4(dq[d] * scale);
   }
+  attn_stamp(2);
   __syncthreads();
 
   // ---- phase B: this wave's 16 keys against all queries
@@ -1145,6 +1162,21 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
       *reinterpret_cast<bf16x4*>(row + 2 * D + 16 * d + 4 * g) = pack4(dv[d]);
     }
   }
+  attn_stamp(3);
+}
+
+// LDS bytes of the short kernels' images (dynamic shared memory)
+template <int HD, int NP>
+struct ShortLds {
+  static constexpr int RS = ShortImg<HD, NP>::RS, PS = 2 * NP + 32;
+  static constexpr int FWD = 2 * NP * RS;
+  static constexpr int BWD = 4 * NP * RS + 2 * NP * PS;
+};
+
+template <typename K>
+static void allow_lds(K kernel, int bytes) {
+  if (bytes > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
 template <int HD, int NP, bool DROP>
@@ -1152,15 +1184,23 @@ struct ShortLaunch {
   static void run(bool bwd, const bf16* d, const bf16* q, const bf16* o, float* lse, const float* lse_in,
                   bf16* outp, int B, int H, int N, float scale, const int64_t* rng, int site, uint32_t thr,
                   float dsc, hipStream_t stream, const bf16* wp, int Dm, uint32_t* kb) {
+    using L = ShortLds<HD, NP>;
+    static const bool attr = [] {
+      allow_lds(&attn_fwd_short_kernel<HD, NP, DROP>, L::FWD);
+      allow_lds(&attn_bwd_short_kernel<HD, NP, DROP, true>, L::BWD);
+      allow_lds(&attn_bwd_short_kernel<HD, NP, DROP, false>, L::BWD);
+      return true;
+    }();
+    (void)attr;
     if (!bwd)
-      hipLaunchKernelGGL((attn_fwd_short_kernel<HD, NP, DROP>), dim3(B * H), dim3(NP * 4), 0, stream, q, outp, lse,
-                         B, H, N, scale, rng, site, thr, dsc, kb);
+      hipLaunchKernelGGL((attn_fwd_short_kernel<HD, NP, DROP>), dim3(B * H), dim3(NP * 4), L::FWD, stream, q, outp,
+                         lse, B, H, N, scale, rng, site, thr, dsc, kb);
     else if (wp != nullptr)
-      hipLaunchKernelGGL((attn_bwd_short_kernel<HD, NP, DROP, true>), dim3(B * H), dim3(NP * 4), 0, stream, d, q, o,
-                         lse_in, outp, B, H, N, scale, rng, site, thr, dsc, wp, Dm, kb);
+      hipLaunchKernelGGL((attn_bwd_short_kernel<HD, NP, DROP, true>), dim3(B * H), dim3(NP * 4), L::BWD, stream, d, q,
+                         o, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, wp, Dm, kb);
     else
-      hipLaunchKernelGGL((attn_bwd_short_kernel<HD, NP, DROP, false>), dim3(B * H), dim3(NP * 4), 0, stream, d, q, o,
-                         lse_in, outp, B, H, N, scale, rng, site, thr, dsc, wp, Dm, kb);
+      hipLaunchKernelGGL((attn_bwd_short_kernel<HD, NP, DROP, false>), dim3(B * H), dim3(NP * 4), L::BWD, stream, d, q,
+                         o, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, wp, Dm, kb);
   }
 };
 
@@ -1448,6 +1488,11 @@ static bool short_disabled() {
 }  // namespace dc
 
 using namespace dc;
+
+void attn_set_stamps(void* buf) {
+  unsigned long long* p = reinterpret_cast<unsigned long long*>(buf);
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_attn_stamps), &p, sizeof(p));
+}
 
 int64_t attn_keep_words(int B, int H, int N, int hd) {
   if (N > SHORT_MAX_N || short_disabled() || (hd != 32 && hd != 64)) return 0;

@@ -78,7 +78,10 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict_
                                                      uint32_t thr_drop, float sc_drop, int site_dp, uint32_t thr_dp,
                                                      float sc_dp, int dy_parts) {
   constexpr int D = VEC * 128;
-  __shared__ float red[NW][2 * D];
+  // dynamic LDS ([NW][2D] floats): static LDS limited the residency of the larger
+  // non-256-thread workgroups (tools/ub_lds_census.hip)
+  extern __shared__ float red_dyn[];
+  float (*red)[2 * D] = reinterpret_cast<float (*)[2 * D]>(red_dyn);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float2* g2 = reinterpret_cast<const float2*>(gamma);
   float2 dgam[VEC], dbet[VEC], gm[VEC], bt[VEC];
@@ -362,8 +365,11 @@ void layernorm_bwd_launch(const void* dy, bool dy_bf16, const float* x, const fl
     return e ? atoi(e) : 0;
   }();
 #define LN_BWD_GO1(R, W, DYB)                                                                                 \
-  LN_DISPATCH(D, hipLaunchKernelGGL((ln_bwd_kernel<VEC, R, W, DYB>), dim3((M + R * W - 1) / (R * W)), dim3(W * 64), \
-                                    0, stream, dy, x, mean, rstd, gamma, beta, g_res, g_out,                   \
+  LN_DISPATCH(D, if (W * 2 * D * sizeof(float) > 65536)                                                         \
+                  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&ln_bwd_kernel<VEC, R, W, DYB>),           \
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, W * 2 * D * sizeof(float));  \
+                hipLaunchKernelGGL((ln_bwd_kernel<VEC, R, W, DYB>), dim3((M + R * W - 1) / (R * W)), dim3(W * 64), \
+                                    W * 2 * D * sizeof(float), stream, dy, x, mean, rstd, gamma, beta, g_res, g_out, \
                                     reinterpret_cast<bf16*>(gy_bf16), reinterpret_cast<bf16*>(y_bf16), dgb_ws,  \
                                     M, tokens, rng, site_drop, td,                                              \
                                     sd, site_dp, tp, sp, dy_parts))
