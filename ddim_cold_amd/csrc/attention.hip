@@ -1290,8 +1290,9 @@ __global__ __launch_bounds__(NP * 4) void qkv_attn_fwd_kernel(QkvAttnArgs a) {
   using I = ShortImg<HD, NP>;
   constexpr int RS = I::RS, KSA = HD / 32, DT = HD / 16, KT = NP / 16;
   static_assert(RS == AC<HD>::S, "image stride");
-  __shared__ __attribute__((aligned(16))) char lds[2 * SLOT + 3 * NP * RS];
-  __shared__ float2 ms[NP];
+  // dynamic LDS: [2 * SLOT + 3 * NP * RS] images, then [NP] float2 (see ShortLds)
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  float2* ms = reinterpret_cast<float2*>(lds + 2 * SLOT + 3 * NP * RS);
   char* ring = lds;
   char* Ql = lds + 2 * SLOT;
   char* Kl = Ql + NP * RS;
@@ -1460,12 +1461,13 @@ __global__ __launch_bounds__(NP * 4) void qkv_attn_fwd_kernel(QkvAttnArgs a) {
 template <int NP, int KS>
 static void launch_qkv_attn(const QkvAttnArgs& a, bool fold, hipStream_t stream) {
   const dim3 grid(a.B * a.H), block(NP * 4);
+  constexpr int lds = 2 * (3 * 32 * 64) + 3 * NP * ShortImg<32, NP>::RS + NP * 8;  // images + ms (dynamic)
   if (a.thr) {
-    if (fold) hipLaunchKernelGGL((qkv_attn_fwd_kernel<32, NP, KS, true, true>), grid, block, 0, stream, a);
-    else hipLaunchKernelGGL((qkv_attn_fwd_kernel<32, NP, KS, true, false>), grid, block, 0, stream, a);
+    if (fold) hipLaunchKernelGGL((qkv_attn_fwd_kernel<32, NP, KS, true, true>), grid, block, lds, stream, a);
+    else hipLaunchKernelGGL((qkv_attn_fwd_kernel<32, NP, KS, true, false>), grid, block, lds, stream, a);
   } else {
-    if (fold) hipLaunchKernelGGL((qkv_attn_fwd_kernel<32, NP, KS, false, true>), grid, block, 0, stream, a);
-    else hipLaunchKernelGGL((qkv_attn_fwd_kernel<32, NP, KS, false, false>), grid, block, 0, stream, a);
+    if (fold) hipLaunchKernelGGL((qkv_attn_fwd_kernel<32, NP, KS, false, true>), grid, block, lds, stream, a);
+    else hipLaunchKernelGGL((qkv_attn_fwd_kernel<32, NP, KS, false, false>), grid, block, lds, stream, a);
   }
 }
 
