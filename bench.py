@@ -71,6 +71,8 @@ def main():
                     help="gradient collectives through torch.distributed (RCCL) or the native RCCL communicator")
     ap.add_argument("--sampler-k", type=int, default=20)
     ap.add_argument("--sampler-n", type=int, default=64)
+    ap.add_argument("--sampler-host-noise", action="store_true",
+                    help="draw the sampler's x_T on the host (torch.normal on CPU, as the reference)")
     ap.add_argument("--no-eager-baseline", action="store_true",
                     help="skip timing the plain eager PyTorch sampler (BASELINE.md's sampling comparator)")
     args = ap.parse_args()
@@ -131,26 +133,28 @@ def main():
         from ddim_cold_amd.diffusion.samplers import DDIMSampler
         model.eval()
         s = DDIMSampler(model, dev, k=args.sampler_k)
-        g = torch.Generator().manual_seed(0)
-        s.sample(args.sampler_n, generator=g)  # capture
+        # x_T drawn on the device (seeded); --sampler-host-noise: on the host as the reference
+        g = torch.Generator(device=dev if not args.sampler_host_noise else "cpu").manual_seed(0)
+        dn = not args.sampler_host_noise
+        s.sample(args.sampler_n, generator=g, device_noise=dn)  # capture
         torch.cuda.synchronize()
-        reps = 5
+        reps = 10
         ts = time.perf_counter()
-        for _ in range(reps):
-            s.sample(args.sampler_n, generator=g)
+        for _ in range(reps):  # every batch: noise draw, the 100-step graph, result copied to the host
+            s.sample(args.sampler_n, generator=g, device_noise=dn)
         torch.cuda.synchronize()
         dt = (time.perf_counter() - ts) / reps
         extra = {"ddim_sampler_img_per_s": round(args.sampler_n / dt, 1),
                  "ddim_sampler_ms_per_batch": round(dt * 1e3, 3),
                  "ddim_sampler_config": {"k": args.sampler_k, "N": args.sampler_n, "steps": len(s.ts),
-                                         "graph": True}}
+                                         "graph": True, "noise": "device" if dn else "host"}}
         if not args.no_eager_baseline:
             # the sampling yardstick is a plain eager PyTorch-ROCm
             # implementation of the same math on the same GPU (fp32, as the
             # reference samples; bf16-autocast variant reported too)
             from ddim_cold_amd.bench.eager_sampler import time_eager_sampler
-            e32 = time_eager_sampler(model, dev, args.sampler_k, args.sampler_n)
-            ebf = time_eager_sampler(model, dev, args.sampler_k, args.sampler_n, autocast_bf16=True)
+            e32 = time_eager_sampler(model, dev, args.sampler_k, args.sampler_n, device_noise=dn)
+            ebf = time_eager_sampler(model, dev, args.sampler_k, args.sampler_n, autocast_bf16=True, device_noise=dn)
             extra["ddim_sampler_eager_torch_fp32_img_per_s"] = round(args.sampler_n / e32, 1)
             extra["ddim_sampler_eager_torch_bf16_img_per_s"] = round(args.sampler_n / ebf, 1)
             extra["ddim_sampler_vs_eager_fp32"] = round(e32 / dt, 2)

@@ -18,10 +18,14 @@ import torch
 
 
 @torch.no_grad()
-def eager_ddim_sample(model, device, k: int, N: int, generator=None, autocast_bf16: bool = False):
+def eager_ddim_sample(model, device, k: int, N: int, generator=None, autocast_bf16: bool = False,
+                      device_noise: bool = False):
     T = model.total_steps
     C, (H, W) = model.in_chans, model.img_size
-    x = torch.normal(0.0, 1.0, (N, C, H, W), generator=generator).to(device)
+    if device_noise:  # same noise policy as the fused sampler under comparison
+        x = torch.randn((N, C, H, W), device=device, generator=generator)
+    else:
+        x = torch.normal(0.0, 1.0, (N, C, H, W), generator=generator).to(device)
     x0 = x
     for t in range(T - 1, 0, -k):
         tt = torch.tensor([t] * N, device=device)
@@ -35,17 +39,18 @@ def eager_ddim_sample(model, device, k: int, N: int, generator=None, autocast_bf
     return (x0.cpu() + 1) / 2
 
 
-def time_eager_sampler(model, device, k: int, N: int, reps: int = 2, autocast_bf16: bool = False) -> float:
+def time_eager_sampler(model, device, k: int, N: int, reps: int = 2, autocast_bf16: bool = False,
+                       device_noise: bool = False) -> float:
     """Seconds per N-image batch (after one warm-up batch)."""
     was = model.training
     model.eval()
     try:
-        g = torch.Generator().manual_seed(0)
-        eager_ddim_sample(model, device, k, N, g, autocast_bf16)
+        g = torch.Generator(device=device if device_noise else "cpu").manual_seed(0)
+        eager_ddim_sample(model, device, k, N, g, autocast_bf16, device_noise)
         torch.cuda.synchronize(device)
         t0 = time.perf_counter()
         for _ in range(reps):
-            eager_ddim_sample(model, device, k, N, g, autocast_bf16)
+            eager_ddim_sample(model, device, k, N, g, autocast_bf16, device_noise)
         torch.cuda.synchronize(device)
         return (time.perf_counter() - t0) / reps
     finally:

@@ -220,12 +220,19 @@ class DDIMSampler:
 
     @torch.no_grad()
     def sample(self, N: int, generator: Optional[torch.Generator] = None, verbose: bool = False,
-               noise: Optional[torch.Tensor] = None) -> torch.Tensor:
+               noise: Optional[torch.Tensor] = None, device_noise: bool = False) -> torch.Tensor:
+        """``device_noise``: draw x_T on the GPU (``generator`` then a device generator)
+        instead of on the host as the reference does (ViT.py:224-225) -- same
+        distribution, a different stream; saves the host draw + copy (~2.5 ms per
+        N=64 batch)."""
         st = self._state(N, False)
         t0 = time.time()
-        if noise is None:
-            noise = torch.normal(0.0, 1.0, (N, self.C, self.H, self.W), generator=generator)
-        st["x"].copy_(noise)
+        if noise is not None:
+            st["x"].copy_(noise)
+        elif device_noise:
+            st["x"].normal_(0.0, 1.0, generator=generator)
+        else:
+            st["x"].copy_(torch.normal(0.0, 1.0, (N, self.C, self.H, self.W), generator=generator))
         st["loop"].run(self.use_graph)
         out = (st["x0"].cpu() + 1) / 2
         if verbose:
