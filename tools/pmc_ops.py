@@ -20,13 +20,19 @@ w3, b3 = bf(3 * D, D, sc=0.05), torch.randn(3 * D, device=dev)
 x = torch.randn(M, D, device=dev)
 g, be = torch.randn(D, device=dev), torch.randn(D, device=dev)
 dqkv = bf(M, 3 * D)
-dw, db = torch.zeros(D, D, device=dev), torch.zeros(D, device=dev)
-dw3, db3 = torch.zeros(3 * D, D, device=dev), torch.zeros(3 * D, device=dev)
-blk = [(a, a, dw, db), (a, a, dw.clone(), db.clone()), (a, a, dw.clone(), db.clone()), (dqkv, a, dw3, db3)]
+def job(nout, k, m=M):
+    return (bf(m, nout, sc=0.1), bf(m, k, sc=0.1), torch.zeros(nout, k, device=dev), torch.zeros(nout, device=dev))
+
+
+# the step's deferred weight-gradient launch: 7 blocks (qkv, proj, fc1, fc2) + head + patch embedding
+wjobs = [job(3 * D, D) if i % 4 == 0 else job(D, D) for i in range(28)] + [job(192, D), job(D, 192, 2048)]
 qkv = bf(3, B, H, N, 32)
 do = bf(B, N, D)
+u = bf(M, D)
 _, mu, rs = ops.layernorm_fwd(x, g, be)
 ws = torch.zeros(ops.LN_REPLICAS, 2 * D, device=dev)
+dyb = bf(M, D)
+keep = ops.attn_keep_buffer(qkv, 0.1)
 n = 7_300_000
 p_, g_, m_, v_ = [torch.randn(n, device=dev) for _ in range(4)]
 pb = torch.empty(n, device=dev, dtype=torch.bfloat16)
@@ -38,11 +44,13 @@ for _ in range(20):
     ops.qkv_fwd(a, w3, b3, B, N, H)
     ops.linear_gelu_fwd(a, w, b, r, 5, 0.1)
     ops.linear_dgrad(dqkv, w3, True)
-    ops.linear_wgrad_group(blk)
-    o, lse = ops.attn_fwd(qkv, 32 ** -0.5, r, 5, 0.1)
-    ops.attn_bwd(do, qkv, o, lse, 32 ** -0.5, r, 5, 0.1)
-    ops.layernorm_fwd(x, g, be)
-    ops.layernorm_bwd(x, x, mu, rs, g, x, g.clone(), be.clone(), N, r, 3, 0.1, 4, 0.1, True, ws)
+    ops.linear_dgrad(a, w, False)
+    ops.linear_dgrad_gelu(a, w, u, r, 5, 0.1)
+    ops.linear_wgrad_multi(wjobs, store=True)
+    o, lse = ops.attn_fwd(qkv, 32 ** -0.5, r, 5, 0.1, keep_out=keep)
+    ops.attn_bwd(do, qkv, o, lse, 32 ** -0.5, r, 5, 0.1, keep=keep)
+    ops.layernorm_bwd(dyb, x, mu, rs, g, x, g.clone(), be.clone(), N, r, 3, 0.1, 4, 0.1, True, ws)
+    ops.sqnorm(g_, sq, 1.0)
     ops.adamw_step(p_, g_, m_, v_, pb, sq, st, hy, 1.0)
 torch.cuda.synchronize()
 print("ok")
