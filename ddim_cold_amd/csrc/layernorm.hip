@@ -230,9 +230,10 @@ __global__ __launch_bounds__(256) void replica_reduce_kernel(float* __restrict__
 // the GEMM accumulated), bf[n] = b[n] + sum_k beta_k W[n][k].  One wave per
 // output row, all folded GEMMs of the model in one launch (after each
 // optimizer step; once per sampling run).
-__global__ __launch_bounds__(256) void ln_fold_kernel(FoldTable tb) {
-  if (tb.tail && blockIdx.x == gridDim.x - 1) {
-    // training-step tail (one workgroup): loss from its partials, counters
+// training-step tail run by the fold launch's last workgroup: loss from its
+// partials (loss_last, EMA), counters
+__device__ __forceinline__ void fold_tail(const FoldTable& tb) {
+  {
     __shared__ float red[2][4];
     float lv = 0.f, sv = 0.f;
     for (int i = threadIdx.x; i < tb.loss_nparts; i += 256) lv += tb.loss_parts[i];
@@ -253,6 +254,12 @@ __global__ __launch_bounds__(256) void ln_fold_kernel(FoldTable tb) {
       tb.step[1] += 1;
       tb.rng[1] += 1;
     }
+  }
+}
+
+__global__ __launch_bounds__(256) void ln_fold_kernel(FoldTable tb) {
+  if (tb.tail && blockIdx.x == gridDim.x - 1) {
+    fold_tail(tb);
     return;
   }
   // two rows per wave (32 lanes each), every load of the row issued before use
@@ -308,6 +315,68 @@ __global__ __launch_bounds__(256) void ln_fold_kernel(FoldTable tb) {
   }
 }
 
+// bf16 weights (the optimizer's shadow), K % 8 == 0: 16 lanes per row (16 rows per
+// workgroup), 16-byte weight loads and stores -- the 32-lane / 8-byte kernel above
+// moved half as many bytes per instruction
+__global__ __launch_bounds__(256) void ln_fold16_kernel(FoldTable tb) {
+  if (tb.tail && blockIdx.x == gridDim.x - 1) {
+    fold_tail(tb);
+    return;
+  }
+  constexpr int IT = 4;  // 16-B chunks per lane: K <= 16 * 8 * IT = 512
+  const int hl = threadIdx.x & 15;
+  const int r = blockIdx.x * 16 + (threadIdx.x >> 4);
+  const bool live = r < tb.start[tb.n];
+  const int rr = live ? r : tb.start[tb.n] - 1;
+  int ji = 0;
+#pragma unroll
+  for (int j = 1; j < FOLD_MAX; ++j)
+    if (j < tb.n && rr >= tb.start[j]) ji = j;
+  const FoldJob& jb = tb.j[ji];
+  const int n = rr - tb.start[ji], K8 = tb.K / 8;
+  const bf16x8* w = reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(jb.w) + (size_t)n * tb.K);
+  const f32x4* g = reinterpret_cast<const f32x4*>(jb.gamma);
+  const f32x4* b = reinterpret_cast<const f32x4*>(jb.beta);
+  bf16x8* o = reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(jb.wf) + (size_t)n * tb.K);
+  bf16x8 wv[IT];
+  f32x4 g0[IT], g1[IT], b0[IT], b1[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int k = hl + 16 * i;
+    const bool ok = k < K8;
+    const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+    wv[i] = w[ok ? k : 0];  // out-of-range chunks: gamma = beta = 0 below zero their terms
+    g0[i] = ok ? g[2 * k] : z;
+    g1[i] = ok ? g[2 * k + 1] : z;
+    b0[i] = ok ? b[2 * k] : z;
+    b1[i] = ok ? b[2 * k + 1] : z;
+  }
+  float cs = 0.f, bs = 0.f;
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int k = hl + 16 * i;
+    const bf16x8 wq = wv[i];
+    const float w0 = bf2f(wq[0]), w1 = bf2f(wq[1]), w2 = bf2f(wq[2]), w3 = bf2f(wq[3]);
+    const float w4 = bf2f(wq[4]), w5 = bf2f(wq[5]), w6 = bf2f(wq[6]), w7 = bf2f(wq[7]);
+    bf16x8 q;
+    q[0] = f2bf(g0[i][0] * w0); q[1] = f2bf(g0[i][1] * w1); q[2] = f2bf(g0[i][2] * w2); q[3] = f2bf(g0[i][3] * w3);
+    q[4] = f2bf(g1[i][0] * w4); q[5] = f2bf(g1[i][1] * w5); q[6] = f2bf(g1[i][2] * w6); q[7] = f2bf(g1[i][3] * w7);
+    cs += ((bf2f(q[0]) + bf2f(q[1])) + (bf2f(q[2]) + bf2f(q[3]))) + ((bf2f(q[4]) + bf2f(q[5])) + (bf2f(q[6]) + bf2f(q[7])));
+    bs += ((b0[i][0] * w0 + b0[i][1] * w1) + (b0[i][2] * w2 + b0[i][3] * w3)) +
+          ((b1[i][0] * w4 + b1[i][1] * w5) + (b1[i][2] * w6 + b1[i][3] * w7));
+    if (live && k < K8) o[k] = q;
+  }
+#pragma unroll
+  for (int m = 8; m > 0; m >>= 1) {
+    cs += __shfl_xor(cs, m, 16);
+    bs += __shfl_xor(bs, m, 16);
+  }
+  if (live && hl == 0) {
+    jb.c[n] = cs;
+    jb.bf[n] = bs + (jb.bias ? jb.bias[n] : 0.f);
+  }
+}
+
 }  // namespace dc
 
 using namespace dc;
@@ -316,6 +385,14 @@ void ln_fold_launch(const FoldTable& tb, hipStream_t stream) {
   if (tb.n <= 0) return;
   if (tb.n > FOLD_MAX || tb.K % 4 || tb.K > 512) throw std::runtime_error("ln_fold: bad table (K % 4, K <= 512)");
   const int rows = tb.start[tb.n];
+  static const bool v16 = [] {
+    const char* e = getenv("DDIM_COLD_FOLD16");
+    return !(e && e[0] == '0');
+  }();
+  if (v16 && tb.w_bf16 && tb.K % 8 == 0) {
+    hipLaunchKernelGGL(ln_fold16_kernel, dim3((rows + 15) / 16 + (tb.tail ? 1 : 0)), dim3(256), 0, stream, tb);
+    return;
+  }
   hipLaunchKernelGGL(ln_fold_kernel, dim3((rows + 7) / 8 + (tb.tail ? 1 : 0)), dim3(256), 0, stream, tb);
 }
 
