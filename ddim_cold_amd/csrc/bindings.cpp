@@ -252,6 +252,15 @@ void attn_stamps(c10::optional<Tensor> buf) {
   attn_set_stamps(p);
 }
 
+void ln_stamps(c10::optional<Tensor> buf) {
+  void* p = nullptr;
+  if (buf.has_value() && buf->defined()) {
+    CHECK_IN((*buf), at::kLong);
+    p = buf->data_ptr();
+  }
+  ln_set_stamps(p);
+}
+
 int64_t attn_keep_words_op(int64_t B, int64_t H, int64_t N, int64_t hd) {
   return attn_keep_words((int)B, (int)H, (int)N, (int)hd);
 }
@@ -1123,6 +1132,7 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("attn_fwd(Tensor qkv, float scale, Tensor rng, int site, float p, Tensor? keep_out=None) -> (Tensor, Tensor)");
   m.def("attn_keep_words(int B, int H, int N, int hd) -> int", &attn_keep_words_op);
   m.def("attn_stamps(Tensor? buf) -> ()", &attn_stamps);
+  m.def("ln_stamps(Tensor? buf) -> ()", &ln_stamps);
   m.def("qkv_attn_fwd(Tensor a, Tensor w, Tensor b, Tensor? ln_st, Tensor? ln_c, float ln_eps, int B, int N, int H, "
         "float scale, Tensor rng, int site, float p, bool save_qkv, Tensor(a!)? ln_mean=None, "
         "Tensor(b!)? ln_rstd=None) -> (Tensor, Tensor, Tensor)");

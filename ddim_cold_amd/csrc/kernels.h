@@ -160,7 +160,8 @@ void replica_reduce_launch(float* ws, float* const* dsts_dev, int G, int C, hipS
 // the short-sequence forward and read by its backward instead of re-hashing
 // (ignored by the long-sequence kernels, which always regenerate)
 int64_t attn_keep_words(int B, int H, int N, int hd);
-void attn_set_stamps(void* buf);  // profiling: [grid][4] phase stamps of the short backward (nullptr: off)
+void attn_set_stamps(void* buf);
+void ln_set_stamps(void* buf);  // profiling: [grid][5] phase stamps of the LayerNorm backward (nullptr: off)  // profiling: [grid][4] phase stamps of the short backward (nullptr: off)
 void attn_fwd_launch(const void* qkv, void* o, float* lse, int B, int H, int N, int hd, float scale,
                      const int64_t* rng, int site, double p, hipStream_t stream, uint32_t* keep_bits = nullptr);
 void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const float* lse, void* dqkv,
