@@ -82,29 +82,67 @@ def _pools(cfg: ExperimentConfig, device, rank: int):
     return tr.float_pool(), va.float_pool()
 
 
+def _eval_batch(prog, P, src, eval_rng, total):
+    """One validation batch: draw, eval-mode forward, smooth-L1 added to ``total`` (device)."""
+    c = prog.cfg
+    x_t, target, t = src()
+    out, _ = prog.forward(P, x_t, t, eval_rng, False, save=False)
+    if out.is_cuda:
+        loss, _ = ops.smooth_l1_fwd_bwd(out, target, c.tokens, c.patch, 1.0)
+    else:
+        loss = torch.nn.functional.smooth_l1_loss(out, target).reshape(1)
+    total += loss.double()
+    eval_rng[1:].add_(1)
+
+
 @torch.no_grad()
 def evaluate(model, engine: TrainEngine, pool: torch.Tensor, idx: torch.Tensor, batch: int, kind: str,
              total_steps: int, eval_rng: torch.Tensor) -> float:
-    """Mean per-batch smooth-L1 over ``pool[idx]`` in eval mode (multi_gpu_trainer.py:32-45)."""
+    """Mean per-batch smooth-L1 over ``pool[idx]`` in eval mode (multi_gpu_trainer.py:32-45).
+
+    On a GPU every full batch is one replay of a captured graph (batch draw from a
+    static index buffer, forward, loss accumulated on the device; captured once per
+    (pool, batch, kind) and kept on the engine); a ragged last batch runs eagerly.
+    One host sync at the end."""
     prog = engine.prog
-    c = prog.cfg
     P = engine.param_tensors
     dev = pool.device
     total = torch.zeros(1, dtype=torch.float64, device=dev)
     nb = 0
-    for s in range(0, idx.numel(), batch):
-        bidx = idx[s:s + batch].to(dev)
-        B = bidx.numel()
-        src = make_batcher(kind, pool, B, eval_rng, total_steps, idx=bidx)
-        x_t, target, t = src()
-        out, _ = prog.forward(P, x_t, t, eval_rng, False, save=False)
-        if dev.type == "cuda":
-            loss, _ = ops.smooth_l1_fwd_bwd(out, target, c.tokens, c.patch, 1.0)
-        else:
-            loss = torch.nn.functional.smooth_l1_loss(out, target).reshape(1)
-        total += loss.double()
+    n_full = idx.numel() // batch if (dev.type == "cuda" and engine.cfg.use_graph) else 0
+    if n_full:
+        key = (pool.data_ptr(), batch, kind, total_steps, eval_rng.data_ptr())
+        cache = engine.__dict__.setdefault("_eval_graphs", {})
+        ent = cache.get(key)
+        if ent is None:
+            from ..utils.observe import no_gc
+            bidx = torch.zeros(batch, dtype=torch.int64, device=dev)
+            acc = torch.zeros(1, dtype=torch.float64, device=dev)
+            src = make_batcher(kind, pool, batch, eval_rng, total_steps, idx=bidx)
+            saved = eval_rng.clone()
+            bidx.copy_(idx[:batch].to(dev))
+            s = torch.cuda.Stream(device=dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):  # warm-up (allocator, kernels)
+                _eval_batch(prog, P, src, eval_rng, acc)
+            torch.cuda.current_stream(dev).wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with no_gc(), torch.cuda.graph(g):
+                _eval_batch(prog, P, src, eval_rng, acc)
+            eval_rng.copy_(saved)  # warm-up and capture leave the counters where they were
+            ent = cache[key] = (g, bidx, acc)
+        g, bidx, acc = ent
+        acc.zero_()
+        for b in range(n_full):
+            bidx.copy_(idx[b * batch:(b + 1) * batch].to(dev), non_blocking=True)
+            g.replay()
+        total += acc
+        nb = n_full
+    for s in range(n_full * batch, idx.numel(), batch):
+        bidx_e = idx[s:s + batch].to(dev)
+        src = make_batcher(kind, pool, bidx_e.numel(), eval_rng, total_steps, idx=bidx_e)
+        _eval_batch(prog, P, src, eval_rng, total)
         nb += 1
-        eval_rng[1] += 1
     return float(total.item()) / max(nb, 1)
 
 

@@ -158,3 +158,26 @@ def test_gradient_overwrite_matches_accumulate(monkeypatch):
     assert eng.flat_g[:eng.acc_hi].abs().max() == 0
     assert all(abs(a - b) <= 1e-4 * abs(b) for a, b in zip(lo, la)), (lo, la)
     assert (po - pa).abs().max().item() <= 2 * 1e-3 * 5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["cold", "gaussian"])
+def test_graph_evaluate_matches_eager(kind):
+    """trainer.evaluate: full validation batches replayed from a captured graph (index buffer,
+    batch draw, forward, device loss sum) == the eager loop; ragged tail batch eager."""
+    from ddim_cold_amd.train.trainer import evaluate
+    torch.manual_seed(0)
+    model = build_model("vit_tiny").cuda().train()
+    pool = synthetic_pool(40, seed=4, device="cuda")
+    idx = torch.randperm(40)[:37]
+    vals = []
+    for use_graph in (True, False):
+        eng = TrainEngine(model, EngineConfig(use_graph=use_graph, temb_rows=7))
+        rng = torch.tensor([123, 0], dtype=torch.int64, device="cuda")
+        v1 = evaluate(model, eng, pool, idx, 8, kind, 2000, rng)
+        v2 = evaluate(model, eng, pool, idx, 8, kind, 2000, rng)  # second call replays the cached graph
+        assert int(rng[1]) == 2 * 5
+        vals.append((v1, v2))
+        eng.detach()
+    (g1, g2), (e1, e2) = vals
+    assert abs(g1 - e1) <= 1e-6 * abs(e1) and abs(g2 - e2) <= 1e-6 * abs(e2), vals
