@@ -148,9 +148,57 @@ void comm_destroy(int64_t h) {
   g_comms[h] = nullptr;
 }
 
+// ---- external graph events (the engine's event-split step, engine.py comm_events)
+// A compute graph records one event per gradient bucket as an event-record node
+// appended to the capture by hand (hipGraphAddEventRecordNode on the capturing
+// stream's current dependencies, which then become that node): the graph stays a
+// single chain, and the host-issued collectives on the comm stream wait on those
+// events after the replay is enqueued.  (torch.cuda.Event(external=True) is refused
+// on ROCm builds, and hipEventRecordWithFlags(.., hipEventRecordExternal) returns
+// invalid-argument inside a capture on this runtime.)
+#define HIP_CHECK(cmd)                                                                   \
+  do {                                                                                   \
+    hipError_t e_ = (cmd);                                                               \
+    TORCH_CHECK(e_ == hipSuccess, "HIP error ", hipGetErrorString(e_), " at ", #cmd);    \
+  } while (0)
+
+int64_t event_create() {
+  hipEvent_t ev;
+  HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  return reinterpret_cast<int64_t>(ev);
+}
+
+void event_record_external(int64_t ev) {
+  hipStream_t s = c10::hip::getCurrentHIPStream().stream();
+  hipEvent_t e = reinterpret_cast<hipEvent_t>(ev);
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  hipGraph_t g = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t nd = 0;
+  HIP_CHECK(hipStreamGetCaptureInfo_v2(s, &st, nullptr, &g, &deps, &nd));
+  if (st != hipStreamCaptureStatusActive) {
+    HIP_CHECK(hipEventRecord(e, s));
+    return;
+  }
+  std::vector<hipGraphNode_t> dv(deps, deps + nd);
+  hipGraphNode_t node;
+  HIP_CHECK(hipGraphAddEventRecordNode(&node, g, dv.data(), dv.size(), e));
+  HIP_CHECK(hipStreamUpdateCaptureDependencies(s, &node, 1, hipStreamSetCaptureDependencies));
+}
+
+void stream_wait_event(int64_t ev) {
+  HIP_CHECK(hipStreamWaitEvent(c10::hip::getCurrentHIPStream().stream(), reinterpret_cast<hipEvent_t>(ev), 0));
+}
+
+void event_destroy(int64_t ev) { HIP_CHECK(hipEventDestroy(reinterpret_cast<hipEvent_t>(ev))); }
+
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(ddim_cold, m) {
+  m.def("event_create() -> int", &event_create);
+  m.def("event_record_external(int event) -> ()", &event_record_external);
+  m.def("stream_wait_event(int event) -> ()", &stream_wait_event);
+  m.def("event_destroy(int event) -> ()", &event_destroy);
   m.def("comm_unique_id() -> Tensor", &comm_unique_id);
   m.def("comm_init(Tensor uid, int world, int rank, int device) -> int", &comm_init);
   m.def("comm_all_reduce_(Tensor(a!) buf, int handle, int op=0) -> ()", &comm_all_reduce_);

@@ -30,6 +30,34 @@ def _store():
     return dist.distributed_c10d._get_default_store()
 
 
+class ExternalEvent:
+    """A HIP event recorded as an external event-record node when captured: the
+    capturing graph keeps a single chain (no cross-stream branch), and a stream
+    that waits on the event after the graph's replay is enqueued orders after that
+    point of the replay (``csrc/comm.cpp`` event_*)."""
+
+    def __init__(self):
+        _ext.load(raise_on_error=True)
+        self.handle = int(torch.ops.ddim_cold.event_create())
+
+    def record(self):
+        """Record on the current stream (inside a capture: an external node)."""
+        torch.ops.ddim_cold.event_record_external(self.handle)
+
+    def wait(self, stream: torch.cuda.Stream):
+        with torch.cuda.stream(stream):
+            torch.ops.ddim_cold.stream_wait_event(self.handle)
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None:
+            try:
+                torch.ops.ddim_cold.event_destroy(h)
+            except Exception:  # interpreter shutdown
+                pass
+            self.handle = None
+
+
 class NativeComm:
     """One RCCL communicator over the ranks of the default process group."""
 

@@ -99,6 +99,16 @@ class EngineConfig:
     # 1.125 segmented (each extra graph launch + stream join costs ~30 us).
     # Falls back to segments if the capture raises.
     graph_comm: bool = True
+    # data parallel, the preferred capture: the step's compute as TWO linear graphs
+    # (forward + backward, then optimizer) whose only cross-stream edges are
+    # external event-record nodes at the bucket boundaries; the collectives are
+    # issued by the host on the comm stream, each waiting on its bucket's event.
+    # A graph with a comm-stream branch (graph_comm) is executed by HIP over
+    # several hardware queues, and every kernel of it then pays a completion
+    # fence (~1.5-2 us each, ~100 kernels): measured on one MI355X with one pass
+    # per bucket standing in for the collective, 1.063 ms/step branched vs 0.870
+    # with the passes inline.  DDIM_COLD_COMM_EVENTS=0: graph_comm / segments.
+    comm_events: bool = os.environ.get("DDIM_COLD_COMM_EVENTS", "0") != "0"
     # micro-batches per optimizer step (batch_fn is called grad_accum times per
     # step; gradients accumulate in the arena, averaged in the optimizer; the
     # all-reduce runs once, after the last micro-batch's backward)
@@ -152,7 +162,8 @@ class TrainEngine:
         self.loss_last = torch.zeros(1, dtype=torch.float32, device=dev)
         self.loss_ema = torch.full((1,), cfg.ema_init, dtype=torch.float32, device=dev)
         self.side = torch.cuda.Stream(device=dev) if (self.is_cuda and cfg.wgrad_stream) else None
-        self.comm = torch.cuda.Stream(device=dev) if (self.is_cuda and self.segmented) else None
+        self.comm = torch.cuda.Stream(device=dev) if (self.is_cuda and self.segmented and
+                                                      os.environ.get("DDIM_COLD_COMM_INLINE") != "1") else None
         if cfg.comm not in ("torch", "native"):
             raise ValueError(f"comm must be 'torch' or 'native', got {cfg.comm!r}")
         self.ncomm = None
@@ -411,6 +422,17 @@ class TrainEngine:
                                              ln_ws=self.ln_ws, wgrad_stream=self.side, embed_with_block0=merge,
                                              ln_final=ln_final, wgrad_tail=tail_w, wgrad_flush=flush_at,
                                              wgrad_store=overwrite):
+                if (self.is_cuda and not self.segmented and i in self.bucket_after
+                        and os.environ.get("DDIM_COLD_DEBUG_FORK") == "1"):
+                    # experiment: the data-parallel graph's fork / join topology with a
+                    # tiny kernel on the side branch instead of a collective
+                    if getattr(self, "_dbg", None) is None:
+                        self._dbg = (torch.cuda.Stream(device=self.device),
+                                     torch.zeros(1, device=self.device))
+                    st_, buf_ = self._dbg
+                    st_.wait_stream(torch.cuda.current_stream(self.device))
+                    with torch.cuda.stream(st_):
+                        buf_.add_(1)
                 if i in self.bucket_after and (self.segmented or i == -1):
                     hi = self.ln_done_at[i]
                     if ln_final is not None:
@@ -426,6 +448,8 @@ class TrainEngine:
                         yield ("bucket", self.bucket_after[i])
             S = None
         self._join_side()  # all weight gradients final before the norm / optimizer
+        if getattr(self, "_dbg", None) is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._dbg[0])
         # optimizer: grads are SUM-reduced over ranks and summed over micro-batches
         # -> average via grad_scale
         gs = 1.0 / (self.world * k_acc)
@@ -448,14 +472,21 @@ class TrainEngine:
         self.prog._keep = None
         yield ("done", -1)
 
-    def _allreduce(self, k: int):
+    def _allreduce(self, k: int, after=None):
+        """Issue bucket ``k``'s collectives on the comm stream, ordered after the
+        current stream (or after the event ``after``: the bucket's boundary inside
+        the replayed compute graph)."""
         if not self.dist_on or (self.world <= 1 and not self.cfg.force_segments):
             return
         ranges = self.bucket_ranges[k]
 
+        fake = os.environ.get("DDIM_COLD_FAKE_COMM") == "1"
+
         def reduce():
             for a, b in ranges:
-                if self.ncomm is not None:
+                if fake:  # topology experiment at 1 rank: one pass over the range per bucket
+                    self.flat_g[a:b].mul_(1.0)
+                elif self.ncomm is not None:
                     if self.flat_gw is None:
                         self.ncomm.all_reduce_(self.flat_g[a:b])
                     else:
@@ -471,8 +502,11 @@ class TrainEngine:
                 self._temb_exchange()
 
         if self.comm is not None:
-            self.comm.wait_stream(torch.cuda.current_stream(self.device))
-            if self.side is not None:  # the bucket's weight gradients come from the side stream
+            if after is not None:
+                after.wait(self.comm)
+            else:
+                self.comm.wait_stream(torch.cuda.current_stream(self.device))
+            if self.side is not None and after is None:  # the bucket's weight gradients come from the side stream
                 self.comm.wait_stream(self.side)
             with torch.cuda.stream(self.comm):
                 reduce()
@@ -515,6 +549,9 @@ class TrainEngine:
                     self._join_comm()
 
     def _capture(self):
+        if self.segmented and self.cfg.comm_events and self.comm is not None:
+            self._capture_impl(graph_comm=False, events=True)
+            return
         if self.segmented and self.cfg.graph_comm and not getattr(self, "_graph_comm_failed", False):
             try:
                 self._capture_impl(graph_comm=True)
@@ -535,7 +572,7 @@ class TrainEngine:
                 if k == len(self.buckets) - 1:
                     self._join_comm()
 
-    def _capture_impl(self, graph_comm: bool):
+    def _capture_impl(self, graph_comm: bool, events: bool = False):
         from ..utils.observe import no_gc
         if self.dist_on and self.is_cuda:
             # let the eager collectives of the warm-up finish and the process-group
@@ -544,12 +581,41 @@ class TrainEngine:
             torch.cuda.synchronize(self.device)
             time.sleep(0.3)
         with no_gc():
-            self._capture_graphs(graph_comm)
+            if events:
+                self._capture_event_graphs()
+            else:
+                self._capture_graphs(graph_comm)
+
+    def _capture_event_graphs(self):
+        """Compute graph (forward + backward, an external event recorded at every
+        bucket boundary) + optimizer graph; see ``EngineConfig.comm_events``."""
+        pool = torch.cuda.graph_pool_handle()
+        nb = len(self.buckets)
+        self._multi = None
+        from ..parallel.comm import ExternalEvent
+        evs = [ExternalEvent() for _ in range(nb)]
+        gen = self._step_iter()
+        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        self._segment_capture = True  # side streams rejoin before each boundary
+        try:
+            with torch.cuda.graph(g1, pool=pool, capture_error_mode=CAPTURE_MODE):
+                for _ in range(nb):
+                    kind, k = next(gen)
+                    assert kind == "bucket", kind
+                    evs[k].record()
+            with torch.cuda.graph(g2, pool=pool, capture_error_mode=CAPTURE_MODE):
+                kind, _ = next(gen)
+                assert kind == "done", kind
+        finally:
+            self._segment_capture = False
+        self._graphs = [g1, g2]
+        self._events = evs
 
     def _capture_graphs(self, graph_comm: bool):
         pool = torch.cuda.graph_pool_handle()
         graphs = []
         self._multi = None
+        self._events = None
         gen = self._step_iter()
         nseg = len(self.buckets) + 1 if (self.segmented and not graph_comm) else 1
         if nseg == 1:
@@ -580,6 +646,14 @@ class TrainEngine:
         gs = self._graphs
         if len(gs) == 1:
             gs[0].replay()
+            return
+        evs = getattr(self, "_events", None)
+        if evs is not None and len(gs) == 2:
+            gs[0].replay()
+            for k, ev in enumerate(evs):
+                self._allreduce(k, after=ev)
+            self._join_comm()
+            gs[1].replay()
             return
         nb = len(self.buckets)
         for k in range(nb):

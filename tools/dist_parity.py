@@ -1,5 +1,6 @@
-"""1-rank RCCL group on one GPU: the distributed engine paths (captured collectives,
-segmented collectives) must reproduce the single-process engine.
+"""1-rank RCCL group on one GPU: the distributed engine paths (event-split graphs with
+host-issued collectives, collectives captured in the step graph, graph segments) must
+reproduce the single-process engine.
 
 Not bit for bit: the grouped weight-gradient GEMM combines its two token slices
 with fp32 atomics (order-dependent last bits), and AdamW turns a last-bit change
@@ -19,7 +20,8 @@ def run(dist_mode, comm="torch", wire="fp32", gauss=False):
     model = build_model("vit_tiny").cuda().train()
     cfg = EngineConfig(lr=1e-3, t_max=100, seed=5, temb_rows=None if gauss else 7,
                        force_segments=dist_mode is not None,
-                       graph_comm=dist_mode == "captured", graph_warmup=2, comm=comm, grad_wire=wire)
+                       graph_comm=dist_mode == "captured", comm_events=dist_mode == "events",
+                       graph_warmup=2, comm=comm, grad_wire=wire)
     eng = TrainEngine(model, cfg)
     pool = synthetic_pool(64, seed=3, device="cuda")
     # Gaussian diffusion (t over the whole table): sparse time_embed row exchange
@@ -65,7 +67,13 @@ if __name__ == "__main__":
     natb, loss4, failed4, ng4 = run("captured", comm="native", wire="bf16")
     gref, gl0, _, _ = run(None, gauss=True)
     gcap, gl1, gfailed, gng = run("captured", gauss=True)
+    # compute graphs split at external events, collectives host-issued on the comm stream
+    ev, loss5, _, ng5 = run("events")
+    evn, loss6, _, ng6 = run("events", comm="native")
+    gev, gl2, _, gng2 = run("events", gauss=True)
     dist.destroy_process_group()
+    assert ng5 == 2 and ng6 == 2 and gng2 == 2, (ng5, ng6, gng2)
+    assert (gref - gev).abs().max().item() <= 2 * 1e-3 * 6 and abs(gl2 - gl0) <= 1e-4 * abs(gl0), (gl0, gl2)
     assert not gfailed and gng == 1, "sparse time_embed exchange not captured"
     assert (gref - gcap).abs().max().item() <= 2 * 1e-3 * 6 and abs(gl1 - gl0) <= 1e-4 * abs(gl0), (gl0, gl1)
     print(f"losses {loss0:.6f} {loss1:.6f} {loss2:.6f} native {loss3:.6f} native-bf16 {loss4:.6f}; "
@@ -76,7 +84,7 @@ if __name__ == "__main__":
     # bf16 wire: a 1-rank all-reduce of the packed gradient is the bf16 rounding of it;
     # Adam's normalisation keeps the update within the same per-step bound
     for name, other, loss in (("captured", cap, loss1), ("segmented", seg, loss2), ("native", nat, loss3),
-                              ("native-bf16", natb, loss4)):
+                              ("native-bf16", natb, loss4), ("events", ev, loss5), ("events-native", evn, loss6)):
         d = (ref - other).abs().max().item()
         assert d <= bound, (name, d)
         tol = 1e-2 if name.endswith("bf16") else 1e-4
