@@ -65,10 +65,17 @@ def main():
                     help="init the RCCL process group and run segmented graphs + collectives even with 1 rank")
     ap.add_argument("--segmented-comm", action="store_true",
                     help="host-issued all-reduces between graph segments instead of capturing them in the step graph")
+    ap.add_argument("--captured-comm", action="store_true",
+                    help="capture the collectives in the step graph (a comm-stream branch) instead of issuing them "
+                         "from the host between the event-split step graphs (the default)")
     ap.add_argument("--grad-wire", default="fp32", choices=["fp32", "bf16"],
                     help="gradient all-reduce wire format (bf16 halves the xGMI bytes)")
     ap.add_argument("--comm", default="torch", choices=["torch", "native"],
                     help="gradient collectives through torch.distributed (RCCL) or the native RCCL communicator")
+    ap.add_argument("--comm-layout", default="auto",
+                    choices=["auto", "overlap-2", "overlap-4", "inline-1"],
+                    help="data parallel: gradient-exchange layout; auto = TrainEngine.autotune_comm() measures "
+                         "each on this job's ranks before the warmup (training state restored afterwards)")
     ap.add_argument("--sampler-k", type=int, default=20)
     ap.add_argument("--sampler-n", type=int, default=64)
     ap.add_argument("--sampler-host-noise", action="store_true",
@@ -101,11 +108,20 @@ def main():
                        wgrad_stream=args.wgrad_stream,
                        temb_rows=int(math.log2(model.img_size[1])) + 1,  # cold t in 1..log2(W)
                        graph_comm=not args.segmented_comm, grad_wire=args.grad_wire,
+                       comm_events=not (args.segmented_comm or args.captured_comm),
                        comm=args.comm, graph_steps=args.graph_steps)
     engine = TrainEngine(model, cfg, device=dev)
     pool = synthetic_pool(1024, tuple(model.img_size), seed=7 + rank, device=dev)
     engine.set_batch_fn(ColdBatcher(pool, args.batch, engine.rng))
 
+    if engine.segmented and dev.type == "cuda":
+        # outside the timed region; parameters / moments / counters / RNG restored
+        if args.comm_layout == "auto":
+            engine.autotune_comm()
+        else:
+            lay = {L[0]: L for L in engine.COMM_LAYOUTS}[args.comm_layout]
+            engine.set_comm_layout(lay[1], lay[2], lay[3])
+            engine.comm_choice = lay[0]
     engine.train_steps(args.warmup)
     if dev.type == "cuda":
         torch.cuda.synchronize()
@@ -181,9 +197,12 @@ def main():
                        "per_gpu_batch": args.batch, "seq_len": model.num_tokens, "parallelism": f"dp{n}",
                        "graph": not args.no_graph, "graph_steps": args.graph_steps, "bucket_blocks": args.bucket_blocks,
                        "allreduce": ("none" if not engine.segmented else "eager" if dev.type != "cuda" else
+                                     "host-issued-between-event-split-graphs" if engine.cfg.comm_events else
                                      "segmented" if (args.segmented_comm or getattr(engine, "_graph_comm_failed", False))
                                      else "captured-in-graph"),
                        "grad_wire": args.grad_wire, "comm": args.comm,
+                       "comm_layout": engine.comm_choice,
+                       "comm_layout_ms": {k: round(v, 4) for k, v in engine.comm_times.items()} or None,
                        "optimizer": "AdamW(wd=0.05)+clip1.0+cosine", "final_loss": round(loss, 5)},
         }
         out.update(extra)

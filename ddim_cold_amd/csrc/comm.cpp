@@ -162,9 +162,14 @@ void comm_destroy(int64_t h) {
     TORCH_CHECK(e_ == hipSuccess, "HIP error ", hipGetErrorString(e_), " at ", #cmd);    \
   } while (0)
 
-int64_t event_create() {
+// flags: extra hipEventCreateWithFlags bits on top of hipEventDisableTiming, e.g.
+// hipEventReleaseToDevice (device-scope release: visible to the comm queue of the
+// same GPU, which is all the bucket's collective needs) or hipEventDisableSystemFence
+// -- the default system-scope fence writes back AND invalidates the L2s, and the
+// compute kernels after it refill them.
+int64_t event_create(int64_t flags) {
   hipEvent_t ev;
-  HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming | static_cast<unsigned>(flags)));
   return reinterpret_cast<int64_t>(ev);
 }
 
@@ -195,7 +200,7 @@ void event_destroy(int64_t ev) { HIP_CHECK(hipEventDestroy(reinterpret_cast<hipE
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(ddim_cold, m) {
-  m.def("event_create() -> int", &event_create);
+  m.def("event_create(int flags=0) -> int", &event_create);
   m.def("event_record_external(int event) -> ()", &event_record_external);
   m.def("stream_wait_event(int event) -> ()", &stream_wait_event);
   m.def("event_destroy(int event) -> ()", &event_destroy);

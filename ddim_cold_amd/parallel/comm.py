@@ -36,9 +36,12 @@ class ExternalEvent:
     that waits on the event after the graph's replay is enqueued orders after that
     point of the replay (``csrc/comm.cpp`` event_*)."""
 
-    def __init__(self):
+    RELEASE_TO_DEVICE = 0x40000000     # hipEventReleaseToDevice
+    DISABLE_SYSTEM_FENCE = 0x20000000  # hipEventDisableSystemFence
+
+    def __init__(self, flags: int = 0):
         _ext.load(raise_on_error=True)
-        self.handle = int(torch.ops.ddim_cold.event_create())
+        self.handle = int(torch.ops.ddim_cold.event_create(int(flags)))
 
     def record(self):
         """Record on the current stream (inside a capture: an external node)."""

@@ -19,13 +19,19 @@ AdamW step, cosine LR step, zero_grad) re-designed for a latency-bound
   Data parallel: one such launch per gradient bucket, so each bucket's
   all-reduce can start while the remaining blocks run backward.  (Issuing them
   on a side stream, ``wgrad_stream=True``, measured slower.)
-* **One hipGraph per step, bucketed RCCL all-reduce inside it.**  Gradient
+* **hipGraphs per step, bucketed RCCL all-reduce between them.**  Gradient
   buckets are contiguous arena ranges closed at transformer-block boundaries
   of the backward; as soon as a bucket's gradients are final its
-  ``all_reduce`` (RCCL over xGMI via ``torch.distributed`` 'nccl') is issued on
+  ``all_reduce`` (RCCL over xGMI via ``torch.distributed`` 'nccl') runs on
   a communication stream, so it overlaps the backward of the remaining
-  blocks, and the optimizer waits on that stream.  The collectives are
-  captured into the same graph (``graph_comm``); the fallback replays
+  blocks, and the optimizer waits on that stream.  Data parallel default
+  (``comm_events``): forward + backward is ONE linear graph carrying an
+  external event-record node per bucket boundary, the optimizer a second; the
+  host issues each bucket's collective on the comm stream behind its event
+  between the two replays (a comm branch inside the graph costs ~30 us per
+  fork on MI355X).  ``autotune_comm()`` picks the bucket layout (or one
+  inline all-reduce) by measuring on the job's own ranks.  Alternatives:
+  collectives captured into the step graph (``graph_comm``) or
   ``n_buckets + 1`` graph segments with host-issued collectives in between.
   Buckets default to ~2 blocks (~7 MB fp32 for ViT-tiny): few enough
   collectives for the per-call latency of 7-link point-to-point xGMI rings,
@@ -99,16 +105,22 @@ class EngineConfig:
     # 1.125 segmented (each extra graph launch + stream join costs ~30 us).
     # Falls back to segments if the capture raises.
     graph_comm: bool = True
-    # data parallel, the preferred capture: the step's compute as TWO linear graphs
+    # data parallel, the default capture: the step's compute as TWO linear graphs
     # (forward + backward, then optimizer) whose only cross-stream edges are
     # external event-record nodes at the bucket boundaries; the collectives are
-    # issued by the host on the comm stream, each waiting on its bucket's event.
-    # A graph with a comm-stream branch (graph_comm) is executed by HIP over
-    # several hardware queues, and every kernel of it then pays a completion
-    # fence (~1.5-2 us each, ~100 kernels): measured on one MI355X with one pass
-    # per bucket standing in for the collective, 1.063 ms/step branched vs 0.870
-    # with the passes inline.  DDIM_COLD_COMM_EVENTS=0: graph_comm / segments.
-    comm_events: bool = os.environ.get("DDIM_COLD_COMM_EVENTS", "0") != "0"
+    # issued by the host on the comm stream (eager RCCL, nothing of it captured),
+    # each waiting on its bucket's event.  A graph with a comm-stream branch
+    # (graph_comm) costs ~30-35 us per fork on MI355X -- measured on one GPU with a
+    # 1-element kernel on a side stream at each of the 5 bucket boundaries: 0.818 ->
+    # 1.013 ms/step -- while the event-split graphs with one elementwise pass per
+    # bucket on the comm stream (standing in for the collective) run at 0.833
+    # (tools/gpu_fence.sh).  DDIM_COLD_COMM_EVENTS=0: graph_comm / segments.
+    comm_events: bool = os.environ.get("DDIM_COLD_COMM_EVENTS", "1") != "0"
+    # data parallel: issue the collectives on the compute stream (no comm stream, no
+    # overlap; with comm_events, host-issued between the two step graphs).  With one
+    # bucket this is the single-process step + one all-reduce of the whole arena;
+    # autotune_comm() measures it against the overlapped layouts on the real ranks.
+    comm_inline: bool = os.environ.get("DDIM_COLD_COMM_INLINE") == "1"
     # micro-batches per optimizer step (batch_fn is called grad_accum times per
     # step; gradients accumulate in the arena, averaged in the optimizer; the
     # all-reduce runs once, after the last micro-batch's backward)
@@ -163,7 +175,9 @@ class TrainEngine:
         self.loss_ema = torch.full((1,), cfg.ema_init, dtype=torch.float32, device=dev)
         self.side = torch.cuda.Stream(device=dev) if (self.is_cuda and cfg.wgrad_stream) else None
         self.comm = torch.cuda.Stream(device=dev) if (self.is_cuda and self.segmented and
-                                                      os.environ.get("DDIM_COLD_COMM_INLINE") != "1") else None
+                                                      not cfg.comm_inline) else None
+        self.comm_choice: Optional[str] = None  # autotune_comm() winner
+        self.comm_times: Dict[str, float] = {}
         if cfg.comm not in ("torch", "native"):
             raise ValueError(f"comm must be 'torch' or 'native', got {cfg.comm!r}")
         self.ncomm = None
@@ -254,12 +268,42 @@ class TrainEngine:
         self.grad_tensors: ModelTensors = collect(views_g, c.depth, c.dim)
         if not c.learn_temb:
             self.grad_tensors.temb = None
+        self._temb_t: List[torch.Tensor] = []
+        # gradient arena below this element is accumulated (embeddings: atomics in the
+        # embedding backward); above it every range has a single writer per step
+        self.acc_hi = min(self.offsets[n][0] for n in self.names if n.rsplit(".", 1)[0] in ln_prefixes)
+        # LayerNorm dgamma/dbeta replica workspace in backward order: final norm,
+        # then norm2, norm1 of blocks L-1 .. 0; destinations = grad-arena views
+        # (weight and bias of one LayerNorm are adjacent: one [2D] range).
+        D = c.dim
+        L = c.depth
+        order = ["norm"]
+        for i in range(L - 1, -1, -1):
+            order += [f"blocks.{i}.norm2", f"blocks.{i}.norm1"]
+        self.ln_order = order
+        dsts = []
+        for nm in order:
+            ow, _ = self.offsets[nm + ".weight"]
+            ob, _ = self.offsets[nm + ".bias"]
+            assert ob == ow + D, "LayerNorm weight/bias must be adjacent in the arena"
+            dsts.append(self.flat_g[ow:ow + 2 * D])
+        self.ln_dsts = dsts
+        self.ln_ws = torch.zeros(len(order), ops.LN_REPLICAS, 2 * D, dtype=torch.float32, device=dev)
+        self.ln_ptrs = torch.tensor([t.data_ptr() for t in dsts], dtype=torch.int64, device=dev) \
+            if dev.type == "cuda" else None
+        self._ln_prefixes = ln_prefixes
+        self._build_buckets()
+
+    def _build_buckets(self):
+        """All-reduce bucket layout from ``cfg.bucket_blocks`` / ``cfg.embed_bucket``
+        (re-run by :meth:`set_comm_layout`)."""
+        c = self.prog.cfg
         # all-reduce buckets: contiguous arena ranges, boundaries after block groups (backward order)
         L = c.depth
         # a block's arena range starts at its first Linear weight (LayerNorms live
         # with the embeddings, see the layout above)
         starts = [min(self.offsets[n][0] for n in self.names if n.startswith(f"blocks.{i}.")
-                      and n.rsplit(".", 1)[0] not in ln_prefixes) for i in range(L)]
+                      and n.rsplit(".", 1)[0] not in self._ln_prefixes) for i in range(L)]
         bb = max(1, self.cfg.bucket_blocks)
         self.bucket_after: Dict[int, int] = {}
         bounds = []
@@ -294,28 +338,6 @@ class TrainEngine:
                     self.temb_bucket = k
                     self.bucket_ranges[k] = [r for a2, b2 in self.bucket_ranges[k]
                                              for r in ((a2, min(b2, to)), (max(a2, to + tn), b2)) if r[1] > r[0]]
-        self._temb_t: List[torch.Tensor] = []
-        # gradient arena below this element is accumulated (embeddings: atomics in the
-        # embedding backward); above it every range has a single writer per step
-        self.acc_hi = min(self.offsets[n][0] for n in self.names if n.rsplit(".", 1)[0] in ln_prefixes)
-        # LayerNorm dgamma/dbeta replica workspace in backward order: final norm,
-        # then norm2, norm1 of blocks L-1 .. 0; destinations = grad-arena views
-        # (weight and bias of one LayerNorm are adjacent: one [2D] range).
-        D = c.dim
-        order = ["norm"]
-        for i in range(L - 1, -1, -1):
-            order += [f"blocks.{i}.norm2", f"blocks.{i}.norm1"]
-        self.ln_order = order
-        dsts = []
-        for nm in order:
-            ow, _ = self.offsets[nm + ".weight"]
-            ob, _ = self.offsets[nm + ".bias"]
-            assert ob == ow + D, "LayerNorm weight/bias must be adjacent in the arena"
-            dsts.append(self.flat_g[ow:ow + 2 * D])
-        self.ln_dsts = dsts
-        self.ln_ws = torch.zeros(len(order), ops.LN_REPLICAS, 2 * D, dtype=torch.float32, device=dev)
-        self.ln_ptrs = torch.tensor([t.data_ptr() for t in dsts], dtype=torch.int64, device=dev) \
-            if dev.type == "cuda" else None
         # LN index range finalised at each bucket boundary (backward order)
         self.ln_done_at = {}
         done = 1
@@ -323,7 +345,7 @@ class TrainEngine:
             done += 2
             if i in self.bucket_after:
                 self.ln_done_at[i] = done
-        self.ln_done_at[-1] = len(order)
+        self.ln_done_at[-1] = len(self.ln_order)
 
     def _refresh_shadow(self):
         self.flat_pb.copy_(self.flat_p.to(torch.bfloat16))
@@ -540,6 +562,84 @@ class TrainEngine:
         if self.comm is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.comm)
 
+    # ------------------------------------------------------------------ comm layout
+    # candidate gradient-exchange layouts for autotune_comm(): (name, bucket_blocks,
+    # embed_bucket, inline).  overlap-*: buckets of 2 / 4 blocks + the embeddings,
+    # all-reduced on the comm stream while the backward goes on; inline-1: ONE
+    # all-reduce of the whole arena on the compute stream after the backward (no
+    # second queue: the single-process step + the collective).  With comm_events
+    # (default) no candidate captures a collective: they are host-issued between
+    # the step's two graphs.
+    COMM_LAYOUTS = (("overlap-2", 2, True, False), ("overlap-4", 4, True, False),
+                    ("inline-1", 1 << 16, False, True))
+
+    def set_comm_layout(self, bucket_blocks: Optional[int] = None, embed_bucket: Optional[bool] = None,
+                        inline: Optional[bool] = None):
+        """Re-bucket the gradient all-reduce and choose where its collectives run (a
+        comm-stream branch overlapping the backward, or inline on the compute
+        stream).  The step graphs are dropped and re-captured after
+        ``graph_warmup`` eager steps of the new layout."""
+        import dataclasses
+        kw = {}
+        if bucket_blocks is not None:
+            kw["bucket_blocks"] = int(bucket_blocks)
+        if embed_bucket is not None:
+            kw["embed_bucket"] = bool(embed_bucket)
+        if inline is not None:
+            kw["comm_inline"] = bool(inline)
+        if self.is_cuda:
+            torch.cuda.synchronize(self.device)
+        self.cfg = dataclasses.replace(self.cfg, **kw)
+        self._build_buckets()
+        if self.is_cuda and self.segmented:
+            self.comm = None if self.cfg.comm_inline else (self.comm or torch.cuda.Stream(device=self.device))
+        self._graphs = None
+        self._multi = None
+        self._events = None
+        self._eager_steps = 0
+
+    def _snapshot_state(self):
+        keys = ("flat_p", "flat_g", "flat_m", "flat_v", "rng", "step_ctr", "loss_ema", "loss_last")
+        return {k: getattr(self, k).clone() for k in keys}, self.steps_done
+
+    def _restore_state(self, snap):
+        tensors, steps = snap
+        for k, v in tensors.items():
+            getattr(self, k).copy_(v)
+        self.steps_done = steps
+        self._refresh_shadow()
+
+    def autotune_comm(self, steps: int = 40, warm: int = 6, layouts=None):
+        """Pick the gradient-exchange layout by measuring it on THIS job's ranks.
+
+        Every layout of ``layouts`` (default :attr:`COMM_LAYOUTS`) runs ``warm``
+        untimed then ``steps`` timed optimizer steps; the time is the max over ranks
+        (one all-reduce, so every rank takes the same decision) and the fastest
+        layout is kept.  Parameters, Adam moments, counters, RNG and loss EMA are
+        restored afterwards: the tuning steps leave no trace in the training state.
+        Returns ``{name: ms_per_step}`` (empty when not data parallel on a GPU)."""
+        if not (self.segmented and self.is_cuda and self.dist_on):
+            return {}
+        import time
+        from ..parallel.dist import all_reduce_max, barrier
+        layouts = list(layouts or self.COMM_LAYOUTS)
+        snap = self._snapshot_state()
+        times: Dict[str, float] = {}
+        for name, bb, eb, inline in layouts:
+            self.set_comm_layout(bb, eb, inline)
+            self.train_steps(warm + self.cfg.graph_warmup)
+            torch.cuda.synchronize(self.device)
+            barrier()
+            t0 = time.perf_counter()
+            self.train_steps(steps)
+            torch.cuda.synchronize(self.device)
+            times[name] = all_reduce_max(time.perf_counter() - t0, self.device) / steps * 1e3
+        best = min(layouts, key=lambda L_: times[L_[0]])
+        self._restore_state(snap)
+        self.set_comm_layout(best[1], best[2], best[3])
+        self.comm_choice, self.comm_times = best[0], times
+        return times
+
     def _run_eager(self):
         gen = self._step_iter()
         for kind, k in gen:
@@ -549,7 +649,7 @@ class TrainEngine:
                     self._join_comm()
 
     def _capture(self):
-        if self.segmented and self.cfg.comm_events and self.comm is not None:
+        if self.segmented and self.cfg.comm_events:
             self._capture_impl(graph_comm=False, events=True)
             return
         if self.segmented and self.cfg.graph_comm and not getattr(self, "_graph_comm_failed", False):
@@ -593,7 +693,10 @@ class TrainEngine:
         nb = len(self.buckets)
         self._multi = None
         from ..parallel.comm import ExternalEvent
-        evs = [ExternalEvent() for _ in range(nb)]
+        # release scope of the boundary events (DDIM_COLD_EVENT_FLAGS: extra
+        # hipEventCreateWithFlags bits, e.g. 0x40000000 = device-scope release)
+        flags = int(os.environ.get("DDIM_COLD_EVENT_FLAGS", "0"), 0)
+        evs = [ExternalEvent(flags) for _ in range(nb)]
         gen = self._step_iter()
         g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         self._segment_capture = True  # side streams rejoin before each boundary
@@ -650,7 +753,7 @@ class TrainEngine:
         evs = getattr(self, "_events", None)
         if evs is not None and len(gs) == 2:
             gs[0].replay()
-            for k, ev in enumerate(evs):
+            for k, ev in enumerate(evs):  # comm stream: waits on the bucket's event; inline: after gs[0]
                 self._allreduce(k, after=ev)
             self._join_comm()
             gs[1].replay()

@@ -272,3 +272,49 @@ def test_engine_fused_cold_batch_matches_unfused_cpu():
     pu, lu, _, tu, yu = run(False)
     assert nf == 3  # the fused path really ran
     assert lf == lu and torch.equal(pf, pu) and torch.equal(tf, tu) and torch.equal(yf, yu)
+
+
+def _layout_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        eng = TrainEngine(_model(drop=False, seed=rank), EngineConfig(lr=1e-3, temb_rows=7), device="cpu")
+        x, y, t = _batch(4, seed=5)
+        t = t % 6 + 1
+        b = 4 // world
+        xb, yb, tb = x[rank * b:(rank + 1) * b], y[rank * b:(rank + 1) * b], t[rank * b:(rank + 1) * b]
+        snap = eng._snapshot_state()
+        res = {}
+        for name, bb, eb, inline in eng.COMM_LAYOUTS:
+            eng.set_comm_layout(bb, eb, inline)
+            cover = sorted(eng.buckets)  # buckets tile the arena for every layout
+            assert cover[0][0] == 0 and cover[-1][1] == eng.numel
+            assert all(a[1] == c[0] for a, c in zip(cover, cover[1:]))
+            if name == "inline-1":
+                assert len(eng.buckets) == 1 and eng.comm is None
+            eng.step(xb, yb, tb)
+            eng.step(xb, yb, tb)
+            res[name] = (eng.flat_p.clone(), eng.flat_m.clone(), eng.loss_ema.clone())
+            eng._restore_state(snap)
+        assert eng.autotune_comm() == {}  # CPU: nothing to tune
+        if rank == 0:
+            torch.save({k: list(v) for k, v in res.items()} | {"p0": snap[0]["flat_p"], "p_end": eng.flat_p.clone()},
+                       out_path)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_comm_layouts_same_training_gloo():
+    """Every gradient-exchange layout autotune_comm() chooses from (2- / 4-block buckets
+    overlapped, one inline bucket) gives the same two training steps over 2 gloo ranks,
+    and the snapshot / restore around the tuning steps leaves the state untouched."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "r.pt")
+        mp.start_processes(_layout_worker, args=(2, free_port(), out), nprocs=2, join=True, start_method="spawn")
+        r = torch.load(out, weights_only=True)
+    assert torch.equal(r["p0"], r["p_end"])
+    base = r["overlap-2"]
+    assert not torch.equal(base[0], r["p0"])
+    for name in ("overlap-4", "inline-1"):
+        for a, b in zip(base, r[name]):
+            assert torch.equal(a, b), name

@@ -15,7 +15,7 @@ from ddim_cold_amd.train.engine import EngineConfig, TrainEngine
 from ddim_cold_amd.data.synthetic import ColdBatcher, GaussianBatcher, synthetic_pool
 
 
-def run(dist_mode, comm="torch", wire="fp32", gauss=False):
+def run(dist_mode, comm="torch", wire="fp32", gauss=False, tune=False, layout=None):
     torch.manual_seed(0)
     model = build_model("vit_tiny").cuda().train()
     cfg = EngineConfig(lr=1e-3, t_max=100, seed=5, temb_rows=None if gauss else 7,
@@ -27,6 +27,13 @@ def run(dist_mode, comm="torch", wire="fp32", gauss=False):
     # Gaussian diffusion (t over the whole table): sparse time_embed row exchange
     eng.set_batch_fn(GaussianBatcher(pool, 16, eng.rng, 2000) if gauss else ColdBatcher(pool, 16, eng.rng))
     assert (eng.temb_bucket is not None) == (gauss and dist_mode is not None)
+    if layout is not None:
+        L = {l[0]: l for l in eng.COMM_LAYOUTS}[layout]
+        eng.set_comm_layout(L[1], L[2], L[3])
+    if tune:  # measures every layout, then restores the training state
+        times = eng.autotune_comm(steps=4, warm=1)
+        assert set(times) == {l[0] for l in eng.COMM_LAYOUTS} and eng.comm_choice in times, times
+        assert eng.steps_done == 0 and int(eng.step_ctr[0]) == 0 and int(eng.rng[1]) == 0
     for _ in range(6):
         eng.train_step()
     torch.cuda.synchronize()
@@ -71,6 +78,9 @@ if __name__ == "__main__":
     ev, loss5, _, ng5 = run("events")
     evn, loss6, _, ng6 = run("events", comm="native")
     gev, gl2, _, gng2 = run("events", gauss=True)
+    # one inline all-reduce between the graphs; the autotuned layout after its tuning steps
+    evi, loss7, _, ng7 = run("events", layout="inline-1")
+    evt, loss8, _, ng8 = run("events", tune=True)
     dist.destroy_process_group()
     assert ng5 == 2 and ng6 == 2 and gng2 == 2, (ng5, ng6, gng2)
     assert (gref - gev).abs().max().item() <= 2 * 1e-3 * 6 and abs(gl2 - gl0) <= 1e-4 * abs(gl0), (gl0, gl2)
@@ -84,7 +94,8 @@ if __name__ == "__main__":
     # bf16 wire: a 1-rank all-reduce of the packed gradient is the bf16 rounding of it;
     # Adam's normalisation keeps the update within the same per-step bound
     for name, other, loss in (("captured", cap, loss1), ("segmented", seg, loss2), ("native", nat, loss3),
-                              ("native-bf16", natb, loss4), ("events", ev, loss5), ("events-native", evn, loss6)):
+                              ("native-bf16", natb, loss4), ("events", ev, loss5), ("events-native", evn, loss6),
+                              ("events-inline", evi, loss7), ("events-autotuned", evt, loss8)):
         d = (ref - other).abs().max().item()
         assert d <= bound, (name, d)
         tol = 1e-2 if name.endswith("bf16") else 1e-4
