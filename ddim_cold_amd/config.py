@@ -31,7 +31,9 @@ Optional extension keys (defaults reproduce the reference behaviour):
 ``dataset`` ('cold' | 'cold_x0' | 'gaussian'), ``synthetic`` (bool: on-device
 synthetic images instead of folders), ``synthetic_size``, ``seed``,
 ``graph`` (hipGraph capture), ``bucket_blocks`` (all-reduce bucket size in
-transformer blocks), ``total_steps`` (DDIM T, default 2000), ``num_workers``,
+transformer blocks), ``comm_autotune`` (data parallel on GPUs: time the bucket
+layouts on the job's ranks before training and keep the fastest, state
+restored; overrides ``bucket_blocks``), ``total_steps`` (DDIM T, default 2000), ``num_workers``,
 ``eval_every`` (epochs), ``log_every`` (steps, default 100), ``ckpt_dir``,
 ``timestep_embedding`` ('learned' | 'sinusoidal'), ``max_steps`` (cap per epoch,
 for smoke runs).
@@ -69,6 +71,7 @@ class ExperimentConfig:
     seed: int = 42
     graph: bool = True
     bucket_blocks: int = 2
+    comm_autotune: bool = True
     total_steps: int = 2000
     num_workers: int = 8
     eval_every: int = 1

@@ -214,6 +214,11 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
             printLog(f"resuming from epoch {start_epoch:8d} of " + cfg.resume, paths.log)
             printLog(f"recovering best_loss {best_loss:4f}", paths.log)
     engine.loss_ema.fill_(loss_rec)
+    if cfg.comm_autotune and engine.segmented and device.type == "cuda":
+        times = engine.autotune_comm()  # training state restored afterwards
+        if rank == 0 and times:
+            printLog(f"# comm layout: {engine.comm_choice} " +
+                     " ".join(f"{k}={v:.4f}ms" for k, v in times.items()), paths.log)
     check_param_sync(engine.flat_p, step=steps)  # replicas start identical
     writer = ScalarWriter(paths.ckpt_dir, enabled=(rank == 0))
     clock = StepClock(device)
