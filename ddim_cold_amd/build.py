@@ -52,6 +52,8 @@ def _flags(inc, abi, resource_usage=False):
     # per-kernel resource remarks (codegen unchanged): the build checks them for
     # scratch memory, see _check_scratch
     f.append("-Rpass-analysis=kernel-resource-usage")
+    # DDIM_COLD_HIPFLAGS: extra hipcc flags, e.g. "-DDDIM_COLD_LN_STAMPS=1" (profiling builds)
+    f += os.environ.get("DDIM_COLD_HIPFLAGS", "").split()
     for d in inc + [py_inc, CSRC, "/opt/rocm/include"]:
         f += ["-I", d]
     return f

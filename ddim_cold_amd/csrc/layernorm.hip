@@ -66,12 +66,21 @@ __global__ __launch_bounds__(NW * 64) void ln_fwd_kernel(const float* __restrict
   }
 }
 
-// profiling aid (tools/ub_lnbwd_stamps.py): when set, thread 0 of every LayerNorm
-// backward workgroup records s_memrealtime at its phase boundaries, [grid][5]
+// profiling aid (tools/ub_lnbwd_stamps.py, build with DDIM_COLD_LN_STAMPS=1): when
+// set, thread 0 of every LayerNorm backward workgroup records s_memrealtime at its
+// phase boundaries, [grid][5].  Compiled out by default: the pointer load and the
+// five tests cost the kernel time in the step profile.
+#ifndef DDIM_COLD_LN_STAMPS
+#define DDIM_COLD_LN_STAMPS 0
+#endif
 __device__ unsigned long long* g_ln_stamps = nullptr;
 __device__ __forceinline__ void ln_stamp(int k) {
+#if DDIM_COLD_LN_STAMPS
   unsigned long long* s = g_ln_stamps;
   if (s != nullptr && threadIdx.x == 0) s[(size_t)blockIdx.x * 5 + k] = __builtin_amdgcn_s_memrealtime();
+#else
+  (void)k;
+#endif
 }
 
 // DYB: dy (and its K-split partials) in bf16 -- the dgrad GEMMs write half the bytes

@@ -21,7 +21,9 @@ _LOCK = threading.Lock()
 _STATE = {"loaded": False, "error": None, "path": None}
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "_C.so")
+# DDIM_COLD_LIB: load another build of the extension (A/B runs of two builds of
+# the same tree, e.g. tools/gpu_lib_ab.sh); default the in-tree _C.so
+LIB_PATH = os.environ.get("DDIM_COLD_LIB") or os.path.join(PKG_DIR, "_C.so")
 
 
 class NativeExtensionError(RuntimeError):

@@ -15,6 +15,7 @@ if [ "${TRAIN:-1}" = "1" ]; then
   cp /tmp/ddc_train/Saved_Models/synthvit_tiny_synthetic/train.log gpurun_out/train_synth.log
 fi
 run bench 300 python bench.py
+run bench_dp1 300 python bench.py --force-dist --no-sampler --steps 1000 --warmup 50
 if [ "${PROF:-1}" = "1" ]; then
   export TMPDIR=/tmp
   rm -rf gpurun_out/prof_step gpurun_out/prof_sampler
