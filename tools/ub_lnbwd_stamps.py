@@ -1,7 +1,11 @@
 """Phase timeline of the LayerNorm backward (ViT-tiny training shape, bf16 dy, replica
 workspace, re-emitted LayerNorm output): thread 0 of every workgroup stamps
 s_memrealtime (100 MHz) at start / first row's loads landed / row stores issued / LDS
-column partials staged / replica atomics issued.  Medians over workgroups (ns)."""
+column partials staged / replica atomics issued.  Medians over workgroups (ns).
+
+Needs a stamps build (compiled out by default):
+    DDIM_COLD_HIPFLAGS=-DDDIM_COLD_LN_STAMPS=1 python -m ddim_cold_amd.build
+"""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
