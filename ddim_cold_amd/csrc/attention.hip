@@ -28,12 +28,21 @@ namespace dc {
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
-// profiling aid (tools/ub_attn_stamps.py): when set, wave 0 of every short-backward
-// workgroup records s_memrealtime (100 MHz) at its phase boundaries, [grid][4]
+// profiling aid (tools/ub_attn_stamps.py, build with DDIM_COLD_ATTN_STAMPS=1): when
+// set, wave 0 of every short-backward workgroup records s_memrealtime (100 MHz) at
+// its phase boundaries, [grid][4].  Compiled out by default (cf. the LayerNorm
+// backward's stamps: 2.2 us per launch in the step profile).
+#ifndef DDIM_COLD_ATTN_STAMPS
+#define DDIM_COLD_ATTN_STAMPS 0
+#endif
 __device__ unsigned long long* g_attn_stamps = nullptr;
 __device__ __forceinline__ void attn_stamp(int k) {
+#if DDIM_COLD_ATTN_STAMPS
   unsigned long long* s = g_attn_stamps;
   if (s != nullptr && threadIdx.x == 0) s[(size_t)blockIdx.x * 4 + k] = __builtin_amdgcn_s_memrealtime();
+#else
+  (void)k;
+#endif
 }
 
 template <int HD>

@@ -1,6 +1,9 @@
 """Phase timeline of the short attention backward (ViT-tiny training shape): wave 0 of
 every workgroup stamps s_memrealtime (100 MHz) at start / after the loads+LDS images /
-after the query phase / at the end.  Prints medians over workgroups (ns)."""
+after the query phase / at the end.  Prints medians over workgroups (ns).
+Needs a stamps build (compiled out by default):
+    DDIM_COLD_HIPFLAGS=-DDDIM_COLD_ATTN_STAMPS=1 python -m ddim_cold_amd.build
+"""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
