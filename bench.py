@@ -70,8 +70,9 @@ def main():
                          "from the host between the event-split step graphs (the default)")
     ap.add_argument("--grad-wire", default="fp32", choices=["fp32", "bf16"],
                     help="gradient all-reduce wire format (bf16 halves the xGMI bytes)")
-    ap.add_argument("--comm", default="torch", choices=["torch", "native"],
-                    help="gradient collectives through torch.distributed (RCCL) or the native RCCL communicator")
+    ap.add_argument("--comm", default="auto", choices=["auto", "torch", "native"],
+                    help="gradient collectives through torch.distributed (RCCL) or the native RCCL communicator "
+                         "(auto: native if it comes up and verifies on every rank)")
     ap.add_argument("--comm-layout", default="auto",
                     choices=["auto", "overlap-2", "overlap-4", "inline-1"],
                     help="data parallel: gradient-exchange layout; auto = TrainEngine.autotune_comm() measures "
@@ -200,13 +201,15 @@ def main():
                                      "host-issued-between-event-split-graphs" if engine.cfg.comm_events else
                                      "segmented" if (args.segmented_comm or getattr(engine, "_graph_comm_failed", False))
                                      else "captured-in-graph"),
-                       "grad_wire": args.grad_wire, "comm": args.comm,
+                       "grad_wire": args.grad_wire,
+                       "comm": engine.comm_backend if engine.segmented else "none",
                        "comm_layout": engine.comm_choice,
                        "comm_layout_ms": {k: round(v, 4) for k, v in engine.comm_times.items()} or None,
                        "optimizer": "AdamW(wd=0.05)+clip1.0+cosine", "final_loss": round(loss, 5)},
         }
         out.update(extra)
         print(json.dumps(out), flush=True)
+    engine.close()
     cleanup()
 
 

@@ -112,9 +112,9 @@ class EngineConfig:
     # each waiting on its bucket's event.  A graph with a comm-stream branch
     # (graph_comm) costs ~30-35 us per fork on MI355X -- measured on one GPU with a
     # 1-element kernel on a side stream at each of the 5 bucket boundaries: 0.818 ->
-    # 1.013 ms/step -- while the event-split graphs with one elementwise pass per
-    # bucket on the comm stream (standing in for the collective) run at 0.833
-    # (tools/gpu_fence.sh).  DDIM_COLD_COMM_EVENTS=0: graph_comm / segments.
+    # 1.013 ms/step -- and with one elementwise pass per bucket on the comm stream
+    # (standing in for the collective) the event-split step runs at 0.937 vs 1.072
+    # captured (tools/gpu_events.sh).  DDIM_COLD_COMM_EVENTS=0: graph_comm / segments.
     comm_events: bool = os.environ.get("DDIM_COLD_COMM_EVENTS", "1") != "0"
     # data parallel: issue the collectives on the compute stream (no comm stream, no
     # overlap; with comm_events, host-issued between the two step graphs).  With one
@@ -133,7 +133,9 @@ class EngineConfig:
     # ncclComm_t, collectives enqueued directly on the comm stream, bf16 wire
     # pack/unpack as two fused kernels).  torch.distributed stays the control
     # plane (rendezvous, barriers, metrics) either way.
-    comm: str = "torch"
+    # "auto" (default): native when it initialises and verifies on every rank of the
+    # default group (GPU), else torch
+    comm: str = "auto"
     # a batch source with ``fused_spec()`` (data.synthetic.ColdBatcher) has its draw
     # fused into the patch-embedding launch (ops.patch_embed_cold_fwd: the patch rows
     # pixelated straight from the pool, x_t never materialised): one launch fewer
@@ -178,14 +180,18 @@ class TrainEngine:
                                                       not cfg.comm_inline) else None
         self.comm_choice: Optional[str] = None  # autotune_comm() winner
         self.comm_times: Dict[str, float] = {}
-        if cfg.comm not in ("torch", "native"):
-            raise ValueError(f"comm must be 'torch' or 'native', got {cfg.comm!r}")
+        if cfg.comm not in ("torch", "native", "auto"):
+            raise ValueError(f"comm must be 'torch', 'native' or 'auto', got {cfg.comm!r}")
         self.ncomm = None
+        default_pg = process_group is None or process_group is dist.group.WORLD
         if cfg.comm == "native" and self.dist_on and self.is_cuda:
-            if process_group is not None and process_group is not dist.group.WORLD:
+            if not default_pg:
                 raise ValueError("comm='native' spans the default process group only")
             from ..parallel.comm import NativeComm
             self.ncomm = NativeComm(dev)
+        elif cfg.comm == "auto" and self.dist_on and self.is_cuda and default_pg:
+            self.ncomm = self._try_native(dev)
+        self.comm_backend = "native" if self.ncomm is not None else "torch"
         self._graphs: Optional[List[torch.cuda.CUDAGraph]] = None
         self._multi = None  # (K-step graph, K) for train_steps
         self._eager_steps = 0
@@ -200,6 +206,40 @@ class TrainEngine:
                 dist.broadcast(self.flat_p, src=0, group=self.pg)
             self._refresh_shadow()
         model._engine = self
+
+    def _try_native(self, dev):
+        """comm='auto': our own RCCL communicator if it comes up and sums correctly on
+        EVERY rank (agreed through the torch process group), else torch.distributed.
+        Its collectives are enqueued straight on the issuing stream; ProcessGroupNCCL
+        runs each on its internal stream behind an event round trip each way (1-rank
+        inline step: 0.849 vs 0.866 ms)."""
+        import warnings
+        nc, ok = None, 1
+        try:
+            from ..parallel.comm import NativeComm
+            nc = NativeComm(dev)
+            x = torch.full((4 * self.world + 3,), float(self.rank + 1), device=dev)
+            nc.all_reduce_(x)
+            torch.cuda.synchronize(dev)
+            ok = int(bool((x == self.world * (self.world + 1) / 2).all()))
+        except Exception as e:  # pragma: no cover - depends on the RCCL build
+            warnings.warn(f"native RCCL communicator unavailable ({e!r}); using torch.distributed")
+            ok = 0
+        flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.pg)
+        if int(flag.item()) == 1:
+            return nc
+        if nc is not None:
+            nc.destroy()
+        return None
+
+    def close(self):
+        """Release the native communicator (before the process group is destroyed)."""
+        if self.ncomm is not None:
+            if self.is_cuda:
+                torch.cuda.synchronize(self.device)
+            self.ncomm.destroy()
+            self.ncomm = None
 
     # ------------------------------------------------------------------ arenas
     def _build_arenas(self):

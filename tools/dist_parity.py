@@ -38,9 +38,9 @@ def run(dist_mode, comm="torch", wire="fp32", gauss=False, tune=False, layout=No
         eng.train_step()
     torch.cuda.synchronize()
     out = eng.flat_p.clone(), float(eng.loss_last), getattr(eng, "_graph_comm_failed", False), len(eng._graphs)
-    if comm == "native":
-        assert eng.ncomm is not None
-        eng.ncomm.destroy()
+    if comm in ("native", "auto"):  # auto: the native communicator came up and verified
+        assert eng.ncomm is not None and eng.comm_backend == "native"
+    eng.close()
     return out
 
 
@@ -81,6 +81,7 @@ if __name__ == "__main__":
     # one inline all-reduce between the graphs; the autotuned layout after its tuning steps
     evi, loss7, _, ng7 = run("events", layout="inline-1")
     evt, loss8, _, ng8 = run("events", tune=True)
+    eva, loss9, _, ng9 = run("events", comm="auto", tune=True)
     dist.destroy_process_group()
     assert ng5 == 2 and ng6 == 2 and gng2 == 2, (ng5, ng6, gng2)
     assert (gref - gev).abs().max().item() <= 2 * 1e-3 * 6 and abs(gl2 - gl0) <= 1e-4 * abs(gl0), (gl0, gl2)
@@ -95,7 +96,8 @@ if __name__ == "__main__":
     # Adam's normalisation keeps the update within the same per-step bound
     for name, other, loss in (("captured", cap, loss1), ("segmented", seg, loss2), ("native", nat, loss3),
                               ("native-bf16", natb, loss4), ("events", ev, loss5), ("events-native", evn, loss6),
-                              ("events-inline", evi, loss7), ("events-autotuned", evt, loss8)):
+                              ("events-inline", evi, loss7), ("events-autotuned", evt, loss8),
+                              ("events-auto-comm-autotuned", eva, loss9)):
         d = (ref - other).abs().max().item()
         assert d <= bound, (name, d)
         tol = 1e-2 if name.endswith("bf16") else 1e-4
