@@ -286,6 +286,7 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
     result = {"steps": steps, "loss_rec": loss_rec, "best_loss": best_loss, "history": history,
               "final_lr": engine.current_lr(), "rng": [int(v) for v in engine.rng.tolist()],
               "eval_rng": [int(v) for v in eval_rng.tolist()]}
+    engine.close()
     pdist.cleanup()
     return result
 
