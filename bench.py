@@ -196,7 +196,8 @@ def main():
                                 f"heads={model.blocks[0].attn.num_heads}, patch={model.patch_size}, "
                                 f"{model.img_size[0]}x{model.img_size[1]})", "global_batch": args.batch * n,
                        "per_gpu_batch": args.batch, "seq_len": model.num_tokens, "parallelism": f"dp{n}",
-                       "graph": not args.no_graph, "graph_steps": args.graph_steps, "bucket_blocks": args.bucket_blocks,
+                       "graph": not args.no_graph, "graph_steps": args.graph_steps,
+                       "bucket_blocks": engine.cfg.bucket_blocks if engine.segmented else None,
                        "allreduce": ("none" if not engine.segmented else "eager" if dev.type != "cuda" else
                                      "host-issued-between-event-split-graphs" if engine.cfg.comm_events else
                                      "segmented" if (args.segmented_comm or getattr(engine, "_graph_comm_failed", False))
