@@ -196,7 +196,9 @@ def main():
                                 f"heads={model.blocks[0].attn.num_heads}, patch={model.patch_size}, "
                                 f"{model.img_size[0]}x{model.img_size[1]})", "global_batch": args.batch * n,
                        "per_gpu_batch": args.batch, "seq_len": model.num_tokens, "parallelism": f"dp{n}",
-                       "graph": not args.no_graph, "graph_steps": args.graph_steps,
+                       "graph": not args.no_graph,
+                       # event-split data parallel: two graphs per step, collectives between
+                       "graph_steps": args.graph_steps if not (engine.segmented and engine.cfg.comm_events) else 1,
                        "bucket_blocks": engine.cfg.bucket_blocks if engine.segmented else None,
                        "allreduce": ("none" if not engine.segmented else "eager" if dev.type != "cuda" else
                                      "host-issued-between-event-split-graphs" if engine.cfg.comm_events else
