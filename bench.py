@@ -138,6 +138,7 @@ def main():
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     elapsed = all_reduce_max(elapsed, dev)
+    engine.check_comm()
     loss = float(engine.loss_last.item())
     if not math.isfinite(loss):
         raise SystemExit(f"non-finite loss {loss}")

@@ -197,6 +197,38 @@ void stream_wait_event(int64_t ev) {
 
 void event_destroy(int64_t ev) { HIP_CHECK(hipEventDestroy(reinterpret_cast<hipEvent_t>(ev))); }
 
+// ---- counter hand-off (engine.py comm_signal="flag"): the compute graph bumps a
+// per-bucket uint32 counter with a kernel node; the comm stream waits until the
+// counter reaches the replay number (wait-value packet, >=).
+void flag_bump(Tensor flags, int64_t k) {
+  TORCH_CHECK(flags.is_cuda() && flags.scalar_type() == at::kInt && flags.is_contiguous(), "flags: int32 cuda");
+  TORCH_CHECK(k >= 0 && k < flags.numel(), "flag index out of range");
+  flag_bump_launch(flags.data_ptr(), (int)k, c10::hip::getCurrentHIPStream().stream());
+}
+
+void stream_wait_flag(Tensor flags, int64_t k, int64_t value) {
+  TORCH_CHECK(flags.is_cuda() && flags.scalar_type() == at::kInt && flags.is_contiguous(), "flags: int32 cuda");
+  TORCH_CHECK(k >= 0 && k < flags.numel(), "flag index out of range");
+  HIP_CHECK(hipStreamWaitValue32(c10::hip::getCurrentHIPStream().stream(),
+                                 reinterpret_cast<uint32_t*>(flags.data_ptr<int>() + k),
+                                 static_cast<uint32_t>(value), hipStreamWaitValueGte, 0xFFFFFFFFu));
+}
+
+// the same wait as a 1-lane polling kernel of ours (bounded, raises err[0] on timeout)
+void flag_wait(Tensor flags, int64_t k, int64_t value, Tensor err) {
+  TORCH_CHECK(flags.is_cuda() && flags.scalar_type() == at::kInt && flags.is_contiguous(), "flags: int32 cuda");
+  TORCH_CHECK(err.is_cuda() && err.scalar_type() == at::kInt && err.numel() >= 1, "err: int32 cuda");
+  TORCH_CHECK(k >= 0 && k < flags.numel(), "flag index out of range");
+  flag_wait_launch(flags.data_ptr(), (int)k, static_cast<unsigned int>(value), err.data_ptr(),
+                   c10::hip::getCurrentHIPStream().stream());
+}
+
+bool stream_wait_value_supported(int64_t device) {
+  int v = 0;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeCanUseStreamWaitValue, (int)device) != hipSuccess) return false;
+  return v != 0;
+}
+
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(ddim_cold, m) {
@@ -204,6 +236,10 @@ TORCH_LIBRARY_FRAGMENT(ddim_cold, m) {
   m.def("event_record_external(int event) -> ()", &event_record_external);
   m.def("stream_wait_event(int event) -> ()", &stream_wait_event);
   m.def("event_destroy(int event) -> ()", &event_destroy);
+  m.def("flag_bump(Tensor(a!) flags, int k) -> ()", &flag_bump);
+  m.def("stream_wait_flag(Tensor flags, int k, int value) -> ()", &stream_wait_flag);
+  m.def("stream_wait_value_supported(int device) -> bool", &stream_wait_value_supported);
+  m.def("flag_wait(Tensor flags, int k, int value, Tensor(a!) err) -> ()", &flag_wait);
   m.def("comm_unique_id() -> Tensor", &comm_unique_id);
   m.def("comm_init(Tensor uid, int world, int rank, int device) -> int", &comm_init);
   m.def("comm_all_reduce_(Tensor(a!) buf, int handle, int op=0) -> ()", &comm_all_reduce_);

@@ -51,9 +51,49 @@ __global__ __launch_bounds__(kThreads) void wire_unpack_kernel(const bf16* __res
     for (int64_t j = n8 * 8; j < n; ++j) dst[j] = bf2f(src[j]);
 }
 
+// Bucket hand-off signal of the event-split data-parallel step (engine.py,
+// comm_signal="flag"): one lane adds 1 to flags[k] with a system-scope release,
+// i.e. after every earlier write of this queue's kernels is visible device-wide;
+// the comm stream waits for the counter with a stream wait-value packet.  A plain
+// kernel node, unlike an event-record node, keeps the compute graph one
+// uninterrupted chain.  Vector-memory atomic (lane-indexed address).
+__global__ __launch_bounds__(64) void flag_bump_kernel(unsigned int* __restrict__ flags, int k) {
+  const unsigned int lane = threadIdx.x;
+  if (lane == 0) __hip_atomic_fetch_add(flags + k + lane, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Comm-stream side of the hand-off: one lane polls flags[k] (system-scope acquire)
+// until it reaches `expected` (wrap-safe), sleeping between polls.  Bounded: after
+// ~2 s (s_memrealtime, 100 MHz) it gives up and raises err[0], so a hand-off that
+// never comes cannot wedge the GPU; the host checks err (FlagSignal.check).
+__global__ __launch_bounds__(64) void flag_wait_kernel(const unsigned int* __restrict__ flags, int k,
+                                                       unsigned int expected, unsigned int* __restrict__ err) {
+  const unsigned int lane = threadIdx.x;
+  if (lane != 0) return;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (true) {
+    const unsigned int v = __hip_atomic_load(flags + k + lane, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (static_cast<int>(v - expected) >= 0) break;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+      __hip_atomic_store(err + lane, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
 }  // namespace dc
 
 using namespace dc;
+
+void flag_wait_launch(const void* flags, int k, unsigned int expected, void* err, hipStream_t stream) {
+  flag_wait_kernel<<<1, 64, 0, stream>>>(reinterpret_cast<const unsigned int*>(flags), k, expected,
+                                         reinterpret_cast<unsigned int*>(err));
+}
+
+void flag_bump_launch(void* flags, int k, hipStream_t stream) {
+  flag_bump_kernel<<<1, 64, 0, stream>>>(reinterpret_cast<unsigned int*>(flags), k);
+}
 
 void wire_pack_launch(const float* src, void* dst, int64_t n, hipStream_t stream) {
   if (n <= 0) return;

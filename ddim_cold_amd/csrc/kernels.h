@@ -230,6 +230,8 @@ void cold_batch_launch(const float* pool, int pool_n, const int64_t* rng, int si
 // gradient wire format (comm_wire.hip): fp32 <-> bf16 (RNE), 16-B aligned buffers
 void wire_pack_launch(const float* src, void* dst, int64_t n, hipStream_t stream);
 void wire_unpack_launch(const void* src, float* dst, int64_t n, hipStream_t stream);
+void flag_bump_launch(void* flags, int k, hipStream_t stream);  // flags[k] += 1, system-scope release
+void flag_wait_launch(const void* flags, int k, unsigned int expected, void* err, hipStream_t stream);
 
 // attention backward with the proj Linear's input gradient fused in (short path):
 // dO = gy @ Wp computed per head inside the kernel (gy [B*N][Dm], Wp [Dm][Dm])

@@ -14,6 +14,7 @@ reductions.
 from __future__ import annotations
 
 import itertools
+import os
 from typing import Optional
 
 import torch
@@ -59,6 +60,54 @@ class ExternalEvent:
             except Exception:  # interpreter shutdown
                 pass
             self.handle = None
+
+
+class FlagSignal:
+    """Per-bucket hand-off counters for the event-split data-parallel step.
+
+    Inside the compute graph, :meth:`bump` is a 1-lane kernel node that adds 1 to
+    ``flags[k]`` with a system-scope release once the bucket's gradients are final;
+    the host then orders a comm-stream collective behind ``flags[k] >= replays``
+    with a stream wait-value packet (:meth:`waiter`).  Unlike an event-record node,
+    the kernel node keeps the graph one uninterrupted chain (measured on MI355X:
+    the comm stream waiting on mid-graph event nodes started only after the whole
+    graph had finished, so nothing overlapped)."""
+
+    def __init__(self, n: int, device):
+        _ext.load(raise_on_error=True)
+        self.flags = torch.zeros(max(1, n), dtype=torch.int32, device=device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        self.expected = 0  # replays of the graph that bumps the counters
+        # comm-stream wait: "kernel" = our bounded 1-lane polling kernel, "stream" =
+        # hipStreamWaitValue32 (DDIM_COLD_FLAG_WAIT)
+        self.mode = os.environ.get("DDIM_COLD_FLAG_WAIT", "kernel")
+
+    @staticmethod
+    def supported(device) -> bool:
+        _ext.load(raise_on_error=True)
+        d = torch.device(device)
+        return bool(torch.ops.ddim_cold.stream_wait_value_supported(d.index if d.index is not None else
+                                                                     torch.cuda.current_device()))
+
+    def bump(self, k: int):
+        torch.ops.ddim_cold.flag_bump(self.flags, int(k))
+
+    def waiter(self, k: int):
+        sig = self
+
+        class _Wait:
+            def wait(self_, stream):
+                with torch.cuda.stream(stream):
+                    if sig.mode == "stream":
+                        torch.ops.ddim_cold.stream_wait_flag(sig.flags, int(k), int(sig.expected))
+                    else:
+                        torch.ops.ddim_cold.flag_wait(sig.flags, int(k), int(sig.expected) & 0xFFFFFFFF, sig.err)
+        return _Wait()
+
+    def check(self):
+        """Raise if a comm-stream wait timed out (its collective then ran on stale data)."""
+        if int(self.err.item()) != 0:
+            raise RuntimeError("data-parallel hand-off: a comm-stream flag wait timed out")
 
 
 class NativeComm:

@@ -121,6 +121,12 @@ class EngineConfig:
     # bucket this is the single-process step + one all-reduce of the whole arena;
     # autotune_comm() measures it against the overlapped layouts on the real ranks.
     comm_inline: bool = os.environ.get("DDIM_COLD_COMM_INLINE") == "1"
+    # event-split step: how the compute graph tells the comm stream a bucket is
+    # final.  "flag": a kernel node bumps a per-bucket counter (system-scope release)
+    # and the comm stream waits on it with a wait-value packet; "event": external
+    # event-record nodes (measured: the comm stream then started only after the
+    # whole compute graph, so the overlapped layouts overlapped nothing).
+    comm_signal: str = os.environ.get("DDIM_COLD_COMM_SIGNAL", "flag")
     # micro-batches per optimizer step (batch_fn is called grad_accum times per
     # step; gradients accumulate in the arena, averaged in the optimizer; the
     # all-reduce runs once, after the last micro-batch's backward)
@@ -176,8 +182,7 @@ class TrainEngine:
         self.loss_last = torch.zeros(1, dtype=torch.float32, device=dev)
         self.loss_ema = torch.full((1,), cfg.ema_init, dtype=torch.float32, device=dev)
         self.side = torch.cuda.Stream(device=dev) if (self.is_cuda and cfg.wgrad_stream) else None
-        self.comm = torch.cuda.Stream(device=dev) if (self.is_cuda and self.segmented and
-                                                      not cfg.comm_inline) else None
+        self.comm = self._comm_stream() if (self.is_cuda and self.segmented and not cfg.comm_inline) else None
         self.comm_choice: Optional[str] = None  # autotune_comm() winner
         self.comm_times: Dict[str, float] = {}
         if cfg.comm not in ("torch", "native", "auto"):
@@ -207,6 +212,13 @@ class TrainEngine:
             self._refresh_shadow()
         model._engine = self
 
+    def _comm_stream(self):
+        """The collectives' stream.  DDIM_COLD_COMM_PRIO=1: a high-priority stream
+        (HIP gives each priority its own hardware queues, so the comm stream cannot
+        share an in-order queue with the compute stream)."""
+        prio = -1 if os.environ.get("DDIM_COLD_COMM_PRIO", "0") == "1" else 0
+        return torch.cuda.Stream(device=self.device, priority=prio)
+
     def _try_native(self, dev):
         """comm='auto': our own RCCL communicator if it comes up and sums correctly on
         EVERY rank (agreed through the torch process group), else torch.distributed.
@@ -232,6 +244,12 @@ class TrainEngine:
         if nc is not None:
             nc.destroy()
         return None
+
+    def check_comm(self):
+        """Raise if a comm-stream hand-off wait timed out (FlagSignal)."""
+        sig = getattr(self, "_signal", None)
+        if sig is not None:
+            sig.check()
 
     def close(self):
         """Release the native communicator (before the process group is destroyed)."""
@@ -632,10 +650,11 @@ class TrainEngine:
         self.cfg = dataclasses.replace(self.cfg, **kw)
         self._build_buckets()
         if self.is_cuda and self.segmented:
-            self.comm = None if self.cfg.comm_inline else (self.comm or torch.cuda.Stream(device=self.device))
+            self.comm = None if self.cfg.comm_inline else (self.comm or self._comm_stream())
         self._graphs = None
         self._multi = None
         self._events = None
+        self._signal = None
         self._eager_steps = 0
 
     def _snapshot_state(self):
@@ -674,6 +693,7 @@ class TrainEngine:
             self.train_steps(steps)
             torch.cuda.synchronize(self.device)
             times[name] = all_reduce_max(time.perf_counter() - t0, self.device) / steps * 1e3
+            self.check_comm()
         best = min(layouts, key=lambda L_: times[L_[0]])
         self._restore_state(snap)
         self.set_comm_layout(best[1], best[2], best[3])
@@ -732,11 +752,16 @@ class TrainEngine:
         pool = torch.cuda.graph_pool_handle()
         nb = len(self.buckets)
         self._multi = None
-        from ..parallel.comm import ExternalEvent
-        # release scope of the boundary events (DDIM_COLD_EVENT_FLAGS: extra
-        # hipEventCreateWithFlags bits, e.g. 0x40000000 = device-scope release)
-        flags = int(os.environ.get("DDIM_COLD_EVENT_FLAGS", "0"), 0)
-        evs = [ExternalEvent(flags) for _ in range(nb)]
+        from ..parallel.comm import ExternalEvent, FlagSignal
+        sig = None
+        if self.cfg.comm_signal == "flag" and self.comm is not None and FlagSignal.supported(self.device):
+            sig = FlagSignal(nb, self.device)
+            evs = [sig.waiter(k) for k in range(nb)]
+        else:
+            # release scope of the boundary events (DDIM_COLD_EVENT_FLAGS: extra
+            # hipEventCreateWithFlags bits, e.g. 0x40000000 = device-scope release)
+            flags = int(os.environ.get("DDIM_COLD_EVENT_FLAGS", "0"), 0)
+            evs = [ExternalEvent(flags) for _ in range(nb)]
         gen = self._step_iter()
         g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         self._segment_capture = True  # side streams rejoin before each boundary
@@ -745,7 +770,10 @@ class TrainEngine:
                 for _ in range(nb):
                     kind, k = next(gen)
                     assert kind == "bucket", kind
-                    evs[k].record()
+                    if sig is not None:
+                        sig.bump(k)
+                    else:
+                        evs[k].record()
             with torch.cuda.graph(g2, pool=pool, capture_error_mode=CAPTURE_MODE):
                 kind, _ = next(gen)
                 assert kind == "done", kind
@@ -753,12 +781,14 @@ class TrainEngine:
             self._segment_capture = False
         self._graphs = [g1, g2]
         self._events = evs
+        self._signal = sig
 
     def _capture_graphs(self, graph_comm: bool):
         pool = torch.cuda.graph_pool_handle()
         graphs = []
         self._multi = None
         self._events = None
+        self._signal = None
         gen = self._step_iter()
         nseg = len(self.buckets) + 1 if (self.segmented and not graph_comm) else 1
         if nseg == 1:
@@ -793,6 +823,9 @@ class TrainEngine:
         evs = getattr(self, "_events", None)
         if evs is not None and len(gs) == 2:
             gs[0].replay()
+            sig = getattr(self, "_signal", None)
+            if sig is not None:
+                sig.expected += 1  # this replay's counter value
             for k, ev in enumerate(evs):  # comm stream: waits on the bucket's event; inline: after gs[0]
                 self._allreduce(k, after=ev)
             self._join_comm()
