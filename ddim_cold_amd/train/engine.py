@@ -58,6 +58,9 @@ ALIGN = 64  # elements (256 B fp32)
 # mode a watchdog poll inside the capture window was seen on MI355X to invalidate
 # the capture (fallback to segments) and abort the process from the watchdog.
 CAPTURE_MODE = "thread_local"
+# event-split data parallel with counter hand-offs: queue the comm stream's work
+# ahead of the compute-graph replay (DDIM_COLD_PREISSUE=0: behind it)
+PREISSUE = os.environ.get("DDIM_COLD_PREISSUE", "1") != "0"
 
 
 @dataclass
@@ -244,6 +247,18 @@ class TrainEngine:
         if nc is not None:
             nc.destroy()
         return None
+
+    def _comm_host_async(self) -> bool:
+        """True when issuing a collective never blocks the host on device progress
+        (RCCL: ours or ProcessGroupNCCL).  gloo with CUDA tensors waits on the host for
+        its device-to-host copy, so its collectives must not be queued ahead of the
+        compute graph they wait for."""
+        if self.ncomm is not None:
+            return True
+        try:
+            return dist.get_backend(self.pg) == "nccl"
+        except Exception:  # pragma: no cover
+            return False
 
     def check_comm(self):
         """Raise if a comm-stream hand-off wait timed out (FlagSignal)."""
@@ -822,12 +837,21 @@ class TrainEngine:
             return
         evs = getattr(self, "_events", None)
         if evs is not None and len(gs) == 2:
-            gs[0].replay()
             sig = getattr(self, "_signal", None)
-            if sig is not None:
+            if sig is not None and self.comm is not None and PREISSUE and self._comm_host_async():
+                # counters: the comm stream's waits + collectives can be queued BEFORE the
+                # compute graph (each waits for its own counter), so the comm queue holds
+                # them when the graph starts instead of receiving them behind it
                 sig.expected += 1  # this replay's counter value
-            for k, ev in enumerate(evs):  # comm stream: waits on the bucket's event; inline: after gs[0]
-                self._allreduce(k, after=ev)
+                for k, ev in enumerate(evs):
+                    self._allreduce(k, after=ev)
+                gs[0].replay()
+            else:
+                gs[0].replay()
+                if sig is not None:
+                    sig.expected += 1
+                for k, ev in enumerate(evs):  # comm stream: waits on the bucket's event; inline: after gs[0]
+                    self._allreduce(k, after=ev)
             self._join_comm()
             gs[1].replay()
             return

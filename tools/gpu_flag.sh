@@ -19,7 +19,7 @@ run() {
 B="python bench.py --steps 1000 --warmup 50 --no-sampler --force-dist"
 for rep in 1 2; do
 run X=fake_flag_overlap2 DDIM_COLD_FAKE_COMM=1 $B --comm-layout overlap-2
-run X=fake_flag_streamwait_overlap2 DDIM_COLD_FLAG_WAIT=stream DDIM_COLD_FAKE_COMM=1 $B --comm-layout overlap-2
+run X=fake_flag_overlap2_nopre DDIM_COLD_PREISSUE=0 DDIM_COLD_FAKE_COMM=1 $B --comm-layout overlap-2
 run X=fake_flag_overlap4 DDIM_COLD_FAKE_COMM=1 $B --comm-layout overlap-4
 run X=fake_flag_inline DDIM_COLD_FAKE_COMM=1 $B --comm-layout inline-1
 run X=rccl_auto $B
