@@ -25,11 +25,12 @@ AdamW step, cosine LR step, zero_grad) re-designed for a latency-bound
   ``all_reduce`` (RCCL over xGMI via ``torch.distributed`` 'nccl') runs on
   a communication stream, so it overlaps the backward of the remaining
   blocks, and the optimizer waits on that stream.  Data parallel default
-  (``comm_events``): forward + backward is ONE linear graph carrying an
-  external event-record node per bucket boundary, the optimizer a second; the
-  host issues each bucket's collective on the comm stream behind its event
-  between the two replays (a comm branch inside the graph costs ~30 us per
-  fork on MI355X).  ``autotune_comm()`` picks the bucket layout (or one
+  (``comm_events``): forward + backward is ONE linear graph that bumps a
+  per-bucket counter at every bucket boundary (a 1-lane kernel node), the
+  optimizer a second; each bucket's collective waits on the comm stream
+  behind a bounded polling kernel for its counter, queued ahead of the
+  compute replay (a comm branch inside the graph costs ~30 us per fork on
+  MI355X; event-record nodes delayed the comm work to the end of the graph).  ``autotune_comm()`` picks the bucket layout (or one
   inline all-reduce) by measuring on the job's own ranks.  Alternatives:
   collectives captured into the step graph (``graph_comm``) or
   ``n_buckets + 1`` graph segments with host-issued collectives in between.
