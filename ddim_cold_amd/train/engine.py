@@ -577,11 +577,13 @@ class TrainEngine:
         ranges = self.bucket_ranges[k]
 
         fake = os.environ.get("DDIM_COLD_FAKE_COMM") == "1"
+        fake_reps = int(os.environ.get("DDIM_COLD_FAKE_COMM_REPS", "1"))  # longer stand-in collectives
 
         def reduce():
             for a, b in ranges:
-                if fake:  # topology experiment at 1 rank: one pass over the range per bucket
-                    self.flat_g[a:b].mul_(1.0)
+                if fake:  # topology experiment at 1 rank: passes over the range stand in for the collective
+                    for _ in range(fake_reps):
+                        self.flat_g[a:b].mul_(1.0)
                 elif self.ncomm is not None:
                     if self.flat_gw is None:
                         self.ncomm.all_reduce_(self.flat_g[a:b])
