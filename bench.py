@@ -15,7 +15,13 @@ keys, rank 0, outside the timed region) the DDIM k=20 / N=64 sampler
 throughput of the hipGraph-captured sampling loop.
 
     python bench.py                       # 1 GPU
+    python bench.py --gpus N              # N ranks, spawned here (one process per GPU)
     torchrun --nproc-per-node N bench.py --gpus N --steps K --warmup W
+
+``--gpus N`` is honoured either way: under torchrun the launched world size must
+equal N (else exit 2); without torchrun env vars and N > 1 this process spawns
+N rank processes itself (multi_gpu_trainer.py:212-219 launches its ranks the same
+way) without touching the GPU, and exits with the first non-zero rank exit code.
 """
 import argparse
 import json
@@ -32,23 +38,7 @@ import torch.distributed as dist
 BASELINE_IMG_S_PER_GPU = 709.0  # 22.2 steps/s x 32 img (train.log, RTX 3090 fp16 AMP)
 
 
-def _init_single(dev_index=0):
-    """1-rank RCCL process group (exercises the collective/segmented path on one GPU)."""
-    import datetime
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", "29517")
-    backend = "nccl" if torch.cuda.is_available() else "gloo"
-    kw = {}
-    if backend == "nccl":
-        from ddim_cold_amd.parallel.dist import graph_safe_nccl_env
-        graph_safe_nccl_env()
-        torch.cuda.set_device(dev_index)
-        kw["device_id"] = torch.device("cuda", dev_index)
-    dist.init_process_group(backend, rank=0, world_size=1, timeout=datetime.timedelta(seconds=300), **kw)
-    return False
-
-
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -83,18 +73,84 @@ def main():
                     help="draw the sampler's x_T on the host (torch.normal on CPU, as the reference)")
     ap.add_argument("--no-eager-baseline", action="store_true",
                     help="skip timing the plain eager PyTorch sampler (BASELINE.md's sampling comparator)")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
-    from ddim_cold_amd.parallel.dist import init_distributed, all_reduce_max, barrier, cleanup, env_world
+
+def _rank_entry(rank: int, world: int, port: int, argv):
+    """Spawned rank process (self-launch): torchrun-style env, then the benchmark."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    run(parse_args(argv))
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """Launch ``n`` rank processes of this benchmark (spawn context) and wait; on the
+    first non-zero exit the others are terminated.  The parent never initialises the
+    GPU (only counts devices), so the children own it.  Returns the exit code."""
+    import multiprocessing as mp
+    from ddim_cold_amd.parallel.dist import free_port
+    ndev = torch.cuda.device_count()  # no HIP context is created by counting
+    if 0 < ndev < n:
+        print(f"bench.py: --gpus {n} but only {ndev} GPU(s) visible", file=sys.stderr)
+        return 2
+    ctx = mp.get_context("spawn")
+    port = free_port()
+    procs = [ctx.Process(target=_rank_entry, args=(r, n, port, argv), name=f"rank{r}") for r in range(n)]
+    for p in procs:
+        p.start()
+    code = 0
+    while any(p.is_alive() for p in procs):
+        for p in procs:
+            p.join(timeout=0.2)
+            if p.exitcode not in (None, 0) and code == 0:
+                code = p.exitcode if p.exitcode > 0 else 1
+                print(f"bench.py: {p.name} exited with code {p.exitcode}; stopping the other ranks",
+                      file=sys.stderr)
+                for q in procs:
+                    if q.is_alive():
+                        q.terminate()
+    for p in procs:
+        p.join()
+        if p.exitcode not in (0, None) and code == 0:
+            code = p.exitcode if p.exitcode > 0 else 1
+    return code
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse_args(argv)
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" in os.environ:  # launched by torchrun (or another env launcher)
+        world = int(os.environ["WORLD_SIZE"])
+        if world != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks",
+                  file=sys.stderr)
+            raise SystemExit(2)
+        run(args)
+        return 0
+    if args.gpus > 1:
+        raise SystemExit(spawn_ranks(args.gpus, argv))
+    run(args)
+    return 0
+
+
+def run(args):
+    from ddim_cold_amd.parallel.dist import (init_distributed, init_single, all_reduce_max, barrier, cleanup,
+                                             env_world)
     world, rank, local = env_world()
-    distributed = init_distributed(world_size=max(world, 2) if args.force_dist and world == 1 else None) \
-        if not (args.force_dist and world == 1) else _init_single(dev_index=local)
+    if args.force_dist and world == 1:
+        distributed = init_single(device_index=local)
+    else:
+        distributed = init_distributed()
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
     else:
         dev = torch.device("cpu")
-    n = world if distributed else 1
+    n = dist.get_world_size() if dist.is_initialized() else 1
+    if n != args.gpus and not (args.force_dist and n == 1):
+        raise SystemExit(f"bench.py: process group has {n} ranks, --gpus {args.gpus}")
 
     from ddim_cold_amd.models import build_model
     from ddim_cold_amd.train.engine import EngineConfig, TrainEngine
@@ -208,6 +264,11 @@ def main():
                        "grad_wire": args.grad_wire,
                        "comm": engine.comm_backend if engine.segmented else "none",
                        "comm_layout": engine.comm_choice,
+                       "handoff": engine.handoff_order,
+                       "rccl_ranks": engine.ncomm.info()[0] if engine.ncomm is not None else
+                       (n if distributed and dist.get_backend() == "nccl" else None),
+                       "launcher": "torchrun/env" if os.environ.get("TORCHELASTIC_RUN_ID") else
+                       ("self-spawn" if n > 1 else "single"),
                        "comm_layout_ms": {k: round(v, 4) for k, v in engine.comm_times.items()} or None,
                        "optimizer": "AdamW(wd=0.05)+clip1.0+cosine", "final_loss": round(loss, 5)},
         }

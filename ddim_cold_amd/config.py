@@ -36,7 +36,9 @@ layouts on the job's ranks before training and keep the fastest, state
 restored; overrides ``bucket_blocks``), ``total_steps`` (DDIM T, default 2000), ``num_workers``,
 ``eval_every`` (epochs), ``log_every`` (steps, default 100), ``ckpt_dir``,
 ``timestep_embedding`` ('learned' | 'sinusoidal'), ``max_steps`` (cap per epoch,
-for smoke runs).
+for smoke runs), ``comm_layout`` (fixed data-parallel gradient-exchange layout
+instead of ``comm_autotune``), ``force_segments`` (testing: run the data-parallel
+step on a 1-rank process group).
 """
 from __future__ import annotations
 
@@ -85,6 +87,8 @@ class ExperimentConfig:
     sync_check_every: int = 0     # debug: cross-rank parameter checksum every N steps (0 = only after init)
     fault_inject_step: int = 0    # testing: raise after this many steps (after logging), to exercise resume
     perf_log: bool = True         # extra '# perf' lines (img/s, device ms/step) next to the reference lines
+    comm_layout: Optional[str] = None  # data parallel: 'overlap-2' | 'overlap-4' | 'inline-1' (skips comm_autotune)
+    force_segments: bool = False  # testing: the data-parallel step (1-rank RCCL group, comm stream) at num_gpus 1
 
     # ------------------------------------------------------------------ derived
     @property
@@ -117,6 +121,8 @@ class ExperimentConfig:
             raise ValueError(f"unknown dataset kind {self.dataset!r}")
         if self.dataset.startswith("cold") and self.image_size[0] != self.image_size[1]:
             raise ValueError("cold (down-sample) datasets require square images (diffusion_loader.py:74)")
+        if self.comm_layout not in (None, "overlap-2", "overlap-4", "inline-1"):
+            raise ValueError(f"unknown comm_layout {self.comm_layout!r}")
         if not self.synthetic and not all(self.dataStorage):
             raise ValueError("dataStorage needs [train_dir, val_dir] unless synthetic: true")
         return self

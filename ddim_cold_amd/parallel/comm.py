@@ -104,10 +104,16 @@ class FlagSignal:
                         torch.ops.ddim_cold.flag_wait(sig.flags, int(k), int(sig.expected) & 0xFFFFFFFF, sig.err)
         return _Wait()
 
+    def failed(self) -> bool:
+        return int(self.err.item()) != 0
+
     def check(self):
         """Raise if a comm-stream wait timed out (its collective then ran on stale data)."""
-        if int(self.err.item()) != 0:
-            raise RuntimeError("data-parallel hand-off: a comm-stream flag wait timed out")
+        if self.failed():
+            raise RuntimeError("data-parallel hand-off: a comm-stream flag wait timed out, so a gradient "
+                               "bucket was all-reduced before its gradients were final; stopping "
+                               "(resume from the last checkpoint; DDIM_COLD_PREISSUE=0 issues the "
+                               "collectives after the compute replay)")
 
 
 class NativeComm:
@@ -143,6 +149,10 @@ class NativeComm:
 
     def broadcast_(self, buf: torch.Tensor, root: int = 0):
         torch.ops.ddim_cold.comm_broadcast_(buf, self.handle, root)
+
+    def info(self):
+        """(ranks, my rank) as RCCL reports them (ncclCommCount / ncclCommUserRank)."""
+        return tuple(int(v) for v in torch.ops.ddim_cold.comm_info(self.handle))
 
     def destroy(self):
         if self.handle is not None:

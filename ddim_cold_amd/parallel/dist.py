@@ -74,6 +74,24 @@ def init_distributed(backend: Optional[str] = None, rank: Optional[int] = None, 
     return True
 
 
+def init_single(backend: Optional[str] = None, device_index: int = 0, timeout_s: int = 300) -> bool:
+    """A 1-rank process group (RCCL on a GPU, else gloo): exercises the data-parallel
+    step (comm stream, collectives, hand-offs) on one device.  Returns True."""
+    if dist.is_initialized():
+        return True
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(free_port()))
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    kw = {}
+    if backend == "nccl":
+        graph_safe_nccl_env()
+        torch.cuda.set_device(device_index)
+        kw["device_id"] = torch.device("cuda", device_index)
+    dist.init_process_group(backend, rank=0, world_size=1, timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return True
+
+
 def is_main() -> bool:
     return not dist.is_initialized() or dist.get_rank() == 0
 

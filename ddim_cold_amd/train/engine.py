@@ -186,7 +186,11 @@ class TrainEngine:
         self.loss_last = torch.zeros(1, dtype=torch.float32, device=dev)
         self.loss_ema = torch.full((1,), cfg.ema_init, dtype=torch.float32, device=dev)
         self.side = torch.cuda.Stream(device=dev) if (self.is_cuda and cfg.wgrad_stream) else None
-        self.comm = self._comm_stream() if (self.is_cuda and self.segmented and not cfg.comm_inline) else None
+        # the comm stream is created once and kept across set_comm_layout() (a stream
+        # created later could land on a hardware queue another stream already holds)
+        self._comm_obj = self._comm_stream() if (self.is_cuda and self.segmented) else None
+        self.comm = None if cfg.comm_inline else self._comm_obj
+        self.handoff_order: Optional[str] = None  # event-split step: "pre-issued" / "post-replay"
         self.comm_choice: Optional[str] = None  # autotune_comm() winner
         self.comm_times: Dict[str, float] = {}
         if cfg.comm not in ("torch", "native", "auto"):
@@ -217,11 +221,25 @@ class TrainEngine:
         model._engine = self
 
     def _comm_stream(self):
-        """The collectives' stream.  DDIM_COLD_COMM_PRIO=1: a high-priority stream
-        (HIP gives each priority its own hardware queues, so the comm stream cannot
-        share an in-order queue with the compute stream)."""
-        prio = -1 if os.environ.get("DDIM_COLD_COMM_PRIO", "0") == "1" else 0
+        """The collectives' stream: high priority by default (DDIM_COLD_COMM_PRIO=0:
+        normal).  HIP keeps a separate pool of hardware queues per priority, so a
+        high-priority comm stream can never share an in-order hardware queue with the
+        normal-priority compute stream -- with GPU_MAX_HW_QUEUES=4 normal-priority
+        streams beyond four do share queues round-robin, and a comm-stream wait
+        queued ahead of the compute graph on a SHARED queue would block that graph
+        (see :meth:`_preissue_ok`)."""
+        prio = -1 if os.environ.get("DDIM_COLD_COMM_PRIO", "1") != "0" else 0
         return torch.cuda.Stream(device=self.device, priority=prio)
+
+    def _preissue_ok(self) -> bool:
+        """Queue the comm stream's counter waits + collectives AHEAD of the compute
+        graph replay only when that cannot deadlock-until-timeout: RCCL issue never
+        blocks the host, and the comm stream has a different priority from the
+        compute stream, i.e. its own hardware queue.  Otherwise the host issues them
+        after the replay (same overlap, ~2-3 us later start per bucket)."""
+        if not (PREISSUE and self.comm is not None and self._comm_host_async()):
+            return False
+        return self.comm.priority != torch.cuda.current_stream(self.device).priority
 
     def _try_native(self, dev):
         """comm='auto': our own RCCL communicator if it comes up and sums correctly on
@@ -230,6 +248,21 @@ class TrainEngine:
         runs each on its internal stream behind an event round trip each way (1-rank
         inline step: 0.849 vs 0.866 ms)."""
         import warnings
+        # every rank must be able to enter ncclCommInitRank before any does: the init
+        # blocks until all ranks have joined, so a rank that fails BEFORE it (no
+        # extension, no comm ops) would leave the others hanging there
+        ready = 1
+        try:
+            from ..ops import _ext
+            _ext.load(raise_on_error=True)
+            ready = int(hasattr(torch.ops.ddim_cold, "comm_init"))
+        except Exception as e:  # pragma: no cover - depends on the build
+            warnings.warn(f"native RCCL communicator unavailable ({e!r})")
+            ready = 0
+        flag = torch.tensor([ready], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.pg)
+        if int(flag.item()) != 1:
+            return None
         nc, ok = None, 1
         try:
             from ..parallel.comm import NativeComm
@@ -262,10 +295,23 @@ class TrainEngine:
             return False
 
     def check_comm(self):
-        """Raise if a comm-stream hand-off wait timed out (FlagSignal)."""
+        """Raise ``RuntimeError`` if a comm-stream hand-off wait timed out (FlagSignal):
+        that bucket's collective then ran on gradients that were not final yet, so the
+        replicas may have diverged -- the run must stop (and resume from a checkpoint),
+        not continue.  One host sync; call at log points, not every step."""
         sig = getattr(self, "_signal", None)
         if sig is not None:
             sig.check()
+
+    def comm_error(self) -> bool:
+        """True if a hand-off wait has timed out since the last :meth:`reset_comm_error`."""
+        sig = getattr(self, "_signal", None)
+        return sig is not None and sig.failed()
+
+    def reset_comm_error(self):
+        sig = getattr(self, "_signal", None)
+        if sig is not None:
+            sig.err.zero_()
 
     def close(self):
         """Release the native communicator (before the process group is destroyed)."""
@@ -289,7 +335,16 @@ class TrainEngine:
         # embedding-backward launch (their dgamma/dbeta replicas are only complete
         # then); placed here they fall in the last all-reduce bucket, so data
         # parallel needs no replica finalize launch per bucket either.
+        # Frozen tensors (requires_grad=False, e.g. the fixed sinusoidal time table,
+        # ViT_draft2drawing.py:140-156) go last, past ``train_hi``: the norm, AdamW and
+        # the all-reduce buckets cover [0, train_hi) only, so a frozen tensor gets no
+        # weight decay, no moments and no optimizer state (torch.optim skips a
+        # parameter whose .grad is None).
+        self.frozen = {n for n, p in named if not p.requires_grad}
+
         def group(n):
+            if n in self.frozen:
+                return 4
             if n.rsplit(".", 1)[0] in ln_prefixes:
                 return 1
             if n.startswith("blocks."):
@@ -297,14 +352,19 @@ class TrainEngine:
             return 3 if n.startswith("head.") else 0
         layout = sorted(named, key=lambda np_: group(np_[0]))  # stable: original order within a group
         off = 0
+        self.train_hi = None
         for n, p in layout:
             ln_bias = n.endswith(".bias") and n[: -len(".bias")] in ln_prefixes
             if not ln_bias:
                 off = _align(off)
+            if n in self.frozen and self.train_hi is None:
+                self.train_hi = off
             self.offsets[n] = (off, p.numel())
             off += p.numel()
         off = _align(off)
         self.numel = off
+        if self.train_hi is None:
+            self.train_hi = off
         dev = self.device
         self.flat_p = torch.zeros(off, dtype=torch.float32, device=dev)
         self.flat_g = torch.zeros(off, dtype=torch.float32, device=dev)
@@ -321,8 +381,12 @@ class TrainEngine:
             vp.copy_(p.data)
             p.data = vp
             vg = self.flat_g[o:o + k].view_as(p)
-            p.grad = vg
+            p.grad = None if n in self.frozen else vg
             views_g[n] = vg
+        # the optimizer's ranges (frozen tensors excluded)
+        th = self.train_hi
+        self.opt_p, self.opt_g, self.opt_m, self.opt_v, self.opt_pb = (
+            t[:th] for t in (self.flat_p, self.flat_g, self.flat_m, self.flat_v, self.flat_pb))
         c = self.prog.cfg
         # LayerNorm fold: gamma-scaled bf16 weights / row sums / folded biases of
         # the QKV, fc1 and head GEMMs, recomputed from the fp32 masters after
@@ -381,7 +445,7 @@ class TrainEngine:
         bb = max(1, self.cfg.bucket_blocks)
         self.bucket_after: Dict[int, int] = {}
         bounds = []
-        end = self.numel
+        end = self.train_hi  # frozen tensors (past train_hi) are never reduced
         j = 0
         for i in range(L - 1, -1, -1):
             if ((L - 1 - i) % bb == bb - 1 and i > 0) or (i == 0 and self.cfg.embed_bucket):
@@ -549,8 +613,8 @@ class TrainEngine:
         # optimizer: grads are SUM-reduced over ranks and summed over micro-batches
         # -> average via grad_scale
         gs = 1.0 / (self.world * k_acc)
-        ops.sqnorm(self.flat_g, self.sqnorm, gs)
-        ops.adamw_step(self.flat_p, self.flat_g, self.flat_m, self.flat_v, self.flat_pb, self.sqnorm,
+        ops.sqnorm(self.opt_g, self.sqnorm, gs)
+        ops.adamw_step(self.opt_p, self.opt_g, self.opt_m, self.opt_v, self.opt_pb, self.sqnorm,
                        self.step_ctr, self.hyper, gs, zero_hi=self.acc_hi if overwrite else None)
         if loss_acc is not None:
             loss_parts = loss_acc
@@ -668,7 +732,7 @@ class TrainEngine:
         self.cfg = dataclasses.replace(self.cfg, **kw)
         self._build_buckets()
         if self.is_cuda and self.segmented:
-            self.comm = None if self.cfg.comm_inline else (self.comm or self._comm_stream())
+            self.comm = None if self.cfg.comm_inline else self._comm_obj
         self._graphs = None
         self._multi = None
         self._events = None
@@ -710,9 +774,19 @@ class TrainEngine:
             t0 = time.perf_counter()
             self.train_steps(steps)
             torch.cuda.synchronize(self.device)
-            times[name] = all_reduce_max(time.perf_counter() - t0, self.device) / steps * 1e3
-            self.check_comm()
-        best = min(layouts, key=lambda L_: times[L_[0]])
+            dt = time.perf_counter() - t0
+            # a layout whose hand-off timed out on ANY rank is disqualified (inf wins
+            # the max-reduction, so every rank drops it); its stale-gradient steps are
+            # undone by the state restore below
+            if self.comm_error():
+                dt = math.inf
+            times[name] = all_reduce_max(dt, self.device) / steps * 1e3
+            self.reset_comm_error()
+        ok = [L_ for L_ in layouts if math.isfinite(times[L_[0]])]
+        if not ok:
+            self._restore_state(snap)
+            raise RuntimeError(f"autotune_comm: every gradient-exchange layout failed its hand-off check: {times}")
+        best = min(ok, key=lambda L_: times[L_[0]])
         self._restore_state(snap)
         self.set_comm_layout(best[1], best[2], best[3])
         self.comm_choice, self.comm_times = best[0], times
@@ -800,6 +874,10 @@ class TrainEngine:
         self._graphs = [g1, g2]
         self._events = evs
         self._signal = sig
+        if sig is not None:
+            self.handoff_order = "pre-issued" if self._preissue_ok() else "post-replay"
+        else:
+            self.handoff_order = "events" if self.comm is not None else "inline"
 
     def _capture_graphs(self, graph_comm: bool):
         pool = torch.cuda.graph_pool_handle()
@@ -841,7 +919,7 @@ class TrainEngine:
         evs = getattr(self, "_events", None)
         if evs is not None and len(gs) == 2:
             sig = getattr(self, "_signal", None)
-            if sig is not None and self.comm is not None and PREISSUE and self._comm_host_async():
+            if sig is not None and self.handoff_order == "pre-issued":
                 # counters: the comm stream's waits + collectives can be queued BEFORE the
                 # compute graph (each waits for its own counter), so the comm queue holds
                 # them when the graph starts instead of receiving them behind it
@@ -931,6 +1009,8 @@ class TrainEngine:
         adam_step = float(self.step_ctr[0].item())
         if adam_step > 0:
             for n, p in zip(self.names, params):
+                if n in self.frozen:  # torch.optim keeps no state for a parameter without .grad
+                    continue
                 o, k = self.offsets[n]
                 opt.state[p] = {"step": torch.tensor(adam_step),
                                 "exp_avg": self.flat_m[o:o + k].view_as(p).clone(),
@@ -945,7 +1025,7 @@ class TrainEngine:
         step = 0
         for i, (n, p) in enumerate(zip(self.names, params)):
             s = st.get(i)
-            if s is None:
+            if s is None or n in self.frozen:
                 continue
             o, k = self.offsets[n]
             self.flat_m[o:o + k].copy_(s["exp_avg"].reshape(-1).to(self.device))

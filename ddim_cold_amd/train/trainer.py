@@ -42,7 +42,7 @@ from ..parallel import dist as pdist
 from ..utils.logging import ScalarWriter, asctime, fmt_epoch, fmt_steps, printLog
 from ..utils.observe import FaultInjected, StepClock, check_param_sync, phase, torch_profiler
 from . import checkpoint as ckpt
-from .engine import EngineConfig, TrainEngine
+from .engine import CAPTURE_MODE, EngineConfig, TrainEngine
 
 
 @dataclass
@@ -126,18 +126,35 @@ def evaluate(model, engine: TrainEngine, pool: torch.Tensor, idx: torch.Tensor, 
             with torch.cuda.stream(s):  # warm-up (allocator, kernels)
                 _eval_batch(prog, P, src, eval_rng, acc)
             torch.cuda.current_stream(dev).wait_stream(s)
+            # same capture discipline as the step graphs (engine.CAPTURE_MODE): drain the
+            # device and let the process-group watchdog drop the finished eager
+            # collectives first, capture thread-local; if the capture still fails,
+            # evaluate eagerly (same values, more launches)
+            torch.cuda.synchronize(dev)
+            if dist.is_available() and dist.is_initialized():
+                time.sleep(0.3)
             g = torch.cuda.CUDAGraph()
-            with no_gc(), torch.cuda.graph(g):
-                _eval_batch(prog, P, src, eval_rng, acc)
+            try:
+                with no_gc(), torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
+                    _eval_batch(prog, P, src, eval_rng, acc)
+                ent = (g, bidx, acc)
+            except Exception as e:  # pragma: no cover - depends on the runtime
+                import warnings
+                warnings.warn(f"eval graph capture failed ({e!r}); evaluating eagerly")
+                torch.cuda.synchronize(dev)
+                ent = (None, bidx, acc)
             eval_rng.copy_(saved)  # warm-up and capture leave the counters where they were
-            ent = cache[key] = (g, bidx, acc)
+            cache[key] = ent
         g, bidx, acc = ent
-        acc.zero_()
-        for b in range(n_full):
-            bidx.copy_(idx[b * batch:(b + 1) * batch].to(dev), non_blocking=True)
-            g.replay()
-        total += acc
-        nb = n_full
+        if g is not None:
+            acc.zero_()
+            for b in range(n_full):
+                bidx.copy_(idx[b * batch:(b + 1) * batch].to(dev), non_blocking=True)
+                g.replay()
+            total += acc
+            nb = n_full
+        else:
+            n_full = 0
     for s in range(n_full * batch, idx.numel(), batch):
         bidx_e = idx[s:s + batch].to(dev)
         src = make_batcher(kind, pool, bidx_e.numel(), eval_rng, total_steps, idx=bidx_e)
@@ -154,6 +171,8 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if world > 1:
         pdist.init_distributed(backend=backend, rank=rank, world_size=world)
+    elif cfg.force_segments:
+        pdist.init_single(backend=backend, device_index=local_rank)
     device = _device_for(rank, local_rank, backend)
     if device.type == "cuda":
         torch.cuda.set_device(device)
@@ -186,7 +205,7 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
     temb_rows = int(math.log2(cfg.image_size[1])) + 1 if cfg.dataset.startswith("cold") else None
     ecfg = EngineConfig(lr=cfg.lr, t_max=steps_per_epoch * cfg.epoch[1], use_graph=cfg.graph,
                         bucket_blocks=cfg.bucket_blocks, seed=cfg.seed * 1000 + rank, temb_rows=temb_rows,
-                        grad_accum=A)
+                        grad_accum=A, force_segments=cfg.force_segments)
     engine = TrainEngine(model, ecfg, device=device)
     # one static index row per micro-batch; the engine calls the batch source A
     # times per step in order (also while capturing), so call j reads row j
@@ -214,11 +233,15 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
             printLog(f"resuming from epoch {start_epoch:8d} of " + cfg.resume, paths.log)
             printLog(f"recovering best_loss {best_loss:4f}", paths.log)
     engine.loss_ema.fill_(loss_rec)
-    if cfg.comm_autotune and engine.segmented and device.type == "cuda":
+    if cfg.comm_autotune and not cfg.comm_layout and engine.segmented and device.type == "cuda":
         times = engine.autotune_comm()  # training state restored afterwards
         if rank == 0 and times:
             printLog(f"# comm layout: {engine.comm_choice} " +
                      " ".join(f"{k}={v:.4f}ms" for k, v in times.items()), paths.log)
+    if cfg.comm_layout and engine.segmented and device.type == "cuda":
+        lay = {L[0]: L for L in engine.COMM_LAYOUTS}[cfg.comm_layout]
+        engine.set_comm_layout(lay[1], lay[2], lay[3])
+        engine.comm_choice = lay[0]
     check_param_sync(engine.flat_p, step=steps)  # replicas start identical
     writer = ScalarWriter(paths.ckpt_dir, enabled=(rank == 0))
     clock = StepClock(device)
@@ -248,6 +271,7 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
                 check_param_sync(engine.flat_p, step=steps)
             if steps % cfg.log_every == 0:
                 window = clock.mark(steps)  # device events: the only sync of the window
+                engine.check_comm()  # a timed-out bucket hand-off stops the run (stale gradients)
                 loss_rec = float(engine.loss_ema.item())
                 if verbose:
                     print(f"[rank {rank}] step {steps} loss_ema {loss_rec:.4f}", flush=True)
@@ -258,10 +282,13 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
                     if cfg.perf_log and window is not None and window[1] > 0:
                         sec, n = window
                         printLog(f"# perf: {n * B * A * world / sec:.1f} img/s  {1e3 * sec / n:.3f} ms/step "
-                                 f"(device, {world} rank(s))", paths.log)
+                                 f"(device, {world} rank(s)" +
+                                 (f", comm {engine.comm_choice or 'default'}/{engine.handoff_order}"
+                                  if engine.segmented else "") + ")", paths.log)
             if cfg.fault_inject_step and steps >= cfg.fault_inject_step:
                 raise FaultInjected(f"fault injected at step {steps} (fault_inject_step)")
         loss_rec = float(engine.loss_ema.item())
+        engine.check_comm()  # epoch end: before evaluating / checkpointing these weights
         if (epoch - start_epoch + 1) % max(cfg.eval_every, 1) == 0 or epoch == end_epoch - 1:
             model.eval()
             vidx = shard_indices(n_val, world, rank, epoch, cfg.seed, shuffle=False, drop_last=False)
@@ -285,7 +312,8 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
     writer.close()
     result = {"steps": steps, "loss_rec": loss_rec, "best_loss": best_loss, "history": history,
               "final_lr": engine.current_lr(), "rng": [int(v) for v in engine.rng.tolist()],
-              "eval_rng": [int(v) for v in eval_rng.tolist()]}
+              "eval_rng": [int(v) for v in eval_rng.tolist()],
+              "comm_choice": engine.comm_choice, "handoff_order": engine.handoff_order}
     engine.close()
     pdist.cleanup()
     return result
@@ -320,10 +348,20 @@ def launch(cfg: ExperimentConfig, exp_name: str, paths: Paths, backend: Optional
              for r in range(world)]
     for p in procs:
         p.start()
+    # drain the result queue WHILE the ranks run: a child cannot exit before its
+    # queued result has been flushed into the pipe, so joining first could deadlock
+    import queue as _queue
+    per_rank = {}
     failed = None
-    while any(p.is_alive() for p in procs):
+    while True:
+        got = False
+        try:
+            r, res = q.get(timeout=0.5)
+            per_rank[r] = res
+            got = True
+        except _queue.Empty:
+            pass
         for p in procs:
-            p.join(timeout=0.5)
             if p.exitcode not in (None, 0) and failed is None:
                 failed = p
         if failed is not None:
@@ -333,13 +371,15 @@ def launch(cfg: ExperimentConfig, exp_name: str, paths: Paths, backend: Optional
             for p in procs:
                 p.join()
             raise RuntimeError(f"rank process {failed.name} exited with code {failed.exitcode}")
+        if len(per_rank) == world or (not got and not any(p.is_alive() for p in procs)):
+            break
+    for p in procs:
+        p.join()
     bad = [p.exitcode for p in procs if p.exitcode != 0]
     if bad:
         raise RuntimeError(f"rank processes failed with exit codes {bad}")
-    per_rank = {}
-    while not q.empty():
-        r, res = q.get()
-        per_rank[r] = res
+    if len(per_rank) != world:
+        raise RuntimeError(f"only ranks {sorted(per_rank)} of {world} reported a result")
     out = dict(per_rank.get(0, {}))
     out["per_rank"] = per_rank  # every rank's result (rank 0's is also the top level)
     return out

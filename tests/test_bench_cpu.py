@@ -25,3 +25,34 @@ def test_bench_torchrun_two_ranks_cpu():
     assert out["n_gpus"] == 2 and out["steps"] == 2 and out["warmup"] == 1
     assert out["config"]["global_batch"] == 64 and out["config"]["parallelism"] == "dp2"
     assert out["higher_is_better"] is True and out["scaling"] == "weak" and out["value"] > 0
+
+
+def _bench(args, env=None, timeout=600):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + args
+    e = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd="/tmp", env=e)
+
+
+def test_bench_self_spawns_gpus_n_cpu():
+    """`python bench.py --gpus 2` without torchrun launches 2 ranks itself (gloo on CPU)."""
+    r = _bench(["--gpus", "2", "--steps", "2", "--warmup", "1", "--no-sampler"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert REQUIRED <= set(out)
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["config"]["global_batch"] == 64 and out["config"]["launcher"] == "self-spawn"
+
+
+def test_bench_world_size_mismatch_fails():
+    """Under an env launcher, --gpus must equal the launched world size."""
+    r = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-sampler"],
+               env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                    "MASTER_PORT": "29599"}, timeout=300)
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert "WORLD_SIZE=1" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]

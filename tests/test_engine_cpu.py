@@ -17,10 +17,10 @@ from ddim_cold_amd.train.engine import EngineConfig, TrainEngine
 CFG = dict(img_size=[16, 16], patch_size=4, embed_dim=32, depth=3, num_heads=2)
 
 
-def _model(drop=True, seed=0):
+def _model(drop=True, seed=0, **extra):
     torch.manual_seed(seed)
     kw = dict(drop_rate=0.1, attn_drop_rate=0.1, drop_path_rate=0.2) if drop else dict(drop_rate=0.0, attn_drop_rate=0.0, drop_path_rate=0.0)
-    return DiffusionVisionTransformer(**CFG, **kw).train()
+    return DiffusionVisionTransformer(**CFG, **kw, **extra).train()
 
 
 def _batch(B, seed=1):
@@ -94,6 +94,47 @@ def test_engine_matches_torch_adamw_clip_cosine():
     eng2.load_scheduler_state_dict(ssd)
     assert torch.equal(eng2.flat_m, eng.flat_m) and torch.equal(eng2.flat_v, eng.flat_v)
     assert int(eng2.step_ctr[0]) == 3 and int(eng2.step_ctr[1]) == 3
+
+
+def test_engine_frozen_sinusoidal_table_matches_torch_adamw():
+    """A requires_grad=False parameter (the fixed sinusoidal timestep table,
+    ViT_draft2drawing.py:140-156) is left alone by the fused optimizer exactly as
+    torch.optim.AdamW leaves a parameter whose .grad is None: no weight decay, no
+    moments, no state entry; every other parameter matches torch step for step."""
+    from ddim_cold_amd.models.vit import positionalencoding1d
+    model = _model(timestep_embedding="sinusoidal")
+    ref_model = _model(timestep_embedding="sinusoidal")
+    table0 = positionalencoding1d(CFG["embed_dim"], 2000)
+    assert torch.equal(model.time_embed.weight.detach(), table0)
+    cfg = EngineConfig(lr=1e-3, t_max=20, max_grad_norm=0.05, seed=11)  # decay would move every element
+    eng = TrainEngine(model, cfg, device="cpu")
+    assert "time_embed.weight" in eng.frozen and eng.offsets["time_embed.weight"][0] >= eng.train_hi
+    assert model.time_embed.weight.grad is None
+    assert all(b <= eng.train_hi for _, b in eng.buckets)
+    opt = torch.optim.AdamW(ref_model.parameters(), lr=1e-3, betas=cfg.betas, eps=cfg.eps, weight_decay=0.05)
+    sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, 20)
+    for step in range(3):
+        x, y, t = _batch(4, seed=step)
+        g, loss_val = _grads(ref_model, x, y, t, torch.tensor([11, step]))
+        for n, p in ref_model.named_parameters():
+            p.grad = g[n].clone() if p.requires_grad else None
+        torch.nn.utils.clip_grad_norm_([p for p in ref_model.parameters() if p.requires_grad], 0.05)
+        opt.step()
+        sched.step()
+        loss = eng.step(x, y, t)
+        assert float(loss) == pytest.approx(loss_val, rel=1e-6)
+    sd_e, sd_r = model.state_dict(), ref_model.state_dict()
+    for n in sd_r:
+        assert torch.allclose(sd_e[n], sd_r[n], atol=2e-6, rtol=1e-5), n
+    for step in range(3, 10):  # 10 steps in all
+        eng.step(*_batch(4, seed=step))
+    assert torch.equal(model.time_embed.weight.detach(), table0)  # bit-identical after training
+    names = [n for n, _ in model.named_parameters()]
+    osd = eng.optimizer_state_dict()
+    assert names.index("time_embed.weight") not in osd["state"]
+    assert len(osd["state"]) == len(names) - 1
+    o2 = torch.optim.AdamW(_model(timestep_embedding="sinusoidal").parameters(), lr=1e-2, weight_decay=0.05)
+    o2.load_state_dict(osd)
 
 
 def test_engine_params_are_arena_views():
