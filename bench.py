@@ -50,7 +50,6 @@ def parse_args(argv=None):
                     help="optimizer steps per hipGraph replay (TrainEngine.train_steps; every step fully executed)")
     ap.add_argument("--bucket-blocks", type=int, default=2)
     ap.add_argument("--no-sampler", action="store_true")
-    ap.add_argument("--wgrad-stream", action="store_true")
     ap.add_argument("--force-dist", action="store_true",
                     help="init the RCCL process group and run segmented graphs + collectives even with 1 rank")
     ap.add_argument("--segmented-comm", action="store_true",
@@ -162,7 +161,6 @@ def run(args):
     lr = base_lr * args.batch * n / 512  # multi_gpu_trainer.py:196
     cfg = EngineConfig(lr=lr, t_max=512 * 100, use_graph=not args.no_graph, bucket_blocks=args.bucket_blocks,
                        seed=42, force_segments=args.force_dist,
-                       wgrad_stream=args.wgrad_stream,
                        temb_rows=int(math.log2(model.img_size[1])) + 1,  # cold t in 1..log2(W)
                        graph_comm=not args.segmented_comm, grad_wire=args.grad_wire,
                        comm_events=not (args.segmented_comm or args.captured_comm),
@@ -232,6 +230,19 @@ def run(args):
             extra["ddim_sampler_eager_torch_fp32_img_per_s"] = round(args.sampler_n / e32, 1)
             extra["ddim_sampler_eager_torch_bf16_img_per_s"] = round(args.sampler_n / ebf, 1)
             extra["ddim_sampler_vs_eager_fp32"] = round(e32 / dt, 2)
+        # BASELINE.json config 5, second half: the draft->drawing img2img call of
+        # ViT_draft2drawing.py:389-409 (9 t_starts 1599..1999, k=10, up to 200 steps)
+        # as ONE batched replayed hipGraph; comparator = the reference's sequential
+        # batch-1 fp32 eager loop on the same GPU
+        from ddim_cold_amd.bench.eager_sampler import time_img2img
+        starts = list(range(1599, 2000, 50))
+        ti = time_img2img(model, dev, starts, 10, reps=10)
+        extra["draft2drawing_ms"] = round(ti * 1e3, 3)
+        extra["draft2drawing_img_per_s"] = round(len(starts) / ti, 1)
+        if not args.no_eager_baseline:
+            te = time_img2img(model, dev, starts, 10, eager=True)
+            extra["draft2drawing_eager_torch_fp32_ms"] = round(te * 1e3, 1)
+            extra["draft2drawing_vs_eager_fp32"] = round(te / ti, 2)
         model.train()
     if rank == 0:
         out = {

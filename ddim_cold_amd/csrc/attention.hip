@@ -955,13 +955,7 @@ __global__ __launch_bounds__(NP * 4) void attn_fwd_short_kernel(const bf16* __re
   }
 }
 
-// Fused projection input-gradient (FUSE): dO of the head is computed in the
-// kernel, dO[b, :, h] = gy[b rows, :] @ Wp[:, h*hd : (h+1)*hd] (the proj
-// Linear's dgrad restricted to this head's columns; `dout` is then gy [B*N][Dm]
-// and `wp` the proj weight [Dm][Dm]), instead of being read from a separate
-// dgrad launch's output.  Same permuted-k MFMA order as the dgrad GEMM (tr
-// reads of the weight slice staged in the P/dS region), bf16-rounded like it.
-template <int HD, int NP, bool DROP, bool FUSE>
+template <int HD, int NP, bool DROP>
 __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __restrict__ dout,
                                                                 const bf16* __restrict__ qkv,
                                                                 const bf16* __restrict__ out,
@@ -969,7 +963,6 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
                                                                 bf16* __restrict__ dqkv, int B, int H, int N,
                                                                 float scale, const int64_t* __restrict__ rng,
                                                                 int site, uint32_t thr, float dsc,
-                                                                const bf16* __restrict__ wp, int Dm,
                                                                 const uint32_t* __restrict__ keep_bits) {
   using I = ShortImg<HD, NP>;
   constexpr int RS = I::RS, PS = 2 * NP + 32, KS = HD / 32, DT = HD / 16, KT = NP / 16;
@@ -997,37 +990,7 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
   iq.load(qkv + (size_t)bh * mat, HD, N);
   ik.load(qkv + ((size_t)B * H + bh) * mat, HD, N);
   iv.load(qkv + ((size_t)2 * B * H + bh) * mat, HD, N);
-  // FUSE: the weight slice Wp[:, h*HD..] ([Dm k-rows][HD], BS-byte rows) goes to the
-  // P/dS region; each wave's gy rows load as permuted-k A fragments
-  constexpr int BS = 2 * HD + 32;
-  constexpr int WCH = HD / 8;  // 16-B chunks per weight-slice row
-  constexpr int WPER = FUSE ? (512 * WCH + NP * 4 - 1) / (NP * 4) : 1;  // Dm <= 512
-  u32x4 wv[WPER];
-  if (FUSE) {
-#pragma unroll
-    for (int i = 0; i < WPER; ++i) {
-      const int c = threadIdx.x + i * NP * 4;
-      const int k = c / WCH, cc = c - k * WCH;
-      wv[i] = k < Dm ? *reinterpret_cast<const u32x4*>(wp + (size_t)k * Dm + h * HD + cc * 8) : u32x4{0u, 0u, 0u, 0u};
-    }
-  } else {
-    id.load(dout + (size_t)b * N * D + h * HD, D, N);
-  }
-  // FUSE: this wave's gy rows as permuted-k A fragments, every 32-deep step's
-  // loads issued up front (Dm <= 512: 16 steps)
-  u32x4 gfr[FUSE ? 16 : 1];
-  if (FUSE) {
-    const int r = wave * 16 + li;
-    const bf16* grow = dout + ((size_t)b * N + (r < N ? r : N - 1)) * Dm;
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      if (32 * s < Dm) {
-        const u32x2 lo = *reinterpret_cast<const u32x2*>(grow + 32 * s + 4 * g);
-        const u32x2 hi = *reinterpret_cast<const u32x2*>(grow + 32 * s + 16 + 4 * g);
-        gfr[s] = u32x4{lo[0], lo[1], hi[0], hi[1]};
-      }
-    }
-  }
+  id.load(dout + (size_t)b * N * D + h * HD, D, N);
   bf16x8 of[KS];
   {
     const bf16* orow = out + ((size_t)b * N + qc) * D + h * HD;
@@ -1042,39 +1005,7 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
   iq.store(Ql);
   ik.store(Kl);
   iv.store(Vl);
-  if (FUSE) {
-#pragma unroll
-    for (int i = 0; i < WPER; ++i) {
-      const int c = threadIdx.x + i * NP * 4;
-      const int k = c / WCH, cc = c - k * WCH;
-      if (k < Dm) *reinterpret_cast<u32x4*>(Pl + k * BS + cc * 16) = wv[i];
-    }
-    __syncthreads();
-    // dO rows 16w..16w+15 of this head: transposed accumulators (lane: row 16w+li,
-    // columns 16ct + 4g..+3), K = Dm in 32-deep steps, permuted k order
-    const int r = wave * 16 + li;
-    f32x4 acc[HD / 16];
-#pragma unroll
-    for (int ct = 0; ct < HD / 16; ++ct) acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      if (32 * s < Dm) {
-        const bf16x8 af = __builtin_bit_cast(bf16x8, gfr[s]);
-#pragma unroll
-        for (int ct = 0; ct < HD / 16; ++ct) acc[ct] = mfma16(frag_t<BS>(Pl, 16 * ct, s, lane), af, acc[ct]);
-      }
-    }
-    if (r < N) {
-#pragma unroll
-      for (int ct = 0; ct < HD / 16; ++ct) *reinterpret_cast<bf16x4*>(Dl + r * RS + (16 * ct + 4 * g) * 2) = pack4(acc[ct]);
-    } else if (r < NP) {
-#pragma unroll
-      for (int ct = 0; ct < HD / 16; ++ct)
-        *reinterpret_cast<bf16x4*>(Dl + r * RS + (16 * ct + 4 * g) * 2) = pack4(f32x4{0.f, 0.f, 0.f, 0.f});
-    }
-  } else {
-    id.store(Dl);
-  }
+  id.store(Dl);
   __syncthreads();
   attn_stamp(1);
 
@@ -1192,299 +1123,56 @@ template <int HD, int NP, bool DROP>
 struct ShortLaunch {
   static void run(bool bwd, const bf16* d, const bf16* q, const bf16* o, float* lse, const float* lse_in,
                   bf16* outp, int B, int H, int N, float scale, const int64_t* rng, int site, uint32_t thr,
-                  float dsc, hipStream_t stream, const bf16* wp, int Dm, uint32_t* kb) {
+                  float dsc, hipStream_t stream, uint32_t* kb) {
     using L = ShortLds<HD, NP>;
     static const bool attr = [] {
       allow_lds(&attn_fwd_short_kernel<HD, NP, DROP>, L::FWD);
-      allow_lds(&attn_bwd_short_kernel<HD, NP, DROP, true>, L::BWD);
-      allow_lds(&attn_bwd_short_kernel<HD, NP, DROP, false>, L::BWD);
+      allow_lds(&attn_bwd_short_kernel<HD, NP, DROP>, L::BWD);
       return true;
     }();
     (void)attr;
     if (!bwd)
       hipLaunchKernelGGL((attn_fwd_short_kernel<HD, NP, DROP>), dim3(B * H), dim3(NP * 4), L::FWD, stream, q, outp,
                          lse, B, H, N, scale, rng, site, thr, dsc, kb);
-    else if (wp != nullptr)
-      hipLaunchKernelGGL((attn_bwd_short_kernel<HD, NP, DROP, true>), dim3(B * H), dim3(NP * 4), L::BWD, stream, d, q,
-                         o, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, wp, Dm, kb);
     else
-      hipLaunchKernelGGL((attn_bwd_short_kernel<HD, NP, DROP, false>), dim3(B * H), dim3(NP * 4), L::BWD, stream, d, q,
-                         o, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, wp, Dm, kb);
+      hipLaunchKernelGGL((attn_bwd_short_kernel<HD, NP, DROP>), dim3(B * H), dim3(NP * 4), L::BWD, stream, d, q,
+                         o, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, kb);
   }
 };
 
 template <int HD, int NP>
 static void launch_short(bool bwd, const bf16* d, const bf16* q, const bf16* o, float* lse, const float* lse_in,
                          bf16* outp, int B, int H, int N, float scale, const int64_t* rng, int site, uint32_t thr,
-                         float dsc, hipStream_t stream, const bf16* wp, int Dm, uint32_t* kb) {
+                         float dsc, hipStream_t stream, uint32_t* kb) {
   if (thr)
-    ShortLaunch<HD, NP, true>::run(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, wp, Dm,
-                                   kb);
+    ShortLaunch<HD, NP, true>::run(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, kb);
   else
-    ShortLaunch<HD, NP, false>::run(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, wp,
-                                    Dm, kb);
+    ShortLaunch<HD, NP, false>::run(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, kb);
 }
 
 template <int HD>
 static void dispatch_short(bool bwd, const bf16* d, const bf16* q, const bf16* o, float* lse, const float* lse_in,
                            bf16* outp, int B, int H, int N, float scale, const int64_t* rng, int site, uint32_t thr,
-                           float dsc, hipStream_t stream, const bf16* wp = nullptr, int Dm = 0,
-                           uint32_t* kb = nullptr) {
+                           float dsc, hipStream_t stream, uint32_t* kb = nullptr) {
   switch ((N + 31) / 32) {
-    case 1: launch_short<HD, 32>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, wp, Dm, kb); break;
-    case 2: launch_short<HD, 64>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, wp, Dm, kb); break;
-    case 3: launch_short<HD, 96>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, wp, Dm, kb); break;
-    default: launch_short<HD, 128>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, wp, Dm, kb); break;
+    case 1: launch_short<HD, 32>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, kb); break;
+    case 2: launch_short<HD, 64>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, kb); break;
+    case 3: launch_short<HD, 96>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, kb); break;
+    default: launch_short<HD, 128>(bwd, d, q, o, lse, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, stream, kb); break;
   }
 }
 
 #define DC_INST_SHORT1(HD, NP, DR)                                                                                 \
   template __global__ void attn_fwd_short_kernel<HD, NP, DR>(const bf16*, bf16*, float*, int, int, int, float,    \
                                                              const int64_t*, int, uint32_t, float, uint32_t*);    \
-  template __global__ void attn_bwd_short_kernel<HD, NP, DR, false>(const bf16*, const bf16*, const bf16*,        \
-                                                                    const float*, bf16*, int, int, int, float,    \
-                                                                    const int64_t*, int, uint32_t, float,         \
-                                                                    const bf16*, int, const uint32_t*);           \
-  template __global__ void attn_bwd_short_kernel<HD, NP, DR, true>(const bf16*, const bf16*, const bf16*,         \
-                                                                   const float*, bf16*, int, int, int, float,     \
-                                                                   const int64_t*, int, uint32_t, float,          \
-                                                                   const bf16*, int, const uint32_t*);
+  template __global__ void attn_bwd_short_kernel<HD, NP, DR>(const bf16*, const bf16*, const bf16*,               \
+                                                              const float*, bf16*, int, int, int, float,          \
+                                                              const int64_t*, int, uint32_t, float,               \
+                                                              const uint32_t*);
 #define DC_INST_SHORT(HD, NP) DC_INST_SHORT1(HD, NP, true) DC_INST_SHORT1(HD, NP, false)
 DC_INST_SHORT(32, 32) DC_INST_SHORT(32, 64) DC_INST_SHORT(32, 96) DC_INST_SHORT(32, 128)
 DC_INST_SHORT(64, 32) DC_INST_SHORT(64, 64) DC_INST_SHORT(64, 96) DC_INST_SHORT(64, 128)
 
-
-// ============================================================================ fused QKV projection + short attention
-// The QKV GEMM of ONE head (its 3*hd weight rows, all N tokens of one sample)
-// computed by the workgroup that then runs the short-sequence attention of
-// that head: Q/K/V never round-trip through global memory (written out only
-// when the backward needs them) and the attention launch disappears.
-//   * workgroup = (b, h), NP/16 waves, wave w owns tokens 16w..16w+15;
-//   * A (the sample's token rows, bf16; the residual stream when the LayerNorm
-//     is folded in) goes global -> registers as MFMA fragments, all k-steps
-//     issued up front; the head's weight panel [3*hd][D] is shared by the waves
-//     through a 2-slot LDS ring (one 32-deep k-step per slot, XOR-swizzled 16-B
-//     chunks), its global loads also issued up front;
-//   * epilogue: LayerNorm fold (rstd*(acc - mean*c) + b') or bias, bf16, into
-//     the padded Q/K/V row images the attention reads (the short kernel's layout).
-struct QkvAttnArgs {
-  const bf16* x;      // [B*N][D] bf16 (raw residual rows when FOLD, else LayerNorm output)
-  const bf16* w;      // [3D][D] bf16 (gamma-folded when FOLD)
-  const float* bias;  // [3D] (folded bias when FOLD)
-  const float* c;     // [3D] row sums of w (FOLD)
-  const float* st;    // [B*N][D/32][2] row statistics slots (FOLD)
-  float eps;
-  float* mean;        // [B*N] optional (written by the h == 0 workgroups)
-  float* rstd;
-  bf16* qkv;          // [3][B][H][N][hd] optional (saved for the backward)
-  bf16* out;          // [B][N][H*hd]
-  float* lse;         // [B][H][N]
-  int B, H, N;
-  float scale;
-  const int64_t* rng;
-  int site;
-  uint32_t thr;
-  float dsc;
-};
-
-template <int HD, int NP, int KS, bool DROP, bool FOLD>
-__global__ __launch_bounds__(NP * 4) void qkv_attn_fwd_kernel(QkvAttnArgs a) {
-  constexpr int NT = NP * 4;
-  constexpr int COLS = 3 * HD;                   // weight panel rows (q | k | v of the head)
-  constexpr int FT = COLS / 16;                  // 16-column output tiles per wave
-  constexpr int CHUNKS = COLS * 4;               // 16-B chunks of one 32-deep k-step of the panel
-  constexpr int CPT = (CHUNKS + NT - 1) / NT;    // chunks per thread per k-step
-  constexpr int SLOT = COLS * 64;                // bytes of one k-step of the panel
-  constexpr int D = KS * 32;
-  using I = ShortImg<HD, NP>;
-  constexpr int RS = I::RS, KSA = HD / 32, DT = HD / 16, KT = NP / 16;
-  static_assert(RS == AC<HD>::S, "image stride");
-  // dynamic LDS: [2 * SLOT + 3 * NP * RS] images, then [NP] float2 (see ShortLds)
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  float2* ms = reinterpret_cast<float2*>(lds + 2 * SLOT + 3 * NP * RS);
-  char* ring = lds;
-  char* Ql = lds + 2 * SLOT;
-  char* Kl = Ql + NP * RS;
-  char* Vl = Kl + NP * RS;
-  const int H = a.H, N = a.N;
-  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
-
-  // ---- every global load up front
-  const int arow = wave * 16 + li;
-  const bf16* ap = a.x + ((size_t)b * N + (arow < N ? arow : N - 1)) * D + 8 * g;
-  bf16x8 af[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) af[ks] = *reinterpret_cast<const bf16x8*>(ap + 32 * ks);
-  u32x4 bv[KS][CPT];
-#pragma unroll
-  for (int i = 0; i < CPT; ++i) {
-    const int c = threadIdx.x + i * NT;
-    const int pr = c >> 2, kc = c & 3;
-    const int sel = pr / HD, d = pr - sel * HD;
-    const bf16* wp = a.w + ((size_t)(sel * H * HD + h * HD + (c < CHUNKS ? d : 0))) * D + 8 * kc;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-      bv[ks][i] = c < CHUNKS ? *reinterpret_cast<const u32x4*>(wp + 32 * ks) : u32x4{0u, 0u, 0u, 0u};
-  }
-  float cb[FT], cc[FT];
-#pragma unroll
-  for (int jt = 0; jt < FT; ++jt) {
-    const int col = 16 * jt + li, sel = col / HD, d = col - sel * HD;
-    const int wrow = sel * H * HD + h * HD + d;
-    cb[jt] = a.bias[wrow];
-    cc[jt] = FOLD ? a.c[wrow] : 0.f;
-  }
-  if (FOLD && threadIdx.x < NP) {
-    const int n = threadIdx.x;
-    float2 m = make_float2(0.f, 1.f);
-    if (n < N) {
-      const float2* sp = reinterpret_cast<const float2*>(a.st) + ((size_t)b * N + n) * KS;
-      float2 t = make_float2(0.f, 0.f);
-#pragma unroll
-      for (int k = 0; k < KS; ++k) {
-        const float2 e = sp[k];
-        t.x += e.x;
-        t.y += e.y;
-      }
-      const float mu = t.x * (1.0f / D);
-      const float var = fmaxf(t.y * (1.0f / D) - mu * mu, 0.f);
-      m = make_float2(mu, rsqrtf(var + a.eps));
-      if (a.mean != nullptr && h == 0) {
-        a.mean[(size_t)b * N + n] = m.x;
-        a.rstd[(size_t)b * N + n] = m.y;
-      }
-    }
-    ms[n] = m;
-  }
-  const uint32_t salt = DROP ? site_salt(a.rng, a.site) : 0u;
-
-  // ---- the head's QKV GEMM: [tokens x D] x [D x 3hd], k-steps through the LDS ring
-  f32x4 acc[FT];
-#pragma unroll
-  for (int jt = 0; jt < FT; ++jt) acc[jt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    char* slot = ring + (ks & 1) * SLOT;
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int c = threadIdx.x + i * NT;
-      const int pr = c >> 2, kc = c & 3;
-      if (c < CHUNKS) *reinterpret_cast<u32x4*>(slot + pr * 64 + ((kc ^ ((pr >> 1) & 3)) << 4)) = bv[ks][i];
-    }
-    __syncthreads();  // also: a wave writing slot ks&1 has passed every wave's k-step ks-2
-#pragma unroll
-    for (int jt = 0; jt < FT; ++jt) {
-      const int pr = 16 * jt + li;
-      const bf16x8 bf = *reinterpret_cast<const bf16x8*>(slot + pr * 64 + ((g ^ ((pr >> 1) & 3)) << 4));
-      acc[jt] = mfma16(af[ks], bf, acc[jt]);
-    }
-  }
-  // ---- epilogue into the Q / K / V row images (padded rows zero)
-#pragma unroll
-  for (int jt = 0; jt < FT; ++jt) {
-    const int col = 16 * jt + li, sel = col / HD, d = col - sel * HD;
-    char* img = sel == 0 ? Ql : (sel == 1 ? Kl : Vl);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = wave * 16 + 4 * g + r;
-      float v = acc[jt][r];
-      if (FOLD) {
-        const float2 m = ms[row];
-        v = (v - m.x * cc[jt]) * m.y;
-      }
-      v += cb[jt];
-      *reinterpret_cast<bf16*>(img + row * RS + d * 2) = f2bf(row < N ? v : 0.f);
-    }
-  }
-  __syncthreads();
-  if (a.qkv != nullptr) {  // head-major [3][B][H][N][hd] for the attention backward
-    constexpr int CR = HD / 8;
-    for (int c = threadIdx.x; c < 3 * N * CR; c += NT) {
-      const int sel = c / (N * CR), rem = c - sel * N * CR, row = rem / CR, ch = rem - row * CR;
-      const char* img = sel == 0 ? Ql : (sel == 1 ? Kl : Vl);
-      *reinterpret_cast<u32x4*>(a.qkv + (((size_t)sel * a.B * H + bh) * N + row) * HD + ch * 8) =
-          *reinterpret_cast<const u32x4*>(img + row * RS + ch * 16);
-    }
-  }
-  if (wave * 16 >= N) return;  // no barrier follows
-
-  // ---- attention of the head (attn_fwd_short_kernel on the images)
-  const int q = wave * 16 + li;
-  bf16x8 qf[KSA];
-#pragma unroll
-  for (int s2 = 0; s2 < KSA; ++s2) qf[s2] = frag_row<HD>(Ql, q, s2, g);
-  const float sl2 = a.scale * LOG2E;
-  f32x4 st[KT];
-#pragma unroll
-  for (int t = 0; t < KT; ++t) {
-    st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s2 = 0; s2 < KSA; ++s2) st[t] = mfma16(frag_row<HD>(Kl, 16 * t + li, s2, g), qf[s2], st[t]);
-  }
-  float mx = -INFINITY;
-#pragma unroll
-  for (int t = 0; t < KT; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float v = (16 * t + 4 * g + r) < N ? st[t][r] * sl2 : -INFINITY;
-      st[t][r] = v;
-      mx = fmaxf(mx, v);
-    }
-  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-  float l = 0.f;
-  const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * attn_mask_ld(N));
-#pragma unroll
-  for (int t = 0; t < KT; ++t) {
-    bool kp[4] = {true, true, true, true};
-    if (DROP) dropout_keep4(salt, rowidx + (uint32_t)(16 * t + 4 * g), a.thr, kp);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float pv = exp2f(st[t][r] - mx);
-      l += pv;
-      if (DROP) pv = kp[r] ? pv * a.dsc : 0.f;
-      st[t][r] = pv;
-    }
-  }
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
-  f32x4 o[DT];
-#pragma unroll
-  for (int d = 0; d < DT; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int s2 = 0; s2 < NP / 32; ++s2) {
-    const bf16x8 pb = pack8(st[2 * s2], st[2 * s2 + 1]);
-#pragma unroll
-    for (int d = 0; d < DT; ++d) o[d] = mfma16(frag_t<RS>(Vl, 16 * d, s2, lane), pb, o[d]);
-  }
-  if (q < N) {
-    const float inv = 1.f / l;
-    bf16* orow = a.out + ((size_t)b * N + q) * (H * HD) + h * HD;
-#pragma unroll
-    for (int d = 0; d < DT; ++d) *reinterpret_cast<bf16x4*>(orow + 16 * d + 4 * g) = pack4(o[d] * inv);
-    if (g == 0 && a.lse != nullptr) a.lse[(size_t)bh * N + q] = (mx + log2f(l)) * LN2;
-  }
-}
-
-template <int NP, int KS>
-static void launch_qkv_attn(const QkvAttnArgs& a, bool fold, hipStream_t stream) {
-  const dim3 grid(a.B * a.H), block(NP * 4);
-  constexpr int lds = 2 * (3 * 32 * 64) + 3 * NP * ShortImg<32, NP>::RS + NP * 8;  // images + ms (dynamic)
-  if (a.thr) {
-    if (fold) hipLaunchKernelGGL((qkv_attn_fwd_kernel<32, NP, KS, true, true>), grid, block, lds, stream, a);
-    else hipLaunchKernelGGL((qkv_attn_fwd_kernel<32, NP, KS, true, false>), grid, block, lds, stream, a);
-  } else {
-    if (fold) hipLaunchKernelGGL((qkv_attn_fwd_kernel<32, NP, KS, false, true>), grid, block, lds, stream, a);
-    else hipLaunchKernelGGL((qkv_attn_fwd_kernel<32, NP, KS, false, false>), grid, block, lds, stream, a);
-  }
-}
-
-#define DC_INST_QA1(NP, KS, DR, FO) template __global__ void qkv_attn_fwd_kernel<32, NP, KS, DR, FO>(QkvAttnArgs);
-#define DC_INST_QA(NP, KS) \
-  DC_INST_QA1(NP, KS, true, true) DC_INST_QA1(NP, KS, true, false) DC_INST_QA1(NP, KS, false, true) \
-  DC_INST_QA1(NP, KS, false, false)
-DC_INST_QA(96, 8) DC_INST_QA(96, 12) DC_INST_QA(96, 16) DC_INST_QA(128, 8) DC_INST_QA(128, 12) DC_INST_QA(128, 16)
 
 constexpr int SHORT_MAX_N = 128;
 
@@ -1520,10 +1208,10 @@ void attn_fwd_launch(const void* qkv, void* o, float* lse, int B, int H, int N, 
   if (N <= SHORT_MAX_N && !short_disabled() && (hd == 32 || hd == 64)) {
     if (hd == 32)
       dispatch_short<32>(false, nullptr, q, nullptr, lse, nullptr, out, B, H, N, scale, rng, site, thr, dsc, stream,
-                         nullptr, 0, keep_bits);
+                         keep_bits);
     else
       dispatch_short<64>(false, nullptr, q, nullptr, lse, nullptr, out, B, H, N, scale, rng, site, thr, dsc, stream,
-                         nullptr, 0, keep_bits);
+                         keep_bits);
     return;
   }
   static const bool v1 = [] {
@@ -1571,8 +1259,8 @@ void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const flo
   const bf16* oo = reinterpret_cast<const bf16*>(o);
   bf16* dq = reinterpret_cast<bf16*>(dqkv);
   if (N <= SHORT_MAX_N && !short_disabled() && (hd == 32 || hd == 64)) {
-    if (hd == 32) dispatch_short<32>(true, d, q, oo, nullptr, lse, dq, B, H, N, scale, rng, site, thr, dsc, stream, nullptr, 0, kb);
-    else dispatch_short<64>(true, d, q, oo, nullptr, lse, dq, B, H, N, scale, rng, site, thr, dsc, stream, nullptr, 0, kb);
+    if (hd == 32) dispatch_short<32>(true, d, q, oo, nullptr, lse, dq, B, H, N, scale, rng, site, thr, dsc, stream, kb);
+    else dispatch_short<64>(true, d, q, oo, nullptr, lse, dq, B, H, N, scale, rng, site, thr, dsc, stream, kb);
     return;
   }
   if (hd == 32) {
@@ -1583,54 +1271,5 @@ void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const flo
     hipLaunchKernelGGL(attn_bwd_dkv_kernel<64>, grid, dim3(256), 0, stream, d, q, lse, delta, dq, B, H, N, scale, rng, site, thr, dsc);
   } else {
     throw std::runtime_error("attention: head dim must be 32 or 64");
-  }
-}
-
-// LDS the fused kernel needs for the weight slice (P/dS region: 2 NP (2 NP + 32) bytes)
-bool attn_bwd_proj_supported(int N, int hd, int Dm) {
-  if (N > SHORT_MAX_N || short_disabled() || (hd != 32 && hd != 64) || Dm % 32 != 0 || Dm > 512) return false;
-  const int NP = 32 * ((N + 31) / 32);
-  return Dm * (2 * hd + 32) <= 2 * NP * (2 * NP + 32);
-}
-
-void attn_bwd_proj_launch(const void* gy, const void* wp, int Dm, const void* qkv, const void* o, const float* lse,
-                          void* dqkv, int B, int H, int N, int hd, float scale, const int64_t* rng, int site,
-                          double p, hipStream_t stream) {
-  if (!attn_bwd_proj_supported(N, hd, Dm) || Dm != H * hd)
-    throw std::runtime_error("attn_bwd_proj: unsupported shape");
-  const uint32_t thr = drop_threshold_host(p);
-  const float dsc = p > 0 ? 1.f / (1.f - (float)p) : 1.f;
-  const bf16* d = reinterpret_cast<const bf16*>(gy);
-  const bf16* q = reinterpret_cast<const bf16*>(qkv);
-  const bf16* oo = reinterpret_cast<const bf16*>(o);
-  const bf16* w = reinterpret_cast<const bf16*>(wp);
-  bf16* dq = reinterpret_cast<bf16*>(dqkv);
-  if (hd == 32) dispatch_short<32>(true, d, q, oo, nullptr, lse, dq, B, H, N, scale, rng, site, thr, dsc, stream, w, Dm);
-  else dispatch_short<64>(true, d, q, oo, nullptr, lse, dq, B, H, N, scale, rng, site, thr, dsc, stream, w, Dm);
-}
-
-bool qkv_attn_supported(int N, int hd, int D) {
-  return hd == 32 && N > 64 && N <= 128 && (D == 256 || D == 384 || D == 512);
-}
-
-void qkv_attn_fwd_launch(const QkvArgs& q, hipStream_t stream) {
-  if (!qkv_attn_supported(q.N, q.hd, q.D)) throw std::runtime_error("qkv_attn_fwd: unsupported shape");
-  QkvAttnArgs a;
-  a.x = reinterpret_cast<const bf16*>(q.x); a.w = reinterpret_cast<const bf16*>(q.w); a.bias = q.bias;
-  a.c = q.c; a.st = q.st; a.eps = q.eps; a.mean = q.mean; a.rstd = q.rstd;
-  a.qkv = reinterpret_cast<bf16*>(q.qkv); a.out = reinterpret_cast<bf16*>(q.out); a.lse = q.lse;
-  a.B = q.B; a.H = q.H; a.N = q.N; a.scale = q.scale; a.rng = q.rng; a.site = q.site;
-  a.thr = drop_threshold_host(q.p);
-  a.dsc = q.p > 0 ? 1.f / (1.f - (float)q.p) : 1.f;
-  const bool fold = q.st != nullptr;
-  const int KS = q.D / 32;
-  if (q.N <= 96) {
-    if (KS == 8) launch_qkv_attn<96, 8>(a, fold, stream);
-    else if (KS == 12) launch_qkv_attn<96, 12>(a, fold, stream);
-    else launch_qkv_attn<96, 16>(a, fold, stream);
-  } else {
-    if (KS == 8) launch_qkv_attn<128, 8>(a, fold, stream);
-    else if (KS == 12) launch_qkv_attn<128, 12>(a, fold, stream);
-    else launch_qkv_attn<128, 16>(a, fold, stream);
   }
 }

@@ -306,41 +306,6 @@ Tensor linear_residual_fwd(Tensor a, Tensor w, Tensor b, Tensor x, int64_t N, Te
   return out;
 }
 
-// x_new = x + DropPath(Dropout(a w^T + b)); (ln, mean, rstd) = LayerNorm(x_new)
-std::tuple<Tensor, Tensor, Tensor, Tensor> linear_residual_ln_fwd(Tensor a, Tensor w, Tensor b, Tensor x,
-                                                                  Tensor gamma, Tensor beta, double eps, int64_t N,
-                                                                  Tensor rng, int64_t site_drop, double p_drop,
-                                                                  int64_t site_dp, double p_dp) {
-  CHECK_IN(a, BF16); CHECK_IN(w, BF16); CHECK_IN(b, F32); CHECK_IN(x, F32); CHECK_IN(gamma, F32);
-  CHECK_IN(beta, F32); check_rng(rng);
-  const c10::DeviceGuard guard(a.device());
-  const int K = a.size(-1);
-  auto a2 = a.view({-1, K});
-  check_linear(a2, w, K);
-  const int M = a2.size(0), D = w.size(0);
-  TORCH_CHECK(x.numel() == (int64_t)M * D && b.numel() == D && gamma.numel() == D && beta.numel() == D &&
-                  M % N == 0, "residual+LN shapes");
-  TORCH_CHECK(gemm_resid_ln_supported(D, K), "residual+LN GEMM: unsupported width D=", D, " / K=", K);
-  auto x_out = at::empty(x.sizes(), x.options());
-  auto ln = at::empty({M, D}, a.options());
-  auto mean = at::empty({M}, x.options());
-  auto rstd = at::empty({M}, x.options());
-  GemmLnArgs g;
-  g.A = a2.data_ptr(); g.W = w.data_ptr(); g.M = M; g.K = K; g.D = D;
-  g.bias = b.data_ptr<float>(); g.res = x.data_ptr<float>(); g.x_out = x_out.data_ptr<float>();
-  g.gamma = gamma.data_ptr<float>(); g.beta = beta.data_ptr<float>(); g.ln_out = ln.data_ptr();
-  g.mean = mean.data_ptr<float>(); g.rstd = rstd.data_ptr<float>(); g.eps = (float)eps;
-  g.tokens = N; g.rng = rng.data_ptr<int64_t>();
-  g.site_drop = site_drop; g.p_drop = p_drop; g.site_dp = site_dp; g.p_dp = p_dp;
-  static const int bm_env = [] {
-    const char* e = getenv("DDIM_COLD_LN_GEMM_BM");
-    return e ? atoi(e) : 0;
-  }();
-  g.bm = bm_env ? bm_env : 32;
-  gemm_resid_ln(g, cur_stream());
-  return {x_out, ln, mean, rstd};
-}
-
 std::tuple<Tensor, Tensor> linear_gelu_fwd(Tensor a, Tensor w, Tensor b, Tensor rng, int64_t site, double p,
                                            c10::optional<Tensor> ln_st, c10::optional<Tensor> ln_c, double ln_eps, c10::optional<Tensor> ln_mean,
                                            c10::optional<Tensor> ln_rstd) {
@@ -360,6 +325,68 @@ std::tuple<Tensor, Tensor> linear_gelu_fwd(Tensor a, Tensor w, Tensor b, Tensor 
   gemm_nt(g, EPI_GELU, cur_stream());
   return {u, h};
 }
+
+static uint32_t drop_thr(double p) {  // == dc::drop_threshold_host (common.h)
+  const double v = p * 65536.0 + 0.5;
+  if (v >= 65536.0) return 65536u;
+  if (v <= 0.0) return 0u;
+  return (uint32_t)v;
+}
+
+// Fused MLP block (csrc/mlp.hip), LayerNorm-folded.  Returns (x_out, u, h); u / h
+// (training: pre-GELU and post-dropout GELU activations for the backward) are
+// empty when save is false.  st_out / xb_out receive the next LayerNorm's row
+// statistics and the bf16 copy of x_out; mean / rstd (optional) the LN2 row stats.
+std::tuple<Tensor, Tensor, Tensor> mlp_fused_fwd(Tensor xb, Tensor x1, Tensor st_in, Tensor w1, Tensor c1, Tensor b1,
+                                                 Tensor w2, Tensor b2, double eps, int64_t N, Tensor rng,
+                                                 int64_t site_f1, int64_t site_f2, double p_drop, int64_t site_dp,
+                                                 double p_dp, bool save, Tensor st_out, Tensor xb_out,
+                                                 c10::optional<Tensor> mean_out, c10::optional<Tensor> rstd_out,
+                                                 int64_t bm) {
+  CHECK_IN(xb, BF16); CHECK_IN(x1, F32); CHECK_IN(st_in, F32); CHECK_IN(w1, BF16); CHECK_IN(c1, F32);
+  CHECK_IN(b1, F32); CHECK_IN(w2, BF16); CHECK_IN(b2, F32); CHECK_IN(st_out, F32); CHECK_IN(xb_out, BF16);
+  check_rng(rng);
+  const c10::DeviceGuard guard(xb.device());
+  const int D = xb.size(-1);
+  const int64_t M = xb.numel() / D;
+  const int Hm = w1.size(0);
+  TORCH_CHECK(w1.dim() == 2 && w1.size(1) == D && w2.dim() == 2 && w2.size(0) == D && w2.size(1) == Hm,
+              "mlp_fused: weight shapes");
+  TORCH_CHECK(c1.numel() == Hm && b1.numel() == Hm && b2.numel() == D, "mlp_fused: bias shapes");
+  TORCH_CHECK(x1.numel() == M * D && st_in.numel() == M * (D / 32) * 2 && st_out.numel() == M * (D / 32) * 2 &&
+                  xb_out.numel() == M * D && M % N == 0,
+              "mlp_fused: activation shapes");
+  TORCH_CHECK(mlp_fused_supported(D, Hm), "mlp_fused: unsupported D=", D, " / hidden=", Hm);
+  TORCH_CHECK(M * std::max(D, Hm) < (1LL << 31) / 4, "mlp_fused: too many rows for 32-bit buffer offsets");
+  auto x_out = at::empty({M, D}, x1.options());
+  Tensor u = save ? at::empty({M, Hm}, xb.options()) : at::empty({0}, xb.options());
+  Tensor h = save ? at::empty({M, Hm}, xb.options()) : at::empty({0}, xb.options());
+  MlpArgs a;
+  a.xb = xb.data_ptr(); a.x1 = x1.data_ptr<float>(); a.st_in = st_in.data_ptr<float>();
+  a.w1 = w1.data_ptr(); a.c1 = c1.data_ptr<float>(); a.b1 = b1.data_ptr<float>();
+  a.w2 = w2.data_ptr(); a.b2 = b2.data_ptr<float>();
+  a.eps = (float)eps; a.M = (int)M; a.D = D; a.H = Hm; a.tokens = (int)N;
+  a.rng = rng.data_ptr<int64_t>();
+  a.site_f1 = (int)site_f1; a.site_f2 = (int)site_f2; a.site_dp = (int)site_dp;
+  a.thr_f1 = a.thr_f2 = drop_thr(p_drop);
+  a.sc_f1 = a.sc_f2 = p_drop > 0 ? 1.f / (1.f - (float)p_drop) : 1.f;
+  a.thr_dp = drop_thr(p_dp);
+  a.sc_dp = p_dp > 0 ? 1.f / (1.f - (float)p_dp) : 1.f;
+  a.x_out = x_out.data_ptr<float>(); a.xb_out = xb_out.data_ptr(); a.st_out = st_out.data_ptr<float>();
+  if (save) {
+    a.u_out = u.data_ptr(); a.h_out = h.data_ptr();
+  }
+  if (mean_out.has_value() && mean_out->defined()) {
+    CHECK_IN((*mean_out), F32); CHECK_IN((*rstd_out), F32);
+    TORCH_CHECK(mean_out->numel() == M && rstd_out->numel() == M, "mlp_fused: mean / rstd shapes");
+    a.mean_out = mean_out->data_ptr<float>(); a.rstd_out = rstd_out->data_ptr<float>();
+  }
+  a.bm = (int)bm;
+  mlp_fused_launch(a, cur_stream());
+  return {x_out, u, h};
+}
+
+bool mlp_fused_ok(int64_t D, int64_t H) { return mlp_fused_supported((int)D, (int)H); }
 
 Tensor head_fwd(Tensor a, Tensor w, Tensor b, int64_t B, int64_t C, int64_t H, int64_t W, int64_t patch,
                 c10::optional<Tensor> ln_st, c10::optional<Tensor> ln_c, double ln_eps, c10::optional<Tensor> ln_mean, c10::optional<Tensor> ln_rstd) {
@@ -383,6 +410,7 @@ Tensor head_fwd(Tensor a, Tensor w, Tensor b, int64_t B, int64_t C, int64_t H, i
 //   mode 1 (DDIM): x0 = clamp(head(a), -1, 1); x <- sqrt(a_tk) x0 + sqrt(1-a_tk) (x - sqrt(a_t) x0)/sqrt(1-a_t)
 //                  in place, x0 written to x0_out; coef = device row {sqrt a_t, sqrt 1-a_t, sqrt a_tk, sqrt 1-a_tk}
 //   mode 2 (cold): x <- clamp(head(a), -1, 1)
+//   mode 4 (img2img): mode 1 with one coefficient row per sample (coef [B][4])
 void head_step_(Tensor a, Tensor w, Tensor b, Tensor x, c10::optional<Tensor> x0_out, c10::optional<Tensor> coef,
                 int64_t patch, int64_t mode, c10::optional<Tensor> ln_st, c10::optional<Tensor> ln_c, double ln_eps,
                 c10::optional<Tensor> patches_out) {
@@ -395,15 +423,15 @@ void head_step_(Tensor a, Tensor w, Tensor b, Tensor x, c10::optional<Tensor> x0
   check_linear(a2, w, K);
   const int N = (H / patch) * (W / patch) + 1;
   TORCH_CHECK(a2.size(0) == B * N && w.size(0) == C * patch * patch && b.numel() == w.size(0), "head shapes");
-  TORCH_CHECK(mode == 1 || mode == 2, "head_step_: mode 1 (ddim) or 2 (clamp)");
+  TORCH_CHECK(mode == 1 || mode == 2 || mode == 4, "head_step_: mode 1 (ddim), 2 (clamp) or 4 (per-sample ddim)");
   GemmArgs g = nt_args(a2, w);
   g.C = x.data_ptr(); g.bias = b.data_ptr<float>();
   g.tokens = N; g.batch = B; g.chans = C; g.img_h = H; g.img_w = W; g.patch = patch;
   g.head_mode = (int)mode;
-  if (mode == 1) {
+  if (mode == 1 || mode == 4) {
     TORCH_CHECK(x0_out.has_value() && coef.has_value(), "ddim mode needs x0_out and coef");
     CHECK_IN((*x0_out), F32); CHECK_IN((*coef), F32);
-    TORCH_CHECK(x0_out->sizes() == x.sizes() && coef->numel() >= 4, "x0_out / coef shapes");
+    TORCH_CHECK(x0_out->sizes() == x.sizes() && coef->numel() >= (mode == 4 ? 4 * B : 4), "x0_out / coef shapes");
     g.res = x.data_ptr<float>(); g.C2 = x0_out->data_ptr(); g.coef = coef->data_ptr<float>();
   }
   if (patches_out.has_value() && patches_out->defined()) {  // the next step's patch rows
@@ -588,41 +616,6 @@ static std::vector<GemmArgs> wgrad_probs(const std::vector<Tensor>& dys, const s
   return probs;
 }
 
-// Grouped weight gradients: one launch for all (dy_i, x_i) -> dW_i += dy_i^T x_i
-// (db_i += colsum dy_i).  The token reduction is split over fp32 atomics (2-way
-// for a full block group, more for small groups); splits == 1 would use a plain
-// read-add-write epilogue.
-void linear_wgrad_group(std::vector<Tensor> dys, std::vector<Tensor> xs, std::vector<Tensor> dws,
-                        std::vector<c10::optional<Tensor>> dbs) {
-  const size_t n = dys.size();
-  TORCH_CHECK(n >= 1, "wgrad_group: empty");
-  const c10::DeviceGuard guard(dys[0].device());
-  int tiles = 0, min_kt = 0;
-  std::vector<GemmArgs> probs = wgrad_probs(dys, xs, dws, dbs, &tiles, &min_kt);
-  static const int forced = [] {
-    const char* e = getenv("DDIM_COLD_WGRAD_GROUP_SPLITS");
-    return e ? atoi(e) : 0;
-  }();
-  // measured (graph-timed, block group 216 tiles): unsplit 25.8 us, 2-way 14.9, 3-way 20.6, 4-way 19.6:
-  // one 64 KiB-LDS workgroup per CU cannot keep enough K tiles in flight, two can
-  // measured: 18.1 us (8-wave) vs 15.0 us (2-way atomic split) per block group ->
-  // opt-in (DDIM_COLD_WGRAD_GROUP8=1): two independently scheduled workgroups per CU
-  // hide latency better than one 8-wave workgroup whose halves share every barrier
-  static const bool eight = [] {
-    const char* e = getenv("DDIM_COLD_WGRAD_GROUP8");
-    return e && e[0] == '1';
-  }();
-  int splits = forced > 0 ? forced : (tiles >= 160 ? 2 : std::min(8, (256 + tiles - 1) / tiles));
-  splits = std::max(1, std::min(splits, min_kt));
-  // full block groups, opt-in: the 8-wave two-half kernel (same in-flight bytes
-  // as the 2-way split, no atomics); splits = 0 selects it
-  if (eight && forced <= 0 && tiles >= 160 && min_kt >= 2) splits = 0;
-  for (size_t i0 = 0; i0 < n; i0 += 6) {
-    const int cnt = (int)std::min<size_t>(6, n - i0);
-    gemm_wgrad_group(probs.data() + i0, cnt, splits, cur_stream());  // splits 0: 8-wave kernel
-  }
-}
-
 // Every weight gradient of a training step in ONE launch (gemm_wgrad_multi_kernel)
 void linear_wgrad_multi(std::vector<Tensor> dys, std::vector<Tensor> xs, std::vector<Tensor> dws,
                         std::vector<c10::optional<Tensor>> dbs, bool store) {
@@ -630,65 +623,6 @@ void linear_wgrad_multi(std::vector<Tensor> dys, std::vector<Tensor> xs, std::ve
   const c10::DeviceGuard guard(dys[0].device());
   std::vector<GemmArgs> probs = wgrad_probs(dys, xs, dws, dbs, nullptr, nullptr);
   gemm_wgrad_multi(probs.data(), (int)probs.size(), cur_stream(), store);
-}
-
-// Token split of weight-gradient riders: enough slices that the riders' tiles
-// number about `target` workgroups (DDIM_COLD_RIDE_WG, default 160), >= 2
-static int ride_splits(int tiles, int min_kt) {
-  static const int target = [] {
-    const char* e = getenv("DDIM_COLD_RIDE_WG");
-    return e ? std::max(16, atoi(e)) : 160;
-  }();
-  int s = (target + tiles - 1) / tiles;
-  s = std::max(2, std::min(s, 8));
-  return std::min(s, std::max(2, min_kt));
-}
-
-// dy @ W (linear_dgrad / linear_dgrad_gelu semantics) with the listed weight
-// gradients riding in the same launch (csrc/gemm.hip gemm_dgrad_ride_kernel).
-// mode 0: plain dgrad (out_fp32, splits as linear_dgrad); mode 1: GELU' dgrad
-// (u, rng, site, p as linear_dgrad_gelu).
-Tensor linear_dgrad_ride(Tensor dy, Tensor w, int64_t mode, bool out_fp32, int64_t splits,
-                         c10::optional<Tensor> u, c10::optional<Tensor> rng, int64_t site, double p,
-                         std::vector<Tensor> dys, std::vector<Tensor> xs, std::vector<Tensor> dws,
-                         std::vector<c10::optional<Tensor>> dbs) {
-  CHECK_IN(dy, BF16); CHECK_IN(w, BF16);
-  const c10::DeviceGuard guard(dy.device());
-  TORCH_CHECK(dy.dim() == 2 && w.dim() == 2 && dy.size(1) == w.size(0), "dgrad shapes");
-  TORCH_CHECK(mode == 0 || mode == 1, "dgrad_ride: mode 0 (plain) or 1 (GELU')");
-  const int M = dy.size(0), Nout = w.size(0), K = w.size(1);
-  TORCH_CHECK(Nout % 8 == 0 && K % 8 == 0, "dgrad dims must be multiples of 8");
-  TORCH_CHECK(dys.size() <= 6, "dgrad_ride: at most 6 riders");
-  GemmArgs g;
-  g.A = dy.data_ptr(); g.B = w.data_ptr();
-  g.M = M; g.N = K; g.K = Nout; g.lda = Nout; g.ldb = K;
-  Tensor dx;
-  int epi;
-  if (mode == 1) {
-    TORCH_CHECK(u.has_value() && rng.has_value(), "dgrad_ride: GELU' needs u and rng");
-    CHECK_IN((*u), BF16); check_rng(*rng);
-    TORCH_CHECK(u->numel() == (int64_t)M * K, "u shape");
-    dx = at::empty({M, K}, dy.options());
-    g.aux = u->data_ptr(); g.rng = rng->data_ptr<int64_t>(); g.site_drop = site; g.p_drop = p;
-    epi = EPI_DGELU;
-  } else {
-    TORCH_CHECK(splits >= 1 && splits <= 4, "dgrad K split: 1..4");
-    dx = splits > 1 ? at::empty({splits, M, K}, dy.options().dtype(out_fp32 ? F32 : BF16))
-                    : at::empty({M, K}, dy.options().dtype(out_fp32 ? F32 : BF16));
-    g.splits = (int)splits;
-    g.split_stride = (long long)M * K;
-    epi = out_fp32 ? EPI_F32 : EPI_BF16;
-  }
-  g.C = dx.data_ptr(); g.ldc = K;
-  int tiles = 0, min_kt = 1;
-  std::vector<GemmArgs> probs;
-  if (!dys.empty()) {
-    probs = wgrad_probs(dys, xs, dws, dbs, &tiles, &min_kt);
-    for (auto& t : dys) TORCH_CHECK(t.device() == dy.device(), "dgrad_ride: riders on another device");
-  }
-  const int ws = probs.empty() ? 2 : ride_splits(tiles, min_kt);
-  gemm_dgrad_ride(g, epi, probs.data(), (int)probs.size(), ws, cur_stream());
-  return dx;
 }
 
 // fp32 <-> bf16 gradient wire (csrc/comm_wire.hip): one fused 16-B-vector
@@ -704,79 +638,6 @@ void wire_unpack(Tensor src, Tensor dst) {
   TORCH_CHECK(src.numel() == dst.numel(), "wire_unpack: sizes");
   const c10::DeviceGuard guard(src.device());
   wire_unpack_launch(src.data_ptr(), dst.data_ptr<float>(), src.numel(), cur_stream());
-}
-
-// Image-group persistent forward of all transformer blocks (csrc/vit_group.hip).
-// ts: VG_TS tensors per block in the order below (None for the optional ones).
-constexpr int VG_TS = 28;
-bool vit_group_ok(int64_t D, int64_t H, int64_t hd, int64_t N, int64_t L) {
-  return vit_group_supported((int)D, (int)H, (int)hd, (int)N, (int)L);
-}
-void vit_group_fwd(std::vector<c10::optional<Tensor>> ts, int64_t L, int64_t B, int64_t N, std::vector<int64_t> sites,
-                   std::vector<double> p_dp, Tensor rng, double p_drop, double p_attn, double scale, double eps,
-                   Tensor ctr, Tensor err, c10::optional<Tensor> stamps) {
-  TORCH_CHECK(L >= 1 && L <= VG_MAXL && (int64_t)ts.size() == L * VG_TS, "vit_group_fwd: tensor list size");
-  TORCH_CHECK((int64_t)sites.size() == 6 * L && (int64_t)p_dp.size() == L, "vit_group_fwd: sites / drop-path list");
-  check_rng(rng);
-  CHECK_IN(ctr, at::kInt); CHECK_IN(err, at::kInt);
-  TORCH_CHECK(ctr.numel() >= B * 16, "vit_group_fwd: counter buffer too small");
-  const int D = 384, M = (int)(B * N);
-  const c10::DeviceGuard guard(rng.device());
-  VgArgs a;
-  a.L = (int)L; a.B = (int)B; a.N = (int)N; a.D = D; a.H = 12; a.hd = 32;
-  TORCH_CHECK(vit_group_supported(a.D, a.H, a.hd, a.N, a.L), "vit_group_fwd: unsupported shape");
-  // (required?, dtype, elements) per slot
-  struct Slot { bool req; c10::ScalarType dt; int64_t n; };
-  const int64_t MD = (int64_t)M * D;
-  const Slot slots[VG_TS] = {
-      {true, BF16, 3 * D * D}, {true, F32, 3 * D}, {true, F32, 3 * D}, {true, BF16, D * D}, {true, F32, D},
-      {true, BF16, D * D}, {true, F32, D}, {true, F32, D}, {true, BF16, D * D}, {true, F32, D},
-      {true, BF16, MD}, {true, F32, (int64_t)M * (D / 32) * 2}, {true, F32, MD},
-      {false, BF16, 3 * MD}, {true, BF16, MD}, {false, F32, B * 12 * N}, {true, F32, MD}, {true, BF16, MD},
-      {true, F32, (int64_t)M * (D / 32) * 2}, {true, BF16, MD}, {true, BF16, MD}, {true, F32, MD}, {true, BF16, MD},
-      {true, F32, (int64_t)M * (D / 32) * 2}, {false, F32, M}, {false, F32, M}, {false, F32, M}, {false, F32, M}};
-  std::vector<void*> ptr(ts.size(), nullptr);
-  for (size_t i = 0; i < ts.size(); ++i) {
-    const Slot& sl = slots[i % VG_TS];
-    if (!ts[i].has_value() || !ts[i]->defined()) {
-      TORCH_CHECK(!sl.req, "vit_group_fwd: tensor ", i % VG_TS, " of block ", i / VG_TS, " is required");
-      continue;
-    }
-    const Tensor& t = *ts[i];
-    CHECK_IN(t, sl.dt);
-    TORCH_CHECK(t.device() == rng.device(), "vit_group_fwd: tensors on different devices");
-    TORCH_CHECK(t.numel() == sl.n, "vit_group_fwd: tensor ", i % VG_TS, " of block ", i / VG_TS, " has ", t.numel(),
-                " elements, expected ", sl.n);
-    ptr[i] = t.data_ptr();
-  }
-  for (int l = 0; l < L; ++l) {
-    void** q = ptr.data() + (size_t)l * VG_TS;
-    VgBlock& b = a.blk[l];
-    b.qkv_wf = q[0]; b.qkv_bf = (const float*)q[1]; b.qkv_c = (const float*)q[2];
-    b.proj_w = q[3]; b.proj_b = (const float*)q[4];
-    b.fc1_wf = q[5]; b.fc1_bf = (const float*)q[6]; b.fc1_c = (const float*)q[7];
-    b.fc2_w = q[8]; b.fc2_b = (const float*)q[9];
-    b.xb_in = q[10]; b.st_in = (const float*)q[11]; b.x_in = (const float*)q[12];
-    b.qkv = q[13]; b.o = q[14]; b.lse = (float*)q[15]; b.x1 = (float*)q[16]; b.x1b = q[17]; b.st1 = (float*)q[18];
-    b.u = q[19]; b.h = q[20]; b.x_out = (float*)q[21]; b.xb_out = q[22]; b.st_out = (float*)q[23];
-    b.m1 = (float*)q[24]; b.r1 = (float*)q[25]; b.m2 = (float*)q[26]; b.r2 = (float*)q[27];
-    const int64_t* s6 = sites.data() + 6 * l;
-    b.site_a = (int)s6[0]; b.site_p = (int)s6[1]; b.site_d1 = (int)s6[2];
-    b.site_f1 = (int)s6[3]; b.site_f2 = (int)s6[4]; b.site_d2 = (int)s6[5];
-    b.p_dp = p_dp[l];
-    TORCH_CHECK((b.m1 == nullptr) == (b.r1 == nullptr) && (b.m2 == nullptr) == (b.r2 == nullptr),
-                "vit_group_fwd: mean / rstd outputs come in pairs");
-  }
-  a.rng = rng.data_ptr<int64_t>();
-  a.p_drop = p_drop; a.p_attn = p_attn; a.scale = (float)scale; a.eps = (float)eps;
-  a.ctr = reinterpret_cast<unsigned*>(ctr.data_ptr<int>());
-  a.err = reinterpret_cast<unsigned*>(err.data_ptr<int>());
-  if (stamps.has_value() && stamps->defined()) {
-    CHECK_IN((*stamps), at::kLong);
-    TORCH_CHECK(stamps->numel() >= B * 6 * VG_MAXL * 32, "vit_group_fwd: stamps buffer too small");
-    a.stamps = stamps->data_ptr();
-  }
-  vit_group_fwd_launch(a, cur_stream());
 }
 
 std::tuple<Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma,
@@ -856,26 +717,6 @@ Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, double scale, Ten
   attn_bwd_launch(dout.data_ptr(), qkv.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), dqkv.data_ptr(),
                   delta.data_ptr<float>(), B, H, N, hd, (float)scale, rng.data_ptr<int64_t>(), site, p,
                   cur_stream(), keep_ptr(keep, B, H, N, hd));
-  return dqkv;
-}
-
-bool attn_bwd_proj_ok(int64_t N, int64_t hd, int64_t D) { return attn_bwd_proj_supported((int)N, (int)hd, (int)D); }
-
-// attention backward with the proj input gradient fused in: gy [B*N][D] (the
-// gradient at the proj output), wp = proj weight [D][D]
-Tensor attn_bwd_proj(Tensor gy, Tensor wp, Tensor qkv, Tensor o, Tensor lse, double scale, Tensor rng, int64_t site,
-                     double p) {
-  CHECK_IN(gy, BF16); CHECK_IN(wp, BF16); CHECK_IN(qkv, BF16); CHECK_IN(o, BF16); CHECK_IN(lse, F32); check_rng(rng);
-  const c10::DeviceGuard guard(qkv.device());
-  TORCH_CHECK(qkv.dim() == 5 && qkv.size(0) == 3, "qkv must be [3,B,H,N,hd]");
-  const int B = qkv.size(1), H = qkv.size(2), N = qkv.size(3), hd = qkv.size(4), D = H * hd;
-  TORCH_CHECK(gy.numel() == (int64_t)B * N * D && wp.numel() == (int64_t)D * D && o.numel() == gy.numel() &&
-                  lse.numel() == (int64_t)B * H * N,
-              "attn_bwd_proj shapes");
-  TORCH_CHECK(attn_bwd_proj_supported(N, hd, D), "attn_bwd_proj: unsupported shape");
-  auto dqkv = at::empty({(int64_t)B * N, 3 * D}, qkv.options());
-  attn_bwd_proj_launch(gy.data_ptr(), wp.data_ptr(), D, qkv.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
-                       dqkv.data_ptr(), B, H, N, hd, (float)scale, rng.data_ptr<int64_t>(), site, p, cur_stream());
   return dqkv;
 }
 
@@ -1076,50 +917,6 @@ void ln_fold_(std::vector<Tensor> ws, std::vector<Tensor> gammas, std::vector<Te
   ln_fold_launch(tb, cur_stream());
 }
 
-// Fused QKV projection + short attention (one workgroup per head): returns
-// (o [B,N,D] bf16, lse [B,H,N] fp32, qkv [3,B,H,N,hd] bf16 or empty).  With
-// ln_st / ln_c the preceding LayerNorm is folded in (a = raw rows, w/b folded).
-std::tuple<Tensor, Tensor, Tensor> qkv_attn_fwd(Tensor a, Tensor w, Tensor b, c10::optional<Tensor> ln_st,
-                                                c10::optional<Tensor> ln_c, double ln_eps, int64_t B, int64_t N,
-                                                int64_t H, double scale, Tensor rng, int64_t site, double p,
-                                                bool save_qkv, c10::optional<Tensor> ln_mean,
-                                                c10::optional<Tensor> ln_rstd) {
-  CHECK_IN(a, BF16); CHECK_IN(w, BF16); CHECK_IN(b, F32); check_rng(rng);
-  const c10::DeviceGuard guard(a.device());
-  const int D = a.size(-1);
-  TORCH_CHECK(a.numel() == B * N * D && w.size(0) == 3 * D && w.size(1) == D && b.numel() == 3 * D && D % H == 0,
-              "qkv_attn_fwd shapes");
-  const int hd = D / H;
-  TORCH_CHECK(qkv_attn_supported(N, hd, D), "qkv_attn_fwd: needs hd 32, 64 < N <= 128, D in {256,384,512}");
-  QkvArgs q;
-  q.x = a.data_ptr(); q.w = w.data_ptr(); q.bias = b.data_ptr<float>();
-  if (ln_st.has_value() && ln_st->defined()) {
-    CHECK_IN((*ln_st), F32);
-    TORCH_CHECK(ln_c.has_value() && ln_c->defined(), "LayerNorm fold needs ln_c");
-    CHECK_IN((*ln_c), F32);
-    TORCH_CHECK(ln_st->numel() == 2 * B * N * (D / 32) && ln_c->numel() == 3 * D, "LayerNorm fold shapes");
-    q.st = ln_st->data_ptr<float>();
-    q.c = ln_c->data_ptr<float>();
-    if (ln_mean.has_value() && ln_mean->defined()) {
-      CHECK_IN((*ln_mean), F32); CHECK_IN((*ln_rstd), F32);
-      TORCH_CHECK(ln_mean->numel() == B * N && ln_rstd->numel() == B * N, "ln_mean / ln_rstd shapes");
-      q.mean = ln_mean->data_ptr<float>();
-      q.rstd = ln_rstd->data_ptr<float>();
-    }
-  }
-  q.eps = (float)ln_eps;
-  auto o = at::empty({B, N, D}, a.options());
-  auto lse = at::empty({B, H, N}, a.options().dtype(F32));
-  Tensor qkv = save_qkv ? at::empty({3, B, H, N, hd}, a.options()) : at::empty({0}, a.options());
-  q.qkv = save_qkv ? qkv.data_ptr() : nullptr;
-  q.out = o.data_ptr(); q.lse = lse.data_ptr<float>();
-  q.B = B; q.H = H; q.N = N; q.hd = hd; q.D = D; q.scale = (float)scale;
-  q.rng = rng.data_ptr<int64_t>(); q.site = site; q.p = p;
-  qkv_attn_fwd_launch(q, cur_stream());
-  return {o, lse, qkv};
-}
-
-bool qkv_attn_ok(int64_t N, int64_t hd, int64_t D) { return qkv_attn_supported(N, hd, D); }
 }  // namespace
 
 TORCH_LIBRARY(ddim_cold, m) {
@@ -1133,18 +930,12 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("attn_keep_words(int B, int H, int N, int hd) -> int", &attn_keep_words_op);
   m.def("attn_stamps(Tensor? buf) -> ()", &attn_stamps);
   m.def("ln_stamps(Tensor? buf) -> ()", &ln_stamps);
-  m.def("qkv_attn_fwd(Tensor a, Tensor w, Tensor b, Tensor? ln_st, Tensor? ln_c, float ln_eps, int B, int N, int H, "
-        "float scale, Tensor rng, int site, float p, bool save_qkv, Tensor(a!)? ln_mean=None, "
-        "Tensor(b!)? ln_rstd=None) -> (Tensor, Tensor, Tensor)");
-  m.def("qkv_attn_ok(int N, int hd, int D) -> bool", &qkv_attn_ok);
   m.def("linear_residual_fwd(Tensor a, Tensor w, Tensor b, Tensor x, int N, Tensor rng, int site_drop, "
         "float p_drop, int site_dp, float p_dp, Tensor(a!)? st_out=None, Tensor(b!)? xb_out=None) -> Tensor");
   m.def("linear_gelu_fwd(Tensor a, Tensor w, Tensor b, Tensor rng, int site, float p, Tensor? ln_st=None, "
         "Tensor? ln_c=None, float ln_eps=1e-5, Tensor(a!)? ln_mean=None, Tensor(b!)? ln_rstd=None) -> (Tensor, Tensor)");
   m.def("linear_fwd(Tensor a, Tensor w, Tensor? b, bool out_fp32, Tensor? ln_st=None, Tensor? ln_c=None, "
         "float ln_eps=1e-5) -> Tensor");
-  m.def("linear_residual_ln_fwd(Tensor a, Tensor w, Tensor b, Tensor x, Tensor gamma, Tensor beta, float eps, "
-        "int N, Tensor rng, int site_drop, float p_drop, int site_dp, float p_dp) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("head_fwd(Tensor a, Tensor w, Tensor b, int B, int C, int H, int W, int patch, Tensor? ln_st=None, "
         "Tensor? ln_c=None, float ln_eps=1e-5, Tensor(a!)? ln_mean=None, Tensor(b!)? ln_rstd=None) -> Tensor");
   m.def("head_step_(Tensor a, Tensor w, Tensor b, Tensor(a!) x, Tensor(b!)? x0_out, Tensor? coef, int patch, "
@@ -1154,21 +945,17 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("smooth_l1_fwd_bwd(Tensor pred, Tensor target, int N, int patch, float beta, Tensor(a!)? loss_last=None, "
         "Tensor(b!)? loss_ema=None, float ema_decay=0.99, bool finish=True) -> (Tensor, Tensor)");
   m.def("img_to_tokgrad(Tensor dimg, int N, int patch) -> Tensor");
+  m.def("mlp_fused_fwd(Tensor xb, Tensor x1, Tensor st_in, Tensor w1, Tensor c1, Tensor b1, Tensor w2, Tensor b2, "
+        "float eps, int N, Tensor rng, int site_f1, int site_f2, float p_drop, int site_dp, float p_dp, bool save, "
+        "Tensor(a!) st_out, Tensor(b!) xb_out, Tensor(c!)? mean_out=None, Tensor(d!)? rstd_out=None, int bm=0) "
+        "-> (Tensor, Tensor, Tensor)");
+  m.def("mlp_fused_ok(int D, int H) -> bool", &mlp_fused_ok);
   m.def("linear_dgrad(Tensor dy, Tensor w, bool out_fp32, int splits=1) -> Tensor");
   m.def("linear_dgrad_gelu(Tensor dy, Tensor w, Tensor u, Tensor rng, int site, float p) -> Tensor");
   m.def("linear_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, Tensor(b!)? db) -> ()");
-  m.def("linear_wgrad_group(Tensor[] dys, Tensor[] xs, Tensor(a!)[] dws, Tensor(b!)?[] dbs) -> ()");
   m.def("wire_pack(Tensor src, Tensor(a!) dst) -> ()");
   m.def("wire_unpack(Tensor src, Tensor(a!) dst) -> ()");
-  m.def("attn_bwd_proj_ok(int N, int hd, int D) -> bool", &attn_bwd_proj_ok);
-  m.def("attn_bwd_proj(Tensor gy, Tensor wp, Tensor qkv, Tensor o, Tensor lse, float scale, Tensor rng, int site, "
-        "float p) -> Tensor");
-  m.def("vit_group_ok(int D, int H, int hd, int N, int L) -> bool", &vit_group_ok);
-  m.def("vit_group_fwd(Tensor?[] ts, int L, int B, int N, int[] sites, float[] p_dp, Tensor rng, float p_drop, "
-        "float p_attn, float scale, float eps, Tensor(a!) ctr, Tensor(b!) err, Tensor(c!)? stamps=None) -> ()");
   m.def("linear_wgrad_multi(Tensor[] dys, Tensor[] xs, Tensor(a!)[] dws, Tensor(b!)?[] dbs, bool store=False) -> ()");
-  m.def("linear_dgrad_ride(Tensor dy, Tensor w, int mode, bool out_fp32, int splits, Tensor? u, Tensor? rng, "
-        "int site, float p, Tensor[] dys, Tensor[] xs, Tensor(a!)[] dws, Tensor(b!)?[] dbs) -> Tensor");
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor? g_res, "
         "Tensor(a!) dgamma, Tensor(b!) dbeta, int N, Tensor rng, int site_drop, float p_drop, int site_dp, "
         "float p_dp, bool emit_gy, Tensor(c!)? ws=None, Tensor? beta=None, Tensor(d!)? y_out=None) -> (Tensor, Tensor)");
@@ -1203,9 +990,9 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("layernorm_fwd", &layernorm_fwd);
   m.impl("qkv_fwd", &qkv_fwd);
   m.impl("attn_fwd", &attn_fwd);
-  m.impl("qkv_attn_fwd", &qkv_attn_fwd);
   m.impl("linear_residual_fwd", &linear_residual_fwd);
   m.impl("linear_gelu_fwd", &linear_gelu_fwd);
+  m.impl("mlp_fused_fwd", &mlp_fused_fwd);
   m.impl("head_fwd", &head_fwd);
   m.impl("smooth_l1_fwd_bwd", &smooth_l1_fwd_bwd);
   m.impl("head_loss", &head_loss);
@@ -1215,13 +1002,8 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("linear_wgrad", &linear_wgrad);
   m.impl("head_step_", &head_step_);
   m.impl("linear_fwd", &linear_fwd);
-  m.impl("linear_residual_ln_fwd", &linear_residual_ln_fwd);
-  m.impl("linear_wgrad_group", &linear_wgrad_group);
-  m.impl("linear_dgrad_ride", &linear_dgrad_ride);
   m.impl("linear_wgrad_multi", &linear_wgrad_multi);
-  m.impl("vit_group_fwd", &vit_group_fwd);
   m.impl("wire_pack", &wire_pack);
-  m.impl("attn_bwd_proj", &attn_bwd_proj);
   m.impl("wire_unpack", &wire_unpack);
   m.impl("layernorm_bwd", &layernorm_bwd);
   m.impl("replica_reduce_", &replica_reduce_);

@@ -34,13 +34,6 @@
 
 namespace dc {
 
-constexpr int WG_MAX = 6;
-struct WgradGroup {
-  GemmParams p[WG_MAX];
-  int tile_start[WG_MAX + 1];
-  int n;
-};
-
 static bool getenv_flag(const char* name) {
   const char* e = getenv(name);
   return e && e[0] == '1';
@@ -400,211 +393,6 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(GemmParams p) {
   gemm_dma_body<BM, BN, WM, WN, AT, BT, EPI, S>(p, tm, bid - tm * tiles_n, blockIdx.z);
 }
 
-// Grouped weight-gradient GEMM: up to WG_MAX independent dW = dy^T x problems
-// (the four linears of a transformer block, plus the head / patch embedding)
-// in ONE launch.  Tiles of all problems share the grid (XCD-aware), blockIdx.z
-// is the token (K) split of every problem.
-template <int EPI, int S>
-__global__ __launch_bounds__(256) void gemm_wgrad_group_kernel(WgradGroup gp) {
-  const int bid = xcd_remap(blockIdx.x, gp.tile_start[gp.n]);
-  int i = 0;
-#pragma unroll
-  for (int j = 1; j < WG_MAX; ++j)
-    if (j < gp.n && bid >= gp.tile_start[j]) i = j;
-  const GemmParams& p = gp.p[i];
-  const int tiles_n = (p.N + 63) / 64;
-  const int local = bid - gp.tile_start[i];
-  const int tm = local / tiles_n;
-  gemm_dma_body<64, 64, 2, 2, true, true, EPI, S>(p, tm, local - tm * tiles_n, blockIdx.z);
-}
-
-// Grouped weight gradient, 8 waves: the two halves of the workgroup (waves 0-3
-// and 4-7) reduce the two halves of the token range of the SAME 64x64 output
-// tile through their own LDS-DMA rings (2 x 64 KiB), then half 1 hands its
-// accumulators to half 0 through LDS and half 0 writes the tile with a plain
-// read-add-write epilogue.  Twice the operand bytes in flight per CU (what the
-// 2-way atomic split bought) without fp32 atomics.  Measured slower than the
-// 2-way atomic split (18.1 vs 15.0 us per block group): opt-in only.
-template <int S>
-__global__ __launch_bounds__(512) void gemm_wgrad_group8_kernel(WgradGroup gp) {
-  constexpr int BMN = 64, FM = 2, FN = 2;
-  using OP = DmaOperand<64, true>;
-  constexpr int STAGE = 2 * OP::BYTES;
-  constexpr int LPT = 2 * OP::PER_WAVE;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int bid = xcd_remap(blockIdx.x, gp.tile_start[gp.n]);
-  int pi = 0;
-#pragma unroll
-  for (int j = 1; j < WG_MAX; ++j)
-    if (j < gp.n && bid >= gp.tile_start[j]) pi = j;
-  const GemmParams& p = gp.p[pi];
-  const int tiles_n = (p.N + 63) / 64;
-  const int local = bid - gp.tile_start[pi];
-  const int tm = local / tiles_n, tn = local - tm * tiles_n;
-  const int m0 = tm * BMN, n0 = tn * BMN;
-
-  const int half = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8);
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & 3);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int g = lane >> 4, li = lane & 15;
-  char* ring = smem + half * S * STAGE;
-
-  const int total_kt = (p.K + BK - 1) / BK;
-  const int h0 = (total_kt + 1) / 2;
-  const int kt0 = half ? h0 : 0;
-  const int nk = half ? total_kt - h0 : h0;
-  const int niter = h0;  // both halves run the same number of barriers
-
-  OP oa, ob;
-  oa.init(p.A, p.lda, p.K, m0, wave, lane);
-  ob.init(p.B, p.ldb, p.K, n0, wave, lane);
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bool do_db = (p.bias != nullptr) && (tn == 0) && (wn == 0);
-  f32x4 dbacc[FM];
-#pragma unroll
-  for (int i = 0; i < FM; ++i) dbacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = f2bf(1.f);
-
-#pragma unroll
-  for (int s = 0; s < S - 1; ++s)
-    if (s < nk) {
-      oa.issue(ring + s * STAGE, kt0 + s, wave);
-      ob.issue(ring + s * STAGE + OP::BYTES, kt0 + s, wave);
-    }
-  for (int kt = 0; kt < niter; ++kt) {
-    const bool active = kt < nk;
-    if (active) vm_wait_rem<LPT>(min(S - 2, nk - 1 - kt));
-    raw_barrier();
-    if (!active) continue;
-    if (kt + S - 1 < nk) {
-      const int st = (kt + S - 1) % S;
-      oa.issue(ring + st * STAGE, kt0 + kt + S - 1, wave);
-      ob.issue(ring + st * STAGE + OP::BYTES, kt0 + kt + S - 1, wave);
-    }
-    const char* la = ring + (kt % S) * STAGE;
-    const char* lb = la + OP::BYTES;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 af[FM], bfr[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = frag_t_swz(la, wm * 32 + i * 16, s, lane);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = frag_t_swz(lb, wn * 32 + j * 16, s, lane);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
-      if (do_db) {
-#pragma unroll
-        for (int i = 0; i < FM; ++i) dbacc[i] = mfma16(af[i], ones, dbacc[i]);
-      }
-    }
-  }
-  // hand half 1's partial tile to half 0 through LDS (rings are done)
-  __syncthreads();
-  f32x4* xch = reinterpret_cast<f32x4*>(smem);  // [FM*FN + FM][256 lanes]
-  const int t = threadIdx.x & 255;
-  if (half == 1) {
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) xch[(i * FN + j) * 256 + t] = acc[i][j];
-#pragma unroll
-    for (int i = 0; i < FM; ++i) xch[(FM * FN + i) * 256 + t] = dbacc[i];
-  }
-  __syncthreads();
-  if (half == 1) return;
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] += xch[(i * FN + j) * 256 + t];
-#pragma unroll
-  for (int i = 0; i < FM; ++i) dbacc[i] += xch[(FM * FN + i) * 256 + t];
-
-  if (do_db && li == 0) {
-    float* db = const_cast<float*>(p.bias);
-    float old[FM][4];
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 32 + i * 16 + 4 * g + r;
-        old[i][r] = m < p.M ? db[m] : 0.f;
-      }
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 32 + i * 16 + 4 * g + r;
-        if (m < p.M) db[m] = old[i][r] + dbacc[i][r];
-      }
-  }
-  run_epilogue_vec<EPI_ACC, FM, FN>(p, acc, m0 + wm * 32, n0 + wn * 32, g, li);
-}
-template __global__ void gemm_wgrad_group8_kernel<4>(WgradGroup);
-
-// Input-gradient GEMM carrying weight-gradient "riders".  The backward chain
-// of a block (dgrad -> LayerNorm bwd -> dgrad -> attention bwd -> ...) is a
-// sequence of latency-bound launches of ~390 workgroups each; the block's four
-// weight gradients are independent of that chain once their operands exist.
-// Instead of one grouped weight-gradient launch per block, each ready
-// dW += dy^T x problem rides as extra workgroups of the NEXT dgrad launch:
-// workgroups [0, nd) are the dgrad's own tiles (K-split slices included, so the
-// grid is 1-D and the slice comes from the block id), [nd, nd + nw) the riders'
-// 64x64 tiles times their token split (fp32 atomics combine the slices).  The
-// dgrad tiles are dispatched first (they are the critical path); the riders
-// fill the CU slots the dgrad leaves idle, so a block's weight gradients cost
-// no launch of their own.  Dynamic LDS = the larger of the two rings.
-template <int BM, int EPI, int S, int SW>
-__global__ __launch_bounds__(256) void gemm_dgrad_ride_kernel(GemmParams p, WgradGroup gp, int dsplits, int wsplits) {
-  const int tiles_n = (p.N + 63) / 64;
-  const int dt = ((p.M + BM - 1) / BM) * tiles_n;
-  const int nd = dt * dsplits;
-  const int b = blockIdx.x;
-  if (b < nd) {
-    const int z = b / dt;
-    const int bid = xcd_remap(b - z * dt, dt);
-    const int tm = bid / tiles_n;
-    GemmParams q = p;
-    // the epilogue's split offset is blockIdx.z * split_stride (0 here): apply it to C
-    if (EPI == EPI_F32) q.C = reinterpret_cast<float*>(p.C) + (long long)z * p.split_stride;
-    else if (EPI == EPI_BF16) q.C = reinterpret_cast<bf16*>(p.C) + (long long)z * p.split_stride;
-    gemm_dma_body<BM, 64, 2, 2, false, true, EPI, S>(q, tm, bid - tm * tiles_n, z);
-    return;
-  }
-  const int wt = gp.tile_start[gp.n];
-  const int lw = b - nd;
-  const int z = lw / wt;
-  const int bid = xcd_remap(lw - z * wt, wt);
-  int i = 0;
-#pragma unroll
-  for (int j = 1; j < WG_MAX; ++j)
-    if (j < gp.n && bid >= gp.tile_start[j]) i = j;
-  const GemmParams& w = gp.p[i];
-  const int wtn = (w.N + 63) / 64;
-  const int local = bid - gp.tile_start[i];
-  const int tm = local / wtn;
-  gemm_dma_body<64, 64, 2, 2, true, true, EPI_ATOMIC, SW>(w, tm, local - tm * wtn, z);
-}
-#define DC_INST_RIDE(BM, EPI)                                                 \
-  template __global__ void gemm_dgrad_ride_kernel<BM, EPI, 3, 3>(GemmParams, WgradGroup, int, int); \
-  template __global__ void gemm_dgrad_ride_kernel<BM, EPI, 4, 3>(GemmParams, WgradGroup, int, int);
-DC_INST_RIDE(32, EPI_BF16)
-DC_INST_RIDE(32, EPI_F32)
-DC_INST_RIDE(32, EPI_DGELU)
-DC_INST_RIDE(64, EPI_BF16)
-DC_INST_RIDE(64, EPI_F32)
-DC_INST_RIDE(64, EPI_DGELU)
-
 template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EPI>
 static void launch_dma(GemmParams p, int splits, hipStream_t stream) {
   const int total_kt = (p.K + BK - 1) / BK;
@@ -738,8 +526,6 @@ DC_INST_DMA2(false, true, EPI_BF16)
 DC_INST_DMA2(false, true, EPI_F32)
 DC_INST_DMA2(false, true, EPI_DGELU)
 DC_INST_DMA(64, true, true, EPI_ATOMIC)
-template __global__ void gemm_wgrad_group_kernel<EPI_ATOMIC, 4>(WgradGroup);
-template __global__ void gemm_wgrad_group_kernel<EPI_ACC, 4>(WgradGroup);
 
 // Whole-backward weight gradient: every dW += dy^T x of a training step (all
 // blocks, head, patch embedding; up to WM_MAX problems) in ONE launch after the
@@ -783,14 +569,6 @@ __global__ __launch_bounds__(256) void gemm_wgrad_multi_kernel(WgradMulti gm) {
   gemm_dma_body<T, TN, 2, 2, true, true, EPI_ACC, S>(p, tm, local - tm * tiles_n, 0);
 }
 template __global__ void gemm_wgrad_multi_kernel<64, 3>(WgradMulti);
-template __global__ void gemm_wgrad_multi_kernel<64, 4>(WgradMulti);
-template __global__ void gemm_wgrad_multi_kernel<128, 3>(WgradMulti);
-template __global__ void gemm_wgrad_multi_kernel<128, 3, 64>(WgradMulti);
-template __global__ void gemm_wgrad_multi_kernel<128, 2, 64>(WgradMulti);
-template __global__ void gemm_wgrad_group_kernel<EPI_ATOMIC, 6>(WgradGroup);
-template __global__ void gemm_wgrad_group_kernel<EPI_ACC, 6>(WgradGroup);
-template __global__ void gemm_wgrad_group_kernel<EPI_ATOMIC, 8>(WgradGroup);
-template __global__ void gemm_wgrad_group_kernel<EPI_ACC, 8>(WgradGroup);
 
 }  // namespace dc
 
@@ -896,100 +674,17 @@ void gemm_wgrad(const GemmArgs& a, int splits, hipStream_t stream) {
   launch_auto<true, true, EPI_ATOMIC>(p, splits, stream);
 }
 
-template <int BM, int EPI>
-static void launch_ride(const GemmParams& p, const WgradGroup& gp, int dsplits, int wsplits, int dtiles,
-                        hipStream_t stream) {
-  constexpr int stage = BM * 128 + 64 * 128;
-  constexpr int per_cu4 = (160 * 1024) / (4 * stage);
-  constexpr int wlds = 3 * (64 * 128 + 64 * 128);
-  const int grid = dtiles * dsplits + gp.tile_start[gp.n] * wsplits;
-  static const bool force_s4 = getenv_flag("DDIM_COLD_GEMM_S4");
-  if (dtiles * dsplits > 256 * per_cu4 && p.ktiles_per_split <= 8 && !force_s4)
-    hipLaunchKernelGGL((gemm_dgrad_ride_kernel<BM, EPI, 3, 3>), dim3(grid), dim3(256), std::max(3 * stage, wlds),
-                       stream, p, gp, dsplits, wsplits);
-  else
-    hipLaunchKernelGGL((gemm_dgrad_ride_kernel<BM, EPI, 4, 3>), dim3(grid), dim3(256), std::max(4 * stage, wlds),
-                       stream, p, gp, dsplits, wsplits);
-}
-
-template <int EPI>
-struct RideTiles {
-  static void launch(const GemmParams& p, const WgradGroup& gp, int dsplits, int wsplits, int bm, hipStream_t s) {
-    const int tn = (p.N + 63) / 64;
-    if (bm == 32) launch_ride<32, EPI>(p, gp, dsplits, wsplits, ((p.M + 31) / 32) * tn, s);
-    else launch_ride<64, EPI>(p, gp, dsplits, wsplits, ((p.M + 63) / 64) * tn, s);
-  }
-};
-
-static WgradGroup make_group(const GemmArgs* probs, int n, int splits) {
-  WgradGroup gp{};
-  gp.n = n;
-  int tiles = 0;
-  for (int i = 0; i < n; ++i) {
-    gp.p[i] = base_params(probs[i]);
-    check_vec(gp.p[i], EPI_ATOMIC);
-    const int kt = (gp.p[i].K + BK - 1) / BK;
-    gp.p[i].ktiles_per_split = (kt + std::max(splits, 1) - 1) / std::max(splits, 1);
-    gp.tile_start[i] = tiles;
-    tiles += ((gp.p[i].M + 63) / 64) * ((gp.p[i].N + 63) / 64);
-  }
-  for (int i = n; i <= WG_MAX; ++i) gp.tile_start[i] = tiles;
-  return gp;
-}
-
-void gemm_dgrad_ride(const GemmArgs& a, int epi, const GemmArgs* probs, int n, int wsplits, hipStream_t stream) {
-  if (n < 0 || n > WG_MAX) throw std::runtime_error("gemm_dgrad_ride: 0..6 riders per launch");
-  if (epi != EPI_BF16 && epi != EPI_F32 && epi != EPI_DGELU) throw std::runtime_error("gemm_dgrad_ride: epilogue");
-  GemmParams p = base_params(a);
-  check_vec(p, epi);
-  const int kt = (p.K + 63) / 64;
-  int dsplits = epi == EPI_DGELU ? 1 : std::max(1, std::min(a.splits, kt));
-  if (epi != EPI_DGELU && dsplits != a.splits && a.splits > 1)
-    throw std::runtime_error("gemm_dgrad_ride: more K slices than k-tiles");
-  if (dsplits > 1 && (p.bias || (kt + dsplits - 1) / dsplits * (dsplits - 1) >= kt))
-    throw std::runtime_error("gemm_dgrad_ride: K split needs no bias and a non-empty last slice");
-  p.ktiles_per_split = (kt + dsplits - 1) / dsplits;
-  dsplits = (kt + p.ktiles_per_split - 1) / p.ktiles_per_split;
-  int wmin_kt = 1 << 30;
-  for (int i = 0; i < n; ++i) wmin_kt = std::min(wmin_kt, (probs[i].K + BK - 1) / BK);
-  // the rider slices combine through fp32 atomics: at least 2 slices, at most one k-tile each
-  wsplits = std::max(2, std::min(wsplits, wmin_kt));
-  const int cfg = pick_tiles(p.M, p.N, p.K, dsplits, false, true);
-  const bool ok = n > 0 && wmin_kt >= 2 && p.K % 64 == 0 && !dma_disabled() && cfg <= 1;
-  if (!ok) {  // separate launches (same results)
-    GemmArgs d = a;
-    gemm_dgrad(d, epi, stream);
-    if (n > 0) gemm_wgrad_group(probs, n, std::max(1, std::min(wsplits, wmin_kt)), stream);
-    return;
-  }
-  const WgradGroup gp = make_group(probs, n, wsplits);
-  const int bm = cfg == 0 ? 32 : 64;
-  switch (epi) {
-    case EPI_BF16: RideTiles<EPI_BF16>::launch(p, gp, dsplits, wsplits, bm, stream); break;
-    case EPI_F32: RideTiles<EPI_F32>::launch(p, gp, dsplits, wsplits, bm, stream); break;
-    default: RideTiles<EPI_DGELU>::launch(p, gp, dsplits, wsplits, bm, stream); break;
-  }
-}
-
 void gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool store) {
   if (n < 1 || n > WM_MAX) throw std::runtime_error("gemm_wgrad_multi: 1..32 problems per launch");
   WgradMulti gm{};
   gm.n = n;
   gm.store = store ? 1 : 0;
   int tiles = 0;
-  // tile: 64 x 64 (three 48 KiB workgroups per CU).  128 x 128 (DDIM_COLD_WGRAD_MULTI_TILE=128:
-  // half the operand bytes per output, one 96 KiB workgroup per CU, ~390 workgroups
-  // in 1.5 rounds) measured 14 us/step slower (0.838 vs 0.824 ms/step, interleaved A/B)
-  // DDIM_COLD_WGRAD_MULTI_TILE=12864 / 128642: 128 x 64 tiles (3 / 2 ring stages): 24 % fewer
-  // operand bytes, yet the step's launch takes the same time (60.8 / 60.1 vs 61.3 us,
-  // tools/gpu_wgm.sh: two workgroups per CU stream no faster than three) and a 1-block
-  // launch is slower (25 vs 17 us) -- opt-in
-  static const int cfg = [] {
-    const char* e = getenv("DDIM_COLD_WGRAD_MULTI_TILE");
-    return e ? atoi(e) : 64;
-  }();
-  const int T = cfg == 128 || cfg == 12864 || cfg == 128642 ? 128 : 64;
-  const int TNc = cfg == 128 ? 128 : 64;
+  // 64 x 64 tiles, 3-stage ring (48 KiB: three workgroups per CU).  Measured
+  // slower and removed: 128 x 128 tiles (half the operand bytes per output, one
+  // 96 KiB workgroup per CU, ~390 workgroups in 1.5 rounds: 0.838 vs 0.824
+  // ms/step), 128 x 64 tiles (24 % fewer operand bytes, same 60-61 us launch),
+  // a 4-stage ring (0.833).
   for (int i = 0; i < n; ++i) {
     const GemmArgs& a = probs[i];
     if (a.N % 4 != 0) throw std::runtime_error("gemm_wgrad_multi: output width must be a multiple of 4");
@@ -998,83 +693,9 @@ void gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool sto
     d.C = reinterpret_cast<float*>(a.C); d.bias = const_cast<float*>(a.bias);
     d.M = a.M; d.N = a.N; d.K = a.K; d.lda = a.lda; d.ldb = a.ldb; d.ldc = a.ldc;
     gm.tile_start[i] = tiles;
-    tiles += ((a.M + T - 1) / T) * ((a.N + TNc - 1) / TNc);
+    tiles += ((a.M + 63) / 64) * ((a.N + 63) / 64);
   }
   for (int i = n; i <= WM_MAX; ++i) gm.tile_start[i] = tiles;
-  if (T == 128 && TNc == 64) {
-    const int st = cfg == 128642 ? 2 : 3;
-    const int lds = st * (128 * 128 + 64 * 128);
-    static const bool attr3 = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_wgrad_multi_kernel<128, 3, 64>),
-                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 3 * (128 * 128 + 64 * 128)) == hipSuccess;
-    (void)attr3;
-    if (st == 2)
-      hipLaunchKernelGGL((gemm_wgrad_multi_kernel<128, 2, 64>), dim3(tiles), dim3(256), lds, stream, gm);
-    else
-      hipLaunchKernelGGL((gemm_wgrad_multi_kernel<128, 3, 64>), dim3(tiles), dim3(256), lds, stream, gm);
-    return;
-  }
-  if (T == 128) {
-    constexpr int lds = 3 * (128 * 128 + 128 * 128);
-    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_wgrad_multi_kernel<128, 3>),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
-    (void)attr;
-    hipLaunchKernelGGL((gemm_wgrad_multi_kernel<128, 3>), dim3(tiles), dim3(256), lds, stream, gm);
-    return;
-  }
-  // 64 x 64: ring depth 3 stages (48 KiB) -> 3 workgroups per CU, 4 (64 KiB) -> 2
-  static const int ring = [] {
-    const char* e = getenv("DDIM_COLD_WGRAD_MULTI_S");
-    return (e && atoi(e) == 4) ? 4 : 3;
-  }();
-  if (ring == 4)
-    hipLaunchKernelGGL((gemm_wgrad_multi_kernel<64, 4>), dim3(tiles), dim3(256), 4 * (64 * 128 + 64 * 128), stream, gm);
-  else
-    hipLaunchKernelGGL((gemm_wgrad_multi_kernel<64, 3>), dim3(tiles), dim3(256), 3 * (64 * 128 + 64 * 128), stream, gm);
+  hipLaunchKernelGGL((gemm_wgrad_multi_kernel<64, 3>), dim3(tiles), dim3(256), 3 * (64 * 128 + 64 * 128), stream, gm);
 }
 
-void gemm_wgrad_group(const GemmArgs* probs, int n, int splits, hipStream_t stream) {
-  if (n < 1 || n > WG_MAX) throw std::runtime_error("gemm_wgrad_group: 1..6 problems per launch");
-  WgradGroup gp{};
-  gp.n = n;
-  int tiles = 0;
-  for (int i = 0; i < n; ++i) {
-    gp.p[i] = base_params(probs[i]);
-    check_vec(gp.p[i], EPI_ATOMIC);
-    const int kt = (gp.p[i].K + BK - 1) / BK;
-    gp.p[i].ktiles_per_split = (kt + std::max(splits, 1) - 1) / std::max(splits, 1);
-    gp.tile_start[i] = tiles;
-    tiles += ((gp.p[i].M + 63) / 64) * ((gp.p[i].N + 63) / 64);
-  }
-  for (int i = n; i <= WG_MAX; ++i) gp.tile_start[i] = tiles;
-  constexpr int lds = 4 * (64 * 128 + 64 * 128);
-  if (splits == 0) {  // 8-wave two-half kernel (no atomics)
-    static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_wgrad_group8_kernel<4>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 2 * lds) == hipSuccess;
-    (void)attr;
-    hipLaunchKernelGGL(gemm_wgrad_group8_kernel<4>, dim3(tiles), dim3(512), 2 * lds, stream, gp);
-    return;
-  }
-  // LDS-DMA ring depth (DDIM_COLD_WGRAD_S = 4 / 6 / 8): the token-reduction loop
-  // is bound by operand bytes in flight per CU
-  static const int ring = [] {
-    const char* e = getenv("DDIM_COLD_WGRAD_S");
-    const int v = e ? atoi(e) : 4;
-    return v >= 8 ? 8 : v >= 6 ? 6 : 4;
-  }();
-  const int slds = ring * (64 * 128 + 64 * 128);
-  auto go = [&](auto kern) {
-    static_assert(true, "");
-    if (slds > 65536)
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, slds);
-    hipLaunchKernelGGL(kern, dim3(tiles, 1, std::max(splits, 1)), dim3(256), slds, stream, gp);
-  };
-  if (splits == 1) {
-    if (ring == 8) go(gemm_wgrad_group_kernel<EPI_ACC, 8>);
-    else if (ring == 6) go(gemm_wgrad_group_kernel<EPI_ACC, 6>);
-    else go(gemm_wgrad_group_kernel<EPI_ACC, 4>);
-  } else {
-    if (ring == 8) go(gemm_wgrad_group_kernel<EPI_ATOMIC, 8>);
-    else if (ring == 6) go(gemm_wgrad_group_kernel<EPI_ATOMIC, 6>);
-    else go(gemm_wgrad_group_kernel<EPI_ATOMIC, 4>);
-  }
-}

@@ -1,4 +1,4 @@
-// Shared gfx950 GEMM building blocks (gemm.hip, gemm_ln.hip): LDS image
+// Shared gfx950 GEMM building blocks (gemm.hip): LDS image
 // swizzles + fragment readers, the LDS-DMA operand loader (bounds-checked
 // `buffer_load ... lds` with the swizzle applied on the source address),
 // counted vmcnt waits, raw barriers and the XCD-aware block remap.

@@ -1,13 +1,13 @@
 // GEMM parameter block and the fused epilogue family (bias, LayerNorm fold
 // consumer/producer, QKV head-major scatter, residual + dropout + drop-path,
 // GELU, head / unpatchify / loss / DDIM update, patch embedding, gradient
-// accumulate), shared by the GEMM kernels (gemm.hip) and the image-group
-// persistent forward (vit_group.hip), so both produce bit-identical outputs.
+// accumulate), shared by every GEMM kernel of gemm.hip.
 //
-// ``PUB`` (VecEpi): the epilogue's hand-off outputs (bf16 residual copy,
-// LayerNorm statistics, GELU output) are stored write-through (sc1) and the
-// statistics it consumes are loaded sc1, for a consumer workgroup of the SAME
-// launch on another XCD (MI355X_MICROARCH.md, inter-workgroup visibility).
+// ``PUB`` (VecEpi, off in every current kernel): the epilogue's hand-off outputs
+// (bf16 residual copy, LayerNorm statistics, GELU output) are stored
+// write-through (sc1) and the statistics it consumes are loaded sc1, for a
+// consumer workgroup of the SAME launch on another XCD (MI355X_MICROARCH.md,
+// inter-workgroup visibility).
 #pragma once
 #include "common.h"
 #include "kernels.h"
@@ -54,10 +54,13 @@ struct GemmParams {
   const int64_t* tsteps;
   int emb_dim;
   int ktiles_per_split;
-  const float* coef;     // HEAD mode 1: {sqrt a_t, sqrt(1-a_t), sqrt a_tk, sqrt(1-a_tk)} (device)
+  const float* coef;     // HEAD mode 1: {sqrt a_t, sqrt(1-a_t), sqrt a_tk, sqrt(1-a_tk)} (device);
+                         //   mode 4: one such row per sample ([batch][4])
   long long split_stride;  // EPI_F32: elements between the K-split output slices
   int head_mode;         // HEAD: 0 image, 1 fused DDIM step (res = x_t in, C = x_next, C2 = x0), 2 clamp,
-                         //   3 training loss (res = target image, C2 = token-layout grad, loss_parts)
+                         //   3 training loss (res = target image, C2 = token-layout grad, loss_parts),
+                         //   4 DDIM step with per-sample coefficients (img2img: a sample that has
+                         //     not reached its start step has the row {0, 1, 0, 1}: x_next = x_t)
   float loss_beta;       // HEAD mode 3: smooth-L1 beta and 1/numel
   float loss_inv_n;
   float* loss_parts;     // HEAD mode 3: one loss partial per workgroup (gridDim.x entries)
@@ -227,7 +230,7 @@ __device__ __forceinline__ float epilogue(const GemmParams& p, long long idx, in
       return (ad < b ? 0.5f * d * d / b : ad - 0.5f * b) * p.loss_inv_n;
     } else {
       // the sampler's x0-hat clamp (ViT.py:229, ViT_draft2drawing.py:280), and for
-      // mode 1 the whole DDIM update (ViT.py:230-234) with x_t preloaded in `pre`
+      // modes 1 / 4 the whole DDIM update (ViT.py:230-234) with x_t preloaded in `pre`
       const float x0 = fminf(fmaxf(v, -1.f), 1.f);
       if (p.head_mode == 2) {
         reinterpret_cast<float*>(p.C)[idx] = x0;
@@ -255,7 +258,8 @@ template <int EPI, int FM, int FN>
 __device__ __forceinline__ void run_epilogue_scalar(const GemmParams& p, const f32x4 (&acc)[FM][FN], int mb, int nb,
                                              int g, int li) {
   constexpr bool ELEM = EPI == EPI_RESID || EPI == EPI_DGELU || EPI == EPI_EMBED || EPI == EPI_ACC;
-  const bool head_ddim = EPI == EPI_HEAD && p.head_mode == 1;
+  const bool head_ps = EPI == EPI_HEAD && p.head_mode == 4;  // per-sample coefficient rows
+  const bool head_ddim = EPI == EPI_HEAD && (p.head_mode == 1 || head_ps);
   const bool head_loss = EPI == EPI_HEAD && p.head_mode == 3;
   RowInfo rows[FM][4];
   long long cols[FN];
@@ -323,7 +327,7 @@ __device__ __forceinline__ void run_epilogue_scalar(const GemmParams& p, const f
   if (p.thr_drop) salt_drop = site_salt(p.rng, p.site_drop);
   if (p.thr_dp) salt_dp = site_salt(p.rng, p.site_dp);
   f32x4 cf = f32x4{0.f, 1.f, 0.f, 0.f};
-  if (head_ddim) cf = f32x4{p.coef[0], p.coef[1], p.coef[2], p.coef[3]};
+  if (head_ddim && !head_ps) cf = f32x4{p.coef[0], p.coef[1], p.coef[2], p.coef[3]};
   float2 ms[FM][4];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -362,13 +366,15 @@ __device__ __forceinline__ void run_epilogue_scalar(const GemmParams& p, const f
       for (int r = 0; r < 4; ++r)
         if (rows[i][r].off >= 0 && colok[j]) {
           const float a = fold ? (acc[i][j][r] - ms[i][r].x * colc[j]) * ms[i][r].y : acc[i][j][r];
+          const float* cs = p.coef + 4 * rows[i][r].b;  // mode 4: this row's sample
+          const f32x4 cfr = head_ps ? f32x4{cs[0], cs[1], cs[2], cs[3]} : cf;
           const float o = epilogue<EPI>(p, rows[i][r].off + cols[j], rows[i][r].b, a + colb[j], pre[i][j][r],
-                                        salt_drop, salt_dp, cf);
+                                        salt_drop, salt_dp, cfr);
           if (prod) {
             part[i][r][j / 2] = f2add(part[i][r][j / 2], make_float2(o, o * o));
             p.xb_out[rows[i][r].off + cols[j]] = f2bf(o);
           }
-          if (EPI == EPI_HEAD && p.patch_out != nullptr && (p.head_mode == 1 || p.head_mode == 2)) {
+          if (EPI == EPI_HEAD && p.patch_out != nullptr && (p.head_mode == 1 || p.head_mode == 2 || head_ps)) {
             // the new image pixel (c, a, b) of patch row (sample, token - 1), conv-im2col order
             const int m = mb + i * 16 + 4 * g + r, n = nb + j * 16 + li;
             const int c = n % p.chans, ab = n / p.chans;

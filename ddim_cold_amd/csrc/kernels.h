@@ -74,41 +74,9 @@ void gemm_nt(const GemmArgs& a, int epi, hipStream_t stream);
 int gemm_nt_grid(int M, int N, int K);
 void gemm_dgrad(const GemmArgs& a, int epi, hipStream_t stream);
 void gemm_wgrad(const GemmArgs& a, int splits, hipStream_t stream);
-// grouped dW += dy^T x for n <= 6 problems in one launch; splits == 1 -> plain
-// read-add-write (one writer per element), else fp32 atomics over token slices
-void gemm_wgrad_group(const GemmArgs* probs, int n, int splits, hipStream_t stream);
-// dgrad (EPI_BF16 / EPI_F32 with a.splits K slices, or EPI_DGELU) carrying n <= 6
-// weight-gradient problems (dW += dy^T x, fp32 atomics over wsplits token slices)
-// as extra workgroups of the same launch
-void gemm_dgrad_ride(const GemmArgs& a, int epi, const GemmArgs* probs, int n, int wsplits, hipStream_t stream);
 // every weight gradient of a step (n <= 32 problems) in one launch, unsplit (plain read-add-write)
 // store: every target is zero on entry (plain stores instead of read-add-write)
 void gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool store = false);
-
-// Row-panel GEMM + residual + LayerNorm epilogue (gemm_ln.hip)
-struct GemmLnArgs {
-  const void* A = nullptr;      // [M][K] bf16
-  const void* W = nullptr;      // [D][K] bf16
-  int M = 0, K = 0, D = 0;
-  const float* bias = nullptr;  // [D]
-  const float* res = nullptr;   // [M][D] residual stream in
-  float* x_out = nullptr;       // [M][D] residual stream out
-  const float* gamma = nullptr;
-  const float* beta = nullptr;
-  void* ln_out = nullptr;       // [M][D] bf16
-  float* mean = nullptr;
-  float* rstd = nullptr;
-  float eps = 1e-5f;
-  int tokens = 1;
-  const int64_t* rng = nullptr;
-  int site_drop = 0;
-  double p_drop = 0.0;
-  int site_dp = 0;
-  double p_dp = 0.0;
-  int bm = 32;                  // row-panel height (32 or 64)
-};
-bool gemm_resid_ln_supported(int D, int K);
-void gemm_resid_ln(const GemmLnArgs& a, hipStream_t stream);
 
 // LayerNorm (layernorm.hip)
 void layernorm_fwd_launch(const float* x, const float* gamma, const float* beta, void* y_bf16, float* mean,
@@ -161,7 +129,7 @@ void replica_reduce_launch(float* ws, float* const* dsts_dev, int G, int C, hipS
 // (ignored by the long-sequence kernels, which always regenerate)
 int64_t attn_keep_words(int B, int H, int N, int hd);
 void attn_set_stamps(void* buf);
-void ln_set_stamps(void* buf);  // profiling: [grid][5] phase stamps of the LayerNorm backward (nullptr: off)  // profiling: [grid][4] phase stamps of the short backward (nullptr: off)
+void ln_set_stamps(void* buf);  // profiling: [grid][5] phase stamps of the LayerNorm backward (nullptr: off)
 void attn_fwd_launch(const void* qkv, void* o, float* lse, int B, int H, int N, int hd, float scale,
                      const int64_t* rng, int site, double p, hipStream_t stream, uint32_t* keep_bits = nullptr);
 void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const float* lse, void* dqkv,
@@ -233,61 +201,33 @@ void wire_unpack_launch(const void* src, float* dst, int64_t n, hipStream_t stre
 void flag_bump_launch(void* flags, int k, hipStream_t stream);  // flags[k] += 1, system-scope release
 void flag_wait_launch(const void* flags, int k, unsigned int expected, void* err, hipStream_t stream);
 
-// attention backward with the proj Linear's input gradient fused in (short path):
-// dO = gy @ Wp computed per head inside the kernel (gy [B*N][Dm], Wp [Dm][Dm])
-bool attn_bwd_proj_supported(int N, int hd, int Dm);
-void attn_bwd_proj_launch(const void* gy, const void* wp, int Dm, const void* qkv, const void* o, const float* lse,
-                          void* dqkv, int B, int H, int N, int hd, float scale, const int64_t* rng, int site,
-                          double p, hipStream_t stream);
-
-// fused QKV projection + short-sequence attention (attention.hip), hd 32, 64 < N <= 128
-struct QkvArgs {
-  const void* x = nullptr;      // [B*N][D] bf16
-  const void* w = nullptr;      // [3D][D] bf16
-  const float* bias = nullptr;  // [3D]
-  const float* c = nullptr;     // [3D] (LayerNorm fold) or null
-  const float* st = nullptr;    // [B*N][D/32][2] (LayerNorm fold) or null
+// Fused MLP block (mlp.hip): x_out = x1 + DropPath(Dropout(fc2(Dropout(GELU(LN(x1) W1^T + b1)))))
+// with the LayerNorm folded in (w1 = bf16(gamma o W1), c1 = its row sums, b1 = b + W1 beta;
+// LN statistics from st_in = {sum, sum^2} per 32-column slot of the xb rows)
+struct MlpArgs {
+  const void* xb = nullptr;       // [M][D] bf16 copy of x1 (the LayerNorm input)
+  const float* x1 = nullptr;      // [M][D] fp32 residual stream in
+  const float* st_in = nullptr;   // [M][D/32][2]
+  const void* w1 = nullptr;       // [H][D] bf16 (gamma-folded)
+  const float* c1 = nullptr;      // [H]
+  const float* b1 = nullptr;      // [H] (folded bias)
+  const void* w2 = nullptr;       // [D][H] bf16
+  const float* b2 = nullptr;      // [D]
   float eps = 1e-5f;
-  float* mean = nullptr;
-  float* rstd = nullptr;
-  void* qkv = nullptr;          // [3][B][H][N][hd] or null
-  void* out = nullptr;          // [B][N][D]
-  float* lse = nullptr;         // [B][H][N] or null
-  int B = 0, H = 0, N = 0, hd = 0, D = 0;
-  float scale = 1.f;
+  int M = 0, D = 0, H = 0, tokens = 1;
   const int64_t* rng = nullptr;
-  int site = 0;
-  double p = 0.0;
+  int site_f1 = 0, site_f2 = 0, site_dp = 0;
+  uint32_t thr_f1 = 0, thr_f2 = 0, thr_dp = 0;
+  float sc_f1 = 1.f, sc_f2 = 1.f, sc_dp = 1.f;
+  float* x_out = nullptr;         // [M][D] fp32
+  void* xb_out = nullptr;         // [M][D] bf16
+  float* st_out = nullptr;        // [M][D/32][2]
+  void* u_out = nullptr;          // [M][H] bf16 pre-GELU (training; null: eval kernel)
+  void* h_out = nullptr;          // [M][H] bf16 post-GELU + dropout (training)
+  float* mean_out = nullptr;      // [M] LayerNorm mean / rstd (training)
+  float* rstd_out = nullptr;
+  int bm = 0;                     // row-panel height 16 / 32 / 64 (0: by M)
 };
-bool qkv_attn_supported(int N, int hd, int D);
-void qkv_attn_fwd_launch(const QkvArgs& a, hipStream_t stream);
-
-// Image-group persistent forward of all transformer blocks (vit_group.hip):
-// D = 384, 12 heads of 32, N <= 80 tokens, LayerNorm-folded weights; one
-// launch (per <= CUs/6 images) replaces the 5 launches per block.
-constexpr int VG_MAXL = 8;
-struct VgBlock {
-  const void *qkv_wf = nullptr, *proj_w = nullptr, *fc1_wf = nullptr, *fc2_w = nullptr;  // bf16
-  const float *qkv_bf = nullptr, *qkv_c = nullptr, *proj_b = nullptr, *fc1_bf = nullptr, *fc1_c = nullptr,
-              *fc2_b = nullptr;
-  const void* xb_in = nullptr;      // [M][D] bf16 residual copy (block input)
-  const float* st_in = nullptr;     // [M][D/32][2] its LayerNorm statistics slots
-  const float* x_in = nullptr;      // [M][D] fp32 residual stream (block input)
-  void *qkv = nullptr, *o = nullptr, *x1b = nullptr, *u = nullptr, *h = nullptr, *xb_out = nullptr;  // bf16
-  float *lse = nullptr, *x1 = nullptr, *st1 = nullptr, *x_out = nullptr, *st_out = nullptr;
-  float *m1 = nullptr, *r1 = nullptr, *m2 = nullptr, *r2 = nullptr;  // optional (saved for the backward)
-  int site_a = 0, site_p = 0, site_d1 = 0, site_f1 = 0, site_f2 = 0, site_d2 = 0;
-  double p_dp = 0.0;
-};
-struct VgArgs {
-  VgBlock blk[VG_MAXL];
-  int L = 0, B = 0, N = 0, D = 0, H = 0, hd = 0;
-  const int64_t* rng = nullptr;
-  double p_drop = 0.0, p_attn = 0.0;
-  float scale = 1.f, eps = 1e-5f;
-  unsigned* ctr = nullptr;  // [B * 16] hand-off counters (zeroed by the launcher)
-  unsigned* err = nullptr;  // set to nonzero if a hand-off wait gave up
-  void* stamps = nullptr;   // optional int64 [grid][VG_MAXL][16] phase timestamps (profiling)
-};
-bool vit_group_supported(int D, int H, int hd, int N, int L);
-void vit_group_fwd_launch(const VgArgs& a, hipStream_t stream);
+bool mlp_fused_supported(int D, int H);
+int mlp_fused_bm(int M);
+void mlp_fused_launch(const MlpArgs& a, hipStream_t stream);

@@ -16,16 +16,14 @@ if the weights they read were reallocated.
 Sampling always runs the denoiser in eval mode (no dropout); the reference's
 ``ViT.py`` CLI forgot ``model.eval()``.
 
-Concurrent chains (option): the samples of a batch never interact, so the
-batch can be split into ``streams`` chunks whose whole chains run on separate
-HIP streams, forked once at the start of the captured loop and joined once at
-the end.  Measured on MI355X (ViT-tiny, N=64, k=20, graph-captured): 1 chain
-46.9 ms, 2 chains 56.2, 4 chains 76.2 — the graph's parallel branches do not
-overlap, so the default is one chain (``DDIM_COLD_SAMPLER_STREAMS`` overrides).
+Every step is ONE forward whose head-GEMM epilogue applies the step (DDIM
+update, cold clamp, or img2img's DDIM update with per-sample coefficients) and
+hands the next step its bf16 patch rows.  (Splitting a batch into concurrent
+chains on separate streams measured slower on MI355X -- ViT-tiny N=64 k=20:
+46.9 / 56.2 / 76.2 ms for 1 / 2 / 4 chains -- and was removed.)
 """
 from __future__ import annotations
 
-import contextlib
 import math
 import os
 import time
@@ -105,43 +103,11 @@ def _patch_rows(model, N: int, device, den) -> Optional[torch.Tensor]:
     return torch.empty(N * (H // p) * (W // p), model.in_chans * p * p, dtype=torch.bfloat16, device=device)
 
 
-def _chain_patches(pbuf, sl, NP: int, first: bool):
+def _chain_patches(pbuf, first: bool):
+    """(patches_in, patches_out) of one step: the first step patchifies x itself."""
     if pbuf is None:
         return None
-    rows = pbuf[(sl.start or 0) * NP:(sl.stop if sl.stop is not None else pbuf.shape[0] // NP) * NP]
-    return (None if first else rows, rows)
-
-
-def default_streams(N: int, device) -> int:
-    env = os.environ.get("DDIM_COLD_SAMPLER_STREAMS")
-    if env:
-        return max(1, int(env))
-    return 1
-
-
-class _Chains:
-    """Split a batch into independent chains, each on its own stream (fork/join around the whole loop)."""
-
-    def __init__(self, N: int, device, streams: int):
-        n = max(1, min(streams, N))
-        bounds = [N * c // n for c in range(n + 1)]
-        self.slices = [slice(bounds[c], bounds[c + 1]) for c in range(n)]
-        cuda = device.type == "cuda" and n > 1
-        self.streams = [torch.cuda.Stream(device=device) for _ in range(n)] if cuda else [None] * n
-        self.device = device
-
-    def run(self, chain):
-        """``chain(sl)`` issues the whole loop for batch slice ``sl``."""
-        main = torch.cuda.current_stream(self.device) if self.streams[0] is not None else None
-        for st in self.streams:
-            if st is not None:
-                st.wait_stream(main)
-        for sl, st in zip(self.slices, self.streams):
-            with (torch.cuda.stream(st) if st is not None else contextlib.nullcontext()):
-                chain(sl)
-        for st in self.streams:
-            if st is not None:
-                main.wait_stream(st)
+    return (None if first else pbuf, pbuf)
 
 
 def _cache(model) -> dict:
@@ -149,7 +115,12 @@ def _cache(model) -> dict:
 
 
 class _GraphLoop:
-    """Capture ``body()`` (a full sampling loop on static buffers) into one hipGraph."""
+    """Capture ``body()`` (a full sampling loop on static buffers) into one hipGraph.
+
+    The first :meth:`run` executes the body eagerly on a side stream (allocator and
+    kernel warm-up; its result is this call's result) and captures the graph;
+    every later run is one replay.  Loops are cached per model and shape
+    (:func:`_cache`), so a repeated call replays."""
 
     def __init__(self, body, device):
         self.body = body
@@ -167,16 +138,20 @@ class _GraphLoop:
                 self.body()  # warm-up (allocator, kernels); also produces this call's result
             torch.cuda.current_stream(self.device).wait_stream(s)
             from ..utils.observe import no_gc
+            # (a capture records the body without running it: the warm-up's
+            # outputs stay this call's result)
             g = torch.cuda.CUDAGraph()
-            with no_gc(), torch.cuda.graph(g):
+            with no_gc(), torch.cuda.graph(g, capture_error_mode="thread_local"):
                 self.body()
             self.graph = g
+            self.replays = 0
             return
         self.graph.replay()
+        self.replays += 1
 
 
 class DDIMSampler:
-    def __init__(self, model, device, k: int = 10, use_graph: bool = True, streams: Optional[int] = None):
+    def __init__(self, model, device, k: int = 10, use_graph: bool = True):
         self.model = model
         self.device = torch.device(device)
         self.k = k
@@ -186,11 +161,9 @@ class DDIMSampler:
         self.use_graph = use_graph and self.device.type == "cuda"
         self.H, self.W = model.img_size
         self.C = model.in_chans
-        self.streams = streams
 
     def _state(self, N: int, record: bool):
-        nstreams = self.streams or default_streams(N, self.device)
-        key = ("ddim", N, self.k, record, str(self.device), nstreams)
+        key = ("ddim", N, self.k, record, str(self.device))
         den = _Denoiser(self.model, self.device)
         cache = _cache(self.model)
         st = cache.get(key)
@@ -202,19 +175,16 @@ class DDIMSampler:
         tt = torch.tensor(self.ts, dtype=torch.int64, device=dev).unsqueeze(1).expand(-1, N).contiguous()
         traj = torch.zeros(len(self.ts), N, self.C, self.H, self.W, device=dev) if record else None
         coef = self.coef
-        chains = _Chains(N, dev, nstreams)
         pbuf = _patch_rows(self.model, N, dev, den)
-        NP = (self.H // self.model.patch_size) * (self.W // self.model.patch_size)
 
-        def chain(sl):
-            xs, x0s = x[sl], x0[sl]
+        def loop():
             for i in range(len(self.ts)):
                 # forward + clamp + DDIM update, one head epilogue
-                den.step_(xs, tt[i][sl], 1, x0s, coef[i], patches=_chain_patches(pbuf, sl, NP, i == 0))
+                den.step_(x, tt[i], 1, x0, coef[i], patches=_chain_patches(pbuf, i == 0))
                 if traj is not None:
-                    traj[i][sl].copy_(x0s)
+                    traj[i].copy_(x0)
 
-        st = {"key": den.key(), "x": x, "x0": x0, "traj": traj, "loop": _GraphLoop(lambda: chains.run(chain), dev)}
+        st = {"key": den.key(), "x": x, "x0": x0, "traj": traj, "loop": _GraphLoop(loop, dev)}
         cache[key] = st
         return st
 
@@ -255,10 +225,8 @@ class DDIMSampler:
 class ColdSampler:
     """Cold de-pixelation sampler: start from constant-colour images, x <- clamp(f(x, t)) for t = S..1."""
 
-    def __init__(self, model, device, use_graph: bool = True, steps: Optional[int] = None,
-                 streams: Optional[int] = None):
+    def __init__(self, model, device, use_graph: bool = True, steps: Optional[int] = None):
         self.model = model
-        self.streams = streams
         self.device = torch.device(device)
         self.steps = steps or cold_steps(model.img_size[1])
         self.use_graph = use_graph and self.device.type == "cuda"
@@ -266,8 +234,7 @@ class ColdSampler:
         self.C = model.in_chans
 
     def _state(self, N: int):
-        nstreams = self.streams or default_streams(N, self.device)
-        key = ("cold", N, self.steps, str(self.device), nstreams)
+        key = ("cold", N, self.steps, str(self.device))
         den = _Denoiser(self.model, self.device)
         cache = _cache(self.model)
         st = cache.get(key)
@@ -278,18 +245,15 @@ class ColdSampler:
         ts = list(range(self.steps, 0, -1))
         tt = torch.tensor(ts, dtype=torch.int64, device=dev).unsqueeze(1).expand(-1, N).contiguous()
         traj = torch.zeros(len(ts), N, self.C, self.H, self.W, device=dev)
-        chains = _Chains(N, dev, nstreams)
         pbuf = _patch_rows(self.model, N, dev, den)
-        NP = (self.H // self.model.patch_size) * (self.W // self.model.patch_size)
 
-        def chain(sl):
-            xs = x[sl]
+        def loop():
             for i in range(len(ts)):
                 # forward + clamp in the head epilogue
-                den.step_(xs, tt[i][sl], 2, patches=_chain_patches(pbuf, sl, NP, i == 0))
-                traj[i][sl].copy_(xs)
+                den.step_(x, tt[i], 2, patches=_chain_patches(pbuf, i == 0))
+                traj[i].copy_(x)
 
-        st = {"key": den.key(), "x": x, "traj": traj, "loop": _GraphLoop(lambda: chains.run(chain), dev)}
+        st = {"key": den.key(), "x": x, "traj": traj, "loop": _GraphLoop(loop, dev)}
         cache[key] = st
         return st
 
@@ -314,43 +278,58 @@ class ColdSampler:
         return [(init + 1) / 2] + [traj[i] for i in range(traj.shape[0])]
 
 
-@torch.no_grad()
-def ddim_from_starts(model, x: torch.Tensor, starts: Sequence[int], k: int, device=None,
-                     use_graph: bool = True) -> torch.Tensor:
-    """DDIM (jump ``k``) from per-sample start steps, all samples in ONE batch.
-
-    Sample i joins the shared descending grid at its own ``starts[i]`` (per-sample
-    activity masks); all starts must lie on one k-grid (``(max - s) % k == 0``).
-    Returns the final clamped x0-hat on the device, in [-1, 1].
-    """
-    device = torch.device(device) if device is not None else x.device
-    T = model.total_steps
-    B = x.shape[0]
+def starts_table(total_steps: int, starts: Sequence[int], k: int):
+    """(descending grid ts, [len(ts), B, 4] per-sample DDIM coefficients) for samples
+    joining one k-grid at their own start steps; a sample whose start is below
+    step t has the identity row {0, 1, 0, 1} there (x_next = x_t exactly)."""
     top = max(starts)
     if any((top - s) % k for s in starts):
         raise ValueError("all start steps must share one k-grid")
     ts = list(range(top, 0, -k))
     if ts[-1] + 1 - k < 0:
         raise ValueError(f"k={k} incompatible with t_start={top}")
-    x = x.to(device).float().contiguous()
-    x0 = torch.zeros_like(x)
-    st = torch.tensor(list(starts), device=device)
-    tt = torch.tensor(ts, dtype=torch.int64, device=device).unsqueeze(1).expand(-1, B).contiguous()
-    active = torch.stack([(st >= t) for t in ts]).view(len(ts), B, 1, 1, 1)
-    coef = torch.tensor([ddim_coefficients(T, t, k) for t in ts], dtype=torch.float32, device=device)
+    ident = (0.0, 1.0, 0.0, 1.0)
+    rows = [[ddim_coefficients(total_steps, t, k) if s >= t else ident for s in starts] for t in ts]
+    return ts, torch.tensor(rows, dtype=torch.float32)
+
+
+@torch.no_grad()
+def ddim_from_starts(model, x: torch.Tensor, starts: Sequence[int], k: int, device=None,
+                     use_graph: bool = True) -> torch.Tensor:
+    """DDIM (jump ``k``) from per-sample start steps, all samples in ONE batch.
+
+    Sample i joins the shared descending grid at its own ``starts[i]``; all starts
+    must lie on one k-grid (``(max - s) % k == 0``).  Every step is ONE forward
+    whose head epilogue applies the update with per-sample coefficients
+    (:func:`ops.head_step_` mode 4: not-yet-started samples get the identity row),
+    and the whole loop is one hipGraph, cached per (B, starts, k): a repeated
+    call is one replay.  Returns the final clamped x0-hat on the device, in [-1, 1].
+    """
+    device = torch.device(device) if device is not None else x.device
+    T = model.total_steps
+    B = x.shape[0]
+    starts = [int(s) for s in starts]
+    key = ("img2img", B, tuple(starts), k, str(device))
     den = _Denoiser(model, device)
-    chains = _Chains(B, device, default_streams(B, device))
+    cache = _cache(model)
+    st = cache.get(key)
+    if st is None or st["key"] != den.key():
+        ts, coef = starts_table(T, starts, k)
+        coef = coef.to(device)
+        xs = torch.zeros(B, model.in_chans, *model.img_size, device=device)
+        x0 = torch.zeros_like(xs)
+        tt = torch.tensor(ts, dtype=torch.int64, device=device).unsqueeze(1).expand(-1, B).contiguous()
+        pbuf = _patch_rows(model, B, device, den)
 
-    def chain(sl):
-        xs, x0s = x[sl], x0[sl]
-        for i in range(len(ts)):
-            x0_raw = den(xs, tt[i][sl])
-            xn, x0c = ops.ddim_step(xs, x0_raw, coef[i])
-            torch.where(active[i][sl], xn, xs, out=xs)
-            torch.where(active[i][sl], x0c, x0s, out=x0s)
+        def loop():
+            for i in range(len(ts)):
+                den.step_(xs, tt[i], 4, x0, coef[i], patches=_chain_patches(pbuf, i == 0))
 
-    _GraphLoop(lambda: chains.run(chain), device).run(use_graph and device.type == "cuda")
-    return x0
+        st = {"key": den.key(), "x": xs, "x0": x0, "loop": _GraphLoop(loop, device)}
+        cache[key] = st
+    st["x"].copy_(x.to(device).float())
+    st["loop"].run(use_graph and device.type == "cuda")
+    return st["x0"]
 
 
 @torch.no_grad()
@@ -363,8 +342,9 @@ def img2img(model, draft: torch.Tensor, t_starts: Sequence[int] = tuple(range(15
     jump k down to the grid's last step; returns the final x0-hat per t_start
     as CPU images in [0, 1], shape [len(t_starts), C, H, W].
 
-    All t_starts on one k-grid run as ONE batch with per-sample activity masks
-    (the reference loops them one at a time at batch 1).
+    All t_starts on one k-grid run as ONE batch, each sample joining the shared
+    step grid at its own start (the reference loops them one at a time at batch
+    1); the loop is one cached hipGraph (:func:`ddim_from_starts`).
     """
     device = torch.device(device) if device is not None else next(model.parameters()).device
     T = model.total_steps
@@ -382,7 +362,13 @@ def img2img(model, draft: torch.Tensor, t_starts: Sequence[int] = tuple(range(15
         return torch.cat([img2img(model, draft[i:i + 1], [s], k, device, generator, use_graph)
                           for i, s in enumerate(starts)])
     eps = torch.normal(0.0, 1.0, (B, C, H, W), generator=generator).to(device)
-    alpha = torch.tensor([img2img_alpha(s, T) for s in starts], device=device).view(B, 1, 1, 1)
-    x = torch.sqrt(1 - alpha) * eps + torch.sqrt(alpha) * draft
+    x = img2img_noised(draft, eps, starts, T)
     x0 = ddim_from_starts(model, x, starts, k, device, use_graph)
     return (x0.cpu() + 1) / 2
+
+
+def img2img_noised(draft: torch.Tensor, eps: torch.Tensor, starts: Sequence[int], total_steps: int) -> torch.Tensor:
+    """x = sqrt(1-a) eps + sqrt(a) draft per start step, a = 1 - sqrt(t_start/T)
+    (ViT_draft2drawing.py:395-396)."""
+    alpha = torch.tensor([img2img_alpha(s, total_steps) for s in starts], device=draft.device).view(-1, 1, 1, 1)
+    return torch.sqrt(1 - alpha) * eps + torch.sqrt(alpha) * draft

@@ -30,7 +30,6 @@ import torch
 from .. import ops
 
 SITE_EMBED = 1
-FUSE_LN = os.environ.get("DDIM_COLD_FUSE_LN", "0") == "1"  # residual GEMM + LayerNorm in one kernel
 # K split of the QKV input-gradient GEMM (reduction dim 3D): the partial products
 # go to separate buffers that the LayerNorm backward sums on load
 QKV_DGRAD_SPLITS = int(os.environ.get("DDIM_COLD_QKV_DGRAD_SPLITS", "2"))
@@ -44,33 +43,11 @@ DGRAD_BF16 = os.environ.get("DDIM_COLD_DGRAD_BF16", "1") == "1"
 # producing GEMM's epilogue accumulates the row statistics; the LayerNorm
 # backward re-emits the normalised rows for the weight gradients.
 FOLD_LN = os.environ.get("DDIM_COLD_LN_FOLD", "1") == "1"
-# QKV projection + attention of a head in one kernel for 64 < N <= 128, hd 32
-# (csrc/attention.hip qkv_attn_fwd_kernel).  Measured on MI355X (ViT-tiny):
-# 19.4 us vs 12.3 + 6.4 us for QKV GEMM + attention at B=32 and 22.9 vs
-# 15.3 + 6.1 at the sampler's N=64 -- no better as a kernel, and the step /
-# sampler graphs get 1.5 % slower -> opt-in (DDIM_COLD_QKV_ATTN=1).
-FUSE_QKV_ATTN = os.environ.get("DDIM_COLD_QKV_ATTN", "0") == "1"
-# Weight gradients ride in the input-gradient launches (csrc/gemm.hip
-# gemm_dgrad_ride_kernel): fc2 (+ head) with the GELU' dgrad, the next block's
-# QKV with the fc1 dgrad, fc1 with the proj dgrad, proj with the QKV dgrad; only
-# block 0's QKV (+ patch embedding) keeps a grouped launch of its own.
-WGRAD_RIDE = os.environ.get("DDIM_COLD_WGRAD_RIDE", "1") == "1"
-# All transformer blocks of the LayerNorm-folded forward as ONE persistent
-# launch of image groups (csrc/vit_group.hip; ViT-tiny shape) instead of 5
-# launches per block.  Same math, bit-identical outputs (tests/test_group_fwd_gpu.py).
-# Measured on MI355X (tools/vg_stamps.py, tools/gpu_group_ab.sh): ~40 us per
-# block at B=32 -- each of the 4 hand-offs per block costs ~1 us wait + ~2.8 us
-# gather of the 50 KB activation panel through memory + the write-through
-# drain, which eats the launch overhead it removes -- so the train step is
-# 0.890 vs 0.871 ms/step and the B=64 sampler (two launches: one 156 KiB-LDS
-# workgroup per CU) is slower too: opt-in (DDIM_COLD_GROUP_FWD=1).
-GROUP_FWD = os.environ.get("DDIM_COLD_GROUP_FWD", "0") == "1"
-# proj input gradient computed per head inside the short attention backward
-# (ops.attn_bwd_proj): one launch fewer per block, but each (b, h) workgroup
-# then runs a K = D GEMM before its attention math; measured slower than the
-# 390-workgroup dgrad + attention backward (0.836 vs 0.823 ms/step, 3
-# interleaved 1000-step pairs, tools/gpu_ap.sh): opt-in (DDIM_COLD_ATTN_PROJ=1)
-ATTN_PROJ = os.environ.get("DDIM_COLD_ATTN_PROJ", "0") == "1"
+# the MLP block (fc1 + GELU + dropout + fc2 + dropout + drop-path + residual) of the
+# LayerNorm-folded forward as ONE launch (csrc/mlp.hip: the hidden rows stay in LDS,
+# the weights stream through a deep LDS-DMA ring); DDIM_COLD_FUSED_MLP=0: the two
+# GEMM launches
+FUSED_MLP = os.environ.get("DDIM_COLD_FUSED_MLP", "1") != "0"
 # the short attention forward stores its dropout keep flags (one 32-bit word per
 # lane, 0.6 MB per block for ViT-tiny at B=32) and the backward reads them instead
 # of re-hashing 2 pairs per 4 probabilities (the mask hash was ~1.9 us of the
@@ -271,10 +248,6 @@ class Saved:
     rf: Optional[torch.Tensor] = None
 
 
-def immediate_wgrad(dy, x, dw, db):
-    ops.linear_wgrad(dy, x, dw, db)
-
-
 class ViTProgram:
     def __init__(self, cfg: ProgramConfig):
         self.cfg = cfg
@@ -320,12 +293,6 @@ class ViTProgram:
                                          c.patch)
         x = x.view(M, D)
         S = Saved(t=t, patches=patches) if save else None
-        # Each residual GEMM carries the LayerNorm that follows it (proj -> norm2,
-        # fc2 -> next block's norm1 / the final norm): ops.linear_residual_ln_fwd.
-        # Off by default: the row-panel kernel concentrates the epilogue traffic on
-        # M/32 workgroups and measured slower than GEMM + LayerNorm (15.5 vs 9.3 us
-        # at M=2080; profiles/README.md).  DDIM_COLD_FUSE_LN=1 enables it.
-        fuse = FUSE_LN and ops.residual_ln_fusable(D, D) and ops.residual_ln_fusable(D, c.hidden)
         l1, m1, r1 = ops.layernorm_fwd(x, P.blocks[0].n1w, P.blocks[0].n1b, c.eps)
         L = len(P.blocks)
         for i, bp in enumerate(P.blocks):
@@ -334,20 +301,12 @@ class ViTProgram:
             qkv = ops.qkv_fwd(l1, bp.qkv_w, bp.qkv_b, B, N, c.heads)
             o, lse = ops.attn_fwd(qkv, c.scale, rng, sa, ad)
             o = o.view(M, D)
-            if fuse:
-                x1, l2, m2, r2 = ops.linear_residual_ln_fwd(o, bp.proj_w, bp.proj_b, x0, bp.n2w, bp.n2b, c.eps, N,
-                                                            rng, sp, pd, sd1, dpr[i])
-            else:
-                x1 = ops.linear_residual_fwd(o, bp.proj_w, bp.proj_b, x0, N, rng, sp, pd, sd1, dpr[i])
-                l2, m2, r2 = ops.layernorm_fwd(x1, bp.n2w, bp.n2b, c.eps)
+            x1 = ops.linear_residual_fwd(o, bp.proj_w, bp.proj_b, x0, N, rng, sp, pd, sd1, dpr[i])
+            l2, m2, r2 = ops.layernorm_fwd(x1, bp.n2w, bp.n2b, c.eps)
             u, h = ops.linear_gelu_fwd(l2, bp.fc1_w, bp.fc1_b, rng, sf1, pd)
             nw, nb = (P.blocks[i + 1].n1w, P.blocks[i + 1].n1b) if i + 1 < L else (P.nw, P.nb)
-            if fuse:
-                x, ln_n, m_n, r_n = ops.linear_residual_ln_fwd(h, bp.fc2_w, bp.fc2_b, x1, nw, nb, c.eps, N, rng, sf2,
-                                                               pd, sd2, dpr[i])
-            else:
-                x = ops.linear_residual_fwd(h, bp.fc2_w, bp.fc2_b, x1, N, rng, sf2, pd, sd2, dpr[i])
-                ln_n, m_n, r_n = ops.layernorm_fwd(x, nw, nb, c.eps)
+            x = ops.linear_residual_fwd(h, bp.fc2_w, bp.fc2_b, x1, N, rng, sf2, pd, sd2, dpr[i])
+            ln_n, m_n, r_n = ops.layernorm_fwd(x, nw, nb, c.eps)
             if save:
                 S.blocks.append((x0, l1, m1, r1, qkv, o, lse, x1, l2, m2, r2, u, h))
             l1, m1, r1 = ln_n, m_n, r_n
@@ -396,37 +355,32 @@ class ViTProgram:
         def stats():
             return (torch.empty(M, dtype=torch.float32, device=dev),
                     torch.empty(M, dtype=torch.float32, device=dev)) if save else (None, None)
-        fused = FUSE_QKV_ATTN and ops.qkv_attn_supported(N, D // c.heads, D)
-        if (GROUP_FWD and not fused and dev.type == "cuda" and P.blocks[0].qkv_wf.dtype == torch.bfloat16
-                and c.hidden == D and ops.vit_group_ok(D, c.heads, D // c.heads, N, L)):
-            x, xb = self._blocks_group(P, x, xb, st, rng, B, pd, ad, dpr, S, stats)
-            blocks = ()
-        else:
-            blocks = enumerate(P.blocks)
-        for i, bp in blocks:
+        fused_mlp = FUSED_MLP and dev.type == "cuda" and ops.mlp_fused_ok(D, c.hidden)
+        for i, bp in enumerate(P.blocks):
             sa, sp, sd1, sf1, sf2, sd2 = block_sites(i)
             x0 = x
             m1, r1 = stats()
             fold = (st[2 * i], bp.qkv_c, c.eps, m1, r1)
-            if fused:
-                o, lse, qkv = ops.qkv_attn_fwd(xb, bp.qkv_wf, bp.qkv_bf, B, N, c.heads, c.scale, rng, sa, ad, save,
-                                               fold=fold)
-            else:
-                qkv = ops.qkv_fwd(xb, bp.qkv_wf, bp.qkv_bf, B, N, c.heads, fold=fold)
-                keep = ops.attn_keep_buffer(qkv, ad) if save and STORE_ATTN_KEEP else None
-                o, lse = ops.attn_fwd(qkv, c.scale, rng, sa, ad, keep_out=keep)
-                if save:
-                    S.keeps.append(keep)
+            qkv = ops.qkv_fwd(xb, bp.qkv_wf, bp.qkv_bf, B, N, c.heads, fold=fold)
+            keep = ops.attn_keep_buffer(qkv, ad) if save and STORE_ATTN_KEEP else None
+            o, lse = ops.attn_fwd(qkv, c.scale, rng, sa, ad, keep_out=keep)
+            if save:
+                S.keeps.append(keep)
             o = o.view(M, D)
             x1b = torch.empty(M, D, dtype=ACT_DTYPE, device=dev)
             x1 = ops.linear_residual_fwd(o, bp.proj_w, bp.proj_b, x0, N, rng, sp, pd, sd1, dpr[i],
                                          st_out=st[2 * i + 1], xb_out=x1b)
             m2, r2 = stats()
-            u, h = ops.linear_gelu_fwd(x1b, bp.fc1_wf, bp.fc1_bf, rng, sf1, pd,
-                                       fold=(st[2 * i + 1], bp.fc1_c, c.eps, m2, r2))
             xb = torch.empty(M, D, dtype=ACT_DTYPE, device=dev)
-            x = ops.linear_residual_fwd(h, bp.fc2_w, bp.fc2_b, x1, N, rng, sf2, pd, sd2, dpr[i],
-                                        st_out=st[2 * i + 2], xb_out=xb)
+            if fused_mlp:
+                x, u, h = ops.mlp_fused_fwd(x1b, x1, st[2 * i + 1], bp.fc1_wf, bp.fc1_c, bp.fc1_bf, bp.fc2_w,
+                                            bp.fc2_b, c.eps, N, rng, sf1, sf2, pd, sd2, dpr[i], save,
+                                            st[2 * i + 2], xb, m2, r2)
+            else:
+                u, h = ops.linear_gelu_fwd(x1b, bp.fc1_wf, bp.fc1_bf, rng, sf1, pd,
+                                           fold=(st[2 * i + 1], bp.fc1_c, c.eps, m2, r2))
+                x = ops.linear_residual_fwd(h, bp.fc2_w, bp.fc2_b, x1, N, rng, sf2, pd, sd2, dpr[i],
+                                            st_out=st[2 * i + 2], xb_out=xb)
             if save:
                 S.blocks.append((x0, None, m1, r1, qkv, o, lse, x1, None, m2, r2, u, h))
         if head_step is not None:
@@ -447,100 +401,43 @@ class ViTProgram:
             S.xL, S.lf, S.mf, S.rf = x, None, mf, rf
         return out, S
 
-    def _blocks_group(self, P: ModelTensors, x, xb, st, rng, B: int, pd: float, ad: float, dpr, S, stats):
-        """Every transformer block of the folded forward in ONE persistent launch
-        (:func:`ops.vit_group_fwd`, csrc/vit_group.hip): same tensors, same values
-        as the per-op sequence of :meth:`_forward_folded`.  Returns the last
-        block's (fp32 residual stream, bf16 copy)."""
-        c = self.cfg
-        N, D, L = c.tokens, c.dim, c.depth
-        M, dev = B * N, x.device
-        save = S is not None
-
-        def bf16(*shape):
-            return torch.empty(*shape, dtype=ACT_DTYPE, device=dev)
-
-        def f32(*shape):
-            return torch.empty(*shape, dtype=torch.float32, device=dev)
-        ts, sites, dps, saved = [], [], [], []
-        for i, bp in enumerate(P.blocks):
-            x0 = x
-            m1, r1 = stats()
-            m2, r2 = stats()
-            qkv = bf16(3, B, c.heads, N, D // c.heads)
-            o, lse = bf16(B, N, D), (f32(B, c.heads, N) if save else None)
-            x1, x1b, u, h = f32(M, D), bf16(M, D), bf16(M, c.hidden), bf16(M, c.hidden)
-            x, xb_new = f32(M, D), bf16(M, D)
-            ts += [bp.qkv_wf, bp.qkv_bf, bp.qkv_c, bp.proj_w, bp.proj_b, bp.fc1_wf, bp.fc1_bf, bp.fc1_c,
-                   bp.fc2_w, bp.fc2_b, xb, st[2 * i], x0,
-                   qkv if save else None, o, lse, x1, x1b, st[2 * i + 1], u, h, x, xb_new, st[2 * i + 2],
-                   m1, r1, m2, r2]
-            sites += list(block_sites(i))
-            dps.append(dpr[i])
-            if save:
-                saved.append((x0, None, m1, r1, qkv, o.view(M, D), lse, x1, None, m2, r2, u, h))
-            xb = xb_new
-        if getattr(self, "_vg_err", None) is None or self._vg_err.device != dev:
-            self._vg_err = torch.zeros(1, dtype=torch.int32, device=dev)
-        ctr = torch.empty(B * 16, dtype=torch.int32, device=dev)
-        ops.vit_group_fwd(ts, L, B, N, sites, dps, rng, pd, ad, c.scale, c.eps, ctr, self._vg_err,
-                          getattr(self, "vg_stamps", None))
-        if save:
-            S.blocks.extend(saved)
-        return x, xb
-
     def supports_fused_loss(self, P: ModelTensors) -> bool:
         return P.folded and fold_width_ok(self.cfg.dim)
 
     # ------------------------------------------------------------------ backward
     def backward_iter(self, P: ModelTensors, G: ModelTensors, S: Saved, dtok: torch.Tensor, rng: torch.Tensor,
                       training: bool = True, wgrad: Optional[Callable] = None,
-                      ln_ws: Optional[torch.Tensor] = None, wgrad_stream=None,
-                      embed_with_block0: bool = False, ln_final=None, wgrad_tail: bool = False,
+                      ln_ws: Optional[torch.Tensor] = None, embed_with_block0: bool = False, ln_final=None,
                       wgrad_flush=None, wgrad_store: bool = False) -> Iterator[int]:
-        """Hand-written backward; yields the block index after each block's grads
-        are issued (L-1 first, then ..., 0) and -1 after the embedding grads.
+        """Hand-written backward; yields the block index after each block's input
+        gradients are issued (L-1 first, then ..., 0) and -1 after the embedding grads.
 
-        ``G`` tensors are fp32 accumulators (``+=``).  By default the weight
-        gradients of each block (qkv, proj, fc1, fc2; plus the head with the
-        last block) are batched and issued as ONE grouped GEMM launch at the end
-        of the block (``ops.WgradBatch``); a ``wgrad`` callable instead issues
-        each one immediately (e.g. on a side stream).  ``ln_ws`` ([2L+1, R, 2D],
-        zero) collects LayerNorm dgamma/dbeta replicas in backward order (final
-        norm, then norm2/norm1 of blocks L-1..0); the caller finalises them
-        with ``ops.replica_reduce_``.  ``embed_with_block0``: the embedding
-        backward runs before block 0's weight gradients are issued, so the
-        patch-embedding weight gradient joins block 0's grouped launch (one
-        launch fewer; no separate gradient bucket for the embeddings then).
-        ``wgrad_tail`` (single process: nothing consumes a block's gradients
-        before the optimizer): EVERY weight gradient is queued and issued as one
-        launch after the embedding backward (:func:`ops.linear_wgrad_multi`), so
-        the block yields then only mark the order, not finished gradients.
-        ``wgrad_flush`` (a set of block indices; data parallel): weight
-        gradients are queued and issued as one launch per gradient bucket --
-        after each listed block (and after the embedding backward) -- so the
-        bucket's all-reduce can start while the rest of the backward runs.
-        ``wgrad_store``: the block / head weight-gradient targets have no other writer
-        this step, so the deferred launches (tail or per bucket) write instead of
+        ``G`` tensors are fp32 accumulators (``+=``).  Weight gradients are deferred:
+        by default EVERY ``dW += dy^T x`` of the backward (4 per block, head, patch
+        embedding) is queued and issued as ONE launch after the embedding backward
+        (:func:`ops.linear_wgrad_multi`; nothing reads a block's gradients before the
+        optimizer), so a block yield only marks the order.  ``wgrad_flush`` (a set of
+        block indices; data parallel): one such launch per gradient bucket -- after
+        each listed block and after the embedding backward -- so the bucket's
+        all-reduce can start while the rest of the backward runs.  A ``wgrad``
+        callable instead receives each job as soon as its operands exist.
+        ``ln_ws`` ([2L+1, R, 2D], zero) collects LayerNorm dgamma/dbeta replicas in
+        backward order (final norm, then norm2/norm1 of blocks L-1..0); the caller
+        finalises them with ``ops.replica_reduce_`` (or ``ln_final``, carried by the
+        embedding-backward launch).  ``embed_with_block0``: the embedding backward
+        runs before block 0's weight gradients are flushed (no separate embedding
+        bucket).  ``wgrad_store``: the block / head weight-gradient targets have no
+        other writer this step, so the deferred launches write instead of
         read-add-writing them (the embedding bucket's patch gradient still adds).
-        """
+        Measured slower on MI355X and removed: weight gradients riding in the
+        input-gradient launches, one grouped launch per block, a side-stream branch
+        for them, the proj input gradient inside the attention backward."""
         def ws(k):
             return None if ln_ws is None else ln_ws[k]
-        # weight gradients ride in the next input-gradient launch (default), unless
-        # the caller supplies its own wgrad callable or a side stream
-        bucketed = wgrad_flush is not None and wgrad is None and wgrad_stream is None and not wgrad_tail
-        tail = (wgrad_tail or bucketed) and wgrad is None and wgrad_stream is None
-        ride = WGRAD_RIDE and wgrad is None and wgrad_stream is None and not tail
-        batch = None
-        tail_jobs = []
-        if tail:
-            wgrad = lambda dy, x, dw, db: tail_jobs.append((dy, x, dw, db))  # noqa: E731
-        elif wgrad is None:
-            batch = wgrad = ops.WgradBatch(wgrad_stream)
-
-        def flush():
-            if batch is not None:
-                batch.flush()
+        bucketed = wgrad is None and wgrad_flush is not None
+        jobs = []
+        if wgrad is None:
+            wgrad = lambda dy, x, dw, db: jobs.append((dy, x, dw, db))  # noqa: E731
         c = self.cfg
         N, D = c.tokens, c.dim
         pd = c.drop if training else 0.0
@@ -562,51 +459,25 @@ class ViTProgram:
         _, _, _, _, sf2, sd2 = block_sites(L - 1)
         g, gy = ops.layernorm_bwd(dlf, S.xL, S.mf, S.rf, P.nw, None, G.nw, G.nb, N, rng, sf2, pd, sd2,
                                   dpr[L - 1], True, ws(0), beta=P.nb if fold else None, y_out=lf if fold else None)
-        if ride:
-            riders = [(dtok, lf, G.head_w, G.head_b)]  # joins block L-1's first launch
-            qkv_job = None  # the previous block's QKV weight gradient (rides on the fc1 dgrad)
-        else:
-            wgrad(dtok, lf, G.head_w, G.head_b)
+        wgrad(dtok, lf, G.head_w, G.head_b)
         for i in range(L - 1, -1, -1):
             x0, l1, m1, r1, qkv, o, lse, x1, l2, m2, r2, u, h = S.blocks[i]
             bp, bg = P.blocks[i], G.blocks[i]
             sa, sp, sd1, sf1, _, _ = block_sites(i)
-            if ride:
-                du = ops.linear_dgrad_ride(gy, bp.fc2_w, riders + [(gy, h, bg.fc2_w, bg.fc2_b)],
-                                           gelu=(u, rng, sf1, pd))
-                dl2 = ops.linear_dgrad_ride(du, bp.fc1_w, [qkv_job] if qkv_job else [], f32)
-                if qkv_job is not None:
-                    yield i + 1  # block i+1's last weight gradient is issued
-                riders, qkv_job = [], None
-            else:
-                wgrad(gy, h, bg.fc2_w, bg.fc2_b)
-                du = ops.linear_dgrad_gelu(gy, bp.fc2_w, u, rng, sf1, pd)
-                dl2 = ops.linear_dgrad(du, bp.fc1_w, f32)
+            wgrad(gy, h, bg.fc2_w, bg.fc2_b)
+            du = ops.linear_dgrad_gelu(gy, bp.fc2_w, u, rng, sf1, pd)
+            dl2 = ops.linear_dgrad(du, bp.fc1_w, f32)
             k2 = 1 + 2 * (L - 1 - i)
             l2 = ln_out(l2)
             g1, gy1 = ops.layernorm_bwd(dl2, x1, m2, r2, bp.n2w, g, bg.n2w, bg.n2b, N, rng, sp, pd, sd1, dpr[i],
                                         True, ws(k2), beta=bp.n2b if fold else None, y_out=l2 if fold else None)
-            fuse_ap = ATTN_PROJ and dtok.is_cuda and ops.attn_bwd_proj_ok(N, D // c.heads, D)
-            riders_q = [(gy1, o, bg.proj_w, bg.proj_b)]
-            if ride and not fuse_ap:
-                do = ops.linear_dgrad_ride(gy1, bp.proj_w, [(du, l2, bg.fc1_w, bg.fc1_b)])
-            elif ride:
-                riders_q.append((du, l2, bg.fc1_w, bg.fc1_b))  # the proj dgrad launch is gone
-            else:
-                wgrad(du, l2, bg.fc1_w, bg.fc1_b)
-                wgrad(gy1, o, bg.proj_w, bg.proj_b)
-                if not fuse_ap:
-                    do = ops.linear_dgrad(gy1, bp.proj_w, False)
-            if fuse_ap:
-                dqkv = ops.attn_bwd_proj(gy1, bp.proj_w, qkv, o, lse, c.scale, rng, sa, ad)
-            else:
-                dqkv = ops.attn_bwd(do, qkv, o, lse, c.scale, rng, sa, ad,
-                                    keep=S.keeps[i] if len(S.keeps) == L else None)
+            wgrad(du, l2, bg.fc1_w, bg.fc1_b)
+            wgrad(gy1, o, bg.proj_w, bg.proj_b)
+            do = ops.linear_dgrad(gy1, bp.proj_w, False)
+            dqkv = ops.attn_bwd(do, qkv, o, lse, c.scale, rng, sa, ad,
+                                keep=S.keeps[i] if len(S.keeps) == L else None)
             qs = QKV_DGRAD_SPLITS if 3 * D >= 768 else 1
-            if ride:
-                dl1 = ops.linear_dgrad_ride(dqkv, bp.qkv_w, riders_q, f32, qs)
-            else:
-                dl1 = ops.linear_dgrad(dqkv, bp.qkv_w, f32, qs)
+            dl1 = ops.linear_dgrad(dqkv, bp.qkv_w, f32, qs)
             l1 = ln_out(l1)
             fk = dict(beta=bp.n1b, y_out=l1) if fold else {}
             if i > 0:
@@ -617,36 +488,29 @@ class ViTProgram:
                 g, gy = ops.layernorm_bwd(dl1, x0, m1, r1, bp.n1w, g1, bg.n1w, bg.n1b, N, rng, 0, 0.0, 0, 0.0,
                                           False, ws(k2 + 1), **fk)
             keep.append((gy1, du, dqkv, l1, l2))
-            if ride and i > 0:
-                qkv_job = (dqkv, l1, bg.qkv_w, bg.qkv_b)
-                continue
             wgrad(dqkv, l1, bg.qkv_w, bg.qkv_b)
             if i == 0 and embed_with_block0:
                 gpatch = self._embed_backward(P, G, S, g, rng, pd, wgrad, ln_final)
-            flush()
-            if bucketed and (i in wgrad_flush or (i == 0 and embed_with_block0)) and tail_jobs:
-                ops.linear_wgrad_multi(tail_jobs, store=wgrad_store)  # this bucket's weight gradients: final now
-                keep.append(tail_jobs)
-                tail_jobs = []
+            if bucketed and (i in wgrad_flush or (i == 0 and embed_with_block0)) and jobs:
+                ops.linear_wgrad_multi(jobs, store=wgrad_store)  # this bucket's weight gradients: final now
+                keep.append(jobs)
+                jobs = []
             yield i
         if not embed_with_block0:
             gpatch = self._embed_backward(P, G, S, g, rng, pd, wgrad, ln_final)
-            flush()
-        if tail and tail_jobs:
-            tiles = sum(-(-dy.shape[1] // 64) * -(-x.shape[1] // 64) for dy, x, _, _ in tail_jobs)
+        if jobs:
+            tiles = sum(-(-dy.shape[1] // 64) * -(-x.shape[1] // 64) for dy, x, _, _ in jobs)
             if bucketed and tiles < 64:
                 # the embedding bucket's patch-embedding gradient alone (18 tiles for
                 # ViT-tiny): unsplit, 18 workgroups walk all 2,048 tokens (~17 us on the
                 # step's critical path); the token-split kernel fills the chip
-                for job in tail_jobs:
+                for job in jobs:
                     ops.linear_wgrad(*job)
             else:
-                ops.linear_wgrad_multi(tail_jobs, store=wgrad_store and wgrad_tail)
-            keep.append(tail_jobs)
+                ops.linear_wgrad_multi(jobs, store=wgrad_store and not bucketed)
+            keep.append(jobs)
         keep.append((gpatch, lf))
-        if batch is not None:
-            keep.append(batch.keep)
-        self._keep = keep  # holds side-stream operands alive until the caller joins
+        self._keep = keep  # operands of the queued launches stay referenced until the next step
         yield -1
 
     def _embed_backward(self, P, G, S, g, rng, pd, wgrad, ln_final=None):

@@ -103,26 +103,6 @@ def qkv_fwd(a, w, b, B: int, N: int, H: int, fold=None):
     return ref.qkv_fwd(a, w, b, B, N, H, st, c, eps, mean, rstd)
 
 
-def qkv_attn_supported(N: int, hd: int, D: int) -> bool:
-    """Shapes the fused QKV + attention kernel covers (csrc/attention.hip)."""
-    return hd == 32 and 64 < N <= 128 and D in (256, 384, 512)
-
-
-def qkv_attn_fwd(a, w, b, B: int, N: int, H: int, scale: float, rng, site: int, p: float, save_qkv: bool,
-                 fold=None):
-    """Fused QKV projection + short attention, one workgroup per head:
-    ``(o [B,N,D], lse [B,H,N], qkv [3,B,H,N,hd] or None)``; ``fold = (ln_st, ln_c,
-    eps[, mean_out, rstd_out])`` folds the preceding LayerNorm in (see :func:`qkv_fwd`)."""
-    st, c, eps, mean, rstd = _fold_args(fold)
-    if _hip(a):
-        o, lse, qkv = _ops().qkv_attn_fwd(a, w, b, st, c, eps, B, N, H, float(scale), rng, site, float(p),
-                                          bool(save_qkv), mean, rstd)
-        return o, lse, (qkv if save_qkv else None)
-    qkv = ref.qkv_fwd(a, w, b, B, N, H, st, c, eps, mean, rstd)
-    o, lse = ref.attn_fwd(qkv, scale, rng, site, p)
-    return o, lse, (qkv if save_qkv else None)
-
-
 def attn_keep_buffer(qkv, p: float):
     """int32 buffer for the attention-dropout keep flags the short-sequence forward
     stores for its backward (one word per lane: no mask re-hashing there), or None
@@ -151,21 +131,6 @@ def linear_residual_fwd(a, w, b, x, N: int, rng, site_drop: int, p_drop: float, 
     return ref.linear_residual_fwd(a, w, b, x, N, rng, site_drop, p_drop, site_dp, p_dp, st_out, xb_out)
 
 
-def residual_ln_fusable(D: int, K: int) -> bool:
-    """Widths the row-panel GEMM + LayerNorm kernel is instantiated for (csrc/gemm_ln.hip)."""
-    return D in (256, 384, 512) and K % 64 == 0
-
-
-def linear_residual_ln_fwd(a, w, b, x, gamma, beta, eps: float, N: int, rng, site_drop: int, p_drop: float,
-                           site_dp: int, p_dp: float):
-    """(x_new, ln(x_new) bf16, mean, rstd) with x_new = x + DropPath(Dropout(a w^T + b)):
-    the residual GEMM and the following LayerNorm in one launch."""
-    if _hip(a):
-        return _ops().linear_residual_ln_fwd(a, w, b, x, gamma, beta, float(eps), N, rng, site_drop,
-                                             float(p_drop), site_dp, float(p_dp))
-    return ref.linear_residual_ln_fwd(a, w, b, x, gamma, beta, eps, N, rng, site_drop, p_drop, site_dp, p_dp)
-
-
 def linear_gelu_fwd(a, w, b, rng, site: int, p: float, fold=None):
     st, c, eps, mean, rstd = _fold_args(fold)
     if _hip(a):
@@ -173,10 +138,44 @@ def linear_gelu_fwd(a, w, b, rng, site: int, p: float, fold=None):
     return ref.linear_gelu_fwd(a, w, b, rng, site, p, st, c, eps, mean, rstd)
 
 
+def _ddim_coef(coef, x):
+    """4 DDIM coefficients as python floats (one row) or [B,1,1,1] tensors (one row per sample)."""
+    if coef.dim() == 2:
+        return [coef[:, i].reshape(-1, 1, 1, 1).to(x.dtype) for i in range(4)]
+    return [float(c) for c in coef.tolist()[:4]]
+
+
+def mlp_fused_ok(D: int, H: int) -> bool:
+    """Widths the fused MLP kernel covers (csrc/mlp.hip: D, H multiples of 128, D >= 256, <= 512)."""
+    return D % 128 == 0 and H % 128 == 0 and 256 <= D <= 512 and 128 <= H <= 512
+
+
+def mlp_fused_fwd(xb, x1, st_in, w1, c1, b1, w2, b2, eps: float, N: int, rng, site_f1: int, site_f2: int,
+                  p_drop: float, site_dp: int, p_dp: float, save: bool, st_out, xb_out, mean_out=None,
+                  rstd_out=None, bm: int = 0):
+    """The LayerNorm-folded MLP block in ONE launch (csrc/mlp.hip):
+    ``x = x1 + DropPath(Dropout(fc2(Dropout(GELU(LN(x1) W1^T + b1)))))`` with ``w1``/``c1``/``b1``
+    the folded fc1 (:class:`LnFold`) and ``st_in`` x1's row statistics.  Returns
+    ``(x, u, h)`` (``u``/``h``: pre-GELU / post-dropout activations for the backward,
+    None unless ``save``); ``st_out`` / ``xb_out`` get x's statistics slots and bf16 copy,
+    ``mean_out`` / ``rstd_out`` the LayerNorm's row statistics.  Same values as
+    :func:`linear_gelu_fwd` + :func:`linear_residual_fwd` (fp32 summation order aside)."""
+    if _hip(xb):
+        x, u, h = _ops().mlp_fused_fwd(xb, x1, st_in, w1, c1, b1, w2, b2, float(eps), int(N), rng, int(site_f1),
+                                       int(site_f2), float(p_drop), int(site_dp), float(p_dp), bool(save), st_out,
+                                       xb_out, mean_out, rstd_out, int(bm))
+        return x, (u if save else None), (h if save else None)
+    u, h = ref.linear_gelu_fwd(xb, w1, b1, rng, site_f1, p_drop, st_in, c1, eps, mean_out, rstd_out)
+    x = ref.linear_residual_fwd(h, w2, b2, x1, N, rng, site_f2, p_drop, site_dp, p_dp, st_out, xb_out)
+    return x, (u if save else None), (h if save else None)
+
+
 def head_step_(a, w, b, x, x0_out, coef, patch: int, mode: int, fold=None, patches_out=None):
     """Head GEMM + sampler step in its epilogue (in place on ``x``): mode 1 = clamp +
     DDIM update (``x0_out`` gets the clamped x0-hat; ``coef`` a device row of
-    ``ddim_coefficients``), mode 2 = clamp only (cold sampler).  ``patches_out``
+    ``ddim_coefficients``), mode 2 = clamp only (cold sampler), mode 4 = mode 1 with
+    one coefficient row per sample (``coef`` [B, 4]; img2img: the row {0, 1, 0, 1}
+    leaves a sample that has not reached its start step unchanged).  ``patches_out``
     (GPU): also the new ``x`` as bf16 patch rows, for the next step's
     :func:`patch_embed_fwd` (``patches_in``)."""
     st, c, eps, _, _ = _fold_args(fold)
@@ -187,7 +186,7 @@ def head_step_(a, w, b, x, x0_out, coef, patch: int, mode: int, fold=None, patch
     if mode == 2:
         x.copy_(torch.clamp(x0_raw, -1.0, 1.0))
         return
-    xn, x0 = ref.ddim_step(x, x0_raw, [float(v) for v in coef.tolist()[:4]])
+    xn, x0 = ref.ddim_step(x, x0_raw, _ddim_coef(coef, x))
     x.copy_(xn)
     x0_out.copy_(x0)
 
@@ -260,35 +259,6 @@ def linear_wgrad(dy, x, dw, db: Optional[torch.Tensor]):
     return ref.linear_wgrad(dy, x, dw, db)
 
 
-def linear_wgrad_group(jobs):
-    """``dW_i += dy_i^T x_i`` (and ``db_i += colsum(dy_i)``) for a list of
-    ``(dy, x, dw, db)`` jobs in ONE grouped launch (csrc/gemm.hip
-    ``gemm_wgrad_group_kernel``)."""
-    if not jobs:
-        return
-    if _hip(jobs[0][0]):
-        dys, xs, dws, dbs = (list(z) for z in zip(*jobs))
-        return _ops().linear_wgrad_group(dys, xs, dws, dbs)
-    for dy, x, dw, db in jobs:
-        ref.linear_wgrad(dy, x, dw, db)
-
-
-def attn_bwd_proj_ok(N: int, hd: int, D: int) -> bool:
-    """Shapes the fused proj-dgrad + short attention backward covers (csrc/attention.hip)."""
-    return _ext.available() and bool(_ops().attn_bwd_proj_ok(N, hd, D))
-
-
-def attn_bwd_proj(gy, wp, qkv, o, lse, scale: float, rng, site: int, p: float):
-    """:func:`attn_bwd` of ``dO = gy @ wp`` (the proj Linear's input gradient)
-    with that GEMM computed per head inside the attention-backward kernel on a
-    GPU (one launch fewer); elsewhere the two ops in sequence."""
-    B, H, N, hd = qkv.shape[1], qkv.shape[2], qkv.shape[3], qkv.shape[4]
-    if _hip(gy) and attn_bwd_proj_ok(N, hd, H * hd):
-        return _ops().attn_bwd_proj(gy, wp, qkv, o, lse, float(scale), rng, int(site), float(p))
-    do = linear_dgrad(gy, wp, False)
-    return attn_bwd(do, qkv, o, lse, scale, rng, site, p)
-
-
 def wire_pack(src, dst):
     """fp32 -> bf16 (round to nearest even) into ``dst`` (gradient wire format)."""
     if _hip(src):
@@ -301,38 +271,6 @@ def wire_unpack(src, dst):
     if _hip(src):
         return _ops().wire_unpack(src, dst)
     dst.copy_(src)
-
-
-def vit_group_ok(D: int, H: int, hd: int, N: int, L: int) -> bool:
-    """Shapes the image-group persistent block forward covers (csrc/vit_group.hip)."""
-    return _ext.available() and bool(_ops().vit_group_ok(D, H, hd, N, L))
-
-
-def vit_group_fwd(ts, L: int, B: int, N: int, sites, p_dp, rng, p_drop: float, p_attn: float, scale: float,
-                  eps: float, ctr, err, stamps=None):
-    """All transformer blocks of the LayerNorm-folded forward in one persistent
-    launch (GPU only; ``ts``: 28 tensors per block, see csrc/bindings.cpp).
-    ``stamps`` (int64 [B*6, 8, 16], optional): per-workgroup phase timestamps."""
-    _ops().vit_group_fwd(ts, L, B, N, [int(v) for v in sites], [float(v) for v in p_dp], rng, float(p_drop),
-                         float(p_attn), float(scale), float(eps), ctr, err, stamps)
-
-
-def linear_dgrad_ride(dy, w, jobs, out_fp32: bool = False, splits: int = 1, gelu=None):
-    """:func:`linear_dgrad` (or, with ``gelu = (u, rng, site, p)``,
-    :func:`linear_dgrad_gelu`) with the weight-gradient ``jobs`` (``(dy, x, dw,
-    db)`` as :func:`linear_wgrad_group`) riding in the SAME launch as extra
-    workgroups (csrc/gemm.hip ``gemm_dgrad_ride_kernel``)."""
-    if _hip(dy):
-        dys, xs, dws, dbs = (list(z) for z in zip(*jobs)) if jobs else ([], [], [], [])
-        if gelu is not None:
-            u, rng, site, p = gelu
-            return _ops().linear_dgrad_ride(dy, w, 1, False, 1, u, rng, int(site), float(p), dys, xs, dws, dbs)
-        return _ops().linear_dgrad_ride(dy, w, 0, bool(out_fp32), int(splits), None, None, 0, 0.0,
-                                        dys, xs, dws, dbs)
-    out = ref.linear_dgrad_gelu(dy, w, *gelu) if gelu is not None else ref.linear_dgrad(dy, w, out_fp32, splits)
-    for j in jobs:
-        ref.linear_wgrad(*j)
-    return out
 
 
 def linear_wgrad_multi(jobs, store: bool = False):
@@ -352,36 +290,6 @@ def linear_wgrad_multi(jobs, store: bool = False):
             if db is not None:
                 db.zero_()
         ref.linear_wgrad(dy, x, dw, db)
-
-
-class WgradBatch:
-    """Collects weight-gradient GEMMs and issues them as one grouped launch on ``flush``.
-
-    With ``stream`` the launch goes to that stream (forked from the current one),
-    so it can run beside the rest of the backward; the caller joins the stream
-    before anything reads the gradients.  Operands are kept referenced in
-    ``self.keep`` until the caller drops the batch.
-    """
-
-    def __init__(self, stream=None):
-        self.jobs = []
-        self.stream = stream
-        self.keep = []
-
-    def __call__(self, dy, x, dw, db):
-        self.jobs.append((dy, x, dw, db))
-
-    def flush(self):
-        jobs, self.jobs = self.jobs, []
-        if not jobs:
-            return
-        if self.stream is None:
-            linear_wgrad_group(jobs)
-            return
-        self.stream.wait_stream(torch.cuda.current_stream(self.stream.device))
-        with torch.cuda.stream(self.stream):
-            linear_wgrad_group(jobs)
-        self.keep.append(jobs)
 
 
 LN_REPLICAS = 16  # csrc/layernorm.hip LN_REPLICAS
@@ -526,9 +434,10 @@ def ddim_step(x_t, x0_raw, coef):
 
 
 def ddim_step_(x, x0_raw, x0_out, coef):
-    if _hip(x):
+    """In-place DDIM step; ``coef`` one row of 4 (GPU kernel) or [B, 4] per sample (torch ops)."""
+    if _hip(x) and coef.dim() == 1:
         return _ops().ddim_step_(x, x0_raw, x0_out, coef)
-    xn, x0 = ref.ddim_step(x, x0_raw, [float(c) for c in coef.tolist()[:4]])
+    xn, x0 = ref.ddim_step(x, x0_raw, _ddim_coef(coef, x))
     x.copy_(xn)
     x0_out.copy_(x0)
 

@@ -242,14 +242,6 @@ def linear_residual_fwd(a, w, b, x, N: int, rng, site_drop: int, p_drop: float,
     return out
 
 
-def linear_residual_ln_fwd(a, w, b, x, gamma, beta, eps: float, N: int, rng, site_drop: int, p_drop: float,
-                           site_dp: int, p_dp: float):
-    """linear_residual_fwd followed by layernorm_fwd of the new residual stream."""
-    xn = linear_residual_fwd(a, w, b, x, N, rng, site_drop, p_drop, site_dp, p_dp)
-    ln, mean, rstd = layernorm_fwd(xn, gamma, beta, eps)
-    return xn, ln, mean, rstd
-
-
 def linear_gelu_fwd(a, w, b, rng, site: int, p: float, st=None, c=None, eps: float = 1e-5, mean_out=None,
                     rstd_out=None):
     """u = a @ w.T + b (bf16, saved); h = Dropout(GELU(u)) (bf16)."""

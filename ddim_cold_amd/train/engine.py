@@ -18,7 +18,7 @@ AdamW step, cosine LR step, zero_grad) re-designed for a latency-bound
   (``ops.linear_wgrad_multi``, 1,548 64x64 tiles, no token split, no atomics).
   Data parallel: one such launch per gradient bucket, so each bucket's
   all-reduce can start while the remaining blocks run backward.  (Issuing them
-  on a side stream, ``wgrad_stream=True``, measured slower.)
+  on a side stream measured slower: 28.2k vs 33.1k img/s.)
 * **hipGraphs per step, bucketed RCCL all-reduce between them.**  Gradient
   buckets are contiguous arena ranges closed at transformer-block boundaries
   of the backward; as soon as a bucket's gradients are final its
@@ -81,11 +81,6 @@ class EngineConfig:
     # all-reduce overlaps the embedding backward and only ~0.4 MB (ViT-tiny) is
     # exposed before the optimizer
     embed_bucket: bool = True
-    # grouped weight-gradient launches on a second stream (a parallel graph
-    # branch), joined only by the all-reduce and the optimizer.  Measured on
-    # MI355X: 28.2k img/s with vs 33.1k without (graph branches of these
-    # latency-bound kernels interfere more than they overlap) -> off.
-    wgrad_stream: bool = False
     seed: int = 42
     loss_beta: float = 1.0
     ema_decay: float = 0.99
@@ -185,7 +180,6 @@ class TrainEngine:
         self.sqnorm = torch.zeros(ops.SQ_PARTS, dtype=torch.float32, device=dev)  # per-block partials
         self.loss_last = torch.zeros(1, dtype=torch.float32, device=dev)
         self.loss_ema = torch.full((1,), cfg.ema_init, dtype=torch.float32, device=dev)
-        self.side = torch.cuda.Stream(device=dev) if (self.is_cuda and cfg.wgrad_stream) else None
         # the comm stream is created once and kept across set_comm_layout() (a stream
         # created later could land on a hardware queue another stream already holds)
         self._comm_obj = self._comm_stream() if (self.is_cuda and self.segmented) else None
@@ -209,7 +203,6 @@ class TrainEngine:
         self._multi = None  # (K-step graph, K) for train_steps
         self._eager_steps = 0
         self.batch_fn: Optional[Callable] = None
-        self._segment_capture = False
         self._static = None
         self.steps_done = 0
         if self.world > 1:
@@ -507,11 +500,7 @@ class TrainEngine:
         all-reduce sums the fresh values in place.  DDIM_COLD_GRAD_OVERWRITE=0:
         accumulate everywhere."""
         return (self.is_cuda and k_acc == 1 and deferred and ln_final is not None
-                and self.side is None and os.environ.get("DDIM_COLD_GRAD_OVERWRITE", "1") != "0")
-
-    def _join_side(self):
-        if self.side is not None:
-            torch.cuda.current_stream(self.device).wait_stream(self.side)
+                and os.environ.get("DDIM_COLD_GRAD_OVERWRITE", "1") != "0")
 
     def _step_iter(self):
         c = self.prog.cfg
@@ -565,34 +554,19 @@ class TrainEngine:
             if self.ln_ptrs is not None and os.environ.get("DDIM_COLD_FUSE_LNFINAL", "1") != "0":
                 hi = self.ln_done_at[-1]
                 ln_final = (self.ln_ws[:hi], self.ln_ptrs[:hi], 2 * c.dim)
-            # single process: every weight gradient in one launch after the backward
-            # (no bucket needs a block's gradients early)
-            tail_w = not self.segmented and os.environ.get("DDIM_COLD_WGRAD_TAIL", "1") != "0"
-            # single process, one micro-batch: every gradient above the embeddings has ONE
-            # producer per step (the tail weight-gradient launch, the LayerNorm finalize), so
-            # those write instead of accumulate and the optimizer zeroes only the embeddings
-            flush_at = set(k for k in self.bucket_after if k >= 0) \
-                if (self.segmented and os.environ.get("DDIM_COLD_WGRAD_BUCKET", "1") != "0") else None
-            overwrite = self._grad_overwrite(k_acc, tail_w or flush_at is not None, ln_final)
+            # single process: every weight gradient in one launch after the backward (no
+            # bucket needs a block's gradients early); data parallel: one launch per
+            # gradient bucket, so its all-reduce can start while the backward goes on
+            flush_at = set(k for k in self.bucket_after if k >= 0) if self.segmented else None
+            # one micro-batch: every gradient above the embeddings has ONE producer per
+            # step (the deferred weight-gradient launches, the LayerNorm finalize), so those
+            # write instead of accumulate and the optimizer zeroes only the embeddings
+            overwrite = self._grad_overwrite(k_acc, True, ln_final)
             if overwrite:
                 ln_final = ln_final + (True,)
-            # data parallel: one weight-gradient launch per gradient bucket (flush_at,
-            # above; DDIM_COLD_WGRAD_BUCKET=0: riders in the input-gradient launches)
             for i in self.prog.backward_iter(self.param_tensors, self.grad_tensors, S, dtok, self.rng, True,
-                                             ln_ws=self.ln_ws, wgrad_stream=self.side, embed_with_block0=merge,
-                                             ln_final=ln_final, wgrad_tail=tail_w, wgrad_flush=flush_at,
-                                             wgrad_store=overwrite):
-                if (self.is_cuda and not self.segmented and i in self.bucket_after
-                        and os.environ.get("DDIM_COLD_DEBUG_FORK") == "1"):
-                    # experiment: the data-parallel graph's fork / join topology with a
-                    # tiny kernel on the side branch instead of a collective
-                    if getattr(self, "_dbg", None) is None:
-                        self._dbg = (torch.cuda.Stream(device=self.device),
-                                     torch.zeros(1, device=self.device))
-                    st_, buf_ = self._dbg
-                    st_.wait_stream(torch.cuda.current_stream(self.device))
-                    with torch.cuda.stream(st_):
-                        buf_.add_(1)
+                                             ln_ws=self.ln_ws, embed_with_block0=merge, ln_final=ln_final,
+                                             wgrad_flush=flush_at, wgrad_store=overwrite):
                 if i in self.bucket_after and (self.segmented or i == -1):
                     hi = self.ln_done_at[i]
                     if ln_final is not None:
@@ -603,13 +577,8 @@ class TrainEngine:
                                             2 * c.dim, dsts=self.ln_dsts[ln_lo:hi])
                         ln_lo = hi
                     if last:
-                        if self._segment_capture:
-                            self._join_side()  # a captured segment must rejoin every stream it forked
                         yield ("bucket", self.bucket_after[i])
             S = None
-        self._join_side()  # all weight gradients final before the norm / optimizer
-        if getattr(self, "_dbg", None) is not None:
-            torch.cuda.current_stream(self.device).wait_stream(self._dbg[0])
         # optimizer: grads are SUM-reduced over ranks and summed over micro-batches
         # -> average via grad_scale
         gs = 1.0 / (self.world * k_acc)
@@ -668,8 +637,6 @@ class TrainEngine:
                 after.wait(self.comm)
             else:
                 self.comm.wait_stream(torch.cuda.current_stream(self.device))
-            if self.side is not None and after is None:  # the bucket's weight gradients come from the side stream
-                self.comm.wait_stream(self.side)
             with torch.cuda.stream(self.comm):
                 reduce()
         else:
@@ -856,21 +823,17 @@ class TrainEngine:
             evs = [ExternalEvent(flags) for _ in range(nb)]
         gen = self._step_iter()
         g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        self._segment_capture = True  # side streams rejoin before each boundary
-        try:
-            with torch.cuda.graph(g1, pool=pool, capture_error_mode=CAPTURE_MODE):
-                for _ in range(nb):
-                    kind, k = next(gen)
-                    assert kind == "bucket", kind
-                    if sig is not None:
-                        sig.bump(k)
-                    else:
-                        evs[k].record()
-            with torch.cuda.graph(g2, pool=pool, capture_error_mode=CAPTURE_MODE):
-                kind, _ = next(gen)
-                assert kind == "done", kind
-        finally:
-            self._segment_capture = False
+        with torch.cuda.graph(g1, pool=pool, capture_error_mode=CAPTURE_MODE):
+            for _ in range(nb):
+                kind, k = next(gen)
+                assert kind == "bucket", kind
+                if sig is not None:
+                    sig.bump(k)
+                else:
+                    evs[k].record()
+        with torch.cuda.graph(g2, pool=pool, capture_error_mode=CAPTURE_MODE):
+            kind, _ = next(gen)
+            assert kind == "done", kind
         self._graphs = [g1, g2]
         self._events = evs
         self._signal = sig
@@ -900,15 +863,11 @@ class TrainEngine:
                         self._captured_step_body()
                 self._multi = (gm, K)
         else:
-            self._segment_capture = True
-            try:
-                for _ in range(nseg):
-                    g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, pool=pool, capture_error_mode=CAPTURE_MODE):
-                        next(gen)
-                    graphs.append(g)
-            finally:
-                self._segment_capture = False
+            for _ in range(nseg):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool, capture_error_mode=CAPTURE_MODE):
+                    next(gen)
+                graphs.append(g)
         self._graphs = graphs
 
     def _replay(self):

@@ -255,6 +255,7 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
     eval_rng = torch.tensor([cfg.seed + 7919 + 1000003 * rank, 0], dtype=torch.int64, device=device)
 
     history = []
+    last_ms = None  # device ms/step of the last full log window
     t_start = time.time()
     for epoch in range(start_epoch, end_epoch):
         model.train()
@@ -271,6 +272,8 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
                 check_param_sync(engine.flat_p, step=steps)
             if steps % cfg.log_every == 0:
                 window = clock.mark(steps)  # device events: the only sync of the window
+                if window is not None and window[1] > 0:
+                    last_ms = 1e3 * window[0] / window[1]
                 engine.check_comm()  # a timed-out bucket hand-off stops the run (stale gradients)
                 loss_rec = float(engine.loss_ema.item())
                 if verbose:
@@ -313,7 +316,8 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
     result = {"steps": steps, "loss_rec": loss_rec, "best_loss": best_loss, "history": history,
               "final_lr": engine.current_lr(), "rng": [int(v) for v in engine.rng.tolist()],
               "eval_rng": [int(v) for v in eval_rng.tolist()],
-              "comm_choice": engine.comm_choice, "handoff_order": engine.handoff_order}
+              "comm_choice": engine.comm_choice, "handoff_order": engine.handoff_order,
+              "ms_per_step": last_ms}
     engine.close()
     pdist.cleanup()
     return result

@@ -205,38 +205,6 @@ def test_folded_program_matches_unfolded():
     assert rel < 3e-2, rel
 
 
-@pytest.mark.parametrize("B,N,H,D,p,fold", [(32, 65, 12, 384, 0.1, True), (8, 65, 12, 384, 0.0, True),
-                                            (4, 100, 8, 256, 0.1, False), (3, 128, 16, 512, 0.0, True),
-                                            (5, 81, 12, 384, 0.0, False)])
-def test_fused_qkv_attention(B, N, H, D, p, fold):
-    """qkv_attn_fwd (QKV GEMM of a head + its attention in one workgroup) == qkv_fwd + attn_fwd."""
-    M = B * N
-    scale = (D // H) ** -0.5
-    if fold:
-        x, a, st, w, g, be, b, wq, c, bq = folded(3 * D, D, M)
-        fk = lambda m, r: (st, c, 1e-5, m, r)
-    else:
-        a = (torch.randn(M, D, device=DEV)).to(torch.bfloat16)
-        wq = (torch.randn(3 * D, D, device=DEV) * 0.05).to(torch.bfloat16)
-        bq = torch.randn(3 * D, device=DEV)
-        fk = lambda m, r: None
-    r = rng()
-    m1, r1 = torch.full((M,), float("nan"), device=DEV), torch.full((M,), float("nan"), device=DEV)
-    o, lse, qkv = ops.qkv_attn_fwd(a, wq, bq, B, N, H, scale, r, 11, p, True, fold=fk(m1, r1))
-    m2, r2 = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
-    qkv_r = ops.qkv_fwd(a, wq, bq, B, N, H, fold=fk(m2, r2))
-    o_r, lse_r = ops.attn_fwd(qkv_r, scale, r, 11, p)
-    close(qkv, qkv_r, 2e-2, 1e-2, "qkv")
-    close(o, o_r, 2e-2, 2e-2, "o")
-    close(lse, lse_r, 2e-3, 1e-3, "lse")
-    if fold:
-        close(m1, m2, 1e-5, 1e-5, "mean")
-        close(r1, r2, 1e-5, 1e-4, "rstd")
-    # eval-mode call: no qkv saved, same output
-    o2, _, q2 = ops.qkv_attn_fwd(a, wq, bq, B, N, H, scale, r, 11, p, False, fold=fk(None, None)[:3] if fold else None)
-    assert q2 is None and torch.equal(o2, o)
-
-
 @pytest.mark.parametrize("splits", [1, 2, 3])
 def test_bf16_dgrad_into_layernorm_bwd(splits):
     """bf16 input-gradient GEMM (optionally K-split into bf16 partials) feeding the

@@ -1,0 +1,116 @@
+"""Fused MLP block (csrc/mlp.hip: fc1 -> GELU -> dropout -> fc2 -> dropout ->
+drop-path -> residual, LayerNorm folded, one launch) vs the two-GEMM HIP path
+(linear_gelu_fwd + linear_residual_fwd) and the fp32 PyTorch reference
+(ops/reference.py, which reproduces the bf16 rounding points)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from ddim_cold_amd import ops
+from ddim_cold_amd.ops import reference as ref
+
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True)
+def _native():
+    from ddim_cold_amd.ops import _ext
+    _ext.load(raise_on_error=True)
+    torch.manual_seed(0)
+
+
+def close(a, b, atol, rtol=0.0, name=""):
+    a, b = a.float(), b.float()
+    err = (a - b).abs()
+    bad = (err > atol + rtol * b.abs()).sum().item()
+    assert bad == 0, f"{name}: {bad} mismatches, max err {err.max().item():.3e}"
+
+
+def _inputs(M, D, H):
+    x1 = torch.randn(M, D, device=DEV) * 2.0 + 0.5
+    st = ref.row_stats(x1)
+    xb = x1.to(torch.bfloat16)
+    w1 = torch.randn(H, D, device=DEV) * 0.05
+    g, be = torch.randn(D, device=DEV), torch.randn(D, device=DEV)
+    b1 = torch.randn(H, device=DEV)
+    w1f = torch.empty(H, D, dtype=torch.bfloat16, device=DEV)
+    c1, b1f = torch.empty(H, device=DEV), torch.empty(H, device=DEV)
+    ops.ln_fold_([w1], [g], [be], [b1], [w1f], [c1], [b1f])
+    w2 = (torch.randn(D, H, device=DEV) * 0.05).to(torch.bfloat16)
+    b2 = torch.randn(D, device=DEV)
+    return x1, xb, st, w1f, c1, b1f, w2, b2
+
+
+@pytest.mark.parametrize("M,D,H,N,pd,pdp,save,bm", [
+    (2080, 384, 384, 65, 0.1, 0.1, True, 0),     # ViT-tiny training block (BM 16)
+    (4160, 384, 384, 65, 0.0, 0.0, False, 0),    # sampler batch (BM 32)
+    (4160, 384, 384, 65, 0.1, 0.0, True, 64),    # 64-row panels
+    (2056, 256, 256, 257, 0.1, 0.2, True, 32),   # oxford_flower width
+    (100, 384, 128, 25, 0.0, 0.3, True, 16),     # ragged last panel, one hidden chunk
+])
+def test_mlp_fused_matches_two_gemm_path(M, D, H, N, pd, pdp, save, bm):
+    x1, xb, st, w1f, c1, b1f, w2, b2 = _inputs(M, D, H)
+    r = torch.tensor([321, 7], dtype=torch.int64, device=DEV)
+    st_out = torch.full((M, D // 32, 2), float("nan"), device=DEV)  # every slot must be written
+    xb_out = torch.empty(M, D, dtype=torch.bfloat16, device=DEV)
+    mean, rstd = torch.full((M,), float("nan"), device=DEV), torch.full((M,), float("nan"), device=DEV)
+    x, u, h = ops.mlp_fused_fwd(xb, x1, st, w1f, c1, b1f, w2, b2, 1e-5, N, r, 11, 12, pd, 13, pdp, save,
+                                st_out, xb_out, mean, rstd, bm=bm)
+    # the unfused HIP path
+    m2, r2 = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+    u2, h2 = ops.linear_gelu_fwd(xb, w1f, b1f, r, 11, pd, fold=(st, c1, 1e-5, m2, r2))
+    st2 = torch.empty_like(st_out)
+    xb2 = torch.empty_like(xb_out)
+    x2 = ops.linear_residual_fwd(h2, w2, b2, x1, N, r, 12, pd, 13, pdp, st_out=st2, xb_out=xb2)
+    close(mean, m2, 1e-6, 1e-5, "LN mean")
+    close(rstd, r2, 1e-6, 1e-5, "LN rstd")
+    if save:
+        close(u, u2, 1e-2, 1e-2, "u")
+        close(h, h2, 1e-2, 1e-2, "h")
+        assert ((u.float() != u2.float()).float().mean() < 1e-3), "u: more than 0.1% differ"
+    else:
+        assert u is None and h is None
+    close(x, x2, 2e-3, 1e-3, "x")
+    close(xb_out, x.to(torch.bfloat16), 0, 0, "bf16 copy")
+    close(st_out, ref.row_stats(x), 1e-3, 1e-4, "row statistics slots")
+    # fp32 reference of the same op sequence
+    ur, hr = ref.linear_gelu_fwd(xb, w1f, b1f, r, 11, pd, st, c1, 1e-5)
+    xr = ref.linear_residual_fwd(hr, w2, b2, x1, N, r, 12, pd, 13, pdp)
+    close(x, xr, 3e-2, 1e-2, "x vs fp32 reference")
+    # deterministic
+    x3, _, _ = ops.mlp_fused_fwd(xb, x1, st, w1f, c1, b1f, w2, b2, 1e-5, N, r, 11, 12, pd, 13, pdp, save,
+                                 torch.empty_like(st_out), torch.empty_like(xb_out), bm=bm)
+    assert torch.equal(x, x3)
+
+
+def test_folded_program_fused_mlp_matches_two_gemm(monkeypatch):
+    """The model forward + backward with the fused MLP == with the two GEMM launches."""
+    from ddim_cold_amd.models import build_model
+    from ddim_cold_amd.models import program as pm
+    from ddim_cold_amd.models.program import ViTProgram, collect, model_tensors
+    m = build_model("vit_tiny").to(DEV).train()
+    prog = ViTProgram.from_model(m)
+    P = model_tensors(m)
+    B = 16
+    img = torch.randn(B, 3, 64, 64, device=DEV).clamp(-1, 1)
+    tgt = torch.randn_like(img).clamp(-1, 1)
+    t = torch.randint(0, 2000, (B,), device=DEV)
+    r = torch.tensor([77, 3], dtype=torch.int64, device=DEV)
+    res = []
+    for fused in (True, False):
+        monkeypatch.setattr(pm, "FUSED_MLP", fused)
+        grads = {n: torch.zeros_like(p) for n, p in m.named_parameters()}
+        G = collect(grads, prog.cfg.depth, prog.cfg.dim)
+        with torch.no_grad():
+            out, S = prog.forward(P, img, t, r, True)
+            loss, dtok = ops.smooth_l1_fwd_bwd(out, tgt, prog.cfg.tokens, prog.cfg.patch)
+            prog.backward(P, G, S, dtok, r, True)
+        torch.cuda.synchronize()
+        res.append((out, loss, grads))
+    (o1, l1, g1), (o2, l2, g2) = res
+    assert (o1 - o2).abs().max() / o2.abs().max() < 1e-3
+    assert abs(l1.item() - l2.item()) < 1e-4 * abs(l2.item()) + 1e-6
+    for n in g1:
+        d = (g1[n] - g2[n]).norm() / (g2[n].norm() + 1e-30)
+        assert d < 1e-2, (n, d.item())

@@ -48,12 +48,13 @@ def test_program_fwd_bwd_vs_reference_ops(name):
 
 @pytest.mark.parametrize("name", ["vit_tiny", "oxford_flower"])
 @pytest.mark.parametrize("embed_with_block0", [True, False])
-@pytest.mark.parametrize("mode", ["ride", "tail", "bucket"])
-def test_backward_wgrad_ride_matches_grouped(name, embed_with_block0, mode, monkeypatch):
-    """Weight gradients riding in the dgrad launches == one grouped launch per block
-    (same backward otherwise; fp32 atomics -> summation order differs slightly), and
-    the block yields keep their order (L-1 .. 0, -1)."""
-    from ddim_cold_amd.models import program as pm
+@pytest.mark.parametrize("mode", ["bucket", "immediate"])
+def test_backward_wgrad_schedules_match(name, embed_with_block0, mode):
+    """The deferred weight gradients (default: ONE launch after the backward) ==
+    one launch per gradient bucket (data parallel) == each issued immediately;
+    same tiles, same unsplit reduction order for the launches (bit-identical
+    except the token-split patch gradient of the embedding bucket), and the block
+    yields keep their order (L-1 .. 0, -1)."""
     torch.manual_seed(0)
     m = build_model(name).to(DEV).train()
     prog = ViTProgram.from_model(m)
@@ -67,14 +68,16 @@ def test_backward_wgrad_ride_matches_grouped(name, embed_with_block0, mode, monk
         out, S = prog.forward(P, img, t, r, True)
         _, dtok = ops.smooth_l1_fwd_bwd(out, tgt, prog.cfg.tokens, prog.cfg.patch)
     results = []
-    for new in (True, False):
-        monkeypatch.setattr(pm, "WGRAD_RIDE", new and mode == "ride")
+    for variant in ("tail", mode):
         grads = {n: torch.zeros_like(p) for n, p in m.named_parameters()}
         G = collect(grads, prog.cfg.depth, prog.cfg.dim)
+        kw = dict(embed_with_block0=embed_with_block0)
+        if variant == "bucket":
+            kw["wgrad_flush"] = {3, 1, 0}
+        elif variant == "immediate":
+            kw["wgrad"] = ops.linear_wgrad
         with torch.no_grad():
-            order = list(prog.backward_iter(P, G, S, dtok, r, True, embed_with_block0=embed_with_block0,
-                                            wgrad_tail=new and mode == "tail",
-                                            wgrad_flush={3, 1, 0} if new and mode == "bucket" else None))
+            order = list(prog.backward_iter(P, G, S, dtok, r, True, **kw))
         torch.cuda.synchronize()
         assert order == list(range(prog.cfg.depth - 1, -1, -1)) + [-1]
         results.append(grads)

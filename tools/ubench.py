@@ -46,9 +46,7 @@ def main():
     res["resid p=0.1"] = t(lambda: ops.linear_residual_fwd(a, w, b, x, N, r, 3, 0.1, 4, 0.1))
     res["resid p=0"] = t(lambda: ops.linear_residual_fwd(a, w, b, x, N, r, 3, 0.0, 4, 0.0))
     g0, b0 = torch.randn(D, device=dev), torch.randn(D, device=dev)
-    res["resid+LN fused p=0.1"] = t(lambda: ops.linear_residual_ln_fwd(a, w, b, x, g0, b0, 1e-5, N, r, 3, 0.1, 4, 0.1))
     a2, x2 = bf(2 * M, D), torch.randn(2 * M, D, device=dev)
-    res["resid+LN fused M=4160 p=0"] = t(lambda: ops.linear_residual_ln_fwd(a2, w, b, x2, g0, b0, 1e-5, N, r, 3, 0., 4, 0.))
     res["resid M=4160 p=0"] = t(lambda: ops.linear_residual_fwd(a2, w, b, x2, N, r, 3, 0.0, 4, 0.0))
     res["ln fwd M=4160"] = t(lambda: ops.layernorm_fwd(x2, g0, b0))
     res["qkv"] = t(lambda: ops.qkv_fwd(a, w3, b3, B, N, H))
@@ -65,7 +63,7 @@ def main():
     res["wgrad 1152x384"] = t(lambda: ops.linear_wgrad(dqkv, a, dw3, db3))
     h_ = bf(M, D)
     blk = [(a, h_, dw, db), (a, h_, dw.clone(), db.clone()), (a, h_, dw.clone(), db.clone()), (dqkv, a, dw3, db3)]
-    res["wgrad group (block: 3x384^2 + 1152x384)"] = t(lambda: ops.linear_wgrad_group(blk))
+    res["wgrad multi (block: 3x384^2 + 1152x384)"] = t(lambda: ops.linear_wgrad_multi(blk))
     g, bb = torch.randn(D, device=dev), torch.randn(D, device=dev)
     res["ln fwd"] = t(lambda: ops.layernorm_fwd(x, g, bb))
     _, mu, rs = ops.layernorm_fwd(x, g, bb)
