@@ -114,6 +114,7 @@ __device__ __forceinline__ RowInfo epi_row(const GemmParams& p, int m) {
     ri.off = (long long)m * p.N;
   } else if (EPI == EPI_HEAD) {
     const int b = m / p.tokens, tok = m - b * p.tokens;
+    ri.b = b;  // sample (head mode 4: per-sample DDIM coefficients)
     if (tok == 0) {
       ri.off = -1;
     } else {

@@ -75,11 +75,25 @@ __global__ __launch_bounds__(256) void mlp_fused_kernel(MlpArgs a) {
   // tensor end read as zero through the buffer bounds check)
   const auto rs_w1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w1), (short)0, H * D * 2, 0x00020000);
   const auto rs_w2 = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w2), (short)0, D * H * 2, 0x00020000);
-  auto issue_w = [&](int t, int slot) {
+  // Tile t of the stream -> (chunk c, k-tile kt).  Each workgroup walks the chunks
+  // and the k-tiles of a chunk in an order rotated by its block id, so the
+  // workgroups running together fetch different weight tiles instead of all
+  // hitting the same L2 lines at once; every output column still sums its k-tiles
+  // in one fixed (rotated) order: deterministic.
+  const int rot = blockIdx.x;
+  auto tile_of = [&](int t, int& c, int& kt, int& q) {
     const bool p1 = t < T1;
     const int t2 = p1 ? t : t - T1;
-    const int kt_n = p1 ? KT1 : KT2;
-    const int c = t2 / kt_n, kt = t2 - c * kt_n;
+    const int kt_n = p1 ? KT1 : KT2, nc = p1 ? NC1 : NC2;
+    const int cq = t2 / kt_n;
+    q = t2 - cq * kt_n;
+    c = (cq + rot) % nc;
+    kt = (q + rot) % kt_n;
+  };
+  auto issue_w = [&](int t, int slot) {
+    const bool p1 = t < T1;
+    int c, kt, q;
+    tile_of(t, c, kt, q);
     const int ld = p1 ? D : H;
     char* dst = ring + slot * WT;
 #pragma unroll
@@ -167,10 +181,10 @@ __global__ __launch_bounds__(256) void mlp_fused_kernel(MlpArgs a) {
         }
     }
     const bool p1 = t < T1;
-    const int t2 = p1 ? t : t - T1;
     const int kt_n = p1 ? KT1 : KT2;
-    const int c = t2 / kt_n, kt = t2 - c * kt_n;
-    if (!p1 && kt == 0) {
+    int c, kt, q;
+    tile_of(t, c, kt, q);
+    if (!p1 && q == 0) {
       // fc2 chunk c: its residual rows x1[m0.., c*128..+127] (fp32) into the A-image
       // region (dead after fc1): BM/2 pieces of two 512-B rows
       const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.x1), (short)0, a.M * D * 4,
@@ -198,7 +212,7 @@ __global__ __launch_bounds__(256) void mlp_fused_kernel(MlpArgs a) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
-    if (kt != kt_n - 1) continue;
+    if (q != kt_n - 1) continue;
 
     // ------------------------------------------------------------ chunk epilogue
     if (p1) {

@@ -200,6 +200,26 @@ def test_img2img_batched_equals_sequential(tiny):
             assert torch.allclose(out[i], ((x0c + 1) / 2)[0], atol=1e-5), s
 
 
+def test_starts_table_identity_rows_and_cache(tiny):
+    """img2img's per-sample coefficient table: a sample joins the grid at its start step
+    and carries the exact identity row {0, 1, 0, 1} before it; repeated calls reuse
+    the cached loop state and reproduce the result."""
+    from ddim_cold_amd.diffusion.samplers import ddim_from_starts, starts_table
+    ts, coef = starts_table(2000, [1199, 1599, 1999], 400)
+    assert ts == [1999, 1599, 1199, 799, 399]
+    assert coef.shape == (5, 3, 4)
+    assert coef[0, 0].tolist() == [0.0, 1.0, 0.0, 1.0] and coef[1, 0].tolist() == [0.0, 1.0, 0.0, 1.0]
+    assert torch.allclose(coef[2, 0], torch.tensor(sch.ddim_coefficients(2000, 1199, 400)))
+    assert torch.allclose(coef[0, 2], torch.tensor(sch.ddim_coefficients(2000, 1999, 400)))
+    with pytest.raises(ValueError):
+        starts_table(2000, [1999, 1998], 10)
+    x = torch.randn(3, 3, 16, 16, generator=torch.Generator().manual_seed(4))
+    a = ddim_from_starts(tiny, x, [1199, 1599, 1999], 400).clone()
+    b = ddim_from_starts(tiny, x, [1199, 1599, 1999], 400).clone()
+    assert torch.equal(a, b)
+    assert sum(1 for k in tiny.__dict__["_sampler_graphs"] if k[0] == "img2img") == 1
+
+
 def test_slerp_and_interpolate(tiny):
     from ddim_cold_amd.diffusion.interpolate import interpolate, slerp
     a, b = torch.randn(1, 3, 4, 4), torch.randn(1, 3, 4, 4)
