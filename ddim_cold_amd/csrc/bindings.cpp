@@ -326,68 +326,6 @@ std::tuple<Tensor, Tensor> linear_gelu_fwd(Tensor a, Tensor w, Tensor b, Tensor 
   return {u, h};
 }
 
-static uint32_t drop_thr(double p) {  // == dc::drop_threshold_host (common.h)
-  const double v = p * 65536.0 + 0.5;
-  if (v >= 65536.0) return 65536u;
-  if (v <= 0.0) return 0u;
-  return (uint32_t)v;
-}
-
-// Fused MLP block (csrc/mlp.hip), LayerNorm-folded.  Returns (x_out, u, h); u / h
-// (training: pre-GELU and post-dropout GELU activations for the backward) are
-// empty when save is false.  st_out / xb_out receive the next LayerNorm's row
-// statistics and the bf16 copy of x_out; mean / rstd (optional) the LN2 row stats.
-std::tuple<Tensor, Tensor, Tensor> mlp_fused_fwd(Tensor xb, Tensor x1, Tensor st_in, Tensor w1, Tensor c1, Tensor b1,
-                                                 Tensor w2, Tensor b2, double eps, int64_t N, Tensor rng,
-                                                 int64_t site_f1, int64_t site_f2, double p_drop, int64_t site_dp,
-                                                 double p_dp, bool save, Tensor st_out, Tensor xb_out,
-                                                 c10::optional<Tensor> mean_out, c10::optional<Tensor> rstd_out,
-                                                 int64_t bm) {
-  CHECK_IN(xb, BF16); CHECK_IN(x1, F32); CHECK_IN(st_in, F32); CHECK_IN(w1, BF16); CHECK_IN(c1, F32);
-  CHECK_IN(b1, F32); CHECK_IN(w2, BF16); CHECK_IN(b2, F32); CHECK_IN(st_out, F32); CHECK_IN(xb_out, BF16);
-  check_rng(rng);
-  const c10::DeviceGuard guard(xb.device());
-  const int D = xb.size(-1);
-  const int64_t M = xb.numel() / D;
-  const int Hm = w1.size(0);
-  TORCH_CHECK(w1.dim() == 2 && w1.size(1) == D && w2.dim() == 2 && w2.size(0) == D && w2.size(1) == Hm,
-              "mlp_fused: weight shapes");
-  TORCH_CHECK(c1.numel() == Hm && b1.numel() == Hm && b2.numel() == D, "mlp_fused: bias shapes");
-  TORCH_CHECK(x1.numel() == M * D && st_in.numel() == M * (D / 32) * 2 && st_out.numel() == M * (D / 32) * 2 &&
-                  xb_out.numel() == M * D && M % N == 0,
-              "mlp_fused: activation shapes");
-  TORCH_CHECK(mlp_fused_supported(D, Hm), "mlp_fused: unsupported D=", D, " / hidden=", Hm);
-  TORCH_CHECK(M * std::max(D, Hm) < (1LL << 31) / 4, "mlp_fused: too many rows for 32-bit buffer offsets");
-  auto x_out = at::empty({M, D}, x1.options());
-  Tensor u = save ? at::empty({M, Hm}, xb.options()) : at::empty({0}, xb.options());
-  Tensor h = save ? at::empty({M, Hm}, xb.options()) : at::empty({0}, xb.options());
-  MlpArgs a;
-  a.xb = xb.data_ptr(); a.x1 = x1.data_ptr<float>(); a.st_in = st_in.data_ptr<float>();
-  a.w1 = w1.data_ptr(); a.c1 = c1.data_ptr<float>(); a.b1 = b1.data_ptr<float>();
-  a.w2 = w2.data_ptr(); a.b2 = b2.data_ptr<float>();
-  a.eps = (float)eps; a.M = (int)M; a.D = D; a.H = Hm; a.tokens = (int)N;
-  a.rng = rng.data_ptr<int64_t>();
-  a.site_f1 = (int)site_f1; a.site_f2 = (int)site_f2; a.site_dp = (int)site_dp;
-  a.thr_f1 = a.thr_f2 = drop_thr(p_drop);
-  a.sc_f1 = a.sc_f2 = p_drop > 0 ? 1.f / (1.f - (float)p_drop) : 1.f;
-  a.thr_dp = drop_thr(p_dp);
-  a.sc_dp = p_dp > 0 ? 1.f / (1.f - (float)p_dp) : 1.f;
-  a.x_out = x_out.data_ptr<float>(); a.xb_out = xb_out.data_ptr(); a.st_out = st_out.data_ptr<float>();
-  if (save) {
-    a.u_out = u.data_ptr(); a.h_out = h.data_ptr();
-  }
-  if (mean_out.has_value() && mean_out->defined()) {
-    CHECK_IN((*mean_out), F32); CHECK_IN((*rstd_out), F32);
-    TORCH_CHECK(mean_out->numel() == M && rstd_out->numel() == M, "mlp_fused: mean / rstd shapes");
-    a.mean_out = mean_out->data_ptr<float>(); a.rstd_out = rstd_out->data_ptr<float>();
-  }
-  a.bm = (int)bm;
-  mlp_fused_launch(a, cur_stream());
-  return {x_out, u, h};
-}
-
-bool mlp_fused_ok(int64_t D, int64_t H) { return mlp_fused_supported((int)D, (int)H); }
-
 Tensor head_fwd(Tensor a, Tensor w, Tensor b, int64_t B, int64_t C, int64_t H, int64_t W, int64_t patch,
                 c10::optional<Tensor> ln_st, c10::optional<Tensor> ln_c, double ln_eps, c10::optional<Tensor> ln_mean, c10::optional<Tensor> ln_rstd) {
   CHECK_IN(a, BF16); CHECK_IN(w, BF16); CHECK_IN(b, F32);
@@ -945,11 +883,6 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("smooth_l1_fwd_bwd(Tensor pred, Tensor target, int N, int patch, float beta, Tensor(a!)? loss_last=None, "
         "Tensor(b!)? loss_ema=None, float ema_decay=0.99, bool finish=True) -> (Tensor, Tensor)");
   m.def("img_to_tokgrad(Tensor dimg, int N, int patch) -> Tensor");
-  m.def("mlp_fused_fwd(Tensor xb, Tensor x1, Tensor st_in, Tensor w1, Tensor c1, Tensor b1, Tensor w2, Tensor b2, "
-        "float eps, int N, Tensor rng, int site_f1, int site_f2, float p_drop, int site_dp, float p_dp, bool save, "
-        "Tensor(a!) st_out, Tensor(b!) xb_out, Tensor(c!)? mean_out=None, Tensor(d!)? rstd_out=None, int bm=0) "
-        "-> (Tensor, Tensor, Tensor)");
-  m.def("mlp_fused_ok(int D, int H) -> bool", &mlp_fused_ok);
   m.def("linear_dgrad(Tensor dy, Tensor w, bool out_fp32, int splits=1) -> Tensor");
   m.def("linear_dgrad_gelu(Tensor dy, Tensor w, Tensor u, Tensor rng, int site, float p) -> Tensor");
   m.def("linear_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, Tensor(b!)? db) -> ()");
@@ -992,7 +925,6 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("attn_fwd", &attn_fwd);
   m.impl("linear_residual_fwd", &linear_residual_fwd);
   m.impl("linear_gelu_fwd", &linear_gelu_fwd);
-  m.impl("mlp_fused_fwd", &mlp_fused_fwd);
   m.impl("head_fwd", &head_fwd);
   m.impl("smooth_l1_fwd_bwd", &smooth_l1_fwd_bwd);
   m.impl("head_loss", &head_loss);

@@ -215,12 +215,12 @@ void stream_wait_flag(Tensor flags, int64_t k, int64_t value) {
 }
 
 // the same wait as a 1-lane polling kernel of ours (bounded, raises err[0] on timeout)
-void flag_wait(Tensor flags, int64_t k, int64_t value, Tensor err) {
+void flag_wait(Tensor flags, int64_t k, int64_t value, Tensor err, int64_t timeout_us) {
   TORCH_CHECK(flags.is_cuda() && flags.scalar_type() == at::kInt && flags.is_contiguous(), "flags: int32 cuda");
   TORCH_CHECK(err.is_cuda() && err.scalar_type() == at::kInt && err.numel() >= 1, "err: int32 cuda");
   TORCH_CHECK(k >= 0 && k < flags.numel(), "flag index out of range");
   flag_wait_launch(flags.data_ptr(), (int)k, static_cast<unsigned int>(value), err.data_ptr(),
-                   c10::hip::getCurrentHIPStream().stream());
+                   c10::hip::getCurrentHIPStream().stream(), timeout_us);
 }
 
 bool stream_wait_value_supported(int64_t device) {
@@ -239,7 +239,7 @@ TORCH_LIBRARY_FRAGMENT(ddim_cold, m) {
   m.def("flag_bump(Tensor(a!) flags, int k) -> ()", &flag_bump);
   m.def("stream_wait_flag(Tensor flags, int k, int value) -> ()", &stream_wait_flag);
   m.def("stream_wait_value_supported(int device) -> bool", &stream_wait_value_supported);
-  m.def("flag_wait(Tensor flags, int k, int value, Tensor(a!) err) -> ()", &flag_wait);
+  m.def("flag_wait(Tensor flags, int k, int value, Tensor(a!) err, int timeout_us=0) -> ()", &flag_wait);
   m.def("comm_unique_id() -> Tensor", &comm_unique_id);
   m.def("comm_init(Tensor uid, int world, int rank, int device) -> int", &comm_init);
   m.def("comm_all_reduce_(Tensor(a!) buf, int handle, int op=0) -> ()", &comm_all_reduce_);

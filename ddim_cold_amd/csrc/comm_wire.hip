@@ -64,17 +64,19 @@ __global__ __launch_bounds__(64) void flag_bump_kernel(unsigned int* __restrict_
 
 // Comm-stream side of the hand-off: one lane polls flags[k] (system-scope acquire)
 // until it reaches `expected` (wrap-safe), sleeping between polls.  Bounded: after
-// ~2 s (s_memrealtime, 100 MHz) it gives up and raises err[0], so a hand-off that
-// never comes cannot wedge the GPU; the host checks err (FlagSignal.check).
+// `ticks` of s_memrealtime (100 MHz; 2e8 = 2 s by default) it gives up and raises
+// err[0], so a hand-off that never comes cannot wedge the GPU; the host checks err
+// (FlagSignal.check).
 __global__ __launch_bounds__(64) void flag_wait_kernel(const unsigned int* __restrict__ flags, int k,
-                                                       unsigned int expected, unsigned int* __restrict__ err) {
+                                                       unsigned int expected, unsigned int* __restrict__ err,
+                                                       unsigned long long ticks) {
   const unsigned int lane = threadIdx.x;
   if (lane != 0) return;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   while (true) {
     const unsigned int v = __hip_atomic_load(flags + k + lane, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
     if (static_cast<int>(v - expected) >= 0) break;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
       __hip_atomic_store(err + lane, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       break;
     }
@@ -86,9 +88,11 @@ __global__ __launch_bounds__(64) void flag_wait_kernel(const unsigned int* __res
 
 using namespace dc;
 
-void flag_wait_launch(const void* flags, int k, unsigned int expected, void* err, hipStream_t stream) {
+void flag_wait_launch(const void* flags, int k, unsigned int expected, void* err, hipStream_t stream,
+                      int64_t timeout_us) {
+  const unsigned long long ticks = timeout_us > 0 ? (unsigned long long)timeout_us * 100ull : 200000000ull;
   flag_wait_kernel<<<1, 64, 0, stream>>>(reinterpret_cast<const unsigned int*>(flags), k, expected,
-                                         reinterpret_cast<unsigned int*>(err));
+                                         reinterpret_cast<unsigned int*>(err), ticks);
 }
 
 void flag_bump_launch(void* flags, int k, hipStream_t stream) {

@@ -199,35 +199,5 @@ void cold_batch_launch(const float* pool, int pool_n, const int64_t* rng, int si
 void wire_pack_launch(const float* src, void* dst, int64_t n, hipStream_t stream);
 void wire_unpack_launch(const void* src, float* dst, int64_t n, hipStream_t stream);
 void flag_bump_launch(void* flags, int k, hipStream_t stream);  // flags[k] += 1, system-scope release
-void flag_wait_launch(const void* flags, int k, unsigned int expected, void* err, hipStream_t stream);
-
-// Fused MLP block (mlp.hip): x_out = x1 + DropPath(Dropout(fc2(Dropout(GELU(LN(x1) W1^T + b1)))))
-// with the LayerNorm folded in (w1 = bf16(gamma o W1), c1 = its row sums, b1 = b + W1 beta;
-// LN statistics from st_in = {sum, sum^2} per 32-column slot of the xb rows)
-struct MlpArgs {
-  const void* xb = nullptr;       // [M][D] bf16 copy of x1 (the LayerNorm input)
-  const float* x1 = nullptr;      // [M][D] fp32 residual stream in
-  const float* st_in = nullptr;   // [M][D/32][2]
-  const void* w1 = nullptr;       // [H][D] bf16 (gamma-folded)
-  const float* c1 = nullptr;      // [H]
-  const float* b1 = nullptr;      // [H] (folded bias)
-  const void* w2 = nullptr;       // [D][H] bf16
-  const float* b2 = nullptr;      // [D]
-  float eps = 1e-5f;
-  int M = 0, D = 0, H = 0, tokens = 1;
-  const int64_t* rng = nullptr;
-  int site_f1 = 0, site_f2 = 0, site_dp = 0;
-  uint32_t thr_f1 = 0, thr_f2 = 0, thr_dp = 0;
-  float sc_f1 = 1.f, sc_f2 = 1.f, sc_dp = 1.f;
-  float* x_out = nullptr;         // [M][D] fp32
-  void* xb_out = nullptr;         // [M][D] bf16
-  float* st_out = nullptr;        // [M][D/32][2]
-  void* u_out = nullptr;          // [M][H] bf16 pre-GELU (training; null: eval kernel)
-  void* h_out = nullptr;          // [M][H] bf16 post-GELU + dropout (training)
-  float* mean_out = nullptr;      // [M] LayerNorm mean / rstd (training)
-  float* rstd_out = nullptr;
-  int bm = 0;                     // row-panel height 16 / 32 / 64 (0: by M)
-};
-bool mlp_fused_supported(int D, int H);
-int mlp_fused_bm(int M);
-void mlp_fused_launch(const MlpArgs& a, hipStream_t stream);
+void flag_wait_launch(const void* flags, int k, unsigned int expected, void* err, hipStream_t stream,
+                      int64_t timeout_us = 0);  // 0: 2 s

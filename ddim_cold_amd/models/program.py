@@ -43,11 +43,6 @@ DGRAD_BF16 = os.environ.get("DDIM_COLD_DGRAD_BF16", "1") == "1"
 # producing GEMM's epilogue accumulates the row statistics; the LayerNorm
 # backward re-emits the normalised rows for the weight gradients.
 FOLD_LN = os.environ.get("DDIM_COLD_LN_FOLD", "1") == "1"
-# the MLP block (fc1 + GELU + dropout + fc2 + dropout + drop-path + residual) of the
-# LayerNorm-folded forward as ONE launch (csrc/mlp.hip: the hidden rows stay in LDS,
-# the weights stream through a deep LDS-DMA ring); DDIM_COLD_FUSED_MLP=0: the two
-# GEMM launches
-FUSED_MLP = os.environ.get("DDIM_COLD_FUSED_MLP", "1") != "0"
 # the short attention forward stores its dropout keep flags (one 32-bit word per
 # lane, 0.6 MB per block for ViT-tiny at B=32) and the backward reads them instead
 # of re-hashing 2 pairs per 4 probabilities (the mask hash was ~1.9 us of the
@@ -355,7 +350,6 @@ class ViTProgram:
         def stats():
             return (torch.empty(M, dtype=torch.float32, device=dev),
                     torch.empty(M, dtype=torch.float32, device=dev)) if save else (None, None)
-        fused_mlp = FUSED_MLP and dev.type == "cuda" and ops.mlp_fused_ok(D, c.hidden)
         for i, bp in enumerate(P.blocks):
             sa, sp, sd1, sf1, sf2, sd2 = block_sites(i)
             x0 = x
@@ -372,15 +366,10 @@ class ViTProgram:
                                          st_out=st[2 * i + 1], xb_out=x1b)
             m2, r2 = stats()
             xb = torch.empty(M, D, dtype=ACT_DTYPE, device=dev)
-            if fused_mlp:
-                x, u, h = ops.mlp_fused_fwd(x1b, x1, st[2 * i + 1], bp.fc1_wf, bp.fc1_c, bp.fc1_bf, bp.fc2_w,
-                                            bp.fc2_b, c.eps, N, rng, sf1, sf2, pd, sd2, dpr[i], save,
-                                            st[2 * i + 2], xb, m2, r2)
-            else:
-                u, h = ops.linear_gelu_fwd(x1b, bp.fc1_wf, bp.fc1_bf, rng, sf1, pd,
-                                           fold=(st[2 * i + 1], bp.fc1_c, c.eps, m2, r2))
-                x = ops.linear_residual_fwd(h, bp.fc2_w, bp.fc2_b, x1, N, rng, sf2, pd, sd2, dpr[i],
-                                            st_out=st[2 * i + 2], xb_out=xb)
+            u, h = ops.linear_gelu_fwd(x1b, bp.fc1_wf, bp.fc1_bf, rng, sf1, pd,
+                                       fold=(st[2 * i + 1], bp.fc1_c, c.eps, m2, r2))
+            x = ops.linear_residual_fwd(h, bp.fc2_w, bp.fc2_b, x1, N, rng, sf2, pd, sd2, dpr[i],
+                                        st_out=st[2 * i + 2], xb_out=xb)
             if save:
                 S.blocks.append((x0, None, m1, r1, qkv, o, lse, x1, None, m2, r2, u, h))
         if head_step is not None:

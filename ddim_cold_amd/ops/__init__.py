@@ -145,31 +145,6 @@ def _ddim_coef(coef, x):
     return [float(c) for c in coef.tolist()[:4]]
 
 
-def mlp_fused_ok(D: int, H: int) -> bool:
-    """Widths the fused MLP kernel covers (csrc/mlp.hip: D, H multiples of 128, D >= 256, <= 512)."""
-    return D % 128 == 0 and H % 128 == 0 and 256 <= D <= 512 and 128 <= H <= 512
-
-
-def mlp_fused_fwd(xb, x1, st_in, w1, c1, b1, w2, b2, eps: float, N: int, rng, site_f1: int, site_f2: int,
-                  p_drop: float, site_dp: int, p_dp: float, save: bool, st_out, xb_out, mean_out=None,
-                  rstd_out=None, bm: int = 0):
-    """The LayerNorm-folded MLP block in ONE launch (csrc/mlp.hip):
-    ``x = x1 + DropPath(Dropout(fc2(Dropout(GELU(LN(x1) W1^T + b1)))))`` with ``w1``/``c1``/``b1``
-    the folded fc1 (:class:`LnFold`) and ``st_in`` x1's row statistics.  Returns
-    ``(x, u, h)`` (``u``/``h``: pre-GELU / post-dropout activations for the backward,
-    None unless ``save``); ``st_out`` / ``xb_out`` get x's statistics slots and bf16 copy,
-    ``mean_out`` / ``rstd_out`` the LayerNorm's row statistics.  Same values as
-    :func:`linear_gelu_fwd` + :func:`linear_residual_fwd` (fp32 summation order aside)."""
-    if _hip(xb):
-        x, u, h = _ops().mlp_fused_fwd(xb, x1, st_in, w1, c1, b1, w2, b2, float(eps), int(N), rng, int(site_f1),
-                                       int(site_f2), float(p_drop), int(site_dp), float(p_dp), bool(save), st_out,
-                                       xb_out, mean_out, rstd_out, int(bm))
-        return x, (u if save else None), (h if save else None)
-    u, h = ref.linear_gelu_fwd(xb, w1, b1, rng, site_f1, p_drop, st_in, c1, eps, mean_out, rstd_out)
-    x = ref.linear_residual_fwd(h, w2, b2, x1, N, rng, site_f2, p_drop, site_dp, p_dp, st_out, xb_out)
-    return x, (u if save else None), (h if save else None)
-
-
 def head_step_(a, w, b, x, x0_out, coef, patch: int, mode: int, fold=None, patches_out=None):
     """Head GEMM + sampler step in its epilogue (in place on ``x``): mode 1 = clamp +
     DDIM update (``x0_out`` gets the clamped x0-hat; ``coef`` a device row of

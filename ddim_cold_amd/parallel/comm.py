@@ -81,6 +81,11 @@ class FlagSignal:
         # comm-stream wait: "kernel" = our bounded 1-lane polling kernel, "stream" =
         # hipStreamWaitValue32 (DDIM_COLD_FLAG_WAIT)
         self.mode = os.environ.get("DDIM_COLD_FLAG_WAIT", "kernel")
+        # the polling kernel's bound (default 2 s; tests shorten it)
+        self.timeout_us = int(os.environ.get("DDIM_COLD_HANDOFF_TIMEOUT_US", "0"))
+        # testing: wait for a counter value the compute graph never reaches, so every
+        # hand-off times out (exercises the failure path end to end)
+        self.skew = int(os.environ.get("DDIM_COLD_TEST_HANDOFF_SKEW", "0"))
 
     @staticmethod
     def supported(device) -> bool:
@@ -101,7 +106,8 @@ class FlagSignal:
                     if sig.mode == "stream":
                         torch.ops.ddim_cold.stream_wait_flag(sig.flags, int(k), int(sig.expected))
                     else:
-                        torch.ops.ddim_cold.flag_wait(sig.flags, int(k), int(sig.expected) & 0xFFFFFFFF, sig.err)
+                        torch.ops.ddim_cold.flag_wait(sig.flags, int(k), int(sig.expected + sig.skew) & 0xFFFFFFFF,
+                                                      sig.err, sig.timeout_us)
         return _Wait()
 
     def failed(self) -> bool:

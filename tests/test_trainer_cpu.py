@@ -183,3 +183,21 @@ def test_cli_entry_points(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     assert any(f.endswith(".png") for f in os.listdir(out))
     assert w.is_file()
+
+
+def test_trainer_stops_on_comm_error(tmp_path, monkeypatch):
+    """The trainer checks the data-parallel hand-off at every log point
+    (TrainEngine.check_comm) and a failure ends the run with an error."""
+    from ddim_cold_amd.train import engine as eng_mod
+    calls = []
+
+    def failing_check(self):
+        calls.append(1)
+        raise RuntimeError("data-parallel hand-off: a comm-stream flag wait timed out (test)")
+    monkeypatch.setattr(eng_mod.TrainEngine, "check_comm", failing_check)
+    cfg = _tiny_cfg(ckpt_dir=str(tmp_path / "Saved_Models"))
+    paths = Paths.make(cfg, "exp", root=str(tmp_path))
+    with pytest.raises(RuntimeError, match="hand-off"):
+        launch(cfg, "exp", paths, backend="gloo")
+    assert len(calls) == 1
+    assert not os.path.exists(os.path.join(paths.ckpt_dir, "lastepoch.pkl"))  # nothing saved after it

@@ -7,8 +7,6 @@ run() { local name=$1 to=$2; shift 2
   echo "=== $name"; timeout -k 10 $to "$@" > gpurun_out/$name.log 2>&1; local rc=$?
   echo "rc=$rc"; tail -${TAILN:-4} gpurun_out/$name.log | cut -c1-800
   if [ $rc -ne 0 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi; }
-run mlp_tests 240 python -u -m pytest tests/test_mlp_gpu.py -x -v -s --timeout 120 --timeout-method thread
-TAILN=8 run ub_mlp 240 python tools/ub_mlp.py
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 run gputests 900 python -u -m pytest tests -m gpu -x -v -s --timeout 200 --timeout-method thread
 run grad_error 300 python tools/grad_error_report.py
