@@ -59,6 +59,25 @@ def _flags(inc, abi, resource_usage=False):
     return f
 
 
+# Codegen flag for every kernel unit: -amdgpu-mfma-vgpr-form (MFMA accumulators
+# in VGPRs instead of AGPRs).  In the flash attention forward the softmax reads
+# every score accumulator and rescales the output accumulators, so the AGPR form
+# paid a v_accvgpr_read/write per element per tile (96 per 32 MFMAs in the loop's
+# .s) and 204 registers (occupancy 2); the VGPR form has none and 152 registers
+# (occupancy 3).  Whole-tree A/B on MI355X (tools/gpu_r3_attn.sh, 2 interleaved
+# 1000-step pairs): attention unit only 0.7982/0.8012 ms/step, every unit
+# 0.7939/0.7954, neither 0.8079/0.8041; sampler k=20 N=64 38.54 / 37.78 / 38.79 ms.
+# DDIM_COLD_VGPR_FORM=none|attention selects the older variants for A/Bs.
+VGPR_FORM_UNITS = {"attention.hip"}
+
+
+def _unit_flags(src, flags):
+    name = os.path.basename(src)
+    mode = os.environ.get("DDIM_COLD_VGPR_FORM", "all")
+    on = mode == "all" or (mode == "attention" and name in VGPR_FORM_UNITS)
+    return flags + (["-mllvm", "-amdgpu-mfma-vgpr-form"] if on and src.endswith(".hip") else [])
+
+
 def _hash(path, flags):
     h = hashlib.sha256()
     h.update(" ".join(flags).encode())
@@ -120,7 +139,7 @@ def build(force: bool = False, jobs: int | None = None, resource_usage: bool = F
     jobs = jobs or min(len(srcs), max(1, min(8, (os.cpu_count() or 4))))
     objs, logs = [], []
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        futs = {ex.submit(_compile, s, flags, force): s for s in srcs}
+        futs = {ex.submit(_compile, s, _unit_flags(s, flags), force): s for s in srcs}
         for fut in cf.as_completed(futs):
             obj, log = fut.result()
             objs.append(obj)

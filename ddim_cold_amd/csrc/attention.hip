@@ -22,6 +22,7 @@
 #include "common.h"
 #include "kernels.h"
 #include <cstdlib>
+#include <type_traits>
 
 namespace dc {
 
@@ -142,13 +143,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
     mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
     const float m_new = fmaxf(m_run, mt);
-    const float alpha = exp2f(m_run - m_new);
+    const float alpha = fexp2(m_run - m_new);
     float ls = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float pv = exp2f(st[t][r] - m_new);
+        float pv = fexp2(st[t][r] - m_new);
         ls += pv;
         if (thr) {
           const int key = kv0 + 16 * t + 4 * g + r;
@@ -221,6 +222,61 @@ struct KvStage {  // one 64-row K tile + one 64-row V tile, register-staged
   }
 };
 
+// One online-softmax update of a 16-query column tile of S^T (lane li = query,
+// 16 of the tile's 64 keys per lane in st, RAW scores): turns st into the
+// probabilities of the P.V MFMAs (dropout applied) and updates the running
+// max / sum and the output accumulators.
+//   * scale folded into one FMA per score: p = exp2(s * sl2 - m), m in scaled
+//     log2 units (the max is taken on raw scores; sl2 > 0)
+//   * key masking only in the tail tile (MASK; full tiles carry none)
+//   * lazy rescale: the reference max m moves only when a tile's max exceeds it
+//     by more than 8 (log2 units), so p <= 2^8 (exact in fp32, same relative
+//     bf16 precision as p <= 1); numerator and denominator use the same m, so
+//     the result is the softmax.  After the first tile the (wave-uniform) branch
+//     that rescales o is almost never taken: the o *= alpha pass (an AGPR read +
+//     mul + write per accumulator element) and the alpha exp leave the loop.
+template <int DT, bool DROP, bool MASK>
+__device__ __forceinline__ void flash_softmax_tile(f32x4 (&st)[4], f32x4 (&o)[DT], float& m_run, float& l_run,
+                                                   int kv0, int N, int g, float sl2, uint32_t salt,
+                                                   uint32_t rowidx, uint32_t thr, float dsc) {
+  float mt = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (MASK && kv0 + 16 * t + 4 * g + r >= N) st[t][r] = -INFINITY;
+      mt = fmaxf(mt, st[t][r]);
+    }
+  mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+  mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+  const float ms = mt * sl2;
+  const bool up = ms > m_run + 8.f;  // m_run = -inf on the first tile: always
+  if (__any(up)) {
+    const float alpha = up ? fexp2(m_run - ms) : 1.f;
+    l_run *= alpha;
+#pragma unroll
+    for (int d = 0; d < DT; ++d) o[d] *= alpha;
+    m_run = up ? ms : m_run;
+  }
+  const float nm = -m_run;
+  float ls = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    bool kp[4] = {true, true, true, true};
+    if (DROP) dropout_keep4(salt, rowidx + (uint32_t)(16 * t + 4 * g), thr, kp);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float pv = fexp2(fmaf(st[t][r], sl2, nm));
+      ls += pv;
+      if (DROP) pv = kp[r] ? pv * dsc : 0.f;
+      st[t][r] = pv;
+    }
+  }
+  ls += __shfl_xor(ls, 16, 64);
+  ls += __shfl_xor(ls, 32, 64);
+  l_run += ls;
+}
+
 template <int HD, bool DROP>
 __global__ __launch_bounds__(256) void attn_fwd_flash2_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                               float* __restrict__ lse, int B, int H, int N,
@@ -258,7 +314,10 @@ __global__ __launch_bounds__(256) void attn_fwd_flash2_kernel(const bf16* __rest
     for (int d = 0; d < C::DT; ++d) o[u][d] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   const int ntiles = (N + 63) / 64;
-  for (int it = 0; it < ntiles; ++it) {
+  const uint32_t rowidx0 = (uint32_t)(((size_t)bh * N + qbase + li) * attn_mask_ld(N));
+  const uint32_t rowstep = (uint32_t)(16 * attn_mask_ld(N));  // second query tile u = 1
+  auto tile = [&](int it, auto mask_tag) {
+    constexpr bool MASK = decltype(mask_tag)::value;
     const int kv0 = it * 64;
     const bool more = it + 1 < ntiles;
     if (more) stg.load(kb, vb, kv0 + 64, N);  // lands during this tile's MFMAs
@@ -277,42 +336,9 @@ __global__ __launch_bounds__(256) void attn_fwd_flash2_kernel(const bf16* __rest
       }
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int q = qbase + 16 * u + li;
-      float mt = -INFINITY;
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = (kv0 + 16 * t + 4 * g + r) < N ? st[u][t][r] * sl2 : -INFINITY;
-          st[u][t][r] = v;
-          mt = fmaxf(mt, v);
-        }
-      mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-      const float m_new = fmaxf(m_run[u], mt);
-      const float alpha = exp2f(m_run[u] - m_new);
-      const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * attn_mask_ld(N) + kv0);
-      float ls = 0.f;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        bool kp[4] = {true, true, true, true};
-        if (DROP) dropout_keep4(salt, rowidx + (uint32_t)(16 * t + 4 * g), thr, kp);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float pv = exp2f(st[u][t][r] - m_new);
-          ls += pv;
-          if (DROP) pv = kp[r] ? pv * dsc : 0.f;
-          st[u][t][r] = pv;
-        }
-      }
-      ls += __shfl_xor(ls, 16, 64);
-      ls += __shfl_xor(ls, 32, 64);
-      l_run[u] = l_run[u] * alpha + ls;
-      m_run[u] = m_new;
-#pragma unroll
-      for (int d = 0; d < C::DT; ++d) o[u][d] *= alpha;
-    }
+    for (int u = 0; u < 2; ++u)
+      flash_softmax_tile<C::DT, DROP, MASK>(st[u], o[u], m_run[u], l_run[u], kv0, N, g, sl2, salt,
+                                            rowidx0 + u * rowstep + kv0, thr, dsc);
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       const bf16x8 pb0 = pack8(st[0][2 * s2], st[0][2 * s2 + 1]);
@@ -326,7 +352,10 @@ __global__ __launch_bounds__(256) void attn_fwd_flash2_kernel(const bf16* __rest
     }
     if (more) stg.store(lds + ((it + 1) & 1) * 2 * C::TILE, lds + ((it + 1) & 1) * 2 * C::TILE + C::TILE);
     __syncthreads();
-  }
+  };
+  const int nfull = N / 64;  // tiles with every key valid
+  for (int it = 0; it < nfull; ++it) tile(it, std::false_type{});
+  if (nfull < ntiles) tile(nfull, std::true_type{});
   const int D = H * HD;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
@@ -421,7 +450,10 @@ __global__ __launch_bounds__(640) void attn_fwd_resident_kernel(const bf16* __re
 #pragma unroll
     for (int d = 0; d < C::DT; ++d) o[u][d] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  for (int kv0 = 0; kv0 < N; kv0 += 64) {
+  const uint32_t rowidx0 = (uint32_t)(((size_t)bh * N + qbase + li) * attn_mask_ld(N));
+  const uint32_t rowstep = (uint32_t)(16 * attn_mask_ld(N));
+  auto chunk = [&](int kv0, auto mask_tag) {
+    constexpr bool MASK = decltype(mask_tag)::value;
     const char* Kc = Kl + kv0 * C::S;
     const char* Vc = Vl + kv0 * C::S;
     f32x4 st[2][4];
@@ -437,42 +469,9 @@ __global__ __launch_bounds__(640) void attn_fwd_resident_kernel(const bf16* __re
       }
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int q = qbase + 16 * u + li;
-      float mt = -INFINITY;
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = (kv0 + 16 * t + 4 * g + r) < N ? st[u][t][r] * sl2 : -INFINITY;
-          st[u][t][r] = v;
-          mt = fmaxf(mt, v);
-        }
-      mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-      const float m_new = fmaxf(m_run[u], mt);
-      const float alpha = exp2f(m_run[u] - m_new);
-      const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * attn_mask_ld(N) + kv0);
-      float ls = 0.f;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        bool kp[4] = {true, true, true, true};
-        if (DROP) dropout_keep4(salt, rowidx + (uint32_t)(16 * t + 4 * g), thr, kp);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float pv = exp2f(st[u][t][r] - m_new);
-          ls += pv;
-          if (DROP) pv = kp[r] ? pv * dsc : 0.f;
-          st[u][t][r] = pv;
-        }
-      }
-      ls += __shfl_xor(ls, 16, 64);
-      ls += __shfl_xor(ls, 32, 64);
-      l_run[u] = l_run[u] * alpha + ls;
-      m_run[u] = m_new;
-#pragma unroll
-      for (int d = 0; d < C::DT; ++d) o[u][d] *= alpha;
-    }
+    for (int u = 0; u < 2; ++u)
+      flash_softmax_tile<C::DT, DROP, MASK>(st[u], o[u], m_run[u], l_run[u], kv0, N, g, sl2, salt,
+                                            rowidx0 + u * rowstep + kv0, thr, dsc);
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       const bf16x8 pb0 = pack8(st[0][2 * s2], st[0][2 * s2 + 1]);
@@ -484,7 +483,10 @@ __global__ __launch_bounds__(640) void attn_fwd_resident_kernel(const bf16* __re
         o[1][d] = mfma16(vf, pb1, o[1][d]);
       }
     }
-  }
+  };
+  const int nfull = N / 64 * 64;
+  for (int kv0 = 0; kv0 < nfull; kv0 += 64) chunk(kv0, std::false_type{});
+  if (nfull < N) chunk(nfull, std::true_type{});
   const int D = H * HD;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
@@ -589,7 +591,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
   stg.store(lds, lds + C::TILE);
   __syncthreads();
   const int ntiles = (N + 63) / 64;
-  for (int it = 0; it < ntiles; ++it) {
+  const float nl2 = -lse2;
+  // key mask only in the tail tile: a padded key has a zero K row (no dQ
+  // contribution) but exp2(0 - lse) can overflow, so it must not reach dS
+  auto tile = [&](int it, auto mask_tag) {
+    constexpr bool MASK = decltype(mask_tag)::value;
     const int kv0 = it * 64;
     const bool more = it + 1 < ntiles;
     if (more) stg.load(kb, vb, kv0 + 64, N);  // next tile lands during this tile's MFMAs
@@ -607,7 +613,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = kv0 + 16 * t + 4 * g + r;
-        const float pr = key < N ? exp2f(st[r] * sl2 - lse2) : 0.f;
+        float pr = fexp2(fmaf(st[r], sl2, nl2));
+        if (MASK && key >= N) pr = 0.f;
         float dpv = dp[r];
         if (thr) {
           const uint32_t idx = (uint32_t)(((size_t)bh * N + q) * attn_mask_ld(N) + key);
@@ -624,7 +631,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
     }
     if (more) stg.store(lds + ((it + 1) & 1) * 2 * C::TILE, lds + ((it + 1) & 1) * 2 * C::TILE + C::TILE);
     __syncthreads();
-  }
+  };
+  const int nfull = N / 64;
+  for (int it = 0; it < nfull; ++it) tile(it, std::false_type{});
+  if (nfull < ntiles) tile(nfull, std::true_type{});
   if (qv) {
     bf16* row = dqkv + ((size_t)b * N + q) * (3 * D) + h * HD;
 #pragma unroll
@@ -739,7 +749,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
       for (int r = 0; r < 4; ++r) {
         const int qr = 16 * t + 4 * g + r;
         const int qq = q0 + qr;
-        const float pr = exp2f(st[r] * sl2 - sl[qr]);
+        const float pr = fexp2(fmaf(st[r], sl2, -sl[qr]));  // padded queries: lse = +inf -> 0
         float pd = pr, dpv = dp[r];
         if (thr) {
           const uint32_t idx = (uint32_t)(((size_t)bh * N + qq) * attn_mask_ld(N) + key);
@@ -903,17 +913,18 @@ __global__ __launch_bounds__(NP * 4) void attn_fwd_short_kernel(const bf16* __re
 #pragma unroll
     for (int s = 0; s < KS; ++s) st[t] = mfma16(frag_row<HD>(Kl, 16 * t + li, s, g), qf[s], st[t]);
   }
-  float mx = -INFINITY;
+  float mx = -INFINITY;  // raw-score max (sl2 > 0), scaled below
 #pragma unroll
   for (int t = 0; t < KT; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float v = (16 * t + 4 * g + r) < N ? st[t][r] * sl2 : -INFINITY;
-      st[t][r] = v;
-      mx = fmaxf(mx, v);
+      if (16 * t + 16 > N && 16 * t + 4 * g + r >= N) st[t][r] = -INFINITY;  // tail tiles only (uniform test first)
+      mx = fmaxf(mx, st[t][r]);
     }
   mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  mx *= sl2;
+  const float nmx = -mx;
   float l = 0.f;
   const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * attn_mask_ld(N));
   uint32_t kbits = 0u;
@@ -923,7 +934,7 @@ __global__ __launch_bounds__(NP * 4) void attn_fwd_short_kernel(const bf16* __re
     if (DROP) dropout_keep4(salt, rowidx + (uint32_t)(16 * t + 4 * g), thr, kp);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float pv = exp2f(st[t][r] - mx);
+      float pv = fexp2(fmaf(st[t][r], sl2, nmx));
       l += pv;
       if (DROP) {
         pv = kp[r] ? pv * dsc : 0.f;
@@ -1046,7 +1057,8 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int key = 16 * t + 4 * g + r;
-      const float pr = key < N ? exp2f(st[r] * sl2 - lse2) : 0.f;
+      float pr = fexp2(fmaf(st[r], sl2, -lse2));
+      if (16 * t + 16 > N && key >= N) pr = 0.f;  // tail tiles only (uniform test first)
       float pd = pr, dpv = dp[r];
       if (DROP) {
         const bool kp = kq[r];

@@ -28,6 +28,13 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
 __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
 
+// bare v_exp_f32.  exp2f() adds a denormal-range fix-up around it (v_cmp +
+// 2 v_cndmask + v_ldexp per call: 3 of every 4 vector instructions of the
+// softmax in the flash forward's loop, counted in its .s); softmax inputs are
+// <= 0 (or <= 8 with the lazy max of the flash kernels) and results below
+// 2^-126 are negligible against the row sum, so the fix-up buys nothing here.
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }

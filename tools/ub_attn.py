@@ -1,4 +1,6 @@
-"""Attention fwd/bwd timings on the model shapes (graph-timed)."""
+"""Attention fwd/bwd timings on the model shapes (graph-timed): ViT-tiny train / sampler
+(N=65), OxfordFlower (N=257), vit_small_200 (N=626), 200x200 at p=4 (N=2501).
+DDIM_COLD_LIB=<other .so> times another build."""
 import os, sys, json
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -7,7 +9,8 @@ from tools.ubench import t
 dev = "cuda"
 r = torch.tensor([1, 2], dtype=torch.int64, device=dev)
 res = {}
-for (B, H, N, hd) in [(32, 12, 65, 32), (32, 4, 257, 64), (64, 4, 257, 64), (32, 6, 626, 64)]:
+SHAPES = [(32, 12, 65, 32), (64, 12, 65, 32), (32, 4, 257, 64), (64, 4, 257, 64), (32, 6, 626, 64), (8, 4, 2501, 64)]
+for (B, H, N, hd) in SHAPES:
     qkv = (torch.randn(3, B, H, N, hd, device=dev) * 0.5).to(torch.bfloat16)
     do = (torch.randn(B, N, H * hd, device=dev)).to(torch.bfloat16)
     for p in (0.0, 0.1):
