@@ -126,13 +126,32 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-__device__ __forceinline__ float gelu_f(float x) {
-  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+// Standard normal CDF Phi(x) = (1 + erf(x / sqrt 2)) / 2 for the exact (erf) GELU of
+// nn.GELU (ViT.py:80).  erff() costs ~40 vector instructions per element (range
+// split + an exp inside; the GELU GEMM epilogue ran ~31 VALU per MFMA in the PMC
+// table).  Abramowitz & Stegun 7.1.28: erf(z) = 1 - t^-16, t = 1 + a1 z + .. + a6 z^6
+// (z >= 0, |error| <= 3e-7), i.e. 6 FMAs, 4 squarings and one v_rcp; the lower tail
+// 1 - erf(z) = t^-16 comes out directly (no cancellation).  The error is three
+// orders of magnitude below the bf16 rounding of the stored activations.
+__device__ __forceinline__ float norm_cdf(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  float t = fmaf(z, 4.30638e-5f, 2.765672e-4f);
+  t = fmaf(z, t, 1.520143e-4f);
+  t = fmaf(z, t, 9.2705272e-3f);
+  t = fmaf(z, t, 4.22820123e-2f);
+  t = fmaf(z, t, 7.05230784e-2f);
+  t = fmaf(z, t, 1.0f);
+  t = t * t;
+  t = t * t;
+  t = t * t;
+  t = t * t;
+  const float tail = 0.5f * __builtin_amdgcn_rcpf(t);  // Phi(-|x|); 0 once t^16 overflows
+  return x >= 0.f ? 1.0f - tail : tail;
 }
+__device__ __forceinline__ float gelu_f(float x) { return x * norm_cdf(x); }
 __device__ __forceinline__ float gelu_grad_f(float x) {
-  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-  const float pdf = __expf(-0.5f * x * x) * 0.39894228040143268f;
-  return cdf + x * pdf;
+  const float pdf = fexp2(-0.72134752044448170f * x * x) * 0.39894228040143268f;  // exp(-x^2/2)/sqrt(2 pi)
+  return norm_cdf(x) + x * pdf;
 }
 
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }

@@ -264,10 +264,12 @@ __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int t
       oa.issue(smem + s * STAGE, kt0 + s, wave);
       ob.issue(smem + s * STAGE + OA::BYTES, kt0 + s, wave);
     }
-  // epilogue operands in flight behind the first operand tiles (see VecEpi)
+  // epilogue operands in flight behind the first operand tiles (see VecEpi).  The
+  // vector epilogues take the SWAPPED accumulator layout: mfma(B, A) = C^T puts 4
+  // consecutive output columns of one row in each lane, no quad transpose.
   constexpr bool VEC = UsesVecEpi<EPI>::value;
-  VecEpi<EPI, FM, FN> ep;
-  if (VEC && p.debug != 3) ep.prefetch(p, m0 + wm * TM, n0 + wn * TN, g, li);
+  VecEpi<EPI, FM, FN, false, VEC> ep;
+  if (VEC) ep.prefetch(p, m0 + wm * TM, n0 + wn * TN, g, li);
 
   // main loop; the bias-gradient MFMA variant is a separate instantiation so the
   // loop carries no per-k-step branch (one made hipcc shuffle the accumulators
@@ -338,7 +340,7 @@ __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int t
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+          for (int j = 0; j < FN; ++j) acc[i][j] = VEC ? mfma16(bfr[j], af[i], acc[i][j]) : mfma16(af[i], bfr[j], acc[i][j]);
         if (DB) {
 #pragma unroll
           for (int i = 0; i < FM; ++i) dbacc[i] = mfma16(af[i], ones, dbacc[i]);
@@ -380,7 +382,7 @@ __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int t
       }
   }
 
-  if (VEC && p.debug != 3) ep.finish(p, acc, li);
+  if (VEC) ep.finish(p, acc, li);
   else run_epilogue_scalar<EPI, FM, FN>(p, acc, m0 + wm * TM, n0 + wn * TN, g, li);
 }
 

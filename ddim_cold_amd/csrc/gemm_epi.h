@@ -80,7 +80,7 @@ struct GemmParams {
   const float* cls_src;
   int acc_store;  // EPI_ACC: the target is known to be zero -- store, don't read-add
   int debug;  // profiling aid (DDIM_COLD_GEMM_DEBUG): 1 = skip the epilogue, 2 = skip the main loop,
-              // 3 = scalar (untransposed) epilogue
+              // 3 = scalar (untransposed) epilogue (register-staged fallback GEMM only)
 };
 
 
@@ -484,17 +484,24 @@ __device__ __forceinline__ f32x4 ld4bf(const bf16* p) {
   return f32x4{bf2f(b[0]), bf2f(b[1]), bf2f(b[2]), bf2f(b[3])};
 }
 
-// Vector epilogue: the MFMA accumulator layout (lane = column, 4 registers =
-// 4 rows) is transposed inside lane quads so each lane owns 4 CONSECUTIVE
-// columns of one row; every load/store of the epilogue is then one 8-/16-byte
-// vector access instead of four 2-/4-byte scalar ones.  Requires N % 4 == 0 and
-// output columns contiguous in groups of 4 (all epilogues except HEAD).
+// Vector epilogue: each lane owns 4 CONSECUTIVE columns of one row, so every
+// load/store of the epilogue is one 8-/16-byte vector access instead of four
+// 2-/4-byte scalar ones.  Requires N % 4 == 0 and output columns contiguous in
+// groups of 4 (all epilogues except HEAD).  Two accumulator layouts:
+//   SW (swapped MFMA operands, the LDS-DMA GEMMs): mfma(B, A) computes C^T, whose
+//     natural layout already is lane = row (li), 4 registers = 4 columns (4g..4g+3)
+//     -- no data movement at all;
+//   !SW (mfma(A, B), the register-staged fallback GEMM): lane = column, 4 registers
+//     = 4 rows, transposed inside lane quads (quad_transpose: ~27 vector
+//     instructions per fragment) to lane = row 4g+x, columns 4q..4q+3.
+// The lanes that share a row are li>>2 = 0..3 (!SW) or g = 0..3 (SW); the LayerNorm
+// statistics reduce over them (lane xor 4, 8 or xor 16, 32).
 //
 // Split in two so the epilogue's global loads (bias, residual, saved
 // pre-activation, embeddings, accumulate target) can be issued BEFORE the main
 // loop (`prefetch`) and land while the MFMAs run: at these sizes a GEMM is a
 // chain of ~3 dependent memory round trips and this removes one of them.
-template <int EPI, int FM, int FN, bool PUB = false>
+template <int EPI, int FM, int FN, bool PUB = false, bool SW = false>
 struct VecEpi {
   static constexpr bool PRE = EPI == EPI_RESID || EPI == EPI_DGELU || EPI == EPI_EMBED || EPI == EPI_ACC;
   static constexpr bool FC = FoldEpi<EPI>::CONSUMER, FP = FoldEpi<EPI>::PRODUCER;
@@ -504,7 +511,7 @@ struct VecEpi {
   f32x4 colb[FN];
   f32x4 pre[FM][FN];
   int rowm[FM];     // GEMM row of the lane's fragment row (-1: out of range)
-  float2 lnst[FM][LN_MAX_SLOTS / 4];  // fold consumer: statistics slots q, q+4, .. of the row
+  float2 lnst[FM][LN_MAX_SLOTS / 4];  // fold consumer: statistics slots u, u+4, .. of the row (u: sharer index)
   f32x4 lnc[FN];    // fold consumer: c of the lane's 4 columns
   bool first_col;   // lane holds column 0 (writes the row's mean / rstd)
   int colbase;      // first column of the wave's tile
@@ -513,22 +520,30 @@ struct VecEpi {
                     //   epilogue's arrays in scratch memory)
   f32x4 clsv[FN];   //   cls + pos[0] + temb[t] of that sample's cls row, the lane's columns
 
+  // lane -> (row within the 16-row fragment, first of its 4 columns within the 16-column fragment)
+  static __device__ __forceinline__ int rsub(int g, int li) { return SW ? li : 4 * g + (li & 3); }
+  static __device__ __forceinline__ int csub(int g, int li) { return SW ? 4 * g : 4 * (li >> 2); }
+  // index 0..3 of the lane among the 4 lanes holding the same row
+  static __device__ __forceinline__ int sharer(int g, int li) { return SW ? g : li >> 2; }
+  template <int K>  // butterfly step k (0, 1) across the row's 4 lanes
+  static __device__ __forceinline__ float2 rowxor(float2 a) { return SW ? f2xor<16 << K>(a) : f2xor<4 << K>(a); }
+
   __device__ __forceinline__ void prefetch(const GemmParams& p, int mb, int nb, int g, int li) {
-    const int x = li & 3, q = li >> 2;
+    const int q = sharer(g, li), cs = csub(g, li), rs = rsub(g, li);
     const bool fold = FC && p.ln_st != nullptr;
     first_col = nb == 0 && q == 0;
     colbase = nb;
     const bool has_bias = (EPI != EPI_ATOMIC) && (EPI != EPI_ACC) && p.bias != nullptr;
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      const int n = nb + j * 16 + 4 * q;
+      const int n = nb + j * 16 + cs;
       colok[j] = n < p.N;
       cols[j] = epi_col<EPI>(p, n);
       colb[j] = (has_bias && colok[j]) ? ld4(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
-      const int m = mb + i * 16 + 4 * g + x;
+      const int m = mb + i * 16 + rs;
       rows[i] = epi_row<EPI>(p, m < p.M ? m : p.M - 1);
       if (m >= p.M) rows[i].off = -1;
       rowm[i] = m < p.M ? m : -1;
@@ -542,7 +557,7 @@ struct VecEpi {
     }
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      const int n = nb + j * 16 + 4 * q;
+      const int n = nb + j * 16 + cs;
       lnc[j] = (fold && colok[j]) ? ld4(p.ln_c + n) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
     cls_i = -1;
@@ -556,7 +571,7 @@ struct VecEpi {
         }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int n = nb + j * 16 + 4 * q;
+        const int n = nb + j * 16 + cs;
         clsv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (cls_i >= 0 && colok[j])
           clsv[j] = ld4(p.cls_src + n) + ld4(p.pos + n) + ld4(p.temb + (size_t)p.tsteps[cls_b] * p.emb_dim + n);
@@ -568,12 +583,12 @@ struct VecEpi {
       for (int j = 0; j < FN; ++j) {
         f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
         if (PRE && rows[i].off >= 0 && colok[j]) {
-          const int n = nb + j * 16 + 4 * q;
+          const int n = nb + j * 16 + cs;
           if (EPI == EPI_RESID) v = ld4(p.res + rows[i].off + n);
           if (EPI == EPI_DGELU) v = ld4bf(p.aux + rows[i].off + n);
           if (EPI == EPI_ACC && !p.acc_store) v = ld4(reinterpret_cast<const float*>(p.C) + rows[i].off + n);
           if (EPI == EPI_EMBED) {
-            const int m = mb + i * 16 + 4 * g + x;
+            const int m = mb + i * 16 + rs;
             const int patch = m - rows[i].b * p.tokens;
             v = ld4(p.pos + (size_t)(patch + 1) * p.emb_dim + n) +
                 ld4(p.temb + (size_t)p.tsteps[rows[i].b] * p.emb_dim + n);
@@ -585,11 +600,12 @@ struct VecEpi {
 
   __device__ __forceinline__ void finish(const GemmParams& p, const f32x4 (&acc_in)[FM][FN], int li) {
     const int x = li & 3;
+    const int g = (threadIdx.x & 63) >> 4;
     f32x4 acc[FM][FN];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = quad_transpose(acc_in[i][j], x);
+      for (int j = 0; j < FN; ++j) acc[i][j] = SW ? acc_in[i][j] : quad_transpose(acc_in[i][j], x);
     uint32_t salt_drop = 0, salt_dp = 0;
     if (p.thr_drop) salt_drop = site_salt(p.rng, p.site_drop);
     if (p.thr_dp) salt_dp = site_salt(p.rng, p.site_dp);
@@ -604,8 +620,8 @@ struct VecEpi {
         float2 t = lnst[i][0];
 #pragma unroll
         for (int k = 1; k < LN_MAX_SLOTS / 4; ++k) t = f2add(t, lnst[i][k]);
-        t = f2add(t, f2xor<4>(t));
-        t = f2add(t, f2xor<8>(t));
+        t = f2add(t, rowxor<0>(t));
+        t = f2add(t, rowxor<1>(t));
         ms[i] = ln_row_stats(p, t);
       } else {
         ms[i] = make_float2(0.f, 1.f);
@@ -702,7 +718,7 @@ struct VecEpi {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         if (cls_i < 0 || !colok[j]) continue;
-        const long long idx = crow + colbase + j * 16 + 4 * (li >> 2);
+        const long long idx = crow + colbase + j * 16 + csub(g, li);
         f32x4 v = clsv[j];
         if (p.thr_drop) {
           bool kp[4];
@@ -721,26 +737,25 @@ struct VecEpi {
 #pragma unroll
         for (int sl = 0; sl < SL; ++sl) {
           float2 t = cpart[sl];
-          t = f2add(t, f2xor<4>(t));
-          t = f2add(t, f2xor<8>(t));
-          if ((li >> 2) == 0 && cls_i >= 0)
+          t = f2add(t, rowxor<0>(t));
+          t = f2add(t, rowxor<1>(t));
+          if (sharer(g, li) == 0 && cls_i >= 0)
             st2f_pub<PUB>(p.st_out + 2 * ((size_t)b * (p.tokens + 1) * np_out + colbase / LN_SLOT + sl), t);
         }
       }
     }
     if (prod) {
-      // the 4 lanes of a row (q = 0..3: lanes x, x+4, x+8, x+12 of the 16-lane
-      // group) hold 32 consecutive columns per slot: reduce, one float2 store per
-      // (row, slot)
+      // the 4 lanes of a row hold 32 consecutive columns per slot (fragments j,
+      // j+1): reduce, one float2 store per (row, slot)
       const int np_out = p.N / LN_SLOT;
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int sl = 0; sl < SL; ++sl) {
           float2 t = part[i][sl];
-          t = f2add(t, f2xor<4>(t));
-          t = f2add(t, f2xor<8>(t));
-          if ((li >> 2) == 0 && rowm[i] >= 0)
+          t = f2add(t, rowxor<0>(t));
+          t = f2add(t, rowxor<1>(t));
+          if (sharer(g, li) == 0 && rowm[i] >= 0)
             st2f_pub<PUB>(p.st_out + 2 * ((size_t)fold_token_row<EPI>(p, rowm[i]) * np_out + colbase / LN_SLOT + sl),
                           t);
         }

@@ -331,6 +331,34 @@ def test_attention_spike_rescale():
     close(o, or_, 2e-2, 2e-2, "o")
 
 
+@pytest.mark.parametrize("B,H,N,hd,p", [(1, 2, 700, 64, 0.0), (1, 2, 700, 64, 0.1), (2, 1, 1030, 32, 0.0),
+                                        (48, 4, 300, 64, 0.0), (48, 4, 300, 64, 0.1)])
+def test_attention_lazy_max_ramp(B, H, N, hd, p):
+    """Flash / resident forwards keep a lazy running max (it moves only when a tile's
+    max exceeds it by 2^8).  Scores that ramp up along the keys, at a different slope
+    per query, make that rescale branch fire at different tiles for different lanes
+    of one wave (and not at all for flat rows): every case against the reference."""
+    g = torch.Generator(device=DEV).manual_seed(3)
+    u = torch.randn(hd, device=DEV, generator=g)
+    u = u / u.norm()
+    a = torch.linspace(0.0, 40.0, N, device=DEV)[torch.randperm(N, device=DEV, generator=g)]  # per-query slope
+    b = torch.linspace(0.0, 8.0, N, device=DEV)                                            # key ramp
+    qkv = torch.empty(3, B, H, N, hd, device=DEV)
+    qkv[0] = a[:, None] * u + 0.05 * torch.randn(B, H, N, hd, device=DEV, generator=g)
+    qkv[1] = b[:, None] * u + 0.05 * torch.randn(B, H, N, hd, device=DEV, generator=g)
+    qkv[2] = torch.randn(B, H, N, hd, device=DEV, generator=g)
+    qkv = qkv.to(torch.bfloat16)
+    r = rng()
+    scale = hd ** -0.5
+    o, lse = ops.attn_fwd(qkv, scale, r, 5, p)
+    or_, lser = ref.attn_fwd(qkv, scale, r, 5, p)
+    close(lse, lser, 1e-3, 1e-4, "lse")
+    close(o, or_, 2e-2, 2e-2, "o")
+    do = bf(B, N, H * hd)
+    close(ops.attn_bwd(do, qkv, o, lse, scale, r, 5, p), ref.attn_bwd(do, qkv, o, lse, scale, r, 5, p),
+          3e-2, 3e-2, "dqkv")
+
+
 # ------------------------------------------------------------------ embedding / loss
 def test_embed_bwd():
     B, N, D = 32, 65, 384
