@@ -610,6 +610,8 @@ static GemmParams base_params(const GemmArgs& a) {
   p.patch_out = reinterpret_cast<bf16*>(a.patch_out);
   p.cls_src = a.cls_src;
   if (p.cls_src != nullptr && p.debug == 3) p.debug = 0;  // the scalar epilogue writes no cls rows
+  p.tok_magic = p.tokens > 1 ? (uint32_t)(0x100000000ull / (uint64_t)p.tokens) : 0xFFFFFFFFu;
+  p.ln_invd = p.K > 0 ? 1.0f / (float)p.K : 0.f;
   return p;
 }
 
@@ -617,6 +619,11 @@ static void check_vec(const GemmParams& p, int epi) {
   // the vector epilogue stores 4 consecutive output columns per lane
   if (epi != EPI_HEAD && (p.N % 4 != 0 || (epi == EPI_QKV && p.hd % 4 != 0) || (epi == EPI_EMBED && p.emb_dim % 4 != 0)))
     throw std::runtime_error("gemm: output width must be a multiple of 4");
+  // ... and indexes its outputs / operands with 32-bit offsets
+  const long long w = std::max({(long long)p.N, (long long)p.ldc, (long long)p.emb_dim});
+  if ((long long)(p.M + p.batch + 1) * w * (p.split_stride > 0 ? 2 : 1) >= (1LL << 31) ||
+      p.split_stride >= (1LL << 30))
+    throw std::runtime_error("gemm: tensors of >= 2^31 elements are not supported by the epilogue's 32-bit indexing");
 }
 
 void gemm_nt(const GemmArgs& a, int epi, hipStream_t stream) {

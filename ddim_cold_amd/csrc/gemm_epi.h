@@ -79,6 +79,8 @@ struct GemmParams {
   bf16* patch_out;
   const float* cls_src;
   int acc_store;  // EPI_ACC: the target is known to be zero -- store, don't read-add
+  uint32_t tok_magic;  // floor(2^32 / tokens) (divmagic: row -> sample without a division)
+  float ln_invd;       // 1 / K (LayerNorm fold consumer: D = K)
   int debug;  // profiling aid (DDIM_COLD_GEMM_DEBUG): 1 = skip the epilogue, 2 = skip the main loop,
               // 3 = scalar (untransposed) epilogue (register-staged fallback GEMM only)
 };
@@ -169,12 +171,48 @@ struct FoldEpi {
 constexpr int LN_SLOT = 32;
 constexpr int LN_MAX_SLOTS = 16;
 
-// (mean, rstd) of a row from its {sum, sum^2} over D = K columns
+// (mean, rstd) of a row from its {sum, sum^2} over D = K columns (1/K from the
+// host; var + eps >= eps > 0, so the bare v_rsq needs no denormal fix-up)
 __device__ __forceinline__ float2 ln_row_stats(const GemmParams& p, float2 st) {
-  const float invd = 1.0f / (float)p.K;
-  const float mu = st.x * invd;
-  const float var = fmaxf(st.y * invd - mu * mu, 0.f);
-  return make_float2(mu, rsqrtf(var + p.ln_eps));
+  const float mu = st.x * p.ln_invd;
+  const float var = fmaxf(st.y * p.ln_invd - mu * mu, 0.f);
+  return make_float2(mu, __builtin_amdgcn_rsqf(var + p.ln_eps));
+}
+
+// m / d for 0 <= m < 2^31 with magic = floor(2^32 / d): the high product is q or
+// q - 1, one compare fixes it (vs ~15 instructions of a division by a runtime d)
+__device__ __forceinline__ int divmagic(int m, int d, uint32_t magic) {
+  int q = (int)__umulhi((uint32_t)m, magic);
+  if (m - q * d >= d) ++q;
+  return q;
+}
+
+// Vector-epilogue destination index, 32-bit (the host checks every output has
+// < 2^31 elements): row part and column part, separable as in epi_row / epi_col.
+struct RowInfo32 {
+  int off;  // -1: skip row
+  int b;    // sample (drop-path / embeddings)
+};
+template <int EPI>
+__device__ __forceinline__ RowInfo32 epi_row32(const GemmParams& p, int m) {
+  RowInfo32 ri;
+  ri.b = 0;
+  if (EPI == EPI_QKV) {
+    const int b = divmagic(m, p.tokens, p.tok_magic), tok = m - b * p.tokens;
+    ri.off = (b * p.heads * p.tokens + tok) * p.hd;
+  } else if (EPI == EPI_RESID) {
+    ri.off = m * p.N;
+    ri.b = p.thr_dp ? divmagic(m, p.tokens, p.tok_magic) : 0;  // drop-path sample (training only)
+  } else if (EPI == EPI_GELU || EPI == EPI_DGELU) {
+    ri.off = m * p.N;
+  } else if (EPI == EPI_EMBED) {
+    const int b = divmagic(m, p.tokens, p.tok_magic);  // tokens = patches per sample here
+    ri.off = (m + b + 1) * p.emb_dim;                  // (b * (P + 1) + patch + 1) * D
+    ri.b = b;
+  } else {
+    ri.off = m * p.ldc;
+  }
+  return ri;
 }
 
 __device__ __forceinline__ float2 f2add(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
@@ -505,8 +543,8 @@ template <int EPI, int FM, int FN, bool PUB = false, bool SW = false>
 struct VecEpi {
   static constexpr bool PRE = EPI == EPI_RESID || EPI == EPI_DGELU || EPI == EPI_EMBED || EPI == EPI_ACC;
   static constexpr bool FC = FoldEpi<EPI>::CONSUMER, FP = FoldEpi<EPI>::PRODUCER;
-  RowInfo rows[FM];
-  long long cols[FN];
+  RowInfo32 rows[FM];
+  int cols[FN];
   bool colok[FN];
   f32x4 colb[FN];
   f32x4 pre[FM][FN];
@@ -525,8 +563,25 @@ struct VecEpi {
   static __device__ __forceinline__ int csub(int g, int li) { return SW ? 4 * g : 4 * (li >> 2); }
   // index 0..3 of the lane among the 4 lanes holding the same row
   static __device__ __forceinline__ int sharer(int g, int li) { return SW ? g : li >> 2; }
-  template <int K>  // butterfly step k (0, 1) across the row's 4 lanes
-  static __device__ __forceinline__ float2 rowxor(float2 a) { return SW ? f2xor<16 << K>(a) : f2xor<4 << K>(a); }
+  // butterfly step K (0, 1) of a sum across the row's 4 lanes: t + partner.  SW:
+  // the partners are 16 / 32 lanes apart, exchanged by v_permlane16/32_swap (the
+  // two swap results ARE {own, partner} in some order: their sum is t + partner,
+  // no address math or LDS crossbar as in __shfl_xor)
+  template <int K>
+  static __device__ __forceinline__ float psum(float v) {
+    const uint32_t u = __float_as_uint(v);
+    if (K == 0) {
+      const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+      return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+    const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  template <int K>
+  static __device__ __forceinline__ float2 rowsum(float2 a) {
+    if (SW) return make_float2(psum<K>(a.x), psum<K>(a.y));
+    return f2add(a, f2xor<4 << K>(a));
+  }
 
   __device__ __forceinline__ void prefetch(const GemmParams& p, int mb, int nb, int g, int li) {
     const int q = sharer(g, li), cs = csub(g, li), rs = rsub(g, li);
@@ -538,13 +593,16 @@ struct VecEpi {
     for (int j = 0; j < FN; ++j) {
       const int n = nb + j * 16 + cs;
       colok[j] = n < p.N;
-      cols[j] = epi_col<EPI>(p, n);
+      // QKV head-major scatter: a 16-column fragment lies inside one head when
+      // hd % 16 == 0, so its (wave-uniform, scalar) base column is mapped once
+      if (EPI == EPI_QKV && (p.hd & 15) == 0) cols[j] = (int)epi_col<EPI>(p, nb + j * 16) + cs;
+      else cols[j] = (int)epi_col<EPI>(p, n);
       colb[j] = (has_bias && colok[j]) ? ld4(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int m = mb + i * 16 + rs;
-      rows[i] = epi_row<EPI>(p, m < p.M ? m : p.M - 1);
+      rows[i] = epi_row32<EPI>(p, m < p.M ? m : p.M - 1);
       if (m >= p.M) rows[i].off = -1;
       rowm[i] = m < p.M ? m : -1;
       const int np_in = p.K / LN_SLOT;
@@ -620,8 +678,7 @@ struct VecEpi {
         float2 t = lnst[i][0];
 #pragma unroll
         for (int k = 1; k < LN_MAX_SLOTS / 4; ++k) t = f2add(t, lnst[i][k]);
-        t = f2add(t, rowxor<0>(t));
-        t = f2add(t, rowxor<1>(t));
+        t = rowsum<1>(rowsum<0>(t));
         ms[i] = ln_row_stats(p, t);
       } else {
         ms[i] = make_float2(0.f, 1.f);
@@ -641,7 +698,7 @@ struct VecEpi {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         if (!colok[j]) continue;
-        const long long idx = rows[i].off + cols[j];
+        const int idx = rows[i].off + cols[j];
         f32x4 v = fold ? (acc[i][j] - ms[i].x * lnc[j]) * ms[i].y + colb[j] : acc[i][j] + colb[j];
         if (EPI == EPI_BF16) {
           st4bf(reinterpret_cast<bf16*>(p.C) + idx + blockIdx.z * p.split_stride, v);
@@ -737,8 +794,7 @@ struct VecEpi {
 #pragma unroll
         for (int sl = 0; sl < SL; ++sl) {
           float2 t = cpart[sl];
-          t = f2add(t, rowxor<0>(t));
-          t = f2add(t, rowxor<1>(t));
+          t = rowsum<1>(rowsum<0>(t));
           if (sharer(g, li) == 0 && cls_i >= 0)
             st2f_pub<PUB>(p.st_out + 2 * ((size_t)b * (p.tokens + 1) * np_out + colbase / LN_SLOT + sl), t);
         }
@@ -753,8 +809,7 @@ struct VecEpi {
 #pragma unroll
         for (int sl = 0; sl < SL; ++sl) {
           float2 t = part[i][sl];
-          t = f2add(t, rowxor<0>(t));
-          t = f2add(t, rowxor<1>(t));
+          t = rowsum<1>(rowsum<0>(t));
           if (sharer(g, li) == 0 && rowm[i] >= 0)
             st2f_pub<PUB>(p.st_out + 2 * ((size_t)fold_token_row<EPI>(p, rowm[i]) * np_out + colbase / LN_SLOT + sl),
                           t);
