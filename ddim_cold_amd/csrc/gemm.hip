@@ -467,11 +467,15 @@ struct DmaTiles<true, BT, EPI> {  // transposed A (wgrad): 64x64
 // DDIM_COLD_GEMM_TILE=0..3 forces a tile.  The LDS-DMA ring needs K % 64 == 0
 // for k-contiguous operands (transposed operands get zero rows past K from the
 // buffer bounds check).
-static int pick_tiles(int M, int N, int K, int splits, bool at, bool bt) {
+static int forced_tile() {
   static const int forced = [] {
     const char* e = getenv("DDIM_COLD_GEMM_TILE");
     return e ? atoi(e) : -1;
   }();
+  return forced;
+}
+static int pick_tiles(int M, int N, int K, int splits, bool at, bool bt) {
+  const int forced = forced_tile();
   static const bool model = getenv_flag("DDIM_COLD_GEMM_TILE_MODEL");
   if (at) return 1;
   if (forced >= 0) return bt && forced > 2 ? 2 : forced;
@@ -498,7 +502,13 @@ template <bool AT, bool BT, int EPI>
 static void launch_auto(GemmParams p, int splits, hipStream_t stream) {
   const bool dma_ok = (AT || BT || p.K % 64 == 0) && (AT || p.K % 64 == 0) && !dma_disabled();
   if (dma_ok) {
-    DmaTiles<AT, BT, EPI>::launch(p, splits, stream, pick_tiles(p.M, p.N, p.K, splits, AT, BT));
+    int cfg = pick_tiles(p.M, p.N, p.K, splits, AT, BT);
+    // the GELU epilogue (erf-GELU + dropout per element, two bf16 outputs) is the
+    // heaviest in vector instructions: twice the waves of 32x64 tiles pay off on the
+    // sampler shape (M=4160: 6.56 vs 7.14 us, tools/gpu_tile_sweep3.sh); the other
+    // epilogues keep 64x64 there (QKV 11.45 vs 13.54, residual 6.65 vs 7.02)
+    if (EPI == EPI_GELU && cfg == 1 && forced_tile() < 0 && ((p.M + 31) / 32) * ((p.N + 63) / 64) <= 1024) cfg = 0;
+    DmaTiles<AT, BT, EPI>::launch(p, splits, stream, cfg);
     return;
   }
   const int tiles64 = ((p.M + 63) / 64) * ((p.N + 63) / 64);
