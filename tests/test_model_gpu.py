@@ -17,6 +17,22 @@ def _rel(a, b):
     return ((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-12)).item()
 
 
+def _frob(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+# Per-tensor bounds, from tools/grad_error_report.py on MI355X (profiles/README.md,
+# round 3): fused program vs the same program on reference ops (identical bf16
+# rounding points, so only summation order / transcendental approximations differ):
+# worst max-rel 5.6e-3, worst Frobenius 4.9e-3 over the 93 gradient tensors;
+# autograd (bf16 MFMA) vs the fp32 model: worst max-rel 8.1e-3, Frobenius 7.0e-3.
+# A bf16 rounding is 2^-9 (2e-3) relative, so the bounds below are a few bf16
+# ulps and ~3-4x the measured worst case.
+PROG_MAXREL, PROG_FROB = 2e-2, 1.5e-2
+FP32_MAXREL, FP32_FROB = 3e-2, 2e-2
+
+
 @pytest.mark.parametrize("name", ["vit_tiny", "oxford_flower"])
 def test_program_fwd_bwd_vs_reference_ops(name):
     torch.manual_seed(0)
@@ -40,10 +56,11 @@ def test_program_fwd_bwd_vs_reference_ops(name):
         torch.cuda.synchronize()
         results.append((out, loss, grads))
     (o1, l1, g1), (o2, l2, g2) = results
-    assert _rel(o1, o2) < 3e-2
+    assert _rel(o1, o2) < PROG_MAXREL
     assert abs(l1.item() - l2.item()) / l2.item() < 1e-2
     for n in g1:
-        assert _rel(g1[n], g2[n]) < 8e-2, n
+        assert _rel(g1[n], g2[n]) < PROG_MAXREL, (n, _rel(g1[n], g2[n]))
+        assert _frob(g1[n], g2[n]) < PROG_FROB, (n, _frob(g1[n], g2[n]))
 
 
 @pytest.mark.parametrize("name", ["vit_tiny", "oxford_flower"])
@@ -96,14 +113,15 @@ def test_autograd_wrapper_matches_plain_model():
     out = m(img, t)
     with torch.no_grad():
         out_ref = m.forward_reference(img, t)
-    assert _rel(out, out_ref) < 3e-2
+    assert _rel(out, out_ref) < FP32_MAXREL
     loss = out.square().mean()
     loss.backward()
     g_fused = {n: p.grad.clone() for n, p in m.named_parameters()}
     m.zero_grad()
     m.forward_reference(img, t).square().mean().backward()
     for n, p in m.named_parameters():
-        assert _rel(g_fused[n], p.grad) < 1e-1, n
+        assert _rel(g_fused[n], p.grad) < FP32_MAXREL, (n, _rel(g_fused[n], p.grad))
+        assert _frob(g_fused[n], p.grad) < FP32_FROB, (n, _frob(g_fused[n], p.grad))
 
 
 def test_high_res_forward():

@@ -12,9 +12,11 @@ from ddim_cold_amd.ops import reference as ref
 
 DEV = "cuda"
 # bounds on |fused - fp32 eager| of final images in [0, 1] after 100-200 DDIM steps
-# (measured on MI355X: see tools/grad_error_report.py and profiles/README.md)
-MEAN_BOUND_K20 = 0.02
-MAX_BOUND_K20 = 0.5
+# (measured on MI355X, round 3, tools/grad_error_report.py: k=20 N=64 mean 7.9e-4,
+# max 5.0e-3 -- the bf16 x0-hat error of each step is re-injected 100 times and
+# amplified up to ~316x by x_t / sqrt(a_t) at t = 1999, so the max bound is looser)
+MEAN_BOUND_K20 = 5e-3
+MAX_BOUND_K20 = 0.1
 
 
 @pytest.fixture(scope="module")
