@@ -70,6 +70,11 @@ def parse_args(argv=None):
     ap.add_argument("--sampler-n", type=int, default=64)
     ap.add_argument("--sampler-host-noise", action="store_true",
                     help="draw the sampler's x_T on the host (torch.normal on CPU, as the reference)")
+    ap.add_argument("--dataset", default="cold", choices=["cold", "gaussian"],
+                    help="training task of the timed steps: cold pixelation pairs (the reference's measured "
+                         "run) or Gaussian DDIM (diffusion_loader.DiffusionDataset: q_sample, t in 0..1999)")
+    ap.add_argument("--no-gaussian", action="store_true",
+                    help="1 GPU: skip the extra Gaussian-DDIM training throughput key")
     ap.add_argument("--no-eager-baseline", action="store_true",
                     help="skip timing the plain eager PyTorch sampler (BASELINE.md's sampling comparator)")
     return ap.parse_args(argv)
@@ -153,7 +158,7 @@ def run(args):
 
     from ddim_cold_amd.models import build_model
     from ddim_cold_amd.train.engine import EngineConfig, TrainEngine
-    from ddim_cold_amd.data.synthetic import ColdBatcher, synthetic_pool
+    from ddim_cold_amd.data.synthetic import ColdBatcher, GaussianBatcher, synthetic_pool
 
     torch.manual_seed(1234)
     model = build_model(args.model).to(dev).train()
@@ -161,13 +166,17 @@ def run(args):
     lr = base_lr * args.batch * n / 512  # multi_gpu_trainer.py:196
     cfg = EngineConfig(lr=lr, t_max=512 * 100, use_graph=not args.no_graph, bucket_blocks=args.bucket_blocks,
                        seed=42, force_segments=args.force_dist,
-                       temb_rows=int(math.log2(model.img_size[1])) + 1,  # cold t in 1..log2(W)
+                       # cold t in 1..log2(W); Gaussian t spans the whole table
+                       temb_rows=int(math.log2(model.img_size[1])) + 1 if args.dataset == "cold" else None,
                        graph_comm=not args.segmented_comm, grad_wire=args.grad_wire,
                        comm_events=not (args.segmented_comm or args.captured_comm),
                        comm=args.comm, graph_steps=args.graph_steps)
     engine = TrainEngine(model, cfg, device=dev)
     pool = synthetic_pool(1024, tuple(model.img_size), seed=7 + rank, device=dev)
-    engine.set_batch_fn(ColdBatcher(pool, args.batch, engine.rng))
+    if args.dataset == "cold":
+        engine.set_batch_fn(ColdBatcher(pool, args.batch, engine.rng))
+    else:
+        engine.set_batch_fn(GaussianBatcher(pool, args.batch, engine.rng, model.total_steps))
 
     if engine.segmented and dev.type == "cuda":
         # outside the timed region; parameters / moments / counters / RNG restored
@@ -200,6 +209,29 @@ def run(args):
     ms = elapsed / args.steps * 1e3
     value = n * args.batch * args.steps / elapsed
     extra = {}
+    if rank == 0 and n == 1 and args.dataset == "cold" and not args.no_gaussian and dev.type == "cuda":
+        # the reference's other training task (DiffusionDataset, diffusion_loader.py:24-58):
+        # Gaussian DDIM, q_sample batch drawn inside the patch-embedding launch, same
+        # model / batch / optimizer; timed the same way (outside the headline number)
+        torch.manual_seed(1234)
+        gm = build_model(args.model).to(dev).train()
+        ge = TrainEngine(gm, EngineConfig(lr=lr, t_max=512 * 100, use_graph=not args.no_graph, seed=43,
+                                          graph_steps=args.graph_steps), device=dev)
+        ge.set_batch_fn(GaussianBatcher(pool, args.batch, ge.rng, gm.total_steps))
+        ge.train_steps(args.warmup)
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        ge.train_steps(args.steps)
+        torch.cuda.synchronize()
+        tg = time.perf_counter() - tg
+        gl = float(ge.loss_last.item())
+        if not math.isfinite(gl):
+            raise SystemExit(f"non-finite Gaussian-DDIM loss {gl}")
+        extra["gaussian_ddim_train_img_per_s"] = round(args.batch * args.steps / tg, 1)
+        extra["gaussian_ddim_train_ms_per_step"] = round(tg / args.steps * 1e3, 4)
+        extra["gaussian_ddim_final_loss"] = round(gl, 5)
+        ge.close()
+        del ge, gm
     # the sampler metric is a 1-GPU number (BASELINE.json config 5): multi-rank runs skip it
     if rank == 0 and n == 1 and not args.no_sampler and dev.type == "cuda":
         from ddim_cold_amd.diffusion.samplers import DDIMSampler
@@ -216,10 +248,10 @@ def run(args):
             s.sample(args.sampler_n, generator=g, device_noise=dn)
         torch.cuda.synchronize()
         dt = (time.perf_counter() - ts) / reps
-        extra = {"ddim_sampler_img_per_s": round(args.sampler_n / dt, 1),
-                 "ddim_sampler_ms_per_batch": round(dt * 1e3, 3),
-                 "ddim_sampler_config": {"k": args.sampler_k, "N": args.sampler_n, "steps": len(s.ts),
-                                         "graph": True, "noise": "device" if dn else "host"}}
+        extra.update({"ddim_sampler_img_per_s": round(args.sampler_n / dt, 1),
+                      "ddim_sampler_ms_per_batch": round(dt * 1e3, 3),
+                      "ddim_sampler_config": {"k": args.sampler_k, "N": args.sampler_n, "steps": len(s.ts),
+                                              "graph": True, "noise": "device" if dn else "host"}})
         if not args.no_eager_baseline:
             # the sampling yardstick is a plain eager PyTorch-ROCm
             # implementation of the same math on the same GPU (fp32, as the
@@ -246,8 +278,9 @@ def run(args):
         model.train()
     if rank == 0:
         out = {
-            "metric": "train imgs/sec (whole node) ViT-tiny 64x64" if args.model == "vit_tiny"
-                      else f"train imgs/sec (whole node) {args.model}",
+            "metric": ("train imgs/sec (whole node) ViT-tiny 64x64" if args.model == "vit_tiny"
+                       else f"train imgs/sec (whole node) {args.model}") +
+                      ("" if args.dataset == "cold" else " Gaussian DDIM"),
             "value": round(value, 1),
             "unit": "img/s",
             "n_gpus": n,
@@ -257,9 +290,12 @@ def run(args):
             "higher_is_better": True,
             "scaling": "weak",
             # the reference's number is for the vit_tiny yaml config only
-            "vs_baseline": round(value / (BASELINE_IMG_S_PER_GPU * n), 3) if args.model == "vit_tiny" else None,
+            "vs_baseline": round(value / (BASELINE_IMG_S_PER_GPU * n), 3)
+                           if args.model == "vit_tiny" and args.dataset == "cold" else None,
             "dtype": "bf16",
-            "data": "synthetic (on-device Oxford-Flowers-shaped pool, cold pixelation pairs), random-init weights",
+            "data": "synthetic (on-device Oxford-Flowers-shaped pool, " +
+                    ("cold pixelation pairs" if args.dataset == "cold" else "Gaussian DDIM q_sample pairs") +
+                    "), random-init weights",
             "config": {"model": f"{args.model} (D={model.embed_dim}, depth={len(model.blocks)}, "
                                 f"heads={model.blocks[0].attn.num_heads}, patch={model.patch_size}, "
                                 f"{model.img_size[0]}x{model.img_size[1]})", "global_batch": args.batch * n,

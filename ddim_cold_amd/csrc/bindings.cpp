@@ -170,13 +170,22 @@ std::tuple<Tensor, Tensor> patch_embed_cold_fwd(Tensor pool, int64_t data_site, 
                                                 bool target_x0, Tensor img, Tensor target, Tensor t, Tensor idx,
                                                 bool write_xt, Tensor w_pe, Tensor b_pe, Tensor cls, Tensor pos,
                                                 Tensor temb, Tensor rng, int64_t site, double p, int64_t patch,
-                                                c10::optional<Tensor> ln_st, c10::optional<Tensor> xb_out) {
+                                                c10::optional<Tensor> ln_st, c10::optional<Tensor> xb_out,
+                                                int64_t gauss_T, int64_t noise_site) {
   CHECK_IN(pool, F32); CHECK_IN(img, F32); CHECK_IN(target, F32); CHECK_IN(t, I64); CHECK_IN(idx, I64);
   const int B = img.size(0), C = img.size(1), H = img.size(2), W = img.size(3);
   TORCH_CHECK(pool.dim() == 4 && pool.size(1) == C && pool.size(2) == H && pool.size(3) == W, "pool shape");
   TORCH_CHECK(target.sizes() == img.sizes() && t.numel() == B && idx.numel() == B, "cold patch-embed shapes");
-  TORCH_CHECK(max_t >= 1 && (1 << max_t) <= W && (1 << max_t) <= H, "max_t");
+  if (gauss_T > 0) {
+    TORCH_CHECK(target_x0, "Gaussian batch: the target is x0");
+    TORCH_CHECK(gauss_T <= temb.size(0), "Gaussian batch: T exceeds the time-embedding rows");
+    TORCH_CHECK((int64_t)B * C * H * W < ((int64_t)1 << 31), "Gaussian batch: 32-bit noise index");
+  } else {
+    TORCH_CHECK(max_t >= 1 && (1 << max_t) <= W && (1 << max_t) <= H, "max_t");
+  }
   ColdSrc cs;
+  cs.gauss_T = gauss_T;
+  cs.noise_site = noise_site;
   cs.pool = pool.data_ptr<float>();
   cs.pool_n = pool.size(0);
   cs.site = data_site;
@@ -781,6 +790,21 @@ std::tuple<Tensor, Tensor> pixelate_pair(Tensor img, c10::optional<Tensor> idx, 
   return {xt, xtm1};
 }
 
+// Gaussian DDIM batch (GaussianBatcher): x_t = q_sample(pool[idx], t, eps), x0 = pool[idx]
+void gauss_batch(Tensor pool, Tensor rng, int64_t site, int64_t noise_site, int64_t T, Tensor x_t, Tensor x0,
+                 Tensor t, Tensor idx, bool draw_idx) {
+  CHECK_IN(pool, F32); check_rng(rng); CHECK_IN(x_t, F32); CHECK_IN(x0, F32); CHECK_IN(t, I64); CHECK_IN(idx, I64);
+  const c10::DeviceGuard guard(pool.device());
+  TORCH_CHECK(x_t.dim() == 4, "gauss_batch: x_t must be [B,C,H,W]");
+  const int B = x_t.size(0), C = x_t.size(1), H = x_t.size(2), W = x_t.size(3);
+  TORCH_CHECK(pool.dim() == 4 && pool.size(1) == C && pool.size(2) == H && pool.size(3) == W, "pool shape");
+  TORCH_CHECK(x0.sizes() == x_t.sizes() && t.numel() == B && idx.numel() == B, "gauss_batch shapes");
+  TORCH_CHECK(T >= 1 && (int64_t)B * C * H * W < ((int64_t)1 << 31), "gauss_batch: T / size");
+  gauss_batch_launch(pool.data_ptr<float>(), pool.size(0), rng.data_ptr<int64_t>(), site, noise_site, T,
+                     x_t.data_ptr<float>(), x0.data_ptr<float>(), t.data_ptr<int64_t>(), idx.data_ptr<int64_t>(),
+                     draw_idx, B, C, H, W, cur_stream());
+}
+
 void cold_batch(Tensor pool, Tensor rng, int64_t site, Tensor x_t, Tensor x_tm1, Tensor t, Tensor idx_ws,
                 int64_t max_t, bool draw_idx) {
   CHECK_IN(pool, F32); check_rng(rng); CHECK_IN(x_t, F32); CHECK_IN(x_tm1, F32); CHECK_IN(t, I64);
@@ -914,7 +938,9 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("patch_embed_cold_fwd(Tensor pool, int data_site, int max_t, bool draw_idx, bool target_x0, "
         "Tensor(a!) img, Tensor(b!) target, Tensor(c!) t, Tensor(d!) idx, bool write_xt, Tensor w_pe, Tensor b_pe, "
         "Tensor cls, Tensor pos, Tensor temb, Tensor rng, int site, float p, int patch, Tensor(e!)? ln_st=None, "
-        "Tensor(f!)? xb_out=None) -> (Tensor, Tensor)");
+        "Tensor(f!)? xb_out=None, int gauss_T=0, int noise_site=0) -> (Tensor, Tensor)");
+  m.def("gauss_batch(Tensor pool, Tensor rng, int site, int noise_site, int T, Tensor(a!) x_t, Tensor(b!) x0, "
+        "Tensor(c!) t, Tensor(d!) idx, bool draw_idx=True) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
@@ -951,4 +977,5 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("q_sample", &q_sample);
   m.impl("pixelate_pair", &pixelate_pair);
   m.impl("cold_batch", &cold_batch);
+  m.impl("gauss_batch", &gauss_batch);
 }

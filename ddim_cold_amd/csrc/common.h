@@ -179,4 +179,26 @@ __device__ __forceinline__ int cold_draw_t(uint32_t salt, int b, int max_t) {
   return 1 + (int)(mix32(((uint32_t)(2 * b + 1) * 0x9E3779B1u) ^ salt) % (uint32_t)max_t);
 }
 
+// Gaussian DDIM batch (diffusion_loader.py:24-58): t ~ U{0..T-1} from the same
+// hash slot as the cold t; eps = element o of randn_kernel's draw over the
+// [B,C,H,W] noise tensor (Box-Muller pair o/2, cos for even o, sin for odd);
+// x_t = sqrt(a_t) x0 + sqrt(1-a_t) eps, a_t = 1 - sqrt((t+1)/T) (q_sample_kernel).
+__device__ __forceinline__ int gauss_draw_t(uint32_t salt, int b, int T) {
+  return (int)(mix32(((uint32_t)(2 * b + 1) * 0x9E3779B1u) ^ salt) % (uint32_t)T);
+}
+__device__ __forceinline__ float gauss_eps(uint32_t nsalt, uint32_t o) {
+  const uint32_t i = o >> 1;
+  const float a = ((float)(mix32((2u * i * 0x9E3779B1u) ^ nsalt) >> 8) + 0.5f) * (1.0f / 16777216.0f);
+  const float b = ((float)(mix32(((2u * i + 1u) * 0x9E3779B1u) ^ nsalt) >> 8) + 0.5f) * (1.0f / 16777216.0f);
+  const float r = sqrtf(-2.f * __logf(a));
+  float s, c;
+  __sincosf(6.283185307179586f * b, &s, &c);
+  return (o & 1u) ? r * s : r * c;
+}
+__device__ __forceinline__ void gauss_coef(int t, int T, float& sa, float& s1a) {
+  const float a = (float)(1.0 - sqrt(((double)t + 1.0) / (double)T));
+  sa = sqrtf(a);
+  s1a = sqrtf(1.f - a);
+}
+
 }  // namespace dc

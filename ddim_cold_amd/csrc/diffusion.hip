@@ -119,6 +119,33 @@ __global__ __launch_bounds__(256) void cold_batch_kernel(const float* __restrict
   }
 }
 
+// Gaussian DDIM batch in ONE launch (GaussianBatcher; diffusion_loader.py:24-58):
+// pool index + t ~ U{0..T-1} per sample from the data site's hash, eps from the
+// noise site, x_t = q_sample(x0, t, eps); the fused patch-embed path derives the
+// same values (embed.hip).
+__global__ __launch_bounds__(256) void gauss_batch_kernel(const float* __restrict__ pool, int pool_n,
+                                                          const int64_t* __restrict__ rng, int site, int noise_site,
+                                                          int T, int64_t* __restrict__ idx, int64_t* __restrict__ t,
+                                                          int draw_idx, float* __restrict__ xt, float* __restrict__ x0o,
+                                                          int B, int per) {
+  const uint32_t salt = site_salt(rng, site), nsalt = site_salt(rng, noise_site);
+  const int n = B * per;
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) {
+    const int b = e / per, rem = e - b * per;
+    const int src = draw_idx ? cold_draw_idx(salt, b, pool_n) : (int)idx[b];
+    const int tt = gauss_draw_t(salt, b, T);
+    if (rem == 0) {
+      if (draw_idx) idx[b] = src;
+      t[b] = tt;
+    }
+    float sa, s1a;
+    gauss_coef(tt, T, sa, s1a);
+    const float x0 = pool[(size_t)src * per + rem];
+    x0o[e] = x0;
+    xt[e] = sa * x0 + s1a * gauss_eps(nsalt, (uint32_t)e);
+  }
+}
+
 static int g_grid(int64_t n) {
   int64_t g = (n + 255) / 256;
   if (g > 4096) g = 4096;
@@ -149,6 +176,14 @@ void pixelate_pair_launch(const float* img, const int64_t* idx, const int64_t* t
                           int C, int H, int W, hipStream_t stream) {
   hipLaunchKernelGGL(pixelate_pair_kernel, dim3(g_grid((int64_t)B * C * H * W)), dim3(256), 0, stream, img, idx, t,
                      x_t, x_tm1, B, C, H, W);
+}
+
+void gauss_batch_launch(const float* pool, int pool_n, const int64_t* rng, int site, int noise_site, int T,
+                        float* x_t, float* x0, int64_t* t, int64_t* idx, bool draw_idx, int B, int C, int H, int W,
+                        hipStream_t stream) {
+  const int per = C * H * W;
+  hipLaunchKernelGGL(gauss_batch_kernel, dim3(g_grid((int64_t)B * per)), dim3(256), 0, stream, pool, pool_n, rng, site,
+                     noise_site, T, idx, t, draw_idx ? 1 : 0, x_t, x0, B, per);
 }
 
 void cold_batch_launch(const float* pool, int pool_n, const int64_t* rng, int site, float* x_t, float* x_tm1,

@@ -28,6 +28,7 @@ __global__ __launch_bounds__(256) void patchify_cls_kernel(const float* __restri
                                                            bf16* __restrict__ xb, int patch_blocks, ColdSrc cs) {
   const int Hp = H / P, Wp = W / P, NP = Hp * Wp, F = C * P * P, N = NP + 1;
   const uint32_t csalt = cs.pool ? site_salt(rng, cs.site) : 0u;
+  const uint32_t nsalt = cs.gauss_T ? site_salt(rng, cs.noise_site) : 0u;
   if ((int)blockIdx.x >= patch_blocks) {
     // cls row of sample b
     const int b = blockIdx.x - patch_blocks;
@@ -35,7 +36,7 @@ __global__ __launch_bounds__(256) void patchify_cls_kernel(const float* __restri
     const uint32_t salt = thr ? site_salt(rng, site) : 0u;
     int64_t tb;
     if (cs.pool) {  // this block owns sample b's draw: publish (t, pool index) for the model
-      tb = cold_draw_t(csalt, b, cs.max_t);
+      tb = cs.gauss_T ? gauss_draw_t(csalt, b, cs.gauss_T) : cold_draw_t(csalt, b, cs.max_t);
       if (threadIdx.x == 0) {
         cs.t_out[b] = tb;
         if (cs.draw_idx) cs.idx[b] = cold_draw_idx(csalt, b, cs.pool_n);
@@ -81,7 +82,20 @@ __global__ __launch_bounds__(256) void patchify_cls_kernel(const float* __restri
     const int hp = pidx / Wp, wp = pidx - hp * Wp;
     const int c = k / (P * P), ij = k - c * P * P, i = ij / P, j = ij - i * P;
     const int y = hp * P + i, xx = wp * P + j;
-    if (cs.pool) {
+    if (cs.pool && cs.gauss_T) {
+      // Gaussian DDIM batch fused in: x_t = sqrt(a_t) x0 + sqrt(1-a_t) eps straight
+      // into the patch row, target = x0 (gauss_batch_kernel's values)
+      const int src = cs.draw_idx ? cold_draw_idx(csalt, b, cs.pool_n) : (int)cs.idx[b];
+      const int tt = gauss_draw_t(csalt, b, cs.gauss_T);
+      float sa, s1a;
+      gauss_coef(tt, cs.gauss_T, sa, s1a);
+      const size_t o = (((size_t)b * C + c) * H + y) * W + xx;
+      const float x0 = cs.pool[((size_t)src * C + c) * H * W + (size_t)y * W + xx];
+      const float xt = sa * x0 + s1a * gauss_eps(nsalt, (uint32_t)o);
+      cs.target[o] = x0;
+      if (cs.x_t) cs.x_t[o] = xt;
+      patches[e] = f2bf(xt);
+    } else if (cs.pool) {
       // cold batch fused in: pixelate the pool image straight into the patch row
       // (x_t) and write the target image (x_{t-1}, or x0) -- same values as
       // cold_batch_kernel + this kernel's image path, one launch fewer

@@ -148,7 +148,14 @@ struct ColdSrc {
   int64_t* t_out = nullptr;  // [B] t (== the `t` the GEMM epilogue reads)
   float* target = nullptr;   // [B,C,H,W] x_{t-1} (or x0)
   float* x_t = nullptr;      // optional [B,C,H,W] x_t image
+  // gauss_T > 0: Gaussian DDIM batch instead (t in 0..T-1, x_t = q_sample(x0, t, eps),
+  // eps drawn at noise_site, target = x0)
+  int gauss_T = 0, noise_site = 0;
 };
+// Gaussian DDIM batch on device in one launch (pool draw, noise, q_sample)
+void gauss_batch_launch(const float* pool, int pool_n, const int64_t* rng, int site, int noise_site, int T,
+                        float* x_t, float* x0, int64_t* t, int64_t* idx, bool draw_idx, int B, int C, int H, int W,
+                        hipStream_t stream);
 void patchify_cls_launch(const float* img, const int64_t* t, const float* cls, const float* pos,
                          const float* temb, void* patches, float* x, int B, int C, int H, int W, int patch,
                          int D, const int64_t* rng, int site, double p, float* st, void* xb, hipStream_t stream,

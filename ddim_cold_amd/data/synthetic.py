@@ -67,7 +67,7 @@ class ColdBatcher:
         """Deferred form for a consumer that fuses the draw into its patch embedding
         (:func:`ops.patch_embed_cold_fwd`): ``((x_t, target, t), cold)`` without launching
         anything; x_t is not materialised (the patch rows are pixelated from the pool)."""
-        cold = (self.pool, SITE_DATA, self.max_t, self.draw, self.target == "x0", self.x_tm1, self.idx, False)
+        cold = (self.pool, SITE_DATA, self.max_t, self.draw, self.target == "x0", self.x_tm1, self.idx, False, 0, 0)
         return (self.x_t, self.x_tm1, self.t), cold
 
     def __call__(self):
@@ -79,7 +79,10 @@ class ColdBatcher:
 
 
 class GaussianBatcher:
-    """Device-side Gaussian DDIM batch source: (q_sample(x0, t, eps), x0, t), t ~ U{0..T-1}."""
+    """Device-side Gaussian DDIM batch source: (q_sample(x0, t, eps), x0, t), t ~ U{0..T-1}
+    (``DiffusionDataset``, diffusion_loader.py:24-58).  One launch (:func:`ops.gauss_batch`:
+    pool draw + noise + q_sample), or none at all when the engine fuses the draw into
+    its patch-embedding launch (:meth:`fused_spec`, same values)."""
 
     def __init__(self, pool: torch.Tensor, batch: int, rng: torch.Tensor, total_steps: int = 2000,
                  idx: torch.Tensor | None = None):
@@ -87,26 +90,23 @@ class GaussianBatcher:
         B, (C, H, W) = batch, pool.shape[1:]
         dev = pool.device
         self.T = total_steps
+        self.x_t = torch.empty(B, C, H, W, device=dev)
         self.x0 = torch.empty(B, C, H, W, device=dev)
-        self.eps = torch.empty(B, C, H, W, device=dev)
+        self.t = torch.empty(B, dtype=torch.int64, device=dev)
+        self.draw = idx is None
+        self.idx = torch.empty(B, dtype=torch.int64, device=dev) if idx is None else idx
         self.rng = rng
-        self.u = torch.empty(2 * B, device=dev)
         self.B = B
-        self.idx = idx
+
+    def fused_spec(self):
+        """``((x_t, x0, t), spec)`` for :func:`ops.patch_embed_cold_fwd` (Gaussian mode)."""
+        cold = (self.pool, SITE_DATA, 1, self.draw, True, self.x0, self.idx, False, self.T, SITE_NOISE)
+        return (self.x_t, self.x0, self.t), cold
 
     def __call__(self):
-        ops.randn_(self.eps, self.rng, SITE_NOISE)
-        ops.randn_(self.u, self.rng, SITE_DATA)
-        # uniform indices / timesteps from the normal draws via the Gaussian CDF
-        u = 0.5 * (1 + torch.erf(self.u / math.sqrt(2)))
-        t = (u[self.B:] * self.T).long().clamp_(0, self.T - 1)
-        if self.idx is None:
-            idx = (u[: self.B] * self.pool.shape[0]).long().clamp_(0, self.pool.shape[0] - 1)
-        else:
-            idx = self.idx
-        torch.index_select(self.pool, 0, idx, out=self.x0)
-        x_t = ops.q_sample(self.x0, t, self.eps, self.T)
-        return x_t, self.x0, t
+        ops.gauss_batch(self.pool, self.rng, SITE_DATA, SITE_NOISE, self.T, self.x_t, self.x0, self.t, self.idx,
+                        self.draw)
+        return self.x_t, self.x0, self.t
 
 
 def make_batcher(kind: str, pool: torch.Tensor, batch: int, rng: torch.Tensor, total_steps: int = 2000,

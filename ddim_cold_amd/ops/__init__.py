@@ -21,7 +21,7 @@ __all__ = [
     "linear_residual_fwd", "linear_gelu_fwd", "head_fwd", "smooth_l1_fwd_bwd", "img_to_tokgrad",
     "linear_dgrad", "linear_dgrad_gelu", "linear_wgrad", "layernorm_bwd", "attn_bwd", "embed_bwd",
     "sqnorm", "adamw_step", "advance_counters", "ddim_step", "ddim_step_", "randn_", "q_sample",
-    "pixelate_pair", "cold_batch", "patch_embed_cold_fwd", "ln_fold_",
+    "pixelate_pair", "cold_batch", "gauss_batch", "patch_embed_cold_fwd", "ln_fold_",
 ]
 
 
@@ -57,15 +57,21 @@ def patch_embed_cold_fwd(cold, img, t, w_pe, b_pe, cls, pos, temb, rng, site: in
     training step): ``cold = (pool, data_site, max_t, draw_idx, target_x0, target,
     idx, write_xt)``; the patch rows are pixelated straight from the pool, ``target``,
     ``t`` and (if ``draw_idx``) ``idx`` are written, ``img`` (x_t) only if ``write_xt``.
-    Same values as ``cold_batch`` then ``patch_embed_fwd``."""
-    pool, dsite, max_t, draw, tx0, target, idx, write_xt = cold
+    Same values as ``cold_batch`` then ``patch_embed_fwd``.  Two optional trailing
+    entries ``(gauss_T, noise_site)`` with ``gauss_T > 0`` select the Gaussian DDIM
+    batch instead (same values as :func:`gauss_batch` then ``patch_embed_fwd``)."""
+    pool, dsite, max_t, draw, tx0, target, idx, write_xt = cold[:8]
+    gT, nsite = (int(cold[8]), int(cold[9])) if len(cold) > 8 else (0, 0)
     if _hip(img):
         return _ops().patch_embed_cold_fwd(pool, int(dsite), int(max_t), bool(draw), bool(tx0), img, target, t, idx,
                                            bool(write_xt), w_pe, b_pe, cls, pos, temb, rng, site, float(p), patch,
-                                           ln_st, xb_out)
-    cold_batch(pool, rng, dsite, img, target, t, idx, max_t, draw)
-    if tx0:
-        torch.index_select(pool, 0, idx, out=target)
+                                           ln_st, xb_out, gT, nsite)
+    if gT > 0:
+        gauss_batch(pool, rng, dsite, nsite, gT, img, target, t, idx, draw)
+    else:
+        cold_batch(pool, rng, dsite, img, target, t, idx, max_t, draw)
+        if tx0:
+            torch.index_select(pool, 0, idx, out=target)
     return patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site, p, patch, ln_st, xb_out)
 
 
@@ -446,6 +452,25 @@ def pixelate_pair(img, idx, t, B: int):
     xt = torch.stack([ref.pixelate(src[i:i + 1], 2 ** int(t[i]))[0] for i in range(B)])
     xtm1 = torch.stack([ref.pixelate(src[i:i + 1], 2 ** (int(t[i]) - 1))[0] for i in range(B)])
     return xt, xtm1
+
+
+def gauss_batch(pool, rng, site: int, noise_site: int, total_steps: int, x_t, x0, t, idx, draw_idx: bool = True):
+    """Gaussian DDIM batch on device in one launch (diffusion_loader.py:24-58): pool
+    index (unless ``draw_idx`` is False: ``idx`` holds them) and t ~ U{0..T-1} from the
+    ``site`` hash, eps = :func:`randn_` of a [B,C,H,W] tensor at ``noise_site``,
+    ``x_t = q_sample(x0, t, eps)``; ``x0`` = the pool images."""
+    if _hip(pool):
+        return _ops().gauss_batch(pool, rng, site, noise_site, total_steps, x_t, x0, t, idx, bool(draw_idx))
+    salt = ref.site_salt(rng, site)
+    B = x_t.shape[0]
+    b = torch.arange(B, dtype=torch.int64)
+    if draw_idx:
+        idx.copy_(ref.mix32(ref._mul32((2 * b) & ref.MASK32, ref.GOLDEN) ^ salt) % pool.shape[0])
+    t.copy_(ref.mix32(ref._mul32((2 * b + 1) & ref.MASK32, ref.GOLDEN) ^ salt) % total_steps)
+    eps = torch.empty_like(x_t)
+    randn_(eps, rng, noise_site)
+    torch.index_select(pool, 0, idx, out=x0)
+    x_t.copy_(ref.q_sample(x0, t, eps, total_steps))
 
 
 def cold_batch(pool, rng, site: int, x_t, x_tm1, t, idx_ws, max_t: int, draw_idx: bool = True):

@@ -134,6 +134,17 @@ def test_cold_batcher_cpu_semantics():
     g = GaussianBatcher(pool, 8, rng)
     xg, x0g, tg = g()
     assert xg.shape == (8, 3, 32, 32) and tg.min() >= 0 and tg.max() < 2000
+    # x_t = q_sample(x0, t, eps) with eps = randn_ at the noise site, x0 = pool[idx]
+    from ddim_cold_amd import ops
+    from ddim_cold_amd.data.synthetic import SITE_NOISE
+    assert torch.equal(x0g, pool[g.idx])
+    eps = torch.empty_like(xg)
+    ops.randn_(eps, rng, SITE_NOISE)
+    a = (1 - torch.sqrt((tg.double() + 1) / 2000)).float().view(-1, 1, 1, 1)
+    assert torch.allclose(xg, a.sqrt() * x0g + (1 - a).sqrt() * eps, atol=1e-6)
+    # the fused-spec form (patch-embedding launch) draws the same batch
+    (xs, x0s, ts), spec = g.fused_spec()
+    assert spec[8] == 2000 and spec[4] is True and xs is g.x_t and x0s is g.x0 and ts is g.t
 
 
 def test_counter_rng_advances():

@@ -181,3 +181,75 @@ def test_graph_evaluate_matches_eager(kind):
         eng.detach()
     (g1, g2), (e1, e2) = vals
     assert abs(g1 - e1) <= 1e-6 * abs(e1) and abs(g2 - e2) <= 1e-6 * abs(e2), vals
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("draw", [True, False])
+def test_gauss_batch_matches_reference_and_fused_embed(draw):
+    """ops.gauss_batch (one launch: pool draw + randn + q_sample) == the CPU reference
+    (same counter hash: t/idx exact, x_t to float rounding of the fast log/sincos), and
+    the Gaussian mode of ops.patch_embed_cold_fwd == gauss_batch then patch_embed_fwd."""
+    from ddim_cold_amd import ops
+    from ddim_cold_amd.data.synthetic import SITE_DATA, SITE_NOISE
+    from ddim_cold_amd.models.program import SITE_EMBED
+    torch.manual_seed(0)
+    model = build_model("vit_tiny").cuda().train()
+    B, D, T = 8, model.embed_dim, model.total_steps
+    N = model.patch_embed.num_patches + 1
+    pool = synthetic_pool(32, seed=2, device="cuda")
+    rng = torch.tensor([11, 5], dtype=torch.int64, device="cuda")
+    idx0 = torch.randint(0, 32, (B,), device="cuda")
+
+    def bufs(dev="cuda"):
+        return (torch.empty(B, 3, 64, 64, device=dev), torch.empty(B, 3, 64, 64, device=dev),
+                torch.empty(B, dtype=torch.int64, device=dev), idx0.clone().to(dev))
+
+    xt, x0, t, idx = bufs()
+    ops.gauss_batch(pool, rng, SITE_DATA, SITE_NOISE, T, xt, x0, t, idx, draw)
+    cx, c0, ct, cidx = bufs("cpu")
+    ops.gauss_batch(pool.cpu(), rng.cpu(), SITE_DATA, SITE_NOISE, T, cx, c0, ct, cidx, draw)
+    torch.cuda.synchronize()
+    assert torch.equal(t.cpu(), ct) and torch.equal(idx.cpu(), cidx) and torch.equal(x0.cpu(), c0)
+    assert int(t.min()) >= 0 and int(t.max()) < T
+    assert (xt.cpu() - cx).abs().max().item() < 2e-4
+    # noise statistics over the batch: standard normal
+    eps = (cx - c0 * torch.sqrt(1 - torch.sqrt((ct.double() + 1) / T)).float().view(-1, 1, 1, 1))
+    eps = eps / torch.sqrt(torch.sqrt((ct.double() + 1) / T)).float().view(-1, 1, 1, 1)
+    assert abs(eps.mean().item()) < 0.02 and abs(eps.std().item() - 1) < 0.02
+
+    pe_w = model.patch_embed.proj.weight.detach().reshape(D, -1).to(torch.bfloat16).contiguous()
+    args = (pe_w, model.patch_embed.proj.bias.detach(), model.cls_token.detach(), model.pos_embed.detach(),
+            model.time_embed.weight.detach(), rng, SITE_EMBED, 0.1, model.patch_size)
+    st = torch.empty(B * N, D // 32, 2, device="cuda")
+    xb = torch.empty(B * N, D, dtype=torch.bfloat16, device="cuda")
+    x_ref, p_ref = ops.patch_embed_fwd(xt, t, *args, ln_st=st, xb_out=xb)
+    xt2, x02, t2, idx2 = bufs()
+    st2, xb2 = torch.empty_like(st), torch.empty_like(xb)
+    spec = (pool, SITE_DATA, 1, draw, True, x02, idx2, True, T, SITE_NOISE)
+    x, p = ops.patch_embed_cold_fwd(spec, xt2, t2, *args, ln_st=st2, xb_out=xb2)
+    torch.cuda.synchronize()
+    assert torch.equal(t2, t) and torch.equal(idx2, idx) and torch.equal(x02, x0)
+    assert (xt2 - xt).abs().max().item() <= 1e-6
+    assert (p.float() - p_ref.float()).abs().max().item() <= 1e-2
+    assert (x - x_ref).abs().max().item() <= 2e-2
+
+
+@pytest.mark.gpu
+def test_engine_gaussian_fused_batch_matches_unfused():
+    """Gaussian DDIM training (t over the whole 2000-row table): the draw fused into the
+    patch-embedding launch trains like the one-launch GaussianBatcher path."""
+    from ddim_cold_amd.data.synthetic import GaussianBatcher
+
+    def run(fuse):
+        torch.manual_seed(0)
+        model = build_model("vit_tiny").cuda().train()
+        eng = TrainEngine(model, EngineConfig(lr=1e-3, t_max=100, seed=3, use_graph=True, graph_warmup=1,
+                                              fuse_batch=fuse))
+        eng.set_batch_fn(GaussianBatcher(synthetic_pool(64, seed=1, device="cuda"), 8, eng.rng, 2000))
+        losses = [float(eng.train_step()) for _ in range(4)]
+        torch.cuda.synchronize()
+        return eng.flat_p.clone(), losses
+    pf, lf = run(True)
+    pu, lu = run(False)
+    assert all(abs(a - b) <= 1e-3 * abs(b) for a, b in zip(lf, lu)), (lf, lu)
+    assert (pf - pu).abs().max().item() <= 2 * 1e-3 * 4
