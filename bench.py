@@ -63,9 +63,9 @@ def parse_args(argv=None):
                     help="gradient collectives through torch.distributed (RCCL) or the native RCCL communicator "
                          "(auto: native if it comes up and verifies on every rank)")
     ap.add_argument("--comm-layout", default="auto",
-                    choices=["auto", "overlap-2", "overlap-4", "inline-1"],
-                    help="data parallel: gradient-exchange layout; auto = TrainEngine.autotune_comm() measures "
-                         "each on this job's ranks before the warmup (training state restored afterwards)")
+                    help="data parallel: gradient-exchange layout (overlap-<blocks per bucket> | inline-1); auto = "
+                         "TrainEngine.autotune_comm() measures the cost model's pick + overlap-2/4 + inline-1 on this "
+                         "job's ranks before the warmup (training state restored afterwards)")
     ap.add_argument("--sampler-k", type=int, default=20)
     ap.add_argument("--sampler-n", type=int, default=64)
     ap.add_argument("--sampler-host-noise", action="store_true",
@@ -178,12 +178,21 @@ def run(args):
     else:
         engine.set_batch_fn(GaussianBatcher(pool, args.batch, engine.rng, model.total_steps))
 
+    comm_model = None
     if engine.segmented and dev.type == "cuda":
         # outside the timed region; parameters / moments / counters / RNG restored
+        if n > 1:
+            # measured all-reduce curve on this job's ranks -> fitted cost model, which
+            # orders the bucket layouts (parallel/costmodel.py); outside the timed region
+            fit, probe = engine.probe_allreduce()
+            comm_model = {"probe_us": {f"{b / 2**20:g}MB": round(u, 1) for b, u in probe.items()},
+                          "alpha_us": round(fit.alpha_us, 2), "algbw_GBs": round(fit.algbw_gbs, 1),
+                          "busbw_GBs": round(fit.busbw_gbs, 1),
+                          "predicted_exposed_us": {L[0]: round(L[4], 1) for L in engine.model_layouts()[:4]}}
         if args.comm_layout == "auto":
             engine.autotune_comm()
         else:
-            lay = {L[0]: L for L in engine.COMM_LAYOUTS}[args.comm_layout]
+            lay = engine.layout_by_name(args.comm_layout)
             engine.set_comm_layout(lay[1], lay[2], lay[3])
             engine.comm_choice = lay[0]
     engine.train_steps(args.warmup)
@@ -317,6 +326,7 @@ def run(args):
                        "launcher": "torchrun/env" if os.environ.get("TORCHELASTIC_RUN_ID") else
                        ("self-spawn" if n > 1 else "single"),
                        "comm_layout_ms": {k: round(v, 4) for k, v in engine.comm_times.items()} or None,
+                       "comm_model": comm_model,
                        "optimizer": "AdamW(wd=0.05)+clip1.0+cosine", "final_loss": round(loss, 5)},
         }
         out.update(extra)

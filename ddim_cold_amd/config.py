@@ -87,7 +87,7 @@ class ExperimentConfig:
     sync_check_every: int = 0     # debug: cross-rank parameter checksum every N steps (0 = only after init)
     fault_inject_step: int = 0    # testing: raise after this many steps (after logging), to exercise resume
     perf_log: bool = True         # extra '# perf' lines (img/s, device ms/step) next to the reference lines
-    comm_layout: Optional[str] = None  # data parallel: 'overlap-2' | 'overlap-4' | 'inline-1' (skips comm_autotune)
+    comm_layout: Optional[str] = None  # data parallel: 'overlap-<blocks>' | 'inline-1' (skips comm_autotune)
     force_segments: bool = False  # testing: the data-parallel step (1-rank RCCL group, comm stream) at num_gpus 1
 
     # ------------------------------------------------------------------ derived
@@ -121,7 +121,9 @@ class ExperimentConfig:
             raise ValueError(f"unknown dataset kind {self.dataset!r}")
         if self.dataset.startswith("cold") and self.image_size[0] != self.image_size[1]:
             raise ValueError("cold (down-sample) datasets require square images (diffusion_loader.py:74)")
-        if self.comm_layout not in (None, "overlap-2", "overlap-4", "inline-1"):
+        if self.comm_layout is not None and not (self.comm_layout == "inline-1" or (
+                self.comm_layout.startswith("overlap-") and self.comm_layout[8:].isdigit()
+                and int(self.comm_layout[8:]) >= 1)):
             raise ValueError(f"unknown comm_layout {self.comm_layout!r}")
         if not self.synthetic and not all(self.dataStorage):
             raise ValueError("dataStorage needs [train_dir, val_dir] unless synthetic: true")

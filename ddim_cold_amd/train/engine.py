@@ -680,6 +680,106 @@ class TrainEngine:
     COMM_LAYOUTS = (("overlap-2", 2, True, False), ("overlap-4", 4, True, False),
                     ("inline-1", 1 << 16, False, True))
 
+    @classmethod
+    def layout_by_name(cls, name: str):
+        """``(name, bucket_blocks, embed_bucket, inline)`` for ``overlap-<blocks>`` /
+        ``inline-1``."""
+        if name == "inline-1":
+            return cls.COMM_LAYOUTS[-1]
+        if name.startswith("overlap-") and name[8:].isdigit() and int(name[8:]) >= 1:
+            return (name, int(name[8:]), True, False)
+        raise ValueError(f"unknown gradient-exchange layout {name!r} (overlap-<blocks> or inline-1)")
+
+    def step_profile(self):
+        """Cost-model view of this engine's step (parallel.costmodel.StepProfile):
+        gradient bytes per block and of the rest (embeddings, head, LayerNorms,
+        active time_embed rows) on the wire, backward timing scaled from the
+        measured ViT-tiny step by this batch's GEMM work."""
+        from ..parallel import costmodel as cm
+        c = self.prog.cfg
+        wire = 2 if self.cfg.grad_wire == "bf16" else 4
+        hidden = self.offsets["blocks.0.mlp.fc1.bias"][1]
+        xb = getattr(self.batch_fn, "x_t", None)
+        B = int(xb.shape[0]) if isinstance(xb, torch.Tensor) else 32
+        prof = cm.vit_step_profile(c.depth, c.dim, hidden, B * c.tokens, 0, wire_bytes=wire)
+        other = max(0.0, self.reduced_numel() - c.depth * prof.block_bytes / wire)
+        prof.embed_bytes = float(other * wire)
+        return prof
+
+    def reduced_numel(self) -> int:
+        """Elements all-reduced per step (inactive time_embed rows / frozen tensors skipped)."""
+        return sum(b - a for rs in self.bucket_ranges for a, b in rs)
+
+    def probe_allreduce(self, sizes_mb=(0.25, 1.0, 4.0, 16.0), reps: int = 10):
+        """Measure the gradient all-reduce on THIS job's ranks (the engine's own comm
+        path: native RCCL communicator or torch.distributed, fp32) at a few sizes and
+        fit ``T = alpha + S / algbw`` (parallel.costmodel.fit_allreduce).  Max over
+        ranks, HIP-event timed on the stream the collectives run on (host clock for
+        gloo on the CPU).  Returns the fitted model and ``{bytes: us}``; ``(None, {})``
+        when not data parallel."""
+        if not (self.dist_on and self.world > 1):
+            return None, {}
+        import time
+        from ..parallel import costmodel as cm
+        from ..parallel.dist import all_reduce_max, barrier
+        n_max = int(max(sizes_mb) * (1 << 20) // 4)
+        buf = torch.zeros(n_max, dtype=torch.float32, device=self.device)
+        out = {}
+
+        def sync():
+            if self.is_cuda:
+                torch.cuda.synchronize(self.device)
+        for mb in sizes_mb:
+            n = int(mb * (1 << 20) // 4)
+            x = buf[:n]
+
+            def ar():
+                if self.ncomm is not None:
+                    self.ncomm.all_reduce_(x)
+                else:
+                    dist.all_reduce(x, group=self.pg)
+            for _ in range(3):
+                ar()
+            sync()
+            barrier()
+            if self.is_cuda:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(reps):
+                    ar()
+                e1.record()
+                sync()
+                us = e0.elapsed_time(e1) * 1e3 / reps
+            else:  # gloo on the CPU: host clock
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    ar()
+                us = (time.perf_counter() - t0) * 1e6 / reps
+            out[4 * n] = all_reduce_max(us, self.device)
+        del buf
+        fit = cm.fit_allreduce(self.world, list(out), list(out.values()))
+        self.comm_fit = fit
+        return fit, out
+
+    def model_layouts(self, model=None):
+        """Layouts ordered by the cost model's predicted exposed comm time:
+        ``[(name, bucket_blocks, embed_bucket, inline, exposed_us)]``; ``model`` =
+        the fitted all-reduce model (:meth:`probe_allreduce`) or the a-priori xGMI
+        ring model of this world size."""
+        from ..parallel import costmodel as cm
+        if model is None:
+            model = getattr(self, "comm_fit", None) or cm.xgmi_ring_model(max(2, min(self.world, 8)))
+        return cm.plan_buckets(self.step_profile(), model)
+
+    def candidate_layouts(self):
+        """autotune_comm()'s default candidates: :attr:`COMM_LAYOUTS` plus the cost
+        model's predicted best (fitted model if :meth:`probe_allreduce` ran)."""
+        cands = list(self.COMM_LAYOUTS)
+        best = self.model_layouts()[0]
+        if best[0] not in [L_[0] for L_ in cands]:
+            cands.insert(0, best[:4])
+        return cands
+
     def set_comm_layout(self, bucket_blocks: Optional[int] = None, embed_bucket: Optional[bool] = None,
                         inline: Optional[bool] = None):
         """Re-bucket the gradient all-reduce and choose where its collectives run (a
@@ -730,7 +830,7 @@ class TrainEngine:
             return {}
         import time
         from ..parallel.dist import all_reduce_max, barrier
-        layouts = list(layouts or self.COMM_LAYOUTS)
+        layouts = list(layouts or self.candidate_layouts())
         snap = self._snapshot_state()
         times: Dict[str, float] = {}
         for name, bb, eb, inline in layouts:

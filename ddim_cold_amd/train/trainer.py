@@ -239,7 +239,7 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
             printLog(f"# comm layout: {engine.comm_choice} " +
                      " ".join(f"{k}={v:.4f}ms" for k, v in times.items()), paths.log)
     if cfg.comm_layout and engine.segmented and device.type == "cuda":
-        lay = {L[0]: L for L in engine.COMM_LAYOUTS}[cfg.comm_layout]
+        lay = engine.layout_by_name(cfg.comm_layout)
         engine.set_comm_layout(lay[1], lay[2], lay[3])
         engine.comm_choice = lay[0]
     check_param_sync(engine.flat_p, step=steps)  # replicas start identical

@@ -57,7 +57,7 @@ def _worker(rank, world, port, out):
         eng.step(*bs[0])  # builds the static batch buffers the graphs read ...
         eng._restore_state(snap)  # ... and is undone
         times = eng.autotune_comm(steps=3, warm=1)
-        assert set(times) == {L[0] for L in eng.COMM_LAYOUTS}, times
+        assert set(times) >= {L[0] for L in eng.COMM_LAYOUTS}, times
         losses = []
         for x, y, t in bs:
             eng.step(x, y, t)

@@ -32,7 +32,7 @@ def run(dist_mode, comm="torch", wire="fp32", gauss=False, tune=False, layout=No
         eng.set_comm_layout(L[1], L[2], L[3])
     if tune:  # measures every layout, then restores the training state
         times = eng.autotune_comm(steps=4, warm=1)
-        assert set(times) == {l[0] for l in eng.COMM_LAYOUTS} and eng.comm_choice in times, times
+        assert set(times) >= {l[0] for l in eng.COMM_LAYOUTS} and eng.comm_choice in times, times
         assert eng.steps_done == 0 and int(eng.step_ctr[0]) == 0 and int(eng.rng[1]) == 0
     for _ in range(6):
         eng.train_step()
