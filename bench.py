@@ -35,6 +35,9 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import torch
 import torch.distributed as dist
 
+# rehearsal of the multi-rank flow on a 1-GPU box: every rank on device 0 over gloo
+# (RCCL refuses two ranks on one device); timings are NOT a scaling measurement
+SHARED_GPU = os.environ.get("DDIM_COLD_REHEARSE_SHARED_GPU") == "1"
 BASELINE_IMG_S_PER_GPU = 709.0  # 22.2 steps/s x 32 img (train.log, RTX 3090 fp16 AMP)
 
 
@@ -94,7 +97,7 @@ def spawn_ranks(n: int, argv) -> int:
     import multiprocessing as mp
     from ddim_cold_amd.parallel.dist import free_port
     ndev = torch.cuda.device_count()  # no HIP context is created by counting
-    if 0 < ndev < n:
+    if 0 < ndev < n and not SHARED_GPU:
         print(f"bench.py: --gpus {n} but only {ndev} GPU(s) visible", file=sys.stderr)
         return 2
     ctx = mp.get_context("spawn")
@@ -143,10 +146,12 @@ def run(args):
     from ddim_cold_amd.parallel.dist import (init_distributed, init_single, all_reduce_max, barrier, cleanup,
                                              env_world)
     world, rank, local = env_world()
+    if SHARED_GPU:
+        local = 0
     if args.force_dist and world == 1:
         distributed = init_single(device_index=local)
     else:
-        distributed = init_distributed()
+        distributed = init_distributed(backend="gloo" if SHARED_GPU else None)
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
@@ -170,7 +175,7 @@ def run(args):
                        temb_rows=int(math.log2(model.img_size[1])) + 1 if args.dataset == "cold" else None,
                        graph_comm=not args.segmented_comm, grad_wire=args.grad_wire,
                        comm_events=not (args.segmented_comm or args.captured_comm),
-                       comm=args.comm, graph_steps=args.graph_steps)
+                       comm="torch" if SHARED_GPU else args.comm, graph_steps=args.graph_steps)
     engine = TrainEngine(model, cfg, device=dev)
     pool = synthetic_pool(1024, tuple(model.img_size), seed=7 + rank, device=dev)
     if args.dataset == "cold":
@@ -302,6 +307,7 @@ def run(args):
             "vs_baseline": round(value / (BASELINE_IMG_S_PER_GPU * n), 3)
                            if args.model == "vit_tiny" and args.dataset == "cold" else None,
             "dtype": "bf16",
+            "rehearsal_shared_gpu_gloo": True if SHARED_GPU else None,
             "data": "synthetic (on-device Oxford-Flowers-shaped pool, " +
                     ("cold pixelation pairs" if args.dataset == "cold" else "Gaussian DDIM q_sample pairs") +
                     "), random-init weights",
