@@ -390,6 +390,41 @@ void head_step_(Tensor a, Tensor w, Tensor b, Tensor x, c10::optional<Tensor> x0
   gemm_nt(g, EPI_HEAD, cur_stream());
 }
 
+// Sampler step on patch rows (EPI_HEADR): x / x0_out / patches_out are [B*P][F]
+// (F = C*p*p in the head's output column order), so every epilogue access is a
+// contiguous 16-byte vector (the image-layout head_step_ scatters 4-byte pixels).
+void head_step_rows_(Tensor a, Tensor w, Tensor b, Tensor x, c10::optional<Tensor> x0_out,
+                     c10::optional<Tensor> coef, int64_t batch, int64_t mode, c10::optional<Tensor> ln_st,
+                     c10::optional<Tensor> ln_c, double ln_eps, c10::optional<Tensor> patches_out) {
+  CHECK_IN(a, BF16); CHECK_IN(w, BF16); CHECK_IN(b, F32); CHECK_IN(x, F32);
+  const c10::DeviceGuard guard(a.device());
+  const int K = a.size(-1);
+  auto a2 = a.view({-1, K});
+  check_linear(a2, w, K);
+  const int F = w.size(0), B = batch;
+  TORCH_CHECK(B >= 1 && x.dim() == 2 && x.size(1) == F && x.size(0) % B == 0, "x must be [B*P, F]");
+  const int NP = x.size(0) / B, N = NP + 1;
+  TORCH_CHECK(a2.size(0) == (int64_t)B * N && b.numel() == F && F % 4 == 0, "head rows shapes");
+  TORCH_CHECK(mode == 1 || mode == 2 || mode == 4, "head_step_rows_: mode 1 (ddim), 2 (clamp) or 4 (per-sample ddim)");
+  GemmArgs g = nt_args(a2, w);
+  g.C = x.data_ptr(); g.bias = b.data_ptr<float>();
+  g.tokens = N; g.batch = B;
+  g.head_mode = (int)mode;
+  if (mode == 1 || mode == 4) {
+    TORCH_CHECK(x0_out.has_value() && coef.has_value(), "ddim mode needs x0_out and coef");
+    CHECK_IN((*x0_out), F32); CHECK_IN((*coef), F32);
+    TORCH_CHECK(x0_out->sizes() == x.sizes() && coef->numel() >= (mode == 4 ? 4 * B : 4), "x0_out / coef shapes");
+    g.res = x.data_ptr<float>(); g.C2 = x0_out->data_ptr(); g.coef = coef->data_ptr<float>();
+  }
+  if (patches_out.has_value() && patches_out->defined()) {
+    CHECK_IN((*patches_out), BF16);
+    TORCH_CHECK(patches_out->sizes() == x.sizes(), "patches_out must be [B*P, F]");
+    g.patch_out = patches_out->data_ptr();
+  }
+  apply_fold(g, B * N, F, ln_st, ln_c, ln_eps, c10::nullopt, c10::nullopt);
+  gemm_nt(g, EPI_HEADR, cur_stream());
+}
+
 // Head GEMM with the training loss in its epilogue (head_mode 3): the smooth-L1
 // of the unpatchified prediction vs `target` (multi_gpu_trainer.py:124) as one
 // partial per workgroup, and its gradient written straight into the token
@@ -902,6 +937,8 @@ TORCH_LIBRARY(ddim_cold, m) {
         "Tensor? ln_c=None, float ln_eps=1e-5, Tensor(a!)? ln_mean=None, Tensor(b!)? ln_rstd=None) -> Tensor");
   m.def("head_step_(Tensor a, Tensor w, Tensor b, Tensor(a!) x, Tensor(b!)? x0_out, Tensor? coef, int patch, "
         "int mode, Tensor? ln_st=None, Tensor? ln_c=None, float ln_eps=1e-5, Tensor(c!)? patches_out=None) -> ()");
+  m.def("head_step_rows_(Tensor a, Tensor w, Tensor b, Tensor(a!) x, Tensor(b!)? x0_out, Tensor? coef, int batch, "
+        "int mode, Tensor? ln_st=None, Tensor? ln_c=None, float ln_eps=1e-5, Tensor(c!)? patches_out=None) -> ()");
   m.def("head_loss(Tensor a, Tensor w, Tensor b, Tensor target, int patch, float beta, Tensor? ln_st=None, "
         "Tensor? ln_c=None, float ln_eps=1e-5, Tensor(a!)? ln_mean=None, Tensor(b!)? ln_rstd=None) -> (Tensor, Tensor)");
   m.def("smooth_l1_fwd_bwd(Tensor pred, Tensor target, int N, int patch, float beta, Tensor(a!)? loss_last=None, "
@@ -959,6 +996,7 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("linear_dgrad_gelu", &linear_dgrad_gelu);
   m.impl("linear_wgrad", &linear_wgrad);
   m.impl("head_step_", &head_step_);
+  m.impl("head_step_rows_", &head_step_rows_);
   m.impl("linear_fwd", &linear_fwd);
   m.impl("linear_wgrad_multi", &linear_wgrad_multi);
   m.impl("wire_pack", &wire_pack);

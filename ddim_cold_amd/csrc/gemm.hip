@@ -507,7 +507,10 @@ static void launch_auto(GemmParams p, int splits, hipStream_t stream) {
     // heaviest in vector instructions: twice the waves of 32x64 tiles pay off on the
     // sampler shape (M=4160: 6.56 vs 7.14 us, tools/gpu_tile_sweep3.sh); the other
     // epilogues keep 64x64 there (QKV 11.45 vs 13.54, residual 6.65 vs 7.02)
-    if (EPI == EPI_GELU && cfg == 1 && forced_tile() < 0 && ((p.M + 31) / 32) * ((p.N + 63) / 64) <= 1024) cfg = 0;
+    // the patch embedding likewise (sampler M=4,096: 7.83 vs 9.08 us, tools/ub_sampler_ends.py)
+    if ((EPI == EPI_GELU || EPI == EPI_EMBED) && cfg == 1 && forced_tile() < 0 &&
+        ((p.M + 31) / 32) * ((p.N + 63) / 64) <= 1024)
+      cfg = 0;
     DmaTiles<AT, BT, EPI>::launch(p, splits, stream, cfg);
     return;
   }
@@ -534,6 +537,7 @@ DC_INST_DMA3(EPI_RESID)
 DC_INST_DMA3(EPI_GELU)
 DC_INST_DMA3(EPI_HEAD)
 DC_INST_DMA3(EPI_EMBED)
+DC_INST_DMA3(EPI_HEADR)
 DC_INST_DMA2(false, true, EPI_BF16)
 DC_INST_DMA2(false, true, EPI_F32)
 DC_INST_DMA2(false, true, EPI_DGELU)
@@ -647,6 +651,10 @@ void gemm_nt(const GemmArgs& a, int epi, hipStream_t stream) {
     case EPI_GELU: launch_auto<false, false, EPI_GELU>(p, 1, stream); break;
     case EPI_HEAD: launch_auto<false, false, EPI_HEAD>(p, 1, stream); break;
     case EPI_EMBED: launch_auto<false, false, EPI_EMBED>(p, 1, stream); break;
+    case EPI_HEADR:
+      if (p.K % 64 != 0 || dma_disabled()) throw std::runtime_error("gemm_nt: EPI_HEADR needs the LDS-DMA GEMM");
+      launch_auto<false, false, EPI_HEADR>(p, 1, stream);
+      break;
     default: throw std::runtime_error("gemm_nt: unsupported epilogue");
   }
 }

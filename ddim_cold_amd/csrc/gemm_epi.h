@@ -160,7 +160,8 @@ __device__ __forceinline__ long long epi_col(const GemmParams& p, int n) {
 template <int EPI>
 struct FoldEpi {
   static constexpr bool CONSUMER =
-      EPI == EPI_QKV || EPI == EPI_GELU || EPI == EPI_BF16 || EPI == EPI_F32 || EPI == EPI_HEAD;
+      EPI == EPI_QKV || EPI == EPI_GELU || EPI == EPI_BF16 || EPI == EPI_F32 || EPI == EPI_HEAD ||
+      EPI == EPI_HEADR;
   static constexpr bool PRODUCER = EPI == EPI_RESID || EPI == EPI_EMBED;
 };
 
@@ -205,6 +206,11 @@ __device__ __forceinline__ RowInfo32 epi_row32(const GemmParams& p, int m) {
     ri.b = p.thr_dp ? divmagic(m, p.tokens, p.tok_magic) : 0;  // drop-path sample (training only)
   } else if (EPI == EPI_GELU || EPI == EPI_DGELU) {
     ri.off = m * p.N;
+  } else if (EPI == EPI_HEADR) {
+    // token row m of sample b -> patch row b*P + tok - 1 = m - b - 1 (cls rows skipped)
+    const int b = divmagic(m, p.tokens, p.tok_magic), tok = m - b * p.tokens;
+    ri.off = tok == 0 ? -1 : (m - b - 1) * p.N;
+    ri.b = b;
   } else if (EPI == EPI_EMBED) {
     const int b = divmagic(m, p.tokens, p.tok_magic);  // tokens = patches per sample here
     ri.off = (m + b + 1) * p.emb_dim;                  // (b * (P + 1) + patch + 1) * D
@@ -541,9 +547,11 @@ __device__ __forceinline__ f32x4 ld4bf(const bf16* p) {
 // chain of ~3 dependent memory round trips and this removes one of them.
 template <int EPI, int FM, int FN, bool PUB = false, bool SW = false>
 struct VecEpi {
-  static constexpr bool PRE = EPI == EPI_RESID || EPI == EPI_DGELU || EPI == EPI_EMBED || EPI == EPI_ACC;
+  static constexpr bool PRE =
+      EPI == EPI_RESID || EPI == EPI_DGELU || EPI == EPI_EMBED || EPI == EPI_ACC || EPI == EPI_HEADR;
   static constexpr bool FC = FoldEpi<EPI>::CONSUMER, FP = FoldEpi<EPI>::PRODUCER;
   RowInfo32 rows[FM];
+  f32x4 hcf[FM];    // HEADR: the row's DDIM coefficients {sqrt a_t, sqrt(1-a_t), sqrt a_tk, sqrt(1-a_tk)}
   int cols[FN];
   bool colok[FN];
   f32x4 colb[FN];
@@ -618,6 +626,12 @@ struct VecEpi {
       const int n = nb + j * 16 + cs;
       lnc[j] = (fold && colok[j]) ? ld4(p.ln_c + n) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    if (EPI == EPI_HEADR) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        hcf[i] = p.head_mode == 4 ? ld4(p.coef + 4 * rows[i].b)
+                 : p.head_mode == 1 ? ld4(p.coef) : f32x4{0.f, 1.f, 0.f, 1.f};
+    }
     cls_i = -1;
     cls_b = 0;
     if (EPI == EPI_EMBED && p.cls_src != nullptr) {
@@ -643,6 +657,7 @@ struct VecEpi {
         if (PRE && rows[i].off >= 0 && colok[j]) {
           const int n = nb + j * 16 + cs;
           if (EPI == EPI_RESID) v = ld4(p.res + rows[i].off + n);
+          if (EPI == EPI_HEADR && p.head_mode != 2) v = ld4(p.res + rows[i].off + n);  // x_t
           if (EPI == EPI_DGELU) v = ld4bf(p.aux + rows[i].off + n);
           if (EPI == EPI_ACC && !p.acc_store) v = ld4(reinterpret_cast<const float*>(p.C) + rows[i].off + n);
           if (EPI == EPI_EMBED) {
@@ -748,6 +763,22 @@ struct VecEpi {
             v[c] = e * gelu_grad_f(pre[i][j][c]);
           }
           st4bf(reinterpret_cast<bf16*>(p.C) + idx, v);
+        } else if (EPI == EPI_HEADR) {
+          // ViT.py:229-234 on the patch rows: x0-hat clamp, then (modes 1 / 4) the DDIM
+          // update with x_t preloaded in `pre`; the new x_t also as the next step's
+          // bf16 patch rows (same index: the embedding weight is column-permuted)
+          f32x4 x0;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) x0[c] = fminf(fmaxf(v[c], -1.f), 1.f);
+          f32x4 xn = x0;
+          if (p.head_mode != 2) {
+            const f32x4 cf = hcf[i];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) xn[c] = cf[2] * x0[c] + cf[3] * ((pre[i][j][c] - cf[0] * x0[c]) / cf[1]);
+            st4(reinterpret_cast<float*>(p.C2) + idx, x0);
+          }
+          st4(reinterpret_cast<float*>(p.C) + idx, xn);
+          if (p.patch_out != nullptr) st4bf(p.patch_out + idx, xn);
         } else if (EPI == EPI_EMBED) {
           v += pre[i][j];
           if (p.thr_drop) {

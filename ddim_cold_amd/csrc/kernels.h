@@ -16,6 +16,8 @@ enum GemmEpi : int {
   EPI_DGELU = 7,   // C bf16 = Dropout(acc) * GELU'(aux)
   EPI_ATOMIC = 8,  // C f32 += acc (split-K / gradient accumulate) ; bias -> fused column sum
   EPI_ACC = 9,     // C f32 += acc, one writer per element (no split) ; bias likewise
+  EPI_HEADR = 10,  // sampler step on patch rows: +bias, clamp (+DDIM update), f32 [B*P][C*p*p]
+                   //   in head-output column order (contiguous: vector epilogue)
 };
 
 struct GemmArgs {

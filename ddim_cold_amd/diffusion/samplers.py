@@ -103,6 +103,52 @@ def _patch_rows(model, N: int, device, den) -> Optional[torch.Tensor]:
     return torch.empty(N * (H // p) * (W // p), model.in_chans * p * p, dtype=torch.bfloat16, device=device)
 
 
+# the sampler state as fp32 patch rows in the head's output column order
+# (ops.image_to_rows): the head epilogue's x_t / x0 / x_next / bf16 patch-row accesses
+# are contiguous 16-byte vectors (ops.head_step_rows_) instead of scattered pixels,
+# and the first step needs no patchify launch either (head GEMM at N=64: 12.2 -> 7.0
+# us, k=20 N=64 sampler 33.40 -> 32.90 ms per batch; profiles/sampler_rows_ab.txt)
+ROWS = os.environ.get("DDIM_COLD_SAMPLER_ROWS", "1") == "1"
+
+
+class _Rows:
+    """Patch-row state of one captured sampling loop (GPU fused path only).
+
+    Inside the loop: :meth:`begin` converts the [N, C, H, W] start image once and
+    permutes the patch-embedding weight's columns into the head's order (so a
+    replay after training uses the current weights); :meth:`step` is one forward
+    with the update in the head epilogue; :meth:`image` converts rows back."""
+
+    def __init__(self, model, N: int, device, den):
+        p = model.patch_size
+        H, W = model.img_size
+        C = model.in_chans
+        NP, F = (H // p) * (W // p), C * p * p
+        self.den, self.p, self.shape = den, p, (N, C, H, W)
+        self.x = torch.zeros(N * NP, F, device=device)
+        self.x0 = torch.zeros_like(self.x)
+        self.pin = torch.empty(N * NP, F, dtype=torch.bfloat16, device=device)
+        self.w = torch.empty_like(den.P.pe_w)
+
+    def begin(self, x_img):
+        self.w.copy_(ops.embed_weight_rows(self.den.P.pe_w, self.shape[1], self.p))
+        self.x.copy_(ops.image_to_rows(x_img, self.p))
+        self.pin.copy_(self.x)
+
+    def step(self, t, mode: int, coef=None):
+        x0 = None if mode == 2 else self.x0.view(self.shape)
+        self.den.step_(self.x.view(self.shape), t, mode, x0, coef, patches=(self.pin, self.pin, self.w))
+
+    def image(self, xr):
+        return ops.rows_to_image(xr, *self.shape, self.p)
+
+
+def _rows_state(model, N: int, device, den) -> Optional[_Rows]:
+    if not (ROWS and PATCH_CHAIN and FUSED_HEAD and den.fused and torch.device(device).type == "cuda"):
+        return None
+    return _Rows(model, N, device, den)
+
+
 def _chain_patches(pbuf, first: bool):
     """(patches_in, patches_out) of one step: the first step patchifies x itself."""
     if pbuf is None:
@@ -176,8 +222,18 @@ class DDIMSampler:
         traj = torch.zeros(len(self.ts), N, self.C, self.H, self.W, device=dev) if record else None
         coef = self.coef
         pbuf = _patch_rows(self.model, N, dev, den)
+        rs = _rows_state(self.model, N, dev, den)
 
         def loop():
+            if rs is not None:
+                rs.begin(x)
+                for i in range(len(self.ts)):
+                    rs.step(tt[i], 1, coef[i])
+                    if traj is not None:
+                        traj[i].copy_(rs.image(rs.x0))
+                x0.copy_(rs.image(rs.x0))
+                x.copy_(rs.image(rs.x))
+                return
             for i in range(len(self.ts)):
                 # forward + clamp + DDIM update, one head epilogue
                 den.step_(x, tt[i], 1, x0, coef[i], patches=_chain_patches(pbuf, i == 0))
@@ -246,8 +302,16 @@ class ColdSampler:
         tt = torch.tensor(ts, dtype=torch.int64, device=dev).unsqueeze(1).expand(-1, N).contiguous()
         traj = torch.zeros(len(ts), N, self.C, self.H, self.W, device=dev)
         pbuf = _patch_rows(self.model, N, dev, den)
+        rs = _rows_state(self.model, N, dev, den)
 
         def loop():
+            if rs is not None:
+                rs.begin(x)
+                for i in range(len(ts)):
+                    rs.step(tt[i], 2)
+                    traj[i].copy_(rs.image(rs.x))
+                x.copy_(rs.image(rs.x))
+                return
             for i in range(len(ts)):
                 # forward + clamp in the head epilogue
                 den.step_(x, tt[i], 2, patches=_chain_patches(pbuf, i == 0))
@@ -320,8 +384,16 @@ def ddim_from_starts(model, x: torch.Tensor, starts: Sequence[int], k: int, devi
         x0 = torch.zeros_like(xs)
         tt = torch.tensor(ts, dtype=torch.int64, device=device).unsqueeze(1).expand(-1, B).contiguous()
         pbuf = _patch_rows(model, B, device, den)
+        rs = _rows_state(model, B, device, den)
 
         def loop():
+            if rs is not None:
+                rs.begin(xs)
+                for i in range(len(ts)):
+                    rs.step(tt[i], 4, coef[i])
+                x0.copy_(rs.image(rs.x0))
+                xs.copy_(rs.image(rs.x))
+                return
             for i in range(len(ts)):
                 den.step_(xs, tt[i], 4, x0, coef[i], patches=_chain_patches(pbuf, i == 0))
 

@@ -335,15 +335,23 @@ class ViTProgram:
         # each slot written once by the producing epilogue
         st = torch.empty(2 * L + 1, M, D // 32, 2, dtype=torch.float32, device=dev)
         xb = torch.empty(M, D, dtype=ACT_DTYPE, device=dev)
-        # sampler steps: head_step = (mode, x0_out, coef, patches_in, patches_out); the
-        # previous step's head left this step's bf16 patch rows in patches_in
+        # sampler steps: head_step = (mode, x0_out, coef, patches_in, patches_out[,
+        # pe_w_rows]); the previous step's head left this step's bf16 patch rows in
+        # patches_in.  With pe_w_rows the sampler state lives in patch rows
+        # (ops.image_to_rows; ``img`` is a [B, C, H, W]-shaped view of that buffer):
+        # the embedding reads the rows through the column-permuted weight and the
+        # head updates them with contiguous vector accesses (ops.head_step_rows_)
         patches_in = head_step[3] if head_step is not None and len(head_step) > 3 else None
+        rows_w = head_step[5] if head_step is not None and len(head_step) > 5 else None
+        if rows_w is not None and patches_in is None:
+            raise ValueError("the patch-row sampler state needs patches_in")
         if cold is not None:
             x, patches = ops.patch_embed_cold_fwd(cold, img, t, P.pe_w, P.pe_b, P.cls, P.pos, P.temb, rng,
                                                   SITE_EMBED, pd, c.patch, ln_st=st[0], xb_out=xb)
         else:
-            x, patches = ops.patch_embed_fwd(img, t, P.pe_w, P.pe_b, P.cls, P.pos, P.temb, rng, SITE_EMBED, pd,
-                                             c.patch, ln_st=st[0], xb_out=xb, patches_in=patches_in)
+            x, patches = ops.patch_embed_fwd(img, t, P.pe_w if rows_w is None else rows_w, P.pe_b, P.cls, P.pos,
+                                             P.temb, rng, SITE_EMBED, pd, c.patch, ln_st=st[0], xb_out=xb,
+                                             patches_in=patches_in)
         x = x.view(M, D)
         S = Saved(t=t, patches=patches) if save else None
 
@@ -375,6 +383,12 @@ class ViTProgram:
         if head_step is not None:
             mode, x0_out, coef = head_step[:3]
             patches_out = head_step[4] if len(head_step) > 4 else None
+            if rows_w is not None:
+                F = P.head_wf.shape[0]
+                ops.head_step_rows_(xb, P.head_wf, P.head_bf, img.view(-1, F),
+                                    None if x0_out is None else x0_out.view(-1, F), coef, B, mode,
+                                    patches_out=patches_out, fold=(st[2 * L], P.head_c, c.eps))
+                return img, S
             ops.head_step_(xb, P.head_wf, P.head_bf, img, x0_out, coef, c.patch, mode, patches_out=patches_out,
                            fold=(st[2 * L], P.head_c, c.eps))
             return img, S

@@ -21,7 +21,8 @@ __all__ = [
     "linear_residual_fwd", "linear_gelu_fwd", "head_fwd", "smooth_l1_fwd_bwd", "img_to_tokgrad",
     "linear_dgrad", "linear_dgrad_gelu", "linear_wgrad", "layernorm_bwd", "attn_bwd", "embed_bwd",
     "sqnorm", "adamw_step", "advance_counters", "ddim_step", "ddim_step_", "randn_", "q_sample",
-    "pixelate_pair", "cold_batch", "gauss_batch", "patch_embed_cold_fwd", "ln_fold_",
+    "pixelate_pair", "cold_batch", "gauss_batch", "head_step_rows_",
+    "image_to_rows", "rows_to_image", "embed_weight_rows", "patch_embed_cold_fwd", "ln_fold_",
 ]
 
 
@@ -170,6 +171,52 @@ def head_step_(a, w, b, x, x0_out, coef, patch: int, mode: int, fold=None, patch
     xn, x0 = ref.ddim_step(x, x0_raw, _ddim_coef(coef, x))
     x.copy_(xn)
     x0_out.copy_(x0)
+
+
+def image_to_rows(x, patch: int):
+    """[B,C,H,W] -> [B*P, C*p*p] patch rows in the head's output column order
+    ((a*p + b)*C + c for pixel (a, b) of the patch, channel c; ViT.py:214-217 unpatchify)."""
+    B, C, H, W = x.shape
+    p = patch
+    return x.reshape(B, C, H // p, p, W // p, p).permute(0, 2, 4, 3, 5, 1).reshape(B * (H // p) * (W // p), p * p * C)
+
+
+def rows_to_image(xr, B: int, C: int, H: int, W: int, patch: int):
+    """Inverse of :func:`image_to_rows`."""
+    p = patch
+    return xr.reshape(B, H // p, W // p, p, p, C).permute(0, 5, 1, 3, 2, 4).reshape(B, C, H, W)
+
+
+def embed_weight_rows(w_pe, C: int, patch: int):
+    """Patch-embedding weight [D, C*p*p] (conv order c, a, b) with its columns permuted
+    to the head's output order, so bf16 patch rows in that order (:func:`head_step_rows_`
+    ``patches_out``) feed :func:`patch_embed_fwd` ``patches_in`` directly."""
+    D = w_pe.shape[0]
+    return w_pe.reshape(D, C, patch, patch).permute(0, 2, 3, 1).reshape(D, C * patch * patch)
+
+
+def head_step_rows_(a, w, b, x, x0_out, coef, batch: int, mode: int, fold=None, patches_out=None):
+    """:func:`head_step_` on patch rows (``x``/``x0_out``/``patches_out`` [B*P, F] in the
+    head's output column order, :func:`image_to_rows`): every epilogue access is a
+    contiguous vector instead of a scattered pixel.  Same math per element."""
+    st, c, eps, _, _ = _fold_args(fold)
+    if _hip(a):
+        return _ops().head_step_rows_(a, w, b, x, x0_out, coef, int(batch), int(mode), st, c, eps, patches_out)
+    F = w.shape[0]
+    NP = x.shape[0] // batch
+    y = ref._lin(a, w, b, st, c, eps)
+    y = y.reshape(batch, NP + 1, F)[:, 1:].reshape(batch * NP, F)
+    x0 = torch.clamp(y, -1.0, 1.0)
+    if mode == 2:
+        x.copy_(x0)
+    else:
+        cf = coef.reshape(-1, 4).float()
+        cf = cf.repeat_interleave(NP, 0) if cf.shape[0] == batch and mode == 4 else cf[:1].expand(x.shape[0], 4)
+        eps_hat = (x - cf[:, 0:1] * x0) / cf[:, 1:2]
+        x.copy_(cf[:, 2:3] * x0 + cf[:, 3:4] * eps_hat)
+        x0_out.copy_(x0)
+    if patches_out is not None:
+        patches_out.copy_(x)
 
 
 def head_fwd(a, w, b, B: int, C: int, H: int, W: int, patch: int, fold=None):

@@ -150,6 +150,7 @@ def test_patch_row_chain(model, monkeypatch):
     res = []
     for on in (False, True):
         monkeypatch.setattr(smp, "PATCH_CHAIN", on)
+        monkeypatch.setattr(smp, "ROWS", False)  # image-layout chain (rows: test_sampler_rows_gpu.py)
         model.__dict__.pop("_sampler_graphs", None)
         res.append(DDIMSampler(model, DEV, k=200).sample(8, noise=noise))
         res.append(ColdSampler(model, DEV).sequence(4, generator=torch.Generator().manual_seed(5))[-1])
