@@ -171,7 +171,7 @@ std::tuple<Tensor, Tensor> patch_embed_cold_fwd(Tensor pool, int64_t data_site, 
                                                 bool write_xt, Tensor w_pe, Tensor b_pe, Tensor cls, Tensor pos,
                                                 Tensor temb, Tensor rng, int64_t site, double p, int64_t patch,
                                                 c10::optional<Tensor> ln_st, c10::optional<Tensor> xb_out,
-                                                int64_t gauss_T, int64_t noise_site) {
+                                                int64_t gauss_T, int64_t noise_site, bool target_rows) {
   CHECK_IN(pool, F32); CHECK_IN(img, F32); CHECK_IN(target, F32); CHECK_IN(t, I64); CHECK_IN(idx, I64);
   const int B = img.size(0), C = img.size(1), H = img.size(2), W = img.size(3);
   TORCH_CHECK(pool.dim() == 4 && pool.size(1) == C && pool.size(2) == H && pool.size(3) == W, "pool shape");
@@ -186,6 +186,7 @@ std::tuple<Tensor, Tensor> patch_embed_cold_fwd(Tensor pool, int64_t data_site, 
   ColdSrc cs;
   cs.gauss_T = gauss_T;
   cs.noise_site = noise_site;
+  cs.target_rows = target_rows;
   cs.pool = pool.data_ptr<float>();
   cs.pool_n = pool.size(0);
   cs.site = data_site;
@@ -429,9 +430,13 @@ void head_step_rows_(Tensor a, Tensor w, Tensor b, Tensor x, c10::optional<Tenso
 // of the unpatchified prediction vs `target` (multi_gpu_trainer.py:124) as one
 // partial per workgroup, and its gradient written straight into the token
 // layout the head backward consumes (cls rows zero).  Returns (partials, dtok).
+// target_rows: `target` ([B, C, H, W]-shaped) holds patch rows [B*P][C*p*p] in the
+// head's output column order (the fused batch draw writes them): vector epilogue
+// (EPI_HEADL) with contiguous target loads instead of scattered pixels.
 std::tuple<Tensor, Tensor> head_loss(Tensor a, Tensor w, Tensor b, Tensor target, int64_t patch, double beta,
                                      c10::optional<Tensor> ln_st, c10::optional<Tensor> ln_c, double ln_eps,
-                                     c10::optional<Tensor> ln_mean, c10::optional<Tensor> ln_rstd) {
+                                     c10::optional<Tensor> ln_mean, c10::optional<Tensor> ln_rstd,
+                                     bool target_rows) {
   CHECK_IN(a, BF16); CHECK_IN(w, BF16); CHECK_IN(b, F32); CHECK_IN(target, F32);
   const c10::DeviceGuard guard(a.device());
   TORCH_CHECK(target.dim() == 4, "target must be [B, C, H, W]");
@@ -453,7 +458,7 @@ std::tuple<Tensor, Tensor> head_loss(Tensor a, Tensor w, Tensor b, Tensor target
   g.loss_inv_n = 1.0f / (float)((int64_t)B * C * H * W);
   g.loss_parts = parts.data_ptr<float>();
   apply_fold(g, M, F, ln_st, ln_c, ln_eps, ln_mean, ln_rstd);
-  gemm_nt(g, EPI_HEAD, cur_stream());
+  gemm_nt(g, target_rows ? EPI_HEADL : EPI_HEAD, cur_stream());
   return {parts, dtok};
 }
 
@@ -940,7 +945,8 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("head_step_rows_(Tensor a, Tensor w, Tensor b, Tensor(a!) x, Tensor(b!)? x0_out, Tensor? coef, int batch, "
         "int mode, Tensor? ln_st=None, Tensor? ln_c=None, float ln_eps=1e-5, Tensor(c!)? patches_out=None) -> ()");
   m.def("head_loss(Tensor a, Tensor w, Tensor b, Tensor target, int patch, float beta, Tensor? ln_st=None, "
-        "Tensor? ln_c=None, float ln_eps=1e-5, Tensor(a!)? ln_mean=None, Tensor(b!)? ln_rstd=None) -> (Tensor, Tensor)");
+        "Tensor? ln_c=None, float ln_eps=1e-5, Tensor(a!)? ln_mean=None, Tensor(b!)? ln_rstd=None, "
+        "bool target_rows=False) -> (Tensor, Tensor)");
   m.def("smooth_l1_fwd_bwd(Tensor pred, Tensor target, int N, int patch, float beta, Tensor(a!)? loss_last=None, "
         "Tensor(b!)? loss_ema=None, float ema_decay=0.99, bool finish=True) -> (Tensor, Tensor)");
   m.def("img_to_tokgrad(Tensor dimg, int N, int patch) -> Tensor");
@@ -975,7 +981,7 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("patch_embed_cold_fwd(Tensor pool, int data_site, int max_t, bool draw_idx, bool target_x0, "
         "Tensor(a!) img, Tensor(b!) target, Tensor(c!) t, Tensor(d!) idx, bool write_xt, Tensor w_pe, Tensor b_pe, "
         "Tensor cls, Tensor pos, Tensor temb, Tensor rng, int site, float p, int patch, Tensor(e!)? ln_st=None, "
-        "Tensor(f!)? xb_out=None, int gauss_T=0, int noise_site=0) -> (Tensor, Tensor)");
+        "Tensor(f!)? xb_out=None, int gauss_T=0, int noise_site=0, bool target_rows=False) -> (Tensor, Tensor)");
   m.def("gauss_batch(Tensor pool, Tensor rng, int site, int noise_site, int T, Tensor(a!) x_t, Tensor(b!) x0, "
         "Tensor(c!) t, Tensor(d!) idx, bool draw_idx=True) -> ()");
 }

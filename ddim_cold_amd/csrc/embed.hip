@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void patchify_cls_kernel(const float* __restri
       const size_t o = (((size_t)b * C + c) * H + y) * W + xx;
       const float x0 = cs.pool[((size_t)src * C + c) * H * W + (size_t)y * W + xx];
       const float xt = sa * x0 + s1a * gauss_eps(nsalt, (uint32_t)o);
-      cs.target[o] = x0;
+      cs.target[cs.target_rows ? row * F + (size_t)ij * C + c : o] = x0;
       if (cs.x_t) cs.x_t[o] = xt;
       patches[e] = f2bf(xt);
     } else if (cs.pool) {
@@ -105,7 +105,8 @@ __global__ __launch_bounds__(256) void patchify_cls_kernel(const float* __restri
       const int f1 = 1 << tt, f0 = cs.target_x0 ? 1 : 1 << (tt - 1);
       const float xt = im[(size_t)pix_src(y, H, f1) * W + pix_src(xx, W, f1)];
       const size_t o = (((size_t)b * C + c) * H + y) * W + xx;
-      cs.target[o] = cs.target_x0 ? im[(size_t)y * W + xx] : im[(size_t)pix_src(y, H, f0) * W + pix_src(xx, W, f0)];
+      cs.target[cs.target_rows ? row * F + (size_t)ij * C + c : o] =
+          cs.target_x0 ? im[(size_t)y * W + xx] : im[(size_t)pix_src(y, H, f0) * W + pix_src(xx, W, f0)];
       if (cs.x_t) cs.x_t[o] = xt;
       patches[e] = f2bf(xt);
     } else {

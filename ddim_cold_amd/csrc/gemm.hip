@@ -538,6 +538,7 @@ DC_INST_DMA3(EPI_GELU)
 DC_INST_DMA3(EPI_HEAD)
 DC_INST_DMA3(EPI_EMBED)
 DC_INST_DMA3(EPI_HEADR)
+DC_INST_DMA3(EPI_HEADL)
 DC_INST_DMA2(false, true, EPI_BF16)
 DC_INST_DMA2(false, true, EPI_F32)
 DC_INST_DMA2(false, true, EPI_DGELU)
@@ -654,6 +655,10 @@ void gemm_nt(const GemmArgs& a, int epi, hipStream_t stream) {
     case EPI_HEADR:
       if (p.K % 64 != 0 || dma_disabled()) throw std::runtime_error("gemm_nt: EPI_HEADR needs the LDS-DMA GEMM");
       launch_auto<false, false, EPI_HEADR>(p, 1, stream);
+      break;
+    case EPI_HEADL:
+      if (p.K % 64 != 0 || dma_disabled()) throw std::runtime_error("gemm_nt: EPI_HEADL needs the LDS-DMA GEMM");
+      launch_auto<false, false, EPI_HEADL>(p, 1, stream);
       break;
     default: throw std::runtime_error("gemm_nt: unsupported epilogue");
   }

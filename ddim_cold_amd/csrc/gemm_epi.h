@@ -161,7 +161,7 @@ template <int EPI>
 struct FoldEpi {
   static constexpr bool CONSUMER =
       EPI == EPI_QKV || EPI == EPI_GELU || EPI == EPI_BF16 || EPI == EPI_F32 || EPI == EPI_HEAD ||
-      EPI == EPI_HEADR;
+      EPI == EPI_HEADR || EPI == EPI_HEADL;
   static constexpr bool PRODUCER = EPI == EPI_RESID || EPI == EPI_EMBED;
 };
 
@@ -206,6 +206,12 @@ __device__ __forceinline__ RowInfo32 epi_row32(const GemmParams& p, int m) {
     ri.b = p.thr_dp ? divmagic(m, p.tokens, p.tok_magic) : 0;  // drop-path sample (training only)
   } else if (EPI == EPI_GELU || EPI == EPI_DGELU) {
     ri.off = m * p.N;
+  } else if (EPI == EPI_HEADL) {
+    // gradient in the token layout (row m, cls rows included: zero); the target's
+    // patch row is m - b - 1 (b = -1 marks a cls row)
+    const int b = divmagic(m, p.tokens, p.tok_magic);
+    ri.off = m * p.N;
+    ri.b = m - b * p.tokens == 0 ? -1 : b;
   } else if (EPI == EPI_HEADR) {
     // token row m of sample b -> patch row b*P + tok - 1 = m - b - 1 (cls rows skipped)
     const int b = divmagic(m, p.tokens, p.tok_magic), tok = m - b * p.tokens;
@@ -547,8 +553,8 @@ __device__ __forceinline__ f32x4 ld4bf(const bf16* p) {
 // chain of ~3 dependent memory round trips and this removes one of them.
 template <int EPI, int FM, int FN, bool PUB = false, bool SW = false>
 struct VecEpi {
-  static constexpr bool PRE =
-      EPI == EPI_RESID || EPI == EPI_DGELU || EPI == EPI_EMBED || EPI == EPI_ACC || EPI == EPI_HEADR;
+  static constexpr bool PRE = EPI == EPI_RESID || EPI == EPI_DGELU || EPI == EPI_EMBED || EPI == EPI_ACC ||
+                              EPI == EPI_HEADR || EPI == EPI_HEADL;
   static constexpr bool FC = FoldEpi<EPI>::CONSUMER, FP = FoldEpi<EPI>::PRODUCER;
   RowInfo32 rows[FM];
   f32x4 hcf[FM];    // HEADR: the row's DDIM coefficients {sqrt a_t, sqrt(1-a_t), sqrt a_tk, sqrt(1-a_tk)}
@@ -658,6 +664,8 @@ struct VecEpi {
           const int n = nb + j * 16 + cs;
           if (EPI == EPI_RESID) v = ld4(p.res + rows[i].off + n);
           if (EPI == EPI_HEADR && p.head_mode != 2) v = ld4(p.res + rows[i].off + n);  // x_t
+          if (EPI == EPI_HEADL && rows[i].b >= 0)  // target patch row (m - b - 1)
+            v = ld4(p.res + (rows[i].off - (rows[i].b + 1) * p.N) + n);
           if (EPI == EPI_DGELU) v = ld4bf(p.aux + rows[i].off + n);
           if (EPI == EPI_ACC && !p.acc_store) v = ld4(reinterpret_cast<const float*>(p.C) + rows[i].off + n);
           if (EPI == EPI_EMBED) {
@@ -684,6 +692,7 @@ struct VecEpi {
     if (p.thr_dp) salt_dp = site_salt(p.rng, p.site_dp);
     const bool fold = FC && p.ln_st != nullptr;
     const bool prod = FP && p.st_out != nullptr;
+    float lsum = 0.f;  // HEADL: this lane's loss contributions
     float2 ms[FM];
     constexpr int SL = FN / 2;  // 32-column statistics slots per wave
     float2 part[FM][SL];
@@ -763,6 +772,20 @@ struct VecEpi {
             v[c] = e * gelu_grad_f(pre[i][j][c]);
           }
           st4bf(reinterpret_cast<bf16*>(p.C) + idx, v);
+        } else if (EPI == EPI_HEADL) {
+          // smooth-L1 vs the target (multi_gpu_trainer.py:124) and its gradient in the
+          // token layout the head backward reads; cls rows get a zero gradient
+          f32x4 gr = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (rows[i].b >= 0) {
+            const float bt = p.loss_beta;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const float d = v[c] - pre[i][j][c], ad = fabsf(d);
+              lsum += (ad < bt ? 0.5f * d * d / bt : ad - 0.5f * bt) * p.loss_inv_n;
+              gr[c] = fminf(fmaxf(d / bt, -1.f), 1.f) * p.loss_inv_n;
+            }
+          }
+          st4bf(reinterpret_cast<bf16*>(p.C) + idx, gr);
         } else if (EPI == EPI_HEADR) {
           // ViT.py:229-234 on the patch rows: x0-hat clamp, then (modes 1 / 4) the DDIM
           // update with x_t preloaded in `pre`; the new x_t also as the next step's
@@ -830,6 +853,13 @@ struct VecEpi {
             st2f_pub<PUB>(p.st_out + 2 * ((size_t)b * (p.tokens + 1) * np_out + colbase / LN_SLOT + sl), t);
         }
       }
+    }
+    if (EPI == EPI_HEADL) {  // one deterministic loss partial per workgroup
+      __shared__ float lred[4];
+      lsum = wave_sum(lsum);
+      if ((threadIdx.x & 63) == 0) lred[threadIdx.x >> 6] = lsum;
+      __syncthreads();
+      if (threadIdx.x == 0) p.loss_parts[blockIdx.x] = (lred[0] + lred[1]) + (lred[2] + lred[3]);
     }
     if (prod) {
       // the 4 lanes of a row hold 32 consecutive columns per slot (fragments j,

@@ -18,6 +18,8 @@ enum GemmEpi : int {
   EPI_ACC = 9,     // C f32 += acc, one writer per element (no split) ; bias likewise
   EPI_HEADR = 10,  // sampler step on patch rows: +bias, clamp (+DDIM update), f32 [B*P][C*p*p]
                    //   in head-output column order (contiguous: vector epilogue)
+  EPI_HEADL = 11,  // training loss on patch rows: smooth-L1 vs a [B*P][C*p*p] target (head order),
+                   //   token-layout bf16 gradient, one loss partial per workgroup
 };
 
 struct GemmArgs {
@@ -153,6 +155,9 @@ struct ColdSrc {
   // gauss_T > 0: Gaussian DDIM batch instead (t in 0..T-1, x_t = q_sample(x0, t, eps),
   // eps drawn at noise_site, target = x0)
   int gauss_T = 0, noise_site = 0;
+  // target written as patch rows [B*P][C*p*p] in the head's output column order
+  // ((a*p + b)*C + c), for the vector loss epilogue (EPI_HEADL)
+  bool target_rows = false;
 };
 // Gaussian DDIM batch on device in one launch (pool draw, noise, q_sample)
 void gauss_batch_launch(const float* pool, int pool_n, const int64_t* rng, int site, int noise_site, int T,

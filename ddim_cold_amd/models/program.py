@@ -48,6 +48,9 @@ FOLD_LN = os.environ.get("DDIM_COLD_LN_FOLD", "1") == "1"
 # of re-hashing 2 pairs per 4 probabilities (the mask hash was ~1.9 us of the
 # backward's ~11 us, tools/ub_drop.py).  Same masks either way.
 STORE_ATTN_KEEP = os.environ.get("DDIM_COLD_ATTN_KEEP", "1") != "0"
+# training with the fused batch draw: loss target as patch rows, vector loss epilogue
+# (EPI_HEADL; head GEMM 11.3 -> see profiles/README.md round 3)
+TARGET_ROWS = os.environ.get("DDIM_COLD_TARGET_ROWS", "1") == "1"
 # dtype of the bf16 activation copies / folded weights the program allocates
 # (tests on CPU switch it to fp32 to isolate the program logic from rounding)
 ACT_DTYPE = torch.bfloat16
@@ -345,9 +348,13 @@ class ViTProgram:
         rows_w = head_step[5] if head_step is not None and len(head_step) > 5 else None
         if rows_w is not None and patches_in is None:
             raise ValueError("the patch-row sampler state needs patches_in")
+        # the fused batch draw writes the loss target as patch rows for the vector
+        # loss epilogue (ops.head_loss target_rows; the target buffer is only read there)
+        tgt_rows = cold is not None and loss is not None and TARGET_ROWS
         if cold is not None:
             x, patches = ops.patch_embed_cold_fwd(cold, img, t, P.pe_w, P.pe_b, P.cls, P.pos, P.temb, rng,
-                                                  SITE_EMBED, pd, c.patch, ln_st=st[0], xb_out=xb)
+                                                  SITE_EMBED, pd, c.patch, ln_st=st[0], xb_out=xb,
+                                                  target_rows=tgt_rows)
         else:
             x, patches = ops.patch_embed_fwd(img, t, P.pe_w if rows_w is None else rows_w, P.pe_b, P.cls, P.pos,
                                              P.temb, rng, SITE_EMBED, pd, c.patch, ln_st=st[0], xb_out=xb,
@@ -396,7 +403,7 @@ class ViTProgram:
         if loss is not None:  # training: the loss and its token-layout gradient from the head GEMM
             target, beta = loss
             out = ops.head_loss(xb, P.head_wf, P.head_bf, target, c.patch, beta,
-                                fold=(st[2 * L], P.head_c, c.eps, mf, rf))
+                                fold=(st[2 * L], P.head_c, c.eps, mf, rf), target_rows=tgt_rows)
         else:
             out = ops.head_fwd(xb, P.head_wf, P.head_bf, B, c.chans, c.img_h, c.img_w, c.patch,
                                fold=(st[2 * L], P.head_c, c.eps, mf, rf))

@@ -53,26 +53,31 @@ def patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site: int, p: float
 
 
 def patch_embed_cold_fwd(cold, img, t, w_pe, b_pe, cls, pos, temb, rng, site: int, p: float, patch: int,
-                         ln_st=None, xb_out=None):
+                         ln_st=None, xb_out=None, target_rows: bool = False):
     """:func:`cold_batch` fused into :func:`patch_embed_fwd` (one launch fewer per
     training step): ``cold = (pool, data_site, max_t, draw_idx, target_x0, target,
     idx, write_xt)``; the patch rows are pixelated straight from the pool, ``target``,
     ``t`` and (if ``draw_idx``) ``idx`` are written, ``img`` (x_t) only if ``write_xt``.
     Same values as ``cold_batch`` then ``patch_embed_fwd``.  Two optional trailing
     entries ``(gauss_T, noise_site)`` with ``gauss_T > 0`` select the Gaussian DDIM
-    batch instead (same values as :func:`gauss_batch` then ``patch_embed_fwd``)."""
+    batch instead (same values as :func:`gauss_batch` then ``patch_embed_fwd``).
+    ``target_rows``: the target is written as patch rows in the head's output column
+    order (:func:`image_to_rows`) into the same buffer, for :func:`head_loss` with
+    ``target_rows``."""
     pool, dsite, max_t, draw, tx0, target, idx, write_xt = cold[:8]
     gT, nsite = (int(cold[8]), int(cold[9])) if len(cold) > 8 else (0, 0)
     if _hip(img):
         return _ops().patch_embed_cold_fwd(pool, int(dsite), int(max_t), bool(draw), bool(tx0), img, target, t, idx,
                                            bool(write_xt), w_pe, b_pe, cls, pos, temb, rng, site, float(p), patch,
-                                           ln_st, xb_out, gT, nsite)
+                                           ln_st, xb_out, gT, nsite, bool(target_rows))
     if gT > 0:
         gauss_batch(pool, rng, dsite, nsite, gT, img, target, t, idx, draw)
     else:
         cold_batch(pool, rng, dsite, img, target, t, idx, max_t, draw)
         if tx0:
             torch.index_select(pool, 0, idx, out=target)
+    if target_rows:
+        target.copy_(image_to_rows(target.clone(), patch).reshape(target.shape))
     return patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site, p, patch, ln_st, xb_out)
 
 
@@ -226,14 +231,18 @@ def head_fwd(a, w, b, B: int, C: int, H: int, W: int, patch: int, fold=None):
     return ref.head_fwd(a, w, b, B, C, H, W, patch, st, c, eps, mean, rstd)
 
 
-def head_loss(a, w, b, target, patch: int, beta: float = 1.0, fold=None):
+def head_loss(a, w, b, target, patch: int, beta: float = 1.0, fold=None, target_rows: bool = False):
     """Head GEMM + mean smooth-L1 vs ``target`` + its gradient in the token layout, in
     one launch: ``(loss_parts, dtok)`` -- the loss is ``loss_parts.sum()`` (finished by
-    the step tail of :func:`ln_fold_`); the predicted image is never materialised."""
+    the step tail of :func:`ln_fold_`); the predicted image is never materialised.
+    ``target_rows``: the [B, C, H, W]-shaped ``target`` buffer holds patch rows in the
+    head's output order (:func:`image_to_rows`; vector epilogue on a GPU)."""
     st, c, eps, mean, rstd = _fold_args(fold)
     if _hip(a):
-        return _ops().head_loss(a, w, b, target, patch, float(beta), st, c, eps, mean, rstd)
+        return _ops().head_loss(a, w, b, target, patch, float(beta), st, c, eps, mean, rstd, bool(target_rows))
     B, C, H, W = target.shape
+    if target_rows:
+        target = rows_to_image(target.reshape(-1, C * patch * patch), B, C, H, W, patch)
     out = ref.head_fwd(a, w, b, B, C, H, W, patch, st, c, eps, mean, rstd)
     N = a.shape[0] // B
     loss, dtok = ref.smooth_l1_fwd_bwd(out, target, N, patch, beta)

@@ -311,6 +311,10 @@ def test_engine_fused_cold_batch_matches_unfused_cpu():
         return eng.flat_p.clone(), losses, len(calls), bat.t.clone(), bat.x_tm1.clone()
     pf, lf, nf, tf, yf = run(True)
     pu, lu, _, tu, yu = run(False)
+    from ddim_cold_amd import ops
+    from ddim_cold_amd.models import program
+    if program.TARGET_ROWS:  # the fused draw wrote the loss target as patch rows
+        yf = ops.rows_to_image(yf.reshape(-1, 3 * 4 * 4), *yf.shape, 4)
     assert nf == 3  # the fused path really ran
     assert lf == lu and torch.equal(pf, pu) and torch.equal(tf, tu) and torch.equal(yf, yu)
 

@@ -71,3 +71,60 @@ def test_rows_sampler_matches_image_layout_sampler():
     assert all((a - b).abs().mean() < 2e-3 for a, b in zip(s1, s0))
     assert len(c1) == len(c0) and all((a - b).abs().max() < 2e-2 for a, b in zip(c1, c0))
     assert (i1 - i0).abs().mean() < 2e-3
+
+
+@pytest.mark.gpu
+def test_head_loss_rows_matches_image_layout():
+    """Training loss epilogue on a patch-row target (EPI_HEADL) == the image-layout one."""
+    torch.manual_seed(1)
+    B, C, H, W, p, D = 32, 3, 64, 64, 8, 384
+    NP, F = (H // p) * (W // p), C * p * p
+    M = B * (NP + 1)
+    a = torch.randn(M, D, device=DEV).to(torch.bfloat16)
+    st = torch.empty(M, D // 32, 2, device=DEV)
+    xa = a.float().view(M, D // 32, 32)
+    st[..., 0], st[..., 1] = xa.sum(-1), (xa * xa).sum(-1)
+    w = (torch.randn(F, D, device=DEV) * 0.05).to(torch.bfloat16)
+    b = torch.randn(F, device=DEV) * 0.1
+    c = w.float().sum(1)
+    tgt = torch.randn(B, C, H, W, device=DEV).clamp(-1, 1)
+    m0, r0, m1, r1 = (torch.empty(M, device=DEV) for _ in range(4))
+    parts0, g0 = ops.head_loss(a, w, b, tgt, p, 1.0, fold=(st, c, 1e-5, m0, r0))
+    rows = ops.image_to_rows(tgt, p).contiguous().view(B, C, H, W)
+    parts1, g1 = ops.head_loss(a, w, b, rows, p, 1.0, fold=(st, c, 1e-5, m1, r1), target_rows=True)
+    torch.cuda.synchronize()
+    assert abs(parts0.sum().item() - parts1.sum().item()) <= 1e-5 * abs(parts0.sum().item()) + 1e-7
+    assert (g0.float() - g1.float()).abs().max().item() <= 1e-6
+    # (row statistics summed in a different fixed order: last-bit differences)
+    assert torch.allclose(m0, m1, rtol=1e-5, atol=1e-6) and torch.allclose(r0, r1, rtol=1e-5)
+    assert g1.view(B, NP + 1, F)[:, 0].abs().max().item() == 0.0  # cls rows: zero gradient
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gauss", [False, True])
+def test_fused_batch_target_rows(gauss):
+    """The fused batch draw's patch-row target == image_to_rows of its image target."""
+    from ddim_cold_amd.data.synthetic import SITE_DATA, SITE_NOISE, synthetic_pool
+    from ddim_cold_amd.models.program import SITE_EMBED
+    torch.manual_seed(0)
+    model = build_model("vit_tiny").to(DEV).train()
+    B, D, p = 8, model.embed_dim, 8
+    N = model.patch_embed.num_patches + 1
+    pool = synthetic_pool(32, seed=2, device=DEV)
+    rng = torch.tensor([11, 5], dtype=torch.int64, device=DEV)
+    pe_w = model.patch_embed.proj.weight.detach().reshape(D, -1).to(torch.bfloat16).contiguous()
+    args = (pe_w, model.patch_embed.proj.bias.detach(), model.cls_token.detach(), model.pos_embed.detach(),
+            model.time_embed.weight.detach(), rng, SITE_EMBED, 0.1, p)
+    outs = []
+    for rows in (False, True):
+        xt, tg = torch.empty(B, 3, 64, 64, device=DEV), torch.empty(B, 3, 64, 64, device=DEV)
+        t, idx = torch.empty(B, dtype=torch.int64, device=DEV), torch.empty(B, dtype=torch.int64, device=DEV)
+        st = torch.empty(B * N, D // 32, 2, device=DEV)
+        xb = torch.empty(B * N, D, dtype=torch.bfloat16, device=DEV)
+        spec = (pool, SITE_DATA, 6, True, gauss, tg, idx, False) + ((2000, SITE_NOISE) if gauss else (0, 0))
+        x, pt = ops.patch_embed_cold_fwd(spec, xt, t, *args, ln_st=st, xb_out=xb, target_rows=rows)
+        outs.append((x, pt, tg, t))
+    torch.cuda.synchronize()
+    (x0, p0, g0, t0), (x1, p1, g1, t1) = outs
+    assert torch.equal(x0, x1) and torch.equal(p0, p1) and torch.equal(t0, t1)
+    assert torch.equal(ops.image_to_rows(g0, p).reshape(g1.shape), g1)
