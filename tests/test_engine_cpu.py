@@ -330,7 +330,9 @@ def _layout_worker(rank, world, port, out_path):
         xb, yb, tb = x[rank * b:(rank + 1) * b], y[rank * b:(rank + 1) * b], t[rank * b:(rank + 1) * b]
         snap = eng._snapshot_state()
         res = {}
-        for name, bb, eb, inline in eng.COMM_LAYOUTS:
+        # the fixed layouts + model-picked bucket sizes (cost model candidates)
+        lays = list(eng.COMM_LAYOUTS) + [eng.layout_by_name(n) for n in ("overlap-1", "overlap-3", "overlap-7")]
+        for name, bb, eb, inline in lays:
             eng.set_comm_layout(bb, eb, inline)
             cover = sorted(eng.buckets)  # buckets tile the arena for every layout
             assert cover[0][0] == 0 and cover[-1][1] == eng.numel
@@ -360,6 +362,6 @@ def test_comm_layouts_same_training_gloo():
     assert torch.equal(r["p0"], r["p_end"])
     base = r["overlap-2"]
     assert not torch.equal(base[0], r["p0"])
-    for name in ("overlap-4", "inline-1"):
+    for name in ("overlap-4", "inline-1", "overlap-1", "overlap-3", "overlap-7"):
         for a, b in zip(base, r[name]):
             assert torch.equal(a, b), name

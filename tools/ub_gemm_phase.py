@@ -32,6 +32,15 @@ for B in (32, 64):
     w3, b3 = bf(3 * D, D, sc=0.05), torch.randn(3 * D, device=dev)
     x = torch.randn(M, D, device=dev)
     res[f"qkv M={M}"] = t(lambda: ops.qkv_fwd(a, w3, b3, B, N, H))
+    # LayerNorm-folded consumers / producer, as in the model
+    st = torch.rand(M, D // 32, 2, device=dev) + 1.0
+    c3, c1 = torch.randn(3 * D, device=dev), torch.randn(D, device=dev)
+    mo, ro = torch.empty(M, device=dev), torch.empty(M, device=dev)
+    so, xo = torch.empty(M, D // 32, 2, device=dev), torch.empty(M, D, dtype=torch.bfloat16, device=dev)
+    res[f"qkv fold M={M}"] = t(lambda: ops.qkv_fwd(a, w3, b3, B, N, H, fold=(st, c3, 1e-5, mo, ro)))
+    res[f"gelu fold M={M}"] = t(lambda: ops.linear_gelu_fwd(a, w, b, r, 5, 0.0, fold=(st, c1, 1e-5, mo, ro)))
+    res[f"resid prod M={M}"] = t(lambda: ops.linear_residual_fwd(a, w, b, x, N, r, 3, 0.0, 4, 0.0, st_out=so,
+                                                                 xb_out=xo))
     res[f"resid M={M}"] = t(lambda: ops.linear_residual_fwd(a, w, b, x, N, r, 3, 0.0, 4, 0.0))
     res[f"gelu M={M}"] = t(lambda: ops.linear_gelu_fwd(a, w, b, r, 5, 0.0))
 res["empty"] = t(lambda: r.add_(0))
