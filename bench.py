@@ -307,7 +307,6 @@ def run(args):
             "vs_baseline": round(value / (BASELINE_IMG_S_PER_GPU * n), 3)
                            if args.model == "vit_tiny" and args.dataset == "cold" else None,
             "dtype": "bf16",
-            "rehearsal_shared_gpu_gloo": True if SHARED_GPU else None,
             "data": "synthetic (on-device Oxford-Flowers-shaped pool, " +
                     ("cold pixelation pairs" if args.dataset == "cold" else "Gaussian DDIM q_sample pairs") +
                     "), random-init weights",
@@ -336,6 +335,8 @@ def run(args):
                        "optimizer": "AdamW(wd=0.05)+clip1.0+cosine", "final_loss": round(loss, 5)},
         }
         out.update(extra)
+        if SHARED_GPU:  # not a scaling measurement: every rank on device 0 over gloo
+            out["rehearsal_shared_gpu_gloo"] = True
         print(json.dumps(out), flush=True)
     engine.close()
     cleanup()
