@@ -189,11 +189,15 @@ def run(args):
         if n > 1:
             # measured all-reduce curve on this job's ranks -> fitted cost model, which
             # orders the bucket layouts (parallel/costmodel.py); outside the timed region
-            fit, probe = engine.probe_allreduce()
-            comm_model = {"probe_us": {f"{b / 2**20:g}MB": round(u, 1) for b, u in probe.items()},
-                          "alpha_us": round(fit.alpha_us, 2), "algbw_GBs": round(fit.algbw_gbs, 1),
-                          "busbw_GBs": round(fit.busbw_gbs, 1),
-                          "predicted_exposed_us": {L[0]: round(L[4], 1) for L in engine.model_layouts()[:4]}}
+            try:
+                fit, probe = engine.probe_allreduce()
+                comm_model = {"probe_us": {f"{b / 2**20:g}MB": round(u, 1) for b, u in probe.items()},
+                              "alpha_us": round(fit.alpha_us, 2), "algbw_GBs": round(fit.algbw_gbs, 1),
+                              "busbw_GBs": round(fit.busbw_gbs, 1),
+                              "predicted_exposed_us": {L[0]: round(L[4], 1) for L in engine.model_layouts()[:4]}}
+            except Exception as e:  # diagnostics only: the benchmark goes on with the fixed candidates
+                comm_model = {"error": repr(e)[:200]}
+                engine.comm_fit = None
         if args.comm_layout == "auto":
             engine.autotune_comm()
         else:
