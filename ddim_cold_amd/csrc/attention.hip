@@ -592,6 +592,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
   __syncthreads();
   const int ntiles = (N + 63) / 64;
   const float nl2 = -lse2;
+  const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * attn_mask_ld(N));
   // key mask only in the tail tile: a padded key has a zero K row (no dQ
   // contribution) but exp2(0 - lse) can overflow, so it must not reach dS
   auto tile = [&](int it, auto mask_tag) {
@@ -610,16 +611,17 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
         st = mfma16(frag_row<HD>(Kl, 16 * t + li, s, g), qf[s], st);
         dp = mfma16(frag_row<HD>(Vl, 16 * t + li, s, g), df[s], dp);
       }
+      // the lane's 4 keys are consecutive elements of one mask row (aligned: the
+      // row stride is a multiple of 4): 2 pair hashes instead of 4 single ones
+      bool kp[4] = {true, true, true, true};
+      if (thr) dropout_keep4(salt, rowidx + (uint32_t)(kv0 + 16 * t + 4 * g), thr, kp);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = kv0 + 16 * t + 4 * g + r;
         float pr = fexp2(fmaf(st[r], sl2, nl2));
         if (MASK && key >= N) pr = 0.f;
         float dpv = dp[r];
-        if (thr) {
-          const uint32_t idx = (uint32_t)(((size_t)bh * N + q) * attn_mask_ld(N) + key);
-          dpv = dropout_keep(salt, idx, thr) ? dpv * dsc : 0.f;
-        }
+        if (thr) dpv = kp[r] ? dpv * dsc : 0.f;
         ds[t][r] = pr * (dpv - dl);
       }
     }
@@ -745,17 +747,32 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
         st = mfma16(frag_row<HD>(Ql, 16 * t + li, s, g), kf[s], st);
         dp = mfma16(frag_row<HD>(Dl, 16 * t + li, s, g), vf[s], dp);
       }
+      // keep flags of (query 16t+4g+r, this lane's key): a mask pair is two adjacent
+      // keys of one row, held by lanes li and li^1 -- each of the two hashes the
+      // pair of 2 of the 4 rows and they swap the results (2 hashes per lane, not 4)
+      bool kp[4] = {true, true, true, true};
+      if (thr) {
+        const int odd = li & 1;
+        uint32_t hw[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int qq = q0 + 16 * t + 4 * g + 2 * odd + u;
+          const uint32_t idx = (uint32_t)(((size_t)bh * N + qq) * attn_mask_ld(N) + (key & ~1));
+          hw[u] = drop_hash(salt, idx >> 1);
+        }
+        const uint32_t p0 = (uint32_t)__shfl_xor((int)hw[0], 1, 64), p1 = (uint32_t)__shfl_xor((int)hw[1], 1, 64);
+        const uint32_t hr[4] = {odd ? p0 : hw[0], odd ? p1 : hw[1], odd ? hw[0] : p0, odd ? hw[1] : p1};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) kp[r] = (odd ? (hr[r] >> 16) : (hr[r] & 0xFFFFu)) >= thr;
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qr = 16 * t + 4 * g + r;
-        const int qq = q0 + qr;
         const float pr = fexp2(fmaf(st[r], sl2, -sl[qr]));  // padded queries: lse = +inf -> 0
         float pd = pr, dpv = dp[r];
         if (thr) {
-          const uint32_t idx = (uint32_t)(((size_t)bh * N + qq) * attn_mask_ld(N) + key);
-          const bool kp = dropout_keep(salt, idx, thr);
-          pd = kp ? pr * dsc : 0.f;
-          dpv = kp ? dpv * dsc : 0.f;
+          pd = kp[r] ? pr * dsc : 0.f;
+          dpv = kp[r] ? dpv * dsc : 0.f;
         }
         pm[t][r] = pd;
         ds[t][r] = pr * (dpv - sd[qr]);
