@@ -15,7 +15,7 @@ from typing import Optional, Sequence
 
 import torch
 
-from .samplers import ddim_from_starts
+from .samplers import _unit_host, ddim_from_starts
 from .schedule import img2img_alpha
 
 
@@ -63,5 +63,5 @@ def interpolate(model, img1: torch.Tensor, img2: torch.Tensor, t_starts: Sequenc
     else:
         x0 = torch.cat([ddim_from_starts(model, x[i * n:(i + 1) * n], starts[i * n:(i + 1) * n], k, device, use_graph)
                         for i in range(len(t_starts))])
-    out = ((x0.cpu() + 1) / 2).view(len(t_starts), n, *img1.shape[-3:])
+    out = _unit_host(x0).view(len(t_starts), n, *img1.shape[-3:])
     return torch.cat([rows[0].unsqueeze(0), out])
