@@ -19,6 +19,6 @@ run bench_dp1 300 python bench.py --force-dist --no-sampler --steps 1000 --warmu
 if [ "${PROF:-1}" = "1" ]; then
   export TMPDIR=/tmp
   rm -rf gpurun_out/prof_step gpurun_out/prof_sampler
-  run prof_step 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_step -o run -- python3 bench.py --steps 50 --warmup 5 --no-sampler --no-graph
+  run prof_step 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_step -o run -- python3 bench.py --steps 50 --warmup 5 --no-sampler --no-graph --no-gaussian
   run prof_sampler 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_sampler -o run -- python3 tools/sampler_prof.py
 fi
