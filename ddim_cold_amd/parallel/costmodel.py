@@ -105,7 +105,7 @@ class StepProfile:
     ``block_bwd_us``: input-gradient backward of one block (its weight gradients are
     deferred to the bucket's launch); ``block_wgrad_us``: that block's share of the
     weight-gradient launch; ``bucket_overhead_us``: fixed cost of one more bucket
-    (its own weight-gradient launch + counter bump, measured ~8-9 us at one rank);
+    (its own weight-gradient launch + counter bump + hand-off, ~13 us at one rank);
     ``tail_us``: embedding backward after block 0; ``block_bytes`` / ``embed_bytes``:
     gradient bytes on the wire (fp32: 4 per parameter, bf16 wire: 2)."""
     depth: int
@@ -119,14 +119,14 @@ class StepProfile:
 
 # ViT-tiny B=32 single-process step (profiles/graph_step_table_r3.txt): ~45 us of
 # input-gradient kernels per block, 54.5 us for the step's weight-gradient GEMMs
-# (7.8 us per block), 9.4 us embedding backward; ~8.5 us per extra bucket
-# (profiles/README.md, 1-rank bucket-count sweep)
+# (7.8 us per block), 9.4 us embedding backward; ~13 us per extra bucket
+# (profiles/dp/bucket_overhead_r3.txt: 1-rank RCCL step with 2 / 3 / 4 / 8 buckets)
 _TINY_BLOCK_WORK = 2080 * 888_576  # tokens x block parameters of that measurement
 
 
 def vit_step_profile(depth: int, dim: int, hidden: int, batch_tokens: int, other_params: int,
                      wire_bytes: int = 4, block_bwd_us: float = 45.0, block_wgrad_us: float = 7.8,
-                     tail_us: float = 9.4, bucket_overhead_us: float = 8.5) -> StepProfile:
+                     tail_us: float = 9.4, bucket_overhead_us: float = 13.0) -> StepProfile:
     """StepProfile from the model shape: the measured ViT-tiny constants, scaled by
     GEMM work (tokens x block parameters) above the per-block launch floor."""
     block_params = 3 * dim * dim + 3 * dim + dim * dim + dim + 2 * dim * hidden + hidden + dim + 4 * dim
