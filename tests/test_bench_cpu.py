@@ -56,3 +56,13 @@ def test_bench_world_size_mismatch_fails():
     assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
     assert "WORLD_SIZE=1" in r.stderr
     assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_bench_gaussian_dataset_two_ranks_cpu():
+    """--dataset gaussian times the Gaussian DDIM task (sparse time_embed row exchange
+    across 2 gloo ranks) and labels the metric / data accordingly (no baseline ratio)."""
+    r = _bench(["--gpus", "2", "--steps", "2", "--warmup", "1", "--no-sampler", "--dataset", "gaussian"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert out["metric"].endswith("Gaussian DDIM") and out["vs_baseline"] is None
+    assert "Gaussian DDIM" in out["data"] and out["n_gpus"] == 2 and out["value"] > 0
