@@ -260,10 +260,11 @@ __device__ __forceinline__ void flash_softmax_tile(f32x4 (&st)[4], f32x4 (&o)[DT
   }
   const float nm = -m_run;
   float ls = 0.f;
+  const uint32_t pg = DROP ? ((rowidx >> 1) + 2u * (uint32_t)g) * DROP_GOLDEN : 0u;  // rowidx even
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     bool kp[4] = {true, true, true, true};
-    if (DROP) dropout_keep4(salt, rowidx + (uint32_t)(16 * t + 4 * g), thr, kp);
+    if (DROP) dropout_keep4_pg(salt, pg + (uint32_t)(8 * t) * DROP_GOLDEN, thr, kp);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float pv = fexp2(fmaf(st[t][r], sl2, nm));
@@ -593,6 +594,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
   const int ntiles = (N + 63) / 64;
   const float nl2 = -lse2;
   const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * attn_mask_ld(N));
+  const uint32_t pgq = ((rowidx >> 1) + 2u * (uint32_t)g) * DROP_GOLDEN;  // pair hash base of this lane's row
   // key mask only in the tail tile: a padded key has a zero K row (no dQ
   // contribution) but exp2(0 - lse) can overflow, so it must not reach dS
   auto tile = [&](int it, auto mask_tag) {
@@ -614,7 +616,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
       // the lane's 4 keys are consecutive elements of one mask row (aligned: the
       // row stride is a multiple of 4): 2 pair hashes instead of 4 single ones
       bool kp[4] = {true, true, true, true};
-      if (thr) dropout_keep4(salt, rowidx + (uint32_t)(kv0 + 16 * t + 4 * g), thr, kp);
+      if (thr) dropout_keep4_pg(salt, pgq + (uint32_t)(kv0 / 2 + 8 * t) * DROP_GOLDEN, thr, kp);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = kv0 + 16 * t + 4 * g + r;
@@ -753,13 +755,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
       bool kp[4] = {true, true, true, true};
       if (thr) {
         const int odd = li & 1;
+        // pair index of (query qq, key pair) = qq_row * ld/2 + key/2: the multiply by the
+        // golden constant is hoisted (pg of query q0+4g+2odd, + (16t+u) rows of ldh*golden)
+        const uint32_t ldh = (uint32_t)(attn_mask_ld(N) >> 1);
+        const uint32_t pb = ((uint32_t)(bh * N + q0 + 4 * g + 2 * odd) * ldh + (uint32_t)(key >> 1)) * DROP_GOLDEN;
+        const uint32_t ldhg = ldh * DROP_GOLDEN;
         uint32_t hw[2];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int qq = q0 + 16 * t + 4 * g + 2 * odd + u;
-          const uint32_t idx = (uint32_t)(((size_t)bh * N + qq) * attn_mask_ld(N) + (key & ~1));
-          hw[u] = drop_hash(salt, idx >> 1);
-        }
+        for (int u = 0; u < 2; ++u) hw[u] = mix32((pb + (uint32_t)(16 * t + u) * ldhg) ^ salt);
         const uint32_t p0 = (uint32_t)__shfl_xor((int)hw[0], 1, 64), p1 = (uint32_t)__shfl_xor((int)hw[1], 1, 64);
         const uint32_t hr[4] = {odd ? p0 : hw[0], odd ? p1 : hw[1], odd ? hw[0] : p0, odd ? hw[1] : p1};
 #pragma unroll
@@ -944,11 +947,12 @@ __global__ __launch_bounds__(NP * 4) void attn_fwd_short_kernel(const bf16* __re
   const float nmx = -mx;
   float l = 0.f;
   const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * attn_mask_ld(N));
+  const uint32_t pgs = ((rowidx >> 1) + 2u * (uint32_t)g) * DROP_GOLDEN;
   uint32_t kbits = 0u;
 #pragma unroll
   for (int t = 0; t < KT; ++t) {
     bool kp[4] = {true, true, true, true};
-    if (DROP) dropout_keep4(salt, rowidx + (uint32_t)(16 * t + 4 * g), thr, kp);
+    if (DROP) dropout_keep4_pg(salt, pgs + (uint32_t)(8 * t) * DROP_GOLDEN, thr, kp);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float pv = fexp2(fmaf(st[t][r], sl2, nmx));
@@ -1068,7 +1072,7 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
 #pragma unroll
         for (int r = 0; r < 4; ++r) kq[r] = (kbits >> (4 * t + r)) & 1u;
       } else {
-        dropout_keep4(salt, rowidx + (uint32_t)(16 * t + 4 * g), thr, kq);
+        dropout_keep4_pg(salt, ((rowidx >> 1) + 2u * (uint32_t)g + 8u * (uint32_t)t) * DROP_GOLDEN, thr, kq);
       }
     }
 #pragma unroll

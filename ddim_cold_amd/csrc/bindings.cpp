@@ -290,6 +290,9 @@ std::tuple<Tensor, Tensor> attn_fwd(Tensor qkv, double scale, Tensor rng, int64_
   TORCH_CHECK(qkv.dim() == 5 && qkv.size(0) == 3, "qkv must be [3,B,H,N,hd]");
   const int B = qkv.size(1), H = qkv.size(2), N = qkv.size(3), hd = qkv.size(4);
   TORCH_CHECK(hd == 32 || hd == 64, "head dim must be 32 or 64");
+  // dropout mask elements are indexed with 32-bit counters (hoisted pair-hash math)
+  TORCH_CHECK(p <= 0 || (int64_t)B * H * N * ((N + 3) & ~3) < ((int64_t)1 << 32),
+              "attention dropout: more than 2^32 mask elements");
   auto o = at::empty({B, N, H * hd}, qkv.options());
   auto lse = at::empty({B, H, N}, qkv.options().dtype(F32));
   attn_fwd_launch(qkv.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), B, H, N, hd, (float)scale,
@@ -699,6 +702,8 @@ Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, double scale, Ten
   TORCH_CHECK(dout.numel() == (int64_t)B * N * H * hd && o.numel() == dout.numel() &&
                   lse.numel() == (int64_t)B * H * N,
               "attn_bwd shapes");
+  TORCH_CHECK(p <= 0 || (int64_t)B * H * N * ((N + 3) & ~3) < ((int64_t)1 << 32),
+              "attention dropout: more than 2^32 mask elements");
   auto dqkv = at::empty({(int64_t)B * N, 3 * H * hd}, qkv.options());
   auto delta = at::empty({(int64_t)B * H * N}, lse.options());
   attn_bwd_launch(dout.data_ptr(), qkv.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), dqkv.data_ptr(),

@@ -103,6 +103,19 @@ __device__ __forceinline__ void dropout_keep4(uint32_t salt, uint32_t idx, uint3
   k[3] = (h1 >> 16) >= thresh;
 }
 
+// dropout_keep4 with the pair hash input precomputed: pg = (idx >> 1) * golden for an even
+// idx.  Consecutive tiles of one mask row differ by a constant number of pairs, so callers
+// hoist the multiply out of their tile loops and add a (constant-folded) offset: 2 of the
+// 3 v_mul_lo_u32 (quarter rate) per hash remain.  Same flags as dropout_keep4.
+constexpr uint32_t DROP_GOLDEN = 0x9E3779B1u;
+__device__ __forceinline__ void dropout_keep4_pg(uint32_t salt, uint32_t pg, uint32_t thresh, bool (&k)[4]) {
+  const uint32_t h0 = mix32(pg ^ salt), h1 = mix32((pg + DROP_GOLDEN) ^ salt);
+  k[0] = (h0 & 0xFFFFu) >= thresh;
+  k[1] = (h0 >> 16) >= thresh;
+  k[2] = (h1 & 0xFFFFu) >= thresh;
+  k[3] = (h1 >> 16) >= thresh;
+}
+
 // attention-probability masks index (b, h, q, key) as (bh * N + q) * ld + key
 // with the row stride padded to 4 (aligned pairs / quads within a row)
 __host__ __device__ __forceinline__ int attn_mask_ld(int N) { return (N + 3) & ~3; }
