@@ -817,7 +817,7 @@ class TrainEngine:
         self.steps_done = steps
         self._refresh_shadow()
 
-    def autotune_comm(self, steps: int = 40, warm: int = 6, layouts=None):
+    def autotune_comm(self, steps: int = 100, warm: int = 10, layouts=None):
         """Pick the gradient-exchange layout by measuring it on THIS job's ranks.
 
         Every layout of ``layouts`` (default :attr:`COMM_LAYOUTS`) runs ``warm``
