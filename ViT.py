@@ -40,7 +40,7 @@ def main(sample_n, acc_k, ckpt, model_name, out_dir, seq_n, seq_k, seed):
     from ddim_cold_amd.models import build_model
     from ddim_cold_amd.train.checkpoint import load_weights
     device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
-    model = build_model(model_name)
+    model = build_model(model_name, init_order="vit")  # ViT.py:184 draw order (weights are loaded anyway)
     if os.path.isfile(ckpt):
         load_weights(model, ckpt, strict=True)
     else:

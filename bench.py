@@ -80,6 +80,9 @@ def parse_args(argv=None):
                     help="1 GPU: skip the extra Gaussian-DDIM training throughput key")
     ap.add_argument("--no-eager-baseline", action="store_true",
                     help="skip timing the plain eager PyTorch sampler (BASELINE.md's sampling comparator)")
+    ap.add_argument("--no-vendor", action="store_true",
+                    help="1 GPU: skip the same-node vendor comparators (stock PyTorch-ROCm ops: hipBLASLt, SDPA, "
+                         "fused AdamW; training step and DDIM sampler each captured whole in one graph)")
     return ap.parse_args(argv)
 
 
@@ -250,6 +253,20 @@ def run(args):
         extra["gaussian_ddim_final_loss"] = round(gl, 5)
         ge.close()
         del ge, gm
+    if rank == 0 and n == 1 and args.dataset == "cold" and not args.no_vendor and dev.type == "cuda":
+        # same-node vendor comparator: the reference step (multi_gpu_trainer.py:115-134) from stock
+        # PyTorch-ROCm ops (hipBLASLt / SDPA / fused AdamW), captured whole in one graph
+        from ddim_cold_amd.bench.vendor_baseline import time_vendor_train
+        torch.manual_seed(1234)
+        vm = build_model(args.model).to(dev).train()
+        vdt, vloss, vkind = time_vendor_train(vm, pool, args.batch, lr, 512 * 100, steps=args.steps,
+                                              warmup=args.warmup)
+        extra["train_vendor_graph_img_per_s"] = round(args.batch / vdt, 1)
+        extra["train_vendor_graph_ms_per_step"] = round(vdt * 1e3, 4)
+        extra["train_vs_vendor_graph"] = round((value / n) / (args.batch / vdt), 2)
+        extra["train_vendor_config"] = {"attn": "sdpa", "optimizer": f"AdamW({vkind})", "graph": True,
+                                        "autocast": "bf16", "final_loss": round(vloss, 5)}
+        del vm
     # the sampler metric is a 1-GPU number (BASELINE.json config 5): multi-rank runs skip it
     if rank == 0 and n == 1 and not args.no_sampler and dev.type == "cuda":
         from ddim_cold_amd.diffusion.samplers import DDIMSampler
@@ -280,6 +297,13 @@ def run(args):
             extra["ddim_sampler_eager_torch_fp32_img_per_s"] = round(args.sampler_n / e32, 1)
             extra["ddim_sampler_eager_torch_bf16_img_per_s"] = round(args.sampler_n / ebf, 1)
             extra["ddim_sampler_vs_eager_fp32"] = round(e32 / dt, 2)
+        if not args.no_vendor:
+            # same-node vendor comparator: the 100-step loop from stock ops (SDPA, hipBLASLt,
+            # bf16 autocast, fp32 update) unrolled into one graph
+            from ddim_cold_amd.bench.vendor_baseline import time_vendor_sampler
+            vs = time_vendor_sampler(model, args.sampler_n, args.sampler_k, reps=5)
+            extra["ddim_sampler_vendor_graph_img_per_s"] = round(args.sampler_n / vs, 1)
+            extra["ddim_sampler_vs_vendor_graph"] = round(vs / dt, 2)
         # BASELINE.json config 5, second half: the draft->drawing img2img call of
         # ViT_draft2drawing.py:389-409 (9 t_starts 1599..1999, k=10, up to 200 steps)
         # as ONE batched replayed hipGraph; comparator = the reference's sequential

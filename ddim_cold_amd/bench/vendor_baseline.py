@@ -1,0 +1,265 @@
+"""Same-node vendor-library comparators: the reference's training step and DDIM
+sampler built from stock PyTorch-ROCm ops (hipBLASLt GEMMs via ``nn.Linear``,
+MIOpen conv, ATen LayerNorm / GELU / dropout, ``F.scaled_dot_product_attention``,
+fused ``torch.optim.AdamW``) and captured WHOLE in one ``torch.cuda.CUDAGraph``
+(a hipGraph on ROCm).  Python dispatch and launch gaps are therefore gone from
+these numbers too: what remains is the vendor kernels themselves, which is the
+comparison the hand-written stack has to win.
+
+* :class:`VendorTrainStep` — `multi_gpu_trainer.py:115-134` as one graph: an
+  on-device cold batch draw (pool index + t ~ U{1..log2 W} + NEAREST pixelation
+  pair, `diffusion_loader.py:79-97`, in plain torch ops), forward under bf16
+  autocast, ``F.smooth_l1_loss``, backward, ``clip_grad_norm_(1.0)``,
+  ``AdamW(wd=0.05, fused=True, capturable=True)`` with the per-iteration cosine
+  LR computed on the device (``CosineAnnealingLR``'s closed form, eta_min 0).
+* :class:`VendorSampler` — the 100-step k=20 DDIM loop of `ViT.py:220-237`
+  (bf16 autocast forward, fp32 clamp / eps-hat / update) unrolled into one graph.
+
+``attn="sdpa"`` (default) runs attention through ``F.scaled_dot_product_attention``
+(the ROCm flash / memory-efficient kernels); ``attn="explicit"`` through the
+reference's materialised softmax (``Attention.forward``).  Everything runs
+eagerly on the CPU (``use_graph=False``) for the plumbing tests.
+"""
+from __future__ import annotations
+
+import math
+import time
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+
+def vendor_forward(model, x: torch.Tensor, t: torch.Tensor, attn: str = "sdpa") -> torch.Tensor:
+    """``model.forward_reference`` with the attention core as
+    ``F.scaled_dot_product_attention`` (``attn='sdpa'``); same parameters, same
+    dropout / drop-path semantics in train mode (`ViT.py:105-137`, `:199-218`)."""
+    if attn == "explicit":
+        return model.forward_reference(x, t)
+    tr = model.training
+    h = _tokens(model, x, t)
+    for blk in model.blocks:
+        a = blk.attn
+        B, N, C = h.shape
+        H = a.num_heads
+        qkv = a.qkv(blk.norm1(h)).view(B, N, 3, H, C // H).permute(2, 0, 3, 1, 4)
+        p = a.attn_drop.p if tr else 0.0
+        y = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], dropout_p=p, scale=a.scale)
+        y = y.transpose(1, 2).reshape(B, N, C)
+        h = h + blk.drop_path(_drop(a.proj(y), a.proj_drop.p, tr))
+        m = blk.mlp
+        z = m.fc2(_drop(m.act(m.fc1(blk.norm2(h))), m.drop.p, tr))
+        h = h + blk.drop_path(_drop(z, m.drop.p, tr))
+    return model.unpatchify(model.head(model.norm(h))[:, 1:, :])
+
+
+def _drop(x, p, training):
+    """Dropout as Bernoulli(1-p) keep mask (fp32 uniform < 1-p) and 1/(1-p) scaling.
+    Not ``F.dropout``: its bf16 kernel inside a captured graph (PyTorch 2.10 / ROCm
+    7) turned the replayed training step NaN after ~12 replays, with fp32 inputs or
+    this form it does not (tools/vendor_debug.py bisection).  Costs the vendor step
+    one uniform-draw launch per dropout site over the native fused kernel."""
+    if not training or p == 0.0:
+        return x
+    keep = 1.0 - p
+    return x * ((torch.rand(x.shape, device=x.device) < keep).to(x.dtype) * (1.0 / keep))
+
+
+def _tokens(model, x, t):
+    """``prepare_tokens`` (`ViT.py:199-206`) with the pos_drop through :func:`_drop`."""
+    B = x.shape[0]
+    tok = model.patch_embed(x)
+    tok = torch.cat((model.cls_token.expand(B, -1, -1).to(tok.dtype), tok), dim=1)
+    return _drop(tok + model.pos_embed + model.time_embed(t).unsqueeze(1), model.pos_drop.p, model.training)
+
+
+def cold_batch_torch(pool: torch.Tensor, batch: int, max_t: int):
+    """(x_t, x_{t-1}, t) with t ~ U{1..max_t}: x_s[h, w] = img[2^s floor(h / 2^s), 2^s floor(w / 2^s)]
+    (NEAREST down to W / 2^s then NEAREST up, `diffusion_loader.py:79-83`), in plain
+    torch ops on ``pool``'s device (graph-capturable with the default generator)."""
+    dev = pool.device
+    P, C, H, W = pool.shape
+    idx = torch.randint(0, P, (batch,), device=dev)
+    t = torch.randint(1, max_t + 1, (batch,), device=dev)
+    img = pool.index_select(0, idx)
+    bi = torch.arange(batch, device=dev)[:, None, None]
+    ar_h = torch.arange(H, device=dev)[None, :]
+    ar_w = torch.arange(W, device=dev)[None, :]
+
+    def pix(s):
+        f = (1 << s)[:, None]
+        rows = (ar_h // f) * f  # [B, H]
+        cols = (ar_w // f) * f  # [B, W]
+        return img.permute(0, 2, 3, 1)[bi, rows[:, :, None], cols[:, None, :]].permute(0, 3, 1, 2)
+
+    return pix(t), pix(t - 1), t
+
+
+class VendorTrainStep:
+    """The reference training step from stock PyTorch-ROCm ops, captured whole."""
+
+    def __init__(self, model, pool: torch.Tensor, batch: int, lr: float, t_max: int, attn: str = "sdpa",
+                 weight_decay: float = 0.05, clip: float = 1.0, use_graph: bool = True):
+        self.model = model.train()
+        self.pool = pool
+        self.batch = batch
+        self.attn = attn
+        self.clip = clip
+        self.max_t = int(math.log2(model.img_size[1]))
+        dev = pool.device
+        self.dev = dev
+        self.cuda = dev.type == "cuda"
+        self.params = [p for p in model.parameters() if p.requires_grad]
+        self.base_lr = lr
+        self.t_max = t_max
+        self.lr_t = torch.tensor(lr, dtype=torch.float32, device=dev)
+        self.step_t = torch.zeros((), dtype=torch.float32, device=dev)
+        kw = dict(lr=self.lr_t, weight_decay=weight_decay)
+        self.optimizer_kind = "fused"
+        if self.cuda:
+            try:
+                self.opt = torch.optim.AdamW(self.params, fused=True, capturable=True, **kw)
+            except (RuntimeError, ValueError):
+                self.opt = torch.optim.AdamW(self.params, foreach=True, capturable=True, **kw)
+                self.optimizer_kind = "foreach-capturable"
+        else:
+            self.opt = torch.optim.AdamW(self.params, lr=lr, weight_decay=weight_decay)
+            self.optimizer_kind = "cpu"
+        self.loss = torch.zeros((), device=dev)
+        self.use_graph = use_graph and self.cuda
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+
+    def _body(self):
+        x_t, target, t = cold_batch_torch(self.pool, self.batch, self.max_t)
+        with torch.autocast(self.dev.type, dtype=torch.bfloat16, enabled=self.cuda, cache_enabled=False):
+            pred = vendor_forward(self.model, x_t, t, self.attn)
+        loss = F.smooth_l1_loss(pred.float(), target)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(self.params, self.clip)
+        if self.cuda:
+            # CosineAnnealingLR(T_max, eta_min=0) stepped per iteration, on the device
+            self.lr_t.copy_(0.5 * self.base_lr * (1 + torch.cos(math.pi * self.step_t / self.t_max)))
+        else:
+            for g in self.opt.param_groups:
+                g["lr"] = 0.5 * self.base_lr * (1 + math.cos(math.pi * float(self.step_t) / self.t_max))
+        self.opt.step()
+        self.step_t += 1
+        self.loss.copy_(loss.detach())
+
+    def _eager(self):
+        self.opt.zero_grad(set_to_none=True)
+        self._body()
+
+    def capture(self, warm: int = 3):
+        s = torch.cuda.Stream(self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(s):
+            for _ in range(warm):
+                self._eager()
+        torch.cuda.current_stream(self.dev).wait_stream(s)
+        torch.cuda.synchronize(self.dev)
+        self.opt.zero_grad(set_to_none=True)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._body()
+        self.graph = g
+
+    def steps(self, n: int):
+        if self.use_graph:
+            if self.graph is None:
+                self.capture()
+            for _ in range(n):
+                self.graph.replay()
+        else:
+            for _ in range(n):
+                self._eager()
+
+
+class VendorSampler:
+    """DDIM k-step sampler (`ViT.py:220-237`) from stock ops, all steps in one graph;
+    x_T drawn on the device, result returned on the host in [0, 1]."""
+
+    def __init__(self, model, N: int, k: int, attn: str = "sdpa", use_graph: bool = True):
+        T = model.total_steps
+        if T % k != 0:
+            raise ValueError(f"k={k} must divide total_steps={T}")
+        self.model = model.eval()
+        self.dev = next(model.parameters()).device
+        self.cuda = self.dev.type == "cuda"
+        self.N, self.k, self.attn = N, k, attn
+        C, (H, W) = model.in_chans, model.img_size
+        self.ts = list(range(T - 1, 0, -k))
+        self.x_in = torch.empty(N, C, H, W, device=self.dev)
+        self.out = torch.empty(N, C, H, W, device=self.dev)
+        self.tt = [torch.full((N,), t, dtype=torch.int64, device=self.dev) for t in self.ts]
+        self.use_graph = use_graph and self.cuda
+        self.graph = None
+
+    @torch.no_grad()
+    def _body(self):
+        T, k = self.model.total_steps, self.k
+        x = self.x_in
+        x0 = x
+        for i, t in enumerate(self.ts):
+            with torch.autocast(self.dev.type, dtype=torch.bfloat16, enabled=self.cuda, cache_enabled=False):
+                x0 = vendor_forward(self.model, x, self.tt[i], self.attn)
+            x0 = torch.clamp(x0.float(), -1.0, 1.0)
+            a_tk = 1 - math.sqrt((t + 1 - k) / T)
+            a_t = 1 - math.sqrt((t + 1) / T) + 1e-5
+            eps = (x - math.sqrt(a_t) * x0) / math.sqrt(1 - a_t)
+            x = math.sqrt(a_tk) * (x / math.sqrt(a_t) + (math.sqrt((1 - a_tk) / a_tk) - math.sqrt((1 - a_t) / a_t)) * eps)
+        self.out.copy_((x0 + 1) / 2)
+
+    def capture(self):
+        s = torch.cuda.Stream(self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        self.x_in.normal_()
+        with torch.cuda.stream(s):
+            self._body()
+        torch.cuda.current_stream(self.dev).wait_stream(s)
+        torch.cuda.synchronize(self.dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._body()
+        self.graph = g
+
+    @torch.no_grad()
+    def sample(self, generator=None) -> torch.Tensor:
+        self.x_in.normal_(generator=generator)
+        if self.use_graph:
+            if self.graph is None:
+                self.capture()
+            self.graph.replay()
+        else:
+            self._body()
+        return self.out.cpu()
+
+
+def time_vendor_train(model, pool, batch: int, lr: float, t_max: int, steps: int = 50, warmup: int = 10,
+                      attn: str = "sdpa"):
+    """(seconds per step, final loss, optimizer kind) of the graph-captured vendor step."""
+    v = VendorTrainStep(model, pool, batch, lr, t_max, attn=attn)
+    v.steps(warmup)
+    torch.cuda.synchronize(v.dev)
+    t0 = time.perf_counter()
+    v.steps(steps)
+    torch.cuda.synchronize(v.dev)
+    dt = (time.perf_counter() - t0) / steps
+    return dt, float(v.loss.item()), v.optimizer_kind
+
+
+def time_vendor_sampler(model, N: int, k: int, reps: int = 5, attn: str = "sdpa") -> float:
+    """Seconds per N-image batch of the graph-captured vendor DDIM sampler."""
+    was = model.training
+    try:
+        s = VendorSampler(model, N, k, attn=attn)
+        g = torch.Generator(device=s.dev).manual_seed(0)
+        s.sample(g)  # capture
+        torch.cuda.synchronize(s.dev)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            s.sample(g)
+        torch.cuda.synchronize(s.dev)
+        return (time.perf_counter() - t0) / reps
+    finally:
+        model.train(was)

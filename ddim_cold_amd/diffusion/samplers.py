@@ -358,6 +358,9 @@ class ColdSampler:
         return [(init + 1) / 2] + [traj[i] for i in range(traj.shape[0])]
 
 
+IMG2IMG_GRAPHS = 8  # cached img2img loops (graph + buffers) per model
+
+
 def starts_table(total_steps: int, starts: Sequence[int], k: int):
     """(descending grid ts, [len(ts), B, 4] per-sample DDIM coefficients) for samples
     joining one k-grid at their own start steps; a sample whose start is below
@@ -383,7 +386,10 @@ def ddim_from_starts(model, x: torch.Tensor, starts: Sequence[int], k: int, devi
     whose head epilogue applies the update with per-sample coefficients
     (:func:`ops.head_step_` mode 4: not-yet-started samples get the identity row),
     and the whole loop is one hipGraph, cached per (B, starts, k): a repeated
-    call is one replay.  Returns the final clamped x0-hat on the device, in [-1, 1].
+    call is one replay (at most ``IMG2IMG_GRAPHS`` such loops stay cached per model,
+    least recently used evicted).  Returns the final clamped x0-hat on the device,
+    in [-1, 1], as a fresh tensor (not the graph's output buffer, which the next call
+    with the same key overwrites).
     """
     device = torch.device(device) if device is not None else x.device
     T = model.total_steps
@@ -391,8 +397,13 @@ def ddim_from_starts(model, x: torch.Tensor, starts: Sequence[int], k: int, devi
     starts = [int(s) for s in starts]
     key = ("img2img", B, tuple(starts), k, str(device))
     cache = _cache(model)
-    st = cache.get(key)
+    st = cache.pop(key, None)
+    if st is not None:
+        cache[key] = st  # most recently used last
     if st is None or st["key"] != _Denoiser.key_of(model):
+        cached = [c for c in cache if isinstance(c, tuple) and c[0] == "img2img"]
+        for old in cached[:max(0, len(cached) - IMG2IMG_GRAPHS + 1)]:
+            del cache[old]
         den = _Denoiser(model, device)
         ts, coef = starts_table(T, starts, k)
         coef = coef.to(device)
@@ -417,7 +428,7 @@ def ddim_from_starts(model, x: torch.Tensor, starts: Sequence[int], k: int, devi
         cache[key] = st
     st["x"].copy_(x.to(device).float())
     st["loop"].run(use_graph and device.type == "cuda")
-    return st["x0"]
+    return st["x0"].clone()
 
 
 @torch.no_grad()

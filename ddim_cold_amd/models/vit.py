@@ -202,8 +202,11 @@ class DiffusionVisionTransformer(nn.Module):
     def __init__(self, img_size=(64, 64), patch_size=8, in_chans=3, embed_dim=256, depth=3,
                  num_heads=4, mlp_ratio=1.0, qkv_bias=True, qk_scale=None, drop_rate=0.1,
                  attn_drop_rate=0.1, drop_path_rate=0.1, norm_layer=nn.LayerNorm,
-                 emb=PatchEmbed, total_steps=2000, timestep_embedding: str = "learned", **kwargs):
+                 emb=PatchEmbed, total_steps=2000, timestep_embedding: str = "learned",
+                 init_order: str = "draft2drawing", **kwargs):
         super().__init__()
+        if init_order not in ("draft2drawing", "vit"):
+            raise ValueError(f"init_order must be 'draft2drawing' or 'vit', got {init_order!r}")
         img_size = list(img_size)
         self.num_features = self.embed_dim = embed_dim
         self.patch_size = patch_size
@@ -226,6 +229,11 @@ class DiffusionVisionTransformer(nn.Module):
         self.cls_token = nn.Parameter(torch.zeros(1, 1, embed_dim))
         self.time_embed = nn.Embedding(total_steps, embed_dim)
         self.pos_embed = nn.Parameter(torch.zeros(1, num_patches + 1, embed_dim))
+        # RNG draw order: the trainer's model class (ViT_draft2drawing.py:194-195, imported by
+        # multi_gpu_trainer.py:6) draws pos_embed before the blocks are built; ViT.py:184 after
+        # the head.  Same seed => same initial weights as the chosen reference class.
+        if init_order == "draft2drawing":
+            trunc_normal_(self.pos_embed, std=0.02)
         self.pos_drop = nn.Dropout(p=drop_rate)
         dpr = [float(v) for v in torch.linspace(0, drop_path_rate, depth)]
         self.blocks = nn.ModuleList([
@@ -235,7 +243,8 @@ class DiffusionVisionTransformer(nn.Module):
             for i in range(depth)])
         self.norm = norm_layer(embed_dim)
         self.head = nn.Linear(embed_dim, in_chans * patch_size ** 2)
-        trunc_normal_(self.pos_embed, std=0.02)
+        if init_order == "vit":
+            trunc_normal_(self.pos_embed, std=0.02)
         trunc_normal_(self.cls_token, std=0.02)
         trunc_normal_(self.time_embed.weight, std=0.02)
         self.apply(self._init_weights)

@@ -92,9 +92,9 @@ def fit_allreduce(world: int, sizes: Sequence[float], times_us: Sequence[float])
     slope = sxy / sxx if sxx > 0 else 0.0
     alpha = my - slope * mx
     if alpha < 0 or slope <= 0:  # noisy small sizes: bandwidth-only fit through the largest
-        alpha = 0.0 if alpha < 0 or slope <= 0 else alpha
+        alpha = 0.0
         i = max(range(n), key=lambda j: sizes[j])
-        slope = max(times_us[i] - alpha, 1e-9) / sizes[i]
+        slope = max(times_us[i], 1e-9) / sizes[i]
     return AllReduceModel(world, alpha, 1.0 / slope / 1e3)
 
 
@@ -106,8 +106,8 @@ class StepProfile:
     deferred to the bucket's launch); ``block_wgrad_us``: that block's share of the
     weight-gradient launch; ``bucket_overhead_us``: fixed cost of one more bucket
     (its own weight-gradient launch + counter bump + hand-off, ~13 us at one rank);
-    ``tail_us``: embedding backward after block 0; ``block_bytes`` / ``embed_bytes``:
-    gradient bytes on the wire (fp32: 4 per parameter, bf16 wire: 2)."""
+    ``tail_us``: embedding backward after block 0; ``block_bytes`` / ``embed_bytes`` /
+    ``head_bytes``: gradient bytes on the wire (fp32: 4 per parameter, bf16 wire: 2)."""
     depth: int
     block_bwd_us: float
     block_wgrad_us: float
@@ -115,25 +115,47 @@ class StepProfile:
     tail_us: float
     block_bytes: float
     embed_bytes: float
+    head_bytes: float = 0.0  # the head Linear: reduced with the LAST block's bucket (first in backward order)
 
 
 # ViT-tiny B=32 single-process step (profiles/graph_step_table_r3.txt): ~45 us of
 # input-gradient kernels per block, 54.5 us for the step's weight-gradient GEMMs
 # (7.8 us per block), 9.4 us embedding backward; ~13 us per extra bucket
 # (profiles/dp/bucket_overhead_r3.txt: 1-rank RCCL step with 2 / 3 / 4 / 8 buckets)
-_TINY_BLOCK_WORK = 2080 * 888_576  # tokens x block parameters of that measurement
+_TINY_BLOCK_WORK = 2080 * 887_040  # tokens x block (Linear) parameters of that measurement
 
 
 def vit_step_profile(depth: int, dim: int, hidden: int, batch_tokens: int, other_params: int,
                      wire_bytes: int = 4, block_bwd_us: float = 45.0, block_wgrad_us: float = 7.8,
                      tail_us: float = 9.4, bucket_overhead_us: float = 13.0) -> StepProfile:
     """StepProfile from the model shape: the measured ViT-tiny constants, scaled by
-    GEMM work (tokens x block parameters) above the per-block launch floor."""
-    block_params = 3 * dim * dim + 3 * dim + dim * dim + dim + 2 * dim * hidden + hidden + dim + 4 * dim
+    GEMM work (tokens x block parameters) above the per-block launch floor.  A
+    block's gradient bytes are its four Linears only: the engine's arena keeps every
+    LayerNorm next to the embeddings, i.e. in the last bucket (``other_params``)."""
+    block_params = 3 * dim * dim + 3 * dim + dim * dim + dim + 2 * dim * hidden + hidden + dim
     r = max(1.0, batch_tokens * block_params / _TINY_BLOCK_WORK)
     return StepProfile(depth=depth, block_bwd_us=block_bwd_us * r, block_wgrad_us=block_wgrad_us * r,
                        bucket_overhead_us=bucket_overhead_us, tail_us=tail_us * r,
                        block_bytes=float(block_params * wire_bytes), embed_bytes=float(other_params * wire_bytes))
+
+
+def bucket_plan(prof: StepProfile, bucket_blocks: int, embed_bucket: bool = True) -> List[Tuple[int, float]]:
+    """(blocks, wire bytes) per bucket in backward order -- the layout
+    ``TrainEngine._build_buckets`` makes: ``bucket_blocks`` blocks per bucket from
+    the last block down (the head with the first of them), the embeddings + every
+    LayerNorm (``embed_bytes``) in a last
+    bucket of their own when ``embed_bucket`` else with block 0's bucket."""
+    out = []
+    left = prof.depth
+    while left > 0:
+        k = min(bucket_blocks, left)
+        left -= k
+        out.append([k, k * prof.block_bytes + (prof.head_bytes if not out else 0.0)])
+    if embed_bucket:
+        out.append([0, prof.embed_bytes])
+    else:
+        out[-1][1] += prof.embed_bytes
+    return [(k, b) for k, b in out]
 
 
 def simulate_step(prof: StepProfile, model: AllReduceModel, bucket_blocks: int, embed_bucket: bool = True,
@@ -145,7 +167,7 @@ def simulate_step(prof: StepProfile, model: AllReduceModel, bucket_blocks: int, 
     order, the embeddings (+ LayerNorms) in their own last bucket when
     ``embed_bucket``, else with block 0's bucket."""
     L = prof.depth
-    total = L * prof.block_bytes + prof.embed_bytes
+    total = L * prof.block_bytes + prof.embed_bytes + prof.head_bytes
     bwd_end = L * (prof.block_bwd_us + prof.block_wgrad_us) + prof.tail_us
     if inline or model.world <= 1:
         comm = model.time_us(total)
@@ -153,27 +175,15 @@ def simulate_step(prof: StepProfile, model: AllReduceModel, bucket_blocks: int, 
     t = 0.0
     q = 0.0  # comm queue free at
     comm_sum = 0.0
-    nb = 0
-    blocks_left = L
-    while blocks_left > 0:
-        k = min(bucket_blocks, blocks_left)
-        blocks_left -= k
+    sizes = bucket_plan(prof, bucket_blocks, embed_bucket)
+    for j, (k, nbytes) in enumerate(sizes):
         t += k * (prof.block_bwd_us + prof.block_wgrad_us) + prof.bucket_overhead_us
-        nbytes = k * prof.block_bytes
-        if blocks_left == 0:
-            if not embed_bucket:
-                t += prof.tail_us
-                nbytes += prof.embed_bytes
+        if j == len(sizes) - 1:
+            t += prof.tail_us  # the embedding backward precedes the last bucket
         c = model.time_us(nbytes)
         q = max(q, t) + c
         comm_sum += c
-        nb += 1
-    if embed_bucket:
-        t += prof.tail_us + prof.bucket_overhead_us
-        c = model.time_us(prof.embed_bytes)
-        q = max(q, t) + c
-        comm_sum += c
-        nb += 1
+    nb = len(sizes)
     # the step's own backward grew by the bucket launches; the optimizer waits for q
     exposed = max(q, t) - bwd_end
     return {"exposed_us": exposed, "comm_us": comm_sum, "buckets": nb, "bwd_us": bwd_end}
@@ -198,7 +208,7 @@ def describe(prof: StepProfile, worlds: Sequence[int] = (2, 4, 8), **model_kw) -
     """Markdown table of the a-priori model over world sizes (for profiles/)."""
     lines = ["| N | algbw GB/s | alpha us | all-reduce of all grads us | best layout | exposed us | "
              "inline exposed us |", "|---:|---:|---:|---:|---|---:|---:|"]
-    total = prof.depth * prof.block_bytes + prof.embed_bytes
+    total = prof.depth * prof.block_bytes + prof.embed_bytes + prof.head_bytes
     for n in worlds:
         m = xgmi_ring_model(n, **model_kw)
         plan = plan_buckets(prof, m)

@@ -702,7 +702,9 @@ class TrainEngine:
         xb = getattr(self.batch_fn, "x_t", None)
         B = int(xb.shape[0]) if isinstance(xb, torch.Tensor) else 32
         prof = cm.vit_step_profile(c.depth, c.dim, hidden, B * c.tokens, 0, wire_bytes=wire)
-        other = max(0.0, self.reduced_numel() - c.depth * prof.block_bytes / wire)
+        head = sum(self.offsets[n][1] for n in ("head.weight", "head.bias") if n in self.offsets)
+        prof.head_bytes = float(head * wire)
+        other = max(0.0, self.reduced_numel() - c.depth * prof.block_bytes / wire - head)
         prof.embed_bytes = float(other * wire)
         return prof
 
@@ -892,13 +894,11 @@ class TrainEngine:
                     self._join_comm()
 
     def _capture_impl(self, graph_comm: bool, events: bool = False):
-        from ..utils.observe import no_gc
+        from ..utils.observe import drain_before_capture, no_gc
         if self.dist_on and self.is_cuda:
-            # let the eager collectives of the warm-up finish and the process-group
-            # watchdog drop them (it polls every ~100 ms) before the capture opens
-            import time
-            torch.cuda.synchronize(self.device)
-            time.sleep(0.3)
+            # the warm-up's eager collectives finished on every rank (and dropped by
+            # the process-group watchdog) before the capture opens
+            drain_before_capture(self.device)
         with no_gc():
             if events:
                 self._capture_event_graphs()

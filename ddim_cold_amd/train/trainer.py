@@ -115,7 +115,7 @@ def evaluate(model, engine: TrainEngine, pool: torch.Tensor, idx: torch.Tensor, 
         cache = engine.__dict__.setdefault("_eval_graphs", {})
         ent = cache.get(key)
         if ent is None:
-            from ..utils.observe import no_gc
+            from ..utils.observe import drain_before_capture, is_capture_error, no_gc
             bidx = torch.zeros(batch, dtype=torch.int64, device=dev)
             acc = torch.zeros(1, dtype=torch.float64, device=dev)
             src = make_batcher(kind, pool, batch, eval_rng, total_steps, idx=bidx)
@@ -126,21 +126,21 @@ def evaluate(model, engine: TrainEngine, pool: torch.Tensor, idx: torch.Tensor, 
             with torch.cuda.stream(s):  # warm-up (allocator, kernels)
                 _eval_batch(prog, P, src, eval_rng, acc)
             torch.cuda.current_stream(dev).wait_stream(s)
-            # same capture discipline as the step graphs (engine.CAPTURE_MODE): drain the
-            # device and let the process-group watchdog drop the finished eager
-            # collectives first, capture thread-local; if the capture still fails,
-            # evaluate eagerly (same values, more launches)
-            torch.cuda.synchronize(dev)
-            if dist.is_available() and dist.is_initialized():
-                time.sleep(0.3)
+            # same capture discipline as the step graphs (engine.CAPTURE_MODE): quiesce
+            # (drain_before_capture), capture thread-local; if the CAPTURE fails,
+            # evaluate eagerly for the rest of the run (same values, more launches) and
+            # say why once; any other error propagates
+            drain_before_capture(dev)
             g = torch.cuda.CUDAGraph()
             try:
                 with no_gc(), torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
                     _eval_batch(prog, P, src, eval_rng, acc)
                 ent = (g, bidx, acc)
             except Exception as e:  # pragma: no cover - depends on the runtime
+                if not is_capture_error(e):
+                    raise
                 import warnings
-                warnings.warn(f"eval graph capture failed ({e!r}); evaluating eagerly")
+                warnings.warn(f"eval graph capture failed ({e!r}); evaluating eagerly for the rest of the run")
                 torch.cuda.synchronize(dev)
                 ent = (None, bidx, acc)
             eval_rng.copy_(saved)  # warm-up and capture leave the counters where they were

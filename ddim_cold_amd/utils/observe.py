@@ -127,3 +127,34 @@ def no_gc():
     finally:
         if was:
             gc.enable()
+
+
+def drain_before_capture(device) -> None:
+    """Quiesce before a hipGraph capture that follows eager collectives.
+
+    1. ``synchronize``: every eager kernel and collective of this rank has finished.
+    2. With a process group: a barrier, so every rank has too (no peer is still
+       inside a collective this rank's capture would wait behind).
+    3. One watchdog period (ProcessGroupNCCL polls its pending work every ~100 ms):
+       the finished works are then dropped instead of being queried while the
+       capture is open.  The capture itself is thread-local (``CAPTURE_MODE``), so a
+       late watchdog query can no longer invalidate it -- the wait only keeps the
+       watchdog's event queries and the capture apart, it is not what makes the
+       capture correct.
+    """
+    import time
+    from ..parallel.dist import barrier
+    if device is not None and torch.device(device).type == "cuda":
+        torch.cuda.synchronize(device)
+    if dist.is_available() and dist.is_initialized():
+        barrier()
+        if device is not None and torch.device(device).type == "cuda":
+            torch.cuda.synchronize(device)
+        time.sleep(0.15)
+
+
+def is_capture_error(e: BaseException) -> bool:
+    """A failure of the graph capture itself (an op illegal during capture, an
+    invalidated capture) -- as opposed to an error in the captured work."""
+    msg = str(e).lower()
+    return isinstance(e, RuntimeError) and any(s in msg for s in ("captur", "graph", "operation not permitted"))

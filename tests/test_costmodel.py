@@ -73,8 +73,15 @@ def test_engine_layout_names_and_model_candidates():
     eng = TrainEngine(build_model("vit_tiny"), EngineConfig(lr=1e-3, t_max=10, temb_rows=7, use_graph=False),
                       device="cpu")
     prof = eng.step_profile()
-    assert prof.block_bytes == 4 * 888_576
-    assert 7 * prof.block_bytes + prof.embed_bytes == pytest.approx(4 * eng.reduced_numel())
+    assert prof.block_bytes == 4 * 887_040  # the four Linears; LayerNorms sit in the last bucket
+    assert 7 * prof.block_bytes + prof.embed_bytes + prof.head_bytes == pytest.approx(4 * eng.reduced_numel())
+    # the simulator's per-bucket bytes are the engine's own bucket ranges, for every layout
+    for bb in (1, 2, 3, 4, 7):
+        for eb in (True, False):
+            eng.set_comm_layout(bb, eb)
+            got = [4 * sum(b - a for a, b in rs) for rs in eng.bucket_ranges]
+            want = [nb for _, nb in cm.bucket_plan(prof, bb, eb)]
+            assert got == pytest.approx(want), (bb, eb)
     eng.world = 2
     cands = eng.candidate_layouts()
     assert {L[0] for L in TrainEngine.COMM_LAYOUTS} <= {L[0] for L in cands}

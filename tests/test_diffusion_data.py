@@ -231,6 +231,22 @@ def test_starts_table_identity_rows_and_cache(tiny):
     assert sum(1 for k in tiny.__dict__["_sampler_graphs"] if k[0] == "img2img") == 1
 
 
+def test_ddim_from_starts_result_not_aliased_and_cache_capped(tiny):
+    """The returned x0-hat is the caller's own tensor (a later call with the same key
+    does not overwrite it), and at most IMG2IMG_GRAPHS img2img loops stay cached."""
+    from ddim_cold_amd.diffusion import samplers as smp
+    x1 = torch.randn(2, 3, 16, 16, generator=torch.Generator().manual_seed(5))
+    x2 = torch.randn(2, 3, 16, 16, generator=torch.Generator().manual_seed(6))
+    a = smp.ddim_from_starts(tiny, x1, [1599, 1999], 400)
+    a_copy = a.clone()
+    b = smp.ddim_from_starts(tiny, x2, [1599, 1999], 400)
+    assert torch.equal(a, a_copy) and not torch.equal(a, b)
+    for i in range(smp.IMG2IMG_GRAPHS + 3):  # distinct keys
+        smp.ddim_from_starts(tiny, x1, [1999 - 100 * i, 1999], 100)
+    n = sum(1 for k in tiny.__dict__["_sampler_graphs"] if k[0] == "img2img")
+    assert n <= smp.IMG2IMG_GRAPHS
+
+
 def test_slerp_and_interpolate(tiny):
     from ddim_cold_amd.diffusion.interpolate import interpolate, slerp
     a, b = torch.randn(1, 3, 4, 4), torch.randn(1, 3, 4, 4)

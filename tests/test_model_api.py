@@ -225,3 +225,71 @@ def test_layernorm_fold_reference_identity():
     # the fold multiplies bf16-rounded (gamma o W); compare against that rounding
     assert (y - expect).abs().max() < 0.05 * expect.abs().max()
     torch.testing.assert_close(mean, x.mean(-1), rtol=1e-5, atol=1e-5)
+
+
+def _reference_draw_order_state(seed, order, img=16, p=4, D=32, depth=2, H=4, T=2000):
+    """Independent replay of the reference constructors' RNG draws (no model class of
+    ours): ViT_draft2drawing.py:186-207 (order 'draft2drawing': pos_embed drawn right
+    after it is created, before the blocks) vs ViT.py:169-187 (order 'vit': after head)."""
+    import torch.nn as nn
+    torch.manual_seed(seed)
+    proj = nn.Conv2d(3, D, kernel_size=p, stride=p)          # PatchEmbed (default init draws)
+    cls = torch.zeros(1, 1, D)
+    temb = nn.Embedding(T, D)                                  # normal_ init draw
+    pos = torch.zeros(1, (img // p) ** 2 + 1, D)
+    if order == "draft2drawing":
+        nn.init.trunc_normal_(pos, std=0.02)
+    blocks = []
+    for _ in range(depth):                                     # Block: LN, qkv, proj, LN, fc1, fc2
+        blocks.append([nn.LayerNorm(D), nn.Linear(D, 3 * D), nn.Linear(D, D), nn.LayerNorm(D),
+                       nn.Linear(D, D), nn.Linear(D, D)])
+    norm = nn.LayerNorm(D)
+    head = nn.Linear(D, 3 * p * p)
+    if order == "vit":
+        nn.init.trunc_normal_(pos, std=0.02)
+    nn.init.trunc_normal_(cls, std=0.02)
+    nn.init.trunc_normal_(temb.weight, std=0.02)
+    # Module.apply: children first, in registration order; Linear -> trunc_normal_ + zero bias
+    for blk in blocks:
+        for m in blk:
+            if isinstance(m, nn.Linear):
+                nn.init.trunc_normal_(m.weight, std=0.02)
+                nn.init.zeros_(m.bias)
+    nn.init.trunc_normal_(head.weight, std=0.02)
+    nn.init.zeros_(head.bias)
+    sd = {"cls_token": cls, "pos_embed": pos, "patch_embed.proj.weight": proj.weight,
+          "patch_embed.proj.bias": proj.bias, "time_embed.weight": temb.weight}
+    names = ["norm1", "attn.qkv", "attn.proj", "norm2", "mlp.fc1", "mlp.fc2"]
+    for i, blk in enumerate(blocks):
+        for n, m in zip(names, blk):
+            sd[f"blocks.{i}.{n}.weight"] = m.weight
+            sd[f"blocks.{i}.{n}.bias"] = m.bias
+    sd.update({"norm.weight": norm.weight, "norm.bias": norm.bias, "head.weight": head.weight,
+               "head.bias": head.bias})
+    return {k: v.detach() for k, v in sd.items()}
+
+
+@pytest.mark.parametrize("order", ["draft2drawing", "vit"])
+def test_init_draw_order_matches_reference_classes(order):
+    from ddim_cold_amd.models.vit import DiffusionVisionTransformer
+    ref = _reference_draw_order_state(11, order)
+    torch.manual_seed(11)
+    m = DiffusionVisionTransformer(img_size=[16, 16], patch_size=4, embed_dim=32, depth=2, num_heads=4,
+                                   init_order=order)
+    sd = m.state_dict()
+    assert list(sd) == list(ref)
+    for k in ref:
+        assert torch.equal(sd[k], ref[k]), k
+
+
+def test_init_order_default_is_trainer_class():
+    from ddim_cold_amd.models.vit import DiffusionVisionTransformer
+    torch.manual_seed(2)
+    a = DiffusionVisionTransformer(img_size=[16, 16], patch_size=4, embed_dim=32, depth=2, num_heads=4)
+    torch.manual_seed(2)
+    b = DiffusionVisionTransformer(img_size=[16, 16], patch_size=4, embed_dim=32, depth=2, num_heads=4,
+                                   init_order="draft2drawing")
+    assert all(torch.equal(x, y) for x, y in zip(a.state_dict().values(), b.state_dict().values()))
+    with pytest.raises(ValueError):
+        DiffusionVisionTransformer(img_size=[16, 16], patch_size=4, embed_dim=32, depth=2, num_heads=4,
+                                   init_order="x")

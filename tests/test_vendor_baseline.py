@@ -1,0 +1,86 @@
+"""The same-node vendor comparators (ddim_cold_amd/bench/vendor_baseline.py):
+CPU plumbing checks of the code the GPU bench captures into one graph, and a
+GPU run of both graphs."""
+import math
+
+import pytest
+import torch
+
+from ddim_cold_amd.bench.eager_sampler import eager_ddim_sample
+from ddim_cold_amd.bench.vendor_baseline import (VendorSampler, VendorTrainStep, cold_batch_torch,
+                                                 vendor_forward)
+from ddim_cold_amd.models.vit import DiffusionVisionTransformer
+from ddim_cold_amd.ops.reference import pixelate
+
+
+def _tiny():
+    torch.manual_seed(0)
+    return DiffusionVisionTransformer(img_size=[16, 16], patch_size=4, embed_dim=32, depth=2, num_heads=4,
+                                      total_steps=2000)
+
+
+def test_sdpa_forward_matches_reference_eval():
+    m = _tiny().eval()
+    x = torch.randn(3, 3, 16, 16)
+    t = torch.tensor([1, 500, 1999])
+    with torch.no_grad():
+        a = vendor_forward(m, x, t, "sdpa")
+        b = m.forward_reference(x, t)
+    torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
+
+
+def test_cold_batch_torch_is_nearest_pixelation():
+    torch.manual_seed(3)
+    pool = torch.rand(10, 3, 64, 64) * 2 - 1
+    x_t, x_tm1, t = cold_batch_torch(pool, 16, 6)
+    assert t.min() >= 1 and t.max() <= 6
+    for b in range(16):
+        # identify the drawn image by its top-left pixel block at the finest level (t-1 >= 0)
+        s = int(t[b])
+        cand = [i for i in range(10) if torch.equal(pixelate(pool[i:i + 1], 2 ** (s - 1))[0], x_tm1[b])]
+        assert cand, "x_{t-1} is not a NEAREST pixelation of a pool image"
+        torch.testing.assert_close(x_t[b], pixelate(pool[cand[0]:cand[0] + 1], 2 ** s)[0], rtol=0, atol=0)
+
+
+def test_vendor_train_step_cpu_runs_and_follows_cosine():
+    m = _tiny()
+    pool = torch.rand(8, 3, 16, 16) * 2 - 1
+    before = [p.detach().clone() for p in m.parameters()]
+    v = VendorTrainStep(m, pool, batch=4, lr=1e-3, t_max=10, use_graph=False)
+    v.steps(3)
+    assert math.isfinite(float(v.loss))
+    assert float(v.step_t) == 3
+    assert any(not torch.equal(a, b) for a, b in zip(before, m.parameters()))
+    # lr used by the 3rd step = cosine at step index 2
+    assert abs(v.opt.param_groups[0]["lr"] - 0.5e-3 * (1 + math.cos(math.pi * 2 / 10))) < 1e-12
+
+
+def test_vendor_sampler_cpu_matches_eager_loop():
+    m = _tiny().eval()
+    s = VendorSampler(m, N=2, k=500, use_graph=False)
+    g = torch.Generator().manual_seed(5)
+    out = s.sample(g)
+    ref = eager_ddim_sample(m, torch.device("cpu"), 500, 2, noise=s.x_in.clone())
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+    assert s.ts == [1999, 1499, 999, 499]
+
+
+@pytest.mark.gpu
+def test_vendor_graphs_gpu():
+    from ddim_cold_amd.bench.vendor_baseline import time_vendor_sampler, time_vendor_train
+    from ddim_cold_amd.data.synthetic import synthetic_pool
+    from ddim_cold_amd.models import build_model
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    m = build_model("vit_tiny").to(dev)
+    pool = synthetic_pool(64, (64, 64), seed=1, device=dev)
+    dt, loss, kind = time_vendor_train(m, pool, 32, 3.125e-4, 51200, steps=5, warmup=3)
+    assert dt > 0 and math.isfinite(loss)
+    # graph replay == eager body on the same model (one more step each; loss finite, params finite)
+    assert all(torch.isfinite(p).all() for p in m.parameters())
+    ts = time_vendor_sampler(m, 8, 200, reps=1)
+    assert ts > 0
+    s = VendorSampler(m, 4, 200)
+    out = s.sample(torch.Generator(device=dev).manual_seed(1))
+    assert out.shape == (4, 3, 64, 64) and torch.isfinite(out).all()
+    assert out.min() >= 0 and out.max() <= 1
