@@ -86,6 +86,7 @@ class ExperimentConfig:
     use_diff_step: bool = False   # True: the model's total_steps = diff_step (reference parses it but keeps 2000)
     sync_check_every: int = 0     # debug: cross-rank parameter checksum every N steps (0 = only after init)
     fault_inject_step: int = 0    # testing: raise after this many steps (after logging), to exercise resume
+    fault_inject_rank: int = -1   # testing: only this rank raises (-1: every rank) -- one dead rank mid-epoch
     perf_log: bool = True         # extra '# perf' lines (img/s, device ms/step) next to the reference lines
     comm_layout: Optional[str] = None  # data parallel: 'overlap-<blocks>' | 'inline-1' (skips comm_autotune)
     force_segments: bool = False  # testing: the data-parallel step (1-rank RCCL group, comm stream) at num_gpus 1

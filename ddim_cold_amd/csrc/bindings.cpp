@@ -271,6 +271,8 @@ void ln_stamps(c10::optional<Tensor> buf) {
   ln_set_stamps(p);
 }
 
+int64_t gemm_tile_override_op(int64_t cfg) { return gemm_set_tile_override((int)cfg); }
+
 int64_t attn_keep_words_op(int64_t B, int64_t H, int64_t N, int64_t hd) {
   return attn_keep_words((int)B, (int)H, (int)N, (int)hd);
 }
@@ -935,6 +937,7 @@ TORCH_LIBRARY(ddim_cold, m) {
         "float ln_eps=1e-5, Tensor(a!)? ln_mean=None, Tensor(b!)? ln_rstd=None) -> Tensor");
   m.def("attn_fwd(Tensor qkv, float scale, Tensor rng, int site, float p, Tensor? keep_out=None) -> (Tensor, Tensor)");
   m.def("attn_keep_words(int B, int H, int N, int hd) -> int", &attn_keep_words_op);
+  m.def("gemm_tile_override(int cfg) -> int", &gemm_tile_override_op);
   m.def("attn_stamps(Tensor? buf) -> ()", &attn_stamps);
   m.def("ln_stamps(Tensor? buf) -> ()", &ln_stamps);
   m.def("linear_residual_fwd(Tensor a, Tensor w, Tensor b, Tensor x, int N, Tensor rng, int site_drop, "

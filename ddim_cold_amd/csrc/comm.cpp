@@ -126,6 +126,20 @@ void comm_all_reduce_bf16_wire_(Tensor buf, Tensor scratch, int64_t h) {
   wire_unpack_launch(scratch.data_ptr(), buf.data_ptr<float>(), n, s);
 }
 
+// out[r * n : (r + 1) * n] = rank r's `in` (n = in.numel()), on the current stream
+// (the sparse time-embedding gradient exchange: (t, row) pairs of every rank)
+void comm_all_gather_(Tensor out, Tensor in, int64_t h) {
+  check_buf(out);
+  check_buf(in);
+  TORCH_CHECK(out.scalar_type() == in.scalar_type(), "all_gather: dtype mismatch");
+  int n = 0;
+  ncclComm_t c = get_comm(h);
+  NCCL_CHECK(ncclCommCount(c, &n));
+  TORCH_CHECK(out.numel() == in.numel() * n, "all_gather: out must hold world x in.numel() elements");
+  const c10::DeviceGuard guard(in.device());
+  NCCL_CHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), (size_t)in.numel(), nccl_dtype(in), c, cur_stream()));
+}
+
 void comm_broadcast_(Tensor buf, int64_t h, int64_t root) {
   check_buf(buf);
   const c10::DeviceGuard guard(buf.device());
@@ -246,6 +260,7 @@ TORCH_LIBRARY_FRAGMENT(ddim_cold, m) {
   m.def("comm_all_reduce_bf16_wire_(Tensor(a!) buf, Tensor(b!) scratch, int handle) -> ()",
         &comm_all_reduce_bf16_wire_);
   m.def("comm_broadcast_(Tensor(a!) buf, int handle, int root=0) -> ()", &comm_broadcast_);
+  m.def("comm_all_gather_(Tensor(a!) out, Tensor inp, int handle) -> ()", &comm_all_gather_);
   m.def("comm_info(int handle) -> (int, int)", &comm_info);
   m.def("comm_destroy(int handle) -> ()", &comm_destroy);
 }

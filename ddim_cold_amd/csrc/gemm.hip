@@ -31,6 +31,8 @@
 #include <cstdlib>
 #include <algorithm>
 #include <type_traits>
+#include <atomic>
+#include <stdexcept>
 
 namespace dc {
 
@@ -213,14 +215,17 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
 //   transposed operand    [64 k][64]    chunk' = chunk ^ (row & 6)   (tr-read conflict-free)
 template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EPI, int S>
 __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int tn, int kz) {
-  static_assert(WM * WN == 4, "4 waves");
+  constexpr int NW = WM * WN;
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  // HEADL reduces its loss partials over 4 waves (VecEpi::finish)
+  static_assert(NW == 4 || EPI != EPI_HEADL, "HEADL: 4 waves");
   static_assert(!AT || BM == 64 || BM == 128, "transposed A: BM 64 or 128 (two half images)");
   static_assert(!BT || BN == 64 || BN == 128, "transposed B: BN 64 or 128 (two half images)");
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
   constexpr bool PERM = AT || BT;
-  using OA = typename DmaOp<BM, AT>::type;
-  using OB = typename DmaOp<BN, BT>::type;
+  using OA = typename DmaOp<BM, AT, NW>::type;
+  using OB = typename DmaOp<BN, BT, NW>::type;
   constexpr int STAGE = OA::BYTES + OB::BYTES;
   constexpr int LPT = OA::PER_WAVE + OB::PER_WAVE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -387,7 +392,7 @@ __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int t
 }
 
 template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EPI, int S>
-__global__ __launch_bounds__(256) void gemm_dma_kernel(GemmParams p) {
+__global__ __launch_bounds__(64 * WM * WN) void gemm_dma_kernel(GemmParams p) {
   const int tiles_n = (p.N + BN - 1) / BN;
   const int tiles_m = (p.M + BM - 1) / BM;
   const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
@@ -405,12 +410,12 @@ static void launch_dma(GemmParams p, int splits, hipStream_t stream) {
   // allows 160 KiB / (4 x stage) workgroups per CU, a 3-stage ring 4/3 of that
   constexpr int stage = BM * 128 + BN * 128;
   constexpr int per_cu4 = (160 * 1024) / (4 * stage);
-  static const bool force_s4 = getenv_flag("DDIM_COLD_GEMM_S4");
-  if (tiles * splits > 256 * per_cu4 && p.ktiles_per_split <= 8 && !force_s4)
-    hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, WM, WN, AT, BT, EPI, 3>), dim3(tiles, 1, splits), dim3(256),
+  constexpr int threads = 64 * WM * WN;
+  if ((tiles * splits > 256 * per_cu4 && p.ktiles_per_split <= 8) || 4 * stage > 160 * 1024)
+    hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, WM, WN, AT, BT, EPI, 3>), dim3(tiles, 1, splits), dim3(threads),
                        3 * stage, stream, p);
   else
-    hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, WM, WN, AT, BT, EPI, 4>), dim3(tiles, 1, splits), dim3(256),
+    hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, WM, WN, AT, BT, EPI, 4>), dim3(tiles, 1, splits), dim3(threads),
                        4 * stage, stream, p);
 }
 
@@ -429,7 +434,36 @@ static void launch_cfg(GemmParams p, int splits, hipStream_t stream) {
 
 // (tag dispatch instead of `if constexpr`: hipcc 7.2 silently drops the host
 // stub of a kernel template first referenced inside an if-constexpr branch)
-// tile configs: 0 = 32x64, 1 = 64x64, 2 = 128x64, 3 = 128x128 (4 waves, 2x2)
+// tile configs: 0 = 32x64, 1 = 64x64, 2 = 128x64, 3 = 128x128 (4 waves, 2x2);
+// 4 = 256x128, 5 = 128x128 (8 waves, 4x2: 512-thread workgroups, for M >= BIG_M)
+constexpr int CFG_W8_256 = 4, CFG_W8_128 = 5;
+template <int EPI>
+struct Wide8 {  // epilogues with no 4-wave workgroup reduction (HEAD / HEADL sum loss partials over 4 waves)
+  static constexpr bool value = EPI == EPI_BF16 || EPI == EPI_F32 || EPI == EPI_QKV || EPI == EPI_RESID ||
+                                EPI == EPI_GELU || EPI == EPI_EMBED || EPI == EPI_DGELU;
+};
+template <bool AT, bool BT, int EPI, bool OK = EPI != EPI_DGELU>
+struct Big256 {
+  static void go(GemmParams p, int splits, hipStream_t stream) { launch_dma<256, 128, 4, 2, AT, BT, EPI>(p, splits, stream); }
+};
+template <bool AT, bool BT, int EPI>
+struct Big256<AT, BT, EPI, false> {
+  static void go(GemmParams, int, hipStream_t) {}
+};
+template <bool AT, bool BT, int EPI, bool OK = Wide8<EPI>::value>
+struct Launch8 {
+  static void go(GemmParams p, int splits, hipStream_t stream, int cfg) {
+    // DGELU at 256x128 spills (88 B/lane of scratch): its 256-row config is the 128-row one
+    if (cfg == CFG_W8_256 && EPI != EPI_DGELU) Big256<AT, BT, EPI>::go(p, splits, stream);
+    else launch_dma<128, 128, 4, 2, AT, BT, EPI>(p, splits, stream);
+  }
+};
+template <bool AT, bool BT, int EPI>
+struct Launch8<AT, BT, EPI, false> {
+  static void go(GemmParams, int, hipStream_t, int) {
+    throw std::runtime_error("gemm: 8-wave tiles are not built for this epilogue");
+  }
+};
 template <bool AT, bool BT, int EPI>
 struct DmaTiles {
   static void launch(GemmParams p, int splits, hipStream_t stream, int cfg) {
@@ -437,17 +471,19 @@ struct DmaTiles {
       case 0: launch_dma<32, 64, 2, 2, AT, BT, EPI>(p, splits, stream); break;
       case 1: launch_dma<64, 64, 2, 2, AT, BT, EPI>(p, splits, stream); break;
       case 2: launch_dma<128, 64, 2, 2, AT, BT, EPI>(p, splits, stream); break;
-      default: launch_dma<128, 128, 2, 2, AT, BT, EPI>(p, splits, stream); break;
+      case 3: launch_dma<128, 128, 2, 2, AT, BT, EPI>(p, splits, stream); break;
+      default: Launch8<AT, BT, EPI>::go(p, splits, stream, cfg); break;
     }
   }
 };
 template <int EPI>
-struct DmaTiles<false, true, EPI> {  // transposed B (dgrad): BN = 64
+struct DmaTiles<false, true, EPI> {  // transposed B (dgrad): BN = 64 (4 waves) or 128 (8 waves)
   static void launch(GemmParams p, int splits, hipStream_t stream, int cfg) {
     switch (cfg) {
       case 0: launch_dma<32, 64, 2, 2, false, true, EPI>(p, splits, stream); break;
       case 1: launch_dma<64, 64, 2, 2, false, true, EPI>(p, splits, stream); break;
-      default: launch_dma<128, 64, 2, 2, false, true, EPI>(p, splits, stream); break;
+      case 2: case 3: launch_dma<128, 64, 2, 2, false, true, EPI>(p, splits, stream); break;
+      default: Launch8<false, true, EPI>::go(p, splits, stream, cfg); break;
     }
   }
 };
@@ -458,57 +494,38 @@ struct DmaTiles<true, BT, EPI> {  // transposed A (wgrad): 64x64
   }
 };
 
-// Tile choice: 64x64 when that alone gives ~1 workgroup per CU, else 32x64.
-// A cost model "operand bytes per CU" (one CU ingests ~80 GB/s of operand tiles,
-// tools/ub_stream.hip) that picks 128x64 / 128x128 for the big shapes measured
-// SLOWER everywhere (qkv 2080x1152x384: 11.9 us at 128x128 vs 7.5 at 64x64;
-// train step -10%): more, smaller workgroups hide latency better than fewer
-// bytes help.  It stays available as DDIM_COLD_GEMM_TILE_MODEL=1, and
-// DDIM_COLD_GEMM_TILE=0..3 forces a tile.  The LDS-DMA ring needs K % 64 == 0
-// for k-contiguous operands (transposed operands get zero rows past K from the
-// buffer bounds check).
-static int forced_tile() {
-  static const int forced = [] {
-    const char* e = getenv("DDIM_COLD_GEMM_TILE");
-    return e ? atoi(e) : -1;
-  }();
-  return forced;
-}
-static int pick_tiles(int M, int N, int K, int splits, bool at, bool bt) {
-  const int forced = forced_tile();
-  static const bool model = getenv_flag("DDIM_COLD_GEMM_TILE_MODEL");
+// Tile choice.  M < BIG_M (ViT-tiny / sampler shapes, M = 2-4k): 64x64 when that
+// alone gives ~1 workgroup per CU, else 32x64.  A cost model "operand bytes per CU"
+// that picked 128x64 / 128x128 for the big shapes of those sizes measured SLOWER
+// everywhere (qkv 2080x1152x384: 11.9 us at 128x128 vs 7.5 at 64x64; train step
+// -10%): more, smaller workgroups hide latency better than fewer bytes help, and was
+// removed.  M >= BIG_M (vit_small_200: M = 20,032): 8-wave 256x128 tiles (4x the
+// MFMA work per operand byte of 64x64, one 144 KiB 3-stage ring per CU), for the
+// epilogues that support them (Wide8).  gemm_set_tile_override() forces a config
+// (tests and micro-benchmarks).  The LDS-DMA ring needs K % 64 == 0 for
+// k-contiguous operands (transposed operands get zero rows past K from the buffer
+// bounds check).
+constexpr int BIG_M = 16384;
+static std::atomic<int> g_tile_override{-1};
+static int pick_tiles(int M, int N, int K, int splits, bool at, bool bt, bool wide8) {
   if (at) return 1;
-  if (forced >= 0) return bt && forced > 2 ? 2 : forced;
-  if (!model) return ((M + 63) / 64) * ((N + 63) / 64) * splits >= 240 ? 1 : 0;
-  const int nk = ((K + 63) / 64 + splits - 1) / splits;
-  const int bms[4] = {32, 64, 128, 128}, bns[4] = {64, 64, 64, 128};
-  const int ncfg = bt ? 3 : 4;
-  int best = 0;
-  long long best_cost = -1, best_tiles = 0;
-  for (int c = 0; c < ncfg; ++c) {
-    const long long tiles = (long long)((M + bms[c] - 1) / bms[c]) * ((N + bns[c] - 1) / bns[c]) * splits;
-    const long long per_cu = (tiles + 255) / 256;
-    const long long cost = per_cu * (bms[c] + bns[c]) * 128LL * nk;
-    if (best_cost < 0 || cost < best_cost || (cost == best_cost && tiles > best_tiles)) {
-      best = c;
-      best_cost = cost;
-      best_tiles = tiles;
-    }
-  }
-  return best;
+  const int forced = g_tile_override.load(std::memory_order_relaxed);
+  if (forced >= 0) return bt && forced == 3 ? 2 : forced;
+  if (wide8 && M >= BIG_M) return CFG_W8_256;
+  return ((M + 63) / 64) * ((N + 63) / 64) * splits >= 240 ? 1 : 0;
 }
 
 template <bool AT, bool BT, int EPI>
 static void launch_auto(GemmParams p, int splits, hipStream_t stream) {
   const bool dma_ok = (AT || BT || p.K % 64 == 0) && (AT || p.K % 64 == 0) && !dma_disabled();
   if (dma_ok) {
-    int cfg = pick_tiles(p.M, p.N, p.K, splits, AT, BT);
+    int cfg = pick_tiles(p.M, p.N, p.K, splits, AT, BT, Wide8<EPI>::value);
     // the GELU epilogue (erf-GELU + dropout per element, two bf16 outputs) is the
     // heaviest in vector instructions: twice the waves of 32x64 tiles pay off on the
     // sampler shape (M=4160: 6.56 vs 7.14 us, tools/gpu_tile_sweep3.sh); the other
     // epilogues keep 64x64 there (QKV 11.45 vs 13.54, residual 6.65 vs 7.02)
     // the patch embedding likewise (sampler M=4,096: 7.83 vs 9.08 us, tools/ub_sampler_ends.py)
-    if ((EPI == EPI_GELU || EPI == EPI_EMBED) && cfg == 1 && forced_tile() < 0 &&
+    if ((EPI == EPI_GELU || EPI == EPI_EMBED) && cfg == 1 && g_tile_override.load(std::memory_order_relaxed) < 0 &&
         ((p.M + 31) / 32) * ((p.N + 63) / 64) <= 1024)
       cfg = 0;
     DmaTiles<AT, BT, EPI>::launch(p, splits, stream, cfg);
@@ -530,18 +547,26 @@ static void launch_auto(GemmParams p, int splits, hipStream_t stream) {
 #define DC_INST_DMA2(AT, BT, EPI) \
   DC_INST_DMA(64, AT, BT, EPI) DC_INST_DMA(32, AT, BT, EPI) DC_INST_DMA(128, AT, BT, EPI)
 #define DC_INST_DMA3(EPI) DC_INST_DMA2(false, false, EPI) DC_INST_DMAT(128, 128, false, false, EPI)
-DC_INST_DMA3(EPI_BF16)
-DC_INST_DMA3(EPI_F32)
-DC_INST_DMA3(EPI_QKV)
-DC_INST_DMA3(EPI_RESID)
-DC_INST_DMA3(EPI_GELU)
+// 8-wave tiles (4x2 waves): 256x128 and 128x128
+#define DC_INST_W8(AT, BT, EPI)                                                    \
+  template __global__ void gemm_dma_kernel<256, 128, 4, 2, AT, BT, EPI, 3>(GemmParams); \
+  template __global__ void gemm_dma_kernel<256, 128, 4, 2, AT, BT, EPI, 4>(GemmParams); \
+  template __global__ void gemm_dma_kernel<128, 128, 4, 2, AT, BT, EPI, 3>(GemmParams); \
+  template __global__ void gemm_dma_kernel<128, 128, 4, 2, AT, BT, EPI, 4>(GemmParams);
+DC_INST_DMA3(EPI_BF16) DC_INST_W8(false, false, EPI_BF16)
+DC_INST_DMA3(EPI_F32) DC_INST_W8(false, false, EPI_F32)
+DC_INST_DMA3(EPI_QKV) DC_INST_W8(false, false, EPI_QKV)
+DC_INST_DMA3(EPI_RESID) DC_INST_W8(false, false, EPI_RESID)
+DC_INST_DMA3(EPI_GELU) DC_INST_W8(false, false, EPI_GELU)
 DC_INST_DMA3(EPI_HEAD)
-DC_INST_DMA3(EPI_EMBED)
+DC_INST_DMA3(EPI_EMBED) DC_INST_W8(false, false, EPI_EMBED)
 DC_INST_DMA3(EPI_HEADR)
 DC_INST_DMA3(EPI_HEADL)
-DC_INST_DMA2(false, true, EPI_BF16)
-DC_INST_DMA2(false, true, EPI_F32)
+DC_INST_DMA2(false, true, EPI_BF16) DC_INST_W8(false, true, EPI_BF16)
+DC_INST_DMA2(false, true, EPI_F32) DC_INST_W8(false, true, EPI_F32)
 DC_INST_DMA2(false, true, EPI_DGELU)
+template __global__ void gemm_dma_kernel<128, 128, 4, 2, false, true, EPI_DGELU, 3>(GemmParams);
+template __global__ void gemm_dma_kernel<128, 128, 4, 2, false, true, EPI_DGELU, 4>(GemmParams);
 DC_INST_DMA(64, true, true, EPI_ATOMIC)
 
 // Whole-backward weight gradient: every dW += dy^T x of a training step (all
@@ -665,18 +690,24 @@ void gemm_nt(const GemmArgs& a, int epi, hipStream_t stream) {
 }
 
 int gemm_nt_grid(int M, int N, int K) {
-  // mirrors launch_auto<false, false, *> (one split)
+  // mirrors launch_auto<false, false, EPI> (one split) for the epilogues that size a
+  // per-workgroup buffer from it (HEAD / HEADL: never 8-wave tiles)
   const bool dma_ok = K % 64 == 0 && !dma_disabled();
   int bm = 64, bn = 64;
   if (dma_ok) {
-    const int cfg = pick_tiles(M, N, K, 1, false, false);
-    const int bms[4] = {32, 64, 128, 128}, bns[4] = {64, 64, 64, 128};
-    bm = bms[cfg < 0 ? 0 : (cfg > 3 ? 3 : cfg)];
-    bn = bns[cfg < 0 ? 0 : (cfg > 3 ? 3 : cfg)];
+    const int cfg = pick_tiles(M, N, K, 1, false, false, false);
+    const int bms[6] = {32, 64, 128, 128, 256, 128}, bns[6] = {64, 64, 64, 128, 128, 128};
+    bm = bms[cfg < 0 ? 0 : (cfg > 5 ? 5 : cfg)];
+    bn = bns[cfg < 0 ? 0 : (cfg > 5 ? 5 : cfg)];
   } else if (((M + 63) / 64) * ((N + 63) / 64) < 240) {
     bm = 32;
   }
   return ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+}
+
+int gemm_set_tile_override(int cfg) {
+  if (cfg < -1 || cfg > 5) throw std::runtime_error("gemm_set_tile_override: -1 (auto) or 0..5");
+  return g_tile_override.exchange(cfg);
 }
 
 void gemm_dgrad(const GemmArgs& a, int epi, hipStream_t stream) {

@@ -96,10 +96,12 @@ __device__ __forceinline__ bf16x8 frag_t_swz(const char* lds, int c0, int s, int
   return frag_t_fence(f);
 }
 
-template <int R, bool T>
+// NW: waves of the workgroup (4 or 8); each wave issues PER_WAVE 1-KiB pieces per K tile
+template <int R, bool T, int NW = 4>
 struct DmaOperand {
-  static constexpr int BYTES = R * 128;          // one 64-deep K tile
-  static constexpr int PER_WAVE = BYTES / 4096;  // 1-KiB pieces per wave
+  static constexpr int BYTES = R * 128;                // one 64-deep K tile
+  static constexpr int PER_WAVE = BYTES / (1024 * NW);  // 1-KiB pieces per wave
+  static_assert(PER_WAVE >= 1 && PER_WAVE * 1024 * NW == BYTES, "operand tile must split into whole pieces per wave");
   bf16* base;
   int nbytes;
   int voff[PER_WAVE];  // per-lane byte offset of piece j at k-tile 0
@@ -135,10 +137,11 @@ struct DmaOperand {
 
 // A transposed operand 128 columns wide is staged as TWO 64-column half images
 // (the transposed-read swizzle and the DMA piece map assume 128-B image rows).
+template <int NW = 4>
 struct DmaOperandT128 {
   static constexpr int BYTES = 2 * 64 * 128;  // one 64-deep K tile, both halves
-  static constexpr int PER_WAVE = 4;
-  DmaOperand<64, true> h0, h1;
+  static constexpr int PER_WAVE = 2 * DmaOperand<64, true, NW>::PER_WAVE;
+  DmaOperand<64, true, NW> h0, h1;
   __device__ __forceinline__ void init(const bf16* base, int ld, int rows_total, int row0, int wave, int lane) {
     h0.init(base, ld, rows_total, row0, wave, lane);
     h1.init(base, ld, rows_total, row0 + 64, wave, lane);
@@ -148,13 +151,13 @@ struct DmaOperandT128 {
     h1.issue(lds_tile + 64 * 128, kt, wave);
   }
 };
-template <int R, bool T>
+template <int R, bool T, int NW = 4>
 struct DmaOp {
-  using type = DmaOperand<R, T>;
+  using type = DmaOperand<R, T, NW>;
 };
-template <>
-struct DmaOp<128, true> {
-  using type = DmaOperandT128;
+template <int NW>
+struct DmaOp<128, true, NW> {
+  using type = DmaOperandT128<NW>;
 };
 // transposed fragment (operand columns c0..c0+15) of a [64 k][64]-per-half image
 __device__ __forceinline__ TrFrag frag_t_half(const char* lds, int c0, int s, int lane) {

@@ -76,6 +76,9 @@ struct GemmArgs {
 void gemm_nt(const GemmArgs& a, int epi, hipStream_t stream);
 // workgroups gemm_nt launches for an [M x N x K] problem (one split)
 int gemm_nt_grid(int M, int N, int K);
+// force a GEMM tile config for every later launch (-1 = automatic choice; 0..5, see
+// gemm.hip "tile configs"); returns the previous setting.  Tests / micro-benchmarks.
+int gemm_set_tile_override(int cfg);
 void gemm_dgrad(const GemmArgs& a, int epi, hipStream_t stream);
 void gemm_wgrad(const GemmArgs& a, int splits, hipStream_t stream);
 // every weight gradient of a step (n <= 32 problems) in one launch, unsplit (plain read-add-write)

@@ -115,6 +115,25 @@ def qkv_fwd(a, w, b, B: int, N: int, H: int, fold=None):
     return ref.qkv_fwd(a, w, b, B, N, H, st, c, eps, mean, rstd)
 
 
+class gemm_tile:
+    """Context manager forcing the GEMM tile config of every launch inside it
+    (csrc/gemm.hip: 0 = 32x64, 1 = 64x64, 2 = 128x64, 3 = 128x128 with 4 waves;
+    4 = 256x128, 5 = 128x128 with 8 waves; -1 = automatic).  Tests and
+    micro-benchmarks; the automatic choice is the production path."""
+
+    def __init__(self, cfg: int):
+        self.cfg = int(cfg)
+        self.prev = -1
+
+    def __enter__(self):
+        self.prev = int(_ops().gemm_tile_override(self.cfg))
+        return self
+
+    def __exit__(self, *exc):
+        _ops().gemm_tile_override(self.prev)
+        return False
+
+
 def attn_keep_buffer(qkv, p: float):
     """int32 buffer for the attention-dropout keep flags the short-sequence forward
     stores for its backward (one word per lane: no mask re-hashing there), or None

@@ -156,6 +156,10 @@ class NativeComm:
     def broadcast_(self, buf: torch.Tensor, root: int = 0):
         torch.ops.ddim_cold.comm_broadcast_(buf, self.handle, root)
 
+    def all_gather_(self, out: torch.Tensor, inp: torch.Tensor):
+        """``out`` = every rank's ``inp`` concatenated in rank order (ncclAllGather)."""
+        torch.ops.ddim_cold.comm_all_gather_(out, inp, self.handle)
+
     def info(self):
         """(ranks, my rank) as RCCL reports them (ncclCommCount / ncclCommUserRank)."""
         return tuple(int(v) for v in torch.ops.ddim_cold.comm_info(self.handle))

@@ -660,8 +660,12 @@ class TrainEngine:
         rows.mul_(first[:, None].to(rows.dtype))
         idx_all = idx.new_empty(self.world * n)
         rows_all = rows.new_empty(self.world * n, g.shape[1])
-        dist.all_gather_into_tensor(idx_all, idx, group=self.pg)
-        dist.all_gather_into_tensor(rows_all, rows, group=self.pg)
+        if self.ncomm is not None:  # every per-step collective on the one gradient communicator
+            self.ncomm.all_gather_(idx_all, idx)
+            self.ncomm.all_gather_(rows_all, rows)
+        else:
+            dist.all_gather_into_tensor(idx_all, idx, group=self.pg)
+            dist.all_gather_into_tensor(rows_all, rows, group=self.pg)
         same = (idx_all[:, None] == idx_all[None, :]).to(rows.dtype)
         g.index_copy_(0, idx_all, same @ rows_all)
 

@@ -288,8 +288,8 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
                                  f"(device, {world} rank(s)" +
                                  (f", comm {engine.comm_choice or 'default'}/{engine.handoff_order}"
                                   if engine.segmented else "") + ")", paths.log)
-            if cfg.fault_inject_step and steps >= cfg.fault_inject_step:
-                raise FaultInjected(f"fault injected at step {steps} (fault_inject_step)")
+            if cfg.fault_inject_step and steps >= cfg.fault_inject_step and cfg.fault_inject_rank in (-1, rank):
+                raise FaultInjected(f"fault injected at step {steps} on rank {rank} (fault_inject_step)")
         loss_rec = float(engine.loss_ema.item())
         engine.check_comm()  # epoch end: before evaluating / checkpointing these weights
         if (epoch - start_epoch + 1) % max(cfg.eval_every, 1) == 0 or epoch == end_epoch - 1:
@@ -348,15 +348,14 @@ def launch(cfg: ExperimentConfig, exp_name: str, paths: Paths, backend: Optional
     ctx = mp.get_context("spawn")
     port = pdist.free_port()
     q = ctx.Queue()
-    procs = [ctx.Process(target=_spawn_entry, args=(r, world, cfg, exp_name, paths, backend, port, q))
-             for r in range(world)]
+    procs = [ctx.Process(target=_spawn_entry, args=(r, world, cfg, exp_name, paths, backend, port, q),
+                         name=f"rank{r}") for r in range(world)]
     for p in procs:
         p.start()
     # drain the result queue WHILE the ranks run: a child cannot exit before its
     # queued result has been flushed into the pipe, so joining first could deadlock
     import queue as _queue
     per_rank = {}
-    failed = None
     while True:
         got = False
         try:
@@ -365,16 +364,17 @@ def launch(cfg: ExperimentConfig, exp_name: str, paths: Paths, backend: Optional
             got = True
         except _queue.Empty:
             pass
-        for p in procs:
-            if p.exitcode not in (None, 0) and failed is None:
-                failed = p
-        if failed is not None:
+        failed = [p for p in procs if p.exitcode not in (None, 0)]
+        if failed:
+            # every rank that has failed by now (the first to die usually takes its
+            # peers' collectives down with it), then stop the rest
+            msg = ", ".join(f"{p.name} (exit {p.exitcode})" for p in failed)
             for p in procs:
                 if p.is_alive():
                     p.terminate()
             for p in procs:
                 p.join()
-            raise RuntimeError(f"rank process {failed.name} exited with code {failed.exitcode}")
+            raise RuntimeError(f"rank process(es) failed: {msg}")
         if len(per_rank) == world or (not got and not any(p.is_alive() for p in procs)):
             break
     for p in procs:

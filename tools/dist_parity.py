@@ -66,6 +66,10 @@ if __name__ == "__main__":
     b = torch.arange(10, device="cuda")
     nc.broadcast_(b, 0)
     assert torch.equal(b, torch.arange(10, device="cuda"))
+    for src in (torch.arange(7, device="cuda"), torch.randn(5, 384, device="cuda")):
+        out = torch.empty_like(src)
+        nc.all_gather_(out, src)
+        assert torch.equal(out, src), "all_gather at 1 rank"
     nc.destroy()
     cap, loss1, failed, ng1 = run("captured")
     seg, loss2, _, ng2 = run("segmented")
@@ -78,6 +82,9 @@ if __name__ == "__main__":
     ev, loss5, _, ng5 = run("events")
     evn, loss6, _, ng6 = run("events", comm="native")
     gev, gl2, _, gng2 = run("events", gauss=True)
+    # the sparse time_embed exchange through the native communicator's all-gather
+    gevn, gl3, _, _ = run("events", comm="native", gauss=True)
+    gcapn, gl4, gfailedn, gngn = run("captured", comm="native", gauss=True)
     # one inline all-reduce between the graphs; the autotuned layout after its tuning steps
     evi, loss7, _, ng7 = run("events", layout="inline-1")
     evt, loss8, _, ng8 = run("events", tune=True)
@@ -87,6 +94,9 @@ if __name__ == "__main__":
     assert ng5 == 2 and ng6 == 2 and gng2 == 2, (ng5, ng6, gng2)
     assert (gref - gev).abs().max().item() <= 2 * 1e-3 * 6 and abs(gl2 - gl0) <= 1e-4 * abs(gl0), (gl0, gl2)
     assert not gfailed and gng == 1, "sparse time_embed exchange not captured"
+    assert not gfailedn and gngn == 1, "native sparse time_embed exchange not captured"
+    for other, gl in ((gevn, gl3), (gcapn, gl4)):
+        assert (gref - other).abs().max().item() <= 2 * 1e-3 * 6 and abs(gl - gl0) <= 1e-4 * abs(gl0), (gl0, gl)
     assert (gref - gcap).abs().max().item() <= 2 * 1e-3 * 6 and abs(gl1 - gl0) <= 1e-4 * abs(gl0), (gl0, gl1)
     print(f"losses {loss0:.6f} {loss1:.6f} {loss2:.6f} native {loss3:.6f} native-bf16 {loss4:.6f}; "
           f"graphs captured={ng1} segmented={ng2} native={ng3}/{ng4}; fallback={failed} {failed3} {failed4}")
