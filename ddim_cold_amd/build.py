@@ -67,15 +67,8 @@ def _flags(inc, abi, resource_usage=False):
 # (occupancy 3).  Whole-tree A/B on MI355X (tools/gpu_r3_attn.sh, 2 interleaved
 # 1000-step pairs): attention unit only 0.7982/0.8012 ms/step, every unit
 # 0.7939/0.7954, neither 0.8079/0.8041; sampler k=20 N=64 38.54 / 37.78 / 38.79 ms.
-# DDIM_COLD_VGPR_FORM=none|attention selects the older variants for A/Bs.
-VGPR_FORM_UNITS = {"attention.hip"}
-
-
 def _unit_flags(src, flags):
-    name = os.path.basename(src)
-    mode = os.environ.get("DDIM_COLD_VGPR_FORM", "all")
-    on = mode == "all" or (mode == "attention" and name in VGPR_FORM_UNITS)
-    return flags + (["-mllvm", "-amdgpu-mfma-vgpr-form"] if on and src.endswith(".hip") else [])
+    return flags + (["-mllvm", "-amdgpu-mfma-vgpr-form"] if src.endswith(".hip") else [])
 
 
 def _hash(path, flags):

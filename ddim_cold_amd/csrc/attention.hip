@@ -238,7 +238,7 @@ struct KvStage {  // one 64-row K tile + one 64-row V tile, register-staged
 template <int DT, bool DROP, bool MASK>
 __device__ __forceinline__ void flash_softmax_tile(f32x4 (&st)[4], f32x4 (&o)[DT], float& m_run, float& l_run,
                                                    int kv0, int N, int g, float sl2, uint32_t salt,
-                                                   uint32_t rowidx, uint32_t thr, float dsc) {
+                                                   uint32_t rowidx, uint32_t thr, float dsc, uint32_t& kbits) {
   float mt = -INFINITY;
 #pragma unroll
   for (int t = 0; t < 4; ++t)
@@ -270,6 +270,7 @@ __device__ __forceinline__ void flash_softmax_tile(f32x4 (&st)[4], f32x4 (&o)[DT
       float pv = fexp2(fmaf(st[t][r], sl2, nm));
       ls += pv;
       if (DROP) pv = kp[r] ? pv * dsc : 0.f;
+      if (DROP) kbits |= (uint32_t)kp[r] << (4 * t + r);
       st[t][r] = pv;
     }
   }
@@ -278,11 +279,43 @@ __device__ __forceinline__ void flash_softmax_tile(f32x4 (&st)[4], f32x4 (&o)[DT
   l_run += ls;
 }
 
+// Stored attention-dropout masks of the long-sequence kernels: one 64-bit word per
+// (b, h, 64-key tile, query), bit k = keep flag of key 64 * tile + k, as two uint32
+// halves: keep[((bh * ntiles + tile) * N + q) * 2 + (k >> 5)] bit (k & 31) -- tile
+// major, so the 16 queries of a wave-instruction store / load 128 contiguous bytes.
+// The forward writes them (a lane's 16 flags are the keys 16t + 4g + r of its query:
+// the 4 lanes g of a query OR their nibbles together), the two backward kernels
+// read them instead of re-hashing every mask element (dQ: the forward's lane layout;
+// dK/dV: the query tile's 64 words staged in LDS, one bit per lane's key).
+__device__ __forceinline__ uint32_t or_xor16(uint32_t u) {  // u | lane (l ^ 16)'s u
+  const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  return r[0] | r[1];
+}
+__device__ __forceinline__ uint32_t or_xor32(uint32_t u) {  // u | lane (l ^ 32)'s u
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return r[0] | r[1];
+}
+__device__ __forceinline__ void keep_store(uint32_t* __restrict__ keep, size_t word, uint32_t kbits, int g,
+                                           bool valid) {
+  const int sh = 4 * g;
+  uint32_t lo = ((kbits & 0xFu) << sh) | (((kbits >> 4) & 0xFu) << (16 + sh));
+  uint32_t hi = (((kbits >> 8) & 0xFu) << sh) | (((kbits >> 12) & 0xFu) << (16 + sh));
+  lo = or_xor32(or_xor16(lo));
+  hi = or_xor32(or_xor16(hi));
+  if (valid && g == 0) *reinterpret_cast<u32x2*>(keep + 2 * word) = u32x2{lo, hi};
+}
+// the 4 flags of keys 16t + 4g + r (r = 0..3) of a query from its tile word
+__device__ __forceinline__ void keep_nibble(const u32x2& w, int t, int g, bool (&kp)[4]) {
+  const uint32_t h = (t < 2 ? w[0] : w[1]) >> (16 * (t & 1) + 4 * g);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) kp[r] = (h >> r) & 1u;
+}
+
 template <int HD, bool DROP>
 __global__ __launch_bounds__(256) void attn_fwd_flash2_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                               float* __restrict__ lse, int B, int H, int N,
                                                               float scale, const int64_t* __restrict__ rng, int site,
-                                                              uint32_t thr, float dsc) {
+                                                              uint32_t thr, float dsc, uint32_t* __restrict__ keep) {
   using C = AC<HD>;
   __shared__ __attribute__((aligned(16))) char lds[4 * C::TILE];  // [buf][K | V]
   const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
@@ -337,9 +370,15 @@ __global__ __launch_bounds__(256) void attn_fwd_flash2_kernel(const bf16* __rest
       }
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < 2; ++u) {
+      uint32_t kbits = 0u;
       flash_softmax_tile<C::DT, DROP, MASK>(st[u], o[u], m_run[u], l_run[u], kv0, N, g, sl2, salt,
-                                            rowidx0 + u * rowstep + kv0, thr, dsc);
+                                            rowidx0 + u * rowstep + kv0, thr, dsc, kbits);
+      if (DROP && keep != nullptr) {
+        const int q = qbase + 16 * u + li;
+        keep_store(keep, ((size_t)bh * ntiles + it) * N + q, kbits, g, q < N);
+      }
+    }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       const bf16x8 pb0 = pack8(st[0][2 * s2], st[0][2 * s2 + 1]);
@@ -376,13 +415,13 @@ __global__ __launch_bounds__(256) void attn_fwd_flash2_kernel(const bf16* __rest
   }
 }
 template __global__ void attn_fwd_flash2_kernel<32, true>(const bf16*, bf16*, float*, int, int, int, float,
-                                                          const int64_t*, int, uint32_t, float);
+                                                          const int64_t*, int, uint32_t, float, uint32_t*);
 template __global__ void attn_fwd_flash2_kernel<32, false>(const bf16*, bf16*, float*, int, int, int, float,
-                                                           const int64_t*, int, uint32_t, float);
+                                                           const int64_t*, int, uint32_t, float, uint32_t*);
 template __global__ void attn_fwd_flash2_kernel<64, true>(const bf16*, bf16*, float*, int, int, int, float,
-                                                          const int64_t*, int, uint32_t, float);
+                                                          const int64_t*, int, uint32_t, float, uint32_t*);
 template __global__ void attn_fwd_flash2_kernel<64, false>(const bf16*, bf16*, float*, int, int, int, float,
-                                                           const int64_t*, int, uint32_t, float);
+                                                           const int64_t*, int, uint32_t, float, uint32_t*);
 
 // ============================================================================ forward, medium sequences
 // Resident-KV forward (128 < N <= 320, e.g. the 257-token OxfordFlower config):
@@ -395,7 +434,8 @@ template <int HD, bool DROP>
 __global__ __launch_bounds__(640) void attn_fwd_resident_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                                 float* __restrict__ lse, int B, int H, int N,
                                                                 float scale, const int64_t* __restrict__ rng,
-                                                                int site, uint32_t thr, float dsc) {
+                                                                int site, uint32_t thr, float dsc,
+                                                                uint32_t* __restrict__ keep) {
   using C = AC<HD>;
   extern __shared__ __attribute__((aligned(16))) char dyn[];
   const int NP = (N + 63) / 64 * 64;  // keys padded to whole 64-key chunks
@@ -453,6 +493,7 @@ __global__ __launch_bounds__(640) void attn_fwd_resident_kernel(const bf16* __re
   }
   const uint32_t rowidx0 = (uint32_t)(((size_t)bh * N + qbase + li) * attn_mask_ld(N));
   const uint32_t rowstep = (uint32_t)(16 * attn_mask_ld(N));
+  const int ntiles = (N + 63) / 64;
   auto chunk = [&](int kv0, auto mask_tag) {
     constexpr bool MASK = decltype(mask_tag)::value;
     const char* Kc = Kl + kv0 * C::S;
@@ -470,9 +511,15 @@ __global__ __launch_bounds__(640) void attn_fwd_resident_kernel(const bf16* __re
       }
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < 2; ++u) {
+      uint32_t kbits = 0u;
       flash_softmax_tile<C::DT, DROP, MASK>(st[u], o[u], m_run[u], l_run[u], kv0, N, g, sl2, salt,
-                                            rowidx0 + u * rowstep + kv0, thr, dsc);
+                                            rowidx0 + u * rowstep + kv0, thr, dsc, kbits);
+      if (DROP && keep != nullptr) {
+        const int q = qbase + 16 * u + li;
+        keep_store(keep, ((size_t)bh * ntiles + kv0 / 64) * N + q, kbits, g, q < N);
+      }
+    }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       const bf16x8 pb0 = pack8(st[0][2 * s2], st[0][2 * s2 + 1]);
@@ -507,17 +554,18 @@ __global__ __launch_bounds__(640) void attn_fwd_resident_kernel(const bf16* __re
   }
 }
 template __global__ void attn_fwd_resident_kernel<32, true>(const bf16*, bf16*, float*, int, int, int, float,
-                                                            const int64_t*, int, uint32_t, float);
+                                                            const int64_t*, int, uint32_t, float, uint32_t*);
 template __global__ void attn_fwd_resident_kernel<32, false>(const bf16*, bf16*, float*, int, int, int, float,
-                                                             const int64_t*, int, uint32_t, float);
+                                                             const int64_t*, int, uint32_t, float, uint32_t*);
 template __global__ void attn_fwd_resident_kernel<64, true>(const bf16*, bf16*, float*, int, int, int, float,
-                                                            const int64_t*, int, uint32_t, float);
+                                                            const int64_t*, int, uint32_t, float, uint32_t*);
 template __global__ void attn_fwd_resident_kernel<64, false>(const bf16*, bf16*, float*, int, int, int, float,
-                                                             const int64_t*, int, uint32_t, float);
+                                                             const int64_t*, int, uint32_t, float, uint32_t*);
 
 template <int HD>
 static void launch_resident(const bf16* q, bf16* out, float* lse, int B, int H, int N, float scale,
-                            const int64_t* rng, int site, uint32_t thr, float dsc, hipStream_t stream) {
+                            const int64_t* rng, int site, uint32_t thr, float dsc, hipStream_t stream,
+                            uint32_t* keep) {
   const int waves = (N + 31) / 32;
   const int NP = (N + 63) / 64 * 64;
   const int lds = 2 * NP * AC<HD>::S;
@@ -531,10 +579,10 @@ static void launch_resident(const bf16* q, bf16* out, float* lse, int B, int H, 
   (void)attr;
   if (thr)
     hipLaunchKernelGGL((attn_fwd_resident_kernel<HD, true>), dim3(B * H), dim3(64 * waves), lds, stream, q, out, lse,
-                       B, H, N, scale, rng, site, thr, dsc);
+                       B, H, N, scale, rng, site, thr, dsc, keep);
   else
     hipLaunchKernelGGL((attn_fwd_resident_kernel<HD, false>), dim3(B * H), dim3(64 * waves), lds, stream, q, out, lse,
-                       B, H, N, scale, rng, site, thr, dsc);
+                       B, H, N, scale, rng, site, thr, dsc, nullptr);
 }
 
 // ============================================================================ backward: dQ (+delta)
@@ -543,7 +591,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
                                                           const bf16* __restrict__ out, const float* __restrict__ lse,
                                                           float* __restrict__ delta, bf16* __restrict__ dqkv, int B,
                                                           int H, int N, float scale, const int64_t* __restrict__ rng,
-                                                          int site, uint32_t thr, float dsc) {
+                                                          int site, uint32_t thr, float dsc,
+                                                          const uint32_t* __restrict__ keep) {
   using C = AC<HD>;
   __shared__ __attribute__((aligned(16))) char lds[4 * C::TILE];  // [buf][K | V], double-buffered
   const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
@@ -597,11 +646,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
   const uint32_t pgq = ((rowidx >> 1) + 2u * (uint32_t)g) * DROP_GOLDEN;  // pair hash base of this lane's row
   // key mask only in the tail tile: a padded key has a zero K row (no dQ
   // contribution) but exp2(0 - lse) can overflow, so it must not reach dS
+  // the forward's stored keep words of this lane's query (one per key tile)
+  const bool kbits = thr && keep != nullptr;
+  const u32x2* kcol = reinterpret_cast<const u32x2*>(keep) + (size_t)bh * ntiles * N + (qv ? q : 0);
   auto tile = [&](int it, auto mask_tag) {
     constexpr bool MASK = decltype(mask_tag)::value;
     const int kv0 = it * 64;
     const bool more = it + 1 < ntiles;
     if (more) stg.load(kb, vb, kv0 + 64, N);  // next tile lands during this tile's MFMAs
+    const u32x2 kw = kbits ? kcol[(size_t)it * N] : u32x2{0u, 0u};
     const char* Kl = lds + (it & 1) * 2 * C::TILE;
     const char* Vl = Kl + C::TILE;
     f32x4 ds[4];
@@ -616,7 +669,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
       // the lane's 4 keys are consecutive elements of one mask row (aligned: the
       // row stride is a multiple of 4): 2 pair hashes instead of 4 single ones
       bool kp[4] = {true, true, true, true};
-      if (thr) dropout_keep4_pg(salt, pgq + (uint32_t)(kv0 / 2 + 8 * t) * DROP_GOLDEN, thr, kp);
+      if (kbits) keep_nibble(kw, t, g, kp);
+      else if (thr) dropout_keep4_pg(salt, pgq + (uint32_t)(kv0 / 2 + 8 * t) * DROP_GOLDEN, thr, kp);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = kv0 + 16 * t + 4 * g + r;
@@ -659,10 +713,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
                                                            const float* __restrict__ delta,
                                                            bf16* __restrict__ dqkv, int B, int H, int N, float scale,
                                                            const int64_t* __restrict__ rng, int site, uint32_t thr,
-                                                           float dsc) {
+                                                           float dsc, const uint32_t* __restrict__ keep) {
   using C = AC<HD>;
   __shared__ __attribute__((aligned(16))) char lds[4 * C::TILE];  // [buf][Q | dO], double-buffered
   __shared__ float s_lse[2][64], s_del[2][64];
+  // the forward's keep words of the query tile (this workgroup's 64 keys), [buf][half][query]
+  __shared__ __attribute__((aligned(16))) uint32_t s_keep[2][2][64];
   const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
   const int D = H * HD;
   const size_t mat = (size_t)N * HD;
@@ -692,6 +748,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
   constexpr int PER = 64 * C::CPR / 256;
   u32x4 rq[PER], rd[PER];
   float rl = INFINITY, rdl = 0.f;
+  const bool kbits = thr && keep != nullptr;
+  const int ntiles = (N + 63) / 64;
+  u32x2 rk = u32x2{0u, 0u};
   auto load_tile = [&](int q0) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
@@ -710,6 +769,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
       const float l = lse[(size_t)bh * N + qc], dd = delta[(size_t)bh * N + qc];
       rl = qq < N ? l * LOG2E : INFINITY;
       rdl = qq < N ? dd : 0.f;
+      if (kbits) rk = reinterpret_cast<const u32x2*>(keep)[((size_t)bh * ntiles + blockIdx.x) * N + qc];
     }
   };
   auto store_tile = [&](int buf) {
@@ -725,12 +785,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
     if (threadIdx.x < 64) {
       s_lse[buf][threadIdx.x] = rl;
       s_del[buf][threadIdx.x] = rdl;
+      s_keep[buf][0][threadIdx.x] = rk[0];
+      s_keep[buf][1][threadIdx.x] = rk[1];
     }
   };
   load_tile(0);
   store_tile(0);
   __syncthreads();
-  const int ntiles = (N + 63) / 64;
+  // this lane's key within the workgroup's 64: bit (kl & 31) of word half kl >> 5 (wave-uniform)
+  const int kl = wave * 16 + li, khalf = kl >> 5, kshift = kl & 31;
   for (int it = 0; it < ntiles; ++it) {
     const int q0 = it * 64;
     const bool more = it + 1 < ntiles;
@@ -753,7 +816,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
       // keys of one row, held by lanes li and li^1 -- each of the two hashes the
       // pair of 2 of the 4 rows and they swap the results (2 hashes per lane, not 4)
       bool kp[4] = {true, true, true, true};
-      if (thr) {
+      if (kbits) {
+        const u32x4 w = *reinterpret_cast<const u32x4*>(&s_keep[buf][khalf][16 * t + 4 * g]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) kp[r] = (w[r] >> kshift) & 1u;
+      } else if (thr) {
         const int odd = li & 1;
         // pair index of (query qq, key pair) = qq_row * ld/2 + key/2: the multiply by the
         // golden constant is hoisted (pg of query q0+4g+2odd, + (16t+u) rows of ldh*golden)
@@ -1209,13 +1276,6 @@ DC_INST_SHORT(64, 32) DC_INST_SHORT(64, 64) DC_INST_SHORT(64, 96) DC_INST_SHORT(
 
 constexpr int SHORT_MAX_N = 128;
 
-static bool short_disabled() {
-  static const bool off = [] {
-    const char* e = getenv("DDIM_COLD_ATTN_NO_SHORT");
-    return e && e[0] == '1';
-  }();
-  return off;
-}
 
 }  // namespace dc
 
@@ -1226,9 +1286,16 @@ void attn_set_stamps(void* buf) {
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_attn_stamps), &p, sizeof(p));
 }
 
+// Long sequences: the flash / resident forwards store one 64-bit keep word per
+// (b, h, 64-key tile, query) for the backward (attn_fwd_launch picks them whenever
+// it is handed a keep buffer); short ones one 32-bit word per lane.
+static bool long_keep_path(int B, int H, int N) { return N >= 384 || (N <= 320 && B * H >= 192); }
+
 int64_t attn_keep_words(int B, int H, int N, int hd) {
-  if (N > SHORT_MAX_N || short_disabled() || (hd != 32 && hd != 64)) return 0;
-  return (int64_t)B * H * (32 * ((N + 31) / 32)) * 4;
+  if (hd != 32 && hd != 64) return 0;
+  if (N <= SHORT_MAX_N) return (int64_t)B * H * (32 * ((N + 31) / 32)) * 4;
+  if (!long_keep_path(B, H, N)) return 0;  // (320, 384) with few heads: v1 forward, masks re-hashed
+  return (int64_t)B * H * N * ((N + 63) / 64) * 2;
 }
 
 void attn_fwd_launch(const void* qkv, void* o, float* lse, int B, int H, int N, int hd, float scale,
@@ -1238,7 +1305,8 @@ void attn_fwd_launch(const void* qkv, void* o, float* lse, int B, int H, int N, 
   const float dsc = p > 0 ? 1.f / (1.f - (float)p) : 1.f;
   const bf16* q = reinterpret_cast<const bf16*>(qkv);
   bf16* out = reinterpret_cast<bf16*>(o);
-  if (N <= SHORT_MAX_N && !short_disabled() && (hd == 32 || hd == 64)) {
+  if (hd != 32 && hd != 64) throw std::runtime_error("attention: head dim must be 32 or 64");
+  if (N <= SHORT_MAX_N) {
     if (hd == 32)
       dispatch_short<32>(false, nullptr, q, nullptr, lse, nullptr, out, B, H, N, scale, rng, site, thr, dsc, stream,
                          keep_bits);
@@ -1247,43 +1315,40 @@ void attn_fwd_launch(const void* qkv, void* o, float* lse, int B, int H, int N, 
                          keep_bits);
     return;
   }
-  static const bool v1 = [] {
-    const char* e = getenv("DDIM_COLD_ATTN_FLASH_V1");
-    return e && e[0] == '1';
-  }();
-  static const bool no_resident = [] {
-    const char* e = getenv("DDIM_COLD_ATTN_NO_RESIDENT");
-    return e && e[0] == '1';
-  }();
+  uint32_t* kb = thr ? keep_bits : nullptr;
   // one workgroup per head: needs ~a workgroup per CU to pay off.  Measured N=257
-  // hd=64: B*H=256 20.1 vs 31.9 us (v1); B*H=128 equal without dropout, 27 vs 22 with
-  if (!v1 && !no_resident && N <= 320 && B * H >= 192 && (hd == 32 || hd == 64)) {
-    if (hd == 32) launch_resident<32>(q, out, lse, B, H, N, scale, rng, site, thr, dsc, stream);
-    else launch_resident<64>(q, out, lse, B, H, N, scale, rng, site, thr, dsc, stream);
+  // hd=64: B*H=256 20.1 vs 31.9 us (one 64-query workgroup per tile); B*H=128 equal
+  // without dropout, 27 vs 22 with
+  if (N <= 320 && B * H >= 192) {
+    if (hd == 32) launch_resident<32>(q, out, lse, B, H, N, scale, rng, site, thr, dsc, stream, kb);
+    else launch_resident<64>(q, out, lse, B, H, N, scale, rng, site, thr, dsc, stream, kb);
     return;
   }
-  // v2 has half the workgroups of v1: measured better from ~600 tokens (N=626:
-  // 63 vs 71 us without dropout), worse at N=257 with dropout (25 vs 22 us)
-  const bool use_v2 = !v1 && N >= 384;
-  const dim3 grid2((N + 127) / 128, B * H);
-  if (use_v2 && hd == 32) {
-    if (thr) hipLaunchKernelGGL((attn_fwd_flash2_kernel<32, true>), grid2, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc);
-    else hipLaunchKernelGGL((attn_fwd_flash2_kernel<32, false>), grid2, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc);
-  } else if (use_v2 && hd == 64) {
-    if (thr) hipLaunchKernelGGL((attn_fwd_flash2_kernel<64, true>), grid2, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc);
-    else hipLaunchKernelGGL((attn_fwd_flash2_kernel<64, false>), grid2, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc);
-  } else if (hd == 32)
+  // v2 (128 queries per workgroup) has half the workgroups of v1: measured better from
+  // ~600 tokens (N=626: 63 vs 71 us without dropout), worse at N=257 with dropout (25 vs 22 us)
+  if (N >= 384) {
+    const dim3 grid2((N + 127) / 128, B * H);
+    if (hd == 32) {
+      if (thr) hipLaunchKernelGGL((attn_fwd_flash2_kernel<32, true>), grid2, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc, kb);
+      else hipLaunchKernelGGL((attn_fwd_flash2_kernel<32, false>), grid2, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc, kb);
+    } else {
+      if (thr) hipLaunchKernelGGL((attn_fwd_flash2_kernel<64, true>), grid2, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc, kb);
+      else hipLaunchKernelGGL((attn_fwd_flash2_kernel<64, false>), grid2, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc, kb);
+    }
+    return;
+  }
+  if (keep_bits != nullptr && thr)
+    throw std::runtime_error("attention: no stored keep masks on this path (attn_keep_words returned 0)");
+  if (hd == 32)
     hipLaunchKernelGGL(attn_fwd_kernel<32>, grid, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc);
-  else if (hd == 64)
-    hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc);
   else
-    throw std::runtime_error("attention: head dim must be 32 or 64");
+    hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc);
 }
 
 void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const float* lse, void* dqkv,
                         float* delta, int B, int H, int N, int hd, float scale, const int64_t* rng, int site,
                         double p, hipStream_t stream, const uint32_t* keep_bits) {
-  uint32_t* kb = const_cast<uint32_t*>(keep_bits);  // read-only in the backward kernel
+  uint32_t* kb = const_cast<uint32_t*>(keep_bits);  // read-only in the backward kernels
   const dim3 grid((N + 63) / 64, B * H);
   const uint32_t thr = drop_threshold_host(p);
   const float dsc = p > 0 ? 1.f / (1.f - (float)p) : 1.f;
@@ -1291,17 +1356,17 @@ void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const flo
   const bf16* q = reinterpret_cast<const bf16*>(qkv);
   const bf16* oo = reinterpret_cast<const bf16*>(o);
   bf16* dq = reinterpret_cast<bf16*>(dqkv);
-  if (N <= SHORT_MAX_N && !short_disabled() && (hd == 32 || hd == 64)) {
+  if (N <= SHORT_MAX_N && (hd == 32 || hd == 64)) {
     if (hd == 32) dispatch_short<32>(true, d, q, oo, nullptr, lse, dq, B, H, N, scale, rng, site, thr, dsc, stream, kb);
     else dispatch_short<64>(true, d, q, oo, nullptr, lse, dq, B, H, N, scale, rng, site, thr, dsc, stream, kb);
     return;
   }
   if (hd == 32) {
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<32>, grid, dim3(256), 0, stream, d, q, oo, lse, delta, dq, B, H, N, scale, rng, site, thr, dsc);
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<32>, grid, dim3(256), 0, stream, d, q, lse, delta, dq, B, H, N, scale, rng, site, thr, dsc);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<32>, grid, dim3(256), 0, stream, d, q, oo, lse, delta, dq, B, H, N, scale, rng, site, thr, dsc, keep_bits);
+    hipLaunchKernelGGL(attn_bwd_dkv_kernel<32>, grid, dim3(256), 0, stream, d, q, lse, delta, dq, B, H, N, scale, rng, site, thr, dsc, keep_bits);
   } else if (hd == 64) {
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<64>, grid, dim3(256), 0, stream, d, q, oo, lse, delta, dq, B, H, N, scale, rng, site, thr, dsc);
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<64>, grid, dim3(256), 0, stream, d, q, lse, delta, dq, B, H, N, scale, rng, site, thr, dsc);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<64>, grid, dim3(256), 0, stream, d, q, oo, lse, delta, dq, B, H, N, scale, rng, site, thr, dsc, keep_bits);
+    hipLaunchKernelGGL(attn_bwd_dkv_kernel<64>, grid, dim3(256), 0, stream, d, q, lse, delta, dq, B, H, N, scale, rng, site, thr, dsc, keep_bits);
   } else {
     throw std::runtime_error("attention: head dim must be 32 or 64");
   }

@@ -558,10 +558,7 @@ void linear_wgrad(Tensor dy, Tensor x, Tensor dw, c10::optional<Tensor> db) {
   // atomic rate ~1.3 TB/s)
   const int tiles = ((Nout + 63) / 64) * ((K + 63) / 64);
   const int kt = (M + 63) / 64;
-  static const int max_splits = [] {
-    const char* e = getenv("DDIM_COLD_WGRAD_SPLITS");
-    return e ? atoi(e) : 8;
-  }();
+  constexpr int max_splits = 8;
   int splits = (256 + tiles - 1) / tiles;
   if (splits > max_splits) splits = max_splits;
   if (splits > kt) splits = kt;

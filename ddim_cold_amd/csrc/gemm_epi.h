@@ -81,8 +81,6 @@ struct GemmParams {
   int acc_store;  // EPI_ACC: the target is known to be zero -- store, don't read-add
   uint32_t tok_magic;  // floor(2^32 / tokens) (divmagic: row -> sample without a division)
   float ln_invd;       // 1 / K (LayerNorm fold consumer: D = K)
-  int debug;  // profiling aid (DDIM_COLD_GEMM_DEBUG): 1 = skip the epilogue, 2 = skip the main loop,
-              // 3 = scalar (untransposed) epilogue (register-staged fallback GEMM only)
 };
 
 
@@ -899,7 +897,7 @@ struct UsesVecEpi {
 template <int EPI, int FM, int FN>
 __device__ __forceinline__ void run_epilogue(const GemmParams& p, const f32x4 (&acc)[FM][FN], int mb, int nb,
                                              int g, int li) {
-  if (!UsesVecEpi<EPI>::value || p.debug == 3) run_epilogue_scalar<EPI, FM, FN>(p, acc, mb, nb, g, li);
+  if (!UsesVecEpi<EPI>::value) run_epilogue_scalar<EPI, FM, FN>(p, acc, mb, nb, g, li);
   else run_epilogue_vec<EPI, FM, FN>(p, acc, mb, nb, g, li);
 }
 

@@ -407,11 +407,7 @@ void ln_fold_launch(const FoldTable& tb, hipStream_t stream) {
   if (tb.n <= 0) return;
   if (tb.n > FOLD_MAX || tb.K % 4 || tb.K > 512) throw std::runtime_error("ln_fold: bad table (K % 4, K <= 512)");
   const int rows = tb.start[tb.n];
-  static const bool v16 = [] {
-    const char* e = getenv("DDIM_COLD_FOLD16");
-    return !(e && e[0] == '0');
-  }();
-  if (v16 && tb.w_bf16 && tb.K % 8 == 0) {
+  if (tb.w_bf16 && tb.K % 8 == 0) {
     hipLaunchKernelGGL(ln_fold16_kernel, dim3((rows + 15) / 16 + (tb.tail ? 1 : 0)), dim3(256), 0, stream, tb);
     return;
   }
@@ -432,21 +428,9 @@ void ln_fold_launch(const FoldTable& tb, hipStream_t stream) {
 void layernorm_fwd_launch(const float* x, const float* gamma, const float* beta, void* y_bf16, float* mean,
                           float* rstd, int M, int D, float eps, hipStream_t stream) {
   if (D % 128) throw std::runtime_error("layernorm: D % 128 != 0");
-  // waves per workgroup (one row each); measured 2.6 us for 2 or 4, 3.0 for 8
-  static const int nw = [] {
-    const char* e = getenv("DDIM_COLD_LN_FWD_WAVES");
-    return e ? atoi(e) : 4;
-  }();
-#define LN_FWD_GO(W)                                                                                        \
-  LN_DISPATCH(D, hipLaunchKernelGGL((ln_fwd_kernel<VEC, W>), dim3((M + W - 1) / W), dim3(W * 64), 0, stream, x, \
+  // 4 waves per workgroup (one row each); measured 2.6 us for 2 or 4, 3.0 for 8
+  LN_DISPATCH(D, hipLaunchKernelGGL((ln_fwd_kernel<VEC, 4>), dim3((M + 3) / 4), dim3(4 * 64), 0, stream, x,
                                     gamma, beta, reinterpret_cast<bf16*>(y_bf16), mean, rstd, M, eps))
-  switch (nw) {
-    case 2: LN_FWD_GO(2); break;
-    case 8: LN_FWD_GO(8); break;
-    case 16: LN_FWD_GO(16); break;
-    default: LN_FWD_GO(4); break;
-  }
-#undef LN_FWD_GO
 }
 
 void layernorm_bwd_launch(const void* dy, bool dy_bf16, const float* x, const float* mean, const float* rstd,
@@ -458,11 +442,6 @@ void layernorm_bwd_launch(const void* dy, bool dy_bf16, const float* x, const fl
   const uint32_t td = drop_threshold_host(p_drop), tp = drop_threshold_host(p_dp);
   const float sd = p_drop > 0 ? 1.f / (1.f - (float)p_drop) : 1.f;
   const float sp = p_dp > 0 ? 1.f / (1.f - (float)p_dp) : 1.f;
-  // shape of the workgroup: rows per wave x waves (DDIM_COLD_LN_BWD_CFG, tuning)
-  static const int cfg = [] {
-    const char* e = getenv("DDIM_COLD_LN_BWD_CFG");
-    return e ? atoi(e) : 0;
-  }();
 #define LN_BWD_GO1(R, W, DYB)                                                                                 \
   LN_DISPATCH(D, if (W * 2 * D * sizeof(float) > 65536)                                                         \
                   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&ln_bwd_kernel<VEC, R, W, DYB>),           \
@@ -477,12 +456,7 @@ void layernorm_bwd_launch(const void* dy, bool dy_bf16, const float* x, const fl
   else LN_BWD_GO1(R, W, false)
   // measured on the ViT-tiny shape (M 2080, D 384, dropout on): 1 row x 8 waves
   // 5.0 us, 2 x 4 5.9, 1 x 4 5.2, 1 x 16 5.1, 2 x 16 7.2
-  switch (cfg) {
-    case 1: LN_BWD_GO(2, 4); break;
-    case 2: LN_BWD_GO(1, 4); break;
-    case 3: LN_BWD_GO(1, 16); break;
-    default: LN_BWD_GO(1, 8); break;
-  }
+  LN_BWD_GO(1, 8)
 #undef LN_BWD_GO
 #undef LN_BWD_GO1
 }

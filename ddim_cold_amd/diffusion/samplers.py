@@ -95,10 +95,10 @@ class _Denoiser:
             self.model.train(was)
 
 
-FUSED_HEAD = os.environ.get("DDIM_COLD_SAMPLER_FUSED_HEAD", "1") == "1"
+FUSED_HEAD = True  # module constants: tests switch them to compare the paths
 # the head epilogue of each step also writes the new x_t as the next step's bf16
 # patch rows, so every step after the first skips the patchify launch
-PATCH_CHAIN = os.environ.get("DDIM_COLD_SAMPLER_PATCH_CHAIN", "1") == "1"
+PATCH_CHAIN = True
 
 
 def _patch_rows(model, N: int, device, den) -> Optional[torch.Tensor]:
@@ -115,7 +115,7 @@ def _patch_rows(model, N: int, device, den) -> Optional[torch.Tensor]:
 # are contiguous 16-byte vectors (ops.head_step_rows_) instead of scattered pixels,
 # and the first step needs no patchify launch either (head GEMM at N=64: 12.2 -> 7.0
 # us, k=20 N=64 sampler 33.40 -> 32.90 ms per batch; profiles/sampler_rows_ab.txt)
-ROWS = os.environ.get("DDIM_COLD_SAMPLER_ROWS", "1") == "1"
+ROWS = True
 
 
 class _Rows:

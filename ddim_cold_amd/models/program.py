@@ -32,25 +32,25 @@ from .. import ops
 SITE_EMBED = 1
 # K split of the QKV input-gradient GEMM (reduction dim 3D): the partial products
 # go to separate buffers that the LayerNorm backward sums on load
-QKV_DGRAD_SPLITS = int(os.environ.get("DDIM_COLD_QKV_DGRAD_SPLITS", "2"))
+QKV_DGRAD_SPLITS = 2
 # the input-gradient GEMMs feeding a LayerNorm backward (head, fc1, QKV) write
 # bf16 (the K-split partials too) instead of fp32: half the bytes on both sides
 # of the dgrad -> LayerNorm-backward hand-off; the LayerNorm backward sums and
 # computes in fp32 (the reference's fp16 autocast hands it fp16 gradients)
-DGRAD_BF16 = os.environ.get("DDIM_COLD_DGRAD_BF16", "1") == "1"
+DGRAD_BF16 = True
 # LayerNorm fold (csrc/gemm.hip): every LayerNorm is folded into the GEMM that
 # consumes it (QKV, fc1, head) -- no LayerNorm launch in the forward.  The
 # producing GEMM's epilogue accumulates the row statistics; the LayerNorm
 # backward re-emits the normalised rows for the weight gradients.
-FOLD_LN = os.environ.get("DDIM_COLD_LN_FOLD", "1") == "1"
+FOLD_LN = True  # False: separate LayerNorm launches (tests compare both)
 # the short attention forward stores its dropout keep flags (one 32-bit word per
 # lane, 0.6 MB per block for ViT-tiny at B=32) and the backward reads them instead
 # of re-hashing 2 pairs per 4 probabilities (the mask hash was ~1.9 us of the
 # backward's ~11 us, tools/ub_drop.py).  Same masks either way.
-STORE_ATTN_KEEP = os.environ.get("DDIM_COLD_ATTN_KEEP", "1") != "0"
+STORE_ATTN_KEEP = True
 # training with the fused batch draw: loss target as patch rows, vector loss epilogue
 # (EPI_HEADL; head GEMM 11.3 -> see profiles/README.md round 3)
-TARGET_ROWS = os.environ.get("DDIM_COLD_TARGET_ROWS", "1") == "1"
+TARGET_ROWS = True
 # dtype of the bf16 activation copies / folded weights the program allocates
 # (tests on CPU switch it to fp32 to isolate the program logic from rounding)
 ACT_DTYPE = torch.bfloat16

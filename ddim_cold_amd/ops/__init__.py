@@ -126,6 +126,7 @@ class gemm_tile:
         self.prev = -1
 
     def __enter__(self):
+        _ext.load(raise_on_error=True)
         self.prev = int(_ops().gemm_tile_override(self.cfg))
         return self
 
@@ -135,9 +136,11 @@ class gemm_tile:
 
 
 def attn_keep_buffer(qkv, p: float):
-    """int32 buffer for the attention-dropout keep flags the short-sequence forward
-    stores for its backward (one word per lane: no mask re-hashing there), or None
-    when there is nothing to store (p = 0, CPU, or a long sequence)."""
+    """int32 buffer for the attention-dropout keep flags the forward stores for its
+    backward (short sequences: one word per lane; long ones: one 64-bit word per
+    query and 64-key tile), so the backward reads masks instead of re-hashing them;
+    None when there is nothing to store (p = 0, CPU, or the one long-sequence
+    forward that keeps no words: 320 < N < 384 with fewer than 192 heads)."""
     if p <= 0 or not _hip(qkv):
         return None
     _, B, H, N, hd = qkv.shape

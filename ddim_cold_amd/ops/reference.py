@@ -65,11 +65,12 @@ def drop_threshold(p: float) -> int:
     return min(int(p * 65536.0 + 0.5), 65536)
 
 
-def keep_mask(numel: int, rng: torch.Tensor, site: int, p: float, device=None) -> torch.Tensor:
-    """Boolean keep-mask over a flat index space [0, numel) (bit-exact with ``dropout_keep``
-    in csrc/common.h): element i uses the 16-bit half (i & 1) of the hash of pair i >> 1."""
+def keep_mask(numel: int, rng: torch.Tensor, site: int, p: float, device=None, start: int = 0) -> torch.Tensor:
+    """Boolean keep-mask over a flat index space [start, start + numel) (bit-exact with
+    ``dropout_keep`` in csrc/common.h): element i uses the 16-bit half (i & 1) of the
+    hash of pair i >> 1 (indices are 32-bit counters)."""
     salt = site_salt(rng, site)
-    idx = torch.arange(numel, dtype=torch.int64, device=device) & MASK32
+    idx = torch.arange(start, start + numel, dtype=torch.int64, device=device) & MASK32
     h = mix32(_mul32(idx >> 1, GOLDEN) ^ salt)
     half = torch.where((idx & 1) == 1, h >> 16, h & 0xFFFF)
     return half >= drop_threshold(p)
@@ -80,11 +81,12 @@ def attn_mask_ld(N: int) -> int:
     return (N + 3) // 4 * 4
 
 
-def attn_keep_mask(B: int, H: int, N: int, rng, site: int, p: float, device=None) -> torch.Tensor:
+def attn_keep_mask(B: int, H: int, N: int, rng, site: int, p: float, device=None, bh0: int = 0) -> torch.Tensor:
     """[B, H, N, N] keep-mask of the attention probabilities; element (b, h, q, key) has
-    flat index ((b*H + h)*N + q) * attn_mask_ld(N) + key."""
+    flat index ((bh0 + b*H + h)*N + q) * attn_mask_ld(N) + key (``bh0``: the first
+    head's position in a larger batch, for checking a slice of one)."""
     ld = attn_mask_ld(N)
-    return keep_mask(B * H * N * ld, rng, site, p, device).view(B, H, N, ld)[..., :N]
+    return keep_mask(B * H * N * ld, rng, site, p, device, start=bh0 * N * ld).view(B, H, N, ld)[..., :N]
 
 
 def _dropout(x: torch.Tensor, rng, site, p) -> torch.Tensor:
@@ -211,7 +213,7 @@ def qkv_fwd(a, w, b, B: int, N: int, H: int, st=None, c=None, eps: float = 1e-5,
     return y.view(B, N, 3, H, D // H).permute(2, 0, 3, 1, 4).contiguous()
 
 
-def attn_fwd(qkv, scale: float, rng, site: int, p: float):
+def attn_fwd(qkv, scale: float, rng, site: int, p: float, bh0: int = 0):
     """softmax(QK^T*scale) (dropout) V -> o [B,N,D] bf16 token-major, lse [B,H,N] fp32."""
     _, B, H, N, hd = qkv.shape
     q, k, v = qkv[0].float(), qkv[1].float(), qkv[2].float()
@@ -219,7 +221,7 @@ def attn_fwd(qkv, scale: float, rng, site: int, p: float):
     lse = torch.logsumexp(s, dim=-1)
     pr = torch.exp(s - lse.unsqueeze(-1))
     if p > 0.0:
-        pr = torch.where(attn_keep_mask(B, H, N, rng, site, p, pr.device), pr / (1.0 - p),
+        pr = torch.where(attn_keep_mask(B, H, N, rng, site, p, pr.device, bh0), pr / (1.0 - p),
                          torch.zeros((), dtype=pr.dtype, device=pr.device))
     # P is rounded to bf16 before the PV product (as the MFMA kernel does)
     o = bf16(pr).float() @ v
@@ -351,7 +353,7 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dgamma, dbeta, N: int, rng,
     return g_out.view(x.shape), gy
 
 
-def attn_bwd(do, qkv, o, lse, scale: float, rng, site: int, p: float):
+def attn_bwd(do, qkv, o, lse, scale: float, rng, site: int, p: float, bh0: int = 0):
     """Flash-style attention backward -> dqkv [B*N, 3D] bf16 token-major."""
     _, B, H, N, hd = qkv.shape
     q, k, v = qkv[0].float(), qkv[1].float(), qkv[2].float()
@@ -360,7 +362,7 @@ def attn_bwd(do, qkv, o, lse, scale: float, rng, site: int, p: float):
     s = (q @ k.transpose(-1, -2)) * scale
     pr = torch.exp(s - lse.unsqueeze(-1))
     if p > 0:
-        m = attn_keep_mask(B, H, N, rng, site, p, pr.device).float() / (1.0 - p)
+        m = attn_keep_mask(B, H, N, rng, site, p, pr.device, bh0).float() / (1.0 - p)
     else:
         m = torch.ones_like(pr)
     pd = pr * m

@@ -68,7 +68,7 @@ class FlagSignal:
     Inside the compute graph, :meth:`bump` is a 1-lane kernel node that adds 1 to
     ``flags[k]`` with a system-scope release once the bucket's gradients are final;
     the host then orders a comm-stream collective behind ``flags[k] >= replays``
-    with a stream wait-value packet (:meth:`waiter`).  Unlike an event-record node,
+    with a bounded polling kernel (:meth:`waiter`).  Unlike an event-record node,
     the kernel node keeps the graph one uninterrupted chain (measured on MI355X:
     the comm stream waiting on mid-graph event nodes started only after the whole
     graph had finished, so nothing overlapped)."""
@@ -78,9 +78,6 @@ class FlagSignal:
         self.flags = torch.zeros(max(1, n), dtype=torch.int32, device=device)
         self.err = torch.zeros(1, dtype=torch.int32, device=device)
         self.expected = 0  # replays of the graph that bumps the counters
-        # comm-stream wait: "kernel" = our bounded 1-lane polling kernel, "stream" =
-        # hipStreamWaitValue32 (DDIM_COLD_FLAG_WAIT)
-        self.mode = os.environ.get("DDIM_COLD_FLAG_WAIT", "kernel")
         # the polling kernel's bound (default 2 s; tests shorten it)
         self.timeout_us = int(os.environ.get("DDIM_COLD_HANDOFF_TIMEOUT_US", "0"))
         # testing: wait for a counter value the compute graph never reaches, so every
@@ -102,12 +99,9 @@ class FlagSignal:
 
         class _Wait:
             def wait(self_, stream):
-                with torch.cuda.stream(stream):
-                    if sig.mode == "stream":
-                        torch.ops.ddim_cold.stream_wait_flag(sig.flags, int(k), int(sig.expected))
-                    else:
-                        torch.ops.ddim_cold.flag_wait(sig.flags, int(k), int(sig.expected + sig.skew) & 0xFFFFFFFF,
-                                                      sig.err, sig.timeout_us)
+                with torch.cuda.stream(stream):  # our bounded 1-lane polling kernel
+                    torch.ops.ddim_cold.flag_wait(sig.flags, int(k), int(sig.expected + sig.skew) & 0xFFFFFFFF,
+                                                  sig.err, sig.timeout_us)
         return _Wait()
 
     def failed(self) -> bool:

@@ -62,23 +62,76 @@ def load_weights(model, path: str, strict: bool = True):
     return missing, unexpected
 
 
-def save_lastepoch(path: str, model, engine, epoch: int, steps: int, loss_rec: float, metric: float):
-    ckpt = {
+def lastepoch_dict(snap, epoch: int, steps: int, loss_rec: float, metric: float) -> dict:
+    """The reference's ``lastepoch.pkl`` dict (multi_gpu_trainer.py:155-163) from a
+    host snapshot of the engine (``TrainEngine.snapshot_to_host``)."""
+    snap.wait()
+    return {
         "epoch": int(epoch),
         "steps": int(steps),
         "loss_rec": float(loss_rec),
         "metric": float(metric),
-        "state_dict": add_prefix(cpu_state_dict(model)),
-        "scheduler": engine.scheduler_state_dict(),
-        "optimizer": _to_cpu(engine.optimizer_state_dict()),
-        "rng": engine.rng.detach().cpu().clone(),
-        "engine_steps": int(engine.steps_done),
+        "state_dict": add_prefix(snap.state_dict()),
+        "scheduler": snap.scheduler_state_dict(),
+        "optimizer": _to_cpu(snap.optimizer_state_dict()),
+        "rng": snap.rng.clone(),
+        "engine_steps": int(snap.steps_done),
         # torch.cuda.amp.GradScaler state_dict layout (the reference does not save it,
         # SURVEY §7.4 D15); bf16 needs no loss scaling, so the scale is fixed at 1
         "scaler": {"scale": 1.0, "growth_factor": 2.0, "backoff_factor": 0.5, "growth_interval": 2000,
                    "_growth_tracker": 0},
     }
-    _atomic_save(ckpt, path)
+
+
+def save_lastepoch(path: str, model, engine, epoch: int, steps: int, loss_rec: float, metric: float):
+    """Synchronous ``lastepoch.pkl`` write (the trainer writes through :class:`CheckpointWriter`)."""
+    _atomic_save(lastepoch_dict(engine.snapshot_to_host(), epoch, steps, loss_rec, metric), path)
+
+
+class CheckpointWriter:
+    """Epoch-end checkpoints off the training critical path.
+
+    ``submit(snapshot, ...)`` returns at once: the snapshot's device copies are
+    already queued on the training stream (``TrainEngine.snapshot_to_host``), and a
+    background thread waits for its host copy, lays out ``bestloss.pkl`` /
+    ``lastepoch.pkl`` and writes them (``torch.save`` to a temp file + atomic rename),
+    while the next epoch trains.  At most one write is in flight: ``submit`` and
+    ``join`` wait for the previous one (and re-raise its error), so the snapshot
+    buffers are never overwritten mid-write and the files on disk are always whole.
+    ``join()`` before exit and before anything reads the files."""
+
+    def __init__(self):
+        self._thread = None
+        self._err: BaseException | None = None
+        self.last_write_s = 0.0
+
+    def submit(self, snap, lastepoch_path: str, epoch: int, steps: int, loss_rec: float, metric: float,
+               best_path: str | None = None):
+        import threading
+        import time
+        self.join()
+
+        def work():
+            try:
+                t0 = time.perf_counter()
+                d = lastepoch_dict(snap, epoch, steps, loss_rec, metric)
+                if best_path is not None:
+                    _atomic_save(strip_prefix(d["state_dict"]), best_path)
+                _atomic_save(d, lastepoch_path)
+                self.last_write_s = time.perf_counter() - t0
+            except BaseException as e:  # surfaced by the next join()
+                self._err = e
+
+        self._thread = threading.Thread(target=work, name="ckpt-writer", daemon=False)
+        self._thread.start()
+
+    def join(self):
+        if self._thread is not None:
+            self._thread.join()
+            self._thread = None
+        if self._err is not None:
+            e, self._err = self._err, None
+            raise RuntimeError(f"checkpoint write failed: {e!r}") from e
 
 
 def load_lastepoch(path: str, model, engine) -> dict:

@@ -113,19 +113,13 @@ class EngineConfig:
     # 1-element kernel on a side stream at each of the 5 bucket boundaries: 0.818 ->
     # 1.013 ms/step -- and with one elementwise pass per bucket on the comm stream
     # (standing in for the collective) the event-split step runs at 0.937 vs 1.072
-    # captured (tools/gpu_events.sh).  DDIM_COLD_COMM_EVENTS=0: graph_comm / segments.
-    comm_events: bool = os.environ.get("DDIM_COLD_COMM_EVENTS", "1") != "0"
+    # captured.  False: graph_comm / segments.
+    comm_events: bool = True
     # data parallel: issue the collectives on the compute stream (no comm stream, no
     # overlap; with comm_events, host-issued between the two step graphs).  With one
     # bucket this is the single-process step + one all-reduce of the whole arena;
     # autotune_comm() measures it against the overlapped layouts on the real ranks.
-    comm_inline: bool = os.environ.get("DDIM_COLD_COMM_INLINE") == "1"
-    # event-split step: how the compute graph tells the comm stream a bucket is
-    # final.  "flag": a kernel node bumps a per-bucket counter (system-scope release)
-    # and the comm stream waits on it with a wait-value packet; "event": external
-    # event-record nodes (measured: the comm stream then started only after the
-    # whole compute graph, so the overlapped layouts overlapped nothing).
-    comm_signal: str = os.environ.get("DDIM_COLD_COMM_SIGNAL", "flag")
+    comm_inline: bool = False
     # micro-batches per optimizer step (batch_fn is called grad_accum times per
     # step; gradients accumulate in the arena, averaged in the optimizer; the
     # all-reduce runs once, after the last micro-batch's backward)
@@ -144,8 +138,8 @@ class EngineConfig:
     # a batch source with ``fused_spec()`` (data.synthetic.ColdBatcher) has its draw
     # fused into the patch-embedding launch (ops.patch_embed_cold_fwd: the patch rows
     # pixelated straight from the pool, x_t never materialised): one launch fewer
-    # per step, identical values.  DDIM_COLD_FUSE_BATCH=0 turns it off.
-    fuse_batch: bool = os.environ.get("DDIM_COLD_FUSE_BATCH", "1") != "0"
+    # per step, identical values.
+    fuse_batch: bool = True
     # optimizer steps per hipGraph replay for train_steps(n) (one graph holding K
     # complete steps, every counter on the device): the inter-replay dispatch gap
     # (~8 us before each step's first kernel in the graph-mode trace) is paid once
@@ -214,15 +208,13 @@ class TrainEngine:
         model._engine = self
 
     def _comm_stream(self):
-        """The collectives' stream: high priority by default (DDIM_COLD_COMM_PRIO=0:
-        normal).  HIP keeps a separate pool of hardware queues per priority, so a
+        """The collectives' stream, high priority.  HIP keeps a separate pool of hardware queues per priority, so a
         high-priority comm stream can never share an in-order hardware queue with the
         normal-priority compute stream -- with GPU_MAX_HW_QUEUES=4 normal-priority
         streams beyond four do share queues round-robin, and a comm-stream wait
         queued ahead of the compute graph on a SHARED queue would block that graph
         (see :meth:`_preissue_ok`)."""
-        prio = -1 if os.environ.get("DDIM_COLD_COMM_PRIO", "1") != "0" else 0
-        return torch.cuda.Stream(device=self.device, priority=prio)
+        return torch.cuda.Stream(device=self.device, priority=-1)
 
     def _preissue_ok(self) -> bool:
         """Queue the comm stream's counter waits + collectives AHEAD of the compute
@@ -497,10 +489,8 @@ class TrainEngine:
         (LayerNorms, blocks, head) is written by exactly one producer per step, which
         then stores instead of adding -- the optimizer zeroes only the embeddings
         (accumulated by atomics) and the deferred launches read no gradients.  The
-        all-reduce sums the fresh values in place.  DDIM_COLD_GRAD_OVERWRITE=0:
-        accumulate everywhere."""
-        return (self.is_cuda and k_acc == 1 and deferred and ln_final is not None
-                and os.environ.get("DDIM_COLD_GRAD_OVERWRITE", "1") != "0")
+        all-reduce sums the fresh values in place."""
+        return self.is_cuda and k_acc == 1 and deferred and ln_final is not None
 
     def _step_iter(self):
         c = self.prog.cfg
@@ -551,7 +541,7 @@ class TrainEngine:
             # the LayerNorm replica finalize rides in the embedding-backward launch (data
             # parallel too: every LayerNorm lives in the last bucket's arena range)
             ln_final = None
-            if self.ln_ptrs is not None and os.environ.get("DDIM_COLD_FUSE_LNFINAL", "1") != "0":
+            if self.ln_ptrs is not None:
                 hi = self.ln_done_at[-1]
                 ln_final = (self.ln_ws[:hi], self.ln_ptrs[:hi], 2 * c.dim)
             # single process: every weight gradient in one launch after the backward (no
@@ -610,13 +600,11 @@ class TrainEngine:
         ranges = self.bucket_ranges[k]
 
         fake = os.environ.get("DDIM_COLD_FAKE_COMM") == "1"
-        fake_reps = int(os.environ.get("DDIM_COLD_FAKE_COMM_REPS", "1"))  # longer stand-in collectives
 
         def reduce():
             for a, b in ranges:
                 if fake:  # topology experiment at 1 rank: passes over the range stand in for the collective
-                    for _ in range(fake_reps):
-                        self.flat_g[a:b].mul_(1.0)
+                    self.flat_g[a:b].mul_(1.0)
                 elif self.ncomm is not None:
                     if self.flat_gw is None:
                         self.ncomm.all_reduce_(self.flat_g[a:b])
@@ -917,14 +905,17 @@ class TrainEngine:
         self._multi = None
         from ..parallel.comm import ExternalEvent, FlagSignal
         sig = None
-        if self.cfg.comm_signal == "flag" and self.comm is not None and FlagSignal.supported(self.device):
+        # the compute graph tells the comm stream a bucket is final by bumping a
+        # per-bucket counter (a 1-lane kernel node, system-scope release) that a
+        # bounded polling kernel on the comm stream waits for.  (External event-record
+        # nodes were measured too: the comm stream then started only after the whole
+        # compute graph, so the overlapped layouts overlapped nothing.)  Inline layout
+        # (no comm stream): events only mark the bucket boundaries.
+        if self.comm is not None:
             sig = FlagSignal(nb, self.device)
             evs = [sig.waiter(k) for k in range(nb)]
         else:
-            # release scope of the boundary events (DDIM_COLD_EVENT_FLAGS: extra
-            # hipEventCreateWithFlags bits, e.g. 0x40000000 = device-scope release)
-            flags = int(os.environ.get("DDIM_COLD_EVENT_FLAGS", "0"), 0)
-            evs = [ExternalEvent(flags) for _ in range(nb)]
+            evs = [ExternalEvent() for _ in range(nb)]
         gen = self._step_iter()
         g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1, pool=pool, capture_error_mode=CAPTURE_MODE):
@@ -1055,32 +1046,72 @@ class TrainEngine:
 
     # ------------------------------------------------------------------ state
     def current_lr(self) -> float:
-        step = int(self.step_ctr[1].item())
-        c = self.cfg
-        if c.t_max <= 0:
-            return c.lr
-        return c.eta_min + (c.lr - c.eta_min) * 0.5 * (1 + math.cos(math.pi * step / c.t_max))
+        return self._lr_at(int(self.step_ctr[1].item()))
 
     def _param_list(self):
         return [p for _, p in self.model.named_parameters()]
 
     def optimizer_state_dict(self) -> dict:
         """torch.optim.AdamW-format state dict (interchangeable with the reference's lastepoch.pkl)."""
+        ctr = self.step_ctr.detach().cpu()
+        return self._optimizer_sd(self.flat_m, self.flat_v, int(ctr[0]), int(ctr[1]))
+
+    def _lr_at(self, sched_step: int) -> float:
+        c = self.cfg
+        if c.t_max <= 0:
+            return c.lr
+        return c.eta_min + (c.lr - c.eta_min) * 0.5 * (1 + math.cos(math.pi * sched_step / c.t_max))
+
+    def _optimizer_sd(self, flat_m: torch.Tensor, flat_v: torch.Tensor, adam_step: int, sched_step: int) -> dict:
+        """AdamW state dict from moment arenas (the live device ones, or a host snapshot)."""
         params = self._param_list()
-        opt = torch.optim.AdamW(params, lr=self.current_lr(), betas=self.cfg.betas, eps=self.cfg.eps,
+        opt = torch.optim.AdamW(params, lr=self._lr_at(sched_step), betas=self.cfg.betas, eps=self.cfg.eps,
                                 weight_decay=self.cfg.weight_decay)
-        adam_step = float(self.step_ctr[0].item())
         if adam_step > 0:
             for n, p in zip(self.names, params):
                 if n in self.frozen:  # torch.optim keeps no state for a parameter without .grad
                     continue
                 o, k = self.offsets[n]
-                opt.state[p] = {"step": torch.tensor(adam_step),
-                                "exp_avg": self.flat_m[o:o + k].view_as(p).clone(),
-                                "exp_avg_sq": self.flat_v[o:o + k].view_as(p).clone()}
+                opt.state[p] = {"step": torch.tensor(float(adam_step)),
+                                "exp_avg": flat_m[o:o + k].view(p.shape).clone(),
+                                "exp_avg_sq": flat_v[o:o + k].view(p.shape).clone()}
         sd = opt.state_dict()
         sd["param_groups"][0]["initial_lr"] = self.cfg.lr
         return sd
+
+    def snapshot_to_host(self) -> "HostSnapshot":
+        """Training state (parameters, Adam moments, counters) for an off-critical-path
+        checkpoint write: device-to-device copies into snapshot buffers on the CURRENT
+        stream (ordered after the last step, ~90 MB at HBM speed for ViT-tiny), then
+        device-to-host copies into pinned buffers on a side stream that the training
+        stream never waits for.  ``HostSnapshot.wait()`` (the writer thread) blocks
+        until the host copy has landed.  The buffers are reused: finish (wait) one
+        snapshot before taking the next."""
+        cur = torch.cuda.current_stream(self.device) if self.is_cuda else None
+        if getattr(self, "_snap", None) is None:
+            pin = self.is_cuda
+            host = [torch.empty(t.shape, dtype=t.dtype, pin_memory=pin)
+                    for t in (self.flat_p, self.flat_m, self.flat_v, self.step_ctr, self.rng)]
+            dev = [torch.empty_like(t) for t in (self.flat_p, self.flat_m, self.flat_v, self.step_ctr, self.rng)] \
+                if self.is_cuda else None
+            side = torch.cuda.Stream(self.device) if self.is_cuda else None
+            self._snap = (host, dev, side)
+        host, dev, side = self._snap
+        src = (self.flat_p, self.flat_m, self.flat_v, self.step_ctr, self.rng)
+        ev = None
+        if self.is_cuda:
+            for d, t in zip(dev, src):
+                d.copy_(t)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                for h, d in zip(host, dev):
+                    h.copy_(d, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(side)
+        else:
+            for h, t in zip(host, src):
+                h.copy_(t)
+        return HostSnapshot(self, *host, ev, int(self.steps_done))
 
     def load_optimizer_state_dict(self, sd: dict):
         st = sd.get("state", {})
@@ -1096,16 +1127,16 @@ class TrainEngine:
             step = int(float(s["step"]))
         self.step_ctr[0] = step
 
-    def scheduler_state_dict(self) -> dict:
-        """torch CosineAnnealingLR-format state dict."""
+    def scheduler_state_dict(self, sched_step: Optional[int] = None) -> dict:
+        """torch CosineAnnealingLR-format state dict (at ``sched_step``, default: now)."""
         params = self._param_list()
         opt = torch.optim.AdamW(params, lr=self.cfg.lr)
         sch = torch.optim.lr_scheduler.CosineAnnealingLR(opt, max(self.cfg.t_max, 1), self.cfg.eta_min)
         sd = sch.state_dict()
-        last = int(self.step_ctr[1].item())
+        last = int(self.step_ctr[1].item()) if sched_step is None else int(sched_step)
         sd["last_epoch"] = last
         sd["_step_count"] = last + 1
-        sd["_last_lr"] = [self.current_lr()]
+        sd["_last_lr"] = [self._lr_at(last)]
         return sd
 
     def load_scheduler_state_dict(self, sd: dict):
@@ -1121,3 +1152,36 @@ class TrainEngine:
             p.data = p.data.clone()
             p.grad = None
         self.model._engine = None
+
+
+class HostSnapshot:
+    """Host copy of an engine's training state (:meth:`TrainEngine.snapshot_to_host`):
+    fp32 parameter / moment arenas, counters and RNG state, plus what is needed to
+    lay them out as the reference's checkpoint dicts without touching the device."""
+
+    def __init__(self, engine: TrainEngine, p, m, v, step_ctr, rng, event, steps_done: int):
+        self.engine, self.p, self.m, self.v, self.step_ctr, self.rng = engine, p, m, v, step_ctr, rng
+        self.event = event
+        self.steps_done = steps_done
+
+    def wait(self):
+        if self.event is not None:
+            self.event.synchronize()
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        """The model's ``state_dict`` (parameter order and shapes) from the snapshot."""
+        eng = self.engine
+        shapes = {n: p.shape for n, p in eng.model.named_parameters()}
+        out = {}
+        for n in eng.model.state_dict().keys():
+            if n not in eng.offsets:
+                raise KeyError(f"{n}: not in the parameter arena (a buffer?) -- snapshot cannot hold it")
+            o, k = eng.offsets[n]
+            out[n] = self.p[o:o + k].view(shapes[n]).clone()
+        return out
+
+    def optimizer_state_dict(self) -> dict:
+        return self.engine._optimizer_sd(self.m, self.v, int(self.step_ctr[0]), int(self.step_ctr[1]))
+
+    def scheduler_state_dict(self) -> dict:
+        return self.engine.scheduler_state_dict(int(self.step_ctr[1]))

@@ -256,7 +256,10 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
 
     history = []
     last_ms = None  # device ms/step of the last full log window
+    ckw = ckpt.CheckpointWriter()
     t_start = time.time()
+    t_run = t_epoch = time.perf_counter()
+    steps0 = steps
     for epoch in range(start_epoch, end_epoch):
         model.train()
         table = shard_indices(n_train, world, rank, epoch, cfg.seed)[: steps_per_epoch * A * B]
@@ -292,6 +295,7 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
                 raise FaultInjected(f"fault injected at step {steps} on rank {rank} (fault_inject_step)")
         loss_rec = float(engine.loss_ema.item())
         engine.check_comm()  # epoch end: before evaluating / checkpointing these weights
+        t_ev = time.perf_counter()
         if (epoch - start_epoch + 1) % max(cfg.eval_every, 1) == 0 or epoch == end_epoch - 1:
             model.eval()
             vidx = shard_indices(n_val, world, rank, epoch, cfg.seed, shuffle=False, drop_last=False)
@@ -301,19 +305,39 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
             vloss = pdist.all_reduce_mean(vloss, device)
             model.train()
             history.append((epoch, vloss))
+            t_ck = time.perf_counter()
             if rank == 0:
                 printLog(fmt_epoch(epoch, vloss), paths.log)
                 writer.add_scalar("loss", vloss, epoch)
-                if vloss < best_loss:
+                best = vloss < best_loss
+                if best:
                     best_loss = vloss
-                    ckpt.save_weights(model, os.path.join(paths.ckpt_dir, "bestloss.pkl"))
-                ckpt.save_lastepoch(os.path.join(paths.ckpt_dir, "lastepoch.pkl"), model, engine, epoch, steps,
-                                    loss_rec, best_loss)
+                # bestloss.pkl / lastepoch.pkl written by a background thread from a
+                # snapshot taken here (device copies on the training stream, host copy
+                # on a side stream) while the next epoch trains
+                ckw.submit(engine.snapshot_to_host(), os.path.join(paths.ckpt_dir, "lastepoch.pkl"), epoch,
+                           steps, loss_rec, best_loss,
+                           best_path=os.path.join(paths.ckpt_dir, "bestloss.pkl") if best else None)
             pdist.barrier()
+            t_end = time.perf_counter()
+            if rank == 0 and cfg.perf_log:
+                wall = t_end - t_epoch
+                printLog(f"# perf: epoch {epoch} end to end {steps_per_epoch * B * A * world / wall:.1f} img/s "
+                         f"({wall:.3f} s: evaluate {1e3 * (t_ck - t_ev):.1f} ms, checkpoint hand-off "
+                         f"{1e3 * (t_end - t_ck):.1f} ms, previous write {1e3 * ckw.last_write_s:.1f} ms "
+                         f"in the background)", paths.log)
+        t_epoch = time.perf_counter()
     if prof is not None:
         prof.__exit__(None, None, None)
+    t_done = time.perf_counter()
+    ckw.join()  # the last epoch's files are complete before the run returns
     writer.close()
+    e2e = (steps - steps0) * B * A * world / max(t_done - t_run, 1e-9)
+    if rank == 0 and cfg.perf_log and steps > steps0:
+        printLog(f"# perf: run end to end {e2e:.1f} img/s over {steps - steps0} steps "
+                 f"({t_done - t_run:.2f} s incl. graph capture, evaluation, checkpoints)", paths.log)
     result = {"steps": steps, "loss_rec": loss_rec, "best_loss": best_loss, "history": history,
+              "e2e_img_per_s": e2e,
               "final_lr": engine.current_lr(), "rng": [int(v) for v in engine.rng.tolist()],
               "eval_rng": [int(v) for v in eval_rng.tolist()],
               "comm_choice": engine.comm_choice, "handoff_order": engine.handoff_order,

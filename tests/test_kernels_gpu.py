@@ -318,6 +318,62 @@ def test_attention_fwd_bwd(B, H, N, hd, p):
         assert torch.equal(ops.attn_bwd(do, qkv, o, lse, scale, r, 5, p, keep=keep), dq)
 
 
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_n2501(p):
+    """The 200x200 / p=4 sequence length (2,501 tokens, 40 key tiles, ragged tail) the
+    long-sequence kernels are benchmarked at: forward, backward, stored keep words."""
+    B, H, N, hd = 2, 2, 2501, 64
+    qkv = bf(3, B, H, N, hd)
+    r = rng()
+    scale = hd ** -0.5
+    keep = ops.attn_keep_buffer(qkv, p)
+    assert (keep is not None) == (p > 0) and (keep is None or keep.numel() == B * H * N * 40 * 2)
+    o, lse = ops.attn_fwd(qkv, scale, r, 5, p, keep_out=keep)
+    or_, lser = ref.attn_fwd(qkv, scale, r, 5, p)
+    close(lse, lser, 1e-3, 1e-4, "lse")
+    close(o, or_, 2e-2, 2e-2, "o")
+    do = bf(B, N, H * hd)
+    dq = ops.attn_bwd(do, qkv, o, lse, scale, r, 5, p, keep=keep)
+    close(dq, ref.attn_bwd(do, qkv, o, lse, scale, r, 5, p), 3e-2, 3e-2, "dqkv")
+    if keep is not None:  # stored words == re-hashed masks, bit for bit
+        assert torch.equal(ops.attn_bwd(do, qkv, o, lse, scale, r, 5, p), dq)
+
+
+def test_attention_mask_index_beyond_2p31():
+    """Dropout mask indices are 32-bit counters (hoisted pair-hash math): at B*H = 400,
+    N = 2,501 they pass 2^31 (signed overflow would show here).  The last head (mask
+    indices ~2.5e9) against the reference's mask for that slice; stored keep words vs
+    re-hashing over the whole batch."""
+    B, H, N, hd, p = 1, 400, 2501, 64, 0.1
+    assert (B * H - 1) * N * ((N + 3) // 4 * 4) > 2 ** 31
+    qkv = bf(3, B, H, N, hd)
+    r = rng()
+    scale = hd ** -0.5
+    keep = ops.attn_keep_buffer(qkv, p)
+    o, lse = ops.attn_fwd(qkv, scale, r, 5, p, keep_out=keep)
+    last = qkv[:, :, H - 1:].contiguous()
+    or_, lser = ref.attn_fwd(last, scale, r, 5, p, bh0=H - 1)
+    D = H * hd
+    close(lse[:, H - 1:], lser, 1e-3, 1e-4, "lse (last head)")
+    close(o[:, :, D - hd:], or_, 2e-2, 2e-2, "o (last head)")
+    do = bf(B, N, D)
+    dq = ops.attn_bwd(do, qkv, o, lse, scale, r, 5, p, keep=keep)
+    dqr = ref.attn_bwd(do[:, :, D - hd:].contiguous(), last, o[:, :, D - hd:].contiguous(), lse[:, H - 1:].contiguous(),
+                       scale, r, 5, p, bh0=H - 1)
+    dqv = dq.view(B * N, 3, D)[:, :, D - hd:].reshape(B * N, 3 * hd)
+    close(dqv, dqr, 3e-2, 3e-2, "dqkv (last head)")
+    assert torch.equal(ops.attn_bwd(do, qkv, o, lse, scale, r, 5, p), dq)
+
+
+def test_attention_mask_index_guard():
+    """More than 2^32 mask elements: refused before launch (dropout on); fine without."""
+    B, H, N, hd = 1, 700, 2501, 32
+    assert B * H * N * ((N + 3) // 4 * 4) >= 2 ** 32
+    qkv = torch.zeros(3, B, H, N, hd, dtype=torch.bfloat16, device=DEV)
+    with pytest.raises(RuntimeError, match="2\\^32"):
+        ops.attn_fwd(qkv, hd ** -0.5, rng(), 5, 0.1)
+
+
 def test_attention_spike_rescale():
     """Force a running-max jump at the second KV tile (online-softmax rescale branch)."""
     B, H, N, hd = 1, 1, 130, 32

@@ -201,3 +201,63 @@ def test_trainer_stops_on_comm_error(tmp_path, monkeypatch):
         launch(cfg, "exp", paths, backend="gloo")
     assert len(calls) == 1
     assert not os.path.exists(os.path.join(paths.ckpt_dir, "lastepoch.pkl"))  # nothing saved after it
+
+
+def test_async_lastepoch_equals_sync_and_resumes_identically(tmp_path):
+    """lastepoch.pkl written by the background CheckpointWriter (host snapshot) holds
+    exactly what the synchronous write holds, and resuming from either gives the
+    same training state."""
+    from ddim_cold_amd.data.synthetic import ColdBatcher, synthetic_pool
+    from ddim_cold_amd.models import DiffusionVisionTransformer
+    from ddim_cold_amd.train.engine import EngineConfig, TrainEngine
+
+    def make():
+        torch.manual_seed(3)
+        m = DiffusionVisionTransformer(img_size=[16, 16], patch_size=4, embed_dim=32, depth=2, num_heads=2)
+        e = TrainEngine(m, EngineConfig(lr=1e-3, t_max=20, use_graph=False, seed=9, temb_rows=5), device="cpu")
+        e.set_batch_fn(ColdBatcher(synthetic_pool(16, size=(16, 16), seed=1), 4, e.rng))
+        return m, e
+
+    m, e = make()
+    for _ in range(3):
+        e.train_step()
+    sync_p, async_p = str(tmp_path / "sync.pkl"), str(tmp_path / "async.pkl")
+    best_p = str(tmp_path / "best.pkl")
+    ckpt.save_lastepoch(sync_p, m, e, 0, 3, 0.5, 0.25)
+    w = ckpt.CheckpointWriter()
+    w.submit(e.snapshot_to_host(), async_p, 0, 3, 0.5, 0.25, best_path=best_p)
+    e.train_step()  # training goes on while the file is written; the snapshot is unaffected
+    w.join()
+    a = torch.load(sync_p, weights_only=True)
+    b = torch.load(async_p, weights_only=True)
+    assert a.keys() == b.keys()
+
+    def eq(x, y):
+        if torch.is_tensor(x):
+            return torch.equal(x, y)
+        if isinstance(x, dict):
+            return x.keys() == y.keys() and all(eq(x[k], y[k]) for k in x)
+        if isinstance(x, (list, tuple)):
+            return len(x) == len(y) and all(eq(u, v) for u, v in zip(x, y))
+        return x == y
+    assert eq(a, b)
+    assert eq(ckpt.strip_prefix(a["state_dict"]), torch.load(best_p, weights_only=True))
+    finals = []
+    for path in (sync_p, async_p):
+        m2, e2 = make()
+        ckpt.load_lastepoch(path, m2, e2)
+        for _ in range(2):
+            e2.train_step()
+        finals.append((e2.flat_p.clone(), e2.flat_m.clone(), e2.step_ctr.clone()))
+    assert all(torch.equal(x, y) for x, y in zip(*finals))
+
+
+def test_checkpoint_writer_surfaces_errors(tmp_path):
+    class Bad:
+        def wait(self):
+            raise OSError("disk full (test)")
+    w = ckpt.CheckpointWriter()
+    w.submit(Bad(), str(tmp_path / "x.pkl"), 0, 0, 0.0, 0.0)
+    with pytest.raises(RuntimeError, match="disk full"):
+        w.join()
+    w.join()  # reported once

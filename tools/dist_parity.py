@@ -15,13 +15,13 @@ from ddim_cold_amd.train.engine import EngineConfig, TrainEngine
 from ddim_cold_amd.data.synthetic import ColdBatcher, GaussianBatcher, synthetic_pool
 
 
-def run(dist_mode, comm="torch", wire="fp32", gauss=False, tune=False, layout=None, signal="flag"):
+def run(dist_mode, comm="torch", wire="fp32", gauss=False, tune=False, layout=None):
     torch.manual_seed(0)
     model = build_model("vit_tiny").cuda().train()
     cfg = EngineConfig(lr=1e-3, t_max=100, seed=5, temb_rows=None if gauss else 7,
                        force_segments=dist_mode is not None,
                        graph_comm=dist_mode == "captured", comm_events=dist_mode == "events",
-                       graph_warmup=2, comm=comm, grad_wire=wire, comm_signal=signal)
+                       graph_warmup=2, comm=comm, grad_wire=wire)
     eng = TrainEngine(model, cfg)
     pool = synthetic_pool(64, seed=3, device="cuda")
     # Gaussian diffusion (t over the whole table): sparse time_embed row exchange
@@ -89,7 +89,6 @@ if __name__ == "__main__":
     evi, loss7, _, ng7 = run("events", layout="inline-1")
     evt, loss8, _, ng8 = run("events", tune=True)
     eva, loss9, _, ng9 = run("events", comm="auto", tune=True)
-    eve, loss10, _, _ = run("events", signal="event")  # event-record nodes instead of counter kernels
     dist.destroy_process_group()
     assert ng5 == 2 and ng6 == 2 and gng2 == 2, (ng5, ng6, gng2)
     assert (gref - gev).abs().max().item() <= 2 * 1e-3 * 6 and abs(gl2 - gl0) <= 1e-4 * abs(gl0), (gl0, gl2)
@@ -108,7 +107,7 @@ if __name__ == "__main__":
     for name, other, loss in (("captured", cap, loss1), ("segmented", seg, loss2), ("native", nat, loss3),
                               ("native-bf16", natb, loss4), ("events", ev, loss5), ("events-native", evn, loss6),
                               ("events-inline", evi, loss7), ("events-autotuned", evt, loss8),
-                              ("events-auto-comm-autotuned", eva, loss9), ("events-event-signal", eve, loss10)):
+                              ("events-auto-comm-autotuned", eva, loss9)):
         d = (ref - other).abs().max().item()
         assert d <= bound, (name, d)
         tol = 1e-2 if name.endswith("bf16") else 1e-4

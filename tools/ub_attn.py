@@ -14,11 +14,16 @@ for (B, H, N, hd) in SHAPES:
     qkv = (torch.randn(3, B, H, N, hd, device=dev) * 0.5).to(torch.bfloat16)
     do = (torch.randn(B, N, H * hd, device=dev)).to(torch.bfloat16)
     for p in (0.0, 0.1):
-        o, lse = ops.attn_fwd(qkv, hd ** -0.5, r, 5, p)
-        f = t(lambda: ops.attn_fwd(qkv, hd ** -0.5, r, 5, p), reps=20)
-        b = t(lambda: ops.attn_bwd(do, qkv, o, lse, hd ** -0.5, r, 5, p), reps=20)
-        fl = 4 * B * H * N * N * hd
-        res[f"B{B} H{H} N{N} hd{hd} p{p}"] = {"fwd_us": round(f, 1), "bwd_us": round(b, 1),
-                                             "fwd_TFLOPs": round(fl / f / 1e6, 1), "bwd_TFLOPs": round(2.5 * fl / b / 1e6, 1)}
+        for stored in ((False, True) if p > 0 else (False,)):
+            keep = ops.attn_keep_buffer(qkv, p) if stored else None
+            if stored and keep is None:
+                continue
+            o, lse = ops.attn_fwd(qkv, hd ** -0.5, r, 5, p, keep_out=keep)
+            f = t(lambda: ops.attn_fwd(qkv, hd ** -0.5, r, 5, p, keep_out=keep), reps=20)
+            b = t(lambda: ops.attn_bwd(do, qkv, o, lse, hd ** -0.5, r, 5, p, keep=keep), reps=20)
+            fl = 4 * B * H * N * N * hd
+            res[f"B{B} H{H} N{N} hd{hd} p{p}" + (" stored-masks" if stored else "")] = {
+                "fwd_us": round(f, 1), "bwd_us": round(b, 1),
+                "fwd_TFLOPs": round(fl / f / 1e6, 1), "bwd_TFLOPs": round(2.5 * fl / b / 1e6, 1)}
 for k, v in res.items():
     print(k, v)
