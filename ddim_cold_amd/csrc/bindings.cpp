@@ -739,15 +739,16 @@ Tensor embed_bwd(Tensor g, Tensor t, Tensor rng, int64_t site, double p, Tensor 
   return gpatch;
 }
 
-void sqnorm(Tensor g, Tensor out, double scale) {
+void sqnorm(Tensor g, Tensor out, double scale, int64_t lz_lo, int64_t lz_hi) {
   CHECK_IN(g, F32); CHECK_IN(out, F32);
   TORCH_CHECK(out.numel() >= SQ_PARTS, "sqnorm: out must hold SQ_PARTS partials");
   const c10::DeviceGuard guard(g.device());
-  sqnorm_launch(g.data_ptr<float>(), g.numel(), out.data_ptr<float>(), (float)scale, cur_stream());
+  sqnorm_launch(g.data_ptr<float>(), g.numel(), out.data_ptr<float>(), (float)scale, cur_stream(), lz_lo, lz_hi);
 }
 
 void adamw_step(Tensor p, Tensor g, Tensor m, Tensor v, c10::optional<Tensor> pbf, Tensor sq, Tensor step,
-                Tensor hyper, double grad_scale, int64_t zero_hi) {
+                Tensor hyper, double grad_scale, int64_t zero_hi, int64_t lz_lo, int64_t lz_hi,
+                c10::optional<Tensor> lazy_decay) {
   CHECK_IN(p, F32); CHECK_IN(g, F32); CHECK_IN(m, F32); CHECK_IN(v, F32); CHECK_IN(sq, F32); CHECK_IN(step, I64);
   CHECK_IN(hyper, F32);
   const c10::DeviceGuard guard(p.device());
@@ -761,9 +762,14 @@ void adamw_step(Tensor p, Tensor g, Tensor m, Tensor v, c10::optional<Tensor> pb
     TORCH_CHECK(pbf->numel() == n, "bf16 shadow size");
     pb = pbf->data_ptr();
   }
+  float* ld = nullptr;
+  if (lazy_decay.has_value() && lazy_decay->defined() && lz_hi > lz_lo) {
+    CHECK_IN((*lazy_decay), F32);
+    ld = lazy_decay->data_ptr<float>();
+  }
   adamw_launch(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), pb, n,
                sq.data_ptr<float>(), step.data_ptr<int64_t>(), hyper.data_ptr<float>(), (float)grad_scale,
-               cur_stream(), zero_hi);
+               cur_stream(), zero_hi, ld ? lz_lo : 0, ld ? lz_hi : 0, ld);
 }
 
 void advance_counters(Tensor step, Tensor rng, c10::optional<Tensor> sq) {
@@ -972,9 +978,10 @@ TORCH_LIBRARY(ddim_cold, m) {
         "Tensor? keep=None) -> Tensor");
   m.def("embed_bwd(Tensor g, Tensor t, Tensor rng, int site, float p, Tensor(a!) dcls, Tensor(b!) dpos, "
         "Tensor(c!) dtemb, Tensor(d!)? ln_ws=None, Tensor? ln_ptrs=None, int ln_C=0, bool ln_store=False) -> Tensor");
-  m.def("sqnorm(Tensor g, Tensor(a!) out, float scale) -> ()");
+  m.def("sqnorm(Tensor g, Tensor(a!) out, float scale, int lz_lo=0, int lz_hi=0) -> ()");
   m.def("adamw_step(Tensor(a!) p, Tensor(b!) g, Tensor(c!) m, Tensor(d!) v, Tensor(e!)? pbf, Tensor sq, "
-        "Tensor step, Tensor hyper, float grad_scale, int zero_hi=-1) -> ()");
+        "Tensor step, Tensor hyper, float grad_scale, int zero_hi=-1, int lz_lo=0, int lz_hi=0, "
+        "Tensor(f!)? lazy_decay=None) -> ()");
   m.def("advance_counters(Tensor(a!) step, Tensor(b!) rng, Tensor? sq) -> ()");
   m.def("ddim_step(Tensor x_t, Tensor x0_raw, Tensor coef) -> (Tensor, Tensor)");
   m.def("ddim_step_(Tensor(a!) x, Tensor x0_raw, Tensor(b!) x0_out, Tensor coef) -> ()");

@@ -192,12 +192,13 @@ void img_to_tokgrad_launch(const float* dimg, void* dtok, int B, int C, int H, i
 // sqnorm writes SQ_PARTS per-block partial sums of (g*scale)^2 (no atomics);
 // adamw / advance sum the partials themselves.
 constexpr int SQ_PARTS = 1024;
-void sqnorm_launch(const float* g, int64_t n, float* partials, float scale, hipStream_t stream);
+void sqnorm_launch(const float* g, int64_t n, float* partials, float scale, hipStream_t stream, int64_t lz_lo = 0,
+                   int64_t lz_hi = 0);
 // zero_hi: zero the gradient arena only below this element (the part that is
 // accumulated into; everything above is overwritten by its producer next step)
 void adamw_launch(float* p, float* g, float* m, float* v, void* p_bf16, int64_t n, const float* sqnorm,
                   const int64_t* step, const float* hyper, float grad_scale, hipStream_t stream,
-                  int64_t zero_hi = -1);
+                  int64_t zero_hi = -1, int64_t lz_lo = 0, int64_t lz_hi = 0, float* lazy_decay = nullptr);
 void advance_counters_launch(int64_t* step, int64_t* rng, const float* sqnorm, hipStream_t stream);
 
 // Diffusion / data (diffusion.hip)

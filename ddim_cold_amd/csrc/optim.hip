@@ -29,23 +29,35 @@ __device__ __forceinline__ float sum_parts(const float* __restrict__ parts) {
   return red[0] + red[1] + red[2] + red[3];
 }
 
-__global__ __launch_bounds__(256) void sqnorm_kernel(const float* __restrict__ g, int64_t n, float* out, float scale) {
+// Lazy range [lz_lo, lz_hi) of the arena (16-B aligned, whole vectors): parameters
+// whose gradient is identically zero for the whole run (cold diffusion's unused
+// time-embedding rows, t > log2 W).  With m = v = 0 forever, AdamW reduces to the
+// decoupled weight decay p *= (1 - lr_t wd); the kernels skip the range (no loads,
+// no stores) and the first block multiplies the pending factor into lazy_decay[0],
+// which TrainEngine.materialize_lazy() applies to the range when it is next read.
+// Vector index j of the compacted space -> arena vector index (the range removed).
+__device__ __forceinline__ int64_t lazy_map(int64_t j, int64_t lo4, int64_t len4) {
+  return j < lo4 ? j : j + len4;
+}
+
+__global__ __launch_bounds__(256) void sqnorm_kernel(const float* __restrict__ g, int64_t n, float* out, float scale,
+                                                     int64_t lo4, int64_t len4) {
   __shared__ float red[4];
   float acc = 0.f;
-  const int64_t n4 = n / 4;
+  const int64_t n4 = n / 4, nc4 = n4 - len4;
   const float4* g4 = reinterpret_cast<const float4*>(g);
   // four independent 16-byte loads in flight per thread before any use
   const int64_t st = (int64_t)gridDim.x * 256;
   int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  for (; i + 3 * st < n4; i += 4 * st) {
+  for (; i + 3 * st < nc4; i += 4 * st) {
     float4 v[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = g4[i + u * st];
+    for (int u = 0; u < 4; ++u) v[u] = g4[lazy_map(i + u * st, lo4, len4)];
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
   }
-  for (; i < n4; i += st) {
-    const float4 v = g4[i];
+  for (; i < nc4; i += st) {
+    const float4 v = g4[lazy_map(i, lo4, len4)];
     acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
   }
   for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
@@ -71,7 +83,8 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, float
                                                     float* __restrict__ v, bf16* __restrict__ pb, int64_t n,
                                                     const float* __restrict__ sqnorm, const int64_t* __restrict__ step,
                                                     const float* __restrict__ hyper, float grad_scale, bool vec,
-                                                    int64_t zero_hi) {
+                                                    int64_t zero_hi, int64_t lo4, int64_t len4,
+                                                    float* __restrict__ lazy_decay) {
   const float sq = sum_parts(sqnorm);
   const bool skip = !isfinite(sq);
   const float base_lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
@@ -86,11 +99,13 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, float
   const float step_size = lr / bc1;
   const float inv_sbc2 = 1.f / sqrtf(bc2);
   const float decay = 1.f - lr * wd;
+  if (len4 > 0 && !skip && blockIdx.x == 0 && threadIdx.x == 0) lazy_decay[0] *= decay;
   // 16-byte vectors (the arenas are allocator-aligned; `vec` is checked on the host),
   // scalar tail.  Same math per element as the scalar path.
   const int64_t nv = vec ? n / 4 : 0;
   const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += stride) {
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < nv - len4; j += stride) {
+    const int64_t i = lazy_map(j, lo4, len4);
     float4 gv = reinterpret_cast<float4*>(g)[i];
     if (4 * i < zero_hi) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (skip) continue;
@@ -143,18 +158,31 @@ static int opt_grid(int64_t n) {
   return (int)g;
 }
 
-void sqnorm_launch(const float* g, int64_t n, float* out, float scale, hipStream_t stream) {
-  hipLaunchKernelGGL(sqnorm_kernel, dim3(SQ_PARTS), dim3(256), 0, stream, g, n, out, scale);
+static void check_lazy(int64_t n, int64_t lz_lo, int64_t lz_hi) {
+  if (lz_hi > lz_lo && (lz_lo < 0 || lz_hi > n / 4 * 4 || lz_lo % 4 || lz_hi % 4))
+    throw std::runtime_error("optimizer lazy range must be whole 16-B vectors inside the arena");
+}
+
+void sqnorm_launch(const float* g, int64_t n, float* out, float scale, hipStream_t stream, int64_t lz_lo,
+                   int64_t lz_hi) {
+  check_lazy(n, lz_lo, lz_hi);
+  const int64_t len4 = lz_hi > lz_lo ? (lz_hi - lz_lo) / 4 : 0;
+  hipLaunchKernelGGL(sqnorm_kernel, dim3(SQ_PARTS), dim3(256), 0, stream, g, n, out, scale, lz_lo / 4, len4);
 }
 
 void adamw_launch(float* p, float* g, float* m, float* v, void* p_bf16, int64_t n, const float* sqnorm,
-                  const int64_t* step, const float* hyper, float grad_scale, hipStream_t stream, int64_t zero_hi) {
+                  const int64_t* step, const float* hyper, float grad_scale, hipStream_t stream, int64_t zero_hi,
+                  int64_t lz_lo, int64_t lz_hi, float* lazy_decay) {
   if (zero_hi < 0 || zero_hi > n) zero_hi = n;
   zero_hi = (zero_hi + 3) / 4 * 4 <= n ? (zero_hi + 3) / 4 * 4 : n;  // whole 16-B vectors
   auto al = [](const void* q, uintptr_t a) { return (reinterpret_cast<uintptr_t>(q) & (a - 1)) == 0; };
   const bool vec = al(p, 16) && al(g, 16) && al(m, 16) && al(v, 16) && (p_bf16 == nullptr || al(p_bf16, 8));
-  hipLaunchKernelGGL(adamw_kernel, dim3(opt_grid(n)), dim3(256), 0, stream, p, g, m, v,
-                     reinterpret_cast<bf16*>(p_bf16), n, sqnorm, step, hyper, grad_scale, vec, zero_hi);
+  check_lazy(n, lz_lo, lz_hi);
+  int64_t len4 = lz_hi > lz_lo ? (lz_hi - lz_lo) / 4 : 0;
+  if (!vec || lazy_decay == nullptr) len4 = 0;
+  hipLaunchKernelGGL(adamw_kernel, dim3(opt_grid(n - 4 * len4)), dim3(256), 0, stream, p, g, m, v,
+                     reinterpret_cast<bf16*>(p_bf16), n, sqnorm, step, hyper, grad_scale, vec, zero_hi, lz_lo / 4,
+                     len4, lazy_decay);
 }
 
 void advance_counters_launch(int64_t* step, int64_t* rng, const float* sqnorm, hipStream_t stream) {

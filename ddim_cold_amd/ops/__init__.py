@@ -437,21 +437,28 @@ def embed_bwd(g, t, rng, site: int, p: float, dcls, dpos, dtemb, ln_final=None):
 SQ_PARTS = 1024  # csrc/kernels.h
 
 
-def sqnorm(g, out, scale: float = 1.0):
-    """Per-block partial sums of (g*scale)^2 into ``out`` (>= SQ_PARTS floats, fully overwritten)."""
+def sqnorm(g, out, scale: float = 1.0, lazy=None):
+    """Per-block partial sums of (g*scale)^2 into ``out`` (>= SQ_PARTS floats, fully overwritten).
+    ``lazy`` = (lo, hi): an arena range whose gradient is identically zero (skipped)."""
+    lo, hi = lazy if lazy is not None else (0, 0)
     if _hip(g):
-        return _ops().sqnorm(g, out, float(scale))
+        return _ops().sqnorm(g, out, float(scale), int(lo), int(hi))
     out.zero_()
     out[0] = (g.float() * scale).pow(2).sum()
 
 
-def adamw_step(p, g, m, v, pbf, sq, step, hyper, grad_scale: float = 1.0, zero_hi: Optional[int] = None):
+def adamw_step(p, g, m, v, pbf, sq, step, hyper, grad_scale: float = 1.0, zero_hi: Optional[int] = None,
+               lazy=None, lazy_decay=None):
     """Fused AdamW over a flat arena (see csrc/optim.hip for the exact math).
     ``zero_hi``: zero the gradients only below this element (the producers of the
-    rest overwrite them next step); default: all."""
+    rest overwrite them next step); default: all.  ``lazy`` = (lo, hi) with
+    ``lazy_decay`` (fp32 [1]): parameters whose gradient and moments are identically
+    zero; they are not touched, their weight decay (1 - lr*wd per step) accumulates
+    into ``lazy_decay`` for ``TrainEngine.materialize_lazy``."""
+    lo, hi = lazy if lazy is not None and lazy_decay is not None else (0, 0)
     if _hip(p):
         return _ops().adamw_step(p, g, m, v, pbf, sq, step, hyper, float(grad_scale),
-                                 -1 if zero_hi is None else int(zero_hi))
+                                 -1 if zero_hi is None else int(zero_hi), int(lo), int(hi), lazy_decay)
     import math
     sqv = float(sq.sum())
     base_lr, b1, b2, eps, wd, max_norm, tmax, eta_min = (float(x) for x in hyper.tolist()[:8])
@@ -467,10 +474,15 @@ def adamw_step(p, g, m, v, pbf, sq, step, hyper, grad_scale: float = 1.0, zero_h
     lr = base_lr
     if tmax > 0:
         lr = eta_min + (base_lr - eta_min) * 0.5 * (1 + math.cos(math.pi * int(step[1]) / tmax))
+    if hi > lo:  # the lazy range: untouched, its decay accumulated (same as the kernel)
+        keep = (p[lo:hi].clone(), m[lo:hi].clone(), v[lo:hi].clone())
+        lazy_decay.mul_(1 - lr * wd)
     p.mul_(1 - lr * wd)
     m.mul_(b1).add_(gi, alpha=1 - b1)
     v.mul_(b2).addcmul_(gi, gi, value=1 - b2)
     p.addcdiv_(m, v.sqrt() / math.sqrt(bc2) + eps, value=-lr / bc1)
+    if hi > lo:
+        p[lo:hi], m[lo:hi], v[lo:hi] = keep
     if pbf is not None:
         pbf.copy_(p.to(torch.bfloat16))
 

@@ -62,6 +62,9 @@ CAPTURE_MODE = "thread_local"
 # event-split data parallel with counter hand-offs: queue the comm stream's work
 # ahead of the compute-graph replay (DDIM_COLD_PREISSUE=0: behind it)
 PREISSUE = os.environ.get("DDIM_COLD_PREISSUE", "1") != "0"
+# the LayerNorm dgamma/dbeta replica finalize rides in the embedding-backward launch
+# (False: a separate replica_reduce_ launch; tests compare the two)
+FUSE_LN_FINAL = True
 
 
 @dataclass
@@ -300,6 +303,7 @@ class TrainEngine:
 
     def close(self):
         """Release the native communicator (before the process group is destroyed)."""
+        self.materialize_lazy()
         if self.ncomm is not None:
             if self.is_cuda:
                 torch.cuda.synchronize(self.device)
@@ -395,6 +399,22 @@ class TrainEngine:
         # gradient arena below this element is accumulated (embeddings: atomics in the
         # embedding backward); above it every range has a single writer per step
         self.acc_hi = min(self.offsets[n][0] for n in self.names if n.rsplit(".", 1)[0] in ln_prefixes)
+        # time_embed rows no sample can select (t >= temb_rows: cold diffusion draws
+        # t in 1..log2 W): zero gradient and zero Adam moments for the whole run, so
+        # AdamW reduces to p *= (1 - lr wd).  The optimizer skips them and
+        # accumulates that factor on the device (lazy_decay); materialize_lazy()
+        # applies it before anything reads them (end of train_steps, snapshots,
+        # state dicts).  ~11 % of the ViT-tiny arena.
+        self.lazy = None
+        self.lazy_decay = torch.ones(1, dtype=torch.float32, device=self.device)
+        self._lazy_dirty = False
+        rows = self.cfg.temb_rows
+        if (rows is not None and 0 < rows < c.total_steps and "time_embed.weight" in self.offsets
+                and "time_embed.weight" not in self.frozen):
+            to, tn = self.offsets["time_embed.weight"]
+            lo, hi = (to + rows * c.dim + 3) // 4 * 4, (to + tn) // 4 * 4
+            if hi > lo and hi <= self.train_hi:
+                self.lazy = (lo, hi)
         # LayerNorm dgamma/dbeta replica workspace in backward order: final norm,
         # then norm2, norm1 of blocks L-1 .. 0; destinations = grad-arena views
         # (weight and bias of one LayerNorm are adjacent: one [2D] range).
@@ -541,7 +561,7 @@ class TrainEngine:
             # the LayerNorm replica finalize rides in the embedding-backward launch (data
             # parallel too: every LayerNorm lives in the last bucket's arena range)
             ln_final = None
-            if self.ln_ptrs is not None:
+            if self.ln_ptrs is not None and FUSE_LN_FINAL:
                 hi = self.ln_done_at[-1]
                 ln_final = (self.ln_ws[:hi], self.ln_ptrs[:hi], 2 * c.dim)
             # single process: every weight gradient in one launch after the backward (no
@@ -572,9 +592,10 @@ class TrainEngine:
         # optimizer: grads are SUM-reduced over ranks and summed over micro-batches
         # -> average via grad_scale
         gs = 1.0 / (self.world * k_acc)
-        ops.sqnorm(self.opt_g, self.sqnorm, gs)
+        ops.sqnorm(self.opt_g, self.sqnorm, gs, lazy=self.lazy)
         ops.adamw_step(self.opt_p, self.opt_g, self.opt_m, self.opt_v, self.opt_pb, self.sqnorm,
-                       self.step_ctr, self.hyper, gs, zero_hi=self.acc_hi if overwrite else None)
+                       self.step_ctr, self.hyper, gs, zero_hi=self.acc_hi if overwrite else None,
+                       lazy=self.lazy, lazy_decay=self.lazy_decay)
         if loss_acc is not None:
             loss_parts = loss_acc
         if tail:
@@ -801,7 +822,8 @@ class TrainEngine:
         self._eager_steps = 0
 
     def _snapshot_state(self):
-        keys = ("flat_p", "flat_g", "flat_m", "flat_v", "rng", "step_ctr", "loss_ema", "loss_last")
+        self.materialize_lazy()
+        keys = ("flat_p", "flat_g", "flat_m", "flat_v", "rng", "step_ctr", "loss_ema", "loss_last", "lazy_decay")
         return {k: getattr(self, k).clone() for k in keys}, self.steps_done
 
     def _restore_state(self, snap):
@@ -809,6 +831,7 @@ class TrainEngine:
         for k, v in tensors.items():
             getattr(self, k).copy_(v)
         self.steps_done = steps
+        self._lazy_dirty = False  # snapshots are taken materialized
         self._refresh_shadow()
 
     def autotune_comm(self, steps: int = 100, warm: int = 10, layouts=None):
@@ -997,10 +1020,12 @@ class TrainEngine:
         self._join_comm()
         gs[nb].replay()
 
-    def train_steps(self, n: int):
+    def train_steps(self, n: int, materialize: bool = True):
         """Run ``n`` optimizer steps (``batch_fn`` draws each step's batch on the device).
         With ``graph_steps = K > 1`` every run of K steps is ONE replay of a K-step
         graph; the remainder (and the eager warm-up) goes through :meth:`train_step`.
+        ``materialize``: apply the lazily accumulated weight decay afterwards (see
+        ``lazy``), so every parameter is current when the call returns.
         Returns the device loss tensor of the last step (no host sync)."""
         done = 0
         while done < n:
@@ -1008,14 +1033,30 @@ class TrainEngine:
             if multi is not None and n - done >= multi[1]:
                 multi[0].replay()
                 self.steps_done += multi[1]
+                self._lazy_dirty = True
                 done += multi[1]
             else:
-                self.train_step()
+                self.train_step(materialize=False)
                 done += 1
+        if materialize:
+            self.materialize_lazy()
         return self.loss_last
 
-    def train_step(self):
-        """Run one optimizer step on the batch produced by ``batch_fn``.
+    def materialize_lazy(self):
+        """Apply the weight decay accumulated for the ``lazy`` rows since the last call
+        (p *= prod(1 - lr_s wd); their moments are zero) and refresh their bf16 shadow."""
+        if self.lazy is None or not self._lazy_dirty:
+            return
+        lo, hi = self.lazy
+        self.flat_p[lo:hi].mul_(self.lazy_decay)
+        self.flat_pb[lo:hi].copy_(self.flat_p[lo:hi])
+        self.lazy_decay.fill_(1.0)
+        self._lazy_dirty = False
+
+    def train_step(self, materialize: bool = True):
+        """Run one optimizer step on the batch produced by ``batch_fn``
+        (``materialize``: as in :meth:`train_steps`; the trainer defers it to the
+        epoch end, where it evaluates and checkpoints).
 
         Returns the device loss tensor (no host sync)."""
         if self.batch_fn is None:
@@ -1029,6 +1070,9 @@ class TrainEngine:
             self._run_eager()
             self._eager_steps += 1
         self.steps_done += 1
+        self._lazy_dirty = True
+        if materialize:
+            self.materialize_lazy()
         return self.loss_last
 
     def step(self, x_t: torch.Tensor, target: torch.Tensor, t: torch.Tensor):
@@ -1053,6 +1097,7 @@ class TrainEngine:
 
     def optimizer_state_dict(self) -> dict:
         """torch.optim.AdamW-format state dict (interchangeable with the reference's lastepoch.pkl)."""
+        self.materialize_lazy()
         ctr = self.step_ctr.detach().cpu()
         return self._optimizer_sd(self.flat_m, self.flat_v, int(ctr[0]), int(ctr[1]))
 
@@ -1087,6 +1132,7 @@ class TrainEngine:
         stream never waits for.  ``HostSnapshot.wait()`` (the writer thread) blocks
         until the host copy has landed.  The buffers are reused: finish (wait) one
         snapshot before taking the next."""
+        self.materialize_lazy()
         cur = torch.cuda.current_stream(self.device) if self.is_cuda else None
         if getattr(self, "_snap", None) is None:
             pin = self.is_cuda
@@ -1144,10 +1190,13 @@ class TrainEngine:
 
     def sync_params_from_model(self):
         """Call after loading weights into ``model`` (its params are arena views)."""
+        self.lazy_decay.fill_(1.0)  # the loaded values are current: no decay pending
+        self._lazy_dirty = False
         self._refresh_shadow()
 
     def detach(self):
         """Release the model from the engine (params stay on the device, as plain tensors)."""
+        self.materialize_lazy()
         for n, p in self.model.named_parameters():
             p.data = p.data.clone()
             p.grad = None

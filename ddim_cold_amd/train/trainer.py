@@ -267,7 +267,7 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
         for s in range(steps_per_epoch):
             idx_dev.copy_(table[s])
             with phase("train_step"):
-                engine.train_step()
+                engine.train_step(materialize=False)  # lazy time_embed decay: applied at the epoch end
             if prof is not None:
                 prof.step()
             steps += 1
@@ -293,6 +293,7 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
                                   if engine.segmented else "") + ")", paths.log)
             if cfg.fault_inject_step and steps >= cfg.fault_inject_step and cfg.fault_inject_rank in (-1, rank):
                 raise FaultInjected(f"fault injected at step {steps} on rank {rank} (fault_inject_step)")
+        engine.materialize_lazy()
         loss_rec = float(engine.loss_ema.item())
         engine.check_comm()  # epoch end: before evaluating / checkpointing these weights
         t_ev = time.perf_counter()

@@ -365,3 +365,68 @@ def test_comm_layouts_same_training_gloo():
     for name in ("overlap-4", "inline-1", "overlap-1", "overlap-3", "overlap-7"):
         for a, b in zip(base, r[name]):
             assert torch.equal(a, b), name
+
+
+def test_lazy_time_embed_decay_matches_torch_adamw():
+    """Cold training (t in 1..6, temb_rows=7): the optimizer skips the 1,993 time_embed
+    rows no sample can select and accumulates their weight decay on the device;
+    materialised, every parameter -- those rows included -- equals torch.optim.AdamW
+    + clip + cosine on the same gradients (rows with zero gradient and moments
+    decay as p *= 1 - lr*wd)."""
+    model = _model()
+    ref_model = _model()
+    cfg = EngineConfig(lr=1e-3, t_max=5, max_grad_norm=0.05, seed=11, temb_rows=7)
+    eng = TrainEngine(model, cfg, device="cpu")
+    assert eng.lazy is not None
+    lo, hi = eng.lazy
+    o, k = eng.offsets["time_embed.weight"]
+    assert lo == o + 7 * model.embed_dim and hi == o + k
+    opt = torch.optim.AdamW(ref_model.parameters(), lr=1e-3, betas=cfg.betas, eps=cfg.eps, weight_decay=0.05)
+    sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, 5)
+    before = eng.flat_p[lo:hi].clone()
+    decay = 1.0
+    batches = [_batch(4, seed=step) for step in range(3)]
+    eng.set_batch_fn(iter([(x, y, t % 6 + 1) for x, y, t in batches]).__next__)
+    for step, (x, y, t) in enumerate(batches):
+        t = t % 6 + 1
+        g, _ = _grads(ref_model, x, y, t, torch.tensor([11, step]))
+        for n, p in ref_model.named_parameters():
+            p.grad = g[n].clone()
+        torch.nn.utils.clip_grad_norm_(ref_model.parameters(), 0.05)
+        decay *= 1 - sched.get_last_lr()[0] * 0.05
+        opt.step()
+        sched.step()
+        eng.train_step(materialize=False)
+        assert torch.equal(eng.flat_p[lo:hi], before)  # untouched while training
+        assert float(eng.lazy_decay) == pytest.approx(decay, rel=1e-6)
+    eng.materialize_lazy()
+    assert float(eng.lazy_decay) == 1.0 and not eng._lazy_dirty
+    sd_e, sd_r = model.state_dict(), ref_model.state_dict()
+    for n in sd_r:
+        assert torch.allclose(sd_e[n], sd_r[n], atol=2e-6, rtol=1e-5), n
+    assert torch.allclose(eng.flat_pb[lo:hi].float(), eng.flat_p[lo:hi].bfloat16().float())
+    # moments of the lazy rows stay exactly zero; the state dict matches torch's
+    osd = eng.optimizer_state_dict()
+    i_t = [n for n, _ in ref_model.named_parameters()].index("time_embed.weight")
+    assert torch.allclose(osd["state"][i_t]["exp_avg"], opt.state_dict()["state"][i_t]["exp_avg"], atol=1e-7)
+    assert float(osd["state"][i_t]["exp_avg"][7:].abs().max()) == 0.0
+
+
+def test_lazy_decay_snapshot_restore_and_load():
+    """A snapshot (autotune_comm / checkpoints) is taken materialised; loading weights
+    discards any pending decay."""
+    model = _model()
+    eng = TrainEngine(model, EngineConfig(lr=1e-3, t_max=50, seed=3, temb_rows=7), device="cpu")
+    x, y, t = _batch(4, seed=1)
+    eng.set_batch_fn(lambda: (x, y, t % 6 + 1))
+    eng.train_steps(2, materialize=False)
+    assert eng._lazy_dirty and float(eng.lazy_decay) < 1.0
+    snap = eng._snapshot_state()
+    assert not eng._lazy_dirty and float(eng.lazy_decay) == 1.0
+    p_mat = eng.flat_p.clone()
+    eng.train_steps(2, materialize=False)
+    eng._restore_state(snap)
+    assert torch.equal(eng.flat_p, p_mat) and float(eng.lazy_decay) == 1.0 and not eng._lazy_dirty
+    eng.train_steps(1, materialize=False)
+    eng.sync_params_from_model()
+    assert float(eng.lazy_decay) == 1.0 and not eng._lazy_dirty

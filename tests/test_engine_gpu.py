@@ -112,10 +112,12 @@ def test_multi_step_graph_matches_single_step_graph():
 @pytest.mark.gpu
 def test_ln_replica_finalize_fused_matches_separate(monkeypatch):
     """LayerNorm dgamma/dbeta replica finalize carried by the embedding-backward launch
-    (DDIM_COLD_FUSE_LNFINAL=1, default) == the separate replica_reduce_ launch (=0):
+    (engine.FUSE_LN_FINAL, default) == the separate replica_reduce_ launch:
     same LayerNorm parameters after the step, replica workspace re-zeroed."""
+    from ddim_cold_amd.train import engine as engine_mod
+
     def run(flag):
-        monkeypatch.setenv("DDIM_COLD_FUSE_LNFINAL", flag)
+        monkeypatch.setattr(engine_mod, "FUSE_LN_FINAL", flag == "1")
         torch.manual_seed(0)
         model = build_model("vit_tiny").cuda().train()
         # no clipping: LayerNorm params after one AdamW step depend only on their own grads
@@ -140,8 +142,11 @@ def test_ln_replica_finalize_fused_matches_separate(monkeypatch):
 def test_gradient_overwrite_matches_accumulate(monkeypatch):
     """Single writer per gradient range (tail weight-gradient launch and LayerNorm finalize
     store, AdamW zeroes only the embeddings) == accumulate + zero everything."""
+    orig = TrainEngine._grad_overwrite
+
     def run(flag):
-        monkeypatch.setenv("DDIM_COLD_GRAD_OVERWRITE", flag)
+        monkeypatch.setattr(TrainEngine, "_grad_overwrite",
+                            orig if flag == "1" else (lambda self, *a, **k: False))
         torch.manual_seed(0)
         model = build_model("vit_tiny").cuda().train()
         eng = TrainEngine(model, EngineConfig(lr=1e-3, t_max=100, seed=3, use_graph=True, graph_warmup=1,

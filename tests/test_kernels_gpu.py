@@ -479,6 +479,38 @@ def test_fused_adamw_matches_torch():
     assert step.tolist() == [steps, steps]
 
 
+def test_fused_adamw_lazy_range_matches_torch():
+    """Rows with identically zero gradient (cold training's unused time_embed rows) are
+    skipped by the kernels; their accumulated decay, applied once, gives torch's AdamW."""
+    torch.manual_seed(2)
+    n, lo, hi = 100_004, 20_480, 97_280
+    p0 = torch.randn(n, device=DEV)
+    pt = p0.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([pt], lr=3e-3, weight_decay=0.05)
+    sch = torch.optim.lr_scheduler.CosineAnnealingLR(opt, 10, 0.0)
+    p, g, m, v = p0.clone(), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    pb = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    sq = torch.zeros(ops.SQ_PARTS, device=DEV)
+    step = torch.zeros(2, dtype=torch.int64, device=DEV)
+    lazy_decay = torch.ones(1, device=DEV)
+    hyper = torch.tensor([3e-3, 0.9, 0.999, 1e-8, 0.05, 1.0, 10.0, 0.0], device=DEV)
+    for s in range(4):
+        grad = torch.randn(n, device=DEV) * (0.001 if s % 2 else 0.1)
+        grad[lo:hi] = 0
+        pt.grad = grad.clone()
+        torch.nn.utils.clip_grad_norm_([pt], 1.0)
+        opt.step()
+        sch.step()
+        g.copy_(grad)
+        ops.sqnorm(g, sq, 1.0, lazy=(lo, hi))
+        ops.adamw_step(p, g, m, v, pb, sq, step, hyper, 1.0, lazy=(lo, hi), lazy_decay=lazy_decay)
+        ops.advance_counters(step, rng(), sq)
+        assert torch.equal(p[lo:hi], p0[lo:hi]) and torch.all(m[lo:hi] == 0) and torch.all(v[lo:hi] == 0)
+    p[lo:hi] *= lazy_decay
+    torch.testing.assert_close(p, pt.detach(), rtol=1e-5, atol=1e-6)
+    assert torch.equal(pb[:lo], p[:lo].bfloat16()) and torch.equal(pb[hi:], p[hi:].bfloat16())
+
+
 # ------------------------------------------------------------------ diffusion / data
 def test_ddim_step():
     x = torch.randn(64, 3, 64, 64, device=DEV)
