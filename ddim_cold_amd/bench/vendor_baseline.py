@@ -9,7 +9,8 @@ comparison the hand-written stack has to win.
 * :class:`VendorTrainStep` — `multi_gpu_trainer.py:115-134` as one graph: an
   on-device cold batch draw (pool index + t ~ U{1..log2 W} + NEAREST pixelation
   pair, `diffusion_loader.py:79-97`, in plain torch ops), forward under bf16
-  autocast, ``F.smooth_l1_loss``, backward, ``clip_grad_norm_(1.0)``,
+  autocast, ``F.smooth_l1_loss`` (mean as a GEMV; bias gradients as GEMMs:
+  :class:`_AddBias`), backward, ``clip_grad_norm_(1.0)``,
   ``AdamW(wd=0.05, fused=True, capturable=True)`` with the per-iteration cosine
   LR computed on the device (``CosineAnnealingLR``'s closed form, eta_min 0).
 * :class:`VendorSampler` — the 100-step k=20 DDIM loop of `ViT.py:220-237`
@@ -33,7 +34,8 @@ import torch.nn.functional as F
 def vendor_forward(model, x: torch.Tensor, t: torch.Tensor, attn: str = "sdpa") -> torch.Tensor:
     """``model.forward_reference`` with the attention core as
     ``F.scaled_dot_product_attention`` (``attn='sdpa'``); same parameters, same
-    dropout / drop-path semantics in train mode (`ViT.py:105-137`, `:199-218`)."""
+    dropout / drop-path semantics in train mode (`ViT.py:105-137`, `:199-218`).
+    Linear layers go through :func:`_linear` (bias gradient as a GEMM)."""
     if attn == "explicit":
         return model.forward_reference(x, t)
     tr = model.training
@@ -42,15 +44,53 @@ def vendor_forward(model, x: torch.Tensor, t: torch.Tensor, attn: str = "sdpa") 
         a = blk.attn
         B, N, C = h.shape
         H = a.num_heads
-        qkv = a.qkv(blk.norm1(h)).view(B, N, 3, H, C // H).permute(2, 0, 3, 1, 4)
+        qkv = _linear(a.qkv, blk.norm1(h)).view(B, N, 3, H, C // H).permute(2, 0, 3, 1, 4)
         p = a.attn_drop.p if tr else 0.0
         y = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], dropout_p=p, scale=a.scale)
         y = y.transpose(1, 2).reshape(B, N, C)
-        h = h + blk.drop_path(_drop(a.proj(y), a.proj_drop.p, tr))
+        h = h + blk.drop_path(_drop(_linear(a.proj, y), a.proj_drop.p, tr))
         m = blk.mlp
-        z = m.fc2(_drop(m.act(m.fc1(blk.norm2(h))), m.drop.p, tr))
+        z = _linear(m.fc2, _drop(m.act(_linear(m.fc1, blk.norm2(h))), m.drop.p, tr))
         h = h + blk.drop_path(_drop(z, m.drop.p, tr))
-    return model.unpatchify(model.head(model.norm(h))[:, 1:, :])
+    return model.unpatchify(_linear(model.head, model.norm(h))[:, 1:, :])
+
+
+class _AddBias(torch.autograd.Function):
+    """y = x + b (b broadcast over the rows) whose bias gradient is a GEMM, ones^T dy,
+    instead of ATen's column reduction.  Captured in one graph with the stock
+    reductions (``nn.Linear`` bias gradients, ``F.smooth_l1_loss``'s mean), the step
+    read stale or garbage reduction outputs from the second replay on: negative
+    "smooth-L1 losses" from replay 2, NaN parameters after ~20 back-to-back replays,
+    while the same step run eagerly trained normally (tools/vendor_debug.py; a lone
+    1M-element ``x.sum()`` graph does replay correctly, so it is specific to the
+    reductions of the step).  With the bias gradients and the loss mean as GEMMs
+    the graph-replayed step tracks the eager one (loss 0.03-0.045 over 300 replays,
+    every parameter finite)."""
+
+    @staticmethod
+    def forward(ctx, x, b):
+        ctx.bshape, ctx.bdtype = b.shape, b.dtype
+        return x + b.to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        g2 = g.reshape(-1, g.shape[-1]).float()
+        ones = torch.ones(1, g2.shape[0], device=g.device, dtype=torch.float32)
+        return g, (ones @ g2).reshape(ctx.bshape).to(ctx.bdtype)
+
+
+def _linear(mod, x):
+    """``nn.Linear`` forward (same weight / bias, bf16 under autocast) with the bias
+    gradient of :class:`_AddBias`."""
+    y = F.linear(x, mod.weight)
+    return _AddBias.apply(y, mod.bias) if mod.bias is not None else y
+
+
+def _mean(x: torch.Tensor) -> torch.Tensor:
+    """Mean as a GEMV (replays correctly inside a captured graph, see :class:`_AddBias`)."""
+    flat = x.reshape(1, -1)
+    ones = torch.ones(flat.shape[1], 1, device=x.device, dtype=x.dtype)
+    return (flat @ ones).reshape(()) * (1.0 / flat.shape[1])
 
 
 def _drop(x, p, training):
@@ -133,7 +173,7 @@ class VendorTrainStep:
         x_t, target, t = cold_batch_torch(self.pool, self.batch, self.max_t)
         with torch.autocast(self.dev.type, dtype=torch.bfloat16, enabled=self.cuda, cache_enabled=False):
             pred = vendor_forward(self.model, x_t, t, self.attn)
-        loss = F.smooth_l1_loss(pred.float(), target)
+        loss = _mean(F.smooth_l1_loss(pred.float(), target, reduction="none"))
         loss.backward()
         torch.nn.utils.clip_grad_norm_(self.params, self.clip)
         if self.cuda:

@@ -11,6 +11,7 @@
 #include <c10/core/DeviceGuard.h>
 
 #include "kernels.h"
+#include <algorithm>
 #include <cstdlib>
 
 using at::Tensor;
@@ -570,6 +571,14 @@ void linear_wgrad(Tensor dy, Tensor x, Tensor dw, c10::optional<Tensor> db) {
 // (db_i += colsum dy_i).  The token reduction is split over fp32 atomics (2-way
 // for a full block group, more for small groups); splits == 1 would use a plain
 // read-add-write epilogue.
+// grad-norm partial buffers: every partial is written (sqnorm: one block each; the
+// fused weight-gradient launch: tiles + tail, rest zeroed) and summed by consumers
+int check_parts(const Tensor& t, const char* who) {
+  TORCH_CHECK(t.numel() >= SQ_PARTS && t.numel() % 256 == 0 && t.numel() < (1 << 24), who,
+              ": grad-norm partials must be >= SQ_PARTS floats, a multiple of 256");
+  return (int)t.numel();
+}
+
 static std::vector<GemmArgs> wgrad_probs(const std::vector<Tensor>& dys, const std::vector<Tensor>& xs,
                                          const std::vector<Tensor>& dws,
                                          const std::vector<c10::optional<Tensor>>& dbs, int* tiles_out,
@@ -606,12 +615,62 @@ static std::vector<GemmArgs> wgrad_probs(const std::vector<Tensor>& dys, const s
 }
 
 // Every weight gradient of a training step in ONE launch (gemm_wgrad_multi_kernel)
+// sq_parts / arena: also write the grad-norm partials of the whole gradient arena
+// (the launch must then be its last writer): the arena ranges outside every dW / db
+// target and outside the lazy range [lz_lo, lz_hi) go to the tail workgroups
 void linear_wgrad_multi(std::vector<Tensor> dys, std::vector<Tensor> xs, std::vector<Tensor> dws,
-                        std::vector<c10::optional<Tensor>> dbs, bool store) {
+                        std::vector<c10::optional<Tensor>> dbs, bool store, c10::optional<Tensor> sq_parts,
+                        c10::optional<Tensor> arena, int64_t lz_lo, int64_t lz_hi) {
   TORCH_CHECK(!dys.empty() && dys.size() <= 32, "wgrad_multi: 1..32 problems");
   const c10::DeviceGuard guard(dys[0].device());
-  std::vector<GemmArgs> probs = wgrad_probs(dys, xs, dws, dbs, nullptr, nullptr);
-  gemm_wgrad_multi(probs.data(), (int)probs.size(), cur_stream(), store);
+  int tiles = 0;
+  std::vector<GemmArgs> probs = wgrad_probs(dys, xs, dws, dbs, &tiles, nullptr);
+  if (!(sq_parts.has_value() && sq_parts->defined())) {
+    gemm_wgrad_multi(probs.data(), (int)probs.size(), cur_stream(), store);
+    return;
+  }
+  TORCH_CHECK(arena.has_value() && arena->defined(), "wgrad_multi: grad-norm partials need the gradient arena");
+  CHECK_IN((*sq_parts), F32); CHECK_IN((*arena), F32);
+  const int np = check_parts(*sq_parts, "wgrad_multi");
+  const float* base = arena->data_ptr<float>();
+  const int64_t n = arena->numel();
+  // element intervals of the targets inside the arena
+  std::vector<std::pair<int64_t, int64_t>> iv;
+  auto add = [&](const Tensor& t) {
+    TORCH_CHECK(t.is_contiguous(), "wgrad_multi: grad-norm fusion needs contiguous targets");
+    const int64_t off = t.data_ptr<float>() - base;
+    TORCH_CHECK(off >= 0 && off + t.numel() <= n, "wgrad_multi: a weight-gradient target lies outside the arena");
+    iv.emplace_back(off, off + t.numel());
+  };
+  for (size_t i = 0; i < dws.size(); ++i) {
+    add(dws[i]);
+    if (dbs[i].has_value() && dbs[i]->defined()) add(*dbs[i]);
+  }
+  if (lz_hi > lz_lo) iv.emplace_back(lz_lo, lz_hi);
+  std::sort(iv.begin(), iv.end());
+  WgradSq sq;
+  sq.parts = sq_parts->data_ptr<float>();
+  sq.nparts = np;
+  sq.base = base;
+  int64_t cur = 0, rest = 0;
+  auto gap = [&](int64_t lo, int64_t hi) {
+    if (hi <= lo) return;
+    TORCH_CHECK(sq.nr < WSQ_MAX_RANGES, "wgrad_multi: more than 16 arena ranges outside the weight gradients");
+    sq.lo[sq.nr] = lo;
+    sq.hi[sq.nr] = hi;
+    ++sq.nr;
+    rest += hi - lo;
+  };
+  for (const auto& [lo, hi] : iv) {
+    TORCH_CHECK(lo >= cur, "wgrad_multi: overlapping weight-gradient targets (the partials would count them twice)");
+    gap(cur, lo);
+    cur = std::max(cur, hi);
+  }
+  gap(cur, n);
+  sq.tail = (int)std::min<int64_t>(64, std::max<int64_t>(1, (rest + 256 * 16 - 1) / (256 * 16)));
+  TORCH_CHECK(tiles + sq.tail <= np, "wgrad_multi: grad-norm partial buffer too small (", np, " < ", tiles, " tiles + ",
+              sq.tail, ")");
+  gemm_wgrad_multi(probs.data(), (int)probs.size(), cur_stream(), store, &sq);
 }
 
 // fp32 <-> bf16 gradient wire (csrc/comm_wire.hip): one fused 16-B-vector
@@ -741,9 +800,9 @@ Tensor embed_bwd(Tensor g, Tensor t, Tensor rng, int64_t site, double p, Tensor 
 
 void sqnorm(Tensor g, Tensor out, double scale, int64_t lz_lo, int64_t lz_hi) {
   CHECK_IN(g, F32); CHECK_IN(out, F32);
-  TORCH_CHECK(out.numel() >= SQ_PARTS, "sqnorm: out must hold SQ_PARTS partials");
+  const int np = check_parts(out, "sqnorm");
   const c10::DeviceGuard guard(g.device());
-  sqnorm_launch(g.data_ptr<float>(), g.numel(), out.data_ptr<float>(), (float)scale, cur_stream(), lz_lo, lz_hi);
+  sqnorm_launch(g.data_ptr<float>(), g.numel(), out.data_ptr<float>(), np, (float)scale, cur_stream(), lz_lo, lz_hi);
 }
 
 void adamw_step(Tensor p, Tensor g, Tensor m, Tensor v, c10::optional<Tensor> pbf, Tensor sq, Tensor step,
@@ -755,7 +814,7 @@ void adamw_step(Tensor p, Tensor g, Tensor m, Tensor v, c10::optional<Tensor> pb
   const int64_t n = p.numel();
   TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n && hyper.numel() >= 8 && step.numel() >= 2,
               "adamw shapes");
-  TORCH_CHECK(sq.numel() >= SQ_PARTS, "adamw: sq must hold SQ_PARTS partials");
+  const int np = check_parts(sq, "adamw");
   void* pb = nullptr;
   if (pbf.has_value() && pbf->defined()) {
     CHECK_IN((*pbf), BF16);
@@ -768,7 +827,7 @@ void adamw_step(Tensor p, Tensor g, Tensor m, Tensor v, c10::optional<Tensor> pb
     ld = lazy_decay->data_ptr<float>();
   }
   adamw_launch(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), pb, n,
-               sq.data_ptr<float>(), step.data_ptr<int64_t>(), hyper.data_ptr<float>(), (float)grad_scale,
+               sq.data_ptr<float>(), np, step.data_ptr<int64_t>(), hyper.data_ptr<float>(), (float)grad_scale,
                cur_stream(), zero_hi, ld ? lz_lo : 0, ld ? lz_hi : 0, ld);
 }
 
@@ -776,12 +835,13 @@ void advance_counters(Tensor step, Tensor rng, c10::optional<Tensor> sq) {
   CHECK_IN(step, I64); check_rng(rng);
   const c10::DeviceGuard guard(step.device());
   const float* s = nullptr;
+  int np = 0;
   if (sq.has_value() && sq->defined()) {
     CHECK_IN((*sq), F32);
-    TORCH_CHECK(sq->numel() >= SQ_PARTS, "advance: sq must hold SQ_PARTS partials");
+    np = check_parts(*sq, "advance");
     s = sq->data_ptr<float>();
   }
-  advance_counters_launch(step.data_ptr<int64_t>(), rng.data_ptr<int64_t>(), s, cur_stream());
+  advance_counters_launch(step.data_ptr<int64_t>(), rng.data_ptr<int64_t>(), s, np, cur_stream());
 }
 
 std::tuple<Tensor, Tensor> ddim_step(Tensor x_t, Tensor x0_raw, Tensor coef) {
@@ -915,7 +975,7 @@ void ln_fold_(std::vector<Tensor> ws, std::vector<Tensor> gammas, std::vector<Te
     TORCH_CHECK(loss_parts.has_value() && loss_parts->defined() && sq.has_value() && sq->defined(),
                 "step tail needs loss_parts and sq");
     CHECK_IN((*loss_parts), F32); CHECK_IN((*sq), F32);
-    TORCH_CHECK(sq->numel() >= SQ_PARTS, "sq must hold SQ_PARTS partials");
+    tb.sq_n = check_parts(*sq, "ln_fold_ tail");
     tb.tail = 1;
     tb.loss_parts = loss_parts->data_ptr<float>();
     tb.loss_nparts = (int)loss_parts->numel();
@@ -966,7 +1026,8 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("linear_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, Tensor(b!)? db) -> ()");
   m.def("wire_pack(Tensor src, Tensor(a!) dst) -> ()");
   m.def("wire_unpack(Tensor src, Tensor(a!) dst) -> ()");
-  m.def("linear_wgrad_multi(Tensor[] dys, Tensor[] xs, Tensor(a!)[] dws, Tensor(b!)?[] dbs, bool store=False) -> ()");
+  m.def("linear_wgrad_multi(Tensor[] dys, Tensor[] xs, Tensor(a!)[] dws, Tensor(b!)?[] dbs, bool store=False, "
+        "Tensor(c!)? sq_parts=None, Tensor? arena=None, int lz_lo=0, int lz_hi=0) -> ()");
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor? g_res, "
         "Tensor(a!) dgamma, Tensor(b!) dbeta, int N, Tensor rng, int site_drop, float p_drop, int site_dp, "
         "float p_dp, bool emit_gy, Tensor(c!)? ws=None, Tensor? beta=None, Tensor(d!)? y_out=None) -> (Tensor, Tensor)");

@@ -15,6 +15,120 @@
 
 namespace dc {
 
+// pix_src(x, n, f) with the two nearest-neighbour scales of one pixelation factor
+// computed once (same float expressions, so the same source index)
+struct PixMap {
+  float s_in, s_out;
+  int ts, n;
+  __device__ PixMap(int n_, int f) : n(n_) {
+    ts = n_ / f;
+    if (ts < 1) ts = 1;
+    s_in = (float)ts / (float)n_;
+    s_out = (float)n_ / (float)ts;
+  }
+  __device__ __forceinline__ int operator()(int x) const {
+    int s = (int)floorf((float)x * s_in);
+    s = s < ts - 1 ? s : ts - 1;
+    const int d = (int)floorf((float)s * s_out);
+    return d < n - 1 ? d : n - 1;
+  }
+};
+
+template <int PT>
+__device__ __forceinline__ void patch_segments(const float* __restrict__ img, bf16* __restrict__ patches, int B, int C,
+                                               int H, int W, int NP, int Wp, uint32_t csalt, uint32_t nsalt,
+                                               int patch_blocks, const ColdSrc& cs, int P_rt = 0) {
+  constexpr int PMAX = PT ? PT : 32;
+  const int P = PT ? PT : P_rt;
+  const int PP = P * P, F = C * PP;
+  const int nseg = B * NP * C * P;
+  for (int u = blockIdx.x * blockDim.x + threadIdx.x; u < nseg; u += patch_blocks * blockDim.x) {
+    const int r1 = u / P, i = u - r1 * P;
+    const int row = r1 / C, c = r1 - row * C;
+    const int b = row / NP, pidx = row - b * NP;
+    const int hp = pidx / Wp, wp = pidx - hp * Wp;
+    const int y = hp * P + i, x0 = wp * P;
+    const size_t o = (((size_t)b * C + c) * H + y) * W + x0;  // image index of element j = 0
+    float v[PMAX];
+    if (cs.pool) {
+      const int src = cs.draw_idx ? cold_draw_idx(csalt, b, cs.pool_n) : (int)cs.idx[b];
+      const float* im = cs.pool + ((size_t)src * C + c) * H * W;
+      float* tg = cs.target + (cs.target_rows ? (size_t)row * F + (size_t)i * P * C + c : o);
+      const int tstride = cs.target_rows ? C : 1;
+      if (cs.gauss_T) {
+        // Gaussian DDIM batch fused in: x_t = sqrt(a_t) x0 + sqrt(1-a_t) eps straight
+        // into the patch row, target = x0 (gauss_batch_kernel's values)
+        const int tt = gauss_draw_t(csalt, b, cs.gauss_T);
+        float sa, s1a;
+        gauss_coef(tt, cs.gauss_T, sa, s1a);
+        const float* ir = im + (size_t)y * W + x0;
+#pragma unroll
+        for (int j = 0; j < PMAX; ++j) {
+          if (!PT && j >= P) break;
+          const float x0v = ir[j];
+          v[j] = sa * x0v + s1a * gauss_eps(nsalt, (uint32_t)(o + j));
+          tg[j * tstride] = x0v;
+        }
+      } else {
+        // cold batch fused in: pixelate the pool image straight into the patch row
+        // (x_t) and write the target image (x_{t-1}, or x0) -- same values as
+        // cold_batch_kernel + the image path, one launch fewer
+        const int tt = cold_draw_t(csalt, b, cs.max_t);
+        const PixMap m1(W, 1 << tt);
+        const float* r1p = im + (size_t)PixMap(H, 1 << tt)(y) * W;
+        if (cs.target_x0) {
+          const float* ir = im + (size_t)y * W + x0;
+#pragma unroll
+          for (int j = 0; j < PMAX; ++j) {
+            if (!PT && j >= P) break;
+            tg[j * tstride] = ir[j];
+          }
+        } else {
+          const PixMap m0(W, 1 << (tt - 1));
+          const float* r0p = im + (size_t)PixMap(H, 1 << (tt - 1))(y) * W;
+#pragma unroll
+          for (int j = 0; j < PMAX; ++j) {
+            if (!PT && j >= P) break;
+            tg[j * tstride] = r0p[m0(x0 + j)];
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < PMAX; ++j) {
+          if (!PT && j >= P) break;
+          v[j] = r1p[m1(x0 + j)];
+        }
+      }
+      if (cs.x_t) {
+#pragma unroll
+        for (int j = 0; j < PMAX; ++j) {
+          if (!PT && j >= P) break;
+          cs.x_t[o + j] = v[j];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < PMAX; ++j) {
+        if (!PT && j >= P) break;
+        v[j] = img[o + j];
+      }
+    }
+    bf16* dst = patches + (size_t)row * F + c * PP + i * P;
+    if constexpr (PT == 8) {
+      bf16x8 w;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w[j] = f2bf(v[j]);
+      *reinterpret_cast<bf16x8*>(dst) = w;
+    } else if constexpr (PT == 4) {
+      bf16x4 w;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = f2bf(v[j]);
+      *reinterpret_cast<bf16x4*>(dst) = w;
+    } else {
+      for (int j = 0; j < P; ++j) dst[j] = f2bf(v[j]);
+    }
+  }
+}
+
 // LayerNorm fold (gemm.hip): with `st` (the first LayerNorm's row statistics,
 // [B*N][D/32][2] slots) the cls-row blocks write their rows' complete
 // {sum, sum^2} into slot 0 (the other slots zero) plus the rows' bf16 copy; the
@@ -73,45 +187,14 @@ __global__ __launch_bounds__(256) void patchify_cls_kernel(const float* __restri
     }
     return;
   }
-  const size_t n_patch = (size_t)B * NP * F;
-  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < n_patch;
-       e += (size_t)patch_blocks * blockDim.x) {
-    const int k = (int)(e % F);
-    const size_t row = e / F;
-    const int b = (int)(row / NP), pidx = (int)(row % NP);
-    const int hp = pidx / Wp, wp = pidx - hp * Wp;
-    const int c = k / (P * P), ij = k - c * P * P, i = ij / P, j = ij - i * P;
-    const int y = hp * P + i, xx = wp * P + j;
-    if (cs.pool && cs.gauss_T) {
-      // Gaussian DDIM batch fused in: x_t = sqrt(a_t) x0 + sqrt(1-a_t) eps straight
-      // into the patch row, target = x0 (gauss_batch_kernel's values)
-      const int src = cs.draw_idx ? cold_draw_idx(csalt, b, cs.pool_n) : (int)cs.idx[b];
-      const int tt = gauss_draw_t(csalt, b, cs.gauss_T);
-      float sa, s1a;
-      gauss_coef(tt, cs.gauss_T, sa, s1a);
-      const size_t o = (((size_t)b * C + c) * H + y) * W + xx;
-      const float x0 = cs.pool[((size_t)src * C + c) * H * W + (size_t)y * W + xx];
-      const float xt = sa * x0 + s1a * gauss_eps(nsalt, (uint32_t)o);
-      cs.target[cs.target_rows ? row * F + (size_t)ij * C + c : o] = x0;
-      if (cs.x_t) cs.x_t[o] = xt;
-      patches[e] = f2bf(xt);
-    } else if (cs.pool) {
-      // cold batch fused in: pixelate the pool image straight into the patch row
-      // (x_t) and write the target image (x_{t-1}, or x0) -- same values as
-      // cold_batch_kernel + this kernel's image path, one launch fewer
-      const int src = cs.draw_idx ? cold_draw_idx(csalt, b, cs.pool_n) : (int)cs.idx[b];
-      const int tt = cold_draw_t(csalt, b, cs.max_t);
-      const float* im = cs.pool + ((size_t)src * C + c) * H * W;
-      const int f1 = 1 << tt, f0 = cs.target_x0 ? 1 : 1 << (tt - 1);
-      const float xt = im[(size_t)pix_src(y, H, f1) * W + pix_src(xx, W, f1)];
-      const size_t o = (((size_t)b * C + c) * H + y) * W + xx;
-      cs.target[cs.target_rows ? row * F + (size_t)ij * C + c : o] =
-          cs.target_x0 ? im[(size_t)y * W + xx] : im[(size_t)pix_src(y, H, f0) * W + pix_src(xx, W, f0)];
-      if (cs.x_t) cs.x_t[o] = xt;
-      patches[e] = f2bf(xt);
-    } else {
-      patches[e] = f2bf(img[(((size_t)b * C + c) * H + y) * W + xx]);
-    }
+  // patch rows: one thread per segment (row, c, i) = the P contiguous row elements
+  // k = c*P*P + i*P + j (one image row of one patch channel): the index split, the
+  // per-sample draw and the pixelation scales are paid once per segment, the P bf16
+  // values leave as one vector store
+  switch (P) {
+    case 8: patch_segments<8>(img, patches, B, C, H, W, NP, Wp, csalt, nsalt, patch_blocks, cs); break;
+    case 4: patch_segments<4>(img, patches, B, C, H, W, NP, Wp, csalt, nsalt, patch_blocks, cs); break;
+    default: patch_segments<0>(img, patches, B, C, H, W, NP, Wp, csalt, nsalt, patch_blocks, cs, P); break;
   }
 }
 
@@ -265,7 +348,10 @@ using namespace dc;
 void patchify_cls_launch(const float* img, const int64_t* t, const float* cls, const float* pos, const float* temb,
                          void* patches, float* x, int B, int C, int H, int W, int patch, int D, const int64_t* rng,
                          int site, double p, float* st, void* xb, hipStream_t stream, ColdSrc cs) {
-  const size_t n = (size_t)B * (H / patch) * (W / patch) * C * patch * patch;
+  // one thread per patch-row segment of `patch` elements (patch_segments)
+  const size_t n = (size_t)B * (H / patch) * (W / patch) * C * patch;
+  if (patch > 32) throw std::invalid_argument("patchify: patch size > 32");
+  if (n >= (size_t)INT32_MAX) throw std::invalid_argument("patchify: too many patch-row segments for 32-bit indexing");
   const uint32_t thr = drop_threshold_host(p);
   const float dsc = p > 0 ? 1.f / (1.f - (float)p) : 1.f;
   const int pb = grid_for(n);

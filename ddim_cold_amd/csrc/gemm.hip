@@ -343,6 +343,7 @@ __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int t
   if (WG && do_db) mainloop(std::true_type{});
   else mainloop(std::false_type{});
 
+  float dbsq = 0.f;  // ACC with sq_parts: this lane's bias-gradient squares
   if (WG && do_db && li == 0) {
     float* db = const_cast<float*>(p.bias);
     float old[FM][4];
@@ -359,14 +360,33 @@ __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int t
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm * TM + i * 16 + 4 * g + r;
         if (m < p.M) {
-          if (EPI == EPI_ATOMIC) atomicAdd(db + m, dbacc[i][r]);
-          else db[m] = old[i][r] + dbacc[i][r];
+          if (EPI == EPI_ATOMIC) {
+            atomicAdd(db + m, dbacc[i][r]);
+          } else {
+            const float o = old[i][r] + dbacc[i][r];
+            db[m] = o;
+            dbsq += o * o;
+          }
         }
       }
   }
 
   if (VEC) ep.finish(p, acc, li);
   else run_epilogue_scalar<EPI, FM, FN>(p, acc, m0 + wm * TM, n0 + wn * TN, g, li);
+  if constexpr (EPI == EPI_ACC && VEC) {
+    if (p.sq_parts) {  // the workgroup's grad-norm partial (fixed reduction order)
+      __shared__ float sred[WM * WN];
+      const float s = wave_sum(ep.sqacc + dbsq);
+      if (lane == 0) sred[wave] = s;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM * WN; ++w) t += sred[w];
+        p.sq_parts[p.sq_slot] = t;
+      }
+    }
+  }
 }
 
 template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EPI, int S>
@@ -555,6 +575,7 @@ DC_INST_DMA(64, true, true, EPI_ATOMIC)
 // must stay under 4 KiB); one token split, so the epilogue is a plain
 // read-add-write (EPI_ACC: deterministic, no fp32 atomics).
 constexpr int WM_MAX = 32;
+constexpr int BIG_WG_K = 16384;  // tokens: 128 x 128 weight-gradient tiles from here
 struct WgDesc {
   const bf16* A;
   const bf16* B;
@@ -567,10 +588,42 @@ struct WgradMulti {
   int tile_start[WM_MAX + 1];
   int n;
   int store;  // every target is zero: plain stores (no read-add)
+  WgradSq sq;  // sq.parts != nullptr: grad-norm partials (kernels.h)
 };
-template <int T, int S, int TN = T>
-__global__ __launch_bounds__(256) void gemm_wgrad_multi_kernel(WgradMulti gm) {
-  const int bid = xcd_remap(blockIdx.x, gm.tile_start[gm.n]);
+// tail workgroup j of the fused grad-norm: squares of the arena ranges no tile
+// writes, then zero the unused partial slots
+template <int NT>
+__device__ __forceinline__ void wgrad_sq_tail(const WgradSq& sq, int tiles, int j) {
+  float s = 0.f;
+  const int64_t stride = (int64_t)sq.tail * NT;
+  for (int r = 0; r < sq.nr; ++r)
+    for (int64_t i = sq.lo[r] + (int64_t)j * NT + threadIdx.x; i < sq.hi[r]; i += stride) {
+      const float v = sq.base[i];
+      s += v * v;
+    }
+  __shared__ float red[NT / 64];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) t += red[w];
+    sq.parts[tiles + j] = t;
+  }
+  for (int i = tiles + sq.tail + j * NT + threadIdx.x; i < sq.nparts; i += sq.tail * NT) sq.parts[i] = 0.f;
+}
+// T x TN output tiles of WM x WN waves: 64 x 64 / 4 waves (ViT-tiny, sampler-sized
+// token counts), 128 x 128 / 8 waves when the reduction runs over >= BIG_WG_K tokens
+// (vit_small_200: 20,032; half the operand bytes per MFMA, ~5 tiles per CU)
+template <int T, int S, int TN = T, int WM = 2, int WN = 2>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_wgrad_multi_kernel(WgradMulti gm) {
+  const int tiles = gm.tile_start[gm.n];
+  if ((int)blockIdx.x >= tiles) {
+    wgrad_sq_tail<64 * WM * WN>(gm.sq, tiles, blockIdx.x - tiles);
+    return;
+  }
+  const int bid = xcd_remap(blockIdx.x, tiles);
   int lo = 0, hi = gm.n - 1;  // problem owning tile `bid`: binary search over tile_start
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -582,13 +635,16 @@ __global__ __launch_bounds__(256) void gemm_wgrad_multi_kernel(WgradMulti gm) {
   p.A = d.A; p.B = d.B; p.C = d.C; p.bias = d.bias;
   p.M = d.M; p.N = d.N; p.K = d.K; p.lda = d.lda; p.ldb = d.ldb; p.ldc = d.ldc;
   p.acc_store = gm.store;
+  p.sq_parts = gm.sq.parts;
+  p.sq_slot = bid;
   p.ktiles_per_split = (d.K + BK - 1) / BK;
   const int tiles_n = (d.N + TN - 1) / TN;
   const int local = bid - gm.tile_start[lo];
   const int tm = local / tiles_n;
-  gemm_dma_body<T, TN, 2, 2, true, true, EPI_ACC, S>(p, tm, local - tm * tiles_n, 0);
+  gemm_dma_body<T, TN, WM, WN, true, true, EPI_ACC, S>(p, tm, local - tm * tiles_n, 0);
 }
 template __global__ void gemm_wgrad_multi_kernel<64, 3>(WgradMulti);
+template __global__ void gemm_wgrad_multi_kernel<128, 4, 128, 4, 2>(WgradMulti);
 
 }  // namespace dc
 
@@ -709,17 +765,21 @@ void gemm_wgrad(const GemmArgs& a, int splits, hipStream_t stream) {
   launch_auto<true, true, EPI_ATOMIC>(p, splits, stream);
 }
 
-void gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool store) {
+void gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool store, const WgradSq* sq) {
   if (n < 1 || n > WM_MAX) throw std::runtime_error("gemm_wgrad_multi: 1..32 problems per launch");
   WgradMulti gm{};
   gm.n = n;
   gm.store = store ? 1 : 0;
   int tiles = 0;
-  // 64 x 64 tiles, 3-stage ring (48 KiB: three workgroups per CU).  Measured
-  // slower and removed: 128 x 128 tiles (half the operand bytes per output, one
-  // 96 KiB workgroup per CU, ~390 workgroups in 1.5 rounds: 0.838 vs 0.824
-  // ms/step), 128 x 64 tiles (24 % fewer operand bytes, same 60-61 us launch),
-  // a 4-stage ring (0.833).
+  // ViT-tiny-sized token counts: 64 x 64 tiles, 3-stage ring (48 KiB: three
+  // workgroups per CU).  Measured slower there and not used: 128 x 128 tiles (half the
+  // operand bytes per output, one 96 KiB workgroup per CU, ~390 workgroups in 1.5
+  // rounds: 0.838 vs 0.824 ms/step), 128 x 64 tiles (24 % fewer operand bytes, same
+  // 60-61 us launch), a 4-stage ring (0.833).  Long reductions (>= BIG_WG_K tokens,
+  // vit_small_200) take 128 x 128 tiles of 8 waves with a 4-stage 128 KiB ring.
+  int kmax = 0;
+  for (int i = 0; i < n; ++i) kmax = std::max(kmax, probs[i].K);
+  const int T = kmax >= BIG_WG_K ? 128 : 64;
   for (int i = 0; i < n; ++i) {
     const GemmArgs& a = probs[i];
     if (a.N % 4 != 0) throw std::runtime_error("gemm_wgrad_multi: output width must be a multiple of 4");
@@ -728,9 +788,23 @@ void gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool sto
     d.C = reinterpret_cast<float*>(a.C); d.bias = const_cast<float*>(a.bias);
     d.M = a.M; d.N = a.N; d.K = a.K; d.lda = a.lda; d.ldb = a.ldb; d.ldc = a.ldc;
     gm.tile_start[i] = tiles;
-    tiles += ((a.M + 63) / 64) * ((a.N + 63) / 64);
+    tiles += ((a.M + T - 1) / T) * ((a.N + T - 1) / T);
   }
   for (int i = n; i <= WM_MAX; ++i) gm.tile_start[i] = tiles;
-  hipLaunchKernelGGL((gemm_wgrad_multi_kernel<64, 3>), dim3(tiles), dim3(256), 3 * (64 * 128 + 64 * 128), stream, gm);
+  int extra = 0;
+  if (sq != nullptr && sq->parts != nullptr) {
+    if (sq->tail < 1 || sq->nr < 0 || sq->nr > WSQ_MAX_RANGES || sq->nparts < tiles + sq->tail)
+      throw std::runtime_error("gemm_wgrad_multi: grad-norm partials need nparts >= tiles + tail and <= 16 ranges");
+    gm.sq = *sq;
+    extra = sq->tail;
+  }
+  static_assert(sizeof(WgradMulti) <= 4000, "kernel argument block");
+  if (T == 128) {
+    constexpr int lds = 4 * 2 * 128 * 128;  // 4 stages x (A + B) 128-wide, 64-deep images
+    hipLaunchKernelGGL((gemm_wgrad_multi_kernel<128, 4, 128, 4, 2>), dim3(tiles + extra), dim3(512), lds, stream, gm);
+  } else {
+    hipLaunchKernelGGL((gemm_wgrad_multi_kernel<64, 3>), dim3(tiles + extra), dim3(256), 3 * (64 * 128 + 64 * 128),
+                       stream, gm);
+  }
 }
 

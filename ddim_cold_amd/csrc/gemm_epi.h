@@ -79,6 +79,8 @@ struct GemmParams {
   bf16* patch_out;
   const float* cls_src;
   int acc_store;  // EPI_ACC: the target is known to be zero -- store, don't read-add
+  float* sq_parts;  // EPI_ACC: sum of squares of this workgroup's final outputs -> sq_parts[sq_slot]
+  int sq_slot;
   uint32_t tok_magic;  // floor(2^32 / tokens) (divmagic: row -> sample without a division)
   float ln_invd;       // 1 / K (LayerNorm fold consumer: D = K)
 };
@@ -569,6 +571,7 @@ struct VecEpi {
   int cls_b;        //   and its sample (kept as a scalar: indexing rowm[cls_i] would put the
                     //   epilogue's arrays in scratch memory)
   f32x4 clsv[FN];   //   cls + pos[0] + temb[t] of that sample's cls row, the lane's columns
+  float sqacc;      // ACC with sq_parts: this lane's sum of squares of the stored values
 
   // lane -> (row within the 16-row fragment, first of its 4 columns within the 16-column fragment)
   static __device__ __forceinline__ int rsub(int g, int li) { return SW ? li : 4 * g + (li & 3); }
@@ -691,6 +694,7 @@ struct VecEpi {
     const bool fold = FC && p.ln_st != nullptr;
     const bool prod = FP && p.st_out != nullptr;
     float lsum = 0.f;  // HEADL: this lane's loss contributions
+    sqacc = 0.f;
     float2 ms[FM];
     constexpr int SL = FN / 2;  // 32-column statistics slots per wave
     float2 part[FM][SL];
@@ -732,7 +736,9 @@ struct VecEpi {
 #pragma unroll
           for (int c = 0; c < 4; ++c) atomicAdd(reinterpret_cast<float*>(p.C) + idx + c, v[c]);
         } else if (EPI == EPI_ACC) {
-          st4(reinterpret_cast<float*>(p.C) + idx, pre[i][j] + v);
+          const f32x4 o = pre[i][j] + v;
+          st4(reinterpret_cast<float*>(p.C) + idx, o);
+          if (p.sq_parts) sqacc += (o.x * o.x + o.y * o.y) + (o.z * o.z + o.w * o.w);
         } else if (EPI == EPI_RESID) {
           bool kp[4] = {true, true, true, true};
           if (p.thr_drop) dropout_keep4(salt_drop, (uint32_t)idx, p.thr_drop, kp);

@@ -83,7 +83,22 @@ void gemm_dgrad(const GemmArgs& a, int epi, hipStream_t stream);
 void gemm_wgrad(const GemmArgs& a, int splits, hipStream_t stream);
 // every weight gradient of a step (n <= 32 problems) in one launch, unsplit (plain read-add-write)
 // store: every target is zero on entry (plain stores instead of read-add-write)
-void gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool store = false);
+// Grad-norm partials fused into the weight-gradient launch (single process: it is the
+// last writer of the gradient arena): every output tile writes the sum of squares of
+// its final dW (+ db) values to parts[tile]; `tail` extra workgroups sum the squares
+// of the arena ranges [lo, hi) no weight-gradient tile writes (embeddings, LayerNorms:
+// final before this launch) into parts[tiles + j], and zero parts[tiles + tail ..
+// nparts).  The optimizer then reads the same partial layout sqnorm writes.
+constexpr int WSQ_MAX_RANGES = 16;
+struct WgradSq {
+  float* parts = nullptr;
+  int nparts = 0;
+  const float* base = nullptr;
+  int nr = 0, tail = 0;
+  int64_t lo[WSQ_MAX_RANGES], hi[WSQ_MAX_RANGES];
+};
+void gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool store = false,
+                      const WgradSq* sq = nullptr);
 
 // LayerNorm (layernorm.hip)
 void layernorm_fwd_launch(const float* x, const float* gamma, const float* beta, void* y_bf16, float* mean,
@@ -125,7 +140,8 @@ struct FoldTable {
   float ema_decay = 0.99f;
   int64_t* step = nullptr;
   int64_t* rng = nullptr;
-  const float* sq = nullptr;  // SQ_PARTS grad-norm partials (non-finite -> optimizer step skipped)
+  const float* sq = nullptr;  // sq_n grad-norm partials (non-finite -> optimizer step skipped)
+  int sq_n = 0;
 };
 void ln_fold_launch(const FoldTable& tb, hipStream_t stream);
 void replica_reduce_launch(float* ws, float* const* dsts_dev, int G, int C, hipStream_t stream);
@@ -189,17 +205,19 @@ void img_to_tokgrad_launch(const float* dimg, void* dtok, int B, int C, int H, i
                            hipStream_t stream);
 
 // Optimizer (optim.hip)
-// sqnorm writes SQ_PARTS per-block partial sums of (g*scale)^2 (no atomics);
-// adamw / advance sum the partials themselves.
+// sqnorm writes `nparts` (>= SQ_PARTS, a multiple of 256) per-block partial sums of
+// (g*scale)^2 (no atomics); adamw / advance / the fold tail sum the partials
+// themselves.  The single-process step instead has the weight-gradient launch write
+// them (gemm_wgrad_multi with WgradSq).
 constexpr int SQ_PARTS = 1024;
-void sqnorm_launch(const float* g, int64_t n, float* partials, float scale, hipStream_t stream, int64_t lz_lo = 0,
-                   int64_t lz_hi = 0);
+void sqnorm_launch(const float* g, int64_t n, float* partials, int nparts, float scale, hipStream_t stream,
+                   int64_t lz_lo = 0, int64_t lz_hi = 0);
 // zero_hi: zero the gradient arena only below this element (the part that is
 // accumulated into; everything above is overwritten by its producer next step)
 void adamw_launch(float* p, float* g, float* m, float* v, void* p_bf16, int64_t n, const float* sqnorm,
-                  const int64_t* step, const float* hyper, float grad_scale, hipStream_t stream,
+                  int nparts, const int64_t* step, const float* hyper, float grad_scale, hipStream_t stream,
                   int64_t zero_hi = -1, int64_t lz_lo = 0, int64_t lz_hi = 0, float* lazy_decay = nullptr);
-void advance_counters_launch(int64_t* step, int64_t* rng, const float* sqnorm, hipStream_t stream);
+void advance_counters_launch(int64_t* step, int64_t* rng, const float* sqnorm, int nparts, hipStream_t stream);
 
 // Diffusion / data (diffusion.hip)
 void ddim_step_launch(const float* x_t, const float* x0_raw, float* x_next, float* x0_out, const float* coef,

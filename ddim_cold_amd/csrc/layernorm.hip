@@ -259,7 +259,7 @@ __device__ __forceinline__ void fold_tail(const FoldTable& tb) {
     __shared__ float red[2][4];
     float lv = 0.f, sv = 0.f;
     for (int i = threadIdx.x; i < tb.loss_nparts; i += 256) lv += tb.loss_parts[i];
-    for (int i = threadIdx.x; i < SQ_PARTS; i += 256) sv += tb.sq[i];
+    for (int i = threadIdx.x; i < tb.sq_n; i += 256) sv += tb.sq[i];
     lv = wave_sum(lv);
     sv = wave_sum(sv);
     if ((threadIdx.x & 63) == 0) {

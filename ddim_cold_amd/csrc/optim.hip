@@ -3,8 +3,10 @@
 // iteration + zero_grad), graph-capturable: every scalar that changes per step
 // (Adam step, scheduler step, RNG step) lives in device memory.
 //
-//   sqnorm  : sum((g*scale)^2) over the grad arena -> SQ_PARTS per-block partials (no
-//             same-address atomics; every consumer block sums the 4 KiB of partials)
+//   sqnorm  : sum((g*scale)^2) over the grad arena -> nparts per-block partials (no
+//             same-address atomics; every consumer block sums the few KiB of partials).
+//             The single-process step skips it: the weight-gradient launch writes the
+//             same partials from its epilogues (gemm.hip WgradSq).
 //   adamw   : clip coef from the norm, cosine LR from the device step, bias
 //             corrections, decoupled weight decay, moment updates, fp32 master
 //             update, bf16 shadow-weight refresh (what the GEMMs read), and the
@@ -16,13 +18,12 @@
 
 namespace dc {
 
-// sum of SQ_PARTS partials by one workgroup (every adamw block does this redundantly:
-// 4 KiB from L2, no atomics, no extra launch)
-__device__ __forceinline__ float sum_parts(const float* __restrict__ parts) {
+// sum of the nparts partials by one workgroup (every adamw block does this redundantly:
+// a few KiB from L2, no atomics, no extra launch)
+__device__ __forceinline__ float sum_parts(const float* __restrict__ parts, int nparts) {
   __shared__ float red[4];
   float v = 0.f;
-#pragma unroll
-  for (int i = 0; i < SQ_PARTS / 256; ++i) v += parts[threadIdx.x + 256 * i];
+  for (int i = threadIdx.x; i < nparts; i += 256) v += parts[i];
   v = wave_sum(v);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
@@ -81,11 +82,12 @@ __device__ __forceinline__ void adamw_elem(float& p, float g, float& m, float& v
 // step  = {adam_step, sched_step}
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                                                     float* __restrict__ v, bf16* __restrict__ pb, int64_t n,
-                                                    const float* __restrict__ sqnorm, const int64_t* __restrict__ step,
+                                                    const float* __restrict__ sqnorm, int nparts,
+                                                    const int64_t* __restrict__ step,
                                                     const float* __restrict__ hyper, float grad_scale, bool vec,
                                                     int64_t zero_hi, int64_t lo4, int64_t len4,
                                                     float* __restrict__ lazy_decay) {
-  const float sq = sum_parts(sqnorm);
+  const float sq = sum_parts(sqnorm, nparts);
   const bool skip = !isfinite(sq);
   const float base_lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
   const float max_norm = hyper[5], tmax = hyper[6], eta_min = hyper[7];
@@ -138,8 +140,9 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, float
   }
 }
 
-__global__ __launch_bounds__(256) void advance_kernel(int64_t* step, int64_t* rng, const float* sqnorm) {
-  const float sq = sqnorm ? sum_parts(sqnorm) : 0.f;
+__global__ __launch_bounds__(256) void advance_kernel(int64_t* step, int64_t* rng, const float* sqnorm,
+                                                      int nparts) {
+  const float sq = sqnorm ? sum_parts(sqnorm, nparts) : 0.f;
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     if (sqnorm == nullptr || isfinite(sq)) step[0] += 1;
     step[1] += 1;
@@ -163,15 +166,15 @@ static void check_lazy(int64_t n, int64_t lz_lo, int64_t lz_hi) {
     throw std::runtime_error("optimizer lazy range must be whole 16-B vectors inside the arena");
 }
 
-void sqnorm_launch(const float* g, int64_t n, float* out, float scale, hipStream_t stream, int64_t lz_lo,
-                   int64_t lz_hi) {
+void sqnorm_launch(const float* g, int64_t n, float* out, int nparts, float scale, hipStream_t stream,
+                   int64_t lz_lo, int64_t lz_hi) {
   check_lazy(n, lz_lo, lz_hi);
   const int64_t len4 = lz_hi > lz_lo ? (lz_hi - lz_lo) / 4 : 0;
-  hipLaunchKernelGGL(sqnorm_kernel, dim3(SQ_PARTS), dim3(256), 0, stream, g, n, out, scale, lz_lo / 4, len4);
+  hipLaunchKernelGGL(sqnorm_kernel, dim3(nparts), dim3(256), 0, stream, g, n, out, scale, lz_lo / 4, len4);
 }
 
 void adamw_launch(float* p, float* g, float* m, float* v, void* p_bf16, int64_t n, const float* sqnorm,
-                  const int64_t* step, const float* hyper, float grad_scale, hipStream_t stream, int64_t zero_hi,
+                  int nparts, const int64_t* step, const float* hyper, float grad_scale, hipStream_t stream, int64_t zero_hi,
                   int64_t lz_lo, int64_t lz_hi, float* lazy_decay) {
   if (zero_hi < 0 || zero_hi > n) zero_hi = n;
   zero_hi = (zero_hi + 3) / 4 * 4 <= n ? (zero_hi + 3) / 4 * 4 : n;  // whole 16-B vectors
@@ -181,10 +184,10 @@ void adamw_launch(float* p, float* g, float* m, float* v, void* p_bf16, int64_t 
   int64_t len4 = lz_hi > lz_lo ? (lz_hi - lz_lo) / 4 : 0;
   if (!vec || lazy_decay == nullptr) len4 = 0;
   hipLaunchKernelGGL(adamw_kernel, dim3(opt_grid(n - 4 * len4)), dim3(256), 0, stream, p, g, m, v,
-                     reinterpret_cast<bf16*>(p_bf16), n, sqnorm, step, hyper, grad_scale, vec, zero_hi, lz_lo / 4,
+                     reinterpret_cast<bf16*>(p_bf16), n, sqnorm, nparts, step, hyper, grad_scale, vec, zero_hi, lz_lo / 4,
                      len4, lazy_decay);
 }
 
-void advance_counters_launch(int64_t* step, int64_t* rng, const float* sqnorm, hipStream_t stream) {
-  hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(256), 0, stream, step, rng, sqnorm);
+void advance_counters_launch(int64_t* step, int64_t* rng, const float* sqnorm, int nparts, hipStream_t stream) {
+  hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(256), 0, stream, step, rng, sqnorm, nparts);
 }

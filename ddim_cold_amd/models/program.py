@@ -418,7 +418,7 @@ class ViTProgram:
     def backward_iter(self, P: ModelTensors, G: ModelTensors, S: Saved, dtok: torch.Tensor, rng: torch.Tensor,
                       training: bool = True, wgrad: Optional[Callable] = None,
                       ln_ws: Optional[torch.Tensor] = None, embed_with_block0: bool = False, ln_final=None,
-                      wgrad_flush=None, wgrad_store: bool = False) -> Iterator[int]:
+                      wgrad_flush=None, wgrad_store: bool = False, wgrad_sq=None) -> Iterator[int]:
         """Hand-written backward; yields the block index after each block's input
         gradients are issued (L-1 first, then ..., 0) and -1 after the embedding grads.
 
@@ -439,12 +439,17 @@ class ViTProgram:
         bucket).  ``wgrad_store``: the block / head weight-gradient targets have no
         other writer this step, so the deferred launches write instead of
         read-add-writing them (the embedding bucket's patch gradient still adds).
+        ``wgrad_sq = (parts, arena, lazy)`` (one deferred launch, no ``wgrad_flush``):
+        that launch also writes the grad-norm partials of the whole gradient arena
+        (:func:`ops.linear_wgrad_multi`), so the optimizer needs no sqnorm pass.
         Measured slower on MI355X and removed: weight gradients riding in the
         input-gradient launches, one grouped launch per block, a side-stream branch
         for them, the proj input gradient inside the attention backward."""
         def ws(k):
             return None if ln_ws is None else ln_ws[k]
         bucketed = wgrad is None and wgrad_flush is not None
+        if wgrad_sq is not None and (bucketed or wgrad is not None):
+            raise ValueError("wgrad_sq needs the single deferred weight-gradient launch")
         jobs = []
         if wgrad is None:
             wgrad = lambda dy, x, dw, db: jobs.append((dy, x, dw, db))  # noqa: E731
@@ -517,7 +522,7 @@ class ViTProgram:
                 for job in jobs:
                     ops.linear_wgrad(*job)
             else:
-                ops.linear_wgrad_multi(jobs, store=wgrad_store and not bucketed)
+                ops.linear_wgrad_multi(jobs, store=wgrad_store and not bucketed, sq=wgrad_sq)
             keep.append(jobs)
         keep.append((gpatch, lf))
         self._keep = keep  # operands of the queued launches stay referenced until the next step

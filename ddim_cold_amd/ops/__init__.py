@@ -332,16 +332,29 @@ def wire_unpack(src, dst):
     dst.copy_(src)
 
 
-def linear_wgrad_multi(jobs, store: bool = False):
+def linear_wgrad_multi(jobs, store: bool = False, sq=None):
     """Every ``(dy, x, dw, db)`` weight-gradient job of a step (<= 32) in ONE launch
     (csrc/gemm.hip ``gemm_wgrad_multi_kernel``; unsplit, deterministic).  ``store``:
-    the targets are zero (``dW = dy^T x`` written, not added: no read of dW)."""
+    the targets are zero (``dW = dy^T x`` written, not added: no read of dW).
+
+    ``sq = (parts, arena, lazy)``: the launch is the last writer of the gradient
+    ``arena`` (every dw / db a view of it), so it also writes the grad-norm partials
+    :func:`sqnorm` would (same buffer layout, scale 1): each output tile the sum of
+    squares of its final values, extra workgroups the arena ranges outside every
+    target and outside ``lazy`` = (lo, hi).  Replaces the separate sqnorm pass."""
     if not jobs:
         return
+    if sq is not None and len(jobs) > 32:
+        raise ValueError("linear_wgrad_multi: grad-norm partials need all jobs in one launch (<= 32)")
     if _hip(jobs[0][0]):
         for a in range(0, len(jobs), 32):
             dys, xs, dws, dbs = (list(z) for z in zip(*jobs[a:a + 32]))
-            _ops().linear_wgrad_multi(dys, xs, dws, dbs, bool(store))
+            if sq is None:
+                _ops().linear_wgrad_multi(dys, xs, dws, dbs, bool(store))
+            else:
+                parts, arena, lazy = sq
+                lo, hi = lazy if lazy is not None else (0, 0)
+                _ops().linear_wgrad_multi(dys, xs, dws, dbs, bool(store), parts, arena, int(lo), int(hi))
         return
     for dy, x, dw, db in jobs:
         if store:
@@ -349,6 +362,9 @@ def linear_wgrad_multi(jobs, store: bool = False):
             if db is not None:
                 db.zero_()
         ref.linear_wgrad(dy, x, dw, db)
+    if sq is not None:
+        parts, arena, lazy = sq
+        sqnorm(arena, parts, 1.0, lazy=lazy)
 
 
 LN_REPLICAS = 16  # csrc/layernorm.hip LN_REPLICAS
@@ -437,8 +453,17 @@ def embed_bwd(g, t, rng, site: int, p: float, dcls, dpos, dtemb, ln_final=None):
 SQ_PARTS = 1024  # csrc/kernels.h
 
 
+def sq_parts_size(n_tiles: int) -> int:
+    """Grad-norm partial buffer size (floats) for a fused weight-gradient launch of
+    ``n_tiles`` 64x64 tiles: room for the tiles, up to 64 tail workgroups, >= SQ_PARTS,
+    a multiple of 256 (what every consumer kernel accepts)."""
+    n = max(SQ_PARTS, n_tiles + 64)
+    return (n + 255) // 256 * 256
+
+
 def sqnorm(g, out, scale: float = 1.0, lazy=None):
-    """Per-block partial sums of (g*scale)^2 into ``out`` (>= SQ_PARTS floats, fully overwritten).
+    """Per-block partial sums of (g*scale)^2 into ``out`` (>= SQ_PARTS floats, a multiple
+    of 256, fully overwritten).
     ``lazy`` = (lo, hi): an arena range whose gradient is identically zero (skipped)."""
     lo, hi = lazy if lazy is not None else (0, 0)
     if _hip(g):

@@ -65,6 +65,10 @@ PREISSUE = os.environ.get("DDIM_COLD_PREISSUE", "1") != "0"
 # the LayerNorm dgamma/dbeta replica finalize rides in the embedding-backward launch
 # (False: a separate replica_reduce_ launch; tests compare the two)
 FUSE_LN_FINAL = True
+# single process: the grad-norm partials come from the weight-gradient launch's
+# epilogues (ops.linear_wgrad_multi sq=) instead of a separate sqnorm pass over the
+# arena (False: the sqnorm kernel; tests compare the two)
+FUSE_SQNORM = True
 
 
 @dataclass
@@ -174,7 +178,10 @@ class TrainEngine:
         b1, b2 = cfg.betas
         self.hyper = torch.tensor([cfg.lr, b1, b2, cfg.eps, cfg.weight_decay, cfg.max_grad_norm,
                                    float(cfg.t_max), cfg.eta_min], dtype=torch.float32, device=dev)
-        self.sqnorm = torch.zeros(ops.SQ_PARTS, dtype=torch.float32, device=dev)  # per-block partials
+        # grad-norm partials (sqnorm, or the fused weight-gradient launch: one per 64x64
+        # output tile + tail workgroups; the 2-D parameter count bounds the tiles)
+        tiles = sum(-(-p.shape[0] // 64) * -(-(p[0].numel()) // 64) for p in model.parameters() if p.dim() >= 2)
+        self.sqnorm = torch.zeros(ops.sq_parts_size(tiles), dtype=torch.float32, device=dev)
         self.loss_last = torch.zeros(1, dtype=torch.float32, device=dev)
         self.loss_ema = torch.full((1,), cfg.ema_init, dtype=torch.float32, device=dev)
         # the comm stream is created once and kept across set_comm_layout() (a stream
@@ -574,9 +581,14 @@ class TrainEngine:
             overwrite = self._grad_overwrite(k_acc, True, ln_final)
             if overwrite:
                 ln_final = ln_final + (True,)
+            # single process, one micro-batch: the deferred weight-gradient launch is the
+            # last writer of the gradient arena and writes the grad-norm partials too
+            fuse_sq = (FUSE_SQNORM and overwrite and flush_at is None and k_acc == 1 and self.world == 1
+                       and self.is_cuda)
             for i in self.prog.backward_iter(self.param_tensors, self.grad_tensors, S, dtok, self.rng, True,
                                              ln_ws=self.ln_ws, embed_with_block0=merge, ln_final=ln_final,
-                                             wgrad_flush=flush_at, wgrad_store=overwrite):
+                                             wgrad_flush=flush_at, wgrad_store=overwrite,
+                                             wgrad_sq=(self.sqnorm, self.opt_g, self.lazy) if fuse_sq else None):
                 if i in self.bucket_after and (self.segmented or i == -1):
                     hi = self.ln_done_at[i]
                     if ln_final is not None:
@@ -592,7 +604,8 @@ class TrainEngine:
         # optimizer: grads are SUM-reduced over ranks and summed over micro-batches
         # -> average via grad_scale
         gs = 1.0 / (self.world * k_acc)
-        ops.sqnorm(self.opt_g, self.sqnorm, gs, lazy=self.lazy)
+        if not fuse_sq:
+            ops.sqnorm(self.opt_g, self.sqnorm, gs, lazy=self.lazy)
         ops.adamw_step(self.opt_p, self.opt_g, self.opt_m, self.opt_v, self.opt_pb, self.sqnorm,
                        self.step_ctr, self.hyper, gs, zero_hi=self.acc_hi if overwrite else None,
                        lazy=self.lazy, lazy_decay=self.lazy_decay)

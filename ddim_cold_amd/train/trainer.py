@@ -260,74 +260,83 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
     t_start = time.time()
     t_run = t_epoch = time.perf_counter()
     steps0 = steps
-    for epoch in range(start_epoch, end_epoch):
-        model.train()
-        table = shard_indices(n_train, world, rank, epoch, cfg.seed)[: steps_per_epoch * A * B]
-        table = table.view(steps_per_epoch, A, B).to(device)
-        for s in range(steps_per_epoch):
-            idx_dev.copy_(table[s])
-            with phase("train_step"):
-                engine.train_step(materialize=False)  # lazy time_embed decay: applied at the epoch end
-            if prof is not None:
-                prof.step()
-            steps += 1
-            if cfg.sync_check_every and steps % cfg.sync_check_every == 0:
-                check_param_sync(engine.flat_p, step=steps)
-            if steps % cfg.log_every == 0:
-                window = clock.mark(steps)  # device events: the only sync of the window
-                if window is not None and window[1] > 0:
-                    last_ms = 1e3 * window[0] / window[1]
-                engine.check_comm()  # a timed-out bucket hand-off stops the run (stale gradients)
-                loss_rec = float(engine.loss_ema.item())
-                if verbose:
-                    print(f"[rank {rank}] step {steps} loss_ema {loss_rec:.4f}", flush=True)
-                if rank == 0:
-                    now = time.time()
-                    printLog(fmt_steps(steps, loss_rec, now - t_start), paths.log)
-                    t_start = now
-                    if cfg.perf_log and window is not None and window[1] > 0:
-                        sec, n = window
-                        printLog(f"# perf: {n * B * A * world / sec:.1f} img/s  {1e3 * sec / n:.3f} ms/step "
-                                 f"(device, {world} rank(s)" +
-                                 (f", comm {engine.comm_choice or 'default'}/{engine.handoff_order}"
-                                  if engine.segmented else "") + ")", paths.log)
-            if cfg.fault_inject_step and steps >= cfg.fault_inject_step and cfg.fault_inject_rank in (-1, rank):
-                raise FaultInjected(f"fault injected at step {steps} on rank {rank} (fault_inject_step)")
-        engine.materialize_lazy()
-        loss_rec = float(engine.loss_ema.item())
-        engine.check_comm()  # epoch end: before evaluating / checkpointing these weights
-        t_ev = time.perf_counter()
-        if (epoch - start_epoch + 1) % max(cfg.eval_every, 1) == 0 or epoch == end_epoch - 1:
-            model.eval()
-            vidx = shard_indices(n_val, world, rank, epoch, cfg.seed, shuffle=False, drop_last=False)
-            eval_rng[1] = epoch * val_batches
-            with phase("evaluate"):
-                vloss = evaluate(model, engine, val_pool, vidx, B, cfg.dataset, cfg.model_total_steps, eval_rng)
-            vloss = pdist.all_reduce_mean(vloss, device)
+    try:
+        for epoch in range(start_epoch, end_epoch):
             model.train()
-            history.append((epoch, vloss))
-            t_ck = time.perf_counter()
-            if rank == 0:
-                printLog(fmt_epoch(epoch, vloss), paths.log)
-                writer.add_scalar("loss", vloss, epoch)
-                best = vloss < best_loss
-                if best:
-                    best_loss = vloss
-                # bestloss.pkl / lastepoch.pkl written by a background thread from a
-                # snapshot taken here (device copies on the training stream, host copy
-                # on a side stream) while the next epoch trains
-                ckw.submit(engine.snapshot_to_host(), os.path.join(paths.ckpt_dir, "lastepoch.pkl"), epoch,
-                           steps, loss_rec, best_loss,
-                           best_path=os.path.join(paths.ckpt_dir, "bestloss.pkl") if best else None)
-            pdist.barrier()
-            t_end = time.perf_counter()
-            if rank == 0 and cfg.perf_log:
-                wall = t_end - t_epoch
-                printLog(f"# perf: epoch {epoch} end to end {steps_per_epoch * B * A * world / wall:.1f} img/s "
-                         f"({wall:.3f} s: evaluate {1e3 * (t_ck - t_ev):.1f} ms, checkpoint hand-off "
-                         f"{1e3 * (t_end - t_ck):.1f} ms, previous write {1e3 * ckw.last_write_s:.1f} ms "
-                         f"in the background)", paths.log)
-        t_epoch = time.perf_counter()
+            table = shard_indices(n_train, world, rank, epoch, cfg.seed)[: steps_per_epoch * A * B]
+            table = table.view(steps_per_epoch, A, B).to(device)
+            for s in range(steps_per_epoch):
+                idx_dev.copy_(table[s])
+                with phase("train_step"):
+                    engine.train_step(materialize=False)  # lazy time_embed decay: applied at the epoch end
+                if prof is not None:
+                    prof.step()
+                steps += 1
+                if cfg.sync_check_every and steps % cfg.sync_check_every == 0:
+                    check_param_sync(engine.flat_p, step=steps)
+                if steps % cfg.log_every == 0:
+                    window = clock.mark(steps)  # device events: the only sync of the window
+                    if window is not None and window[1] > 0:
+                        last_ms = 1e3 * window[0] / window[1]
+                    engine.check_comm()  # a timed-out bucket hand-off stops the run (stale gradients)
+                    loss_rec = float(engine.loss_ema.item())
+                    if verbose:
+                        print(f"[rank {rank}] step {steps} loss_ema {loss_rec:.4f}", flush=True)
+                    if rank == 0:
+                        now = time.time()
+                        printLog(fmt_steps(steps, loss_rec, now - t_start), paths.log)
+                        t_start = now
+                        if cfg.perf_log and window is not None and window[1] > 0:
+                            sec, n = window
+                            printLog(f"# perf: {n * B * A * world / sec:.1f} img/s  {1e3 * sec / n:.3f} ms/step "
+                                     f"(device, {world} rank(s)" +
+                                     (f", comm {engine.comm_choice or 'default'}/{engine.handoff_order}"
+                                      if engine.segmented else "") + ")", paths.log)
+                if cfg.fault_inject_step and steps >= cfg.fault_inject_step and cfg.fault_inject_rank in (-1, rank):
+                    raise FaultInjected(f"fault injected at step {steps} on rank {rank} (fault_inject_step)")
+            engine.materialize_lazy()
+            loss_rec = float(engine.loss_ema.item())
+            engine.check_comm()  # epoch end: before evaluating / checkpointing these weights
+            t_ev = time.perf_counter()
+            if (epoch - start_epoch + 1) % max(cfg.eval_every, 1) == 0 or epoch == end_epoch - 1:
+                model.eval()
+                vidx = shard_indices(n_val, world, rank, epoch, cfg.seed, shuffle=False, drop_last=False)
+                eval_rng[1] = epoch * val_batches
+                with phase("evaluate"):
+                    vloss = evaluate(model, engine, val_pool, vidx, B, cfg.dataset, cfg.model_total_steps, eval_rng)
+                vloss = pdist.all_reduce_mean(vloss, device)
+                model.train()
+                history.append((epoch, vloss))
+                t_ck = time.perf_counter()
+                if rank == 0:
+                    printLog(fmt_epoch(epoch, vloss), paths.log)
+                    writer.add_scalar("loss", vloss, epoch)
+                    best = vloss < best_loss
+                    if best:
+                        best_loss = vloss
+                    # bestloss.pkl / lastepoch.pkl written by a background thread from a
+                    # snapshot taken here (device copies on the training stream, host copy
+                    # on a side stream) while the next epoch trains
+                    ckw.submit(engine.snapshot_to_host(), os.path.join(paths.ckpt_dir, "lastepoch.pkl"), epoch,
+                               steps, loss_rec, best_loss,
+                               best_path=os.path.join(paths.ckpt_dir, "bestloss.pkl") if best else None)
+                pdist.barrier()
+                t_end = time.perf_counter()
+                if rank == 0 and cfg.perf_log:
+                    wall = t_end - t_epoch
+                    printLog(f"# perf: epoch {epoch} end to end {steps_per_epoch * B * A * world / wall:.1f} img/s "
+                             f"({wall:.3f} s: evaluate {1e3 * (t_ck - t_ev):.1f} ms, checkpoint hand-off "
+                             f"{1e3 * (t_end - t_ck):.1f} ms, previous write {1e3 * ckw.last_write_s:.1f} ms "
+                             f"in the background)", paths.log)
+            t_epoch = time.perf_counter()
+    except BaseException:
+        # a failing step (or an injected fault) must not cut the previous epoch's
+        # background checkpoint write short: the resume reads those files
+        try:
+            ckw.join()
+        except RuntimeError as werr:
+            print(f"[rank {rank}] {werr}", flush=True)
+        raise
     if prof is not None:
         prof.__exit__(None, None, None)
     t_done = time.perf_counter()

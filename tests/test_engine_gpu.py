@@ -36,14 +36,15 @@ def test_graph_step_matches_eager(grad_accum):
 @pytest.mark.gpu
 @pytest.mark.parametrize("target", ["prev", "x0"])
 @pytest.mark.parametrize("draw", [True, False])
-def test_patch_embed_cold_matches_cold_batch_then_embed(target, draw):
+@pytest.mark.parametrize("name", ["vit_tiny", "oxford_flower"])  # patch 8 / patch 4 segments
+def test_patch_embed_cold_matches_cold_batch_then_embed(target, draw, name):
     """ops.patch_embed_cold_fwd (batch draw fused into the patchify launch) == cold_batch
     followed by patch_embed_fwd, bit for bit (tokens, patch rows, target, t, idx, LN stats)."""
     from ddim_cold_amd import ops
     from ddim_cold_amd.data.synthetic import SITE_DATA
     from ddim_cold_amd.models.program import SITE_EMBED
     torch.manual_seed(0)
-    model = build_model("vit_tiny").cuda().train()
+    model = build_model(name).cuda().train()
     B, D = 8, model.embed_dim
     N = model.patch_embed.num_patches + 1
     pool = synthetic_pool(32, seed=2, device="cuda")
@@ -107,6 +108,37 @@ def test_multi_step_graph_matches_single_step_graph():
     assert int(eng.step_ctr[0]) == 9 and int(eng.rng[1]) == 9
     assert abs(em - es) <= 1e-4 * abs(es), (em, es)
     assert (pm - ps).abs().max().item() <= 2 * 1e-3 * 9
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph", [False, True])
+def test_fused_grad_norm_matches_sqnorm_pass(monkeypatch, graph):
+    """Grad-norm partials written by the weight-gradient launch (engine.FUSE_SQNORM,
+    default) == the separate sqnorm pass: same squared norm of the step's gradient
+    (clipping active: a norm error would move every parameter), same parameters and
+    counters after several steps (lazy time-embedding range on)."""
+    from ddim_cold_amd.train import engine as engine_mod
+
+    def run(flag):
+        monkeypatch.setattr(engine_mod, "FUSE_SQNORM", flag)
+        torch.manual_seed(0)
+        model = build_model("vit_tiny").cuda().train()
+        eng = TrainEngine(model, EngineConfig(lr=1e-3, t_max=100, seed=3, use_graph=graph, graph_warmup=1,
+                                              temb_rows=7, max_grad_norm=0.5))
+        eng.set_batch_fn(ColdBatcher(synthetic_pool(64, seed=1, device="cuda"), 8, eng.rng))
+        eng.train_step()
+        torch.cuda.synchronize()
+        sq1 = eng.sqnorm.double().sum().item()
+        eng.train_steps(5)
+        torch.cuda.synchronize()
+        return sq1, eng.flat_p.clone(), eng.step_ctr.clone(), float(eng.loss_ema)
+    sf, pf, cf, ef = run(True)
+    su, pu, cu, eu = run(False)
+    assert sf > 0.25, "clipping must be active for the comparison to mean anything"
+    assert abs(sf - su) <= 1e-5 * su, (sf, su)
+    assert torch.equal(cf, cu)
+    assert abs(ef - eu) <= 1e-5 * abs(eu)
+    assert (pf - pu).abs().max().item() <= 1e-5
 
 
 @pytest.mark.gpu

@@ -183,7 +183,8 @@ def test_head_step_per_sample_coefficients():
     close(pout.float(), ref.patchify_bf16(xk, p).reshape(B * (N - 1), -1).float(), 0, 0, "patch rows")
 
 
-@pytest.mark.parametrize("B,C,H,W,p,D,pd", [(4, 3, 64, 64, 8, 384, 0.1), (2, 3, 64, 64, 4, 256, 0.0)])
+@pytest.mark.parametrize("B,C,H,W,p,D,pd", [(4, 3, 64, 64, 8, 384, 0.1), (2, 3, 64, 64, 4, 256, 0.0),
+                                            (2, 3, 64, 64, 16, 128, 0.1)])  # p=16: the generic segment path
 def test_patch_embed(B, C, H, W, p, D, pd):
     N = (H // p) * (W // p) + 1
     img = torch.randn(B, C, H, W, device=DEV)
@@ -265,14 +266,15 @@ def test_linear_fwd(M, N, K, f32, bias):
     close(y.float(), yr.float(), 3e-2, 2e-2, "y")
 
 
-@pytest.mark.parametrize("n", [1, 7, 30])
-def test_linear_wgrad_multi(n):
-    """Every weight gradient of a step in one launch == per-problem reference (bias or not, odd shapes)."""
+@pytest.mark.parametrize("n,big", [(1, False), (7, False), (30, False), (5, True)])
+def test_linear_wgrad_multi(n, big):
+    """Every weight gradient of a step in one launch == per-problem reference (bias or not, odd shapes).
+    ``big``: a reduction over >= 16,384 tokens (vit_small_200: 128 x 128 tiles, 8 waves)."""
     shapes = [(1152, 384), (384, 384), (384, 384), (384, 384), (192, 384), (384, 192), (64, 96), (256, 128)]
     jobs, refs = [], []
     for i in range(n):
         nout, k = shapes[i % len(shapes)]
-        m = 2080 if i % 3 else 300
+        m = (20032 if i % 2 else 16500) if big else (2080 if i % 3 else 300)
         dy, x = bf(m, nout), bf(m, k)
         dw0 = torch.randn(nout, k, device=DEV) * 0.1
         db0 = torch.randn(nout, device=DEV) if i % 2 == 0 else None
@@ -285,6 +287,66 @@ def test_linear_wgrad_multi(n):
         close(dw, dw2, 2e-2, 1e-4, "dw")
         if db is not None:
             close(db, db2, 2e-2, 1e-4, "db")
+
+
+@pytest.mark.parametrize("store", [False, True])
+@pytest.mark.parametrize("lazy", [None, (64, 64 + 4 * 1000)])
+@pytest.mark.parametrize("big", [False, True])
+def test_linear_wgrad_multi_sqnorm_partials(store, lazy, big):
+    """Grad-norm partials from the weight-gradient launch (engine FUSE_SQNORM): targets
+    are views of one arena with gaps the tail workgroups cover (and a lazy range they
+    skip); the partials sum to the arena's sum of squares, dW / db unchanged, unused
+    slots zero, and the optimizer kernels accept the buffer."""
+    shapes = [(1152, 384, True), (384, 384, True), (384, 1536, False), (192, 384, True), (64, 96, True)]
+    sizes = [n * k + (n if b else 0) for n, k, b in shapes]
+    lo0 = 64 + 4 * 1000 + 1000  # after the lazy range and a gap of "embedding" gradients
+    arena = torch.zeros(lo0 + sum(sizes) + len(shapes) * 777 + 13, device=DEV)
+    arena[:lo0].normal_()
+    if lazy is not None:
+        arena[lazy[0]:lazy[1]] = 0  # a lazy range has a zero gradient by construction
+    off = lo0
+    jobs, refs = [], []
+    for i, (nout, k, hb) in enumerate(shapes):
+        m = (20032 if i % 2 else 16400) if big else (2080 if i % 2 else 300)
+        dy, x = bf(m, nout), bf(m, k)
+        dw = arena[off:off + nout * k].view(nout, k)
+        off += nout * k
+        db = None
+        if hb:
+            db = arena[off:off + nout]
+            off += nout
+        if not store:
+            dw.normal_()
+            if db is not None:
+                db.normal_()
+        arena[off:off + 777].normal_()  # a gap no tile writes
+        off += 777
+        dw2, db2 = dw.clone(), (db.clone() if db is not None else None)
+        if store:
+            dw2.zero_()
+            if db2 is not None:
+                db2.zero_()
+        ref.linear_wgrad(dy, x, dw2, db2)
+        refs.append((dw2, db2))
+        jobs.append((dy, x, dw, db))
+    parts = torch.full((ops.sq_parts_size(2000),), float("nan"), device=DEV)
+    ops.linear_wgrad_multi(jobs, store=store, sq=(parts, arena, lazy))
+    for (_, _, dw, db), (dw2, db2) in zip(jobs, refs):
+        close(dw, dw2, 2e-2, 1e-4, "dw")
+        if db is not None:
+            close(db, db2, 2e-2, 1e-4, "db")
+    assert torch.isfinite(parts).all(), "every partial slot is written"
+    expect = arena.double().pow(2).sum().item()
+    got = parts.double().sum().item()
+    assert abs(got - expect) <= 1e-5 * expect, (got, expect)
+    # the sqnorm kernel writes the same quantity into the same layout
+    parts2 = torch.empty_like(parts)
+    ops.sqnorm(arena, parts2, 1.0, lazy=lazy)
+    assert abs(parts2.double().sum().item() - expect) <= 1e-5 * expect
+    with pytest.raises(RuntimeError, match="grad-norm partials"):
+        ops.linear_wgrad_multi(jobs, sq=(torch.zeros(256, device=DEV), arena, lazy))
+    with pytest.raises(RuntimeError, match="outside the arena"):
+        ops.linear_wgrad_multi(jobs, sq=(parts, arena[:lo0], None))
 
 
 # ------------------------------------------------------------------ attention
