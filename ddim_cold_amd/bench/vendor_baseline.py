@@ -265,10 +265,10 @@ class VendorSampler:
 
     @torch.no_grad()
     def sample(self, generator=None) -> torch.Tensor:
+        if self.use_graph and self.graph is None:
+            self.capture()  # (draws a scratch x_T of its own for the warm-up)
         self.x_in.normal_(generator=generator)
         if self.use_graph:
-            if self.graph is None:
-                self.capture()
             self.graph.replay()
         else:
             self._body()

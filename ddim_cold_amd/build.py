@@ -52,7 +52,7 @@ def _flags(inc, abi, resource_usage=False):
     # per-kernel resource remarks (codegen unchanged): the build checks them for
     # scratch memory, see _check_scratch
     f.append("-Rpass-analysis=kernel-resource-usage")
-    # DDIM_COLD_HIPFLAGS: extra hipcc flags, e.g. "-DDDIM_COLD_LN_STAMPS=1" (profiling builds)
+    # DDIM_COLD_HIPFLAGS: extra hipcc flags (e.g. "-save-temps" to inspect the ISA)
     f += os.environ.get("DDIM_COLD_HIPFLAGS", "").split()
     for d in inc + [py_inc, CSRC, "/opt/rocm/include"]:
         f += ["-I", d]

@@ -29,23 +29,6 @@ namespace dc {
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
-// profiling aid (tools/ub_attn_stamps.py, build with DDIM_COLD_ATTN_STAMPS=1): when
-// set, wave 0 of every short-backward workgroup records s_memrealtime (100 MHz) at
-// its phase boundaries, [grid][4].  Compiled out by default (cf. the LayerNorm
-// backward's stamps: 2.2 us per launch in the step profile).
-#ifndef DDIM_COLD_ATTN_STAMPS
-#define DDIM_COLD_ATTN_STAMPS 0
-#endif
-__device__ unsigned long long* g_attn_stamps = nullptr;
-__device__ __forceinline__ void attn_stamp(int k) {
-#if DDIM_COLD_ATTN_STAMPS
-  unsigned long long* s = g_attn_stamps;
-  if (s != nullptr && threadIdx.x == 0) s[(size_t)blockIdx.x * 4 + k] = __builtin_amdgcn_s_memrealtime();
-#else
-  (void)k;
-#endif
-}
-
 template <int HD>
 struct AC {
   static constexpr int S = 2 * HD + 32;   // LDS row stride in bytes
@@ -1068,9 +1051,8 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
   // dynamic LDS (4 * NP * RS + 2 * NP * PS bytes, see short_lds): the same image as a
   // static array (79,872 B at NP 96) got ONE 384-thread workgroup per CU instead of two
   // -- 128 of the ViT-tiny step's 384 workgroups then waited for a second round
-  // (tools/ub_attn_stamps.py, tools/ub_lds_census.hip)
+  // (workgroup-entry timestamps, tools/ub_lds_census.hip)
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  attn_stamp(0);
   char* Ql = lds;
   char* Kl = Ql + NP * RS;
   char* Vl = Kl + NP * RS;
@@ -1106,7 +1088,6 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
   iv.store(Vl);
   id.store(Dl);
   __syncthreads();
-  attn_stamp(1);
 
   // ---- phase A: this wave's 16 queries against all keys
   const float lse2 = qv ? lse_raw * LOG2E : INFINITY;
@@ -1173,7 +1154,6 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
 #pragma unroll
     for (int d = 0; d < DT; ++d) *reinterpret_cast<bf16x4*>(row + 16 * d + 4 * g) = pack4(dq[d] * scale);
   }
-  attn_stamp(2);
   __syncthreads();
 
   // ---- phase B: this wave's 16 keys against all queries
@@ -1202,7 +1182,6 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
       *reinterpret_cast<bf16x4*>(row + 2 * D + 16 * d + 4 * g) = pack4(dv[d]);
     }
   }
-  attn_stamp(3);
 }
 
 // LDS bytes of the short kernels' images (dynamic shared memory)
@@ -1280,11 +1259,6 @@ constexpr int SHORT_MAX_N = 128;
 }  // namespace dc
 
 using namespace dc;
-
-void attn_set_stamps(void* buf) {
-  unsigned long long* p = reinterpret_cast<unsigned long long*>(buf);
-  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_attn_stamps), &p, sizeof(p));
-}
 
 // Long sequences: the flash / resident forwards store one 64-bit keep word per
 // (b, h, 64-key tile, query) for the backward (attn_fwd_launch picks them whenever

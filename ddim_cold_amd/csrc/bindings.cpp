@@ -254,24 +254,6 @@ Tensor qkv_fwd(Tensor a, Tensor w, Tensor b, int64_t B, int64_t N, int64_t H, c1
 
 // attention-dropout keep-flag words the short forward stores for the backward
 // (0: this shape takes the long-sequence kernels, which regenerate the masks)
-void attn_stamps(c10::optional<Tensor> buf) {
-  void* p = nullptr;
-  if (buf.has_value() && buf->defined()) {
-    CHECK_IN((*buf), at::kLong);
-    p = buf->data_ptr();
-  }
-  attn_set_stamps(p);
-}
-
-void ln_stamps(c10::optional<Tensor> buf) {
-  void* p = nullptr;
-  if (buf.has_value() && buf->defined()) {
-    CHECK_IN((*buf), at::kLong);
-    p = buf->data_ptr();
-  }
-  ln_set_stamps(p);
-}
-
 int64_t gemm_tile_override_op(int64_t cfg) { return gemm_set_tile_override((int)cfg); }
 
 int64_t attn_keep_words_op(int64_t B, int64_t H, int64_t N, int64_t hd) {
@@ -616,61 +598,78 @@ static std::vector<GemmArgs> wgrad_probs(const std::vector<Tensor>& dys, const s
 
 // Every weight gradient of a training step in ONE launch (gemm_wgrad_multi_kernel)
 // sq_parts / arena: also write the grad-norm partials of the whole gradient arena
-// (the launch must then be its last writer): the arena ranges outside every dW / db
-// target and outside the lazy range [lz_lo, lz_hi) go to the tail workgroups
+// (the launches must then be its last writers): the arena ranges outside every dW /
+// db target and outside the lazy range [lz_lo, lz_hi) go to the tail workgroups of
+// the last launch.  More than 32 problems: consecutive launches of <= 32, each
+// writing its tiles' partials after the previous launch's.
 void linear_wgrad_multi(std::vector<Tensor> dys, std::vector<Tensor> xs, std::vector<Tensor> dws,
                         std::vector<c10::optional<Tensor>> dbs, bool store, c10::optional<Tensor> sq_parts,
                         c10::optional<Tensor> arena, int64_t lz_lo, int64_t lz_hi) {
-  TORCH_CHECK(!dys.empty() && dys.size() <= 32, "wgrad_multi: 1..32 problems");
+  TORCH_CHECK(!dys.empty() && dys.size() == xs.size() && dys.size() == dws.size() && dys.size() == dbs.size(),
+              "wgrad_multi: one dy, x, dw, db per problem");
   const c10::DeviceGuard guard(dys[0].device());
-  int tiles = 0;
-  std::vector<GemmArgs> probs = wgrad_probs(dys, xs, dws, dbs, &tiles, nullptr);
-  if (!(sq_parts.has_value() && sq_parts->defined())) {
-    gemm_wgrad_multi(probs.data(), (int)probs.size(), cur_stream(), store);
-    return;
-  }
-  TORCH_CHECK(arena.has_value() && arena->defined(), "wgrad_multi: grad-norm partials need the gradient arena");
-  CHECK_IN((*sq_parts), F32); CHECK_IN((*arena), F32);
-  const int np = check_parts(*sq_parts, "wgrad_multi");
-  const float* base = arena->data_ptr<float>();
-  const int64_t n = arena->numel();
-  // element intervals of the targets inside the arena
-  std::vector<std::pair<int64_t, int64_t>> iv;
-  auto add = [&](const Tensor& t) {
-    TORCH_CHECK(t.is_contiguous(), "wgrad_multi: grad-norm fusion needs contiguous targets");
-    const int64_t off = t.data_ptr<float>() - base;
-    TORCH_CHECK(off >= 0 && off + t.numel() <= n, "wgrad_multi: a weight-gradient target lies outside the arena");
-    iv.emplace_back(off, off + t.numel());
-  };
-  for (size_t i = 0; i < dws.size(); ++i) {
-    add(dws[i]);
-    if (dbs[i].has_value() && dbs[i]->defined()) add(*dbs[i]);
-  }
-  if (lz_hi > lz_lo) iv.emplace_back(lz_lo, lz_hi);
-  std::sort(iv.begin(), iv.end());
+  const bool fused = sq_parts.has_value() && sq_parts->defined();
   WgradSq sq;
-  sq.parts = sq_parts->data_ptr<float>();
-  sq.nparts = np;
-  sq.base = base;
-  int64_t cur = 0, rest = 0;
-  auto gap = [&](int64_t lo, int64_t hi) {
-    if (hi <= lo) return;
-    TORCH_CHECK(sq.nr < WSQ_MAX_RANGES, "wgrad_multi: more than 16 arena ranges outside the weight gradients");
-    sq.lo[sq.nr] = lo;
-    sq.hi[sq.nr] = hi;
-    ++sq.nr;
-    rest += hi - lo;
-  };
-  for (const auto& [lo, hi] : iv) {
-    TORCH_CHECK(lo >= cur, "wgrad_multi: overlapping weight-gradient targets (the partials would count them twice)");
-    gap(cur, lo);
-    cur = std::max(cur, hi);
+  int np = 0;
+  if (fused) {
+    TORCH_CHECK(arena.has_value() && arena->defined(), "wgrad_multi: grad-norm partials need the gradient arena");
+    CHECK_IN((*sq_parts), F32); CHECK_IN((*arena), F32);
+    np = check_parts(*sq_parts, "wgrad_multi");
+    const float* base = arena->data_ptr<float>();
+    const int64_t n = arena->numel();
+    // element intervals of the targets inside the arena
+    std::vector<std::pair<int64_t, int64_t>> iv;
+    auto add = [&](const Tensor& t) {
+      TORCH_CHECK(t.is_contiguous(), "wgrad_multi: grad-norm fusion needs contiguous targets");
+      const int64_t off = t.data_ptr<float>() - base;
+      TORCH_CHECK(off >= 0 && off + t.numel() <= n, "wgrad_multi: a weight-gradient target lies outside the arena");
+      iv.emplace_back(off, off + t.numel());
+    };
+    for (size_t i = 0; i < dws.size(); ++i) {
+      add(dws[i]);
+      if (dbs[i].has_value() && dbs[i]->defined()) add(*dbs[i]);
+    }
+    if (lz_hi > lz_lo) iv.emplace_back(lz_lo, lz_hi);
+    std::sort(iv.begin(), iv.end());
+    sq.base = base;
+    int64_t cur = 0, rest = 0;
+    auto gap = [&](int64_t lo, int64_t hi) {
+      if (hi <= lo) return;
+      TORCH_CHECK(sq.nr < WSQ_MAX_RANGES, "wgrad_multi: more than 16 arena ranges outside the weight gradients");
+      sq.lo[sq.nr] = lo;
+      sq.hi[sq.nr] = hi;
+      ++sq.nr;
+      rest += hi - lo;
+    };
+    for (const auto& [lo, hi] : iv) {
+      TORCH_CHECK(lo >= cur, "wgrad_multi: overlapping weight-gradient targets (the partials would count them twice)");
+      gap(cur, lo);
+      cur = std::max(cur, hi);
+    }
+    gap(cur, n);
+    sq.tail = (int)std::min<int64_t>(64, std::max<int64_t>(1, (rest + 256 * 16 - 1) / (256 * 16)));
   }
-  gap(cur, n);
-  sq.tail = (int)std::min<int64_t>(64, std::max<int64_t>(1, (rest + 256 * 16 - 1) / (256 * 16)));
-  TORCH_CHECK(tiles + sq.tail <= np, "wgrad_multi: grad-norm partial buffer too small (", np, " < ", tiles, " tiles + ",
-              sq.tail, ")");
-  gemm_wgrad_multi(probs.data(), (int)probs.size(), cur_stream(), store, &sq);
+  const size_t total = dys.size();
+  int used = 0;  // partial slots written by earlier launches
+  for (size_t a = 0; a < total; a += 32) {
+    const size_t e = std::min(total, a + 32);
+    std::vector<Tensor> d(dys.begin() + a, dys.begin() + e), x(xs.begin() + a, xs.begin() + e),
+        w(dws.begin() + a, dws.begin() + e);
+    std::vector<c10::optional<Tensor>> b(dbs.begin() + a, dbs.begin() + e);
+    std::vector<GemmArgs> probs = wgrad_probs(d, x, w, b, nullptr, nullptr);
+    if (!fused) {
+      gemm_wgrad_multi(probs.data(), (int)probs.size(), cur_stream(), store);
+      continue;
+    }
+    WgradSq s = sq;
+    s.parts = sq_parts->data_ptr<float>() + used;
+    s.nparts = np - used;
+    if (e < total) {  // tail ranges and zero fill ride in the last launch
+      s.nr = 0;
+      s.tail = 0;
+    }
+    used += gemm_wgrad_multi(probs.data(), (int)probs.size(), cur_stream(), store, &s);
+  }
 }
 
 // fp32 <-> bf16 gradient wire (csrc/comm_wire.hip): one fused 16-B-vector
@@ -1001,8 +1000,6 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("attn_fwd(Tensor qkv, float scale, Tensor rng, int site, float p, Tensor? keep_out=None) -> (Tensor, Tensor)");
   m.def("attn_keep_words(int B, int H, int N, int hd) -> int", &attn_keep_words_op);
   m.def("gemm_tile_override(int cfg) -> int", &gemm_tile_override_op);
-  m.def("attn_stamps(Tensor? buf) -> ()", &attn_stamps);
-  m.def("ln_stamps(Tensor? buf) -> ()", &ln_stamps);
   m.def("linear_residual_fwd(Tensor a, Tensor w, Tensor b, Tensor x, int N, Tensor rng, int site_drop, "
         "float p_drop, int site_dp, float p_dp, Tensor(a!)? st_out=None, Tensor(b!)? xb_out=None) -> Tensor");
   m.def("linear_gelu_fwd(Tensor a, Tensor w, Tensor b, Tensor rng, int site, float p, Tensor? ln_st=None, "

@@ -765,7 +765,7 @@ void gemm_wgrad(const GemmArgs& a, int splits, hipStream_t stream) {
   launch_auto<true, true, EPI_ATOMIC>(p, splits, stream);
 }
 
-void gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool store, const WgradSq* sq) {
+int gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool store, const WgradSq* sq) {
   if (n < 1 || n > WM_MAX) throw std::runtime_error("gemm_wgrad_multi: 1..32 problems per launch");
   WgradMulti gm{};
   gm.n = n;
@@ -793,8 +793,9 @@ void gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool sto
   for (int i = n; i <= WM_MAX; ++i) gm.tile_start[i] = tiles;
   int extra = 0;
   if (sq != nullptr && sq->parts != nullptr) {
-    if (sq->tail < 1 || sq->nr < 0 || sq->nr > WSQ_MAX_RANGES || sq->nparts < tiles + sq->tail)
-      throw std::runtime_error("gemm_wgrad_multi: grad-norm partials need nparts >= tiles + tail and <= 16 ranges");
+    if (sq->tail < 0 || sq->nr < 0 || sq->nr > WSQ_MAX_RANGES || sq->nparts < tiles + sq->tail)
+      throw std::runtime_error("gemm_wgrad_multi: grad-norm partial buffer too small (nparts < tiles + tail) "
+                               "or more than 16 ranges");
     gm.sq = *sq;
     extra = sq->tail;
   }
@@ -806,5 +807,6 @@ void gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool sto
     hipLaunchKernelGGL((gemm_wgrad_multi_kernel<64, 3>), dim3(tiles + extra), dim3(256), 3 * (64 * 128 + 64 * 128),
                        stream, gm);
   }
+  return tiles;
 }
 

@@ -97,8 +97,10 @@ struct WgradSq {
   int nr = 0, tail = 0;
   int64_t lo[WSQ_MAX_RANGES], hi[WSQ_MAX_RANGES];
 };
-void gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool store = false,
-                      const WgradSq* sq = nullptr);
+// returns the output tiles launched (grad-norm partial slots used before the tail);
+// sq->tail = 0: no tail workgroups, no zero fill (all but the last launch of a step)
+int gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool store = false,
+                     const WgradSq* sq = nullptr);
 
 // LayerNorm (layernorm.hip)
 void layernorm_fwd_launch(const float* x, const float* gamma, const float* beta, void* y_bf16, float* mean,
@@ -151,8 +153,6 @@ void replica_reduce_launch(float* ws, float* const* dsts_dev, int G, int C, hipS
 // the short-sequence forward and read by its backward instead of re-hashing
 // (ignored by the long-sequence kernels, which always regenerate)
 int64_t attn_keep_words(int B, int H, int N, int hd);
-void attn_set_stamps(void* buf);
-void ln_set_stamps(void* buf);  // profiling: [grid][5] phase stamps of the LayerNorm backward (nullptr: off)
 void attn_fwd_launch(const void* qkv, void* o, float* lse, int B, int H, int N, int hd, float scale,
                      const int64_t* rng, int site, double p, hipStream_t stream, uint32_t* keep_bits = nullptr);
 void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const float* lse, void* dqkv,

@@ -66,23 +66,6 @@ __global__ __launch_bounds__(NW * 64) void ln_fwd_kernel(const float* __restrict
   }
 }
 
-// profiling aid (tools/ub_lnbwd_stamps.py, build with DDIM_COLD_LN_STAMPS=1): when
-// set, thread 0 of every LayerNorm backward workgroup records s_memrealtime at its
-// phase boundaries, [grid][5].  Compiled out by default: the pointer load and the
-// five tests cost the kernel time in the step profile.
-#ifndef DDIM_COLD_LN_STAMPS
-#define DDIM_COLD_LN_STAMPS 0
-#endif
-__device__ unsigned long long* g_ln_stamps = nullptr;
-__device__ __forceinline__ void ln_stamp(int k) {
-#if DDIM_COLD_LN_STAMPS
-  unsigned long long* s = g_ln_stamps;
-  if (s != nullptr && threadIdx.x == 0) s[(size_t)blockIdx.x * 5 + k] = __builtin_amdgcn_s_memrealtime();
-#else
-  (void)k;
-#endif
-}
-
 // DYB: dy (and its K-split partials) in bf16 -- the dgrad GEMMs write half the bytes
 template <int VEC, int RPW, int NW, bool DYB>
 __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict__ dyv, const float* __restrict__ x,
@@ -109,7 +92,6 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict_
     gm[i] = g2[lane + 64 * i];
     bt[i] = y_out ? reinterpret_cast<const float2*>(beta)[lane + 64 * i] : make_float2(0.f, 0.f);
   }
-  ln_stamp(0);
   uint32_t salt_drop = 0, salt_dp = 0;
   if (gy) {
     if (thr_drop) salt_drop = site_salt(rng, site_drop);
@@ -171,7 +153,6 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict_
     }
     const float c1 = wave_sum(s1) * (1.0f / D);
     const float c2 = wave_sum(s2) * (1.0f / D);
-    if (j == 0) ln_stamp(1);  // the row's loads have landed
     float dpsc = 1.f;
     if (gy && thr_dp) dpsc = dropout_keep(salt_dp, (uint32_t)(row / tokens), thr_dp) ? sc_dp : 0.f;
 #pragma unroll
@@ -203,7 +184,6 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict_
       }
     }
   }
-  ln_stamp(2);
   // column partials: waves -> LDS -> one atomic per column per workgroup
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
@@ -214,7 +194,6 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict_
     red[wave][D + c + 1] = dbet[i].y;
   }
   __syncthreads();
-  ln_stamp(3);
   // dgamma||dbeta replicas: ws[R][2D], workgroup b adds into replica b % R (spreads the
   // same-address atomic contention of ~M/8 workgroups over R replicas)
   float* rep = dgb_ws + (size_t)(blockIdx.x % LN_REPLICAS) * 2 * D;
@@ -224,7 +203,6 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict_
     for (int w = 0; w < NW; ++w) s += red[w][c];
     atomicAdd(rep + c, s);
   }
-  ln_stamp(4);
 }
 
 // dst[g][c] += sum_r ws[g][r][c]; ws zeroed.  One launch finalises many LayerNorms.
@@ -462,11 +440,6 @@ void layernorm_bwd_launch(const void* dy, bool dy_bf16, const float* x, const fl
 }
 
 int ln_replicas() { return LN_REPLICAS; }
-
-void ln_set_stamps(void* buf) {
-  unsigned long long* p = reinterpret_cast<unsigned long long*>(buf);
-  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_ln_stamps), &p, sizeof(p));
-}
 
 void replica_reduce_launch(float* ws, float* const* dsts_dev, int G, int C, hipStream_t stream) {
   hipLaunchKernelGGL(replica_reduce_kernel, dim3((C + 255) / 256, G), dim3(256), 0, stream, ws, dsts_dev, C);

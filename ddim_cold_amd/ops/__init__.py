@@ -344,17 +344,14 @@ def linear_wgrad_multi(jobs, store: bool = False, sq=None):
     target and outside ``lazy`` = (lo, hi).  Replaces the separate sqnorm pass."""
     if not jobs:
         return
-    if sq is not None and len(jobs) > 32:
-        raise ValueError("linear_wgrad_multi: grad-norm partials need all jobs in one launch (<= 32)")
-    if _hip(jobs[0][0]):
-        for a in range(0, len(jobs), 32):
-            dys, xs, dws, dbs = (list(z) for z in zip(*jobs[a:a + 32]))
-            if sq is None:
-                _ops().linear_wgrad_multi(dys, xs, dws, dbs, bool(store))
-            else:
-                parts, arena, lazy = sq
-                lo, hi = lazy if lazy is not None else (0, 0)
-                _ops().linear_wgrad_multi(dys, xs, dws, dbs, bool(store), parts, arena, int(lo), int(hi))
+    if _hip(jobs[0][0]):  # (more than 32 jobs: consecutive launches of <= 32)
+        dys, xs, dws, dbs = (list(z) for z in zip(*jobs))
+        if sq is None:
+            _ops().linear_wgrad_multi(dys, xs, dws, dbs, bool(store))
+        else:
+            parts, arena, lazy = sq
+            lo, hi = lazy if lazy is not None else (0, 0)
+            _ops().linear_wgrad_multi(dys, xs, dws, dbs, bool(store), parts, arena, int(lo), int(hi))
         return
     for dy, x, dw, db in jobs:
         if store:

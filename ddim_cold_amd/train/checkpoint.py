@@ -104,6 +104,16 @@ class CheckpointWriter:
         self._thread = None
         self._err: BaseException | None = None
         self.last_write_s = 0.0
+        # the last write's phases (s): host copy wait, dict layout, file writes
+        self.last_write_parts = (0.0, 0.0, 0.0)
+
+    @staticmethod
+    def warm():
+        """One-time costs of the first write paid up front, not inside the first
+        epoch: torch.save's serializer and the zip writer (to memory)."""
+        import io
+        buf = io.BytesIO()
+        torch.save({"w": torch.zeros(4), "step": 0, "nested": {"a": [1.0]}}, buf)
 
     def submit(self, snap, lastepoch_path: str, epoch: int, steps: int, loss_rec: float, metric: float,
                best_path: str | None = None):
@@ -114,11 +124,16 @@ class CheckpointWriter:
         def work():
             try:
                 t0 = time.perf_counter()
+                snap.wait()
+                t1 = time.perf_counter()
                 d = lastepoch_dict(snap, epoch, steps, loss_rec, metric)
+                t2 = time.perf_counter()
                 if best_path is not None:
                     _atomic_save(strip_prefix(d["state_dict"]), best_path)
                 _atomic_save(d, lastepoch_path)
-                self.last_write_s = time.perf_counter() - t0
+                t3 = time.perf_counter()
+                self.last_write_s = t3 - t0
+                self.last_write_parts = (t1 - t0, t2 - t1, t3 - t2)
             except BaseException as e:  # surfaced by the next join()
                 self._err = e
 

@@ -41,6 +41,7 @@ AdamW step, cosine LR step, zero_grad) re-designed for a latency-bound
 from __future__ import annotations
 
 import math
+import copy
 import os
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Tuple
@@ -1187,11 +1188,16 @@ class TrainEngine:
         self.step_ctr[0] = step
 
     def scheduler_state_dict(self, sched_step: Optional[int] = None) -> dict:
-        """torch CosineAnnealingLR-format state dict (at ``sched_step``, default: now)."""
-        params = self._param_list()
-        opt = torch.optim.AdamW(params, lr=self.cfg.lr)
-        sch = torch.optim.lr_scheduler.CosineAnnealingLR(opt, max(self.cfg.t_max, 1), self.cfg.eta_min)
-        sd = sch.state_dict()
+        """torch CosineAnnealingLR-format state dict (at ``sched_step``, default: now).
+        The key layout comes from a real scheduler built once and cached (building a
+        torch optimizer costs ~1.5 s the first time in a process -- it imports the
+        compiler stack -- which must not land in a background checkpoint write)."""
+        if getattr(self, "_sched_template", None) is None:
+            opt = torch.optim.AdamW([torch.zeros(1, requires_grad=True)], lr=self.cfg.lr)
+            sch = torch.optim.lr_scheduler.CosineAnnealingLR(opt, max(self.cfg.t_max, 1), self.cfg.eta_min)
+            self._sched_template = sch.state_dict()
+        sd = copy.deepcopy(self._sched_template)
+        sd["base_lrs"] = [self.cfg.lr]
         last = int(self.step_ctr[1].item()) if sched_step is None else int(sched_step)
         sd["last_epoch"] = last
         sd["_step_count"] = last + 1

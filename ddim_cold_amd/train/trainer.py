@@ -257,6 +257,12 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
     history = []
     last_ms = None  # device ms/step of the last full log window
     ckw = ckpt.CheckpointWriter()
+    if rank == 0:
+        ckw.warm()
+        # the first torch optimizer / scheduler built in a process imports the compiler stack
+        # (~1.5 s): pay it here, not inside the first background checkpoint write
+        engine.scheduler_state_dict()
+        engine._optimizer_sd(engine.flat_m, engine.flat_v, 0, 0)
     t_start = time.time()
     t_run = t_epoch = time.perf_counter()
     steps0 = steps
@@ -327,7 +333,9 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
                     printLog(f"# perf: epoch {epoch} end to end {steps_per_epoch * B * A * world / wall:.1f} img/s "
                              f"({wall:.3f} s: evaluate {1e3 * (t_ck - t_ev):.1f} ms, checkpoint hand-off "
                              f"{1e3 * (t_end - t_ck):.1f} ms, previous write {1e3 * ckw.last_write_s:.1f} ms "
-                             f"in the background)", paths.log)
+                             f"in the background: host copy wait {1e3 * ckw.last_write_parts[0]:.1f}, layout "
+                             f"{1e3 * ckw.last_write_parts[1]:.1f}, files {1e3 * ckw.last_write_parts[2]:.1f})",
+                             paths.log)
             t_epoch = time.perf_counter()
     except BaseException:
         # a failing step (or an injected fault) must not cut the previous epoch's

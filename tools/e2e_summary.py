@@ -12,6 +12,7 @@ WIN = re.compile(r"# perf: ([\d.]+) img/s\s+([\d.]+) ms/step \(device")
 STEPS = re.compile(r"steps:\s+(\d+) loss: ([\d.]+) time_cost: ([\d.]+)")
 EPOCH = re.compile(r"# perf: epoch (\d+) end to end ([\d.]+) img/s \(([\d.]+) s: evaluate ([\d.]+) ms, "
                    r"checkpoint hand-off ([\d.]+) ms, previous write ([\d.]+) ms")
+PARTS = re.compile(r"host copy wait ([\d.]+), layout ([\d.]+), files ([\d.]+)")
 RUN = re.compile(r"# perf: run end to end ([\d.]+) img/s over (\d+) steps \(([\d.]+) s")
 EPOCH_LINE = re.compile(r"^epoch:\s+(\d+)")
 
@@ -36,7 +37,8 @@ def main(path, title=None):
             continue
         m = EPOCH.search(ln)
         if m:
-            epochs.append(tuple(float(v) for v in m.groups()))
+            p = PARTS.search(ln)
+            epochs.append(tuple(float(v) for v in m.groups()) + (p.group(0) if p else "",))
             continue
         m = RUN.search(ln)
         if m:
@@ -59,10 +61,10 @@ def main(path, title=None):
                 f"of a steady window.", ""]
     if epochs:
         out += ["| epoch | end-to-end img/s | % of steady | wall s | evaluate ms | checkpoint hand-off ms | "
-                "previous write (background) ms |", "|---:|---:|---:|---:|---:|---:|---:|"]
-        for e, rate, wall, ev, ck, wr in epochs:
+                "previous write (background) ms | its phases (ms) |", "|---:|---:|---:|---:|---:|---:|---:|---|"]
+        for e, rate, wall, ev, ck, wr, parts in epochs:
             out.append(f"| {int(e)} | {rate:,.1f} | {100 * rate / st_rate:.1f} % | {wall:.3f} | {ev:.1f} | "
-                       f"{ck:.1f} | {wr:.1f} |")
+                       f"{ck:.1f} | {wr:.1f} | {parts} |")
         later = [x[1] for x in epochs[1:]] or [epochs[0][1]]
         out += ["", f"Epochs after the first (graph capture is in epoch 0): median end to end "
                     f"**{statistics.median(later):,.1f} img/s = {100 * statistics.median(later) / st_rate:.1f} %** "
