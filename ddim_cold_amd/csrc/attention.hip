@@ -569,7 +569,12 @@ static void launch_resident(const bf16* q, bf16* out, float* lse, int B, int H, 
 }
 
 // ============================================================================ backward: dQ (+delta)
-template <int HD>
+// U query groups of 16 per wave (64 U queries per workgroup): every K / V fragment a
+// wave reads from LDS feeds U MFMAs (S and dP of each group), and every K^T fragment of
+// the dQ update U more.  U = 1 is the one launched (see attn_bwd_launch: U = 2 costs
+// occupancy); the two 32-key halves of a tile each run S / dP -> dS -> dQ in turn, so
+// only half a tile's dS is live (128 -> 114 VGPRs).
+template <int HD, int U>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ qkv,
                                                           const bf16* __restrict__ out, const float* __restrict__ lse,
                                                           float* __restrict__ delta, bf16* __restrict__ dqkv, int B,
@@ -585,90 +590,123 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
   const bf16* kb = qkv + ((size_t)B * H + bh) * mat;
   const bf16* vb = qkv + ((size_t)2 * B * H + bh) * mat;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
-  const int q = blockIdx.x * 64 + wave * 16 + li;
-  const bool qv = q < N;
   KvStage<HD> stg;
   stg.load(kb, vb, 0, N);
   const float sl2 = scale * LOG2E;
   const uint32_t salt = thr ? site_salt(rng, site) : 0u;
+  const int ntiles = (N + 63) / 64;
+  const bool kbits = thr && keep != nullptr;
 
-  // dO and O rows of this lane's query are token-major [B, N, D] with head offset h*HD
-  const bf16* dorow = dout + ((size_t)b * N + (qv ? q : 0)) * D + h * HD;
-  const bf16* orow = out + ((size_t)b * N + (qv ? q : 0)) * D + h * HD;
-  bf16x8 qf[C::KS], df[C::KS];
-  float dl = 0.f;
+  int q[U];
+  bf16x8 qf[U][C::KS], df[U][C::KS];
+  float dl[U], nl2[U];
+  uint32_t pgq[U];
+  const u32x2* kcol[U];
 #pragma unroll
-  for (int s = 0; s < C::KS; ++s) {
-    qf[s] = frag_glb<HD>(qb, q, N, s, g);
-    bf16x8 dv, ov;
-    if (qv) {
-      dv = *reinterpret_cast<const bf16x8*>(dorow + 32 * s + 8 * g);
-      ov = *reinterpret_cast<const bf16x8*>(orow + 32 * s + 8 * g);
-    } else {
+  for (int u = 0; u < U; ++u) {
+    q[u] = blockIdx.x * (64 * U) + wave * (16 * U) + 16 * u + li;
+    const bool qv = q[u] < N;
+    // dO and O rows of this lane's query are token-major [B, N, D] with head offset h*HD
+    const bf16* dorow = dout + ((size_t)b * N + (qv ? q[u] : 0)) * D + h * HD;
+    const bf16* orow = out + ((size_t)b * N + (qv ? q[u] : 0)) * D + h * HD;
+    float s = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { dv[j] = f2bf(0.f); ov[j] = f2bf(0.f); }
+    for (int k = 0; k < C::KS; ++k) {
+      qf[u][k] = frag_glb<HD>(qb, q[u], N, k, g);
+      bf16x8 dv, ov;
+      if (qv) {
+        dv = *reinterpret_cast<const bf16x8*>(dorow + 32 * k + 8 * g);
+        ov = *reinterpret_cast<const bf16x8*>(orow + 32 * k + 8 * g);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { dv[j] = f2bf(0.f); ov[j] = f2bf(0.f); }
+      }
+      df[u][k] = dv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += bf2f(dv[j]) * bf2f(ov[j]);
     }
-    df[s] = dv;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dl += bf2f(dv[j]) * bf2f(ov[j]);
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    dl[u] = s;
+    if (qv && g == 0) delta[(size_t)bh * N + q[u]] = s;
+    nl2[u] = qv ? -lse[(size_t)bh * N + q[u]] * LOG2E : -INFINITY;
+    const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q[u]) * attn_mask_ld(N));
+    pgq[u] = ((rowidx >> 1) + 2u * (uint32_t)g) * DROP_GOLDEN;  // pair hash base of this lane's row
+    // the forward's stored keep words of this lane's query (one per key tile)
+    kcol[u] = reinterpret_cast<const u32x2*>(keep) + (size_t)bh * ntiles * N + (qv ? q[u] : 0);
   }
-  dl += __shfl_xor(dl, 16, 64);
-  dl += __shfl_xor(dl, 32, 64);
-  if (qv && g == 0) delta[(size_t)bh * N + q] = dl;
-  const float lse2 = qv ? lse[(size_t)bh * N + q] * LOG2E : INFINITY;
 
-  f32x4 dq[C::DT];
+  f32x4 dq[U][C::DT];
 #pragma unroll
-  for (int d = 0; d < C::DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int d = 0; d < C::DT; ++d) dq[u][d] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   stg.store(lds, lds + C::TILE);
   __syncthreads();
-  const int ntiles = (N + 63) / 64;
-  const float nl2 = -lse2;
-  const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * attn_mask_ld(N));
-  const uint32_t pgq = ((rowidx >> 1) + 2u * (uint32_t)g) * DROP_GOLDEN;  // pair hash base of this lane's row
   // key mask only in the tail tile: a padded key has a zero K row (no dQ
   // contribution) but exp2(0 - lse) can overflow, so it must not reach dS
-  // the forward's stored keep words of this lane's query (one per key tile)
-  const bool kbits = thr && keep != nullptr;
-  const u32x2* kcol = reinterpret_cast<const u32x2*>(keep) + (size_t)bh * ntiles * N + (qv ? q : 0);
   auto tile = [&](int it, auto mask_tag) {
     constexpr bool MASK = decltype(mask_tag)::value;
     const int kv0 = it * 64;
     const bool more = it + 1 < ntiles;
     if (more) stg.load(kb, vb, kv0 + 64, N);  // next tile lands during this tile's MFMAs
-    const u32x2 kw = kbits ? kcol[(size_t)it * N] : u32x2{0u, 0u};
+    u32x2 kw[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) kw[u] = kbits ? kcol[u][(size_t)it * N] : u32x2{0u, 0u};
     const char* Kl = lds + (it & 1) * 2 * C::TILE;
     const char* Vl = Kl + C::TILE;
-    f32x4 ds[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < C::KS; ++s) {
-        st = mfma16(frag_row<HD>(Kl, 16 * t + li, s, g), qf[s], st);
-        dp = mfma16(frag_row<HD>(Vl, 16 * t + li, s, g), df[s], dp);
-      }
-      // the lane's 4 keys are consecutive elements of one mask row (aligned: the
-      // row stride is a multiple of 4): 2 pair hashes instead of 4 single ones
-      bool kp[4] = {true, true, true, true};
-      if (kbits) keep_nibble(kw, t, g, kp);
-      else if (thr) dropout_keep4_pg(salt, pgq + (uint32_t)(kv0 / 2 + 8 * t) * DROP_GOLDEN, thr, kp);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kv0 + 16 * t + 4 * g + r;
-        float pr = fexp2(fmaf(st[r], sl2, nl2));
-        if (MASK && key >= N) pr = 0.f;
-        float dpv = dp[r];
-        if (thr) dpv = kp[r] ? dpv * dsc : 0.f;
-        ds[t][r] = pr * (dpv - dl);
-      }
-    }
+    // two halves of 32 keys: dS of a half feeds its dQ MFMAs right away (half the
+    // live dS registers)
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      const bf16x8 sb = pack8(ds[2 * s2], ds[2 * s2 + 1]);
+      f32x4 ds[U][2];
 #pragma unroll
-      for (int d = 0; d < C::DT; ++d) dq[d] = mfma16(frag_t<C::S>(Kl, 16 * d, s2, lane), sb, dq[d]);
+      for (int th = 0; th < 2; ++th) {
+        const int t = 2 * s2 + th;
+        f32x4 st[U], dp[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          st[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+          dp[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int s = 0; s < C::KS; ++s) {
+          const bf16x8 kfr = frag_row<HD>(Kl, 16 * t + li, s, g);
+          const bf16x8 vfr = frag_row<HD>(Vl, 16 * t + li, s, g);
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            st[u] = mfma16(kfr, qf[u][s], st[u]);
+            dp[u] = mfma16(vfr, df[u][s], dp[u]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          // the lane's 4 keys are consecutive elements of one mask row (aligned: the
+          // row stride is a multiple of 4): 2 pair hashes instead of 4 single ones
+          bool kp[4] = {true, true, true, true};
+          if (kbits) keep_nibble(kw[u], t, g, kp);
+          else if (thr) dropout_keep4_pg(salt, pgq[u] + (uint32_t)(kv0 / 2 + 8 * t) * DROP_GOLDEN, thr, kp);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = kv0 + 16 * t + 4 * g + r;
+            float pr = fexp2(fmaf(st[u][r], sl2, nl2[u]));
+            if (MASK && key >= N) pr = 0.f;
+            float dpv = dp[u][r];
+            if (thr) dpv = kp[r] ? dpv * dsc : 0.f;
+            ds[u][th][r] = pr * (dpv - dl[u]);
+          }
+        }
+      }
+      bf16x8 sb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) sb[u] = pack8(ds[u][0], ds[u][1]);
+#pragma unroll
+      for (int d = 0; d < C::DT; ++d) {
+        const bf16x8 kt = frag_t<C::S>(Kl, 16 * d, s2, lane);
+#pragma unroll
+        for (int u = 0; u < U; ++u) dq[u][d] = mfma16(kt, sb[u], dq[u][d]);
+      }
     }
     if (more) stg.store(lds + ((it + 1) & 1) * 2 * C::TILE, lds + ((it + 1) & 1) * 2 * C::TILE + C::TILE);
     __syncthreads();
@@ -676,20 +714,28 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
   const int nfull = N / 64;
   for (int it = 0; it < nfull; ++it) tile(it, std::false_type{});
   if (nfull < ntiles) tile(nfull, std::true_type{});
-  if (qv) {
-    bf16* row = dqkv + ((size_t)b * N + q) * (3 * D) + h * HD;
 #pragma unroll
-    for (int d = 0; d < C::DT; ++d) {
-      bf16x4 v;
-      v[0] = f2bf(dq[d][0] * scale); v[1] = f2bf(dq[d][1] * scale);
-      v[2] = f2bf(dq[d][2] * scale); v[3] = f2bf(dq[d][3] * scale);
-      *reinterpret_cast<bf16x4*>(row + 16 * d + 4 * g) = v;
+  for (int u = 0; u < U; ++u) {
+    if (q[u] < N) {
+      bf16* row = dqkv + ((size_t)b * N + q[u]) * (3 * D) + h * HD;
+#pragma unroll
+      for (int d = 0; d < C::DT; ++d) {
+        bf16x4 v;
+        v[0] = f2bf(dq[u][d][0] * scale); v[1] = f2bf(dq[u][d][1] * scale);
+        v[2] = f2bf(dq[u][d][2] * scale); v[3] = f2bf(dq[u][d][3] * scale);
+        *reinterpret_cast<bf16x4*>(row + 16 * d + 4 * g) = v;
+      }
     }
   }
 }
 
 // ============================================================================ backward: dK, dV
-template <int HD>
+// U key groups of 16 per wave (64 U keys per workgroup): every Q / dO fragment read
+// from LDS feeds the S^T and dP^T MFMAs of U key groups, every dO^T / Q^T fragment the
+// dV / dK updates of U groups (see attn_bwd_dq_kernel).  Per 32-query half of a tile:
+// S^T / dP^T -> P / dS -> dV / dK, so half a tile's P and dS are live: 186 -> 150
+// VGPRs, 2 -> 3 waves per SIMD, N=626 backward 161 -> 146 us (p=0.1, stored masks).
+template <int HD, int U>
 __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restrict__ dout,
                                                            const bf16* __restrict__ qkv,
                                                            const float* __restrict__ lse,
@@ -700,8 +746,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
   using C = AC<HD>;
   __shared__ __attribute__((aligned(16))) char lds[4 * C::TILE];  // [buf][Q | dO], double-buffered
   __shared__ float s_lse[2][64], s_del[2][64];
-  // the forward's keep words of the query tile (this workgroup's 64 keys), [buf][half][query]
-  __shared__ __attribute__((aligned(16))) uint32_t s_keep[2][2][64];
+  // the forward's keep words of the query tile for this workgroup's U 64-key tiles,
+  // [buf][key tile][half][query]
+  __shared__ __attribute__((aligned(16))) uint32_t s_keep[2][U][2][64];
   const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
   const int D = H * HD;
   const size_t mat = (size_t)N * HD;
@@ -709,31 +756,36 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
   const bf16* kb = qkv + ((size_t)B * H + bh) * mat;
   const bf16* vb = qkv + ((size_t)2 * B * H + bh) * mat;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
-  const int key = blockIdx.x * 64 + wave * 16 + li;  // this lane's key (column of S)
   const float sl2 = scale * LOG2E;
   const uint32_t salt = thr ? site_salt(rng, site) : 0u;
 
-  bf16x8 kf[C::KS], vf[C::KS];
+  int key[U];  // this lane's keys (columns of S)
+  bf16x8 kf[U][C::KS], vf[U][C::KS];
+  f32x4 dk[U][C::DT], dv[U][C::DT];
 #pragma unroll
-  for (int s = 0; s < C::KS; ++s) {
-    kf[s] = frag_glb<HD>(kb, key, N, s, g);
-    vf[s] = frag_glb<HD>(vb, key, N, s, g);
-  }
-  f32x4 dk[C::DT], dv[C::DT];
+  for (int u = 0; u < U; ++u) {
+    key[u] = blockIdx.x * (64 * U) + wave * (16 * U) + 16 * u + li;
 #pragma unroll
-  for (int d = 0; d < C::DT; ++d) {
-    dk[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-    dv[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < C::KS; ++s) {
+      kf[u][s] = frag_glb<HD>(kb, key[u], N, s, g);
+      vf[u][s] = frag_glb<HD>(vb, key[u], N, s, g);
+    }
+#pragma unroll
+    for (int d = 0; d < C::DT; ++d) {
+      dk[u][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dv[u][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   }
 
   // register-staged prefetch of the next query tile: Q rows (head-major), dO rows
-  // (token-major, head slice), LSE and delta
+  // (token-major, head slice), LSE, delta and the keep words
   constexpr int PER = 64 * C::CPR / 256;
   u32x4 rq[PER], rd[PER];
   float rl = INFINITY, rdl = 0.f;
   const bool kbits = thr && keep != nullptr;
   const int ntiles = (N + 63) / 64;
   u32x2 rk = u32x2{0u, 0u};
+  const int kt_mine = blockIdx.x * U + (threadIdx.x >> 6);  // key tile whose word this thread stages
   auto load_tile = [&](int q0) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
@@ -746,13 +798,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
       rq[i] = q0 + r < N ? qv4 : z;
       rd[i] = q0 + r < N ? dv4 : z;
     }
-    if (threadIdx.x < 64) {
-      const int qq = q0 + threadIdx.x;
+    if (threadIdx.x < 64 * U) {
+      const int qq = q0 + (threadIdx.x & 63);
       const int qc = qq < N ? qq : N - 1;
-      const float l = lse[(size_t)bh * N + qc], dd = delta[(size_t)bh * N + qc];
-      rl = qq < N ? l * LOG2E : INFINITY;
-      rdl = qq < N ? dd : 0.f;
-      if (kbits) rk = reinterpret_cast<const u32x2*>(keep)[((size_t)bh * ntiles + blockIdx.x) * N + qc];
+      if (threadIdx.x < 64) {
+        const float l = lse[(size_t)bh * N + qc], dd = delta[(size_t)bh * N + qc];
+        rl = qq < N ? l * LOG2E : INFINITY;
+        rdl = qq < N ? dd : 0.f;
+      }
+      if (kbits && kt_mine < ntiles) rk = reinterpret_cast<const u32x2*>(keep)[((size_t)bh * ntiles + kt_mine) * N + qc];
     }
   };
   auto store_tile = [&](int buf) {
@@ -768,15 +822,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
     if (threadIdx.x < 64) {
       s_lse[buf][threadIdx.x] = rl;
       s_del[buf][threadIdx.x] = rdl;
-      s_keep[buf][0][threadIdx.x] = rk[0];
-      s_keep[buf][1][threadIdx.x] = rk[1];
+    }
+    if (threadIdx.x < 64 * U) {
+      s_keep[buf][threadIdx.x >> 6][0][threadIdx.x & 63] = rk[0];
+      s_keep[buf][threadIdx.x >> 6][1][threadIdx.x & 63] = rk[1];
     }
   };
   load_tile(0);
   store_tile(0);
   __syncthreads();
-  // this lane's key within the workgroup's 64: bit (kl & 31) of word half kl >> 5 (wave-uniform)
-  const int kl = wave * 16 + li, khalf = kl >> 5, kshift = kl & 31;
   for (int it = 0; it < ntiles; ++it) {
     const int q0 = it * 64;
     const bool more = it + 1 < ntiles;
@@ -786,78 +840,118 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
     const char* Dl = Ql + C::TILE;
     const float* sl = s_lse[buf];
     const float* sd = s_del[buf];
-    f32x4 pm[4], ds[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < C::KS; ++s) {
-        st = mfma16(frag_row<HD>(Ql, 16 * t + li, s, g), kf[s], st);
-        dp = mfma16(frag_row<HD>(Dl, 16 * t + li, s, g), vf[s], dp);
-      }
-      // keep flags of (query 16t+4g+r, this lane's key): a mask pair is two adjacent
-      // keys of one row, held by lanes li and li^1 -- each of the two hashes the
-      // pair of 2 of the 4 rows and they swap the results (2 hashes per lane, not 4)
-      bool kp[4] = {true, true, true, true};
-      if (kbits) {
-        const u32x4 w = *reinterpret_cast<const u32x4*>(&s_keep[buf][khalf][16 * t + 4 * g]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) kp[r] = (w[r] >> kshift) & 1u;
-      } else if (thr) {
-        const int odd = li & 1;
-        // pair index of (query qq, key pair) = qq_row * ld/2 + key/2: the multiply by the
-        // golden constant is hoisted (pg of query q0+4g+2odd, + (16t+u) rows of ldh*golden)
-        const uint32_t ldh = (uint32_t)(attn_mask_ld(N) >> 1);
-        const uint32_t pb = ((uint32_t)(bh * N + q0 + 4 * g + 2 * odd) * ldh + (uint32_t)(key >> 1)) * DROP_GOLDEN;
-        const uint32_t ldhg = ldh * DROP_GOLDEN;
-        uint32_t hw[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) hw[u] = mix32((pb + (uint32_t)(16 * t + u) * ldhg) ^ salt);
-        const uint32_t p0 = (uint32_t)__shfl_xor((int)hw[0], 1, 64), p1 = (uint32_t)__shfl_xor((int)hw[1], 1, 64);
-        const uint32_t hr[4] = {odd ? p0 : hw[0], odd ? p1 : hw[1], odd ? hw[0] : p0, odd ? hw[1] : p1};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) kp[r] = (odd ? (hr[r] >> 16) : (hr[r] & 0xFFFFu)) >= thr;
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int qr = 16 * t + 4 * g + r;
-        const float pr = fexp2(fmaf(st[r], sl2, -sl[qr]));  // padded queries: lse = +inf -> 0
-        float pd = pr, dpv = dp[r];
-        if (thr) {
-          pd = kp[r] ? pr * dsc : 0.f;
-          dpv = kp[r] ? dpv * dsc : 0.f;
-        }
-        pm[t][r] = pd;
-        ds[t][r] = pr * (dpv - sd[qr]);
-      }
-    }
+    // two halves of 32 queries: P / dS of a half feed its dV / dK MFMAs right away
+    // (half the live P / dS registers)
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      const bf16x8 pb = pack8(pm[2 * s2], pm[2 * s2 + 1]);
-      const bf16x8 sb = pack8(ds[2 * s2], ds[2 * s2 + 1]);
+    f32x4 pm[U][2], ds[U][2];
+#pragma unroll
+    for (int th = 0; th < 2; ++th) {
+      const int t = 2 * s2 + th;
+      f32x4 st[U], dp[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        st[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) {
+        const bf16x8 qfr = frag_row<HD>(Ql, 16 * t + li, s, g);
+        const bf16x8 dfr = frag_row<HD>(Dl, 16 * t + li, s, g);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          st[u] = mfma16(qfr, kf[u][s], st[u]);
+          dp[u] = mfma16(dfr, vf[u][s], dp[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        // keep flags of (query 16t+4g+r, this lane's key u)
+        bool kp[4] = {true, true, true, true};
+        if (kbits) {
+          // this lane's key within the workgroup's 64 U: word (tile kl >> 6, half
+          // (kl >> 5) & 1), bit kl & 31 -- wave-uniform tile and half
+          const int kl = wave * (16 * U) + 16 * u + li;
+          const u32x4 w = *reinterpret_cast<const u32x4*>(&s_keep[buf][kl >> 6][(kl >> 5) & 1][16 * t + 4 * g]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) kp[r] = (w[r] >> (kl & 31)) & 1u;
+        } else if (thr) {
+          // a mask pair is two adjacent keys of one row, held by lanes li and li^1 --
+          // each of the two hashes the pair of 2 of the 4 rows and they swap the results
+          // (2 hashes per lane, not 4); the golden-constant multiply is hoisted
+          const int odd = li & 1;
+          const uint32_t ldh = (uint32_t)(attn_mask_ld(N) >> 1);
+          const uint32_t pb = ((uint32_t)(bh * N + q0 + 4 * g + 2 * odd) * ldh + (uint32_t)(key[u] >> 1)) * DROP_GOLDEN;
+          const uint32_t ldhg = ldh * DROP_GOLDEN;
+          uint32_t hw[2];
+#pragma unroll
+          for (int v = 0; v < 2; ++v) hw[v] = mix32((pb + (uint32_t)(16 * t + v) * ldhg) ^ salt);
+          const uint32_t p0 = (uint32_t)__shfl_xor((int)hw[0], 1, 64), p1 = (uint32_t)__shfl_xor((int)hw[1], 1, 64);
+          const uint32_t hr[4] = {odd ? p0 : hw[0], odd ? p1 : hw[1], odd ? hw[0] : p0, odd ? hw[1] : p1};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) kp[r] = (odd ? (hr[r] >> 16) : (hr[r] & 0xFFFFu)) >= thr;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qr = 16 * t + 4 * g + r;
+          const float pr = fexp2(fmaf(st[u][r], sl2, -sl[qr]));  // padded queries: lse = +inf -> 0
+          float pd = pr, dpv = dp[u][r];
+          if (thr) {
+            pd = kp[r] ? pr * dsc : 0.f;
+            dpv = kp[r] ? dpv * dsc : 0.f;
+          }
+          pm[u][th][r] = pd;
+          ds[u][th][r] = pr * (dpv - sd[qr]);
+        }
+      }
+    }
+    {
+      bf16x8 pb[U], sb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        pb[u] = pack8(pm[u][0], pm[u][1]);
+        sb[u] = pack8(ds[u][0], ds[u][1]);
+      }
 #pragma unroll
       for (int d = 0; d < C::DT; ++d) {
-        dv[d] = mfma16(frag_t<C::S>(Dl, 16 * d, s2, lane), pb, dv[d]);
-        dk[d] = mfma16(frag_t<C::S>(Ql, 16 * d, s2, lane), sb, dk[d]);
+        const bf16x8 dT = frag_t<C::S>(Dl, 16 * d, s2, lane);
+        const bf16x8 qT = frag_t<C::S>(Ql, 16 * d, s2, lane);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          dv[u][d] = mfma16(dT, pb[u], dv[u][d]);
+          dk[u][d] = mfma16(qT, sb[u], dk[u][d]);
+        }
       }
+    }
     }
     if (more) store_tile(buf ^ 1);
     __syncthreads();
   }
-  if (key < N) {
-    bf16* row = dqkv + ((size_t)b * N + key) * (3 * D) + h * HD;
 #pragma unroll
-    for (int d = 0; d < C::DT; ++d) {
-      bf16x4 kv, vv;
-      kv[0] = f2bf(dk[d][0] * scale); kv[1] = f2bf(dk[d][1] * scale);
-      kv[2] = f2bf(dk[d][2] * scale); kv[3] = f2bf(dk[d][3] * scale);
-      vv[0] = f2bf(dv[d][0]); vv[1] = f2bf(dv[d][1]);
-      vv[2] = f2bf(dv[d][2]); vv[3] = f2bf(dv[d][3]);
-      *reinterpret_cast<bf16x4*>(row + D + 16 * d + 4 * g) = kv;
-      *reinterpret_cast<bf16x4*>(row + 2 * D + 16 * d + 4 * g) = vv;
+  for (int u = 0; u < U; ++u) {
+    if (key[u] < N) {
+      bf16* row = dqkv + ((size_t)b * N + key[u]) * (3 * D) + h * HD;
+#pragma unroll
+      for (int d = 0; d < C::DT; ++d) {
+        bf16x4 kv, vv;
+        kv[0] = f2bf(dk[u][d][0] * scale); kv[1] = f2bf(dk[u][d][1] * scale);
+        kv[2] = f2bf(dk[u][d][2] * scale); kv[3] = f2bf(dk[u][d][3] * scale);
+        vv[0] = f2bf(dv[u][d][0]); vv[1] = f2bf(dv[u][d][1]);
+        vv[2] = f2bf(dv[u][d][2]); vv[3] = f2bf(dv[u][d][3]);
+        *reinterpret_cast<bf16x4*>(row + D + 16 * d + 4 * g) = kv;
+        *reinterpret_cast<bf16x4*>(row + 2 * D + 16 * d + 4 * g) = vv;
+      }
     }
   }
 }
+#define DC_INST_BWD(HD, U)                                                                                       \
+  template __global__ void attn_bwd_dq_kernel<HD, U>(const bf16*, const bf16*, const bf16*, const float*, float*,  \
+                                                     bf16*, int, int, int, float, const int64_t*, int, uint32_t,  \
+                                                     float, const uint32_t*);                                     \
+  template __global__ void attn_bwd_dkv_kernel<HD, U>(const bf16*, const bf16*, const float*, const float*, bf16*, \
+                                                      int, int, int, float, const int64_t*, int, uint32_t, float,  \
+                                                      const uint32_t*);
+DC_INST_BWD(32, 1) DC_INST_BWD(32, 2) DC_INST_BWD(64, 1) DC_INST_BWD(64, 2)
 
 // ============================================================================ short sequences (N <= 128)
 // One workgroup per (b, h) holding the WHOLE sequence: NP = 32*ceil(N/32) padded
@@ -1319,6 +1413,15 @@ void attn_fwd_launch(const void* qkv, void* o, float* lse, int B, int H, int N, 
     hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc);
 }
 
+// long-sequence backward: 16-row groups per wave (0: automatic; tests and benchmarks force 1 / 2)
+static int g_bwd_groups = 0;
+int attn_set_bwd_groups(int u) {
+  if (u < 0 || u > 2) throw std::runtime_error("attn_set_bwd_groups: 0 (auto), 1 or 2");
+  const int old = g_bwd_groups;
+  g_bwd_groups = u;
+  return old;
+}
+
 void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const float* lse, void* dqkv,
                         float* delta, int B, int H, int N, int hd, float scale, const int64_t* rng, int site,
                         double p, hipStream_t stream, const uint32_t* keep_bits) {
@@ -1335,13 +1438,21 @@ void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const flo
     else dispatch_short<64>(true, d, q, oo, nullptr, lse, dq, B, H, N, scale, rng, site, thr, dsc, stream, kb);
     return;
   }
-  if (hd == 32) {
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<32>, grid, dim3(256), 0, stream, d, q, oo, lse, delta, dq, B, H, N, scale, rng, site, thr, dsc, keep_bits);
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<32>, grid, dim3(256), 0, stream, d, q, lse, delta, dq, B, H, N, scale, rng, site, thr, dsc, keep_bits);
-  } else if (hd == 64) {
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<64>, grid, dim3(256), 0, stream, d, q, oo, lse, delta, dq, B, H, N, scale, rng, site, thr, dsc, keep_bits);
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<64>, grid, dim3(256), 0, stream, d, q, lse, delta, dq, B, H, N, scale, rng, site, thr, dsc, keep_bits);
-  } else {
-    throw std::runtime_error("attention: head dim must be 32 or 64");
-  }
+  if (hd != 32 && hd != 64) throw std::runtime_error("attention: head dim must be 32 or 64");
+  // one 16-row group per wave.  Two (U = 2: each LDS fragment feeds two MFMAs) measured
+  // slower at every shape (tools/ub_attn.py, N=626 p=0.1 stored masks: 154.1 vs 146.1 us;
+  // N=2,501: 448 vs 337): 174 / 236 VGPRs put dQ / dK-dV at 2 waves per SIMD, against 4 / 3
+  // for U = 1 -- the kernels need the latency hiding more than the LDS bandwidth
+  const int U = g_bwd_groups > 0 ? g_bwd_groups : 1;
+  const dim3 gridu((N + 64 * U - 1) / (64 * U), B * H);
+#define DC_LAUNCH_BWD(HDV, UV)                                                                                        \
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<HDV, UV>), gridu, dim3(256), 0, stream, d, q, oo, lse, delta, dq, B, H, N,  \
+                     scale, rng, site, thr, dsc, keep_bits);                                                         \
+  hipLaunchKernelGGL((attn_bwd_dkv_kernel<HDV, UV>), gridu, dim3(256), 0, stream, d, q, lse, delta, dq, B, H, N,     \
+                     scale, rng, site, thr, dsc, keep_bits);
+  if (hd == 32 && U == 1) { DC_LAUNCH_BWD(32, 1) }
+  else if (hd == 32) { DC_LAUNCH_BWD(32, 2) }
+  else if (U == 1) { DC_LAUNCH_BWD(64, 1) }
+  else { DC_LAUNCH_BWD(64, 2) }
+#undef DC_LAUNCH_BWD
 }

@@ -26,9 +26,9 @@ def main():
     print(f"# Per-wave hardware counters: {title}\n")
     print("Medians per dispatch; cycles = 4 x SQ_WAVE_CYCLES / SQ_WAVES; wait = SQ_WAIT_ANY (parked on "
           "s_waitcnt / barrier), stall = SQ_WAIT_INST_ANY (issue-stalled), both as % of wave cycles.\n")
-    print("| kernel | waves | cycles/wave | wait % | stall % | VALU/wave | MFMA/wave | SALU/wave | LDS/wave | "
-          "VMEM rd/wave | VMEM wr/wave |")
-    print("|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
+    print("| kernel | waves | cycles/wave | wait % | stall % | VALU/wave | MFMA/wave | VALU/MFMA | SALU/wave | "
+          "LDS/wave | LDS bank conflict cycles/wave | VMEM rd/wave | VMEM wr/wave | L2->HBM fetch MB | write MB |")
+    print("|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
     for k, cs in sorted(agg.items()):
         if any(x in k for x in ("elementwise", "Fill", "copy", "at::")):
             continue
@@ -37,9 +37,13 @@ def main():
         wc = max(m.get("SQ_WAVE_CYCLES", 1), 1)
         print(f"| `{k}` | {w:.0f} | {4 * wc / w:.0f} | {100 * m.get('SQ_WAIT_ANY', 0) / wc:.0f} | "
               f"{100 * m.get('SQ_WAIT_INST_ANY', 0) / wc:.0f} | {m.get('SQ_INSTS_VALU', 0) / w:.0f} | "
-              f"{m.get('SQ_INSTS_MFMA', 0) / w:.0f} | {m.get('SQ_INSTS_SALU', 0) / w:.0f} | "
-              f"{m.get('SQ_INSTS_LDS', 0) / w:.0f} | {m.get('SQ_INSTS_VMEM_RD', 0) / w:.0f} | "
-              f"{m.get('SQ_INSTS_VMEM_WR', 0) / w:.0f} |")
+              f"{m.get('SQ_INSTS_MFMA', 0) / w:.0f} | "
+              f"{m.get('SQ_INSTS_VALU', 0) / max(m.get('SQ_INSTS_MFMA', 0), 1):.1f} | "
+              f"{m.get('SQ_INSTS_SALU', 0) / w:.0f} | "
+              f"{m.get('SQ_INSTS_LDS', 0) / w:.0f} | {m.get('SQ_LDS_BANK_CONFLICT', 0) / w:.1f} | "
+              f"{m.get('SQ_INSTS_VMEM_RD', 0) / w:.0f} | "
+              f"{m.get('SQ_INSTS_VMEM_WR', 0) / w:.0f} | {m.get('FETCH_SIZE', 0) / 1024:.1f} | "
+              f"{m.get('WRITE_SIZE', 0) / 1024:.1f} |")
 
 
 if __name__ == "__main__":
