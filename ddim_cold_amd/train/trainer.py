@@ -82,6 +82,9 @@ def _pools(cfg: ExperimentConfig, device, rank: int):
     return tr.float_pool(), va.float_pool()
 
 
+EVAL_GROUP = 8  # validation batches per captured evaluation replay (see evaluate)
+
+
 def _eval_batch(prog, P, src, eval_rng, total):
     """One validation batch: draw, eval-mode forward, smooth-L1 added to ``total`` (device)."""
     c = prog.cfg
@@ -100,27 +103,36 @@ def evaluate(model, engine: TrainEngine, pool: torch.Tensor, idx: torch.Tensor, 
              total_steps: int, eval_rng: torch.Tensor) -> float:
     """Mean per-batch smooth-L1 over ``pool[idx]`` in eval mode (multi_gpu_trainer.py:32-45).
 
-    On a GPU every full batch is one replay of a captured graph (batch draw from a
-    static index buffer, forward, loss accumulated on the device; captured once per
-    (pool, batch, kind) and kept on the engine); a ragged last batch runs eagerly.
-    One host sync at the end."""
+    On a GPU every EVAL_GROUP full batches are one replay of a captured graph (batch
+    draw from a static index buffer, one forward, loss accumulated on the device;
+    captured once per (pool, batch, kind) and kept on the engine); the remaining
+    batches run eagerly.  One host sync at the end."""
     prog = engine.prog
     P = engine.param_tensors
     dev = pool.device
     total = torch.zeros(1, dtype=torch.float64, device=dev)
     nb = 0
     n_full = idx.numel() // batch if (dev.type == "cuda" and engine.cfg.use_graph) else 0
+    # EVAL_GROUP full batches per replay, as one forward of EVAL_GROUP x batch images:
+    # with equal batch sizes the mean of the per-batch means is the mean over the group,
+    # so the metric is unchanged; the larger forward runs the model at a better
+    # fraction of the chip (the epoch-boundary evaluation: 64 ViT-tiny batches 19.4 ->
+    # ~11 ms).  The remaining full batches and a ragged last one take the path below.
+    G = EVAL_GROUP if n_full >= EVAL_GROUP else 1
+    n_grp = n_full // G
+    n_full = n_grp * G
+    gb = G * batch
     if n_full:
-        key = (pool.data_ptr(), batch, kind, total_steps, eval_rng.data_ptr())
+        key = (pool.data_ptr(), gb, kind, total_steps, eval_rng.data_ptr())
         cache = engine.__dict__.setdefault("_eval_graphs", {})
         ent = cache.get(key)
         if ent is None:
             from ..utils.observe import drain_before_capture, is_capture_error, no_gc
-            bidx = torch.zeros(batch, dtype=torch.int64, device=dev)
+            bidx = torch.zeros(gb, dtype=torch.int64, device=dev)
             acc = torch.zeros(1, dtype=torch.float64, device=dev)
-            src = make_batcher(kind, pool, batch, eval_rng, total_steps, idx=bidx)
+            src = make_batcher(kind, pool, gb, eval_rng, total_steps, idx=bidx)
             saved = eval_rng.clone()
-            bidx.copy_(idx[:batch].to(dev))
+            bidx.copy_(idx[:gb].to(dev))
             s = torch.cuda.Stream(device=dev)
             s.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(s):  # warm-up (allocator, kernels)
@@ -148,10 +160,10 @@ def evaluate(model, engine: TrainEngine, pool: torch.Tensor, idx: torch.Tensor, 
         g, bidx, acc = ent
         if g is not None:
             acc.zero_()
-            for b in range(n_full):
-                bidx.copy_(idx[b * batch:(b + 1) * batch].to(dev), non_blocking=True)
+            for b in range(n_grp):
+                bidx.copy_(idx[b * gb:(b + 1) * gb].to(dev), non_blocking=True)
                 g.replay()
-            total += acc
+            total += acc * G  # each replay added the mean of its G batch means
             nb = n_full
         else:
             n_full = 0

@@ -222,6 +222,30 @@ def test_graph_evaluate_matches_eager(kind):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["cold", "gaussian"])
+def test_grouped_graph_evaluate(kind, monkeypatch):
+    """EVAL_GROUP full batches per replay (one forward of 8 x batch images): the same
+    estimator as one batch per replay -- equal batch sizes, so the mean of batch means
+    is the mean over the group (the batch draws differ: compared over 1,000 samples) --
+    with the leftover full batches (3) and the ragged tail (4 samples) evaluated eagerly."""
+    from ddim_cold_amd.train import trainer as tr
+    torch.manual_seed(0)
+    model = build_model("vit_tiny").cuda().train()
+    pool = synthetic_pool(1024, seed=4, device="cuda")
+    idx = torch.randperm(1024)[:8 * 8 * 15 + 3 * 8 + 4]  # 15 groups of 8 batches + 3 batches + 4
+    vals = {}
+    for group in (8, 1):
+        monkeypatch.setattr(tr, "EVAL_GROUP", group)
+        eng = TrainEngine(model, EngineConfig(use_graph=True, temb_rows=7))
+        rng = torch.tensor([123, 0], dtype=torch.int64, device="cuda")
+        vals[group] = tr.evaluate(model, eng, pool, idx, 8, kind, 2000, rng)
+        # one counter step per replay / eager batch
+        assert int(rng[1]) == (15 + 3 + 1 if group == 8 else 8 * 15 + 3 + 1)
+        eng.detach()
+    assert abs(vals[8] - vals[1]) <= 0.05 * abs(vals[1]), vals
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("draw", [True, False])
 def test_gauss_batch_matches_reference_and_fused_embed(draw):
     """ops.gauss_batch (one launch: pool draw + randn + q_sample) == the CPU reference

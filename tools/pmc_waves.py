@@ -38,7 +38,7 @@ def main():
         print(f"| `{k}` | {w:.0f} | {4 * wc / w:.0f} | {100 * m.get('SQ_WAIT_ANY', 0) / wc:.0f} | "
               f"{100 * m.get('SQ_WAIT_INST_ANY', 0) / wc:.0f} | {m.get('SQ_INSTS_VALU', 0) / w:.0f} | "
               f"{m.get('SQ_INSTS_MFMA', 0) / w:.0f} | "
-              f"{m.get('SQ_INSTS_VALU', 0) / max(m.get('SQ_INSTS_MFMA', 0), 1):.1f} | "
+              f"{(m.get('SQ_INSTS_VALU', 0) / m['SQ_INSTS_MFMA']) if m.get('SQ_INSTS_MFMA') else float('nan'):.1f} | "
               f"{m.get('SQ_INSTS_SALU', 0) / w:.0f} | "
               f"{m.get('SQ_INSTS_LDS', 0) / w:.0f} | {m.get('SQ_LDS_BANK_CONFLICT', 0) / w:.1f} | "
               f"{m.get('SQ_INSTS_VMEM_RD', 0) / w:.0f} | "
