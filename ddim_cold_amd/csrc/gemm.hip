@@ -509,7 +509,11 @@ static int pick_tiles(int M, int N, int K, int splits, bool at, bool bt, bool wi
   if (at) return 1;
   const int forced = g_tile_override.load(std::memory_order_relaxed);
   if (forced >= 0) return bt && forced == 3 ? 2 : forced;
-  if (wide8 && M >= BIG_M) return CFG_W8_256;
+  // 8-wave 256x128 tiles only when they still give about one tile per CU: the
+  // oxford_flower sampler's N = 256 GEMMs (M = 16,448: 130 such tiles) run faster on
+  // 64x64 / 32x64 tiles (tools/ub_gemm_large.py 16448 .. 256: residual 19.7 vs 15.9 us,
+  // GELU 16.0 vs 13.2; vit_small_200 N = 384 at M = 20,032: 237 tiles, 8-wave faster)
+  if (wide8 && M >= BIG_M && ((M + 255) / 256) * ((N + 127) / 128) >= 236) return CFG_W8_256;
   return ((M + 63) / 64) * ((N + 63) / 64) * splits >= 240 ? 1 : 0;
 }
 
@@ -517,7 +521,9 @@ template <bool AT, bool BT, int EPI>
 static void launch_auto(GemmParams p, int splits, hipStream_t stream) {
   const bool dma_ok = (AT || BT || p.K % 64 == 0) && (AT || p.K % 64 == 0);
   if (dma_ok) {
-    int cfg = pick_tiles(p.M, p.N, p.K, splits, AT, BT, Wide8<EPI>::value);
+    // DGELU (input gradient through GELU + dropout, bf16 out) stays on 4-wave tiles at
+    // every measured M (M = 20,032: 25.5 vs 26.5 us; 40,064: 42.1 vs 49.9)
+    int cfg = pick_tiles(p.M, p.N, p.K, splits, AT, BT, Wide8<EPI>::value && EPI != EPI_DGELU);
     // the GELU epilogue (erf-GELU + dropout per element, two bf16 outputs) is the
     // heaviest in vector instructions: twice the waves of 32x64 tiles pay off on the
     // sampler shape (M=4160: 6.56 vs 7.14 us, tools/gpu_tile_sweep3.sh); the other

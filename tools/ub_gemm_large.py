@@ -1,7 +1,7 @@
 """Large-M GEMMs of the vit_small_200 training step (M = B*N = 32*626 = 20,032 token rows,
 D = 384) for every tile config (ops.gemm_tile; -1 = automatic choice) vs hipBLASLt
 (torch.matmul, bf16 out) on the same shapes; graph-timed (tools/ubench.t).
-usage: python tools/ub_gemm_large.py [M] [tiles, e.g. -1,1,4,5]"""
+usage: python tools/ub_gemm_large.py [M] [tiles, e.g. -1,1,4,5] [D (default 384)]"""
 import os
 import sys
 
@@ -14,7 +14,8 @@ from tools.ubench import t  # noqa: E402
 dev = "cuda"
 M = int(sys.argv[1]) if len(sys.argv) > 1 else 20032
 TILES = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [-1, 1, 3, 4, 5]
-D, B, H = 384, 32, 6
+D = int(sys.argv[3]) if len(sys.argv) > 3 else 384
+B, H = 32, D // 64
 N = M // B
 torch.manual_seed(0)
 
@@ -28,6 +29,8 @@ a = bf(M, D)
 w, b = bf(D, D, sc=0.05), torch.randn(D, device=dev)
 w3, b3 = bf(3 * D, D, sc=0.05), torch.randn(3 * D, device=dev)
 x = torch.randn(M, D, device=dev)
+w4, b4 = bf(4 * D, D, sc=0.05), torch.randn(4 * D, device=dev)
+w4t, h4 = bf(D, 4 * D, sc=0.05), bf(M, 4 * D)
 dq = bf(M, 3 * D)
 st = torch.empty(M, D // 32, 2, device=dev)
 xb = torch.empty(M, D, dtype=torch.bfloat16, device=dev)
@@ -38,7 +41,10 @@ cases = [
     ("resid fwd p=.1 dp=.1 +stats", fl1,
      lambda: ops.linear_residual_fwd(a, w, b, x, N, r, 3, 0.1, 4, 0.1, st_out=st, xb_out=xb),
      lambda: torch.matmul(a, w.t())),
-    ("gelu fwd p=0.1", fl1, lambda: ops.linear_gelu_fwd(a, w, b, r, 5, 0.1), None),
+    ("gelu fwd p=0.1 (D x D)", fl1, lambda: ops.linear_gelu_fwd(a, w, b, r, 5, 0.1), None),
+    ("gelu fwd p=0 (4D x D)", 4 * fl1, lambda: ops.linear_gelu_fwd(a, w4, b4, r, 5, 0.0), None),
+    ("resid fwd K=4D", 4 * fl1, lambda: ops.linear_residual_fwd(h4, w4t, b, x, N, r, 3, 0.0, 4, 0.0),
+     lambda: torch.matmul(h4, w4t.t())),
     ("dgrad K=384 bf16 out", fl1, lambda: ops.linear_dgrad(a, w, False), lambda: torch.matmul(a, w)),
     ("dgrad K=384 f32 out", fl1, lambda: ops.linear_dgrad(a, w, True), None),
     ("dgrad-gelu p=0.1", fl1, lambda: ops.linear_dgrad_gelu(a, w, xb, r, 11, 0.1), None),

@@ -37,10 +37,11 @@ for i in range(4):
           flush=True)
 
 # 2. vendor training step: graph vs eager loss trajectory
+MODEL = sys.argv[1] if len(sys.argv) > 1 else "vit_tiny"
 pool = synthetic_pool(1024, (64, 64), seed=7, device=dev)
 for graph in (False, True):
     torch.manual_seed(1234)
-    m = build_model("vit_tiny").to(dev).train()
+    m = build_model(MODEL).to(dev).train()
     st = vb.VendorTrainStep(m, pool, 32, 3.125e-4, 51200, use_graph=graph)
     trace = []
     for i in range(300):
@@ -48,7 +49,8 @@ for graph in (False, True):
         if (i + 1) % 25 == 0:
             trace.append(round(float(st.loss), 4))
     nonfinite = sum(1 for p in m.parameters() if not torch.isfinite(p).all())
-    print(f"vendor step {'graph' if graph else 'eager'}: loss every 25 steps {trace}; non-finite params {nonfinite}",
+    print(f"{MODEL} vendor step {'graph' if graph else 'eager'}: loss every 25 steps {trace}; "
+          f"non-finite params {nonfinite}",
           flush=True)
 
 # 3. vendor sampler: graph vs eager on the same x_T
