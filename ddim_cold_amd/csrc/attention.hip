@@ -571,9 +571,9 @@ static void launch_resident(const bf16* q, bf16* out, float* lse, int B, int H, 
 // ============================================================================ backward: dQ (+delta)
 // U query groups of 16 per wave (64 U queries per workgroup): every K / V fragment a
 // wave reads from LDS feeds U MFMAs (S and dP of each group), and every K^T fragment of
-// the dQ update U more.  U = 1 is the one launched (see attn_bwd_launch: U = 2 costs
-// occupancy); the two 32-key halves of a tile each run S / dP -> dS -> dQ in turn, so
-// only half a tile's dS is live (128 -> 114 VGPRs).
+// the dQ update U more.  Only U = 1 is built (attn_bwd_launch: U = 2 measured slower,
+// it costs occupancy); the two 32-key halves of a tile each run S / dP -> dS -> dQ in
+// turn, so only half a tile's dS is live (128 -> 114 VGPRs).
 template <int HD, int U>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ qkv,
                                                           const bf16* __restrict__ out, const float* __restrict__ lse,
@@ -951,7 +951,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
   template __global__ void attn_bwd_dkv_kernel<HD, U>(const bf16*, const bf16*, const float*, const float*, bf16*, \
                                                       int, int, int, float, const int64_t*, int, uint32_t, float,  \
                                                       const uint32_t*);
-DC_INST_BWD(32, 1) DC_INST_BWD(32, 2) DC_INST_BWD(64, 1) DC_INST_BWD(64, 2)
+DC_INST_BWD(32, 1) DC_INST_BWD(64, 1)
 
 // ============================================================================ short sequences (N <= 128)
 // One workgroup per (b, h) holding the WHOLE sequence: NP = 32*ceil(N/32) padded
@@ -1413,15 +1413,6 @@ void attn_fwd_launch(const void* qkv, void* o, float* lse, int B, int H, int N, 
     hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc);
 }
 
-// long-sequence backward: 16-row groups per wave (0: automatic; tests and benchmarks force 1 / 2)
-static int g_bwd_groups = 0;
-int attn_set_bwd_groups(int u) {
-  if (u < 0 || u > 2) throw std::runtime_error("attn_set_bwd_groups: 0 (auto), 1 or 2");
-  const int old = g_bwd_groups;
-  g_bwd_groups = u;
-  return old;
-}
-
 void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const float* lse, void* dqkv,
                         float* delta, int B, int H, int N, int hd, float scale, const int64_t* rng, int site,
                         double p, hipStream_t stream, const uint32_t* keep_bits) {
@@ -1439,20 +1430,18 @@ void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const flo
     return;
   }
   if (hd != 32 && hd != 64) throw std::runtime_error("attention: head dim must be 32 or 64");
-  // one 16-row group per wave.  Two (U = 2: each LDS fragment feeds two MFMAs) measured
-  // slower at every shape (tools/ub_attn.py, N=626 p=0.1 stored masks: 154.1 vs 146.1 us;
-  // N=2,501: 448 vs 337): 174 / 236 VGPRs put dQ / dK-dV at 2 waves per SIMD, against 4 / 3
-  // for U = 1 -- the kernels need the latency hiding more than the LDS bandwidth
-  const int U = g_bwd_groups > 0 ? g_bwd_groups : 1;
-  const dim3 gridu((N + 64 * U - 1) / (64 * U), B * H);
+  // one 16-row group per wave (U = 1).  Measured slower and not built: U = 2 (every
+  // LDS fragment feeding two MFMAs; N=626 p=0.1 stored masks 154.1 vs 146.1 us, N=2,501
+  // 448 vs 337: 174 / 236 VGPRs put dQ / dK-dV at 2 waves per SIMD against 4 / 3), and
+  // a dK/dV prefetch two query tiles ahead in two register sets (178 VGPRs, 2 waves per
+  // SIMD: 180 vs 146 us) -- the kernels need the latency hiding of occupancy more
+  const dim3 gridu((N + 63) / 64, B * H);
 #define DC_LAUNCH_BWD(HDV, UV)                                                                                        \
   hipLaunchKernelGGL((attn_bwd_dq_kernel<HDV, UV>), gridu, dim3(256), 0, stream, d, q, oo, lse, delta, dq, B, H, N,  \
                      scale, rng, site, thr, dsc, keep_bits);                                                         \
   hipLaunchKernelGGL((attn_bwd_dkv_kernel<HDV, UV>), gridu, dim3(256), 0, stream, d, q, lse, delta, dq, B, H, N,     \
                      scale, rng, site, thr, dsc, keep_bits);
-  if (hd == 32 && U == 1) { DC_LAUNCH_BWD(32, 1) }
-  else if (hd == 32) { DC_LAUNCH_BWD(32, 2) }
-  else if (U == 1) { DC_LAUNCH_BWD(64, 1) }
-  else { DC_LAUNCH_BWD(64, 2) }
+  if (hd == 32) { DC_LAUNCH_BWD(32, 1) }
+  else { DC_LAUNCH_BWD(64, 1) }
 #undef DC_LAUNCH_BWD
 }

@@ -155,7 +155,6 @@ void replica_reduce_launch(float* ws, float* const* dsts_dev, int G, int C, hipS
 int64_t attn_keep_words(int B, int H, int N, int hd);
 void attn_fwd_launch(const void* qkv, void* o, float* lse, int B, int H, int N, int hd, float scale,
                      const int64_t* rng, int site, double p, hipStream_t stream, uint32_t* keep_bits = nullptr);
-int attn_set_bwd_groups(int u);  // long-sequence backward row groups per wave (0 auto, 1, 2); returns the old value
 void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const float* lse, void* dqkv,
                      float* delta, int B, int H, int N, int hd, float scale, const int64_t* rng, int site,
                      double p, hipStream_t stream, const uint32_t* keep_bits = nullptr);

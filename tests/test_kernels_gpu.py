@@ -383,35 +383,6 @@ def test_attention_fwd_bwd(B, H, N, hd, p):
         assert torch.equal(ops.attn_bwd(do, qkv, o, lse, scale, r, 5, p, keep=keep), dq)
 
 
-@pytest.mark.parametrize("B,H,N,hd,p", [(2, 3, 130, 64, 0.2), (1, 2, 400, 32, 0.1), (2, 3, 513, 64, 0.0),
-                                        (2, 2, 626, 64, 0.1), (1, 2, 2501, 64, 0.1), (3, 2, 200, 32, 0.0)])
-def test_attention_bwd_row_groups(B, H, N, hd, p):
-    """Long-sequence backward with 1 and 2 row groups per wave (ops attn_bwd_groups; the
-    automatic choice takes 2 at the model shapes): both match the reference and each
-    other bit for bit (same per-element accumulation order), with re-hashed masks and
-    with the forward's stored keep words."""
-    qkv = bf(3, B, H, N, hd)
-    r = rng()
-    scale = hd ** -0.5
-    keep = ops.attn_keep_buffer(qkv, p)
-    o, lse = ops.attn_fwd(qkv, scale, r, 5, p, keep_out=keep)
-    do = bf(B, N, H * hd)
-    ref_dq = ref.attn_bwd(do, qkv, o, lse, scale, r, 5, p)
-    outs = {}
-    for u in (1, 2):
-        old = torch.ops.ddim_cold.attn_bwd_groups(u)
-        try:
-            outs[u] = ops.attn_bwd(do, qkv, o, lse, scale, r, 5, p)
-            if keep is not None:
-                assert torch.equal(ops.attn_bwd(do, qkv, o, lse, scale, r, 5, p, keep=keep), outs[u])
-        finally:
-            torch.ops.ddim_cold.attn_bwd_groups(old)
-        close(outs[u], ref_dq, 3e-2, 3e-2, f"dqkv U={u}")
-    assert torch.equal(outs[1], outs[2])
-    with pytest.raises(RuntimeError):
-        torch.ops.ddim_cold.attn_bwd_groups(3)
-
-
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_attention_n2501(p):
     """The 200x200 / p=4 sequence length (2,501 tokens, 40 key tiles, ragged tail) the

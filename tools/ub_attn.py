@@ -1,7 +1,6 @@
 """Attention fwd/bwd timings on the model shapes (graph-timed): ViT-tiny train / sampler
-(N=65), OxfordFlower (N=257), vit_small_200 (N=626), 200x200 at p=4 (N=2501); the
-long-sequence backward with 1 and 2 row groups per wave (bwd_us_u1 / bwd_us_u2) and the
-automatic choice (bwd_us).  DDIM_COLD_LIB=<other .so> times another build."""
+(N=65), OxfordFlower (N=257), vit_small_200 (N=626), 200x200 at p=4 (N=2501).
+DDIM_COLD_LIB=<other .so> times another build."""
 import os, sys, json
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -25,12 +24,6 @@ for (B, H, N, hd) in SHAPES:
             fl = 4 * B * H * N * N * hd
             row = {"fwd_us": round(f, 1), "bwd_us": round(b, 1),
                    "fwd_TFLOPs": round(fl / f / 1e6, 1), "bwd_TFLOPs": round(2.5 * fl / b / 1e6, 1)}
-            if N > 128 and hasattr(torch.ops.ddim_cold, "attn_bwd_groups"):
-                for u in (1, 2):
-                    old = torch.ops.ddim_cold.attn_bwd_groups(u)
-                    row[f"bwd_us_u{u}"] = round(t(lambda: ops.attn_bwd(do, qkv, o, lse, hd ** -0.5, r, 5, p, keep=keep),
-                                                  reps=20), 1)
-                    torch.ops.ddim_cold.attn_bwd_groups(old)
             res[f"B{B} H{H} N{N} hd{hd} p{p}" + (" stored-masks" if stored else "")] = row
 for k, v in res.items():
     print(k, v)
