@@ -9,8 +9,9 @@ comparison the hand-written stack has to win.
 * :class:`VendorTrainStep` — `multi_gpu_trainer.py:115-134` as one graph: an
   on-device cold batch draw (pool index + t ~ U{1..log2 W} + NEAREST pixelation
   pair, `diffusion_loader.py:79-97`, in plain torch ops), forward under bf16
-  autocast, ``F.smooth_l1_loss`` (mean as a GEMV; bias gradients as GEMMs:
-  :class:`_AddBias`), backward, ``clip_grad_norm_(1.0)``,
+  autocast (the patch embedding as one GEMM: :func:`_patch_gemm`),
+  ``F.smooth_l1_loss`` (mean as a GEMV; bias gradients as GEMMs: :class:`_AddBias`),
+  backward, ``clip_grad_norm_(1.0)``,
   ``AdamW(wd=0.05, fused=True, capturable=True)`` with the per-iteration cosine
   LR computed on the device (``CosineAnnealingLR``'s closed form, eta_min 0).
 * :class:`VendorSampler` — the 100-step k=20 DDIM loop of `ViT.py:220-237`
@@ -31,7 +32,7 @@ import torch
 import torch.nn.functional as F
 
 
-def vendor_forward(model, x: torch.Tensor, t: torch.Tensor, attn: str = "sdpa") -> torch.Tensor:
+def vendor_forward(model, x: torch.Tensor, t: torch.Tensor, attn: str = "sdpa", patch: str = "conv") -> torch.Tensor:
     """``model.forward_reference`` with the attention core as
     ``F.scaled_dot_product_attention`` (``attn='sdpa'``); same parameters, same
     dropout / drop-path semantics in train mode (`ViT.py:105-137`, `:199-218`).
@@ -39,7 +40,7 @@ def vendor_forward(model, x: torch.Tensor, t: torch.Tensor, attn: str = "sdpa") 
     if attn == "explicit":
         return model.forward_reference(x, t)
     tr = model.training
-    h = _tokens(model, x, t)
+    h = _tokens(model, x, t, patch)
     for blk in model.blocks:
         a = blk.attn
         B, N, C = h.shape
@@ -79,10 +80,10 @@ class _AddBias(torch.autograd.Function):
         return g, (ones @ g2).reshape(ctx.bshape).to(ctx.bdtype)
 
 
-def _linear(mod, x):
+def _linear(mod, x, weight=None):
     """``nn.Linear`` forward (same weight / bias, bf16 under autocast) with the bias
     gradient of :class:`_AddBias`."""
-    y = F.linear(x, mod.weight)
+    y = F.linear(x, mod.weight if weight is None else weight)
     return _AddBias.apply(y, mod.bias) if mod.bias is not None else y
 
 
@@ -105,10 +106,25 @@ def _drop(x, p, training):
     return x * ((torch.rand(x.shape, device=x.device) < keep).to(x.dtype) * (1.0 / keep))
 
 
-def _tokens(model, x, t):
+def _patch_gemm(model, x):
+    """The patch embedding's stride-p convolution as im2col rows times the reshaped conv
+    weight (one GEMM, same values as ``nn.Conv2d`` up to summation order).  The training
+    comparator uses it (``VendorTrainStep(patch="gemm")``): with the MIOpen convolution
+    the graph-replayed oxford_flower (p=4) step turned its parameters NaN in some runs and
+    not others (tools/vendor_flower_check.py: conv 81 non-finite tensors after 220
+    replays in one run, finite in the next; the GEMM form finite and bit-identical with
+    and without host syncs between replays)."""
+    pe = model.patch_embed
+    p = pe.patch_size
+    B, C, H, W = x.shape
+    rows = x.reshape(B, C, H // p, p, W // p, p).permute(0, 2, 4, 1, 3, 5).reshape(B, -1, C * p * p)
+    return _linear(pe.proj, rows, weight=pe.proj.weight.reshape(pe.proj.weight.shape[0], -1))
+
+
+def _tokens(model, x, t, patch="conv"):
     """``prepare_tokens`` (`ViT.py:199-206`) with the pos_drop through :func:`_drop`."""
     B = x.shape[0]
-    tok = model.patch_embed(x)
+    tok = model.patch_embed(x) if patch == "conv" else _patch_gemm(model, x)
     tok = torch.cat((model.cls_token.expand(B, -1, -1).to(tok.dtype), tok), dim=1)
     return _drop(tok + model.pos_embed + model.time_embed(t).unsqueeze(1), model.pos_drop.p, model.training)
 
@@ -139,8 +155,9 @@ class VendorTrainStep:
     """The reference training step from stock PyTorch-ROCm ops, captured whole."""
 
     def __init__(self, model, pool: torch.Tensor, batch: int, lr: float, t_max: int, attn: str = "sdpa",
-                 weight_decay: float = 0.05, clip: float = 1.0, use_graph: bool = True):
+                 weight_decay: float = 0.05, clip: float = 1.0, use_graph: bool = True, patch: str = "gemm"):
         self.model = model.train()
+        self.patch = patch
         self.pool = pool
         self.batch = batch
         self.attn = attn
@@ -172,7 +189,7 @@ class VendorTrainStep:
     def _body(self):
         x_t, target, t = cold_batch_torch(self.pool, self.batch, self.max_t)
         with torch.autocast(self.dev.type, dtype=torch.bfloat16, enabled=self.cuda, cache_enabled=False):
-            pred = vendor_forward(self.model, x_t, t, self.attn)
+            pred = vendor_forward(self.model, x_t, t, self.attn, self.patch)
         loss = _mean(F.smooth_l1_loss(pred.float(), target, reduction="none"))
         loss.backward()
         torch.nn.utils.clip_grad_norm_(self.params, self.clip)

@@ -57,6 +57,20 @@ def test_gemm_bias_grad_and_mean_match_stock_ops():
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
 
 
+def test_patch_gemm_matches_conv():
+    """The comparator's GEMM patch embedding == nn.Conv2d (values and gradients)."""
+    from ddim_cold_amd.bench.vendor_baseline import _patch_gemm
+    m = _tiny()
+    x = torch.randn(2, 3, 16, 16, requires_grad=True)
+    a = _patch_gemm(m, x)
+    b = m.patch_embed(x)
+    torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
+    ga = torch.autograd.grad(a.square().sum(), [x, m.patch_embed.proj.weight, m.patch_embed.proj.bias])
+    gb = torch.autograd.grad(b.square().sum(), [x, m.patch_embed.proj.weight, m.patch_embed.proj.bias])
+    for u, v in zip(ga, gb):
+        torch.testing.assert_close(u, v, rtol=1e-4, atol=1e-5)
+
+
 def test_vendor_train_step_cpu_runs_and_follows_cosine():
     m = _tiny()
     pool = torch.rand(8, 3, 16, 16) * 2 - 1
