@@ -199,6 +199,7 @@ __global__ __launch_bounds__(256) void patchify_cls_kernel(const float* __restri
 }
 
 // part A: (n,d) -> dpos (+dcls) ; part B: (b,d) -> dtemb[t_b] ; part C: patch-row grads (bf16)
+constexpr int EMB_TCHUNK = 64;  // tokens per part-B workgroup
 __global__ __launch_bounds__(256) void embed_bwd_kernel(const float* __restrict__ g, const int64_t* __restrict__ t,
                                                         float* __restrict__ dcls, float* __restrict__ dpos,
                                                         float* __restrict__ dtemb, bf16* __restrict__ gpatch, int B,
@@ -229,21 +230,26 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const float* __restrict_
     dpos[e] += s;
     if (n == 0) dcls[d] += s;
   } else if (bid < blocksA + blocksB) {
-    const int e = (bid - blocksA) * 256 + threadIdx.x;
+    // (b, d) sums over EMB_TCHUNK-token chunks, one chunk per workgroup row: a serial
+    // walk over all N tokens per thread took 61.6 us at N = 626 (48 workgroups)
+    const int nch = (N + EMB_TCHUNK - 1) / EMB_TCHUNK;
+    const int bb = bid - blocksA, ch = bb % nch;
+    const int e = (bb / nch) * 256 + threadIdx.x;
     if (e >= B * D) return;
     const int b = e / D, d = e - b * D;
+    const int n0 = ch * EMB_TCHUNK, n1 = min(N, n0 + EMB_TCHUNK);
     float s = 0.f;
-    int n = 0;
-    for (; n + 8 <= N; n += 8) {
+    int n = n0;
+    for (; n + 8 <= n1; n += 8) {
       float v[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) v[u] = g[((size_t)b * N + n + u) * D + d];
 #pragma unroll
       for (int u = 0; u < 8; ++u) s += thr ? (dropout_keep(salt, (uint32_t)(((size_t)b * N + n + u) * D + d), thr) ? v[u] * dsc : 0.f) : v[u];
     }
-    for (; n < N; ++n) s += gm(((size_t)b * N + n) * D + d);
+    for (; n < n1; ++n) s += gm(((size_t)b * N + n) * D + d);
     const int64_t tb = t[b];
-    atomicAdd(dtemb + (size_t)tb * D + d, s);
+    atomicAdd(dtemb + (size_t)tb * D + d, s);  // samples sharing a t add here too
   } else if (bid >= blocksA + blocksB + blocksC) {
     // part D: LayerNorm dgamma/dbeta replica finalize (replica_reduce_kernel's work;
     // every LayerNorm backward has run before the embedding backward)
@@ -362,7 +368,7 @@ void patchify_cls_launch(const float* img, const int64_t* t, const float* cls, c
 
 void embed_bwd_launch(const float* g, const int64_t* t, float* dcls, float* dpos, float* dtemb, void* gpatch, int B,
                       int N, int D, const int64_t* rng, int site, double p, hipStream_t stream, ReplicaFinal rf) {
-  const int blocksA = cdiv(N * D, 256), blocksB = cdiv(B * D, 256);
+  const int blocksA = cdiv(N * D, 256), blocksB = cdiv(B * D, 256) * cdiv(N, EMB_TCHUNK);
   const int blocksC = grid_for((size_t)B * (N - 1) * D);
   const int blocksD = rf.ws ? rf.G * cdiv(rf.C, 256) : 0;
   const uint32_t thr = drop_threshold_host(p);
