@@ -33,6 +33,10 @@ SITE_EMBED = 1
 # K split of the QKV input-gradient GEMM (reduction dim 3D): the partial products
 # go to separate buffers that the LayerNorm backward sums on load
 QKV_DGRAD_SPLITS = 2
+# ... only below this many token rows: at vit_small_200's 20,032 the unsplit 8-wave
+# GEMM already has ~1 tile per CU and the split's extra partial costs more
+# (tools/ab_module_constant.py: 6.578 / 6.610 vs 6.523 / 6.541 ms/step)
+QKV_SPLIT_MAX_M = 16384
 # the input-gradient GEMMs feeding a LayerNorm backward (head, fc1, QKV) write
 # bf16 (the K-split partials too) instead of fp32: half the bytes on both sides
 # of the dgrad -> LayerNorm-backward hand-off; the LayerNorm backward sums and
@@ -491,7 +495,7 @@ class ViTProgram:
             do = ops.linear_dgrad(gy1, bp.proj_w, False)
             dqkv = ops.attn_bwd(do, qkv, o, lse, c.scale, rng, sa, ad,
                                 keep=S.keeps[i] if len(S.keeps) == L else None)
-            qs = QKV_DGRAD_SPLITS if 3 * D >= 768 else 1
+            qs = QKV_DGRAD_SPLITS if 3 * D >= 768 and M < QKV_SPLIT_MAX_M else 1
             dl1 = ops.linear_dgrad(dqkv, bp.qkv_w, f32, qs)
             l1 = ln_out(l1)
             fk = dict(beta=bp.n1b, y_out=l1) if fold else {}
