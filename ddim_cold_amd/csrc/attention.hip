@@ -263,36 +263,25 @@ __device__ __forceinline__ void flash_softmax_tile(f32x4 (&st)[4], f32x4 (&o)[DT
 }
 
 // Stored attention-dropout masks of the long-sequence kernels: one 64-bit word per
-// (b, h, 64-key tile, query), bit k = keep flag of key 64 * tile + k, as two uint32
-// halves: keep[((bh * ntiles + tile) * N + q) * 2 + (k >> 5)] bit (k & 31) -- tile
-// major, so the 16 queries of a wave-instruction store / load 128 contiguous bytes.
-// The forward writes them (a lane's 16 flags are the keys 16t + 4g + r of its query:
-// the 4 lanes g of a query OR their nibbles together), the two backward kernels
-// read them instead of re-hashing every mask element (dQ: the forward's lane layout;
-// dK/dV: the query tile's 64 words staged in LDS, one bit per lane's key).
-__device__ __forceinline__ uint32_t or_xor16(uint32_t u) {  // u | lane (l ^ 16)'s u
-  const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
-  return r[0] | r[1];
-}
-__device__ __forceinline__ uint32_t or_xor32(uint32_t u) {  // u | lane (l ^ 32)'s u
-  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-  return r[0] | r[1];
-}
+// (b, h, 64-key tile, query) = four 16-bit groups in the forward's lane layout: group g
+// (bits 16 g .. 16 g + 15 of the word, i.e. uint16 [((bh * ntiles + tile) * N + q) * 4 + g])
+// holds the keep flags of keys 16 t + 4 g + r at bit 4 t + r -- each forward lane stores
+// its own 16 flags (no cross-lane assembly; the 64 lanes of a wave-instruction write 128
+// contiguous bytes), the two backward kernels read them instead of re-hashing every mask
+// element (dQ: the forward's lane layout; dK/dV: the query tile's words staged in LDS,
+// one bit per lane's key at position keep_bitpos(key)).
 __device__ __forceinline__ void keep_store(uint32_t* __restrict__ keep, size_t word, uint32_t kbits, int g,
                                            bool valid) {
-  const int sh = 4 * g;
-  uint32_t lo = ((kbits & 0xFu) << sh) | (((kbits >> 4) & 0xFu) << (16 + sh));
-  uint32_t hi = (((kbits >> 8) & 0xFu) << sh) | (((kbits >> 12) & 0xFu) << (16 + sh));
-  lo = or_xor32(or_xor16(lo));
-  hi = or_xor32(or_xor16(hi));
-  if (valid && g == 0) *reinterpret_cast<u32x2*>(keep + 2 * word) = u32x2{lo, hi};
+  if (valid) reinterpret_cast<uint16_t*>(keep)[word * 4 + g] = (uint16_t)kbits;
 }
 // the 4 flags of keys 16t + 4g + r (r = 0..3) of a query from its tile word
 __device__ __forceinline__ void keep_nibble(const u32x2& w, int t, int g, bool (&kp)[4]) {
-  const uint32_t h = (t < 2 ? w[0] : w[1]) >> (16 * (t & 1) + 4 * g);
+  const uint32_t h = (g < 2 ? w[0] : w[1]) >> (16 * (g & 1) + 4 * t);
 #pragma unroll
   for (int r = 0; r < 4; ++r) kp[r] = (h >> r) & 1u;
 }
+// bit position of key k (0..63 within its tile) in the tile word
+__device__ __forceinline__ int keep_bitpos(int k) { return 16 * ((k >> 2) & 3) + 4 * (k >> 4) + (k & 3); }
 
 template <int HD, bool DROP>
 __global__ __launch_bounds__(256) void attn_fwd_flash2_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
@@ -869,12 +858,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
         // keep flags of (query 16t+4g+r, this lane's key u)
         bool kp[4] = {true, true, true, true};
         if (kbits) {
-          // this lane's key within the workgroup's 64 U: word (tile kl >> 6, half
-          // (kl >> 5) & 1), bit kl & 31 -- wave-uniform tile and half
+          // this lane's key within the workgroup's 64 U: word of tile kl >> 6, bit
+          // keep_bitpos (half pos >> 5 of the staged 64-bit word)
           const int kl = wave * (16 * U) + 16 * u + li;
-          const u32x4 w = *reinterpret_cast<const u32x4*>(&s_keep[buf][kl >> 6][(kl >> 5) & 1][16 * t + 4 * g]);
+          const int pos = keep_bitpos(kl & 63);
+          const u32x4 w = *reinterpret_cast<const u32x4*>(&s_keep[buf][kl >> 6][pos >> 5][16 * t + 4 * g]);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) kp[r] = (w[r] >> (kl & 31)) & 1u;
+          for (int r = 0; r < 4; ++r) kp[r] = (w[r] >> (pos & 31)) & 1u;
         } else if (thr) {
           // a mask pair is two adjacent keys of one row, held by lanes li and li^1 --
           // each of the two hashes the pair of 2 of the 4 rows and they swap the results

@@ -30,13 +30,12 @@ import torch
 from .. import ops
 
 SITE_EMBED = 1
-# K split of the QKV input-gradient GEMM (reduction dim 3D): the partial products
-# go to separate buffers that the LayerNorm backward sums on load
-QKV_DGRAD_SPLITS = 2
-# ... only below this many token rows: at vit_small_200's 20,032 the unsplit 8-wave
-# GEMM already has ~1 tile per CU and the split's extra partial costs more
-# (tools/ab_module_constant.py: 6.578 / 6.610 vs 6.523 / 6.541 ms/step)
-QKV_SPLIT_MAX_M = 16384
+# K split of the QKV input-gradient GEMM (reduction dim 3D; the partial products go to
+# separate buffers that the LayerNorm backward sums on load).  Unsplit measured best at
+# every model size this round (tools/ab_module_constant.py, two interleaved reps each:
+# ViT-tiny 0.7349 / 0.7348 ms/step unsplit vs 0.7386 / 0.7358 with 2 and 0.7475 / 0.7357
+# with 3; vit_small_200 6.523 / 6.541 vs 6.578 / 6.610 with 2)
+QKV_DGRAD_SPLITS = 1
 # the input-gradient GEMMs feeding a LayerNorm backward (head, fc1, QKV) write
 # bf16 (the K-split partials too) instead of fp32: half the bytes on both sides
 # of the dgrad -> LayerNorm-backward hand-off; the LayerNorm backward sums and
@@ -495,7 +494,7 @@ class ViTProgram:
             do = ops.linear_dgrad(gy1, bp.proj_w, False)
             dqkv = ops.attn_bwd(do, qkv, o, lse, c.scale, rng, sa, ad,
                                 keep=S.keeps[i] if len(S.keeps) == L else None)
-            qs = QKV_DGRAD_SPLITS if 3 * D >= 768 and M < QKV_SPLIT_MAX_M else 1
+            qs = QKV_DGRAD_SPLITS if 3 * D >= 768 else 1
             dl1 = ops.linear_dgrad(dqkv, bp.qkv_w, f32, qs)
             l1 = ln_out(l1)
             fk = dict(beta=bp.n1b, y_out=l1) if fold else {}
