@@ -111,7 +111,7 @@ def _patch_gemm(model, x):
     weight (one GEMM, same values as ``nn.Conv2d`` up to summation order).  The training
     comparator uses it (``VendorTrainStep(patch="gemm")``): with the MIOpen convolution
     the graph-replayed oxford_flower (p=4) step turned its parameters NaN in some runs and
-    not others (tools/vendor_flower_check.py: conv 81 non-finite tensors after 220
+    not others (tools/vendor_debug.py patch: conv 81 non-finite tensors after 220
     replays in one run, finite in the next; the GEMM form finite and bit-identical with
     and without host syncs between replays)."""
     pe = model.patch_embed
