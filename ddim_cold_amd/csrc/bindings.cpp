@@ -651,8 +651,8 @@ void linear_wgrad_multi(std::vector<Tensor> dys, std::vector<Tensor> xs, std::ve
   }
   const size_t total = dys.size();
   int used = 0;  // partial slots written by earlier launches
-  for (size_t a = 0; a < total; a += 32) {
-    const size_t e = std::min(total, a + 32);
+  for (size_t a = 0; a < total; a += WGRAD_MULTI_MAX) {
+    const size_t e = std::min(total, a + (size_t)WGRAD_MULTI_MAX);
     std::vector<Tensor> d(dys.begin() + a, dys.begin() + e), x(xs.begin() + a, xs.begin() + e),
         w(dws.begin() + a, dws.begin() + e);
     std::vector<c10::optional<Tensor>> b(dbs.begin() + a, dbs.begin() + e);

@@ -190,7 +190,8 @@ __global__ __launch_bounds__(256) void patchify_cls_kernel(const float* __restri
   // patch rows: one thread per segment (row, c, i) = the P contiguous row elements
   // k = c*P*P + i*P + j (one image row of one patch channel): the index split, the
   // per-sample draw and the pixelation scales are paid once per segment, the P bf16
-  // values leave as one vector store
+  // values leave as one vector store.  Image order instead (wp fastest: coalesced image
+  // reads / target writes, patch stores F apart) took the vit_small_200 batch 21.2 -> 47.5 us
   switch (P) {
     case 8: patch_segments<8>(img, patches, B, C, H, W, NP, Wp, csalt, nsalt, patch_blocks, cs); break;
     case 4: patch_segments<4>(img, patches, B, C, H, W, NP, Wp, csalt, nsalt, patch_blocks, cs); break;

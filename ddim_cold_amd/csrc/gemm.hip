@@ -580,8 +580,12 @@ DC_INST_DMA(64, true, true, EPI_ATOMIC)
 // operand tiles.  Problems are compact descriptors (the kernel-argument block
 // must stay under 4 KiB); one token split, so the epilogue is a plain
 // read-add-write (EPI_ACC: deterministic, no fp32 atomics).
-constexpr int WM_MAX = 32;
+constexpr int WM_MAX = WGRAD_MULTI_MAX;
 constexpr int BIG_WG_K = 16384;  // tokens: 128 x 128 weight-gradient tiles from here
+// their LDS ring: 4 x 32 KiB, one workgroup per CU.  A 2-stage ring (two workgroups per CU,
+// to soften the last-wave tail of ~5.1 tile rounds) took the vit_small_200 weight
+// gradients 638 -> 1,183 us (and 48 problems per launch did not merge its two launches)
+constexpr int BIG_WG_STAGES = 4;
 struct WgDesc {
   const bf16* A;
   const bf16* B;
@@ -650,7 +654,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_wgrad_multi_kernel(WgradMul
   gemm_dma_body<T, TN, WM, WN, true, true, EPI_ACC, S>(p, tm, local - tm * tiles_n, 0);
 }
 template __global__ void gemm_wgrad_multi_kernel<64, 3>(WgradMulti);
-template __global__ void gemm_wgrad_multi_kernel<128, 4, 128, 4, 2>(WgradMulti);
+template __global__ void gemm_wgrad_multi_kernel<128, BIG_WG_STAGES, 128, 4, 2>(WgradMulti);
 
 }  // namespace dc
 
@@ -772,7 +776,7 @@ void gemm_wgrad(const GemmArgs& a, int splits, hipStream_t stream) {
 }
 
 int gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool store, const WgradSq* sq) {
-  if (n < 1 || n > WM_MAX) throw std::runtime_error("gemm_wgrad_multi: 1..32 problems per launch");
+  if (n < 1 || n > WM_MAX) throw std::runtime_error("gemm_wgrad_multi: 1..WGRAD_MULTI_MAX problems per launch");
   WgradMulti gm{};
   gm.n = n;
   gm.store = store ? 1 : 0;
@@ -807,8 +811,8 @@ int gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool stor
   }
   static_assert(sizeof(WgradMulti) <= 4000, "kernel argument block");
   if (T == 128) {
-    constexpr int lds = 4 * 2 * 128 * 128;  // 4 stages x (A + B) 128-wide, 64-deep images
-    hipLaunchKernelGGL((gemm_wgrad_multi_kernel<128, 4, 128, 4, 2>), dim3(tiles + extra), dim3(512), lds, stream, gm);
+    constexpr int lds = BIG_WG_STAGES * 2 * 128 * 128;  // stages x (A + B) 128-wide, 64-deep images
+    hipLaunchKernelGGL((gemm_wgrad_multi_kernel<128, BIG_WG_STAGES, 128, 4, 2>), dim3(tiles + extra), dim3(512), lds, stream, gm);
   } else {
     hipLaunchKernelGGL((gemm_wgrad_multi_kernel<64, 3>), dim3(tiles + extra), dim3(256), 3 * (64 * 128 + 64 * 128),
                        stream, gm);

@@ -90,6 +90,7 @@ void gemm_wgrad(const GemmArgs& a, int splits, hipStream_t stream);
 // final before this launch) into parts[tiles + j], and zero parts[tiles + tail ..
 // nparts).  The optimizer then reads the same partial layout sqnorm writes.
 constexpr int WSQ_MAX_RANGES = 16;
+constexpr int WGRAD_MULTI_MAX = 32;  // problems per gemm_wgrad_multi launch (kernel-argument block)
 struct WgradSq {
   float* parts = nullptr;
   int nparts = 0;
