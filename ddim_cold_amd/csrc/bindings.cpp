@@ -693,7 +693,9 @@ std::tuple<Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tenso
                                          bool emit_gy, c10::optional<Tensor> ws, c10::optional<Tensor> beta, c10::optional<Tensor> y_out) {
   CHECK_CUDA(dy); CHECK_CONTIG(dy);
   TORCH_CHECK(dy.scalar_type() == F32 || dy.scalar_type() == BF16, "dy must be fp32 or bf16");
-  CHECK_IN(x, F32); CHECK_IN(mean, F32); CHECK_IN(rstd, F32); CHECK_IN(gamma, F32);
+  CHECK_CUDA(x); CHECK_CONTIG(x);
+  TORCH_CHECK(x.scalar_type() == F32 || x.scalar_type() == BF16, "layernorm_bwd: x must be fp32 or bf16");
+  CHECK_IN(mean, F32); CHECK_IN(rstd, F32); CHECK_IN(gamma, F32);
   CHECK_IN(dgamma, F32); CHECK_IN(dbeta, F32); check_rng(rng);
   const c10::DeviceGuard guard(x.device());
   const int D = x.size(-1), M = x.numel() / D;
@@ -710,7 +712,8 @@ std::tuple<Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tenso
   }
   const int R = ln_replicas();
   const bool own_ws = !(ws.has_value() && ws->defined());
-  Tensor w = own_ws ? at::zeros({R, 2 * D}, x.options()) : *ws;
+  const auto f32o = x.options().dtype(F32);
+  Tensor w = own_ws ? at::zeros({R, 2 * D}, f32o) : *ws;
   if (!own_ws) {
     CHECK_IN(w, F32);
     TORCH_CHECK(w.numel() == (int64_t)R * 2 * D, "ln ws must hold ln_replicas x 2D floats");
@@ -726,9 +729,9 @@ std::tuple<Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tenso
     bp = beta->data_ptr<float>();
     yp = y_out->data_ptr();
   }
-  auto g_out = at::empty(x.sizes(), x.options());
+  auto g_out = at::empty(x.sizes(), f32o);
   Tensor gy = emit_gy ? at::empty({M, D}, x.options().dtype(BF16)) : at::empty({0}, x.options().dtype(BF16));
-  layernorm_bwd_launch(dy.data_ptr(), dy.scalar_type() == BF16, x.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+  layernorm_bwd_launch(dy.data_ptr(), dy.scalar_type() == BF16, x.data_ptr(), x.scalar_type() == BF16, mean.data_ptr<float>(), rstd.data_ptr<float>(),
                        gamma.data_ptr<float>(), bp, gr, g_out.data_ptr<float>(), emit_gy ? gy.data_ptr() : nullptr,
                        yp, w.data_ptr<float>(), M, D, N, rng.data_ptr<int64_t>(), site_drop, p_drop, site_dp, p_dp,
                        parts, cur_stream());

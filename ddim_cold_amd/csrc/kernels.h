@@ -108,7 +108,7 @@ void layernorm_fwd_launch(const float* x, const float* gamma, const float* beta,
                           float* rstd, int M, int D, float eps, hipStream_t stream);
 // dgamma||dbeta partials go into ws [ln_replicas()][2D] (must be zero on entry);
 // replica_reduce_launch adds them into the destinations and re-zeroes ws.
-void layernorm_bwd_launch(const void* dy, bool dy_bf16, const float* x, const float* mean, const float* rstd,
+void layernorm_bwd_launch(const void* dy, bool dy_bf16, const void* x, bool x_bf16, const float* mean, const float* rstd,
                           const float* gamma, const float* beta, const float* g_res, float* g_out, void* gy_bf16,
                           void* y_bf16, float* dgb_ws, int M,
                           int D, int tokens, const int64_t* rng, int site_drop, double p_drop, int site_dp,

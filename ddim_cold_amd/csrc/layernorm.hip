@@ -66,9 +66,11 @@ __global__ __launch_bounds__(NW * 64) void ln_fwd_kernel(const float* __restrict
   }
 }
 
-// DYB: dy (and its K-split partials) in bf16 -- the dgrad GEMMs write half the bytes
-template <int VEC, int RPW, int NW, bool DYB>
-__global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict__ dyv, const float* __restrict__ x,
+// DYB: dy (and its K-split partials) in bf16 -- the dgrad GEMMs write half the bytes.
+// XB: x is the bf16 copy of the LayerNorm input, the operand the folded forward GEMM
+// actually normalised (x_hat from it is the forward's own), 2 bytes per element less
+template <int VEC, int RPW, int NW, bool DYB, bool XB>
+__global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict__ dyv, const void* __restrict__ x,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
                                                      const float* __restrict__ g_res,
@@ -105,7 +107,8 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict_
   for (int j = 0; j < RPW; ++j) {
     rows[j] = (blockIdx.x * NW + wave) * RPW + j;
     const int row = rows[j] < M ? rows[j] : M - 1;
-    const float2* xr = reinterpret_cast<const float2*>(x + (size_t)row * D);
+    const float2* xr = reinterpret_cast<const float2*>(reinterpret_cast<const float*>(x) + (size_t)row * D);
+    const bf16x2* xr16 = reinterpret_cast<const bf16x2*>(reinterpret_cast<const bf16*>(x) + (size_t)row * D);
     const float2* gr = reinterpret_cast<const float2*>(g_res + (size_t)row * D);
     auto ldy = [&](int pt, int i) -> float2 {
       const size_t off = (size_t)pt * M * D + (size_t)row * D;
@@ -117,7 +120,12 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict_
     };
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
-      xv[j][i] = xr[lane + 64 * i];
+      if (XB) {
+        const bf16x2 e = xr16[lane + 64 * i];
+        xv[j][i] = make_float2(bf2f(e[0]), bf2f(e[1]));
+      } else {
+        xv[j][i] = xr[lane + 64 * i];
+      }
       dv[j][i] = ldy(0, i);
       rv[j][i] = g_res ? gr[lane + 64 * i] : make_float2(0.f, 0.f);
     }
@@ -411,7 +419,7 @@ void layernorm_fwd_launch(const float* x, const float* gamma, const float* beta,
                                     gamma, beta, reinterpret_cast<bf16*>(y_bf16), mean, rstd, M, eps))
 }
 
-void layernorm_bwd_launch(const void* dy, bool dy_bf16, const float* x, const float* mean, const float* rstd,
+void layernorm_bwd_launch(const void* dy, bool dy_bf16, const void* x, bool x_bf16, const float* mean, const float* rstd,
                           const float* gamma, const float* beta, const float* g_res, float* g_out, void* gy_bf16,
                           void* y_bf16, float* dgb_ws, int M,
                           int D, int tokens, const int64_t* rng, int site_drop, double p_drop, int site_dp,
@@ -420,18 +428,20 @@ void layernorm_bwd_launch(const void* dy, bool dy_bf16, const float* x, const fl
   const uint32_t td = drop_threshold_host(p_drop), tp = drop_threshold_host(p_dp);
   const float sd = p_drop > 0 ? 1.f / (1.f - (float)p_drop) : 1.f;
   const float sp = p_dp > 0 ? 1.f / (1.f - (float)p_dp) : 1.f;
-#define LN_BWD_GO1(R, W, DYB)                                                                                 \
+#define LN_BWD_GO1(R, W, DYB, XB)                                                                             \
   LN_DISPATCH(D, if (W * 2 * D * sizeof(float) > 65536)                                                         \
-                  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&ln_bwd_kernel<VEC, R, W, DYB>),           \
+                  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&ln_bwd_kernel<VEC, R, W, DYB, XB>),           \
                                             hipFuncAttributeMaxDynamicSharedMemorySize, W * 2 * D * sizeof(float));  \
-                hipLaunchKernelGGL((ln_bwd_kernel<VEC, R, W, DYB>), dim3((M + R * W - 1) / (R * W)), dim3(W * 64), \
+                hipLaunchKernelGGL((ln_bwd_kernel<VEC, R, W, DYB, XB>), dim3((M + R * W - 1) / (R * W)), dim3(W * 64), \
                                     W * 2 * D * sizeof(float), stream, dy, x, mean, rstd, gamma, beta, g_res, g_out, \
                                     reinterpret_cast<bf16*>(gy_bf16), reinterpret_cast<bf16*>(y_bf16), dgb_ws,  \
                                     M, tokens, rng, site_drop, td,                                              \
                                     sd, site_dp, tp, sp, dy_parts))
-#define LN_BWD_GO(R, W)           \
-  if (dy_bf16) LN_BWD_GO1(R, W, true) \
-  else LN_BWD_GO1(R, W, false)
+#define LN_BWD_GO(R, W)                      \
+  if (dy_bf16 && x_bf16) LN_BWD_GO1(R, W, true, true)  \
+  else if (dy_bf16) LN_BWD_GO1(R, W, true, false)      \
+  else if (x_bf16) LN_BWD_GO1(R, W, false, true)       \
+  else LN_BWD_GO1(R, W, false, false)
   // measured on the ViT-tiny shape (M 2080, D 384, dropout on): 1 row x 8 waves
   // 5.0 us, 2 x 4 5.9, 1 x 4 5.2, 1 x 16 5.1, 2 x 16 7.2
   LN_BWD_GO(1, 8)

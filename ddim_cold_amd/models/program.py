@@ -41,6 +41,10 @@ QKV_DGRAD_SPLITS = 1
 # of the dgrad -> LayerNorm-backward hand-off; the LayerNorm backward sums and
 # computes in fp32 (the reference's fp16 autocast hands it fp16 gradients)
 DGRAD_BF16 = True
+# LayerNorm backward of a folded LayerNorm reads the bf16 copy of its input -- the
+# operand the folded GEMM normalised in the forward -- instead of the fp32 residual
+# stream: 2 of its 18 bytes per element, and the fp32 block inputs are not saved
+LN_BWD_XB = True
 # LayerNorm fold (csrc/gemm.hip): every LayerNorm is folded into the GEMM that
 # consumes it (QKV, fc1, head) -- no LayerNorm launch in the forward.  The
 # producing GEMM's epilogue accumulates the row statistics; the LayerNorm
@@ -370,7 +374,7 @@ class ViTProgram:
                     torch.empty(M, dtype=torch.float32, device=dev)) if save else (None, None)
         for i, bp in enumerate(P.blocks):
             sa, sp, sd1, sf1, sf2, sd2 = block_sites(i)
-            x0 = x
+            x0, x0b = x, xb
             m1, r1 = stats()
             fold = (st[2 * i], bp.qkv_c, c.eps, m1, r1)
             qkv = ops.qkv_fwd(xb, bp.qkv_wf, bp.qkv_bf, B, N, c.heads, fold=fold)
@@ -389,7 +393,9 @@ class ViTProgram:
             x = ops.linear_residual_fwd(h, bp.fc2_w, bp.fc2_b, x1, N, rng, sf2, pd, sd2, dpr[i],
                                         st_out=st[2 * i + 2], xb_out=xb)
             if save:
-                S.blocks.append((x0, None, m1, r1, qkv, o, lse, x1, None, m2, r2, u, h))
+                # the LayerNorm backwards read the bf16 copies the folded GEMMs normalised
+                xs0, xs1 = (x0b, x1b) if LN_BWD_XB else (x0, x1)
+                S.blocks.append((xs0, None, m1, r1, qkv, o, lse, xs1, None, m2, r2, u, h))
         if head_step is not None:
             mode, x0_out, coef = head_step[:3]
             patches_out = head_step[4] if len(head_step) > 4 else None
@@ -411,7 +417,7 @@ class ViTProgram:
             out = ops.head_fwd(xb, P.head_wf, P.head_bf, B, c.chans, c.img_h, c.img_w, c.patch,
                                fold=(st[2 * L], P.head_c, c.eps, mf, rf))
         if save:
-            S.xL, S.lf, S.mf, S.rf = x, None, mf, rf
+            S.xL, S.lf, S.mf, S.rf = xb if LN_BWD_XB else x, None, mf, rf
         return out, S
 
     def supports_fused_loss(self, P: ModelTensors) -> bool:
