@@ -265,13 +265,29 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const float* __restrict_
     }
     rf.dsts[gi][c] = rf.store ? s : rf.dsts[gi][c] + s;
   } else {
-    const size_t total = (size_t)B * (N - 1) * D;
-    for (size_t e = (size_t)(bid - blocksA - blocksB) * 256 + threadIdx.x; e < total;
-         e += (size_t)blocksC * 256) {
-      const size_t row = e / D;
-      const int d = (int)(e - row * D);
-      const int b = (int)(row / (N - 1)), i = (int)(row % (N - 1));
-      gpatch[e] = f2bf(gm(((size_t)b * N + 1 + i) * D + d));
+    // part C: 4 consecutive columns per thread (one 16-B load, two pair hashes, one 8-B
+    // store) with 32-bit index math (the launcher checks the size); one element per
+    // thread with 64-bit divisions was ~1/3 of this launch at vit_small_200
+    const int D4 = D >> 2, NP = N - 1, total4 = B * NP * D4;
+    for (int e = (bid - blocksA - blocksB) * 256 + threadIdx.x; e < total4; e += blocksC * 256) {
+      const int row = e / D4, d = (e - row * D4) * 4;
+      const int b = row / NP, i = row - b * NP;
+      const int src = (b * N + 1 + i) * D + d;
+      float4 v = *reinterpret_cast<const float4*>(g + src);
+      if (thr) {
+        bool k[4];
+        dropout_keep4(salt, (uint32_t)src, thr, k);
+        v.x = k[0] ? v.x * dsc : 0.f;
+        v.y = k[1] ? v.y * dsc : 0.f;
+        v.z = k[2] ? v.z * dsc : 0.f;
+        v.w = k[3] ? v.w * dsc : 0.f;
+      }
+      bf16x4 o;
+      o[0] = f2bf(v.x);
+      o[1] = f2bf(v.y);
+      o[2] = f2bf(v.z);
+      o[3] = f2bf(v.w);
+      *reinterpret_cast<bf16x4*>(gpatch + (size_t)e * 4) = o;
     }
   }
 }
@@ -370,7 +386,9 @@ void patchify_cls_launch(const float* img, const int64_t* t, const float* cls, c
 void embed_bwd_launch(const float* g, const int64_t* t, float* dcls, float* dpos, float* dtemb, void* gpatch, int B,
                       int N, int D, const int64_t* rng, int site, double p, hipStream_t stream, ReplicaFinal rf) {
   const int blocksA = cdiv(N * D, 256), blocksB = cdiv(B * D, 256) * cdiv(N, EMB_TCHUNK);
-  const int blocksC = grid_for((size_t)B * (N - 1) * D);
+  if (D % 4 != 0) throw std::invalid_argument("embed_bwd: D must be a multiple of 4");
+  if ((size_t)B * N * D >= (size_t)INT32_MAX) throw std::invalid_argument("embed_bwd: too many elements for 32-bit indexing");
+  const int blocksC = grid_for((size_t)B * (N - 1) * D / 4);
   const int blocksD = rf.ws ? rf.G * cdiv(rf.C, 256) : 0;
   const uint32_t thr = drop_threshold_host(p);
   const float dsc = p > 0 ? 1.f / (1.f - (float)p) : 1.f;
