@@ -221,7 +221,7 @@ struct KvStage {  // one 64-row K tile + one 64-row V tile, register-staged
 template <int DT, bool DROP, bool MASK>
 __device__ __forceinline__ void flash_softmax_tile(f32x4 (&st)[4], f32x4 (&o)[DT], float& m_run, float& l_run,
                                                    int kv0, int N, int g, float sl2, uint32_t salt,
-                                                   uint32_t rowidx, uint32_t thr, float dsc, uint32_t& kbits) {
+                                                   uint32_t rowidx, uint32_t thr, uint32_t& kbits) {
   float mt = -INFINITY;
 #pragma unroll
   for (int t = 0; t < 4; ++t)
@@ -252,7 +252,7 @@ __device__ __forceinline__ void flash_softmax_tile(f32x4 (&st)[4], f32x4 (&o)[DT
     for (int r = 0; r < 4; ++r) {
       float pv = fexp2(fmaf(st[t][r], sl2, nm));
       ls += pv;
-      if (DROP) pv = kp[r] ? pv * dsc : 0.f;
+      if (DROP) pv = kp[r] ? pv : 0.f;  // the keep scale 1/(1-p) goes into the final 1/l
       if (DROP) kbits |= (uint32_t)kp[r] << (4 * t + r);
       st[t][r] = pv;
     }
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(256) void attn_fwd_flash2_kernel(const bf16* __rest
     for (int u = 0; u < 2; ++u) {
       uint32_t kbits = 0u;
       flash_softmax_tile<C::DT, DROP, MASK>(st[u], o[u], m_run[u], l_run[u], kv0, N, g, sl2, salt,
-                                            rowidx0 + u * rowstep + kv0, thr, dsc, kbits);
+                                            rowidx0 + u * rowstep + kv0, thr, kbits);
       if (DROP && keep != nullptr) {
         const int q = qbase + 16 * u + li;
         keep_store(keep, ((size_t)bh * ntiles + it) * N + q, kbits, g, q < N);
@@ -373,7 +373,7 @@ __global__ __launch_bounds__(256) void attn_fwd_flash2_kernel(const bf16* __rest
   for (int u = 0; u < 2; ++u) {
     const int q = qbase + 16 * u + li;
     if (q < N) {
-      const float inv = 1.f / l_run[u];
+      const float inv = (DROP ? dsc : 1.f) / l_run[u];  // dropout keep scale folded in
       bf16* orow = out + ((size_t)b * N + q) * D + h * HD;
 #pragma unroll
       for (int d = 0; d < C::DT; ++d) {
@@ -486,7 +486,7 @@ __global__ __launch_bounds__(640) void attn_fwd_resident_kernel(const bf16* __re
     for (int u = 0; u < 2; ++u) {
       uint32_t kbits = 0u;
       flash_softmax_tile<C::DT, DROP, MASK>(st[u], o[u], m_run[u], l_run[u], kv0, N, g, sl2, salt,
-                                            rowidx0 + u * rowstep + kv0, thr, dsc, kbits);
+                                            rowidx0 + u * rowstep + kv0, thr, kbits);
       if (DROP && keep != nullptr) {
         const int q = qbase + 16 * u + li;
         keep_store(keep, ((size_t)bh * ntiles + kv0 / 64) * N + q, kbits, g, q < N);
@@ -512,7 +512,7 @@ __global__ __launch_bounds__(640) void attn_fwd_resident_kernel(const bf16* __re
   for (int u = 0; u < 2; ++u) {
     const int q = qbase + 16 * u + li;
     if (q < N) {
-      const float inv = 1.f / l_run[u];
+      const float inv = (DROP ? dsc : 1.f) / l_run[u];  // dropout keep scale folded in
       bf16* orow = out + ((size_t)b * N + q) * D + h * HD;
 #pragma unroll
       for (int d = 0; d < C::DT; ++d) {
@@ -1092,7 +1092,7 @@ __global__ __launch_bounds__(NP * 4) void attn_fwd_short_kernel(const bf16* __re
       float pv = fexp2(fmaf(st[t][r], sl2, nmx));
       l += pv;
       if (DROP) {
-        pv = kp[r] ? pv * dsc : 0.f;
+        pv = kp[r] ? pv : 0.f;  // keep scale folded into the final 1/l
         kbits |= (kp[r] ? 1u : 0u) << (4 * t + r);
       }
       st[t][r] = pv;
@@ -1113,7 +1113,7 @@ __global__ __launch_bounds__(NP * 4) void attn_fwd_short_kernel(const bf16* __re
     for (int d = 0; d < DT; ++d) o[d] = mfma16(frag_t<RS>(Vl, 16 * d, s2, lane), pb, o[d]);
   }
   if (q < N) {
-    const float inv = 1.f / l;
+    const float inv = (DROP ? dsc : 1.f) / l;
     bf16* orow = out + ((size_t)b * N + q) * (H * HD) + h * HD;
 #pragma unroll
     for (int d = 0; d < DT; ++d) *reinterpret_cast<bf16x4*>(orow + 16 * d + 4 * g) = pack4(o[d] * inv);
