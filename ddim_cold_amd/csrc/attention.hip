@@ -682,6 +682,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
             float pr = fexp2(fmaf(st[u][r], sl2, nl2[u]));
             if (MASK && key >= N) pr = 0.f;
             float dpv = dp[u][r];
+            // (factoring dsc out of dS -- delta / dsc here, dsc in the final dQ / dK / dV
+            // scales -- measured no faster: N=626 p=0.1 stored masks 145.5 vs 146.4 us)
             if (thr) dpv = kp[r] ? dpv * dsc : 0.f;
             ds[u][th][r] = pr * (dpv - dl[u]);
           }
