@@ -116,7 +116,7 @@ void layernorm_bwd_launch(const void* dy, bool dy_bf16, const void* x, bool x_bf
 int ln_replicas();
 
 // LayerNorm fold weights for the GEMMs that consume a LayerNorm (layernorm.hip)
-constexpr int FOLD_MAX = 16;
+constexpr int FOLD_MAX = 32;  // GEMMs per fold launch (vit_small_200: 25 in one launch)
 struct FoldJob {
   const void* w;       // [rows][K] weight: fp32 master, or its bf16 shadow (FoldTable::w_bf16)
   const float* gamma;  // [K]

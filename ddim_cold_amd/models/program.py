@@ -45,6 +45,8 @@ DGRAD_BF16 = True
 # operand the folded GEMM normalised in the forward -- instead of the fp32 residual
 # stream: 2 of its 18 bytes per element, and the fp32 block inputs are not saved
 LN_BWD_XB = True
+# GEMMs per LayerNorm-fold launch (csrc/kernels.h FOLD_MAX)
+FOLD_MAX = 32
 # LayerNorm fold (csrc/gemm.hip): every LayerNorm is folded into the GEMM that
 # consumes it (QKV, fc1, head) -- no LayerNorm launch in the forward.  The
 # producing GEMM's epilogue accumulates the row statistics; the LayerNorm
@@ -197,10 +199,10 @@ class LnFold:
     def refresh(self, tail=None):
         """Recompute the folded weights; ``tail`` (see :func:`ops.ln_fold_`) rides
         along in the last launch."""
-        for a in range(0, len(self.keys), 16):
-            ks = self.keys[a:a + 16]
-            src = self.src[a:a + 16]
-            last = a + 16 >= len(self.keys)
+        for a in range(0, len(self.keys), FOLD_MAX):
+            ks = self.keys[a:a + FOLD_MAX]
+            src = self.src[a:a + FOLD_MAX]
+            last = a + FOLD_MAX >= len(self.keys)
             ops.ln_fold_([w.reshape(w.shape[0], -1) for w, _, _, _ in src], [g for _, g, _, _ in src],
                          [b for _, _, b, _ in src], [bias for _, _, _, bias in src],
                          [self.out[k][0] for k in ks], [self.out[k][1] for k in ks], [self.out[k][2] for k in ks],

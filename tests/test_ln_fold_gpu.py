@@ -57,11 +57,13 @@ def test_ln_fold_kernel(rows, K):
     close(outs[2], exp[2], 1e-3, 1e-5, "bf")
 
 
-def test_ln_fold_kernel_many():
-    """16 GEMMs of different row counts in one launch (the model's table)."""
+@pytest.mark.parametrize("n", [16, 25])
+def test_ln_fold_kernel_many(n):
+    """n GEMMs of different row counts in one launch (the model's table: 15 for ViT-tiny,
+    25 for vit_small_200)."""
     K = 128
     jobs = [(torch.randn(r, K, device=DEV), torch.randn(K, device=DEV), torch.randn(K, device=DEV),
-             torch.randn(r, device=DEV) if i % 3 else None) for i, r in enumerate([384, 128, 40, 8] * 4)]
+             torch.randn(r, device=DEV) if i % 3 else None) for i, r in enumerate(([384, 128, 40, 8] * 7)[:n])]
     outs = [(torch.empty(w.shape[0], K, dtype=torch.bfloat16, device=DEV), torch.empty(w.shape[0], device=DEV),
              torch.empty(w.shape[0], device=DEV)) for w, _, _, _ in jobs]
     ops.ln_fold_(*[list(z) for z in zip(*jobs)], *[list(z) for z in zip(*outs)])
