@@ -176,31 +176,34 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
 // global loads are issued before the current tile's MFMAs and land in
 // registers, then go to the other LDS buffer — one barrier per tile and no
 // exposed load latency.  Dropout is a template flag (branch-free softmax).
+// The padded-row zeroing happens in store(), not load(): a select on the loaded
+// registers right after the loads made the compiler wait for them there (s_waitcnt
+// vmcnt(0) before the tile's MFMAs), i.e. the "prefetch" was a blocking load.
 template <int HD>
 struct KvStage {  // one 64-row K tile + one 64-row V tile, register-staged
   static constexpr int CPR = HD / 8;
   static constexpr int PER = 64 * CPR / 256;  // 16-B chunks per thread per matrix
   u32x4 k[PER], v[PER];
+  bool ok[PER];
   __device__ __forceinline__ void load(const bf16* __restrict__ kb, const bf16* __restrict__ vb, int r0, int N) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = threadIdx.x + i * 256;
       const int r = c / CPR, cc = c - r * CPR;
       const int rr = r0 + r < N ? r0 + r : N - 1;
-      const u32x4 z = {0u, 0u, 0u, 0u};
-      const u32x4 kv = *reinterpret_cast<const u32x4*>(kb + (size_t)rr * HD + cc * 8);
-      const u32x4 vv = *reinterpret_cast<const u32x4*>(vb + (size_t)rr * HD + cc * 8);
-      k[i] = r0 + r < N ? kv : z;
-      v[i] = r0 + r < N ? vv : z;
+      ok[i] = r0 + r < N;
+      k[i] = *reinterpret_cast<const u32x4*>(kb + (size_t)rr * HD + cc * 8);
+      v[i] = *reinterpret_cast<const u32x4*>(vb + (size_t)rr * HD + cc * 8);
     }
   }
   __device__ __forceinline__ void store(char* kl, char* vl) const {
+    const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = threadIdx.x + i * 256;
       const int r = c / CPR, cc = c - r * CPR;
-      *reinterpret_cast<u32x4*>(kl + r * AC<HD>::S + cc * 16) = k[i];
-      *reinterpret_cast<u32x4*>(vl + r * AC<HD>::S + cc * 16) = v[i];
+      *reinterpret_cast<u32x4*>(kl + r * AC<HD>::S + cc * 16) = ok[i] ? k[i] : z;
+      *reinterpret_cast<u32x4*>(vl + r * AC<HD>::S + cc * 16) = ok[i] ? v[i] : z;
     }
   }
 };
@@ -631,6 +634,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
 #pragma unroll
     for (int d = 0; d < C::DT; ++d) dq[u][d] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  u32x2 kwc[U];  // keep words of the tile about to run (prefetched with its K / V)
+#pragma unroll
+  for (int u = 0; u < U; ++u) kwc[u] = kbits ? kcol[u][0] : u32x2{0u, 0u};
   stg.store(lds, lds + C::TILE);
   __syncthreads();
   // key mask only in the tail tile: a padded key has a zero K row (no dQ
@@ -639,10 +645,18 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
     constexpr bool MASK = decltype(mask_tag)::value;
     const int kv0 = it * 64;
     const bool more = it + 1 < ntiles;
-    if (more) stg.load(kb, vb, kv0 + 64, N);  // next tile lands during this tile's MFMAs
+    // the next tile's keep words and K / V in one batch, issued on every tile (the last
+    // one reloads itself, unused): behind an `if (more)` the compiler's path-merged count
+    // was vmcnt(0), and a word loaded in the tile that uses it waited right away -- both
+    // exposed the prefetch latency
     u32x2 kw[U];
+    const int itn = more ? it + 1 : it;
 #pragma unroll
-    for (int u = 0; u < U; ++u) kw[u] = kbits ? kcol[u][(size_t)it * N] : u32x2{0u, 0u};
+    for (int u = 0; u < U; ++u) {
+      kw[u] = kwc[u];
+      kwc[u] = kbits ? kcol[u][(size_t)itn * N] : u32x2{0u, 0u};
+    }
+    stg.load(kb, vb, itn * 64, N);  // next tile lands during this tile's MFMAs
     const char* Kl = lds + (it & 1) * 2 * C::TILE;
     const char* Vl = Kl + C::TILE;
     // two halves of 32 keys: dS of a half feeds its dQ MFMAs right away (half the
@@ -771,8 +785,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
   // register-staged prefetch of the next query tile: Q rows (head-major), dO rows
   // (token-major, head slice), LSE, delta and the keep words
   constexpr int PER = 64 * C::CPR / 256;
+  // raw loads here, padded-row selects in store_tile (see KvStage: a select next to the
+  // loads waits for them)
   u32x4 rq[PER], rd[PER];
-  float rl = INFINITY, rdl = 0.f;
+  bool rok[PER];
+  float rl = 0.f, rdl = 0.f;
+  bool rlv = false;
   const bool kbits = thr && keep != nullptr;
   const int ntiles = (N + 63) / 64;
   u32x2 rk = u32x2{0u, 0u};
@@ -783,19 +801,17 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
       const int c = threadIdx.x + i * 256;
       const int r = c / C::CPR, cc = c - r * C::CPR;
       const int rr = q0 + r < N ? q0 + r : N - 1;
-      const u32x4 z = {0u, 0u, 0u, 0u};
-      const u32x4 qv4 = *reinterpret_cast<const u32x4*>(qb + (size_t)rr * HD + cc * 8);
-      const u32x4 dv4 = *reinterpret_cast<const u32x4*>(dout + ((size_t)b * N + rr) * D + h * HD + cc * 8);
-      rq[i] = q0 + r < N ? qv4 : z;
-      rd[i] = q0 + r < N ? dv4 : z;
+      rok[i] = q0 + r < N;
+      rq[i] = *reinterpret_cast<const u32x4*>(qb + (size_t)rr * HD + cc * 8);
+      rd[i] = *reinterpret_cast<const u32x4*>(dout + ((size_t)b * N + rr) * D + h * HD + cc * 8);
     }
     if (threadIdx.x < 64 * U) {
       const int qq = q0 + (threadIdx.x & 63);
       const int qc = qq < N ? qq : N - 1;
       if (threadIdx.x < 64) {
-        const float l = lse[(size_t)bh * N + qc], dd = delta[(size_t)bh * N + qc];
-        rl = qq < N ? l * LOG2E : INFINITY;
-        rdl = qq < N ? dd : 0.f;
+        rl = lse[(size_t)bh * N + qc];
+        rdl = delta[(size_t)bh * N + qc];
+        rlv = qq < N;
       }
       if (kbits && kt_mine < ntiles) rk = reinterpret_cast<const u32x2*>(keep)[((size_t)bh * ntiles + kt_mine) * N + qc];
     }
@@ -807,12 +823,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
     for (int i = 0; i < PER; ++i) {
       const int c = threadIdx.x + i * 256;
       const int r = c / C::CPR, cc = c - r * C::CPR;
-      *reinterpret_cast<u32x4*>(ql + r * C::S + cc * 16) = rq[i];
-      *reinterpret_cast<u32x4*>(dl + r * C::S + cc * 16) = rd[i];
+      const u32x4 z = {0u, 0u, 0u, 0u};
+      *reinterpret_cast<u32x4*>(ql + r * C::S + cc * 16) = rok[i] ? rq[i] : z;
+      *reinterpret_cast<u32x4*>(dl + r * C::S + cc * 16) = rok[i] ? rd[i] : z;
     }
     if (threadIdx.x < 64) {
-      s_lse[buf][threadIdx.x] = rl;
-      s_del[buf][threadIdx.x] = rdl;
+      s_lse[buf][threadIdx.x] = rlv ? rl * LOG2E : INFINITY;
+      s_del[buf][threadIdx.x] = rlv ? rdl : 0.f;
     }
     if (threadIdx.x < 64 * U) {
       s_keep[buf][threadIdx.x >> 6][0][threadIdx.x & 63] = rk[0];
