@@ -72,13 +72,14 @@ __host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
 }
 
 // rng = device pointer to int64[2] = {seed, step}
-__device__ __forceinline__ uint32_t site_salt(const int64_t* rng, int site) {
-  const uint64_t seed = (uint64_t)rng[0];
-  const uint64_t step = (uint64_t)rng[1];
+__device__ __forceinline__ uint32_t site_salt_v(uint64_t seed, uint64_t step, int site) {
   const uint32_t s_lo = (uint32_t)seed, s_hi = (uint32_t)(seed >> 32);
   const uint32_t a = mix32((uint32_t)step * 0x9E3779B9u + s_hi);
   const uint32_t b = mix32(s_lo ^ a);
   return mix32(b + (uint32_t)site * 0x85EBCA6Bu);
+}
+__device__ __forceinline__ uint32_t site_salt(const int64_t* rng, int site) {
+  return site_salt_v((uint64_t)rng[0], (uint64_t)rng[1], site);
 }
 
 // Dropout masks (counter-based, regenerated in backward): element i of a site

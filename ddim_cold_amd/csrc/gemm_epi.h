@@ -572,6 +572,7 @@ struct VecEpi {
                     //   epilogue's arrays in scratch memory)
   f32x4 clsv[FN];   //   cls + pos[0] + temb[t] of that sample's cls row, the lane's columns
   float sqacc;      // ACC with sq_parts: this lane's sum of squares of the stored values
+  int64_t rng0, rng1;  // the step's {seed, step}, loaded by prefetch (dropout salts)
 
   // lane -> (row within the 16-row fragment, first of its 4 columns within the 16-column fragment)
   static __device__ __forceinline__ int rsub(int g, int li) { return SW ? li : 4 * g + (li & 3); }
@@ -600,6 +601,11 @@ struct VecEpi {
 
   __device__ __forceinline__ void prefetch(const GemmParams& p, int mb, int nb, int g, int li) {
     const int q = sharer(g, li), cs = csub(g, li), rs = rsub(g, li);
+    rng0 = rng1 = 0;
+    if (p.thr_drop || p.thr_dp) {
+      rng0 = p.rng[0];
+      rng1 = p.rng[1];
+    }
     const bool fold = FC && p.ln_st != nullptr;
     first_col = nb == 0 && q == 0;
     colbase = nb;
@@ -614,10 +620,12 @@ struct VecEpi {
       else cols[j] = (int)epi_col<EPI>(p, n);
       colb[j] = (has_bias && colok[j]) ? ld4(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    int rowsafe[FM];  // the row offset with m clamped (RESID / DGELU operand loads)
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int m = mb + i * 16 + rs;
       rows[i] = epi_row32<EPI>(p, m < p.M ? m : p.M - 1);
+      rowsafe[i] = rows[i].off;
       if (m >= p.M) rows[i].off = -1;
       rowm[i] = m < p.M ? m : -1;
       const int np_in = p.K / LN_SLOT;
@@ -661,13 +669,19 @@ struct VecEpi {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (PRE && rows[i].off >= 0 && colok[j]) {
+        if (EPI == EPI_RESID || EPI == EPI_DGELU) {
+          // unconditional loads at a clamped row / column (finish skips those lanes): a
+          // load under a condition became a phi copy that waited for it right here --
+          // and, vmcnt being in order, for the operand DMA issued before it
           const int n = nb + j * 16 + cs;
-          if (EPI == EPI_RESID) v = ld4(p.res + rows[i].off + n);
+          const int ns = colok[j] ? n : p.N - 4;
+          if (EPI == EPI_RESID) v = ld4(p.res + rowsafe[i] + ns);
+          else v = ld4bf(p.aux + rowsafe[i] + ns);
+        } else if (PRE && rows[i].off >= 0 && colok[j]) {
+          const int n = nb + j * 16 + cs;
           if (EPI == EPI_HEADR && p.head_mode != 2) v = ld4(p.res + rows[i].off + n);  // x_t
           if (EPI == EPI_HEADL && rows[i].b >= 0)  // target patch row (m - b - 1)
             v = ld4(p.res + (rows[i].off - (rows[i].b + 1) * p.N) + n);
-          if (EPI == EPI_DGELU) v = ld4bf(p.aux + rows[i].off + n);
           if (EPI == EPI_ACC && !p.acc_store) v = ld4(reinterpret_cast<const float*>(p.C) + rows[i].off + n);
           if (EPI == EPI_EMBED) {
             const int m = mb + i * 16 + rs;
@@ -681,6 +695,13 @@ struct VecEpi {
   }
 
   __device__ __forceinline__ void finish(const GemmParams& p, const f32x4 (&acc_in)[FM][FN], int li) {
+    // every prefetched operand (and the rng words) has long landed: one explicit
+    // vmcnt(0) here, BEFORE the first store.  Without it the compiler (operands loaded
+    // under conditions, stores under conditions: a path-merged count) waited vmcnt(0)
+    // at each fragment's first use, i.e. for all the epilogue stores issued so far,
+    // and the salts were loaded here and waited for twice.  (gfx9 encoding: vmcnt 0,
+    // expcnt 7, lgkmcnt 15.)
+    __builtin_amdgcn_s_waitcnt(0x0F70);
     const int x = li & 3;
     const int g = (threadIdx.x & 63) >> 4;
     f32x4 acc[FM][FN];
@@ -689,8 +710,8 @@ struct VecEpi {
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = SW ? acc_in[i][j] : quad_transpose(acc_in[i][j], x);
     uint32_t salt_drop = 0, salt_dp = 0;
-    if (p.thr_drop) salt_drop = site_salt(p.rng, p.site_drop);
-    if (p.thr_dp) salt_dp = site_salt(p.rng, p.site_dp);
+    if (p.thr_drop) salt_drop = site_salt_v((uint64_t)rng0, (uint64_t)rng1, p.site_drop);
+    if (p.thr_dp) salt_dp = site_salt_v((uint64_t)rng0, (uint64_t)rng1, p.site_dp);
     const bool fold = FC && p.ln_st != nullptr;
     const bool prod = FP && p.st_out != nullptr;
     float lsum = 0.f;  // HEADL: this lane's loss contributions

@@ -94,11 +94,10 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict_
     gm[i] = g2[lane + 64 * i];
     bt[i] = y_out ? reinterpret_cast<const float2*>(beta)[lane + 64 * i] : make_float2(0.f, 0.f);
   }
-  uint32_t salt_drop = 0, salt_dp = 0;
-  if (gy) {
-    if (thr_drop) salt_drop = site_salt(rng, site_drop);
-    if (thr_dp) salt_dp = site_salt(rng, site_dp);
-  }
+  // rng words loaded here, with the rows' loads, and the salts computed after ONE
+  // explicit wait for all of them (below): site_salt() here was sunk by the compiler
+  // past the row-data wait, one more dependent round trip per wave
+  const uint64_t rng0 = (uint64_t)rng[0], rng1 = (uint64_t)rng[1];  // rng: always a valid [2]
   // RPW rows per wave, all rows' loads issued before any use (latency-bound op)
   float2 xv[RPW][VEC], dv[RPW][VEC], rv[RPW][VEC];
   float muv[RPW], rsv[RPW];
@@ -109,7 +108,10 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict_
     const int row = rows[j] < M ? rows[j] : M - 1;
     const float2* xr = reinterpret_cast<const float2*>(reinterpret_cast<const float*>(x) + (size_t)row * D);
     const bf16x2* xr16 = reinterpret_cast<const bf16x2*>(reinterpret_cast<const bf16*>(x) + (size_t)row * D);
-    const float2* gr = reinterpret_cast<const float2*>(g_res + (size_t)row * D);
+    // unconditional load (g_out when there is no residual gradient: same shape, the value
+    // is dropped below): `g_res ? load : 0` became a phi copy that waited for every load
+    // issued before it
+    const float2* gr = reinterpret_cast<const float2*>((g_res ? g_res : g_out) + (size_t)row * D);
     auto ldy = [&](int pt, int i) -> float2 {
       const size_t off = (size_t)pt * M * D + (size_t)row * D;
       if (DYB) {
@@ -127,7 +129,7 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict_
         xv[j][i] = xr[lane + 64 * i];
       }
       dv[j][i] = ldy(0, i);
-      rv[j][i] = g_res ? gr[lane + 64 * i] : make_float2(0.f, 0.f);
+      rv[j][i] = gr[lane + 64 * i];
     }
     for (int pt = 1; pt < dy_parts; ++pt) {  // K-split dgrad partials
 #pragma unroll
@@ -140,6 +142,11 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict_
     muv[j] = mean[row];
     rsv[j] = rstd[row];
   }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): rows + rng words (gfx9: expcnt 7, lgkmcnt 15)
+  // unconditional (a few VALU ops): a use only under `if (gy)` let LLVM sink the loads
+  // into that block, past the wait
+  const uint32_t salt_drop = site_salt_v(rng0, rng1, site_drop);
+  const uint32_t salt_dp = site_salt_v(rng0, rng1, site_dp);
 #pragma unroll
   for (int j = 0; j < RPW; ++j) {
     const int row = rows[j];
@@ -166,8 +173,8 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict_
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
       const int c = lane + 64 * i;
-      float2 o = make_float2((dxh[i].x - c1 - xh[i].x * c2) * rs + rv[j][i].x,
-                             (dxh[i].y - c1 - xh[i].y * c2) * rs + rv[j][i].y);
+      const float2 r = g_res ? rv[j][i] : make_float2(0.f, 0.f);
+      float2 o = make_float2((dxh[i].x - c1 - xh[i].x * c2) * rs + r.x, (dxh[i].y - c1 - xh[i].y * c2) * rs + r.y);
       reinterpret_cast<float2*>(g_out + (size_t)row * D)[c] = o;
       if (y_out) {
         // the LayerNorm output itself (bf16), for the weight gradient of the GEMM
