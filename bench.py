@@ -204,9 +204,7 @@ def run(args):
         if args.comm_layout == "auto":
             engine.autotune_comm()
         else:
-            lay = engine.layout_by_name(args.comm_layout)
-            engine.set_comm_layout(lay[1], lay[2], lay[3])
-            engine.comm_choice = lay[0]
+            engine.apply_layout(args.comm_layout)
     engine.train_steps(args.warmup)
     if dev.type == "cuda":
         torch.cuda.synchronize()
@@ -349,7 +347,10 @@ def run(args):
                        "allreduce": ("none" if not engine.segmented else "eager" if dev.type != "cuda" else
                                      "host-issued-between-event-split-graphs" if engine.cfg.comm_events else
                                      "segmented" if (args.segmented_comm or getattr(engine, "_graph_comm_failed", False))
-                                     else "captured-in-graph"),
+                                     else "captured-in-graph-inline" if engine.cfg.comm_inline
+                                     else "captured-in-graph-comm-branch"),
+                       "autotune_s": round(getattr(engine, "autotune_s", 0.0), 2) or None,
+                       "autotune_dropped": getattr(engine, "autotune_errors", None) or None,
                        "grad_wire": args.grad_wire,
                        "comm": engine.comm_backend if engine.segmented else "none",
                        "comm_layout": engine.comm_choice,

@@ -38,7 +38,9 @@ restored; overrides ``bucket_blocks``), ``total_steps`` (DDIM T, default 2000), 
 ``timestep_embedding`` ('learned' | 'sinusoidal'), ``max_steps`` (cap per epoch,
 for smoke runs), ``comm_layout`` (fixed data-parallel gradient-exchange layout
 instead of ``comm_autotune``), ``force_segments`` (testing: run the data-parallel
-step on a 1-rank process group).
+step on a 1-rank process group), ``graph_steps`` (optimizer steps per hipGraph
+replay, default 4; the batch rows come from a device table indexed by the step
+counter, so one replay runs K whole steps).
 """
 from __future__ import annotations
 
@@ -88,8 +90,9 @@ class ExperimentConfig:
     fault_inject_step: int = 0    # testing: raise after this many steps (after logging), to exercise resume
     fault_inject_rank: int = -1   # testing: only this rank raises (-1: every rank) -- one dead rank mid-epoch
     perf_log: bool = True         # extra '# perf' lines (img/s, device ms/step) next to the reference lines
-    comm_layout: Optional[str] = None  # data parallel: 'overlap-<blocks>' | 'inline-1' (skips comm_autotune)
+    comm_layout: Optional[str] = None  # data parallel: '[graph-]overlap-<blocks>' | '[graph-]inline-1' (skips comm_autotune)
     force_segments: bool = False  # testing: the data-parallel step (1-rank RCCL group, comm stream) at num_gpus 1
+    graph_steps: int = 4          # optimizer steps per replayed hipGraph (1: one graph per step)
 
     # ------------------------------------------------------------------ derived
     @property
@@ -122,10 +125,12 @@ class ExperimentConfig:
             raise ValueError(f"unknown dataset kind {self.dataset!r}")
         if self.dataset.startswith("cold") and self.image_size[0] != self.image_size[1]:
             raise ValueError("cold (down-sample) datasets require square images (diffusion_loader.py:74)")
-        if self.comm_layout is not None and not (self.comm_layout == "inline-1" or (
-                self.comm_layout.startswith("overlap-") and self.comm_layout[8:].isdigit()
-                and int(self.comm_layout[8:]) >= 1)):
-            raise ValueError(f"unknown comm_layout {self.comm_layout!r}")
+        if self.comm_layout is not None:
+            base = self.comm_layout[6:] if self.comm_layout.startswith("graph-") else self.comm_layout
+            if not (base == "inline-1" or (base.startswith("overlap-") and base[8:].isdigit() and int(base[8:]) >= 1)):
+                raise ValueError(f"unknown comm_layout {self.comm_layout!r}")
+        if self.graph_steps < 1:
+            raise ValueError("graph_steps must be >= 1")
         if not self.synthetic and not all(self.dataStorage):
             raise ValueError("dataStorage needs [train_dir, val_dir] unless synthetic: true")
         return self

@@ -162,6 +162,30 @@ std::tuple<Tensor, Tensor> patch_embed_fwd(Tensor img, Tensor t, Tensor w_pe, Te
                           patches_in);
 }
 
+// Pool indices of a batch source that reads them (!draw_idx): a [B] vector, or with
+// `ctr` a stepped table [rows][...] read at row ctr[0] % rows, elements off..off+B
+// (the trainer's epoch DistributedSampler table indexed by the device step counter).
+struct IdxSel {
+  int64_t* p;
+  const int64_t* ctr;
+  int rows, stride;
+};
+static IdxSel idx_select(const Tensor& idx, const c10::optional<Tensor>& ctr, int64_t off, int B, bool draw_idx,
+                         const char* what) {
+  if (ctr.has_value() && ctr->defined()) {
+    CHECK_IN((*ctr), I64);
+    TORCH_CHECK(ctr->device() == idx.device() && ctr->numel() >= 1, what, ": step counter");
+    TORCH_CHECK(!draw_idx, what, ": a stepped index table is read, not drawn");
+    TORCH_CHECK(idx.dim() >= 2 && idx.size(0) >= 1, what, ": a stepped index table is [rows, ...]");
+    const int64_t rows = idx.size(0), stride = idx.numel() / rows;
+    TORCH_CHECK(off >= 0 && off + B <= stride && idx.numel() < ((int64_t)1 << 31), what,
+                ": batch offset outside the table row");
+    return {idx.data_ptr<int64_t>() + off, ctr->data_ptr<int64_t>(), (int)rows, (int)stride};
+  }
+  TORCH_CHECK(idx.numel() == B && off == 0, what, ": idx shape");
+  return {idx.data_ptr<int64_t>(), nullptr, 1, 0};
+}
+
 // patch_embed_fwd with the cold-diffusion batch draw fused into the patchify launch
 // (cold_batch + patch_embed_fwd in one launch fewer): `img` is the x_t buffer (its
 // shape drives the launch; written only if write_xt), `target`, `t` and `idx` are outputs
@@ -172,11 +196,13 @@ std::tuple<Tensor, Tensor> patch_embed_cold_fwd(Tensor pool, int64_t data_site, 
                                                 bool write_xt, Tensor w_pe, Tensor b_pe, Tensor cls, Tensor pos,
                                                 Tensor temb, Tensor rng, int64_t site, double p, int64_t patch,
                                                 c10::optional<Tensor> ln_st, c10::optional<Tensor> xb_out,
-                                                int64_t gauss_T, int64_t noise_site, bool target_rows) {
+                                                int64_t gauss_T, int64_t noise_site, bool target_rows,
+                                                c10::optional<Tensor> idx_ctr, int64_t idx_off) {
   CHECK_IN(pool, F32); CHECK_IN(img, F32); CHECK_IN(target, F32); CHECK_IN(t, I64); CHECK_IN(idx, I64);
   const int B = img.size(0), C = img.size(1), H = img.size(2), W = img.size(3);
   TORCH_CHECK(pool.dim() == 4 && pool.size(1) == C && pool.size(2) == H && pool.size(3) == W, "pool shape");
-  TORCH_CHECK(target.sizes() == img.sizes() && t.numel() == B && idx.numel() == B, "cold patch-embed shapes");
+  TORCH_CHECK(target.sizes() == img.sizes() && t.numel() == B, "cold patch-embed shapes");
+  const IdxSel is = idx_select(idx, idx_ctr, idx_off, B, draw_idx, "cold patch-embed");
   if (gauss_T > 0) {
     TORCH_CHECK(target_x0, "Gaussian batch: the target is x0");
     TORCH_CHECK(gauss_T <= temb.size(0), "Gaussian batch: T exceeds the time-embedding rows");
@@ -194,7 +220,10 @@ std::tuple<Tensor, Tensor> patch_embed_cold_fwd(Tensor pool, int64_t data_site, 
   cs.max_t = max_t;
   cs.draw_idx = draw_idx;
   cs.target_x0 = target_x0;
-  cs.idx = idx.data_ptr<int64_t>();
+  cs.idx = is.p;
+  cs.idx_ctr = is.ctr;
+  cs.idx_rows = is.rows;
+  cs.idx_stride = is.stride;
   cs.t_out = t.data_ptr<int64_t>();
   cs.target = target.data_ptr<float>();
   cs.x_t = write_xt ? img.data_ptr<float>() : nullptr;
@@ -904,31 +933,33 @@ std::tuple<Tensor, Tensor> pixelate_pair(Tensor img, c10::optional<Tensor> idx, 
 
 // Gaussian DDIM batch (GaussianBatcher): x_t = q_sample(pool[idx], t, eps), x0 = pool[idx]
 void gauss_batch(Tensor pool, Tensor rng, int64_t site, int64_t noise_site, int64_t T, Tensor x_t, Tensor x0,
-                 Tensor t, Tensor idx, bool draw_idx) {
+                 Tensor t, Tensor idx, bool draw_idx, c10::optional<Tensor> idx_ctr, int64_t idx_off) {
   CHECK_IN(pool, F32); check_rng(rng); CHECK_IN(x_t, F32); CHECK_IN(x0, F32); CHECK_IN(t, I64); CHECK_IN(idx, I64);
   const c10::DeviceGuard guard(pool.device());
   TORCH_CHECK(x_t.dim() == 4, "gauss_batch: x_t must be [B,C,H,W]");
   const int B = x_t.size(0), C = x_t.size(1), H = x_t.size(2), W = x_t.size(3);
   TORCH_CHECK(pool.dim() == 4 && pool.size(1) == C && pool.size(2) == H && pool.size(3) == W, "pool shape");
-  TORCH_CHECK(x0.sizes() == x_t.sizes() && t.numel() == B && idx.numel() == B, "gauss_batch shapes");
+  TORCH_CHECK(x0.sizes() == x_t.sizes() && t.numel() == B, "gauss_batch shapes");
   TORCH_CHECK(T >= 1 && (int64_t)B * C * H * W < ((int64_t)1 << 31), "gauss_batch: T / size");
+  const IdxSel is = idx_select(idx, idx_ctr, idx_off, B, draw_idx, "gauss_batch");
   gauss_batch_launch(pool.data_ptr<float>(), pool.size(0), rng.data_ptr<int64_t>(), site, noise_site, T,
-                     x_t.data_ptr<float>(), x0.data_ptr<float>(), t.data_ptr<int64_t>(), idx.data_ptr<int64_t>(),
-                     draw_idx, B, C, H, W, cur_stream());
+                     x_t.data_ptr<float>(), x0.data_ptr<float>(), t.data_ptr<int64_t>(), is.p,
+                     draw_idx, B, C, H, W, cur_stream(), is.ctr, is.rows, is.stride);
 }
 
 void cold_batch(Tensor pool, Tensor rng, int64_t site, Tensor x_t, Tensor x_tm1, Tensor t, Tensor idx_ws,
-                int64_t max_t, bool draw_idx) {
+                int64_t max_t, bool draw_idx, c10::optional<Tensor> idx_ctr, int64_t idx_off) {
   CHECK_IN(pool, F32); check_rng(rng); CHECK_IN(x_t, F32); CHECK_IN(x_tm1, F32); CHECK_IN(t, I64);
   CHECK_IN(idx_ws, I64);
   const c10::DeviceGuard guard(pool.device());
   const int B = x_t.size(0), C = x_t.size(1), H = x_t.size(2), W = x_t.size(3);
   TORCH_CHECK(pool.dim() == 4 && pool.size(1) == C && pool.size(2) == H && pool.size(3) == W, "pool shape");
-  TORCH_CHECK(x_tm1.sizes() == x_t.sizes() && t.numel() == B && idx_ws.numel() == B, "cold_batch shapes");
+  TORCH_CHECK(x_tm1.sizes() == x_t.sizes() && t.numel() == B, "cold_batch shapes");
   TORCH_CHECK(max_t >= 1 && (1 << max_t) <= W, "max_t");
+  const IdxSel is = idx_select(idx_ws, idx_ctr, idx_off, B, draw_idx, "cold_batch");
   cold_batch_launch(pool.data_ptr<float>(), pool.size(0), rng.data_ptr<int64_t>(), site, x_t.data_ptr<float>(),
-                    x_tm1.data_ptr<float>(), t.data_ptr<int64_t>(), idx_ws.data_ptr<int64_t>(), B, C, H, W, max_t,
-                    draw_idx, cur_stream());
+                    x_tm1.data_ptr<float>(), t.data_ptr<int64_t>(), is.p, B, C, H, W, max_t,
+                    draw_idx, cur_stream(), is.ctr, is.rows, is.stride);
 }
 
 
@@ -1050,13 +1081,14 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("q_sample(Tensor x0, Tensor t, Tensor eps, int total_steps) -> Tensor");
   m.def("pixelate_pair(Tensor img, Tensor? idx, Tensor t, int B) -> (Tensor, Tensor)");
   m.def("cold_batch(Tensor pool, Tensor rng, int site, Tensor(a!) x_t, Tensor(b!) x_tm1, Tensor(c!) t, "
-        "Tensor(d!) idx_ws, int max_t, bool draw_idx=True) -> ()");
+        "Tensor(d!) idx_ws, int max_t, bool draw_idx=True, Tensor? idx_ctr=None, int idx_off=0) -> ()");
   m.def("patch_embed_cold_fwd(Tensor pool, int data_site, int max_t, bool draw_idx, bool target_x0, "
         "Tensor(a!) img, Tensor(b!) target, Tensor(c!) t, Tensor(d!) idx, bool write_xt, Tensor w_pe, Tensor b_pe, "
         "Tensor cls, Tensor pos, Tensor temb, Tensor rng, int site, float p, int patch, Tensor(e!)? ln_st=None, "
-        "Tensor(f!)? xb_out=None, int gauss_T=0, int noise_site=0, bool target_rows=False) -> (Tensor, Tensor)");
+        "Tensor(f!)? xb_out=None, int gauss_T=0, int noise_site=0, bool target_rows=False, Tensor? idx_ctr=None, "
+        "int idx_off=0) -> (Tensor, Tensor)");
   m.def("gauss_batch(Tensor pool, Tensor rng, int site, int noise_site, int T, Tensor(a!) x_t, Tensor(b!) x0, "
-        "Tensor(c!) t, Tensor(d!) idx, bool draw_idx=True) -> ()");
+        "Tensor(c!) t, Tensor(d!) idx, bool draw_idx=True, Tensor? idx_ctr=None, int idx_off=0) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {

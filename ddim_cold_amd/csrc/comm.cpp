@@ -237,6 +237,24 @@ void flag_wait(Tensor flags, int64_t k, int64_t value, Tensor err, int64_t timeo
                    c10::hip::getCurrentHIPStream().stream(), timeout_us);
 }
 
+// in-process loopback all-reduce (LoopbackPair): endpoint e of two, on the current stream
+void pair_all_reduce_(Tensor buf, Tensor stage, Tensor flags, int64_t e, Tensor err, int64_t timeout_us) {
+  TORCH_CHECK(buf.is_cuda() && buf.scalar_type() == at::kFloat && buf.is_contiguous(), "buf: fp32 cuda contiguous");
+  TORCH_CHECK(stage.is_cuda() && stage.scalar_type() == at::kFloat && stage.is_contiguous() && stage.dim() == 2 &&
+                  stage.size(0) == 2 && stage.size(1) >= buf.numel(),
+              "stage: [2, >= numel] fp32");
+  TORCH_CHECK(flags.is_cuda() && flags.scalar_type() == at::kInt && flags.numel() >= pair_allreduce_flags(),
+              "flags: int32 cuda, pair_allreduce_flags() entries");
+  TORCH_CHECK(err.is_cuda() && err.scalar_type() == at::kInt && err.numel() >= 1, "err: int32 cuda");
+  TORCH_CHECK(e == 0 || e == 1, "endpoint must be 0 or 1");
+  TORCH_CHECK(buf.device() == stage.device() && buf.device() == flags.device() && buf.device() == err.device(),
+              "one device");
+  pair_allreduce_launch(buf.data_ptr<float>(), buf.numel(), stage.data_ptr<float>(), stage.size(1), flags.data_ptr(),
+                        (int)e, err.data_ptr(), timeout_us, c10::hip::getCurrentHIPStream().stream());
+}
+
+int64_t pair_flags_size() { return pair_allreduce_flags(); }
+
 bool stream_wait_value_supported(int64_t device) {
   int v = 0;
   if (hipDeviceGetAttribute(&v, hipDeviceAttributeCanUseStreamWaitValue, (int)device) != hipSuccess) return false;
@@ -254,6 +272,9 @@ TORCH_LIBRARY_FRAGMENT(ddim_cold, m) {
   m.def("stream_wait_flag(Tensor flags, int k, int value) -> ()", &stream_wait_flag);
   m.def("stream_wait_value_supported(int device) -> bool", &stream_wait_value_supported);
   m.def("flag_wait(Tensor flags, int k, int value, Tensor(a!) err, int timeout_us=0) -> ()", &flag_wait);
+  m.def("pair_all_reduce_(Tensor(a!) buf, Tensor(b!) stage, Tensor(c!) flags, int e, Tensor(d!) err, "
+        "int timeout_us=0) -> ()", &pair_all_reduce_);
+  m.def("pair_flags_size() -> int", &pair_flags_size);
   m.def("comm_unique_id() -> Tensor", &comm_unique_id);
   m.def("comm_init(Tensor uid, int world, int rank, int device) -> int", &comm_init);
   m.def("comm_all_reduce_(Tensor(a!) buf, int handle, int op=0) -> ()", &comm_all_reduce_);

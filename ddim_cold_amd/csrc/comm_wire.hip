@@ -66,7 +66,9 @@ __global__ __launch_bounds__(64) void flag_bump_kernel(unsigned int* __restrict_
 // until it reaches `expected` (wrap-safe), sleeping between polls.  Bounded: after
 // `ticks` of s_memrealtime (100 MHz; 2e8 = 2 s by default) it gives up and raises
 // err[0], so a hand-off that never comes cannot wedge the GPU; the host checks err
-// (FlagSignal.check).
+// (FlagSignal.check).  Fail-fast: once err is raised (by this or any earlier wait)
+// every later wait returns at once, so a broken hand-off layout costs ONE timeout,
+// not one per bucket per step, before the host sees the error and drops it.
 __global__ __launch_bounds__(64) void flag_wait_kernel(const unsigned int* __restrict__ flags, int k,
                                                        unsigned int expected, unsigned int* __restrict__ err,
                                                        unsigned long long ticks) {
@@ -76,6 +78,7 @@ __global__ __launch_bounds__(64) void flag_wait_kernel(const unsigned int* __res
   while (true) {
     const unsigned int v = __hip_atomic_load(flags + k + lane, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
     if (static_cast<int>(v - expected) >= 0) break;
+    if (__hip_atomic_load(err + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) break;
     if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
       __hip_atomic_store(err + lane, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       break;
@@ -84,9 +87,90 @@ __global__ __launch_bounds__(64) void flag_wait_kernel(const unsigned int* __res
   }
 }
 
+// In-process loopback all-reduce between TWO endpoints on ONE device: stands in for
+// RCCL when one process drives two data-parallel engines (parallel/comm.py
+// LoopbackPair), so each engine's comm-stream work depends on the OTHER engine's
+// compute replay -- the cross-rank dependency a 1-rank group never creates.
+// Workgroup b of endpoint e owns chunk b of the buffer and pairs only with
+// workgroup b of the peer's launch (no grid-wide barrier; both launches are
+// kPairBlocks workgroups, co-resident on a 256-CU device):
+//   1. c = arrive[e][b] + 1 (its own counter: graph replays need no host value)
+//   2. copy the chunk into stage[e]; publish arrive[e][b] = c (agent release)
+//   3. wait for arrive[1-e][b] >= c; chunk = stage[0] + stage[1] (the same order on
+//      both endpoints: bit-identical replicas)
+//   4. publish done[e][b] = c; wait for done[1-e][b] >= c (the peer has read
+//      stage[e], so the next collective may overwrite it)
+// Waits are bounded (err[0] raised, later waits return at once), so a hand-off
+// that never comes cannot wedge the GPU.
+constexpr int kPairBlocks = 64;
+
+__device__ __forceinline__ bool pair_wait(const unsigned int* f, unsigned int c, unsigned int* err,
+                                          unsigned long long ticks, unsigned int lane) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (true) {
+    const unsigned int v = __hip_atomic_load(f + lane, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if (static_cast<int>(v - c) >= 0) return true;
+    if (__hip_atomic_load(err + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return false;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+      __hip_atomic_store(err + lane, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+__global__ __launch_bounds__(256) void pair_allreduce_kernel(float* __restrict__ buf, int64_t n,
+                                                             float* __restrict__ stage, int64_t stage_n,
+                                                             unsigned int* __restrict__ flags, int e,
+                                                             unsigned int* __restrict__ err, unsigned long long ticks) {
+  __shared__ unsigned int sh_c;
+  __shared__ int sh_ok;
+  const int b = blockIdx.x;
+  const unsigned int lane = threadIdx.x;
+  unsigned int* arrive = flags;                  // [2][kPairBlocks]
+  unsigned int* done = flags + 2 * kPairBlocks;  // [2][kPairBlocks]
+  const int64_t chunk = (n + kPairBlocks - 1) / kPairBlocks;
+  const int64_t lo = b * chunk, hi = lo + chunk < n ? lo + chunk : n;
+  if (lane == 0) {
+    sh_c = __hip_atomic_load(arrive + e * kPairBlocks + b + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    sh_ok = 1;
+  }
+  __syncthreads();
+  const unsigned int c = sh_c;
+  float* mine = stage + (int64_t)e * stage_n;
+  for (int64_t i = lo + lane; i < hi; i += 256) mine[i] = buf[i];
+  __threadfence();
+  __syncthreads();
+  if (lane == 0) {
+    __hip_atomic_store(arrive + e * kPairBlocks + b + lane, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    sh_ok = pair_wait(arrive + (1 - e) * kPairBlocks + b, c, err, ticks, lane) ? 1 : 0;
+  }
+  __syncthreads();
+  if (sh_ok) {
+    const float* s0 = stage;
+    const float* s1 = stage + stage_n;
+    for (int64_t i = lo + lane; i < hi; i += 256) buf[i] = s0[i] + s1[i];
+  }
+  __threadfence();
+  __syncthreads();
+  if (lane == 0) {
+    __hip_atomic_store(done + e * kPairBlocks + b + lane, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    pair_wait(done + (1 - e) * kPairBlocks + b, c, err, ticks, lane);
+  }
+}
+
 }  // namespace dc
 
 using namespace dc;
+
+int pair_allreduce_flags() { return 4 * kPairBlocks; }
+
+void pair_allreduce_launch(float* buf, int64_t n, float* stage, int64_t stage_n, void* flags, int e, void* err,
+                           int64_t timeout_us, hipStream_t stream) {
+  const unsigned long long ticks = timeout_us > 0 ? (unsigned long long)timeout_us * 100ull : 200000000ull;
+  pair_allreduce_kernel<<<kPairBlocks, 256, 0, stream>>>(buf, n, stage, stage_n, reinterpret_cast<unsigned int*>(flags),
+                                                         e, reinterpret_cast<unsigned int*>(err), ticks);
+}
 
 void flag_wait_launch(const void* flags, int k, unsigned int expected, void* err, hipStream_t stream,
                       int64_t timeout_us) {

@@ -94,8 +94,10 @@ __global__ __launch_bounds__(256) void cold_batch_kernel(const float* __restrict
                                                          const int64_t* __restrict__ rng, int site, int max_t,
                                                          int64_t* __restrict__ idx, int64_t* __restrict__ t,
                                                          int draw_idx, float* __restrict__ xt, float* __restrict__ xtm1,
-                                                         int B, int C, int H, int W) {
+                                                         int B, int C, int H, int W, const int64_t* __restrict__ idx_ctr,
+                                                         int idx_rows, int idx_stride) {
   const uint32_t salt = site_salt(rng, site);
+  if (idx_ctr) idx += (idx_ctr[0] % idx_rows) * idx_stride;  // stepped index table row
   const int64_t per = (int64_t)C * H * W;
   const int64_t n = (int64_t)B * per;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
@@ -127,8 +129,10 @@ __global__ __launch_bounds__(256) void gauss_batch_kernel(const float* __restric
                                                           const int64_t* __restrict__ rng, int site, int noise_site,
                                                           int T, int64_t* __restrict__ idx, int64_t* __restrict__ t,
                                                           int draw_idx, float* __restrict__ xt, float* __restrict__ x0o,
-                                                          int B, int per) {
+                                                          int B, int per, const int64_t* __restrict__ idx_ctr,
+                                                          int idx_rows, int idx_stride) {
   const uint32_t salt = site_salt(rng, site), nsalt = site_salt(rng, noise_site);
+  if (idx_ctr) idx += (idx_ctr[0] % idx_rows) * idx_stride;  // stepped index table row
   const int n = B * per;
   for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) {
     const int b = e / per, rem = e - b * per;
@@ -180,15 +184,15 @@ void pixelate_pair_launch(const float* img, const int64_t* idx, const int64_t* t
 
 void gauss_batch_launch(const float* pool, int pool_n, const int64_t* rng, int site, int noise_site, int T,
                         float* x_t, float* x0, int64_t* t, int64_t* idx, bool draw_idx, int B, int C, int H, int W,
-                        hipStream_t stream) {
+                        hipStream_t stream, const int64_t* idx_ctr, int idx_rows, int idx_stride) {
   const int per = C * H * W;
   hipLaunchKernelGGL(gauss_batch_kernel, dim3(g_grid((int64_t)B * per)), dim3(256), 0, stream, pool, pool_n, rng, site,
-                     noise_site, T, idx, t, draw_idx ? 1 : 0, x_t, x0, B, per);
+                     noise_site, T, idx, t, draw_idx ? 1 : 0, x_t, x0, B, per, idx_ctr, idx_rows, idx_stride);
 }
 
 void cold_batch_launch(const float* pool, int pool_n, const int64_t* rng, int site, float* x_t, float* x_tm1,
                        int64_t* t, int64_t* idx_ws, int B, int C, int H, int W, int max_t, bool draw_idx,
-                       hipStream_t stream) {
+                       hipStream_t stream, const int64_t* idx_ctr, int idx_rows, int idx_stride) {
   hipLaunchKernelGGL(cold_batch_kernel, dim3(g_grid((int64_t)B * C * H * W)), dim3(256), 0, stream, pool, pool_n, rng,
-                     site, max_t, idx_ws, t, draw_idx ? 1 : 0, x_t, x_tm1, B, C, H, W);
+                     site, max_t, idx_ws, t, draw_idx ? 1 : 0, x_t, x_tm1, B, C, H, W, idx_ctr, idx_rows, idx_stride);
 }

@@ -141,6 +141,7 @@ __global__ __launch_bounds__(256) void patchify_cls_kernel(const float* __restri
                                                            uint32_t thr, float dsc, float* __restrict__ st,
                                                            bf16* __restrict__ xb, int patch_blocks, ColdSrc cs) {
   const int Hp = H / P, Wp = W / P, NP = Hp * Wp, F = C * P * P, N = NP + 1;
+  if (cs.idx_ctr) cs.idx += (cs.idx_ctr[0] % cs.idx_rows) * cs.idx_stride;  // stepped index table row
   const uint32_t csalt = cs.pool ? site_salt(rng, cs.site) : 0u;
   const uint32_t nsalt = cs.gauss_T ? site_salt(rng, cs.noise_site) : 0u;
   if ((int)blockIdx.x >= patch_blocks) {

@@ -178,11 +178,16 @@ struct ColdSrc {
   // target written as patch rows [B*P][C*p*p] in the head's output column order
   // ((a*p + b)*C + c), for the vector loss epilogue (EPI_HEADL)
   bool target_rows = false;
+  // stepped index table (!draw_idx): the batch reads idx + (idx_ctr[0] % idx_rows) *
+  // idx_stride, i.e. row <device step counter> of an epoch's [steps][micro][B]
+  // DistributedSampler table -- K-step graphs replay with no host copy per step
+  const int64_t* idx_ctr = nullptr;
+  int idx_rows = 1, idx_stride = 0;
 };
 // Gaussian DDIM batch on device in one launch (pool draw, noise, q_sample)
 void gauss_batch_launch(const float* pool, int pool_n, const int64_t* rng, int site, int noise_site, int T,
                         float* x_t, float* x0, int64_t* t, int64_t* idx, bool draw_idx, int B, int C, int H, int W,
-                        hipStream_t stream);
+                        hipStream_t stream, const int64_t* idx_ctr = nullptr, int idx_rows = 1, int idx_stride = 0);
 void patchify_cls_launch(const float* img, const int64_t* t, const float* cls, const float* pos,
                          const float* temb, void* patches, float* x, int B, int C, int H, int W, int patch,
                          int D, const int64_t* rng, int site, double p, float* st, void* xb, hipStream_t stream,
@@ -230,7 +235,7 @@ void q_sample_launch(const float* x0, const int64_t* t, const float* eps, float*
                      int total_steps, hipStream_t stream);
 void cold_batch_launch(const float* pool, int pool_n, const int64_t* rng, int site, float* x_t, float* x_tm1,
                        int64_t* t, int64_t* idx_ws, int B, int C, int H, int W, int max_t, bool draw_idx,
-                       hipStream_t stream);
+                       hipStream_t stream, const int64_t* idx_ctr = nullptr, int idx_rows = 1, int idx_stride = 0);
 
 // gradient wire format (comm_wire.hip): fp32 <-> bf16 (RNE), 16-B aligned buffers
 void wire_pack_launch(const float* src, void* dst, int64_t n, hipStream_t stream);
@@ -238,3 +243,8 @@ void wire_unpack_launch(const void* src, float* dst, int64_t n, hipStream_t stre
 void flag_bump_launch(void* flags, int k, hipStream_t stream);  // flags[k] += 1, system-scope release
 void flag_wait_launch(const void* flags, int k, unsigned int expected, void* err, hipStream_t stream,
                       int64_t timeout_us = 0);  // 0: 2 s
+// in-process loopback all-reduce of two endpoints on one device (testing the
+// cross-engine hand-off): flags = pair_allreduce_flags() zeroed uint32, stage = 2 x stage_n
+int pair_allreduce_flags();
+void pair_allreduce_launch(float* buf, int64_t n, float* stage, int64_t stage_n, void* flags, int e, void* err,
+                           int64_t timeout_us, hipStream_t stream);

@@ -46,11 +46,13 @@ class ColdBatcher:
     indices) from the engine's RNG state and writes (x_t, target, t) into static
     buffers.  target = x_{t-1} (``ColdDownSampleDataset``) or x0 (``target='x0'``,
     ``ColdDownSampleDataset_au``).  With ``idx`` (a static device int64[B] the host
-    fills each step from a shard table) the batch follows DistributedSampler order.
+    fills each step from a shard table) the batch follows DistributedSampler order;
+    with ``idx_step = (ctr, off)`` as well, ``idx`` is the whole epoch table and the
+    batch reads its row ``ctr[0] % rows`` (:func:`ops.stepped_idx`) -- no host copy.
     """
 
     def __init__(self, pool: torch.Tensor, batch: int, rng: torch.Tensor, max_t: int | None = None,
-                 target: str = "prev", idx: torch.Tensor | None = None):
+                 target: str = "prev", idx: torch.Tensor | None = None, idx_step=None):
         self.pool = pool
         B, (C, H, W) = batch, pool.shape[1:]
         self.max_t = max_t or int(math.log2(W))
@@ -62,19 +64,22 @@ class ColdBatcher:
         self.idx = torch.empty(B, dtype=torch.int64, device=dev) if idx is None else idx
         self.rng = rng
         self.target = target
+        self.idx_step = idx_step
 
     def fused_spec(self):
         """Deferred form for a consumer that fuses the draw into its patch embedding
         (:func:`ops.patch_embed_cold_fwd`): ``((x_t, target, t), cold)`` without launching
         anything; x_t is not materialised (the patch rows are pixelated from the pool)."""
-        cold = (self.pool, SITE_DATA, self.max_t, self.draw, self.target == "x0", self.x_tm1, self.idx, False, 0, 0)
+        cold = (self.pool, SITE_DATA, self.max_t, self.draw, self.target == "x0", self.x_tm1, self.idx, False, 0, 0,
+                self.idx_step)
         return (self.x_t, self.x_tm1, self.t), cold
 
     def __call__(self):
         ops.cold_batch(self.pool, self.rng, SITE_DATA, self.x_t, self.x_tm1, self.t, self.idx, self.max_t,
-                       self.draw)
+                       self.draw, idx_step=self.idx_step)
         if self.target == "x0":
-            torch.index_select(self.pool, 0, self.idx, out=self.x_tm1)
+            torch.index_select(self.pool, 0, ops.stepped_idx(self.idx, self.idx_step, self.t.shape[0]),
+                               out=self.x_tm1)
         return self.x_t, self.x_tm1, self.t
 
 
@@ -85,7 +90,7 @@ class GaussianBatcher:
     its patch-embedding launch (:meth:`fused_spec`, same values)."""
 
     def __init__(self, pool: torch.Tensor, batch: int, rng: torch.Tensor, total_steps: int = 2000,
-                 idx: torch.Tensor | None = None):
+                 idx: torch.Tensor | None = None, idx_step=None):
         self.pool = pool
         B, (C, H, W) = batch, pool.shape[1:]
         dev = pool.device
@@ -97,25 +102,26 @@ class GaussianBatcher:
         self.idx = torch.empty(B, dtype=torch.int64, device=dev) if idx is None else idx
         self.rng = rng
         self.B = B
+        self.idx_step = idx_step
 
     def fused_spec(self):
         """``((x_t, x0, t), spec)`` for :func:`ops.patch_embed_cold_fwd` (Gaussian mode)."""
-        cold = (self.pool, SITE_DATA, 1, self.draw, True, self.x0, self.idx, False, self.T, SITE_NOISE)
+        cold = (self.pool, SITE_DATA, 1, self.draw, True, self.x0, self.idx, False, self.T, SITE_NOISE, self.idx_step)
         return (self.x_t, self.x0, self.t), cold
 
     def __call__(self):
         ops.gauss_batch(self.pool, self.rng, SITE_DATA, SITE_NOISE, self.T, self.x_t, self.x0, self.t, self.idx,
-                        self.draw)
+                        self.draw, idx_step=self.idx_step)
         return self.x_t, self.x0, self.t
 
 
 def make_batcher(kind: str, pool: torch.Tensor, batch: int, rng: torch.Tensor, total_steps: int = 2000,
-                 idx: torch.Tensor | None = None):
+                 idx: torch.Tensor | None = None, idx_step=None):
     """Batch source for a dataset kind: 'cold' | 'cold_x0' | 'gaussian' (config key ``dataset``)."""
     if kind == "cold":
-        return ColdBatcher(pool, batch, rng, idx=idx)
+        return ColdBatcher(pool, batch, rng, idx=idx, idx_step=idx_step)
     if kind == "cold_x0":
-        return ColdBatcher(pool, batch, rng, target="x0", idx=idx)
+        return ColdBatcher(pool, batch, rng, target="x0", idx=idx, idx_step=idx_step)
     if kind == "gaussian":
-        return GaussianBatcher(pool, batch, rng, total_steps, idx=idx)
+        return GaussianBatcher(pool, batch, rng, total_steps, idx=idx, idx_step=idx_step)
     raise ValueError(kind)

@@ -63,19 +63,22 @@ def patch_embed_cold_fwd(cold, img, t, w_pe, b_pe, cls, pos, temb, rng, site: in
     batch instead (same values as :func:`gauss_batch` then ``patch_embed_fwd``).
     ``target_rows``: the target is written as patch rows in the head's output column
     order (:func:`image_to_rows`) into the same buffer, for :func:`head_loss` with
-    ``target_rows``."""
+    ``target_rows``.  An 11th entry ``idx_step = (ctr, off)`` (or None): ``idx`` is a
+    stepped table read at row ``ctr[0] % rows`` (see :func:`stepped_idx`)."""
     pool, dsite, max_t, draw, tx0, target, idx, write_xt = cold[:8]
     gT, nsite = (int(cold[8]), int(cold[9])) if len(cold) > 8 else (0, 0)
+    step = cold[10] if len(cold) > 10 else None
     if _hip(img):
+        ctr, off = step if step is not None else (None, 0)
         return _ops().patch_embed_cold_fwd(pool, int(dsite), int(max_t), bool(draw), bool(tx0), img, target, t, idx,
                                            bool(write_xt), w_pe, b_pe, cls, pos, temb, rng, site, float(p), patch,
-                                           ln_st, xb_out, gT, nsite, bool(target_rows))
+                                           ln_st, xb_out, gT, nsite, bool(target_rows), ctr, int(off))
     if gT > 0:
-        gauss_batch(pool, rng, dsite, nsite, gT, img, target, t, idx, draw)
+        gauss_batch(pool, rng, dsite, nsite, gT, img, target, t, idx, draw, idx_step=step)
     else:
-        cold_batch(pool, rng, dsite, img, target, t, idx, max_t, draw)
+        cold_batch(pool, rng, dsite, img, target, t, idx, max_t, draw, idx_step=step)
         if tx0:
-            torch.index_select(pool, 0, idx, out=target)
+            torch.index_select(pool, 0, stepped_idx(idx, step, img.shape[0]), out=target)
     if target_rows:
         target.copy_(image_to_rows(target.clone(), patch).reshape(target.shape))
     return patch_embed_fwd(img, t, w_pe, b_pe, cls, pos, temb, rng, site, p, patch, ln_st, xb_out)
@@ -566,16 +569,33 @@ def pixelate_pair(img, idx, t, B: int):
     return xt, xtm1
 
 
-def gauss_batch(pool, rng, site: int, noise_site: int, total_steps: int, x_t, x0, t, idx, draw_idx: bool = True):
+def stepped_idx(idx, idx_step, B: int):
+    """The [B] pool indices a batch source reads: ``idx`` itself, or with ``idx_step =
+    (ctr, off)`` row ``ctr[0] % rows`` of the stepped table ``idx`` ([rows, ...]),
+    elements ``off .. off+B`` (the trainer's epoch table indexed by the device step
+    counter, so a K-step graph needs no host copy per step)."""
+    if idx_step is None:
+        return idx
+    ctr, off = idx_step
+    r = torch.remainder(ctr.reshape(-1)[:1], idx.shape[0])  # device ops: graph-capturable, no host sync
+    return idx.reshape(idx.shape[0], -1).index_select(0, r)[0, int(off):int(off) + B]
+
+
+def gauss_batch(pool, rng, site: int, noise_site: int, total_steps: int, x_t, x0, t, idx, draw_idx: bool = True,
+                idx_step=None):
     """Gaussian DDIM batch on device in one launch (diffusion_loader.py:24-58): pool
-    index (unless ``draw_idx`` is False: ``idx`` holds them) and t ~ U{0..T-1} from the
-    ``site`` hash, eps = :func:`randn_` of a [B,C,H,W] tensor at ``noise_site``,
-    ``x_t = q_sample(x0, t, eps)``; ``x0`` = the pool images."""
+    index (unless ``draw_idx`` is False: ``idx`` holds them; ``idx_step``: see
+    :func:`stepped_idx`) and t ~ U{0..T-1} from the ``site`` hash, eps =
+    :func:`randn_` of a [B,C,H,W] tensor at ``noise_site``, ``x_t = q_sample(x0, t,
+    eps)``; ``x0`` = the pool images."""
     if _hip(pool):
-        return _ops().gauss_batch(pool, rng, site, noise_site, total_steps, x_t, x0, t, idx, bool(draw_idx))
+        ctr, off = idx_step if idx_step is not None else (None, 0)
+        return _ops().gauss_batch(pool, rng, site, noise_site, total_steps, x_t, x0, t, idx, bool(draw_idx), ctr,
+                                  int(off))
     salt = ref.site_salt(rng, site)
     B = x_t.shape[0]
     b = torch.arange(B, dtype=torch.int64)
+    idx = stepped_idx(idx, idx_step, B)
     if draw_idx:
         idx.copy_(ref.mix32(ref._mul32((2 * b) & ref.MASK32, ref.GOLDEN) ^ salt) % pool.shape[0])
     t.copy_(ref.mix32(ref._mul32((2 * b + 1) & ref.MASK32, ref.GOLDEN) ^ salt) % total_steps)
@@ -585,14 +605,17 @@ def gauss_batch(pool, rng, site: int, noise_site: int, total_steps: int, x_t, x0
     x_t.copy_(ref.q_sample(x0, t, eps, total_steps))
 
 
-def cold_batch(pool, rng, site: int, x_t, x_tm1, t, idx_ws, max_t: int, draw_idx: bool = True):
+def cold_batch(pool, rng, site: int, x_t, x_tm1, t, idx_ws, max_t: int, draw_idx: bool = True, idx_step=None):
     """Cold pixelation batch on device: t ~ U{1..max_t} (and pool indices unless
-    ``draw_idx`` is False, in which case ``idx_ws`` holds them), x_t / x_{t-1}."""
+    ``draw_idx`` is False, in which case ``idx_ws`` holds them; ``idx_step``: see
+    :func:`stepped_idx`), x_t / x_{t-1}."""
     if _hip(pool):
-        return _ops().cold_batch(pool, rng, site, x_t, x_tm1, t, idx_ws, max_t, bool(draw_idx))
+        ctr, off = idx_step if idx_step is not None else (None, 0)
+        return _ops().cold_batch(pool, rng, site, x_t, x_tm1, t, idx_ws, max_t, bool(draw_idx), ctr, int(off))
     salt = ref.site_salt(rng, site)
     B = x_t.shape[0]
     b = torch.arange(B, dtype=torch.int64)
+    idx_ws = stepped_idx(idx_ws, idx_step, B)
     if draw_idx:
         idx_ws.copy_(ref.mix32(ref._mul32((2 * b) & ref.MASK32, ref.GOLDEN) ^ salt) % pool.shape[0])
     t.copy_(1 + ref.mix32(ref._mul32((2 * b + 1) & ref.MASK32, ref.GOLDEN) ^ salt) % max_t)

@@ -116,6 +116,50 @@ class FlagSignal:
                                "collectives after the compute replay)")
 
 
+class LoopbackPair:
+    """Two data-parallel "ranks" in ONE process on ONE device, for testing the
+    multi-rank hand-off where RCCL cannot run (it refuses two ranks per device).
+
+    ``endpoint(e)`` is a communicator for engine ``e`` (:meth:`TrainEngine.attach_comm`):
+    its ``all_reduce_`` is one launch of ``pair_allreduce_kernel`` (csrc/comm_wire.hip)
+    on the caller's stream that waits, on the device, for the OTHER endpoint's
+    matching launch and then writes stage[0] + stage[1] -- so engine 0's comm-stream
+    work depends on engine 1's compute replay and vice versa, as across real ranks,
+    and both replicas get bit-identical sums.  The collective counter lives on the
+    device (graph-capturable); waits are bounded (``err``)."""
+
+    def __init__(self, device, max_numel: int, timeout_us: int = 0):
+        _ext.load(raise_on_error=True)
+        self.device = torch.device(device)
+        self.stage = torch.zeros(2, max_numel, dtype=torch.float32, device=self.device)
+        self.flags = torch.zeros(int(torch.ops.ddim_cold.pair_flags_size()), dtype=torch.int32, device=self.device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.timeout_us = int(timeout_us)
+
+    def endpoint(self, e: int) -> "_LoopbackEndpoint":
+        return _LoopbackEndpoint(self, int(e))
+
+    def failed(self) -> bool:
+        return int(self.err.item()) != 0
+
+
+class _LoopbackEndpoint:
+    def __init__(self, pair: LoopbackPair, e: int):
+        self.pair, self.e = pair, e
+
+    def all_reduce_(self, buf: torch.Tensor, op: int = SUM):
+        if op != SUM:
+            raise NotImplementedError("loopback pair: SUM only")
+        p = self.pair
+        torch.ops.ddim_cold.pair_all_reduce_(buf, p.stage, p.flags, self.e, p.err, p.timeout_us)
+
+    def info(self):
+        return (2, self.e)
+
+    def destroy(self):
+        pass
+
+
 class NativeComm:
     """One RCCL communicator over the ranks of the default process group."""
 

@@ -91,14 +91,16 @@ def save_lastepoch(path: str, model, engine, epoch: int, steps: int, loss_rec: f
 class CheckpointWriter:
     """Epoch-end checkpoints off the training critical path.
 
-    ``submit(snapshot, ...)`` returns at once: the snapshot's device copies are
-    already queued on the training stream (``TrainEngine.snapshot_to_host``), and a
-    background thread waits for its host copy, lays out ``bestloss.pkl`` /
-    ``lastepoch.pkl`` and writes them (``torch.save`` to a temp file + atomic rename),
-    while the next epoch trains.  At most one write is in flight: ``submit`` and
-    ``join`` wait for the previous one (and re-raise its error), so the snapshot
-    buffers are never overwritten mid-write and the files on disk are always whole.
-    ``join()`` before exit and before anything reads the files."""
+    ``submit(take_snapshot, ...)`` returns at once: it first waits for the previous
+    write (and re-raises its error), THEN calls ``take_snapshot()``
+    (``TrainEngine.snapshot_to_host``: device copies queued on the training stream
+    into buffers reused by every snapshot), and a background thread waits for the
+    host copy, lays out ``bestloss.pkl`` / ``lastepoch.pkl`` and writes them
+    (``torch.save`` to a temp file + atomic rename) while the next epoch trains.
+    Taking the snapshot only after the join is what keeps a new snapshot from
+    overwriting the buffers a slow previous write is still reading.  An already
+    taken snapshot object is accepted too (its caller guarantees no write is in
+    flight).  ``join()`` before exit and before anything reads the files."""
 
     def __init__(self):
         self._thread = None
@@ -120,6 +122,8 @@ class CheckpointWriter:
         import threading
         import time
         self.join()
+        if callable(snap) and not hasattr(snap, "wait"):
+            snap = snap()  # the snapshot buffers are free: the previous write has finished
 
         def work():
             try:

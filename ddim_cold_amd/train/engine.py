@@ -309,6 +309,21 @@ class TrainEngine:
         if sig is not None:
             sig.err.zero_()
 
+    def attach_comm(self, comm, world: int):
+        """Drive the gradient exchange through ``comm`` (the ``all_reduce_`` of a
+        NativeComm-like object) as one of ``world`` data-parallel replicas without a
+        process group -- e.g. two engines of one process on one device joined by a
+        :class:`parallel.comm.LoopbackPair` (tests of the cross-rank hand-off).  Needs
+        ``force_segments`` (the data-parallel step); the replicas must start from the
+        same parameters (no broadcast here)."""
+        if not (self.segmented and self.is_cuda):
+            raise ValueError("attach_comm needs a GPU engine built with force_segments=True")
+        self.ncomm = comm
+        self.world = int(world)
+        self.comm_backend = type(comm).__name__
+        self._graphs = None
+        self._multi = None
+
     def close(self):
         """Release the native communicator (before the process group is destroyed)."""
         self.materialize_lazy()
@@ -630,7 +645,7 @@ class TrainEngine:
         """Issue bucket ``k``'s collectives on the comm stream, ordered after the
         current stream (or after the event ``after``: the bucket's boundary inside
         the replayed compute graph)."""
-        if not self.dist_on or (self.world <= 1 and not self.cfg.force_segments):
+        if self.ncomm is None and (not self.dist_on or (self.world <= 1 and not self.cfg.force_segments)):
             return
         ranges = self.bucket_ranges[k]
 
@@ -701,21 +716,35 @@ class TrainEngine:
     # embed_bucket, inline).  overlap-*: buckets of 2 / 4 blocks + the embeddings,
     # all-reduced on the comm stream while the backward goes on; inline-1: ONE
     # all-reduce of the whole arena on the compute stream after the backward (no
-    # second queue: the single-process step + the collective).  With comm_events
-    # (default) no candidate captures a collective: they are host-issued between
-    # the step's two graphs.
-    COMM_LAYOUTS = (("overlap-2", 2, True, False), ("overlap-4", 4, True, False),
-                    ("inline-1", 1 << 16, False, True))
+    # second queue: the single-process step + the collective).  These run
+    # event-split: collectives host-issued between the step's two graphs.
+    # graph-inline-1: the same single all-reduce CAPTURED on the compute stream
+    # inside the step graph -- one linear graph, no second queue, no host hand-off,
+    # so ``graph_steps`` K-step graphs work data parallel too (the event-split
+    # layouts replay two graphs per step).  graph-<overlap>: the captured comm-stream
+    # branch (a fork/join per bucket inside the graph, K-step graphs as well).
+    COMM_LAYOUTS = (("graph-inline-1", 1 << 16, False, True), ("overlap-2", 2, True, False),
+                    ("overlap-4", 4, True, False), ("inline-1", 1 << 16, False, True))
 
     @classmethod
     def layout_by_name(cls, name: str):
-        """``(name, bucket_blocks, embed_bucket, inline)`` for ``overlap-<blocks>`` /
-        ``inline-1``."""
-        if name == "inline-1":
-            return cls.COMM_LAYOUTS[-1]
-        if name.startswith("overlap-") and name[8:].isdigit() and int(name[8:]) >= 1:
-            return (name, int(name[8:]), True, False)
-        raise ValueError(f"unknown gradient-exchange layout {name!r} (overlap-<blocks> or inline-1)")
+        """``(name, bucket_blocks, embed_bucket, inline)`` for ``[graph-]overlap-<blocks>``
+        / ``[graph-]inline-1`` (``graph-``: collectives captured in the step graph)."""
+        base = name[6:] if name.startswith("graph-") else name
+        if base == "inline-1":
+            return (name, 1 << 16, False, True)
+        if base.startswith("overlap-") and base[8:].isdigit() and int(base[8:]) >= 1:
+            return (name, int(base[8:]), True, False)
+        raise ValueError(f"unknown gradient-exchange layout {name!r} ([graph-]overlap-<blocks> or "
+                         "[graph-]inline-1)")
+
+    def apply_layout(self, layout):
+        """Switch to a layout given by name or ``(name, bucket_blocks, embed_bucket,
+        inline[, ...])``; records it as :attr:`comm_choice`."""
+        L = self.layout_by_name(layout) if isinstance(layout, str) else tuple(layout)
+        self.set_comm_layout(L[1], L[2], L[3], captured=L[0].startswith("graph-"))
+        self.comm_choice = L[0]
+        return L
 
     def step_profile(self):
         """Cost-model view of this engine's step (parallel.costmodel.StepProfile):
@@ -806,15 +835,16 @@ class TrainEngine:
         cands = list(self.COMM_LAYOUTS)
         best = self.model_layouts()[0]
         if best[0] not in [L_[0] for L_ in cands]:
-            cands.insert(0, best[:4])
+            cands.insert(1, best[:4])  # right after graph-inline-1 (the time budget runs in order)
         return cands
 
     def set_comm_layout(self, bucket_blocks: Optional[int] = None, embed_bucket: Optional[bool] = None,
-                        inline: Optional[bool] = None):
+                        inline: Optional[bool] = None, captured: Optional[bool] = None):
         """Re-bucket the gradient all-reduce and choose where its collectives run (a
         comm-stream branch overlapping the backward, or inline on the compute
-        stream).  The step graphs are dropped and re-captured after
-        ``graph_warmup`` eager steps of the new layout."""
+        stream) and how (``captured``: inside the step graph; else host-issued
+        between the event-split graphs).  The step graphs are dropped and
+        re-captured after ``graph_warmup`` eager steps of the new layout."""
         import dataclasses
         kw = {}
         if bucket_blocks is not None:
@@ -823,6 +853,9 @@ class TrainEngine:
             kw["embed_bucket"] = bool(embed_bucket)
         if inline is not None:
             kw["comm_inline"] = bool(inline)
+        if captured is not None:
+            kw["comm_events"] = not captured
+            kw["graph_comm"] = bool(captured)
         if self.is_cuda:
             torch.cuda.synchronize(self.device)
         self.cfg = dataclasses.replace(self.cfg, **kw)
@@ -848,46 +881,80 @@ class TrainEngine:
         self._lazy_dirty = False  # snapshots are taken materialized
         self._refresh_shadow()
 
-    def autotune_comm(self, steps: int = 100, warm: int = 10, layouts=None):
+    def autotune_comm(self, steps: int = 100, warm: int = 10, layouts=None, budget_s: Optional[float] = None):
         """Pick the gradient-exchange layout by measuring it on THIS job's ranks.
 
-        Every layout of ``layouts`` (default :attr:`COMM_LAYOUTS`) runs ``warm``
-        untimed then ``steps`` timed optimizer steps; the time is the max over ranks
-        (one all-reduce, so every rank takes the same decision) and the fastest
-        layout is kept.  Parameters, Adam moments, counters, RNG and loss EMA are
-        restored afterwards: the tuning steps leave no trace in the training state.
-        Returns ``{name: ms_per_step}`` (empty when not data parallel on a GPU)."""
+        Every layout of ``layouts`` (default :meth:`candidate_layouts`) runs
+        ``graph_warmup`` eager steps, its capture and ``warm`` replayed steps, is
+        checked, then timed over ``steps`` optimizer steps; the time is the max over
+        ranks (so every rank takes the same decision) and the fastest layout is kept.
+        Fail-fast, so the tuning can never eat the job's time limit:
+
+        * a layout whose warm-up raised (a capture the RCCL build refuses) or whose
+          counter hand-off timed out on ANY rank is dropped right after the warm-up
+          (the timed-out wait raises the error word; every later wait then returns
+          at once, so a broken layout costs one timeout, not one per bucket and step);
+        * ``budget_s`` (default ``DDIM_COLD_AUTOTUNE_BUDGET_S``, 30 s) bounds the whole
+          tuning: once spent (max over ranks), the remaining candidates are skipped.
+
+        Parameters, Adam moments, counters, RNG and loss EMA are restored afterwards:
+        the tuning steps leave no trace in the training state.  Returns
+        ``{name: ms_per_step}`` (``inf``: failed, ``nan``: skipped for time; empty
+        when not data parallel on a GPU)."""
         if not (self.segmented and self.is_cuda and self.dist_on):
             return {}
         import time
+        import warnings
         from ..parallel.dist import all_reduce_max, barrier
+        if budget_s is None:
+            budget_s = float(os.environ.get("DDIM_COLD_AUTOTUNE_BUDGET_S", "30"))
         layouts = list(layouts or self.candidate_layouts())
         snap = self._snapshot_state()
         times: Dict[str, float] = {}
-        for name, bb, eb, inline in layouts:
-            self.set_comm_layout(bb, eb, inline)
-            self.train_steps(warm + self.cfg.graph_warmup)
-            torch.cuda.synchronize(self.device)
+        self.autotune_errors: Dict[str, str] = {}
+        t_begin = time.perf_counter()
+        for L in layouts:
+            name = L[0]
+            if all_reduce_max(time.perf_counter() - t_begin, self.device) > budget_s:
+                times[name] = math.nan
+                continue
+            failed = 0.0
+            try:
+                self.apply_layout(L)
+                self.train_steps(self.cfg.graph_warmup + warm)
+                torch.cuda.synchronize(self.device)
+                if self.comm_error():
+                    failed = 1.0
+                    self.autotune_errors[name] = "hand-off wait timed out"
+            except Exception as e:  # noqa: BLE001 - a candidate that cannot run is dropped, not fatal
+                failed = 1.0
+                self.autotune_errors[name] = repr(e)[:300]
+                torch.cuda.synchronize(self.device)
+            # every rank drops the layout if it failed on ANY rank; its stale-gradient
+            # steps are undone by the state restore below
+            if all_reduce_max(failed, self.device) > 0:
+                times[name] = math.inf
+                self.reset_comm_error()
+                continue
             barrier()
             t0 = time.perf_counter()
             self.train_steps(steps)
             torch.cuda.synchronize(self.device)
             dt = time.perf_counter() - t0
-            # a layout whose hand-off timed out on ANY rank is disqualified (inf wins
-            # the max-reduction, so every rank drops it); its stale-gradient steps are
-            # undone by the state restore below
             if self.comm_error():
                 dt = math.inf
             times[name] = all_reduce_max(dt, self.device) / steps * 1e3
             self.reset_comm_error()
         ok = [L_ for L_ in layouts if math.isfinite(times[L_[0]])]
-        if not ok:
-            self._restore_state(snap)
-            raise RuntimeError(f"autotune_comm: every gradient-exchange layout failed its hand-off check: {times}")
-        best = min(ok, key=lambda L_: times[L_[0]])
         self._restore_state(snap)
-        self.set_comm_layout(best[1], best[2], best[3])
-        self.comm_choice, self.comm_times = best[0], times
+        if not ok:
+            raise RuntimeError(f"autotune_comm: no gradient-exchange layout ran: {times} {self.autotune_errors}")
+        for name, err in self.autotune_errors.items():
+            warnings.warn(f"autotune_comm: layout {name} dropped ({err})")
+        best = min(ok, key=lambda L_: times[L_[0]])
+        self.apply_layout(best)
+        self.comm_times = times
+        self.autotune_s = time.perf_counter() - t_begin
         return times
 
     def _run_eager(self):
@@ -1186,6 +1253,25 @@ class TrainEngine:
             self.flat_v[o:o + k].copy_(s["exp_avg_sq"].reshape(-1).to(self.device))
             step = int(float(s["step"]))
         self.step_ctr[0] = step
+        self._check_lazy_moments()
+
+    def _check_lazy_moments(self):
+        """The lazy time_embed rows assume zero Adam moments for the whole run.  A
+        resumed state whose moments are non-zero there (a Gaussian-diffusion run, a
+        different image size / ``temb_rows``) turns the shortcut off, so those rows
+        keep moving as torch.optim.AdamW would move them."""
+        if self.lazy is None:
+            return
+        lo, hi = self.lazy
+        if bool(self.flat_m[lo:hi].any()) or bool(self.flat_v[lo:hi].any()):
+            import warnings
+            warnings.warn("optimizer state has non-zero Adam moments on time_embed rows this run cannot "
+                          "select; updating them every step (lazy weight decay off)")
+            self.materialize_lazy()
+            self.lazy = None
+            self._graphs = None
+            self._multi = None
+            self._eager_steps = 0
 
     def scheduler_state_dict(self, sched_step: Optional[int] = None) -> dict:
         """torch CosineAnnealingLR-format state dict (at ``sched_step``, default: now).

@@ -175,6 +175,27 @@ def evaluate(model, engine: TrainEngine, pool: torch.Tensor, idx: torch.Tensor, 
     return float(total.item()) / max(nb, 1)
 
 
+class _MicroCycle:
+    """grad_accum > 1: the engine calls its batch source once per micro-batch, in
+    order (also while capturing); call j of a step goes to micro-batch j's batcher,
+    fused draw (``fused_spec``) included."""
+
+    def __init__(self, batchers):
+        self.batchers = batchers
+        self.calls = 0
+
+    def _next(self):
+        b = self.batchers[self.calls % len(self.batchers)]
+        self.calls += 1
+        return b
+
+    def __call__(self):
+        return self._next()()
+
+    def fused_spec(self):
+        return self._next().fused_spec()
+
+
 def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, paths: Paths,
                  local_rank: Optional[int] = None, backend: Optional[str] = None, verbose: bool = False) -> dict:
     local_rank = rank if local_rank is None else local_rank
@@ -217,21 +238,18 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
     temb_rows = int(math.log2(cfg.image_size[1])) + 1 if cfg.dataset.startswith("cold") else None
     ecfg = EngineConfig(lr=cfg.lr, t_max=steps_per_epoch * cfg.epoch[1], use_graph=cfg.graph,
                         bucket_blocks=cfg.bucket_blocks, seed=cfg.seed * 1000 + rank, temb_rows=temb_rows,
-                        grad_accum=A, force_segments=cfg.force_segments)
+                        grad_accum=A, force_segments=cfg.force_segments, graph_steps=cfg.graph_steps)
     engine = TrainEngine(model, ecfg, device=device)
-    # one static index row per micro-batch; the engine calls the batch source A
-    # times per step in order (also while capturing), so call j reads row j
-    idx_dev = torch.zeros(A, B, dtype=torch.int64, device=device)
-    batchers = [make_batcher(cfg.dataset, train_pool, B, engine.rng, cfg.model_total_steps, idx=idx_dev[j])
-                for j in range(A)]
-    calls = [0]
-
-    def batch_fn():
-        j = calls[0] % A
-        calls[0] += 1
-        return batchers[j]()
-
-    engine.set_batch_fn(batch_fn)
+    # the epoch's DistributedSampler table [steps, micro-batch, B] lives on the device
+    # (refilled once per epoch); the batch draw reads row ``scheduler step %
+    # steps_per_epoch`` through the engine's device step counter, so replays need no
+    # host copy per step and one hipGraph replay can run K whole steps.  Every epoch
+    # starts at a multiple of steps_per_epoch (resume included), so epoch e reads rows
+    # 0..steps_per_epoch-1 in order, as DistributedSampler batches.
+    table_dev = torch.zeros(steps_per_epoch, A, B, dtype=torch.int64, device=device)
+    batchers = [make_batcher(cfg.dataset, train_pool, B, engine.rng, cfg.model_total_steps, idx=table_dev,
+                             idx_step=(engine.step_ctr[1:2], j * B)) for j in range(A)]
+    engine.set_batch_fn(batchers[0] if A == 1 else _MicroCycle(batchers))
 
     start_epoch, end_epoch = int(cfg.epoch[0]), int(cfg.epoch[1])
     loss_rec, steps, best_loss = 5.0, 0, 5.0
@@ -251,9 +269,7 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
             printLog(f"# comm layout: {engine.comm_choice} " +
                      " ".join(f"{k}={v:.4f}ms" for k, v in times.items()), paths.log)
     if cfg.comm_layout and engine.segmented and device.type == "cuda":
-        lay = engine.layout_by_name(cfg.comm_layout)
-        engine.set_comm_layout(lay[1], lay[2], lay[3])
-        engine.comm_choice = lay[0]
+        engine.apply_layout(cfg.comm_layout)
     check_param_sync(engine.flat_p, step=steps)  # replicas start identical
     writer = ScalarWriter(paths.ckpt_dir, enabled=(rank == 0))
     clock = StepClock(device)
@@ -282,14 +298,25 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
         for epoch in range(start_epoch, end_epoch):
             model.train()
             table = shard_indices(n_train, world, rank, epoch, cfg.seed)[: steps_per_epoch * A * B]
-            table = table.view(steps_per_epoch, A, B).to(device)
-            for s in range(steps_per_epoch):
-                idx_dev.copy_(table[s])
-                with phase("train_step"):
-                    engine.train_step(materialize=False)  # lazy time_embed decay: applied at the epoch end
+            table_dev.copy_(table.view(steps_per_epoch, A, B))
+            s = 0
+            while s < steps_per_epoch:
+                # run up to the next point the host must act at (log line, sync check,
+                # injected fault, epoch end): whole K-step graph replays in between
+                n = steps_per_epoch - s
+                n = min(n, cfg.log_every - steps % cfg.log_every)
+                if cfg.sync_check_every:
+                    n = min(n, cfg.sync_check_every - steps % cfg.sync_check_every)
+                if cfg.fault_inject_step and steps < cfg.fault_inject_step:
+                    n = min(n, cfg.fault_inject_step - steps)
+                if prof is not None:
+                    n = 1
+                with phase("train_steps"):
+                    engine.train_steps(n, materialize=False)  # lazy time_embed decay: applied at the epoch end
                 if prof is not None:
                     prof.step()
-                steps += 1
+                steps += n
+                s += n
                 if cfg.sync_check_every and steps % cfg.sync_check_every == 0:
                     check_param_sync(engine.flat_p, step=steps)
                 if steps % cfg.log_every == 0:
@@ -334,8 +361,9 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
                         best_loss = vloss
                     # bestloss.pkl / lastepoch.pkl written by a background thread from a
                     # snapshot taken here (device copies on the training stream, host copy
-                    # on a side stream) while the next epoch trains
-                    ckw.submit(engine.snapshot_to_host(), os.path.join(paths.ckpt_dir, "lastepoch.pkl"), epoch,
+                    # on a side stream) while the next epoch trains; the writer takes the
+                    # snapshot only once the previous write has released its buffers
+                    ckw.submit(engine.snapshot_to_host, os.path.join(paths.ckpt_dir, "lastepoch.pkl"), epoch,
                                steps, loss_rec, best_loss,
                                best_path=os.path.join(paths.ckpt_dir, "bestloss.pkl") if best else None)
                 pdist.barrier()

@@ -155,6 +155,22 @@ def drain_before_capture(device) -> None:
 
 def is_capture_error(e: BaseException) -> bool:
     """A failure of the graph capture itself (an op illegal during capture, an
-    invalidated capture) -- as opposed to an error in the captured work."""
-    msg = str(e).lower()
-    return isinstance(e, RuntimeError) and any(s in msg for s in ("captur", "graph", "operation not permitted"))
+    invalidated capture) -- as opposed to an error in the captured work.  Matched
+    on the HIP runtime's capture error names / messages (and torch's own capture
+    checks), not on any message that merely mentions a graph."""
+    if not isinstance(e, RuntimeError):
+        return False
+    msg = str(e)
+    return any(s in msg for s in CAPTURE_ERROR_MARKERS)
+
+
+# HIP error names/strings a failed stream capture surfaces as (hipGetErrorName /
+# hipGetErrorString), plus torch's "not allowed while capturing" checks
+CAPTURE_ERROR_MARKERS = (
+    "hipErrorStreamCaptureUnsupported", "hipErrorStreamCaptureInvalidated", "hipErrorStreamCaptureMerge",
+    "hipErrorStreamCaptureUnmatched", "hipErrorStreamCaptureUnjoined", "hipErrorStreamCaptureIsolation",
+    "hipErrorStreamCaptureImplicit", "hipErrorStreamCaptureWrongThread", "hipErrorCapturedEvent",
+    "operation not permitted when stream is capturing", "operation would make the legacy stream depend",
+    "capture sequence", "stream is capturing", "during CUDA graph capture", "during graph capture",
+    "not permitted when stream is capturing",
+)

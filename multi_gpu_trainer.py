@@ -7,6 +7,13 @@ per-GPU batch (x2 for AMP) and the LR (base_lr * batch * num_gpus / 512),
 creates ``Saved_Models/<ExpName><framework>/`` with a copy of the YAML and
 ``train.log``, and trains ``num_gpus`` ranks (spawned here, or one rank per
 process under ``torchrun``), on the MI355X engine.
+
+The reference module's library functions are importable from here with their
+signatures (``ddim_cold_amd/train/compat.py``): ``printLog(string, fileName)``,
+``init_process_group(world_size, rank)``, ``evaluate(model, dataloader, device)``
+and the rank worker ``main(rank, world_size, initializing, amp, batch_size,
+epoch_num, lr, resume, datadir, SavedDir, log, CheckpointDir, image_size,
+diff_step, patch_size, embed_dim, depth, head)``; the command line is :func:`cli`.
 """
 import argparse
 import os
@@ -14,8 +21,10 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+from ddim_cold_amd.train.compat import evaluate, init_process_group, main, printLog  # noqa: E402,F401
 
-def main(argv=None):
+
+def cli(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("exp_name", help="experiment name: <ExpName>.yaml")
     ap.add_argument("--root", default=os.path.dirname(os.path.abspath(__file__)),
@@ -36,4 +45,4 @@ def main(argv=None):
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    sys.exit(cli())

@@ -85,7 +85,11 @@ def test_engine_layout_names_and_model_candidates():
     eng.world = 2
     cands = eng.candidate_layouts()
     assert {L[0] for L in TrainEngine.COMM_LAYOUTS} <= {L[0] for L in cands}
-    assert cands[0][0] == eng.model_layouts()[0][0] and len(cands[0]) == 4
+    best = eng.model_layouts()[0][0]
+    assert best in {L[0] for L in cands} and all(len(L) == 4 for L in cands)
+    assert cands[0][0] == "graph-inline-1"  # the captured inline layout is measured first
+    assert TrainEngine.layout_by_name("graph-inline-1") == ("graph-inline-1", 1 << 16, False, True)
+    assert TrainEngine.layout_by_name("graph-overlap-4") == ("graph-overlap-4", 4, True, False)
     cfg = ExperimentConfig(synthetic=True, comm_layout="overlap-5")
     assert cfg.validate() is cfg
     with pytest.raises(ValueError):

@@ -259,3 +259,21 @@ def test_slerp_and_interpolate(tiny):
     assert out.shape == (3, 3, 3, 16, 16)
     assert torch.allclose(out[0, 0], (img1 + 1) / 2) and torch.allclose(out[0, 2], (img2 + 1) / 2)
     assert out.min() >= 0 and out.max() <= 1
+
+
+def test_stepped_index_table_cpu():
+    """Batch rows from a [rows, micro, B] table at the device step counter (the trainer's
+    K-step-graph batch source) == the explicit [B] index row."""
+    from ddim_cold_amd import ops
+    from ddim_cold_amd.data.synthetic import make_batcher
+    pool = synthetic_pool(24, size=(16, 16))
+    table = torch.randperm(24)[:18].reshape(3, 2, 3)
+    ctr = torch.tensor([0, 5])
+    rng = torch.tensor([7, 2])
+    for kind in ("cold", "cold_x0", "gaussian"):
+        for j in range(2):
+            want = table[5 % 3, j]
+            assert torch.equal(ops.stepped_idx(table, (ctr[1:], 3 * j), 3), want)
+            a = make_batcher(kind, pool, 3, rng, idx=table, idx_step=(ctr[1:], 3 * j))()
+            b = make_batcher(kind, pool, 3, rng, idx=want.clone())()
+            assert all(torch.equal(u, v) for u, v in zip(a, b)), kind

@@ -66,8 +66,7 @@ def _world_worker(rank, world, port, out_path):
         res = {}
         for name, wire, gauss, layout in VARIANTS:
             eng = _engine(wire, gauss, seed=rank)  # different init per rank: rank 0's is broadcast
-            lay = eng.layout_by_name(layout)
-            eng.set_comm_layout(lay[1], lay[2], lay[3])
+            eng.apply_layout(layout)
             assert (eng.temb_bucket is not None) == (gauss and layout != "inline-1") or gauss
             x, y, t = _batch(gauss)
             sl = slice(rank * b, (rank + 1) * b)

@@ -332,12 +332,14 @@ def _layout_worker(rank, world, port, out_path):
         res = {}
         # the fixed layouts + model-picked bucket sizes (cost model candidates)
         lays = list(eng.COMM_LAYOUTS) + [eng.layout_by_name(n) for n in ("overlap-1", "overlap-3", "overlap-7")]
-        for name, bb, eb, inline in lays:
-            eng.set_comm_layout(bb, eb, inline)
+        for L in lays:
+            name = L[0]
+            eng.apply_layout(L)
+            assert eng.comm_choice == name and eng.cfg.comm_events == (not name.startswith("graph-"))
             cover = sorted(eng.buckets)  # buckets tile the arena for every layout
             assert cover[0][0] == 0 and cover[-1][1] == eng.numel
             assert all(a[1] == c[0] for a, c in zip(cover, cover[1:]))
-            if name == "inline-1":
+            if name.endswith("inline-1"):
                 assert len(eng.buckets) == 1 and eng.comm is None
             eng.step(xb, yb, tb)
             eng.step(xb, yb, tb)
@@ -362,7 +364,7 @@ def test_comm_layouts_same_training_gloo():
     assert torch.equal(r["p0"], r["p_end"])
     base = r["overlap-2"]
     assert not torch.equal(base[0], r["p0"])
-    for name in ("overlap-4", "inline-1", "overlap-1", "overlap-3", "overlap-7"):
+    for name in ("overlap-4", "inline-1", "graph-inline-1", "overlap-1", "overlap-3", "overlap-7"):
         for a, b in zip(base, r[name]):
             assert torch.equal(a, b), name
 
@@ -430,3 +432,28 @@ def test_lazy_decay_snapshot_restore_and_load():
     eng.train_steps(1, materialize=False)
     eng.sync_params_from_model()
     assert float(eng.lazy_decay) == 1.0 and not eng._lazy_dirty
+
+
+def test_resume_with_moments_on_lazy_rows_turns_lazy_off():
+    """An optimizer state whose Adam moments are non-zero on the rows the cold run can
+    never select (e.g. from a Gaussian-diffusion run) disables the lazy shortcut, so
+    those rows keep their torch.optim.AdamW updates."""
+    model = _model()
+    eng = TrainEngine(model, EngineConfig(lr=1e-3, t_max=50, seed=3, temb_rows=7), device="cpu")
+    assert eng.lazy is not None
+    sd = eng._optimizer_sd(eng.flat_m, eng.flat_v, 0, 0)
+    names = [n for n, _ in model.named_parameters()]
+    i_t = names.index("time_embed.weight")
+    shape = model.time_embed.weight.shape
+    m = torch.zeros(shape)
+    m[100] = 0.5
+    sd["state"] = {i_t: {"step": torch.tensor(3.0), "exp_avg": m, "exp_avg_sq": m.abs()}}
+    with pytest.warns(UserWarning, match="lazy weight decay off"):
+        eng.load_optimizer_state_dict(sd)
+    assert eng.lazy is None
+    # zero moments there (a cold run's own checkpoint): the shortcut stays on
+    eng2 = TrainEngine(_model(), EngineConfig(lr=1e-3, t_max=50, seed=3, temb_rows=7), device="cpu")
+    sd["state"][i_t]["exp_avg"] = torch.zeros(shape)
+    sd["state"][i_t]["exp_avg_sq"] = torch.zeros(shape)
+    eng2.load_optimizer_state_dict(sd)
+    assert eng2.lazy is not None

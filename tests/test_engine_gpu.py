@@ -318,3 +318,65 @@ def test_engine_gaussian_fused_batch_matches_unfused():
     pu, lu = run(False)
     assert all(abs(a - b) <= 1e-3 * abs(b) for a, b in zip(lf, lu)), (lf, lu)
     assert (pf - pu).abs().max().item() <= 2 * 1e-3 * 4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["cold", "cold_x0", "gaussian"])
+def test_stepped_index_table_matches_explicit_rows(kind):
+    """The trainer's device table (batch rows read at ``step counter % rows``, so K-step
+    graphs need no host copy) draws the same batches as an explicit [B] index vector,
+    for the fused patch-embedding draw and the stand-alone batch kernels."""
+    from ddim_cold_amd import ops
+    from ddim_cold_amd.data.synthetic import make_batcher
+    torch.manual_seed(0)
+    pool = synthetic_pool(40, seed=2, device="cuda")
+    rows, A, B = 5, 2, 8
+    table = torch.randperm(40, device="cuda")[: rows * A * B].reshape(rows, A, B).contiguous()
+    rng = torch.tensor([11, 3], dtype=torch.int64, device="cuda")
+    ctr = torch.tensor([0, 7], dtype=torch.int64, device="cuda")  # step 7 -> row 2
+    for j in range(A):
+        want_idx = table[7 % rows, j].clone()
+        st = make_batcher(kind, pool, B, rng, idx=table, idx_step=(ctr[1:2], j * B))
+        ex = make_batcher(kind, pool, B, rng, idx=want_idx)
+        a, b = st(), ex()
+        torch.cuda.synchronize()
+        assert all(torch.equal(u, v) for u, v in zip(a, b)), (kind, j)
+        assert torch.equal(ops.stepped_idx(table, (ctr[1:2], j * B), B), want_idx)
+        (xs, ts_, tt), spec = st.fused_spec()
+        assert spec[10] is not None and spec[6] is table
+    with pytest.raises(RuntimeError):  # a stepped table is read, never drawn into
+        ops.cold_batch(pool, rng, 3, torch.empty(B, 3, 64, 64, device="cuda"), torch.empty(B, 3, 64, 64, device="cuda"),
+                       torch.empty(B, dtype=torch.int64, device="cuda"), table, 6, True, idx_step=(ctr[1:2], 0))
+    with pytest.raises(RuntimeError):  # batch offset past the end of a table row
+        ops.cold_batch(pool, rng, 3, torch.empty(B, 3, 64, 64, device="cuda"), torch.empty(B, 3, 64, 64, device="cuda"),
+                       torch.empty(B, dtype=torch.int64, device="cuda"), table, 6, False, idx_step=(ctr[1:2], A * B - 4))
+
+
+@pytest.mark.gpu
+def test_patch_embed_cold_stepped_table_matches_explicit():
+    from ddim_cold_amd import ops
+    from ddim_cold_amd.data.synthetic import SITE_DATA
+    from ddim_cold_amd.models.program import SITE_EMBED
+    torch.manual_seed(0)
+    model = build_model("vit_tiny").cuda().train()
+    B, D = 8, model.embed_dim
+    N = model.patch_embed.num_patches + 1
+    pool = synthetic_pool(32, seed=2, device="cuda")
+    rng = torch.tensor([11, 5], dtype=torch.int64, device="cuda")
+    table = torch.randint(0, 32, (3, 1, B), device="cuda")
+    ctr = torch.tensor([4], dtype=torch.int64, device="cuda")  # row 1
+    pe_w = model.patch_embed.proj.weight.detach().reshape(D, -1).to(torch.bfloat16).contiguous()
+    args = (pe_w, model.patch_embed.proj.bias.detach(), model.cls_token.detach(), model.pos_embed.detach(),
+            model.time_embed.weight.detach(), rng, SITE_EMBED, 0.1, model.patch_size)
+
+    def run(idx, step):
+        xt, tg = torch.empty(B, 3, 64, 64, device="cuda"), torch.empty(B, 3, 64, 64, device="cuda")
+        t = torch.empty(B, dtype=torch.int64, device="cuda")
+        st, xb = torch.empty(B * N, D // 32, 2, device="cuda"), torch.empty(B * N, D, dtype=torch.bfloat16, device="cuda")
+        cold = (pool, SITE_DATA, 6, False, False, tg, idx, True, 0, 0, step)
+        x, p = ops.patch_embed_cold_fwd(cold, xt, t, *args, ln_st=st, xb_out=xb)
+        return x, p, xt, tg, t, st, xb
+    a = run(table, (ctr, 0))
+    b = run(table[1, 0].clone(), None)
+    torch.cuda.synchronize()
+    assert all(torch.equal(u, v) for u, v in zip(a, b))

@@ -252,6 +252,44 @@ def test_async_lastepoch_equals_sync_and_resumes_identically(tmp_path):
     assert all(torch.equal(x, y) for x, y in zip(*finals))
 
 
+def test_back_to_back_snapshots_do_not_tear_a_slow_write(tmp_path, monkeypatch):
+    """A second epoch-end submit while the first write is still laying out its file
+    must not overwrite the snapshot buffers under it (the trainer passes the snapshot
+    callable, which the writer calls only after joining the previous write)."""
+    import time
+    from ddim_cold_amd.data.synthetic import ColdBatcher, synthetic_pool
+    from ddim_cold_amd.models import DiffusionVisionTransformer
+    from ddim_cold_amd.train.engine import EngineConfig, TrainEngine
+
+    torch.manual_seed(3)
+    m = DiffusionVisionTransformer(img_size=[16, 16], patch_size=4, embed_dim=32, depth=2, num_heads=2)
+    e = TrainEngine(m, EngineConfig(lr=1e-2, t_max=20, use_graph=False, seed=9, temb_rows=5), device="cpu")
+    e.set_batch_fn(ColdBatcher(synthetic_pool(16, size=(16, 16), seed=1), 4, e.rng))
+    for _ in range(2):
+        e.train_step()
+    want = {k: v.clone() for k, v in m.state_dict().items()}
+    real = ckpt.lastepoch_dict
+    calls = []
+
+    def slow_layout(snap, *a):
+        calls.append(1)
+        if len(calls) == 1:
+            time.sleep(0.5)  # the first write is still reading its snapshot...
+        return real(snap, *a)
+    monkeypatch.setattr(ckpt, "lastepoch_dict", slow_layout)
+    w = ckpt.CheckpointWriter()
+    p1, p2 = str(tmp_path / "e0.pkl"), str(tmp_path / "e1.pkl")
+    w.submit(e.snapshot_to_host, p1, 0, 2, 0.5, 0.25)
+    for _ in range(3):  # ...when the next epoch ends and snapshots again
+        e.train_step()
+    w.submit(e.snapshot_to_host, p2, 1, 5, 0.4, 0.2)
+    w.join()
+    got = ckpt.strip_prefix(torch.load(p1, weights_only=True)["state_dict"])
+    assert all(torch.equal(got[k], want[k]) for k in want)
+    later = ckpt.strip_prefix(torch.load(p2, weights_only=True)["state_dict"])
+    assert any(not torch.equal(later[k], want[k]) for k in want)
+
+
 def test_checkpoint_writer_surfaces_errors(tmp_path):
     class Bad:
         def wait(self):
@@ -261,3 +299,65 @@ def test_checkpoint_writer_surfaces_errors(tmp_path):
     with pytest.raises(RuntimeError, match="disk full"):
         w.join()
     w.join()  # reported once
+
+
+def test_is_capture_error_matches_capture_failures_only():
+    from ddim_cold_amd.utils.observe import is_capture_error
+    assert is_capture_error(RuntimeError("HIP error: operation not permitted when stream is capturing"))
+    assert is_capture_error(RuntimeError("hipErrorStreamCaptureInvalidated: capture invalidated"))
+    # real errors that merely mention a graph are not swallowed into the eager fallback
+    assert not is_capture_error(RuntimeError("shape mismatch in graph input buffer"))
+    assert not is_capture_error(RuntimeError("HIP error: an illegal memory access was encountered"))
+    assert not is_capture_error(ValueError("hipErrorStreamCaptureInvalidated"))
+
+
+def test_reference_l5_api_shims(tmp_path):
+    """multi_gpu_trainer's library functions with the reference signatures
+    (multi_gpu_trainer.py:18-51): evaluate() over a torch DataLoader of
+    ColdDownSampleDataset batches equals the per-batch mean smooth-L1, and main(rank,
+    world_size, ...) trains one rank into the reference's log / checkpoint files."""
+    import importlib.util
+    import numpy as np
+    from PIL import Image
+    from torch.utils.data import DataLoader
+    from ddim_cold_amd.data.datasets import ColdDownSampleDataset
+    from ddim_cold_amd.models import DiffusionVisionTransformer
+    spec = importlib.util.spec_from_file_location("mgt", os.path.join(ROOT, "multi_gpu_trainer.py"))
+    mgt = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mgt)
+    for d in ("train", "val"):
+        os.makedirs(tmp_path / d)
+        g = np.random.default_rng(3 if d == "train" else 4)
+        for i in range(12):
+            Image.fromarray(g.integers(0, 255, (20, 20, 3), dtype=np.uint8)).save(tmp_path / d / f"{i}.png")
+    torch.manual_seed(0)
+    model = DiffusionVisionTransformer(img_size=[16, 16], patch_size=4, embed_dim=32, depth=2, num_heads=2)
+    ds = ColdDownSampleDataset(str(tmp_path / "val"), imgSize=[16, 16])
+    loader = DataLoader(ds, batch_size=4, shuffle=False)
+    import random
+    random.seed(5)
+    np.random.seed(5)
+    torch.manual_seed(5)  # the dataset draws each sample's t at random
+    got = mgt.evaluate(model, loader, "cpu")
+    assert not model.training
+    want = []
+    random.seed(5)
+    np.random.seed(5)
+    torch.manual_seed(5)
+    with torch.no_grad():
+        for x, y, t in loader:
+            want.append(torch.nn.functional.smooth_l1_loss(model(x, t), y).item())
+    assert got == pytest.approx(float(np.array(want).mean()), rel=1e-6)
+    log = str(tmp_path / "Saved_Models" / "exp" / "train.log")
+    os.makedirs(os.path.dirname(log), exist_ok=True)
+    mgt.printLog("hello", log)
+    res = mgt.main(0, 1, "init.pkl", True, 4, [0, 1], 1e-3, "none",
+                   [str(tmp_path / "train"), str(tmp_path / "val")], str(tmp_path / "Saved_Models") + "/", log,
+                   str(tmp_path / "Saved_Models" / "exp") + "/", [16, 16], 4, 4, 32, 2, 2,
+                   backend="gloo", graph=False, log_every=1, num_workers=0)
+    assert res["steps"] == 3  # 12 images // batch 4
+    text = open(log).read()
+    assert text.startswith("hello\nDate: ") and "TrainSet batchs:3" in text and "epoch:    0" in text
+    assert os.path.isfile(tmp_path / "Saved_Models" / "init.pkl")
+    ck = torch.load(tmp_path / "Saved_Models" / "exp" / "lastepoch.pkl", weights_only=True)
+    assert ck["steps"] == 3 and ck["scheduler"]["base_lrs"] == [pytest.approx(1e-3)]

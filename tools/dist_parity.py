@@ -15,27 +15,31 @@ from ddim_cold_amd.train.engine import EngineConfig, TrainEngine
 from ddim_cold_amd.data.synthetic import ColdBatcher, GaussianBatcher, synthetic_pool
 
 
-def run(dist_mode, comm="torch", wire="fp32", gauss=False, tune=False, layout=None):
+def run(dist_mode, comm="torch", wire="fp32", gauss=False, tune=False, layout=None, graph_steps=1):
     torch.manual_seed(0)
     model = build_model("vit_tiny").cuda().train()
     cfg = EngineConfig(lr=1e-3, t_max=100, seed=5, temb_rows=None if gauss else 7,
                        force_segments=dist_mode is not None,
                        graph_comm=dist_mode == "captured", comm_events=dist_mode == "events",
-                       graph_warmup=2, comm=comm, grad_wire=wire)
+                       graph_warmup=2, comm=comm, grad_wire=wire, graph_steps=graph_steps)
     eng = TrainEngine(model, cfg)
     pool = synthetic_pool(64, seed=3, device="cuda")
     # Gaussian diffusion (t over the whole table): sparse time_embed row exchange
     eng.set_batch_fn(GaussianBatcher(pool, 16, eng.rng, 2000) if gauss else ColdBatcher(pool, 16, eng.rng))
     assert (eng.temb_bucket is not None) == (gauss and dist_mode is not None)
     if layout is not None:
-        L = {l[0]: l for l in eng.COMM_LAYOUTS}[layout]
-        eng.set_comm_layout(L[1], L[2], L[3])
+        eng.apply_layout(layout)
     if tune:  # measures every layout, then restores the training state
         times = eng.autotune_comm(steps=4, warm=1)
         assert set(times) >= {l[0] for l in eng.COMM_LAYOUTS} and eng.comm_choice in times, times
         assert eng.steps_done == 0 and int(eng.step_ctr[0]) == 0 and int(eng.rng[1]) == 0
-    for _ in range(6):
-        eng.train_step()
+    if graph_steps > 1:  # 2 eager + capture, then one replay of the K-step graph
+        eng.train_steps(2)
+        eng.train_steps(4)
+        assert eng._multi is not None and eng._multi[1] == graph_steps == 4, "no K-step graph"
+    else:
+        for _ in range(6):
+            eng.train_step()
     torch.cuda.synchronize()
     out = eng.flat_p.clone(), float(eng.loss_last), getattr(eng, "_graph_comm_failed", False), len(eng._graphs)
     if comm in ("native", "auto"):  # auto: the native communicator came up and verified
@@ -89,6 +93,11 @@ if __name__ == "__main__":
     evi, loss7, _, ng7 = run("events", layout="inline-1")
     evt, loss8, _, ng8 = run("events", tune=True)
     eva, loss9, _, ng9 = run("events", comm="auto", tune=True)
+    # the captured inline layout: ONE all-reduce on the compute stream inside the step
+    # graph, and a 4-step graph replayed (data parallel with K-step graphs)
+    gin, loss10, gfail10, ng10 = run("events", comm="native", layout="graph-inline-1", graph_steps=4)
+    gint, loss11, gfail11, _ = run("events", comm="torch", layout="graph-inline-1", graph_steps=4)
+    assert not (gfail10 or gfail11) and ng10 == 1, (gfail10, gfail11, ng10)
     dist.destroy_process_group()
     assert ng5 == 2 and ng6 == 2 and gng2 == 2, (ng5, ng6, gng2)
     assert (gref - gev).abs().max().item() <= 2 * 1e-3 * 6 and abs(gl2 - gl0) <= 1e-4 * abs(gl0), (gl0, gl2)
@@ -107,7 +116,8 @@ if __name__ == "__main__":
     for name, other, loss in (("captured", cap, loss1), ("segmented", seg, loss2), ("native", nat, loss3),
                               ("native-bf16", natb, loss4), ("events", ev, loss5), ("events-native", evn, loss6),
                               ("events-inline", evi, loss7), ("events-autotuned", evt, loss8),
-                              ("events-auto-comm-autotuned", eva, loss9)):
+                              ("events-auto-comm-autotuned", eva, loss9), ("graph-inline-1-native-K4", gin, loss10),
+                              ("graph-inline-1-torch-K4", gint, loss11)):
         d = (ref - other).abs().max().item()
         assert d <= bound, (name, d)
         tol = 1e-2 if name.endswith("bf16") else 1e-4
