@@ -315,6 +315,13 @@ def run(args):
             te = time_img2img(model, dev, starts, 10, eager=True)
             extra["draft2drawing_eager_torch_fp32_ms"] = round(te * 1e3, 1)
             extra["draft2drawing_vs_eager_fp32"] = round(te / ti, 2)
+        if not args.no_vendor:
+            # same batching (9 starts in one batch on the shared grid) and one graph, stock
+            # ops: the kernel-quality comparator of the img2img path
+            from ddim_cold_amd.bench.vendor_baseline import time_vendor_img2img
+            tv = time_vendor_img2img(model, starts, 10, reps=5)
+            extra["draft2drawing_vendor_graph_ms"] = round(tv * 1e3, 3)
+            extra["draft2drawing_vs_vendor_graph"] = round(tv / ti, 2)
         model.train()
     if rank == 0:
         out = {

@@ -16,6 +16,12 @@ comparison the hand-written stack has to win.
   LR computed on the device (``CosineAnnealingLR``'s closed form, eta_min 0).
 * :class:`VendorSampler` — the 100-step k=20 DDIM loop of `ViT.py:220-237`
   (bf16 autocast forward, fp32 clamp / eps-hat / update) unrolled into one graph.
+* :class:`VendorImg2Img` — the draft->drawing call of `ViT_draft2drawing.py:389-409`
+  with the same batching as the fused path (all 9 t_starts in ONE batch on the
+  shared k=10 grid, per-sample coefficients, a not-yet-started sample kept by an
+  identity row) unrolled into one graph: the batched vendor counterpart of
+  :func:`ddim_cold_amd.diffusion.samplers.img2img`, so the ratio measures kernels,
+  not batching or dispatch.
 
 ``attn="sdpa"`` (default) runs attention through ``F.scaled_dot_product_attention``
 (the ROCm flash / memory-efficient kernels); ``attn="explicit"`` through the
@@ -290,6 +296,92 @@ class VendorSampler:
         else:
             self._body()
         return self.out.cpu()
+
+
+class VendorImg2Img:
+    """Batched draft->drawing DDIM loop from stock ops, all steps in one graph: sample i
+    joins the shared descending k-grid at ``starts[i]`` (identity coefficients before
+    that, :func:`ddim_cold_amd.diffusion.samplers.starts_table`); per step a bf16
+    autocast forward, fp32 clamp, eps-hat and update with per-sample coefficients."""
+
+    def __init__(self, model, starts, k: int = 10, attn: str = "sdpa", use_graph: bool = True):
+        from ..diffusion.samplers import starts_table
+        self.model = model.eval()
+        self.dev = next(model.parameters()).device
+        self.cuda = self.dev.type == "cuda"
+        self.starts, self.k, self.attn = list(starts), k, attn
+        B = len(self.starts)
+        C, (H, W) = model.in_chans, model.img_size
+        self.ts, coef = starts_table(model.total_steps, self.starts, k)
+        self.coef = coef.to(self.dev).view(len(self.ts), B, 4, 1, 1, 1)
+        self.tt = [torch.full((B,), t, dtype=torch.int64, device=self.dev) for t in self.ts]
+        self.x_in = torch.zeros(B, C, H, W, device=self.dev)
+        self.out = torch.empty(B, C, H, W, device=self.dev)
+        self.use_graph = use_graph and self.cuda
+        self.graph = None
+
+    @torch.no_grad()
+    def _body(self):
+        x = self.x_in
+        x0 = x
+        for i in range(len(self.ts)):
+            with torch.autocast(self.dev.type, dtype=torch.bfloat16, enabled=self.cuda, cache_enabled=False):
+                x0 = vendor_forward(self.model, x, self.tt[i], self.attn)
+            x0 = torch.clamp(x0.float(), -1.0, 1.0)
+            c = self.coef[i]
+            eps = (x - c[:, 0] * x0) / c[:, 1]
+            x = c[:, 2] * x0 + c[:, 3] * eps
+        self.out.copy_((x0 + 1) / 2)
+
+    def capture(self):
+        s = torch.cuda.Stream(self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(s):
+            self._body()
+        torch.cuda.current_stream(self.dev).wait_stream(s)
+        torch.cuda.synchronize(self.dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._body()
+        self.graph = g
+
+    @torch.no_grad()
+    def __call__(self, draft: torch.Tensor, generator=None) -> torch.Tensor:
+        """One call as :func:`samplers.img2img` makes it: eps drawn on the host, the
+        noised starts formed on the device, the loop, the result on the host in [0, 1]."""
+        from ..diffusion.samplers import img2img_noised
+        B = len(self.starts)
+        C, (H, W) = self.model.in_chans, self.model.img_size
+        eps = torch.normal(0.0, 1.0, (B, C, H, W), generator=generator).to(self.dev)
+        d = draft.to(self.dev).float()
+        d = d.unsqueeze(0) if d.dim() == 3 else d
+        self.x_in.copy_(img2img_noised(d.expand(B, -1, -1, -1), eps, self.starts, self.model.total_steps))
+        if self.use_graph:
+            if self.graph is None:
+                self.capture()
+            self.graph.replay()
+        else:
+            self._body()
+        return self.out.cpu()
+
+
+def time_vendor_img2img(model, starts, k: int = 10, reps: int = 5, attn: str = "sdpa") -> float:
+    """Seconds per draft->drawing call of the graph-captured batched vendor loop."""
+    was = model.training
+    try:
+        v = VendorImg2Img(model, starts, k, attn=attn)
+        g = torch.Generator().manual_seed(0)
+        C, (H, W) = model.in_chans, model.img_size
+        draft = torch.rand(1, C, H, W, generator=g) * 2 - 1
+        v(draft, g)  # capture
+        torch.cuda.synchronize(v.dev)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            v(draft, g)
+        torch.cuda.synchronize(v.dev)
+        return (time.perf_counter() - t0) / reps
+    finally:
+        model.train(was)
 
 
 def time_vendor_train(model, pool, batch: int, lr: float, t_max: int, steps: int = 50, warmup: int = 10,

@@ -94,6 +94,22 @@ def test_vendor_sampler_cpu_matches_eager_loop():
     assert s.ts == [1999, 1499, 999, 499]
 
 
+def test_vendor_img2img_cpu_matches_sequential_reference_loop():
+    """The batched vendor draft->drawing loop (all starts in one batch on the shared
+    grid) == the reference's one-start-at-a-time loop (ViT_draft2drawing.py:394-409)."""
+    from ddim_cold_amd.bench.eager_sampler import eager_img2img
+    from ddim_cold_amd.bench.vendor_baseline import VendorImg2Img
+    m = _tiny().eval()
+    starts = [1599, 1649, 1699]
+    v = VendorImg2Img(m, starts, k=50, use_graph=False)
+    C, (H, W) = m.in_chans, m.img_size
+    draft = torch.rand(1, C, H, W, generator=torch.Generator().manual_seed(2)) * 2 - 1
+    out = v(draft, torch.Generator().manual_seed(7))
+    eps = torch.normal(0.0, 1.0, (3, C, H, W), generator=torch.Generator().manual_seed(7))
+    ref = eager_img2img(m, torch.device("cpu"), draft, starts, 50, eps)
+    torch.testing.assert_close(out, (ref + 1) / 2, rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.gpu
 def test_vendor_graphs_gpu():
     from ddim_cold_amd.bench.vendor_baseline import time_vendor_sampler, time_vendor_train
@@ -128,3 +144,5 @@ def test_vendor_graphs_gpu():
     out = s.sample(torch.Generator(device=dev).manual_seed(1))
     assert out.shape == (4, 3, 64, 64) and torch.isfinite(out).all()
     assert out.min() >= 0 and out.max() <= 1
+    from ddim_cold_amd.bench.vendor_baseline import time_vendor_img2img
+    assert time_vendor_img2img(m, list(range(1599, 2000, 50)), 10, reps=1) > 0
