@@ -701,6 +701,75 @@ void linear_wgrad_multi(std::vector<Tensor> dys, std::vector<Tensor> xs, std::ve
   }
 }
 
+// dy @ W followed by the LayerNorm backward in ONE launch (csrc/gemm_lnbwd.hip): same
+// arguments and outputs as layernorm_bwd(linear_dgrad(dy, w), x, ...) with x bf16
+std::tuple<Tensor, Tensor> linear_dgrad_lnbwd(Tensor dy, Tensor w, Tensor x, Tensor mean, Tensor rstd, Tensor gamma,
+                                              c10::optional<Tensor> g_res, Tensor dgamma, Tensor dbeta, int64_t N,
+                                              Tensor rng, int64_t site_drop, double p_drop, int64_t site_dp,
+                                              double p_dp, bool emit_gy, c10::optional<Tensor> ws,
+                                              c10::optional<Tensor> beta, c10::optional<Tensor> y_out) {
+  CHECK_IN(dy, BF16); CHECK_IN(w, BF16); CHECK_IN(x, BF16);
+  CHECK_IN(mean, F32); CHECK_IN(rstd, F32); CHECK_IN(gamma, F32); CHECK_IN(dgamma, F32); CHECK_IN(dbeta, F32);
+  check_rng(rng);
+  const c10::DeviceGuard guard(x.device());
+  const int D = x.size(-1), M = x.numel() / D;
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == D, "linear_dgrad_lnbwd: w must be [K, D]");
+  const int K = w.size(0);
+  TORCH_CHECK(gemm_lnbwd_supported(D, K), "linear_dgrad_lnbwd: unsupported D / K (D 256 | 384, K % 64 == 0)");
+  TORCH_CHECK(dy.numel() == (int64_t)M * K && dy.size(-1) == K, "linear_dgrad_lnbwd: dy must be [M, K]");
+  TORCH_CHECK(mean.numel() == M && rstd.numel() == M && gamma.numel() == D && dgamma.numel() == D &&
+                  dbeta.numel() == D && M % N == 0 && (int64_t)M * D < ((int64_t)1 << 31),
+              "linear_dgrad_lnbwd shapes");
+  LnBwdParams p;
+  p.dy = dy.data_ptr();
+  p.w = w.data_ptr();
+  p.M = M;
+  p.K = K;
+  p.x = x.data_ptr();
+  p.mean = mean.data_ptr<float>();
+  p.rstd = rstd.data_ptr<float>();
+  p.gamma = gamma.data_ptr<float>();
+  if (g_res.has_value() && g_res->defined()) {
+    CHECK_IN((*g_res), F32);
+    TORCH_CHECK(g_res->numel() == x.numel(), "g_res shape");
+    p.g_res = g_res->data_ptr<float>();
+  }
+  const int R = ln_replicas();
+  const bool own_ws = !(ws.has_value() && ws->defined());
+  const auto f32o = x.options().dtype(F32);
+  Tensor wsp = own_ws ? at::zeros({R, 2 * D}, f32o) : *ws;
+  if (!own_ws) {
+    CHECK_IN(wsp, F32);
+    TORCH_CHECK(wsp.numel() == (int64_t)R * 2 * D, "ln ws must hold ln_replicas x 2D floats");
+  }
+  p.ws = wsp.data_ptr<float>();
+  p.replicas = R;
+  if (y_out.has_value() && y_out->defined()) {
+    TORCH_CHECK(beta.has_value() && beta->defined(), "y_out needs beta");
+    CHECK_IN((*beta), F32); CHECK_IN((*y_out), BF16);
+    TORCH_CHECK(beta->numel() == D && y_out->numel() == x.numel(), "beta / y_out shapes");
+    p.beta = beta->data_ptr<float>();
+    p.y_out = y_out->data_ptr();
+  }
+  auto g_out = at::empty(x.sizes(), f32o);
+  Tensor gy = emit_gy ? at::empty({M, D}, x.options().dtype(BF16)) : at::empty({0}, x.options().dtype(BF16));
+  p.g_out = g_out.data_ptr<float>();
+  p.gy = emit_gy ? gy.data_ptr() : nullptr;
+  p.tokens = (int)N;
+  p.rng = rng.data_ptr<int64_t>();
+  p.site_drop = (int)site_drop;
+  p.site_dp = (int)site_dp;
+  gemm_lnbwd_launch(p, D, p_drop, p_dp, cur_stream());
+  if (own_ws) {
+    auto s = wsp.sum(0);
+    dgamma.add_(s.narrow(0, 0, D));
+    dbeta.add_(s.narrow(0, D, D));
+  }
+  return {g_out, gy};
+}
+
+bool lnbwd_fused_supported(int64_t D, int64_t K) { return gemm_lnbwd_supported((int)D, (int)K); }
+
 // fp32 <-> bf16 gradient wire (csrc/comm_wire.hip): one fused 16-B-vector
 // kernel each way (the torch-collective bf16 wire path of the train engine)
 void wire_pack(Tensor src, Tensor dst) {
@@ -1059,6 +1128,10 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("wire_unpack(Tensor src, Tensor(a!) dst) -> ()");
   m.def("linear_wgrad_multi(Tensor[] dys, Tensor[] xs, Tensor(a!)[] dws, Tensor(b!)?[] dbs, bool store=False, "
         "Tensor(c!)? sq_parts=None, Tensor? arena=None, int lz_lo=0, int lz_hi=0) -> ()");
+  m.def("linear_dgrad_lnbwd(Tensor dy, Tensor w, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor? g_res, "
+        "Tensor(a!) dgamma, Tensor(b!) dbeta, int N, Tensor rng, int site_drop, float p_drop, int site_dp, "
+        "float p_dp, bool emit_gy, Tensor(c!)? ws=None, Tensor? beta=None, Tensor(d!)? y_out=None) -> (Tensor, Tensor)");
+  m.def("lnbwd_fused_supported(int D, int K) -> bool", &lnbwd_fused_supported);
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor? g_res, "
         "Tensor(a!) dgamma, Tensor(b!) dbeta, int N, Tensor rng, int site_drop, float p_drop, int site_dp, "
         "float p_dp, bool emit_gy, Tensor(c!)? ws=None, Tensor? beta=None, Tensor(d!)? y_out=None) -> (Tensor, Tensor)");
@@ -1113,6 +1186,7 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("wire_pack", &wire_pack);
   m.impl("wire_unpack", &wire_unpack);
   m.impl("layernorm_bwd", &layernorm_bwd);
+  m.impl("linear_dgrad_lnbwd", &linear_dgrad_lnbwd);
   m.impl("replica_reduce_", &replica_reduce_);
   m.impl("ln_fold_", &ln_fold_);
   m.impl("attn_bwd", &attn_bwd);

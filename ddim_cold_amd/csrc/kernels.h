@@ -115,6 +115,33 @@ void layernorm_bwd_launch(const void* dy, bool dy_bf16, const void* x, bool x_bf
                           double p_dp, int dy_parts, hipStream_t stream);
 int ln_replicas();
 
+// input-gradient GEMM + LayerNorm backward in one launch (gemm_lnbwd.hip): the outputs
+// of linear_dgrad followed by layernorm_bwd_launch (x bf16, fp32 dl never materialised)
+struct LnBwdParams {
+  const void* dy = nullptr;    // [M][K] gradient of the GEMM output (A)
+  const void* w = nullptr;     // [K][D] nn.Linear weight (B, transposed operand)
+  int M = 0, K = 0;
+  const void* x = nullptr;     // [M][D] LayerNorm input (bf16 copy)
+  const float* mean = nullptr;
+  const float* rstd = nullptr;
+  const float* gamma = nullptr;
+  const float* beta = nullptr;  // with y_out
+  const float* g_res = nullptr; // [M][D] residual gradient (optional)
+  float* g_out = nullptr;       // [M][D]
+  void* gy = nullptr;           // [M][D] optional
+  void* y_out = nullptr;        // [M][D] optional
+  float* ws = nullptr;          // [replicas][2D] dgamma || dbeta partials (+=)
+  int replicas = 16;
+  int tokens = 1;
+  const int64_t* rng = nullptr;
+  int site_drop = 0, site_dp = 0;
+  uint32_t thr_drop = 0, thr_dp = 0;
+  float sc_drop = 1.f, sc_dp = 1.f;
+};
+bool gemm_lnbwd_supported(int D, int K);
+// p_drop / p_dp: dropout and drop-path probabilities of gy (thresholds / scales set here)
+void gemm_lnbwd_launch(LnBwdParams p, int D, double p_drop, double p_dp, hipStream_t stream);
+
 // LayerNorm fold weights for the GEMMs that consume a LayerNorm (layernorm.hip)
 constexpr int FOLD_MAX = 32;  // GEMMs per fold launch (vit_small_200: 25 in one launch)
 struct FoldJob {

@@ -45,6 +45,11 @@ DGRAD_BF16 = True
 # operand the folded GEMM normalised in the forward -- instead of the fp32 residual
 # stream: 2 of its 18 bytes per element, and the fp32 block inputs are not saved
 LN_BWD_XB = True
+# the input-gradient GEMM feeding a LayerNorm backward (head, fc1, QKV) and that
+# LayerNorm backward as ONE launch (csrc/gemm_lnbwd.hip: full-row tiles, the LN
+# backward in the GEMM epilogue, the bf16 dl hand-off gone) where the shapes allow
+# (ops.lnbwd_fused_ok); False: linear_dgrad + layernorm_bwd (tests compare the two)
+FUSE_LN_BWD = True
 # GEMMs per LayerNorm-fold launch (csrc/kernels.h FOLD_MAX)
 FOLD_MAX = 32
 # LayerNorm fold (csrc/gemm.hip): every LayerNorm is folded into the GEMM that
@@ -480,11 +485,20 @@ class ViTProgram:
             return torch.empty(M, D, dtype=ACT_DTYPE, device=dtok.device) if fold else lo
         f32 = not DGRAD_BF16
         keep = []
-        dlf = ops.linear_dgrad(dtok, P.head_w, f32)
+
+        def dgrad_ln(dy, w, splits, x, *ln_args, **ln_kw):
+            """dy @ w, then the LayerNorm backward -- one launch when fused (keep: the
+            operand of the bf16 hand-off, if any, stays referenced)"""
+            if (FUSE_LN_BWD and x.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16
+                    and ops.lnbwd_fused_ok(x.shape[-1], w.shape[0])):
+                return ops.linear_dgrad_lnbwd(dy, w, x, *ln_args, **ln_kw)
+            dl = ops.linear_dgrad(dy, w, f32, splits)
+            keep.append(dl)
+            return ops.layernorm_bwd(dl, x, *ln_args, **ln_kw)
         lf = ln_out(S.lf)
         _, _, _, _, sf2, sd2 = block_sites(L - 1)
-        g, gy = ops.layernorm_bwd(dlf, S.xL, S.mf, S.rf, P.nw, None, G.nw, G.nb, N, rng, sf2, pd, sd2,
-                                  dpr[L - 1], True, ws(0), beta=P.nb if fold else None, y_out=lf if fold else None)
+        g, gy = dgrad_ln(dtok, P.head_w, 1, S.xL, S.mf, S.rf, P.nw, None, G.nw, G.nb, N, rng, sf2, pd, sd2,
+                         dpr[L - 1], True, ws(0), beta=P.nb if fold else None, y_out=lf if fold else None)
         wgrad(dtok, lf, G.head_w, G.head_b)
         for i in range(L - 1, -1, -1):
             x0, l1, m1, r1, qkv, o, lse, x1, l2, m2, r2, u, h = S.blocks[i]
@@ -492,27 +506,25 @@ class ViTProgram:
             sa, sp, sd1, sf1, _, _ = block_sites(i)
             wgrad(gy, h, bg.fc2_w, bg.fc2_b)
             du = ops.linear_dgrad_gelu(gy, bp.fc2_w, u, rng, sf1, pd)
-            dl2 = ops.linear_dgrad(du, bp.fc1_w, f32)
             k2 = 1 + 2 * (L - 1 - i)
             l2 = ln_out(l2)
-            g1, gy1 = ops.layernorm_bwd(dl2, x1, m2, r2, bp.n2w, g, bg.n2w, bg.n2b, N, rng, sp, pd, sd1, dpr[i],
-                                        True, ws(k2), beta=bp.n2b if fold else None, y_out=l2 if fold else None)
+            g1, gy1 = dgrad_ln(du, bp.fc1_w, 1, x1, m2, r2, bp.n2w, g, bg.n2w, bg.n2b, N, rng, sp, pd, sd1, dpr[i],
+                               True, ws(k2), beta=bp.n2b if fold else None, y_out=l2 if fold else None)
             wgrad(du, l2, bg.fc1_w, bg.fc1_b)
             wgrad(gy1, o, bg.proj_w, bg.proj_b)
             do = ops.linear_dgrad(gy1, bp.proj_w, False)
             dqkv = ops.attn_bwd(do, qkv, o, lse, c.scale, rng, sa, ad,
                                 keep=S.keeps[i] if len(S.keeps) == L else None)
             qs = QKV_DGRAD_SPLITS if 3 * D >= 768 else 1
-            dl1 = ops.linear_dgrad(dqkv, bp.qkv_w, f32, qs)
             l1 = ln_out(l1)
             fk = dict(beta=bp.n1b, y_out=l1) if fold else {}
             if i > 0:
                 _, _, _, _, psf2, psd2 = block_sites(i - 1)
-                g, gy = ops.layernorm_bwd(dl1, x0, m1, r1, bp.n1w, g1, bg.n1w, bg.n1b, N, rng, psf2, pd, psd2,
-                                          dpr[i - 1], True, ws(k2 + 1), **fk)
+                g, gy = dgrad_ln(dqkv, bp.qkv_w, qs, x0, m1, r1, bp.n1w, g1, bg.n1w, bg.n1b, N, rng, psf2, pd, psd2,
+                                 dpr[i - 1], True, ws(k2 + 1), **fk)
             else:
-                g, gy = ops.layernorm_bwd(dl1, x0, m1, r1, bp.n1w, g1, bg.n1w, bg.n1b, N, rng, 0, 0.0, 0, 0.0,
-                                          False, ws(k2 + 1), **fk)
+                g, gy = dgrad_ln(dqkv, bp.qkv_w, qs, x0, m1, r1, bp.n1w, g1, bg.n1w, bg.n1b, N, rng, 0, 0.0, 0, 0.0,
+                                 False, ws(k2 + 1), **fk)
             keep.append((gy1, du, dqkv, l1, l2))
             wgrad(dqkv, l1, bg.qkv_w, bg.qkv_b)
             if i == 0 and embed_with_block0:

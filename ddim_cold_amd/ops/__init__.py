@@ -391,6 +391,29 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dgamma, dbeta, N: int, rng, s
                              site_dp, p_dp, emit_gy)
 
 
+def lnbwd_fused_ok(D: int, K: int) -> bool:
+    """Shapes :func:`linear_dgrad_lnbwd` runs as one launch (D 256 / 384, K % 64 == 0)."""
+    return D in (256, 384) and K % 64 == 0 and K >= 64
+
+
+def linear_dgrad_lnbwd(dy, w, x, mean, rstd, gamma, g_res, dgamma, dbeta, N: int, rng, site_drop: int,
+                       p_drop: float, site_dp: int, p_dp: float, emit_gy: bool, ws: Optional[torch.Tensor] = None,
+                       beta=None, y_out=None):
+    """``layernorm_bwd(linear_dgrad(dy, w), x, ...)`` as ONE launch on the GPU
+    (csrc/gemm_lnbwd.hip: full-row tiles, the LayerNorm backward in the GEMM epilogue;
+    the input gradient of the LayerNorm output is never materialised).  ``x`` is the
+    bf16 LayerNorm input; same outputs and replica-workspace semantics as
+    :func:`layernorm_bwd` (the GEMM result enters the LayerNorm backward in fp32, not
+    rounded to bf16 first)."""
+    if _hip(x):
+        g_out, gy = _ops().linear_dgrad_lnbwd(dy, w, x, mean, rstd, gamma, g_res, dgamma, dbeta, N, rng, site_drop,
+                                              float(p_drop), site_dp, float(p_dp), bool(emit_gy), ws, beta, y_out)
+        return g_out, (gy if emit_gy else None)
+    dl = linear_dgrad(dy, w, True)
+    return layernorm_bwd(dl, x, mean, rstd, gamma, g_res, dgamma, dbeta, N, rng, site_drop, p_drop, site_dp, p_dp,
+                         emit_gy, ws, beta, y_out)
+
+
 def ln_fold_(ws, gammas, betas, biases, wfs, cs, bfs, tail=None):
     """LayerNorm fold weights for GEMMs that consume a LayerNorm (one launch on GPU):
     ``wf = bf16(gamma o W)``, ``c = rowsum(wf)``, ``bf = b + W beta``.

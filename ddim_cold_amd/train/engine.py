@@ -738,11 +738,30 @@ class TrainEngine:
         raise ValueError(f"unknown gradient-exchange layout {name!r} ([graph-]overlap-<blocks> or "
                          "[graph-]inline-1)")
 
+    def _comm_capturable(self) -> bool:
+        """Can the gradient collectives be captured into a hipGraph?  RCCL (our
+        communicator or ProcessGroupNCCL) and the device loopback pair can; gloo
+        stages CUDA tensors through the host and aborts the process inside a capture."""
+        if self.ncomm is not None:
+            return True
+        try:
+            return self.dist_on and dist.get_backend(self.pg) == "nccl"
+        except Exception:  # pragma: no cover
+            return False
+
     def apply_layout(self, layout):
         """Switch to a layout given by name or ``(name, bucket_blocks, embed_bucket,
-        inline[, ...])``; records it as :attr:`comm_choice`."""
+        inline[, ...])``; records it as :attr:`comm_choice`.  A captured (``graph-``)
+        layout on a non-capturable backend (gloo) runs as its event-split form."""
         L = self.layout_by_name(layout) if isinstance(layout, str) else tuple(layout)
-        self.set_comm_layout(L[1], L[2], L[3], captured=L[0].startswith("graph-"))
+        captured = L[0].startswith("graph-")
+        if captured and self.is_cuda and self.segmented and not self._comm_capturable():
+            import warnings
+            warnings.warn(f"layout {L[0]}: collectives of this backend cannot be captured in a hipGraph; "
+                          f"running {L[0][6:]} (event-split)")
+            L = (L[0][6:],) + tuple(L[1:])
+            captured = False
+        self.set_comm_layout(L[1], L[2], L[3], captured=captured)
         self.comm_choice = L[0]
         return L
 
@@ -833,6 +852,8 @@ class TrainEngine:
         """autotune_comm()'s default candidates: :attr:`COMM_LAYOUTS` plus the cost
         model's predicted best (fitted model if :meth:`probe_allreduce` ran)."""
         cands = list(self.COMM_LAYOUTS)
+        if self.is_cuda and self.segmented and not self._comm_capturable():
+            cands = [L_ for L_ in cands if not L_[0].startswith("graph-")]
         best = self.model_layouts()[0]
         if best[0] not in [L_[0] for L_ in cands]:
             cands.insert(1, best[:4])  # right after graph-inline-1 (the time budget runs in order)

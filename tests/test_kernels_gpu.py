@@ -77,6 +77,76 @@ def test_layernorm_bwd(emit, p):
         assert gy is None
 
 
+@pytest.mark.parametrize("M,K,D,N", [(2080, 384, 384, 65), (2080, 1152, 384, 65), (2080, 192, 384, 65),
+                                     (8224, 256, 256, 257), (8224, 768, 256, 257), (20032, 384, 384, 626),
+                                     (20032, 1152, 384, 626), (2085, 384, 384, 5)])
+@pytest.mark.parametrize("mode", ["full", "final", "no_gy"])
+def test_linear_dgrad_lnbwd_fused(M, K, D, N, mode):
+    """dy @ W and the LayerNorm backward in one launch (csrc/gemm_lnbwd.hip: full-row
+    tiles, a ragged last tile for M = 2,085) == linear_dgrad in fp32 then the fp32
+    LayerNorm-backward oracle; the replica workspace sums to dgamma / dbeta."""
+    dy = bf(M, K)
+    w = bf(K, D, scale=0.05)
+    x = (torch.randn(M, D, device=DEV) * 2 + 0.5).to(torch.bfloat16)
+    g = torch.randn(D, device=DEV)
+    b = torch.randn(D, device=DEV)
+    _, mu, rs = ref.layernorm_fwd(x.float(), g, b)
+    gres = None if mode == "final" else torch.randn(M, D, device=DEV)
+    emit = mode != "no_gy"
+    p, pdp = (0.1, 0.2) if emit else (0.0, 0.0)
+    r = rng()
+    ws = torch.zeros(ops.LN_REPLICAS, 2 * D, device=DEV)
+    y_out = torch.empty(M, D, dtype=torch.bfloat16, device=DEV)
+    dgz, dbz = torch.zeros(D, device=DEV), torch.zeros(D, device=DEV)
+    assert ops.lnbwd_fused_ok(D, K)
+    go, gy = ops.linear_dgrad_lnbwd(dy, w, x, mu, rs, g, gres, dgz, dbz, N, r, 7, p, 8, pdp, emit, ws, beta=b,
+                                    y_out=y_out)
+    dl = dy.float() @ w.float()
+    dg2, db2 = torch.zeros(D, device=DEV), torch.zeros(D, device=DEV)
+    gor, gyr = ref.layernorm_bwd(dl, x.float(), mu, rs, g, gres, dg2, db2, N, r, 7, p, 8, pdp, emit)
+    scale = gor.abs().max().item()
+    close(go, gor, 2e-3 * scale, 1e-3, "g_out")
+    ws_sum = ws.sum(0)
+    close(ws_sum[:D], dg2, 2e-3 * dg2.abs().max().item(), 1e-3, "dgamma")
+    close(ws_sum[D:], db2, 2e-3 * db2.abs().max().item(), 1e-3, "dbeta")
+    yr = (x.float() - mu[:, None]) * rs[:, None] * g + b
+    close(y_out, yr, 2e-2, 1e-2, "y_out")
+    if emit:
+        close(gy, gyr, 4e-3 * scale, 1e-2, "gy")
+        # the same dropout / drop-path masks: the oracle's dropped elements are zero here too
+        assert (gy.float()[gyr.float() == 0] == 0).all()
+    else:
+        assert gy is None
+    # without a workspace the partials land in dgamma / dbeta
+    dg3, db3 = torch.zeros(D, device=DEV), torch.zeros(D, device=DEV)
+    ops.linear_dgrad_lnbwd(dy, w, x, mu, rs, g, gres, dg3, db3, N, r, 7, p, 8, pdp, emit)
+    close(dg3, ws_sum[:D], 1e-4 * dg2.abs().max().item(), 1e-4, "dgamma (own ws)")
+
+
+def test_linear_dgrad_lnbwd_matches_two_launch_path():
+    """Fused == the two-launch path (bf16 dl hand-off) within the bf16 rounding of dl."""
+    M, K, D, N = 2080, 384, 384, 65
+    dy, w = bf(M, K), bf(K, D, scale=0.05)
+    x = torch.randn(M, D, device=DEV).to(torch.bfloat16)
+    g, b = torch.randn(D, device=DEV), torch.randn(D, device=DEV)
+    _, mu, rs = ref.layernorm_fwd(x.float(), g, b)
+    gres = torch.randn(M, D, device=DEV)
+    r = rng()
+    outs = []
+    for fused in (True, False):
+        ws = torch.zeros(ops.LN_REPLICAS, 2 * D, device=DEV)
+        z = torch.zeros(D, device=DEV)
+        if fused:
+            go, gy = ops.linear_dgrad_lnbwd(dy, w, x, mu, rs, g, gres, z, z.clone(), N, r, 7, 0.1, 8, 0.2, True, ws)
+        else:
+            dl = ops.linear_dgrad(dy, w, False)
+            go, gy = ops.layernorm_bwd(dl, x, mu, rs, g, gres, z, z.clone(), N, r, 7, 0.1, 8, 0.2, True, ws)
+        outs.append((go, gy, ws.sum(0)))
+    (a, b_, c), (a2, b2, c2) = outs
+    close(a, a2, 1e-2 * a2.abs().max().item(), 1e-2, "g_out")
+    close(c, c2, 1e-2 * c2.abs().max().item(), 1e-2, "dgamma||dbeta")
+
+
 # ------------------------------------------------------------------ GEMMs
 @pytest.mark.parametrize("B,N,H,D", [(32, 65, 12, 384), (4, 257, 4, 256), (3, 17, 2, 64 * 2)])
 def test_qkv_fwd(B, N, H, D):

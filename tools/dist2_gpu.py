@@ -57,7 +57,8 @@ def _worker(rank, world, port, out):
         eng.step(*bs[0])  # builds the static batch buffers the graphs read ...
         eng._restore_state(snap)  # ... and is undone
         times = eng.autotune_comm(steps=3, warm=1)
-        assert set(times) >= {L[0] for L in eng.COMM_LAYOUTS}, times
+        # gloo cannot be captured: the captured (graph-) layouts are not candidates
+        assert set(times) >= {L[0] for L in eng.COMM_LAYOUTS if not L[0].startswith("graph-")}, times
         losses = []
         for x, y, t in bs:
             eng.step(x, y, t)

@@ -1,0 +1,23 @@
+#!/bin/bash
+# round 5: fused input-gradient GEMM + LayerNorm backward -- numerics, then the step
+# time of both models (fused vs two-launch in the same box) and step tables
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out/r5c
+export PYTHONUNBUFFERED=1
+step() {
+  local name=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@"
+  local rc=$?
+  echo "$name rc=$rc"
+  case $rc in 0) return 0 ;; 1) [ -n "$SOFT" ] && return 0; echo "stopping after $name (rc=1)"; exit 1 ;; *) echo "stopping after $name (rc=$rc)"; exit $rc ;; esac
+}
+step pytest_lnbwd 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_kernels_gpu.py \
+  tests/test_model_gpu.py -k "lnbwd or fused_dgrad or program_fwd_bwd or autograd" > gpurun_out/r5c/pytest_lnbwd.log 2>&1
+SOFT=1 step pytest_dist 300 python -u -m pytest -x -q --timeout 250 --timeout-method thread tests/test_dist_gpu.py \
+  > gpurun_out/r5c/pytest_dist.log 2>&1
+step ab_tiny 300 python tools/ab_module_constant.py ddim_cold_amd.models.program FUSE_LN_BWD 1,0 2 -- \
+  --steps 300 --warmup 30 --no-sampler --no-vendor --no-gaussian > gpurun_out/r5c/ab_tiny.txt 2>&1
+step ab_small 400 python tools/ab_module_constant.py ddim_cold_amd.models.program FUSE_LN_BWD 1,0 2 -- \
+  --model vit_small_200 --steps 40 --warmup 8 --no-sampler --no-vendor --no-gaussian > gpurun_out/r5c/ab_small.txt 2>&1
+step prof_tiny 300 bash tools/gpu_prof_step.sh r5c/prof_tiny --steps 30 --warmup 10
+step prof_small 300 bash tools/gpu_prof_step.sh r5c/prof_small --model vit_small_200 --steps 20 --warmup 5

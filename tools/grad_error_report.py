@@ -66,37 +66,62 @@ def program_vs_ref_ops(name):
     report(f"{name} program vs reference ops", [("out", o1, o2)] + [(n, g1[n], g2[n]) for n in g1])
 
 
-def autograd_vs_fp32(name):
+def autograd_vs_fp32(name, depth=None, train=False, B=4, loss="square"):
+    """Fused autograd path (bf16 MFMA kernels, hand-written backward) vs the plain fp32
+    model's autograd (``forward_reference``), forward output and every gradient.
+    ``train``: train mode with every dropout / drop-path probability 0 (the training
+    kernels, no random masks)."""
     torch.manual_seed(0)
-    m = build_model(name).to(DEV).eval()
-    B = 4
-    img = torch.randn(B, 3, 64, 64, device=DEV)
+    kw = {} if depth is None else {"depth": depth}
+    if train:
+        kw.update(drop_rate=0.0, attn_drop_rate=0.0, drop_path_rate=0.0)
+    m = build_model(name, **kw).to(DEV).train(train)
+    H, W = m.img_size
+    img = torch.randn(B, 3, H, W, device=DEV).clamp(-1, 1)
+    tgt = torch.randn(B, 3, H, W, device=DEV).clamp(-1, 1)
     t = torch.randint(0, 2000, (B,), device=DEV)
+
+    def lossf(o):
+        return o.square().mean() if loss == "square" else torch.nn.functional.smooth_l1_loss(o, tgt)
     out = m(img, t)
-    out.square().mean().backward()
+    lossf(out).backward()
     g = {n: p.grad.clone() for n, p in m.named_parameters()}
     m.zero_grad()
     ref = m.forward_reference(img, t)
-    ref.square().mean().backward()
-    report(f"{name} autograd (bf16 MFMA) vs fp32 model", [("out", out.detach(), ref.detach())] +
+    lossf(ref).backward()
+    tag = f"{name}{'' if depth is None else f' depth {depth}'} {'train p=0' if train else 'eval'} {loss}"
+    report(f"{tag}: autograd (bf16 MFMA) vs fp32 model", [("out", out.detach(), ref.detach())] +
            [(n, g[n], p.grad) for n, p in m.named_parameters()])
 
 
-def sampler_vs_eager():
+def sampler_vs_eager(name="vit_tiny", k=20, N=64, depth=None):
     from ddim_cold_amd.bench.eager_sampler import eager_ddim_sample
     from ddim_cold_amd.diffusion.samplers import DDIMSampler
     torch.manual_seed(0)
-    m = build_model("vit_tiny").to(DEV).eval()
-    noise = torch.normal(0.0, 1.0, (64, 3, 64, 64), generator=torch.Generator().manual_seed(5))
-    fused = DDIMSampler(m, DEV, k=20).sample(64, noise=noise)
-    eager = eager_ddim_sample(m, DEV, 20, 64, noise=noise.to(DEV))
+    m = build_model(name, **({} if depth is None else {"depth": depth})).to(DEV).eval()
+    H, W = m.img_size
+    noise = torch.normal(0.0, 1.0, (N, 3, H, W), generator=torch.Generator().manual_seed(5))
+    fused = DDIMSampler(m, DEV, k=k).sample(N, noise=noise)
+    eager = eager_ddim_sample(m, DEV, k, N, noise=noise.to(DEV))
     d = (fused - eager).abs()
-    print(f"## sampler k=20 N=64 (100 steps) fused vs eager fp32: mean |d| {d.mean():.3e}  "
+    print(f"## {name} sampler k={k} N={N} ({2000 // k} steps) fused vs eager fp32: mean |d| {d.mean():.3e}  "
           f"max |d| {d.max():.3e}  frob {frob(fused, eager):.3e}  (images in [0,1])", flush=True)
 
 
 if __name__ == "__main__":
-    for nm in ("vit_tiny", "oxford_flower"):
-        program_vs_ref_ops(nm)
-        autograd_vs_fp32(nm)
-    sampler_vs_eager()
+    which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if which in ("all", "base"):
+        for nm in ("vit_tiny", "oxford_flower"):
+            program_vs_ref_ops(nm)
+            autograd_vs_fp32(nm)
+        sampler_vs_eager()
+    if which in ("all", "r5"):
+        # round 5: the fp32-oracle coverage of the non-yaml configs, train (p=0) and eval,
+        # the smooth-L1 training loss; the flash path (626 tokens) at depth 2-3
+        autograd_vs_fp32("oxford_flower", train=True, loss="smooth_l1")
+        autograd_vs_fp32("oxford_flower", train=False, loss="smooth_l1")
+        autograd_vs_fp32("vit_small_200", depth=3, train=True, B=2, loss="smooth_l1")
+        autograd_vs_fp32("vit_small_200", depth=3, train=False, B=2, loss="smooth_l1")
+        autograd_vs_fp32("vit_small_200", depth=2, train=True, B=2, loss="square")
+        sampler_vs_eager("oxford_flower", k=20, N=16)
+        sampler_vs_eager("vit_small_200", k=200, N=4, depth=3)
