@@ -109,6 +109,21 @@ void comm_all_reduce_(Tensor buf, int64_t h, int64_t op) {
                            get_comm(h), cur_stream()));
 }
 
+// Several in-place all-reduces as ONE RCCL group (one fused launch instead of one per
+// buffer): a gradient bucket whose range is split around the time-embedding rows no
+// sample can select is two ranges of one arena
+void comm_all_reduce_many_(std::vector<Tensor> bufs, int64_t h, int64_t op) {
+  TORCH_CHECK(!bufs.empty(), "all_reduce_many: no buffers");
+  for (const auto& b : bufs) check_buf(b);
+  const c10::DeviceGuard guard(bufs[0].device());
+  ncclComm_t c = get_comm(h);
+  hipStream_t s = cur_stream();
+  NCCL_CHECK(ncclGroupStart());
+  for (const auto& b : bufs)
+    NCCL_CHECK(ncclAllReduce(b.data_ptr(), b.data_ptr(), (size_t)b.numel(), nccl_dtype(b), nccl_op(op), c, s));
+  NCCL_CHECK(ncclGroupEnd());
+}
+
 // In-place SUM all-reduce of an fp32 range over a bf16 wire:
 // pack fp32 -> bf16 scratch, all-reduce bf16, unpack back into the fp32 range.
 void comm_all_reduce_bf16_wire_(Tensor buf, Tensor scratch, int64_t h) {
@@ -278,6 +293,7 @@ TORCH_LIBRARY_FRAGMENT(ddim_cold, m) {
   m.def("comm_unique_id() -> Tensor", &comm_unique_id);
   m.def("comm_init(Tensor uid, int world, int rank, int device) -> int", &comm_init);
   m.def("comm_all_reduce_(Tensor(a!) buf, int handle, int op=0) -> ()", &comm_all_reduce_);
+  m.def("comm_all_reduce_many_(Tensor(a!)[] bufs, int handle, int op=0) -> ()", &comm_all_reduce_many_);
   m.def("comm_all_reduce_bf16_wire_(Tensor(a!) buf, Tensor(b!) scratch, int handle) -> ()",
         &comm_all_reduce_bf16_wire_);
   m.def("comm_broadcast_(Tensor(a!) buf, int handle, int root=0) -> ()", &comm_broadcast_);

@@ -50,6 +50,9 @@ LN_BWD_XB = True
 # backward in the GEMM epilogue, the bf16 dl hand-off gone) where the shapes allow
 # (ops.lnbwd_fused_ok); False: linear_dgrad + layernorm_bwd (tests compare the two)
 FUSE_LN_BWD = True
+# ... only for reduction dims up to this (each workgroup streams the whole [K, D] weight
+# through its CU: ~70 GB/s per CU from L2, so K = 3D (the QKV input gradient) costs 3x)
+FUSE_LN_BWD_MAX_K = 1 << 30
 # GEMMs per LayerNorm-fold launch (csrc/kernels.h FOLD_MAX)
 FOLD_MAX = 32
 # LayerNorm fold (csrc/gemm.hip): every LayerNorm is folded into the GEMM that
@@ -490,7 +493,7 @@ class ViTProgram:
             """dy @ w, then the LayerNorm backward -- one launch when fused (keep: the
             operand of the bf16 hand-off, if any, stays referenced)"""
             if (FUSE_LN_BWD and x.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16
-                    and ops.lnbwd_fused_ok(x.shape[-1], w.shape[0])):
+                    and w.shape[0] <= FUSE_LN_BWD_MAX_K and ops.lnbwd_fused_ok(x.shape[-1], w.shape[0])):
                 return ops.linear_dgrad_lnbwd(dy, w, x, *ln_args, **ln_kw)
             dl = ops.linear_dgrad(dy, w, f32, splits)
             keep.append(dl)

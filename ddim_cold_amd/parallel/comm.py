@@ -187,6 +187,10 @@ class NativeComm:
     def all_reduce_(self, buf: torch.Tensor, op: int = SUM):
         torch.ops.ddim_cold.comm_all_reduce_(buf, self.handle, op)
 
+    def all_reduce_many_(self, bufs, op: int = SUM):
+        """In-place all-reduces of several buffers as ONE RCCL group (one launch)."""
+        torch.ops.ddim_cold.comm_all_reduce_many_(list(bufs), self.handle, op)
+
     def all_reduce_bf16_wire_(self, buf: torch.Tensor, scratch: torch.Tensor):
         """SUM all-reduce of an fp32 range over a bf16 wire (pack, reduce, unpack)."""
         torch.ops.ddim_cold.comm_all_reduce_bf16_wire_(buf, scratch, self.handle)

@@ -652,6 +652,13 @@ class TrainEngine:
         fake = os.environ.get("DDIM_COLD_FAKE_COMM") == "1"
 
         def reduce():
+            many = getattr(self.ncomm, "all_reduce_many_", None)
+            if many is not None and self.flat_gw is None and not fake and len(ranges) > 1:
+                # the bucket's ranges as one RCCL group: one launch
+                many([self.flat_g[a:b] for a, b in ranges])
+                if k == self.temb_bucket:
+                    self._temb_exchange()
+                return
             for a, b in ranges:
                 if fake:  # topology experiment at 1 rank: passes over the range stand in for the collective
                     self.flat_g[a:b].mul_(1.0)

@@ -74,6 +74,10 @@ if __name__ == "__main__":
         out = torch.empty_like(src)
         nc.all_gather_(out, src)
         assert torch.equal(out, src), "all_gather at 1 rank"
+    parts = [torch.randn(1001, device="cuda"), torch.randn(77, 3, device="cuda")]
+    want = [p.clone() for p in parts]
+    nc.all_reduce_many_(parts)  # one RCCL group over both buffers
+    assert all(torch.equal(p, w) for p, w in zip(parts, want)), "all_reduce_many at 1 rank"
     nc.destroy()
     cap, loss1, failed, ng1 = run("captured")
     seg, loss2, _, ng2 = run("segmented")

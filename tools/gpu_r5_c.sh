@@ -19,5 +19,9 @@ step ab_tiny 300 python tools/ab_module_constant.py ddim_cold_amd.models.program
   --steps 300 --warmup 30 --no-sampler --no-vendor --no-gaussian > gpurun_out/r5c/ab_tiny.txt 2>&1
 step ab_small 400 python tools/ab_module_constant.py ddim_cold_amd.models.program FUSE_LN_BWD 1,0 2 -- \
   --model vit_small_200 --steps 40 --warmup 8 --no-sampler --no-vendor --no-gaussian > gpurun_out/r5c/ab_small.txt 2>&1
+step ab_tiny_k 300 python tools/ab_module_constant.py ddim_cold_amd.models.program FUSE_LN_BWD_MAX_K 4096,512 2 -- \
+  --steps 300 --warmup 30 --no-sampler --no-vendor --no-gaussian > gpurun_out/r5c/ab_tiny_maxk.txt 2>&1
+step ab_small_k 400 python tools/ab_module_constant.py ddim_cold_amd.models.program FUSE_LN_BWD_MAX_K 4096,512 2 -- \
+  --model vit_small_200 --steps 40 --warmup 8 --no-sampler --no-vendor --no-gaussian > gpurun_out/r5c/ab_small_maxk.txt 2>&1
 step prof_tiny 300 bash tools/gpu_prof_step.sh r5c/prof_tiny --steps 30 --warmup 10
 step prof_small 300 bash tools/gpu_prof_step.sh r5c/prof_small --model vit_small_200 --steps 20 --warmup 5
