@@ -314,6 +314,53 @@ std::tuple<Tensor, Tensor> attn_fwd(Tensor qkv, double scale, Tensor rng, int64_
   return {o, lse};
 }
 
+// QKV projection (LayerNorm folded) + short-sequence attention forward in ONE launch
+// (attention.hip qkv_attn_short_kernel): the outputs of qkv_fwd(fold) then attn_fwd
+std::tuple<Tensor, Tensor, Tensor> qkv_attn_fwd(Tensor xb, Tensor wf, Tensor bf, Tensor c, Tensor st, double eps,
+                                                c10::optional<Tensor> mean_out, c10::optional<Tensor> rstd_out,
+                                                int64_t B, int64_t N, int64_t H, double scale, Tensor rng,
+                                                int64_t site, double p, c10::optional<Tensor> keep_out) {
+  CHECK_IN(xb, BF16); CHECK_IN(wf, BF16); CHECK_IN(bf, F32); CHECK_IN(c, F32); CHECK_IN(st, F32); check_rng(rng);
+  const c10::DeviceGuard guard(xb.device());
+  const int D = xb.size(-1), hd = D / H;
+  TORCH_CHECK(xb.numel() == B * N * D && D % H == 0, "qkv_attn: xb must be [B*N, D]");
+  TORCH_CHECK(wf.dim() == 2 && wf.size(0) == 3 * D && wf.size(1) == D && bf.numel() == 3 * D && c.numel() == 3 * D,
+              "qkv_attn: folded weight / bias / c shapes");
+  TORCH_CHECK(st.numel() == B * N * (D / 32) * 2, "qkv_attn: statistics slots must be [B*N, D/32, 2]");
+  TORCH_CHECK(qkv_attn_supported((int)N, hd, D), "qkv_attn: unsupported shape (N <= 128, hd 32 | 64, D % 128 == 0)");
+  TORCH_CHECK(p <= 0 || (int64_t)B * H * N * ((N + 3) & ~3) < ((int64_t)1 << 32),
+              "attention dropout: more than 2^32 mask elements");
+  QkvAttnParams q;
+  q.xb = xb.data_ptr();
+  q.wf = wf.data_ptr();
+  q.bf = bf.data_ptr<float>();
+  q.c = c.data_ptr<float>();
+  q.st = st.data_ptr<float>();
+  if (mean_out.has_value() && mean_out->defined()) {
+    TORCH_CHECK(rstd_out.has_value() && rstd_out->defined(), "mean_out needs rstd_out");
+    CHECK_IN((*mean_out), F32); CHECK_IN((*rstd_out), F32);
+    TORCH_CHECK(mean_out->numel() == B * N && rstd_out->numel() == B * N, "mean / rstd shapes");
+    q.mean_out = mean_out->data_ptr<float>();
+    q.rstd_out = rstd_out->data_ptr<float>();
+  }
+  auto qkv = at::empty({3, B, H, N, hd}, xb.options());
+  auto o = at::empty({B, N, D}, xb.options());
+  auto lse = at::empty({B, H, N}, xb.options().dtype(F32));
+  q.qkv = qkv.data_ptr();
+  q.out = o.data_ptr();
+  q.lse = lse.data_ptr<float>();
+  q.keep_bits = keep_ptr(keep_out, (int)B, (int)H, (int)N, hd);
+  q.B = (int)B; q.H = (int)H; q.N = (int)N; q.D = D;
+  q.eps = (float)eps;
+  q.scale = (float)scale;
+  q.rng = rng.data_ptr<int64_t>();
+  q.site = (int)site;
+  qkv_attn_launch(q, hd, p, cur_stream());
+  return {qkv, o, lse};
+}
+
+bool qkv_attn_supported_op(int64_t N, int64_t hd, int64_t D) { return qkv_attn_supported((int)N, (int)hd, (int)D); }
+
 Tensor linear_residual_fwd(Tensor a, Tensor w, Tensor b, Tensor x, int64_t N, Tensor rng, int64_t site_drop,
                            double p_drop, int64_t site_dp, double p_dp, c10::optional<Tensor> st_out, c10::optional<Tensor> xb_out) {
   CHECK_IN(a, BF16); CHECK_IN(w, BF16); CHECK_IN(b, F32); CHECK_IN(x, F32); check_rng(rng);
@@ -1128,6 +1175,10 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("wire_unpack(Tensor src, Tensor(a!) dst) -> ()");
   m.def("linear_wgrad_multi(Tensor[] dys, Tensor[] xs, Tensor(a!)[] dws, Tensor(b!)?[] dbs, bool store=False, "
         "Tensor(c!)? sq_parts=None, Tensor? arena=None, int lz_lo=0, int lz_hi=0) -> ()");
+  m.def("qkv_attn_fwd(Tensor xb, Tensor wf, Tensor bf, Tensor c, Tensor st, float eps, Tensor(a!)? mean_out, "
+        "Tensor(b!)? rstd_out, int B, int N, int H, float scale, Tensor rng, int site, float p, "
+        "Tensor(c!)? keep_out=None) -> (Tensor, Tensor, Tensor)");
+  m.def("qkv_attn_supported(int N, int hd, int D) -> bool", &qkv_attn_supported_op);
   m.def("linear_dgrad_lnbwd(Tensor dy, Tensor w, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor? g_res, "
         "Tensor(a!) dgamma, Tensor(b!) dbeta, int N, Tensor rng, int site_drop, float p_drop, int site_dp, "
         "float p_dp, bool emit_gy, Tensor(c!)? ws=None, Tensor? beta=None, Tensor(d!)? y_out=None) -> (Tensor, Tensor)");
@@ -1187,6 +1238,7 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("wire_unpack", &wire_unpack);
   m.impl("layernorm_bwd", &layernorm_bwd);
   m.impl("linear_dgrad_lnbwd", &linear_dgrad_lnbwd);
+  m.impl("qkv_attn_fwd", &qkv_attn_fwd);
   m.impl("replica_reduce_", &replica_reduce_);
   m.impl("ln_fold_", &ln_fold_);
   m.impl("attn_bwd", &attn_bwd);

@@ -139,6 +139,31 @@ struct LnBwdParams {
   float sc_drop = 1.f, sc_dp = 1.f;
 };
 bool gemm_lnbwd_supported(int D, int K);
+
+// the block's QKV Linear (LayerNorm folded) + the short-sequence attention forward in
+// one launch (attention.hip qkv_attn_short_kernel); outputs = ops.qkv_fwd(fold) then
+// ops.attn_fwd: qkv [3][B][H][N][hd], out [B*N][D], lse, keep words, mean / rstd
+struct QkvAttnParams {
+  const void* xb = nullptr;   // [B*N][D] LayerNorm input (bf16 copy)
+  const void* wf = nullptr;   // [3D][D] gamma-scaled QKV weight
+  const float* bf = nullptr;      // [3D] folded bias
+  const float* c = nullptr;       // [3D] row sums of wf
+  const float* st = nullptr;      // [B*N][D/32][2] {sum, sum^2} slots of x
+  float* mean_out = nullptr;      // [B*N] optional (saved for the LayerNorm backward)
+  float* rstd_out = nullptr;
+  void* qkv = nullptr;
+  void* out = nullptr;
+  float* lse = nullptr;
+  uint32_t* keep_bits = nullptr;
+  int B = 0, H = 0, N = 0, D = 0;
+  float eps = 1e-5f, invd = 0.f, scale = 1.f;
+  const int64_t* rng = nullptr;
+  int site = 0;
+  uint32_t thr = 0;
+  float dsc = 1.f;
+};
+bool qkv_attn_supported(int N, int hd, int D);
+void qkv_attn_launch(QkvAttnParams p, int hd, double drop_p, hipStream_t stream);
 // p_drop / p_dp: dropout and drop-path probabilities of gy (thresholds / scales set here)
 void gemm_lnbwd_launch(LnBwdParams p, int D, double p_drop, double p_dp, hipStream_t stream);
 

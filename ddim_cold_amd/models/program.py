@@ -53,6 +53,10 @@ FUSE_LN_BWD = True
 # ... only for reduction dims up to this (each workgroup streams the whole [K, D] weight
 # through its CU: ~70 GB/s per CU from L2, so K = 3D (the QKV input gradient) costs 3x)
 FUSE_LN_BWD_MAX_K = 1 << 30
+# short sequences (ViT-tiny: 65 tokens): the block's QKV projection and the attention
+# forward as ONE launch (ops.qkv_attn_fwd: each (sample, head) workgroup computes its
+# q / k / v and attends from LDS); False: qkv_fwd + attn_fwd (tests compare the two)
+FUSE_QKV_ATTN = True
 # GEMMs per LayerNorm-fold launch (csrc/kernels.h FOLD_MAX)
 FOLD_MAX = 32
 # LayerNorm fold (csrc/gemm.hip): every LayerNorm is folded into the GEMM that
@@ -387,9 +391,15 @@ class ViTProgram:
             x0, x0b = x, xb
             m1, r1 = stats()
             fold = (st[2 * i], bp.qkv_c, c.eps, m1, r1)
-            qkv = ops.qkv_fwd(xb, bp.qkv_wf, bp.qkv_bf, B, N, c.heads, fold=fold)
-            keep = ops.attn_keep_buffer(qkv, ad) if save and STORE_ATTN_KEEP else None
-            o, lse = ops.attn_fwd(qkv, c.scale, rng, sa, ad, keep_out=keep)
+            if FUSE_QKV_ATTN and xb.is_cuda and ops.qkv_attn_ok(N, D // c.heads, D):
+                keep = (ops.qkv_attn_keep_buffer(B, c.heads, N, D // c.heads, ad, dev)
+                        if save and STORE_ATTN_KEEP else None)
+                qkv, o, lse = ops.qkv_attn_fwd(xb, bp.qkv_wf, bp.qkv_bf, B, N, c.heads, fold, c.scale, rng, sa, ad,
+                                               keep_out=keep)
+            else:
+                qkv = ops.qkv_fwd(xb, bp.qkv_wf, bp.qkv_bf, B, N, c.heads, fold=fold)
+                keep = ops.attn_keep_buffer(qkv, ad) if save and STORE_ATTN_KEEP else None
+                o, lse = ops.attn_fwd(qkv, c.scale, rng, sa, ad, keep_out=keep)
             if save:
                 S.keeps.append(keep)
             o = o.view(M, D)

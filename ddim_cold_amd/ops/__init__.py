@@ -138,6 +138,35 @@ class gemm_tile:
         return False
 
 
+def qkv_attn_ok(N: int, hd: int, D: int) -> bool:
+    """Shapes :func:`qkv_attn_fwd` runs as one launch (the short-sequence attention path)."""
+    return 1 <= N <= 128 and hd in (32, 64) and D % 128 == 0 and D % hd == 0 and D // 32 <= 64
+
+
+def qkv_attn_keep_buffer(B: int, H: int, N: int, hd: int, p: float, device):
+    """The keep-flag buffer of :func:`qkv_attn_fwd` (see :func:`attn_keep_buffer`)."""
+    if p <= 0 or torch.device(device).type != "cuda":
+        return None
+    n = int(_ops().attn_keep_words(B, H, N, hd))
+    return torch.empty(n, dtype=torch.int32, device=device) if n > 0 else None
+
+
+def qkv_attn_fwd(xb, wf, bf, B: int, N: int, H: int, fold, scale: float, rng, site: int, p: float, keep_out=None):
+    """:func:`qkv_fwd` (LayerNorm folded: ``fold = (ln_st, ln_c, eps, mean_out,
+    rstd_out)``) followed by :func:`attn_fwd`, as ONE launch on the GPU for short
+    sequences (csrc/attention.hip qkv_attn_short_kernel: the head's q / k / v computed
+    by its attention workgroup, written for the backward and kept in LDS).  Returns
+    ``(qkv, o, lse)``, the same values (summation order aside) and the same dropout
+    keep flags as the two-launch path."""
+    st, c, eps, mean, rstd = _fold_args(fold)
+    if _hip(xb):
+        return _ops().qkv_attn_fwd(xb, wf, bf, c, st, float(eps), mean, rstd, B, N, H, float(scale), rng, site,
+                                   float(p), keep_out)
+    qkv = qkv_fwd(xb, wf, bf, B, N, H, fold=fold)
+    o, lse = attn_fwd(qkv, scale, rng, site, p)
+    return qkv, o, lse
+
+
 def attn_keep_buffer(qkv, p: float):
     """int32 buffer for the attention-dropout keep flags the forward stores for its
     backward (short sequences: one word per lane; long ones: one 64-bit word per

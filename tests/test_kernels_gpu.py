@@ -696,3 +696,50 @@ def test_cold_batch_and_q_sample():
     tt = torch.randint(0, 2000, (B,), device=DEV)
     close(ops.q_sample(x0, tt, eps, 2000), ref.q_sample(x0, tt, eps, 2000), 1e-5, 1e-5, "q_sample")
 
+
+
+@pytest.mark.parametrize("B,N,H,D,p", [(32, 65, 12, 384, 0.1), (64, 65, 12, 384, 0.0), (3, 17, 4, 256, 0.1),
+                                       (2, 100, 4, 256, 0.0), (5, 32, 12, 384, 0.1), (4, 128, 6, 384, 0.2)])
+def test_qkv_attn_fused_matches_two_launches(B, N, H, D, p):
+    """QKV projection (LayerNorm folded) + short attention in one launch == qkv_fwd(fold)
+    then attn_fwd: q / k / v, attention output, LSE, row mean / rstd within the GEMM's
+    summation-order noise, and the dropout keep words bit for bit."""
+    M, hd = B * N, D // H
+    assert ops.qkv_attn_ok(N, hd, D)
+    x = torch.randn(M, D, device=DEV) * 1.5 + 0.3
+    xb = x.to(torch.bfloat16)
+    st = torch.stack([x.view(M, D // 32, 32).sum(-1), (x * x).view(M, D // 32, 32).sum(-1)], -1).contiguous()
+    gamma, beta = torch.randn(D, device=DEV) * 0.5 + 1, torch.randn(D, device=DEV) * 0.1
+    w, bias = torch.randn(3 * D, D, device=DEV) * 0.05, torch.randn(3 * D, device=DEV) * 0.1
+    wf = (w * gamma).to(torch.bfloat16)
+    c = wf.float().sum(1)
+    bf_ = bias + w @ beta
+    r = rng()
+    scale = hd ** -0.5
+    outs = []
+    for fused in (True, False):
+        mean, rstd = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+        fold = (st, c, 1e-5, mean, rstd)
+        if fused:
+            keep = ops.qkv_attn_keep_buffer(B, H, N, hd, p, DEV)
+            qkv, o, lse = ops.qkv_attn_fwd(xb, wf, bf_, B, N, H, fold, scale, r, 9, p, keep_out=keep)
+        else:
+            qkv = ops.qkv_fwd(xb, wf, bf_, B, N, H, fold=fold)
+            keep = ops.attn_keep_buffer(qkv, p)
+            o, lse = ops.attn_fwd(qkv, scale, r, 9, p, keep_out=keep)
+        outs.append((qkv, o, lse, mean, rstd, keep))
+    (q1, o1, l1, m1, s1, k1), (q2, o2, l2, m2, s2, k2) = outs
+    close(q1, q2, 2e-2, 1e-2, "qkv")
+    close(o1, o2, 2e-2, 2e-2, "attention out")
+    close(l1, l2, 1e-2, 1e-3, "lse")
+    close(m1, m2, 1e-5, 1e-5, "mean")
+    close(s1, s2, 1e-5, 1e-4, "rstd")
+    if p > 0:
+        assert k1 is not None and torch.equal(k1, k2), "keep words"
+    else:
+        assert k1 is None
+    # and against the fp32 oracle of the two ops
+    qr = ref.qkv_fwd(xb, wf, bf_, B, N, H, st, c, 1e-5, None, None)
+    close(q1, qr, 3e-2, 2e-2, "qkv vs oracle")
+    orf, _ = ref.attn_fwd(q1, scale, r, 9, p)
+    close(o1, orf, 2e-2, 2e-2, "attention vs oracle")

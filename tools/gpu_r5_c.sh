@@ -12,7 +12,7 @@ step() {
   case $rc in 0) return 0 ;; 1) [ -n "$SOFT" ] && return 0; echo "stopping after $name (rc=1)"; exit 1 ;; *) echo "stopping after $name (rc=$rc)"; exit $rc ;; esac
 }
 step pytest_lnbwd 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_kernels_gpu.py \
-  tests/test_model_gpu.py -k "lnbwd or fused_dgrad or program_fwd_bwd or autograd" > gpurun_out/r5c/pytest_lnbwd.log 2>&1
+  tests/test_model_gpu.py -k "lnbwd or fused_dgrad or program_fwd_bwd or autograd or qkv_att" > gpurun_out/r5c/pytest_lnbwd.log 2>&1
 SOFT=1 step pytest_dist 300 python -u -m pytest -x -q --timeout 250 --timeout-method thread tests/test_dist_gpu.py \
   > gpurun_out/r5c/pytest_dist.log 2>&1
 step ab_tiny 300 python tools/ab_module_constant.py ddim_cold_amd.models.program FUSE_LN_BWD 1,0 2 -- \
@@ -23,5 +23,7 @@ step ab_tiny_k 300 python tools/ab_module_constant.py ddim_cold_amd.models.progr
   --steps 300 --warmup 30 --no-sampler --no-vendor --no-gaussian > gpurun_out/r5c/ab_tiny_maxk.txt 2>&1
 step ab_small_k 400 python tools/ab_module_constant.py ddim_cold_amd.models.program FUSE_LN_BWD_MAX_K 4096,512 2 -- \
   --model vit_small_200 --steps 40 --warmup 8 --no-sampler --no-vendor --no-gaussian > gpurun_out/r5c/ab_small_maxk.txt 2>&1
+step ab_tiny_qa 300 python tools/ab_module_constant.py ddim_cold_amd.models.program FUSE_QKV_ATTN 1,0 2 -- \
+  --steps 300 --warmup 30 --no-sampler --no-vendor --no-gaussian > gpurun_out/r5c/ab_tiny_qkvattn.txt 2>&1
 step prof_tiny 300 bash tools/gpu_prof_step.sh r5c/prof_tiny --steps 30 --warmup 10
 step prof_small 300 bash tools/gpu_prof_step.sh r5c/prof_small --model vit_small_200 --steps 20 --warmup 5
