@@ -222,10 +222,16 @@ struct KvStage {  // one 64-row K tile + one 64-row V tile, register-staged
 //     the result is the softmax.  After the first tile the (wave-uniform) branch
 //     that rescales o is almost never taken: the o *= alpha pass (an AGPR read +
 //     mul + write per accumulator element) and the alpha exp leave the loop.
+//   * dropout: st keeps the UNdropped probabilities (the row sum l is taken before
+//     dropout); dm[t][j] is the packed drop mask (drop_mask2) of the keys 16t+4g+2j,
+//     +1, AND-NOT-ed onto the packed bf16 pair by pack8_drop -- no per-element
+//     compare / select -- and dbits the tile's 16 drop flags of this lane (bit
+//     drop_bit(t, r), keep_store)
 template <int DT, bool DROP, bool MASK>
 __device__ __forceinline__ void flash_softmax_tile(f32x4 (&st)[4], f32x4 (&o)[DT], float& m_run, float& l_run,
                                                    int kv0, int N, int g, float sl2, uint32_t salt,
-                                                   uint32_t rowidx, uint32_t thr, uint32_t& kbits) {
+                                                   uint32_t rowidx, uint32_t thr2, uint32_t (&dm)[4][2],
+                                                   uint32_t& dbits) {
   float mt = -INFINITY;
 #pragma unroll
   for (int t = 0; t < 4; ++t)
@@ -247,45 +253,65 @@ __device__ __forceinline__ void flash_softmax_tile(f32x4 (&st)[4], f32x4 (&o)[DT
   }
   const float nm = -m_run;
   float ls = 0.f;
-  const uint32_t pg = DROP ? ((rowidx >> 1) + 2u * (uint32_t)g) * DROP_GOLDEN : 0u;  // rowidx even
+  const uint32_t pgs = DROP ? ((rowidx >> 1) + 2u * (uint32_t)g) * DROP_GOLDEN + salt : 0u;  // rowidx even
+  uint32_t db = 0u;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    bool kp[4] = {true, true, true, true};
-    if (DROP) dropout_keep4_pg(salt, pg + (uint32_t)(8 * t) * DROP_GOLDEN, thr, kp);
+    if (DROP) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        dm[t][j] = drop_mask2(drop_mix(pgs + (uint32_t)(8 * t + j) * DROP_GOLDEN), thr2);
+        db |= dm[t][j] & ((1u << (2 * t + j)) | (1u << (16 + 2 * t + j)));
+      }
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float pv = fexp2(fmaf(st[t][r], sl2, nm));
+      const float pv = fexp2(fmaf(st[t][r], sl2, nm));  // the keep scale 1/(1-p) goes into the final 1/l
       ls += pv;
-      if (DROP) pv = kp[r] ? pv : 0.f;  // the keep scale 1/(1-p) goes into the final 1/l
-      if (DROP) kbits |= (uint32_t)kp[r] << (4 * t + r);
       st[t][r] = pv;
     }
   }
+  if (DROP) dbits = (db & 0xFFu) | ((db >> 8) & 0xFF00u);
   ls += __shfl_xor(ls, 16, 64);
   ls += __shfl_xor(ls, 32, 64);
   l_run += ls;
 }
 
+// pack8 with the drop masks of flash_softmax_tile applied to the bf16 pairs (keys
+// 16ta+4g+{0,1}, {2,3}, then 16tb+4g+...)
+__device__ __forceinline__ bf16x8 pack8_drop(const f32x4& a, const f32x4& b, const uint32_t (&ma)[2],
+                                             const uint32_t (&mb)[2]) {
+  u32x4 w = __builtin_bit_cast(u32x4, pack8(a, b));
+  w[0] &= ~ma[0];
+  w[1] &= ~ma[1];
+  w[2] &= ~mb[0];
+  w[3] &= ~mb[1];
+  return __builtin_bit_cast(bf16x8, w);
+}
+
 // Stored attention-dropout masks of the long-sequence kernels: one 64-bit word per
 // (b, h, 64-key tile, query) = four 16-bit groups in the forward's lane layout: group g
 // (bits 16 g .. 16 g + 15 of the word, i.e. uint16 [((bh * ntiles + tile) * N + q) * 4 + g])
-// holds the keep flags of keys 16 t + 4 g + r at bit 4 t + r -- each forward lane stores
-// its own 16 flags (no cross-lane assembly; the 64 lanes of a wave-instruction write 128
-// contiguous bytes), the two backward kernels read them instead of re-hashing every mask
-// element (dQ: the forward's lane layout; dK/dV: the query tile's words staged in LDS,
-// one bit per lane's key at position keep_bitpos(key)).
-__device__ __forceinline__ void keep_store(uint32_t* __restrict__ keep, size_t word, uint32_t kbits, int g,
+// holds the DROP flags of keys 16 t + 4 g + r at bit drop_bit(t, r) -- each forward lane
+// stores its own 16 flags (no cross-lane assembly; the 64 lanes of a wave-instruction
+// write 128 contiguous bytes), the two backward kernels read them instead of re-hashing
+// every mask element (dQ: the forward's lane layout; dK/dV: the query tile's words staged
+// in LDS, one bit per lane's key at position keep_bitpos(key)).  The order within a group
+// is the forward's mask order: the low halves of its 8 pair hashes (r even) in bits 0-7,
+// the high halves (r odd) in bits 8-15.
+__device__ __forceinline__ constexpr int drop_bit(int t, int r) { return 8 * (r & 1) + 2 * t + (r >> 1); }
+__device__ __forceinline__ void keep_store(uint32_t* __restrict__ keep, size_t word, uint32_t dbits, int g,
                                            bool valid) {
-  if (valid) reinterpret_cast<uint16_t*>(keep)[word * 4 + g] = (uint16_t)kbits;
+  if (valid) reinterpret_cast<uint16_t*>(keep)[word * 4 + g] = (uint16_t)dbits;
 }
-// the 4 flags of keys 16t + 4g + r (r = 0..3) of a query from its tile word
+// the 4 keep flags of keys 16t + 4g + r (r = 0..3) of a query from its tile word
 __device__ __forceinline__ void keep_nibble(const u32x2& w, int t, int g, bool (&kp)[4]) {
-  const uint32_t h = (g < 2 ? w[0] : w[1]) >> (16 * (g & 1) + 4 * t);
+  const uint32_t h = (g < 2 ? w[0] : w[1]) >> (16 * (g & 1));
 #pragma unroll
-  for (int r = 0; r < 4; ++r) kp[r] = (h >> r) & 1u;
+  for (int r = 0; r < 4; ++r) kp[r] = !((h >> drop_bit(t, r)) & 1u);
 }
-// bit position of key k (0..63 within its tile) in the tile word
-__device__ __forceinline__ int keep_bitpos(int k) { return 16 * ((k >> 2) & 3) + 4 * (k >> 4) + (k & 3); }
+// bit position of key k (0..63 within its tile) in the tile word (a DROP flag)
+__device__ __forceinline__ int keep_bitpos(int k) { return 16 * ((k >> 2) & 3) + drop_bit(k >> 4, k & 3); }
 
 template <int HD, bool DROP>
 __global__ __launch_bounds__(256) void attn_fwd_flash2_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
@@ -303,6 +329,7 @@ __global__ __launch_bounds__(256) void attn_fwd_flash2_kernel(const bf16* __rest
   const int qbase = blockIdx.x * 128 + wave * 32;
   const float sl2 = scale * LOG2E;
   const uint32_t salt = DROP ? site_salt(rng, site) : 0u;
+  const uint32_t thr2 = (thr >> 1) * 0x10001u;  // thr / 2 in both 16-bit halves (drop_mask2)
 
   KvStage<HD> stg;
   stg.load(kb, vb, 0, N);
@@ -345,20 +372,23 @@ __global__ __launch_bounds__(256) void attn_fwd_flash2_kernel(const bf16* __rest
         st[1][t] = mfma16(kf, qf[1][s], st[1][t]);
       }
     }
+    uint32_t dm[2][4][2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      uint32_t kbits = 0u;
+      uint32_t dbits = 0u;
       flash_softmax_tile<C::DT, DROP, MASK>(st[u], o[u], m_run[u], l_run[u], kv0, N, g, sl2, salt,
-                                            rowidx0 + u * rowstep + kv0, thr, kbits);
+                                            rowidx0 + u * rowstep + kv0, thr2, dm[u], dbits);
       if (DROP && keep != nullptr) {
         const int q = qbase + 16 * u + li;
-        keep_store(keep, ((size_t)bh * ntiles + it) * N + q, kbits, g, q < N);
+        keep_store(keep, ((size_t)bh * ntiles + it) * N + q, dbits, g, q < N);
       }
     }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      const bf16x8 pb0 = pack8(st[0][2 * s2], st[0][2 * s2 + 1]);
-      const bf16x8 pb1 = pack8(st[1][2 * s2], st[1][2 * s2 + 1]);
+      const bf16x8 pb0 = DROP ? pack8_drop(st[0][2 * s2], st[0][2 * s2 + 1], dm[0][2 * s2], dm[0][2 * s2 + 1])
+                              : pack8(st[0][2 * s2], st[0][2 * s2 + 1]);
+      const bf16x8 pb1 = DROP ? pack8_drop(st[1][2 * s2], st[1][2 * s2 + 1], dm[1][2 * s2], dm[1][2 * s2 + 1])
+                              : pack8(st[1][2 * s2], st[1][2 * s2 + 1]);
 #pragma unroll
       for (int d = 0; d < C::DT; ++d) {
         const bf16x8 vf = frag_t<C::S>(Vl, 16 * d, s2, lane);
@@ -455,6 +485,7 @@ __global__ __launch_bounds__(640) void attn_fwd_resident_kernel(const bf16* __re
 #pragma unroll
     for (int s = 0; s < C::KS; ++s) qf[u][s] = frag_glb<HD>(qb, qbase + 16 * u + li, N, s, g);
   const uint32_t salt = DROP ? site_salt(rng, site) : 0u;
+  const uint32_t thr2 = (thr >> 1) * 0x10001u;  // thr / 2 in both 16-bit halves (drop_mask2)
   const float sl2 = scale * LOG2E;
   __syncthreads();
 
@@ -486,20 +517,23 @@ __global__ __launch_bounds__(640) void attn_fwd_resident_kernel(const bf16* __re
         st[1][t] = mfma16(kf, qf[1][s], st[1][t]);
       }
     }
+    uint32_t dm[2][4][2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      uint32_t kbits = 0u;
+      uint32_t dbits = 0u;
       flash_softmax_tile<C::DT, DROP, MASK>(st[u], o[u], m_run[u], l_run[u], kv0, N, g, sl2, salt,
-                                            rowidx0 + u * rowstep + kv0, thr, kbits);
+                                            rowidx0 + u * rowstep + kv0, thr2, dm[u], dbits);
       if (DROP && keep != nullptr) {
         const int q = qbase + 16 * u + li;
-        keep_store(keep, ((size_t)bh * ntiles + kv0 / 64) * N + q, kbits, g, q < N);
+        keep_store(keep, ((size_t)bh * ntiles + kv0 / 64) * N + q, dbits, g, q < N);
       }
     }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      const bf16x8 pb0 = pack8(st[0][2 * s2], st[0][2 * s2 + 1]);
-      const bf16x8 pb1 = pack8(st[1][2 * s2], st[1][2 * s2 + 1]);
+      const bf16x8 pb0 = DROP ? pack8_drop(st[0][2 * s2], st[0][2 * s2 + 1], dm[0][2 * s2], dm[0][2 * s2 + 1])
+                              : pack8(st[0][2 * s2], st[0][2 * s2 + 1]);
+      const bf16x8 pb1 = DROP ? pack8_drop(st[1][2 * s2], st[1][2 * s2 + 1], dm[1][2 * s2], dm[1][2 * s2 + 1])
+                              : pack8(st[1][2 * s2], st[1][2 * s2 + 1]);
 #pragma unroll
       for (int d = 0; d < C::DT; ++d) {
         const bf16x8 vf = frag_t<C::S>(Vc, 16 * d, s2, lane);
@@ -884,7 +918,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
           const int pos = keep_bitpos(kl & 63);
           const u32x4 w = *reinterpret_cast<const u32x4*>(&s_keep[buf][kl >> 6][pos >> 5][16 * t + 4 * g]);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) kp[r] = (w[r] >> (pos & 31)) & 1u;
+          for (int r = 0; r < 4; ++r) kp[r] = !((w[r] >> (pos & 31)) & 1u);  // stored DROP flags
         } else if (thr) {
           // a mask pair is two adjacent keys of one row, held by lanes li and li^1 --
           // each of the two hashes the pair of 2 of the 4 rows and they swap the results
@@ -895,7 +929,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
           const uint32_t ldhg = ldh * DROP_GOLDEN;
           uint32_t hw[2];
 #pragma unroll
-          for (int v = 0; v < 2; ++v) hw[v] = mix32((pb + (uint32_t)(16 * t + v) * ldhg) ^ salt);
+          for (int v = 0; v < 2; ++v) hw[v] = drop_mix(pb + (uint32_t)(16 * t + v) * ldhg + salt);
           const uint32_t p0 = (uint32_t)__shfl_xor((int)hw[0], 1, 64), p1 = (uint32_t)__shfl_xor((int)hw[1], 1, 64);
           const uint32_t hr[4] = {odd ? p0 : hw[0], odd ? p1 : hw[1], odd ? hw[0] : p0, odd ? hw[1] : p1};
 #pragma unroll

@@ -5,10 +5,10 @@
 //   A[row l&15][k 8(l>>4)+j] / B[k][col l&15]; C/D col = l&15,
 //   row = 4(l>>4)+reg).
 // * Counter-based dropout hash — bit-identical to
-//   ddim_cold_amd/ops/reference.py (keep_mask / site_salt).  Masks are never
-//   stored: forward and backward regenerate them from (seed, step, site, idx),
-//   and (seed, step) are read from device memory so graph replays draw fresh
-//   masks every step.
+//   ddim_cold_amd/ops/reference.py (keep_mask / site_salt).  Elementwise sites
+//   regenerate their masks in backward from (seed, step, site, idx) (the attention
+//   kernels store theirs as bits); (seed, step) are read from device memory so
+//   graph replays draw fresh masks every step.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -82,12 +82,31 @@ __device__ __forceinline__ uint32_t site_salt(const int64_t* rng, int site) {
   return site_salt_v((uint64_t)rng[0], (uint64_t)rng[1], site);
 }
 
-// Dropout masks (counter-based, regenerated in backward): element i of a site
-// keeps iff the 16-bit half (i & 1) of mix32(((i >> 1) * golden) ^ salt) is
-// >= thr, thr = round(p * 2^16).  One hash serves an aligned pair of elements
-// (v_mul_lo_u32 is quarter rate: the hash dominated the dropout cost).
+// Dropout masks (counter-based): element i of a site keeps iff the 16-bit half
+// (i & 1) of drop_mix((i >> 1) * golden + salt) is >= thr, thr = 2 round(p 2^15)
+// (even, so "half >= thr" is "(half >> 1) >= thr / 2": the attention forward tests
+// both halves of a hash at once with 16-bit packed ops).  One hash serves an aligned
+// pair of elements.
+//
+// drop_mix: xorshift-multiply rounds with 24-bit multipliers.  v_mul_u32_u24 is full
+// rate, v_mul_lo_u32 (lowbias32's 32-bit multiplies, mix32 above) quarter rate, and
+// the shifts by 16 fold into one SDWA xor each: 5 vector instructions instead of
+// ~13 issue cycles, in the flash-attention forward's VALU-bound softmax loop.  The
+// first multiply reads only the low 24 bits (the top byte enters through the first
+// xorshift), so this is not a bijection; the dropout statistics are what matter
+// (drop rate, pair / neighbour independence at p = 0.1 over 2^25 elements: within
+// sampling noise; tests/test_diffusion_data.py::test_drop_mix_statistics).
+constexpr uint32_t DROP_MUL1 = 0xED5AD5u, DROP_MUL2 = 0x2C1B3Du;  // 24-bit odd constants
+__host__ __device__ __forceinline__ uint32_t drop_mix(uint32_t x) {
+  x ^= x >> 16;
+  x = (x & 0xFFFFFFu) * DROP_MUL1;
+  x ^= x >> 16;
+  x = (x & 0xFFFFFFu) * DROP_MUL2;
+  x ^= x >> 16;
+  return x;
+}
 __device__ __forceinline__ uint32_t drop_hash(uint32_t salt, uint32_t pair) {
-  return mix32((pair * 0x9E3779B1u) ^ salt);
+  return drop_mix(pair * 0x9E3779B1u + salt);
 }
 
 __device__ __forceinline__ bool dropout_keep(uint32_t salt, uint32_t idx, uint32_t thresh) {
@@ -106,11 +125,11 @@ __device__ __forceinline__ void dropout_keep4(uint32_t salt, uint32_t idx, uint3
 
 // dropout_keep4 with the pair hash input precomputed: pg = (idx >> 1) * golden for an even
 // idx.  Consecutive tiles of one mask row differ by a constant number of pairs, so callers
-// hoist the multiply out of their tile loops and add a (constant-folded) offset: 2 of the
-// 3 v_mul_lo_u32 (quarter rate) per hash remain.  Same flags as dropout_keep4.
+// hoist the multiply (v_mul_lo_u32, quarter rate) out of their tile loops and add a
+// (constant-folded) offset.  Same flags as dropout_keep4.
 constexpr uint32_t DROP_GOLDEN = 0x9E3779B1u;
 __device__ __forceinline__ void dropout_keep4_pg(uint32_t salt, uint32_t pg, uint32_t thresh, bool (&k)[4]) {
-  const uint32_t h0 = mix32(pg ^ salt), h1 = mix32((pg + DROP_GOLDEN) ^ salt);
+  const uint32_t h0 = drop_mix(pg + salt), h1 = drop_mix(pg + DROP_GOLDEN + salt);
   k[0] = (h0 & 0xFFFFu) >= thresh;
   k[1] = (h0 >> 16) >= thresh;
   k[2] = (h1 & 0xFFFFu) >= thresh;
@@ -121,11 +140,22 @@ __device__ __forceinline__ void dropout_keep4_pg(uint32_t salt, uint32_t pg, uin
 // with the row stride padded to 4 (aligned pairs / quads within a row)
 __host__ __device__ __forceinline__ int attn_mask_ld(int N) { return (N + 3) & ~3; }
 
+// drop mask of both 16-bit halves of a pair hash: 0xFFFF in each half whose element
+// drops ((half >> 1) < thr / 2, i.e. half < thr for the even thr), 0 where it keeps --
+// three packed 16-bit ops for two elements; AND-NOT it onto the packed bf16 pair
+__device__ __forceinline__ uint32_t drop_mask2(uint32_t h, uint32_t thr_half2) {
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  typedef short i16x2 __attribute__((ext_vector_type(2)));
+  const u16x2 d = (__builtin_bit_cast(u16x2, h) >> (unsigned short)1) - __builtin_bit_cast(u16x2, thr_half2);
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(i16x2, d) >> (short)15);
+}
+
+// even threshold 2 round(p 2^15) (see drop_mix)
 inline uint32_t drop_threshold_host(double p) {
-  double v = p * 65536.0 + 0.5;
-  if (v >= 65536.0) return 65536u;  // drop everything
+  double v = p * 32768.0 + 0.5;
+  if (v >= 32768.0) return 65536u;  // drop everything
   if (v <= 0.0) return 0u;
-  return (uint32_t)v;
+  return 2u * (uint32_t)v;
 }
 
 // ----------------------------------------------------------------------------- reductions

@@ -48,15 +48,22 @@ LN_BWD_XB = True
 # the input-gradient GEMM feeding a LayerNorm backward (head, fc1, QKV) and that
 # LayerNorm backward as ONE launch (csrc/gemm_lnbwd.hip: full-row tiles, the LN
 # backward in the GEMM epilogue, the bf16 dl hand-off gone) where the shapes allow
-# (ops.lnbwd_fused_ok); False: linear_dgrad + layernorm_bwd (tests compare the two)
-FUSE_LN_BWD = True
-# ... only for reduction dims up to this (each workgroup streams the whole [K, D] weight
-# through its CU: ~70 GB/s per CU from L2, so K = 3D (the QKV input gradient) costs 3x)
+# (ops.lnbwd_fused_ok); False: linear_dgrad + layernorm_bwd (tests compare the two).
+# Measured SLOWER at every shape and off (profiles/fused_ln_qkv_r5_ab.txt): each
+# full-row workgroup streams the whole [K, D] weight through its CU (~70 GB/s per CU
+# from L2) and ViT-tiny has only M / 32 = 65 of them -- ViT-tiny 0.722 -> 0.858 ms/step
+# (fc1 input gradient + LN2 27.4 us vs 11.2 for the two launches), vit_small_200
+# 6.00 -> 6.63 ms; fusing only the head (K <= 512) still 0.720 -> 0.770
+FUSE_LN_BWD = False
+# ... only for reduction dims up to this
 FUSE_LN_BWD_MAX_K = 1 << 30
 # short sequences (ViT-tiny: 65 tokens): the block's QKV projection and the attention
 # forward as ONE launch (ops.qkv_attn_fwd: each (sample, head) workgroup computes its
-# q / k / v and attends from LDS); False: qkv_fwd + attn_fwd (tests compare the two)
-FUSE_QKV_ATTN = True
+# q / k / v and attends from LDS); False: qkv_fwd + attn_fwd (tests compare the two).
+# Measured slower and off: 14.7 us per block vs 6.8 + 5.8 for the two launches (the
+# per-head GEMM of 384 workgroups with register-staged operands is slower than the
+# 390-tile LDS-DMA GEMM; ViT-tiny 0.8533 vs 0.8604 ms/step with the fused LN on)
+FUSE_QKV_ATTN = False
 # GEMMs per LayerNorm-fold launch (csrc/kernels.h FOLD_MAX)
 FOLD_MAX = 32
 # LayerNorm fold (csrc/gemm.hip): every LayerNorm is folded into the GEMM that

@@ -60,9 +60,26 @@ def site_salt(rng: torch.Tensor, site: int) -> int:
     return mix32((b + _mul32(site & MASK32, SALT_C2)) & MASK32)
 
 
+DROP_MUL1 = 0xED5AD5
+DROP_MUL2 = 0x2C1B3D
+
+
+def drop_mix(x):
+    """Dropout pair hash (csrc/common.h ``drop_mix``): xorshift-multiply rounds with
+    24-bit multipliers (full-rate ``v_mul_u32_u24`` on gfx950)."""
+    x = x ^ (x >> 16)
+    x = ((x & 0xFFFFFF) * DROP_MUL1) & MASK32
+    x = x ^ (x >> 16)
+    x = ((x & 0xFFFFFF) * DROP_MUL2) & MASK32
+    x = x ^ (x >> 16)
+    return x
+
+
 def drop_threshold(p: float) -> int:
-    """Drop iff the element's 16-bit hash half < threshold; threshold = round(p * 2^16)."""
-    return min(int(p * 65536.0 + 0.5), 65536)
+    """Drop iff the element's 16-bit hash half < threshold; threshold = 2 round(p * 2^15)
+    (even: the attention forward compares the halves shifted right by one)."""
+    v = p * 32768.0 + 0.5
+    return 65536 if v >= 32768.0 else 2 * max(int(v), 0)
 
 
 def keep_mask(numel: int, rng: torch.Tensor, site: int, p: float, device=None, start: int = 0) -> torch.Tensor:
@@ -71,7 +88,7 @@ def keep_mask(numel: int, rng: torch.Tensor, site: int, p: float, device=None, s
     hash of pair i >> 1 (indices are 32-bit counters)."""
     salt = site_salt(rng, site)
     idx = torch.arange(start, start + numel, dtype=torch.int64, device=device) & MASK32
-    h = mix32(_mul32(idx >> 1, GOLDEN) ^ salt)
+    h = drop_mix((_mul32(idx >> 1, GOLDEN) + salt) & MASK32)
     half = torch.where((idx & 1) == 1, h >> 16, h & 0xFFFF)
     return half >= drop_threshold(p)
 

@@ -156,6 +156,23 @@ def test_counter_rng_advances():
     assert not torch.equal(a, ref.keep_mask(10000, torch.tensor([7, 1]), 5, 0.1))
 
 
+@pytest.mark.parametrize("p", [0.1, 0.5])
+def test_drop_mix_statistics(p):
+    """The 24-bit-multiplier dropout hash (csrc/common.h drop_mix): drop rate, the two
+    halves of one pair hash, neighbouring pairs and attention rows (stride ld) are
+    independent within sampling noise (2^21 elements, 3 sigma)."""
+    n = 1 << 21
+    for step in (0, 1, 12345):
+        k = ref.keep_mask(n, torch.tensor([20240521, step]), 3, p).float()
+        sig = (p * (1 - p) / n) ** 0.5
+        assert abs(1 - k.mean().item() - p) < 4 * sig
+        even, odd = k[0::2], k[1::2]
+        for a, b in ((even, odd), (odd[:-1], even[1:]), (k[:-640], k[640:]), (k[:-2], k[2:])):
+            c = torch.corrcoef(torch.stack([a, b]))[0, 1].item()
+            assert abs(c) < 4 / (a.numel() ** 0.5), c
+    assert ref.drop_threshold(0.1) == 6554 and ref.drop_threshold(1.0) == 65536 and ref.drop_threshold(0.0) == 0
+
+
 # ----------------------------------------------------------------------------- samplers (CPU reference path)
 @pytest.fixture(scope="module")
 def tiny():

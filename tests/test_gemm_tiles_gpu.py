@@ -34,7 +34,7 @@ def rng(seed=1234, step=5):
 def close(a, b, atol, rtol=0.0, name=""):
     a, b = a.float(), b.float()
     err = (a - b).abs()
-    bad = (err > atol + rtol * b.abs()).sum().item()
+    bad = (~(err <= atol + rtol * b.abs())).sum().item()  # NaN counts as a mismatch
     assert bad == 0, f"{name}: {bad} mismatches, max err {err.max().item():.3e}"
 
 

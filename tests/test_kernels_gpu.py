@@ -33,7 +33,7 @@ def close(a, b, atol, rtol=0.0, name=""):
     a, b = a.float(), b.float()
     err = (a - b).abs()
     tol = atol + rtol * b.abs()
-    bad = (err > tol).sum().item()
+    bad = (~(err <= tol)).sum().item()  # NaN counts as a mismatch
     assert bad == 0, f"{name}: {bad} mismatches, max err {err.max().item():.3e}"
 
 
@@ -114,7 +114,10 @@ def test_linear_dgrad_lnbwd_fused(M, K, D, N, mode):
     if emit:
         close(gy, gyr, 4e-3 * scale, 1e-2, "gy")
         # the same dropout / drop-path masks: the oracle's dropped elements are zero here too
-        assert (gy.float()[gyr.float() == 0] == 0).all()
+        # (not where the oracle's g_out itself cancelled to exactly 0: tools/debug_lnbwd.py
+        # found one such element, ours 2.4e-8, in 800k)
+        dropped = (gyr.float() == 0) & (gor.view(M, D) != 0)
+        assert (gy.float()[dropped] == 0).all()
     else:
         assert gy is None
     # without a workspace the partials land in dgamma / dbeta
@@ -722,10 +725,14 @@ def test_qkv_attn_fused_matches_two_launches(B, N, H, D, p):
         fold = (st, c, 1e-5, mean, rstd)
         if fused:
             keep = ops.qkv_attn_keep_buffer(B, H, N, hd, p, DEV)
+            if keep is not None:
+                keep.zero_()  # padded rows' words are not written: compare zeros there
             qkv, o, lse = ops.qkv_attn_fwd(xb, wf, bf_, B, N, H, fold, scale, r, 9, p, keep_out=keep)
         else:
             qkv = ops.qkv_fwd(xb, wf, bf_, B, N, H, fold=fold)
             keep = ops.attn_keep_buffer(qkv, p)
+            if keep is not None:
+                keep.zero_()
             o, lse = ops.attn_fwd(qkv, scale, r, 9, p, keep_out=keep)
         outs.append((qkv, o, lse, mean, rstd, keep))
     (q1, o1, l1, m1, s1, k1), (q2, o2, l2, m2, s2, k2) = outs

@@ -1,7 +1,10 @@
 #!/bin/bash
-# round 5: fused input-gradient GEMM + LayerNorm backward -- numerics, then the step
+# round 5: fused input-gradient GEMM + LayerNorm backward, fused QKV + short attention, the new
+# dropout hash -- numerics, then the step
 # time of both models (fused vs two-launch in the same box) and step tables
 cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out/r5d
+timeout -k 10 240 python -u tools/debug_lnbwd.py > gpurun_out/r5d/debug_lnbwd2.txt 2>&1 || exit $?
 mkdir -p gpurun_out/r5c
 export PYTHONUNBUFFERED=1
 step() {
@@ -11,7 +14,7 @@ step() {
   echo "$name rc=$rc"
   case $rc in 0) return 0 ;; 1) [ -n "$SOFT" ] && return 0; echo "stopping after $name (rc=1)"; exit 1 ;; *) echo "stopping after $name (rc=$rc)"; exit $rc ;; esac
 }
-step pytest_lnbwd 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_kernels_gpu.py \
+SOFT=1 step pytest_lnbwd 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_kernels_gpu.py \
   tests/test_model_gpu.py -k "lnbwd or fused_dgrad or program_fwd_bwd or autograd or qkv_att" > gpurun_out/r5c/pytest_lnbwd.log 2>&1
 SOFT=1 step pytest_dist 300 python -u -m pytest -x -q --timeout 250 --timeout-method thread tests/test_dist_gpu.py \
   > gpurun_out/r5c/pytest_dist.log 2>&1
@@ -27,3 +30,7 @@ step ab_tiny_qa 300 python tools/ab_module_constant.py ddim_cold_amd.models.prog
   --steps 300 --warmup 30 --no-sampler --no-vendor --no-gaussian > gpurun_out/r5c/ab_tiny_qkvattn.txt 2>&1
 step prof_tiny 300 bash tools/gpu_prof_step.sh r5c/prof_tiny --steps 30 --warmup 10
 step prof_small 300 bash tools/gpu_prof_step.sh r5c/prof_small --model vit_small_200 --steps 20 --warmup 5
+# dropout hash with 24-bit multipliers + packed drop masks (this tree) vs the previous build
+step ub_attn_new 200 python tools/ub_attn.py > gpurun_out/r5c/ub_attn_new.txt 2>&1
+step ub_attn_old 200 env DDIM_COLD_LIB=ablibs/_C_pre_dropmix.so python tools/ub_attn.py > gpurun_out/r5c/ub_attn_old.txt 2>&1
+BENCH_ARGS="--model vit_small_200 --steps 40 --warmup 8" REPS=2 NO_DIST=1 step ab_dropmix 600 bash tools/gpu_lib_ab.sh ablibs/_C_pre_dropmix.so > gpurun_out/r5c/ab_dropmix_small.txt 2>&1
