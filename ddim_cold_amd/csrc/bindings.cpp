@@ -284,6 +284,15 @@ Tensor qkv_fwd(Tensor a, Tensor w, Tensor b, int64_t B, int64_t N, int64_t H, c1
 // attention-dropout keep-flag words the short forward stores for the backward
 // (0: this shape takes the long-sequence kernels, which regenerate the masks)
 int64_t gemm_tile_override_op(int64_t cfg) { return gemm_set_tile_override((int)cfg); }
+// GEMM phase stamps (tools/ub_gemm_stamps.py): an int32 buffer, or None to stop
+void gemm_stamps_op(c10::optional<Tensor> buf) {
+  if (buf.has_value() && buf->defined()) {
+    TORCH_CHECK(buf->is_cuda() && buf->scalar_type() == at::kInt && buf->is_contiguous(), "gemm_stamps: int32 cuda");
+    gemm_set_stamps(reinterpret_cast<uint32_t*>(buf->data_ptr<int32_t>()));
+  } else {
+    gemm_set_stamps(nullptr);
+  }
+}
 
 int64_t attn_keep_words_op(int64_t B, int64_t H, int64_t N, int64_t hd) {
   return attn_keep_words((int)B, (int)H, (int)N, (int)hd);
@@ -1150,6 +1159,7 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("attn_fwd(Tensor qkv, float scale, Tensor rng, int site, float p, Tensor? keep_out=None) -> (Tensor, Tensor)");
   m.def("attn_keep_words(int B, int H, int N, int hd) -> int", &attn_keep_words_op);
   m.def("gemm_tile_override(int cfg) -> int", &gemm_tile_override_op);
+  m.def("gemm_stamps(Tensor? buf) -> ()", &gemm_stamps_op);
   m.def("linear_residual_fwd(Tensor a, Tensor w, Tensor b, Tensor x, int N, Tensor rng, int site_drop, "
         "float p_drop, int site_dp, float p_dp, Tensor(a!)? st_out=None, Tensor(b!)? xb_out=None) -> Tensor");
   m.def("linear_gelu_fwd(Tensor a, Tensor w, Tensor b, Tensor rng, int site, float p, Tensor? ln_st=None, "

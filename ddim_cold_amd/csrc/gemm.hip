@@ -227,6 +227,8 @@ __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int t
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int g = lane >> 4, li = lane & 15;
+  uint32_t st_t0 = 0, st_t1 = 0, st_t2 = 0;
+  if (p.stamps) st_t0 = stamp_now();
 
   OA oa;
   OB ob;
@@ -272,6 +274,7 @@ __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int t
       const int rem = min(S - 2, nk - 1 - kt);
       vm_wait_rem<LPT>(rem);
       raw_barrier();
+      if (p.stamps && kt == 0) st_t1 = stamp_now();
       if (kt + S - 1 < nk) {
         const int st = (kt + S - 1) % S;
         oa.issue(smem + st * STAGE, kt0 + kt + S - 1, wave);
@@ -342,6 +345,7 @@ __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int t
   };
   if (WG && do_db) mainloop(std::true_type{});
   else mainloop(std::false_type{});
+  if (p.stamps) st_t2 = stamp_now();
 
   float dbsq = 0.f;  // ACC with sq_parts: this lane's bias-gradient squares
   if (WG && do_db && li == 0) {
@@ -373,6 +377,16 @@ __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int t
 
   if (VEC) ep.finish(p, acc, li);
   else run_epilogue_scalar<EPI, FM, FN>(p, acc, m0 + wm * TM, n0 + wn * TN, g, li);
+  if (p.stamps) {
+    __syncthreads();  // the last wave's epilogue
+    if (threadIdx.x == 0) {
+      const uint32_t t3 = stamp_now();
+      uint32_t* o = p.stamps + (size_t)((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * GEMM_STAMP_WORDS;
+      o[0] = st_t0; o[1] = st_t1; o[2] = st_t2; o[3] = t3;
+      o[4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+      o[5] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    }
+  }
   if constexpr (EPI == EPI_ACC && VEC) {
     if (p.sq_parts) {  // the workgroup's grad-norm partial (fixed reduction order)
       __shared__ float sred[WM * WN];
@@ -661,8 +675,12 @@ template __global__ void gemm_wgrad_multi_kernel<128, BIG_WG_STAGES, 128, 4, 2>(
 // ============================================================================ host API
 using namespace dc;
 
+static std::atomic<uint32_t*> g_stamps{nullptr};
+uint32_t* gemm_set_stamps(uint32_t* buf) { return g_stamps.exchange(buf); }
+
 static GemmParams base_params(const GemmArgs& a) {
   GemmParams p{};
+  p.stamps = g_stamps.load(std::memory_order_relaxed);
   p.A = reinterpret_cast<const bf16*>(a.A);
   p.B = reinterpret_cast<const bf16*>(a.B);
   p.M = a.M; p.N = a.N; p.K = a.K;

@@ -83,7 +83,15 @@ struct GemmParams {
   int sq_slot;
   uint32_t tok_magic;  // floor(2^32 / tokens) (divmagic: row -> sample without a division)
   float ln_invd;       // 1 / K (LayerNorm fold consumer: D = K)
+  uint32_t* stamps;    // phase profiling (gemm_set_stamps): per workgroup GEMM_STAMP_WORDS words
 };
+
+// Phase stamps of the LDS-DMA GEMM (tools/ub_gemm_stamps.py): s_memrealtime (100 MHz)
+// at workgroup start, first operand stage ready, main loop done, epilogue done, plus
+// the HW_ID / XCC_ID registers (which CU ran it).  Thread 0 stores them with vector
+// stores; nullptr (the default) costs one uniform branch per phase.
+constexpr int GEMM_STAMP_WORDS = 6;
+__device__ __forceinline__ uint32_t stamp_now() { return (uint32_t)__builtin_amdgcn_s_memrealtime(); }
 
 
 // Epilogue in two phases: (1) every global load the epilogue needs (bias per

@@ -79,6 +79,9 @@ int gemm_nt_grid(int M, int N, int K);
 // force a GEMM tile config for every later launch (-1 = automatic choice; 0..5, see
 // gemm.hip "tile configs"); returns the previous setting.  Tests / micro-benchmarks.
 int gemm_set_tile_override(int cfg);
+// phase stamps of every later LDS-DMA GEMM launch (GEMM_STAMP_WORDS words per
+// workgroup, gemm_epi.h) into buf; nullptr turns them off.  Returns the previous buffer.
+uint32_t* gemm_set_stamps(uint32_t* buf);
 void gemm_dgrad(const GemmArgs& a, int epi, hipStream_t stream);
 void gemm_wgrad(const GemmArgs& a, int splits, hipStream_t stream);
 // every weight gradient of a step (n <= 32 problems) in one launch, unsplit (plain read-add-write)

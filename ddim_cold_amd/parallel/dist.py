@@ -80,7 +80,7 @@ def init_single(backend: Optional[str] = None, device_index: int = 0, timeout_s:
     if dist.is_initialized():
         return True
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", str(free_port()))
+    own_port = "MASTER_PORT" not in os.environ
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     kw = {}
@@ -88,7 +88,19 @@ def init_single(backend: Optional[str] = None, device_index: int = 0, timeout_s:
         graph_safe_nccl_env()
         torch.cuda.set_device(device_index)
         kw["device_id"] = torch.device("cuda", device_index)
-    dist.init_process_group(backend, rank=0, world_size=1, timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    # a port found free can be taken before the store binds it (other processes' RCCL
+    # bootstrap sockets are ephemeral too: seen once as EADDRINUSE in the GPU suite) --
+    # a port we picked ourselves is re-picked
+    for attempt in range(5):
+        if own_port:
+            os.environ["MASTER_PORT"] = str(free_port())
+        try:
+            dist.init_process_group(backend, rank=0, world_size=1, timeout=datetime.timedelta(seconds=timeout_s),
+                                    **kw)
+            return True
+        except Exception as e:  # torch.distributed.DistNetworkError
+            if not own_port or attempt == 4 or "EADDRINUSE" not in str(e) and "address already in use" not in str(e):
+                raise
     return True
 
 

@@ -331,7 +331,7 @@ def test_stepped_index_table_matches_explicit_rows(kind):
     torch.manual_seed(0)
     pool = synthetic_pool(40, seed=2, device="cuda")
     rows, A, B = 5, 2, 8
-    table = torch.randperm(40, device="cuda")[: rows * A * B].reshape(rows, A, B).contiguous()
+    table = torch.randint(0, 40, (rows, A, B), device="cuda")
     rng = torch.tensor([11, 3], dtype=torch.int64, device="cuda")
     ctr = torch.tensor([0, 7], dtype=torch.int64, device="cuda")  # step 7 -> row 2
     for j in range(A):
