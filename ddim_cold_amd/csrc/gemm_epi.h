@@ -91,6 +91,8 @@ struct GemmParams {
 // the HW_ID / XCC_ID registers (which CU ran it).  Thread 0 stores them with vector
 // stores; nullptr (the default) costs one uniform branch per phase.
 constexpr int GEMM_STAMP_WORDS = 6;
+
+static __device__ const int64_t kEpiNoRng[2] = {0, 0};  // rng words of GEMMs without dropout
 __device__ __forceinline__ uint32_t stamp_now() { return (uint32_t)__builtin_amdgcn_s_memrealtime(); }
 
 
@@ -609,11 +611,14 @@ struct VecEpi {
 
   __device__ __forceinline__ void prefetch(const GemmParams& p, int mb, int nb, int g, int li) {
     const int q = sharer(g, li), cs = csub(g, li), rs = rsub(g, li);
-    rng0 = rng1 = 0;
-    if (p.thr_drop || p.thr_dp) {
-      rng0 = p.rng[0];
-      rng1 = p.rng[1];
-    }
+    // uniform pointer select + constant-address-space loads -> scalar loads: a vector
+    // load under the dropout condition was waited for on the spot (vmcnt(0): the
+    // operand stages issued before it too -- tools/ub_gemm_stamps.py, first stage of
+    // the vit_small_200 GELU GEMM 2.7 us vs 1.8 without dropout)
+    const int64_t* rp = (p.thr_drop || p.thr_dp) ? p.rng : kEpiNoRng;
+    const auto* rs4 = (const __attribute__((address_space(4))) int64_t*)(uintptr_t)rp;
+    rng0 = rs4[0];
+    rng1 = rs4[1];
     const bool fold = FC && p.ln_st != nullptr;
     first_col = nb == 0 && q == 0;
     colbase = nb;

@@ -2,7 +2,7 @@
 stamps, ops gemm_stamps): start -> first operand stage ready -> main loop done ->
 epilogue done, per workgroup, plus which CU ran it.  Shapes: the vit_small_200 step
 (M = 20,032 token rows, D = 384) and the ViT-tiny step (M = 2,080).
-usage: python tools/ub_gemm_stamps.py [M (default 20032)]"""
+usage: python tools/ub_gemm_stamps.py [M (default 20032)] [tile configs, e.g. -1,4,5,3,1 (ops.gemm_tile)]"""
 import os
 import sys
 
@@ -44,16 +44,19 @@ cases = [
     ("dgrad fp32 K=1152", lambda: ops.linear_dgrad(dy3, w3, True)),
     ("plain bf16", lambda: ops.linear_fwd(a, w, b)),
 ]
-buf = torch.zeros(1 << 20, dtype=torch.int32, device=dev)
-for name, fn in cases:
-    for _ in range(3):
+TILES = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [-1]
+buf = torch.zeros(6 << 17, dtype=torch.int32, device=dev)
+for (name0, fn), tile in [(c, tl) for c in cases for tl in TILES]:
+    name = name0 + ("" if tile < 0 else f" [tile cfg {tile}]")
+    with ops.gemm_tile(tile):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        buf.zero_()
+        T.gemm_stamps(buf)
         fn()
-    torch.cuda.synchronize()
-    buf.zero_()
-    T.gemm_stamps(buf)
-    fn()
-    torch.cuda.synchronize()
-    T.gemm_stamps(None)
+        torch.cuda.synchronize()
+        T.gemm_stamps(None)
     s = buf.view(-1, 6)
     s = s[s[:, 3] != 0].to(torch.int64).cpu()
     if s.numel() == 0:
