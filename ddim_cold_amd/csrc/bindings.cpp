@@ -841,6 +841,69 @@ void wire_unpack(Tensor src, Tensor dst) {
   wire_unpack_launch(src.data_ptr(), dst.data_ptr<float>(), src.numel(), cur_stream());
 }
 
+// LayerNorm backward fused into the input-gradient GEMM that consumes its output
+// (gemm_lnpro.hip): the outputs of layernorm_bwd(dl, x, ..., emit_gy=True, ws) and of
+// linear_dgrad(gy, w) (u == None) or linear_dgrad_gelu(gy, w, u, rng, gsite, gp).
+// Returns (g_out, gy, out).
+std::tuple<Tensor, Tensor, Tensor> lnbwd_dgrad(Tensor dl, Tensor x, Tensor mean, Tensor rstd, Tensor gamma,
+                                               c10::optional<Tensor> g_res, int64_t N, Tensor rng, int64_t site_drop,
+                                               double p_drop, int64_t site_dp, double p_dp, Tensor ws,
+                                               c10::optional<Tensor> beta, c10::optional<Tensor> y_out, Tensor w,
+                                               c10::optional<Tensor> u, int64_t gsite, double gp) {
+  CHECK_IN(dl, BF16); CHECK_IN(x, BF16); CHECK_IN(w, BF16);
+  CHECK_IN(mean, F32); CHECK_IN(rstd, F32); CHECK_IN(gamma, F32); CHECK_IN(ws, F32);
+  check_rng(rng);
+  const c10::DeviceGuard guard(x.device());
+  const int D = x.size(-1), M = x.numel() / D;
+  TORCH_CHECK(w.dim() == 2 && w.size(0) == D, "lnbwd_dgrad: w must be [D, N] (nn.Linear weight with in-features D)");
+  const int Nw = w.size(1);
+  TORCH_CHECK(gemm_lnpro_supported(D, D, Nw), "lnbwd_dgrad: D 256 | 384, N % 64 == 0");
+  TORCH_CHECK(dl.numel() == x.numel() && mean.numel() == M && rstd.numel() == M && gamma.numel() == D && M % N == 0 &&
+                  ws.numel() == (int64_t)ln_replicas() * 2 * D && (int64_t)M * std::max(D, Nw) < ((int64_t)1 << 31),
+              "lnbwd_dgrad shapes");
+  LnProParams q;
+  q.dl = dl.data_ptr(); q.x = x.data_ptr();
+  q.mean = mean.data_ptr<float>(); q.rstd = rstd.data_ptr<float>(); q.gamma = gamma.data_ptr<float>();
+  if (g_res.has_value() && g_res->defined()) {
+    CHECK_IN((*g_res), F32);
+    TORCH_CHECK(g_res->numel() == x.numel(), "g_res shape");
+    q.g_res = g_res->data_ptr<float>();
+  }
+  if (y_out.has_value() && y_out->defined()) {
+    TORCH_CHECK(beta.has_value() && beta->defined(), "y_out needs beta");
+    CHECK_IN((*beta), F32); CHECK_IN((*y_out), BF16);
+    TORCH_CHECK(beta->numel() == D && y_out->numel() == x.numel(), "beta / y_out shapes");
+    q.beta = beta->data_ptr<float>();
+    q.y_out = y_out->data_ptr();
+  }
+  auto g_out = at::empty(x.sizes(), x.options().dtype(F32));
+  auto gy = at::empty({M, D}, x.options().dtype(BF16));
+  auto out = at::empty({M, Nw}, x.options().dtype(BF16));
+  q.g_out = g_out.data_ptr<float>();
+  q.gy = gy.data_ptr();
+  q.ws = ws.data_ptr<float>();
+  q.replicas = ln_replicas();
+  q.tokens = (int)N;
+  q.rng = rng.data_ptr<int64_t>();
+  q.site_drop = (int)site_drop;
+  q.site_dp = (int)site_dp;
+  GemmArgs g;
+  g.B = w.data_ptr();
+  g.M = M; g.N = Nw; g.K = D; g.lda = D; g.ldb = Nw;
+  g.C = out.data_ptr(); g.ldc = Nw;
+  const bool gelu = u.has_value() && u->defined();
+  if (gelu) {
+    CHECK_IN((*u), BF16);
+    TORCH_CHECK(u->numel() == (int64_t)M * Nw, "u shape");
+    g.aux = u->data_ptr();
+    g.rng = rng.data_ptr<int64_t>(); g.site_drop = (int)gsite; g.p_drop = gp;
+  }
+  gemm_lnpro_launch(g, gelu ? EPI_DGELU : EPI_BF16, q, p_drop, p_dp, cur_stream());
+  return {g_out, gy, out};
+}
+
+bool lnpro_supported_op(int64_t D, int64_t K, int64_t N) { return gemm_lnpro_supported((int)D, (int)K, (int)N); }
+
 std::tuple<Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma,
                                          c10::optional<Tensor> g_res, Tensor dgamma, Tensor dbeta, int64_t N,
                                          Tensor rng, int64_t site_drop, double p_drop, int64_t site_dp, double p_dp,
@@ -1180,6 +1243,10 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("img_to_tokgrad(Tensor dimg, int N, int patch) -> Tensor");
   m.def("linear_dgrad(Tensor dy, Tensor w, bool out_fp32, int splits=1) -> Tensor");
   m.def("linear_dgrad_gelu(Tensor dy, Tensor w, Tensor u, Tensor rng, int site, float p) -> Tensor");
+  m.def("lnbwd_dgrad(Tensor dl, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor? g_res, int N, Tensor rng, "
+        "int site_drop, float p_drop, int site_dp, float p_dp, Tensor(a!) ws, Tensor? beta, Tensor(b!)? y_out, "
+        "Tensor w, Tensor? u, int gsite, float gp) -> (Tensor, Tensor, Tensor)");
+  m.def("lnpro_supported(int D, int K, int N) -> bool", &lnpro_supported_op);
   m.def("linear_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, Tensor(b!)? db) -> ()");
   m.def("wire_pack(Tensor src, Tensor(a!) dst) -> ()");
   m.def("wire_unpack(Tensor src, Tensor(a!) dst) -> ()");
@@ -1239,6 +1306,7 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("img_to_tokgrad", &img_to_tokgrad);
   m.impl("linear_dgrad", &linear_dgrad);
   m.impl("linear_dgrad_gelu", &linear_dgrad_gelu);
+  m.impl("lnbwd_dgrad", &lnbwd_dgrad);
   m.impl("linear_wgrad", &linear_wgrad);
   m.impl("head_step_", &head_step_);
   m.impl("head_step_rows_", &head_step_rows_);

@@ -711,6 +711,11 @@ static GemmParams base_params(const GemmArgs& a) {
   return p;
 }
 
+GemmParams dc::gemm_params_from_args(const GemmArgs& a) {
+  GemmParams p = base_params(a);
+  return p;
+}
+
 static void check_vec(const GemmParams& p, int epi) {
   // the vector epilogue stores 4 consecutive output columns per lane
   if (epi != EPI_HEAD && (p.N % 4 != 0 || (epi == EPI_QKV && p.hd % 4 != 0) || (epi == EPI_EMBED && p.emb_dim % 4 != 0)))

@@ -86,6 +86,9 @@ struct GemmParams {
   uint32_t* stamps;    // phase profiling (gemm_set_stamps): per workgroup GEMM_STAMP_WORDS words
 };
 
+// the kernel parameter block of a host GemmArgs (gemm.hip base_params)
+GemmParams gemm_params_from_args(const GemmArgs& a);
+
 // Phase stamps of the LDS-DMA GEMM (tools/ub_gemm_stamps.py): s_memrealtime (100 MHz)
 // at workgroup start, first operand stage ready, main loop done, epilogue done, plus
 // the HW_ID / XCC_ID registers (which CU ran it).  Thread 0 stores them with vector

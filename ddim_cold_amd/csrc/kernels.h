@@ -118,6 +118,35 @@ void layernorm_bwd_launch(const void* dy, bool dy_bf16, const void* x, bool x_bf
                           double p_dp, int dy_parts, hipStream_t stream);
 int ln_replicas();
 
+// LayerNorm backward as the prologue of the input-gradient GEMM consuming its output
+// (gemm_lnpro.hip): the outputs of layernorm_bwd_launch (x and dl bf16) plus the GEMM
+// gy W with the consumer's epilogue (EPI_BF16 / EPI_DGELU); the GEMM's K is D.
+struct LnProParams {
+  const void* dl = nullptr;     // [M][D] gradient of the LayerNorm output (bf16)
+  const void* x = nullptr;      // [M][D] LayerNorm input (bf16 copy)
+  const float* mean = nullptr;
+  const float* rstd = nullptr;
+  const float* gamma = nullptr;
+  const float* beta = nullptr;  // with y_out
+  const float* g_res = nullptr; // [M][D] residual gradient (optional)
+  float* g_out = nullptr;       // [M][D]
+  void* gy = nullptr;           // [M][D] bf16
+  void* y_out = nullptr;        // [M][D] bf16, optional
+  float* ws = nullptr;          // [replicas][2D] dgamma || dbeta partials
+  int replicas = 1;
+  int tokens = 1;
+  const int64_t* rng = nullptr;
+  int site_drop = 0;
+  uint32_t thr_drop = 0;
+  float sc_drop = 1.f;
+  int site_dp = 0;
+  uint32_t thr_dp = 0;
+  float sc_dp = 1.f;
+};
+bool gemm_lnpro_supported(int D, int K, int N);
+// a: the consumer GEMM (B = W [D][N] nn.Linear weight, M, N, K = D, C, epilogue extras)
+void gemm_lnpro_launch(const GemmArgs& a, int epi, LnProParams q, double p_drop, double p_dp, hipStream_t stream);
+
 // input-gradient GEMM + LayerNorm backward in one launch (gemm_lnbwd.hip): the outputs
 // of linear_dgrad followed by layernorm_bwd_launch (x bf16, fp32 dl never materialised)
 struct LnBwdParams {

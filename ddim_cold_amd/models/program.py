@@ -64,6 +64,15 @@ FUSE_LN_BWD_MAX_K = 1 << 30
 # per-head GEMM of 384 workgroups with register-staged operands is slower than the
 # 390-tile LDS-DMA GEMM; ViT-tiny 0.8533 vs 0.8604 ms/step with the fused LN on)
 FUSE_QKV_ATTN = False
+# every LayerNorm backward whose gy feeds an input-gradient GEMM with K = D (the final
+# norm and norm1 of blocks > 0 -> the fc2 input gradient of the block below, norm2 ->
+# the proj input gradient) runs as the PROLOGUE of that GEMM (ops.lnbwd_dgrad,
+# csrc/gemm_lnpro.hip: each workgroup computes the LayerNorm backward of its 32-row
+# panel into LDS); False: layernorm_bwd + the GEMM (tests compare the two).  Needs the
+# single deferred weight-gradient launch (a queued job may name an LN output that only
+# the next block's launch writes)
+FUSE_LN_PRO = False
+FUSE_LN_PRO_ON_CPU = False  # tests: the same call sequence through the ops CPU fallbacks
 # GEMMs per LayerNorm-fold launch (csrc/kernels.h FOLD_MAX)
 FOLD_MAX = 32
 # LayerNorm fold (csrc/gemm.hip): every LayerNorm is folded into the GEMM that
@@ -484,6 +493,7 @@ class ViTProgram:
         def ws(k):
             return None if ln_ws is None else ln_ws[k]
         bucketed = wgrad is None and wgrad_flush is not None
+        user_wgrad = wgrad is not None
         if wgrad_sq is not None and (bucketed or wgrad is not None):
             raise ValueError("wgrad_sq needs the single deferred weight-gradient launch")
         jobs = []
@@ -515,37 +525,83 @@ class ViTProgram:
             dl = ops.linear_dgrad(dy, w, f32, splits)
             keep.append(dl)
             return ops.layernorm_bwd(dl, x, *ln_args, **ln_kw)
+        # LayerNorm backward as the prologue of the GEMM consuming gy (FUSE_LN_PRO)
+        on_cpu = FUSE_LN_PRO_ON_CPU and not dtok.is_cuda  # the ops' CPU fallbacks, any shape / dtype
+        pro = (FUSE_LN_PRO and (dtok.is_cuda or on_cpu) and not bucketed and not user_wgrad
+               and QKV_DGRAD_SPLITS == 1
+               and (on_cpu or (DGRAD_BF16 and S.xL.dtype == torch.bfloat16
+                               and all(ops.lnpro_ok(D, bp.fc2_w) and ops.lnpro_ok(D, bp.proj_w) for bp in P.blocks))))
+        pend = None  # (dl, x, ln args, ln kwargs) of a LayerNorm backward waiting for its consumer
+
+        def ln_then(dl_args, w, u=None, gsite=0, gp=0.0):
+            """the pending LayerNorm backward fused with its consumer GEMM: (g_out, gy, out);
+            without a replica workspace (no ln_ws) dgamma / dbeta are added directly"""
+            dl, x, la, (dgam, dbet) = dl_args
+            wsl = la[10]
+            if wsl is None:
+                wsl = torch.zeros(ops.LN_REPLICAS, 2 * D, device=dl.device)
+                la = la[:10] + (wsl,) + la[11:]
+            res = ops.lnbwd_dgrad(dl, x, *la, w=w, u=u, gsite=gsite, gp=gp)
+            if dl_args[2][10] is None:
+                with torch.no_grad():
+                    dgam.add_(wsl[:, :D].sum(0))
+                    dbet.add_(wsl[:, D:].sum(0))
+            return res
+
         lf = ln_out(S.lf)
         _, _, _, _, sf2, sd2 = block_sites(L - 1)
-        g, gy = dgrad_ln(dtok, P.head_w, 1, S.xL, S.mf, S.rf, P.nw, None, G.nw, G.nb, N, rng, sf2, pd, sd2,
-                         dpr[L - 1], True, ws(0), beta=P.nb if fold else None, y_out=lf if fold else None)
+        if pro:
+            dl = ops.linear_dgrad(dtok, P.head_w, False, 1)
+            keep.append(dl)
+            pend = (dl, S.xL, (S.mf, S.rf, P.nw, None, N, rng, sf2, pd, sd2, dpr[L - 1], ws(0),
+                               P.nb if fold else None, lf if fold else None), (G.nw, G.nb))
+        else:
+            g, gy = dgrad_ln(dtok, P.head_w, 1, S.xL, S.mf, S.rf, P.nw, None, G.nw, G.nb, N, rng, sf2, pd, sd2,
+                             dpr[L - 1], True, ws(0), beta=P.nb if fold else None, y_out=lf if fold else None)
         wgrad(dtok, lf, G.head_w, G.head_b)
         for i in range(L - 1, -1, -1):
             x0, l1, m1, r1, qkv, o, lse, x1, l2, m2, r2, u, h = S.blocks[i]
             bp, bg = P.blocks[i], G.blocks[i]
             sa, sp, sd1, sf1, _, _ = block_sites(i)
+            if pend is not None:
+                g, gy, du = ln_then(pend, bp.fc2_w, u, sf1, pd)
+                pend = None
+            else:
+                du = ops.linear_dgrad_gelu(gy, bp.fc2_w, u, rng, sf1, pd)
             wgrad(gy, h, bg.fc2_w, bg.fc2_b)
-            du = ops.linear_dgrad_gelu(gy, bp.fc2_w, u, rng, sf1, pd)
             k2 = 1 + 2 * (L - 1 - i)
             l2 = ln_out(l2)
-            g1, gy1 = dgrad_ln(du, bp.fc1_w, 1, x1, m2, r2, bp.n2w, g, bg.n2w, bg.n2b, N, rng, sp, pd, sd1, dpr[i],
-                               True, ws(k2), beta=bp.n2b if fold else None, y_out=l2 if fold else None)
+            if pro:
+                dl = ops.linear_dgrad(du, bp.fc1_w, False, 1)
+                keep.append(dl)
+                g1, gy1, do = ln_then((dl, x1, (m2, r2, bp.n2w, g, N, rng, sp, pd, sd1, dpr[i], ws(k2),
+                                                bp.n2b if fold else None, l2 if fold else None), (bg.n2w, bg.n2b)),
+                                      bp.proj_w)
+            else:
+                g1, gy1 = dgrad_ln(du, bp.fc1_w, 1, x1, m2, r2, bp.n2w, g, bg.n2w, bg.n2b, N, rng, sp, pd, sd1,
+                                   dpr[i], True, ws(k2), beta=bp.n2b if fold else None, y_out=l2 if fold else None)
+                do = ops.linear_dgrad(gy1, bp.proj_w, False)
             wgrad(du, l2, bg.fc1_w, bg.fc1_b)
             wgrad(gy1, o, bg.proj_w, bg.proj_b)
-            do = ops.linear_dgrad(gy1, bp.proj_w, False)
             dqkv = ops.attn_bwd(do, qkv, o, lse, c.scale, rng, sa, ad,
                                 keep=S.keeps[i] if len(S.keeps) == L else None)
             qs = QKV_DGRAD_SPLITS if 3 * D >= 768 else 1
             l1 = ln_out(l1)
             fk = dict(beta=bp.n1b, y_out=l1) if fold else {}
-            if i > 0:
+            if i > 0 and pro:
+                _, _, _, _, psf2, psd2 = block_sites(i - 1)
+                dl = ops.linear_dgrad(dqkv, bp.qkv_w, False, 1)
+                keep.append(dl)
+                pend = (dl, x0, (m1, r1, bp.n1w, g1, N, rng, psf2, pd, psd2, dpr[i - 1], ws(k2 + 1),
+                                 bp.n1b if fold else None, l1 if fold else None), (bg.n1w, bg.n1b))
+            elif i > 0:
                 _, _, _, _, psf2, psd2 = block_sites(i - 1)
                 g, gy = dgrad_ln(dqkv, bp.qkv_w, qs, x0, m1, r1, bp.n1w, g1, bg.n1w, bg.n1b, N, rng, psf2, pd, psd2,
                                  dpr[i - 1], True, ws(k2 + 1), **fk)
             else:
                 g, gy = dgrad_ln(dqkv, bp.qkv_w, qs, x0, m1, r1, bp.n1w, g1, bg.n1w, bg.n1b, N, rng, 0, 0.0, 0, 0.0,
                                  False, ws(k2 + 1), **fk)
-            keep.append((gy1, du, dqkv, l1, l2))
+            keep.append((gy1, du, dqkv, l1, l2, do))
             wgrad(dqkv, l1, bg.qkv_w, bg.qkv_b)
             if i == 0 and embed_with_block0:
                 gpatch = self._embed_backward(P, G, S, g, rng, pd, wgrad, ln_final)

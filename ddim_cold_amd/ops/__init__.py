@@ -420,6 +420,30 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dgamma, dbeta, N: int, rng, s
                              site_dp, p_dp, emit_gy)
 
 
+def lnpro_ok(D: int, w) -> bool:
+    """Shapes :func:`lnbwd_dgrad` runs as one launch: D 256 / 384 and the consumer's
+    nn.Linear weight ``w`` [out = D, in = N] with N % 64 == 0."""
+    return D in (256, 384) and w.dim() == 2 and w.shape[0] == D and w.shape[1] % 64 == 0
+
+
+def lnbwd_dgrad(dl, x, mean, rstd, gamma, g_res, N: int, rng, site_drop: int, p_drop: float, site_dp: int,
+                p_dp: float, ws, beta, y_out, w, u=None, gsite: int = 0, gp: float = 0.0):
+    """``g_out, gy = layernorm_bwd(dl, x, ..., emit_gy=True, ws)`` and the input-gradient
+    GEMM consuming gy -- ``linear_dgrad(gy, w)`` (``u`` None) or
+    ``linear_dgrad_gelu(gy, w, u, rng, gsite, gp)`` -- as ONE launch on the GPU
+    (csrc/gemm_lnpro.hip: each GEMM workgroup computes the LayerNorm backward of its row
+    panel into LDS).  ``dl`` and ``x`` bf16.  Returns ``(g_out, gy, out)``."""
+    if _hip(x):
+        return _ops().lnbwd_dgrad(dl, x, mean, rstd, gamma, g_res, N, rng, site_drop, float(p_drop), site_dp,
+                                  float(p_dp), ws, beta, y_out, w, u, gsite, float(gp))
+    D = x.shape[-1]
+    with torch.no_grad():  # an op, like the kernel: the replica views of ws take two in-place adds
+        g_out, gy = layernorm_bwd(dl, x, mean, rstd, gamma, g_res, ws[0, :D], ws[0, D:], N, rng, site_drop,
+                                  p_drop, site_dp, p_dp, True, ws, beta, y_out)
+        out = linear_dgrad(gy, w, False) if u is None else linear_dgrad_gelu(gy, w, u, rng, gsite, gp)
+    return g_out, gy, out
+
+
 def lnbwd_fused_ok(D: int, K: int) -> bool:
     """Shapes :func:`linear_dgrad_lnbwd` runs as one launch (D 256 / 384, K % 64 == 0)."""
     return D in (256, 384) and K % 64 == 0 and K >= 64

@@ -77,6 +77,43 @@ def test_layernorm_bwd(emit, p):
         assert gy is None
 
 
+@pytest.mark.parametrize("M,D,Nw,N", [(2080, 384, 384, 65), (20032, 384, 384, 626), (8224, 256, 256, 257),
+                                      (2085, 384, 384, 5), (2080, 384, 768, 65)])
+@pytest.mark.parametrize("mode", ["resid_gelu", "final_gelu", "resid_bf16", "nodrop_bf16"])
+def test_lnbwd_dgrad_prologue(M, D, Nw, N, mode):
+    """LayerNorm backward as the prologue of its consumer GEMM (csrc/gemm_lnpro.hip) ==
+    layernorm_bwd then linear_dgrad / linear_dgrad_gelu (two launches): g_out, gy, the
+    re-emitted LayerNorm output, the replica dgamma / dbeta and the GEMM output; a ragged
+    last row panel for M = 2,085."""
+    dl = bf(M, D)
+    x = (torch.randn(M, D, device=DEV) * 2 + 0.5).to(torch.bfloat16)
+    g, b = torch.randn(D, device=DEV), torch.randn(D, device=DEV)
+    _, mu, rs = ref.layernorm_fwd(x.float(), g, b)
+    gres = None if mode.startswith("final") else torch.randn(M, D, device=DEV)
+    p, pdp = (0.0, 0.0) if mode.startswith("nodrop") else (0.1, 0.2)
+    w = bf(D, Nw, scale=0.05)
+    u = bf(M, Nw) if mode.endswith("gelu") else None
+    r = rng()
+    outs = []
+    for fused in (True, False):
+        ws = torch.zeros(ops.LN_REPLICAS, 2 * D, device=DEV)
+        y = torch.empty(M, D, dtype=torch.bfloat16, device=DEV)
+        if fused:
+            go, gy, out = ops.lnbwd_dgrad(dl, x, mu, rs, g, gres, N, r, 7, p, 8, pdp, ws, b, y, w, u, 9, 0.1)
+        else:
+            go, gy = ops.layernorm_bwd(dl, x, mu, rs, g, gres, ws[0, :D], ws[0, D:], N, r, 7, p, 8, pdp, True, ws,
+                                       b, y)
+            out = ops.linear_dgrad(gy, w, False) if u is None else ops.linear_dgrad_gelu(gy, w, u, r, 9, 0.1)
+        outs.append((go, gy, out, y, ws.sum(0)))
+    (go1, gy1, o1, y1, w1), (go2, gy2, o2, y2, w2) = outs
+    scale = go2.abs().max().item()
+    close(go1, go2, 1e-5 * scale, 1e-5, "g_out")
+    close(gy1, gy2, 1e-2 * scale, 1e-2, "gy")
+    close(y1, y2, 1e-2, 1e-2, "LayerNorm output")
+    close(w1, w2, 1e-3 * w2.abs().max().item(), 1e-4, "dgamma || dbeta")
+    close(o1, o2, 2e-2 * o2.abs().max().item(), 2e-2, "GEMM output")
+
+
 @pytest.mark.parametrize("M,K,D,N", [(2080, 384, 384, 65), (2080, 1152, 384, 65), (2080, 192, 384, 65),
                                      (8224, 256, 256, 257), (8224, 768, 256, 257), (20032, 384, 384, 626),
                                      (20032, 1152, 384, 626), (2085, 384, 384, 5)])

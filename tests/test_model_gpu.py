@@ -169,6 +169,38 @@ def test_fused_dgrad_layernorm_backward_matches_two_launches(name, monkeypatch):
         assert _frob(g1[n], g2[n]) < PROG_FROB, (n, _frob(g1[n], g2[n]))
 
 
+@pytest.mark.parametrize("name", ["vit_tiny", "oxford_flower"])
+def test_layernorm_backward_prologue_matches_two_launches(name, monkeypatch):
+    """program.FUSE_LN_PRO (each LayerNorm backward inside the input-gradient GEMM that
+    consumes its gy) == layernorm_bwd + the GEMM, every gradient."""
+    from ddim_cold_amd.models import program
+    torch.manual_seed(0)
+    m = build_model(name).to(DEV).train()
+    prog = ViTProgram.from_model(m)
+    P = model_tensors(m)
+    B = 8
+    img = torch.randn(B, 3, 64, 64, device=DEV).clamp(-1, 1)
+    tgt = torch.randn_like(img).clamp(-1, 1)
+    t = torch.randint(0, 2000, (B,), device=DEV)
+    r = torch.tensor([77, 3], dtype=torch.int64, device=DEV)
+    with torch.no_grad():
+        out, S = prog.forward(P, img, t, r, True)
+        _, dtok = ops.smooth_l1_fwd_bwd(out, tgt, prog.cfg.tokens, prog.cfg.patch)
+    res = []
+    for fused in (True, False):
+        monkeypatch.setattr(program, "FUSE_LN_PRO", fused)
+        grads = {n: torch.zeros_like(p) for n, p in m.named_parameters()}
+        G = collect(grads, prog.cfg.depth, prog.cfg.dim)
+        with torch.no_grad():
+            prog.backward(P, G, S, dtok, r, True)
+        torch.cuda.synchronize()
+        res.append(grads)
+    g1, g2 = res
+    for n in g1:
+        assert _rel(g1[n], g2[n]) < PROG_MAXREL, (n, _rel(g1[n], g2[n]))
+        assert _frob(g1[n], g2[n]) < PROG_FROB, (n, _frob(g1[n], g2[n]))
+
+
 @pytest.mark.parametrize("training", [True, False])
 def test_fused_qkv_attention_forward_matches_two_launches(training, monkeypatch):
     """program.FUSE_QKV_ATTN (ViT-tiny: QKV + attention in one launch per block) == the
