@@ -57,6 +57,8 @@ __global__ __launch_bounds__(256) void gemm_lnpro_kernel(GemmParams p, LnProPara
   const int wm = wave / WN, wn = wave % WN;
   const int g = lane >> 4, li = lane & 15;
 
+  uint32_t st_t0 = 0, st_t1 = 0, st_t2 = 0;
+  if (p.stamps) st_t0 = stamp_now();
   // W stages first: they land while the LayerNorm prologue runs
   OB ob;
   ob.init(p.B, p.ldb, p.K, n0, wave, lane);
@@ -77,11 +79,16 @@ __global__ __launch_bounds__(256) void gemm_lnpro_kernel(GemmParams p, LnProPara
     // gamma / beta through LDS: loaded from global per chunk, the compiler hoisted all
     // of them (and the residual rows) to the top -- 343 VGPRs
     __shared__ __attribute__((aligned(16))) float lgam[D], lbet[D];
-    for (int i = threadIdx.x; i < D / 4; i += 256) {
-      reinterpret_cast<f32x4*>(lgam)[i] = reinterpret_cast<const f32x4*>(q.gamma)[i];
-      reinterpret_cast<f32x4*>(lbet)[i] = q.beta ? reinterpret_cast<const f32x4*>(q.beta)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    __syncthreads();
+    __shared__ __attribute__((aligned(16))) float lred[4][2 * D];  // dgamma || dbeta per wave
+    // staged behind the first pass's row loads (one memory round trip for both)
+    auto stage_gamma = [&]() {
+      for (int i = threadIdx.x; i < D / 4; i += 256) {
+        reinterpret_cast<f32x4*>(lgam)[i] = reinterpret_cast<const f32x4*>(q.gamma)[i];
+        reinterpret_cast<f32x4*>(lbet)[i] =
+            q.beta ? reinterpret_cast<const f32x4*>(q.beta)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      __syncthreads();
+    };
     const uint32_t salt_drop = q.thr_drop ? site_salt_v(rng0, rng1, q.site_drop) : 0u;
     const uint32_t salt_dp = q.thr_dp ? site_salt_v(rng0, rng1, q.site_dp) : 0u;
     auto unpack = [](const u32x4& w, float (&f)[8]) {
@@ -118,6 +125,7 @@ __global__ __launch_bounds__(256) void gemm_lnpro_kernel(GemmParams p, LnProPara
         gres[v][0] = *reinterpret_cast<const f32x4*>(grr + c);
         gres[v][1] = *reinterpret_cast<const f32x4*>(grr + c + 4);
       }
+      if (pass == 0) stage_gamma();
       // pass A: row sums of dxh and dxh x_hat (16 lanes), column partials
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -191,12 +199,12 @@ __global__ __launch_bounds__(256) void gemm_lnpro_kernel(GemmParams p, LnProPara
           }
         }
       }
-      asm volatile("" ::: "memory");  // keep the second pass's loads below the first's use
     }
     // dgamma / dbeta of the column-0 workgroups: the wave's 4 rows x 2 passes summed
-    // (lanes 16 apart), one atomic per column per wave into replica blockIdx % replicas
+    // (lanes 16 apart), the 4 waves through LDS, then ONE atomic per column per workgroup
+    // into replica blockIdx % replicas (one per column per wave: the waves' atomics on
+    // the same addresses serialised, ~8 us of the column-0 workgroups)
     if (col0) {
-      float* rep = q.ws + (size_t)(blockIdx.x % q.replicas) * 2 * D;
 #pragma unroll
       for (int v = 0; v < NV; ++v)
 #pragma unroll
@@ -208,13 +216,18 @@ __global__ __launch_bounds__(256) void gemm_lnpro_kernel(GemmParams p, LnProPara
           b2 += __shfl_xor(b2, 32, 64);
           if (lane < 16) {
             const int c = 8 * (sub + 16 * v) + k;
-            atomicAdd(rep + c, a);
-            atomicAdd(rep + D + c, b2);
+            lred[wave][c] = a;
+            lred[wave][D + c] = b2;
           }
         }
+      __syncthreads();
+      float* rep = q.ws + (size_t)(blockIdx.x % q.replicas) * 2 * D;
+      for (int c = threadIdx.x; c < 2 * D; c += 256)
+        atomicAdd(rep + c, (lred[0][c] + lred[1][c]) + (lred[2][c] + lred[3][c]));
     }
   }
   __syncthreads();  // the A panel is complete
+  if (p.stamps) st_t1 = stamp_now();
 
   // ---------------------------------------------------------------- main loop (W only)
   f32x4 acc[FM][FN];
@@ -247,7 +260,17 @@ __global__ __launch_bounds__(256) void gemm_lnpro_kernel(GemmParams p, LnProPara
         for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
     }
   }
+  if (p.stamps) st_t2 = stamp_now();
   ep.finish(p, acc, li);
+  if (p.stamps) {  // same layout as gemm_dma_body: start, prologue done, main loop done, end
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t* o = p.stamps + (size_t)blockIdx.x * GEMM_STAMP_WORDS;
+      o[0] = st_t0; o[1] = st_t1; o[2] = st_t2; o[3] = stamp_now();
+      o[4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+      o[5] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+    }
+  }
 }
 
 template <int D, int EPI>

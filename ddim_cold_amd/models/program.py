@@ -70,7 +70,11 @@ FUSE_QKV_ATTN = False
 # csrc/gemm_lnpro.hip: each workgroup computes the LayerNorm backward of its 32-row
 # panel into LDS); False: layernorm_bwd + the GEMM (tests compare the two).  Needs the
 # single deferred weight-gradient launch (a queued job may name an LN output that only
-# the next block's launch writes)
+# the next block's launch writes).  Measured slower and off (profiles/ln_prologue_r5.md):
+# every one of the N/64 column workgroups re-reads its 32 rows of dl, x and the fp32
+# residual gradient (6x the row bytes through each CU's ~70 GB/s ingest): ~13.7 us per
+# fused launch vs 5.7 + 6.5 for the two (ViT-tiny 0.727 -> 0.95 ms/step before the
+# dgamma / dbeta and staging fixes, still a loss after them)
 FUSE_LN_PRO = False
 FUSE_LN_PRO_ON_CPU = False  # tests: the same call sequence through the ops CPU fallbacks
 # GEMMs per LayerNorm-fold launch (csrc/kernels.h FOLD_MAX)
