@@ -227,8 +227,10 @@ __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int t
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int g = lane >> 4, li = lane & 15;
+#ifdef DDIM_COLD_GEMM_STAMPS
   uint32_t st_t0 = 0, st_t1 = 0, st_t2 = 0;
   if (p.stamps) st_t0 = stamp_now();
+#endif
 
   OA oa;
   OB ob;
@@ -274,7 +276,9 @@ __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int t
       const int rem = min(S - 2, nk - 1 - kt);
       vm_wait_rem<LPT>(rem);
       raw_barrier();
+#ifdef DDIM_COLD_GEMM_STAMPS
       if (p.stamps && kt == 0) st_t1 = stamp_now();
+#endif
       if (kt + S - 1 < nk) {
         const int st = (kt + S - 1) % S;
         oa.issue(smem + st * STAGE, kt0 + kt + S - 1, wave);
@@ -345,7 +349,9 @@ __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int t
   };
   if (WG && do_db) mainloop(std::true_type{});
   else mainloop(std::false_type{});
+#ifdef DDIM_COLD_GEMM_STAMPS
   if (p.stamps) st_t2 = stamp_now();
+#endif
 
   float dbsq = 0.f;  // ACC with sq_parts: this lane's bias-gradient squares
   if (WG && do_db && li == 0) {
@@ -377,6 +383,7 @@ __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int t
 
   if (VEC) ep.finish(p, acc, li);
   else run_epilogue_scalar<EPI, FM, FN>(p, acc, m0 + wm * TM, n0 + wn * TN, g, li);
+#ifdef DDIM_COLD_GEMM_STAMPS
   if (p.stamps) {
     __syncthreads();  // the last wave's epilogue
     if (threadIdx.x == 0) {
@@ -387,6 +394,7 @@ __device__ __forceinline__ void gemm_dma_body(const GemmParams& p, int tm, int t
       o[5] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
     }
   }
+#endif
   if constexpr (EPI == EPI_ACC && VEC) {
     if (p.sq_parts) {  // the workgroup's grad-norm partial (fixed reduction order)
       __shared__ float sred[WM * WN];

@@ -92,7 +92,9 @@ GemmParams gemm_params_from_args(const GemmArgs& a);
 // Phase stamps of the LDS-DMA GEMM (tools/ub_gemm_stamps.py): s_memrealtime (100 MHz)
 // at workgroup start, first operand stage ready, main loop done, epilogue done, plus
 // the HW_ID / XCC_ID registers (which CU ran it).  Thread 0 stores them with vector
-// stores; nullptr (the default) costs one uniform branch per phase.
+// stores.  Compiled only with -DDDIM_COLD_GEMM_STAMPS (DDIM_COLD_HIPFLAGS at build
+// time): even untaken, the stamp branches cost the ViT-tiny step 1.5-2 % in a same-box
+// A/B (profiles/stamps_cost_r5.txt) -- they changed the main loop's code.
 constexpr int GEMM_STAMP_WORDS = 6;
 
 static __device__ const int64_t kEpiNoRng[2] = {0, 0};  // rng words of GEMMs without dropout

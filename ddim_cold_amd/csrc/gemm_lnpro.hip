@@ -57,8 +57,10 @@ __global__ __launch_bounds__(256) void gemm_lnpro_kernel(GemmParams p, LnProPara
   const int wm = wave / WN, wn = wave % WN;
   const int g = lane >> 4, li = lane & 15;
 
+#ifdef DDIM_COLD_GEMM_STAMPS
   uint32_t st_t0 = 0, st_t1 = 0, st_t2 = 0;
   if (p.stamps) st_t0 = stamp_now();
+#endif
   // W stages first: they land while the LayerNorm prologue runs
   OB ob;
   ob.init(p.B, p.ldb, p.K, n0, wave, lane);
@@ -227,7 +229,9 @@ __global__ __launch_bounds__(256) void gemm_lnpro_kernel(GemmParams p, LnProPara
     }
   }
   __syncthreads();  // the A panel is complete
+#ifdef DDIM_COLD_GEMM_STAMPS
   if (p.stamps) st_t1 = stamp_now();
+#endif
 
   // ---------------------------------------------------------------- main loop (W only)
   f32x4 acc[FM][FN];
@@ -260,8 +264,11 @@ __global__ __launch_bounds__(256) void gemm_lnpro_kernel(GemmParams p, LnProPara
         for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
     }
   }
+#ifdef DDIM_COLD_GEMM_STAMPS
   if (p.stamps) st_t2 = stamp_now();
+#endif
   ep.finish(p, acc, li);
+#ifdef DDIM_COLD_GEMM_STAMPS
   if (p.stamps) {  // same layout as gemm_dma_body: start, prologue done, main loop done, end
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -271,6 +278,7 @@ __global__ __launch_bounds__(256) void gemm_lnpro_kernel(GemmParams p, LnProPara
       o[5] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
     }
   }
+#endif
 }
 
 template <int D, int EPI>

@@ -2,7 +2,9 @@
 stamps, ops gemm_stamps): start -> first operand stage ready -> main loop done ->
 epilogue done, per workgroup, plus which CU ran it.  Shapes: the vit_small_200 step
 (M = 20,032 token rows, D = 384) and the ViT-tiny step (M = 2,080).
-usage: python tools/ub_gemm_stamps.py [M (default 20032)] [tile configs, e.g. -1,4,5,3,1 (ops.gemm_tile)]"""
+usage: python tools/ub_gemm_stamps.py [M (default 20032)] [tile configs, e.g. -1,4,5,3,1 (ops.gemm_tile)]
+Needs a stamps build of the extension (the stamp code costs the production step ~1.5 %):
+  DDIM_COLD_HIPFLAGS=-DDDIM_COLD_GEMM_STAMPS python -m ddim_cold_amd.build --force"""
 import os
 import sys
 
@@ -73,7 +75,8 @@ for (name0, fn), tile in [(c, tl) for c in cases for tl in TILES]:
     s = buf.view(-1, 6)
     s = s[s[:, 3] != 0].to(torch.int64).cpu()
     if s.numel() == 0:
-        print(name, ": no stamps (not an LDS-DMA launch)")
+        print(name, ": no stamps (not an LDS-DMA launch, or the extension was built without "
+              "-DDDIM_COLD_GEMM_STAMPS)")
         continue
     t0 = s[:, 0].min()
     st0, st1, st2, st3 = ((s[:, i] - t0).float() * 0.01 for i in range(4))  # 100 MHz -> us
