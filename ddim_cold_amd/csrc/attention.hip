@@ -39,6 +39,27 @@ struct AC {
   static constexpr int CPR = HD / 8;      // 16-B chunks per row
 };
 
+// Block coordinates of the long-sequence kernels (grid = query / key tiles x B*H):
+// consecutive linear block ids are dispatched round-robin over the 8 XCDs, so the
+// gridDim.x workgroups of one (b, h) -- which all read the same Q / dO or K / V rows --
+// landed on 8 different L2s (each fetching them: dK/dV and dQ pulled 141 / 146 MB past
+// L2 for ~80 MB of operands, profiles/pmc_hires_r5.md).  xcd_remap gives each XCD a
+// contiguous range of (b, h)s instead.  DC_ATTN_XCD=0 restores the plain mapping (A/B).
+#ifndef DC_ATTN_XCD
+#define DC_ATTN_XCD 1
+#endif
+struct Blk {
+  int x, y;
+};
+__device__ __forceinline__ Blk attn_block() {
+#if DC_ATTN_XCD
+  const int l = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+  return {l % (int)gridDim.x, l / (int)gridDim.x};
+#else
+  return {(int)blockIdx.x, (int)blockIdx.y};
+#endif
+}
+
 // stage rows r0..r0+63 of a [N][HD] bf16 matrix into a padded LDS image
 template <int HD>
 __device__ __forceinline__ void stage64(char* lds, const bf16* __restrict__ base, int r0, int N) {
@@ -320,13 +341,14 @@ __global__ __launch_bounds__(256) void attn_fwd_flash2_kernel(const bf16* __rest
                                                               uint32_t thr, float dsc, uint32_t* __restrict__ keep) {
   using C = AC<HD>;
   __shared__ __attribute__((aligned(16))) char lds[4 * C::TILE];  // [buf][K | V]
-  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const Blk blk = attn_block();
+  const int bh = blk.y, b = bh / H, h = bh - b * H;
   const size_t mat = (size_t)N * HD;
   const bf16* qb = qkv + (size_t)bh * mat;
   const bf16* kb = qkv + ((size_t)B * H + bh) * mat;
   const bf16* vb = qkv + ((size_t)2 * B * H + bh) * mat;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
-  const int qbase = blockIdx.x * 128 + wave * 32;
+  const int qbase = blk.x * 128 + wave * 32;
   const float sl2 = scale * LOG2E;
   const uint32_t salt = DROP ? site_salt(rng, site) : 0u;
   const uint32_t thr2 = (thr >> 1) * 0x10001u;  // thr / 2 in both 16-bit halves (drop_mask2)
@@ -610,7 +632,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
                                                           const uint32_t* __restrict__ keep) {
   using C = AC<HD>;
   __shared__ __attribute__((aligned(16))) char lds[4 * C::TILE];  // [buf][K | V], double-buffered
-  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const Blk blk = attn_block();
+  const int bh = blk.y, b = bh / H, h = bh - b * H;
   const int D = H * HD;
   const size_t mat = (size_t)N * HD;
   const bf16* qb = qkv + (size_t)bh * mat;
@@ -631,7 +654,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
   const u32x2* kcol[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    q[u] = blockIdx.x * (64 * U) + wave * (16 * U) + 16 * u + li;
+    q[u] = blk.x * (64 * U) + wave * (16 * U) + 16 * u + li;
     const bool qv = q[u] < N;
     // dO and O rows of this lane's query are token-major [B, N, D] with head offset h*HD
     const bf16* dorow = dout + ((size_t)b * N + (qv ? q[u] : 0)) * D + h * HD;
@@ -789,7 +812,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
   // the forward's keep words of the query tile for this workgroup's U 64-key tiles,
   // [buf][key tile][half][query]
   __shared__ __attribute__((aligned(16))) uint32_t s_keep[2][U][2][64];
-  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const Blk blk = attn_block();
+  const int bh = blk.y, b = bh / H, h = bh - b * H;
   const int D = H * HD;
   const size_t mat = (size_t)N * HD;
   const bf16* qb = qkv + (size_t)bh * mat;
@@ -804,7 +828,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
   f32x4 dk[U][C::DT], dv[U][C::DT];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    key[u] = blockIdx.x * (64 * U) + wave * (16 * U) + 16 * u + li;
+    key[u] = blk.x * (64 * U) + wave * (16 * U) + 16 * u + li;
 #pragma unroll
     for (int s = 0; s < C::KS; ++s) {
       kf[u][s] = frag_glb<HD>(kb, key[u], N, s, g);
@@ -829,7 +853,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
   const bool kbits = thr && keep != nullptr;
   const int ntiles = (N + 63) / 64;
   u32x2 rk = u32x2{0u, 0u};
-  const int kt_mine = blockIdx.x * U + (threadIdx.x >> 6);  // key tile whose word this thread stages
+  const int kt_mine = blk.x * U + (threadIdx.x >> 6);  // key tile whose word this thread stages
   auto load_tile = [&](int q0) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
