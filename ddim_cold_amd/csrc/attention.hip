@@ -325,12 +325,6 @@ __device__ __forceinline__ void keep_store(uint32_t* __restrict__ keep, size_t w
                                            bool valid) {
   if (valid) reinterpret_cast<uint16_t*>(keep)[word * 4 + g] = (uint16_t)dbits;
 }
-// the 4 keep flags of keys 16t + 4g + r (r = 0..3) of a query from its tile word
-__device__ __forceinline__ void keep_nibble(const u32x2& w, int t, int g, bool (&kp)[4]) {
-  const uint32_t h = (g < 2 ? w[0] : w[1]) >> (16 * (g & 1));
-#pragma unroll
-  for (int r = 0; r < 4; ++r) kp[r] = !((h >> drop_bit(t, r)) & 1u);
-}
 // bit position of key k (0..63 within its tile) in the tile word (a DROP flag)
 __device__ __forceinline__ int keep_bitpos(int k) { return 16 * ((k >> 2) & 3) + drop_bit(k >> 4, k & 3); }
 
@@ -745,9 +739,20 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
         for (int u = 0; u < U; ++u) {
           // the lane's 4 keys are consecutive elements of one mask row (aligned: the
           // row stride is a multiple of 4): 2 pair hashes instead of 4 single ones
-          bool kp[4] = {true, true, true, true};
-          if (kbits) keep_nibble(kw[u], t, g, kp);
-          else if (thr) dropout_keep4_pg(salt, pgq[u] + (uint32_t)(kv0 / 2 + 8 * t) * DROP_GOLDEN, thr, kp);
+          // dropout multipliers (dsc kept, 0 dropped): the stored DROP flag sign-extended
+          // into a mask clearing dsc
+          float fk[4] = {1.f, 1.f, 1.f, 1.f};
+          if (kbits) {
+            const uint32_t hw = (g < 2 ? kw[u][0] : kw[u][1]) >> (16 * (g & 1));
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              fk[r] = __uint_as_float(__float_as_uint(dsc) & ~(uint32_t)__builtin_amdgcn_sbfe((int)hw, drop_bit(t, r), 1));
+          } else if (thr) {
+            bool kp[4];
+            dropout_keep4_pg(salt, pgq[u] + (uint32_t)(kv0 / 2 + 8 * t) * DROP_GOLDEN, thr, kp);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) fk[r] = kp[r] ? dsc : 0.f;
+          }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int key = kv0 + 16 * t + 4 * g + r;
@@ -756,7 +761,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
             float dpv = dp[u][r];
             // (factoring dsc out of dS -- delta / dsc here, dsc in the final dQ / dK / dV
             // scales -- measured no faster: N=626 p=0.1 stored masks 145.5 vs 146.4 us)
-            if (thr) dpv = kp[r] ? dpv * dsc : 0.f;
+            if (thr) dpv = dpv * fk[r];
             ds[u][th][r] = pr * (dpv - dl[u]);
           }
         }
@@ -933,17 +938,21 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        // keep flags of (query 16t+4g+r, this lane's key u)
-        bool kp[4] = {true, true, true, true};
+        // dropout multipliers of (query 16t+4g+r, this lane's key u): dsc kept, 0 dropped
+        float fk[4] = {1.f, 1.f, 1.f, 1.f};
         if (kbits) {
           // this lane's key within the workgroup's 64 U: word of tile kl >> 6, bit
-          // keep_bitpos (half pos >> 5 of the staged 64-bit word)
+          // keep_bitpos (half pos >> 5 of the staged 64-bit word); the stored DROP flag,
+          // sign-extended to a 0 / all-ones word, clears dsc (bfe + and-not per element,
+          // no compare / select pair per product)
           const int kl = wave * (16 * U) + 16 * u + li;
           const int pos = keep_bitpos(kl & 63);
           const u32x4 w = *reinterpret_cast<const u32x4*>(&s_keep[buf][kl >> 6][pos >> 5][16 * t + 4 * g]);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) kp[r] = !((w[r] >> (pos & 31)) & 1u);  // stored DROP flags
+          for (int r = 0; r < 4; ++r)
+            fk[r] = __uint_as_float(__float_as_uint(dsc) & ~(uint32_t)__builtin_amdgcn_sbfe((int)w[r], pos & 31, 1));
         } else if (thr) {
+          bool kp[4];
           // a mask pair is two adjacent keys of one row, held by lanes li and li^1 --
           // each of the two hashes the pair of 2 of the 4 rows and they swap the results
           // (2 hashes per lane, not 4); the golden-constant multiply is hoisted
@@ -958,15 +967,17 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
           const uint32_t hr[4] = {odd ? p0 : hw[0], odd ? p1 : hw[1], odd ? hw[0] : p0, odd ? hw[1] : p1};
 #pragma unroll
           for (int r = 0; r < 4; ++r) kp[r] = (odd ? (hr[r] >> 16) : (hr[r] & 0xFFFFu)) >= thr;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) fk[r] = kp[r] ? dsc : 0.f;
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int qr = 16 * t + 4 * g + r;
           const float pr = fexp2(fmaf(st[u][r], sl2, -sl[qr]));  // padded queries: lse = +inf -> 0
           float pd = pr, dpv = dp[u][r];
-          if (thr) {
-            pd = kp[r] ? pr * dsc : 0.f;
-            dpv = kp[r] ? dpv * dsc : 0.f;
+          if (thr) {  // dropped: pr * 0 = +0, dpv * 0 = +-0 (the same dS: pr * (+-0 - delta))
+            pd = pr * fk[r];
+            dpv = dpv * fk[r];
           }
           pm[u][th][r] = pd;
           ds[u][th][r] = pr * (dpv - sd[qr]);
@@ -1276,13 +1287,19 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
       dp = mfma16(frag_row<HD>(Vl, 16 * t + li, s, g), df[s], dp);
     }
     f32x4 pm;
-    bool kq[4] = {true, true, true, true};
+    // dropout multipliers: dsc kept, 0 dropped (stored KEEP flags sign-extended into a
+    // mask on dsc: bfe + and per element, no compare / select pair per product)
+    float fk[4] = {1.f, 1.f, 1.f, 1.f};
     if (DROP) {
       if (have_bits) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) kq[r] = (kbits >> (4 * t + r)) & 1u;
+        for (int r = 0; r < 4; ++r)
+          fk[r] = __uint_as_float(__float_as_uint(dsc) & (uint32_t)__builtin_amdgcn_sbfe((int)kbits, 4 * t + r, 1));
       } else {
+        bool kq[4];
         dropout_keep4_pg(salt, ((rowidx >> 1) + 2u * (uint32_t)g + 8u * (uint32_t)t) * DROP_GOLDEN, thr, kq);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) fk[r] = kq[r] ? dsc : 0.f;
       }
     }
 #pragma unroll
@@ -1291,10 +1308,9 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
       float pr = fexp2(fmaf(st[r], sl2, -lse2));
       if (16 * t + 16 > N && key >= N) pr = 0.f;  // tail tiles only (uniform test first)
       float pd = pr, dpv = dp[r];
-      if (DROP) {
-        const bool kp = kq[r];
-        pd = kp ? pr * dsc : 0.f;
-        dpv = kp ? dpv * dsc : 0.f;
+      if (DROP) {  // dropped: pr * 0 = +0, dpv * 0 = +-0 (the same dS)
+        pd = pr * fk[r];
+        dpv = dpv * fk[r];
       }
       pm[r] = pd;
       ds[t][r] = pr * (dpv - dl);
