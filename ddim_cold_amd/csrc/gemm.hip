@@ -651,11 +651,14 @@ __device__ __forceinline__ void wgrad_sq_tail(const WgradSq& sq, int tiles, int 
 template <int T, int S, int TN = T, int WM = 2, int WN = 2>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_wgrad_multi_kernel(WgradMulti gm) {
   const int tiles = gm.tile_start[gm.n];
-  if ((int)blockIdx.x >= tiles) {
-    wgrad_sq_tail<64 * WM * WN>(gm.sq, tiles, blockIdx.x - tiles);
+  // the grad-norm tail workgroups first, so their strided sweeps over the untiled arena
+  // ranges overlap the tiles instead of trailing them (within noise: profiles/tail_first_r5.txt)
+  const int extra = (int)gridDim.x - tiles;
+  if ((int)blockIdx.x < extra) {
+    wgrad_sq_tail<64 * WM * WN>(gm.sq, tiles, blockIdx.x);
     return;
   }
-  const int bid = xcd_remap(blockIdx.x, tiles);
+  const int bid = xcd_remap((int)blockIdx.x - extra, tiles);
   int lo = 0, hi = gm.n - 1;  // problem owning tile `bid`: binary search over tile_start
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;

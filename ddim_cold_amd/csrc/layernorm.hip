@@ -273,14 +273,17 @@ __device__ __forceinline__ void fold_tail(const FoldTable& tb) {
 }
 
 __global__ __launch_bounds__(256) void ln_fold_kernel(FoldTable tb) {
-  if (tb.tail && blockIdx.x == gridDim.x - 1) {
+  // the tail workgroup first, so its serial partial sums overlap the fold rows instead of
+  // trailing them (measured within noise: profiles/tail_first_r5.txt)
+  if (tb.tail && blockIdx.x == 0) {
     fold_tail(tb);
     return;
   }
+  const int bx = (int)blockIdx.x - (tb.tail ? 1 : 0);
   // two rows per wave (32 lanes each), every load of the row issued before use
   constexpr int IT = 4;  // float4 per lane: K <= 32 * 4 * IT = 512
   const int hl = threadIdx.x & 31;
-  const int r = blockIdx.x * 8 + (threadIdx.x >> 5);
+  const int r = bx * 8 + (threadIdx.x >> 5);
   const bool live = r < tb.start[tb.n];
   const int rr = live ? r : tb.start[tb.n] - 1;
   int ji = 0;
@@ -334,13 +337,16 @@ __global__ __launch_bounds__(256) void ln_fold_kernel(FoldTable tb) {
 // workgroup), 16-byte weight loads and stores -- the 32-lane / 8-byte kernel above
 // moved half as many bytes per instruction
 __global__ __launch_bounds__(256) void ln_fold16_kernel(FoldTable tb) {
-  if (tb.tail && blockIdx.x == gridDim.x - 1) {
+  // the tail workgroup first, so its serial partial sums overlap the fold rows instead of
+  // trailing them (measured within noise: profiles/tail_first_r5.txt)
+  if (tb.tail && blockIdx.x == 0) {
     fold_tail(tb);
     return;
   }
+  const int bx = (int)blockIdx.x - (tb.tail ? 1 : 0);
   constexpr int IT = 4;  // 16-B chunks per lane: K <= 16 * 8 * IT = 512
   const int hl = threadIdx.x & 15;
-  const int r = blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int r = bx * 16 + (threadIdx.x >> 4);
   const bool live = r < tb.start[tb.n];
   const int rr = live ? r : tb.start[tb.n] - 1;
   int ji = 0;
