@@ -693,8 +693,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
   __syncthreads();
   // key mask only in the tail tile: a padded key has a zero K row (no dQ
   // contribution) but exp2(0 - lse) can overflow, so it must not reach dS
-  auto tile = [&](int it, auto mask_tag) {
+  // KB (stored drop flags present) as a compile-time tag: a runtime kbits / rehash branch
+  // per element group merged the two paths' multipliers through phi copies
+  auto tile = [&](int it, auto mask_tag, auto kb_tag) {
     constexpr bool MASK = decltype(mask_tag)::value;
+    constexpr bool KB = decltype(kb_tag)::value;
     const int kv0 = it * 64;
     const bool more = it + 1 < ntiles;
     // the next tile's keep words and K / V in one batch, issued on every tile (the last
@@ -706,7 +709,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       kw[u] = kwc[u];
-      kwc[u] = kbits ? kcol[u][(size_t)itn * N] : u32x2{0u, 0u};
+      kwc[u] = KB ? kcol[u][(size_t)itn * N] : u32x2{0u, 0u};
     }
     stg.load(kb, vb, itn * 64, N);  // next tile lands during this tile's MFMAs
     const char* Kl = lds + (it & 1) * 2 * C::TILE;
@@ -737,32 +740,35 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          // the lane's 4 keys are consecutive elements of one mask row (aligned: the
-          // row stride is a multiple of 4): 2 pair hashes instead of 4 single ones
           // dropout multipliers (dsc kept, 0 dropped): the stored DROP flag sign-extended
-          // into a mask clearing dsc
+          // into a mask clearing dsc; without stored flags the lane's 4 keys are
+          // consecutive elements of one mask row (aligned: the row stride is a multiple of
+          // 4), 2 pair hashes instead of 4 single ones
           float fk[4] = {1.f, 1.f, 1.f, 1.f};
-          if (kbits) {
+          if constexpr (KB) {
             const uint32_t hw = (g < 2 ? kw[u][0] : kw[u][1]) >> (16 * (g & 1));
 #pragma unroll
             for (int r = 0; r < 4; ++r)
               fk[r] = __uint_as_float(__float_as_uint(dsc) & ~(uint32_t)__builtin_amdgcn_sbfe((int)hw, drop_bit(t, r), 1));
-          } else if (thr) {
-            bool kp[4];
-            dropout_keep4_pg(salt, pgq[u] + (uint32_t)(kv0 / 2 + 8 * t) * DROP_GOLDEN, thr, kp);
+          } else {
+            if (thr) {
+              bool kp[4];
+              dropout_keep4_pg(salt, pgq[u] + (uint32_t)(kv0 / 2 + 8 * t) * DROP_GOLDEN, thr, kp);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) fk[r] = kp[r] ? dsc : 0.f;
+              for (int r = 0; r < 4; ++r) fk[r] = kp[r] ? dsc : 0.f;
+            }
           }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int key = kv0 + 16 * t + 4 * g + r;
             float pr = fexp2(fmaf(st[u][r], sl2, nl2[u]));
             if (MASK && key >= N) pr = 0.f;
-            float dpv = dp[u][r];
             // (factoring dsc out of dS -- delta / dsc here, dsc in the final dQ / dK / dV
-            // scales -- measured no faster: N=626 p=0.1 stored masks 145.5 vs 146.4 us)
-            if (thr) dpv = dpv * fk[r];
-            ds[u][th][r] = pr * (dpv - dl[u]);
+            // scales -- measured no faster: N=626 p=0.1 stored masks 145.5 vs 146.4 us).
+            // One explicit fma: the KB and rehash instantiations must round alike (stored
+            // flags == re-hashed masks, bit for bit), not per the compiler's contraction
+            const float dd = (KB || thr) ? fmaf(dp[u][r], fk[r], -dl[u]) : dp[u][r] - dl[u];
+            ds[u][th][r] = pr * dd;
           }
         }
       }
@@ -780,8 +786,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
     __syncthreads();
   };
   const int nfull = N / 64;
-  for (int it = 0; it < nfull; ++it) tile(it, std::false_type{});
-  if (nfull < ntiles) tile(nfull, std::true_type{});
+  auto run = [&](auto kb_tag) {
+    for (int it = 0; it < nfull; ++it) tile(it, std::false_type{}, kb_tag);
+    if (nfull < ntiles) tile(nfull, std::true_type{}, kb_tag);
+  };
+  if (kbits) run(std::true_type{});
+  else run(std::false_type{});
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     if (q[u] < N) {
@@ -903,6 +913,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
   load_tile(0);
   store_tile(0);
   __syncthreads();
+  // (the stored-flag path as a compile-time tag, as in the dQ kernel, measured slower here:
+  // 77.0 -> 84.1 us at N = 626, profiles/attn_bwd_kbtag_r5.txt)
   for (int it = 0; it < ntiles; ++it) {
     const int q0 = it * 64;
     const bool more = it + 1 < ntiles;
