@@ -1290,6 +1290,10 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
   dl += __shfl_xor(dl, 32, 64);
   const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * attn_mask_ld(N));
   f32x4 ds[KT];
+  // KB (stored flags present) as a compile-time tag, as in attn_bwd_dq_kernel: no runtime
+  // branch per key tile whose two multiplier definitions meet in phi copies
+  auto phase_a = [&](auto kb_tag) {
+  constexpr bool KB = decltype(kb_tag)::value;
 #pragma unroll
   for (int t = 0; t < KT; ++t) {
     f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1302,8 +1306,8 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
     // dropout multipliers: dsc kept, 0 dropped (stored KEEP flags sign-extended into a
     // mask on dsc: bfe + and per element, no compare / select pair per product)
     float fk[4] = {1.f, 1.f, 1.f, 1.f};
-    if (DROP) {
-      if (have_bits) {
+    if constexpr (DROP) {
+      if constexpr (KB) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           fk[r] = __uint_as_float(__float_as_uint(dsc) & (uint32_t)__builtin_amdgcn_sbfe((int)kbits, 4 * t + r, 1));
@@ -1319,17 +1323,17 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
       const int key = 16 * t + 4 * g + r;
       float pr = fexp2(fmaf(st[r], sl2, -lse2));
       if (16 * t + 16 > N && key >= N) pr = 0.f;  // tail tiles only (uniform test first)
-      float pd = pr, dpv = dp[r];
-      if (DROP) {  // dropped: pr * 0 = +0, dpv * 0 = +-0 (the same dS)
-        pd = pr * fk[r];
-        dpv = dpv * fk[r];
-      }
-      pm[r] = pd;
-      ds[t][r] = pr * (dpv - dl);
+      // dropped: pr * 0 = +0, fma(dp, 0, -delta) = -delta; one explicit fma so both
+      // instantiations round alike (stored flags == re-hashed masks, bit for bit)
+      pm[r] = DROP ? pr * fk[r] : pr;
+      ds[t][r] = pr * (DROP ? fmaf(dp[r], fk[r], -dl) : dp[r] - dl);
     }
     *reinterpret_cast<bf16x4*>(Pl + pimg_off(q, (16 * t + 4 * g) * 2, PS)) = pack4(pm);
     *reinterpret_cast<bf16x4*>(Sl + pimg_off(q, (16 * t + 4 * g) * 2, PS)) = pack4(ds[t]);
   }
+  };
+  if (have_bits) phase_a(std::true_type{});
+  else phase_a(std::false_type{});
   f32x4 dq[DT];
 #pragma unroll
   for (int d = 0; d < DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
