@@ -327,6 +327,10 @@ __device__ __forceinline__ void keep_store(uint32_t* __restrict__ keep, size_t w
 }
 // bit position of key k (0..63 within its tile) in the tile word (a DROP flag)
 __device__ __forceinline__ int keep_bitpos(int k) { return 16 * ((k >> 2) & 3) + drop_bit(k >> 4, k & 3); }
+// Short-sequence kernels: one 32-bit word per lane (query, lane group g) with the DROP flag
+// of key 16 t + 4 g + r at bit short_drop_bit(t, r) (t < 8): the low / high halves of the
+// pair masks of drop_mask2 land in bits 2t + j / 16 + 2t + j, one AND-OR per pair
+__device__ __forceinline__ constexpr int short_drop_bit(int t, int r) { return 16 * (r & 1) + 2 * t + (r >> 1); }
 
 template <int HD, bool DROP>
 __global__ __launch_bounds__(256) void attn_fwd_flash2_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
@@ -1182,26 +1186,30 @@ __global__ __launch_bounds__(NP * 4) void attn_fwd_short_kernel(const bf16* __re
   const float nmx = -mx;
   float l = 0.f;
   const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * attn_mask_ld(N));
-  const uint32_t pgs = ((rowidx >> 1) + 2u * (uint32_t)g) * DROP_GOLDEN;
-  uint32_t kbits = 0u;
+  const uint32_t pgs = DROP ? ((rowidx >> 1) + 2u * (uint32_t)g) * DROP_GOLDEN + salt : 0u;
+  const uint32_t thr2 = (thr >> 1) * 0x10001u;  // thr / 2 in both 16-bit halves (drop_mask2)
+  // dropout as packed 16-bit drop masks AND-NOT-ed onto the bf16 P pairs (as in the flash
+  // forward: no per-element compare / select), the drop flags from the same masks
+  uint32_t dm[KT][2], db = 0u;
 #pragma unroll
   for (int t = 0; t < KT; ++t) {
-    bool kp[4] = {true, true, true, true};
-    if (DROP) dropout_keep4_pg(salt, pgs + (uint32_t)(8 * t) * DROP_GOLDEN, thr, kp);
+    if (DROP) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        dm[t][j] = drop_mask2(drop_mix(pgs + (uint32_t)(8 * t + j) * DROP_GOLDEN), thr2);
+        db |= dm[t][j] & ((1u << (2 * t + j)) | (1u << (16 + 2 * t + j)));
+      }
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float pv = fexp2(fmaf(st[t][r], sl2, nmx));
+      const float pv = fexp2(fmaf(st[t][r], sl2, nmx));  // keep scale folded into the final 1/l
       l += pv;
-      if (DROP) {
-        pv = kp[r] ? pv : 0.f;  // keep scale folded into the final 1/l
-        kbits |= (kp[r] ? 1u : 0u) << (4 * t + r);
-      }
       st[t][r] = pv;
     }
   }
-  // the keep flags of this lane's (query, 16t + 4g + r) elements for the backward
-  // (same lane layout there): one word per lane instead of re-hashing KT*2 pairs
-  if (DROP && keep_bits != nullptr) keep_bits[((size_t)bh * NP + q) * 4 + g] = kbits;
+  // the drop flags of this lane's (query, 16t + 4g + r) elements for the backward
+  // (short_drop_bit layout): one word per lane instead of re-hashing KT*2 pairs
+  if (DROP && keep_bits != nullptr) keep_bits[((size_t)bh * NP + q) * 4 + g] = db;
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
   f32x4 o[DT];
@@ -1209,7 +1217,8 @@ __global__ __launch_bounds__(NP * 4) void attn_fwd_short_kernel(const bf16* __re
   for (int d = 0; d < DT; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s2 = 0; s2 < NP / 32; ++s2) {
-    const bf16x8 pb = pack8(st[2 * s2], st[2 * s2 + 1]);
+    const bf16x8 pb = DROP ? pack8_drop(st[2 * s2], st[2 * s2 + 1], dm[2 * s2], dm[2 * s2 + 1])
+                           : pack8(st[2 * s2], st[2 * s2 + 1]);
 #pragma unroll
     for (int d = 0; d < DT; ++d) o[d] = mfma16(frag_t<RS>(Vl, 16 * d, s2, lane), pb, o[d]);
   }
@@ -1264,7 +1273,7 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
     for (int s = 0; s < KS; ++s) of[s] = *reinterpret_cast<const bf16x8*>(orow + 32 * s + 8 * g);
   }
   const float lse_raw = lse[(size_t)bh * N + qc];
-  // the forward's keep flags (attn_fwd_short_kernel layout) when it stored them
+  // the forward's drop flags (short_drop_bit layout) when it stored them
   const bool have_bits = DROP && keep_bits != nullptr;
   const uint32_t kbits = have_bits ? keep_bits[((size_t)bh * NP + q) * 4 + g] : 0u;
   const uint32_t salt = DROP ? site_salt(rng, site) : 0u;
@@ -1303,14 +1312,15 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
       dp = mfma16(frag_row<HD>(Vl, 16 * t + li, s, g), df[s], dp);
     }
     f32x4 pm;
-    // dropout multipliers: dsc kept, 0 dropped (stored KEEP flags sign-extended into a
-    // mask on dsc: bfe + and per element, no compare / select pair per product)
+    // dropout multipliers: dsc kept, 0 dropped (stored DROP flags, short_drop_bit layout,
+    // sign-extended into a mask clearing dsc: bfe + and-not per element)
     float fk[4] = {1.f, 1.f, 1.f, 1.f};
     if constexpr (DROP) {
       if constexpr (KB) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          fk[r] = __uint_as_float(__float_as_uint(dsc) & (uint32_t)__builtin_amdgcn_sbfe((int)kbits, 4 * t + r, 1));
+          fk[r] = __uint_as_float(__float_as_uint(dsc) &
+                                  ~(uint32_t)__builtin_amdgcn_sbfe((int)kbits, short_drop_bit(t, r), 1));
       } else {
         bool kq[4];
         dropout_keep4_pg(salt, ((rowidx >> 1) + 2u * (uint32_t)g + 8u * (uint32_t)t) * DROP_GOLDEN, thr, kq);
@@ -1618,24 +1628,27 @@ __global__ __launch_bounds__(NP * 4) void qkv_attn_short_kernel(QkvAttnParams p)
   const float nmx = -mx;
   float l = 0.f;
   const uint32_t rowidx = (uint32_t)(((size_t)bh * N + tok) * attn_mask_ld(N));
-  const uint32_t pgs = ((rowidx >> 1) + 2u * (uint32_t)g) * DROP_GOLDEN;
-  uint32_t kbits = 0u;
+  const uint32_t pgs = DROP ? ((rowidx >> 1) + 2u * (uint32_t)g) * DROP_GOLDEN + salt : 0u;
+  const uint32_t thr2 = (p.thr >> 1) * 0x10001u;
+  // packed drop masks and short_drop_bit flags, as attn_fwd_short_kernel
+  uint32_t dm[KT][2], db = 0u;
 #pragma unroll
   for (int t = 0; t < KT; ++t) {
-    bool kp[4] = {true, true, true, true};
-    if (DROP) dropout_keep4_pg(salt, pgs + (uint32_t)(8 * t) * DROP_GOLDEN, p.thr, kp);
+    if (DROP) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        dm[t][j] = drop_mask2(drop_mix(pgs + (uint32_t)(8 * t + j) * DROP_GOLDEN), thr2);
+        db |= dm[t][j] & ((1u << (2 * t + j)) | (1u << (16 + 2 * t + j)));
+      }
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float pv = fexp2(fmaf(st[t][r], sl2, nmx));
+      const float pv = fexp2(fmaf(st[t][r], sl2, nmx));
       l += pv;
-      if (DROP) {
-        pv = kp[r] ? pv : 0.f;
-        kbits |= (kp[r] ? 1u : 0u) << (4 * t + r);
-      }
       st[t][r] = pv;
     }
   }
-  if (DROP && p.keep_bits != nullptr) p.keep_bits[((size_t)bh * NP + tok) * 4 + g] = kbits;
+  if (DROP && p.keep_bits != nullptr) p.keep_bits[((size_t)bh * NP + tok) * 4 + g] = db;
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
   f32x4 o[DT];
@@ -1643,7 +1656,8 @@ __global__ __launch_bounds__(NP * 4) void qkv_attn_short_kernel(QkvAttnParams p)
   for (int d = 0; d < DT; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s2i = 0; s2i < NP / 32; ++s2i) {
-    const bf16x8 pb = pack8(st[2 * s2i], st[2 * s2i + 1]);
+    const bf16x8 pb = DROP ? pack8_drop(st[2 * s2i], st[2 * s2i + 1], dm[2 * s2i], dm[2 * s2i + 1])
+                           : pack8(st[2 * s2i], st[2 * s2i + 1]);
 #pragma unroll
     for (int d = 0; d < DT; ++d) o[d] = mfma16(frag_t<RS>(Vl, 16 * d, s2i, lane), pb, o[d]);
   }
