@@ -817,7 +817,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
 // dV / dK updates of U groups (see attn_bwd_dq_kernel).  Per 32-query half of a tile:
 // S^T / dP^T -> P / dS -> dV / dK, so half a tile's P and dS are live: 186 -> 150
 // VGPRs, 2 -> 3 waves per SIMD, N=626 backward 161 -> 146 us (p=0.1, stored masks).
-template <int HD, int U>
+//
+// KB: the forward's stored drop flags are read (a kernel-level template parameter: the
+// same as a tag on the loop body measured slower, profiles/attn_bwd_kbtag_r5.txt)
+template <int HD, int U, bool KB>
 __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restrict__ dout,
                                                            const bf16* __restrict__ qkv,
                                                            const float* __restrict__ lse,
@@ -869,7 +872,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
   bool rok[PER];
   float rl = 0.f, rdl = 0.f;
   bool rlv = false;
-  const bool kbits = thr && keep != nullptr;
+  constexpr bool kbits = KB;  // the launcher passes KB only with stored flags and thr > 0
   const int ntiles = (N + 63) / 64;
   u32x2 rk = u32x2{0u, 0u};
   const int kt_mine = blk.x * U + (threadIdx.x >> 6);  // key tile whose word this thread stages
@@ -990,13 +993,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
         for (int r = 0; r < 4; ++r) {
           const int qr = 16 * t + 4 * g + r;
           const float pr = fexp2(fmaf(st[u][r], sl2, -sl[qr]));  // padded queries: lse = +inf -> 0
-          float pd = pr, dpv = dp[u][r];
-          if (thr) {  // dropped: pr * 0 = +0, dpv * 0 = +-0 (the same dS: pr * (+-0 - delta))
-            pd = pr * fk[r];
-            dpv = dpv * fk[r];
-          }
+          // dropped: pr * 0 = +0 and fma(dp, 0, -delta) = -delta; one explicit fma so the
+          // KB and re-hash instantiations round alike (stored flags == re-hashed masks)
+          const float pd = (KB || thr) ? pr * fk[r] : pr;
+          const float dd = (KB || thr) ? fmaf(dp[u][r], fk[r], -sd[qr]) : dp[u][r] - sd[qr];
           pm[u][th][r] = pd;
-          ds[u][th][r] = pr * (dpv - sd[qr]);
+          ds[u][th][r] = pr * dd;
         }
       }
     }
@@ -1043,9 +1045,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
   template __global__ void attn_bwd_dq_kernel<HD, U>(const bf16*, const bf16*, const bf16*, const float*, float*,  \
                                                      bf16*, int, int, int, float, const int64_t*, int, uint32_t,  \
                                                      float, const uint32_t*);                                     \
-  template __global__ void attn_bwd_dkv_kernel<HD, U>(const bf16*, const bf16*, const float*, const float*, bf16*, \
-                                                      int, int, int, float, const int64_t*, int, uint32_t, float,  \
-                                                      const uint32_t*);
+  template __global__ void attn_bwd_dkv_kernel<HD, U, true>(const bf16*, const bf16*, const float*, const float*,  \
+                                                            bf16*, int, int, int, float, const int64_t*, int,      \
+                                                            uint32_t, float, const uint32_t*);                     \
+  template __global__ void attn_bwd_dkv_kernel<HD, U, false>(const bf16*, const bf16*, const float*, const float*, \
+                                                             bf16*, int, int, int, float, const int64_t*, int,     \
+                                                             uint32_t, float, const uint32_t*);
 DC_INST_BWD(32, 1) DC_INST_BWD(64, 1)
 
 // ============================================================================ short sequences (N <= 128)
@@ -1804,8 +1809,12 @@ void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const flo
 #define DC_LAUNCH_BWD(HDV, UV)                                                                                        \
   hipLaunchKernelGGL((attn_bwd_dq_kernel<HDV, UV>), gridu, dim3(256), 0, stream, d, q, oo, lse, delta, dq, B, H, N,  \
                      scale, rng, site, thr, dsc, keep_bits);                                                         \
-  hipLaunchKernelGGL((attn_bwd_dkv_kernel<HDV, UV>), gridu, dim3(256), 0, stream, d, q, lse, delta, dq, B, H, N,     \
-                     scale, rng, site, thr, dsc, keep_bits);
+  if (thr && keep_bits)                                                                                               \
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<HDV, UV, true>), gridu, dim3(256), 0, stream, d, q, lse, delta, dq, B, H, \
+                       N, scale, rng, site, thr, dsc, keep_bits);                                                    \
+  else                                                                                                                \
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<HDV, UV, false>), gridu, dim3(256), 0, stream, d, q, lse, delta, dq, B,   \
+                       H, N, scale, rng, site, thr, dsc, keep_bits);
   if (hd == 32) { DC_LAUNCH_BWD(32, 1) }
   else { DC_LAUNCH_BWD(64, 1) }
 #undef DC_LAUNCH_BWD
