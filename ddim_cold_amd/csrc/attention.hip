@@ -621,7 +621,7 @@ static void launch_resident(const bf16* q, bf16* out, float* lse, int B, int H, 
 // the dQ update U more.  Only U = 1 is built (attn_bwd_launch: U = 2 measured slower,
 // it costs occupancy); the two 32-key halves of a tile each run S / dP -> dS -> dQ in
 // turn, so only half a tile's dS is live (128 -> 114 VGPRs).
-template <int HD, int U>
+template <int HD, int U, bool KB>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ qkv,
                                                           const bf16* __restrict__ out, const float* __restrict__ lse,
                                                           float* __restrict__ delta, bf16* __restrict__ dqkv, int B,
@@ -643,7 +643,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
   const float sl2 = scale * LOG2E;
   const uint32_t salt = thr ? site_salt(rng, site) : 0u;
   const int ntiles = (N + 63) / 64;
-  const bool kbits = thr && keep != nullptr;
+  constexpr bool kbits = KB;  // the launcher passes KB only with stored flags and thr > 0
 
   int q[U];
   bf16x8 qf[U][C::KS], df[U][C::KS];
@@ -697,11 +697,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
   __syncthreads();
   // key mask only in the tail tile: a padded key has a zero K row (no dQ
   // contribution) but exp2(0 - lse) can overflow, so it must not reach dS
-  // KB (stored drop flags present) as a compile-time tag: a runtime kbits / rehash branch
-  // per element group merged the two paths' multipliers through phi copies
-  auto tile = [&](int it, auto mask_tag, auto kb_tag) {
+  // KB (stored drop flags present) is a kernel template parameter: a runtime kbits / rehash
+  // branch per element group merged the two paths' multipliers through phi copies
+  auto tile = [&](int it, auto mask_tag) {
     constexpr bool MASK = decltype(mask_tag)::value;
-    constexpr bool KB = decltype(kb_tag)::value;
     const int kv0 = it * 64;
     const bool more = it + 1 < ntiles;
     // the next tile's keep words and K / V in one batch, issued on every tile (the last
@@ -790,12 +789,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
     __syncthreads();
   };
   const int nfull = N / 64;
-  auto run = [&](auto kb_tag) {
-    for (int it = 0; it < nfull; ++it) tile(it, std::false_type{}, kb_tag);
-    if (nfull < ntiles) tile(nfull, std::true_type{}, kb_tag);
-  };
-  if (kbits) run(std::true_type{});
-  else run(std::false_type{});
+  for (int it = 0; it < nfull; ++it) tile(it, std::false_type{});
+  if (nfull < ntiles) tile(nfull, std::true_type{});
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     if (q[u] < N) {
@@ -1042,9 +1037,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const bf16* __restric
   }
 }
 #define DC_INST_BWD(HD, U)                                                                                       \
-  template __global__ void attn_bwd_dq_kernel<HD, U>(const bf16*, const bf16*, const bf16*, const float*, float*,  \
-                                                     bf16*, int, int, int, float, const int64_t*, int, uint32_t,  \
-                                                     float, const uint32_t*);                                     \
+  template __global__ void attn_bwd_dq_kernel<HD, U, true>(const bf16*, const bf16*, const bf16*, const float*,   \
+                                                           float*, bf16*, int, int, int, float, const int64_t*,    \
+                                                           int, uint32_t, float, const uint32_t*);                 \
+  template __global__ void attn_bwd_dq_kernel<HD, U, false>(const bf16*, const bf16*, const bf16*, const float*,  \
+                                                            float*, bf16*, int, int, int, float, const int64_t*,   \
+                                                            int, uint32_t, float, const uint32_t*);                \
   template __global__ void attn_bwd_dkv_kernel<HD, U, true>(const bf16*, const bf16*, const float*, const float*,  \
                                                             bf16*, int, int, int, float, const int64_t*, int,      \
                                                             uint32_t, float, const uint32_t*);                     \
@@ -1807,14 +1805,17 @@ void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const flo
   // SIMD: 180 vs 146 us) -- the kernels need the latency hiding of occupancy more
   const dim3 gridu((N + 63) / 64, B * H);
 #define DC_LAUNCH_BWD(HDV, UV)                                                                                        \
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<HDV, UV>), gridu, dim3(256), 0, stream, d, q, oo, lse, delta, dq, B, H, N,  \
-                     scale, rng, site, thr, dsc, keep_bits);                                                         \
-  if (thr && keep_bits)                                                                                               \
+  if (thr && keep_bits) {                                                                                             \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<HDV, UV, true>), gridu, dim3(256), 0, stream, d, q, oo, lse, delta, dq, B,  \
+                       H, N, scale, rng, site, thr, dsc, keep_bits);                                                 \
     hipLaunchKernelGGL((attn_bwd_dkv_kernel<HDV, UV, true>), gridu, dim3(256), 0, stream, d, q, lse, delta, dq, B, H, \
                        N, scale, rng, site, thr, dsc, keep_bits);                                                    \
-  else                                                                                                                \
+  } else {                                                                                                            \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<HDV, UV, false>), gridu, dim3(256), 0, stream, d, q, oo, lse, delta, dq,  \
+                       B, H, N, scale, rng, site, thr, dsc, keep_bits);                                              \
     hipLaunchKernelGGL((attn_bwd_dkv_kernel<HDV, UV, false>), gridu, dim3(256), 0, stream, d, q, lse, delta, dq, B,   \
-                       H, N, scale, rng, site, thr, dsc, keep_bits);
+                       H, N, scale, rng, site, thr, dsc, keep_bits);                                                 \
+  }
   if (hd == 32) { DC_LAUNCH_BWD(32, 1) }
   else { DC_LAUNCH_BWD(64, 1) }
 #undef DC_LAUNCH_BWD
