@@ -1234,7 +1234,7 @@ __global__ __launch_bounds__(NP * 4) void attn_fwd_short_kernel(const bf16* __re
   }
 }
 
-template <int HD, int NP, bool DROP>
+template <int HD, int NP, bool DROP, bool KB>
 __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __restrict__ dout,
                                                                 const bf16* __restrict__ qkv,
                                                                 const bf16* __restrict__ out,
@@ -1276,8 +1276,9 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
     for (int s = 0; s < KS; ++s) of[s] = *reinterpret_cast<const bf16x8*>(orow + 32 * s + 8 * g);
   }
   const float lse_raw = lse[(size_t)bh * N + qc];
-  // the forward's drop flags (short_drop_bit layout) when it stored them
-  const bool have_bits = DROP && keep_bits != nullptr;
+  // the forward's drop flags (short_drop_bit layout) when it stored them (KB: a kernel
+  // template parameter, so the flag and re-hash paths are separate instantiations)
+  constexpr bool have_bits = DROP && KB;
   const uint32_t kbits = have_bits ? keep_bits[((size_t)bh * NP + q) * 4 + g] : 0u;
   const uint32_t salt = DROP ? site_salt(rng, site) : 0u;
   iq.store(Ql);
@@ -1302,10 +1303,6 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
   dl += __shfl_xor(dl, 32, 64);
   const uint32_t rowidx = (uint32_t)(((size_t)bh * N + q) * attn_mask_ld(N));
   f32x4 ds[KT];
-  // KB (stored flags present) as a compile-time tag, as in attn_bwd_dq_kernel: no runtime
-  // branch per key tile whose two multiplier definitions meet in phi copies
-  auto phase_a = [&](auto kb_tag) {
-  constexpr bool KB = decltype(kb_tag)::value;
 #pragma unroll
   for (int t = 0; t < KT; ++t) {
     f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1344,9 +1341,6 @@ __global__ __launch_bounds__(NP * 4) void attn_bwd_short_kernel(const bf16* __re
     *reinterpret_cast<bf16x4*>(Pl + pimg_off(q, (16 * t + 4 * g) * 2, PS)) = pack4(pm);
     *reinterpret_cast<bf16x4*>(Sl + pimg_off(q, (16 * t + 4 * g) * 2, PS)) = pack4(ds[t]);
   }
-  };
-  if (have_bits) phase_a(std::true_type{});
-  else phase_a(std::false_type{});
   f32x4 dq[DT];
 #pragma unroll
   for (int d = 0; d < DT; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1413,16 +1407,20 @@ struct ShortLaunch {
     using L = ShortLds<HD, NP>;
     static const bool attr = [] {
       allow_lds(&attn_fwd_short_kernel<HD, NP, DROP>, L::FWD);
-      allow_lds(&attn_bwd_short_kernel<HD, NP, DROP>, L::BWD);
+      allow_lds(&attn_bwd_short_kernel<HD, NP, DROP, false>, L::BWD);
+      allow_lds(&attn_bwd_short_kernel<HD, NP, DROP, DROP>, L::BWD);
       return true;
     }();
     (void)attr;
     if (!bwd)
       hipLaunchKernelGGL((attn_fwd_short_kernel<HD, NP, DROP>), dim3(B * H), dim3(NP * 4), L::FWD, stream, q, outp,
                          lse, B, H, N, scale, rng, site, thr, dsc, kb);
+    else if (DROP && kb != nullptr)  // stored drop flags: the KB instantiation
+      hipLaunchKernelGGL((attn_bwd_short_kernel<HD, NP, DROP, DROP>), dim3(B * H), dim3(NP * 4), L::BWD, stream, d,
+                         q, o, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, kb);
     else
-      hipLaunchKernelGGL((attn_bwd_short_kernel<HD, NP, DROP>), dim3(B * H), dim3(NP * 4), L::BWD, stream, d, q,
-                         o, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, kb);
+      hipLaunchKernelGGL((attn_bwd_short_kernel<HD, NP, DROP, false>), dim3(B * H), dim3(NP * 4), L::BWD, stream, d,
+                         q, o, lse_in, outp, B, H, N, scale, rng, site, thr, dsc, kb);
   }
 };
 
@@ -1451,11 +1449,16 @@ static void dispatch_short(bool bwd, const bf16* d, const bf16* q, const bf16* o
 #define DC_INST_SHORT1(HD, NP, DR)                                                                                 \
   template __global__ void attn_fwd_short_kernel<HD, NP, DR>(const bf16*, bf16*, float*, int, int, int, float,    \
                                                              const int64_t*, int, uint32_t, float, uint32_t*);    \
-  template __global__ void attn_bwd_short_kernel<HD, NP, DR>(const bf16*, const bf16*, const bf16*,               \
-                                                              const float*, bf16*, int, int, int, float,          \
-                                                              const int64_t*, int, uint32_t, float,               \
-                                                              const uint32_t*);
-#define DC_INST_SHORT(HD, NP) DC_INST_SHORT1(HD, NP, true) DC_INST_SHORT1(HD, NP, false)
+  template __global__ void attn_bwd_short_kernel<HD, NP, DR, false>(const bf16*, const bf16*, const bf16*,        \
+                                                                     const float*, bf16*, int, int, int, float,   \
+                                                                     const int64_t*, int, uint32_t, float,        \
+                                                                     const uint32_t*);
+#define DC_INST_SHORT(HD, NP)                                                                                      \
+  DC_INST_SHORT1(HD, NP, true) DC_INST_SHORT1(HD, NP, false)                                                       \
+  template __global__ void attn_bwd_short_kernel<HD, NP, true, true>(const bf16*, const bf16*, const bf16*,        \
+                                                                      const float*, bf16*, int, int, int, float,  \
+                                                                      const int64_t*, int, uint32_t, float,       \
+                                                                      const uint32_t*);
 DC_INST_SHORT(32, 32) DC_INST_SHORT(32, 64) DC_INST_SHORT(32, 96) DC_INST_SHORT(32, 128)
 DC_INST_SHORT(64, 32) DC_INST_SHORT(64, 64) DC_INST_SHORT(64, 96) DC_INST_SHORT(64, 128)
 
