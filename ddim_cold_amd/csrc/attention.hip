@@ -21,7 +21,7 @@
 //   qkv Linear's output columns) so the qkv dgrad/wgrad GEMMs consume it directly.
 #include "common.h"
 #include "kernels.h"
-#include "gemm_common.h"  // frag_k / swz: the QKV phase of qkv_attn_short_kernel
+#include "gemm_common.h"  // xcd_remap
 #include <cstdlib>
 #include <type_traits>
 
@@ -1465,241 +1465,6 @@ DC_INST_SHORT(64, 32) DC_INST_SHORT(64, 64) DC_INST_SHORT(64, 96) DC_INST_SHORT(
 
 constexpr int SHORT_MAX_N = 128;
 
-// ============================================================================ QKV projection + short attention
-// The block's QKV Linear (LayerNorm folded in) and the short-sequence attention forward
-// in ONE launch, one workgroup per (b, h) as attn_fwd_short_kernel (ViT.py:100-117):
-//   phase A: [q | k | v] of head h for the NP (padded) tokens of sample b =
-//            x_b (gamma o W_h)^T through the MFMAs, K-chunks of 64 double-buffered in LDS,
-//            then the fold consumer's epilogue rstd (acc - mean c) + (b + W beta) with
-//            mean / rstd from the producer's {sum, sum^2} slots (gemm_epi.h FoldEpi);
-//            written to the head-major qkv buffer (the backward's operand) AND into the
-//            LDS K / V / Q images the attention reads -- no qkv round trip through HBM
-//            before the attention, one launch and one kernel boundary fewer per block;
-//   phase B: the attention of attn_fwd_short_kernel, unchanged (same dropout masks,
-//            same keep words, same LSE).
-// The weight rows of head h are re-read by the B workgroups of that head and the token
-// rows of sample b by its H workgroups: L2 traffic, not HBM.
-template <int HD, int NP, bool DROP>
-__global__ __launch_bounds__(NP * 4) void qkv_attn_short_kernel(QkvAttnParams p) {
-  constexpr int NT = NP * 4, NW = NP / 16;
-  constexpr int FQ = 3 * HD / 16;   // 16-column fragments of [q | k | v]
-  constexpr int WR = 3 * HD;        // weight rows of the head
-  constexpr int XB = NP * 128, WB = WR * 128, STG = XB + WB;  // one 64-deep K chunk
-  constexpr int PX = NP * 8 / NT, PW = (WR * 8 + NT - 1) / NT;  // 16-B pieces per thread
-  static_assert(PX * NT == NP * 8, "token pieces split over the threads");
-  using I = ShortImg<HD, NP>;
-  constexpr int RS = I::RS, KS = HD / 32, DT = HD / 16, KT = NP / 16;
-  static_assert(3 * NP * RS <= 2 * STG, "attention images fit in the staging buffers");
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int B = p.B, H = p.H, N = p.N, D = p.D;
-  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
-  const int tok = wave * 16 + li;  // this lane's token (phase A row, phase B query)
-  const int nk = D / 64;
-  const bf16* xbp = reinterpret_cast<const bf16*>(p.xb);
-  const bf16* wfp = reinterpret_cast<const bf16*>(p.wf);
-  bf16* qkvp = reinterpret_cast<bf16*>(p.qkv);
-
-  // ---- phase A: register-staged loads, double-buffered LDS chunks
-  u32x4 rx[PX], rw[PW];
-  auto load = [&](int kc) {
-#pragma unroll
-    for (int i = 0; i < PX; ++i) {
-      const int c = threadIdx.x + i * NT, r = c >> 3, pc = c & 7;
-      const int rr = r < N ? r : N - 1;
-      const u32x4 v = *reinterpret_cast<const u32x4*>(xbp + (size_t)(b * N + rr) * D + kc * 64 + pc * 8);
-      const u32x4 z = {0u, 0u, 0u, 0u};
-      rx[i] = r < N ? v : z;
-    }
-#pragma unroll
-    for (int i = 0; i < PW; ++i) {
-      const int c = threadIdx.x + i * NT, r = c >> 3, pc = c & 7;
-      const int rr = r < WR ? r : WR - 1;  // (PW * NT > WR * 8: the surplus pieces are not stored)
-      const int grow = (rr / HD) * D + h * HD + (rr % HD);  // q / k / v row of head h in [3D, D]
-      rw[i] = *reinterpret_cast<const u32x4*>(wfp + (size_t)grow * D + kc * 64 + pc * 8);
-    }
-  };
-  auto store = [&](char* buf) {
-#pragma unroll
-    for (int i = 0; i < PX; ++i) {
-      const int c = threadIdx.x + i * NT, r = c >> 3, pc = c & 7;
-      *reinterpret_cast<u32x4*>(buf + r * 128 + 16 * (pc ^ swz(r))) = rx[i];
-    }
-#pragma unroll
-    for (int i = 0; i < PW; ++i) {
-      const int c = threadIdx.x + i * NT, r = c >> 3, pc = c & 7;
-      if (PW * NT == WR * 8 || r < WR) *reinterpret_cast<u32x4*>(buf + XB + r * 128 + 16 * (pc ^ swz(r))) = rw[i];
-    }
-  };
-  // epilogue operands, issued with the first chunk: the row's statistics slots, c / b'
-  const int np_in = D / 32;  // slots per row (multiple of 4: D % 128 == 0)
-  const int m = b * N + (tok < N ? tok : N - 1);
-  float2 sl[4] = {};
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {  // slots g, g + 4, .. (np_in <= 64; constant register indices)
-    const int k = g + 4 * i;
-    if (k < np_in) {
-      const float2 v = *reinterpret_cast<const float2*>(p.st + 2 * ((size_t)m * np_in + k));
-      sl[i & 3].x += v.x;
-      sl[i & 3].y += v.y;
-    }
-  }
-  load(0);
-  store(lds);
-  __syncthreads();
-  f32x4 acc[FQ];
-#pragma unroll
-  for (int j = 0; j < FQ; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int kc = 0; kc < nk; ++kc) {
-    const bool more = kc + 1 < nk;
-    if (more) load(kc + 1);
-    const char* xs = lds + (kc & 1) * STG;
-    const char* ws = xs + XB;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bf16x8 xf = frag_k(xs, tok, s, g);
-#pragma unroll
-      for (int j = 0; j < FQ; ++j) acc[j] = mfma16(frag_k(ws, 16 * j + li, s, g), xf, acc[j]);
-    }
-    if (more) store(lds + ((kc + 1) & 1) * STG);
-    __syncthreads();
-  }
-  // fold consumer epilogue (swapped layout: lane = token row li of the wave, columns
-  // 16 j + 4 g .. + 3 of [q | k | v]); the row statistics in a fixed order
-  float2 s2 = make_float2((sl[0].x + sl[1].x) + (sl[2].x + sl[3].x), (sl[0].y + sl[1].y) + (sl[2].y + sl[3].y));
-  {
-    uint32_t ux = __float_as_uint(s2.x), uy = __float_as_uint(s2.y);
-    auto r16x = __builtin_amdgcn_permlane16_swap(ux, ux, false, false);
-    auto r16y = __builtin_amdgcn_permlane16_swap(uy, uy, false, false);
-    s2 = make_float2(__uint_as_float(r16x[0]) + __uint_as_float(r16x[1]),
-                     __uint_as_float(r16y[0]) + __uint_as_float(r16y[1]));
-    ux = __float_as_uint(s2.x);
-    uy = __float_as_uint(s2.y);
-    auto r32x = __builtin_amdgcn_permlane32_swap(ux, ux, false, false);
-    auto r32y = __builtin_amdgcn_permlane32_swap(uy, uy, false, false);
-    s2 = make_float2(__uint_as_float(r32x[0]) + __uint_as_float(r32x[1]),
-                     __uint_as_float(r32y[0]) + __uint_as_float(r32y[1]));
-  }
-  const float mu = s2.x * p.invd;
-  const float rstd = __builtin_amdgcn_rsqf(fmaxf(s2.y * p.invd - mu * mu, 0.f) + p.eps);
-  if (h == 0 && g == 0 && tok < N && p.mean_out != nullptr) {
-    p.mean_out[b * N + tok] = mu;
-    p.rstd_out[b * N + tok] = rstd;
-  }
-  char* Kl = lds;
-  char* Vl = lds + NP * RS;
-  char* Ql = lds + 2 * NP * RS;
-  const size_t mat = (size_t)N * HD;
-#pragma unroll
-  for (int j = 0; j < FQ; ++j) {
-    const int col = 16 * j + 4 * g, which = col / HD, d = col % HD;  // 4 columns inside one slice
-    const int gc = which * D + h * HD + d;
-    const f32x4 cv = *reinterpret_cast<const f32x4*>(p.c + gc);
-    const f32x4 bv = *reinterpret_cast<const f32x4*>(p.bf + gc);
-    bf16x4 v;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = f2bf(tok < N ? (acc[j][r] - mu * cv[r]) * rstd + bv[r] : 0.f);
-    if (tok < N)
-      *reinterpret_cast<bf16x4*>(qkvp + ((size_t)which * B * H + bh) * mat + (size_t)tok * HD + d) = v;
-    char* img = which == 0 ? Ql : (which == 1 ? Kl : Vl);
-    *reinterpret_cast<bf16x4*>(img + tok * RS + d * 2) = v;
-  }
-  __syncthreads();
-
-  // ---- phase B: attn_fwd_short_kernel on the LDS images
-  if (wave * 16 >= N) return;  // no barrier follows
-  bf16x8 qf[KS];
-#pragma unroll
-  for (int s = 0; s < KS; ++s) qf[s] = frag_row<HD>(Ql, tok, s, g);
-  const uint32_t salt = DROP ? site_salt(p.rng, p.site) : 0u;
-  const float sl2 = p.scale * LOG2E;
-  f32x4 st[KT];
-#pragma unroll
-  for (int t = 0; t < KT; ++t) {
-    st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < KS; ++s) st[t] = mfma16(frag_row<HD>(Kl, 16 * t + li, s, g), qf[s], st[t]);
-  }
-  float mx = -INFINITY;
-#pragma unroll
-  for (int t = 0; t < KT; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (16 * t + 16 > N && 16 * t + 4 * g + r >= N) st[t][r] = -INFINITY;
-      mx = fmaxf(mx, st[t][r]);
-    }
-  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-  mx *= sl2;
-  const float nmx = -mx;
-  float l = 0.f;
-  const uint32_t rowidx = (uint32_t)(((size_t)bh * N + tok) * attn_mask_ld(N));
-  const uint32_t pgs = DROP ? ((rowidx >> 1) + 2u * (uint32_t)g) * DROP_GOLDEN + salt : 0u;
-  const uint32_t thr2 = (p.thr >> 1) * 0x10001u;
-  // packed drop masks and short_drop_bit flags, as attn_fwd_short_kernel
-  uint32_t dm[KT][2], db = 0u;
-#pragma unroll
-  for (int t = 0; t < KT; ++t) {
-    if (DROP) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        dm[t][j] = drop_mask2(drop_mix(pgs + (uint32_t)(8 * t + j) * DROP_GOLDEN), thr2);
-        db |= dm[t][j] & ((1u << (2 * t + j)) | (1u << (16 + 2 * t + j)));
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float pv = fexp2(fmaf(st[t][r], sl2, nmx));
-      l += pv;
-      st[t][r] = pv;
-    }
-  }
-  if (DROP && p.keep_bits != nullptr) p.keep_bits[((size_t)bh * NP + tok) * 4 + g] = db;
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
-  f32x4 o[DT];
-#pragma unroll
-  for (int d = 0; d < DT; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int s2i = 0; s2i < NP / 32; ++s2i) {
-    const bf16x8 pb = DROP ? pack8_drop(st[2 * s2i], st[2 * s2i + 1], dm[2 * s2i], dm[2 * s2i + 1])
-                           : pack8(st[2 * s2i], st[2 * s2i + 1]);
-#pragma unroll
-    for (int d = 0; d < DT; ++d) o[d] = mfma16(frag_t<RS>(Vl, 16 * d, s2i, lane), pb, o[d]);
-  }
-  if (tok < N) {
-    const float inv = (DROP ? p.dsc : 1.f) / l;
-    bf16* orow = reinterpret_cast<bf16*>(p.out) + ((size_t)b * N + tok) * D + h * HD;
-#pragma unroll
-    for (int d = 0; d < DT; ++d) *reinterpret_cast<bf16x4*>(orow + 16 * d + 4 * g) = pack4(o[d] * inv);
-    if (g == 0) p.lse[(size_t)bh * N + tok] = (mx + log2f(l)) * LN2;
-  }
-}
-#define DC_INST_QKVA(HD, NP)                                                          \
-  template __global__ void qkv_attn_short_kernel<HD, NP, true>(QkvAttnParams);        \
-  template __global__ void qkv_attn_short_kernel<HD, NP, false>(QkvAttnParams);
-DC_INST_QKVA(32, 32) DC_INST_QKVA(32, 64) DC_INST_QKVA(32, 96) DC_INST_QKVA(32, 128)
-DC_INST_QKVA(64, 32) DC_INST_QKVA(64, 64) DC_INST_QKVA(64, 96) DC_INST_QKVA(64, 128)
-
-template <int HD, int NP>
-static void launch_qkv_attn(QkvAttnParams p, hipStream_t stream) {
-  constexpr int WR = 3 * HD, STG = NP * 128 + WR * 128;
-  constexpr int lds = 2 * STG;
-  static const bool attr = [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&qkv_attn_short_kernel<HD, NP, true>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&qkv_attn_short_kernel<HD, NP, false>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    return true;
-  }();
-  (void)attr;
-  if (p.thr)
-    hipLaunchKernelGGL((qkv_attn_short_kernel<HD, NP, true>), dim3(p.B * p.H), dim3(NP * 4), lds, stream, p);
-  else
-    hipLaunchKernelGGL((qkv_attn_short_kernel<HD, NP, false>), dim3(p.B * p.H), dim3(NP * 4), lds, stream, p);
-}
-
-
 }  // namespace dc
 
 using namespace dc;
@@ -1761,27 +1526,6 @@ void attn_fwd_launch(const void* qkv, void* o, float* lse, int B, int H, int N, 
     hipLaunchKernelGGL(attn_fwd_kernel<32>, grid, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc);
   else
     hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, stream, q, out, lse, B, H, N, scale, rng, site, thr, dsc);
-}
-
-bool qkv_attn_supported(int N, int hd, int D) {
-  return N >= 1 && N <= SHORT_MAX_N && (hd == 32 || hd == 64) && D % 128 == 0 && D % hd == 0 && D / 32 <= 64;
-}
-
-void qkv_attn_launch(QkvAttnParams p, int hd, double drop_p, hipStream_t stream) {
-  if (!qkv_attn_supported(p.N, hd, p.D)) throw std::runtime_error("qkv_attn: unsupported shape");
-  p.thr = drop_threshold_host(drop_p);
-  p.dsc = drop_p > 0 ? 1.f / (1.f - (float)drop_p) : 1.f;
-  p.invd = 1.f / (float)p.D;
-  const int np = (p.N + 31) / 32;
-#define DC_QKVA_GO(HDV)                                     \
-  switch (np) {                                             \
-    case 1: launch_qkv_attn<HDV, 32>(p, stream); break;     \
-    case 2: launch_qkv_attn<HDV, 64>(p, stream); break;     \
-    case 3: launch_qkv_attn<HDV, 96>(p, stream); break;     \
-    default: launch_qkv_attn<HDV, 128>(p, stream); break;   \
-  }
-  if (hd == 32) { DC_QKVA_GO(32) } else { DC_QKVA_GO(64) }
-#undef DC_QKVA_GO
 }
 
 void attn_bwd_launch(const void* dout, const void* qkv, const void* o, const float* lse, void* dqkv,

@@ -323,53 +323,6 @@ std::tuple<Tensor, Tensor> attn_fwd(Tensor qkv, double scale, Tensor rng, int64_
   return {o, lse};
 }
 
-// QKV projection (LayerNorm folded) + short-sequence attention forward in ONE launch
-// (attention.hip qkv_attn_short_kernel): the outputs of qkv_fwd(fold) then attn_fwd
-std::tuple<Tensor, Tensor, Tensor> qkv_attn_fwd(Tensor xb, Tensor wf, Tensor bf, Tensor c, Tensor st, double eps,
-                                                c10::optional<Tensor> mean_out, c10::optional<Tensor> rstd_out,
-                                                int64_t B, int64_t N, int64_t H, double scale, Tensor rng,
-                                                int64_t site, double p, c10::optional<Tensor> keep_out) {
-  CHECK_IN(xb, BF16); CHECK_IN(wf, BF16); CHECK_IN(bf, F32); CHECK_IN(c, F32); CHECK_IN(st, F32); check_rng(rng);
-  const c10::DeviceGuard guard(xb.device());
-  const int D = xb.size(-1), hd = D / H;
-  TORCH_CHECK(xb.numel() == B * N * D && D % H == 0, "qkv_attn: xb must be [B*N, D]");
-  TORCH_CHECK(wf.dim() == 2 && wf.size(0) == 3 * D && wf.size(1) == D && bf.numel() == 3 * D && c.numel() == 3 * D,
-              "qkv_attn: folded weight / bias / c shapes");
-  TORCH_CHECK(st.numel() == B * N * (D / 32) * 2, "qkv_attn: statistics slots must be [B*N, D/32, 2]");
-  TORCH_CHECK(qkv_attn_supported((int)N, hd, D), "qkv_attn: unsupported shape (N <= 128, hd 32 | 64, D % 128 == 0)");
-  TORCH_CHECK(p <= 0 || (int64_t)B * H * N * ((N + 3) & ~3) < ((int64_t)1 << 32),
-              "attention dropout: more than 2^32 mask elements");
-  QkvAttnParams q;
-  q.xb = xb.data_ptr();
-  q.wf = wf.data_ptr();
-  q.bf = bf.data_ptr<float>();
-  q.c = c.data_ptr<float>();
-  q.st = st.data_ptr<float>();
-  if (mean_out.has_value() && mean_out->defined()) {
-    TORCH_CHECK(rstd_out.has_value() && rstd_out->defined(), "mean_out needs rstd_out");
-    CHECK_IN((*mean_out), F32); CHECK_IN((*rstd_out), F32);
-    TORCH_CHECK(mean_out->numel() == B * N && rstd_out->numel() == B * N, "mean / rstd shapes");
-    q.mean_out = mean_out->data_ptr<float>();
-    q.rstd_out = rstd_out->data_ptr<float>();
-  }
-  auto qkv = at::empty({3, B, H, N, hd}, xb.options());
-  auto o = at::empty({B, N, D}, xb.options());
-  auto lse = at::empty({B, H, N}, xb.options().dtype(F32));
-  q.qkv = qkv.data_ptr();
-  q.out = o.data_ptr();
-  q.lse = lse.data_ptr<float>();
-  q.keep_bits = keep_ptr(keep_out, (int)B, (int)H, (int)N, hd);
-  q.B = (int)B; q.H = (int)H; q.N = (int)N; q.D = D;
-  q.eps = (float)eps;
-  q.scale = (float)scale;
-  q.rng = rng.data_ptr<int64_t>();
-  q.site = (int)site;
-  qkv_attn_launch(q, hd, p, cur_stream());
-  return {qkv, o, lse};
-}
-
-bool qkv_attn_supported_op(int64_t N, int64_t hd, int64_t D) { return qkv_attn_supported((int)N, (int)hd, (int)D); }
-
 Tensor linear_residual_fwd(Tensor a, Tensor w, Tensor b, Tensor x, int64_t N, Tensor rng, int64_t site_drop,
                            double p_drop, int64_t site_dp, double p_dp, c10::optional<Tensor> st_out, c10::optional<Tensor> xb_out) {
   CHECK_IN(a, BF16); CHECK_IN(w, BF16); CHECK_IN(b, F32); CHECK_IN(x, F32); check_rng(rng);
@@ -757,75 +710,6 @@ void linear_wgrad_multi(std::vector<Tensor> dys, std::vector<Tensor> xs, std::ve
   }
 }
 
-// dy @ W followed by the LayerNorm backward in ONE launch (csrc/gemm_lnbwd.hip): same
-// arguments and outputs as layernorm_bwd(linear_dgrad(dy, w), x, ...) with x bf16
-std::tuple<Tensor, Tensor> linear_dgrad_lnbwd(Tensor dy, Tensor w, Tensor x, Tensor mean, Tensor rstd, Tensor gamma,
-                                              c10::optional<Tensor> g_res, Tensor dgamma, Tensor dbeta, int64_t N,
-                                              Tensor rng, int64_t site_drop, double p_drop, int64_t site_dp,
-                                              double p_dp, bool emit_gy, c10::optional<Tensor> ws,
-                                              c10::optional<Tensor> beta, c10::optional<Tensor> y_out) {
-  CHECK_IN(dy, BF16); CHECK_IN(w, BF16); CHECK_IN(x, BF16);
-  CHECK_IN(mean, F32); CHECK_IN(rstd, F32); CHECK_IN(gamma, F32); CHECK_IN(dgamma, F32); CHECK_IN(dbeta, F32);
-  check_rng(rng);
-  const c10::DeviceGuard guard(x.device());
-  const int D = x.size(-1), M = x.numel() / D;
-  TORCH_CHECK(w.dim() == 2 && w.size(1) == D, "linear_dgrad_lnbwd: w must be [K, D]");
-  const int K = w.size(0);
-  TORCH_CHECK(gemm_lnbwd_supported(D, K), "linear_dgrad_lnbwd: unsupported D / K (D 256 | 384, K % 64 == 0)");
-  TORCH_CHECK(dy.numel() == (int64_t)M * K && dy.size(-1) == K, "linear_dgrad_lnbwd: dy must be [M, K]");
-  TORCH_CHECK(mean.numel() == M && rstd.numel() == M && gamma.numel() == D && dgamma.numel() == D &&
-                  dbeta.numel() == D && M % N == 0 && (int64_t)M * D < ((int64_t)1 << 31),
-              "linear_dgrad_lnbwd shapes");
-  LnBwdParams p;
-  p.dy = dy.data_ptr();
-  p.w = w.data_ptr();
-  p.M = M;
-  p.K = K;
-  p.x = x.data_ptr();
-  p.mean = mean.data_ptr<float>();
-  p.rstd = rstd.data_ptr<float>();
-  p.gamma = gamma.data_ptr<float>();
-  if (g_res.has_value() && g_res->defined()) {
-    CHECK_IN((*g_res), F32);
-    TORCH_CHECK(g_res->numel() == x.numel(), "g_res shape");
-    p.g_res = g_res->data_ptr<float>();
-  }
-  const int R = ln_replicas();
-  const bool own_ws = !(ws.has_value() && ws->defined());
-  const auto f32o = x.options().dtype(F32);
-  Tensor wsp = own_ws ? at::zeros({R, 2 * D}, f32o) : *ws;
-  if (!own_ws) {
-    CHECK_IN(wsp, F32);
-    TORCH_CHECK(wsp.numel() == (int64_t)R * 2 * D, "ln ws must hold ln_replicas x 2D floats");
-  }
-  p.ws = wsp.data_ptr<float>();
-  p.replicas = R;
-  if (y_out.has_value() && y_out->defined()) {
-    TORCH_CHECK(beta.has_value() && beta->defined(), "y_out needs beta");
-    CHECK_IN((*beta), F32); CHECK_IN((*y_out), BF16);
-    TORCH_CHECK(beta->numel() == D && y_out->numel() == x.numel(), "beta / y_out shapes");
-    p.beta = beta->data_ptr<float>();
-    p.y_out = y_out->data_ptr();
-  }
-  auto g_out = at::empty(x.sizes(), f32o);
-  Tensor gy = emit_gy ? at::empty({M, D}, x.options().dtype(BF16)) : at::empty({0}, x.options().dtype(BF16));
-  p.g_out = g_out.data_ptr<float>();
-  p.gy = emit_gy ? gy.data_ptr() : nullptr;
-  p.tokens = (int)N;
-  p.rng = rng.data_ptr<int64_t>();
-  p.site_drop = (int)site_drop;
-  p.site_dp = (int)site_dp;
-  gemm_lnbwd_launch(p, D, p_drop, p_dp, cur_stream());
-  if (own_ws) {
-    auto s = wsp.sum(0);
-    dgamma.add_(s.narrow(0, 0, D));
-    dbeta.add_(s.narrow(0, D, D));
-  }
-  return {g_out, gy};
-}
-
-bool lnbwd_fused_supported(int64_t D, int64_t K) { return gemm_lnbwd_supported((int)D, (int)K); }
-
 // fp32 <-> bf16 gradient wire (csrc/comm_wire.hip): one fused 16-B-vector
 // kernel each way (the torch-collective bf16 wire path of the train engine)
 void wire_pack(Tensor src, Tensor dst) {
@@ -840,69 +724,6 @@ void wire_unpack(Tensor src, Tensor dst) {
   const c10::DeviceGuard guard(src.device());
   wire_unpack_launch(src.data_ptr(), dst.data_ptr<float>(), src.numel(), cur_stream());
 }
-
-// LayerNorm backward fused into the input-gradient GEMM that consumes its output
-// (gemm_lnpro.hip): the outputs of layernorm_bwd(dl, x, ..., emit_gy=True, ws) and of
-// linear_dgrad(gy, w) (u == None) or linear_dgrad_gelu(gy, w, u, rng, gsite, gp).
-// Returns (g_out, gy, out).
-std::tuple<Tensor, Tensor, Tensor> lnbwd_dgrad(Tensor dl, Tensor x, Tensor mean, Tensor rstd, Tensor gamma,
-                                               c10::optional<Tensor> g_res, int64_t N, Tensor rng, int64_t site_drop,
-                                               double p_drop, int64_t site_dp, double p_dp, Tensor ws,
-                                               c10::optional<Tensor> beta, c10::optional<Tensor> y_out, Tensor w,
-                                               c10::optional<Tensor> u, int64_t gsite, double gp) {
-  CHECK_IN(dl, BF16); CHECK_IN(x, BF16); CHECK_IN(w, BF16);
-  CHECK_IN(mean, F32); CHECK_IN(rstd, F32); CHECK_IN(gamma, F32); CHECK_IN(ws, F32);
-  check_rng(rng);
-  const c10::DeviceGuard guard(x.device());
-  const int D = x.size(-1), M = x.numel() / D;
-  TORCH_CHECK(w.dim() == 2 && w.size(0) == D, "lnbwd_dgrad: w must be [D, N] (nn.Linear weight with in-features D)");
-  const int Nw = w.size(1);
-  TORCH_CHECK(gemm_lnpro_supported(D, D, Nw), "lnbwd_dgrad: D 256 | 384, N % 64 == 0");
-  TORCH_CHECK(dl.numel() == x.numel() && mean.numel() == M && rstd.numel() == M && gamma.numel() == D && M % N == 0 &&
-                  ws.numel() == (int64_t)ln_replicas() * 2 * D && (int64_t)M * std::max(D, Nw) < ((int64_t)1 << 31),
-              "lnbwd_dgrad shapes");
-  LnProParams q;
-  q.dl = dl.data_ptr(); q.x = x.data_ptr();
-  q.mean = mean.data_ptr<float>(); q.rstd = rstd.data_ptr<float>(); q.gamma = gamma.data_ptr<float>();
-  if (g_res.has_value() && g_res->defined()) {
-    CHECK_IN((*g_res), F32);
-    TORCH_CHECK(g_res->numel() == x.numel(), "g_res shape");
-    q.g_res = g_res->data_ptr<float>();
-  }
-  if (y_out.has_value() && y_out->defined()) {
-    TORCH_CHECK(beta.has_value() && beta->defined(), "y_out needs beta");
-    CHECK_IN((*beta), F32); CHECK_IN((*y_out), BF16);
-    TORCH_CHECK(beta->numel() == D && y_out->numel() == x.numel(), "beta / y_out shapes");
-    q.beta = beta->data_ptr<float>();
-    q.y_out = y_out->data_ptr();
-  }
-  auto g_out = at::empty(x.sizes(), x.options().dtype(F32));
-  auto gy = at::empty({M, D}, x.options().dtype(BF16));
-  auto out = at::empty({M, Nw}, x.options().dtype(BF16));
-  q.g_out = g_out.data_ptr<float>();
-  q.gy = gy.data_ptr();
-  q.ws = ws.data_ptr<float>();
-  q.replicas = ln_replicas();
-  q.tokens = (int)N;
-  q.rng = rng.data_ptr<int64_t>();
-  q.site_drop = (int)site_drop;
-  q.site_dp = (int)site_dp;
-  GemmArgs g;
-  g.B = w.data_ptr();
-  g.M = M; g.N = Nw; g.K = D; g.lda = D; g.ldb = Nw;
-  g.C = out.data_ptr(); g.ldc = Nw;
-  const bool gelu = u.has_value() && u->defined();
-  if (gelu) {
-    CHECK_IN((*u), BF16);
-    TORCH_CHECK(u->numel() == (int64_t)M * Nw, "u shape");
-    g.aux = u->data_ptr();
-    g.rng = rng.data_ptr<int64_t>(); g.site_drop = (int)gsite; g.p_drop = gp;
-  }
-  gemm_lnpro_launch(g, gelu ? EPI_DGELU : EPI_BF16, q, p_drop, p_dp, cur_stream());
-  return {g_out, gy, out};
-}
-
-bool lnpro_supported_op(int64_t D, int64_t K, int64_t N) { return gemm_lnpro_supported((int)D, (int)K, (int)N); }
 
 std::tuple<Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma,
                                          c10::optional<Tensor> g_res, Tensor dgamma, Tensor dbeta, int64_t N,
@@ -1243,23 +1064,11 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("img_to_tokgrad(Tensor dimg, int N, int patch) -> Tensor");
   m.def("linear_dgrad(Tensor dy, Tensor w, bool out_fp32, int splits=1) -> Tensor");
   m.def("linear_dgrad_gelu(Tensor dy, Tensor w, Tensor u, Tensor rng, int site, float p) -> Tensor");
-  m.def("lnbwd_dgrad(Tensor dl, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor? g_res, int N, Tensor rng, "
-        "int site_drop, float p_drop, int site_dp, float p_dp, Tensor(a!) ws, Tensor? beta, Tensor(b!)? y_out, "
-        "Tensor w, Tensor? u, int gsite, float gp) -> (Tensor, Tensor, Tensor)");
-  m.def("lnpro_supported(int D, int K, int N) -> bool", &lnpro_supported_op);
   m.def("linear_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, Tensor(b!)? db) -> ()");
   m.def("wire_pack(Tensor src, Tensor(a!) dst) -> ()");
   m.def("wire_unpack(Tensor src, Tensor(a!) dst) -> ()");
   m.def("linear_wgrad_multi(Tensor[] dys, Tensor[] xs, Tensor(a!)[] dws, Tensor(b!)?[] dbs, bool store=False, "
         "Tensor(c!)? sq_parts=None, Tensor? arena=None, int lz_lo=0, int lz_hi=0) -> ()");
-  m.def("qkv_attn_fwd(Tensor xb, Tensor wf, Tensor bf, Tensor c, Tensor st, float eps, Tensor(a!)? mean_out, "
-        "Tensor(b!)? rstd_out, int B, int N, int H, float scale, Tensor rng, int site, float p, "
-        "Tensor(c!)? keep_out=None) -> (Tensor, Tensor, Tensor)");
-  m.def("qkv_attn_supported(int N, int hd, int D) -> bool", &qkv_attn_supported_op);
-  m.def("linear_dgrad_lnbwd(Tensor dy, Tensor w, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor? g_res, "
-        "Tensor(a!) dgamma, Tensor(b!) dbeta, int N, Tensor rng, int site_drop, float p_drop, int site_dp, "
-        "float p_dp, bool emit_gy, Tensor(c!)? ws=None, Tensor? beta=None, Tensor(d!)? y_out=None) -> (Tensor, Tensor)");
-  m.def("lnbwd_fused_supported(int D, int K) -> bool", &lnbwd_fused_supported);
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor? g_res, "
         "Tensor(a!) dgamma, Tensor(b!) dbeta, int N, Tensor rng, int site_drop, float p_drop, int site_dp, "
         "float p_dp, bool emit_gy, Tensor(c!)? ws=None, Tensor? beta=None, Tensor(d!)? y_out=None) -> (Tensor, Tensor)");
@@ -1306,7 +1115,6 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("img_to_tokgrad", &img_to_tokgrad);
   m.impl("linear_dgrad", &linear_dgrad);
   m.impl("linear_dgrad_gelu", &linear_dgrad_gelu);
-  m.impl("lnbwd_dgrad", &lnbwd_dgrad);
   m.impl("linear_wgrad", &linear_wgrad);
   m.impl("head_step_", &head_step_);
   m.impl("head_step_rows_", &head_step_rows_);
@@ -1315,8 +1123,6 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("wire_pack", &wire_pack);
   m.impl("wire_unpack", &wire_unpack);
   m.impl("layernorm_bwd", &layernorm_bwd);
-  m.impl("linear_dgrad_lnbwd", &linear_dgrad_lnbwd);
-  m.impl("qkv_attn_fwd", &qkv_attn_fwd);
   m.impl("replica_reduce_", &replica_reduce_);
   m.impl("ln_fold_", &ln_fold_);
   m.impl("attn_bwd", &attn_bwd);

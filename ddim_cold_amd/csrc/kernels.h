@@ -118,87 +118,6 @@ void layernorm_bwd_launch(const void* dy, bool dy_bf16, const void* x, bool x_bf
                           double p_dp, int dy_parts, hipStream_t stream);
 int ln_replicas();
 
-// LayerNorm backward as the prologue of the input-gradient GEMM consuming its output
-// (gemm_lnpro.hip): the outputs of layernorm_bwd_launch (x and dl bf16) plus the GEMM
-// gy W with the consumer's epilogue (EPI_BF16 / EPI_DGELU); the GEMM's K is D.
-struct LnProParams {
-  const void* dl = nullptr;     // [M][D] gradient of the LayerNorm output (bf16)
-  const void* x = nullptr;      // [M][D] LayerNorm input (bf16 copy)
-  const float* mean = nullptr;
-  const float* rstd = nullptr;
-  const float* gamma = nullptr;
-  const float* beta = nullptr;  // with y_out
-  const float* g_res = nullptr; // [M][D] residual gradient (optional)
-  float* g_out = nullptr;       // [M][D]
-  void* gy = nullptr;           // [M][D] bf16
-  void* y_out = nullptr;        // [M][D] bf16, optional
-  float* ws = nullptr;          // [replicas][2D] dgamma || dbeta partials
-  int replicas = 1;
-  int tokens = 1;
-  const int64_t* rng = nullptr;
-  int site_drop = 0;
-  uint32_t thr_drop = 0;
-  float sc_drop = 1.f;
-  int site_dp = 0;
-  uint32_t thr_dp = 0;
-  float sc_dp = 1.f;
-};
-bool gemm_lnpro_supported(int D, int K, int N);
-// a: the consumer GEMM (B = W [D][N] nn.Linear weight, M, N, K = D, C, epilogue extras)
-void gemm_lnpro_launch(const GemmArgs& a, int epi, LnProParams q, double p_drop, double p_dp, hipStream_t stream);
-
-// input-gradient GEMM + LayerNorm backward in one launch (gemm_lnbwd.hip): the outputs
-// of linear_dgrad followed by layernorm_bwd_launch (x bf16, fp32 dl never materialised)
-struct LnBwdParams {
-  const void* dy = nullptr;    // [M][K] gradient of the GEMM output (A)
-  const void* w = nullptr;     // [K][D] nn.Linear weight (B, transposed operand)
-  int M = 0, K = 0;
-  const void* x = nullptr;     // [M][D] LayerNorm input (bf16 copy)
-  const float* mean = nullptr;
-  const float* rstd = nullptr;
-  const float* gamma = nullptr;
-  const float* beta = nullptr;  // with y_out
-  const float* g_res = nullptr; // [M][D] residual gradient (optional)
-  float* g_out = nullptr;       // [M][D]
-  void* gy = nullptr;           // [M][D] optional
-  void* y_out = nullptr;        // [M][D] optional
-  float* ws = nullptr;          // [replicas][2D] dgamma || dbeta partials (+=)
-  int replicas = 16;
-  int tokens = 1;
-  const int64_t* rng = nullptr;
-  int site_drop = 0, site_dp = 0;
-  uint32_t thr_drop = 0, thr_dp = 0;
-  float sc_drop = 1.f, sc_dp = 1.f;
-};
-bool gemm_lnbwd_supported(int D, int K);
-
-// the block's QKV Linear (LayerNorm folded) + the short-sequence attention forward in
-// one launch (attention.hip qkv_attn_short_kernel); outputs = ops.qkv_fwd(fold) then
-// ops.attn_fwd: qkv [3][B][H][N][hd], out [B*N][D], lse, keep words, mean / rstd
-struct QkvAttnParams {
-  const void* xb = nullptr;   // [B*N][D] LayerNorm input (bf16 copy)
-  const void* wf = nullptr;   // [3D][D] gamma-scaled QKV weight
-  const float* bf = nullptr;      // [3D] folded bias
-  const float* c = nullptr;       // [3D] row sums of wf
-  const float* st = nullptr;      // [B*N][D/32][2] {sum, sum^2} slots of x
-  float* mean_out = nullptr;      // [B*N] optional (saved for the LayerNorm backward)
-  float* rstd_out = nullptr;
-  void* qkv = nullptr;
-  void* out = nullptr;
-  float* lse = nullptr;
-  uint32_t* keep_bits = nullptr;
-  int B = 0, H = 0, N = 0, D = 0;
-  float eps = 1e-5f, invd = 0.f, scale = 1.f;
-  const int64_t* rng = nullptr;
-  int site = 0;
-  uint32_t thr = 0;
-  float dsc = 1.f;
-};
-bool qkv_attn_supported(int N, int hd, int D);
-void qkv_attn_launch(QkvAttnParams p, int hd, double drop_p, hipStream_t stream);
-// p_drop / p_dp: dropout and drop-path probabilities of gy (thresholds / scales set here)
-void gemm_lnbwd_launch(LnBwdParams p, int D, double p_drop, double p_dp, hipStream_t stream);
-
 // LayerNorm fold weights for the GEMMs that consume a LayerNorm (layernorm.hip)
 constexpr int FOLD_MAX = 32;  // GEMMs per fold launch (vit_small_200: 25 in one launch)
 struct FoldJob {

@@ -45,38 +45,6 @@ DGRAD_BF16 = True
 # operand the folded GEMM normalised in the forward -- instead of the fp32 residual
 # stream: 2 of its 18 bytes per element, and the fp32 block inputs are not saved
 LN_BWD_XB = True
-# the input-gradient GEMM feeding a LayerNorm backward (head, fc1, QKV) and that
-# LayerNorm backward as ONE launch (csrc/gemm_lnbwd.hip: full-row tiles, the LN
-# backward in the GEMM epilogue, the bf16 dl hand-off gone) where the shapes allow
-# (ops.lnbwd_fused_ok); False: linear_dgrad + layernorm_bwd (tests compare the two).
-# Measured SLOWER at every shape and off (profiles/fused_ln_qkv_r5_ab.txt): each
-# full-row workgroup streams the whole [K, D] weight through its CU (~70 GB/s per CU
-# from L2) and ViT-tiny has only M / 32 = 65 of them -- ViT-tiny 0.722 -> 0.858 ms/step
-# (fc1 input gradient + LN2 27.4 us vs 11.2 for the two launches), vit_small_200
-# 6.00 -> 6.63 ms; fusing only the head (K <= 512) still 0.720 -> 0.770
-FUSE_LN_BWD = False
-# ... only for reduction dims up to this
-FUSE_LN_BWD_MAX_K = 1 << 30
-# short sequences (ViT-tiny: 65 tokens): the block's QKV projection and the attention
-# forward as ONE launch (ops.qkv_attn_fwd: each (sample, head) workgroup computes its
-# q / k / v and attends from LDS); False: qkv_fwd + attn_fwd (tests compare the two).
-# Measured slower and off: 14.7 us per block vs 6.8 + 5.8 for the two launches (the
-# per-head GEMM of 384 workgroups with register-staged operands is slower than the
-# 390-tile LDS-DMA GEMM; ViT-tiny 0.8533 vs 0.8604 ms/step with the fused LN on)
-FUSE_QKV_ATTN = False
-# every LayerNorm backward whose gy feeds an input-gradient GEMM with K = D (the final
-# norm and norm1 of blocks > 0 -> the fc2 input gradient of the block below, norm2 ->
-# the proj input gradient) runs as the PROLOGUE of that GEMM (ops.lnbwd_dgrad,
-# csrc/gemm_lnpro.hip: each workgroup computes the LayerNorm backward of its 32-row
-# panel into LDS); False: layernorm_bwd + the GEMM (tests compare the two).  Needs the
-# single deferred weight-gradient launch (a queued job may name an LN output that only
-# the next block's launch writes).  Measured slower and off (profiles/ln_prologue_r5.md):
-# every one of the N/64 column workgroups re-reads its 32 rows of dl, x and the fp32
-# residual gradient (6x the row bytes through each CU's ~70 GB/s ingest): ~13.7 us per
-# fused launch vs 5.7 + 6.5 for the two (ViT-tiny 0.727 -> 0.95 ms/step before the
-# dgamma / dbeta and staging fixes, still a loss after them)
-FUSE_LN_PRO = False
-FUSE_LN_PRO_ON_CPU = False  # tests: the same call sequence through the ops CPU fallbacks
 # GEMMs per LayerNorm-fold launch (csrc/kernels.h FOLD_MAX)
 FOLD_MAX = 32
 # LayerNorm fold (csrc/gemm.hip): every LayerNorm is folded into the GEMM that
@@ -411,15 +379,9 @@ class ViTProgram:
             x0, x0b = x, xb
             m1, r1 = stats()
             fold = (st[2 * i], bp.qkv_c, c.eps, m1, r1)
-            if FUSE_QKV_ATTN and xb.is_cuda and ops.qkv_attn_ok(N, D // c.heads, D):
-                keep = (ops.qkv_attn_keep_buffer(B, c.heads, N, D // c.heads, ad, dev)
-                        if save and STORE_ATTN_KEEP else None)
-                qkv, o, lse = ops.qkv_attn_fwd(xb, bp.qkv_wf, bp.qkv_bf, B, N, c.heads, fold, c.scale, rng, sa, ad,
-                                               keep_out=keep)
-            else:
-                qkv = ops.qkv_fwd(xb, bp.qkv_wf, bp.qkv_bf, B, N, c.heads, fold=fold)
-                keep = ops.attn_keep_buffer(qkv, ad) if save and STORE_ATTN_KEEP else None
-                o, lse = ops.attn_fwd(qkv, c.scale, rng, sa, ad, keep_out=keep)
+            qkv = ops.qkv_fwd(xb, bp.qkv_wf, bp.qkv_bf, B, N, c.heads, fold=fold)
+            keep = ops.attn_keep_buffer(qkv, ad) if save and STORE_ATTN_KEEP else None
+            o, lse = ops.attn_fwd(qkv, c.scale, rng, sa, ad, keep_out=keep)
             if save:
                 S.keeps.append(keep)
             o = o.view(M, D)
@@ -493,11 +455,12 @@ class ViTProgram:
         (:func:`ops.linear_wgrad_multi`), so the optimizer needs no sqnorm pass.
         Measured slower on MI355X and removed: weight gradients riding in the
         input-gradient launches, one grouped launch per block, a side-stream branch
-        for them, the proj input gradient inside the attention backward."""
+        for them, the proj input gradient inside the attention backward, the
+        LayerNorm backward in the epilogue or the prologue of its neighbouring GEMM
+        (profiles/fused_ln_qkv_r5_ab.txt, profiles/ln_prologue_r5.md)."""
         def ws(k):
             return None if ln_ws is None else ln_ws[k]
         bucketed = wgrad is None and wgrad_flush is not None
-        user_wgrad = wgrad is not None
         if wgrad_sq is not None and (bucketed or wgrad is not None):
             raise ValueError("wgrad_sq needs the single deferred weight-gradient launch")
         jobs = []
@@ -521,70 +484,27 @@ class ViTProgram:
         keep = []
 
         def dgrad_ln(dy, w, splits, x, *ln_args, **ln_kw):
-            """dy @ w, then the LayerNorm backward -- one launch when fused (keep: the
-            operand of the bf16 hand-off, if any, stays referenced)"""
-            if (FUSE_LN_BWD and x.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16
-                    and w.shape[0] <= FUSE_LN_BWD_MAX_K and ops.lnbwd_fused_ok(x.shape[-1], w.shape[0])):
-                return ops.linear_dgrad_lnbwd(dy, w, x, *ln_args, **ln_kw)
+            """dy @ w, then the LayerNorm backward (keep: the bf16 hand-off stays referenced)"""
             dl = ops.linear_dgrad(dy, w, f32, splits)
             keep.append(dl)
             return ops.layernorm_bwd(dl, x, *ln_args, **ln_kw)
-        # LayerNorm backward as the prologue of the GEMM consuming gy (FUSE_LN_PRO)
-        on_cpu = FUSE_LN_PRO_ON_CPU and not dtok.is_cuda  # the ops' CPU fallbacks, any shape / dtype
-        pro = (FUSE_LN_PRO and (dtok.is_cuda or on_cpu) and not bucketed and not user_wgrad
-               and QKV_DGRAD_SPLITS == 1
-               and (on_cpu or (DGRAD_BF16 and S.xL.dtype == torch.bfloat16
-                               and all(ops.lnpro_ok(D, bp.fc2_w) and ops.lnpro_ok(D, bp.proj_w) for bp in P.blocks))))
-        pend = None  # (dl, x, ln args, ln kwargs) of a LayerNorm backward waiting for its consumer
-
-        def ln_then(dl_args, w, u=None, gsite=0, gp=0.0):
-            """the pending LayerNorm backward fused with its consumer GEMM: (g_out, gy, out);
-            without a replica workspace (no ln_ws) dgamma / dbeta are added directly"""
-            dl, x, la, (dgam, dbet) = dl_args
-            wsl = la[10]
-            if wsl is None:
-                wsl = torch.zeros(ops.LN_REPLICAS, 2 * D, device=dl.device)
-                la = la[:10] + (wsl,) + la[11:]
-            res = ops.lnbwd_dgrad(dl, x, *la, w=w, u=u, gsite=gsite, gp=gp)
-            if dl_args[2][10] is None:
-                with torch.no_grad():
-                    dgam.add_(wsl[:, :D].sum(0))
-                    dbet.add_(wsl[:, D:].sum(0))
-            return res
 
         lf = ln_out(S.lf)
         _, _, _, _, sf2, sd2 = block_sites(L - 1)
-        if pro:
-            dl = ops.linear_dgrad(dtok, P.head_w, False, 1)
-            keep.append(dl)
-            pend = (dl, S.xL, (S.mf, S.rf, P.nw, None, N, rng, sf2, pd, sd2, dpr[L - 1], ws(0),
-                               P.nb if fold else None, lf if fold else None), (G.nw, G.nb))
-        else:
-            g, gy = dgrad_ln(dtok, P.head_w, 1, S.xL, S.mf, S.rf, P.nw, None, G.nw, G.nb, N, rng, sf2, pd, sd2,
-                             dpr[L - 1], True, ws(0), beta=P.nb if fold else None, y_out=lf if fold else None)
+        g, gy = dgrad_ln(dtok, P.head_w, 1, S.xL, S.mf, S.rf, P.nw, None, G.nw, G.nb, N, rng, sf2, pd, sd2,
+                         dpr[L - 1], True, ws(0), beta=P.nb if fold else None, y_out=lf if fold else None)
         wgrad(dtok, lf, G.head_w, G.head_b)
         for i in range(L - 1, -1, -1):
             x0, l1, m1, r1, qkv, o, lse, x1, l2, m2, r2, u, h = S.blocks[i]
             bp, bg = P.blocks[i], G.blocks[i]
             sa, sp, sd1, sf1, _, _ = block_sites(i)
-            if pend is not None:
-                g, gy, du = ln_then(pend, bp.fc2_w, u, sf1, pd)
-                pend = None
-            else:
-                du = ops.linear_dgrad_gelu(gy, bp.fc2_w, u, rng, sf1, pd)
+            du = ops.linear_dgrad_gelu(gy, bp.fc2_w, u, rng, sf1, pd)
             wgrad(gy, h, bg.fc2_w, bg.fc2_b)
             k2 = 1 + 2 * (L - 1 - i)
             l2 = ln_out(l2)
-            if pro:
-                dl = ops.linear_dgrad(du, bp.fc1_w, False, 1)
-                keep.append(dl)
-                g1, gy1, do = ln_then((dl, x1, (m2, r2, bp.n2w, g, N, rng, sp, pd, sd1, dpr[i], ws(k2),
-                                                bp.n2b if fold else None, l2 if fold else None), (bg.n2w, bg.n2b)),
-                                      bp.proj_w)
-            else:
-                g1, gy1 = dgrad_ln(du, bp.fc1_w, 1, x1, m2, r2, bp.n2w, g, bg.n2w, bg.n2b, N, rng, sp, pd, sd1,
-                                   dpr[i], True, ws(k2), beta=bp.n2b if fold else None, y_out=l2 if fold else None)
-                do = ops.linear_dgrad(gy1, bp.proj_w, False)
+            g1, gy1 = dgrad_ln(du, bp.fc1_w, 1, x1, m2, r2, bp.n2w, g, bg.n2w, bg.n2b, N, rng, sp, pd, sd1,
+                               dpr[i], True, ws(k2), beta=bp.n2b if fold else None, y_out=l2 if fold else None)
+            do = ops.linear_dgrad(gy1, bp.proj_w, False)
             wgrad(du, l2, bg.fc1_w, bg.fc1_b)
             wgrad(gy1, o, bg.proj_w, bg.proj_b)
             dqkv = ops.attn_bwd(do, qkv, o, lse, c.scale, rng, sa, ad,
@@ -592,13 +512,7 @@ class ViTProgram:
             qs = QKV_DGRAD_SPLITS if 3 * D >= 768 else 1
             l1 = ln_out(l1)
             fk = dict(beta=bp.n1b, y_out=l1) if fold else {}
-            if i > 0 and pro:
-                _, _, _, _, psf2, psd2 = block_sites(i - 1)
-                dl = ops.linear_dgrad(dqkv, bp.qkv_w, False, 1)
-                keep.append(dl)
-                pend = (dl, x0, (m1, r1, bp.n1w, g1, N, rng, psf2, pd, psd2, dpr[i - 1], ws(k2 + 1),
-                                 bp.n1b if fold else None, l1 if fold else None), (bg.n1w, bg.n1b))
-            elif i > 0:
+            if i > 0:
                 _, _, _, _, psf2, psd2 = block_sites(i - 1)
                 g, gy = dgrad_ln(dqkv, bp.qkv_w, qs, x0, m1, r1, bp.n1w, g1, bg.n1w, bg.n1b, N, rng, psf2, pd, psd2,
                                  dpr[i - 1], True, ws(k2 + 1), **fk)

@@ -138,35 +138,6 @@ class gemm_tile:
         return False
 
 
-def qkv_attn_ok(N: int, hd: int, D: int) -> bool:
-    """Shapes :func:`qkv_attn_fwd` runs as one launch (the short-sequence attention path)."""
-    return 1 <= N <= 128 and hd in (32, 64) and D % 128 == 0 and D % hd == 0 and D // 32 <= 64
-
-
-def qkv_attn_keep_buffer(B: int, H: int, N: int, hd: int, p: float, device):
-    """The keep-flag buffer of :func:`qkv_attn_fwd` (see :func:`attn_keep_buffer`)."""
-    if p <= 0 or torch.device(device).type != "cuda":
-        return None
-    n = int(_ops().attn_keep_words(B, H, N, hd))
-    return torch.empty(n, dtype=torch.int32, device=device) if n > 0 else None
-
-
-def qkv_attn_fwd(xb, wf, bf, B: int, N: int, H: int, fold, scale: float, rng, site: int, p: float, keep_out=None):
-    """:func:`qkv_fwd` (LayerNorm folded: ``fold = (ln_st, ln_c, eps, mean_out,
-    rstd_out)``) followed by :func:`attn_fwd`, as ONE launch on the GPU for short
-    sequences (csrc/attention.hip qkv_attn_short_kernel: the head's q / k / v computed
-    by its attention workgroup, written for the backward and kept in LDS).  Returns
-    ``(qkv, o, lse)``, the same values (summation order aside) and the same dropout
-    keep flags as the two-launch path."""
-    st, c, eps, mean, rstd = _fold_args(fold)
-    if _hip(xb):
-        return _ops().qkv_attn_fwd(xb, wf, bf, c, st, float(eps), mean, rstd, B, N, H, float(scale), rng, site,
-                                   float(p), keep_out)
-    qkv = qkv_fwd(xb, wf, bf, B, N, H, fold=fold)
-    o, lse = attn_fwd(qkv, scale, rng, site, p)
-    return qkv, o, lse
-
-
 def attn_keep_buffer(qkv, p: float):
     """int32 buffer for the attention-dropout keep flags the forward stores for its
     backward (short sequences: one word per lane; long ones: one 64-bit word per
@@ -418,53 +389,6 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dgamma, dbeta, N: int, rng, s
         ref.layernorm_out_(x, mean, rstd, gamma, beta, y_out)
     return ref.layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dgamma, dbeta, N, rng, site_drop, p_drop,
                              site_dp, p_dp, emit_gy)
-
-
-def lnpro_ok(D: int, w) -> bool:
-    """Shapes :func:`lnbwd_dgrad` runs as one launch: D 256 / 384 and the consumer's
-    nn.Linear weight ``w`` [out = D, in = N] with N % 64 == 0."""
-    return D in (256, 384) and w.dim() == 2 and w.shape[0] == D and w.shape[1] % 64 == 0
-
-
-def lnbwd_dgrad(dl, x, mean, rstd, gamma, g_res, N: int, rng, site_drop: int, p_drop: float, site_dp: int,
-                p_dp: float, ws, beta, y_out, w, u=None, gsite: int = 0, gp: float = 0.0):
-    """``g_out, gy = layernorm_bwd(dl, x, ..., emit_gy=True, ws)`` and the input-gradient
-    GEMM consuming gy -- ``linear_dgrad(gy, w)`` (``u`` None) or
-    ``linear_dgrad_gelu(gy, w, u, rng, gsite, gp)`` -- as ONE launch on the GPU
-    (csrc/gemm_lnpro.hip: each GEMM workgroup computes the LayerNorm backward of its row
-    panel into LDS).  ``dl`` and ``x`` bf16.  Returns ``(g_out, gy, out)``."""
-    if _hip(x):
-        return _ops().lnbwd_dgrad(dl, x, mean, rstd, gamma, g_res, N, rng, site_drop, float(p_drop), site_dp,
-                                  float(p_dp), ws, beta, y_out, w, u, gsite, float(gp))
-    D = x.shape[-1]
-    with torch.no_grad():  # an op, like the kernel: the replica views of ws take two in-place adds
-        g_out, gy = layernorm_bwd(dl, x, mean, rstd, gamma, g_res, ws[0, :D], ws[0, D:], N, rng, site_drop,
-                                  p_drop, site_dp, p_dp, True, ws, beta, y_out)
-        out = linear_dgrad(gy, w, False) if u is None else linear_dgrad_gelu(gy, w, u, rng, gsite, gp)
-    return g_out, gy, out
-
-
-def lnbwd_fused_ok(D: int, K: int) -> bool:
-    """Shapes :func:`linear_dgrad_lnbwd` runs as one launch (D 256 / 384, K % 64 == 0)."""
-    return D in (256, 384) and K % 64 == 0 and K >= 64
-
-
-def linear_dgrad_lnbwd(dy, w, x, mean, rstd, gamma, g_res, dgamma, dbeta, N: int, rng, site_drop: int,
-                       p_drop: float, site_dp: int, p_dp: float, emit_gy: bool, ws: Optional[torch.Tensor] = None,
-                       beta=None, y_out=None):
-    """``layernorm_bwd(linear_dgrad(dy, w), x, ...)`` as ONE launch on the GPU
-    (csrc/gemm_lnbwd.hip: full-row tiles, the LayerNorm backward in the GEMM epilogue;
-    the input gradient of the LayerNorm output is never materialised).  ``x`` is the
-    bf16 LayerNorm input; same outputs and replica-workspace semantics as
-    :func:`layernorm_bwd` (the GEMM result enters the LayerNorm backward in fp32, not
-    rounded to bf16 first)."""
-    if _hip(x):
-        g_out, gy = _ops().linear_dgrad_lnbwd(dy, w, x, mean, rstd, gamma, g_res, dgamma, dbeta, N, rng, site_drop,
-                                              float(p_drop), site_dp, float(p_dp), bool(emit_gy), ws, beta, y_out)
-        return g_out, (gy if emit_gy else None)
-    dl = linear_dgrad(dy, w, True)
-    return layernorm_bwd(dl, x, mean, rstd, gamma, g_res, dgamma, dbeta, N, rng, site_drop, p_drop, site_dp, p_dp,
-                         emit_gy, ws, beta, y_out)
 
 
 def ln_fold_(ws, gammas, betas, biases, wfs, cs, bfs, tail=None):

@@ -173,17 +173,12 @@ def _folded(m, named):
     return fold.attach(P)
 
 
-@pytest.mark.parametrize("ln_pro", [False, True])
 @pytest.mark.parametrize("cfg", [dict(img_size=[32, 32], patch_size=8, embed_dim=128, depth=3, num_heads=4),
                                  dict(img_size=[16, 16], patch_size=4, embed_dim=64, depth=2, num_heads=2)])
-def test_program_layernorm_fold_matches_autograd(fp32_reference, cfg, ln_pro, monkeypatch):
+def test_program_layernorm_fold_matches_autograd(fp32_reference, cfg):
     """LayerNorm fold (forward without LayerNorm launches: statistics from the producing
     epilogue, gamma/beta folded into the consumer GEMM, LayerNorm outputs re-emitted
-    by the backward) == autograd of the unfolded forward, all dropout sites active.
-    ``ln_pro``: the backward's call sequence with every LayerNorm backward but block 0's
-    norm1 deferred into its consumer GEMM (ops.lnbwd_dgrad, program.FUSE_LN_PRO)."""
-    from ddim_cold_amd.models import program
-    monkeypatch.setattr(program, "FUSE_LN_PRO_ON_CPU", ln_pro)
+    by the backward) == autograd of the unfolded forward, all dropout sites active."""
     torch.manual_seed(0)
     m = DiffusionVisionTransformer(drop_rate=0.1, attn_drop_rate=0.1, drop_path_rate=0.2, **cfg).train()
     with torch.no_grad():  # non-trivial LayerNorm affine parameters

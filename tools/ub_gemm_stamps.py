@@ -46,19 +46,6 @@ cases = [
     ("dgrad fp32 K=1152", lambda: ops.linear_dgrad(dy3, w3, True)),
     ("plain bf16", lambda: ops.linear_fwd(a, w, b)),
 ]
-# LayerNorm-backward prologue GEMM (csrc/gemm_lnpro.hip): phases = prologue (LN backward
-# into the LDS panel) / main loop / epilogue
-_g, _b = torch.randn(D, device=dev), torch.randn(D, device=dev)
-_mu, _rs = torch.randn(M, device=dev), torch.rand(M, device=dev) + 0.5
-_ws = torch.zeros(ops.LN_REPLICAS, 2 * D, device=dev)
-_y = torch.empty(M, D, dtype=torch.bfloat16, device=dev)
-_u = bf(M, D)
-cases += [
-    ("LN-bwd prologue + dgrad bf16", lambda: ops.lnbwd_dgrad(a, a, _mu, _rs, _g, x, N, r, 7, 0.1, 8, 0.1, _ws, _b, _y,
-                                                             w)),
-    ("LN-bwd prologue + dgrad DGELU", lambda: ops.lnbwd_dgrad(a, a, _mu, _rs, _g, x, N, r, 7, 0.1, 8, 0.1, _ws, _b,
-                                                              _y, w, _u, 9, 0.1)),
-]
 TILES = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [-1]
 buf = torch.zeros(6 << 17, dtype=torch.int32, device=dev)
 for (name0, fn), tile in [(c, tl) for c in cases for tl in TILES]:
