@@ -78,6 +78,9 @@ def parse_args(argv=None):
                          "run) or Gaussian DDIM (diffusion_loader.DiffusionDataset: q_sample, t in 0..1999)")
     ap.add_argument("--no-gaussian", action="store_true",
                     help="1 GPU: skip the extra Gaussian-DDIM training throughput key")
+    ap.add_argument("--no-hires", action="store_true",
+                    help="1 GPU: skip the extra vit_small_200 (200x200, BASELINE.json config 4) and "
+                         "oxford_flower training keys")
     ap.add_argument("--no-eager-baseline", action="store_true",
                     help="skip timing the plain eager PyTorch sampler (BASELINE.md's sampling comparator)")
     ap.add_argument("--no-vendor", action="store_true",
@@ -86,43 +89,76 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
-def _rank_entry(rank: int, world: int, port: int, argv):
+# Bounds that keep a hung multi-GPU run diagnosable inside the driver's 600 s limit
+# (ddim_cold_amd/parallel/watchdog.py): the process-group timeout, every rank's own
+# deadline (prints all ranks' last phases, then exits) and the self-spawning parent's.
+PG_TIMEOUT_S = int(os.environ.get("DDIM_COLD_PG_TIMEOUT_S", "120"))
+RANK_DEADLINE_S = float(os.environ.get("DDIM_COLD_DEADLINE_S", "450"))
+SPAWN_DEADLINE_S = float(os.environ.get("DDIM_COLD_SPAWN_DEADLINE_S", str(RANK_DEADLINE_S + 30)))
+
+
+def _rank_entry(rank: int, world: int, port: int, argv, phase_dir: str):
     """Spawned rank process (self-launch): torchrun-style env, then the benchmark."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world), DDIM_COLD_PHASE_DIR=phase_dir)
     run(parse_args(argv))
 
 
-def spawn_ranks(n: int, argv) -> int:
+def spawn_ranks(n: int, argv, deadline_s: float = None) -> int:
     """Launch ``n`` rank processes of this benchmark (spawn context) and wait; on the
     first non-zero exit the others are terminated.  The parent never initialises the
-    GPU (only counts devices), so the children own it.  Returns the exit code."""
+    GPU (only counts devices), so the children own it.  A wall-clock deadline
+    (``DDIM_COLD_SPAWN_DEADLINE_S``) bounds the whole launch: when it passes, the
+    parent prints every rank's last phase (watchdog.report_dir), terminates the
+    ranks and returns 124.  Returns the exit code."""
     import multiprocessing as mp
+    import shutil
+    import tempfile
     from ddim_cold_amd.parallel.dist import free_port
+    from ddim_cold_amd.parallel.watchdog import report_dir
+    deadline_s = SPAWN_DEADLINE_S if deadline_s is None else deadline_s
     ndev = torch.cuda.device_count()  # no HIP context is created by counting
     if 0 < ndev < n and not SHARED_GPU:
         print(f"bench.py: --gpus {n} but only {ndev} GPU(s) visible", file=sys.stderr)
         return 2
     ctx = mp.get_context("spawn")
     port = free_port()
-    procs = [ctx.Process(target=_rank_entry, args=(r, n, port, argv), name=f"rank{r}") for r in range(n)]
+    phase_dir = tempfile.mkdtemp(prefix="ddim_cold_phases_")
+    t0 = time.time()
+    procs = [ctx.Process(target=_rank_entry, args=(r, n, port, argv, phase_dir), name=f"rank{r}")
+             for r in range(n)]
     for p in procs:
         p.start()
     code = 0
-    while any(p.is_alive() for p in procs):
-        for p in procs:
-            p.join(timeout=0.2)
-            if p.exitcode not in (None, 0) and code == 0:
-                code = p.exitcode if p.exitcode > 0 else 1
-                print(f"bench.py: {p.name} exited with code {p.exitcode}; stopping the other ranks",
-                      file=sys.stderr)
+    try:
+        while any(p.is_alive() for p in procs):
+            for p in procs:
+                p.join(timeout=0.2)
+                if p.exitcode not in (None, 0) and code == 0:
+                    code = p.exitcode if p.exitcode > 0 else 1
+                    print(f"bench.py: {p.name} exited with code {p.exitcode}; stopping the other ranks\n"
+                          f"{report_dir(phase_dir, n, since=t0)}", file=sys.stderr, flush=True)
+                    for q in procs:
+                        if q.is_alive():
+                            q.terminate()
+            if code == 0 and time.time() - t0 > deadline_s:
+                code = 124
+                print(f"bench.py: launch deadline of {deadline_s:.0f}s passed; terminating the ranks\n"
+                      f"{report_dir(phase_dir, n, since=t0)}", file=sys.stderr, flush=True)
                 for q in procs:
                     if q.is_alive():
                         q.terminate()
-    for p in procs:
-        p.join()
-        if p.exitcode not in (0, None) and code == 0:
-            code = p.exitcode if p.exitcode > 0 else 1
+                t_kill = time.time() + 10
+                for q in procs:
+                    q.join(timeout=max(0.1, t_kill - time.time()))
+                    if q.is_alive():
+                        q.kill()
+        for p in procs:
+            p.join()
+            if p.exitcode not in (0, None) and code == 0:
+                code = p.exitcode if p.exitcode > 0 else 1
+    finally:
+        shutil.rmtree(phase_dir, ignore_errors=True)
     return code
 
 
@@ -145,16 +181,57 @@ def main(argv=None):
     return 0
 
 
+def _time_train(args, name, dataset, dev, lr, seed, prefix, pool=None):
+    """One extra 1-GPU training measurement outside the headline number: model
+    ``name`` on the ``dataset`` task at the headline's per-GPU batch, optimizer and
+    graph settings, ``--warmup`` untimed then exactly ``--steps`` timed steps between
+    synchronizes.  Returns ``{prefix_img_per_s, prefix_ms_per_step, prefix_final_loss}``."""
+    from ddim_cold_amd.models import build_model
+    from ddim_cold_amd.train.engine import EngineConfig, TrainEngine
+    from ddim_cold_amd.data.synthetic import ColdBatcher, GaussianBatcher, synthetic_pool
+    torch.manual_seed(1234)
+    m = build_model(name).to(dev).train()
+    if pool is None or tuple(pool.shape[-2:]) != tuple(m.img_size):
+        pool = synthetic_pool(1024, tuple(m.img_size), seed=7, device=dev)
+    cold = dataset == "cold"
+    e = TrainEngine(m, EngineConfig(lr=lr, t_max=512 * 100, use_graph=not args.no_graph, seed=seed,
+                                    temb_rows=int(math.log2(m.img_size[1])) + 1 if cold else None,
+                                    graph_steps=args.graph_steps), device=dev)
+    e.set_batch_fn(ColdBatcher(pool, args.batch, e.rng) if cold else
+                   GaussianBatcher(pool, args.batch, e.rng, m.total_steps))
+    e.train_steps(args.warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e.train_steps(args.steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    loss = float(e.loss_last.item())
+    if not math.isfinite(loss):
+        raise SystemExit(f"non-finite {prefix} loss {loss}")
+    e.close()
+    del e, m, pool
+    torch.cuda.empty_cache()
+    return {f"{prefix}_img_per_s": round(args.batch * args.steps / dt, 1),
+            f"{prefix}_ms_per_step": round(dt / args.steps * 1e3, 4),
+            f"{prefix}_final_loss": round(loss, 5)}
+
+
 def run(args):
     from ddim_cold_amd.parallel.dist import (init_distributed, init_single, all_reduce_max, barrier, cleanup,
                                              env_world)
+    from ddim_cold_amd.parallel import watchdog
+    from ddim_cold_amd.parallel.watchdog import phase
     world, rank, local = env_world()
     if SHARED_GPU:
         local = 0
+    # per-rank phase markers on stderr + a deadline that names every rank's last phase
+    watchdog.install(rank, world, deadline_s=RANK_DEADLINE_S)
+    phase("pg-init", world=world, timeout_s=PG_TIMEOUT_S)
     if args.force_dist and world == 1:
-        distributed = init_single(device_index=local)
+        distributed = init_single(device_index=local, timeout_s=PG_TIMEOUT_S)
     else:
-        distributed = init_distributed(backend="gloo" if SHARED_GPU else None)
+        distributed = init_distributed(backend="gloo" if SHARED_GPU else None, timeout_s=PG_TIMEOUT_S)
+    phase("pg-ready", backend=dist.get_backend() if dist.is_initialized() else "none")
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
@@ -179,7 +256,9 @@ def run(args):
                        graph_comm=not args.segmented_comm, grad_wire=args.grad_wire,
                        comm_events=not (args.segmented_comm or args.captured_comm),
                        comm="torch" if SHARED_GPU else args.comm, graph_steps=args.graph_steps)
+    phase("engine-build", model=args.model)
     engine = TrainEngine(model, cfg, device=dev)
+    phase("engine-ready", comm=engine.comm_backend if engine.segmented else "none")
     pool = synthetic_pool(1024, tuple(model.img_size), seed=7 + rank, device=dev)
     if args.dataset == "cold":
         engine.set_batch_fn(ColdBatcher(pool, args.batch, engine.rng))
@@ -192,6 +271,7 @@ def run(args):
         if n > 1:
             # measured all-reduce curve on this job's ranks -> fitted cost model, which
             # orders the bucket layouts (parallel/costmodel.py); outside the timed region
+            phase("probe-allreduce")
             try:
                 fit, probe = engine.probe_allreduce()
                 comm_model = {"probe_us": {f"{b / 2**20:g}MB": round(u, 1) for b, u in probe.items()},
@@ -202,15 +282,18 @@ def run(args):
                 comm_model = {"error": repr(e)[:200]}
                 engine.comm_fit = None
         if args.comm_layout == "auto":
+            phase("autotune")
             engine.autotune_comm()
         else:
             engine.apply_layout(args.comm_layout)
+    phase("warmup", steps=args.warmup, layout=engine.comm_choice)
     engine.train_steps(args.warmup)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
+    phase("timed", steps=args.steps)
     t0 = time.perf_counter()
     engine.train_steps(args.steps)
     if dev.type == "cuda":
@@ -219,6 +302,7 @@ def run(args):
     if dev.type == "cuda":
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    phase("timed-done", ms_per_step=round(elapsed / args.steps * 1e3, 4))
     elapsed = all_reduce_max(elapsed, dev)
     engine.check_comm()
     loss = float(engine.loss_last.item())
@@ -232,25 +316,19 @@ def run(args):
         # the reference's other training task (DiffusionDataset, diffusion_loader.py:24-58):
         # Gaussian DDIM, q_sample batch drawn inside the patch-embedding launch, same
         # model / batch / optimizer; timed the same way (outside the headline number)
-        torch.manual_seed(1234)
-        gm = build_model(args.model).to(dev).train()
-        ge = TrainEngine(gm, EngineConfig(lr=lr, t_max=512 * 100, use_graph=not args.no_graph, seed=43,
-                                          graph_steps=args.graph_steps), device=dev)
-        ge.set_batch_fn(GaussianBatcher(pool, args.batch, ge.rng, gm.total_steps))
-        ge.train_steps(args.warmup)
-        torch.cuda.synchronize()
-        tg = time.perf_counter()
-        ge.train_steps(args.steps)
-        torch.cuda.synchronize()
-        tg = time.perf_counter() - tg
-        gl = float(ge.loss_last.item())
-        if not math.isfinite(gl):
-            raise SystemExit(f"non-finite Gaussian-DDIM loss {gl}")
-        extra["gaussian_ddim_train_img_per_s"] = round(args.batch * args.steps / tg, 1)
-        extra["gaussian_ddim_train_ms_per_step"] = round(tg / args.steps * 1e3, 4)
-        extra["gaussian_ddim_final_loss"] = round(gl, 5)
-        ge.close()
-        del ge, gm
+        phase("extra:gaussian-ddim")
+        extra.update(_time_train(args, args.model, "gaussian", dev, lr, seed=43, pool=pool,
+                                 prefix="gaussian_ddim"))
+    if rank == 0 and n == 1 and args.dataset == "cold" and args.model == "vit_tiny" and not args.no_hires \
+            and dev.type == "cuda":
+        # BASELINE.json config 4 (the 200x200 high-resolution path) and the
+        # sampling CLI's oxford_flower model (ViT.py:277), trained the same way as the
+        # headline: same per-GPU batch, full AdamW step, K-step graphs, timed between
+        # synchronizes over exactly --steps steps after --warmup (1 GPU; the scaling
+        # curve is the headline model's)
+        for name, key in (("vit_small_200", "vit_small_200_train"), ("oxford_flower", "oxford_flower_train")):
+            phase(f"extra:{name}")
+            extra.update(_time_train(args, name, "cold", dev, lr, seed=44, prefix=key))
     if rank == 0 and n == 1 and args.dataset == "cold" and not args.no_vendor and dev.type == "cuda":
         # same-node vendor comparator: the reference step (multi_gpu_trainer.py:115-134) from stock
         # PyTorch-ROCm ops (hipBLASLt / SDPA / fused AdamW), captured whole in one graph
@@ -347,11 +425,12 @@ def run(args):
                                 f"heads={model.blocks[0].attn.num_heads}, patch={model.patch_size}, "
                                 f"{model.img_size[0]}x{model.img_size[1]})", "global_batch": args.batch * n,
                        "per_gpu_batch": args.batch, "seq_len": model.num_tokens, "parallelism": f"dp{n}",
-                       "graph": not args.no_graph,
+                       "graph": bool(engine.cfg.use_graph),
                        # event-split data parallel: two graphs per step, collectives between
                        "graph_steps": args.graph_steps if not (engine.segmented and engine.cfg.comm_events) else 1,
                        "bucket_blocks": engine.cfg.bucket_blocks if engine.segmented else None,
                        "allreduce": ("none" if not engine.segmented else "eager" if dev.type != "cuda" else
+                                     "eager-inline-fallback" if engine.comm_fallback else
                                      "host-issued-between-event-split-graphs" if engine.cfg.comm_events else
                                      "segmented" if (args.segmented_comm or getattr(engine, "_graph_comm_failed", False))
                                      else "captured-in-graph-inline" if engine.cfg.comm_inline
@@ -360,6 +439,8 @@ def run(args):
                        "autotune_dropped": getattr(engine, "autotune_errors", None) or None,
                        "grad_wire": args.grad_wire,
                        "comm": engine.comm_backend if engine.segmented else "none",
+                       "native_comm_error": engine.native_error,
+                       "comm_fallback": engine.comm_fallback,
                        "comm_layout": engine.comm_choice,
                        "handoff": engine.handoff_order,
                        "rccl_ranks": engine.ncomm.info()[0] if engine.ncomm is not None else
@@ -374,8 +455,10 @@ def run(args):
         if SHARED_GPU:  # not a scaling measurement: every rank on device 0 over gloo
             out["rehearsal_shared_gpu_gloo"] = True
         print(json.dumps(out), flush=True)
+    phase("teardown")
     engine.close()
     cleanup()
+    phase("done")
 
 
 if __name__ == "__main__":

@@ -25,8 +25,14 @@
 #include <c10/core/DeviceGuard.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <memory>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "kernels.h"
@@ -87,19 +93,77 @@ Tensor comm_unique_id() {
   return out;
 }
 
-int64_t comm_init(Tensor uid, int64_t world, int64_t rank, int64_t device) {
+// ncclCommInitRank blocks until every rank has joined and the transports are up; a
+// rank whose peers never arrive (or a transport setup that never completes) would
+// block the process forever.  The init runs on a helper thread and the caller waits
+// at most timeout_ms (0: no bound): on timeout this raises "comm_init timed out" and
+// the caller falls back to torch.distributed's communicator.  The helper thread is
+// detached and left behind (there is no handle to abort before the init returns);
+// comm_init_leaked() counts them.  A nonblocking communicator (config.blocking = 0)
+// would give an abortable handle, but it also makes every later RCCL call
+// asynchronous -- group launches from an RCCL thread -- which a thread-local
+// hipGraph capture of the step cannot record.
+// test_hang (testing only): the helper thread sleeps past the bound instead of
+// initialising (exercises the timeout / fallback path on one rank).
+struct InitJob {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool done = false;
+  ncclResult_t res = ncclSuccess;
+  ncclComm_t comm = nullptr;
+};
+std::atomic<int> g_init_leaked{0};
+
+int64_t comm_init(Tensor uid, int64_t world, int64_t rank, int64_t device, int64_t timeout_ms, bool test_hang) {
   TORCH_CHECK(!uid.is_cuda() && uid.scalar_type() == at::kByte && uid.numel() == NCCL_UNIQUE_ID_BYTES,
               "uid must be a CPU uint8 tensor of ", NCCL_UNIQUE_ID_BYTES, " bytes");
   TORCH_CHECK(world >= 1 && rank >= 0 && rank < world, "bad world/rank");
   ncclUniqueId id;
   std::memcpy(id.internal, uid.contiguous().data_ptr<uint8_t>(), sizeof(id.internal));
-  const c10::DeviceGuard guard(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
-  ncclComm_t comm;
-  NCCL_CHECK(ncclCommInitRank(&comm, (int)world, id, (int)rank));
+  auto job = std::make_shared<InitJob>();
+  const int dev = (int)device, nr = (int)world, r = (int)rank;
+  const int64_t sleep_ms = test_hang ? std::max<int64_t>(2 * timeout_ms, 1000) : 0;
+  std::thread th([job, id, dev, nr, r, sleep_ms]() {
+    ncclComm_t comm = nullptr;
+    ncclResult_t res = ncclSuccess;
+    if (sleep_ms > 0) {
+      std::this_thread::sleep_for(std::chrono::milliseconds(sleep_ms));
+      res = ncclInternalError;
+    } else {
+      (void)hipSetDevice(dev);
+      res = ncclCommInitRank(&comm, nr, id, r);
+    }
+    std::lock_guard<std::mutex> lk(job->mu);
+    job->res = res;
+    job->comm = comm;
+    job->done = true;
+    job->cv.notify_all();
+  });
+  bool done;
+  {
+    std::unique_lock<std::mutex> lk(job->mu);
+    if (timeout_ms > 0)
+      done = job->cv.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return job->done; });
+    else {
+      job->cv.wait(lk, [&] { return job->done; });
+      done = true;
+    }
+  }
+  if (!done) {
+    th.detach();
+    g_init_leaked.fetch_add(1);
+    TORCH_CHECK(false, "comm_init timed out after ", timeout_ms, " ms (rank ", rank, " of ", world,
+                "): ncclCommInitRank did not return");
+  }
+  th.join();
+  TORCH_CHECK(job->res == ncclSuccess, "RCCL error ", (int)job->res, " (", ncclGetErrorString(job->res),
+              ") at ncclCommInitRank");
   std::lock_guard<std::mutex> lk(g_mu);
-  g_comms.push_back(comm);
+  g_comms.push_back(job->comm);
   return (int64_t)g_comms.size() - 1;
 }
+
+int64_t comm_init_leaked() { return g_init_leaked.load(); }
 
 // In-place all-reduce of a contiguous GPU buffer on the current stream.
 void comm_all_reduce_(Tensor buf, int64_t h, int64_t op) {
@@ -291,7 +355,9 @@ TORCH_LIBRARY_FRAGMENT(ddim_cold, m) {
         "int timeout_us=0) -> ()", &pair_all_reduce_);
   m.def("pair_flags_size() -> int", &pair_flags_size);
   m.def("comm_unique_id() -> Tensor", &comm_unique_id);
-  m.def("comm_init(Tensor uid, int world, int rank, int device) -> int", &comm_init);
+  m.def("comm_init(Tensor uid, int world, int rank, int device, int timeout_ms=0, bool test_hang=False) -> int",
+        &comm_init);
+  m.def("comm_init_leaked() -> int", &comm_init_leaked);
   m.def("comm_all_reduce_(Tensor(a!) buf, int handle, int op=0) -> ()", &comm_all_reduce_);
   m.def("comm_all_reduce_many_(Tensor(a!)[] bufs, int handle, int op=0) -> ()", &comm_all_reduce_many_);
   m.def("comm_all_reduce_bf16_wire_(Tensor(a!) buf, Tensor(b!) scratch, int handle) -> ()",

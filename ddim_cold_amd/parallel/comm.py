@@ -163,7 +163,12 @@ class _LoopbackEndpoint:
 class NativeComm:
     """One RCCL communicator over the ranks of the default process group."""
 
-    def __init__(self, device: torch.device, key: Optional[str] = None):
+    def __init__(self, device: torch.device, key: Optional[str] = None, timeout_s: Optional[float] = None):
+        """``timeout_s`` bounds ``ncclCommInitRank`` (default
+        ``DDIM_COLD_NATIVE_INIT_TIMEOUT_S``, 90 s; 0: unbounded): past it the init raises
+        instead of blocking the process forever (csrc/comm.cpp comm_init).  Testing:
+        ``DDIM_COLD_TEST_NATIVE_INIT=fail`` raises before the init, ``=hang`` makes the
+        init time out."""
         if not dist.is_initialized():
             raise RuntimeError("NativeComm needs an initialised torch.distributed process group (rendezvous)")
         _ext.load(raise_on_error=True)
@@ -180,7 +185,14 @@ class NativeComm:
         raw = store.get(key)  # blocks until rank 0 has published the id
         uid = torch.tensor(list(raw), dtype=torch.uint8)
         idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
-        self.handle = int(torch.ops.ddim_cold.comm_init(uid, self.world, self.rank, idx))
+        if timeout_s is None:
+            timeout_s = float(os.environ.get("DDIM_COLD_NATIVE_INIT_TIMEOUT_S", "90"))
+        hook = os.environ.get("DDIM_COLD_TEST_NATIVE_INIT", "")
+        if hook == "fail":
+            raise RuntimeError("DDIM_COLD_TEST_NATIVE_INIT=fail: native RCCL communicator init refused (test hook)")
+        self.handle = None
+        self.handle = int(torch.ops.ddim_cold.comm_init(uid, self.world, self.rank, idx, int(timeout_s * 1000),
+                                                        hook == "hang"))
         n, r = torch.ops.ddim_cold.comm_info(self.handle)
         assert (n, r) == (self.world, self.rank), (n, r, self.world, self.rank)
 
@@ -210,3 +222,9 @@ class NativeComm:
         if self.handle is not None:
             torch.ops.ddim_cold.comm_destroy(self.handle)
             self.handle = None
+
+    @staticmethod
+    def leaked_inits() -> int:
+        """Init helper threads left behind by timed-out inits in this process."""
+        _ext.load(raise_on_error=True)
+        return int(torch.ops.ddim_cold.comm_init_leaked())

@@ -195,6 +195,8 @@ class TrainEngine:
         if cfg.comm not in ("torch", "native", "auto"):
             raise ValueError(f"comm must be 'torch', 'native' or 'auto', got {cfg.comm!r}")
         self.ncomm = None
+        self.native_error: Optional[str] = None  # why comm='auto' fell back to torch.distributed
+        self.comm_fallback: Optional[str] = None  # autotune_comm: why no layout ran (eager inline fallback)
         default_pg = process_group is None or process_group is dist.group.WORLD
         if cfg.comm == "native" and self.dist_on and self.is_cuda:
             if not default_pg:
@@ -205,6 +207,7 @@ class TrainEngine:
             self.ncomm = self._try_native(dev)
         self.comm_backend = "native" if self.ncomm is not None else "torch"
         self._graphs: Optional[List[torch.cuda.CUDAGraph]] = None
+        self._graph_comm_failed = False  # captured collectives refused -> per-bucket segments
         self._multi = None  # (K-step graph, K) for train_steps
         self._eager_steps = 0
         self.batch_fn: Optional[Callable] = None
@@ -244,6 +247,8 @@ class TrainEngine:
         runs each on its internal stream behind an event round trip each way (1-rank
         inline step: 0.849 vs 0.866 ms)."""
         import warnings
+        from ..parallel.watchdog import phase
+        phase("native-comm:check")
         # every rank must be able to enter ncclCommInitRank before any does: the init
         # blocks until all ranks have joined, so a rank that fails BEFORE it (no
         # extension, no comm ops) would leave the others hanging there
@@ -260,22 +265,31 @@ class TrainEngine:
         if int(flag.item()) != 1:
             return None
         nc, ok = None, 1
+        phase("native-comm:init")
         try:
             from ..parallel.comm import NativeComm
             nc = NativeComm(dev)
+            phase("native-comm:verify", ranks=nc.info()[0])
             x = torch.full((4 * self.world + 3,), float(self.rank + 1), device=dev)
             nc.all_reduce_(x)
             torch.cuda.synchronize(dev)
             ok = int(bool((x == self.world * (self.world + 1) / 2).all()))
-        except Exception as e:  # pragma: no cover - depends on the RCCL build
+            if not ok:
+                self.native_error = "verification sum mismatch"
+        except Exception as e:  # noqa: BLE001 - any failure falls back to torch.distributed
             warnings.warn(f"native RCCL communicator unavailable ({e!r}); using torch.distributed")
+            self.native_error = repr(e)[:300]
             ok = 0
         flag = torch.tensor([ok], dtype=torch.int32, device=dev)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.pg)
         if int(flag.item()) == 1:
+            phase("native-comm:ready", ranks=self.world)
             return nc
-        if nc is not None:
+        if self.native_error is None:
+            self.native_error = "failed on another rank"
+        if nc is not None and nc.handle is not None:
             nc.destroy()
+        phase("native-comm:fallback-torch", error=self.native_error)
         return None
 
     def _comm_host_async(self) -> bool:
@@ -318,6 +332,10 @@ class TrainEngine:
         same parameters (no broadcast here)."""
         if not (self.segmented and self.is_cuda):
             raise ValueError("attach_comm needs a GPU engine built with force_segments=True")
+        if self.temb_bucket is not None and not hasattr(comm, "all_gather_"):
+            raise ValueError(f"{type(comm).__name__} has no all_gather_, which this engine's sparse time-embedding "
+                             "gradient exchange needs (Gaussian diffusion: temb_rows=None); build the engine "
+                             "with temb_rows or temb_sparse=False")
         self.ncomm = comm
         self.world = int(world)
         self.comm_backend = type(comm).__name__
@@ -895,6 +913,7 @@ class TrainEngine:
         self._events = None
         self._signal = None
         self._eager_steps = 0
+        self._graph_comm_failed = False
 
     def _snapshot_state(self):
         self.materialize_lazy()
@@ -923,19 +942,26 @@ class TrainEngine:
           (the timed-out wait raises the error word; every later wait then returns
           at once, so a broken layout costs one timeout, not one per bucket and step);
         * ``budget_s`` (default ``DDIM_COLD_AUTOTUNE_BUDGET_S``, 30 s) bounds the whole
-          tuning: once spent (max over ranks), the remaining candidates are skipped.
+          tuning: once spent (max over ranks), the remaining candidates are skipped;
+        * if NO layout ran, the engine does not raise: it falls back to
+          :meth:`fallback_eager_inline` (no graphs, no hand-offs, one all-reduce on the
+          compute stream; on torch.distributed's communicator if ours fails too) and
+          records the reason in :attr:`comm_fallback`.
 
         Parameters, Adam moments, counters, RNG and loss EMA are restored afterwards:
         the tuning steps leave no trace in the training state.  Returns
         ``{name: ms_per_step}`` (``inf``: failed, ``nan``: skipped for time; empty
-        when not data parallel on a GPU)."""
+        when not data parallel on a GPU).  Testing: ``DDIM_COLD_TEST_FAIL_LAYOUTS=1``
+        makes every candidate fail after its warm-up."""
         if not (self.segmented and self.is_cuda and self.dist_on):
             return {}
         import time
         import warnings
         from ..parallel.dist import all_reduce_max, barrier
+        from ..parallel.watchdog import phase
         if budget_s is None:
             budget_s = float(os.environ.get("DDIM_COLD_AUTOTUNE_BUDGET_S", "30"))
+        force_fail = os.environ.get("DDIM_COLD_TEST_FAIL_LAYOUTS") == "1"
         layouts = list(layouts or self.candidate_layouts())
         snap = self._snapshot_state()
         times: Dict[str, float] = {}
@@ -946,10 +972,13 @@ class TrainEngine:
             if all_reduce_max(time.perf_counter() - t_begin, self.device) > budget_s:
                 times[name] = math.nan
                 continue
+            phase(f"autotune:{name}")
             failed = 0.0
             try:
                 self.apply_layout(L)
                 self.train_steps(self.cfg.graph_warmup + warm)
+                if force_fail:
+                    raise RuntimeError("DDIM_COLD_TEST_FAIL_LAYOUTS=1 (test hook)")
                 torch.cuda.synchronize(self.device)
                 if self.comm_error():
                     failed = 1.0
@@ -975,15 +1004,65 @@ class TrainEngine:
             self.reset_comm_error()
         ok = [L_ for L_ in layouts if math.isfinite(times[L_[0]])]
         self._restore_state(snap)
-        if not ok:
-            raise RuntimeError(f"autotune_comm: no gradient-exchange layout ran: {times} {self.autotune_errors}")
         for name, err in self.autotune_errors.items():
             warnings.warn(f"autotune_comm: layout {name} dropped ({err})")
-        best = min(ok, key=lambda L_: times[L_[0]])
-        self.apply_layout(best)
         self.comm_times = times
+        if not ok:
+            warnings.warn(f"autotune_comm: no gradient-exchange layout ran ({times}); falling back to the "
+                          "eager inline all-reduce")
+            self.fallback_eager_inline(f"no layout ran: {sorted(self.autotune_errors)}")
+        else:
+            best = min(ok, key=lambda L_: times[L_[0]])
+            self.apply_layout(best)
+            phase("autotune:chosen", layout=best[0], ms=round(times[best[0]], 4))
         self.autotune_s = time.perf_counter() - t_begin
         return times
+
+    def fallback_eager_inline(self, reason: str, verify_steps: int = 2):
+        """Last-resort data-parallel step: no hipGraphs, no comm stream, no counter
+        hand-offs -- forward + backward eagerly, then ONE all-reduce of the whole
+        gradient arena on the compute stream, then the optimizer (the reference's
+        DDP step minus the bucket overlap).  ``verify_steps`` eager steps are run on
+        every rank (state restored afterwards); if they fail on any rank while our
+        own RCCL communicator is in use, it is dropped for torch.distributed's and
+        the check repeats.  Sets :attr:`comm_choice` = ``"eager-inline"`` and
+        :attr:`comm_fallback` = ``reason``."""
+        import dataclasses
+        import warnings
+        from ..parallel.dist import all_reduce_max
+        from ..parallel.watchdog import phase
+        phase("comm-fallback:eager-inline", reason=reason)
+        self.set_comm_layout(1 << 16, False, True, captured=False)
+        self.cfg = dataclasses.replace(self.cfg, use_graph=False)
+        self.comm_choice = "eager-inline"
+        self.comm_fallback = reason
+        for attempt in range(2):
+            snap = self._snapshot_state()
+            failed, err = 0.0, None
+            try:
+                self.train_steps(verify_steps)
+                if self.is_cuda:
+                    torch.cuda.synchronize(self.device)
+                if not bool(torch.isfinite(self.loss_last).all()):
+                    failed, err = 1.0, "non-finite loss"
+            except Exception as e:  # noqa: BLE001
+                failed, err = 1.0, repr(e)[:300]
+                if self.is_cuda:
+                    torch.cuda.synchronize(self.device)
+            self._restore_state(snap)
+            if all_reduce_max(failed, self.device) == 0:
+                phase("comm-fallback:verified", comm=self.comm_backend)
+                return
+            if attempt == 0 and self.ncomm is not None and self.dist_on:
+                warnings.warn(f"eager inline fallback failed on the native communicator ({err}); "
+                              "switching to torch.distributed")
+                self.ncomm.destroy()
+                self.ncomm = None
+                self.comm_backend = "torch"
+                self.comm_fallback = reason + "; native communicator dropped"
+                continue
+            break
+        raise RuntimeError(f"data parallel: even the eager inline all-reduce step failed ({err}); {reason}")
 
     def _run_eager(self):
         gen = self._step_iter()
@@ -997,11 +1076,15 @@ class TrainEngine:
         if self.segmented and self.cfg.comm_events:
             self._capture_impl(graph_comm=False, events=True)
             return
-        if self.segmented and self.cfg.graph_comm and not getattr(self, "_graph_comm_failed", False):
+        if self.segmented and self.cfg.graph_comm and not self._graph_comm_failed:
             try:
                 self._capture_impl(graph_comm=True)
                 return
             except Exception as e:  # pragma: no cover - depends on the RCCL build
+                if (self.comm_choice or "").startswith("graph-"):
+                    # a captured layout was asked for (autotune candidate or explicit): its
+                    # failure must reach autotune_comm / the caller, not be timed as segments
+                    raise
                 import warnings
                 warnings.warn(f"capturing collectives in the step graph failed ({e!r}); "
                               "falling back to per-bucket graph segments")

@@ -243,9 +243,11 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
     # the epoch's DistributedSampler table [steps, micro-batch, B] lives on the device
     # (refilled once per epoch); the batch draw reads row ``scheduler step %
     # steps_per_epoch`` through the engine's device step counter, so replays need no
-    # host copy per step and one hipGraph replay can run K whole steps.  Every epoch
-    # starts at a multiple of steps_per_epoch (resume included), so epoch e reads rows
-    # 0..steps_per_epoch-1 in order, as DistributedSampler batches.
+    # host copy per step and one hipGraph replay can run K whole steps.  The table is
+    # rotated by the epoch's starting counter (one host read per epoch), so epoch e
+    # reads its DistributedSampler batches in order even when the counter does not
+    # start the epoch at a multiple of steps_per_epoch (a resume from a checkpoint of
+    # another num_gpus / batch size / max_steps, or of the reference trainer).
     table_dev = torch.zeros(steps_per_epoch, A, B, dtype=torch.int64, device=device)
     batchers = [make_batcher(cfg.dataset, train_pool, B, engine.rng, cfg.model_total_steps, idx=table_dev,
                              idx_step=(engine.step_ctr[1:2], j * B)) for j in range(A)]
@@ -298,7 +300,8 @@ def train_worker(rank: int, world: int, cfg: ExperimentConfig, exp_name: str, pa
         for epoch in range(start_epoch, end_epoch):
             model.train()
             table = shard_indices(n_train, world, rank, epoch, cfg.seed)[: steps_per_epoch * A * B]
-            table_dev.copy_(table.view(steps_per_epoch, A, B))
+            base = int(engine.step_ctr[1].item()) % steps_per_epoch  # the row this epoch's first step reads
+            table_dev.copy_(table.view(steps_per_epoch, A, B).roll(base, 0))
             s = 0
             while s < steps_per_epoch:
                 # run up to the next point the host must act at (log line, sync check,

@@ -164,13 +164,22 @@ def is_capture_error(e: BaseException) -> bool:
     return any(s in msg for s in CAPTURE_ERROR_MARKERS)
 
 
-# HIP error names/strings a failed stream capture surfaces as (hipGetErrorName /
-# hipGetErrorString), plus torch's "not allowed while capturing" checks
+# HIP error names a failed stream capture surfaces as (hipGetErrorName) and the
+# runtime's hipGetErrorString texts for them -- torch reports the latter (the strings
+# are the ones libamdhip64.so of ROCm 7.2 carries) -- plus torch's own "not allowed
+# while capturing" checks
 CAPTURE_ERROR_MARKERS = (
     "hipErrorStreamCaptureUnsupported", "hipErrorStreamCaptureInvalidated", "hipErrorStreamCaptureMerge",
     "hipErrorStreamCaptureUnmatched", "hipErrorStreamCaptureUnjoined", "hipErrorStreamCaptureIsolation",
     "hipErrorStreamCaptureImplicit", "hipErrorStreamCaptureWrongThread", "hipErrorCapturedEvent",
-    "operation not permitted when stream is capturing", "operation would make the legacy stream depend",
+    "operation not permitted when stream is capturing",
+    "operation failed due to a previous error during capture",
+    "operation would result in a merge of separate capture sequences",
+    "capture was not ended in the same stream as it began",
+    "capturing stream has unjoined work",
+    "dependency created on uncaptured work in another stream",
+    "operation would make the legacy stream depend on a capturing blocking stream",
+    "operation not permitted on an event last recorded in a capturing stream",
+    "attempt to terminate a thread-local capture sequence from another thread",
     "capture sequence", "stream is capturing", "during CUDA graph capture", "during graph capture",
-    "not permitted when stream is capturing",
 )

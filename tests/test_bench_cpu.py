@@ -66,3 +66,43 @@ def test_bench_gaussian_dataset_two_ranks_cpu():
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
     assert out["metric"].endswith("Gaussian DDIM") and out["vs_baseline"] is None
     assert "Gaussian DDIM" in out["data"] and out["n_gpus"] == 2 and out["value"] > 0
+
+
+def test_bench_stalled_rank_is_named_before_the_deadline_self_spawn():
+    """One rank stalls at the timed phase (the other then waits in the collective
+    bracket): `bench.py --gpus 2` exits non-zero well before the driver's 600 s and the
+    stderr names the stuck rank and its phase (watchdog phase files + deadlines)."""
+    import time
+    t0 = time.time()
+    r = _bench(["--gpus", "2", "--steps", "2", "--warmup", "1", "--no-sampler"],
+               env={"DDIM_COLD_TEST_STALL": "1:timed", "DDIM_COLD_DEADLINE_S": "60",
+                    "DDIM_COLD_SPAWN_DEADLINE_S": "75"}, timeout=300)
+    dt = time.time() - t0
+    assert r.returncode != 0, r.stdout[-2000:]
+    assert dt < 150, dt
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    err = r.stderr
+    assert "stuck rank(s): rank 1 in phase 'timed'" in err, err[-4000:]
+    assert "rank 0: phase 'timed'" in err, err[-4000:]
+    # every rank marked its phases on stderr
+    assert "phase=pg-ready" in err and "phase=warmup" in err
+
+
+def test_bench_stalled_rank_torchrun_rank_deadline():
+    """Under torchrun (the driver's launcher) each rank's own deadline thread names the
+    stuck rank and exits; torchrun then stops the job."""
+    import time
+    from ddim_cold_amd.parallel.dist import free_port
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps",
+           "2", "--warmup", "1", "--no-sampler"]
+    t0 = time.time()
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd="/tmp",
+                       env=dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2", DDIM_COLD_TEST_STALL="0:engine-ready",
+                                DDIM_COLD_DEADLINE_S="60"))
+    assert r.returncode != 0
+    assert time.time() - t0 < 150
+    assert "[ddim_cold watchdog]" in r.stderr, r.stderr[-4000:]
+    assert "deadline of 60s passed" in r.stderr
+    # rank 0 stalled after building its engine; rank 1 went on into the warm-up's collectives
+    assert "stuck rank(s): rank 0 in phase 'engine-ready'" in r.stderr, r.stderr[-4000:]

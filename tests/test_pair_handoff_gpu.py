@@ -99,3 +99,15 @@ def test_two_engines_cross_queue_handoff(layout, K, monkeypatch):
     assert dp <= 2 * LR * (n_eager + n_graph), (layout, dp)
     dl = abs(float(engs[0].loss_last) * 0.5 + float(engs[1].loss_last) * 0.5 - float(ref.loss_last))
     assert dl <= 1e-3 * abs(float(ref.loss_last)), (layout, dl)
+
+
+def test_attach_comm_rejects_sparse_temb_engine_without_all_gather():
+    """A Gaussian-diffusion engine (temb_rows None) exchanges the time-embedding
+    gradient by all-gather; the loopback endpoint has only all_reduce_, so attaching it
+    must fail up front instead of at the first step."""
+    torch.manual_seed(100)
+    model = build_model("vit_tiny").cuda().train()
+    eng = TrainEngine(model, EngineConfig(lr=LR, t_max=100, seed=5, temb_rows=None, force_segments=True))
+    pair = LoopbackPair("cuda", eng.numel)
+    with pytest.raises(ValueError, match="all_gather_"):
+        eng.attach_comm(pair.endpoint(0), 2)

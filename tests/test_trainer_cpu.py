@@ -305,6 +305,11 @@ def test_is_capture_error_matches_capture_failures_only():
     from ddim_cold_amd.utils.observe import is_capture_error
     assert is_capture_error(RuntimeError("HIP error: operation not permitted when stream is capturing"))
     assert is_capture_error(RuntimeError("hipErrorStreamCaptureInvalidated: capture invalidated"))
+    # the runtime's hipGetErrorString texts (what torch reports)
+    for msg in ("operation failed due to a previous error during capture", "capturing stream has unjoined work",
+                "dependency created on uncaptured work in another stream",
+                "operation not permitted on an event last recorded in a capturing stream"):
+        assert is_capture_error(RuntimeError(f"HIP error: {msg}")), msg
     # real errors that merely mention a graph are not swallowed into the eager fallback
     assert not is_capture_error(RuntimeError("shape mismatch in graph input buffer"))
     assert not is_capture_error(RuntimeError("HIP error: an illegal memory access was encountered"))
@@ -361,3 +366,18 @@ def test_reference_l5_api_shims(tmp_path):
     assert os.path.isfile(tmp_path / "Saved_Models" / "init.pkl")
     ck = torch.load(tmp_path / "Saved_Models" / "exp" / "lastepoch.pkl", weights_only=True)
     assert ck["steps"] == 3 and ck["scheduler"]["base_lrs"] == [pytest.approx(1e-3)]
+
+
+def test_epoch_table_rotation_keeps_sampler_order_for_any_start_counter():
+    """The trainer's device step table is rotated by the epoch's starting scheduler
+    counter, so step j of the epoch reads DistributedSampler batch j even when a resume
+    left the counter at a non-multiple of steps_per_epoch (trainer.py epoch start)."""
+    from ddim_cold_amd import ops
+    spe, A, B = 5, 1, 3
+    table = torch.arange(spe * A * B, dtype=torch.int64).view(spe, A, B)
+    for start in (0, 5, 7, 13):
+        dev_table = table.roll(start % spe, 0)
+        for j in range(spe):
+            ctr = torch.tensor([start + j])
+            got = ops.stepped_idx(dev_table, (ctr, 0), B)
+            assert torch.equal(got, table[j, 0]), (start, j)
