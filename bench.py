@@ -23,12 +23,15 @@ equal N (else exit 2); without torchrun env vars and N > 1 this process spawns
 N rank processes itself (multi_gpu_trainer.py:212-219 launches its ranks the same
 way) without touching the GPU, and exits with the first non-zero rank exit code.
 """
+import time
+
+_T_START = time.time()  # process start: the rank deadline counts the interpreter / torch import too
+
 import argparse
 import json
 import math
 import os
 import sys
-import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
@@ -225,7 +228,7 @@ def run(args):
     if SHARED_GPU:
         local = 0
     # per-rank phase markers on stderr + a deadline that names every rank's last phase
-    watchdog.install(rank, world, deadline_s=RANK_DEADLINE_S)
+    watchdog.install(rank, world, deadline_s=RANK_DEADLINE_S, since=_T_START)
     phase("pg-init", world=world, timeout_s=PG_TIMEOUT_S)
     if args.force_dist and world == 1:
         distributed = init_single(device_index=local, timeout_s=PG_TIMEOUT_S)
@@ -318,7 +321,7 @@ def run(args):
         # model / batch / optimizer; timed the same way (outside the headline number)
         phase("extra:gaussian-ddim")
         extra.update(_time_train(args, args.model, "gaussian", dev, lr, seed=43, pool=pool,
-                                 prefix="gaussian_ddim"))
+                                 prefix="gaussian_ddim_train"))
     if rank == 0 and n == 1 and args.dataset == "cold" and args.model == "vit_tiny" and not args.no_hires \
             and dev.type == "cuda":
         # BASELINE.json config 4 (the 200x200 high-resolution path) and the

@@ -234,9 +234,13 @@ def _short(v) -> str:
 
 # ---------------------------------------------------------------------- module-level log
 def install(rank: int, world: int, directory: Optional[str] = None, deadline_s: Optional[float] = None,
-            echo: bool = True) -> PhaseLog:
-    """Create the process's phase log (and its deadline thread if ``deadline_s``)."""
-    global _LOG
+            echo: bool = True, since: Optional[float] = None) -> PhaseLog:
+    """Create the process's phase log (and its deadline thread if ``deadline_s``,
+    counted from ``since``: default the import of this module; pass the process's
+    start time to include the interpreter / torch import)."""
+    global _LOG, _T0
+    if since is not None:
+        _T0 = float(since)
     _LOG = PhaseLog(rank, world, directory, echo=echo)
     _LOG.mark("start", pid=os.getpid())
     if deadline_s is not None and deadline_s > 0:
