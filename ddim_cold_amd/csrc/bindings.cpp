@@ -748,14 +748,19 @@ std::tuple<Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tenso
     TORCH_CHECK(g_res->numel() == x.numel(), "g_res shape");
     gr = g_res->data_ptr<float>();
   }
-  const int R = ln_replicas();
+  // workspace [R + T][2D]: R = ln_replicas(M) group rows (overwritten), then T rows of
+  // arrival tickets (zero on entry, left zero); the slots are per-call scratch
+  const int R = ln_replicas(M), T = ln_ticket_rows(M, D);
   const bool own_ws = !(ws.has_value() && ws->defined());
   const auto f32o = x.options().dtype(F32);
-  Tensor w = own_ws ? at::zeros({R, 2 * D}, f32o) : *ws;
+  Tensor w = own_ws ? at::zeros({R + T, 2 * D}, f32o) : *ws;
   if (!own_ws) {
     CHECK_IN(w, F32);
-    TORCH_CHECK(w.numel() == (int64_t)R * 2 * D, "ln ws must hold ln_replicas x 2D floats");
+    TORCH_CHECK(w.numel() == (int64_t)(R + T) * 2 * D, "ln ws must hold ln_ws_rows(M, D) x 2D floats (",
+                R + T, " rows for M = ", M, ")");
   }
+  auto slots = at::empty({(int64_t)ln_bwd_workgroups(M), 2 * D}, f32o);
+  unsigned* tickets = reinterpret_cast<unsigned*>(w.data_ptr<float>() + (size_t)R * 2 * D);
   // y_out: also emit the LayerNorm output bf16 (x_hat gamma + beta) for the weight
   // gradient of the GEMM that consumed it through the LayerNorm fold
   const float* bp = nullptr;
@@ -772,22 +777,28 @@ std::tuple<Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tenso
   layernorm_bwd_launch(dy.data_ptr(), dy.scalar_type() == BF16, x.data_ptr(), x.scalar_type() == BF16, mean.data_ptr<float>(), rstd.data_ptr<float>(),
                        gamma.data_ptr<float>(), bp, gr, g_out.data_ptr<float>(), emit_gy ? gy.data_ptr() : nullptr,
                        yp, w.data_ptr<float>(), M, D, N, rng.data_ptr<int64_t>(), site_drop, p_drop, site_dp, p_dp,
-                       parts, cur_stream());
+                       parts, slots.data_ptr<float>(), tickets, cur_stream());
   if (own_ws) {
-    auto s = w.sum(0);
+    auto s = w.narrow(0, 0, R).sum(0);
     dgamma.add_(s.narrow(0, 0, D));
     dbeta.add_(s.narrow(0, D, D));
   }
   return {g_out, gy};
 }
 
-void replica_reduce_(Tensor ws, Tensor dst_ptrs, int64_t C) {
+int64_t ln_replicas_op(int64_t M) { return ln_replicas((int)M); }
+int64_t ln_ws_rows_op(int64_t M, int64_t D) { return ln_replicas((int)M) + ln_ticket_rows((int)M, (int)D); }
+
+// ws [G][rows][C]: rows 0..R-1 of each LayerNorm workspace added into its destination
+void replica_reduce_(Tensor ws, Tensor dst_ptrs, int64_t C, int64_t R) {
   CHECK_IN(ws, F32); CHECK_IN(dst_ptrs, I64);
   const c10::DeviceGuard guard(ws.device());
   const int G = dst_ptrs.numel();
-  TORCH_CHECK(ws.numel() == (int64_t)G * ln_replicas() * C, "replica ws shape");
+  TORCH_CHECK(G > 0 && C > 0 && ws.numel() % ((int64_t)G * C) == 0, "replica ws shape");
+  const int rows = (int)(ws.numel() / ((int64_t)G * C));
+  TORCH_CHECK(R >= 1 && R <= rows, "replica rows");
   replica_reduce_launch(ws.data_ptr<float>(), reinterpret_cast<float* const*>(dst_ptrs.data_ptr<int64_t>()), G, C,
-                        cur_stream());
+                        (int)R, rows, cur_stream());
 }
 
 Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, double scale, Tensor rng, int64_t site, double p,
@@ -811,7 +822,8 @@ Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, double scale, Ten
 }
 
 Tensor embed_bwd(Tensor g, Tensor t, Tensor rng, int64_t site, double p, Tensor dcls, Tensor dpos, Tensor dtemb,
-                 c10::optional<Tensor> ln_ws, c10::optional<Tensor> ln_ptrs, int64_t ln_C, bool ln_store) {
+                 c10::optional<Tensor> ln_ws, c10::optional<Tensor> ln_ptrs, int64_t ln_C, bool ln_store,
+                 int64_t ln_R) {
   CHECK_IN(g, F32); CHECK_IN(t, I64); check_rng(rng); CHECK_IN(dcls, F32); CHECK_IN(dpos, F32); CHECK_IN(dtemb, F32);
   const c10::DeviceGuard guard(g.device());
   TORCH_CHECK(g.dim() == 3, "g must be [B,N,D]");
@@ -825,9 +837,11 @@ Tensor embed_bwd(Tensor g, Tensor t, Tensor rng, int64_t site, double p, Tensor 
     TORCH_CHECK(ln_ptrs.has_value() && ln_ptrs->defined(), "ln_ws needs ln_ptrs");
     CHECK_IN((*ln_ptrs), I64);
     rf.G = ln_ptrs->numel();
-    rf.R = ln_replicas();
     rf.C = ln_C;
-    TORCH_CHECK(ln_C > 0 && ln_ws->numel() == (int64_t)rf.G * rf.R * ln_C, "replica ws shape");
+    TORCH_CHECK(rf.G > 0 && ln_C > 0 && ln_ws->numel() % ((int64_t)rf.G * ln_C) == 0, "replica ws shape");
+    rf.rows = (int)(ln_ws->numel() / ((int64_t)rf.G * ln_C));
+    rf.R = (int)ln_R;
+    TORCH_CHECK(rf.R >= 1 && rf.R <= rf.rows, "ln_R: replica rows to sum");
     rf.ws = ln_ws->data_ptr<float>();
     rf.dsts = reinterpret_cast<float* const*>(ln_ptrs->data_ptr<int64_t>());
     rf.store = ln_store ? 1 : 0;
@@ -1072,14 +1086,16 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor? g_res, "
         "Tensor(a!) dgamma, Tensor(b!) dbeta, int N, Tensor rng, int site_drop, float p_drop, int site_dp, "
         "float p_dp, bool emit_gy, Tensor(c!)? ws=None, Tensor? beta=None, Tensor(d!)? y_out=None) -> (Tensor, Tensor)");
-  m.def("replica_reduce_(Tensor(a!) ws, Tensor dst_ptrs, int C) -> ()");
+  m.def("replica_reduce_(Tensor ws, Tensor dst_ptrs, int C, int R) -> ()");
+  m.def("ln_replicas(int M) -> int", &ln_replicas_op);
+  m.def("ln_ws_rows(int M, int D) -> int", &ln_ws_rows_op);
   m.def("ln_fold_(Tensor[] ws, Tensor[] gammas, Tensor[] betas, Tensor?[] biases, Tensor(a!)[] wfs, Tensor(b!)[] cs, "
         "Tensor(c!)[] bfs, Tensor? loss_parts=None, Tensor(d!)? loss_last=None, Tensor(e!)? loss_ema=None, "
         "float ema_decay=0.99, Tensor(f!)? step=None, Tensor(g!)? rng=None, Tensor? sq=None) -> ()");
   m.def("attn_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, float scale, Tensor rng, int site, float p, "
         "Tensor? keep=None) -> Tensor");
   m.def("embed_bwd(Tensor g, Tensor t, Tensor rng, int site, float p, Tensor(a!) dcls, Tensor(b!) dpos, "
-        "Tensor(c!) dtemb, Tensor(d!)? ln_ws=None, Tensor? ln_ptrs=None, int ln_C=0, bool ln_store=False) -> Tensor");
+        "Tensor(c!) dtemb, Tensor? ln_ws=None, Tensor? ln_ptrs=None, int ln_C=0, bool ln_store=False, int ln_R=0) -> Tensor");
   m.def("sqnorm(Tensor g, Tensor(a!) out, float scale, int lz_lo=0, int lz_hi=0) -> ()");
   m.def("adamw_step(Tensor(a!) p, Tensor(b!) g, Tensor(c!) m, Tensor(d!) v, Tensor(e!)? pbf, Tensor sq, "
         "Tensor step, Tensor hyper, float grad_scale, int zero_hi=-1, int lz_lo=0, int lz_hi=0, "

@@ -159,6 +159,21 @@ inline uint32_t drop_threshold_host(double p) {
 }
 
 // ----------------------------------------------------------------------------- reductions
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned int gu32;
+
+// write-through 8-B store / L1-bypassing 8-B load (agent-scope relaxed atomics:
+// global_store_dwordx2 sc1 / global_load_dwordx2 sc1)
+__device__ __forceinline__ void st8_sc1(void* p, uint64_t v) {
+  __hip_atomic_store((gu64*)p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld8_sc1(const void* p) {
+  return __hip_atomic_load((gu64*)const_cast<void*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_f2_sc1(float* p, float a, float b) {
+  st8_sc1(p, (uint64_t)__float_as_uint(a) | ((uint64_t)__float_as_uint(b) << 32));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -12,6 +12,7 @@
 //    read (inverse of the head's unpatchify; cls rows zero).
 #include "common.h"
 #include "kernels.h"
+#include <algorithm>
 
 namespace dc {
 
@@ -200,14 +201,20 @@ __global__ __launch_bounds__(256) void patchify_cls_kernel(const float* __restri
   }
 }
 
-// part A: (n,d) -> dpos (+dcls) ; part B: (b,d) -> dtemb[t_b] ; part C: patch-row grads (bf16)
-constexpr int EMB_TCHUNK = 64;  // tokens per part-B workgroup
+// part A: (n,d) -> dpos (+dcls) ; part B: dtemb rows ; part C: patch-row grads (bf16) ;
+// part D: LayerNorm dgamma/dbeta finalize.  No fp32 atomics anywhere: every output
+// element has one writer and a fixed summation order (two runs are bit-identical).
+// Part B: one workgroup per (distinct timestep, 64-column block): the samples sharing
+// that t in sample order, all tokens, 16 token lanes x 16 float4 column lanes, then the
+// 16 lanes summed in lane order through LDS.
+constexpr int EMB_BCOLS = 64;    // columns per part-B workgroup
+constexpr int EMB_BMAX = 256;    // samples per part-B pass (the launcher adds passes beyond)
 __global__ __launch_bounds__(256) void embed_bwd_kernel(const float* __restrict__ g, const int64_t* __restrict__ t,
                                                         float* __restrict__ dcls, float* __restrict__ dpos,
                                                         float* __restrict__ dtemb, bf16* __restrict__ gpatch, int B,
                                                         int N, int D, const int64_t* __restrict__ rng, int site,
                                                         uint32_t thr, float dsc, int blocksA, int blocksB,
-                                                        int blocksC, ReplicaFinal rf) {
+                                                        int blocksC, ReplicaFinal rf, int pb0, int pbn) {
   const uint32_t salt = thr ? site_salt(rng, site) : 0u;
   auto gm = [&](size_t idx) -> float {
     const float v = g[idx];
@@ -232,38 +239,96 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const float* __restrict_
     dpos[e] += s;
     if (n == 0) dcls[d] += s;
   } else if (bid < blocksA + blocksB) {
-    // (b, d) sums over EMB_TCHUNK-token chunks, one chunk per workgroup row: a serial
-    // walk over all N tokens per thread took 61.6 us at N = 626 (48 workgroups)
-    const int nch = (N + EMB_TCHUNK - 1) / EMB_TCHUNK;
-    const int bb = bid - blocksA, ch = bb % nch;
-    const int e = (bb / nch) * 256 + threadIdx.x;
-    if (e >= B * D) return;
-    const int b = e / D, d = e - b * D;
-    const int n0 = ch * EMB_TCHUNK, n1 = min(N, n0 + EMB_TCHUNK);
-    float s = 0.f;
-    int n = n0;
-    for (; n + 8 <= n1; n += 8) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = g[((size_t)b * N + n + u) * D + d];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s += thr ? (dropout_keep(salt, (uint32_t)(((size_t)b * N + n + u) * D + d), thr) ? v[u] * dsc : 0.f) : v[u];
+    // part B: workgroup (j, column block): the j-th distinct timestep in sample order
+    // (owner = its first sample), summed over every sample with that t and every token
+    // samples [pb0, pb0 + pbn) of this pass (pbn <= EMB_BMAX)
+    const int nd = (D + EMB_BCOLS - 1) / EMB_BCOLS;
+    const int bb = bid - blocksA, j = bb / nd, d0 = (bb - j * nd) * EMB_BCOLS;
+    __shared__ int64_t ts[EMB_BMAX];
+    __shared__ int firsts[EMB_BMAX];
+    __shared__ int own[2];
+    __shared__ float4 racc[16][EMB_BCOLS / 4];
+    for (int b = threadIdx.x; b < pbn; b += 256) ts[b] = t[pb0 + b];
+    if (threadIdx.x == 0) own[0] = -1;
+    __syncthreads();
+    for (int b = threadIdx.x; b < pbn; b += 256) {  // first occurrence of its t in the pass?
+      bool first = true;
+      for (int b2 = 0; b2 < b; ++b2) first = first && ts[b2] != ts[b];
+      firsts[b] = first ? 1 : 0;
     }
-    for (; n < n1; ++n) s += gm(((size_t)b * N + n) * D + d);
-    const int64_t tb = t[b];
-    atomicAdd(dtemb + (size_t)tb * D + d, s);  // samples sharing a t add here too
+    __syncthreads();
+    for (int b = threadIdx.x; b < pbn; b += 256) {  // the j-th first occurrence owns slot j
+      int rank = 0;
+      for (int b2 = 0; b2 < b; ++b2) rank += firsts[b2];
+      if (firsts[b] && rank == j) own[0] = b;
+    }
+    __syncthreads();
+    if (own[0] < 0) return;  // fewer than j + 1 distinct timesteps
+    const int b0 = own[0];
+    const int64_t t0 = ts[b0];
+    const int cl = threadIdx.x & 15, tl = threadIdx.x >> 4;  // column lane (float4), token lane
+    const int d = d0 + 4 * cl;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (d < D) {
+      for (int bl = b0; bl < pbn; ++bl) {
+        if (ts[bl] != t0) continue;
+        const int b = pb0 + bl;
+        const float* gb = g + (size_t)b * N * D + d;
+        int n = tl;
+        for (; n + 48 < N; n += 64) {  // four tokens in flight per lane
+          float4 v[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(gb + (size_t)(n + 16 * u) * D);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            if (thr) {
+              bool k[4];
+              dropout_keep4(salt, (uint32_t)(((size_t)b * N + n + 16 * u) * D + d), thr, k);
+              v[u].x = k[0] ? v[u].x * dsc : 0.f;
+              v[u].y = k[1] ? v[u].y * dsc : 0.f;
+              v[u].z = k[2] ? v[u].z * dsc : 0.f;
+              v[u].w = k[3] ? v[u].w * dsc : 0.f;
+            }
+            acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+          }
+        }
+        for (; n < N; n += 16) {
+          float4 v = *reinterpret_cast<const float4*>(gb + (size_t)n * D);
+          if (thr) {
+            bool k[4];
+            dropout_keep4(salt, (uint32_t)(((size_t)b * N + n) * D + d), thr, k);
+            v.x = k[0] ? v.x * dsc : 0.f;
+            v.y = k[1] ? v.y * dsc : 0.f;
+            v.z = k[2] ? v.z * dsc : 0.f;
+            v.w = k[3] ? v.w * dsc : 0.f;
+          }
+          acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        }
+      }
+    }
+    racc[tl][cl] = acc;
+    __syncthreads();
+    if (tl == 0 && d < D) {
+      float4 s4 = racc[0][cl];
+#pragma unroll
+      for (int l = 1; l < 16; ++l) {
+        const float4 q = racc[l][cl];
+        s4.x += q.x; s4.y += q.y; s4.z += q.z; s4.w += q.w;
+      }
+      float4* dst = reinterpret_cast<float4*>(dtemb + (size_t)t0 * D + d);
+      float4 o = *dst;  // this workgroup is the row's only writer in the launch
+      o.x += s4.x; o.y += s4.y; o.z += s4.z; o.w += s4.w;
+      *dst = o;
+    }
   } else if (bid >= blocksA + blocksB + blocksC) {
     // part D: LayerNorm dgamma/dbeta replica finalize (replica_reduce_kernel's work;
     // every LayerNorm backward has run before the embedding backward)
     const int rb = bid - blocksA - blocksB - blocksC, cb = (rf.C + 255) / 256;
     const int gi = rb / cb, c = (rb - gi * cb) * 256 + threadIdx.x;
     if (c >= rf.C) return;
-    float* w = rf.ws + (size_t)gi * rf.R * rf.C + c;
+    const float* w = rf.ws + (size_t)gi * rf.rows * rf.C + c;
     float s = 0.f;
-    for (int r = 0; r < rf.R; ++r) {
-      s += w[(size_t)r * rf.C];
-      w[(size_t)r * rf.C] = 0.f;
-    }
+    for (int r = 0; r < rf.R; ++r) s += w[(size_t)r * rf.C];  // row order: deterministic
     rf.dsts[gi][c] = rf.store ? s : rf.dsts[gi][c] + s;
   } else {
     // part C: 4 consecutive columns per thread (one 16-B load, two pair hashes, one 8-B
@@ -386,7 +451,8 @@ void patchify_cls_launch(const float* img, const int64_t* t, const float* cls, c
 
 void embed_bwd_launch(const float* g, const int64_t* t, float* dcls, float* dpos, float* dtemb, void* gpatch, int B,
                       int N, int D, const int64_t* rng, int site, double p, hipStream_t stream, ReplicaFinal rf) {
-  const int blocksA = cdiv(N * D, 256), blocksB = cdiv(B * D, 256) * cdiv(N, EMB_TCHUNK);
+  const int pbn0 = std::min(B, EMB_BMAX);
+  const int blocksA = cdiv(N * D, 256), blocksB = pbn0 * cdiv(D, EMB_BCOLS);
   if (D % 4 != 0) throw std::invalid_argument("embed_bwd: D must be a multiple of 4");
   if ((size_t)B * N * D >= (size_t)INT32_MAX) throw std::invalid_argument("embed_bwd: too many elements for 32-bit indexing");
   const int blocksC = grid_for((size_t)B * (N - 1) * D / 4);
@@ -395,7 +461,15 @@ void embed_bwd_launch(const float* g, const int64_t* t, float* dcls, float* dpos
   const float dsc = p > 0 ? 1.f / (1.f - (float)p) : 1.f;
   hipLaunchKernelGGL(embed_bwd_kernel, dim3(blocksA + blocksB + blocksC + blocksD), dim3(256), 0, stream, g, t, dcls,
                      dpos, dtemb, reinterpret_cast<bf16*>(gpatch), B, N, D, rng, site, thr, dsc, blocksA, blocksB,
-                     blocksC, rf);
+                     blocksC, rf, 0, pbn0);
+  // batches beyond EMB_BMAX samples: further part-B passes (stream-ordered: each adds
+  // to the rows the previous passes wrote; a sample's t is owned in its own pass)
+  for (int pb0 = EMB_BMAX; pb0 < B; pb0 += EMB_BMAX) {
+    const int pbn = std::min(B - pb0, EMB_BMAX), nb = pbn * cdiv(D, EMB_BCOLS);
+    hipLaunchKernelGGL(embed_bwd_kernel, dim3(nb), dim3(256), 0, stream, g, t, dcls, dpos, dtemb,
+                       reinterpret_cast<bf16*>(gpatch), B, N, D, rng, site, thr, dsc, 0, nb, 0, ReplicaFinal(), pb0,
+                       pbn);
+  }
 }
 
 int smooth_l1_launch(const float* pred, const float* target, float* loss, float* partials, void* dtok, int B,

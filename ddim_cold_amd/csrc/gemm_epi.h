@@ -14,18 +14,6 @@
 
 namespace dc {
 
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-typedef __attribute__((address_space(1))) unsigned int gu32;
-
-// write-through 8-B store / L1-bypassing 8-B load (agent-scope relaxed atomics:
-// global_store_dwordx2 sc1 / global_load_dwordx2 sc1)
-__device__ __forceinline__ void st8_sc1(void* p, uint64_t v) {
-  __hip_atomic_store((gu64*)p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t ld8_sc1(const void* p) {
-  return __hip_atomic_load((gu64*)const_cast<void*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 struct GemmParams {
   const bf16* A;
   const bf16* B;

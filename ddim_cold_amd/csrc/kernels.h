@@ -109,14 +109,19 @@ int gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool stor
 // LayerNorm (layernorm.hip)
 void layernorm_fwd_launch(const float* x, const float* gamma, const float* beta, void* y_bf16, float* mean,
                           float* rstd, int M, int D, float eps, hipStream_t stream);
-// dgamma||dbeta partials go into ws [ln_replicas()][2D] (must be zero on entry);
-// replica_reduce_launch adds them into the destinations and re-zeroes ws.
+// dgamma||dbeta: each workgroup stores its column partial in slots [ln_bwd_workgroups(M)][2D]
+// (scratch), and per group of 16 workgroups the last to arrive writes the group's sum, in
+// workgroup order, to row g of ws [ln_replicas(M)][2D]; tickets [ln_replicas(M)] must be
+// zero on entry (the last arriver re-zeroes its ticket).  replica_reduce_launch adds the
+// R rows of each workspace into its destination, in row order: deterministic.
 void layernorm_bwd_launch(const void* dy, bool dy_bf16, const void* x, bool x_bf16, const float* mean, const float* rstd,
                           const float* gamma, const float* beta, const float* g_res, float* g_out, void* gy_bf16,
                           void* y_bf16, float* dgb_ws, int M,
                           int D, int tokens, const int64_t* rng, int site_drop, double p_drop, int site_dp,
-                          double p_dp, int dy_parts, hipStream_t stream);
-int ln_replicas();
+                          double p_dp, int dy_parts, float* slots, unsigned* tickets, hipStream_t stream);
+int ln_bwd_workgroups(int M);
+int ln_replicas(int M);
+int ln_ticket_rows(int M, int D);
 
 // LayerNorm fold weights for the GEMMs that consume a LayerNorm (layernorm.hip)
 constexpr int FOLD_MAX = 32;  // GEMMs per fold launch (vit_small_200: 25 in one launch)
@@ -150,7 +155,8 @@ struct FoldTable {
   int sq_n = 0;
 };
 void ln_fold_launch(const FoldTable& tb, hipStream_t stream);
-void replica_reduce_launch(float* ws, float* const* dsts_dev, int G, int C, hipStream_t stream);
+// ws [G][rows][C]: sums rows 0..R-1 of each workspace
+void replica_reduce_launch(const float* ws, float* const* dsts_dev, int G, int C, int R, int rows, hipStream_t stream);
 
 // Attention (attention.hip)
 // keep_bits: optional [attn_keep_words] attention-dropout keep flags, written by
@@ -197,9 +203,9 @@ void patchify_cls_launch(const float* img, const int64_t* t, const float* cls, c
                          ColdSrc cs = ColdSrc());
 // optional LayerNorm replica finalize carried by the embedding-backward launch
 struct ReplicaFinal {
-  float* ws = nullptr;          // [G][R][C] replicas (re-zeroed)
+  const float* ws = nullptr;    // [G][rows][C] LayerNorm workspaces: rows 0..R-1 summed in order
   float* const* dsts = nullptr; // [G] device pointers to the [C] grad ranges (+=, or = with store)
-  int G = 0, R = 0, C = 0;
+  int G = 0, R = 0, C = 0, rows = 0;
   int store = 0;
 };
 void embed_bwd_launch(const float* g, const int64_t* t, float* dcls, float* dpos, float* dtemb, void* gpatch,

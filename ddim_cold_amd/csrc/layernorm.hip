@@ -8,14 +8,19 @@
 //   * the residual-gradient add  g_out = g_res + dLN/dx,
 //   * the *next* residual branch's gradient prep  gy = bf16(g_out * dropout
 //     mask * drop-path scale)  (masks regenerated from the counter hash),
-//   * dgamma/dbeta column partials reduced per workgroup through LDS then one
-//     fp32 atomic per column per workgroup.
+//   * dgamma/dbeta column partials, deterministic: reduced per workgroup through
+//     LDS into a slot of its own (write-through), then per group of LN_GROUP
+//     consecutive workgroups the last to arrive (agent-scope ticket) sums the
+//     group's slots in workgroup order into the group's row of the workspace; the
+//     finalize (replica_reduce / the embedding-backward launch) sums those rows in
+//     row order.  No fp32 atomics: two runs are bit-identical.
 #include "common.h"
 #include "kernels.h"
 
 namespace dc {
 
-constexpr int LN_REPLICAS = 16;
+constexpr int LN_NW = 8;      // waves (rows) per workgroup of the backward
+constexpr int LN_GROUP = 16;  // workgroups per in-launch reduction group
 
 template <int VEC, int NW>
 __global__ __launch_bounds__(NW * 64) void ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
@@ -78,7 +83,8 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict_
                                                      bf16* __restrict__ y_out, float* __restrict__ dgb_ws, int M,
                                                      int tokens, const int64_t* __restrict__ rng, int site_drop,
                                                      uint32_t thr_drop, float sc_drop, int site_dp, uint32_t thr_dp,
-                                                     float sc_dp, int dy_parts) {
+                                                     float sc_dp, int dy_parts, float* __restrict__ slots,
+                                                     unsigned* __restrict__ tickets) {
   constexpr int D = VEC * 128;
   // dynamic LDS ([NW][2D] floats): static LDS limited the residency of the larger
   // non-256-thread workgroups (tools/ub_lds_census.hip)
@@ -199,7 +205,8 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict_
       }
     }
   }
-  // column partials: waves -> LDS -> one atomic per column per workgroup
+  // column partials: waves -> LDS -> this workgroup's slot, stored write-through (sc1:
+  // read by the group's last workgroup, possibly on another XCD), then drained
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
     const int c = 2 * (lane + 64 * i);
@@ -209,33 +216,57 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict_
     red[wave][D + c + 1] = dbet[i].y;
   }
   __syncthreads();
-  // dgamma||dbeta replicas: ws[R][2D], workgroup b adds into replica b % R (spreads the
-  // same-address atomic contention of ~M/8 workgroups over R replicas)
-  float* rep = dgb_ws + (size_t)(blockIdx.x % LN_REPLICAS) * 2 * D;
-  for (int c = threadIdx.x; c < 2 * D; c += NW * 64) {
-    float s = 0.f;
+  float* slot = slots + (size_t)blockIdx.x * 2 * D;
+  for (int c = 2 * threadIdx.x; c < 2 * D; c += 2 * NW * 64) {
+    float s0 = 0.f, s1 = 0.f;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) s += red[w][c];
-    atomicAdd(rep + c, s);
+    for (int w = 0; w < NW; ++w) {
+      s0 += red[w][c];
+      s1 += red[w][c + 1];
+    }
+    st_f2_sc1(slot + c, s0, s1);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its slot stores
+  __syncthreads();
+  // group ticket (agent scope); the workgroup whose add comes last reduces the group.
+  // "I am last" goes through the one LDS array (red[0][0]) after the barrier
+  const int grp = blockIdx.x / LN_GROUP, g0 = grp * LN_GROUP;
+  const int g1 = min((int)gridDim.x, g0 + LN_GROUP);
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add((gu32*)(tickets + grp), 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = prev == (unsigned)(g1 - g0 - 1);
+    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    red[0][0] = last ? 1.f : 0.f;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if (red[0][0] == 0.f) return;
+  // the group's slots in workgroup order (sc1 loads: L1-bypassing, like the stores)
+  float* row = dgb_ws + (size_t)grp * 2 * D;
+  for (int c = 2 * threadIdx.x; c < 2 * D; c += 2 * NW * 64) {
+    float s0 = 0.f, s1 = 0.f;
+    for (int b = g0; b < g1; ++b) {
+      const uint64_t v = ld8_sc1(slots + (size_t)b * 2 * D + c);
+      s0 += __uint_as_float((uint32_t)v);
+      s1 += __uint_as_float((uint32_t)(v >> 32));
+    }
+    row[c] = s0;
+    row[c + 1] = s1;
+  }
+  if (threadIdx.x == 0) __hip_atomic_store((gu32*)(tickets + grp), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// dst[g][c] += sum_r ws[g][r][c]; ws zeroed.  One launch finalises many LayerNorms.
-__global__ __launch_bounds__(256) void replica_reduce_kernel(float* __restrict__ ws, float* const* __restrict__ dsts,
-                                                             int C) {
+// dst[g][c] += sum_{r < R} ws[g][r][c] (rows of stride `rows`), in row order.  One
+// launch finalises many LayerNorms.
+__global__ __launch_bounds__(256) void replica_reduce_kernel(const float* __restrict__ ws,
+                                                             float* const* __restrict__ dsts, int C, int R, int rows) {
   const int gi = blockIdx.y;
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
-  float* w = ws + (size_t)gi * LN_REPLICAS * C + c;
-  float v[LN_REPLICAS];
-#pragma unroll
-  for (int r = 0; r < LN_REPLICAS; ++r) v[r] = w[(size_t)r * C];
+  const float* w = ws + (size_t)gi * rows * C + c;
   float s = 0.f;
-#pragma unroll
-  for (int r = 0; r < LN_REPLICAS; ++r) {
-    s += v[r];
-    w[(size_t)r * C] = 0.f;
-  }
+  for (int r = 0; r < R; ++r) s += w[(size_t)r * C];
   dsts[gi][c] += s;
 }
 
@@ -436,7 +467,7 @@ void layernorm_bwd_launch(const void* dy, bool dy_bf16, const void* x, bool x_bf
                           const float* gamma, const float* beta, const float* g_res, float* g_out, void* gy_bf16,
                           void* y_bf16, float* dgb_ws, int M,
                           int D, int tokens, const int64_t* rng, int site_drop, double p_drop, int site_dp,
-                          double p_dp, int dy_parts, hipStream_t stream) {
+                          double p_dp, int dy_parts, float* slots, unsigned* tickets, hipStream_t stream) {
   if (D % 128) throw std::runtime_error("layernorm: D % 128 != 0");
   const uint32_t td = drop_threshold_host(p_drop), tp = drop_threshold_host(p_dp);
   const float sd = p_drop > 0 ? 1.f / (1.f - (float)p_drop) : 1.f;
@@ -449,7 +480,7 @@ void layernorm_bwd_launch(const void* dy, bool dy_bf16, const void* x, bool x_bf
                                     W * 2 * D * sizeof(float), stream, dy, x, mean, rstd, gamma, beta, g_res, g_out, \
                                     reinterpret_cast<bf16*>(gy_bf16), reinterpret_cast<bf16*>(y_bf16), dgb_ws,  \
                                     M, tokens, rng, site_drop, td,                                              \
-                                    sd, site_dp, tp, sp, dy_parts))
+                                    sd, site_dp, tp, sp, dy_parts, slots, tickets))
 #define LN_BWD_GO(R, W)                      \
   if (dy_bf16 && x_bf16) LN_BWD_GO1(R, W, true, true)  \
   else if (dy_bf16) LN_BWD_GO1(R, W, true, false)      \
@@ -457,13 +488,16 @@ void layernorm_bwd_launch(const void* dy, bool dy_bf16, const void* x, bool x_bf
   else LN_BWD_GO1(R, W, false, false)
   // measured on the ViT-tiny shape (M 2080, D 384, dropout on): 1 row x 8 waves
   // 5.0 us, 2 x 4 5.9, 1 x 4 5.2, 1 x 16 5.1, 2 x 16 7.2
+  static_assert(LN_NW == 8, "ln_bwd launch: 8 waves");
   LN_BWD_GO(1, 8)
 #undef LN_BWD_GO
 #undef LN_BWD_GO1
 }
 
-int ln_replicas() { return LN_REPLICAS; }
+int ln_bwd_workgroups(int M) { return (M + LN_NW - 1) / LN_NW; }
+int ln_replicas(int M) { return (ln_bwd_workgroups(M) + LN_GROUP - 1) / LN_GROUP; }
+int ln_ticket_rows(int M, int D) { return (ln_replicas(M) + 2 * D - 1) / (2 * D); }
 
-void replica_reduce_launch(float* ws, float* const* dsts_dev, int G, int C, hipStream_t stream) {
-  hipLaunchKernelGGL(replica_reduce_kernel, dim3((C + 255) / 256, G), dim3(256), 0, stream, ws, dsts_dev, C);
+void replica_reduce_launch(const float* ws, float* const* dsts_dev, int G, int C, int R, int rows, hipStream_t stream) {
+  hipLaunchKernelGGL(replica_reduce_kernel, dim3((C + 255) / 256, G), dim3(256), 0, stream, ws, dsts_dev, C, R, rows);
 }

@@ -367,15 +367,27 @@ def linear_wgrad_multi(jobs, store: bool = False, sq=None):
         sqnorm(arena, parts, 1.0, lazy=lazy)
 
 
-LN_REPLICAS = 16  # csrc/layernorm.hip LN_REPLICAS
+def ln_replicas(M: int) -> int:
+    """Rows of a LayerNorm backward workspace that hold dgamma||dbeta group partials
+    for ``M`` rows (csrc/layernorm.hip: one per 16 workgroups of 8 rows)."""
+    return -(-(-(-M // 8)) // 16)
+
+
+def ln_ws_rows(M: int, D: int) -> int:
+    """Rows ([rows, 2D] floats) of the workspace :func:`layernorm_bwd` takes for ``M``
+    rows of width ``D``: the :func:`ln_replicas` partial rows, then the arrival tickets
+    (zero on entry, left zero)."""
+    R = ln_replicas(M)
+    return R + -(-R // (2 * D))
 
 
 def layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dgamma, dbeta, N: int, rng, site_drop: int, p_drop: float,
                   site_dp: int, p_dp: float, emit_gy: bool, ws: Optional[torch.Tensor] = None, beta=None,
                   y_out=None):
-    """LayerNorm backward.  With ``ws`` ([LN_REPLICAS, 2D], zero on entry) the
-    dgamma||dbeta partials stay in the replica workspace (finalise later with
-    :func:`replica_reduce_`); otherwise they are added into dgamma / dbeta.
+    """LayerNorm backward.  With ``ws`` ([ln_ws_rows(M, D), 2D], zero on entry) the
+    dgamma||dbeta partials stay in the workspace's first :func:`ln_replicas` rows
+    (finalise later with :func:`replica_reduce_`; deterministic, no atomics);
+    otherwise they are added into dgamma / dbeta.
     ``y_out`` (with ``beta``): also write the LayerNorm output (bf16) — the
     forward folded the LayerNorm into the next GEMM and never stored it."""
     if _hip(x):
@@ -417,16 +429,18 @@ def ln_fold_(ws, gammas, betas, biases, wfs, cs, bfs, tail=None):
         advance_counters(step, rng, sq)
 
 
-def replica_reduce_(ws, dst_ptrs, C: int, dsts=None):
-    """dst[g] += ws[g].sum(0) for G LayerNorm replica workspaces; ws re-zeroed.
+def replica_reduce_(ws, dst_ptrs, C: int, R: int, dsts=None):
+    """dst[g] += ws[g, :R].sum(0) (rows in order) for G LayerNorm workspaces
+    ([G, rows, C]; ``R`` = :func:`ln_replicas` of the backward's row count).
 
     ``dst_ptrs`` is a device int64 tensor of destination addresses (GPU); the
-    CPU path takes the destination tensors in ``dsts`` instead."""
+    CPU path takes the destination tensors in ``dsts`` instead (and re-zeroes the
+    rows: its LayerNorm backward accumulates into row 0)."""
     if _hip(ws):
-        return _ops().replica_reduce_(ws, dst_ptrs, C)
+        return _ops().replica_reduce_(ws, dst_ptrs, C, int(R))
     for g, d in enumerate(dsts):
-        d.add_(ws[g].sum(0))
-    ws.zero_()
+        d.add_(ws[g, :R].sum(0))
+    ws[:, :R].zero_()
 
 
 def attn_bwd(do, qkv, o, lse, scale: float, rng, site: int, p: float, keep=None):
@@ -437,13 +451,14 @@ def attn_bwd(do, qkv, o, lse, scale: float, rng, site: int, p: float, keep=None)
 
 
 def embed_bwd(g, t, rng, site: int, p: float, dcls, dpos, dtemb, ln_final=None):
-    """``ln_final = (ws, dst_ptrs, C[, store])``: the LayerNorm replica finalize
+    """``ln_final = (ws, dst_ptrs, C, R[, store])``: the LayerNorm finalize
     (:func:`replica_reduce_`) rides in the same launch (GPU only); ``store``: the
-    destinations get the replica sum instead of having it added."""
+    destinations get the sum instead of having it added.  Deterministic: no fp32
+    atomics (the time-embedding rows are summed per distinct timestep)."""
     if _hip(g):
-        ws, ptrs, C = ln_final[:3] if ln_final is not None else (None, None, 0)
-        store = bool(ln_final[3]) if ln_final is not None and len(ln_final) > 3 else False
-        return _ops().embed_bwd(g, t, rng, site, float(p), dcls, dpos, dtemb, ws, ptrs, int(C), store)
+        ws, ptrs, C, R = ln_final[:4] if ln_final is not None else (None, None, 0, 0)
+        store = bool(ln_final[4]) if ln_final is not None and len(ln_final) > 4 else False
+        return _ops().embed_bwd(g, t, rng, site, float(p), dcls, dpos, dtemb, ws, ptrs, int(C), store, int(R))
     if ln_final is not None:
         raise ValueError("ln_final needs the HIP extension (use replica_reduce_ on CPU)")
     return ref.embed_bwd(g, t, rng, site, p, dcls, dpos, dtemb)

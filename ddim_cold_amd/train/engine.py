@@ -472,11 +472,26 @@ class TrainEngine:
             assert ob == ow + D, "LayerNorm weight/bias must be adjacent in the arena"
             dsts.append(self.flat_g[ow:ow + 2 * D])
         self.ln_dsts = dsts
-        self.ln_ws = torch.zeros(len(order), ops.LN_REPLICAS, 2 * D, dtype=torch.float32, device=dev)
+        # workspace rows depend on the backward's row count (ops.ln_ws_rows): allocated by
+        # _ensure_ln_ws at the first step of a batch size (eager, never inside a capture)
+        self.ln_ws = None
+        self.ln_R = 0
         self.ln_ptrs = torch.tensor([t.data_ptr() for t in dsts], dtype=torch.int64, device=dev) \
             if dev.type == "cuda" else None
         self._ln_prefixes = ln_prefixes
         self._build_buckets()
+
+    def _ensure_ln_ws(self, M: int):
+        """LayerNorm dgamma/dbeta workspaces ([2L+1, ops.ln_ws_rows(M, D), 2D], zero) for
+        backward passes of ``M`` token rows."""
+        D = self.prog.cfg.dim
+        rows = ops.ln_ws_rows(M, D)
+        if self.ln_ws is not None and self.ln_ws.shape[1] == rows:
+            return
+        if self.is_cuda and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("the batch size changed inside a graph capture (LayerNorm workspace)")
+        self.ln_ws = torch.zeros(len(self.ln_order), rows, 2 * D, dtype=torch.float32, device=self.device)
+        self.ln_R = ops.ln_replicas(M)
 
     def _build_buckets(self):
         """All-reduce bucket layout from ``cfg.bucket_blocks`` / ``cfg.embed_bucket``
@@ -576,6 +591,7 @@ class TrainEngine:
             else:
                 img, tgt, t = self.batch_fn()
             self._temb_t.append(t)
+            self._ensure_ln_ws(int(t.shape[0]) * c.tokens)
             if fused_loss:
                 # head GEMM epilogue computes the loss partials and the token-layout gradient
                 (loss_parts, dtok), S = self.prog.forward(self.param_tensors, img, t, self.rng, True,
@@ -604,7 +620,7 @@ class TrainEngine:
             ln_final = None
             if self.ln_ptrs is not None and FUSE_LN_FINAL:
                 hi = self.ln_done_at[-1]
-                ln_final = (self.ln_ws[:hi], self.ln_ptrs[:hi], 2 * c.dim)
+                ln_final = (self.ln_ws[:hi], self.ln_ptrs[:hi], 2 * c.dim, self.ln_R)
             # single process: every weight gradient in one launch after the backward (no
             # bucket needs a block's gradients early); data parallel: one launch per
             # gradient bucket, so its all-reduce can start while the backward goes on
@@ -630,7 +646,7 @@ class TrainEngine:
                     if hi > ln_lo:
                         ops.replica_reduce_(self.ln_ws[ln_lo:hi],
                                             None if self.ln_ptrs is None else self.ln_ptrs[ln_lo:hi],
-                                            2 * c.dim, dsts=self.ln_dsts[ln_lo:hi])
+                                            2 * c.dim, self.ln_R, dsts=self.ln_dsts[ln_lo:hi])
                         ln_lo = hi
                     if last:
                         yield ("bucket", self.bucket_after[i])

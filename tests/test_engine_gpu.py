@@ -27,9 +27,9 @@ def test_graph_step_matches_eager(grad_accum):
     pg, lg, eng = _run(True, grad_accum)
     pe, le, _ = _run(False, grad_accum)
     assert eng._graphs is not None and len(eng._graphs) == 1
-    assert all(abs(a - b) <= 1e-4 * abs(b) for a, b in zip(lg, le)), (lg, le)
-    # AdamW turns last-bit differences of near-zero grads (fp32 atomics) into <= 2*lr per step
-    assert (pg - pe).abs().max().item() <= 2 * 1e-3 * 5
+    # the graph replays exactly the eager step's kernels; no fp32 atomics: bit-identical
+    assert lg == le, (lg, le)
+    assert torch.equal(pg, pe)
     assert int(eng.rng[1]) == 5 * grad_accum and int(eng.step_ctr[0]) == 5
 
 
@@ -86,9 +86,15 @@ def test_engine_fused_batch_matches_unfused():
         return eng.flat_p.clone(), losses
     pf, lf = run(True)
     pu, lu = run(False)
-    # the two runs draw bit-identical batches (test above) and share every kernel; the
-    # fp32 atomics of the LayerNorm-replica and time-embedding gradients make any two
-    # runs differ at the ~1e-5 level by step 4
+    pf2, lf2 = run(True)
+    # no gradient reduction uses fp32 atomics (LayerNorm dgamma/dbeta: ordered in-launch
+    # group sums; time embedding: one writer per row): two identical runs are
+    # bit-identical after 4 steps
+    assert lf == lf2, (lf, lf2)
+    assert torch.equal(pf, pf2)
+    # fused vs unfused draw bit-identical batches (test above) but sum the loss in a
+    # different order (target as patch rows in the vector loss epilogue): last-bit
+    # differences of the loss scale that AdamW turns into <= ~2 lr per step
     assert all(abs(a - b) <= 2e-4 * abs(b) for a, b in zip(lf, lu)), (lf, lu)
     assert (pf - pu).abs().max().item() <= 2 * 1e-3 * 4
 
@@ -149,7 +155,8 @@ def test_fused_grad_norm_matches_sqnorm_pass(monkeypatch, graph):
 def test_ln_replica_finalize_fused_matches_separate(monkeypatch):
     """LayerNorm dgamma/dbeta replica finalize carried by the embedding-backward launch
     (engine.FUSE_LN_FINAL, default) == the separate replica_reduce_ launch:
-    same LayerNorm parameters after the step, replica workspace re-zeroed."""
+    same LayerNorm parameters after the step (bit-identical: both sum the workspace
+    rows in order), arrival tickets left zero."""
     from ddim_cold_amd.train import engine as engine_mod
 
     def run(flag):
@@ -165,13 +172,13 @@ def test_ln_replica_finalize_fused_matches_separate(monkeypatch):
         ln = torch.cat([eng.flat_p[eng.offsets[n + ".weight"][0]:eng.offsets[n + ".weight"][0] + 2 * model.embed_dim]
                         for n in eng.ln_order])
         # the step must have touched every LayerNorm parameter
-        return ln.clone(), float(eng.ln_ws.abs().max()), eng.flat_m.clone()
+        return ln.clone(), float(eng.ln_ws[:, eng.ln_R:].abs().max()), eng.flat_m.clone()
     lf, wf, mf = run("1")
     lu, wu, mu = run("0")
     assert wf == 0.0 and wu == 0.0
     init = torch.cat([torch.ones(384), torch.zeros(384)]).cuda().repeat(15)
     assert (lf - init).abs().max() > 0
-    torch.testing.assert_close(lf, lu, rtol=0, atol=1e-6)
+    assert torch.equal(lf, lu)
 
 
 @pytest.mark.gpu

@@ -77,6 +77,38 @@ def test_layernorm_bwd(emit, p):
         assert gy is None
 
 
+@pytest.mark.parametrize("M,D,N", [(2080, 384, 65), (20032, 384, 626), (8224, 256, 257), (40, 128, 5)])
+def test_layernorm_bwd_workspace_deterministic(M, D, N):
+    """dgamma||dbeta through the workspace (per-workgroup slots, in-launch group sums by
+    the last arriver, rows finalised in order): == the fp32 oracle, BIT-identical over
+    repeated launches (no fp32 atomics), the arrival tickets left zero for the next call,
+    and replica_reduce_ == the in-launch finalize of embed_bwd."""
+    x = torch.randn(M, D, device=DEV)
+    g, b = torch.randn(D, device=DEV), torch.randn(D, device=DEV)
+    _, mu, rs = ref.layernorm_fwd(x, g, b)
+    dy, gres = torch.randn(M, D, device=DEV), torch.randn(M, D, device=DEV)
+    r = rng()
+    R, rows = ops.ln_replicas(M), ops.ln_ws_rows(M, D)
+    assert R == -(-(-(-M // 8)) // 16) and rows > R
+    ws = torch.zeros(1, rows, 2 * D, device=DEV)
+    outs = []
+    for _ in range(3):
+        z = torch.zeros(D, device=DEV)
+        go, gy = ops.layernorm_bwd(dy, x, mu, rs, g, gres, z, z.clone(), N, r, 7, 0.1, 8, 0.2, True, ws[0])
+        dst = torch.zeros(2 * D, device=DEV)
+        ops.replica_reduce_(ws, torch.tensor([dst.data_ptr()], dtype=torch.int64, device=DEV), 2 * D, R)
+        torch.cuda.synchronize()
+        assert not ws[0, R:].any(), "arrival tickets must be left zero"
+        outs.append((go, gy, dst))
+    for go, gy, dst in outs[1:]:
+        assert torch.equal(go, outs[0][0]) and torch.equal(gy, outs[0][1])
+        assert torch.equal(dst, outs[0][2]), "dgamma||dbeta differ between identical launches"
+    dg2, db2 = torch.zeros(D, device=DEV), torch.zeros(D, device=DEV)
+    ref.layernorm_bwd(dy, x, mu, rs, g, gres, dg2, db2, N, r, 7, 0.1, 8, 0.2, True)
+    close(outs[0][2][:D], dg2, 2e-3 * dg2.abs().max().item(), 1e-4, "dgamma")
+    close(outs[0][2][D:], db2, 2e-3 * db2.abs().max().item(), 1e-4, "dbeta")
+
+
 # ------------------------------------------------------------------ GEMMs
 @pytest.mark.parametrize("B,N,H,D", [(32, 65, 12, 384), (4, 257, 4, 256), (3, 17, 2, 64 * 2)])
 def test_qkv_fwd(B, N, H, D):
@@ -493,6 +525,34 @@ def test_embed_bwd(B, N, D):
         outs.append((gp, dcls, dpos, dtemb))
     for a, b, n in zip(outs[0], outs[1], ["gpatch", "dcls", "dpos", "dtemb"]):
         close(a, b, 2e-2 if n == "gpatch" else 1e-3, 1e-3, n)
+
+
+@pytest.mark.parametrize("B,N,D,tset", [(32, 65, 384, "cold"), (32, 626, 384, "cold"), (32, 65, 384, "gauss"),
+                                        (300, 17, 128, "cold")])
+def test_embed_bwd_time_embedding_deterministic(B, N, D, tset):
+    """The time-embedding gradient is summed per distinct timestep in sample order (no
+    fp32 atomics): bit-identical across launches, == the fp32 oracle; more than 256
+    samples take extra part-B passes (300 samples)."""
+    g = torch.randn(B, N, D, device=DEV)
+    gen = torch.Generator().manual_seed(3)
+    t = (torch.randint(1, 7, (B,), generator=gen) if tset == "cold" else torch.randint(0, 2000, (B,), generator=gen))
+    t = t.to(DEV)
+    r = rng()
+    res = []
+    for _ in range(3):
+        dcls, dpos, dtemb = torch.zeros(D, device=DEV), torch.zeros(N, D, device=DEV), torch.zeros(2000, D, device=DEV)
+        ops.embed_bwd(g, t, r, 1, 0.1, dcls, dpos, dtemb)
+        torch.cuda.synchronize()
+        res.append((dcls, dpos, dtemb))
+    for o in res[1:]:
+        assert all(torch.equal(a, b) for a, b in zip(o, res[0]))
+    dcls, dpos, dtemb = torch.zeros(D, device=DEV), torch.zeros(N, D, device=DEV), torch.zeros(2000, D, device=DEV)
+    ref.embed_bwd(g, t, r, 1, 0.1, dcls, dpos, dtemb)
+    close(res[0][2], dtemb, 1e-3 * dtemb.abs().max().item(), 1e-3, "dtemb")
+    close(res[0][1], dpos, 1e-3 * dpos.abs().max().item(), 1e-3, "dpos")
+    untouched = torch.ones(2000, dtype=torch.bool, device=DEV)
+    untouched[t] = False
+    assert not res[0][2][untouched].any()
 
 
 @pytest.mark.parametrize("p", [8, 4])

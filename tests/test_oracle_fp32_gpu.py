@@ -59,7 +59,8 @@ def test_fused_fwd_bwd_vs_fp32_autograd(name, depth, B, train):
         assert _frob(g[n], p.grad) < FROB, (n, _frob(g[n], p.grad))
 
 
-@pytest.mark.parametrize("name,depth,k,N", [("oxford_flower", None, 20, 16), ("vit_small_200", 3, 200, 4)])
+@pytest.mark.parametrize("name,depth,k,N", [("oxford_flower", None, 20, 16), ("vit_small_200", 3, 200, 4),
+                                            ("vit_small_200", None, 20, 8)])
 def test_sampler_vs_fp32_eager_loop(name, depth, k, N):
     from ddim_cold_amd.bench.eager_sampler import eager_ddim_sample
     from ddim_cold_amd.diffusion.samplers import DDIMSampler
@@ -70,4 +71,5 @@ def test_sampler_vs_fp32_eager_loop(name, depth, k, N):
     fused = DDIMSampler(m, DEV, k=k).sample(N, noise=noise)
     eager = eager_ddim_sample(m, DEV, k, N, noise=noise.to(DEV))
     d = (fused - eager).abs()
+    print(f"{name} depth {depth or len(m.blocks)} k={k} N={N}: mean |d| {d.mean().item():.3e} max {d.max().item():.3e}")
     assert d.mean() < SAMPLER_MEAN and d.max() < SAMPLER_MAX, (d.mean().item(), d.max().item())

@@ -125,3 +125,9 @@ if __name__ == "__main__":
         autograd_vs_fp32("vit_small_200", depth=2, train=True, B=2, loss="square")
         sampler_vs_eager("oxford_flower", k=20, N=16)
         sampler_vs_eager("vit_small_200", k=200, N=4, depth=3)
+    if which in ("all", "r6"):
+        # round 6: the benchmarked long-sequence sampler configuration at full depth
+        # (vit_small_200, depth 12, 626 tokens, k=20 -> 100 steps), N=8, and the
+        # ViT-tiny training gradients of the full model against the fp32 model
+        sampler_vs_eager("vit_small_200", k=20, N=8)
+        autograd_vs_fp32("vit_small_200", train=True, B=2, loss="smooth_l1")
