@@ -642,11 +642,46 @@ static std::vector<GemmArgs> wgrad_probs(const std::vector<Tensor>& dys, const s
 // writing its tiles' partials after the previous launch's.
 void linear_wgrad_multi(std::vector<Tensor> dys, std::vector<Tensor> xs, std::vector<Tensor> dws,
                         std::vector<c10::optional<Tensor>> dbs, bool store, c10::optional<Tensor> sq_parts,
-                        c10::optional<Tensor> arena, int64_t lz_lo, int64_t lz_hi) {
+                        c10::optional<Tensor> arena, int64_t lz_lo, int64_t lz_hi, c10::optional<Tensor> emb_g,
+                        c10::optional<Tensor> emb_t, c10::optional<Tensor> emb_rng, int64_t emb_site, double emb_p,
+                        c10::optional<Tensor> emb_cls, c10::optional<Tensor> emb_pos, c10::optional<Tensor> emb_temb,
+                        int64_t emb_owners, c10::optional<Tensor> ln_ws, c10::optional<Tensor> ln_ptrs,
+                        std::vector<int64_t> ln_offs, int64_t ln_C, int64_t ln_R, bool ln_store) {
   TORCH_CHECK(!dys.empty() && dys.size() == xs.size() && dys.size() == dws.size() && dys.size() == dbs.size(),
               "wgrad_multi: one dy, x, dw, db per problem");
   const c10::DeviceGuard guard(dys[0].device());
   const bool fused = sq_parts.has_value() && sq_parts->defined();
+  // embedding gradients + LayerNorm finalize as extra workgroups (embed_parts.h)
+  const bool with_emb = emb_g.has_value() && emb_g->defined();
+  WgradEmbed we{};
+  std::vector<std::pair<int64_t, int64_t>> covered;  // arena ranges the embedding workgroups write
+  if (with_emb) {
+    const Tensor& g = *emb_g;
+    CHECK_IN(g, F32); CHECK_IN((*emb_t), I64); check_rng(*emb_rng);
+    CHECK_IN((*emb_cls), F32); CHECK_IN((*emb_pos), F32); CHECK_IN((*emb_temb), F32);
+    TORCH_CHECK(g.dim() == 3, "emb_g must be [B, N, D]");
+    const int B = g.size(0), N = g.size(1), D = g.size(2);
+    TORCH_CHECK(emb_t->numel() == B && emb_cls->numel() == D && emb_pos->numel() == (int64_t)N * D &&
+                    emb_temb->size(-1) == D && D % 4 == 0 && B <= 256 && emb_owners >= 1 && emb_owners <= B,
+                "wgrad_multi embedding shapes (B <= 256, D % 4 == 0, 1 <= owners <= B)");
+    we.e = embed_grad_args(g.data_ptr<float>(), emb_t->data_ptr<int64_t>(), emb_cls->data_ptr<float>(),
+                           emb_pos->data_ptr<float>(), emb_temb->data_ptr<float>(), B, N, D,
+                           emb_rng->data_ptr<int64_t>(), (int)emb_site, emb_p, 0, B);
+    we.e.owners = (int)emb_owners;
+    if (ln_ws.has_value() && ln_ws->defined()) {
+      CHECK_IN((*ln_ws), F32); CHECK_IN((*ln_ptrs), I64);
+      we.rf.G = ln_ptrs->numel();
+      we.rf.C = (int)ln_C;
+      TORCH_CHECK(we.rf.G > 0 && ln_C > 0 && ln_ws->numel() % ((int64_t)we.rf.G * ln_C) == 0 &&
+                      (int64_t)ln_offs.size() == we.rf.G, "wgrad_multi: LayerNorm workspace / offsets");
+      we.rf.rows = (int)(ln_ws->numel() / ((int64_t)we.rf.G * ln_C));
+      we.rf.R = (int)ln_R;
+      TORCH_CHECK(we.rf.R >= 1 && we.rf.R <= we.rf.rows, "wgrad_multi: ln_R");
+      we.rf.ws = ln_ws->data_ptr<float>();
+      we.rf.dsts = reinterpret_cast<float* const*>(ln_ptrs->data_ptr<int64_t>());
+      we.rf.store = ln_store ? 1 : 0;
+    }
+  }
   WgradSq sq;
   int np = 0;
   if (fused) {
@@ -667,7 +702,25 @@ void linear_wgrad_multi(std::vector<Tensor> dys, std::vector<Tensor> xs, std::ve
       add(dws[i]);
       if (dbs[i].has_value() && dbs[i]->defined()) add(*dbs[i]);
     }
+    std::sort(iv.begin(), iv.end());
+    for (size_t i = 1; i < iv.size(); ++i)
+      TORCH_CHECK(iv[i].first >= iv[i - 1].second,
+                  "wgrad_multi: overlapping weight-gradient targets (the partials would count them twice)");
+    // ranges the tail skips without a tile writing them: the lazy range (zero forever)
+    // and the embedding workgroups' outputs (they write their own partials)
     if (lz_hi > lz_lo) iv.emplace_back(lz_lo, lz_hi);
+    if (with_emb) {
+      auto cov = [&](const Tensor& t) {
+        const int64_t off = t.data_ptr<float>() - base;
+        TORCH_CHECK(off >= 0 && off + t.numel() <= n, "wgrad_multi: an embedding gradient lies outside the arena");
+        iv.emplace_back(off, off + t.numel());
+      };
+      cov(*emb_cls); cov(*emb_pos); cov(*emb_temb);
+      for (int64_t o : ln_offs) {
+        TORCH_CHECK(o >= 0 && o + ln_C <= n, "wgrad_multi: a LayerNorm gradient lies outside the arena");
+        iv.emplace_back(o, o + ln_C);
+      }
+    }
     std::sort(iv.begin(), iv.end());
     sq.base = base;
     int64_t cur = 0, rest = 0;
@@ -680,7 +733,6 @@ void linear_wgrad_multi(std::vector<Tensor> dys, std::vector<Tensor> xs, std::ve
       rest += hi - lo;
     };
     for (const auto& [lo, hi] : iv) {
-      TORCH_CHECK(lo >= cur, "wgrad_multi: overlapping weight-gradient targets (the partials would count them twice)");
       gap(cur, lo);
       cur = std::max(cur, hi);
     }
@@ -696,18 +748,31 @@ void linear_wgrad_multi(std::vector<Tensor> dys, std::vector<Tensor> xs, std::ve
     std::vector<c10::optional<Tensor>> b(dbs.begin() + a, dbs.begin() + e);
     std::vector<GemmArgs> probs = wgrad_probs(d, x, w, b, nullptr, nullptr);
     if (!fused) {
-      gemm_wgrad_multi(probs.data(), (int)probs.size(), cur_stream(), store);
+      gemm_wgrad_multi(probs.data(), (int)probs.size(), cur_stream(), store, nullptr,
+                       (with_emb && e == total) ? &we : nullptr);
       continue;
     }
     WgradSq s = sq;
     s.parts = sq_parts->data_ptr<float>() + used;
     s.nparts = np - used;
-    if (e < total) {  // tail ranges and zero fill ride in the last launch
+    if (e < total) {  // tail ranges, zero fill and embedding workgroups ride in the last launch
       s.nr = 0;
       s.tail = 0;
     }
-    used += gemm_wgrad_multi(probs.data(), (int)probs.size(), cur_stream(), store, &s);
+    used += gemm_wgrad_multi(probs.data(), (int)probs.size(), cur_stream(), store, &s,
+                             (with_emb && e == total) ? &we : nullptr);
   }
+  TORCH_CHECK(!with_emb || fused || total <= (size_t)WGRAD_MULTI_MAX, "wgrad_multi: embedding parts need sq fusion "
+              "or one launch");
+}
+
+// grad-norm partial slots the embedding workgroups of a wgrad_multi launch take
+int64_t wgrad_embed_slots(int64_t B, int64_t N, int64_t D, int64_t owners, int64_t n_ln, int64_t ln_C, bool wide) {
+  WgradEmbed we{};
+  we.e.B = (int)B; we.e.N = (int)N; we.e.D = (int)D; we.e.owners = (int)owners;
+  float dummy = 0.f;
+  if (n_ln > 0) { we.rf.ws = &dummy; we.rf.G = (int)n_ln; we.rf.C = (int)ln_C; }
+  return wgrad_embed_workgroups(we, wide);
 }
 
 // fp32 <-> bf16 gradient wire (csrc/comm_wire.hip): one fused 16-B-vector
@@ -728,7 +793,8 @@ void wire_unpack(Tensor src, Tensor dst) {
 std::tuple<Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma,
                                          c10::optional<Tensor> g_res, Tensor dgamma, Tensor dbeta, int64_t N,
                                          Tensor rng, int64_t site_drop, double p_drop, int64_t site_dp, double p_dp,
-                                         bool emit_gy, c10::optional<Tensor> ws, c10::optional<Tensor> beta, c10::optional<Tensor> y_out) {
+                                         bool emit_gy, c10::optional<Tensor> ws, c10::optional<Tensor> beta, c10::optional<Tensor> y_out,
+                                         c10::optional<Tensor> gp_out, int64_t site_emb, double p_emb) {
   CHECK_CUDA(dy); CHECK_CONTIG(dy);
   TORCH_CHECK(dy.scalar_type() == F32 || dy.scalar_type() == BF16, "dy must be fp32 or bf16");
   CHECK_CUDA(x); CHECK_CONTIG(x);
@@ -748,19 +814,22 @@ std::tuple<Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tenso
     TORCH_CHECK(g_res->numel() == x.numel(), "g_res shape");
     gr = g_res->data_ptr<float>();
   }
-  // workspace [R + T][2D]: R = ln_replicas(M) group rows (overwritten), then T rows of
-  // arrival tickets (zero on entry, left zero); the slots are per-call scratch
-  const int R = ln_replicas(M), T = ln_ticket_rows(M, D);
+  // workspace [S][2D]: one dgamma||dbeta slot per backward workgroup (overwritten)
+  const int S = ln_bwd_workgroups(M);
   const bool own_ws = !(ws.has_value() && ws->defined());
   const auto f32o = x.options().dtype(F32);
-  Tensor w = own_ws ? at::zeros({R + T, 2 * D}, f32o) : *ws;
+  Tensor w = own_ws ? at::empty({S, 2 * D}, f32o) : *ws;
   if (!own_ws) {
     CHECK_IN(w, F32);
-    TORCH_CHECK(w.numel() == (int64_t)(R + T) * 2 * D, "ln ws must hold ln_ws_rows(M, D) x 2D floats (",
-                R + T, " rows for M = ", M, ")");
+    TORCH_CHECK(w.numel() == (int64_t)S * 2 * D, "ln ws must hold ln_ws_rows(M) x 2D floats (", S,
+                " rows for M = ", M, ")");
   }
-  auto slots = at::empty({(int64_t)ln_bwd_workgroups(M), 2 * D}, f32o);
-  unsigned* tickets = reinterpret_cast<unsigned*>(w.data_ptr<float>() + (size_t)R * 2 * D);
+  void* gpp = nullptr;
+  if (gp_out.has_value() && gp_out->defined()) {  // the patch-embedding input gradient
+    CHECK_IN((*gp_out), BF16);
+    TORCH_CHECK(N > 1 && gp_out->numel() == (int64_t)(M / N) * (N - 1) * D, "gp_out must be [B*(N-1), D]");
+    gpp = gp_out->data_ptr();
+  }
   // y_out: also emit the LayerNorm output bf16 (x_hat gamma + beta) for the weight
   // gradient of the GEMM that consumed it through the LayerNorm fold
   const float* bp = nullptr;
@@ -777,17 +846,16 @@ std::tuple<Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tenso
   layernorm_bwd_launch(dy.data_ptr(), dy.scalar_type() == BF16, x.data_ptr(), x.scalar_type() == BF16, mean.data_ptr<float>(), rstd.data_ptr<float>(),
                        gamma.data_ptr<float>(), bp, gr, g_out.data_ptr<float>(), emit_gy ? gy.data_ptr() : nullptr,
                        yp, w.data_ptr<float>(), M, D, N, rng.data_ptr<int64_t>(), site_drop, p_drop, site_dp, p_dp,
-                       parts, slots.data_ptr<float>(), tickets, cur_stream());
+                       parts, gpp, (int)site_emb, p_emb, cur_stream());
   if (own_ws) {
-    auto s = w.narrow(0, 0, R).sum(0);
+    auto s = w.sum(0);
     dgamma.add_(s.narrow(0, 0, D));
     dbeta.add_(s.narrow(0, D, D));
   }
   return {g_out, gy};
 }
 
-int64_t ln_replicas_op(int64_t M) { return ln_replicas((int)M); }
-int64_t ln_ws_rows_op(int64_t M, int64_t D) { return ln_replicas((int)M) + ln_ticket_rows((int)M, (int)D); }
+int64_t ln_ws_rows_op(int64_t M) { return ln_bwd_workgroups((int)M); }
 
 // ws [G][rows][C]: rows 0..R-1 of each LayerNorm workspace added into its destination
 void replica_reduce_(Tensor ws, Tensor dst_ptrs, int64_t C, int64_t R) {
@@ -1082,13 +1150,17 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("wire_pack(Tensor src, Tensor(a!) dst) -> ()");
   m.def("wire_unpack(Tensor src, Tensor(a!) dst) -> ()");
   m.def("linear_wgrad_multi(Tensor[] dys, Tensor[] xs, Tensor(a!)[] dws, Tensor(b!)?[] dbs, bool store=False, "
-        "Tensor(c!)? sq_parts=None, Tensor? arena=None, int lz_lo=0, int lz_hi=0) -> ()");
+        "Tensor(c!)? sq_parts=None, Tensor? arena=None, int lz_lo=0, int lz_hi=0, Tensor? emb_g=None, "
+        "Tensor? emb_t=None, Tensor? emb_rng=None, int emb_site=0, float emb_p=0.0, Tensor(d!)? emb_cls=None, "
+        "Tensor(e!)? emb_pos=None, Tensor(f!)? emb_temb=None, int emb_owners=0, Tensor? ln_ws=None, "
+        "Tensor? ln_ptrs=None, int[] ln_offs=[], int ln_C=0, int ln_R=0, bool ln_store=False) -> ()");
+  m.def("wgrad_embed_slots(int B, int N, int D, int owners, int n_ln, int ln_C, bool wide) -> int", &wgrad_embed_slots);
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor? g_res, "
         "Tensor(a!) dgamma, Tensor(b!) dbeta, int N, Tensor rng, int site_drop, float p_drop, int site_dp, "
-        "float p_dp, bool emit_gy, Tensor(c!)? ws=None, Tensor? beta=None, Tensor(d!)? y_out=None) -> (Tensor, Tensor)");
+        "float p_dp, bool emit_gy, Tensor(c!)? ws=None, Tensor? beta=None, Tensor(d!)? y_out=None, "
+        "Tensor(e!)? gp_out=None, int site_emb=0, float p_emb=0.0) -> (Tensor, Tensor)");
   m.def("replica_reduce_(Tensor ws, Tensor dst_ptrs, int C, int R) -> ()");
-  m.def("ln_replicas(int M) -> int", &ln_replicas_op);
-  m.def("ln_ws_rows(int M, int D) -> int", &ln_ws_rows_op);
+  m.def("ln_ws_rows(int M) -> int", &ln_ws_rows_op);
   m.def("ln_fold_(Tensor[] ws, Tensor[] gammas, Tensor[] betas, Tensor?[] biases, Tensor(a!)[] wfs, Tensor(b!)[] cs, "
         "Tensor(c!)[] bfs, Tensor? loss_parts=None, Tensor(d!)? loss_last=None, Tensor(e!)? loss_ema=None, "
         "float ema_decay=0.99, Tensor(f!)? step=None, Tensor(g!)? rng=None, Tensor? sq=None) -> ()");

@@ -179,6 +179,37 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// Column sums of R slot rows (the LayerNorm dgamma/dbeta finalize), fixed order
+// (deterministic): a workgroup of NT threads covers 16 columns c0.. with NT/16 slot lanes,
+// lane l summing rows l, l + NT/16, ... (eight loads in flight), then the lanes in lane
+// order.  red: >= NT floats of LDS.  Returns the column total in the threads of lane 0
+// (column c0 + threadIdx.x), 0 elsewhere.
+template <int NT>
+__device__ __forceinline__ float slot_colsum16(const float* __restrict__ w, int C, int R, int c0, float* red) {
+  constexpr int SL = NT / 16;
+  const int cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int c = c0 + cl;
+  float s = 0.f;
+  if (c < C) {
+    int r = sl;
+    for (; r + 7 * SL < R; r += 8 * SL) {
+      float a[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] = w[(size_t)(r + u * SL) * C + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += a[u];
+    }
+    for (; r < R; r += SL) s += w[(size_t)r * C + c];
+  }
+  red[sl * 16 + cl] = s;
+  __syncthreads();
+  float t = 0.f;
+  if (sl == 0) {
+    for (int l = 0; l < SL; ++l) t += red[l * 16 + cl];
+  }
+  return t;
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

@@ -12,6 +12,7 @@
 //    read (inverse of the head's unpatchify; cls rows zero).
 #include "common.h"
 #include "kernels.h"
+#include "embed_parts.h"
 #include <algorithm>
 
 namespace dc {
@@ -202,135 +203,23 @@ __global__ __launch_bounds__(256) void patchify_cls_kernel(const float* __restri
 }
 
 // part A: (n,d) -> dpos (+dcls) ; part B: dtemb rows ; part C: patch-row grads (bf16) ;
-// part D: LayerNorm dgamma/dbeta finalize.  No fp32 atomics anywhere: every output
-// element has one writer and a fixed summation order (two runs are bit-identical).
-// Part B: one workgroup per (distinct timestep, 64-column block): the samples sharing
-// that t in sample order, all tokens, 16 token lanes x 16 float4 column lanes, then the
-// 16 lanes summed in lane order through LDS.
-constexpr int EMB_BCOLS = 64;    // columns per part-B workgroup
-constexpr int EMB_BMAX = 256;    // samples per part-B pass (the launcher adds passes beyond)
-__global__ __launch_bounds__(256) void embed_bwd_kernel(const float* __restrict__ g, const int64_t* __restrict__ t,
-                                                        float* __restrict__ dcls, float* __restrict__ dpos,
-                                                        float* __restrict__ dtemb, bf16* __restrict__ gpatch, int B,
-                                                        int N, int D, const int64_t* __restrict__ rng, int site,
-                                                        uint32_t thr, float dsc, int blocksA, int blocksB,
-                                                        int blocksC, ReplicaFinal rf, int pb0, int pbn) {
-  const uint32_t salt = thr ? site_salt(rng, site) : 0u;
-  auto gm = [&](size_t idx) -> float {
-    const float v = g[idx];
-    if (!thr) return v;
-    return dropout_keep(salt, (uint32_t)idx, thr) ? v * dsc : 0.f;
-  };
+// part D: LayerNorm dgamma/dbeta finalize.  Parts A, B, D are embed_parts.h (shared with
+// the weight-gradient launch); no fp32 atomics anywhere.
+__global__ __launch_bounds__(256) void embed_bwd_kernel(EmbedGrad e, bf16* __restrict__ gpatch, int blocksA,
+                                                        int blocksB, int blocksC, ReplicaFinal rf) {
+  __shared__ __attribute__((aligned(16))) char smem[emb_smem_bytes(256)];
   const int bid = blockIdx.x;
   if (bid < blocksA) {
-    const int e = bid * 256 + threadIdx.x;
-    if (e >= N * D) return;
-    const int n = e / D, d = e - n * D;
-    float s = 0.f;
-    int b = 0;
-    for (; b + 8 <= B; b += 8) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = g[((size_t)(b + u) * N + n) * D + d];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s += thr ? (dropout_keep(salt, (uint32_t)(((size_t)(b + u) * N + n) * D + d), thr) ? v[u] * dsc : 0.f) : v[u];
-    }
-    for (; b < B; ++b) s += gm(((size_t)b * N + n) * D + d);
-    dpos[e] += s;
-    if (n == 0) dcls[d] += s;
+    emb_part_a<256>(e, bid, nullptr, reinterpret_cast<float*>(smem));
   } else if (bid < blocksA + blocksB) {
-    // part B: workgroup (j, column block): the j-th distinct timestep in sample order
-    // (owner = its first sample), summed over every sample with that t and every token
-    // samples [pb0, pb0 + pbn) of this pass (pbn <= EMB_BMAX)
-    const int nd = (D + EMB_BCOLS - 1) / EMB_BCOLS;
-    const int bb = bid - blocksA, j = bb / nd, d0 = (bb - j * nd) * EMB_BCOLS;
-    __shared__ int64_t ts[EMB_BMAX];
-    __shared__ int firsts[EMB_BMAX];
-    __shared__ int own[2];
-    __shared__ float4 racc[16][EMB_BCOLS / 4];
-    for (int b = threadIdx.x; b < pbn; b += 256) ts[b] = t[pb0 + b];
-    if (threadIdx.x == 0) own[0] = -1;
-    __syncthreads();
-    for (int b = threadIdx.x; b < pbn; b += 256) {  // first occurrence of its t in the pass?
-      bool first = true;
-      for (int b2 = 0; b2 < b; ++b2) first = first && ts[b2] != ts[b];
-      firsts[b] = first ? 1 : 0;
-    }
-    __syncthreads();
-    for (int b = threadIdx.x; b < pbn; b += 256) {  // the j-th first occurrence owns slot j
-      int rank = 0;
-      for (int b2 = 0; b2 < b; ++b2) rank += firsts[b2];
-      if (firsts[b] && rank == j) own[0] = b;
-    }
-    __syncthreads();
-    if (own[0] < 0) return;  // fewer than j + 1 distinct timesteps
-    const int b0 = own[0];
-    const int64_t t0 = ts[b0];
-    const int cl = threadIdx.x & 15, tl = threadIdx.x >> 4;  // column lane (float4), token lane
-    const int d = d0 + 4 * cl;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (d < D) {
-      for (int bl = b0; bl < pbn; ++bl) {
-        if (ts[bl] != t0) continue;
-        const int b = pb0 + bl;
-        const float* gb = g + (size_t)b * N * D + d;
-        int n = tl;
-        for (; n + 48 < N; n += 64) {  // four tokens in flight per lane
-          float4 v[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(gb + (size_t)(n + 16 * u) * D);
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            if (thr) {
-              bool k[4];
-              dropout_keep4(salt, (uint32_t)(((size_t)b * N + n + 16 * u) * D + d), thr, k);
-              v[u].x = k[0] ? v[u].x * dsc : 0.f;
-              v[u].y = k[1] ? v[u].y * dsc : 0.f;
-              v[u].z = k[2] ? v[u].z * dsc : 0.f;
-              v[u].w = k[3] ? v[u].w * dsc : 0.f;
-            }
-            acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
-          }
-        }
-        for (; n < N; n += 16) {
-          float4 v = *reinterpret_cast<const float4*>(gb + (size_t)n * D);
-          if (thr) {
-            bool k[4];
-            dropout_keep4(salt, (uint32_t)(((size_t)b * N + n) * D + d), thr, k);
-            v.x = k[0] ? v.x * dsc : 0.f;
-            v.y = k[1] ? v.y * dsc : 0.f;
-            v.z = k[2] ? v.z * dsc : 0.f;
-            v.w = k[3] ? v.w * dsc : 0.f;
-          }
-          acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-        }
-      }
-    }
-    racc[tl][cl] = acc;
-    __syncthreads();
-    if (tl == 0 && d < D) {
-      float4 s4 = racc[0][cl];
-#pragma unroll
-      for (int l = 1; l < 16; ++l) {
-        const float4 q = racc[l][cl];
-        s4.x += q.x; s4.y += q.y; s4.z += q.z; s4.w += q.w;
-      }
-      float4* dst = reinterpret_cast<float4*>(dtemb + (size_t)t0 * D + d);
-      float4 o = *dst;  // this workgroup is the row's only writer in the launch
-      o.x += s4.x; o.y += s4.y; o.z += s4.z; o.w += s4.w;
-      *dst = o;
-    }
+    emb_part_b<256>(e, bid - blocksA, smem, nullptr);
   } else if (bid >= blocksA + blocksB + blocksC) {
-    // part D: LayerNorm dgamma/dbeta replica finalize (replica_reduce_kernel's work;
-    // every LayerNorm backward has run before the embedding backward)
-    const int rb = bid - blocksA - blocksB - blocksC, cb = (rf.C + 255) / 256;
-    const int gi = rb / cb, c = (rb - gi * cb) * 256 + threadIdx.x;
-    if (c >= rf.C) return;
-    const float* w = rf.ws + (size_t)gi * rf.rows * rf.C + c;
-    float s = 0.f;
-    for (int r = 0; r < rf.R; ++r) s += w[(size_t)r * rf.C];  // row order: deterministic
-    rf.dsts[gi][c] = rf.store ? s : rf.dsts[gi][c] + s;
+    emb_part_d<256>(rf, bid - blocksA - blocksB - blocksC, smem, nullptr);
   } else {
+    const float* g = e.g;
+    const int B = e.B, N = e.N, D = e.D;
+    const uint32_t thr = e.thr, salt = thr ? site_salt(e.rng, e.site) : 0u;
+    const float dsc = e.dsc;
     // part C: 4 consecutive columns per thread (one 16-B load, two pair hashes, one 8-B
     // store) with 32-bit index math (the launcher checks the size); one element per
     // thread with 64-bit divisions was ~1/3 of this launch at vit_small_200
@@ -451,25 +340,38 @@ void patchify_cls_launch(const float* img, const int64_t* t, const float* cls, c
 
 void embed_bwd_launch(const float* g, const int64_t* t, float* dcls, float* dpos, float* dtemb, void* gpatch, int B,
                       int N, int D, const int64_t* rng, int site, double p, hipStream_t stream, ReplicaFinal rf) {
-  const int pbn0 = std::min(B, EMB_BMAX);
-  const int blocksA = cdiv(N * D, 256), blocksB = pbn0 * cdiv(D, EMB_BCOLS);
   if (D % 4 != 0) throw std::invalid_argument("embed_bwd: D must be a multiple of 4");
   if ((size_t)B * N * D >= (size_t)INT32_MAX) throw std::invalid_argument("embed_bwd: too many elements for 32-bit indexing");
+  EmbedGrad e = embed_grad_args(g, t, dcls, dpos, dtemb, B, N, D, rng, site, p, 0, std::min(B, EMB_BMAX));
+  const int blocksA = cdiv(N * D, 256), blocksB = e.pbn * cdiv(D, EMB_BCOLS);
   const int blocksC = grid_for((size_t)B * (N - 1) * D / 4);
-  const int blocksD = rf.ws ? rf.G * cdiv(rf.C, 256) : 0;
-  const uint32_t thr = drop_threshold_host(p);
-  const float dsc = p > 0 ? 1.f / (1.f - (float)p) : 1.f;
-  hipLaunchKernelGGL(embed_bwd_kernel, dim3(blocksA + blocksB + blocksC + blocksD), dim3(256), 0, stream, g, t, dcls,
-                     dpos, dtemb, reinterpret_cast<bf16*>(gpatch), B, N, D, rng, site, thr, dsc, blocksA, blocksB,
-                     blocksC, rf, 0, pbn0);
-  // batches beyond EMB_BMAX samples: further part-B passes (stream-ordered: each adds
-  // to the rows the previous passes wrote; a sample's t is owned in its own pass)
+  const int blocksD = rf.ws ? rf.G * cdiv(rf.C, 16) : 0;
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3(blocksA + blocksB + blocksC + blocksD), dim3(256), 0, stream, e,
+                     reinterpret_cast<bf16*>(gpatch), blocksA, blocksB, blocksC, rf);
+  // batches beyond EMB_BMAX samples: further part-B passes (stream-ordered: each adds to
+  // the rows the previous passes wrote; a sample's t is owned in its own pass)
   for (int pb0 = EMB_BMAX; pb0 < B; pb0 += EMB_BMAX) {
-    const int pbn = std::min(B - pb0, EMB_BMAX), nb = pbn * cdiv(D, EMB_BCOLS);
-    hipLaunchKernelGGL(embed_bwd_kernel, dim3(nb), dim3(256), 0, stream, g, t, dcls, dpos, dtemb,
-                       reinterpret_cast<bf16*>(gpatch), B, N, D, rng, site, thr, dsc, 0, nb, 0, ReplicaFinal(), pb0,
-                       pbn);
+    EmbedGrad ep = e;
+    ep.pb0 = pb0;
+    ep.pbn = std::min(B - pb0, EMB_BMAX);
+    const int nb = ep.pbn * cdiv(D, EMB_BCOLS);
+    hipLaunchKernelGGL(embed_bwd_kernel, dim3(nb), dim3(256), 0, stream, ep, reinterpret_cast<bf16*>(gpatch), 0, nb,
+                       0, ReplicaFinal());
   }
+}
+
+EmbedGrad embed_grad_args(const float* g, const int64_t* t, float* dcls, float* dpos, float* dtemb, int B, int N,
+                          int D, const int64_t* rng, int site, double p, int pb0, int pbn) {
+  EmbedGrad e;
+  e.g = g; e.t = t; e.dcls = dcls; e.dpos = dpos; e.dtemb = dtemb;
+  e.B = B; e.N = N; e.D = D;
+  e.thr = drop_threshold_host(p);
+  e.dsc = p > 0 ? 1.f / (1.f - (float)p) : 1.f;
+  e.rng = rng;
+  e.site = site;
+  e.pb0 = pb0; e.pbn = pbn;
+  e.owners = pbn;
+  return e;
 }
 
 int smooth_l1_launch(const float* pred, const float* target, float* loss, float* partials, void* dtok, int B,

@@ -28,6 +28,7 @@
 #include "kernels.h"
 #include "gemm_common.h"
 #include "gemm_epi.h"
+#include "embed_parts.h"
 #include <cstdlib>
 #include <algorithm>
 #include <type_traits>
@@ -621,11 +622,17 @@ struct WgradMulti {
   int n;
   int store;  // every target is zero: plain stores (no read-add)
   WgradSq sq;  // sq.parts != nullptr: grad-norm partials (kernels.h)
+  // embedding gradients + LayerNorm finalize as extra workgroups (embed_parts.h parts A,
+  // B, D; single-process step): nA / nB / nD workgroups after the grad-norm tail, each
+  // writing its grad-norm partial to slot tiles + sq.tail + (its index among them)
+  EmbedGrad emb;
+  ReplicaFinal rf;
+  int nA, nB, nD;
 };
-// tail workgroup j of the fused grad-norm: squares of the arena ranges no tile
-// writes, then zero the unused partial slots
+// tail workgroup j of the fused grad-norm: squares of the arena ranges no tile or
+// embedding workgroup writes, then zero the unused partial slots (from zfrom on)
 template <int NT>
-__device__ __forceinline__ void wgrad_sq_tail(const WgradSq& sq, int tiles, int j) {
+__device__ __forceinline__ void wgrad_sq_tail(const WgradSq& sq, int tiles, int j, int zfrom) {
   float s = 0.f;
   const int64_t stride = (int64_t)sq.tail * NT;
   for (int r = 0; r < sq.nr; ++r)
@@ -643,7 +650,7 @@ __device__ __forceinline__ void wgrad_sq_tail(const WgradSq& sq, int tiles, int 
     for (int w = 0; w < NT / 64; ++w) t += red[w];
     sq.parts[tiles + j] = t;
   }
-  for (int i = tiles + sq.tail + j * NT + threadIdx.x; i < sq.nparts; i += sq.tail * NT) sq.parts[i] = 0.f;
+  for (int i = zfrom + j * NT + threadIdx.x; i < sq.nparts; i += sq.tail * NT) sq.parts[i] = 0.f;
 }
 // T x TN output tiles of WM x WN waves: 64 x 64 / 4 waves (ViT-tiny, sampler-sized
 // token counts), 128 x 128 / 8 waves when the reduction runs over >= BIG_WG_K tokens
@@ -653,12 +660,28 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_wgrad_multi_kernel(WgradMul
   const int tiles = gm.tile_start[gm.n];
   // the grad-norm tail workgroups first, so their strided sweeps over the untiled arena
   // ranges overlap the tiles instead of trailing them (within noise: profiles/tail_first_r5.txt)
-  const int extra = (int)gridDim.x - tiles;
-  if ((int)blockIdx.x < extra) {
-    wgrad_sq_tail<64 * WM * WN>(gm.sq, tiles, blockIdx.x);
+  // block order: the grad-norm tail and the embedding parts first (their strided sweeps
+  // and latency-bound column sums overlap the tiles instead of trailing them:
+  // profiles/tail_first_r5.txt; embedding parts last measured 1 % slower per ViT-tiny
+  // step on one box: profiles/embed_in_wgrad_r6.txt), then the tiles
+  constexpr int NT = 64 * WM * WN;
+  const int ne = gm.nA + gm.nB + gm.nD;
+  const int tail = (int)gridDim.x - tiles - ne;
+  if ((int)blockIdx.x < tail) {
+    wgrad_sq_tail<NT>(gm.sq, tiles, blockIdx.x, tiles + tail + ne);
     return;
   }
-  const int bid = xcd_remap((int)blockIdx.x - extra, tiles);
+  if ((int)blockIdx.x < tail + ne) {
+    // embedding parts: their scratch is the LDS operand ring (unused by them)
+    extern __shared__ __attribute__((aligned(16))) char smem_emb[];
+    const int k = (int)blockIdx.x - tail;
+    float* sqp = gm.sq.parts ? gm.sq.parts + tiles + tail + k : nullptr;
+    if (k < gm.nA) emb_part_a<NT>(gm.emb, k, sqp, reinterpret_cast<float*>(smem_emb));
+    else if (k < gm.nA + gm.nB) emb_part_b<NT>(gm.emb, k - gm.nA, smem_emb, sqp);
+    else emb_part_d<NT>(gm.rf, k - gm.nA - gm.nB, smem_emb, sqp);
+    return;
+  }
+  const int bid = xcd_remap((int)blockIdx.x - tail - ne, tiles);
   int lo = 0, hi = gm.n - 1;  // problem owning tile `bid`: binary search over tile_start
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -809,7 +832,15 @@ void gemm_wgrad(const GemmArgs& a, int splits, hipStream_t stream) {
   launch_auto<true, true, EPI_ATOMIC>(p, splits, stream);
 }
 
-int gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool store, const WgradSq* sq) {
+int wgrad_embed_workgroups(const WgradEmbed& emb, bool wide) {
+  const int NT = wide ? 512 : 256;
+  const EmbedGrad& e = emb.e;
+  return (e.N * e.D + NT - 1) / NT + e.owners * ((e.D + EMB_BCOLS - 1) / EMB_BCOLS) +
+         (emb.rf.ws ? emb.rf.G * ((emb.rf.C + 15) / 16) : 0);
+}
+
+int gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool store, const WgradSq* sq,
+                     const WgradEmbed* emb) {
   if (n < 1 || n > WM_MAX) throw std::runtime_error("gemm_wgrad_multi: 1..WGRAD_MULTI_MAX problems per launch");
   WgradMulti gm{};
   gm.n = n;
@@ -836,12 +867,25 @@ int gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool stor
   }
   for (int i = n; i <= WM_MAX; ++i) gm.tile_start[i] = tiles;
   int extra = 0;
+  if (emb != nullptr) {
+    const int NT = T == 128 ? 512 : 256;
+    const EmbedGrad& e = emb->e;
+    if (e.B > EMB_BMAX || e.pbn != e.B || e.pb0 != 0 || e.D % 4)
+      throw std::runtime_error("gemm_wgrad_multi: embedding parts need <= 256 samples (one part-B pass), D % 4 == 0");
+    gm.emb = e;
+    gm.rf = emb->rf;
+    gm.nA = (e.N * e.D + NT - 1) / NT;
+    gm.nB = e.owners * ((e.D + EMB_BCOLS - 1) / EMB_BCOLS);
+    gm.nD = emb->rf.ws ? emb->rf.G * ((emb->rf.C + 15) / 16) : 0;
+    extra += gm.nA + gm.nB + gm.nD;
+    if (extra != wgrad_embed_workgroups(*emb, T == 128)) throw std::logic_error("wgrad_embed_workgroups");
+  }
   if (sq != nullptr && sq->parts != nullptr) {
-    if (sq->tail < 0 || sq->nr < 0 || sq->nr > WSQ_MAX_RANGES || sq->nparts < tiles + sq->tail)
-      throw std::runtime_error("gemm_wgrad_multi: grad-norm partial buffer too small (nparts < tiles + tail) "
-                               "or more than 16 ranges");
+    if (sq->tail < 0 || sq->nr < 0 || sq->nr > WSQ_MAX_RANGES || sq->nparts < tiles + sq->tail + extra)
+      throw std::runtime_error("gemm_wgrad_multi: grad-norm partial buffer too small (nparts < tiles + tail + "
+                               "embedding workgroups) or more than 16 ranges");
     gm.sq = *sq;
-    extra = sq->tail;
+    extra += sq->tail;
   }
   static_assert(sizeof(WgradMulti) <= 4000, "kernel argument block");
   if (T == 128) {

@@ -102,26 +102,30 @@ struct WgradSq {
   int64_t lo[WSQ_MAX_RANGES], hi[WSQ_MAX_RANGES];
 };
 // returns the output tiles launched (grad-norm partial slots used before the tail);
-// sq->tail = 0: no tail workgroups, no zero fill (all but the last launch of a step)
+// sq->tail = 0: no tail workgroups, no zero fill (all but the last launch of a step).
+// emb (optional): the embedding gradients and the LayerNorm slot finalize ride in the
+// launch as extra workgroups (embed_parts.h), each writing the grad-norm partial of its
+// outputs after the tail's slots.
+struct WgradEmbed;  // below
 int gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool store = false,
-                     const WgradSq* sq = nullptr);
+                     const WgradSq* sq = nullptr, const WgradEmbed* emb = nullptr);
+int wgrad_embed_workgroups(const WgradEmbed& emb, bool wide);  // extra workgroups (= grad-norm slots) emb takes
 
 // LayerNorm (layernorm.hip)
 void layernorm_fwd_launch(const float* x, const float* gamma, const float* beta, void* y_bf16, float* mean,
                           float* rstd, int M, int D, float eps, hipStream_t stream);
-// dgamma||dbeta: each workgroup stores its column partial in slots [ln_bwd_workgroups(M)][2D]
-// (scratch), and per group of 16 workgroups the last to arrive writes the group's sum, in
-// workgroup order, to row g of ws [ln_replicas(M)][2D]; tickets [ln_replicas(M)] must be
-// zero on entry (the last arriver re-zeroes its ticket).  replica_reduce_launch adds the
-// R rows of each workspace into its destination, in row order: deterministic.
+// dgamma||dbeta: workgroup w of the backward (ln_bwd_workgroups(M) of them) stores its
+// column partial in row w of slots [ln_bwd_workgroups(M)][2D] (plain stores, no
+// atomics); replica_reduce_launch (or the embedding backward / weight-gradient
+// launch) sums the rows in row order: deterministic.  gp_bf16 (optional): the
+// patch-embedding input gradient (g_out rows 1..N-1 per sample, embedding dropout
+// p_emb at site_emb, bf16, patch-row order).
 void layernorm_bwd_launch(const void* dy, bool dy_bf16, const void* x, bool x_bf16, const float* mean, const float* rstd,
                           const float* gamma, const float* beta, const float* g_res, float* g_out, void* gy_bf16,
-                          void* y_bf16, float* dgb_ws, int M,
+                          void* y_bf16, float* slots, int M,
                           int D, int tokens, const int64_t* rng, int site_drop, double p_drop, int site_dp,
-                          double p_dp, int dy_parts, float* slots, unsigned* tickets, hipStream_t stream);
+                          double p_dp, int dy_parts, void* gp_bf16, int site_emb, double p_emb, hipStream_t stream);
 int ln_bwd_workgroups(int M);
-int ln_replicas(int M);
-int ln_ticket_rows(int M, int D);
 
 // LayerNorm fold weights for the GEMMs that consume a LayerNorm (layernorm.hip)
 constexpr int FOLD_MAX = 32;  // GEMMs per fold launch (vit_small_200: 25 in one launch)
@@ -208,6 +212,28 @@ struct ReplicaFinal {
   int G = 0, R = 0, C = 0, rows = 0;
   int store = 0;
 };
+// Embedding-gradient reductions (embed_parts.h): the argument block
+struct EmbedGrad {
+  const float* g = nullptr;      // [B][N][D] gradient of the embedding output (the last LayerNorm's g_out)
+  const int64_t* t = nullptr;    // [B] timesteps
+  float* dcls = nullptr;         // [D]
+  float* dpos = nullptr;         // [N][D]
+  float* dtemb = nullptr;        // [T][D]
+  int B = 0, N = 0, D = 0;
+  const int64_t* rng = nullptr;  // {seed, step}: the dropout salt is derived on the device
+  int site = 0;
+  uint32_t thr = 0;              // embedding dropout (pos_drop)
+  float dsc = 1.f;
+  int pb0 = 0, pbn = 0;          // part-B sample pass
+  int owners = 0;                // part-B timestep slots launched (<= distinct timesteps possible)
+};
+// the embedding parts as extra workgroups of the weight-gradient launch (gemm.hip)
+struct WgradEmbed {
+  EmbedGrad e;
+  ReplicaFinal rf;
+};
+EmbedGrad embed_grad_args(const float* g, const int64_t* t, float* dcls, float* dpos, float* dtemb, int B, int N,
+                          int D, const int64_t* rng, int site, double p, int pb0, int pbn);
 void embed_bwd_launch(const float* g, const int64_t* t, float* dcls, float* dpos, float* dtemb, void* gpatch,
                       int B, int N, int D, const int64_t* rng, int site, double p, hipStream_t stream, ReplicaFinal rf = ReplicaFinal());
 // returns the number of per-block loss partials written; finish = false leaves

@@ -9,18 +9,21 @@
 //   * the *next* residual branch's gradient prep  gy = bf16(g_out * dropout
 //     mask * drop-path scale)  (masks regenerated from the counter hash),
 //   * dgamma/dbeta column partials, deterministic: reduced per workgroup through
-//     LDS into a slot of its own (write-through), then per group of LN_GROUP
-//     consecutive workgroups the last to arrive (agent-scope ticket) sums the
-//     group's slots in workgroup order into the group's row of the workspace; the
-//     finalize (replica_reduce / the embedding-backward launch) sums those rows in
-//     row order.  No fp32 atomics: two runs are bit-identical.
+//     LDS into a slot of its own (one row of the workspace, plain stores); a later
+//     launch (replica_reduce, the embedding backward or the weight-gradient launch)
+//     sums the slots in slot order.  No fp32 atomics: two runs are bit-identical.
+//     (An in-launch reduction -- write-through slots, an agent-scope ticket, the
+//     last of 16 workgroups summing -- measured 5.7 -> 12.5 us per ViT-tiny launch:
+//     every workgroup then waits for its stores to drain, and the last arriver's
+//     acquire + slot reads trail the launch.)
 #include "common.h"
 #include "kernels.h"
+#include <algorithm>
 
 namespace dc {
 
-constexpr int LN_NW = 8;      // waves (rows) per workgroup of the backward
-constexpr int LN_GROUP = 16;  // workgroups per in-launch reduction group
+constexpr int LN_NW = 8;        // waves (rows) per workgroup of the backward
+constexpr int LN_MAX_WG = 512;  // backward workgroups (= dgamma/dbeta slots) at most
 
 template <int VEC, int NW>
 __global__ __launch_bounds__(NW * 64) void ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
@@ -73,18 +76,24 @@ __global__ __launch_bounds__(NW * 64) void ln_fwd_kernel(const float* __restrict
 
 // DYB: dy (and its K-split partials) in bf16 -- the dgrad GEMMs write half the bytes.
 // XB: x is the bf16 copy of the LayerNorm input, the operand the folded forward GEMM
-// actually normalised (x_hat from it is the forward's own), 2 bytes per element less
+// actually normalised (x_hat from it is the forward's own), 2 bytes per element less.
+// Rows: groups of NW*RPW rows, workgroup-strided (grid = ln_bwd_workgroups(M), at most
+// LN_MAX_WG: the dgamma/dbeta slots a finalize reads stay bounded at large M).
+// gp (the last LayerNorm of the backward, whose output gradient feeds the embedding):
+// also the patch-row gradient of the patch embedding -- g_out rows 1..N-1 of each
+// sample with the embedding dropout (site_emb) applied, bf16, in patch-row order
+// (what the embedding backward's part C wrote).
 template <int VEC, int RPW, int NW, bool DYB, bool XB>
 __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict__ dyv, const void* __restrict__ x,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
                                                      const float* __restrict__ g_res,
                                                      float* __restrict__ g_out, bf16* __restrict__ gy,
-                                                     bf16* __restrict__ y_out, float* __restrict__ dgb_ws, int M,
+                                                     bf16* __restrict__ y_out, float* __restrict__ slots, int M,
                                                      int tokens, const int64_t* __restrict__ rng, int site_drop,
                                                      uint32_t thr_drop, float sc_drop, int site_dp, uint32_t thr_dp,
-                                                     float sc_dp, int dy_parts, float* __restrict__ slots,
-                                                     unsigned* __restrict__ tickets) {
+                                                     float sc_dp, int dy_parts, bf16* __restrict__ gp, int site_emb,
+                                                     uint32_t thr_emb, float sc_emb) {
   constexpr int D = VEC * 128;
   // dynamic LDS ([NW][2D] floats): static LDS limited the residency of the larger
   // non-256-thread workgroups (tools/ub_lds_census.hip)
@@ -104,109 +113,126 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict_
   // explicit wait for all of them (below): site_salt() here was sunk by the compiler
   // past the row-data wait, one more dependent round trip per wave
   const uint64_t rng0 = (uint64_t)rng[0], rng1 = (uint64_t)rng[1];  // rng: always a valid [2]
-  // RPW rows per wave, all rows' loads issued before any use (latency-bound op)
-  float2 xv[RPW][VEC], dv[RPW][VEC], rv[RPW][VEC];
-  float muv[RPW], rsv[RPW];
-  int rows[RPW];
+  for (int grp = blockIdx.x; grp * NW * RPW < M; grp += gridDim.x) {
+    // RPW rows per wave, all rows' loads issued before any use (latency-bound op)
+    float2 xv[RPW][VEC], dv[RPW][VEC], rv[RPW][VEC];
+    float muv[RPW], rsv[RPW];
+    int rows[RPW];
 #pragma unroll
-  for (int j = 0; j < RPW; ++j) {
-    rows[j] = (blockIdx.x * NW + wave) * RPW + j;
-    const int row = rows[j] < M ? rows[j] : M - 1;
-    const float2* xr = reinterpret_cast<const float2*>(reinterpret_cast<const float*>(x) + (size_t)row * D);
-    const bf16x2* xr16 = reinterpret_cast<const bf16x2*>(reinterpret_cast<const bf16*>(x) + (size_t)row * D);
-    // unconditional load (g_out when there is no residual gradient: same shape, the value
-    // is dropped below): `g_res ? load : 0` became a phi copy that waited for every load
-    // issued before it
-    const float2* gr = reinterpret_cast<const float2*>((g_res ? g_res : g_out) + (size_t)row * D);
-    auto ldy = [&](int pt, int i) -> float2 {
-      const size_t off = (size_t)pt * M * D + (size_t)row * D;
-      if (DYB) {
-        const bf16x2 e = reinterpret_cast<const bf16x2*>(reinterpret_cast<const bf16*>(dyv) + off)[lane + 64 * i];
-        return make_float2(bf2f(e[0]), bf2f(e[1]));
-      }
-      return reinterpret_cast<const float2*>(reinterpret_cast<const float*>(dyv) + off)[lane + 64 * i];
-    };
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) {
-      if (XB) {
-        const bf16x2 e = xr16[lane + 64 * i];
-        xv[j][i] = make_float2(bf2f(e[0]), bf2f(e[1]));
-      } else {
-        xv[j][i] = xr[lane + 64 * i];
-      }
-      dv[j][i] = ldy(0, i);
-      rv[j][i] = gr[lane + 64 * i];
-    }
-    for (int pt = 1; pt < dy_parts; ++pt) {  // K-split dgrad partials
+    for (int j = 0; j < RPW; ++j) {
+      rows[j] = (grp * NW + wave) * RPW + j;
+      const int row = rows[j] < M ? rows[j] : M - 1;
+      const float2* xr = reinterpret_cast<const float2*>(reinterpret_cast<const float*>(x) + (size_t)row * D);
+      const bf16x2* xr16 = reinterpret_cast<const bf16x2*>(reinterpret_cast<const bf16*>(x) + (size_t)row * D);
+      // unconditional load (g_out when there is no residual gradient: same shape, the value
+      // is dropped below): `g_res ? load : 0` became a phi copy that waited for every load
+      // issued before it
+      const float2* gr = reinterpret_cast<const float2*>((g_res ? g_res : g_out) + (size_t)row * D);
+      auto ldy = [&](int pt, int i) -> float2 {
+        const size_t off = (size_t)pt * M * D + (size_t)row * D;
+        if (DYB) {
+          const bf16x2 e = reinterpret_cast<const bf16x2*>(reinterpret_cast<const bf16*>(dyv) + off)[lane + 64 * i];
+          return make_float2(bf2f(e[0]), bf2f(e[1]));
+        }
+        return reinterpret_cast<const float2*>(reinterpret_cast<const float*>(dyv) + off)[lane + 64 * i];
+      };
 #pragma unroll
       for (int i = 0; i < VEC; ++i) {
-        const float2 e = ldy(pt, i);
-        dv[j][i].x += e.x;
-        dv[j][i].y += e.y;
-      }
-    }
-    muv[j] = mean[row];
-    rsv[j] = rstd[row];
-  }
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): rows + rng words (gfx9: expcnt 7, lgkmcnt 15)
-  // unconditional (a few VALU ops): a use only under `if (gy)` let LLVM sink the loads
-  // into that block, past the wait
-  const uint32_t salt_drop = site_salt_v(rng0, rng1, site_drop);
-  const uint32_t salt_dp = site_salt_v(rng0, rng1, site_dp);
-#pragma unroll
-  for (int j = 0; j < RPW; ++j) {
-    const int row = rows[j];
-    if (row >= M) continue;
-    const float mu = muv[j], rs = rsv[j];
-    float2 xh[VEC], dxh[VEC];
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) {
-      const float2 dvv = dv[j][i];
-      xh[i] = make_float2((xv[j][i].x - mu) * rs, (xv[j][i].y - mu) * rs);
-      dgam[i].x += dvv.x * xh[i].x;
-      dgam[i].y += dvv.y * xh[i].y;
-      dbet[i].x += dvv.x;
-      dbet[i].y += dvv.y;
-      dxh[i] = make_float2(dvv.x * gm[i].x, dvv.y * gm[i].y);
-      s1 += dxh[i].x + dxh[i].y;
-      s2 += dxh[i].x * xh[i].x + dxh[i].y * xh[i].y;
-    }
-    const float c1 = wave_sum(s1) * (1.0f / D);
-    const float c2 = wave_sum(s2) * (1.0f / D);
-    float dpsc = 1.f;
-    if (gy && thr_dp) dpsc = dropout_keep(salt_dp, (uint32_t)(row / tokens), thr_dp) ? sc_dp : 0.f;
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) {
-      const int c = lane + 64 * i;
-      const float2 r = g_res ? rv[j][i] : make_float2(0.f, 0.f);
-      float2 o = make_float2((dxh[i].x - c1 - xh[i].x * c2) * rs + r.x, (dxh[i].y - c1 - xh[i].y * c2) * rs + r.y);
-      reinterpret_cast<float2*>(g_out + (size_t)row * D)[c] = o;
-      if (y_out) {
-        // the LayerNorm output itself (bf16), for the weight gradient of the GEMM
-        // that consumed it with the LayerNorm folded in (no forward LayerNorm launch)
-        bf16x2 yv;
-        yv[0] = f2bf(xh[i].x * gm[i].x + bt[i].x);
-        yv[1] = f2bf(xh[i].y * gm[i].y + bt[i].y);
-        reinterpret_cast<bf16x2*>(y_out + (size_t)row * D)[c] = yv;
-      }
-      if (gy) {
-        float a = o.x * dpsc, b = o.y * dpsc;
-        if (thr_drop) {
-          const uint32_t idx = (uint32_t)((size_t)row * D + 2 * c);
-          const uint32_t hh = drop_hash(salt_drop, idx >> 1);  // idx even: one hash for the pair
-          a = (hh & 0xFFFFu) >= thr_drop ? a * sc_drop : 0.f;
-          b = (hh >> 16) >= thr_drop ? b * sc_drop : 0.f;
+        if (XB) {
+          const bf16x2 e = xr16[lane + 64 * i];
+          xv[j][i] = make_float2(bf2f(e[0]), bf2f(e[1]));
+        } else {
+          xv[j][i] = xr[lane + 64 * i];
         }
-        bf16x2 h;
-        h[0] = f2bf(a);
-        h[1] = f2bf(b);
-        reinterpret_cast<bf16x2*>(gy + (size_t)row * D)[c] = h;
+        dv[j][i] = ldy(0, i);
+        rv[j][i] = gr[lane + 64 * i];
+      }
+      for (int pt = 1; pt < dy_parts; ++pt) {  // K-split dgrad partials
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+          const float2 e = ldy(pt, i);
+          dv[j][i].x += e.x;
+          dv[j][i].y += e.y;
+        }
+      }
+      muv[j] = mean[row];
+      rsv[j] = rstd[row];
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): rows + rng words (gfx9: expcnt 7, lgkmcnt 15)
+    // unconditional (a few VALU ops): a use only under `if (gy)` let LLVM sink the loads
+    // into that block, past the wait
+    const uint32_t salt_drop = site_salt_v(rng0, rng1, site_drop);
+    const uint32_t salt_dp = site_salt_v(rng0, rng1, site_dp);
+    const uint32_t salt_emb = site_salt_v(rng0, rng1, site_emb);
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+      const int row = rows[j];
+      if (row >= M) continue;
+      const float mu = muv[j], rs = rsv[j];
+      float2 xh[VEC], dxh[VEC];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        const float2 dvv = dv[j][i];
+        xh[i] = make_float2((xv[j][i].x - mu) * rs, (xv[j][i].y - mu) * rs);
+        dgam[i].x += dvv.x * xh[i].x;
+        dgam[i].y += dvv.y * xh[i].y;
+        dbet[i].x += dvv.x;
+        dbet[i].y += dvv.y;
+        dxh[i] = make_float2(dvv.x * gm[i].x, dvv.y * gm[i].y);
+        s1 += dxh[i].x + dxh[i].y;
+        s2 += dxh[i].x * xh[i].x + dxh[i].y * xh[i].y;
+      }
+      const float c1 = wave_sum(s1) * (1.0f / D);
+      const float c2 = wave_sum(s2) * (1.0f / D);
+      float dpsc = 1.f;
+      if (gy && thr_dp) dpsc = dropout_keep(salt_dp, (uint32_t)(row / tokens), thr_dp) ? sc_dp : 0.f;
+      const int tok = row % tokens;
+      bf16* gprow = (gp && tok != 0) ? gp + ((size_t)(row / tokens) * (tokens - 1) + tok - 1) * D : nullptr;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        const int c = lane + 64 * i;
+        const float2 r = g_res ? rv[j][i] : make_float2(0.f, 0.f);
+        float2 o = make_float2((dxh[i].x - c1 - xh[i].x * c2) * rs + r.x, (dxh[i].y - c1 - xh[i].y * c2) * rs + r.y);
+        reinterpret_cast<float2*>(g_out + (size_t)row * D)[c] = o;
+        if (y_out) {
+          // the LayerNorm output itself (bf16), for the weight gradient of the GEMM
+          // that consumed it with the LayerNorm folded in (no forward LayerNorm launch)
+          bf16x2 yv;
+          yv[0] = f2bf(xh[i].x * gm[i].x + bt[i].x);
+          yv[1] = f2bf(xh[i].y * gm[i].y + bt[i].y);
+          reinterpret_cast<bf16x2*>(y_out + (size_t)row * D)[c] = yv;
+        }
+        if (gy) {
+          float a = o.x * dpsc, b = o.y * dpsc;
+          if (thr_drop) {
+            const uint32_t idx = (uint32_t)((size_t)row * D + 2 * c);
+            const uint32_t hh = drop_hash(salt_drop, idx >> 1);  // idx even: one hash for the pair
+            a = (hh & 0xFFFFu) >= thr_drop ? a * sc_drop : 0.f;
+            b = (hh >> 16) >= thr_drop ? b * sc_drop : 0.f;
+          }
+          bf16x2 h;
+          h[0] = f2bf(a);
+          h[1] = f2bf(b);
+          reinterpret_cast<bf16x2*>(gy + (size_t)row * D)[c] = h;
+        }
+        if (gprow) {  // patch-embedding input gradient (embedding dropout, same pair hash)
+          float a = o.x, b = o.y;
+          if (thr_emb) {
+            const uint32_t hh = drop_hash(salt_emb, (uint32_t)((size_t)row * D + 2 * c) >> 1);
+            a = (hh & 0xFFFFu) >= thr_emb ? a * sc_emb : 0.f;
+            b = (hh >> 16) >= thr_emb ? b * sc_emb : 0.f;
+          }
+          bf16x2 h;
+          h[0] = f2bf(a);
+          h[1] = f2bf(b);
+          reinterpret_cast<bf16x2*>(gprow)[c] = h;
+        }
       }
     }
   }
-  // column partials: waves -> LDS -> this workgroup's slot, stored write-through (sc1:
-  // read by the group's last workgroup, possibly on another XCD), then drained
+  // column partials: waves -> LDS -> this workgroup's slot (plain stores, summed in
+  // slot order by a later launch: deterministic, no atomics)
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
     const int c = 2 * (lane + 64 * i);
@@ -217,57 +243,22 @@ __global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const void* __restrict_
   }
   __syncthreads();
   float* slot = slots + (size_t)blockIdx.x * 2 * D;
-  for (int c = 2 * threadIdx.x; c < 2 * D; c += 2 * NW * 64) {
-    float s0 = 0.f, s1 = 0.f;
+  for (int c = threadIdx.x; c < 2 * D; c += NW * 64) {
+    float s = 0.f;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      s0 += red[w][c];
-      s1 += red[w][c + 1];
-    }
-    st_f2_sc1(slot + c, s0, s1);
+    for (int w = 0; w < NW; ++w) s += red[w][c];
+    slot[c] = s;
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its slot stores
-  __syncthreads();
-  // group ticket (agent scope); the workgroup whose add comes last reduces the group.
-  // "I am last" goes through the one LDS array (red[0][0]) after the barrier
-  const int grp = blockIdx.x / LN_GROUP, g0 = grp * LN_GROUP;
-  const int g1 = min((int)gridDim.x, g0 + LN_GROUP);
-  if (threadIdx.x == 0) {
-    const unsigned prev = __hip_atomic_fetch_add((gu32*)(tickets + grp), 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = prev == (unsigned)(g1 - g0 - 1);
-    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    red[0][0] = last ? 1.f : 0.f;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  if (red[0][0] == 0.f) return;
-  // the group's slots in workgroup order (sc1 loads: L1-bypassing, like the stores)
-  float* row = dgb_ws + (size_t)grp * 2 * D;
-  for (int c = 2 * threadIdx.x; c < 2 * D; c += 2 * NW * 64) {
-    float s0 = 0.f, s1 = 0.f;
-    for (int b = g0; b < g1; ++b) {
-      const uint64_t v = ld8_sc1(slots + (size_t)b * 2 * D + c);
-      s0 += __uint_as_float((uint32_t)v);
-      s1 += __uint_as_float((uint32_t)(v >> 32));
-    }
-    row[c] = s0;
-    row[c + 1] = s1;
-  }
-  if (threadIdx.x == 0) __hip_atomic_store((gu32*)(tickets + grp), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// dst[g][c] += sum_{r < R} ws[g][r][c] (rows of stride `rows`), in row order.  One
-// launch finalises many LayerNorms.
+// dst[g][c] += sum_{r < R} ws[g][r][c] (rows of stride `rows`) in a fixed order
+// (common.h slot_colsum16).  One launch finalises many LayerNorms.
 __global__ __launch_bounds__(256) void replica_reduce_kernel(const float* __restrict__ ws,
                                                              float* const* __restrict__ dsts, int C, int R, int rows) {
-  const int gi = blockIdx.y;
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  const float* w = ws + (size_t)gi * rows * C + c;
-  float s = 0.f;
-  for (int r = 0; r < R; ++r) s += w[(size_t)r * C];
-  dsts[gi][c] += s;
+  __shared__ float red[256];
+  const int gi = blockIdx.y, c0 = blockIdx.x * 16;
+  const float t = slot_colsum16<256>(ws + (size_t)gi * rows * C, C, R, c0, red);
+  if (threadIdx.x < 16 && c0 + (int)threadIdx.x < C) dsts[gi][c0 + threadIdx.x] += t;
 }
 
 // LayerNorm fold weights (see gemm.hip "LayerNorm fold"): for each GEMM that
@@ -465,22 +456,24 @@ void layernorm_fwd_launch(const float* x, const float* gamma, const float* beta,
 
 void layernorm_bwd_launch(const void* dy, bool dy_bf16, const void* x, bool x_bf16, const float* mean, const float* rstd,
                           const float* gamma, const float* beta, const float* g_res, float* g_out, void* gy_bf16,
-                          void* y_bf16, float* dgb_ws, int M,
+                          void* y_bf16, float* slots, int M,
                           int D, int tokens, const int64_t* rng, int site_drop, double p_drop, int site_dp,
-                          double p_dp, int dy_parts, float* slots, unsigned* tickets, hipStream_t stream) {
+                          double p_dp, int dy_parts, void* gp_bf16, int site_emb, double p_emb, hipStream_t stream) {
   if (D % 128) throw std::runtime_error("layernorm: D % 128 != 0");
-  const uint32_t td = drop_threshold_host(p_drop), tp = drop_threshold_host(p_dp);
+  const uint32_t td = drop_threshold_host(p_drop), tp = drop_threshold_host(p_dp), te = drop_threshold_host(p_emb);
   const float sd = p_drop > 0 ? 1.f / (1.f - (float)p_drop) : 1.f;
   const float sp = p_dp > 0 ? 1.f / (1.f - (float)p_dp) : 1.f;
+  const float se = p_emb > 0 ? 1.f / (1.f - (float)p_emb) : 1.f;
 #define LN_BWD_GO1(R, W, DYB, XB)                                                                             \
   LN_DISPATCH(D, if (W * 2 * D * sizeof(float) > 65536)                                                         \
                   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&ln_bwd_kernel<VEC, R, W, DYB, XB>),           \
                                             hipFuncAttributeMaxDynamicSharedMemorySize, W * 2 * D * sizeof(float));  \
-                hipLaunchKernelGGL((ln_bwd_kernel<VEC, R, W, DYB, XB>), dim3((M + R * W - 1) / (R * W)), dim3(W * 64), \
+                hipLaunchKernelGGL((ln_bwd_kernel<VEC, R, W, DYB, XB>), dim3(ln_bwd_workgroups(M)), dim3(W * 64), \
                                     W * 2 * D * sizeof(float), stream, dy, x, mean, rstd, gamma, beta, g_res, g_out, \
-                                    reinterpret_cast<bf16*>(gy_bf16), reinterpret_cast<bf16*>(y_bf16), dgb_ws,  \
+                                    reinterpret_cast<bf16*>(gy_bf16), reinterpret_cast<bf16*>(y_bf16), slots,   \
                                     M, tokens, rng, site_drop, td,                                              \
-                                    sd, site_dp, tp, sp, dy_parts, slots, tickets))
+                                    sd, site_dp, tp, sp, dy_parts, reinterpret_cast<bf16*>(gp_bf16), site_emb,  \
+                                    te, se))
 #define LN_BWD_GO(R, W)                      \
   if (dy_bf16 && x_bf16) LN_BWD_GO1(R, W, true, true)  \
   else if (dy_bf16) LN_BWD_GO1(R, W, true, false)      \
@@ -494,10 +487,8 @@ void layernorm_bwd_launch(const void* dy, bool dy_bf16, const void* x, bool x_bf
 #undef LN_BWD_GO1
 }
 
-int ln_bwd_workgroups(int M) { return (M + LN_NW - 1) / LN_NW; }
-int ln_replicas(int M) { return (ln_bwd_workgroups(M) + LN_GROUP - 1) / LN_GROUP; }
-int ln_ticket_rows(int M, int D) { return (ln_replicas(M) + 2 * D - 1) / (2 * D); }
+int ln_bwd_workgroups(int M) { return std::max(1, std::min((M + LN_NW - 1) / LN_NW, LN_MAX_WG)); }
 
 void replica_reduce_launch(const float* ws, float* const* dsts_dev, int G, int C, int R, int rows, hipStream_t stream) {
-  hipLaunchKernelGGL(replica_reduce_kernel, dim3((C + 255) / 256, G), dim3(256), 0, stream, ws, dsts_dev, C, R, rows);
+  hipLaunchKernelGGL(replica_reduce_kernel, dim3((C + 15) / 16, G), dim3(256), 0, stream, ws, dsts_dev, C, R, rows);
 }

@@ -429,7 +429,8 @@ class ViTProgram:
     def backward_iter(self, P: ModelTensors, G: ModelTensors, S: Saved, dtok: torch.Tensor, rng: torch.Tensor,
                       training: bool = True, wgrad: Optional[Callable] = None,
                       ln_ws: Optional[torch.Tensor] = None, embed_with_block0: bool = False, ln_final=None,
-                      wgrad_flush=None, wgrad_store: bool = False, wgrad_sq=None) -> Iterator[int]:
+                      wgrad_flush=None, wgrad_store: bool = False, wgrad_sq=None,
+                      embed_fused=None) -> Iterator[int]:
         """Hand-written backward; yields the block index after each block's input
         gradients are issued (L-1 first, then ..., 0) and -1 after the embedding grads.
 
@@ -453,6 +454,11 @@ class ViTProgram:
         ``wgrad_sq = (parts, arena, lazy)`` (one deferred launch, no ``wgrad_flush``):
         that launch also writes the grad-norm partials of the whole gradient arena
         (:func:`ops.linear_wgrad_multi`), so the optimizer needs no sqnorm pass.
+        ``embed_fused = (owners, ln_offs)`` (with ``wgrad_sq``): no embedding-backward
+        launch -- the last LayerNorm backward writes the patch-row gradient and the
+        cls / pos / time-embedding gradients and the LayerNorm finalize (``ln_final``,
+        ``ln_offs`` = its destinations' arena offsets) run as extra workgroups of the
+        weight-gradient launch (``owners`` >= the distinct timesteps of a batch).
         Measured slower on MI355X and removed: weight gradients riding in the
         input-gradient launches, one grouped launch per block, a side-stream branch
         for them, the proj input gradient inside the attention backward, the
@@ -463,6 +469,9 @@ class ViTProgram:
         bucketed = wgrad is None and wgrad_flush is not None
         if wgrad_sq is not None and (bucketed or wgrad is not None):
             raise ValueError("wgrad_sq needs the single deferred weight-gradient launch")
+        if embed_fused is not None and (wgrad_sq is None or G.temb is None or not embed_with_block0):
+            raise ValueError("embed_fused needs wgrad_sq, a trainable time embedding and embed_with_block0")
+        emb_spec = None
         jobs = []
         if wgrad is None:
             wgrad = lambda dy, x, dw, db: jobs.append((dy, x, dw, db))  # noqa: E731
@@ -517,11 +526,24 @@ class ViTProgram:
                 g, gy = dgrad_ln(dqkv, bp.qkv_w, qs, x0, m1, r1, bp.n1w, g1, bg.n1w, bg.n1b, N, rng, psf2, pd, psd2,
                                  dpr[i - 1], True, ws(k2 + 1), **fk)
             else:
+                if embed_fused is not None:  # the patch-row gradient from this LayerNorm backward
+                    Bs = S.t.shape[0]
+                    gpatch = torch.empty(Bs * (N - 1), D, dtype=ACT_DTYPE, device=dtok.device)
+                    fk = dict(fk, gp_out=gpatch, site_emb=SITE_EMBED, p_emb=pd)
                 g, gy = dgrad_ln(dqkv, bp.qkv_w, qs, x0, m1, r1, bp.n1w, g1, bg.n1w, bg.n1b, N, rng, 0, 0.0, 0, 0.0,
                                  False, ws(k2 + 1), **fk)
             keep.append((gy1, du, dqkv, l1, l2, do))
             wgrad(dqkv, l1, bg.qkv_w, bg.qkv_b)
-            if i == 0 and embed_with_block0:
+            if i == 0 and embed_with_block0 and embed_fused is not None:
+                wgrad(gpatch, S.patches, G.pe_w, G.pe_b)
+                owners, ln_offs = embed_fused
+                ln = None
+                if ln_final is not None:
+                    lw, lp, lC, lR = ln_final[:4]
+                    ln = (lw, lp, ln_offs, lC, lR, bool(ln_final[4]) if len(ln_final) > 4 else False)
+                emb_spec = (g.view(S.t.shape[0], N, D), S.t, rng, SITE_EMBED, pd, G.cls, G.pos, G.temb,
+                            min(int(owners), S.t.shape[0]), ln)
+            elif i == 0 and embed_with_block0:
                 gpatch = self._embed_backward(P, G, S, g, rng, pd, wgrad, ln_final)
             if bucketed and (i in wgrad_flush or (i == 0 and embed_with_block0)) and jobs:
                 ops.linear_wgrad_multi(jobs, store=wgrad_store)  # this bucket's weight gradients: final now
@@ -539,7 +561,7 @@ class ViTProgram:
                 for job in jobs:
                     ops.linear_wgrad(*job)
             else:
-                ops.linear_wgrad_multi(jobs, store=wgrad_store and not bucketed, sq=wgrad_sq)
+                ops.linear_wgrad_multi(jobs, store=wgrad_store and not bucketed, sq=wgrad_sq, embed=emb_spec)
             keep.append(jobs)
         keep.append((gpatch, lf))
         self._keep = keep  # operands of the queued launches stay referenced until the next step

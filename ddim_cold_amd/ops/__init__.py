@@ -335,7 +335,15 @@ def wire_unpack(src, dst):
     dst.copy_(src)
 
 
-def linear_wgrad_multi(jobs, store: bool = False, sq=None):
+def wgrad_embed_slots(B: int, N: int, D: int, owners: int, n_ln: int, ln_C: int, wide: bool) -> int:
+    """Grad-norm partial slots (= extra workgroups) the embedding parts of
+    :func:`linear_wgrad_multi` take (``wide``: the 512-thread tiles of >= 16,384-token
+    reductions)."""
+    nt = 512 if wide else 256
+    return -(-(N * D) // nt) + owners * -(-D // 16) + (n_ln * -(-ln_C // 16) if n_ln else 0)
+
+
+def linear_wgrad_multi(jobs, store: bool = False, sq=None, embed=None):
     """Every ``(dy, x, dw, db)`` weight-gradient job of a step (<= 32) in ONE launch
     (csrc/gemm.hip ``gemm_wgrad_multi_kernel``; unsplit, deterministic).  ``store``:
     the targets are zero (``dW = dy^T x`` written, not added: no read of dW).
@@ -344,17 +352,29 @@ def linear_wgrad_multi(jobs, store: bool = False, sq=None):
     ``arena`` (every dw / db a view of it), so it also writes the grad-norm partials
     :func:`sqnorm` would (same buffer layout, scale 1): each output tile the sum of
     squares of its final values, extra workgroups the arena ranges outside every
-    target and outside ``lazy`` = (lo, hi).  Replaces the separate sqnorm pass."""
+    target and outside ``lazy`` = (lo, hi).  Replaces the separate sqnorm pass.
+
+    ``embed = (g, t, rng, site, p, dcls, dpos, dtemb, owners, ln)``: the cls / pos /
+    time-embedding gradients of :func:`embed_bwd` (parts A, B; ``g`` the embedding
+    output gradient [B, N, D], ``owners`` >= the distinct timesteps a batch can hold)
+    and, with ``ln = (ws, dst_ptrs, offs, C, R, store)``, the LayerNorm slot finalize
+    ride in the same launch as extra workgroups (each writing the grad-norm partials of
+    its outputs); the patch-row gradient comes from the last LayerNorm backward
+    (:func:`layernorm_bwd` ``gp_out``).  Deterministic."""
     if not jobs:
         return
     if _hip(jobs[0][0]):  # (more than 32 jobs: consecutive launches of <= 32)
         dys, xs, dws, dbs = (list(z) for z in zip(*jobs))
-        if sq is None:
-            _ops().linear_wgrad_multi(dys, xs, dws, dbs, bool(store))
-        else:
-            parts, arena, lazy = sq
-            lo, hi = lazy if lazy is not None else (0, 0)
+        parts, arena, (lo, hi) = (None, None, (0, 0)) if sq is None else \
+            (sq[0], sq[1], sq[2] if sq[2] is not None else (0, 0))
+        if embed is None:
             _ops().linear_wgrad_multi(dys, xs, dws, dbs, bool(store), parts, arena, int(lo), int(hi))
+            return
+        g, t, rng, site, p, dcls, dpos, dtemb, owners, ln = embed
+        lw, lp, loffs, lC, lR, lst = ln if ln is not None else (None, None, [], 0, 0, False)
+        _ops().linear_wgrad_multi(dys, xs, dws, dbs, bool(store), parts, arena, int(lo), int(hi), g, t, rng,
+                                  int(site), float(p), dcls, dpos, dtemb, int(owners), lw, lp,
+                                  [int(o) for o in loffs], int(lC), int(lR), bool(lst))
         return
     for dy, x, dw, db in jobs:
         if store:
@@ -362,45 +382,50 @@ def linear_wgrad_multi(jobs, store: bool = False, sq=None):
             if db is not None:
                 db.zero_()
         ref.linear_wgrad(dy, x, dw, db)
+    if embed is not None:
+        g, t, rng, site, p, dcls, dpos, dtemb, owners, ln = embed
+        ref.embed_bwd(g, t, rng, site, p, dcls, dpos, dtemb)
+        if ln is not None:
+            raise ValueError("the LayerNorm finalize in the weight-gradient launch needs the HIP extension")
     if sq is not None:
         parts, arena, lazy = sq
         sqnorm(arena, parts, 1.0, lazy=lazy)
 
 
-def ln_replicas(M: int) -> int:
-    """Rows of a LayerNorm backward workspace that hold dgamma||dbeta group partials
-    for ``M`` rows (csrc/layernorm.hip: one per 16 workgroups of 8 rows)."""
-    return -(-(-(-M // 8)) // 16)
-
-
-def ln_ws_rows(M: int, D: int) -> int:
-    """Rows ([rows, 2D] floats) of the workspace :func:`layernorm_bwd` takes for ``M``
-    rows of width ``D``: the :func:`ln_replicas` partial rows, then the arrival tickets
-    (zero on entry, left zero)."""
-    R = ln_replicas(M)
-    return R + -(-R // (2 * D))
+def ln_ws_rows(M: int) -> int:
+    """Rows ([rows, 2D] floats) of the dgamma||dbeta workspace :func:`layernorm_bwd`
+    takes for ``M`` rows: one slot per backward workgroup (csrc/layernorm.hip: 8 rows per
+    workgroup, at most 512 workgroups), each overwritten by its workgroup, summed in slot
+    order by :func:`replica_reduce_` (deterministic, no atomics)."""
+    return max(1, min(-(-M // 8), 512))
 
 
 def layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dgamma, dbeta, N: int, rng, site_drop: int, p_drop: float,
                   site_dp: int, p_dp: float, emit_gy: bool, ws: Optional[torch.Tensor] = None, beta=None,
-                  y_out=None):
-    """LayerNorm backward.  With ``ws`` ([ln_ws_rows(M, D), 2D], zero on entry) the
-    dgamma||dbeta partials stay in the workspace's first :func:`ln_replicas` rows
-    (finalise later with :func:`replica_reduce_`; deterministic, no atomics);
-    otherwise they are added into dgamma / dbeta.
+                  y_out=None, gp_out=None, site_emb: int = 0, p_emb: float = 0.0):
+    """LayerNorm backward.  With ``ws`` ([ln_ws_rows(M), 2D]) the dgamma||dbeta
+    partials stay in the workspace slots (finalise later with :func:`replica_reduce_`;
+    deterministic, no atomics); otherwise they are added into dgamma / dbeta.
     ``y_out`` (with ``beta``): also write the LayerNorm output (bf16) — the
-    forward folded the LayerNorm into the next GEMM and never stored it."""
+    forward folded the LayerNorm into the next GEMM and never stored it.
+    ``gp_out`` ([B*(N-1), D] bf16; the last LayerNorm of the backward): also write the
+    patch-embedding input gradient, g_out's token rows 1..N-1 with the embedding
+    dropout (``site_emb``, ``p_emb``) -- what :func:`embed_bwd` returns."""
     if _hip(x):
         g_out, gy = _ops().layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dgamma, dbeta, N, rng, site_drop,
-                                         float(p_drop), site_dp, float(p_dp), bool(emit_gy), ws, beta, y_out)
+                                         float(p_drop), site_dp, float(p_dp), bool(emit_gy), ws, beta, y_out,
+                                         gp_out, int(site_emb), float(p_emb))
         return g_out, (gy if emit_gy else None)
     if ws is not None:
         D = x.shape[-1]
         dgamma, dbeta = ws[0, :D], ws[0, D:]
     if y_out is not None:
         ref.layernorm_out_(x, mean, rstd, gamma, beta, y_out)
-    return ref.layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dgamma, dbeta, N, rng, site_drop, p_drop,
-                             site_dp, p_dp, emit_gy)
+    g_out, gy = ref.layernorm_bwd(dy, x, mean, rstd, gamma, g_res, dgamma, dbeta, N, rng, site_drop, p_drop,
+                                  site_dp, p_dp, emit_gy)
+    if gp_out is not None:
+        gp_out.copy_(ref.embed_patch_grad(g_out.view(-1, N, x.shape[-1]), rng, site_emb, p_emb))
+    return g_out, gy
 
 
 def ln_fold_(ws, gammas, betas, biases, wfs, cs, bfs, tail=None):
@@ -431,7 +456,7 @@ def ln_fold_(ws, gammas, betas, biases, wfs, cs, bfs, tail=None):
 
 def replica_reduce_(ws, dst_ptrs, C: int, R: int, dsts=None):
     """dst[g] += ws[g, :R].sum(0) (rows in order) for G LayerNorm workspaces
-    ([G, rows, C]; ``R`` = :func:`ln_replicas` of the backward's row count).
+    ([G, rows, C]; ``R`` = :func:`ln_ws_rows` of the backward's row count).
 
     ``dst_ptrs`` is a device int64 tensor of destination addresses (GPU); the
     CPU path takes the destination tensors in ``dsts`` instead (and re-zeroes the

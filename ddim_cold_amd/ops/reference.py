@@ -394,6 +394,13 @@ def attn_bwd(do, qkv, o, lse, scale: float, rng, site: int, p: float, bh0: int =
     return bf16(d.permute(1, 3, 0, 2, 4).reshape(B * N, 3 * H * hd))
 
 
+def embed_patch_grad(g, rng, site: int, p: float):
+    """The patch-row gradient of :func:`embed_bwd` alone: token rows 1..N-1 of ``g``
+    ([B, N, D]) with the embedding dropout, bf16, [B*(N-1), D]."""
+    B, N, D = g.shape
+    return bf16(_dropout(g.float(), rng, site, p)[:, 1:, :].reshape(B * (N - 1), D))
+
+
 def embed_bwd(g, t, rng, site: int, p: float, dcls, dpos, dtemb):
     """Grads of cls/pos/time embeddings (+=) and the patch-row grad (bf16) for the conv wgrad."""
     B, N, D = g.shape

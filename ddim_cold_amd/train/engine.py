@@ -70,6 +70,11 @@ FUSE_LN_FINAL = True
 # epilogues (ops.linear_wgrad_multi sq=) instead of a separate sqnorm pass over the
 # arena (False: the sqnorm kernel; tests compare the two)
 FUSE_SQNORM = True
+# with FUSE_SQNORM: no embedding-backward launch -- the last LayerNorm backward writes
+# the patch-row gradient, and the cls / pos / time-embedding gradients and the
+# LayerNorm finalize run as extra workgroups of the weight-gradient launch
+# (csrc/embed_parts.h; False: embed_bwd as its own launch; tests compare the two)
+FUSE_EMBED_WGRAD = True
 
 
 @dataclass
@@ -182,6 +187,7 @@ class TrainEngine:
         # grad-norm partials (sqnorm, or the fused weight-gradient launch: one per 64x64
         # output tile + tail workgroups; the 2-D parameter count bounds the tiles)
         tiles = sum(-(-p.shape[0] // 64) * -(-(p[0].numel()) // 64) for p in model.parameters() if p.dim() >= 2)
+        self._sq_tiles = tiles
         self.sqnorm = torch.zeros(ops.sq_parts_size(tiles), dtype=torch.float32, device=dev)
         self.loss_last = torch.zeros(1, dtype=torch.float32, device=dev)
         self.loss_ema = torch.full((1,), cfg.ema_init, dtype=torch.float32, device=dev)
@@ -481,17 +487,34 @@ class TrainEngine:
         self._ln_prefixes = ln_prefixes
         self._build_buckets()
 
-    def _ensure_ln_ws(self, M: int):
-        """LayerNorm dgamma/dbeta workspaces ([2L+1, ops.ln_ws_rows(M, D), 2D], zero) for
-        backward passes of ``M`` token rows."""
-        D = self.prog.cfg.dim
-        rows = ops.ln_ws_rows(M, D)
-        if self.ln_ws is not None and self.ln_ws.shape[1] == rows:
+    def _ensure_batch_buffers(self, B: int):
+        """Buffers sized by the batch: the LayerNorm dgamma/dbeta slot workspaces
+        ([2L+1, ops.ln_ws_rows(B N), 2D]) and room in the grad-norm partials for the
+        embedding workgroups of the weight-gradient launch (FUSE_EMBED_WGRAD)."""
+        c = self.prog.cfg
+        D, M = c.dim, B * c.tokens
+        rows = ops.ln_ws_rows(M)
+        nparts = ops.sq_parts_size(self._sq_tiles + ops.wgrad_embed_slots(
+            B, c.tokens, D, self._emb_owners(B), len(self.ln_order), 2 * D, M >= 16384))
+        if (self.ln_ws is not None and self.ln_ws.shape[1] == rows and self.sqnorm.numel() >= nparts):
             return
         if self.is_cuda and torch.cuda.is_current_stream_capturing():
             raise RuntimeError("the batch size changed inside a graph capture (LayerNorm workspace)")
         self.ln_ws = torch.zeros(len(self.ln_order), rows, 2 * D, dtype=torch.float32, device=self.device)
-        self.ln_R = ops.ln_replicas(M)
+        self.ln_R = rows
+        if self.sqnorm.numel() < nparts:
+            self.sqnorm = torch.zeros(nparts, dtype=torch.float32, device=self.device)
+
+    def _ln_offs(self):
+        """Arena offsets (elements, from the optimizer's gradient view) of the LayerNorm
+        gradient ranges, in ``ln_order``."""
+        base = self.opt_g.data_ptr()
+        return [(d.data_ptr() - base) // 4 for d in self.ln_dsts]
+
+    def _emb_owners(self, B: int) -> int:
+        """Distinct timesteps a batch of ``B`` can hold (time-embedding gradient rows)."""
+        rows = self.cfg.temb_rows
+        return max(1, min(B, rows if rows is not None else self.prog.cfg.total_steps))
 
     def _build_buckets(self):
         """All-reduce bucket layout from ``cfg.bucket_blocks`` / ``cfg.embed_bucket``
@@ -591,7 +614,7 @@ class TrainEngine:
             else:
                 img, tgt, t = self.batch_fn()
             self._temb_t.append(t)
-            self._ensure_ln_ws(int(t.shape[0]) * c.tokens)
+            self._ensure_batch_buffers(int(t.shape[0]))
             if fused_loss:
                 # head GEMM epilogue computes the loss partials and the token-layout gradient
                 (loss_parts, dtok), S = self.prog.forward(self.param_tensors, img, t, self.rng, True,
@@ -635,10 +658,16 @@ class TrainEngine:
             # last writer of the gradient arena and writes the grad-norm partials too
             fuse_sq = (FUSE_SQNORM and overwrite and flush_at is None and k_acc == 1 and self.world == 1
                        and self.is_cuda)
+            B = int(t.shape[0])
+            emb_fused = None
+            if (fuse_sq and FUSE_EMBED_WGRAD and merge and self.grad_tensors.temb is not None and B <= 256
+                    and ln_final is not None):
+                emb_fused = (self._emb_owners(B), self._ln_offs()[:ln_final[1].numel()])
             for i in self.prog.backward_iter(self.param_tensors, self.grad_tensors, S, dtok, self.rng, True,
                                              ln_ws=self.ln_ws, embed_with_block0=merge, ln_final=ln_final,
                                              wgrad_flush=flush_at, wgrad_store=overwrite,
-                                             wgrad_sq=(self.sqnorm, self.opt_g, self.lazy) if fuse_sq else None):
+                                             wgrad_sq=(self.sqnorm, self.opt_g, self.lazy) if fuse_sq else None,
+                                             embed_fused=emb_fused):
                 if i in self.bucket_after and (self.segmented or i == -1):
                     hi = self.ln_done_at[i]
                     if ln_final is not None:

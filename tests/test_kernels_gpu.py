@@ -79,34 +79,39 @@ def test_layernorm_bwd(emit, p):
 
 @pytest.mark.parametrize("M,D,N", [(2080, 384, 65), (20032, 384, 626), (8224, 256, 257), (40, 128, 5)])
 def test_layernorm_bwd_workspace_deterministic(M, D, N):
-    """dgamma||dbeta through the workspace (per-workgroup slots, in-launch group sums by
-    the last arriver, rows finalised in order): == the fp32 oracle, BIT-identical over
-    repeated launches (no fp32 atomics), the arrival tickets left zero for the next call,
-    and replica_reduce_ == the in-launch finalize of embed_bwd."""
+    """dgamma||dbeta through the slot workspace (one slot per workgroup, workgroup-strided
+    rows past 512 workgroups, slots summed in order by replica_reduce_): == the fp32
+    oracle and BIT-identical over repeated launches (no fp32 atomics).  gp_out (the
+    last LayerNorm of a backward) == the embedding backward's patch-row gradient."""
     x = torch.randn(M, D, device=DEV)
     g, b = torch.randn(D, device=DEV), torch.randn(D, device=DEV)
     _, mu, rs = ref.layernorm_fwd(x, g, b)
     dy, gres = torch.randn(M, D, device=DEV), torch.randn(M, D, device=DEV)
     r = rng()
-    R, rows = ops.ln_replicas(M), ops.ln_ws_rows(M, D)
-    assert R == -(-(-(-M // 8)) // 16) and rows > R
-    ws = torch.zeros(1, rows, 2 * D, device=DEV)
+    R = ops.ln_ws_rows(M)
+    assert R == max(1, min(-(-M // 8), 512))
+    ws = torch.zeros(1, R, 2 * D, device=DEV)
     outs = []
     for _ in range(3):
         z = torch.zeros(D, device=DEV)
-        go, gy = ops.layernorm_bwd(dy, x, mu, rs, g, gres, z, z.clone(), N, r, 7, 0.1, 8, 0.2, True, ws[0])
+        gp = torch.empty(M // N * (N - 1), D, dtype=torch.bfloat16, device=DEV)
+        go, gy = ops.layernorm_bwd(dy, x, mu, rs, g, gres, z, z.clone(), N, r, 7, 0.1, 8, 0.2, True, ws[0],
+                                   gp_out=gp, site_emb=1, p_emb=0.1)
         dst = torch.zeros(2 * D, device=DEV)
         ops.replica_reduce_(ws, torch.tensor([dst.data_ptr()], dtype=torch.int64, device=DEV), 2 * D, R)
         torch.cuda.synchronize()
-        assert not ws[0, R:].any(), "arrival tickets must be left zero"
-        outs.append((go, gy, dst))
-    for go, gy, dst in outs[1:]:
-        assert torch.equal(go, outs[0][0]) and torch.equal(gy, outs[0][1])
+        outs.append((go, gy, dst, gp))
+    for go, gy, dst, gp in outs[1:]:
+        assert torch.equal(go, outs[0][0]) and torch.equal(gy, outs[0][1]) and torch.equal(gp, outs[0][3])
         assert torch.equal(dst, outs[0][2]), "dgamma||dbeta differ between identical launches"
     dg2, db2 = torch.zeros(D, device=DEV), torch.zeros(D, device=DEV)
-    ref.layernorm_bwd(dy, x, mu, rs, g, gres, dg2, db2, N, r, 7, 0.1, 8, 0.2, True)
+    gor, _ = ref.layernorm_bwd(dy, x, mu, rs, g, gres, dg2, db2, N, r, 7, 0.1, 8, 0.2, True)
     close(outs[0][2][:D], dg2, 2e-3 * dg2.abs().max().item(), 1e-4, "dgamma")
     close(outs[0][2][D:], db2, 2e-3 * db2.abs().max().item(), 1e-4, "dbeta")
+    close(outs[0][0], gor, 1e-4, 1e-4, "g_out")
+    gpr = ref.embed_patch_grad(outs[0][0].view(-1, N, D), r, 1, 0.1)
+    close(outs[0][3], gpr, 2e-2, 1e-2, "patch-row gradient")
+    assert torch.equal(outs[0][3] == 0, gpr == 0), "embedding dropout masks differ"
 
 
 # ------------------------------------------------------------------ GEMMs
