@@ -685,11 +685,11 @@ class TrainEngine:
         gs = 1.0 / (self.world * k_acc)
         if not fuse_sq:
             ops.sqnorm(self.opt_g, self.sqnorm, gs, lazy=self.lazy)
+        if loss_acc is not None:
+            loss_parts = loss_acc
         ops.adamw_step(self.opt_p, self.opt_g, self.opt_m, self.opt_v, self.opt_pb, self.sqnorm,
                        self.step_ctr, self.hyper, gs, zero_hi=self.acc_hi if overwrite else None,
                        lazy=self.lazy, lazy_decay=self.lazy_decay)
-        if loss_acc is not None:
-            loss_parts = loss_acc
         if tail:
             self.lnfold.refresh(tail=(loss_parts, self.loss_last, self.loss_ema, self.cfg.ema_decay, self.step_ctr,
                                       self.rng, self.sqnorm))

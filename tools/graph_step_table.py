@@ -6,7 +6,7 @@ import csv, sys, statistics, re
 rows = list(csv.DictReader(open(sys.argv[1])))
 k = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-ends = [i for i, x in enumerate(k) if "adamw_kernel" in x[2]]
+ends = [i for i, x in enumerate(k) if "adamw_kernel" in x[2]]  # a step ends with its optimizer
 sel = ends[-steps - 1:]
 segs = [k[a + 1:b + 1] for a, b in zip(sel, sel[1:])]
 n = min(len(s) for s in segs)
