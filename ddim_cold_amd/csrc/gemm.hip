@@ -432,12 +432,17 @@ static void launch_dma(GemmParams p, int splits, hipStream_t stream) {
   constexpr int stage = BM * 128 + BN * 128;
   constexpr int per_cu4 = (160 * 1024) / (4 * stage);
   constexpr int threads = 64 * WM * WN;
-  if ((tiles * splits > 256 * per_cu4 && p.ktiles_per_split <= 8) || 4 * stage > 160 * 1024)
-    hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, WM, WN, AT, BT, EPI, 3>), dim3(tiles, 1, splits), dim3(threads),
-                       3 * stage, stream, p);
-  else
-    hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, WM, WN, AT, BT, EPI, 4>), dim3(tiles, 1, splits), dim3(threads),
-                       4 * stage, stream, p);
+  if constexpr (3 * stage > 160 * 1024) {  // 256x192: 2-stage ring (explicitly instantiated below)
+    hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, WM, WN, AT, BT, EPI, 2>), dim3(tiles, 1, splits), dim3(threads),
+                       2 * stage, stream, p);
+  } else {
+    if ((tiles * splits > 256 * per_cu4 && p.ktiles_per_split <= 8) || 4 * stage > 160 * 1024)
+      hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, WM, WN, AT, BT, EPI, 3>), dim3(tiles, 1, splits), dim3(threads),
+                         3 * stage, stream, p);
+    else
+      hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, WM, WN, AT, BT, EPI, 4>), dim3(tiles, 1, splits), dim3(threads),
+                         4 * stage, stream, p);
+  }
 }
 
 template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EPI>
@@ -457,7 +462,7 @@ static void launch_cfg(GemmParams p, int splits, hipStream_t stream) {
 // stub of a kernel template first referenced inside an if-constexpr branch)
 // tile configs: 0 = 32x64, 1 = 64x64, 2 = 128x64, 3 = 128x128 (4 waves, 2x2);
 // 4 = 256x128, 5 = 128x128 (8 waves, 4x2: 512-thread workgroups, for M >= BIG_M)
-constexpr int CFG_W8_256 = 4, CFG_W8_128 = 5;
+constexpr int CFG_W8_256 = 4, CFG_W8_128 = 5, CFG_W8_192 = 6;
 template <int EPI>
 struct Wide8 {  // epilogues with no 4-wave workgroup reduction (HEAD / HEADL sum loss partials over 4 waves)
   static constexpr bool value = EPI == EPI_BF16 || EPI == EPI_F32 || EPI == EPI_QKV || EPI == EPI_RESID ||
@@ -471,9 +476,21 @@ template <bool AT, bool BT, int EPI>
 struct Big256<AT, BT, EPI, false> {
   static void go(GemmParams, int, hipStream_t) {}
 };
+template <bool AT, bool BT, int EPI, bool OK = !BT && (EPI == EPI_BF16 || EPI == EPI_QKV || EPI == EPI_GELU)>
+struct Big192 {  // 256x192 tiles, 2-stage ring (57 KiB per stage): N = 1152 in 6 column tiles
+  static void go(GemmParams p, int splits, hipStream_t stream) { launch_dma<256, 192, 4, 2, AT, BT, EPI>(p, splits, stream); }
+};
+template <bool AT, bool BT, int EPI>
+struct Big192<AT, BT, EPI, false> {  // not built for this epilogue: the 256-row config
+  static void go(GemmParams p, int splits, hipStream_t stream) {
+    if (EPI != EPI_DGELU) Big256<AT, BT, EPI>::go(p, splits, stream);
+    else launch_dma<128, 128, 4, 2, AT, BT, EPI>(p, splits, stream);
+  }
+};
 template <bool AT, bool BT, int EPI, bool OK = Wide8<EPI>::value>
 struct Launch8 {
   static void go(GemmParams p, int splits, hipStream_t stream, int cfg) {
+    if (cfg == CFG_W8_192) { Big192<AT, BT, EPI>::go(p, splits, stream); return; }
     // DGELU at 256x128 spills (88 B/lane of scratch): its 256-row config is the 128-row one
     if (cfg == CFG_W8_256 && EPI != EPI_DGELU) Big256<AT, BT, EPI>::go(p, splits, stream);
     else launch_dma<128, 128, 4, 2, AT, BT, EPI>(p, splits, stream);
@@ -528,7 +545,7 @@ struct DmaTiles<true, BT, EPI> {  // transposed A (wgrad): 64x64
 // bounds check).
 constexpr int BIG_M = 16384;
 static std::atomic<int> g_tile_override{-1};
-static int pick_tiles(int M, int N, int K, int splits, bool at, bool bt, bool wide8) {
+static int pick_tiles(int M, int N, int K, int splits, bool at, bool bt, bool wide8, bool qkv = false) {
   if (at) return 1;
   const int forced = g_tile_override.load(std::memory_order_relaxed);
   if (forced >= 0) return bt && forced == 3 ? 2 : forced;
@@ -536,7 +553,11 @@ static int pick_tiles(int M, int N, int K, int splits, bool at, bool bt, bool wi
   // oxford_flower sampler's N = 256 GEMMs (M = 16,448: 130 such tiles) run faster on
   // 64x64 / 32x64 tiles (tools/ub_gemm_large.py 16448 .. 256: residual 19.7 vs 15.9 us,
   // GELU 16.0 vs 13.2; vit_small_200 N = 384 at M = 20,032: 237 tiles, 8-wave faster)
-  if (wide8 && M >= BIG_M && ((M + 255) / 256) * ((N + 127) / 128) >= 236) return CFG_W8_256;
+  // the QKV projection (N = 3D = 1,152 at vit_small_200): 256x192 tiles, 2-stage ring --
+  // 474 workgroups (1.85 rounds of 256 CUs) instead of 711 (2.8 rounds): 489 -> 453 us of
+  // QKV per step (profiles/qkv192_r6.txt)
+  if (wide8 && M >= BIG_M && ((M + 255) / 256) * ((N + 127) / 128) >= 236)
+    return qkv && N % 192 == 0 ? CFG_W8_192 : CFG_W8_256;
   return ((M + 63) / 64) * ((N + 63) / 64) * splits >= 240 ? 1 : 0;
 }
 
@@ -546,7 +567,7 @@ static void launch_auto(GemmParams p, int splits, hipStream_t stream) {
   if (dma_ok) {
     // DGELU (input gradient through GELU + dropout, bf16 out) stays on 4-wave tiles at
     // every measured M (M = 20,032: 25.5 vs 26.5 us; 40,064: 42.1 vs 49.9)
-    int cfg = pick_tiles(p.M, p.N, p.K, splits, AT, BT, Wide8<EPI>::value && EPI != EPI_DGELU);
+    int cfg = pick_tiles(p.M, p.N, p.K, splits, AT, BT, Wide8<EPI>::value && EPI != EPI_DGELU, EPI == EPI_QKV);
     // the GELU epilogue (erf-GELU + dropout per element, two bf16 outputs) is the
     // heaviest in vector instructions: twice the waves of 32x64 tiles pay off on the
     // sampler shape (M=4160: 6.56 vs 7.14 us, tools/gpu_tile_sweep3.sh); the other
@@ -580,6 +601,8 @@ static void launch_auto(GemmParams p, int splits, hipStream_t stream) {
   template __global__ void gemm_dma_kernel<256, 128, 4, 2, AT, BT, EPI, 4>(GemmParams); \
   template __global__ void gemm_dma_kernel<128, 128, 4, 2, AT, BT, EPI, 3>(GemmParams); \
   template __global__ void gemm_dma_kernel<128, 128, 4, 2, AT, BT, EPI, 4>(GemmParams);
+#define DC_INST_W192(EPI) template __global__ void gemm_dma_kernel<256, 192, 4, 2, false, false, EPI, 2>(GemmParams);
+DC_INST_W192(EPI_BF16) DC_INST_W192(EPI_QKV) DC_INST_W192(EPI_GELU)
 DC_INST_DMA3(EPI_BF16) DC_INST_W8(false, false, EPI_BF16)
 DC_INST_DMA3(EPI_F32) DC_INST_W8(false, false, EPI_F32)
 DC_INST_DMA3(EPI_QKV) DC_INST_W8(false, false, EPI_QKV)
@@ -801,7 +824,7 @@ int gemm_nt_grid(int M, int N, int K) {
 }
 
 int gemm_set_tile_override(int cfg) {
-  if (cfg < -1 || cfg > 5) throw std::runtime_error("gemm_set_tile_override: -1 (auto) or 0..5");
+  if (cfg < -1 || cfg > 6) throw std::runtime_error("gemm_set_tile_override: -1 (auto) or 0..6");
   return g_tile_override.exchange(cfg);
 }
 

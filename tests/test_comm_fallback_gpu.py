@@ -55,3 +55,13 @@ def test_bench_completes_on_eager_inline_when_every_layout_fails():
     assert c["autotune_dropped"] and all("test hook" in v for v in c["autotune_dropped"].values())
     assert out["value"] > 0 and c["final_loss"] > 0
     assert "phase=comm-fallback:verified" in err
+
+
+def test_autotune_budget_zero_skips_every_layout_and_falls_back():
+    """DDIM_COLD_AUTOTUNE_BUDGET_S=0: the tuning budget is spent before the first candidate,
+    every layout is skipped for time, and the bench still completes on the eager inline
+    all-reduce."""
+    out, err = _bench({"DDIM_COLD_AUTOTUNE_BUDGET_S": "0"})
+    c = out["config"]
+    assert c["comm_layout"] == "eager-inline" and c["comm_fallback"], c
+    assert out["value"] > 0 and c["final_loss"] > 0

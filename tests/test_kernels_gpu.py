@@ -115,7 +115,10 @@ def test_layernorm_bwd_workspace_deterministic(M, D, N):
 
 
 # ------------------------------------------------------------------ GEMMs
-@pytest.mark.parametrize("B,N,H,D", [(32, 65, 12, 384), (4, 257, 4, 256), (3, 17, 2, 64 * 2)])
+# (32, 626, 6, 384): vit_small_200's M = 20,032 -> the 256x192 2-stage tiles (gemm.hip Big192);
+# (27, 626, 6, 384): M = 16,902, a partial last row tile of those
+@pytest.mark.parametrize("B,N,H,D", [(32, 65, 12, 384), (4, 257, 4, 256), (3, 17, 2, 64 * 2), (32, 626, 6, 384),
+                                     (27, 626, 6, 384)])
 def test_qkv_fwd(B, N, H, D):
     a = bf(B * N, D)
     w = bf(3 * D, D, scale=0.05)

@@ -114,3 +114,30 @@ def test_rehearse_shared_gpu_flag_on_cpu():
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
     assert out["rehearsal_shared_gpu_gloo"] is True and out["n_gpus"] == 2
+
+
+def test_bench_deadline_switches_parse():
+    """DDIM_COLD_PG_TIMEOUT_S / DDIM_COLD_DEADLINE_S / DDIM_COLD_SPAWN_DEADLINE_S set bench.py's
+    process-group timeout and the rank / parent deadlines (the stall tests in
+    tests/test_bench_cpu.py exercise the deadlines end to end)."""
+    code = "import bench; print(bench.PG_TIMEOUT_S, bench.RANK_DEADLINE_S, bench.SPAWN_DEADLINE_S)"
+    r = _py(code)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split() == ["120", "450.0", "480.0"]
+    r = _py(code, {"DDIM_COLD_PG_TIMEOUT_S": "45", "DDIM_COLD_DEADLINE_S": "100"})
+    assert r.stdout.split() == ["45", "100.0", "130.0"]
+    r = _py(code, {"DDIM_COLD_SPAWN_DEADLINE_S": "7"})
+    assert r.stdout.split()[2] == "7.0"
+
+
+def test_phase_dir_switch(tmp_path):
+    """DDIM_COLD_PHASE_DIR names the directory the ranks' phase markers go to (else one keyed
+    by the launcher's run id / master port); report_dir() reads them back."""
+    code = ("from ddim_cold_amd.parallel import watchdog as w; print(w.default_dir()); "
+            "p = w.PhaseLog(1, 2, echo=False); p.mark('probe'); print(p.dir)")
+    r = _py(code, {"DDIM_COLD_PHASE_DIR": str(tmp_path)})
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split() == [str(tmp_path), str(tmp_path)]
+    assert any(f.startswith("rank1") or "1" in f for f in os.listdir(tmp_path))
+    r = _py("from ddim_cold_amd.parallel import watchdog as w; print(w.default_dir())", {"MASTER_PORT": "29513"})
+    assert r.stdout.strip().endswith("ddim_cold_phases_29513")

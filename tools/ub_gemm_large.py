@@ -38,6 +38,8 @@ fl1 = 2 * M * D * D
 fl3 = 2 * M * D * 3 * D
 cases = [
     ("qkv fwd (head-major scatter)", fl3, lambda: ops.qkv_fwd(a, w3, b3, B, N, H), lambda: torch.matmul(a, w3.t())),
+    ("plain bf16 out N=3D", fl3, lambda: ops.linear_fwd(a, w3, b3), None),
+    ("gelu fwd p=0 (3D x D)", fl3, lambda: ops.linear_gelu_fwd(a, w3, b3, r, 5, 0.0), None),
     ("resid fwd p=.1 dp=.1 +stats", fl1,
      lambda: ops.linear_residual_fwd(a, w, b, x, N, r, 3, 0.1, 4, 0.1, st_out=st, xb_out=xb),
      lambda: torch.matmul(a, w.t())),
