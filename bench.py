@@ -54,6 +54,10 @@ def parse_args(argv=None):
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--graph-steps", type=int, default=4,
                     help="optimizer steps per hipGraph replay (TrainEngine.train_steps; every step fully executed)")
+    ap.add_argument("--graph-warmup", type=int, default=1,
+                    help="eager steps before the graphs are captured (EngineConfig.graph_warmup): with 1, the "
+                         "rest of the --warmup steps replay the captured K-step graph, so the timed steps start "
+                         "on a graph that has run and a device that is busy (profiles/first_replay_r6.txt)")
     ap.add_argument("--bucket-blocks", type=int, default=2)
     ap.add_argument("--no-sampler", action="store_true")
     ap.add_argument("--force-dist", action="store_true",
@@ -199,7 +203,7 @@ def _time_train(args, name, dataset, dev, lr, seed, prefix, pool=None):
     cold = dataset == "cold"
     e = TrainEngine(m, EngineConfig(lr=lr, t_max=512 * 100, use_graph=not args.no_graph, seed=seed,
                                     temb_rows=int(math.log2(m.img_size[1])) + 1 if cold else None,
-                                    graph_steps=args.graph_steps), device=dev)
+                                    graph_steps=args.graph_steps, graph_warmup=args.graph_warmup), device=dev)
     e.set_batch_fn(ColdBatcher(pool, args.batch, e.rng) if cold else
                    GaussianBatcher(pool, args.batch, e.rng, m.total_steps))
     e.train_steps(args.warmup)
@@ -258,7 +262,8 @@ def run(args):
                        temb_rows=int(math.log2(model.img_size[1])) + 1 if args.dataset == "cold" else None,
                        graph_comm=not args.segmented_comm, grad_wire=args.grad_wire,
                        comm_events=not (args.segmented_comm or args.captured_comm),
-                       comm="torch" if SHARED_GPU else args.comm, graph_steps=args.graph_steps)
+                       comm="torch" if SHARED_GPU else args.comm, graph_steps=args.graph_steps,
+                       graph_warmup=args.graph_warmup)
     phase("engine-build", model=args.model)
     engine = TrainEngine(model, cfg, device=dev)
     phase("engine-ready", comm=engine.comm_backend if engine.segmented else "none")
@@ -431,6 +436,7 @@ def run(args):
                        "graph": bool(engine.cfg.use_graph),
                        # event-split data parallel: two graphs per step, collectives between
                        "graph_steps": args.graph_steps if not (engine.segmented and engine.cfg.comm_events) else 1,
+                       "graph_warmup": engine.cfg.graph_warmup,
                        "bucket_blocks": engine.cfg.bucket_blocks if engine.segmented else None,
                        "allreduce": ("none" if not engine.segmented else "eager" if dev.type != "cuda" else
                                      "eager-inline-fallback" if engine.comm_fallback else
