@@ -13,6 +13,8 @@
 #include "kernels.h"
 #include <algorithm>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 using at::Tensor;
 
@@ -634,6 +636,20 @@ static std::vector<GemmArgs> wgrad_probs(const std::vector<Tensor>& dys, const s
   return probs;
 }
 
+// Tickets of the K-split weight-gradient tail: 4,096 ints per device, zeroed once (outside
+// any graph: the first call is an eager step); each split tile's last piece resets its
+// ticket, so every launch finds them zero.  One stream at a time uses them (the
+// weight-gradient launches of a step run on its compute stream).
+static int* split_tickets(const c10::Device& dev) {
+  static std::mutex mu;
+  static std::map<int, Tensor> bufs;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = bufs.find(dev.index());
+  if (it == bufs.end())
+    it = bufs.emplace(dev.index(), at::zeros({4096}, at::TensorOptions().dtype(at::kInt).device(dev))).first;
+  return it->second.data_ptr<int>();
+}
+
 // Every weight gradient of a training step in ONE launch (gemm_wgrad_multi_kernel)
 // sq_parts / arena: also write the grad-norm partials of the whole gradient arena
 // (the launches must then be its last writers): the arena ranges outside every dW /
@@ -740,16 +756,58 @@ void linear_wgrad_multi(std::vector<Tensor> dys, std::vector<Tensor> xs, std::ve
     sq.tail = (int)std::min<int64_t>(64, std::max<int64_t>(1, (rest + 256 * 16 - 1) / (256 * 16)));
   }
   const size_t total = dys.size();
+  // launches of <= WGRAD_MULTI_MAX problems with balanced tile counts (each launch's
+  // K-split tail then fills its last round; 32 + 18 problems left a 0.9-round launch)
+  int kmax = 0;
+  for (const auto& t : dys) kmax = std::max<int>(kmax, (int)t.size(0));
+  const int T = wgrad_multi_tile(kmax);
+  std::vector<int64_t> ptiles(total);
+  int64_t all_tiles = 0;
+  for (size_t i = 0; i < total; ++i) {
+    ptiles[i] = ((dys[i].size(1) + T - 1) / T) * ((xs[i].size(1) + T - 1) / T);
+    all_tiles += ptiles[i];
+  }
+  const size_t L = (total + WGRAD_MULTI_MAX - 1) / WGRAD_MULTI_MAX;
+  std::vector<size_t> cuts{0};
+  int64_t cum = 0;
+  for (size_t i = 0; i + 1 < total && cuts.size() < L; ++i) {
+    cum += ptiles[i];
+    const bool full = i + 1 - cuts.back() == (size_t)WGRAD_MULTI_MAX;
+    if (full || cum * (int64_t)L >= all_tiles * (int64_t)cuts.size()) cuts.push_back(i + 1);
+  }
+  cuts.push_back(total);
+  bool ok = true;
+  for (size_t c = 0; c + 1 < cuts.size(); ++c) ok = ok && cuts[c + 1] - cuts[c] <= (size_t)WGRAD_MULTI_MAX;
+  if (!ok) {  // cannot balance within the problem limit: plain chunks
+    cuts.clear();
+    for (size_t a = 0; a < total; a += WGRAD_MULTI_MAX) cuts.push_back(a);
+    cuts.push_back(total);
+  }
   int used = 0;  // partial slots written by earlier launches
-  for (size_t a = 0; a < total; a += WGRAD_MULTI_MAX) {
-    const size_t e = std::min(total, a + (size_t)WGRAD_MULTI_MAX);
+  for (size_t ci = 0; ci + 1 < cuts.size(); ++ci) {
+    const size_t a = cuts[ci], e = cuts[ci + 1];
+    // K-split tail of wide launches: workspace from the caching allocator (the capture's
+    // pool inside a graph), tickets in a per-device buffer every last piece resets
+    float* sws = nullptr;
+    int* scnt = nullptr;
+    Tensor ws_t;
+    if (T == 128) {
+      int64_t ct = 0;
+      for (size_t i = a; i < e; ++i) ct += ptiles[i];
+      const int64_t nf = wgrad_split_ws_floats((int)ct);
+      if (nf > 0) {
+        ws_t = at::empty({nf}, dys[0].options().dtype(F32));
+        sws = ws_t.data_ptr<float>();
+        scnt = split_tickets(dys[0].device());
+      }
+    }
     std::vector<Tensor> d(dys.begin() + a, dys.begin() + e), x(xs.begin() + a, xs.begin() + e),
         w(dws.begin() + a, dws.begin() + e);
     std::vector<c10::optional<Tensor>> b(dbs.begin() + a, dbs.begin() + e);
     std::vector<GemmArgs> probs = wgrad_probs(d, x, w, b, nullptr, nullptr);
     if (!fused) {
       gemm_wgrad_multi(probs.data(), (int)probs.size(), cur_stream(), store, nullptr,
-                       (with_emb && e == total) ? &we : nullptr);
+                       (with_emb && e == total) ? &we : nullptr, sws, scnt);
       continue;
     }
     WgradSq s = sq;
@@ -760,7 +818,7 @@ void linear_wgrad_multi(std::vector<Tensor> dys, std::vector<Tensor> xs, std::ve
       s.tail = 0;
     }
     used += gemm_wgrad_multi(probs.data(), (int)probs.size(), cur_stream(), store, &s,
-                             (with_emb && e == total) ? &we : nullptr);
+                             (with_emb && e == total) ? &we : nullptr, sws, scnt);
   }
   TORCH_CHECK(!with_emb || fused || total <= (size_t)WGRAD_MULTI_MAX, "wgrad_multi: embedding parts need sq fusion "
               "or one launch");

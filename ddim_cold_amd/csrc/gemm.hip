@@ -651,6 +651,13 @@ struct WgradMulti {
   EmbedGrad emb;
   ReplicaFinal rf;
   int nA, nB, nD;
+  // K-split tail (wide tiles): the first `whole` tiles run whole; the R = tiles - whole
+  // last ones in `split` K pieces each, written to ws (per piece: T x T partial + T bias
+  // partial), the last piece of a tile to finish (ticket in cnt[tile - whole]) sums the
+  // pieces in piece order into the target (deterministic) and writes the tile's partial
+  int whole, split;
+  float* ws;
+  int* cnt;
 };
 // tail workgroup j of the fused grad-norm: squares of the arena ranges no tile or
 // embedding workgroup writes, then zero the unused partial slots (from zfrom on)
@@ -689,7 +696,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_wgrad_multi_kernel(WgradMul
   // step on one box: profiles/embed_in_wgrad_r6.txt), then the tiles
   constexpr int NT = 64 * WM * WN;
   const int ne = gm.nA + gm.nB + gm.nD;
-  const int tail = (int)gridDim.x - tiles - ne;
+  const int tail = (int)gridDim.x - tiles - (tiles - gm.whole) * (gm.split - 1) - ne;
   if ((int)blockIdx.x < tail) {
     wgrad_sq_tail<NT>(gm.sq, tiles, blockIdx.x, tiles + tail + ne);
     return;
@@ -704,7 +711,16 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_wgrad_multi_kernel(WgradMul
     else emb_part_d<NT>(gm.rf, k - gm.nA - gm.nB, smem_emb, sqp);
     return;
   }
-  const int bid = xcd_remap((int)blockIdx.x - tail - ne, tiles);
+  const int u = (int)blockIdx.x - tail - ne;
+  const int R = tiles - gm.whole;
+  int bid, piece = 0;
+  if (u < gm.whole) {
+    bid = xcd_remap(u, gm.whole);
+  } else {  // K piece of a split tile; the pieces with one K range share an XCD
+    const int j = xcd_remap(u - gm.whole, R * gm.split);
+    piece = j / R;
+    bid = gm.whole + (j - piece * R);
+  }
   int lo = 0, hi = gm.n - 1;  // problem owning tile `bid`: binary search over tile_start
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -718,11 +734,86 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_wgrad_multi_kernel(WgradMul
   p.acc_store = gm.store;
   p.sq_parts = gm.sq.parts;
   p.sq_slot = bid;
-  p.ktiles_per_split = (d.K + BK - 1) / BK;
+  const int nkt = (d.K + BK - 1) / BK;
+  p.ktiles_per_split = nkt;
   const int tiles_n = (d.N + TN - 1) / TN;
   const int local = bid - gm.tile_start[lo];
-  const int tm = local / tiles_n;
-  gemm_dma_body<T, TN, WM, WN, true, true, EPI_ACC, S>(p, tm, local - tm * tiles_n, 0);
+  const int tm = local / tiles_n, tn = local - tm * tiles_n;
+  if (u < gm.whole) {
+    gemm_dma_body<T, TN, WM, WN, true, true, EPI_ACC, S>(p, tm, tn, 0);
+    return;
+  }
+  // split tile: this piece's partial product (plain stores) into its workspace slot, the
+  // target pointers rebased so the epilogue's (row, column) land at (0, 0) of the slot
+  constexpr int PS = T * TN + T;  // floats per piece slot: tile + bias partial
+  float* slot = gm.ws + (size_t)((bid - gm.whole) * gm.split + piece) * PS;
+  const int m0 = tm * T, n0 = tn * TN;
+  p.C = slot - ((ptrdiff_t)m0 * TN + n0);
+  p.ldc = TN;
+  p.bias = d.bias ? slot + T * TN - m0 : nullptr;
+  p.acc_store = 1;
+  p.sq_parts = nullptr;
+  p.ktiles_per_split = (nkt + gm.split - 1) / gm.split;
+  gemm_dma_body<T, TN, WM, WN, true, true, EPI_ACC, S>(p, tm, tn, piece);
+  // publish (every storing wave drained, then one release), take a ticket; the last
+  // piece of the tile sums all of them (cdna_hip_programming.md G16 ticket recipe)
+  __shared__ int s_last;
+  __shared__ float s_red[NT / 64];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(gm.cnt + (bid - gm.whole), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == gm.split - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      gm.cnt[bid - gm.whole] = 0;  // every piece has taken its ticket: ready for the next launch
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  const float* base = gm.ws + (size_t)((bid - gm.whole) * gm.split) * PS;
+  const int rows = min(T, d.M - m0), cols = min(TN, d.N - n0);
+  float q = 0.f;
+  for (int i = threadIdx.x; i < T * TN / 4; i += NT) {  // 4 columns per thread-step
+    const int r = (4 * i) / TN, c = 4 * i - r * TN;
+    if (r >= rows || c >= cols) continue;
+    f32x4 v = *reinterpret_cast<const f32x4*>(base + 4 * i);
+    for (int k = 1; k < gm.split; ++k) {
+      const f32x4 w = *reinterpret_cast<const f32x4*>(base + (size_t)k * PS + 4 * i);
+      v[0] += w[0]; v[1] += w[1]; v[2] += w[2]; v[3] += w[3];
+    }
+    f32x4* dst = reinterpret_cast<f32x4*>(d.C + (size_t)(m0 + r) * d.ldc + n0 + c);
+    if (!gm.store) {
+      const f32x4 o = *dst;
+      v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
+    }
+    *dst = v;
+    q += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+  }
+  if (d.bias && tn == 0) {
+    for (int r = threadIdx.x; r < rows; r += NT) {
+      float v = base[T * TN + r];
+      for (int k = 1; k < gm.split; ++k) v += base[(size_t)k * PS + T * TN + r];
+      const float o = gm.store ? v : d.bias[m0 + r] + v;
+      d.bias[m0 + r] = o;
+      q += o * o;
+    }
+  }
+  if (gm.sq.parts) {
+    q = wave_sum(q);
+    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = q;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < NT / 64; ++w) t += s_red[w];
+      gm.sq.parts[bid] = t;
+    }
+  }
 }
 template __global__ void gemm_wgrad_multi_kernel<64, 3>(WgradMulti);
 template __global__ void gemm_wgrad_multi_kernel<128, BIG_WG_STAGES, 128, 4, 2>(WgradMulti);
@@ -862,8 +953,38 @@ int wgrad_embed_workgroups(const WgradEmbed& emb, bool wide) {
          (emb.rf.ws ? emb.rf.G * ((emb.rf.C + 15) / 16) : 0);
 }
 
+// K pieces for the tail tiles of a wide (one workgroup per CU) launch: with W whole rounds
+// of 256 tiles and R tiles left, R x s pieces take ceil(R s / 256) / s tile times instead
+// of one (profiles/wgrad_split_r6.txt); s = 1 (no split) when nothing is gained
+static int cu_count() {  // one wide workgroup per CU (256 on the MI355X)
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+int wgrad_split_factor(int tiles) {
+  const int C = cu_count(), R = tiles % C;
+  if (R == 0) return 1;
+  int best = 1;
+  double bt = 1.0;
+  for (int s = 2; s <= WGRAD_MAX_SPLIT; ++s) {
+    const double t = (double)((R * s + C - 1) / C) / s;
+    if (t < bt - 1e-9) { bt = t; best = s; }
+  }
+  return best;
+}
+int wgrad_multi_tile(int kmax) { return kmax >= BIG_WG_K ? 128 : 64; }
+int64_t wgrad_split_ws_floats(int tiles) {
+  const int s = wgrad_split_factor(tiles);
+  return s > 1 ? (int64_t)(tiles % cu_count()) * s * (128 * 128 + 128) : 0;
+}
+
 int gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool store, const WgradSq* sq,
-                     const WgradEmbed* emb) {
+                     const WgradEmbed* emb, float* split_ws, int* split_cnt) {
   if (n < 1 || n > WM_MAX) throw std::runtime_error("gemm_wgrad_multi: 1..WGRAD_MULTI_MAX problems per launch");
   WgradMulti gm{};
   gm.n = n;
@@ -911,9 +1032,24 @@ int gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool stor
     extra += sq->tail;
   }
   static_assert(sizeof(WgradMulti) <= 4000, "kernel argument block");
+  gm.whole = tiles;
+  gm.split = 1;
+  int pieces = 0;
+  if (T == 128 && split_ws != nullptr && split_cnt != nullptr) {
+    const int s = wgrad_split_factor(tiles);
+    if (s > 1) {
+      const int R = tiles % cu_count();
+      gm.whole = tiles - R;
+      gm.split = s;
+      gm.ws = split_ws;
+      gm.cnt = split_cnt;
+      pieces = R * s - R;  // extra workgroups beyond one per tile
+    }
+  }
   if (T == 128) {
     constexpr int lds = BIG_WG_STAGES * 2 * 128 * 128;  // stages x (A + B) 128-wide, 64-deep images
-    hipLaunchKernelGGL((gemm_wgrad_multi_kernel<128, BIG_WG_STAGES, 128, 4, 2>), dim3(tiles + extra), dim3(512), lds, stream, gm);
+    hipLaunchKernelGGL((gemm_wgrad_multi_kernel<128, BIG_WG_STAGES, 128, 4, 2>), dim3(tiles + pieces + extra), dim3(512),
+                       lds, stream, gm);
   } else {
     hipLaunchKernelGGL((gemm_wgrad_multi_kernel<64, 3>), dim3(tiles + extra), dim3(256), 3 * (64 * 128 + 64 * 128),
                        stream, gm);

@@ -306,10 +306,13 @@ def test_linear_fwd(M, N, K, f32, bias):
     close(y.float(), yr.float(), 3e-2, 2e-2, "y")
 
 
-@pytest.mark.parametrize("n,big", [(1, False), (7, False), (30, False), (5, True)])
+@pytest.mark.parametrize("n,big", [(1, False), (7, False), (30, False), (5, True), (36, True)])
 def test_linear_wgrad_multi(n, big):
     """Every weight gradient of a step in one launch == per-problem reference (bias or not, odd shapes).
-    ``big``: a reduction over >= 16,384 tokens (vit_small_200: 128 x 128 tiles, 8 waves)."""
+    ``big``: a reduction over >= 16,384 tokens (vit_small_200: 128 x 128 tiles, 8 waves); there
+    the tiles past the last whole round of 256 run as K pieces summed by the last one
+    (5 problems: 60 tiles in 4 pieces; 36: two launches with balanced tile counts, each
+    with a split tail)."""
     shapes = [(1152, 384), (384, 384), (384, 384), (384, 384), (192, 384), (384, 192), (64, 96), (256, 128)]
     jobs, refs = [], []
     for i in range(n):
@@ -327,6 +330,29 @@ def test_linear_wgrad_multi(n, big):
         close(dw, dw2, 2e-2, 1e-4, "dw")
         if db is not None:
             close(db, db2, 2e-2, 1e-4, "db")
+
+
+def test_linear_wgrad_multi_split_tail_deterministic():
+    """vit_small_200's weight gradients (24 problems of a 6-block half: 324 tiles = one whole
+    round + 68 tiles in 3 K pieces): bit-identical over repeated launches (the pieces are
+    summed in piece order by whichever finishes last) and == the reference."""
+    shapes = [(1152, 384), (384, 384), (384, 384), (384, 384)] * 6
+    data = [(bf(20032, n), bf(20032, k)) for n, k in shapes]
+    outs = []
+    for _ in range(3):
+        jobs = [(dy, x, torch.zeros(dy.shape[1], x.shape[1], device=DEV), torch.zeros(dy.shape[1], device=DEV))
+                for dy, x in data]
+        ops.linear_wgrad_multi(jobs, store=True)
+        torch.cuda.synchronize()
+        outs.append(jobs)
+    for jobs in outs[1:]:
+        for (_, _, dw, db), (_, _, dw0, db0) in zip(jobs, outs[0]):
+            assert torch.equal(dw, dw0) and torch.equal(db, db0), "split-tail weight gradients differ between launches"
+    for (dy, x, dw, db) in outs[0][-4:]:  # the last block's problems hold the split tiles
+        dw2, db2 = torch.zeros_like(dw), torch.zeros_like(db)
+        ref.linear_wgrad(dy, x, dw2, db2)
+        close(dw, dw2, 2e-2, 1e-4, "dw")
+        close(db, db2, 2e-2, 1e-4, "db")
 
 
 @pytest.mark.parametrize("store", [False, True])
