@@ -915,6 +915,29 @@ std::tuple<Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tenso
 
 int64_t ln_ws_rows_op(int64_t M) { return ln_bwd_workgroups((int)M); }
 
+// dsts[i] = srcs[i]^T (bf16 [R][C] -> [C][R]), every matrix of the list in launches of
+// <= TRANSPOSE_MAX matrices (the input-gradient GEMMs' transposed weight shadows)
+void transpose_bf16_(std::vector<Tensor> srcs, std::vector<Tensor> dsts) {
+  TORCH_CHECK(!srcs.empty() && srcs.size() == dsts.size(), "transpose_bf16_: one dst per src");
+  const c10::DeviceGuard guard(srcs[0].device());
+  for (size_t a = 0; a < srcs.size(); a += TRANSPOSE_MAX) {
+    const size_t e = std::min(srcs.size(), a + (size_t)TRANSPOSE_MAX);
+    std::vector<const void*> sp;
+    std::vector<void*> dp;
+    std::vector<int> R, C;
+    for (size_t i = a; i < e; ++i) {
+      CHECK_IN(srcs[i], BF16); CHECK_IN(dsts[i], BF16);
+      TORCH_CHECK(srcs[i].dim() == 2 && dsts[i].dim() == 2 && dsts[i].size(0) == srcs[i].size(1) &&
+                      dsts[i].size(1) == srcs[i].size(0), "transpose_bf16_: dst must be [C, R] for src [R, C]");
+      sp.push_back(srcs[i].data_ptr());
+      dp.push_back(dsts[i].data_ptr());
+      R.push_back((int)srcs[i].size(0));
+      C.push_back((int)srcs[i].size(1));
+    }
+    transpose_bf16_launch(sp.data(), dp.data(), R.data(), C.data(), (int)sp.size(), cur_stream());
+  }
+}
+
 // ws [G][rows][C]: rows 0..R-1 of each LayerNorm workspace added into its destination
 void replica_reduce_(Tensor ws, Tensor dst_ptrs, int64_t C, int64_t R) {
   CHECK_IN(ws, F32); CHECK_IN(dst_ptrs, I64);
@@ -1219,6 +1242,7 @@ TORCH_LIBRARY(ddim_cold, m) {
         "Tensor(e!)? gp_out=None, int site_emb=0, float p_emb=0.0) -> (Tensor, Tensor)");
   m.def("replica_reduce_(Tensor ws, Tensor dst_ptrs, int C, int R) -> ()");
   m.def("ln_ws_rows(int M) -> int", &ln_ws_rows_op);
+  m.def("transpose_bf16_(Tensor[] srcs, Tensor(a!)[] dsts) -> ()");
   m.def("ln_fold_(Tensor[] ws, Tensor[] gammas, Tensor[] betas, Tensor?[] biases, Tensor(a!)[] wfs, Tensor(b!)[] cs, "
         "Tensor(c!)[] bfs, Tensor? loss_parts=None, Tensor(d!)? loss_last=None, Tensor(e!)? loss_ema=None, "
         "float ema_decay=0.99, Tensor(f!)? step=None, Tensor(g!)? rng=None, Tensor? sq=None) -> ()");
@@ -1270,6 +1294,7 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("wire_unpack", &wire_unpack);
   m.impl("layernorm_bwd", &layernorm_bwd);
   m.impl("replica_reduce_", &replica_reduce_);
+  m.impl("transpose_bf16_", &transpose_bf16_);
   m.impl("ln_fold_", &ln_fold_);
   m.impl("attn_bwd", &attn_bwd);
   m.impl("embed_bwd", &embed_bwd);

@@ -135,6 +135,11 @@ void layernorm_bwd_launch(const void* dy, bool dy_bf16, const void* x, bool x_bf
                           double p_dp, int dy_parts, void* gp_bf16, int site_emb, double p_emb, hipStream_t stream);
 int ln_bwd_workgroups(int M);
 
+// dst[i] = src[i]^T for bf16 matrices [R][C] (transpose.hip; R, C multiples of 8)
+constexpr int TRANSPOSE_MAX = 96;
+void transpose_bf16_launch(const void* const* srcs, void* const* dsts, const int* R, const int* C, int n,
+                           hipStream_t stream);
+
 // LayerNorm fold weights for the GEMMs that consume a LayerNorm (layernorm.hip)
 constexpr int FOLD_MAX = 32;  // GEMMs per fold launch (vit_small_200: 25 in one launch)
 struct FoldJob {

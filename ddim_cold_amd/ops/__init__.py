@@ -392,6 +392,16 @@ def linear_wgrad_multi(jobs, store: bool = False, sq=None, embed=None):
         sqnorm(arena, parts, 1.0, lazy=lazy)
 
 
+def transpose_bf16_(srcs, dsts):
+    """``dsts[i] = srcs[i].T`` for bf16 matrices (one launch per 96; csrc/transpose.hip):
+    the transposed weight shadows the input-gradient GEMMs read k-contiguous."""
+    if srcs and _hip(srcs[0]):
+        _ops().transpose_bf16_(list(srcs), list(dsts))
+        return
+    for s_, d_ in zip(srcs, dsts):
+        d_.copy_(s_.t())
+
+
 def ln_ws_rows(M: int) -> int:
     """Rows ([rows, 2D] floats) of the dgamma||dbeta workspace :func:`layernorm_bwd`
     takes for ``M`` rows: one slot per backward workgroup (csrc/layernorm.hip: 8 rows per

@@ -75,6 +75,41 @@ FUSE_SQNORM = True
 # LayerNorm finalize run as extra workgroups of the weight-gradient launch
 # (csrc/embed_parts.h; False: embed_bwd as its own launch; tests compare the two)
 FUSE_EMBED_WGRAD = True
+# models of at least this many tokens per sample (vit_small_200: 626) keep transposed bf16
+# shadows of the QKV / proj / fc1 weights, re-transposed after every optimizer step, so
+# their input-gradient GEMMs run on the k-contiguous operand path
+# (tools/ub_dgrad_layout.py: QKV 31.7 -> 25.5 us, K = 384 15.0 -> 13.5 us at M = 20,032;
+# ViT-tiny's M = 2,080 gains ~0.5 us per GEMM, less than the transpose launch costs)
+TRANSPOSED_DGRAD_MIN_TOKENS = 512
+
+
+class TransposedShadows:
+    """Transposed copies ([in][out], bf16) of the blocks' QKV, proj and fc1 weight shadows in
+    one arena; :meth:`refresh` re-transposes all of them in one launch (after every
+    optimizer step, inside the step graph), :meth:`attach` sets ``qkv_wt`` / ``proj_wt`` /
+    ``fc1_wt`` on the program's block tensors."""
+
+    KINDS = ("qkv", "proj", "fc1")
+
+    def __init__(self, P: ModelTensors):
+        self.src = []
+        for bp in P.blocks:
+            self.src += [getattr(bp, k + "_w") for k in self.KINDS]
+        n = sum(w.numel() for w in self.src)
+        self.arena = torch.empty(n, dtype=torch.bfloat16, device=self.src[0].device)
+        self.dst, o = [], 0
+        for w in self.src:
+            self.dst.append(self.arena[o:o + w.numel()].view(w.shape[1], w.shape[0]))
+            o += w.numel()
+
+    def refresh(self):
+        ops.transpose_bf16_(self.src, self.dst)
+
+    def attach(self, P: ModelTensors) -> ModelTensors:
+        for i, bp in enumerate(P.blocks):
+            for j, k in enumerate(self.KINDS):
+                setattr(bp, k + "_wt", self.dst[3 * i + j])
+        return P
 
 
 @dataclass
@@ -439,6 +474,11 @@ class TrainEngine:
         self.param_tensors: ModelTensors = collect(views_p, c.depth, c.dim)
         if self.lnfold is not None:
             self.lnfold.attach(self.param_tensors)
+        self.wt = None
+        if self.is_cuda and c.tokens >= TRANSPOSED_DGRAD_MIN_TOKENS:
+            self.wt = TransposedShadows(self.param_tensors)
+            self.wt.attach(self.param_tensors)
+            self.wt.refresh()
         self.grad_tensors: ModelTensors = collect(views_g, c.depth, c.dim)
         if not c.learn_temb:
             self.grad_tensors.temb = None
@@ -573,6 +613,8 @@ class TrainEngine:
         self.flat_pb.copy_(self.flat_p.to(torch.bfloat16))
         if getattr(self, "lnfold", None) is not None:
             self.lnfold.refresh()
+        if getattr(self, "wt", None) is not None:
+            self.wt.refresh()
 
     # ------------------------------------------------------------------ step program
     def set_batch_fn(self, fn: Callable):
@@ -690,6 +732,8 @@ class TrainEngine:
         ops.adamw_step(self.opt_p, self.opt_g, self.opt_m, self.opt_v, self.opt_pb, self.sqnorm,
                        self.step_ctr, self.hyper, gs, zero_hi=self.acc_hi if overwrite else None,
                        lazy=self.lazy, lazy_decay=self.lazy_decay)
+        if self.wt is not None:  # the input-gradient GEMMs' transposed shadows of the new weights
+            self.wt.refresh()
         if tail:
             self.lnfold.refresh(tail=(loss_parts, self.loss_last, self.loss_ema, self.cfg.ema_decay, self.step_ctr,
                                       self.rng, self.sqnorm))

@@ -418,3 +418,50 @@ def test_embed_in_wgrad_launch_matches_separate_launch(monkeypatch, dataset):
     assert lf == lf2 and torch.equal(pf, pf2)
     assert all(abs(a - b) <= 1e-5 * abs(b) for a, b in zip(lf, ls)), (lf, ls)
     assert (pf - ps).abs().max().item() <= 1e-5
+
+
+@pytest.mark.gpu
+def test_transposed_weight_shadows_match_transposed_operand_path(monkeypatch):
+    """Long-sequence models keep W^T shadows of the QKV / proj / fc1 weights
+    (engine.TransposedShadows, refreshed after every optimizer step inside the graph) and
+    run those input-gradient GEMMs on the k-contiguous path: same training as the
+    transposed-operand path within the GEMMs' accumulation-order rounding, and the shadows
+    equal the transposed bf16 weights after the run."""
+    from ddim_cold_amd.train import engine as E
+
+    def run(min_tokens):
+        monkeypatch.setattr(E, "TRANSPOSED_DGRAD_MIN_TOKENS", min_tokens)
+        torch.manual_seed(0)
+        model = build_model("vit_small_200", depth=2).cuda().train()
+        eng = TrainEngine(model, EngineConfig(lr=1e-3, t_max=100, seed=3, use_graph=True, graph_warmup=1,
+                                              temb_rows=8, graph_steps=2))
+        eng.set_batch_fn(ColdBatcher(synthetic_pool(32, (200, 200), seed=1, device="cuda"), 4, eng.rng))
+        losses = [float(eng.train_steps(2)) for _ in range(2)]
+        torch.cuda.synchronize()
+        return eng, losses
+
+    e1, l1 = run(512)
+    assert e1.wt is not None and e1.param_tensors.blocks[0].qkv_wt is not None
+    for bp in e1.param_tensors.blocks:
+        for k in ("qkv", "proj", "fc1"):
+            assert torch.equal(getattr(bp, k + "_wt"), getattr(bp, k + "_w").t()), k
+    e0, l0 = run(10 ** 9)
+    assert e0.wt is None and e0.param_tensors.blocks[0].qkv_wt is None
+    for a, b in zip(l1, l0):
+        assert abs(a - b) <= 1e-4 * abs(b), (l1, l0)
+    # Adam moves an element by ~lr per step whatever its gradient's size, so elements
+    # with near-zero gradients may step differently under different rounding: bound the
+    # largest difference by the 4 steps' reach and require almost all to agree closely
+    d = (e1.flat_p - e0.flat_p).abs()
+    assert d.max().item() <= 2 * 4 * 1e-3, d.max().item()
+    assert (d > 1e-4).float().mean().item() < 0.01, (d > 1e-4).float().mean().item()
+
+
+@pytest.mark.gpu
+def test_transpose_bf16_op():
+    from ddim_cold_amd import ops
+    srcs = [torch.randn(r, c, device="cuda").to(torch.bfloat16) for r, c in ((1152, 384), (384, 384), (8, 72), (200, 136))]
+    dsts = [torch.empty(s.shape[1], s.shape[0], dtype=torch.bfloat16, device="cuda") for s in srcs]
+    ops.transpose_bf16_(srcs, dsts)
+    for s, d in zip(srcs, dsts):
+        assert torch.equal(d, s.t())
