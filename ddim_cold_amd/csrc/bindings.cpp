@@ -559,6 +559,24 @@ Tensor linear_dgrad_gelu(Tensor dy, Tensor w, Tensor u, Tensor rng, int64_t site
   return du;
 }
 
+// the same with the transposed weight wt = W^T [in][out] (k-contiguous operand path)
+Tensor linear_dgrad_gelu_t(Tensor dy, Tensor wt, Tensor u, Tensor rng, int64_t site, double p) {
+  CHECK_IN(dy, BF16); CHECK_IN(wt, BF16); CHECK_IN(u, BF16); check_rng(rng);
+  const c10::DeviceGuard guard(dy.device());
+  TORCH_CHECK(dy.dim() == 2 && wt.dim() == 2 && dy.size(1) == wt.size(1), "dgrad shapes (wt = W^T)");
+  const int M = dy.size(0), Nout = wt.size(1), K = wt.size(0);
+  TORCH_CHECK(u.numel() == (int64_t)M * K, "u shape");
+  TORCH_CHECK(Nout % 64 == 0 && K % 8 == 0, "dgrad (transposed weight): K % 64 == 0, N % 8 == 0");
+  auto du = at::empty({M, K}, dy.options());
+  GemmArgs g;
+  g.A = dy.data_ptr(); g.B = wt.data_ptr();
+  g.M = M; g.N = K; g.K = Nout; g.lda = Nout; g.ldb = Nout;
+  g.C = du.data_ptr(); g.ldc = K; g.aux = u.data_ptr();
+  g.rng = rng.data_ptr<int64_t>(); g.site_drop = site; g.p_drop = p;
+  gemm_nt(g, EPI_DGELU, cur_stream());
+  return du;
+}
+
 void linear_wgrad(Tensor dy, Tensor x, Tensor dw, c10::optional<Tensor> db) {
   CHECK_IN(dy, BF16); CHECK_IN(x, BF16); CHECK_IN(dw, F32);
   const c10::DeviceGuard guard(dy.device());
@@ -1227,6 +1245,7 @@ TORCH_LIBRARY(ddim_cold, m) {
   m.def("img_to_tokgrad(Tensor dimg, int N, int patch) -> Tensor");
   m.def("linear_dgrad(Tensor dy, Tensor w, bool out_fp32, int splits=1) -> Tensor");
   m.def("linear_dgrad_gelu(Tensor dy, Tensor w, Tensor u, Tensor rng, int site, float p) -> Tensor");
+  m.def("linear_dgrad_gelu_t(Tensor dy, Tensor wt, Tensor u, Tensor rng, int site, float p) -> Tensor");
   m.def("linear_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, Tensor(b!)? db) -> ()");
   m.def("wire_pack(Tensor src, Tensor(a!) dst) -> ()");
   m.def("wire_unpack(Tensor src, Tensor(a!) dst) -> ()");
@@ -1285,6 +1304,7 @@ TORCH_LIBRARY_IMPL(ddim_cold, CUDA, m) {
   m.impl("img_to_tokgrad", &img_to_tokgrad);
   m.impl("linear_dgrad", &linear_dgrad);
   m.impl("linear_dgrad_gelu", &linear_dgrad_gelu);
+  m.impl("linear_dgrad_gelu_t", &linear_dgrad_gelu_t);
   m.impl("linear_wgrad", &linear_wgrad);
   m.impl("head_step_", &head_step_);
   m.impl("head_step_rows_", &head_step_rows_);

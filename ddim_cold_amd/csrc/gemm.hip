@@ -615,6 +615,9 @@ DC_INST_DMA3(EPI_HEADL)
 DC_INST_DMA2(false, true, EPI_BF16) DC_INST_W8(false, true, EPI_BF16)
 DC_INST_DMA2(false, true, EPI_F32) DC_INST_W8(false, true, EPI_F32)
 DC_INST_DMA2(false, true, EPI_DGELU)
+DC_INST_DMA3(EPI_DGELU)  // the same on the k-contiguous path (transposed weight shadow)
+template __global__ void gemm_dma_kernel<128, 128, 4, 2, false, false, EPI_DGELU, 3>(GemmParams);
+template __global__ void gemm_dma_kernel<128, 128, 4, 2, false, false, EPI_DGELU, 4>(GemmParams);
 template __global__ void gemm_dma_kernel<128, 128, 4, 2, false, true, EPI_DGELU, 3>(GemmParams);
 template __global__ void gemm_dma_kernel<128, 128, 4, 2, false, true, EPI_DGELU, 4>(GemmParams);
 DC_INST_DMA(64, true, true, EPI_ATOMIC)
@@ -886,6 +889,7 @@ void gemm_nt(const GemmArgs& a, int epi, hipStream_t stream) {
     case EPI_GELU: launch_auto<false, false, EPI_GELU>(p, 1, stream); break;
     case EPI_HEAD: launch_auto<false, false, EPI_HEAD>(p, 1, stream); break;
     case EPI_EMBED: launch_auto<false, false, EPI_EMBED>(p, 1, stream); break;
+    case EPI_DGELU: launch_auto<false, false, EPI_DGELU>(p, 1, stream); break;  // dgrad through GELU, W^T given
     case EPI_HEADR:
       if (p.K % 64 != 0) throw std::runtime_error("gemm_nt: EPI_HEADR needs the LDS-DMA GEMM");
       launch_auto<false, false, EPI_HEADR>(p, 1, stream);

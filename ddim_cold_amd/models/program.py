@@ -102,6 +102,7 @@ class BlockTensors:
     qkv_wt: Optional[torch.Tensor] = None
     proj_wt: Optional[torch.Tensor] = None
     fc1_wt: Optional[torch.Tensor] = None
+    fc2_wt: Optional[torch.Tensor] = None
 
 
 @dataclass
@@ -519,7 +520,7 @@ class ViTProgram:
             x0, l1, m1, r1, qkv, o, lse, x1, l2, m2, r2, u, h = S.blocks[i]
             bp, bg = P.blocks[i], G.blocks[i]
             sa, sp, sd1, sf1, _, _ = block_sites(i)
-            du = ops.linear_dgrad_gelu(gy, bp.fc2_w, u, rng, sf1, pd)
+            du = ops.linear_dgrad_gelu(gy, bp.fc2_w, u, rng, sf1, pd, wt=bp.fc2_wt)
             wgrad(gy, h, bg.fc2_w, bg.fc2_b)
             k2 = 1 + 2 * (L - 1 - i)
             l2 = ln_out(l2)

@@ -309,8 +309,12 @@ def linear_dgrad(dy, w, out_fp32: bool, splits: int = 1):
     return ref.linear_dgrad(dy, w, out_fp32, splits)
 
 
-def linear_dgrad_gelu(dy, w, u, rng, site: int, p: float):
+def linear_dgrad_gelu(dy, w, u, rng, site: int, p: float, wt=None):
+    """``(dy @ W) * gelu'(u)`` with the dropout mask of ``site``; ``wt`` (= W^T, bf16
+    [in][out]): the product on the k-contiguous operand path."""
     if _hip(dy):
+        if wt is not None:
+            return _ops().linear_dgrad_gelu_t(dy, wt, u, rng, site, float(p))
         return _ops().linear_dgrad_gelu(dy, w, u, rng, site, float(p))
     return ref.linear_dgrad_gelu(dy, w, u, rng, site, p)
 

@@ -76,7 +76,7 @@ FUSE_SQNORM = True
 # (csrc/embed_parts.h; False: embed_bwd as its own launch; tests compare the two)
 FUSE_EMBED_WGRAD = True
 # models of at least this many tokens per sample (vit_small_200: 626) keep transposed bf16
-# shadows of the QKV / proj / fc1 weights, re-transposed after every optimizer step, so
+# shadows of the QKV / proj / fc1 / fc2 weights, re-transposed after every optimizer step, so
 # their input-gradient GEMMs run on the k-contiguous operand path
 # (tools/ub_dgrad_layout.py: QKV 31.7 -> 25.5 us, K = 384 15.0 -> 13.5 us at M = 20,032;
 # ViT-tiny's M = 2,080 gains ~0.5 us per GEMM, less than the transpose launch costs)
@@ -84,12 +84,13 @@ TRANSPOSED_DGRAD_MIN_TOKENS = 512
 
 
 class TransposedShadows:
-    """Transposed copies ([in][out], bf16) of the blocks' QKV, proj and fc1 weight shadows in
-    one arena; :meth:`refresh` re-transposes all of them in one launch (after every
-    optimizer step, inside the step graph), :meth:`attach` sets ``qkv_wt`` / ``proj_wt`` /
-    ``fc1_wt`` on the program's block tensors."""
+    """Transposed copies ([in][out], bf16) of the blocks' QKV, proj, fc1 and fc2 weight
+    shadows in one arena; :meth:`refresh` re-transposes all of them in one launch (after
+    every optimizer step, inside the step graph), :meth:`attach` sets ``qkv_wt`` /
+    ``proj_wt`` / ``fc1_wt`` / ``fc2_wt`` on the program's block tensors (fc2: the
+    input gradient through GELU)."""
 
-    KINDS = ("qkv", "proj", "fc1")
+    KINDS = ("qkv", "proj", "fc1", "fc2")
 
     def __init__(self, P: ModelTensors):
         self.src = []
@@ -108,7 +109,7 @@ class TransposedShadows:
     def attach(self, P: ModelTensors) -> ModelTensors:
         for i, bp in enumerate(P.blocks):
             for j, k in enumerate(self.KINDS):
-                setattr(bp, k + "_wt", self.dst[3 * i + j])
+                setattr(bp, k + "_wt", self.dst[len(self.KINDS) * i + j])
         return P
 
 

@@ -443,7 +443,7 @@ def test_transposed_weight_shadows_match_transposed_operand_path(monkeypatch):
     e1, l1 = run(512)
     assert e1.wt is not None and e1.param_tensors.blocks[0].qkv_wt is not None
     for bp in e1.param_tensors.blocks:
-        for k in ("qkv", "proj", "fc1"):
+        for k in ("qkv", "proj", "fc1", "fc2"):
             assert torch.equal(getattr(bp, k + "_wt"), getattr(bp, k + "_w").t()), k
     e0, l0 = run(10 ** 9)
     assert e0.wt is None and e0.param_tensors.blocks[0].qkv_wt is None

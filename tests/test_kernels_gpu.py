@@ -273,13 +273,18 @@ def test_dgrad_ksplit(M, Nout, K, splits):
         close(dg1, dg2, 1e-2, 1e-4, "ln dgamma (summed partials)")
 
 
-def test_dgrad_gelu():
-    M, N, K = 2080, 384, 384
+@pytest.mark.parametrize("M,N,K", [(2080, 384, 384), (20032, 384, 384), (300, 256, 128)])
+def test_dgrad_gelu(M, N, K):
+    """dU = (dY W) * gelu'(u) with dropout; also from the transposed weight W^T (the
+    k-contiguous operand path the long-sequence engine uses): same values, same masks."""
     dy, w, u = bf(M, N), bf(N, K, scale=0.05), bf(M, K)
     r = rng()
     du = ops.linear_dgrad_gelu(dy, w, u, r, 11, 0.1)
     dur = ref.linear_dgrad_gelu(dy, w, u, r, 11, 0.1)
     close(du, dur, 2e-2, 1e-2, "dgelu")
+    dut = ops.linear_dgrad_gelu(dy, w, u, r, 11, 0.1, wt=w.t().contiguous())
+    close(dut, dur, 2e-2, 1e-2, "dgelu (W^T)")
+    assert torch.equal(dut == 0, dur == 0), "dropout masks differ"
 
 
 @pytest.mark.parametrize("M,Nout,K", [(2080, 384, 384), (2080, 1152, 384), (2080, 192, 384), (8224, 256, 256),

@@ -26,3 +26,13 @@ for M in (20032, 2080):
         fl = 2 * M * out * inn
         print(f"M={M:6d} K={out:5d} N={inn}: W (transposed-B path) {a:6.2f} us  W^T (forward path) {b:6.2f} us"
               f"  ({fl / a / 1e6:4.0f} vs {fl / b / 1e6:4.0f} TF, max|d| {d:.1e}, {'f32' if f32 else 'bf16'} out)", flush=True)
+# input gradient through GELU (fc2): dU = (dY W) * gelu'(u), dropout p = 0.1
+r = torch.tensor([1, 2], dtype=torch.int64, device=dev)
+for M in (20032, 2080):
+    dy = torch.randn(M, 384, device=dev).to(torch.bfloat16)
+    w = (torch.randn(384, 384, device=dev) * 0.05).to(torch.bfloat16)
+    u = torch.randn(M, 384, device=dev).to(torch.bfloat16)
+    wt = w.t().contiguous()
+    a = t(lambda: ops.linear_dgrad_gelu(dy, w, u, r, 11, 0.1))
+    b = t(lambda: ops.linear_dgrad_gelu(dy, w, u, r, 11, 0.1, wt=wt))
+    print(f"dgelu M={M:6d} K=384 N=384: W {a:6.2f} us  W^T {b:6.2f} us", flush=True)
