@@ -809,10 +809,10 @@ void linear_wgrad_multi(std::vector<Tensor> dys, std::vector<Tensor> xs, std::ve
     float* sws = nullptr;
     int* scnt = nullptr;
     Tensor ws_t;
-    if (T == 128) {
+    {
       int64_t ct = 0;
       for (size_t i = a; i < e; ++i) ct += ptiles[i];
-      const int64_t nf = wgrad_split_ws_floats((int)ct);
+      const int64_t nf = wgrad_split_ws_floats((int)ct, T);
       if (nf > 0) {
         ws_t = at::empty({nf}, dys[0].options().dtype(F32));
         sws = ws_t.data_ptr<float>();

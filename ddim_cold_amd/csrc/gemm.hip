@@ -757,7 +757,11 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_wgrad_multi_kernel(WgradMul
   p.acc_store = 1;
   p.sq_parts = nullptr;
   p.ktiles_per_split = (nkt + gm.split - 1) / gm.split;
-  gemm_dma_body<T, TN, WM, WN, true, true, EPI_ACC, S>(p, tm, tn, piece);
+  if (piece * p.ktiles_per_split < nkt) {
+    gemm_dma_body<T, TN, WM, WN, true, true, EPI_ACC, S>(p, tm, tn, piece);
+  } else {  // a piece past the last k-tile (short reductions): a zero partial
+    for (int i = threadIdx.x; i < PS; i += NT) slot[i] = 0.f;
+  }
   // publish (every storing wave drained, then one release), take a ticket; the last
   // piece of the tile sums all of them (cdna_hip_programming.md G16 ticket recipe)
   __shared__ int s_last;
@@ -970,9 +974,14 @@ static int cu_count() {  // one wide workgroup per CU (256 on the MI355X)
   }();
   return n;
 }
-int wgrad_split_factor(int tiles) {
-  const int C = cu_count(), R = tiles % C;
-  if (R == 0) return 1;
+// workgroup slots of one round: one 128 x 128 (128 KiB ring) or three 64 x 64 (48 KiB)
+// weight-gradient workgroups per CU
+static int wgrad_slots(int T) { return (T == 128 ? 1 : 3) * cu_count(); }
+int wgrad_split_factor(int tiles, int T) {
+  const int C = wgrad_slots(T), R = tiles % C;
+  // 64 x 64 tiles (three workgroups per CU): splitting ViT-tiny's 12-tile tail in 6 pieces
+  // measured slower (0.7107 -> 0.7146 ms/step, profiles/wgrad_split_r6.txt) -- wide tiles only
+  if (R == 0 || T != 128) return 1;
   int best = 1;
   double bt = 1.0;
   for (int s = 2; s <= WGRAD_MAX_SPLIT; ++s) {
@@ -982,9 +991,9 @@ int wgrad_split_factor(int tiles) {
   return best;
 }
 int wgrad_multi_tile(int kmax) { return kmax >= BIG_WG_K ? 128 : 64; }
-int64_t wgrad_split_ws_floats(int tiles) {
-  const int s = wgrad_split_factor(tiles);
-  return s > 1 ? (int64_t)(tiles % cu_count()) * s * (128 * 128 + 128) : 0;
+int64_t wgrad_split_ws_floats(int tiles, int T) {
+  const int s = wgrad_split_factor(tiles, T);
+  return s > 1 ? (int64_t)(tiles % wgrad_slots(T)) * s * (T * T + T) : 0;
 }
 
 int gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool store, const WgradSq* sq,
@@ -1039,10 +1048,10 @@ int gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool stor
   gm.whole = tiles;
   gm.split = 1;
   int pieces = 0;
-  if (T == 128 && split_ws != nullptr && split_cnt != nullptr) {
-    const int s = wgrad_split_factor(tiles);
+  if (split_ws != nullptr && split_cnt != nullptr) {
+    const int s = wgrad_split_factor(tiles, T);
     if (s > 1) {
-      const int R = tiles % cu_count();
+      const int R = tiles % wgrad_slots(T);
       gm.whole = tiles - R;
       gm.split = s;
       gm.ws = split_ws;
@@ -1055,8 +1064,8 @@ int gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool stor
     hipLaunchKernelGGL((gemm_wgrad_multi_kernel<128, BIG_WG_STAGES, 128, 4, 2>), dim3(tiles + pieces + extra), dim3(512),
                        lds, stream, gm);
   } else {
-    hipLaunchKernelGGL((gemm_wgrad_multi_kernel<64, 3>), dim3(tiles + extra), dim3(256), 3 * (64 * 128 + 64 * 128),
-                       stream, gm);
+    hipLaunchKernelGGL((gemm_wgrad_multi_kernel<64, 3>), dim3(tiles + pieces + extra), dim3(256),
+                       3 * (64 * 128 + 64 * 128), stream, gm);
   }
   return tiles;
 }

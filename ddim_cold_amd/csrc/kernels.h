@@ -107,13 +107,14 @@ struct WgradSq {
 // launch as extra workgroups (embed_parts.h), each writing the grad-norm partial of its
 // outputs after the tail's slots.
 struct WgradEmbed;  // below
-// split_ws / split_cnt (wide 128 x 128 tiles only): workspace of wgrad_split_ws_floats(tiles)
-// floats and tiles % 256 zeroed ints -- the tail tiles past the last whole round of 256
-// run as wgrad_split_factor(tiles) K pieces each, summed in piece order (deterministic)
+// split_ws / split_cnt: workspace of wgrad_split_ws_floats(tiles, T) floats and zeroed
+// tickets -- the tail tiles past the last whole round of workgroup slots (256 CUs x 1
+// wide or x 3 64 x 64 workgroups) run as wgrad_split_factor(tiles, T) K pieces each,
+// summed in piece order (deterministic)
 constexpr int WGRAD_MAX_SPLIT = 6;
-int wgrad_split_factor(int tiles);
+int wgrad_split_factor(int tiles, int T);
 int wgrad_multi_tile(int kmax);  // output tile edge gemm_wgrad_multi uses for reductions over kmax tokens
-int64_t wgrad_split_ws_floats(int tiles);
+int64_t wgrad_split_ws_floats(int tiles, int T);
 int gemm_wgrad_multi(const GemmArgs* probs, int n, hipStream_t stream, bool store = false,
                      const WgradSq* sq = nullptr, const WgradEmbed* emb = nullptr, float* split_ws = nullptr,
                      int* split_cnt = nullptr);

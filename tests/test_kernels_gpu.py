@@ -337,6 +337,26 @@ def test_linear_wgrad_multi(n, big):
             close(db, db2, 2e-2, 1e-4, "db")
 
 
+def test_linear_wgrad_multi_vit_tiny_tiles():
+    """ViT-tiny's 1,548 64 x 64 weight-gradient tiles (two launches' worth of problems,
+    balanced) at a short reduction (K = 520 tokens) == the reference."""
+    shapes = [(1152, 384), (384, 384), (384, 384), (384, 384)] * 7 + [(192, 384), (384, 192)]
+    jobs, refs = [], []
+    for i, (n, k) in enumerate(shapes):
+        m = 520
+        dy, x = bf(m, n), bf(m, k)
+        dw, db = torch.randn(n, k, device=DEV), (torch.randn(n, device=DEV) if i % 2 == 0 else None)
+        dw2, db2 = dw.clone(), (db.clone() if db is not None else None)
+        ref.linear_wgrad(dy, x, dw2, db2)
+        jobs.append((dy, x, dw, db))
+        refs.append((dw2, db2))
+    ops.linear_wgrad_multi(jobs)
+    for (_, _, dw, db), (dw2, db2) in zip(jobs, refs):
+        close(dw, dw2, 2e-2, 1e-4, "dw")
+        if db is not None:
+            close(db, db2, 2e-2, 1e-4, "db")
+
+
 def test_linear_wgrad_multi_split_tail_deterministic():
     """vit_small_200's weight gradients (24 problems of a 6-block half: 324 tiles = one whole
     round + 68 tiles in 3 K pieces): bit-identical over repeated launches (the pieces are
