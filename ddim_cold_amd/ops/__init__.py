@@ -410,7 +410,10 @@ def ln_ws_rows(M: int) -> int:
     """Rows ([rows, 2D] floats) of the dgamma||dbeta workspace :func:`layernorm_bwd`
     takes for ``M`` rows: one slot per backward workgroup (csrc/layernorm.hip: 8 rows per
     workgroup, at most 512 workgroups), each overwritten by its workgroup, summed in slot
-    order by :func:`replica_reduce_` (deterministic, no atomics)."""
+    order by :func:`replica_reduce_` (deterministic, no atomics).  The loaded extension's
+    own count when there is one (one source of truth; A/B runs load other builds)."""
+    if native_available():
+        return int(_ops().ln_ws_rows(int(M)))
     return max(1, min(-(-M // 8), 512))
 
 
