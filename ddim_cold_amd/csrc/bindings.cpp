@@ -654,17 +654,18 @@ static std::vector<GemmArgs> wgrad_probs(const std::vector<Tensor>& dys, const s
   return probs;
 }
 
-// Tickets of the K-split weight-gradient tail: 4,096 ints per device, zeroed once (outside
-// any graph: the first call is an eager step); each split tile's last piece resets its
-// ticket, so every launch finds them zero.  One stream at a time uses them (the
-// weight-gradient launches of a step run on its compute stream).
+// Tickets of the K-split weight-gradient tail: 4,096 ints per (device, stream), zeroed
+// once (the first call is an eager step, outside any graph); each split tile's last piece
+// resets its ticket, so every launch on that stream finds them zero (launches on one
+// stream run in order; two streams -- e.g. two engines in one process -- get their own).
 static int* split_tickets(const c10::Device& dev) {
   static std::mutex mu;
-  static std::map<int, Tensor> bufs;
+  static std::map<std::pair<int, int64_t>, Tensor> bufs;
+  const auto key = std::make_pair((int)dev.index(), (int64_t)c10::hip::getCurrentHIPStream(dev.index()).id());
   std::lock_guard<std::mutex> lk(mu);
-  auto it = bufs.find(dev.index());
+  auto it = bufs.find(key);
   if (it == bufs.end())
-    it = bufs.emplace(dev.index(), at::zeros({4096}, at::TensorOptions().dtype(at::kInt).device(dev))).first;
+    it = bufs.emplace(key, at::zeros({4096}, at::TensorOptions().dtype(at::kInt).device(dev))).first;
   return it->second.data_ptr<int>();
 }
 
