@@ -635,6 +635,9 @@ constexpr int BIG_WG_K = 16384;  // tokens: 128 x 128 weight-gradient tiles from
 // to soften the last-wave tail of ~5.1 tile rounds) took the vit_small_200 weight
 // gradients 638 -> 1,183 us (and 48 problems per launch did not merge its two launches)
 constexpr int BIG_WG_STAGES = 4;
+// the ring plus the kernel's static LDS (ticket flag, wave sums) within one CU's 160 KiB: a
+// 5-stage ring (163,952 B with the statics) is refused at launch (invalid allocation)
+static_assert(BIG_WG_STAGES * 2 * 128 * 128 + 256 <= 160 * 1024, "weight-gradient ring exceeds the LDS of one CU");
 struct WgDesc {
   const bf16* A;
   const bf16* B;
