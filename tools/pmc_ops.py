@@ -30,7 +30,7 @@ qkv = bf(3, B, H, N, 32)
 do = bf(B, N, D)
 u = bf(M, D)
 _, mu, rs = ops.layernorm_fwd(x, g, be)
-ws = torch.zeros(ops.ln_ws_rows(M, D), 2 * D, device=dev)
+ws = torch.zeros(ops.ln_ws_rows(M), 2 * D, device=dev)
 dyb = bf(M, D)
 keep = ops.attn_keep_buffer(qkv, 0.1)
 n = 7_300_000
